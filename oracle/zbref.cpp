@@ -1,0 +1,1260 @@
+// zbref — ORACLE / TEST INFRASTRUCTURE ONLY.
+//
+// A sequential CPU restatement of the reference's workflow-instance stepping path (Zeebe
+// 0.12.0-SNAPSHOT broker-core). It exists to *check* the product (libzbgpu.so) and to give the
+// CPU baseline timed by bench.py; it is never called by the product. Parity is pinned by the
+// reference's own known-answer tests transcribed under tests/golden (see tests/test_oracle_*.py).
+//
+// What it restates (file:line in /root/reference):
+//   FIFO driver              logstreams/src/main/java/io/zeebe/logstreams/processor/StreamProcessorController.java:296-414
+//   processor registrations  broker-core/src/main/java/io/zeebe/broker/workflow/processor/WorkflowInstanceStreamProcessor.java:90-182
+//   CREATE/CREATED/JOB/CORRELATE/CANCEL/UPDATE_PAYLOAD       same file :224-576
+//   step dispatch + guards   broker-core/.../workflow/processor/BpmnStepProcessor.java:92-251
+//   step handlers            broker-core/.../workflow/processor/{activity,catchevent,exclusivegw,flownode,process,
+//                            sequenceflow,servicetask,subprocess}/*.java
+//   index writes             broker-core/.../workflow/processor/ElementInstanceWriter.java:64-110
+//   element instance index   broker-core/.../workflow/index/{ElementInstance,ElementInstanceIndex}.java
+//   key generator            broker-core/.../logstreams/processor/KeyGenerator.java:28-72
+//   typed writers            broker-core/.../logstreams/processor/TypedCommandWriterImpl.java:85-143,
+//                            TypedStreamWriterImpl.java:44-152 (a non-batch writer keeps only its last record)
+//   transformer              broker-core/.../workflow/model/transformation/** + bpmn-model/.../traversal/ModelWalker.java:53-69
+//   record values            broker-core/.../workflow/data/WorkflowInstanceRecord.java:39-60,
+//                            broker-core/.../job/data/{JobRecord,JobHeaders}.java, broker-core/.../incident/data/IncidentRecord.java
+//   canonical job harness    broker-core/src/test/java/io/zeebe/broker/util/TestStreams.java:112-142 and
+//                            broker-core/src/test/.../workflow/processor/WorkflowInstanceStreamProcessorTest.java:206-211
+//                            (JOB CREATE command at its FIFO position -> JOB CREATED(k), JOB COMPLETED(k); job keys
+//                            from KeyGenerator(2, 5))
+// Positions are log sequence numbers (0-based record index); byte positions of the real log are out of scope.
+#include <chrono>
+#include <cstdio>
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "zbref_el.hpp"
+#include "zbref_mapping.hpp"
+#include "zbref_xml.hpp"
+
+namespace zbref {
+
+// ------------------------------------------------------------------------------ protocol enums
+enum ValueType : uint8_t { VT_JOB = 0, VT_WORKFLOW_INSTANCE = 5, VT_INCIDENT = 6, VT_MESSAGE = 10,
+                           VT_MESSAGE_SUBSCRIPTION = 11, VT_WORKFLOW_INSTANCE_SUBSCRIPTION = 12 };
+enum RecordType : uint8_t { RT_EVENT = 0, RT_COMMAND = 1, RT_REJECTION = 2 };
+enum WfIntent : uint8_t {
+  CREATE = 0, CREATED = 1, START_EVENT_OCCURRED = 2, END_EVENT_OCCURRED = 3, SEQUENCE_FLOW_TAKEN = 4,
+  GATEWAY_ACTIVATED = 5, ELEMENT_READY = 6, ELEMENT_ACTIVATED = 7, ELEMENT_COMPLETING = 8, ELEMENT_COMPLETED = 9,
+  ELEMENT_TERMINATING = 10, ELEMENT_TERMINATED = 11, CANCEL = 12, CANCELING = 13, UPDATE_PAYLOAD = 14,
+  PAYLOAD_UPDATED = 15
+};
+enum JobIntentE : uint8_t { JOB_CREATE = 0, JOB_CREATED = 1, JOB_COMPLETED = 5, JOB_CANCEL = 12 };
+enum IncidentIntentE : uint8_t { INCIDENT_CREATE = 0 };
+enum WisIntent : uint8_t { WIS_CORRELATE = 2, WIS_CORRELATED = 3 };
+enum RejectionTypeE : uint8_t { REJ_BAD_VALUE = 0, REJ_NOT_APPLICABLE = 1, REJ_PROCESSING_ERROR = 2, REJ_NULL = 255 };
+enum ErrorTypeE : uint8_t { ERR_UNKNOWN = 0, ERR_IO_MAPPING = 1, ERR_JOB_NO_RETRIES = 2, ERR_CONDITION = 3 };
+
+static const char* ERROR_TYPE_NAMES[] = {"UNKNOWN", "IO_MAPPING_ERROR", "JOB_NO_RETRIES", "CONDITION_ERROR"};
+
+// BpmnStep.java:20-54
+enum Step : uint8_t {
+  S_NONE = 0, S_TAKE_SEQUENCE_FLOW, S_CONSUME_TOKEN, S_EXCLUSIVE_SPLIT, S_CREATE_JOB, S_APPLY_INPUT_MAPPING,
+  S_APPLY_OUTPUT_MAPPING, S_ACTIVATE_GATEWAY, S_SUBSCRIBE_TO_INTERMEDIATE_MESSAGE, S_START_STATEFUL_ELEMENT,
+  S_TRIGGER_END_EVENT, S_TRIGGER_START_EVENT, S_TERMINATE_CONTAINED_INSTANCES, S_TERMINATE_JOB_TASK,
+  S_TERMINATE_ELEMENT, S_PROPAGATE_TERMINATION, S_CANCEL_PROCESS, S_COMPLETE_PROCESS, S_UNBOUND = 255
+};
+
+static const bytes EMPTY_DOCUMENT = bytes("\x80", 1);
+
+// ------------------------------------------------------------------------------ record values
+struct WfValue {  // WorkflowInstanceRecord.java:39-60
+  bytes bpmn_process_id;
+  int32_t version = -1;
+  int64_t workflow_key = -1;
+  int64_t workflow_instance_key = -1;
+  bytes activity_id;
+  bytes payload = EMPTY_DOCUMENT;
+  int64_t scope_instance_key = -1;
+  void set_payload(const bytes& p) {  // DocumentValue.wrap: nil / empty -> {}
+    if (p.empty() || (p.size() == 1 && (uint8_t)p[0] == 0xc0)) payload = EMPTY_DOCUMENT;
+    else {
+      if (mp_format_type((uint8_t)p[0]) != MpType::MAP)
+        throw ZbError("Document has invalid format. On root level an object is only allowed.");
+      payload = p;
+    }
+  }
+  bytes encode() const {
+    MpWriter w;
+    w.map_header(7);
+    w.str("bpmnProcessId"); w.str(bpmn_process_id);
+    w.str("version"); w.integer(version);
+    w.str("workflowKey"); w.integer(workflow_key);
+    w.str("workflowInstanceKey"); w.integer(workflow_instance_key);
+    w.str("activityId"); w.str(activity_id);
+    w.str("payload"); w.bin(payload);
+    w.str("scopeInstanceKey"); w.integer(scope_instance_key);
+    return w.b;
+  }
+};
+
+struct JobValue {  // JobRecord.java:35-53 + JobHeaders.java:33-51
+  int64_t deadline = INT64_MIN;  // Protocol.INSTANT_NULL_VALUE
+  bytes worker;
+  int32_t retries = -1;
+  bytes type;
+  bytes h_bpmn_process_id;
+  int32_t h_version = -1;
+  int64_t h_workflow_key = -1;
+  int64_t h_workflow_instance_key = -1;
+  bytes h_activity_id;
+  int64_t h_activity_instance_key = -1;
+  bytes custom_headers = EMPTY_DOCUMENT;  // PackedProperty, written raw
+  bytes payload = EMPTY_DOCUMENT;
+  bytes encode() const {
+    MpWriter w;
+    w.map_header(7);
+    w.str("deadline"); w.integer(deadline);
+    w.str("worker"); w.str(worker);
+    w.str("retries"); w.integer(retries);
+    w.str("type"); w.str(type);
+    w.str("headers");
+    w.map_header(6);
+    w.str("bpmnProcessId"); w.str(h_bpmn_process_id);
+    w.str("workflowDefinitionVersion"); w.integer(h_version);
+    w.str("workflowKey"); w.integer(h_workflow_key);
+    w.str("workflowInstanceKey"); w.integer(h_workflow_instance_key);
+    w.str("activityId"); w.str(h_activity_id);
+    w.str("activityInstanceKey"); w.integer(h_activity_instance_key);
+    w.str("customHeaders"); w.raw(custom_headers);
+    w.str("payload"); w.bin(payload);
+    return w.b;
+  }
+};
+
+struct IncidentValue {  // IncidentRecord.java
+  uint8_t error_type = ERR_UNKNOWN;
+  bytes error_message;
+  int64_t failure_event_position = -1;
+  bytes bpmn_process_id;
+  int64_t workflow_instance_key = -1;
+  bytes activity_id;
+  int64_t activity_instance_key = -1;
+  int64_t job_key = -1;
+  bytes payload = EMPTY_DOCUMENT;
+  bytes encode() const {
+    MpWriter w;
+    w.map_header(9);
+    w.str("errorType"); w.str(ERROR_TYPE_NAMES[error_type]);
+    w.str("errorMessage"); w.str(error_message);
+    w.str("failureEventPosition"); w.integer(failure_event_position);
+    w.str("bpmnProcessId"); w.str(bpmn_process_id);
+    w.str("workflowInstanceKey"); w.integer(workflow_instance_key);
+    w.str("activityId"); w.str(activity_id);
+    w.str("activityInstanceKey"); w.integer(activity_instance_key);
+    w.str("jobKey"); w.integer(job_key);
+    w.str("payload"); w.bin(payload);
+    return w.b;
+  }
+};
+
+struct WisValue {  // WorkflowInstanceSubscriptionRecord (subscription/message/data)
+  int32_t partition_id = 0;
+  int64_t workflow_instance_key = -1;
+  int64_t activity_instance_key = -1;
+  bytes message_name;
+  bytes payload = EMPTY_DOCUMENT;
+  bytes encode() const {
+    MpWriter w;
+    w.map_header(5);
+    w.str("partitionId"); w.integer(partition_id);
+    w.str("workflowInstanceKey"); w.integer(workflow_instance_key);
+    w.str("activityInstanceKey"); w.integer(activity_instance_key);
+    w.str("messageName"); w.str(message_name);
+    w.str("payload"); w.bin(payload);
+    return w.b;
+  }
+};
+
+struct Record {
+  int64_t position = 0;
+  int64_t source_position = -1;
+  int64_t key = -1;
+  uint8_t record_type = RT_EVENT;
+  uint8_t value_type = VT_WORKFLOW_INSTANCE;
+  uint8_t intent = 0;
+  uint8_t rejection_type = REJ_NULL;
+  std::string rejection_reason;
+  WfValue wf;
+  JobValue job;
+  IncidentValue inc;
+  WisValue wis;
+  bytes encode_value() const {
+    switch (value_type) {
+      case VT_WORKFLOW_INSTANCE: return wf.encode();
+      case VT_JOB: return job.encode();
+      case VT_INCIDENT: return inc.encode();
+      case VT_WORKFLOW_INSTANCE_SUBSCRIPTION: return wis.encode();
+    }
+    return bytes();
+  }
+};
+
+// ------------------------------------------------------------------------------ executable model
+enum ElemKind : uint8_t { K_PROCESS, K_START_EVENT, K_END_EVENT, K_SERVICE_TASK, K_SUB_PROCESS,
+                          K_EXCLUSIVE_GATEWAY, K_INTERMEDIATE_CATCH, K_SEQUENCE_FLOW };
+
+struct Element {
+  ElemKind kind;
+  bytes id;
+  std::map<uint8_t, uint8_t> steps;  // intent -> BpmnStep (EnumMap)
+  std::vector<Element*> outgoing;    // executable (walk) order
+  std::vector<Element*> outgoing_with_condition;
+  Element* default_flow = nullptr;
+  Element* target = nullptr;         // sequence flow
+  Element* start_event = nullptr;    // containers
+  std::shared_ptr<CompiledCondition> condition;
+  bytes job_type;
+  int32_t retries = 3;
+  bytes encoded_headers = EMPTY_DOCUMENT;  // JobRecord.NO_HEADERS
+  bytes message_name;
+  JsonPathQuery correlation_key;
+  bool has_io_mapping = false;
+  uint8_t get_step(uint8_t intent) const {
+    auto it = steps.find(intent);
+    return it == steps.end() ? S_UNBOUND : it->second;
+  }
+};
+
+struct Workflow {
+  int64_t key;
+  int32_t version;
+  bytes bpmn_process_id;
+  std::vector<std::unique_ptr<Element>> storage;
+  std::unordered_map<bytes, Element*> by_id;
+  Element* process = nullptr;
+  Element* get(const bytes& id) const {
+    auto it = by_id.find(id);
+    return it == by_id.end() ? nullptr : it->second;
+  }
+};
+
+// ------------------------------------------------------------------------------ transformer
+// BpmnTransformer.java:52-83: two ModelWalker passes; each node's handlers run supertype-first
+// (TypeHierarchyVisitor.java:34-41).
+class Transformer {
+ public:
+  std::vector<std::unique_ptr<Workflow>> transform(const XmlNode& doc) {
+    const XmlNode* defs = nullptr;
+    for (auto& c : doc.children)
+      if (c->name == "definitions") defs = c.get();
+    if (!defs) throw ZbError("no definitions element");
+    defs_ = defs;
+    walk(defs, 1);
+    walk(defs, 2);
+    return std::move(workflows_);
+  }
+
+ private:
+  const XmlNode* defs_ = nullptr;
+  std::vector<std::unique_ptr<Workflow>> workflows_;
+  Workflow* current_ = nullptr;
+  uint8_t current_outgoing_step_ = S_NONE;
+
+  static bool is_flow_node(const std::string& n) {
+    return n == "startEvent" || n == "endEvent" || n == "serviceTask" || n == "subProcess" ||
+           n == "exclusiveGateway" || n == "intermediateCatchEvent" || n == "parallelGateway" || n == "task" ||
+           n == "userTask" || n == "receiveTask" || n == "sendTask" || n == "scriptTask" ||
+           n == "businessRuleTask" || n == "manualTask" || n == "callActivity" || n == "inclusiveGateway" ||
+           n == "eventBasedGateway" || n == "complexGateway" || n == "intermediateThrowEvent" ||
+           n == "boundaryEvent" || n == "transaction";
+  }
+  static bool is_flow_element(const std::string& n) { return is_flow_node(n) || n == "sequenceFlow"; }
+  static bool is_activity(const std::string& n) {
+    return n == "serviceTask" || n == "subProcess" || n == "task" || n == "userTask" || n == "receiveTask" ||
+           n == "sendTask" || n == "scriptTask" || n == "businessRuleTask" || n == "manualTask" ||
+           n == "callActivity" || n == "transaction";
+  }
+
+  // ModelWalker.walk: children pushed with addFirst => siblings visited last-to-first
+  void walk(const XmlNode* root, int pass) {
+    std::deque<const XmlNode*> todo{root};
+    while (!todo.empty()) {
+      const XmlNode* n = todo.front();
+      todo.pop_front();
+      visit(n, pass);
+      for (auto& c : n->children) todo.push_front(c.get());
+    }
+  }
+
+  static std::vector<const XmlNode*> kids(const XmlNode* n, const char* name) {
+    std::vector<const XmlNode*> out;
+    for (auto& c : n->children)
+      if (c->name == name) out.push_back(c.get());
+    return out;
+  }
+  static const XmlNode* ext(const XmlNode* n, const char* name) {
+    for (auto* e : kids(n, "extensionElements"))
+      for (auto& c : e->children)
+        if (c->name == name) return c.get();
+    return nullptr;
+  }
+  static std::string id_of(const XmlNode* n) {
+    const std::string* a = n->attr("id");
+    return a ? *a : std::string();
+  }
+
+  void visit(const XmlNode* n, int pass) {
+    const std::string& nm = n->name;
+    if (pass == 1) {
+      if (nm == "process") {  // CreateWorkflowHandler
+        auto wf = std::make_unique<Workflow>();
+        wf->bpmn_process_id = id_of(n);
+        auto e = std::make_unique<Element>();
+        e->kind = K_PROCESS;
+        e->id = wf->bpmn_process_id;
+        wf->process = e.get();
+        wf->by_id[e->id] = e.get();
+        wf->storage.push_back(std::move(e));
+        current_ = wf.get();
+        workflows_.push_back(std::move(wf));
+      } else if (is_flow_element(nm)) {  // FlowElementHandler: ELEMENT_FACTORIES
+        ElemKind k;
+        if (nm == "endEvent") k = K_END_EVENT;
+        else if (nm == "exclusiveGateway") k = K_EXCLUSIVE_GATEWAY;
+        else if (nm == "intermediateCatchEvent") k = K_INTERMEDIATE_CATCH;
+        else if (nm == "sequenceFlow") k = K_SEQUENCE_FLOW;
+        else if (nm == "serviceTask") k = K_SERVICE_TASK;
+        else if (nm == "startEvent") k = K_START_EVENT;
+        else if (nm == "subProcess") k = K_SUB_PROCESS;
+        else throw ZbError("unsupported element type: " + nm);  // factory lookup returns null (NPE)
+        auto e = std::make_unique<Element>();
+        e->kind = k;
+        e->id = id_of(n);
+        current_->by_id[e->id] = e.get();
+        current_->storage.push_back(std::move(e));
+      }
+      return;
+    }
+    // pass 2
+    if (nm == "process") {  // ProcessHandler
+      for (auto& w : workflows_)
+        if (w->bpmn_process_id == id_of(n)) current_ = w.get();
+      Element* p = current_->process;
+      p->steps[ELEMENT_READY] = S_APPLY_INPUT_MAPPING;
+      p->steps[ELEMENT_ACTIVATED] = S_TRIGGER_START_EVENT;
+      p->steps[ELEMENT_COMPLETING] = S_COMPLETE_PROCESS;
+      p->steps[ELEMENT_TERMINATING] = S_TERMINATE_CONTAINED_INSTANCES;
+      return;
+    }
+    if (!is_flow_element(nm)) return;
+    Element* e = current_->get(id_of(n));
+    if (nm == "sequenceFlow") {  // SequenceFlowHandler
+      const std::vector<const XmlNode*> conds = kids(n, "conditionExpression");
+      if (!conds.empty()) {
+        auto c = std::make_shared<CompiledCondition>(create_condition(conds[0]->text));
+        e->condition = c;
+      }
+      const std::string* sref = n->attr("sourceRef");
+      const std::string* tref = n->attr("targetRef");
+      Element* src = sref ? current_->get(*sref) : nullptr;
+      Element* tgt = tref ? current_->get(*tref) : nullptr;
+      if (!src || !tgt) throw ZbError("sequence flow with unknown source/target");
+      src->outgoing.push_back(e);
+      if (src->kind == K_EXCLUSIVE_GATEWAY && e->condition) src->outgoing_with_condition.push_back(e);
+      e->target = tgt;
+      uint8_t step;
+      if (tgt->kind == K_SERVICE_TASK || tgt->kind == K_SUB_PROCESS || tgt->kind == K_INTERMEDIATE_CATCH)
+        step = S_START_STATEFUL_ELEMENT;
+      else if (tgt->kind == K_EXCLUSIVE_GATEWAY) step = S_ACTIVATE_GATEWAY;
+      else if (tgt->kind == K_END_EVENT) step = S_TRIGGER_END_EVENT;
+      else throw ZbError("Unsupported element");
+      e->steps[SEQUENCE_FLOW_TAKEN] = step;
+      return;
+    }
+    // FlowNodeHandler (supertype first)
+    {
+      const XmlNode* io = ext(n, "ioMapping");
+      if (io) e->has_io_mapping = true;
+      size_t n_out = kids(n, "outgoing").size();  // FlowNode.getOutgoing(): <outgoing> references
+      current_outgoing_step_ = n_out == 0 ? S_CONSUME_TOKEN : S_TAKE_SEQUENCE_FLOW;
+    }
+    if (is_activity(nm)) {  // ActivityHandler
+      e->steps[ELEMENT_READY] = S_APPLY_INPUT_MAPPING;
+      e->steps[ELEMENT_COMPLETING] = S_APPLY_OUTPUT_MAPPING;
+      e->steps[ELEMENT_COMPLETED] = current_outgoing_step_;
+      e->steps[ELEMENT_TERMINATED] = S_PROPAGATE_TERMINATION;
+    }
+    if (nm == "endEvent") {
+      e->steps[END_EVENT_OCCURRED] = current_outgoing_step_;
+    } else if (nm == "startEvent") {
+      const XmlNode* scope = n->parent;
+      if (scope->name == "subProcess") current_->get(id_of(scope))->start_event = e;
+      else current_->process->start_event = e;
+      e->steps[START_EVENT_OCCURRED] = current_outgoing_step_;
+    } else if (nm == "exclusiveGateway") {
+      const std::string* def = n->attr("default");
+      if (def) e->default_flow = current_->get(*def);
+      // bind: EXCLUSIVE_SPLIT iff the first *model-order* outgoing flow has a condition
+      std::vector<const XmlNode*> outs = kids(n, "outgoing");
+      bool first_has_cond = false;
+      if (!outs.empty()) {
+        std::string fid = outs[0]->text;
+        // trim whitespace of the reference text
+        while (!fid.empty() && (fid.back() == ' ' || fid.back() == '\n' || fid.back() == '\r' || fid.back() == '\t')) fid.pop_back();
+        size_t b = 0;
+        while (b < fid.size() && (fid[b] == ' ' || fid[b] == '\n' || fid[b] == '\r' || fid[b] == '\t')) b++;
+        fid = fid.substr(b);
+        const XmlNode* flow = find_by_id(defs_, fid);
+        first_has_cond = flow && !kids(flow, "conditionExpression").empty();
+      }
+      e->steps[GATEWAY_ACTIVATED] = first_has_cond ? S_EXCLUSIVE_SPLIT : current_outgoing_step_;
+    } else if (nm == "serviceTask") {
+      const XmlNode* td = ext(n, "taskDefinition");
+      if (td) {
+        if (const std::string* t = td->attr("type")) e->job_type = *t;
+        if (const std::string* r = td->attr("retries")) e->retries = std::stoi(*r);
+      }
+      const XmlNode* th = ext(n, "taskHeaders");
+      if (th) {
+        std::vector<const XmlNode*> hs = kids(th, "header");
+        if (hs.empty()) e->encoded_headers = bytes();  // UnsafeBuffer(0,0)
+        else {
+          MpWriter w;
+          w.map_header((uint32_t)hs.size());
+          for (auto* h : hs) {
+            w.str(h->attr("key") ? *h->attr("key") : std::string());
+            w.str(h->attr("value") ? *h->attr("value") : std::string());
+          }
+          e->encoded_headers = w.b;
+        }
+      }
+      e->steps[ELEMENT_ACTIVATED] = S_CREATE_JOB;
+      e->steps[ELEMENT_TERMINATING] = S_TERMINATE_JOB_TASK;
+    } else if (nm == "subProcess") {
+      e->steps[ELEMENT_ACTIVATED] = S_TRIGGER_START_EVENT;
+      e->steps[ELEMENT_TERMINATING] = S_TERMINATE_CONTAINED_INSTANCES;
+    } else if (nm == "intermediateCatchEvent") {
+      std::vector<const XmlNode*> defsv = kids(n, "messageEventDefinition");
+      if (defsv.empty()) throw ZbError("intermediate catch event without message");
+      const std::string* mref = defsv[0]->attr("messageRef");
+      const XmlNode* msg = mref ? find_by_id(defs_, *mref) : nullptr;
+      if (!msg) throw ZbError("message not found");
+      const XmlNode* sub = ext(msg, "subscription");
+      JsonPathCompiler jc;
+      e->correlation_key = jc.compile(sub && sub->attr("correlationKey") ? *sub->attr("correlationKey") : "");
+      e->message_name = msg->attr("name") ? *msg->attr("name") : std::string();
+      e->steps[ELEMENT_READY] = S_APPLY_INPUT_MAPPING;
+      e->steps[ELEMENT_ACTIVATED] = S_SUBSCRIBE_TO_INTERMEDIATE_MESSAGE;
+      e->steps[ELEMENT_COMPLETING] = S_APPLY_OUTPUT_MAPPING;
+      e->steps[ELEMENT_COMPLETED] = current_outgoing_step_;
+      e->steps[ELEMENT_TERMINATING] = S_TERMINATE_ELEMENT;
+      e->steps[ELEMENT_TERMINATED] = S_PROPAGATE_TERMINATION;
+    }
+  }
+
+  static const XmlNode* find_by_id(const XmlNode* n, const std::string& id) {
+    const std::string* a = n->attr("id");
+    if (a && *a == id) return n;
+    for (auto& c : n->children)
+      if (const XmlNode* f = find_by_id(c.get(), id)) return f;
+    return nullptr;
+  }
+};
+
+// ------------------------------------------------------------------------------ index
+struct ElementInstance {  // ElementInstance.java:30-111
+  int64_t key;
+  ElementInstance* parent;
+  uint8_t state;
+  WfValue value;
+  std::vector<ElementInstance*> children;
+  int64_t job_key = 0;
+};
+
+struct ElementInstanceIndex {  // ElementInstanceIndex.java:25-65
+  std::unordered_map<int64_t, std::unique_ptr<ElementInstance>> instances;
+  ElementInstance* new_instance(ElementInstance* parent, int64_t key, const WfValue& v, uint8_t state) {
+    auto ei = std::make_unique<ElementInstance>();
+    ei->key = key;
+    ei->parent = parent;
+    if (parent) parent->children.push_back(ei.get());
+    ei->state = state;
+    ei->value = v;
+    ElementInstance* raw = ei.get();
+    auto it = instances.find(key);
+    if (it != instances.end()) graveyard.push_back(std::move(it->second));  // replaced object stays referenced
+    instances[key] = std::move(ei);
+    return raw;
+  }
+  ElementInstance* get(int64_t key) {
+    auto it = instances.find(key);
+    return it == instances.end() ? nullptr : it->second.get();
+  }
+  void remove(int64_t key) {
+    auto it = instances.find(key);
+    if (it == instances.end()) return;
+    ElementInstance* ei = it->second.get();
+    if (ei->parent) {
+      auto& ch = ei->parent->children;
+      for (size_t i = 0; i < ch.size(); i++)
+        if (ch[i] == ei) { ch.erase(ch.begin() + i); break; }
+    }
+    graveyard.push_back(std::move(it->second));  // children may still point at it
+    instances.erase(it);
+  }
+  std::vector<std::unique_ptr<ElementInstance>> graveyard;
+};
+
+struct KeyGenerator {  // KeyGenerator.java:28-56
+  int64_t next;
+  int64_t step;
+  int64_t next_key() { int64_t k = next; next += step; return k; }
+};
+
+// A side effect emitted by the engine (response / message-subscription open).
+struct SideEffect {
+  int kind;  // 1 = open message subscription
+  int64_t workflow_instance_key;
+  int64_t activity_instance_key;
+  bytes message_name;
+  bytes correlation_key;
+  int32_t partition;  // target partition (abs(hash % P))
+};
+
+// ------------------------------------------------------------------------------ engine
+class Engine {
+ public:
+  int partition_id = 0;
+  int partition_count = 1;
+  std::vector<Record> log;
+  std::vector<SideEffect> side_effects;
+  KeyGenerator wf_keys{1, 5};
+  KeyGenerator job_keys{2, 5};
+  ElementInstanceIndex index;
+  std::vector<std::unique_ptr<Workflow>> workflows;
+  std::map<std::pair<int64_t, bytes>, bytes> job_payloads;  // (workflow key, activity id) -> completion payload
+  int64_t created = 0, completed = 0, canceled = 0;
+  size_t processed = 0;
+  std::string last_error;
+
+  void deploy(const std::string& xml, int64_t key, int32_t version) {
+    XmlReader xr;
+    auto doc = xr.parse(xml);
+    Transformer tr;
+    auto wfs = tr.transform(*doc);
+    int64_t k = key;
+    for (auto& w : wfs) {
+      for (auto& e : w->storage) {
+        if (e->has_io_mapping) throw ZbError("io mappings are not supported by the oracle yet");
+        if (e->condition && !e->condition->valid) throw ZbError("invalid condition: " + e->condition->error);
+      }
+      w->key = k++;
+      w->version = version;
+      workflows.push_back(std::move(w));
+    }
+  }
+
+  Workflow* by_key(int64_t key) {
+    for (auto& w : workflows)
+      if (w->key == key) return w.get();
+    return nullptr;
+  }
+  Workflow* by_id_version(const bytes& id, int32_t v) {
+    for (auto& w : workflows)
+      if (w->bpmn_process_id == id && w->version == v) return w.get();
+    return nullptr;
+  }
+  Workflow* latest(const bytes& id) {
+    Workflow* best = nullptr;
+    for (auto& w : workflows)
+      if (w->bpmn_process_id == id && (!best || w->version > best->version)) best = w.get();
+    return best;
+  }
+
+  void append(Record r) {
+    r.position = (int64_t)log.size();
+    log.push_back(std::move(r));
+  }
+
+  void submit_create(const bytes& process_id, int32_t version, int64_t workflow_key, const bytes& payload) {
+    Record r;
+    r.record_type = RT_COMMAND;
+    r.value_type = VT_WORKFLOW_INSTANCE;
+    r.intent = CREATE;
+    r.key = -1;
+    r.wf.bpmn_process_id = process_id;
+    r.wf.version = version;
+    r.wf.workflow_key = workflow_key;
+    r.wf.set_payload(payload);
+    append(std::move(r));
+  }
+  void submit_cancel(int64_t key) {
+    Record r;
+    r.record_type = RT_COMMAND;
+    r.intent = CANCEL;
+    r.key = key;
+    append(std::move(r));
+  }
+  void submit_correlate(int64_t wf_instance_key, int64_t activity_instance_key, const bytes& name,
+                        const bytes& payload) {
+    Record r;
+    r.record_type = RT_COMMAND;
+    r.value_type = VT_WORKFLOW_INSTANCE_SUBSCRIPTION;
+    r.intent = WIS_CORRELATE;
+    r.key = -1;
+    r.wis.partition_id = partition_id;
+    r.wis.workflow_instance_key = wf_instance_key;
+    r.wis.activity_instance_key = activity_instance_key;
+    r.wis.message_name = name;
+    r.wis.payload = payload.empty() ? EMPTY_DOCUMENT : payload;
+    append(std::move(r));
+  }
+
+  size_t run(size_t max_records = SIZE_MAX) {
+    size_t n = 0;
+    while (processed < log.size() && n < max_records) {
+      process(processed);
+      processed++;
+      n++;
+    }
+    return n;
+  }
+
+  // ---- typed writer (TypedStreamWriterImpl / TypedCommandWriterImpl) for one processed record
+  struct Writer {
+    Engine* eng;
+    bool batch = false;
+    std::vector<Record> staged;
+    void stage(Record r) {
+      if (batch) staged.push_back(std::move(r));
+      else { staged.clear(); staged.push_back(std::move(r)); }
+    }
+    void new_batch() { batch = true; staged.clear(); }
+  };
+
+ private:
+  Writer* w_ = nullptr;
+  ElInterpreter interp_;
+  JsonPathExecutor jp_;
+
+  // ElementInstanceWriter.writeNewEvent :64-84
+  int64_t write_new_wf_event(uint8_t intent, const WfValue& v) {
+    int64_t key = wf_keys.next_key();
+    Record r;
+    r.key = key; r.record_type = RT_EVENT; r.value_type = VT_WORKFLOW_INSTANCE; r.intent = intent; r.wf = v;
+    w_->stage(std::move(r));
+    if (intent == ELEMENT_READY) {
+      if (v.scope_instance_key >= 0) index.new_instance(index.get(v.scope_instance_key), key, v, intent);
+      else index.new_instance(nullptr, key, v, intent);
+    }
+    return key;
+  }
+  // ElementInstanceWriter.writeFollowUpEvent :86-110
+  void write_followup_wf_event(int64_t key, uint8_t intent, const WfValue& v) {
+    Record r;
+    r.key = key; r.record_type = RT_EVENT; r.value_type = VT_WORKFLOW_INSTANCE; r.intent = intent; r.wf = v;
+    w_->stage(std::move(r));
+    if (intent == ELEMENT_COMPLETED || intent == ELEMENT_TERMINATED) {
+      index.remove(key);
+    } else {
+      ElementInstance* ei = index.get(key);
+      if (!ei) throw ZbError("NullPointerException: no element instance for follow-up event");
+      ei->state = intent;
+      ei->value = v;
+    }
+    if (key == v.workflow_instance_key) {
+      if (intent == ELEMENT_TERMINATED) canceled++;
+      else if (intent == ELEMENT_COMPLETED) completed++;
+    }
+  }
+  // plain TypedStreamWriter.writeFollowUpEvent (no index side effects)
+  void stage_event(int64_t key, uint8_t vt, uint8_t intent, const Record& proto) {
+    Record r = proto;
+    r.key = key; r.record_type = RT_EVENT; r.value_type = vt; r.intent = intent;
+    w_->stage(std::move(r));
+  }
+  void write_rejection(const Record& cmd, uint8_t type, const std::string& reason) {
+    Record r = cmd;
+    r.record_type = RT_REJECTION;
+    r.rejection_type = type;
+    r.rejection_reason = reason;
+    w_->stage(std::move(r));
+  }
+
+  // BpmnStepContext.raiseIncident :141-162
+  void raise_incident(const Record& rec, uint8_t error_type, const std::string& msg) {
+    Record r;
+    r.key = -1; r.record_type = RT_COMMAND; r.value_type = VT_INCIDENT; r.intent = INCIDENT_CREATE;
+    r.inc.error_type = error_type;
+    r.inc.error_message = msg;
+    r.inc.failure_event_position = rec.position;
+    r.inc.activity_instance_key = rec.key;
+    r.inc.bpmn_process_id = rec.wf.bpmn_process_id;
+    r.inc.workflow_instance_key = rec.wf.workflow_instance_key;
+    r.inc.activity_id = rec.wf.activity_id;
+    w_->stage(std::move(r));
+  }
+
+  void process(size_t pos) {
+    const Record rec = log[pos];  // copy: the log grows while processing
+    Writer w{this};
+    w_ = &w;
+    try {
+      dispatch(rec);
+    } catch (const ZbError& e) {
+      // StreamProcessorController.onFailure: the partition stops processing
+      last_error = std::string("processing failed at position ") + std::to_string(pos) + ": " + e.what();
+      throw;
+    }
+    w_ = nullptr;
+    for (auto& r : w.staged) {
+      r.source_position = rec.position;
+      append(std::move(r));
+    }
+  }
+
+  void dispatch(const Record& rec) {
+    if (rec.value_type == VT_WORKFLOW_INSTANCE) {
+      if (rec.record_type == RT_COMMAND) {
+        if (rec.intent == CREATE) process_create(rec);
+        else if (rec.intent == CANCEL) process_cancel(rec);
+        else if (rec.intent == UPDATE_PAYLOAD) process_update_payload(rec);
+      } else if (rec.record_type == RT_EVENT) {
+        switch (rec.intent) {
+          case CREATED:  // WorkflowInstanceCreatedEventProcessor :380-394
+            created++;
+            index.new_instance(nullptr, rec.key, rec.wf, ELEMENT_READY);
+            break;
+          case SEQUENCE_FLOW_TAKEN: case ELEMENT_READY: case ELEMENT_ACTIVATED: case ELEMENT_COMPLETING:
+          case START_EVENT_OCCURRED: case END_EVENT_OCCURRED: case GATEWAY_ACTIVATED: case ELEMENT_COMPLETED:
+          case ELEMENT_TERMINATING: case ELEMENT_TERMINATED:
+            bpmn_step(rec);
+            break;
+          default: break;
+        }
+      }
+    } else if (rec.value_type == VT_JOB) {
+      if (rec.record_type == RT_COMMAND && rec.intent == JOB_CREATE) harness_job_create(rec);
+      else if (rec.record_type == RT_EVENT && rec.intent == JOB_CREATED) process_job_created(rec);
+      else if (rec.record_type == RT_EVENT && rec.intent == JOB_COMPLETED) process_job_completed(rec);
+    } else if (rec.value_type == VT_WORKFLOW_INSTANCE_SUBSCRIPTION) {
+      if (rec.record_type == RT_COMMAND && rec.intent == WIS_CORRELATE) process_correlate(rec);
+    }
+  }
+
+  // CreateWorkflowInstanceEventProcessor :224-368 (all workflows are deployed locally; a miss
+  // rejects with BAD_VALUE "Workflow is not deployed" as after a failed fetch)
+  void process_create(const Record& cmd) {
+    Record c = cmd;
+    int64_t instance_key = wf_keys.next_key();
+    c.wf.workflow_instance_key = instance_key;
+    Workflow* wf = nullptr;
+    if (c.wf.workflow_key <= 0) {
+      if (c.wf.version > 0) {
+        wf = by_id_version(c.wf.bpmn_process_id, c.wf.version);
+        if (wf) c.wf.workflow_key = wf->key;
+      } else {
+        wf = latest(c.wf.bpmn_process_id);
+        if (wf) { c.wf.workflow_key = wf->key; c.wf.version = wf->version; }
+      }
+    } else {
+      wf = by_key(c.wf.workflow_key);
+      if (wf) { c.wf.version = wf->version; c.wf.bpmn_process_id = wf->bpmn_process_id; }
+    }
+    if (!wf) {
+      write_rejection(c, REJ_BAD_VALUE, "Workflow is not deployed");
+      return;
+    }
+    c.wf.activity_id = c.wf.bpmn_process_id;
+    w_->new_batch();
+    Record a; a.key = instance_key; a.record_type = RT_EVENT; a.value_type = VT_WORKFLOW_INSTANCE;
+    a.intent = CREATED; a.wf = c.wf;
+    w_->stage(a);
+    a.intent = ELEMENT_READY;
+    w_->stage(a);
+  }
+
+  void process_cancel(const Record& cmd) {  // CancelWorkflowInstanceProcessor :511-555
+    ElementInstance* wi = index.get(cmd.key);
+    bool can = wi && (wi->state == ELEMENT_READY || wi->state == ELEMENT_ACTIVATED || wi->state == ELEMENT_COMPLETING);
+    if (!can) {
+      write_rejection(cmd, REJ_NOT_APPLICABLE, "Workflow instance is not running");
+      return;
+    }
+    WfValue v = wi->value;
+    v.payload = EMPTY_DOCUMENT;
+    w_->new_batch();
+    Record a; a.key = cmd.key; a.record_type = RT_EVENT; a.value_type = VT_WORKFLOW_INSTANCE; a.wf = v;
+    a.intent = CANCELING; w_->stage(a);
+    a.intent = ELEMENT_TERMINATING; w_->stage(a);
+    wi->state = ELEMENT_TERMINATING;
+  }
+
+  void process_update_payload(const Record& cmd) {  // UpdatePayloadProcessor :557-576
+    ElementInstance* wi = index.get(cmd.wf.workflow_instance_key);
+    if (wi) {
+      wi->value.set_payload(cmd.wf.payload);
+      Record a = cmd; a.record_type = RT_EVENT; a.intent = PAYLOAD_UPDATED;
+      w_->stage(a);
+    } else {
+      write_rejection(cmd, REJ_NOT_APPLICABLE, "Workflow instance is not running");
+    }
+  }
+
+  void process_job_created(const Record& rec) {  // JobCreatedProcessor :408-426
+    int64_t aik = rec.job.h_activity_instance_key;
+    if (aik > 0) {
+      ElementInstance* ai = index.get(aik);
+      if (ai) ai->job_key = rec.key;
+    }
+  }
+  void process_job_completed(const Record& rec) {  // JobCompletedEventProcessor :428-453
+    int64_t aik = rec.job.h_activity_instance_key;
+    ElementInstance* ai = index.get(aik);
+    if (ai) {
+      WfValue v = ai->value;
+      v.set_payload(rec.job.payload);
+      Record a; a.key = aik; a.record_type = RT_EVENT; a.value_type = VT_WORKFLOW_INSTANCE;
+      a.intent = ELEMENT_COMPLETING; a.wf = v;
+      w_->stage(a);
+      ai->state = ELEMENT_COMPLETING;
+      ai->job_key = -1;
+      ai->value = v;
+    }
+  }
+  void process_correlate(const Record& rec) {  // CorrelateWorkflowInstanceSubscription :455-509
+    ElementInstance* ei = index.get(rec.wis.activity_instance_key);
+    if (!ei) {
+      write_rejection(rec, REJ_NOT_APPLICABLE, "activity is not active anymore");
+      return;
+    }
+    WfValue v = ei->value;
+    v.set_payload(rec.wis.payload);
+    w_->new_batch();
+    Record a = rec; a.record_type = RT_EVENT; a.intent = WIS_CORRELATED;
+    w_->stage(a);
+    Record b; b.key = rec.wis.activity_instance_key; b.record_type = RT_EVENT; b.value_type = VT_WORKFLOW_INSTANCE;
+    b.intent = ELEMENT_COMPLETING; b.wf = v;
+    w_->stage(b);
+    ei->state = ELEMENT_COMPLETING;
+    ei->value = v;
+  }
+
+  // canonical harness: the job processor as a deterministic FIFO participant
+  void harness_job_create(const Record& cmd) {
+    int64_t job_key = job_keys.next_key();
+    w_->new_batch();
+    Record a = cmd;
+    a.key = job_key; a.record_type = RT_EVENT; a.intent = JOB_CREATED;
+    w_->stage(a);
+    Record b = cmd;
+    b.key = job_key; b.record_type = RT_EVENT; b.intent = JOB_COMPLETED;
+    auto it = job_payloads.find({cmd.job.h_workflow_key, cmd.job.h_activity_id});
+    b.job.payload = it == job_payloads.end() ? EMPTY_DOCUMENT : it->second;
+    w_->stage(b);
+  }
+
+  // ---------------------------------------------------------------- BpmnStepProcessor :177-251
+  void bpmn_step(const Record& rec) {
+    Workflow* wf = by_key(rec.wf.workflow_key);
+    if (!wf) throw ZbError("workflow not deployed");
+    Element* el = wf->get(rec.wf.activity_id);
+    ElementInstance* ei = index.get(rec.key);
+    ElementInstance* scope = index.get(rec.wf.scope_instance_key);
+    if (!ei && !scope) return;
+    // step guards :128-150
+    bool ok;
+    switch (rec.intent) {
+      case ELEMENT_READY: case ELEMENT_ACTIVATED: case ELEMENT_COMPLETING:
+        if (!ei) throw ZbError("NullPointerException in noConcurrentTransitionGuard");
+        ok = rec.intent == ei->state; break;
+      case ELEMENT_COMPLETED: case END_EVENT_OCCURRED: case GATEWAY_ACTIVATED: case START_EVENT_OCCURRED:
+      case SEQUENCE_FLOW_TAKEN:
+        ok = scope && scope->state == ELEMENT_ACTIVATED; break;
+      case ELEMENT_TERMINATING: ok = true; break;
+      case ELEMENT_TERMINATED: ok = scope && scope->state == ELEMENT_TERMINATING; break;
+      default: ok = false;
+    }
+    if (!ok) return;
+    if (!el) throw ZbError("NullPointerException: unknown element");
+    uint8_t step = el->get_step(rec.intent);
+    if (step == S_UNBOUND || step == S_NONE) return;
+    handle(step, rec, el, ei, scope, wf);
+  }
+
+  void handle(uint8_t step, const Record& rec, Element* el, ElementInstance* ei, ElementInstance* scope, Workflow* wf) {
+    WfValue v = rec.wf;
+    switch (step) {
+      case S_APPLY_INPUT_MAPPING:  // InputMappingHandler (no mappings)
+        write_followup_wf_event(rec.key, ELEMENT_ACTIVATED, v);
+        break;
+      case S_APPLY_OUTPUT_MAPPING: {  // OutputMappingHandler :42-85 (outputBehavior null => merge)
+        try {
+          bytes merged = merge_documents(v.payload, scope->value.payload);
+          v.set_payload(merged);
+        } catch (const MappingError& e) {
+          raise_incident(rec, ERR_IO_MAPPING, e.what());
+          break;
+        }
+        write_followup_wf_event(rec.key, ELEMENT_COMPLETED, v);
+        break;
+      }
+      case S_CREATE_JOB: {  // CreateJobHandler :33-56
+        Record j;
+        j.key = -1; j.record_type = RT_COMMAND; j.value_type = VT_JOB; j.intent = JOB_CREATE;
+        j.job.type = el->job_type;
+        j.job.retries = el->retries;
+        j.job.payload = v.payload;
+        j.job.h_bpmn_process_id = v.bpmn_process_id;
+        j.job.h_version = v.version;
+        j.job.h_workflow_key = v.workflow_key;
+        j.job.h_workflow_instance_key = v.workflow_instance_key;
+        j.job.h_activity_id = el->id;
+        j.job.h_activity_instance_key = rec.key;
+        j.job.custom_headers = el->encoded_headers;
+        w_->stage(std::move(j));
+        break;
+      }
+      case S_EXCLUSIVE_SPLIT: {  // ExclusiveSplitHandler :38-71
+        Element* chosen = nullptr;
+        try {
+          for (Element* f : el->outgoing_with_condition) {
+            if (interp_.eval(f->condition->root.get(), (const uint8_t*)v.payload.data(), v.payload.size())) {
+              chosen = f;
+              break;
+            }
+          }
+          if (!chosen) chosen = el->default_flow;
+        } catch (const ConditionError& e) {
+          raise_incident(rec, ERR_CONDITION, e.what());
+          break;
+        }
+        if (chosen) {
+          v.activity_id = chosen->id;
+          write_new_wf_event(SEQUENCE_FLOW_TAKEN, v);
+        } else {
+          raise_incident(rec, ERR_CONDITION, "All conditions evaluated to false and no default flow is set.");
+        }
+        break;
+      }
+      case S_CONSUME_TOKEN: {  // ConsumeTokenHandler :30-43
+        WfValue sv = scope->value;
+        sv.payload = v.payload;
+        write_followup_wf_event(v.scope_instance_key, ELEMENT_COMPLETING, sv);
+        break;
+      }
+      case S_TAKE_SEQUENCE_FLOW:  // TakeSequenceFlowHandler :30-38
+        v.activity_id = el->outgoing.at(0)->id;
+        write_new_wf_event(SEQUENCE_FLOW_TAKEN, v);
+        break;
+      case S_ACTIVATE_GATEWAY:
+        v.activity_id = el->target->id;
+        write_new_wf_event(GATEWAY_ACTIVATED, v);
+        break;
+      case S_START_STATEFUL_ELEMENT:
+        v.activity_id = el->target->id;
+        write_new_wf_event(ELEMENT_READY, v);
+        break;
+      case S_TRIGGER_END_EVENT:
+        v.activity_id = el->target->id;
+        write_new_wf_event(END_EVENT_OCCURRED, v);
+        break;
+      case S_TRIGGER_START_EVENT:  // TriggerStartEventHandler :30-39
+        if (!el->start_event) throw ZbError("NullPointerException: container without start event");
+        v.activity_id = el->start_event->id;
+        v.scope_instance_key = rec.key;
+        write_new_wf_event(START_EVENT_OCCURRED, v);
+        break;
+      case S_COMPLETE_PROCESS:  // CompleteProcessHandler :28-35
+        write_followup_wf_event(rec.key, ELEMENT_COMPLETED, v);
+        break;
+      case S_SUBSCRIBE_TO_INTERMEDIATE_MESSAGE: {  // SubscribeMessageHandler :77-141
+        jp_.run(el->correlation_key.filters, (const uint8_t*)v.payload.data(), v.payload.size());
+        if (jp_.results.size() != 1) throw ZbError("Failed to extract correlation-key: no result");
+        MpReader r((const uint8_t*)v.payload.data() + jp_.results[0].position, jp_.results[0].length);
+        MpToken t = r.read_token();
+        bytes ck;
+        if (t.type == MpType::STRING) ck = t.value();
+        else if (t.type == MpType::INTEGER) {
+          ck.resize(8);  // UnsafeBuffer.putLong: native (little endian) byte order
+          uint64_t u = (uint64_t)t.ival;
+          for (int i = 0; i < 8; i++) ck[i] = (char)((u >> (8 * i)) & 0xff);
+        } else throw ZbError("Failed to extract correlation-key: wrong type");
+        int32_t h = 0;  // SubscriptionUtil.getSubscriptionHashCode (signed bytes)
+        for (char c : ck) h = (int32_t)((uint32_t)h * 31u + (uint32_t)(int32_t)(int8_t)c);
+        int32_t part = h % partition_count;
+        if (part < 0) part = -part;
+        side_effects.push_back({1, v.workflow_instance_key, rec.key, el->message_name, ck, part});
+        break;
+      }
+      case S_TERMINATE_ELEMENT:
+      case S_TERMINATE_JOB_TASK: {  // TerminateElementHandler / TerminateServiceTaskHandler
+        w_->new_batch();
+        if (step == S_TERMINATE_JOB_TASK && ei && ei->job_key > 0) {
+          Record j;
+          j.key = ei->job_key; j.record_type = RT_COMMAND; j.value_type = VT_JOB; j.intent = JOB_CANCEL;
+          j.job.type = bytes();
+          j.job.h_bpmn_process_id = v.bpmn_process_id;
+          j.job.h_version = v.version;
+          j.job.h_workflow_instance_key = v.workflow_instance_key;
+          j.job.h_activity_id = v.activity_id;
+          j.job.h_activity_instance_key = ei->key;
+          w_->stage(std::move(j));
+        }
+        write_followup_wf_event(rec.key, ELEMENT_TERMINATED, v);
+        break;
+      }
+      case S_TERMINATE_CONTAINED_INSTANCES: {  // TerminateContainedElementsHandler :31-53
+        if (ei->children.empty()) {
+          write_followup_wf_event(rec.key, ELEMENT_TERMINATED, v);
+        } else {
+          ElementInstance* child = ei->children[0];
+          if (child->state == ELEMENT_READY || child->state == ELEMENT_ACTIVATED || child->state == ELEMENT_COMPLETING)
+            write_followup_wf_event(child->key, ELEMENT_TERMINATING, child->value);
+        }
+        break;
+      }
+      case S_PROPAGATE_TERMINATION:  // PropagateTerminationHandler :29-40
+        if (scope->children.empty()) write_followup_wf_event(scope->key, ELEMENT_TERMINATED, scope->value);
+        break;
+      default:
+        break;
+    }
+    (void)wf;
+  }
+};
+
+}  // namespace zbref
+
+// =============================================================================== C API (ctypes)
+using namespace zbref;
+
+struct zbref_record {
+  int64_t position;
+  int64_t source_position;
+  int64_t key;
+  uint8_t record_type;
+  uint8_t value_type;
+  uint8_t intent;
+  uint8_t rejection_type;
+  uint32_t value_len;
+};
+
+extern "C" {
+
+void* zbref_new(int partition_id, int partition_count) {
+  auto* e = new Engine();
+  e->partition_id = partition_id;
+  e->partition_count = partition_count;
+  return e;
+}
+void zbref_free(void* h) { delete (Engine*)h; }
+
+const char* zbref_last_error(void* h) { return ((Engine*)h)->last_error.c_str(); }
+
+int zbref_deploy(void* h, const char* xml, size_t len, int64_t workflow_key, int32_t version) {
+  Engine* e = (Engine*)h;
+  try {
+    e->deploy(std::string(xml, len), workflow_key, version);
+    return 0;
+  } catch (const std::exception& ex) {
+    e->last_error = ex.what();
+    return -1;
+  }
+}
+
+int zbref_set_job_payload(void* h, int64_t workflow_key, const char* activity_id, const uint8_t* p, size_t n) {
+  Engine* e = (Engine*)h;
+  e->job_payloads[{workflow_key, bytes(activity_id)}] = bytes((const char*)p, n);
+  return 0;
+}
+
+int zbref_submit_create(void* h, const char* process_id, int32_t version, int64_t workflow_key, const uint8_t* p,
+                        size_t n) {
+  Engine* e = (Engine*)h;
+  try {
+    e->submit_create(bytes(process_id), version, workflow_key, bytes((const char*)p, n));
+    return 0;
+  } catch (const std::exception& ex) {
+    e->last_error = ex.what();
+    return -1;
+  }
+}
+
+int zbref_submit_cancel(void* h, int64_t key) {
+  ((Engine*)h)->submit_cancel(key);
+  return 0;
+}
+
+int zbref_submit_correlate(void* h, int64_t wik, int64_t aik, const char* name, const uint8_t* p, size_t n) {
+  ((Engine*)h)->submit_correlate(wik, aik, bytes(name), bytes((const char*)p, n));
+  return 0;
+}
+
+// Process until the log is exhausted (quiescence) or max records; returns #processed or -1.
+int64_t zbref_run(void* h, int64_t max_records) {
+  Engine* e = (Engine*)h;
+  try {
+    return (int64_t)e->run(max_records < 0 ? SIZE_MAX : (size_t)max_records);
+  } catch (const std::exception& ex) {
+    if (e->last_error.empty()) e->last_error = ex.what();
+    return -1;
+  }
+}
+
+int64_t zbref_log_size(void* h) { return (int64_t)((Engine*)h)->log.size(); }
+
+// Fills header and returns the encoded value into buf (if cap suffices); returns value length.
+int64_t zbref_get_record(void* h, int64_t i, zbref_record* out, uint8_t* buf, size_t cap) {
+  Engine* e = (Engine*)h;
+  const Record& r = e->log.at((size_t)i);
+  bytes v = r.encode_value();
+  out->position = r.position;
+  out->source_position = r.source_position;
+  out->key = r.key;
+  out->record_type = r.record_type;
+  out->value_type = r.value_type;
+  out->intent = r.intent;
+  out->rejection_type = r.rejection_type;
+  out->value_len = (uint32_t)v.size();
+  if (buf && v.size() <= cap) std::memcpy(buf, v.data(), v.size());
+  return (int64_t)v.size();
+}
+
+// Writes the whole log as a flat buffer: per record [zbref_record][value bytes].
+int64_t zbref_dump_log(void* h, int64_t from, int64_t to, uint8_t* buf, size_t cap) {
+  Engine* e = (Engine*)h;
+  size_t off = 0;
+  if (to < 0 || to > (int64_t)e->log.size()) to = (int64_t)e->log.size();
+  for (int64_t i = from; i < to; i++) {
+    const Record& r = e->log[(size_t)i];
+    bytes v = r.encode_value();
+    size_t need = sizeof(zbref_record) + v.size();
+    if (buf && off + need <= cap) {
+      zbref_record hr{r.position, r.source_position, r.key, r.record_type, r.value_type, r.intent, r.rejection_type,
+                      (uint32_t)v.size()};
+      std::memcpy(buf + off, &hr, sizeof(hr));
+      std::memcpy(buf + off + sizeof(hr), v.data(), v.size());
+    }
+    off += need;
+  }
+  return (int64_t)off;
+}
+
+void zbref_counters(void* h, int64_t* out) {
+  Engine* e = (Engine*)h;
+  out[0] = e->created;
+  out[1] = e->completed;
+  out[2] = e->canceled;
+  out[3] = (int64_t)e->index.instances.size();
+  out[4] = e->wf_keys.next;
+  out[5] = e->job_keys.next;
+}
+
+int64_t zbref_side_effects(void* h, int64_t i, int64_t* keys, int32_t* partition, uint8_t* ck, size_t cap) {
+  Engine* e = (Engine*)h;
+  if (i < 0) return (int64_t)e->side_effects.size();
+  const SideEffect& s = e->side_effects.at((size_t)i);
+  keys[0] = s.workflow_instance_key;
+  keys[1] = s.activity_instance_key;
+  *partition = s.partition;
+  if (s.correlation_key.size() <= cap) std::memcpy(ck, s.correlation_key.data(), s.correlation_key.size());
+  return (int64_t)s.correlation_key.size();
+}
+
+// ---- unit-level entry points for the reference's known-answer tests
+// returns 1/0 for true/false, -1 compile error, -2 evaluation error (message in err)
+int zbref_eval_condition(const char* expr, const uint8_t* doc, size_t n, char* err, size_t errcap) {
+  CompiledCondition c = create_condition(expr);
+  if (!c.valid) {
+    std::snprintf(err, errcap, "%s", c.error.c_str());
+    return -1;
+  }
+  ElInterpreter in;
+  try {
+    return in.eval(c.root.get(), doc, n) ? 1 : 0;
+  } catch (const std::exception& ex) {
+    std::snprintf(err, errcap, "%s", ex.what());
+    return -2;
+  }
+}
+
+// Evaluate one compiled condition against several documents in sequence (constant mutation persists).
+int zbref_eval_condition_seq(const char* expr, const uint8_t* docs, const uint32_t* lens, int ndocs, int* results) {
+  CompiledCondition c = create_condition(expr);
+  if (!c.valid) return -1;
+  ElInterpreter in;
+  size_t off = 0;
+  for (int i = 0; i < ndocs; i++) {
+    try {
+      results[i] = in.eval(c.root.get(), docs + off, lens[i]) ? 1 : 0;
+    } catch (const std::exception&) {
+      results[i] = -2;
+    }
+    off += lens[i];
+  }
+  return 0;
+}
+
+int64_t zbref_merge(const uint8_t* src, size_t ns, const uint8_t* tgt, size_t nt, uint8_t* out, size_t cap, char* err,
+                    size_t errcap) {
+  try {
+    bytes r = merge_documents(bytes((const char*)src, ns), bytes((const char*)tgt, nt));
+    if (r.size() <= cap) std::memcpy(out, r.data(), r.size());
+    return (int64_t)r.size();
+  } catch (const std::exception& ex) {
+    std::snprintf(err, errcap, "%s", ex.what());
+    return -1;
+  }
+}
+
+// returns #results (positions/lengths written pairwise), -1 invalid query (err has message)
+int zbref_query(const char* path, const uint8_t* doc, size_t n, int32_t* out, int cap, char* err, size_t errcap) {
+  JsonPathCompiler jc;
+  JsonPathQuery q = jc.compile(path);
+  if (!q.valid()) {
+    std::snprintf(err, errcap, "%s", q.error.c_str());
+    return -1;
+  }
+  JsonPathExecutor ex;
+  ex.run(q.filters, doc, n);
+  int k = 0;
+  for (auto& r : ex.results) {
+    if (k < cap) { out[2 * k] = r.position; out[2 * k + 1] = r.length; }
+    k++;
+  }
+  return k;
+}
+
+int32_t zbref_subscription_hash(const uint8_t* p, size_t n) {
+  int32_t h = 0;
+  for (size_t i = 0; i < n; i++) h = (int32_t)((uint32_t)h * 31u + (uint32_t)(int32_t)(int8_t)p[i]);
+  return h;
+}
+
+int64_t zbref_encode_int(int64_t v, uint8_t* out) {
+  MpWriter w;
+  w.integer(v);
+  std::memcpy(out, w.b.data(), w.b.size());
+  return (int64_t)w.b.size();
+}
+
+int64_t zbref_encode_float(double v, uint8_t* out) {
+  MpWriter w;
+  w.floating(v);
+  std::memcpy(out, w.b.data(), w.b.size());
+  return (int64_t)w.b.size();
+}
+
+// Wall-clock timing helper for the CPU baseline: run to quiescence, return seconds.
+double zbref_run_timed(void* h, int64_t* processed) {
+  auto t0 = std::chrono::steady_clock::now();
+  int64_t n = zbref_run(h, -1);
+  auto t1 = std::chrono::steady_clock::now();
+  *processed = n;
+  return std::chrono::duration<double>(t1 - t0).count();
+}
+
+}  // extern "C"

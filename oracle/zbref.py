@@ -1,0 +1,229 @@
+"""ctypes binding of the zbref oracle (ORACLE / TEST INFRASTRUCTURE ONLY).
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the checker
+and the CPU baseline. The product path (zeebe_amd) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import struct
+import subprocess
+from typing import List, NamedTuple, Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libzbref.so")
+
+
+def build() -> str:
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        vp, i64, i32, sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_size_t
+        cp, u8p = ctypes.c_char_p, ctypes.c_char_p
+        L.zbref_new.restype = vp
+        L.zbref_new.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.zbref_free.argtypes = [vp]
+        L.zbref_last_error.restype = cp
+        L.zbref_last_error.argtypes = [vp]
+        L.zbref_deploy.argtypes = [vp, cp, sz, i64, i32]
+        L.zbref_set_job_payload.argtypes = [vp, i64, cp, u8p, sz]
+        L.zbref_submit_create.argtypes = [vp, cp, i32, i64, u8p, sz]
+        L.zbref_submit_cancel.argtypes = [vp, i64]
+        L.zbref_submit_correlate.argtypes = [vp, i64, i64, cp, u8p, sz]
+        L.zbref_run.restype = i64
+        L.zbref_run.argtypes = [vp, i64]
+        L.zbref_log_size.restype = i64
+        L.zbref_log_size.argtypes = [vp]
+        L.zbref_dump_log.restype = i64
+        L.zbref_dump_log.argtypes = [vp, i64, i64, ctypes.c_void_p, sz]
+        L.zbref_counters.argtypes = [vp, ctypes.POINTER(i64)]
+        L.zbref_side_effects.restype = i64
+        L.zbref_side_effects.argtypes = [vp, i64, ctypes.POINTER(i64), ctypes.POINTER(i32), ctypes.c_void_p, sz]
+        L.zbref_eval_condition.argtypes = [cp, u8p, sz, ctypes.c_char_p, sz]
+        L.zbref_eval_condition_seq.argtypes = [cp, u8p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
+                                               ctypes.POINTER(ctypes.c_int)]
+        L.zbref_merge.restype = i64
+        L.zbref_merge.argtypes = [u8p, sz, u8p, sz, ctypes.c_void_p, sz, ctypes.c_char_p, sz]
+        L.zbref_query.argtypes = [cp, u8p, sz, ctypes.POINTER(i32), ctypes.c_int, ctypes.c_char_p, sz]
+        L.zbref_subscription_hash.restype = i32
+        L.zbref_subscription_hash.argtypes = [u8p, sz]
+        L.zbref_encode_int.restype = i64
+        L.zbref_encode_int.argtypes = [i64, ctypes.c_void_p]
+        L.zbref_encode_float.restype = i64
+        L.zbref_encode_float.argtypes = [ctypes.c_double, ctypes.c_void_p]
+        L.zbref_run_timed.restype = ctypes.c_double
+        L.zbref_run_timed.argtypes = [vp, ctypes.POINTER(i64)]
+        _lib = L
+    return _lib
+
+
+_HDR = struct.Struct("<qqqBBBBI")  # zbref_record
+
+
+class Record(NamedTuple):
+    position: int
+    source_position: int
+    key: int
+    record_type: int
+    value_type: int
+    intent: int
+    rejection_type: int
+    value: bytes
+
+
+def parse_log(buf: bytes) -> List[Record]:
+    out = []
+    off = 0
+    while off < len(buf):
+        pos, src, key, rt, vt, it, rj, vlen = _HDR.unpack_from(buf, off)
+        off += _HDR.size
+        out.append(Record(pos, src, key, rt, vt, it, rj, bytes(buf[off:off + vlen])))
+        off += vlen
+    return out
+
+
+class ZbrefError(RuntimeError):
+    pass
+
+
+class Oracle:
+    """One partition of the sequential reference restatement."""
+
+    def __init__(self, partition_id: int = 0, partition_count: int = 1):
+        self._L = lib()
+        self._h = self._L.zbref_new(partition_id, partition_count)
+
+    def close(self):
+        if self._h:
+            self._L.zbref_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _err(self) -> str:
+        return self._L.zbref_last_error(self._h).decode("utf-8", "replace")
+
+    def deploy(self, xml: bytes, workflow_key: int, version: int = 1):
+        if isinstance(xml, str):
+            xml = xml.encode()
+        if self._L.zbref_deploy(self._h, xml, len(xml), workflow_key, version) != 0:
+            raise ZbrefError(self._err())
+
+    def set_job_payload(self, workflow_key: int, activity_id: str, payload: bytes):
+        self._L.zbref_set_job_payload(self._h, workflow_key, activity_id.encode(), payload, len(payload))
+
+    def create(self, process_id: str, payload: bytes = b"\x80", version: int = -1, workflow_key: int = -1):
+        if self._L.zbref_submit_create(self._h, process_id.encode(), version, workflow_key, payload, len(payload)):
+            raise ZbrefError(self._err())
+
+    def cancel(self, key: int):
+        self._L.zbref_submit_cancel(self._h, key)
+
+    def correlate(self, wf_instance_key: int, activity_instance_key: int, message_name: str, payload: bytes):
+        self._L.zbref_submit_correlate(self._h, wf_instance_key, activity_instance_key, message_name.encode(),
+                                       payload, len(payload))
+
+    def run(self, max_records: int = -1) -> int:
+        n = self._L.zbref_run(self._h, max_records)
+        if n < 0:
+            raise ZbrefError(self._err())
+        return n
+
+    def run_timed(self):
+        n = ctypes.c_int64()
+        t = self._L.zbref_run_timed(self._h, ctypes.byref(n))
+        if n.value < 0:
+            raise ZbrefError(self._err())
+        return n.value, t
+
+    def log_size(self) -> int:
+        return self._L.zbref_log_size(self._h)
+
+    def records(self, start: int = 0, end: int = -1) -> List[Record]:
+        need = self._L.zbref_dump_log(self._h, start, end, None, 0)
+        buf = ctypes.create_string_buffer(max(need, 1))
+        self._L.zbref_dump_log(self._h, start, end, buf, need)
+        return parse_log(buf.raw[:need])
+
+    def dump(self, start: int = 0, end: int = -1) -> bytes:
+        need = self._L.zbref_dump_log(self._h, start, end, None, 0)
+        buf = ctypes.create_string_buffer(max(need, 1))
+        self._L.zbref_dump_log(self._h, start, end, buf, need)
+        return buf.raw[:need]
+
+    def counters(self) -> dict:
+        arr = (ctypes.c_int64 * 6)()
+        self._L.zbref_counters(self._h, arr)
+        return dict(created=arr[0], completed=arr[1], canceled=arr[2], live_instances=arr[3],
+                    next_wf_key=arr[4], next_job_key=arr[5])
+
+    def side_effects(self):
+        n = self._L.zbref_side_effects(self._h, -1, None, None, None, 0)
+        out = []
+        for i in range(n):
+            keys = (ctypes.c_int64 * 2)()
+            part = ctypes.c_int32()
+            buf = ctypes.create_string_buffer(4096)
+            ln = self._L.zbref_side_effects(self._h, i, keys, ctypes.byref(part), buf, 4096)
+            out.append((keys[0], keys[1], part.value, buf.raw[:ln]))
+        return out
+
+
+def eval_condition(expr: str, doc: bytes):
+    """Returns True/False, or raises ValueError(compile msg) / RuntimeError(eval msg)."""
+    err = ctypes.create_string_buffer(4096)
+    r = lib().zbref_eval_condition(expr.encode(), doc, len(doc), err, 4096)
+    if r == -1:
+        raise ValueError(err.value.decode())
+    if r == -2:
+        raise RuntimeError(err.value.decode())
+    return bool(r)
+
+
+def merge(source: bytes, target: bytes) -> bytes:
+    out = ctypes.create_string_buffer(65536)
+    err = ctypes.create_string_buffer(4096)
+    n = lib().zbref_merge(source, len(source), target, len(target), out, 65536, err, 4096)
+    if n < 0:
+        raise RuntimeError(err.value.decode())
+    return out.raw[:n]
+
+
+def query(path: str, doc: bytes):
+    out = (ctypes.c_int32 * 256)()
+    err = ctypes.create_string_buffer(4096)
+    n = lib().zbref_query(path.encode(), doc, len(doc), out, 128, err, 4096)
+    if n < 0:
+        raise ValueError(err.value.decode())
+    return [doc[out[2 * i]:out[2 * i] + out[2 * i + 1]] for i in range(min(n, 128))]
+
+
+def subscription_hash(b: bytes) -> int:
+    return lib().zbref_subscription_hash(b, len(b))
+
+
+def encode_int(v: int) -> bytes:
+    buf = ctypes.create_string_buffer(16)
+    n = lib().zbref_encode_int(v, buf)
+    return buf.raw[:n]
+
+
+def encode_float(v: float) -> bytes:
+    buf = ctypes.create_string_buffer(16)
+    n = lib().zbref_encode_float(v, buf)
+    return buf.raw[:n]
