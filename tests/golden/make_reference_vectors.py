@@ -1,0 +1,299 @@
+"""Generate tests/golden/reference_vectors.json: the reference's own known-answer vectors.
+
+Every expected value below is TRANSCRIBED from the reference test named next to it (inputs are
+re-encoded with python-msgpack the way the reference tests encode them with Jackson's msgpack
+mapper: minimal ints, float64 doubles, str keys). Nothing here is produced by running the oracle;
+the oracle is checked against this file (tests/test_oracle_golden.py) and then serves as the
+checker of the GPU engine.
+
+Run:  python tests/golden/make_reference_vectors.py
+"""
+import json
+import math
+import os
+import sys
+
+import msgpack
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from zeebe_amd import bpmn  # noqa: E402
+
+
+def mp(obj) -> str:
+    return msgpack.packb(obj, use_bin_type=True).hex()
+
+
+def jl(s: str):
+    """The reference tests write JSON with single quotes (JSON_MAPPER ALLOW_SINGLE_QUOTES)."""
+    return json.loads(s.replace("'", '"'))
+
+
+def conditions():
+    # json-el/src/test/java/io/zeebe/msgpack/el/JsonConditionInterpreterTest.java:35-93
+    nan, inf = float("nan"), float("inf")
+    v = [
+        ("$.foo == 'bar'", {"foo": "bar"}, True), ("$.foo == 'bar'", {"foo": "baz"}, False),
+        ("$.foo == true", {"foo": True}, True), ("$.foo == true", {"foo": False}, False),
+        ("$.foo == 3", {"foo": 3}, True), ("$.foo == 3", {"foo": 4}, False),
+        ("$.foo == 2.5", {"foo": 2.5}, True), ("$.foo == 2.5", {"foo": 2.6}, False),
+        ("$.foo == 2", {"foo": 2.0}, True), ("$.foo == 2.0", {"foo": 2}, True),
+        ("$.foo == null", {"foo": None}, True), ("$.foo == null", {"foo": "bar"}, False),
+        ("$.foo == $.bar", {"foo": "a", "bar": "a"}, True), ("$.foo == $.bar", {"foo": "a", "bar": "b"}, False),
+        ("$.foo != 'bar'", {"foo": "baz"}, True), ("$.foo != 'bar'", {"foo": "bar"}, False),
+        ("$.foo != null", {"foo": "bar"}, True), ("$.foo != null", {"foo": None}, False),
+        ("$.foo < 5", {"foo": 4}, True), ("$.foo < 5", {"foo": 5}, False),
+        ("$.foo <= 5", {"foo": 5}, True), ("$.foo <= 5", {"foo": 6}, False),
+        ("$.foo <= 5.0", {"foo": 4.8}, True), ("$.foo <= 5.0", {"foo": 5}, True),
+        ("$.foo <= 5.0", {"foo": 5.1}, False),
+        ("$.foo > 5", {"foo": 6}, True), ("$.foo > 5", {"foo": 5}, False),
+        ("$.foo >= 5", {"foo": 5}, True), ("$.foo >= 5", {"foo": 4}, False),
+        ("$.foo < $.bar", {"foo": 1, "bar": 2}, True), ("$.foo < $.bar", {"foo": 2, "bar": 2}, False),
+        ("$.foo == 1 || $.foo == 2", {"foo": 1}, True), ("$.foo == 1 || $.foo == 2", {"foo": 2}, True),
+        ("$.foo == 1 || $.foo == 2", {"foo": 3}, False),
+        ("$.foo == 1 || $.foo == 2 || $.foo == 3", {"foo": 3}, True),
+        ("$.foo == 1 || $.foo == 2 || $.foo == 3", {"foo": 4}, False),
+        ("$.foo > 2 && $.foo > 3", {"foo": 4}, True), ("$.foo > 2 && $.foo > 3", {"foo": 3}, False),
+        ("$.foo > 2 && $.foo > 3", {"foo": 2}, False),
+        ("$.foo > 2 && $.foo > 3 && $.foo > 4", {"foo": 5}, True),
+        ("$.foo > 2 && $.foo > 3 && $.foo > 4", {"foo": 4}, False),
+        ("$.foo == 1 || $.foo > 2 && $.foo > 3", {"foo": 4}, True),
+        ("$.foo == 1 || $.foo > 2 && $.foo > 3", {"foo": 1}, True),
+        ("$.foo == 1 || $.foo > 2 && $.foo > 3", {"foo": 2}, False),
+        ("$.foo == 1 || $.foo > 2 && $.foo > 3", {"foo": 3}, False),
+        ("($.foo == 1 || $.foo > 2) && $.foo > 3", {"foo": 4}, True),
+        ("($.foo == 1 || $.foo > 2) && $.foo > 3", {"foo": 1}, False),
+        ("($.foo == 1 || $.foo > 2) && $.foo > 3", {"foo": 2}, False),
+        ("($.foo == 1 || $.foo > 2) && $.foo > 3", {"foo": 3}, False),
+        ("$.foo < 5", {"foo": nan}, False), ("$.foo > 5", {"foo": nan}, False),
+        ("$.foo < 5", {"foo": inf}, False), ("$.foo > 5", {"foo": inf}, True),
+        ("$.foo < 5", {"foo": -inf}, True), ("$.foo > 5", {"foo": -inf}, False),
+    ]
+    return [{"expr": e, "doc": mp(d), "expected": r} for e, d, r in v]
+
+
+def condition_errors():
+    # json-el/src/test/java/io/zeebe/msgpack/el/JsonConditionTest.java:34-141
+    return [
+        {"expr": "$.foo == $.bar || $.foo > 2 || $.bar <= 2", "doc": mp({"foo": 2, "bar": 2}), "expected": True},
+        {"expr": "$.foo == $.bar || $.foo > 2 || $.bar <= 2", "doc": mp({"foo": 2, "bar": 3}), "expected": False},
+        {"expr": "$.foo > 3", "doc": mp({"foo": "bar"}),
+         "error": "Cannot compare values of different types: STRING and INTEGER"},
+        {"expr": "$.foo > 3", "doc": mp({"bar": 4}), "error": "JSON path '$.foo' has no result"},
+        {"expr": "$.foo > 3", "doc": mp({"foo": None}),
+         "error": "Cannot compare values of different types: NIL and INTEGER"},
+        {"expr": "$.foo == $.bar", "doc": mp({"foo": [1, 2, 3], "bar": [4, 5, 6]}),
+         "error": "Cannot compare value of type: ARRAY"},
+        {"expr": "$.foo == $.bar", "doc": mp({"foo": {"a": 1}, "bar": {"b": 2}}),
+         "error": "Cannot compare value of type: MAP"},
+        {"expr": "$.foo < $.bar", "doc": mp({"foo": "a", "bar": "b"}),
+         "error": "Cannot compare values. Expected number but found: STRING"},
+    ]
+
+
+def parser_valid():
+    # json-el/src/test/java/io/zeebe/msgpack/el/JsonConditionParserTest.java:29-58
+    return ["$.foo == 'bar'", '$.foo == "bar"', "$.foo == true", "$.foo == 21", "$.foo == 2.5", "$.foo == $.bar",
+            "$.foo.bar == true", "$.foo[1] == true", "'foo' == 'bar'", "$.foo != 'bar'", "$.foo < 100",
+            "$.foo <= -100", "$.foo > 2.5", "$.foo >= 2.5", "$.foo >= .5", "$.foo >= -.5", "$.foo >= $.bar",
+            "2 < 4", "$.foo > 2 && $.foo < 4", "$.foo > 2 && $.foo < 4 && $.bar > 12", "$.foo > 2 || $.bar < 4",
+            "$.foo > 2 || $.bar < 4 || $.foobar == 21", "$.foo > 2 && $.foo < 4 || $.bar == 6", "($.foo == 2)",
+            "$.foo > 2 && ($.foo < 4 || $.bar == 6)"]
+
+
+def parser_failures():
+    # json-el/src/test/java/io/zeebe/msgpack/el/JsonConditionParserFailureMessageTest.java:33-49
+    # and JsonConditionTest.shouldReportParseFailure (:61-68)
+    return [
+        ["", "expression is empty"],
+        ["foo", "expected comparison, disjunction or conjunction."],
+        ["$.foo", "expected comparison operator ('==', '!=', '<', '<=', '>', '>=')"],
+        ["$.foo ==", "expected literal (JSON path, string, number, boolean, null)"],
+        ["$.foo < 'bar'", "expected number or JSON path"],
+        ["$.foo < true", "expected number or JSON path"],
+        ["$.foo == { 'a': 2 }", "expected literal (JSON path, string, number, boolean, null)"],
+        ["$.foo == [1, 2, 3]", "expected literal (JSON path, string, number, boolean, null)"],
+        ["$.foo + 3", "expected comparison operator ('==', '!=', '<', '<=', '>', '>=')"],
+        ["$.foo or $.bar", "expected comparison operator ('==', '!=', '<', '<=', '>', '>=')"],
+        ["$.foo < 3 &&", "expected comparison"],
+        ["$.foo < 3 ||", "expected comparison"],
+        ["($.foo < 3", "`)' expected but end of source found"],
+        ["$.foo.. < 3", "Unexpected json-path"],
+        ["$.foo < NaN", "expected number or JSON path"],
+        ["$.foo < Infinity", "expected number or JSON path"],
+        ["$.foo < -Infinity", "expected number or JSON path"],
+    ]
+
+
+def merges():
+    # json-path/src/test/java/io/zeebe/msgpack/mapping/MappingMergeParameterizedTest.java:42-180
+    # (the rows whose mapping column is null = default top-level merge; compared as JSON trees)
+    nested = ("{'arr':[{'obj':{'value':'x', 'otherArr':[{'test':'hallo'}, {'obj':{'arr':[0, 1]}} ]}}, "
+              "{'otherValue':1}], 'ab':{'b':{'value':'y'}}}")
+    rows = [
+        ("{'hallo':'twsewas','int':1}", "{'foo':'bar','int':3}", "{'hallo':'twsewas','foo':'bar','int':1}"),
+        ("{'foo':'bar','int':1,'obj':{'test':'ok'},'array':[1,2,3]}",
+         "{'foo':'bar','int':3,'obj':{'test':'ok'},'array':[1],'test':'value'}",
+         "{'foo':'bar','int':1,'obj':{'test':'ok'},'array':[1,2,3],'test':'value'}"),
+        (nested, "{'foo':'bar','int':3,'obj':{'test':'ok'},'array':[1],'test':'value'}",
+         nested[:-1] + ",'foo':'bar','int':3,'obj':{'test':'ok'},'array':[1],'test':'value'}"),
+        (nested, "{'foo':'bar','int':3,'ab':{'c':{'value':'z'}},'array':[1],'test':'value'}",
+         nested[:-1] + ",'foo':'bar','int':3,'array':[1],'test':'value'}"),
+        # MappingMergeTest.shouldMergeTwiceWithoutMappings :181-220
+        ("{'test':'thisValue'}", "{'arr':[0, 1], 'obj':{'int':1}, 'test':'value'}",
+         "{'arr':[0, 1], 'obj':{'int':1}, 'test':'thisValue'}"),
+        ("{'other':[2, 3]}", "{'arr':[0, 1], 'obj':{'int':1}, 'test':'thisValue'}",
+         "{'arr':[0, 1], 'obj':{'int':1}, 'test':'thisValue', 'other':[2, 3]}"),
+    ]
+    out = [{"source": mp(jl(s)), "target": mp(jl(t)), "expected_json": jl(e)} for s, t, e in rows]
+    # MappingMergeTest :221-264 byte-exact nil / empty cases
+    out += [
+        {"source": "c0", "target": "80", "expected_hex": "80"},
+        {"source": "80", "target": "c0", "expected_hex": "80"},
+        {"source": "c0", "target": "c0", "expected_hex": "c0"},
+    ]
+    # WorkflowTaskIOMappingTest.shouldUseWFPayloadIfCompleteWithNoPayload :569-590 (byte exact) and
+    # MsgPackUtil.JSON_DOCUMENT/OTHER_DOCUMENT/MERGED_OTHER_WITH_JSON_DOCUMENT
+    # (broker-core/src/test/java/io/zeebe/broker/test/MsgPackUtil.java:31-34)
+    jd = jl("{'string':'value', 'jsonObject':{'testAttr':'test'}}")
+    od = jl("{'string':'bar', 'otherObject':{'testAttr':'test'}}")
+    out += [
+        {"source": "80", "target": mp(jd), "expected_hex": mp(jd)},
+        {"source": mp(od), "target": mp(jd),
+         "expected_json": jl("{'string':'bar', 'jsonObject':{'testAttr':'test'}, 'otherObject':{'testAttr':'test'}}")},
+        {"source": mp(jd), "target": mp(jd), "expected_json": jd},
+    ]
+    return out
+
+
+def writer():
+    # msgpack-core/src/test/java/io/zeebe/msgpack/spec/MsgPackWriterTest.java:43-120
+    ints = [(5, "05"), ((1 << 8) - 1, "ccff"), ((1 << 16) - 1, "cdffff"), ((1 << 32) - 1, "ceffffffff"),
+            ((1 << 63) - 1, "cf7fffffffffffffff"), (-(1 << 7), "d080"), (-(1 << 15), "d18000"),
+            (-(1 << 31), "d280000000"), (-(1 << 63), "d38000000000000000"), (-1, "ff"), (-32, "e0"),
+            (-33, "d0df"), (127, "7f"), (128, "cc80")]
+    floats = [(123.0, "ca42f60000"), (1.7976931348623157e308, "cb7fefffffffffffff")]
+    return {"ints": ints, "floats": floats}
+
+
+def hashes():
+    # protocol/src/test/java/io/zeebe/protocol/SubscriptionUtilTest.java:29-43
+    return [["a", 97], ["b", 98], ["c", 99], ["", 0]]
+
+
+WF = {"CREATE": 0, "CREATED": 1, "START_EVENT_OCCURRED": 2, "END_EVENT_OCCURRED": 3, "SEQUENCE_FLOW_TAKEN": 4,
+      "GATEWAY_ACTIVATED": 5, "ELEMENT_READY": 6, "ELEMENT_ACTIVATED": 7, "ELEMENT_COMPLETING": 8,
+      "ELEMENT_COMPLETED": 9, "ELEMENT_TERMINATING": 10, "ELEMENT_TERMINATED": 11, "CANCEL": 12, "CANCELING": 13}
+
+
+def workflows():
+    B = bpmn.Bpmn
+    out = []
+    # WorkflowInstanceFunctionalTest.testWorkflowInstanceStatesWithServiceTask :518-556
+    m = (B.create_executable_process("process").start_event("a").service_task("b", type="foo")
+         .end_event("c").done())
+    out.append({"name": "states_with_service_task", "xml": m.to_xml(), "process": "process",
+                "instances": [{"payload": "80"}], "job_payloads": {},
+                "expect_wf_intents": ["CREATE", "CREATED", "ELEMENT_READY", "ELEMENT_ACTIVATED",
+                                      "START_EVENT_OCCURRED", "SEQUENCE_FLOW_TAKEN", "ELEMENT_READY",
+                                      "ELEMENT_ACTIVATED", "ELEMENT_COMPLETING", "ELEMENT_COMPLETED",
+                                      "SEQUENCE_FLOW_TAKEN", "END_EVENT_OCCURRED", "ELEMENT_COMPLETING",
+                                      "ELEMENT_COMPLETED"]})
+    # :558-597
+    m = (B.create_executable_process("workflow").start_event().exclusive_gateway("xor")
+         .sequence_flow_id("s1").condition("$.foo < 5").end_event("a").move_to_last_exclusive_gateway()
+         .default_flow().sequence_flow_id("s2").end_event("b").done())
+    out.append({"name": "states_with_exclusive_gateway", "xml": m.to_xml(), "process": "workflow",
+                "instances": [{"payload": mp({"foo": 4})}], "job_payloads": {},
+                "expect_wf_intents": ["CREATE", "CREATED", "ELEMENT_READY", "ELEMENT_ACTIVATED",
+                                      "START_EVENT_OCCURRED", "SEQUENCE_FLOW_TAKEN", "GATEWAY_ACTIVATED",
+                                      "SEQUENCE_FLOW_TAKEN", "END_EVENT_OCCURRED", "ELEMENT_COMPLETING",
+                                      "ELEMENT_COMPLETED"]})
+    # shouldSpitOnExclusiveGateway :351-393 (end event reached per payload)
+    m = (B.create_executable_process("workflow").start_event().exclusive_gateway("xor")
+         .sequence_flow_id("s1").condition("$.foo < 5").end_event("a").move_to_last_gateway()
+         .sequence_flow_id("s2").condition("$.foo >= 5 && $.foo < 10").end_event("b")
+         .move_to_last_exclusive_gateway().default_flow().sequence_flow_id("s3").end_event("c").done())
+    out.append({"name": "split_on_exclusive_gateway", "xml": m.to_xml(), "process": "workflow",
+                "instances": [{"payload": mp({"foo": 4})}, {"payload": mp({"foo": 8})},
+                              {"payload": mp({"foo": 12})}], "job_payloads": {},
+                "expect_end_event": ["a", "b", "c"]})
+    # shouldJoinOnExclusiveGateway :395-442 (flows taken per instance)
+    m = (B.create_executable_process("workflow").start_event().exclusive_gateway("split")
+         .sequence_flow_id("s1").condition("$.foo < 5").exclusive_gateway("joinRequest")
+         .move_to_last_exclusive_gateway().default_flow().sequence_flow_id("s2").connect_to("joinRequest")
+         .end_event("end").done())
+    out.append({"name": "join_on_exclusive_gateway", "xml": m.to_xml(), "process": "workflow",
+                "instances": [{"payload": mp({"foo": 4})}, {"payload": mp({"foo": 8})}], "job_payloads": {},
+                "expect_flows_contain": [["s1"], ["s2"]], "expect_flows_exclude": [["s2"], ["s1"]]})
+    # EmbeddedSubProcessTest.shouldCompleteEmbeddedSubProcess :132-165 (+ scope keys :123-128)
+    sp = (B.create_executable_process("process").start_event("start").sequence_flow_id("flow1")
+          .sub_process("subProcess"))
+    (sp.embedded_sub_process().start_event("subProcessStart").sequence_flow_id("subProcessFlow1")
+     .service_task("subProcessTask", type="type").sequence_flow_id("subProcessFlow2").end_event("subProcessEnd"))
+    m = sp.sequence_flow_id("flow2").end_event("end").done()
+    seq = [("CREATED", "process"), ("ELEMENT_READY", "process"), ("ELEMENT_ACTIVATED", "process"),
+           ("START_EVENT_OCCURRED", "start"), ("SEQUENCE_FLOW_TAKEN", "flow1"), ("ELEMENT_READY", "subProcess"),
+           ("ELEMENT_ACTIVATED", "subProcess"), ("START_EVENT_OCCURRED", "subProcessStart"),
+           ("SEQUENCE_FLOW_TAKEN", "subProcessFlow1"), ("ELEMENT_READY", "subProcessTask"),
+           ("ELEMENT_ACTIVATED", "subProcessTask"), ("ELEMENT_COMPLETING", "subProcessTask"),
+           ("ELEMENT_COMPLETED", "subProcessTask"), ("SEQUENCE_FLOW_TAKEN", "subProcessFlow2"),
+           ("END_EVENT_OCCURRED", "subProcessEnd"), ("ELEMENT_COMPLETING", "subProcess"),
+           ("ELEMENT_COMPLETED", "subProcess"), ("SEQUENCE_FLOW_TAKEN", "flow2"), ("END_EVENT_OCCURRED", "end"),
+           ("ELEMENT_COMPLETING", "process"), ("ELEMENT_COMPLETED", "process")]
+    out.append({"name": "embedded_sub_process", "xml": m.to_xml(), "process": "process",
+                "instances": [{"payload": mp({"key": "val"})}], "job_payloads": {},
+                "expect_wf_events": [list(x) for x in seq],
+                "expect_scope_checks": True})
+    # shouldCompleteNestedSubProcess :293-344
+    outer = B.create_executable_process("process").start_event().sub_process("outerSubProcess")
+    inner_start = outer.embedded_sub_process().start_event()
+    inner_sp = inner_start.sub_process("innerSubProcess")
+    inner_sp.embedded_sub_process().start_event().service_task("task", type="type").end_event()
+    inner_sp.end_event()
+    m = outer.end_event().done()
+    seq = [("ELEMENT_READY", "outerSubProcess"), ("ELEMENT_ACTIVATED", "outerSubProcess"),
+           ("ELEMENT_READY", "innerSubProcess"), ("ELEMENT_ACTIVATED", "innerSubProcess"),
+           ("ELEMENT_READY", "task"), ("ELEMENT_ACTIVATED", "task"), ("ELEMENT_COMPLETING", "task"),
+           ("ELEMENT_COMPLETED", "task"), ("ELEMENT_COMPLETING", "innerSubProcess"),
+           ("ELEMENT_COMPLETED", "innerSubProcess"), ("ELEMENT_COMPLETING", "outerSubProcess"),
+           ("ELEMENT_COMPLETED", "outerSubProcess")]
+    out.append({"name": "nested_sub_process", "xml": m.to_xml(), "process": "process",
+                "instances": [{"payload": "80"}], "job_payloads": {},
+                "expect_filtered_events": [list(x) for x in seq],
+                "filter_ids": ["innerSubProcess", "outerSubProcess", "task"]})
+    # WorkflowTaskIOMappingTest.shouldNotSeePayloadOfWorkflowInstanceBefore :462-495
+    jd = jl("{'string':'value', 'jsonObject':{'testAttr':'test'}}")
+    m = (B.create_executable_process("process").start_event().service_task("service", type="external")
+         .end_event().done())
+    out.append({"name": "io_payload_isolation", "xml": m.to_xml(), "process": "process",
+                "instances": [{"payload": mp(jd), "job_payload": mp(jd)},
+                              {"payload": "80", "job_payload": mp({"foo": "bar"})}],
+                "expect_task_completed_payload_json": [jd, {"foo": "bar"}]})
+    # shouldUseWFPayloadIfCompleteWithNoPayload :569-590 (byte exact)
+    out.append({"name": "io_no_job_payload_byte_exact", "xml": m.to_xml(), "process": "process",
+                "instances": [{"payload": mp(jd), "job_payload": "80"}],
+                "expect_task_completed_payload_hex": [mp(jd)]})
+    return out
+
+
+def main():
+    data = {
+        "conditions": conditions(),
+        "condition_errors": condition_errors(),
+        "parser_valid": parser_valid(),
+        "parser_failures": parser_failures(),
+        "merges": merges(),
+        "writer": writer(),
+        "hashes": hashes(),
+        "workflows": workflows(),
+        "wf_intents": WF,
+    }
+    with open(os.path.join(HERE, "reference_vectors.json"), "w") as f:
+        json.dump(data, f, indent=1, allow_nan=False, default=str)
+    print("wrote", os.path.join(HERE, "reference_vectors.json"))
+
+
+if __name__ == "__main__":
+    main()

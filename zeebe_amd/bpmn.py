@@ -189,19 +189,23 @@ class FlowNodeBuilder:
     def move_to_node(self, ident: str) -> "FlowNodeBuilder":
         return FlowNodeBuilder(self._ctx, self._ctx.by_id[ident])
 
+    def _find_last_gateway(self, tags) -> "FlowNodeBuilder":
+        # AbstractFlowNodeBuilder.findLastGateway :326-339: walk unique previous nodes backwards
+        node = self._node
+        while True:
+            prev = [n for n in self._all_nodes() if n.tag == "bpmn:sequenceFlow"
+                    and n.attrs.get("targetRef") == node.id]
+            if len(prev) != 1:
+                raise ValueError("Unable to determine an unique previous gateway of %s" % node.id)
+            node = self._ctx.by_id[prev[0].attrs["sourceRef"]]
+            if node.tag in tags:
+                return FlowNodeBuilder(self._ctx, node)
+
     def move_to_last_gateway(self) -> "FlowNodeBuilder":
-        n = self._node
-        # last gateway created in document order within this scope chain
-        for cand in reversed(self._all_nodes()):
-            if cand.tag in ("bpmn:exclusiveGateway", "bpmn:parallelGateway"):
-                return FlowNodeBuilder(self._ctx, cand)
-        raise ValueError("no gateway before %s" % n.id)
+        return self._find_last_gateway(("bpmn:exclusiveGateway", "bpmn:parallelGateway"))
 
     def move_to_last_exclusive_gateway(self) -> "FlowNodeBuilder":
-        for cand in reversed(self._all_nodes()):
-            if cand.tag == "bpmn:exclusiveGateway":
-                return FlowNodeBuilder(self._ctx, cand)
-        raise ValueError("no exclusive gateway")
+        return self._find_last_gateway(("bpmn:exclusiveGateway",))
 
     def _all_nodes(self) -> List[_Node]:
         out: List[_Node] = []
