@@ -1,0 +1,147 @@
+/*
+ * zb_engine.h — C ABI of the MI355X batched BPMN stepping core (libzbgpu.so).
+ *
+ * This is the drop-in boundary for the reference's workflow-instance stepping path: a thin
+ * JNI/FFI shim registered as the reference's TypedRecordProcessor for the same
+ * (recordType, valueType, intent) keys as
+ *   broker-core/src/main/java/io/zeebe/broker/workflow/processor/WorkflowInstanceStreamProcessor.java:103-169
+ * forwards the records of one processing tick into zb_submit_*, calls zb_step, and appends the
+ * records returned by zb_drain to the log (INTEGRATION.md shows the binding).
+ *
+ * Conventions:
+ *   - plain C types only, caller-owned buffers, int status codes (0 ok, <0 error); nothing throws
+ *     across the ABI and no pointer passed in is retained after the call returns;
+ *   - one handle = one partition = one HIP device + one HIP stream; a handle is thread-affine
+ *     (the reference runs one actor per stream processor, StreamProcessorController.java:39);
+ *   - records come back in exact reference log order (FIFO == breadth-first waves),
+ *     with keys from the partition's KeyGenerator(1, 5) / job KeyGenerator(2, 5)
+ *     (broker-core/.../logstreams/processor/KeyGenerator.java:28-60).
+ */
+#ifndef ZB_ENGINE_H
+#define ZB_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------------------------- */
+#define ZB_OK 0
+#define ZB_EINVAL (-1)        /* bad argument */
+#define ZB_ENOMEM (-2)        /* device capacity (log / element rows / payload arena) exhausted */
+#define ZB_EUNSUPPORTED (-3)  /* model or payload shape the GPU path does not implement (never a silent fallback) */
+#define ZB_EDEPLOY (-4)       /* deployment resource rejected (parse / transform / condition compile error) */
+#define ZB_EDEVICE (-5)       /* HIP runtime error */
+#define ZB_EAGAIN (-6)        /* stepping stopped at max_waves before quiescence; call zb_step again */
+#define ZB_EPROCESSING (-7)   /* processing failure: the partition stops (StreamProcessorController.onFailure) */
+
+/* ---- protocol enums (protocol/src/main/resources/protocol.xml:31-67, protocol intent classes) -- */
+#define ZB_VT_JOB 0
+#define ZB_VT_WORKFLOW_INSTANCE 5
+#define ZB_VT_INCIDENT 6
+#define ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION 12
+#define ZB_RT_EVENT 0
+#define ZB_RT_COMMAND 1
+#define ZB_RT_COMMAND_REJECTION 2
+
+typedef struct zb_engine zb_engine;
+
+typedef struct zb_config {
+  int32_t device;           /* HIP device ordinal */
+  int32_t partition_id;
+  int32_t partition_count;
+  int32_t reserved0;
+  uint64_t log_capacity;    /* max records in the device log (32 B descriptor + 8 B row links each) */
+  uint64_t row_capacity;    /* max element-instance rows (SoA state, 64 B each) */
+  uint64_t arena_bytes;     /* payload arena (msgpack documents, 8-byte aligned blobs) */
+  uint64_t staging_records; /* max records staged by zb_submit_* between steps */
+} zb_config;
+
+/* The 32-byte record descriptor kept in HBM for every record of the log. */
+typedef struct zb_rec {
+  int64_t key;        /* record key (-1 = null key) */
+  int64_t scope_key;  /* WF: value.scopeInstanceKey; JOB: headers.activityInstanceKey; INCIDENT: activityInstanceKey */
+  int64_t inst_key;   /* value.workflowInstanceKey */
+  uint32_t payload;   /* payload ref (arena offset / 8); INCIDENT: detail ref */
+  uint16_t elem;      /* global element index (value.activityId); 0xffff = none */
+  uint8_t intent;
+  uint8_t kind;       /* bits 0-3 value type, bits 4-5 record type, bit 6 = 2nd record of a batch */
+} zb_rec;
+
+/* Serialized record as handed back for log append. value bytes are the exact msgpack value
+ * (UnpackedObject.write) of the reference record; position = log sequence number. */
+typedef struct zb_record_header {
+  int64_t position;
+  int64_t source_position;
+  int64_t key;
+  uint8_t record_type;
+  uint8_t value_type;
+  uint8_t intent;
+  uint8_t rejection_type; /* 255 = none */
+  uint32_t value_length;
+  uint64_t value_offset;  /* into the value buffer passed to zb_drain */
+} zb_record_header;
+
+typedef struct zb_step_stats {
+  uint64_t waves;              /* wave kernels that processed >= 1 record */
+  uint64_t launches;           /* wave kernels launched (incl. the final empty one) */
+  uint64_t records_processed;
+  uint64_t records_written;
+  uint64_t transitions;        /* WORKFLOW_INSTANCE events written (streamprocessor_events_count{written}, WF only) */
+  uint64_t completed_instances;/* process-level ELEMENT_COMPLETED written */
+  uint64_t merges;             /* default output merges performed */
+  uint64_t merge_bytes;        /* sum of (job + scope + result) payload bytes of those merges */
+  uint64_t condition_payload_bytes; /* payload bytes read by exclusive-gateway evaluations */
+  double wave_kernel_ms;       /* sum of per-launch wave kernel durations (HIP events on the engine stream) */
+  double wall_ms;              /* host wall time of the zb_step call */
+} zb_step_stats;
+
+/* ---- lifecycle ------------------------------------------------------------------------- */
+int zb_engine_create(const zb_config* cfg, zb_engine** out);
+void zb_engine_destroy(zb_engine* e);
+const char* zb_last_error(const zb_engine* e);
+/* Clears records, element instances, payloads and key generators (deployments stay).
+ * keep_staged != 0 keeps the staged input batch so that it is injected again by the next zb_step. */
+int zb_reset(zb_engine* e, int keep_staged);
+
+/* ---- deployment (WorkflowCache.addWorkflow + BpmnTransformer) -------------------------- */
+/* Deploys every executable process of a BPMN 2.0 XML resource; process i gets workflow_key + i. */
+int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t* bpmn_xml, size_t len);
+/* Canonical job harness: payload of the JOB COMPLETED event appended for every
+ * JOB CREATE command of the given service task (default: empty document). */
+int zb_set_job_completion_payload(zb_engine* e, int64_t workflow_key, const char* activity_id,
+                                  const uint8_t* payload, size_t len);
+
+/* ---- input --------------------------------------------------------------------------- */
+/* Stages n WORKFLOW_INSTANCE CREATE commands (ExecuteCommandRequest, ClientApiMessageHandler.java:147-162)
+ * addressed like the reference's CreateWorkflowInstanceEventProcessor: workflow_key > 0 by key,
+ * else version > 0 by (bpmn_process_id, version), else latest version of bpmn_process_id.
+ * payloads: concatenated msgpack documents, offsets[i]..offsets[i+1] (n+1 entries). */
+int zb_submit_creates(zb_engine* e, const char* bpmn_process_id, int32_t version, int64_t workflow_key,
+                      size_t n, const uint8_t* payloads, const uint64_t* offsets);
+
+/* ---- stepping ------------------------------------------------------------------------ */
+/* Injects staged input at the log tail and runs lockstep waves until quiescence (ZB_OK) or
+ * max_waves (ZB_EAGAIN). stats may be NULL. */
+int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats);
+
+/* ---- output -------------------------------------------------------------------------- */
+int64_t zb_log_size(zb_engine* e);
+/* Copies raw descriptors [start, start+count) to host. */
+int zb_read_descriptors(zb_engine* e, int64_t start, int64_t count, zb_rec* out);
+/* Serializes records [start, start+count) on the GPU into reference value bytes and copies them
+ * back: headers[count], value bytes into values (capacity values_cap); *values_len = bytes needed.
+ * If values_cap is too small nothing is copied and ZB_ENOMEM is returned with *values_len set. */
+int zb_drain(zb_engine* e, int64_t start, int64_t count, zb_record_header* headers, uint8_t* values,
+             size_t values_cap, size_t* values_len);
+/* counters: [0] created [1] completed [2] canceled [3] next wf key [4] next job key
+ *           [5] rows allocated [6] arena bytes used [7] log size */
+int zb_counters(zb_engine* e, int64_t out[8]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ZB_ENGINE_H */

@@ -1,0 +1,132 @@
+"""GPU engine (libzbgpu.so, via its C ABI) vs the oracle, record for record.
+
+Every record the GPU writes is compared with the oracle's record at the same log position:
+key, record type, value type, intent and the full msgpack value bytes (bit-exact). Sizes are
+chosen so the oracle finishes in seconds; BASELINE-size runs are checked through size-independent
+properties (tests/test_gpu_properties.py).
+"""
+import msgpack
+import pytest
+
+from oracle import zbref
+from zeebe_amd import bpmn, workloads
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(**kw):
+    from zeebe_amd.engine import Engine
+
+    return Engine(**kw)
+
+
+def _run_both(xml, process, payloads, job_payloads=None, wf_key=100, **cap):
+    o = zbref.Oracle()
+    o.deploy(xml, wf_key, 1)
+    e = _engine(**cap)
+    e.deploy(xml, wf_key, 1)
+    for act, p in (job_payloads or {}).items():
+        o.set_job_payload(wf_key, act, p)
+        e.set_job_payload(wf_key, act, p)
+    for p in payloads:
+        o.create(process, p)
+    e.create(process, payloads)
+    o.run()
+    st = e.step()
+    assert st["quiescent"]
+    return o, e, st
+
+
+def _compare(o, e):
+    ref = o.records()
+    got = e.records()
+    assert len(got) == len(ref), (len(got), len(ref))
+    for a, b in zip(ref, got):
+        assert (a.position, a.key, a.record_type, a.value_type, a.intent) == \
+               (b.position, b.key, b.record_type, b.value_type, b.intent), (a, b)
+        assert a.value == b.value, (a.position, msgpack.unpackb(a.value, raw=False),
+                                    msgpack.unpackb(b.value, raw=False))
+    return ref
+
+
+def test_golden_workflows(vectors):
+    for spec in vectors["workflows"]:
+        payloads = [bytes.fromhex(i["payload"]) for i in spec["instances"]]
+        jp = {}
+        if spec["instances"] and "job_payload" in spec["instances"][0]:
+            # one job payload per workflow (the harness schedules per task): use the first
+            jp = {"service": bytes.fromhex(spec["instances"][0]["job_payload"])}
+            payloads = payloads[:1]
+        o, e, st = _run_both(spec["xml"], spec["process"], payloads, jp)
+        _compare(o, e)
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 1000])
+def test_config1_shape(n):
+    cfg = workloads.CONFIGS["c1"]
+    blob, offs = cfg["payloads"](n)
+    o, e, st = _run_both(cfg["workflow"]().to_xml(), cfg["process"], workloads.split(blob, offs), cfg["job_payloads"]())
+    ref = _compare(o, e)
+    assert st["transitions"] == 13 * n
+    assert st["completed_instances"] == n
+    assert o.counters()["completed"] == n
+
+
+@pytest.mark.parametrize("n", [3, 300])
+def test_config2_shape(n):
+    cfg = workloads.CONFIGS["c2"]
+    blob, offs = cfg["payloads"](n)
+    o, e, st = _run_both(cfg["workflow"]().to_xml(), cfg["process"], workloads.split(blob, offs),
+                         cfg["job_payloads"](), log_capacity=1 << 20, row_capacity=1 << 18)
+    _compare(o, e)
+    assert st["transitions"] == 108 * n
+    assert st["merges"] == 20 * n
+
+
+@pytest.mark.parametrize("n", [5, 3000])
+def test_config3_shape(n):
+    cfg = workloads.CONFIGS["c3"]
+    blob, offs = cfg["payloads"](n)
+    o, e, st = _run_both(cfg["workflow"]().to_xml(), cfg["process"], workloads.split(blob, offs))
+    _compare(o, e)
+    assert st["completed_instances"] == n
+
+
+def test_subprocess_chain():
+    cfg = workloads.CONFIGS["c4twin"]
+    blob, offs = cfg["payloads"](200)
+    o, e, st = _run_both(cfg["workflow"]().to_xml(), cfg["process"], workloads.split(blob, offs),
+                         cfg["job_payloads"](), log_capacity=1 << 20, row_capacity=1 << 18)
+    _compare(o, e)
+
+
+def test_condition_incidents_and_rejections():
+    # type errors, missing paths, NaN, no default flow -> IncidentIntent.CREATE commands (CONDITION_ERROR)
+    m = (bpmn.Bpmn.create_executable_process("wf").start_event("s").exclusive_gateway("x")
+         .sequence_flow_id("a").condition("$.foo < 5").end_event("ea").move_to_node("x")
+         .sequence_flow_id("b").condition("$.foo == 'x' || $.bar >= 2.5").end_event("eb").done())
+    payloads = [msgpack.packb(d) for d in
+                ({"foo": 1}, {"foo": 9}, {"foo": "x"}, {"bar": 3}, {"foo": None}, {"foo": float("nan")},
+                 {"foo": 7, "bar": 2.5}, {"foo": [1, 2]}, {"foo": {"a": 1}}, {}, {"foo": 1, "foo2": True})]
+    o, e, st = _run_both(m.to_xml(), "wf", payloads)
+    ref = _compare(o, e)
+    assert any(r.value_type == 6 for r in ref)
+    # unknown process -> CREATE rejection (key generated anyway)
+    o2, e2, _ = _run_both(m.to_xml(), "nope", [b"\x80", b"\x80"])
+    _compare(o2, e2)
+
+
+def test_merge_shapes():
+    # payload shapes through the default output merge (nested maps/arrays, overwrite, new keys)
+    m = (bpmn.Bpmn.create_executable_process("p").start_event("s").service_task("t", type="t")
+         .end_event("e").done())
+    cases = [
+        ({"a": 1, "b": {"c": [1, 2, {"d": "x"}]}}, {"b": 5, "z": [1, {"y": None}]}),
+        ({"a": 1}, {"a": {"nested": True}}),          # source container vs target leaf: target leaf survives
+        ({"a": {"x": 1}}, {"a": 2.5}),               # source leaf wins over target container
+        ({}, {"k%d" % i: i for i in range(20)}),     # map16 header
+        ({"s" * 40: "v" * 300}, {"q": b"\x00\x01"}),  # str8/str16/bin
+    ]
+    for tgt, src in cases:
+        o, e, st = _run_both(m.to_xml(), "p", [msgpack.packb(tgt)], {"t": msgpack.packb(src)})
+        _compare(o, e)

@@ -1,0 +1,167 @@
+// zb_device.hpp — data layout shared by the host model compiler and the gfx950 kernels.
+//
+// Everything the wave kernels read is a flat, 8-byte-aligned table in HBM:
+//   * DevElem[]      one 64-byte row per flow element of every deployed workflow (activityId index)
+//   * DevWorkflow[]  workflow key / version / process element
+//   * code[]         exclusive-gateway condition programs (json-el compiled to a jump program)
+//   * DevConst[]     condition constants; DevQuery[]/DevFilter[] compiled json-path queries
+//   * pool[]         byte pool: element ids, job types, message names, filter keys, string constants
+#pragma once
+#include <cstdint>
+
+#include "../../include/zb_engine.h"
+
+namespace zbg {
+
+constexpr uint16_t NO_ELEM = 0xffff;
+constexpr uint32_t NO_ROW = 0xffffffffu;
+constexpr uint32_t NO_REF = 0xffffffffu;
+
+// element kinds (FlowElementHandler.java:46-57 factories + the process)
+enum Kind : uint8_t { EK_PROCESS = 0, EK_START = 1, EK_END = 2, EK_TASK = 3, EK_SUB = 4, EK_XOR = 5, EK_CATCH = 6,
+                      EK_FLOW = 7 };
+
+// BpmnStep.java:20-54 (same order)
+enum Step : uint8_t {
+  ST_NONE = 0, ST_TAKE_SEQUENCE_FLOW, ST_CONSUME_TOKEN, ST_EXCLUSIVE_SPLIT, ST_CREATE_JOB, ST_APPLY_INPUT_MAPPING,
+  ST_APPLY_OUTPUT_MAPPING, ST_ACTIVATE_GATEWAY, ST_SUBSCRIBE_TO_INTERMEDIATE_MESSAGE, ST_START_STATEFUL_ELEMENT,
+  ST_TRIGGER_END_EVENT, ST_TRIGGER_START_EVENT, ST_TERMINATE_CONTAINED_INSTANCES, ST_TERMINATE_JOB_TASK,
+  ST_TERMINATE_ELEMENT, ST_PROPAGATE_TERMINATION, ST_CANCEL_PROCESS, ST_COMPLETE_PROCESS, ST_UNBOUND = 255
+};
+
+// WorkflowInstanceIntent.java:18-38
+enum WfIntent : uint8_t {
+  WI_CREATE = 0, WI_CREATED = 1, WI_START_EVENT_OCCURRED = 2, WI_END_EVENT_OCCURRED = 3, WI_SEQUENCE_FLOW_TAKEN = 4,
+  WI_GATEWAY_ACTIVATED = 5, WI_ELEMENT_READY = 6, WI_ELEMENT_ACTIVATED = 7, WI_ELEMENT_COMPLETING = 8,
+  WI_ELEMENT_COMPLETED = 9, WI_ELEMENT_TERMINATING = 10, WI_ELEMENT_TERMINATED = 11, WI_CANCEL = 12,
+  WI_CANCELING = 13, WI_UPDATE_PAYLOAD = 14, WI_PAYLOAD_UPDATED = 15
+};
+enum JobIntentG : uint8_t { JI_CREATE = 0, JI_CREATED = 1, JI_COMPLETED = 5, JI_CANCEL = 12 };
+
+// record kind byte
+__host__ __device__ inline uint8_t make_kind(uint8_t vt, uint8_t rt, bool cont) {
+  return (uint8_t)(vt | (rt << 4) | (cont ? 0x40 : 0));
+}
+__host__ __device__ inline uint8_t kind_vt(uint8_t k) { return k & 0x0f; }
+__host__ __device__ inline uint8_t kind_rt(uint8_t k) { return (k >> 4) & 0x03; }
+__host__ __device__ inline bool kind_cont(uint8_t k) { return (k & 0x40) != 0; }
+
+struct DevElem {              // 72 bytes
+  uint8_t kind;
+  uint8_t flags;              // bit0: has io mapping (rejected at deploy for now)
+  uint16_t wf;                // workflow index
+  uint8_t step[12];           // by WF intent 0..11
+  uint16_t out0;              // first executable outgoing flow (TakeSequenceFlowHandler uses get(0))
+  uint16_t target;            // sequence flow target
+  uint16_t start;             // container start event
+  uint16_t dflt;              // exclusive gateway default flow
+  uint16_t cond_begin;        // exclusive gateway: conditioned flows in executable order (cond_flows[])
+  uint16_t cond_count;
+  uint16_t ck_query;          // intermediate message catch: correlation key query
+  uint16_t n_out;             // number of executable outgoing flows
+  uint32_t cond_prog;         // sequence flow: condition program offset in code[] (NO_REF = none)
+  int32_t retries;            // service task
+  uint32_t job_payload;       // service task: harness completion payload ref (0 = {})
+  uint32_t id_off;            // element id (activityId) in pool
+  uint16_t id_len;
+  uint16_t type_len;          // job type length
+  uint32_t type_off;          // job type in pool
+  uint32_t headers_off;       // encoded custom headers in pool (raw msgpack)
+  uint32_t headers_len;
+  uint32_t msg_off;           // message name in pool
+  uint16_t msg_len;
+  uint16_t pad0;
+};
+static_assert(sizeof(DevElem) == 72, "DevElem layout is 72 bytes");
+
+struct DevWorkflow {          // 32 bytes
+  int64_t key;
+  int32_t version;
+  uint16_t process_elem;
+  uint16_t pid_len;           // bpmnProcessId
+  uint32_t pid_off;
+  uint32_t pad[3];
+};
+static_assert(sizeof(DevWorkflow) == 32, "DevWorkflow must stay 32 bytes");
+
+// ---- json-path (JsonPathQueryCompiler filter ids) ----
+enum FilterId : uint8_t { F_ROOT = 0, F_MAP_KEY = 1, F_INDEX = 2, F_WILDCARD = 3 };
+struct DevFilter {            // 16 bytes
+  uint8_t id;
+  uint8_t pad;
+  uint16_t key_len;
+  int32_t index;
+  uint32_t key_off;
+  uint32_t pad2;
+};
+struct DevQuery {             // 16 bytes
+  uint16_t first;             // index of first filter
+  uint16_t count;
+  uint16_t expr_len;          // expression text (for incident messages, host side)
+  uint16_t fast;              // 1: [ROOT, MAP_KEY k] -> top-level lookup fast path
+  uint32_t expr_off;
+  uint32_t pad;
+};
+
+// ---- json-el constants / program ----
+enum TokType : uint8_t { TT_INTEGER = 0, TT_FLOAT = 1, TT_BOOLEAN = 2, TT_NIL = 3, TT_MAP = 4, TT_ARRAY = 5,
+                         TT_BINARY = 6, TT_STRING = 7, TT_EXTENSION = 8 };
+struct DevConst {             // 24 bytes
+  uint8_t type;
+  uint8_t bval;
+  uint16_t str_len;
+  uint32_t str_off;
+  int64_t ival;
+  double fval;
+};
+enum CmpOp : uint8_t { OP_EQ = 0, OP_NE, OP_LT, OP_LE, OP_GT, OP_GE };
+enum Opcode : uint8_t { PC_CMP = 1, PC_JF = 2, PC_JT = 3, PC_END = 4 };
+// one instruction = 2 x uint32:
+//   w0: [7:0] opcode  [11:8] cmp op  [12] lhs is path  [13] rhs is path  [31:16] jump target (instr index)
+//   w1: [15:0] lhs index (const or query)  [31:16] rhs index
+
+// incident detail codes (host formats the reference's error messages)
+enum ErrCode : uint8_t {
+  EC_NO_FLOW = 1,        // "All conditions evaluated to false and no default flow is set."
+  EC_PATH_NO_RESULT = 2, // "JSON path '%s' has no result."
+  EC_PATH_MULTI = 3,     // "JSON path '%s' has more than one result."
+  EC_DIFF_TYPES = 4,     // "Cannot compare values of different types: %s and %s"
+  EC_CMP_TYPE = 5,       // "Cannot compare value of type: %s"
+  EC_NOT_NUMBER = 6,     // "Cannot compare values. Expected number but found: %s"
+  EC_MAPPING_NOT_MAP = 7 // "Processing failed, since mapping will result in a non map object (json object)."
+};
+
+// device error flags (sticky, host checks after each batch of waves)
+enum DevErr : uint32_t {
+  DE_LOG_FULL = 1u, DE_ROWS_FULL = 2u, DE_ARENA_FULL = 4u, DE_UNSUPPORTED = 8u, DE_PROCESSING = 16u,
+  DE_LOOKBACK_TIMEOUT = 32u, DE_BAD_PAYLOAD = 64u
+};
+
+// Per-wave header (double buffered: wave w reads hdr[w&1], writes hdr[(w+1)&1])
+struct WaveHdr {
+  int64_t begin, end;          // input range in the log
+  int64_t wf_next, job_next;   // key generators (next key)
+  int64_t rows_next;           // row allocator
+  int64_t arena_next;          // payload arena bump pointer (bytes)
+  int64_t transitions;         // cumulative WF events written
+  int64_t completed;           // cumulative process-level ELEMENT_COMPLETED
+  int64_t created;             // cumulative CREATED processed
+  int64_t merges, merge_bytes, cond_bytes;
+  int64_t pad[4];
+};
+static_assert(sizeof(WaveHdr) == 128, "WaveHdr is 128 bytes");
+
+// element-instance row hot fields (16 B); keys live in a separate 32 B array
+struct RowMeta {
+  uint32_t payload;
+  uint32_t parent;
+  uint16_t elem;
+  uint8_t state;               // WF intent of the indexed state; 0 = no instance
+  uint8_t flags;
+  int32_t nchild;
+};
+struct RowKeys {
+  int64_t key, scope_key, inst_key, job_key;
+};
+
+}  // namespace zbg

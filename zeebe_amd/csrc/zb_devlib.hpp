@@ -1,0 +1,549 @@
+// zb_devlib.hpp — per-thread msgpack, json-path, json-el and merge routines for the gfx950 kernels.
+//
+// Semantics follow the reference exactly where the hot path observes them:
+//   token reading:     msgpack-core/.../spec/MsgPackReader.java:302-345 (readToken)
+//   query executor:    json-path/.../query/MsgPackQueryExecutor.java:60-144 (full traversal, no early exit)
+//   condition types:   json-el/.../JsonConditionInterpreter.java:138-240
+//   default merge:     json-path/.../mapping/{MsgPackDocumentIndexer,MsgPackTree,MsgPackDocumentTreeWriter}.java
+// Shapes the kernels do not implement set DE_UNSUPPORTED instead of guessing.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "zb_device.hpp"
+
+namespace zbg {
+
+// ------------------------------------------------------------------------------ msgpack reading
+struct Tok {
+  uint8_t type;      // TokType
+  uint8_t hdr;       // header length
+  uint32_t len;      // str/bin payload length, map entries / array elements
+  uint32_t total;    // header + payload (containers: header only)
+  int64_t ival;
+  double fval;
+  bool bval;
+};
+
+__device__ __forceinline__ uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
+__device__ __forceinline__ uint32_t be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+__device__ __forceinline__ uint64_t be64(const uint8_t* p) { return ((uint64_t)be32(p) << 32) | be32(p + 4); }
+
+// Reads the token at p (n bytes available). Returns false on malformed / unsupported input.
+__device__ inline bool read_tok(const uint8_t* p, uint32_t n, Tok& t) {
+  if (n == 0) return false;
+  uint8_t b = p[0];
+  t.hdr = 1; t.len = 0; t.ival = 0; t.fval = 0; t.bval = false;
+  if (b <= 0x7f || b >= 0xe0) { t.type = TT_INTEGER; t.ival = (int8_t)b; t.total = 1; return true; }
+  if ((b & 0xf0) == 0x80) { t.type = TT_MAP; t.len = b & 0x0f; t.total = 1; return true; }
+  if ((b & 0xf0) == 0x90) { t.type = TT_ARRAY; t.len = b & 0x0f; t.total = 1; return true; }
+  if ((b & 0xe0) == 0xa0) { t.type = TT_STRING; t.len = b & 0x1f; t.total = 1 + t.len; return t.total <= n; }
+  uint32_t need;
+  switch (b) {
+    case 0xc0: t.type = TT_NIL; t.total = 1; return true;
+    case 0xc2: case 0xc3: t.type = TT_BOOLEAN; t.bval = b == 0xc3; t.total = 1; return true;
+    case 0xcc: if (n < 2) return false; t.type = TT_INTEGER; t.ival = p[1]; t.total = 2; return true;
+    case 0xcd: if (n < 3) return false; t.type = TT_INTEGER; t.ival = be16(p + 1); t.total = 3; return true;
+    case 0xce: if (n < 5) return false; t.type = TT_INTEGER; t.ival = be32(p + 1); t.total = 5; return true;
+    case 0xcf: if (n < 9) return false; t.type = TT_INTEGER; t.ival = (int64_t)be64(p + 1); t.total = 9;
+      return t.ival >= 0;  // MsgPackReader.ensurePositive
+    case 0xd0: if (n < 2) return false; t.type = TT_INTEGER; t.ival = (int8_t)p[1]; t.total = 2; return true;
+    case 0xd1: if (n < 3) return false; t.type = TT_INTEGER; t.ival = (int16_t)be16(p + 1); t.total = 3; return true;
+    case 0xd2: if (n < 5) return false; t.type = TT_INTEGER; t.ival = (int32_t)be32(p + 1); t.total = 5; return true;
+    case 0xd3: if (n < 9) return false; t.type = TT_INTEGER; t.ival = (int64_t)be64(p + 1); t.total = 9; return true;
+    case 0xca: {
+      if (n < 5) return false;
+      uint32_t u = be32(p + 1);
+      t.type = TT_FLOAT; t.fval = (double)__uint_as_float(u); t.total = 5; return true;
+    }
+    case 0xcb: {
+      if (n < 9) return false;
+      t.type = TT_FLOAT; t.fval = __longlong_as_double((long long)be64(p + 1)); t.total = 9; return true;
+    }
+    case 0xd9: if (n < 2) return false; t.type = TT_STRING; t.len = p[1]; t.hdr = 2; break;
+    case 0xda: if (n < 3) return false; t.type = TT_STRING; t.len = be16(p + 1); t.hdr = 3; break;
+    case 0xdb: if (n < 5) return false; t.type = TT_STRING; t.len = be32(p + 1); t.hdr = 5; break;
+    case 0xc4: if (n < 2) return false; t.type = TT_BINARY; t.len = p[1]; t.hdr = 2; break;
+    case 0xc5: if (n < 3) return false; t.type = TT_BINARY; t.len = be16(p + 1); t.hdr = 3; break;
+    case 0xc6: if (n < 5) return false; t.type = TT_BINARY; t.len = be32(p + 1); t.hdr = 5; break;
+    case 0xdc: if (n < 3) return false; t.type = TT_ARRAY; t.len = be16(p + 1); t.total = 3; return true;
+    case 0xdd: if (n < 5) return false; t.type = TT_ARRAY; t.len = be32(p + 1); t.total = 5; return true;
+    case 0xde: if (n < 3) return false; t.type = TT_MAP; t.len = be16(p + 1); t.total = 3; return true;
+    case 0xdf: if (n < 5) return false; t.type = TT_MAP; t.len = be32(p + 1); t.total = 5; return true;
+    default: return false;  // extensions / never-used: "Unsupported token format"
+  }
+  need = t.hdr + t.len;
+  if (need > n || (int32_t)t.len < 0) return false;
+  t.total = need;
+  return true;
+}
+
+// Returns the offset just past the value starting at pos, or 0xffffffff if malformed.
+__device__ inline uint32_t skip_value(const uint8_t* d, uint32_t n, uint32_t pos) {
+  uint64_t pending = 1;
+  while (pending > 0) {
+    Tok t;
+    if (pos >= n || !read_tok(d + pos, n - pos, t)) return 0xffffffffu;
+    pos += t.total;
+    pending -= 1;
+    if (t.type == TT_MAP) pending += 2ull * t.len;
+    else if (t.type == TT_ARRAY) pending += t.len;
+  }
+  return pos;
+}
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+
+// ------------------------------------------------------------------------------ json-path
+struct QueryResult {
+  uint32_t count;   // number of results (saturating)
+  uint32_t pos, len;  // first result
+};
+
+// [ROOT, MAP_KEY k] fast path: every top-level value under key k (the executor's results for this
+// two-filter query are exactly those, in document order; container values are whole results).
+__device__ inline bool query_fast(const uint8_t* d, uint32_t n, const uint8_t* key, uint32_t klen,
+                                  QueryResult& r) {
+  r.count = 0; r.pos = 0; r.len = 0;
+  Tok t;
+  if (!read_tok(d, n, t)) return n == 0;
+  if (t.type != TT_MAP) return true;  // root filter needs a container; arrays give no key matches
+  uint32_t pos = t.total;
+  for (uint32_t i = 0; i < t.len; i++) {
+    Tok k;
+    if (pos >= n || !read_tok(d + pos, n - pos, k)) return false;
+    uint32_t kpos = pos;
+    pos += k.total;
+    uint32_t vend = skip_value(d, n, pos);
+    if (vend == 0xffffffffu) return false;
+    if (k.type == TT_STRING && k.len == klen && bytes_eq(d + kpos + k.hdr, key, klen)) {
+      if (r.count == 0) { r.pos = pos; r.len = vend - pos; }
+      r.count++;
+    } else if (k.type == TT_MAP || k.type == TT_ARRAY) {
+      return false;  // container map keys: the reference's traversal would descend; not supported here
+    }
+    pos = vend;
+  }
+  return true;
+}
+
+// General executor (literal state machine of MsgPackQueryExecutor.visitElement), depth <= 30.
+constexpr int JP_MAX_DEPTH = 30;
+__device__ inline bool query_general(const uint8_t* d, uint32_t n, const DevFilter* f, uint32_t nf,
+                                     const uint8_t* pool, QueryResult& r) {
+  r.count = 0; r.pos = 0; r.len = 0;
+  int cur[JP_MAX_DEPTH], num[JP_MAX_DEPTH], app[JP_MAX_DEPTH], dyn[JP_MAX_DEPTH];
+  bool ismap[JP_MAX_DEPTH];
+  int depth = 0;
+  int matching = -1;
+  uint32_t mstart = 0;
+  uint32_t pos = 0;
+  if (nf == 0) return true;
+  while (pos < n) {
+    Tok t;
+    if (!read_tok(d + pos, n - pos, t)) return true;  // traverser stops on an invalid token
+    int cf = 0;
+    if (depth > 0) { cur[depth - 1] += 1; cf = app[depth - 1]; }
+    bool match = false;
+    if (cf >= 0) {
+      const DevFilter& F = f[cf];
+      switch (F.id) {
+        case F_ROOT: match = depth == 0 && (t.type == TT_MAP || t.type == TT_ARRAY); break;
+        case F_MAP_KEY:
+          if (depth > 0 && ismap[depth - 1]) {
+            int L = depth - 1;
+            if (cur[L] == 0) dyn[L] = -1;
+            if (cur[L] == dyn[L]) { dyn[L] = -1; match = true; }
+            else if (cur[L] % 2 == 0 && t.type == TT_STRING && t.len == F.key_len &&
+                     bytes_eq(d + pos + t.hdr, pool + F.key_off, F.key_len))
+              dyn[L] = cur[L] + 1;
+          }
+          break;
+        case F_INDEX: match = depth > 0 && !ismap[depth - 1] && F.index == cur[depth - 1]; break;
+        case F_WILDCARD: match = (depth > 0 && ismap[depth - 1]) ? (cur[depth - 1] % 2 != 0) : true; break;
+      }
+    }
+    if (t.type == TT_MAP || t.type == TT_ARRAY) {
+      if (depth >= JP_MAX_DEPTH) return false;
+      cur[depth] = -1;
+      num[depth] = t.type == TT_MAP ? 2 * (int)t.len : (int)t.len;
+      app[depth] = -1;
+      ismap[depth] = t.type == TT_MAP;
+      dyn[depth] = 0;
+      depth++;
+    }
+    if (match) {
+      if ((uint32_t)cf + 1 == nf) {
+        if (t.type != TT_MAP && t.type != TT_ARRAY) {
+          if (r.count == 0) { r.pos = pos; r.len = t.total; }
+          r.count++;
+        } else {
+          matching = depth - 1;
+          mstart = pos;
+        }
+      } else {
+        app[depth - 1 < 0 ? 0 : depth - 1] = cf + 1;
+      }
+    }
+    pos += t.total;
+    while (depth > 0 && cur[depth - 1] + 1 >= num[depth - 1]) {
+      if (matching == depth - 1) {
+        if (r.count == 0) { r.pos = mstart; r.len = pos - mstart; }
+        r.count++;
+        matching = -1;
+      }
+      depth--;
+    }
+  }
+  return true;
+}
+
+__device__ inline bool run_query(const uint8_t* d, uint32_t n, const DevQuery& q, const DevFilter* filters,
+                                 const uint8_t* pool, QueryResult& r) {
+  if (q.fast) {
+    const DevFilter& k = filters[q.first + 1];
+    return query_fast(d, n, pool + k.key_off, k.key_len, r);
+  }
+  return query_general(d, n, filters + q.first, q.count, pool, r);
+}
+
+// ------------------------------------------------------------------------------ json-el VM
+struct CondOut {
+  uint8_t err;   // 0 ok, else ErrCode
+  uint8_t a, b;  // type codes / args
+  uint16_t q;    // query index for path errors
+};
+
+struct Operand {
+  uint8_t type;
+  bool bval;
+  int64_t ival;
+  double fval;
+  const uint8_t* s;
+  uint32_t slen;
+};
+
+__device__ inline bool load_operand(bool is_path, uint32_t idx, const uint8_t* doc, uint32_t n, const DevConst* consts,
+                                    const DevQuery* queries, const DevFilter* filters, const uint8_t* pool,
+                                    Operand& o, CondOut& out, bool& unsupported) {
+  if (!is_path) {
+    const DevConst& c = consts[idx];
+    o.type = c.type; o.bval = c.bval; o.ival = c.ival; o.fval = c.fval; o.s = pool + c.str_off; o.slen = c.str_len;
+    return true;
+  }
+  QueryResult r;
+  if (!run_query(doc, n, queries[idx], filters, pool, r)) { unsupported = true; return false; }
+  if (r.count == 0) { out.err = EC_PATH_NO_RESULT; out.q = (uint16_t)idx; return false; }
+  if (r.count > 1) { out.err = EC_PATH_MULTI; out.q = (uint16_t)idx; return false; }
+  Tok t;
+  if (!read_tok(doc + r.pos, r.len, t)) { unsupported = true; return false; }
+  o.type = t.type; o.bval = t.bval; o.ival = t.ival; o.fval = t.fval;
+  o.s = doc + r.pos + t.hdr; o.slen = t.len;
+  return true;
+}
+
+// ensureSameType: INTEGER<->FLOAT promotion, else error on type mismatch
+__device__ __forceinline__ bool same_type(Operand& x, Operand& y, CondOut& out) {
+  if (x.type == TT_INTEGER && y.type == TT_FLOAT) { x.type = TT_FLOAT; x.fval = (double)x.ival; }
+  else if (x.type == TT_FLOAT && y.type == TT_INTEGER) { y.type = TT_FLOAT; y.fval = (double)y.ival; }
+  else if (x.type != y.type) { out.err = EC_DIFF_TYPES; out.a = x.type; out.b = y.type; return false; }
+  return true;
+}
+
+// Evaluates one compiled condition; returns result (valid when out.err == 0 && !unsupported).
+__device__ inline bool eval_condition(uint32_t pc, const uint32_t* code, const uint8_t* doc, uint32_t n,
+                                      const DevConst* consts, const DevQuery* queries, const DevFilter* filters,
+                                      const uint8_t* pool, CondOut& out, bool& unsupported) {
+  bool r = false;
+  out.err = 0;
+  for (int guard = 0; guard < 4096; guard++) {
+    uint32_t w0 = code[2 * pc], w1 = code[2 * pc + 1];
+    uint32_t opc = w0 & 0xff;
+    if (opc == PC_END) return r;
+    if (opc == PC_JF) { if (!r) { pc = w0 >> 16; continue; } pc++; continue; }
+    if (opc == PC_JT) { if (r) { pc = w0 >> 16; continue; } pc++; continue; }
+    // PC_CMP
+    uint32_t op = (w0 >> 8) & 0xf;
+    Operand x, y;
+    if (!load_operand((w0 >> 12) & 1, w1 & 0xffff, doc, n, consts, queries, filters, pool, x, out, unsupported))
+      return false;
+    if (!load_operand((w0 >> 13) & 1, w1 >> 16, doc, n, consts, queries, filters, pool, y, out, unsupported))
+      return false;
+    if (op == OP_EQ || op == OP_NE) {
+      bool eq;
+      if (x.type == TT_NIL) eq = y.type == TT_NIL;
+      else if (y.type == TT_NIL) eq = false;
+      else {
+        if (!same_type(x, y, out)) return false;
+        switch (x.type) {
+          case TT_STRING: eq = x.slen == y.slen && bytes_eq(x.s, y.s, x.slen); break;
+          case TT_BOOLEAN: eq = x.bval == y.bval; break;
+          case TT_INTEGER: eq = x.ival == y.ival; break;
+          case TT_FLOAT: eq = x.fval == y.fval; break;
+          default: out.err = EC_CMP_TYPE; out.a = x.type; return false;
+        }
+      }
+      r = (op == OP_EQ) ? eq : !eq;
+    } else {
+      if (!same_type(x, y, out)) return false;
+      if (x.type != TT_INTEGER && x.type != TT_FLOAT) { out.err = EC_NOT_NUMBER; out.a = x.type; return false; }
+      if (x.type == TT_INTEGER) {
+        r = op == OP_LT ? x.ival < y.ival : op == OP_LE ? x.ival <= y.ival : op == OP_GT ? x.ival > y.ival
+                                                                                       : x.ival >= y.ival;
+      } else {
+        r = op == OP_LT ? x.fval < y.fval : op == OP_LE ? x.fval <= y.fval : op == OP_GT ? x.fval > y.fval
+                                                                                       : x.fval >= y.fval;
+      }
+    }
+    pc++;
+  }
+  unsupported = true;
+  return false;
+}
+
+// ------------------------------------------------------------------------------ merge
+// Top-level merge(source = job/message payload, target = scope payload), MappingProcessor.merge
+// without mappings. Implemented structurally:
+//   root children = target keys (document order) then source keys not in target;
+//   value = source's if present (MsgPackTree.merge: source node types/leaves win, non-root child
+//   sets replaced), else target's; a target *leaf* at the same path as a source container wins
+//   (stale leafMap entry; MsgPackDocumentTreeWriter checks isLeaf first).
+// Containers are re-encoded with minimal headers and keys re-encoded as minimal strings, leaves
+// copied raw (MsgPackDocumentTreeWriter.writeNode). Unsupported (flagged): duplicate keys, keys
+// containing '[' / ']' (node-id collisions in the reference), non-string keys, source and target
+// both holding a container under the same top-level key, depth > MERGE_MAX_DEPTH.
+constexpr int MERGE_MAX_DEPTH = 16;
+
+struct Out {
+  uint8_t* dst;   // nullptr: size pass
+  uint32_t n;
+  __device__ __forceinline__ void put(uint8_t b) { if (dst) dst[n] = b; n++; }
+  __device__ __forceinline__ void put_bytes(const uint8_t* s, uint32_t len) {
+    if (dst) for (uint32_t i = 0; i < len; i++) dst[n + i] = s[i];
+    n += len;
+  }
+  __device__ inline void map_hdr(uint32_t c) {
+    if (c < 16) put(0x80 | c);
+    else if (c < 65536) { put(0xde); put(c >> 8); put(c & 0xff); }
+    else { put(0xdf); put(c >> 24); put((c >> 16) & 0xff); put((c >> 8) & 0xff); put(c & 0xff); }
+  }
+  __device__ inline void arr_hdr(uint32_t c) {
+    if (c < 16) put(0x90 | c);
+    else if (c < 65536) { put(0xdc); put(c >> 8); put(c & 0xff); }
+    else { put(0xdd); put(c >> 24); put((c >> 16) & 0xff); put((c >> 8) & 0xff); put(c & 0xff); }
+  }
+  __device__ inline void str(const uint8_t* s, uint32_t c) {
+    if (c < 32) put(0xa0 | c);
+    else if (c < 256) { put(0xd9); put(c); }
+    else if (c < 65536) { put(0xda); put(c >> 8); put(c & 0xff); }
+    else { put(0xdb); put(c >> 24); put((c >> 16) & 0xff); put((c >> 8) & 0xff); put(c & 0xff); }
+    put_bytes(s, c);
+  }
+};
+
+__device__ inline bool key_ok(const uint8_t* s, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++)
+    if (s[i] == '[' || s[i] == ']') return false;
+  return true;
+}
+
+// Re-encodes the value at pos (a subtree of one document) the way the tree writer would,
+// given that no node of the other document shadows it. Returns end offset or 0xffffffff.
+__device__ inline uint32_t reencode(const uint8_t* d, uint32_t n, uint32_t pos, Out& o, bool& unsupported) {
+  // explicit stack of remaining children per open container; keys re-encoded, leaves raw
+  uint32_t remain[MERGE_MAX_DEPTH];
+  bool is_map[MERGE_MAX_DEPTH];
+  bool expect_key[MERGE_MAX_DEPTH];
+  int depth = 0;
+  for (;;) {
+    Tok t;
+    if (pos >= n || !read_tok(d + pos, n - pos, t)) return 0xffffffffu;
+    bool key_slot = depth > 0 && is_map[depth - 1] && expect_key[depth - 1];
+    if (key_slot) {
+      if (t.type != TT_STRING || !key_ok(d + pos + t.hdr, t.len)) { unsupported = true; return 0xffffffffu; }
+      // duplicate key check among the siblings already passed is done by the caller for the root;
+      // nested maps: check the rest of this map for the same key
+      o.str(d + pos + t.hdr, t.len);
+      pos += t.total;
+      expect_key[depth - 1] = false;
+      continue;
+    }
+    if (t.type == TT_MAP || t.type == TT_ARRAY) {
+      if (t.type == TT_MAP) {
+        // duplicate keys inside a nested map would be deduplicated by LinkedHashSet: flag them
+        uint32_t kp = pos + t.total;
+        for (uint32_t i = 0; i < t.len; i++) {
+          Tok ki;
+          if (kp >= n || !read_tok(d + kp, n - kp, ki)) return 0xffffffffu;
+          uint32_t vend_i = skip_value(d, n, kp + ki.total);
+          if (vend_i == 0xffffffffu) return vend_i;
+          uint32_t kj = vend_i;
+          for (uint32_t j = i + 1; j < t.len; j++) {
+            Tok kk;
+            if (kj >= n || !read_tok(d + kj, n - kj, kk)) return 0xffffffffu;
+            if (kk.type == ki.type && kk.len == ki.len && bytes_eq(d + kj + kk.hdr, d + kp + ki.hdr, ki.len)) {
+              unsupported = true;
+              return 0xffffffffu;
+            }
+            kj = skip_value(d, n, kj + kk.total);
+            if (kj == 0xffffffffu) return kj;
+          }
+          kp = vend_i;
+        }
+        o.map_hdr(t.len);
+      } else {
+        o.arr_hdr(t.len);
+      }
+      pos += t.total;
+      if (t.len > 0) {
+        if (depth >= MERGE_MAX_DEPTH) { unsupported = true; return 0xffffffffu; }
+        remain[depth] = t.len;
+        is_map[depth] = t.type == TT_MAP;
+        expect_key[depth] = t.type == TT_MAP;
+        depth++;
+        continue;
+      }
+    } else {
+      o.put_bytes(d + pos, t.total);
+      pos += t.total;
+    }
+    // a value completed: pop finished containers
+    while (depth > 0) {
+      remain[depth - 1] -= 1;
+      if (remain[depth - 1] > 0) {
+        if (is_map[depth - 1]) expect_key[depth - 1] = true;
+        break;
+      }
+      depth--;
+    }
+    if (depth == 0) return pos;
+  }
+}
+
+struct RootEntry {
+  uint32_t kpos, klen, vpos, vend;
+};
+
+// find key in a root map starting after the header; returns entry via e (vpos==0 if absent)
+__device__ inline bool find_key(const uint8_t* d, uint32_t n, uint32_t first, uint32_t count, const uint8_t* key,
+                                uint32_t klen, RootEntry& e) {
+  uint32_t pos = first;
+  for (uint32_t i = 0; i < count; i++) {
+    Tok k;
+    if (pos >= n || !read_tok(d + pos, n - pos, k)) return false;
+    uint32_t vp = pos + k.total;
+    uint32_t ve = skip_value(d, n, vp);
+    if (ve == 0xffffffffu) return false;
+    if (k.type == TT_STRING && k.len == klen && bytes_eq(d + pos + k.hdr, key, klen)) {
+      e.kpos = pos + k.hdr; e.klen = k.len; e.vpos = vp; e.vend = ve;
+      return true;
+    }
+    pos = ve;
+  }
+  e.vpos = 0;
+  return true;
+}
+
+// Validates a root map: string keys, no brackets, no duplicates. Returns false on malformed.
+__device__ inline bool check_root(const uint8_t* d, uint32_t n, uint32_t first, uint32_t count, bool& unsupported) {
+  uint32_t pos = first;
+  for (uint32_t i = 0; i < count; i++) {
+    Tok k;
+    if (pos >= n || !read_tok(d + pos, n - pos, k)) return false;
+    if (k.type != TT_STRING || !key_ok(d + pos + k.hdr, k.len)) { unsupported = true; return true; }
+    uint32_t vp = pos + k.total;
+    uint32_t ve = skip_value(d, n, vp);
+    if (ve == 0xffffffffu) return false;
+    // duplicates among later keys
+    RootEntry e;
+    uint32_t rest = ve;
+    uint32_t remaining = count - i - 1;
+    if (remaining > 0) {
+      if (!find_key(d, n, rest, remaining, d + pos + k.hdr, k.len, e)) return false;
+      if (e.vpos != 0) { unsupported = true; return true; }
+    }
+    pos = ve;
+  }
+  return true;
+}
+
+// Performs the merge into o (size pass when o.dst == nullptr). Returns false when malformed.
+__device__ inline bool merge_docs(const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint32_t nt, Out& o,
+                                  bool& unsupported) {
+  Tok ts, tt;
+  bool src_nil = ns == 0 || (ns >= 1 && src[0] == 0xc0);
+  bool tgt_nil = nt == 0 || (nt >= 1 && tgt[0] == 0xc0);
+  if (!src_nil && (!read_tok(src, ns, ts) || ts.type != TT_MAP)) { unsupported = true; return true; }
+  if (!tgt_nil && (!read_tok(tgt, nt, tt) || tt.type != TT_MAP)) { unsupported = true; return true; }
+  // empty tree -> writeNil; the only consumer (DocumentValue.wrap) turns NIL into {} (0x80)
+  if (src_nil && tgt_nil) { o.put(0x80); return true; }
+  uint32_t sc = src_nil ? 0 : ts.len, tc = tgt_nil ? 0 : tt.len;
+  uint32_t sf = src_nil ? 0 : ts.total, tf = tgt_nil ? 0 : tt.total;
+  if (!src_nil && !check_root(src, ns, sf, sc, unsupported)) return false;
+  if (!tgt_nil && !check_root(tgt, nt, tf, tc, unsupported)) return false;
+  if (unsupported) return true;
+  // count result keys
+  uint32_t total = tc;
+  {
+    uint32_t pos = sf;
+    for (uint32_t i = 0; i < sc; i++) {
+      Tok k;
+      read_tok(src + pos, ns - pos, k);
+      RootEntry e;
+      if (!find_key(tgt, nt, tf, tc, src + pos + k.hdr, k.len, e)) return false;
+      if (e.vpos == 0) total++;
+      pos = skip_value(src, ns, pos + k.total);
+    }
+  }
+  o.map_hdr(total);
+  // target keys in order
+  uint32_t pos = tf;
+  for (uint32_t i = 0; i < tc; i++) {
+    Tok k;
+    read_tok(tgt + pos, nt - pos, k);
+    uint32_t vp = pos + k.total;
+    uint32_t ve = skip_value(tgt, nt, vp);
+    o.str(tgt + pos + k.hdr, k.len);
+    RootEntry e;
+    if (!find_key(src, ns, sf, sc, tgt + pos + k.hdr, k.len, e)) return false;
+    if (e.vpos == 0) {
+      if (reencode(tgt, nt, vp, o, unsupported) == 0xffffffffu) return unsupported;
+    } else {
+      Tok sv, tv;
+      read_tok(src + e.vpos, ns - e.vpos, sv);
+      read_tok(tgt + vp, nt - vp, tv);
+      bool s_cont = sv.type == TT_MAP || sv.type == TT_ARRAY;
+      bool t_cont = tv.type == TT_MAP || tv.type == TT_ARRAY;
+      if (!s_cont) o.put_bytes(src + e.vpos, e.vend - e.vpos);   // source leaf wins
+      else if (!t_cont) o.put_bytes(tgt + vp, ve - vp);          // quirk: target leaf survives
+      else { unsupported = true; return true; }                   // both containers: deep shadowing
+    }
+    pos = ve;
+  }
+  // source keys not in target
+  pos = sf;
+  for (uint32_t i = 0; i < sc; i++) {
+    Tok k;
+    read_tok(src + pos, ns - pos, k);
+    uint32_t vp = pos + k.total;
+    RootEntry e;
+    if (!find_key(tgt, nt, tf, tc, src + pos + k.hdr, k.len, e)) return false;
+    uint32_t ve;
+    if (e.vpos == 0) {
+      o.str(src + pos + k.hdr, k.len);
+      ve = reencode(src, ns, vp, o, unsupported);
+      if (ve == 0xffffffffu) return unsupported;
+    } else {
+      ve = skip_value(src, ns, vp);
+    }
+    pos = ve;
+  }
+  return true;
+}
+
+}  // namespace zbg

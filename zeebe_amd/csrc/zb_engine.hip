@@ -1,0 +1,589 @@
+// zb_engine.hip — host side of libzbgpu.so: the C ABI of include/zb_engine.h.
+//
+// One handle = one partition on one HIP device with one stream. zb_step launches one wave
+// kernel per breadth-first generation, in batches of WAVES_PER_SYNC launches between host
+// checks of the device wave header (quiescence = empty generation). No CPU fallback exists:
+// every record is processed by the gfx950 kernels, and anything they do not implement is
+// reported as ZB_EUNSUPPORTED.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <chrono>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "zb_kernels.hpp"
+#include "zb_model.hpp"
+
+using namespace zbg;
+
+namespace {
+
+constexpr int WAVES_PER_SYNC = 16;
+constexpr uint64_t STATIC_ARENA_BYTES = 1ull << 20;  // {} at ref 0 + harness job completion payloads
+
+template <class T>
+struct DevVec {
+  T* p = nullptr;
+  size_t n = 0;
+  void free() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  hipError_t upload(const std::vector<T>& v, hipStream_t s) {
+    if (v.size() > n || !p) {
+      free();
+      size_t cap = v.empty() ? 1 : v.size();
+      hipError_t e = hipMalloc(&p, cap * sizeof(T));
+      if (e != hipSuccess) return e;
+      n = cap;
+    }
+    if (v.empty()) return hipSuccess;
+    return hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
+  }
+};
+
+}  // namespace
+
+struct zb_engine {
+  zb_config cfg{};
+  hipStream_t stream = nullptr;
+  std::string err;
+
+  ModelTables model;
+  DevVec<DevElem> d_elems;
+  DevVec<DevWorkflow> d_wfs;
+  DevVec<uint16_t> d_cond;
+  DevVec<uint32_t> d_code;
+  DevVec<DevConst> d_consts;
+  DevVec<DevQuery> d_queries;
+  DevVec<DevFilter> d_filters;
+  DevVec<uint8_t> d_pool;
+
+  // device state
+  zb_rec* log = nullptr;
+  uint64_t* links = nullptr;
+  RowMeta* rmeta = nullptr;
+  RowKeys* rkeys = nullptr;
+  uint8_t* arena = nullptr;
+  WaveHdr* hdr = nullptr;
+  unsigned long long* status = nullptr;
+  uint64_t status_tiles = 0;
+  uint32_t* tickets = nullptr;
+  uint32_t* derr = nullptr;
+  uint64_t* dstats = nullptr;
+  WaveHdr* h_hdr_pinned = nullptr;  // pinned mirror for D2H polling
+  uint32_t* h_err_pinned = nullptr;
+
+  int64_t wave = 0;
+  WaveHdr host_hdr{};
+  bool failed = false;
+
+  // static arena region (ref 0 = {}, harness payloads)
+  std::vector<uint8_t> static_blobs;
+
+  // staged input
+  std::vector<zb_rec> staged;
+  std::vector<uint8_t> staged_arena;
+  struct PendingRange {
+    int64_t first, last;  // staged indices
+    int64_t workflow_key;
+    int32_t version;
+    uint32_t pid_off;
+    uint16_t pid_len;
+  };
+  std::vector<PendingRange> pending_ranges;
+  DevVec<zb_rec> d_staged;
+  DevVec<uint8_t> d_staged_arena;
+  bool staged_uploaded = false;
+
+  // submitted command ranges (serialization of CREATE commands / rejections)
+  std::vector<CmdRange> ranges;
+  std::vector<uint8_t> cmd_pool;
+  DevVec<CmdRange> d_ranges;
+  DevVec<uint8_t> d_cmd_pool;
+
+  // timing
+  std::vector<hipEvent_t> ev;
+};
+
+namespace {
+
+int fail(zb_engine* e, int code, const std::string& msg) {
+  e->err = msg;
+  return code;
+}
+
+#define HIPCHECK(e, call)                                                              \
+  do {                                                                                 \
+    hipError_t _r = (call);                                                            \
+    if (_r != hipSuccess) return fail((e), ZB_EDEVICE, std::string(#call) + ": " + hipGetErrorString(_r)); \
+  } while (0)
+
+uint32_t add_blob(std::vector<uint8_t>& arena, const uint8_t* p, uint32_t n) {
+  size_t off = arena.size();
+  size_t total = (4 + (size_t)n + 7) & ~(size_t)7;
+  arena.resize(off + total, 0);
+  std::memcpy(arena.data() + off, &n, 4);
+  if (n) std::memcpy(arena.data() + off + 4, p, n);
+  return (uint32_t)(off >> 3);
+}
+
+int upload_model(zb_engine* e) {
+  HIPCHECK(e, e->d_elems.upload(e->model.elems, e->stream));
+  HIPCHECK(e, e->d_wfs.upload(e->model.workflows, e->stream));
+  HIPCHECK(e, e->d_cond.upload(e->model.cond_flows, e->stream));
+  HIPCHECK(e, e->d_code.upload(e->model.code, e->stream));
+  HIPCHECK(e, e->d_consts.upload(e->model.consts, e->stream));
+  HIPCHECK(e, e->d_queries.upload(e->model.queries, e->stream));
+  HIPCHECK(e, e->d_filters.upload(e->model.filters, e->stream));
+  HIPCHECK(e, e->d_pool.upload(e->model.pool, e->stream));
+  if (e->static_blobs.size() > STATIC_ARENA_BYTES) return fail(e, ZB_ENOMEM, "static payload region full");
+  HIPCHECK(e, hipMemcpyAsync(e->arena, e->static_blobs.data(), e->static_blobs.size(), hipMemcpyHostToDevice,
+                             e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  return ZB_OK;
+}
+
+WaveParams wave_params(zb_engine* e) {
+  WaveParams p;
+  p.log = e->log;
+  p.links = e->links;
+  p.rmeta = e->rmeta;
+  p.rkeys = e->rkeys;
+  p.arena = e->arena;
+  p.elems = e->d_elems.p;
+  p.wfs = e->d_wfs.p;
+  p.cond_flows = e->d_cond.p;
+  p.code = e->d_code.p;
+  p.consts = e->d_consts.p;
+  p.queries = e->d_queries.p;
+  p.filters = e->d_filters.p;
+  p.pool = e->d_pool.p;
+  p.hdr = e->hdr;
+  p.status = e->status;
+  p.tickets = e->tickets;
+  p.err = e->derr;
+  p.stats = e->dstats;
+  p.log_cap = e->cfg.log_capacity;
+  p.row_cap = e->cfg.row_capacity;
+  p.arena_cap = e->cfg.arena_bytes;
+  p.wave = e->wave;
+  return p;
+}
+
+int check_device_errors(zb_engine* e, uint32_t flags) {
+  if (!flags) return ZB_OK;
+  e->failed = true;
+  std::string m = "device error flags:";
+  if (flags & DE_LOG_FULL) m += " log-capacity";
+  if (flags & DE_ROWS_FULL) m += " row-capacity";
+  if (flags & DE_ARENA_FULL) m += " arena-capacity";
+  if (flags & DE_UNSUPPORTED) m += " unsupported-shape";
+  if (flags & DE_PROCESSING) m += " processing-failure";
+  if (flags & DE_LOOKBACK_TIMEOUT) m += " lookback-timeout";
+  if (flags & DE_BAD_PAYLOAD) m += " malformed-payload";
+  int code = ZB_EPROCESSING;
+  if (flags & (DE_LOG_FULL | DE_ROWS_FULL | DE_ARENA_FULL)) code = ZB_ENOMEM;
+  else if (flags & DE_UNSUPPORTED) code = ZB_EUNSUPPORTED;
+  return fail(e, code, m);
+}
+
+}  // namespace
+
+extern "C" {
+
+int zb_engine_create(const zb_config* cfg, zb_engine** out) {
+  if (!cfg || !out) return ZB_EINVAL;
+  *out = nullptr;
+  auto* e = new zb_engine();
+  e->cfg = *cfg;
+  if (e->cfg.log_capacity == 0) e->cfg.log_capacity = 1ull << 22;
+  if (e->cfg.row_capacity == 0) e->cfg.row_capacity = 1ull << 20;
+  if (e->cfg.arena_bytes == 0) e->cfg.arena_bytes = 64ull << 20;
+  if (e->cfg.arena_bytes < 2 * STATIC_ARENA_BYTES) e->cfg.arena_bytes = 2 * STATIC_ARENA_BYTES;
+  if (e->cfg.partition_count <= 0) e->cfg.partition_count = 1;
+  if (e->cfg.log_capacity >= (1ull << 40) || e->cfg.row_capacity >= 0xffffffffull ||
+      e->cfg.arena_bytes >= (8ull << 32)) {
+    delete e;
+    return ZB_EINVAL;
+  }
+  auto cleanup = [&](int code) {
+    zb_engine_destroy(e);
+    return code;
+  };
+  if (hipSetDevice(cfg->device) != hipSuccess) return cleanup(ZB_EDEVICE);
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return cleanup(ZB_EDEVICE);
+  const uint64_t L = e->cfg.log_capacity;
+  e->status_tiles = (L + 255) / 256 + 1;
+  if (hipMalloc(&e->log, L * sizeof(zb_rec)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->links, L * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->rmeta, e->cfg.row_capacity * sizeof(RowMeta)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->rkeys, e->cfg.row_capacity * sizeof(RowKeys)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->arena, e->cfg.arena_bytes) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->hdr, 2 * sizeof(WaveHdr)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->status, e->status_tiles * 3 * sizeof(unsigned long long)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->tickets, 128 * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->derr, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->dstats, 8 * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipHostMalloc(&e->h_hdr_pinned, 2 * sizeof(WaveHdr)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipHostMalloc(&e->h_err_pinned, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  e->ev.resize(2 * WAVES_PER_SYNC);
+  for (auto& x : e->ev)
+    if (hipEventCreate(&x) != hipSuccess) return cleanup(ZB_EDEVICE);
+  const uint8_t empty = 0x80;
+  add_blob(e->static_blobs, &empty, 1);  // ref 0 = {} (DocumentValue.EMPTY_DOCUMENT)
+  if (hipMemcpy(e->arena, e->static_blobs.data(), e->static_blobs.size(), hipMemcpyHostToDevice) != hipSuccess)
+    return cleanup(ZB_EDEVICE);
+  int rc = zb_reset(e, 0);
+  if (rc != ZB_OK) return cleanup(rc);
+  *out = e;
+  return ZB_OK;
+}
+
+void zb_engine_destroy(zb_engine* e) {
+  if (!e) return;
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  for (auto& x : e->ev)
+    if (x) (void)hipEventDestroy(x);
+  void* ps[] = {e->log, e->links, e->rmeta, e->rkeys, e->arena, e->hdr, e->status, e->tickets, e->derr, e->dstats};
+  for (void* p : ps)
+    if (p) (void)hipFree(p);
+  if (e->h_hdr_pinned) (void)hipHostFree(e->h_hdr_pinned);
+  if (e->h_err_pinned) (void)hipHostFree(e->h_err_pinned);
+  e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_consts.free();
+  e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
+  e->d_ranges.free(); e->d_cmd_pool.free();
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+const char* zb_last_error(const zb_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+int zb_reset(zb_engine* e, int keep_staged) {
+  if (!e) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  e->wave = 0;
+  e->failed = false;
+  WaveHdr h{};
+  h.begin = h.end = 0;
+  h.wf_next = 1;   // KeyGenerator.createWorkflowInstanceKeyGenerator: (1, 5)
+  h.job_next = 2;  // KeyGenerator.createJobKeyGenerator: (2, 5)
+  h.rows_next = 0;
+  h.arena_next = (int64_t)STATIC_ARENA_BYTES;
+  e->host_hdr = h;
+  HIPCHECK(e, hipMemcpyAsync(e->hdr, &h, sizeof(h), hipMemcpyHostToDevice, e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->status, 0, e->status_tiles * 3 * sizeof(unsigned long long), e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->tickets, 0, 128 * sizeof(uint32_t), e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->derr, 0, sizeof(uint32_t), e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->dstats, 0, 8 * sizeof(uint64_t), e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  e->ranges.clear();
+  e->cmd_pool.clear();
+  if (!keep_staged) {
+    e->staged.clear();
+    e->staged_arena.clear();
+    e->pending_ranges.clear();
+    e->staged_uploaded = false;
+  }
+  return ZB_OK;
+}
+
+int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t* xml, size_t len) {
+  if (!e || !xml) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  std::string msg;
+  int rc = compile_deployment(e->model, std::string((const char*)xml, len), workflow_key, version, msg);
+  if (rc != ZB_OK) return fail(e, rc, msg);
+  return upload_model(e);
+}
+
+int zb_set_job_completion_payload(zb_engine* e, int64_t workflow_key, const char* activity_id, const uint8_t* payload,
+                                  size_t len) {
+  if (!e || !activity_id) return ZB_EINVAL;
+  int wfi = -1;
+  for (size_t i = 0; i < e->model.workflows.size(); i++)
+    if (e->model.workflows[i].key == workflow_key) wfi = (int)i;
+  if (wfi < 0) return fail(e, ZB_EINVAL, "unknown workflow key");
+  bool found = false;
+  uint32_t ref = 0;
+  if (len > 0 && !(len == 1 && payload[0] == 0xc0)) {
+    if ((payload[0] & 0xf0) != 0x80 && payload[0] != 0xde && payload[0] != 0xdf)
+      return fail(e, ZB_EINVAL, "job payload must be a msgpack map");
+    ref = add_blob(e->static_blobs, payload, (uint32_t)len);
+  }
+  for (size_t i = 0; i < e->model.elems.size(); i++) {
+    DevElem& el = e->model.elems[i];
+    if (el.wf == wfi && el.kind == EK_TASK && e->model.elem_ids[i] == activity_id) {
+      el.job_payload = ref;
+      found = true;
+    }
+  }
+  if (!found) return fail(e, ZB_EINVAL, "no service task with that id");
+  return upload_model(e);
+}
+
+int zb_submit_creates(zb_engine* e, const char* pid, int32_t version, int64_t workflow_key, size_t n,
+                      const uint8_t* payloads, const uint64_t* offsets) {
+  if (!e || (n > 0 && (!payloads || !offsets)) || !pid) return ZB_EINVAL;
+  // resolve like CreateWorkflowInstanceEventProcessor (all workflows are deployed locally)
+  uint16_t pelem = NO_ELEM;
+  const std::string spid(pid);
+  const auto& W = e->model.workflows;
+  if (workflow_key > 0) {
+    for (auto& w : W)
+      if (w.key == workflow_key) pelem = w.process_elem;
+  } else if (version > 0) {
+    for (auto& w : W)
+      if (w.version == version && e->model.str(w.pid_off, w.pid_len) == spid) pelem = w.process_elem;
+  } else {
+    int32_t best = INT32_MIN;
+    for (auto& w : W)
+      if (e->model.str(w.pid_off, w.pid_len) == spid && w.version > best) { best = w.version; pelem = w.process_elem; }
+  }
+  zb_engine::PendingRange pr;
+  pr.first = (int64_t)e->staged.size();
+  pr.last = pr.first + (int64_t)n;
+  pr.workflow_key = workflow_key;
+  pr.version = version;
+  pr.pid_off = (uint32_t)e->cmd_pool.size();
+  pr.pid_len = (uint16_t)spid.size();
+  e->cmd_pool.insert(e->cmd_pool.end(), spid.begin(), spid.end());
+  e->staged.reserve(e->staged.size() + n);
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t* p = payloads + offsets[i];
+    uint64_t len = offsets[i + 1] - offsets[i];
+    uint32_t ref;
+    if (len == 0 || (len == 1 && p[0] == 0xc0)) {
+      const uint8_t empty = 0x80;  // DocumentValue: nil / empty -> {}
+      ref = add_blob(e->staged_arena, &empty, 1);
+    } else {
+      uint8_t b = p[0];
+      if (!((b & 0xf0) == 0x80 || b == 0xde || b == 0xdf))
+        return fail(e, ZB_EINVAL, "Document has invalid format. On root level an object is only allowed.");
+      ref = add_blob(e->staged_arena, p, (uint32_t)len);
+    }
+    zb_rec d;
+    d.key = -1;
+    d.scope_key = -1;
+    d.inst_key = -1;
+    d.payload = ref;
+    d.elem = pelem;
+    d.intent = WI_CREATE;
+    d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_COMMAND, false);
+    e->staged.push_back(d);
+  }
+  e->pending_ranges.push_back(pr);
+  e->staged_uploaded = false;
+  return ZB_OK;
+}
+
+int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
+  if (!e) return ZB_EINVAL;
+  if (e->failed) return fail(e, ZB_EPROCESSING, "partition stopped after a processing failure: " + e->err);
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  auto t0 = std::chrono::steady_clock::now();
+  zb_step_stats st{};
+  // ---- inject staged input at the log tail (engine is quiescent between steps)
+  if (!e->staged.empty()) {
+    const int64_t n = (int64_t)e->staged.size();
+    if ((uint64_t)(e->host_hdr.end + n) > e->cfg.log_capacity) return fail(e, ZB_ENOMEM, "log capacity");
+    if ((uint64_t)e->host_hdr.arena_next + e->staged_arena.size() > e->cfg.arena_bytes)
+      return fail(e, ZB_ENOMEM, "arena capacity");
+    if (!e->staged_uploaded) {
+      HIPCHECK(e, e->d_staged.upload(e->staged, e->stream));
+      HIPCHECK(e, e->d_staged_arena.upload(e->staged_arena, e->stream));
+      e->staged_uploaded = true;
+    }
+    InjectParams ip;
+    ip.log = e->log;
+    ip.links = e->links;
+    ip.arena = e->arena;
+    ip.staged = e->d_staged.p;
+    ip.staged_arena = e->d_staged_arena.p;
+    ip.n = n;
+    ip.log_base = e->host_hdr.end;
+    ip.arena_base = (uint64_t)e->host_hdr.arena_next;
+    ip.staged_bytes = e->staged_arena.size();
+    launch_inject(ip, e->stream);
+    for (auto& pr : e->pending_ranges) {
+      CmdRange r{};
+      r.pos_begin = ip.log_base + pr.first;
+      r.pos_end = ip.log_base + pr.last;
+      r.workflow_key = pr.workflow_key;
+      r.version = pr.version;
+      r.pid_off = pr.pid_off;
+      r.pid_len = pr.pid_len;
+      e->ranges.push_back(r);
+    }
+    e->host_hdr.end += n;
+    e->host_hdr.arena_next += (int64_t)e->staged_arena.size();
+    HIPCHECK(e, hipMemcpyAsync(e->hdr + (e->wave & 1), &e->host_hdr, sizeof(WaveHdr), hipMemcpyHostToDevice,
+                               e->stream));
+  }
+  const int64_t processed_from = e->host_hdr.begin;
+  const int64_t written_from = e->host_hdr.end;
+  uint64_t stats_before[8];
+  HIPCHECK(e, hipMemcpy(stats_before, e->dstats, sizeof(stats_before), hipMemcpyDeviceToHost));
+  const int grid = 2048;
+  uint32_t launched = 0;
+  bool quiescent = e->host_hdr.begin == e->host_hdr.end;
+  while (!quiescent && (max_waves == 0 || launched < max_waves)) {
+    int batch = WAVES_PER_SYNC;
+    if (max_waves) batch = std::min<int>(batch, (int)(max_waves - launched));
+    for (int i = 0; i < batch; i++) {
+      if (e->wave % 127 == 0 && e->wave > 0) {
+        // tile-status epochs wrap every 127 waves: clear stale granules (stream ordered)
+        HIPCHECK(e, hipMemsetAsync(e->status, 0, e->status_tiles * 3 * sizeof(unsigned long long), e->stream));
+      }
+      WaveParams p = wave_params(e);
+      HIPCHECK(e, hipEventRecord(e->ev[2 * i], e->stream));
+      launch_wave(p, grid, e->stream);
+      HIPCHECK(e, hipEventRecord(e->ev[2 * i + 1], e->stream));
+      e->wave++;
+    }
+    HIPCHECK(e, hipGetLastError());
+    HIPCHECK(e, hipMemcpyAsync(e->h_hdr_pinned, e->hdr + (e->wave & 1), sizeof(WaveHdr), hipMemcpyDeviceToHost,
+                               e->stream));
+    HIPCHECK(e, hipMemcpyAsync(e->h_err_pinned, e->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHECK(e, hipStreamSynchronize(e->stream));
+    for (int i = 0; i < batch; i++) {
+      float ms = 0;
+      HIPCHECK(e, hipEventElapsedTime(&ms, e->ev[2 * i], e->ev[2 * i + 1]));
+      st.wave_kernel_ms += ms;
+    }
+    launched += batch;
+    st.launches += batch;
+    e->host_hdr = e->h_hdr_pinned[0];
+    int rc = check_device_errors(e, *e->h_err_pinned);
+    if (rc != ZB_OK) return rc;
+    quiescent = e->host_hdr.begin == e->host_hdr.end;
+  }
+  uint64_t stats_after[8];
+  HIPCHECK(e, hipMemcpy(stats_after, e->dstats, sizeof(stats_after), hipMemcpyDeviceToHost));
+  st.records_processed = (uint64_t)(e->host_hdr.begin - processed_from);
+  st.records_written = (uint64_t)(e->host_hdr.end - written_from);
+  st.transitions = stats_after[0] - stats_before[0];
+  st.completed_instances = stats_after[1] - stats_before[1];
+  st.merges = stats_after[3] - stats_before[3];
+  st.merge_bytes = stats_after[4] - stats_before[4];
+  st.condition_payload_bytes = stats_after[5] - stats_before[5];
+  st.waves = stats_after[6] - stats_before[6];
+  st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (stats) *stats = st;
+  if (!quiescent) return ZB_EAGAIN;
+  return ZB_OK;
+}
+
+int64_t zb_log_size(zb_engine* e) { return e ? e->host_hdr.end : -1; }
+
+int zb_read_descriptors(zb_engine* e, int64_t start, int64_t count, zb_rec* out) {
+  if (!e || start < 0 || count < 0 || start + count > e->host_hdr.end || (!out && count)) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  HIPCHECK(e, hipMemcpyAsync(out, e->log + start, count * sizeof(zb_rec), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  return ZB_OK;
+}
+
+int zb_drain(zb_engine* e, int64_t start, int64_t count, zb_record_header* headers, uint8_t* values,
+             size_t values_cap, size_t* values_len) {
+  if (!e || start < 0 || count < 0 || start + count > e->host_hdr.end) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  if (count == 0) {
+    if (values_len) *values_len = 0;
+    return ZB_OK;
+  }
+  HIPCHECK(e, e->d_ranges.upload(e->ranges, e->stream));
+  HIPCHECK(e, e->d_cmd_pool.upload(e->cmd_pool, e->stream));
+  uint64_t* d_len = nullptr;
+  uint64_t* d_off = nullptr;
+  void* d_tmp = nullptr;
+  size_t tmp_bytes = 0;
+  zb_record_header* d_hdrs = nullptr;
+  uint8_t* d_out = nullptr;
+  int rc = ZB_OK;
+  auto cleanup = [&]() {
+    if (d_len) (void)hipFree(d_len);
+    if (d_off) (void)hipFree(d_off);
+    if (d_tmp) (void)hipFree(d_tmp);
+    if (d_hdrs) (void)hipFree(d_hdrs);
+    if (d_out) (void)hipFree(d_out);
+  };
+  SerParams sp{};
+  sp.log = e->log;
+  sp.arena = e->arena;
+  sp.elems = e->d_elems.p;
+  sp.wfs = e->d_wfs.p;
+  sp.queries = e->d_queries.p;
+  sp.pool = e->d_pool.p;
+  sp.ranges = e->d_ranges.p;
+  sp.nranges = (int32_t)e->ranges.size();
+  sp.cmd_pool = e->d_cmd_pool.p;
+  sp.start = start;
+  sp.count = count;
+  do {
+    if (hipMalloc(&d_len, (count + 1) * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(&d_off, (count + 1) * sizeof(uint64_t)) != hipSuccess) { rc = fail(e, ZB_ENOMEM, "drain buffers"); break; }
+    if (hipMemsetAsync(d_len, 0, (count + 1) * sizeof(uint64_t), e->stream) != hipSuccess) { rc = ZB_EDEVICE; break; }
+    sp.lengths = (uint32_t*)nullptr;
+    // size pass writes 32-bit lengths into the low half of a 64-bit array
+    SerParams sz = sp;
+    sz.lengths = (uint32_t*)d_off;  // scratch
+    launch_ser_size(sz, e->stream);
+    // widen to 64-bit for the scan: reuse a tiny conversion via hipcub TransformInputIterator
+    hipcub::TransformInputIterator<uint64_t, hipcub::CastOp<uint64_t>, const uint32_t*> it(
+        (const uint32_t*)d_off, hipcub::CastOp<uint64_t>());
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, it, d_len, (int)count, e->stream) != hipSuccess) {
+      rc = fail(e, ZB_EDEVICE, "scan sizing");
+      break;
+    }
+    if (hipMalloc(&d_tmp, tmp_bytes + 16) != hipSuccess) { rc = fail(e, ZB_ENOMEM, "scan temp"); break; }
+    if (hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_bytes, it, d_len, (int)count, e->stream) != hipSuccess) {
+      rc = fail(e, ZB_EDEVICE, "scan");
+      break;
+    }
+    uint64_t last_off = 0;
+    uint32_t last_len = 0;
+    if (hipMemcpyAsync(&last_off, d_len + count - 1, 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+        hipMemcpyAsync(&last_len, ((uint32_t*)d_off) + count - 1, 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess) { rc = fail(e, ZB_EDEVICE, "drain size"); break; }
+    const uint64_t total = last_off + last_len;
+    if (values_len) *values_len = total;
+    if (!values || !headers || values_cap < total) { rc = ZB_ENOMEM; break; }
+    if (hipMalloc(&d_out, total + 1) != hipSuccess || hipMalloc(&d_hdrs, count * sizeof(zb_record_header)) != hipSuccess) {
+      rc = fail(e, ZB_ENOMEM, "drain output");
+      break;
+    }
+    SerParams wr = sp;
+    wr.offsets = d_len;
+    wr.out = d_out;
+    wr.headers = d_hdrs;
+    launch_ser_write(wr, e->stream);
+    if (hipMemcpyAsync(values, d_out, total, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+        hipMemcpyAsync(headers, d_hdrs, count * sizeof(zb_record_header), hipMemcpyDeviceToHost, e->stream) !=
+            hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess) { rc = fail(e, ZB_EDEVICE, "drain copy"); break; }
+  } while (0);
+  cleanup();
+  return rc;
+}
+
+int zb_counters(zb_engine* e, int64_t out[8]) {
+  if (!e || !out) return ZB_EINVAL;
+  uint64_t s[8];
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  HIPCHECK(e, hipMemcpy(s, e->dstats, sizeof(s), hipMemcpyDeviceToHost));
+  out[0] = (int64_t)s[2];
+  out[1] = (int64_t)s[1];
+  out[2] = 0;
+  out[3] = e->host_hdr.wf_next;
+  out[4] = e->host_hdr.job_next;
+  out[5] = e->host_hdr.rows_next;
+  out[6] = e->host_hdr.arena_next;
+  out[7] = e->host_hdr.end;
+  return ZB_OK;
+}
+
+}  // extern "C"

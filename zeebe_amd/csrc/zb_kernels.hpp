@@ -1,0 +1,79 @@
+// zb_kernels.hpp — kernel parameter blocks and launchers shared by zb_engine.cpp and the .hip files.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "zb_device.hpp"
+
+namespace zbg {
+
+struct WaveParams {
+  zb_rec* log;
+  uint64_t* links;        // per record: row_self | row_scope << 32
+  RowMeta* rmeta;
+  RowKeys* rkeys;
+  uint8_t* arena;
+  const DevElem* elems;
+  const DevWorkflow* wfs;
+  const uint16_t* cond_flows;
+  const uint32_t* code;
+  const DevConst* consts;
+  const DevQuery* queries;
+  const DevFilter* filters;
+  const uint8_t* pool;
+  WaveHdr* hdr;           // [2], double buffered
+  unsigned long long* status;  // 3 granules per tile
+  uint32_t* tickets;      // [128]
+  uint32_t* err;          // sticky DevErr flags
+  uint64_t* stats;        // [8] transitions, completed, created, merges, merge_bytes, cond_bytes, waves
+  uint64_t log_cap, row_cap, arena_cap;
+  int64_t wave;
+};
+
+void launch_wave(const WaveParams& p, int grid, hipStream_t stream);
+
+// submitted CREATE commands: one range per zb_submit_creates call (serialization of their values)
+struct CmdRange {
+  int64_t pos_begin, pos_end;
+  int64_t workflow_key;
+  int32_t version;
+  uint16_t pid_len;
+  uint16_t pad;
+  uint32_t pid_off;       // in the engine's command string pool (device copy in SerParams.cmd_pool)
+  uint32_t pad2;
+};
+
+struct SerParams {
+  const zb_rec* log;
+  const uint8_t* arena;
+  const DevElem* elems;
+  const DevWorkflow* wfs;
+  const DevQuery* queries;
+  const uint8_t* pool;
+  const CmdRange* ranges;
+  int32_t nranges;
+  const uint8_t* cmd_pool;
+  int64_t start, count;
+  const uint64_t* offsets;  // exclusive offsets of value bytes (count+1), write pass
+  uint32_t* lengths;        // size pass output
+  uint8_t* out;
+  zb_record_header* headers;
+};
+
+void launch_ser_size(const SerParams& p, hipStream_t stream);
+void launch_ser_write(const SerParams& p, hipStream_t stream);
+
+struct InjectParams {
+  zb_rec* log;
+  uint64_t* links;
+  uint8_t* arena;
+  const zb_rec* staged;
+  const uint8_t* staged_arena;
+  int64_t n;
+  int64_t log_base;       // where the staged records go
+  uint64_t arena_base;    // byte offset in the arena for the staged payload blobs
+  uint64_t staged_bytes;
+};
+
+void launch_inject(const InjectParams& p, hipStream_t stream);
+
+}  // namespace zbg

@@ -1,0 +1,257 @@
+// zb_serialize.hip — descriptor -> exact reference record value bytes (two passes: size, write).
+//
+// Value layouts (UnpackedObject.write: declared properties in declaration order, ObjectValue.java:140-153):
+//   WorkflowInstanceRecord  broker-core/.../workflow/data/WorkflowInstanceRecord.java:39-60
+//   JobRecord + JobHeaders  broker-core/.../job/data/JobRecord.java:35-53, JobHeaders.java:33-51
+//   IncidentRecord          broker-core/.../incident/data/IncidentRecord.java (EnumProperty -> enum name string)
+// Integer encoding is MsgPackWriter.writeInteger (msgpack-core/.../spec/MsgPackWriter.java:143-201).
+#include <hip/hip_runtime.h>
+
+#include "zb_devlib.hpp"
+#include "zb_kernels.hpp"
+
+namespace zbg {
+
+struct W : Out {
+  __device__ inline void integer(int64_t v) {
+    if (v < -(1LL << 5)) {
+      if (v < -(1LL << 15)) {
+        if (v < -(1LL << 31)) { put(0xd3); for (int i = 7; i >= 0; i--) put((uint8_t)((uint64_t)v >> (8 * i))); }
+        else { put(0xd2); for (int i = 3; i >= 0; i--) put((uint8_t)((uint32_t)v >> (8 * i))); }
+      } else {
+        if (v < -(1 << 7)) { put(0xd1); put((uint8_t)((uint16_t)v >> 8)); put((uint8_t)v); }
+        else { put(0xd0); put((uint8_t)v); }
+      }
+    } else if (v < (1 << 7)) {
+      put((uint8_t)v);
+    } else if (v < (1LL << 16)) {
+      if (v < (1 << 8)) { put(0xcc); put((uint8_t)v); }
+      else { put(0xcd); put((uint8_t)(v >> 8)); put((uint8_t)v); }
+    } else if (v < (1LL << 32)) {
+      put(0xce); for (int i = 3; i >= 0; i--) put((uint8_t)(v >> (8 * i)));
+    } else {
+      put(0xcf); for (int i = 7; i >= 0; i--) put((uint8_t)((uint64_t)v >> (8 * i)));
+    }
+  }
+  __device__ inline void key(const char* s) {
+    uint32_t n = 0;
+    while (s[n]) n++;
+    str((const uint8_t*)s, n);
+  }
+  __device__ inline void bin(const uint8_t* s, uint32_t n) {
+    if (n < 256) { put(0xc4); put((uint8_t)n); }
+    else if (n < 65536) { put(0xc5); put((uint8_t)(n >> 8)); put((uint8_t)n); }
+    else { put(0xc6); for (int i = 3; i >= 0; i--) put((uint8_t)(n >> (8 * i))); }
+    put_bytes(s, n);
+  }
+  __device__ inline void cstr(const char* s) {  // append raw chars (message text)
+    while (*s) put((uint8_t)*s++);
+  }
+};
+
+__device__ const char* const TYPE_NAMES[9] = {"INTEGER", "FLOAT", "BOOLEAN", "NIL", "MAP", "ARRAY",
+                                             "BINARY", "STRING", "EXTENSION"};
+__device__ const char* const ERROR_TYPES[4] = {"UNKNOWN", "IO_MAPPING_ERROR", "JOB_NO_RETRIES", "CONDITION_ERROR"};
+
+__device__ inline uint32_t dstrlen(const char* s) {
+  uint32_t n = 0;
+  while (s[n]) n++;
+  return n;
+}
+
+// incident error message (JsonConditionInterpreter / ExclusiveSplitHandler / MappingProcessor texts)
+__device__ inline void message(W& w, const SerParams& P, const uint8_t* det, bool size_only_hdr) {
+  const uint8_t code = det[1], a = det[2], b = det[3];
+  const uint16_t q = *(const uint16_t*)(det + 4);
+  // compute length first (string header needs it)
+  W m;
+  m.dst = nullptr;
+  m.n = 0;
+  for (int pass = 0; pass < 2; pass++) {
+    W& o = pass == 0 ? m : w;
+    if (pass == 1) {
+      uint32_t len = m.n;
+      if (len < 32) o.put(0xa0 | len);
+      else if (len < 256) { o.put(0xd9); o.put((uint8_t)len); }
+      else { o.put(0xda); o.put((uint8_t)(len >> 8)); o.put((uint8_t)len); }
+    }
+    switch (code) {
+      case EC_NO_FLOW: o.cstr("All conditions evaluated to false and no default flow is set."); break;
+      case EC_PATH_NO_RESULT:
+      case EC_PATH_MULTI: {
+        const DevQuery& qq = P.queries[q];
+        o.cstr("JSON path '");
+        o.put_bytes(P.pool + qq.expr_off, qq.expr_len);
+        o.cstr(code == EC_PATH_NO_RESULT ? "' has no result." : "' has more than one result.");
+        break;
+      }
+      case EC_DIFF_TYPES:
+        o.cstr("Cannot compare values of different types: ");
+        o.cstr(TYPE_NAMES[a < 9 ? a : 8]);
+        o.cstr(" and ");
+        o.cstr(TYPE_NAMES[b < 9 ? b : 8]);
+        break;
+      case EC_CMP_TYPE: o.cstr("Cannot compare value of type: "); o.cstr(TYPE_NAMES[a < 9 ? a : 8]); break;
+      case EC_NOT_NUMBER:
+        o.cstr("Cannot compare values. Expected number but found: ");
+        o.cstr(TYPE_NAMES[a < 9 ? a : 8]);
+        break;
+      case EC_MAPPING_NOT_MAP:
+        o.cstr("Processing failed, since mapping will result in a non map object (json object).");
+        break;
+    }
+  }
+  (void)size_only_hdr;
+}
+
+__device__ inline const CmdRange* find_range(const SerParams& P, int64_t pos) {
+  int lo = 0, hi = P.nranges - 1;
+  while (lo <= hi) {
+    int mid = (lo + hi) >> 1;
+    const CmdRange& r = P.ranges[mid];
+    if (pos < r.pos_begin) hi = mid - 1;
+    else if (pos >= r.pos_end) lo = mid + 1;
+    else return &r;
+  }
+  return nullptr;
+}
+
+__device__ inline void encode_value(const SerParams& P, int64_t pos, const zb_rec& d, W& w) {
+  const uint8_t vt = kind_vt(d.kind), rt = kind_rt(d.kind);
+  uint32_t plen = 0;
+  const uint8_t* pl = nullptr;
+  if (vt != ZB_VT_INCIDENT) {
+    const uint8_t* p = P.arena + (uint64_t)d.payload * 8;
+    plen = *(const uint32_t*)p;
+    pl = p + 4;
+  }
+  if (vt == ZB_VT_WORKFLOW_INSTANCE) {
+    w.map_hdr(7);
+    const bool submitted = d.intent == WI_CREATE && (rt == ZB_RT_COMMAND || rt == ZB_RT_COMMAND_REJECTION);
+    if (submitted) {
+      const CmdRange* r = find_range(P, rt == ZB_RT_COMMAND ? pos : d.scope_key);
+      w.key("bpmnProcessId");
+      if (r) w.str(P.cmd_pool + r->pid_off, r->pid_len); else w.str(nullptr, 0);
+      w.key("version"); w.integer(r ? r->version : -1);
+      w.key("workflowKey"); w.integer(r ? r->workflow_key : -1);
+      w.key("workflowInstanceKey"); w.integer(rt == ZB_RT_COMMAND ? -1 : d.inst_key);
+      w.key("activityId"); w.str(nullptr, 0);
+      w.key("payload"); w.bin(pl, plen);
+      w.key("scopeInstanceKey"); w.integer(-1);
+      return;
+    }
+    const DevElem& e = P.elems[d.elem];
+    const DevWorkflow& wf = P.wfs[e.wf];
+    w.key("bpmnProcessId"); w.str(P.pool + wf.pid_off, wf.pid_len);
+    w.key("version"); w.integer(wf.version);
+    w.key("workflowKey"); w.integer(wf.key);
+    w.key("workflowInstanceKey"); w.integer(d.inst_key);
+    w.key("activityId"); w.str(P.pool + e.id_off, e.id_len);
+    w.key("payload"); w.bin(pl, plen);
+    w.key("scopeInstanceKey"); w.integer(d.scope_key);
+  } else if (vt == ZB_VT_JOB) {
+    const DevElem& e = P.elems[d.elem];
+    const DevWorkflow& wf = P.wfs[e.wf];
+    w.map_hdr(7);
+    w.key("deadline"); w.integer(INT64_MIN);
+    w.key("worker"); w.str(nullptr, 0);
+    w.key("retries"); w.integer(e.retries);
+    w.key("type"); w.str(P.pool + e.type_off, e.type_len);
+    w.key("headers");
+    w.map_hdr(6);
+    w.key("bpmnProcessId"); w.str(P.pool + wf.pid_off, wf.pid_len);
+    w.key("workflowDefinitionVersion"); w.integer(wf.version);
+    w.key("workflowKey"); w.integer(wf.key);
+    w.key("workflowInstanceKey"); w.integer(d.inst_key);
+    w.key("activityId"); w.str(P.pool + e.id_off, e.id_len);
+    w.key("activityInstanceKey"); w.integer(d.scope_key);
+    w.key("customHeaders");
+    if (e.headers_off == NO_REF) w.put(0x80);  // JobRecord.NO_HEADERS
+    else w.put_bytes(P.pool + e.headers_off, e.headers_len);
+    w.key("payload"); w.bin(pl, plen);
+  } else if (vt == ZB_VT_INCIDENT) {
+    const uint8_t* det = P.arena + (uint64_t)d.payload * 8 + 4;
+    const DevElem& e = P.elems[d.elem];
+    const DevWorkflow& wf = P.wfs[e.wf];
+    w.map_hdr(9);
+    w.key("errorType"); w.key(ERROR_TYPES[det[0] < 4 ? det[0] : 0]);
+    w.key("errorMessage"); message(w, P, det, false);
+    w.key("failureEventPosition"); w.integer(*(const int64_t*)(det + 12));
+    w.key("bpmnProcessId"); w.str(P.pool + wf.pid_off, wf.pid_len);
+    w.key("workflowInstanceKey"); w.integer(d.inst_key);
+    w.key("activityId"); w.str(P.pool + e.id_off, e.id_len);
+    w.key("activityInstanceKey"); w.integer(d.scope_key);
+    w.key("jobKey"); w.integer(-1);
+    w.key("payload"); w.bin((const uint8_t*)"\x80", 1);
+  }
+}
+
+__global__ void k_ser_size(SerParams P) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P.count) return;
+  const int64_t pos = P.start + i;
+  const zb_rec d = P.log[pos];
+  W w;
+  w.dst = nullptr;
+  w.n = 0;
+  encode_value(P, pos, d, w);
+  P.lengths[i] = w.n;
+}
+
+__global__ void k_ser_write(SerParams P) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P.count) return;
+  const int64_t pos = P.start + i;
+  const zb_rec d = P.log[pos];
+  W w;
+  w.dst = P.out + P.offsets[i];
+  w.n = 0;
+  encode_value(P, pos, d, w);
+  zb_record_header h;
+  h.position = pos;
+  h.source_position = -1;
+  h.key = d.key;
+  h.record_type = kind_rt(d.kind);
+  h.value_type = kind_vt(d.kind);
+  h.intent = d.intent;
+  h.rejection_type = kind_rt(d.kind) == ZB_RT_COMMAND_REJECTION ? 0 /*BAD_VALUE*/ : 255;
+  h.value_length = w.n;
+  h.value_offset = P.offsets[i];
+  P.headers[i] = h;
+}
+
+void launch_ser_size(const SerParams& p, hipStream_t s) {
+  if (p.count <= 0) return;
+  hipLaunchKernelGGL(k_ser_size, dim3((unsigned)((p.count + 255) / 256)), dim3(256), 0, s, p);
+}
+void launch_ser_write(const SerParams& p, hipStream_t s) {
+  if (p.count <= 0) return;
+  hipLaunchKernelGGL(k_ser_write, dim3((unsigned)((p.count + 255) / 256)), dim3(256), 0, s, p);
+}
+
+// ------------------------------------------------------------------------------ input injection
+__global__ void k_inject(InjectParams P) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t base_ref = (uint32_t)(P.arena_base >> 3);
+  for (int64_t i = tid; i < P.n; i += stride) {
+    zb_rec d = P.staged[i];
+    d.payload += base_ref;
+    P.log[P.log_base + i] = d;
+    P.links[P.log_base + i] = ~0ull;  // no rows yet
+  }
+  const uint64_t nw = P.staged_bytes / 8;
+  const uint64_t* src = (const uint64_t*)P.staged_arena;
+  uint64_t* dst = (uint64_t*)(P.arena + P.arena_base);
+  for (uint64_t i = tid; i < nw; i += stride) dst[i] = src[i];
+}
+
+void launch_inject(const InjectParams& p, hipStream_t s) {
+  int64_t work = p.n > (int64_t)(p.staged_bytes / 8) ? p.n : (int64_t)(p.staged_bytes / 8);
+  int grid = (int)((work + 255) / 256);
+  if (grid > 4096) grid = 4096;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(k_inject, dim3(grid), dim3(256), 0, s, p);
+}
+
+}  // namespace zbg

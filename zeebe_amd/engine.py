@@ -1,0 +1,214 @@
+"""Python binding of libzbgpu.so (ctypes over the C ABI in include/zb_engine.h).
+
+The product path: every call goes to the HIP engine. If the shared library is missing this module
+raises at import time -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import struct
+from typing import List, NamedTuple, Optional, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libzbgpu.so")
+
+ZB_OK, ZB_EINVAL, ZB_ENOMEM, ZB_EUNSUPPORTED, ZB_EDEPLOY, ZB_EDEVICE, ZB_EAGAIN, ZB_EPROCESSING = \
+    0, -1, -2, -3, -4, -5, -6, -7
+_NAMES = {0: "ZB_OK", -1: "ZB_EINVAL", -2: "ZB_ENOMEM", -3: "ZB_EUNSUPPORTED", -4: "ZB_EDEPLOY",
+          -5: "ZB_EDEVICE", -6: "ZB_EAGAIN", -7: "ZB_EPROCESSING"}
+
+
+class ZbError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__("%s: %s" % (_NAMES.get(code, code), msg))
+        self.code = code
+
+
+class zb_config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("partition_id", ctypes.c_int32),
+                ("partition_count", ctypes.c_int32), ("reserved0", ctypes.c_int32),
+                ("log_capacity", ctypes.c_uint64), ("row_capacity", ctypes.c_uint64),
+                ("arena_bytes", ctypes.c_uint64), ("staging_records", ctypes.c_uint64)]
+
+
+class zb_rec(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_int64), ("scope_key", ctypes.c_int64), ("inst_key", ctypes.c_int64),
+                ("payload", ctypes.c_uint32), ("elem", ctypes.c_uint16), ("intent", ctypes.c_uint8),
+                ("kind", ctypes.c_uint8)]
+
+
+class zb_record_header(ctypes.Structure):
+    _fields_ = [("position", ctypes.c_int64), ("source_position", ctypes.c_int64), ("key", ctypes.c_int64),
+                ("record_type", ctypes.c_uint8), ("value_type", ctypes.c_uint8), ("intent", ctypes.c_uint8),
+                ("rejection_type", ctypes.c_uint8), ("value_length", ctypes.c_uint32),
+                ("value_offset", ctypes.c_uint64)]
+
+
+class zb_step_stats(ctypes.Structure):
+    _fields_ = [("waves", ctypes.c_uint64), ("launches", ctypes.c_uint64),
+                ("records_processed", ctypes.c_uint64), ("records_written", ctypes.c_uint64),
+                ("transitions", ctypes.c_uint64), ("completed_instances", ctypes.c_uint64),
+                ("merges", ctypes.c_uint64), ("merge_bytes", ctypes.c_uint64),
+                ("condition_payload_bytes", ctypes.c_uint64), ("wave_kernel_ms", ctypes.c_double),
+                ("wall_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class Record(NamedTuple):
+    position: int
+    source_position: int
+    key: int
+    record_type: int
+    value_type: int
+    intent: int
+    rejection_type: int
+    value: bytes
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libzbgpu.so not built (%s): run __graft_entry__.build()" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        vp = ctypes.c_void_p
+        L.zb_engine_create.argtypes = [ctypes.POINTER(zb_config), ctypes.POINTER(vp)]
+        L.zb_engine_destroy.argtypes = [vp]
+        L.zb_last_error.restype = ctypes.c_char_p
+        L.zb_last_error.argtypes = [vp]
+        L.zb_reset.argtypes = [vp, ctypes.c_int]
+        L.zb_deploy.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_char_p, ctypes.c_size_t]
+        L.zb_set_job_completion_payload.argtypes = [vp, ctypes.c_int64, ctypes.c_char_p, ctypes.c_char_p,
+                                                    ctypes.c_size_t]
+        L.zb_submit_creates.argtypes = [vp, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t,
+                                        ctypes.c_void_p, ctypes.c_void_p]
+        L.zb_step.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(zb_step_stats)]
+        L.zb_log_size.restype = ctypes.c_int64
+        L.zb_log_size.argtypes = [vp]
+        L.zb_read_descriptors.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
+        L.zb_drain.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+        L.zb_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
+        _lib = L
+    return _lib
+
+
+EXPORTED_SYMBOLS = ["zb_engine_create", "zb_engine_destroy", "zb_last_error", "zb_reset", "zb_deploy",
+                    "zb_set_job_completion_payload", "zb_submit_creates", "zb_step", "zb_log_size",
+                    "zb_read_descriptors", "zb_drain", "zb_counters"]
+
+
+class Engine:
+    """One partition of the GPU stepping core (one HIP device + stream)."""
+
+    def __init__(self, device: int = 0, partition_id: int = 0, partition_count: int = 1,
+                 log_capacity: int = 1 << 22, row_capacity: int = 1 << 20, arena_bytes: int = 64 << 20):
+        self._L = lib()
+        cfg = zb_config(device, partition_id, partition_count, 0, log_capacity, row_capacity, arena_bytes, 0)
+        h = ctypes.c_void_p()
+        rc = self._L.zb_engine_create(ctypes.byref(cfg), ctypes.byref(h))
+        if rc != ZB_OK:
+            raise ZbError(rc, "zb_engine_create failed")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.zb_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int):
+        if rc != ZB_OK:
+            raise ZbError(rc, self._L.zb_last_error(self._h).decode("utf-8", "replace"))
+        return rc
+
+    def reset(self, keep_staged: bool = False):
+        self._check(self._L.zb_reset(self._h, 1 if keep_staged else 0))
+
+    def deploy(self, xml, workflow_key: int, version: int = 1):
+        if isinstance(xml, str):
+            xml = xml.encode()
+        self._check(self._L.zb_deploy(self._h, workflow_key, version, xml, len(xml)))
+
+    def set_job_payload(self, workflow_key: int, activity_id: str, payload: bytes):
+        self._check(self._L.zb_set_job_completion_payload(self._h, workflow_key, activity_id.encode(), payload,
+                                                          len(payload)))
+
+    def create(self, process_id: str, payloads: Sequence[bytes], version: int = -1, workflow_key: int = -1):
+        import numpy as np
+
+        n = len(payloads)
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        if n:
+            offs[1:] = np.cumsum([len(p) for p in payloads], dtype=np.uint64)
+        blob = b"".join(payloads)
+        buf = ctypes.create_string_buffer(blob, max(len(blob), 1))
+        self._check(self._L.zb_submit_creates(self._h, process_id.encode(), version, workflow_key, n, buf,
+                                              offs.ctypes.data))
+
+    def create_packed(self, process_id: str, blob: bytes, offsets, version: int = -1, workflow_key: int = -1):
+        """Bulk form: offsets is a uint64 numpy array of n+1 entries into blob."""
+        buf = ctypes.create_string_buffer(blob, max(len(blob), 1))
+        n = len(offsets) - 1
+        self._check(self._L.zb_submit_creates(self._h, process_id.encode(), version, workflow_key, n, buf,
+                                              offsets.ctypes.data))
+
+    def step(self, max_waves: int = 0) -> dict:
+        st = zb_step_stats()
+        rc = self._L.zb_step(self._h, max_waves, ctypes.byref(st))
+        if rc not in (ZB_OK, ZB_EAGAIN):
+            self._check(rc)
+        d = st.as_dict()
+        d["quiescent"] = rc == ZB_OK
+        return d
+
+    def log_size(self) -> int:
+        return self._L.zb_log_size(self._h)
+
+    def descriptors(self, start: int = 0, count: Optional[int] = None):
+        import numpy as np
+
+        if count is None:
+            count = self.log_size() - start
+        arr = (zb_rec * max(count, 1))()
+        self._check(self._L.zb_read_descriptors(self._h, start, count, arr))
+        dt = np.dtype([("key", "<i8"), ("scope_key", "<i8"), ("inst_key", "<i8"), ("payload", "<u4"),
+                       ("elem", "<u2"), ("intent", "u1"), ("kind", "u1")])
+        return np.frombuffer(bytes(arr)[:count * 32], dtype=dt)
+
+    def records(self, start: int = 0, count: Optional[int] = None) -> List[Record]:
+        if count is None:
+            count = self.log_size() - start
+        if count <= 0:
+            return []
+        hdrs = (zb_record_header * count)()
+        need = ctypes.c_size_t(0)
+        rc = self._L.zb_drain(self._h, start, count, hdrs, None, 0, ctypes.byref(need))
+        if rc not in (ZB_OK, ZB_ENOMEM):
+            self._check(rc)
+        buf = ctypes.create_string_buffer(max(need.value, 1))
+        self._check(self._L.zb_drain(self._h, start, count, hdrs, buf, need.value, ctypes.byref(need)))
+        raw = buf.raw
+        out = []
+        for h in hdrs:
+            v = raw[h.value_offset:h.value_offset + h.value_length]
+            out.append(Record(h.position, h.source_position, h.key, h.record_type, h.value_type, h.intent,
+                              h.rejection_type, v))
+        return out
+
+    def counters(self) -> dict:
+        arr = (ctypes.c_int64 * 8)()
+        self._check(self._L.zb_counters(self._h, arr))
+        return dict(created=arr[0], completed=arr[1], canceled=arr[2], next_wf_key=arr[3], next_job_key=arr[4],
+                    rows=arr[5], arena_bytes=arr[6], log_size=arr[7])

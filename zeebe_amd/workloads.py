@@ -1,0 +1,94 @@
+"""Synthetic inputs for BASELINE.json's configurations.
+
+Shared by the parity tests and bench.py. Payloads are msgpack documents built with the
+reference writer's encoding rules (MsgPackWriter.java:143-305: minimal integers, fixstr keys);
+all generators are deterministic (seeded counter-based RNG, numpy Philox, seed 42).
+"""
+from __future__ import annotations
+
+import struct
+from typing import List, Tuple
+
+import numpy as np
+
+from . import bpmn
+
+
+def mp_int(v: int) -> bytes:
+    """MsgPackWriter.writeInteger (signed semantics)."""
+    if v < -(1 << 5):
+        if v < -(1 << 15):
+            return b"\xd3" + struct.pack(">q", v) if v < -(1 << 31) else b"\xd2" + struct.pack(">i", v)
+        return b"\xd1" + struct.pack(">h", v) if v < -(1 << 7) else b"\xd0" + struct.pack(">b", v)
+    if v < (1 << 7):
+        return struct.pack(">b", v) if v < 0 else bytes([v])
+    if v < (1 << 16):
+        return b"\xcc" + bytes([v]) if v < (1 << 8) else b"\xcd" + struct.pack(">H", v)
+    return b"\xce" + struct.pack(">I", v) if v < (1 << 32) else b"\xcf" + struct.pack(">q", v)
+
+
+def mp_str(s: str) -> bytes:
+    b = s.encode()
+    n = len(b)
+    if n < 32:
+        return bytes([0xa0 | n]) + b
+    if n < 256:
+        return b"\xd9" + bytes([n]) + b
+    return b"\xda" + struct.pack(">H", n) + b
+
+
+def order_payloads(n: int, start: int = 0) -> Tuple[bytes, np.ndarray]:
+    """{"orderId": i} for i in [start, start+n): packed blob + uint64 offsets (n+1)."""
+    head = b"\x81" + mp_str("orderId")
+    parts = [head + mp_int(i) for i in range(start, start + n)]
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(p) for p in parts], dtype=np.uint64)
+    return b"".join(parts), offs
+
+
+def order_string_payloads(n: int, start: int = 0) -> Tuple[bytes, np.ndarray]:
+    """C5: {"orderId": "order-<i>"}."""
+    head = b"\x81" + mp_str("orderId")
+    parts = [head + mp_str("order-%d" % i) for i in range(start, start + n)]
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(p) for p in parts], dtype=np.uint64)
+    return b"".join(parts), offs
+
+
+REGIONS = ("EU", "US", "APAC")
+
+
+def xor_payloads(n: int, seed: int = 42, start: int = 0) -> Tuple[bytes, np.ndarray]:
+    """C3: {"amount": U[0,2000), "region": EU|US|APAC, "score": U[0,1) float64} (Philox, seed 42)."""
+    g = np.random.Generator(np.random.Philox(key=seed))
+    if start:
+        g.bit_generator.advance(start)
+    amount = g.integers(0, 2000, size=n)
+    region = g.integers(0, 3, size=n)
+    score = g.random(size=n)
+    ka, kr, ks = mp_str("amount"), mp_str("region"), mp_str("score")
+    regs = [mp_str(r) for r in REGIONS]
+    parts = []
+    for a, r, s in zip(amount.tolist(), region.tolist(), score.tolist()):
+        f = struct.pack(">f", s)
+        sv = b"\xca" + f if struct.unpack(">f", f)[0] == s else b"\xcb" + struct.pack(">d", s)
+        parts.append(b"\x83" + ka + mp_int(a) + kr + regs[r] + ks + sv)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(p) for p in parts], dtype=np.uint64)
+    return b"".join(parts), offs
+
+
+def split(blob: bytes, offs: np.ndarray) -> List[bytes]:
+    o = offs.tolist()
+    return [blob[o[i]:o[i + 1]] for i in range(len(o) - 1)]
+
+
+CONFIGS = {
+    "c1": dict(workflow=bpmn.config1_workflow, process="process", payloads=order_payloads,
+               job_payloads=lambda: {"task": b"\x81" + mp_str("done") + b"\xc3"}),
+    "c2": dict(workflow=lambda: bpmn.chain_workflow(20), process="chain", payloads=order_payloads,
+               job_payloads=lambda: {"t%d" % k: b"\x81" + mp_str("step") + mp_int(k) for k in range(1, 21)}),
+    "c3": dict(workflow=bpmn.xor_workflow, process="xor", payloads=xor_payloads, job_payloads=lambda: {}),
+    "c4twin": dict(workflow=lambda: bpmn.subprocess_chain_workflow(8), process="subs", payloads=order_payloads,
+                   job_payloads=lambda: {"task%d" % k: b"\x81" + mp_str("sub") + mp_int(k) for k in range(1, 9)}),
+}
