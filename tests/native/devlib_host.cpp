@@ -1,0 +1,51 @@
+// TEST ONLY: compiles the kernels' per-thread routines (zeebe_amd/csrc/zb_devlib.hpp) for the host so
+// that their byte-level logic can be fuzzed against the oracle on CPU (tests/test_devlib_host.py).
+// Nothing here is part of the product; the product runs these routines only inside the HIP kernels.
+#include <cstdint>
+#include <cstring>
+#define __device__
+#define __host__
+#define __forceinline__ inline
+#define __global__
+static inline float __uint_as_float(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+static inline double __longlong_as_double(long long u) { double d; std::memcpy(&d, &u, 8); return d; }
+#define HIP_INCLUDE_HIP_HIP_RUNTIME_H
+#include "../../zeebe_amd/csrc/zb_devlib.hpp"
+
+using namespace zbg;
+
+extern "C" {
+// returns length, -1 malformed, -2 unsupported
+long devlib_merge(const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint32_t nt, uint8_t* out, uint32_t cap) {
+  Out o{nullptr, 0};
+  bool unsup = false;
+  if (!merge_docs(src, ns, tgt, nt, o, unsup)) return -1;
+  if (unsup) return -2;
+  if (o.n > cap) return -3;
+  Out w{out, 0};
+  bool u2 = false;
+  merge_docs(src, ns, tgt, nt, w, u2);
+  if (w.n != o.n) return -4;
+  return (long)w.n;
+}
+// returns count of results; first result pos/len in out[0..1]; -1 unsupported
+long devlib_query(const uint8_t* doc, uint32_t n, const uint8_t* f_ids, const int32_t* f_idx,
+                  const uint8_t* keys, const uint32_t* key_off, const uint32_t* key_len, uint32_t nf, int fast,
+                  uint32_t* out) {
+  DevFilter fs[32];
+  for (uint32_t i = 0; i < nf; i++) {
+    fs[i] = DevFilter{};
+    fs[i].id = f_ids[i];
+    fs[i].index = f_idx[i];
+    fs[i].key_off = key_off[i];
+    fs[i].key_len = (uint16_t)key_len[i];
+  }
+  QueryResult r;
+  bool ok = fast ? query_fast(doc, n, keys + fs[1].key_off, fs[1].key_len, r)
+                 : query_general(doc, n, fs, nf, keys, r);
+  if (!ok) return -1;
+  out[0] = r.pos;
+  out[1] = r.len;
+  return r.count;
+}
+}

@@ -1,0 +1,122 @@
+"""Fuzz the kernels' per-thread byte routines (merge, json-path) against the oracle on CPU.
+
+tests/native/devlib_host.cpp compiles zeebe_amd/csrc/zb_devlib.hpp for the host (test only); the
+same source runs inside the HIP kernels, so logic bugs show up here without a GPU.
+"""
+import ctypes
+import os
+import random
+import subprocess
+
+import msgpack
+import pytest
+
+from oracle import zbref
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+NATIVE = os.path.join(HERE, "native")
+
+
+@pytest.fixture(scope="module")
+def devlib():
+    src = os.path.join(NATIVE, "devlib_host.cpp")
+    so = os.path.join(NATIVE, "libdevlib_host.so")
+    hdr = os.path.join(HERE, "..", "zeebe_amd", "csrc", "zb_devlib.hpp")
+    if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(src), os.path.getmtime(hdr)):
+        subprocess.check_call(["g++", "-O1", "-std=c++17", "-fPIC", "-shared", "-I/opt/rocm/include", "-o", so, src])
+    L = ctypes.CDLL(so)
+    L.devlib_merge.restype = ctypes.c_long
+    L.devlib_merge.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p,
+                               ctypes.c_uint32]
+    L.devlib_query.restype = ctypes.c_long
+    return L
+
+
+def rand_value(r, depth):
+    k = r.random()
+    if depth > 0 and k < 0.2:
+        return {rand_key(r): rand_value(r, depth - 1) for _ in range(r.randint(0, 4))}
+    if depth > 0 and k < 0.35:
+        return [rand_value(r, depth - 1) for _ in range(r.randint(0, 4))]
+    return r.choice([None, True, False, r.randint(-2 ** 40, 2 ** 40), r.randint(-200, 300), r.random() * 100,
+                     "s" * r.randint(0, 40), b"\x01\x02"])
+
+
+def rand_key(r):
+    return r.choice(["a", "b", "c", "d", "0", "1", "2", "key", "x" * 33])
+
+
+def rand_doc(r, depth=3):
+    return {rand_key(r): rand_value(r, depth) for _ in range(r.randint(0, 5))}
+
+
+def dev_merge(L, src, tgt):
+    out = ctypes.create_string_buffer(1 << 16)
+    n = L.devlib_merge(src, len(src), tgt, len(tgt), out, 1 << 16)
+    return n, out.raw[:max(n, 0)]
+
+
+def test_merge_fuzz_vs_oracle(devlib):
+    r = random.Random(7)
+    checked = unsupported = 0
+    for _ in range(3000):
+        s, t = rand_doc(r), rand_doc(r)
+        if r.random() < 0.3:  # overlapping keys with mixed shapes
+            for k in list(s)[:2]:
+                t[k] = rand_value(r, 2)
+        sb, tb = msgpack.packb(s), msgpack.packb(t)
+        n, got = dev_merge(devlib, sb, tb)
+        if n == -2:
+            unsupported += 1
+            continue
+        assert n >= 0, (s, t, n)
+        ref = zbref.merge(sb, tb)
+        ref = b"\x80" if ref == b"\xc0" else ref
+        assert got == ref, (s, t, got.hex(), ref.hex())
+        checked += 1
+    assert unsupported == 0
+    assert checked > 2900
+
+
+def test_merge_byte_vectors(devlib, vectors):
+    for v in vectors["merges"]:
+        sb, tb = bytes.fromhex(v["source"]), bytes.fromhex(v["target"])
+        n, got = dev_merge(devlib, sb, tb)
+        assert n >= 0
+        ref = zbref.merge(sb, tb)
+        assert got == (b"\x80" if ref == b"\xc0" else ref)
+
+
+def _filters(path):
+    """Compile a simple path the way JsonPathQueryCompiler does (for the fuzz only: $.a.b, $.a[1], $.*)."""
+    ids, idx, keys, koff, klen = [0], [0], b"", [0], [0]
+    i = 1
+    toks = path[1:].replace("[", ".").replace("]", "").split(".")[1:] if path != "$" else []
+    for t in toks:
+        if t == "*":
+            ids.append(3); idx.append(0); koff.append(0); klen.append(0)
+        elif t.isdigit():
+            ids.append(2); idx.append(int(t)); koff.append(0); klen.append(0)
+        else:
+            ids.append(1); idx.append(0); koff.append(len(keys)); klen.append(len(t)); keys += t.encode()
+    return ids, idx, keys, koff, klen
+
+
+def test_query_fuzz_vs_oracle(devlib):
+    r = random.Random(11)
+    paths = ["$.a", "$.b", "$.key", "$.a.b", "$.a.c", "$.a[1]", "$.b[0]", "$.*", "$.a.*", "$.0"]
+    for _ in range(3000):
+        doc = msgpack.packb(rand_doc(r))
+        for p in paths:
+            ids, idx, keys, koff, klen = _filters(p)
+            nf = len(ids)
+            A = lambda t, v: (t * len(v))(*v)  # noqa: E731
+            out = (ctypes.c_uint32 * 2)()
+            fast = 1 if (nf == 2 and ids[1] == 1) else 0
+            for use_fast in ({fast, 0} if fast else {0}):
+                cnt = devlib.devlib_query(doc, len(doc), bytes(ids), A(ctypes.c_int32, idx), keys or b"\0",
+                                          A(ctypes.c_uint32, koff), A(ctypes.c_uint32, klen), nf, use_fast, out)
+                ref = zbref.query(p, doc)
+                assert cnt == len(ref), (p, msgpack.unpackb(doc, raw=False), cnt, len(ref), use_fast)
+                if cnt:
+                    assert doc[out[0]:out[0] + out[1]] == ref[0], (p, doc.hex())

@@ -57,7 +57,10 @@ def test_golden_workflows(vectors):
             # one job payload per workflow (the harness schedules per task): use the first
             jp = {"service": bytes.fromhex(spec["instances"][0]["job_payload"])}
             payloads = payloads[:1]
-        o, e, st = _run_both(spec["xml"], spec["process"], payloads, jp)
+        try:
+            o, e, st = _run_both(spec["xml"], spec["process"], payloads, jp)
+        except Exception as ex:
+            raise AssertionError("%s: %s" % (spec["name"], ex))
         _compare(o, e)
 
 

@@ -308,15 +308,14 @@ __device__ inline bool eval_condition(uint32_t pc, const uint32_t* code, const u
 
 // ------------------------------------------------------------------------------ merge
 // Top-level merge(source = job/message payload, target = scope payload), MappingProcessor.merge
-// without mappings. Implemented structurally:
+// without mappings. Implemented structurally (write_node below):
 //   root children = target keys (document order) then source keys not in target;
 //   value = source's if present (MsgPackTree.merge: source node types/leaves win, non-root child
 //   sets replaced), else target's; a target *leaf* at the same path as a source container wins
 //   (stale leafMap entry; MsgPackDocumentTreeWriter checks isLeaf first).
 // Containers are re-encoded with minimal headers and keys re-encoded as minimal strings, leaves
 // copied raw (MsgPackDocumentTreeWriter.writeNode). Unsupported (flagged): duplicate keys, keys
-// containing '[' / ']' (node-id collisions in the reference), non-string keys, source and target
-// both holding a container under the same top-level key, depth > MERGE_MAX_DEPTH.
+// containing '[' / ']' (node-id collisions in the reference), non-string keys, depth > MERGE_MAX_DEPTH.
 constexpr int MERGE_MAX_DEPTH = 16;
 
 struct Out {
@@ -352,76 +351,152 @@ __device__ inline bool key_ok(const uint8_t* s, uint32_t n) {
   return true;
 }
 
-// Re-encodes the value at pos (a subtree of one document) the way the tree writer would,
-// given that no node of the other document shadows it. Returns end offset or 0xffffffff.
-__device__ inline uint32_t reencode(const uint8_t* d, uint32_t n, uint32_t pos, Out& o, bool& unsupported) {
-  // explicit stack of remaining children per open container; keys re-encoded, leaves raw
-  uint32_t remain[MERGE_MAX_DEPTH];
-  bool is_map[MERGE_MAX_DEPTH];
-  bool expect_key[MERGE_MAX_DEPTH];
-  int depth = 0;
-  for (;;) {
-    Tok t;
-    if (pos >= n || !read_tok(d + pos, n - pos, t)) return 0xffffffffu;
-    bool key_slot = depth > 0 && is_map[depth - 1] && expect_key[depth - 1];
-    if (key_slot) {
-      if (t.type != TT_STRING || !key_ok(d + pos + t.hdr, t.len)) { unsupported = true; return 0xffffffffu; }
-      // duplicate key check among the siblings already passed is done by the caller for the root;
-      // nested maps: check the rest of this map for the same key
-      o.str(d + pos + t.hdr, t.len);
-      pos += t.total;
-      expect_key[depth - 1] = false;
-      continue;
+// Is the key (bytes) the canonical decimal form of an array index? (node ids "$[a][0]" collide for
+// map key "0" and array element 0, MsgPackTreeNodeIdConstructor.construct)
+__device__ inline bool parse_index(const uint8_t* s, uint32_t n, uint32_t& idx) {
+  if (n == 0 || n > 9) return false;
+  if (n > 1 && s[0] == '0') return false;
+  uint32_t v = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (s[i] < '0' || s[i] > '9') return false;
+    v = v * 10 + (s[i] - '0');
+  }
+  idx = v;
+  return true;
+}
+
+constexpr uint32_t NONE_POS = 0xffffffffu;
+
+// child of the container at cpos (in doc d) named by a map key (kp,kn) or an array index (when kp == nullptr).
+// Returns NONE_POS when absent; sets unsupported on duplicate keys.
+__device__ inline uint32_t child_of(const uint8_t* d, uint32_t n, uint32_t cpos, const uint8_t* kp, uint32_t kn,
+                                    uint32_t index, bool& unsupported) {
+  if (cpos == NONE_POS) return NONE_POS;
+  Tok c;
+  if (!read_tok(d + cpos, n - cpos, c)) return NONE_POS;
+  uint32_t pos = cpos + c.total;
+  if (c.type == TT_ARRAY) {
+    uint32_t want = index;
+    if (kp && !parse_index(kp, kn, want)) return NONE_POS;
+    if (want >= c.len) return NONE_POS;
+    for (uint32_t i = 0; i < want; i++) {
+      pos = skip_value(d, n, pos);
+      if (pos == 0xffffffffu) return NONE_POS;
     }
-    if (t.type == TT_MAP || t.type == TT_ARRAY) {
-      if (t.type == TT_MAP) {
-        // duplicate keys inside a nested map would be deduplicated by LinkedHashSet: flag them
-        uint32_t kp = pos + t.total;
-        for (uint32_t i = 0; i < t.len; i++) {
+    return pos;
+  }
+  // map: match the key text (array index -> its decimal text)
+  uint8_t buf[10];
+  if (!kp) {
+    uint32_t v = index, l = 0;
+    uint8_t tmp[10];
+    do { tmp[l++] = (uint8_t)('0' + v % 10); v /= 10; } while (v);
+    for (uint32_t i = 0; i < l; i++) buf[i] = tmp[l - 1 - i];
+    kp = buf;
+    kn = l;
+  }
+  uint32_t found = NONE_POS;
+  for (uint32_t i = 0; i < c.len; i++) {
+    Tok k;
+    if (pos >= n || !read_tok(d + pos, n - pos, k)) return NONE_POS;
+    uint32_t vp = pos + k.total;
+    if (k.type == TT_STRING && k.len == kn && bytes_eq(d + pos + k.hdr, kp, kn)) {
+      if (found != NONE_POS) { unsupported = true; return NONE_POS; }
+      found = vp;
+    }
+    pos = skip_value(d, n, vp);
+    if (pos == 0xffffffffu) return NONE_POS;
+  }
+  return found;
+}
+
+// Writes the node at spos of document `d` as MsgPackDocumentTreeWriter would when the other
+// document `t` holds the node tpos at the same path (NONE_POS: no node there): a leaf of `t`
+// shadows a container of `d` (stale leafMap entry wins isLeaf); otherwise `d`'s structure is
+// written with minimal headers / re-encoded keys and its leaves copied raw.
+// Returns false when malformed (unsupported set separately).
+__device__ inline bool write_node(const uint8_t* d, uint32_t n, uint32_t spos, const uint8_t* t, uint32_t tn,
+                                  uint32_t tpos, Out& o, bool& unsupported) {
+  struct Frame {
+    uint32_t next, remaining, tcont, idx;
+    bool is_map;
+  };
+  Frame st[MERGE_MAX_DEPTH];
+  int depth = 0;
+  uint32_t cur_s = spos, cur_t = tpos;
+  for (;;) {
+    // ---- handle node (cur_s, cur_t)
+    Tok ts;
+    if (cur_s >= n || !read_tok(d + cur_s, n - cur_s, ts)) return false;
+    const bool s_cont = ts.type == TT_MAP || ts.type == TT_ARRAY;
+    bool t_leaf = false, t_cont = false;
+    Tok tt;
+    if (cur_t != NONE_POS) {
+      if (!read_tok(t + cur_t, tn - cur_t, tt)) return false;
+      t_cont = tt.type == TT_MAP || tt.type == TT_ARRAY;
+      t_leaf = !t_cont;
+    }
+    if (!s_cont) {
+      o.put_bytes(d + cur_s, ts.total);
+    } else if (t_leaf) {
+      o.put_bytes(t + cur_t, tt.total);
+    } else {
+      if (ts.type == TT_MAP) {
+        // keys must be unique strings without brackets (LinkedHashSet dedup / node-id collisions)
+        uint32_t kp = cur_s + ts.total;
+        for (uint32_t i = 0; i < ts.len; i++) {
           Tok ki;
-          if (kp >= n || !read_tok(d + kp, n - kp, ki)) return 0xffffffffu;
+          if (kp >= n || !read_tok(d + kp, n - kp, ki)) return false;
+          if (ki.type != TT_STRING || !key_ok(d + kp + ki.hdr, ki.len)) { unsupported = true; return true; }
           uint32_t vend_i = skip_value(d, n, kp + ki.total);
-          if (vend_i == 0xffffffffu) return vend_i;
+          if (vend_i == 0xffffffffu) return false;
           uint32_t kj = vend_i;
-          for (uint32_t j = i + 1; j < t.len; j++) {
+          for (uint32_t j = i + 1; j < ts.len; j++) {
             Tok kk;
-            if (kj >= n || !read_tok(d + kj, n - kj, kk)) return 0xffffffffu;
-            if (kk.type == ki.type && kk.len == ki.len && bytes_eq(d + kj + kk.hdr, d + kp + ki.hdr, ki.len)) {
+            if (kj >= n || !read_tok(d + kj, n - kj, kk)) return false;
+            if (kk.type == TT_STRING && kk.len == ki.len && bytes_eq(d + kj + kk.hdr, d + kp + ki.hdr, ki.len)) {
               unsupported = true;
-              return 0xffffffffu;
+              return true;
             }
             kj = skip_value(d, n, kj + kk.total);
-            if (kj == 0xffffffffu) return kj;
+            if (kj == 0xffffffffu) return false;
           }
           kp = vend_i;
         }
-        o.map_hdr(t.len);
+        o.map_hdr(ts.len);
       } else {
-        o.arr_hdr(t.len);
+        o.arr_hdr(ts.len);
       }
-      pos += t.total;
-      if (t.len > 0) {
-        if (depth >= MERGE_MAX_DEPTH) { unsupported = true; return 0xffffffffu; }
-        remain[depth] = t.len;
-        is_map[depth] = t.type == TT_MAP;
-        expect_key[depth] = t.type == TT_MAP;
-        depth++;
-        continue;
+      if (ts.len > 0) {
+        if (depth >= MERGE_MAX_DEPTH) { unsupported = true; return true; }
+        st[depth++] = Frame{cur_s + ts.total, ts.len, t_cont ? cur_t : NONE_POS, 0, ts.type == TT_MAP};
       }
-    } else {
-      o.put_bytes(d + pos, t.total);
-      pos += t.total;
     }
-    // a value completed: pop finished containers
-    while (depth > 0) {
-      remain[depth - 1] -= 1;
-      if (remain[depth - 1] > 0) {
-        if (is_map[depth - 1]) expect_key[depth - 1] = true;
-        break;
+    // ---- next child
+    for (;;) {
+      if (depth == 0) return true;
+      Frame& f = st[depth - 1];
+      if (f.remaining == 0) { depth--; continue; }
+      uint32_t vpos;
+      if (f.is_map) {
+        Tok k;
+        if (f.next >= n || !read_tok(d + f.next, n - f.next, k)) return false;
+        o.str(d + f.next + k.hdr, k.len);
+        vpos = f.next + k.total;
+        cur_t = child_of(t, tn, f.tcont, d + f.next + k.hdr, k.len, 0, unsupported);
+      } else {
+        vpos = f.next;
+        cur_t = child_of(t, tn, f.tcont, nullptr, 0, f.idx, unsupported);
       }
-      depth--;
+      if (unsupported) return true;
+      uint32_t vend = skip_value(d, n, vpos);
+      if (vend == 0xffffffffu) return false;
+      f.next = vend;
+      f.remaining--;
+      f.idx++;
+      cur_s = vpos;
+      break;
     }
-    if (depth == 0) return pos;
   }
 }
 
@@ -512,17 +587,12 @@ __device__ inline bool merge_docs(const uint8_t* src, uint32_t ns, const uint8_t
     RootEntry e;
     if (!find_key(src, ns, sf, sc, tgt + pos + k.hdr, k.len, e)) return false;
     if (e.vpos == 0) {
-      if (reencode(tgt, nt, vp, o, unsupported) == 0xffffffffu) return unsupported;
+      if (!write_node(tgt, nt, vp, nullptr, 0, NONE_POS, o, unsupported)) return false;  // target only
     } else {
-      Tok sv, tv;
-      read_tok(src + e.vpos, ns - e.vpos, sv);
-      read_tok(tgt + vp, nt - vp, tv);
-      bool s_cont = sv.type == TT_MAP || sv.type == TT_ARRAY;
-      bool t_cont = tv.type == TT_MAP || tv.type == TT_ARRAY;
-      if (!s_cont) o.put_bytes(src + e.vpos, e.vend - e.vpos);   // source leaf wins
-      else if (!t_cont) o.put_bytes(tgt + vp, ve - vp);          // quirk: target leaf survives
-      else { unsupported = true; return true; }                   // both containers: deep shadowing
+      // source node wins, except where the target holds a leaf at the same path
+      if (!write_node(src, ns, e.vpos, tgt, nt, vp, o, unsupported)) return false;
     }
+    if (unsupported) return true;
     pos = ve;
   }
   // source keys not in target
@@ -534,12 +604,12 @@ __device__ inline bool merge_docs(const uint8_t* src, uint32_t ns, const uint8_t
     RootEntry e;
     if (!find_key(tgt, nt, tf, tc, src + pos + k.hdr, k.len, e)) return false;
     uint32_t ve;
+    ve = skip_value(src, ns, vp);
+    if (ve == 0xffffffffu) return false;
     if (e.vpos == 0) {
       o.str(src + pos + k.hdr, k.len);
-      ve = reencode(src, ns, vp, o, unsupported);
-      if (ve == 0xffffffffu) return unsupported;
-    } else {
-      ve = skip_value(src, ns, vp);
+      if (!write_node(src, ns, vp, nullptr, 0, NONE_POS, o, unsupported)) return false;  // source only
+      if (unsupported) return true;
     }
     pos = ve;
   }

@@ -74,6 +74,7 @@ struct zb_engine {
   uint32_t* tickets = nullptr;
   uint32_t* derr = nullptr;
   uint64_t* dstats = nullptr;
+  uint64_t* derr_info = nullptr;
   WaveHdr* h_hdr_pinned = nullptr;  // pinned mirror for D2H polling
   uint32_t* h_err_pinned = nullptr;
 
@@ -166,6 +167,7 @@ WaveParams wave_params(zb_engine* e) {
   p.status = e->status;
   p.tickets = e->tickets;
   p.err = e->derr;
+  p.err_info = e->derr_info;
   p.stats = e->dstats;
   p.log_cap = e->cfg.log_capacity;
   p.row_cap = e->cfg.row_capacity;
@@ -185,6 +187,9 @@ int check_device_errors(zb_engine* e, uint32_t flags) {
   if (flags & DE_PROCESSING) m += " processing-failure";
   if (flags & DE_LOOKBACK_TIMEOUT) m += " lookback-timeout";
   if (flags & DE_BAD_PAYLOAD) m += " malformed-payload";
+  uint64_t info = ~0ull;
+  if (hipMemcpy(&info, e->derr_info, sizeof(info), hipMemcpyDeviceToHost) == hipSuccess && info != ~0ull)
+    m += " (first at log position " + std::to_string(info >> 8) + ", site " + std::to_string(info & 0xff) + ")";
   int code = ZB_EPROCESSING;
   if (flags & (DE_LOG_FULL | DE_ROWS_FULL | DE_ARENA_FULL)) code = ZB_ENOMEM;
   else if (flags & DE_UNSUPPORTED) code = ZB_EUNSUPPORTED;
@@ -228,6 +233,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->tickets, 128 * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->derr, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->dstats, 8 * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->derr_info, sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_hdr_pinned, 2 * sizeof(WaveHdr)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_err_pinned, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   e->ev.resize(2 * WAVES_PER_SYNC);
@@ -248,7 +254,8 @@ void zb_engine_destroy(zb_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (auto& x : e->ev)
     if (x) (void)hipEventDestroy(x);
-  void* ps[] = {e->log, e->links, e->rmeta, e->rkeys, e->arena, e->hdr, e->status, e->tickets, e->derr, e->dstats};
+  void* ps[] = {e->log, e->links, e->rmeta, e->rkeys, e->arena, e->hdr, e->status, e->tickets, e->derr, e->dstats,
+                e->derr_info};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->h_hdr_pinned) (void)hipHostFree(e->h_hdr_pinned);
@@ -278,6 +285,7 @@ int zb_reset(zb_engine* e, int keep_staged) {
   HIPCHECK(e, hipMemsetAsync(e->status, 0, e->status_tiles * 3 * sizeof(unsigned long long), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->tickets, 0, 128 * sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->derr, 0, sizeof(uint32_t), e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->derr_info, 0xff, sizeof(uint64_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->dstats, 0, 8 * sizeof(uint64_t), e->stream));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
   e->ranges.clear();

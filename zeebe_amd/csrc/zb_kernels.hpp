@@ -24,6 +24,7 @@ struct WaveParams {
   unsigned long long* status;  // 3 granules per tile
   uint32_t* tickets;      // [128]
   uint32_t* err;          // sticky DevErr flags
+  uint64_t* err_info;     // min over failing records of (position << 8 | site)
   uint64_t* stats;        // [8] transitions, completed, created, merges, merge_bytes, cond_bytes, waves
   uint64_t log_cap, row_cap, arena_cap;
   int64_t wave;

@@ -53,11 +53,16 @@ struct TState {
   uint8_t d_type, d_code, d_a, d_b;
   uint16_t d_q;
   int64_t d_pos;
-  uint32_t err;
+  uint32_t err, err_site;
   // stats
   uint32_t transitions, completed, created, merges;
   uint32_t merge_bytes, cond_bytes;
 };
+
+__device__ __forceinline__ void fail_at(TState& t, uint32_t flag, uint32_t site) {
+  if (!t.err) t.err_site = site;
+  t.err |= flag;
+}
 
 __device__ __forceinline__ const uint8_t* payload_ptr(const uint8_t* arena, uint32_t ref, uint32_t& len) {
   const uint8_t* p = arena + (uint64_t)ref * 8;
@@ -68,7 +73,7 @@ __device__ __forceinline__ const uint8_t* payload_ptr(const uint8_t* arena, uint
 __device__ __forceinline__ uint32_t blob_bytes(uint32_t len) { return (4 + len + 7) & ~7u; }
 
 __device__ __forceinline__ Slot& add_slot(TState& t) {
-  if (t.ns >= MAX_SLOTS) { t.err |= DE_PROCESSING; return t.s[MAX_SLOTS - 1]; }
+  if (t.ns >= MAX_SLOTS) { fail_at(t, DE_PROCESSING, 1); return t.s[MAX_SLOTS - 1]; }
   Slot& s = t.s[t.ns++];
   s.flags = 0; s.ord = 0; s.rord = 0;
   return s;
@@ -115,7 +120,7 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
   bool ok;
   switch (intent) {
     case WI_ELEMENT_READY: case WI_ELEMENT_ACTIVATED: case WI_ELEMENT_COMPLETING:
-      if (!self_alive) { t.err |= DE_PROCESSING; return; }  // NPE in noConcurrentTransitionGuard
+      if (!self_alive) { fail_at(t, DE_PROCESSING, 2); return; }  // NPE in noConcurrentTransitionGuard
       ok = P.rmeta[rself].state == intent;
       break;
     case WI_ELEMENT_COMPLETED: case WI_END_EVENT_OCCURRED: case WI_GATEWAY_ACTIVATED:
@@ -127,7 +132,7 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
     default: ok = false;
   }
   if (!ok) return;
-  if (rec.elem == NO_ELEM) { t.err |= DE_PROCESSING; return; }
+  if (rec.elem == NO_ELEM) { fail_at(t, DE_PROCESSING, 3); return; }
   const DevElem el = P.elems[rec.elem];
   const uint8_t step = el.step[intent];
   if (step == ST_UNBOUND || step == ST_NONE) return;
@@ -144,16 +149,16 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
       break;
     }
     case ST_APPLY_OUTPUT_MAPPING: {  // OutputMappingHandler :42-85, outputBehavior null -> merge
-      if (!scope_alive) { t.err |= DE_PROCESSING; return; }
+      if (!scope_alive) { fail_at(t, DE_PROCESSING, 4); return; }
       uint32_t ns_, nt_;
       const uint8_t* src = payload_ptr(P.arena, rec.payload, ns_);
       const uint32_t tref = P.rmeta[rscope].payload;
       const uint8_t* tgt = payload_ptr(P.arena, tref, nt_);
       Out o{nullptr, 0};
       bool unsup = false;
-      if (!merge_docs(src, ns_, tgt, nt_, o, unsup)) { t.err |= DE_BAD_PAYLOAD; return; }
-      if (unsup) { t.err |= DE_UNSUPPORTED; return; }
-      if (t.merge) { t.err |= DE_UNSUPPORTED; return; }
+      if (!merge_docs(src, ns_, tgt, nt_, o, unsup)) { fail_at(t, DE_BAD_PAYLOAD, 5); return; }
+      if (unsup) { fail_at(t, DE_UNSUPPORTED, 6); return; }
+      if (t.merge) { fail_at(t, DE_UNSUPPORTED, 7); return; }
       t.merge = true;
       t.m_src = rec.payload; t.m_tgt = tref; t.m_len = o.n;
       t.m_bytes = blob_bytes(o.n);
@@ -188,7 +193,7 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
         const uint16_t flow = P.cond_flows[el.cond_begin + i];
         const bool r = eval_condition(P.elems[flow].cond_prog, P.code, doc, n, P.consts, P.queries, P.filters,
                                       P.pool, co, unsup);
-        if (unsup) { t.err |= DE_UNSUPPORTED; return; }
+        if (unsup) { fail_at(t, DE_UNSUPPORTED, 8); return; }
         if (co.err) break;
         if (r) { chosen = flow; break; }
       }
@@ -211,7 +216,7 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
       break;
     }
     case ST_CONSUME_TOKEN: {  // ConsumeTokenHandler :30-43
-      if (!scope_alive) { t.err |= DE_PROCESSING; return; }
+      if (!scope_alive) { fail_at(t, DE_PROCESSING, 9); return; }
       RowMeta& m = P.rmeta[rscope];
       const RowKeys k = P.rkeys[rscope];
       Slot& s = add_slot(t);
@@ -235,7 +240,7 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
       if (step == ST_TAKE_SEQUENCE_FLOW) { s.d.elem = el.out0; out_intent = WI_SEQUENCE_FLOW_TAKEN; }
       else if (step == ST_ACTIVATE_GATEWAY) { s.d.elem = el.target; out_intent = WI_GATEWAY_ACTIVATED; }
       else { s.d.elem = el.target; out_intent = WI_END_EVENT_OCCURRED; }
-      if (s.d.elem == NO_ELEM) { t.err |= DE_PROCESSING; return; }
+      if (s.d.elem == NO_ELEM) { fail_at(t, DE_PROCESSING, 10); return; }
       wf_event(t, s, out_intent, t.ns > 1);
       s.flags |= SF_KEY_WF; s.ord = (uint8_t)t.nwf++;
       s.rself = NO_ROW; s.rscope = rscope;
@@ -254,7 +259,7 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
       break;
     }
     case ST_TRIGGER_START_EVENT: {  // TriggerStartEventHandler :30-39
-      if (el.start == NO_ELEM) { t.err |= DE_PROCESSING; return; }
+      if (el.start == NO_ELEM) { fail_at(t, DE_PROCESSING, 11); return; }
       Slot& s = add_slot(t);
       s.d = rec;
       s.d.elem = el.start;
@@ -275,7 +280,7 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
     }
     default:
       // message subscription, termination: not on the GPU path yet (flagged, never silently skipped)
-      t.err |= DE_UNSUPPORTED;
+      fail_at(t, DE_UNSUPPORTED, 12);
       break;
   }
 }
@@ -285,7 +290,7 @@ __device__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t p
   const uint8_t vt = kind_vt(rec.kind), rt = kind_rt(rec.kind);
   if (vt == ZB_VT_WORKFLOW_INSTANCE) {
     if (rt == ZB_RT_COMMAND) {
-      if (rec.intent != WI_CREATE) { t.err |= DE_UNSUPPORTED; return; }
+      if (rec.intent != WI_CREATE) { fail_at(t, DE_UNSUPPORTED, 13); return; }
       // CreateWorkflowInstanceEventProcessor :233-368: key first, then resolve (done at submit)
       const uint8_t ord = (uint8_t)t.nwf++;
       if (rec.elem == NO_ELEM) {
@@ -312,7 +317,7 @@ __device__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t p
       }
     } else if (rt == ZB_RT_EVENT) {
       if (rec.intent == WI_CREATED) {  // WorkflowInstanceCreatedEventProcessor: index insert (READY)
-        if (rself == NO_ROW) { t.err |= DE_ROWS_FULL; return; }
+        if (rself == NO_ROW) { fail_at(t, DE_ROWS_FULL, 14); return; }
         RowMeta m;
         m.payload = rec.payload; m.parent = NO_ROW; m.elem = rec.elem; m.state = WI_ELEMENT_READY; m.flags = 0;
         m.nchild = 0;
@@ -419,7 +424,7 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
     // ---------------- 1. process
     TState t;
     t.ns = t.nwf = t.njob = t.nrow = 0;
-    t.bytes = 0; t.merge = false; t.detail = false; t.err = 0;
+    t.bytes = 0; t.merge = false; t.detail = false; t.err = 0; t.err_site = 0;
     t.transitions = t.completed = t.created = t.merges = 0;
     t.merge_bytes = t.cond_bytes = 0;
     const int64_t r = begin + tile * WG + threadIdx.x;
@@ -576,7 +581,11 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
     }
 
     // ---------------- stats + header
-    if (err) atomicOr(&s_err, err);
+    if (err) {
+      atomicOr(&s_err, err);
+      // first failing record (lowest position) and the code site that flagged it
+      atomicMin((unsigned long long*)P.err_info, ((unsigned long long)r << 8) | (t.err_site & 0xff));
+    }
     if (t.transitions) atomicAdd(&s_stats[0], t.transitions);
     if (t.completed) atomicAdd(&s_stats[1], t.completed);
     if (t.created) atomicAdd(&s_stats[2], t.created);
