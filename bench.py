@@ -1,0 +1,174 @@
+"""bench.py — BPMN element transitions/s on MI355X (BASELINE.json metric), one partition per GPU.
+
+Workload (BASELINE.json configs[1]): a 20-service-task chain, 1,000,000 concurrent
+instances per GPU (all CREATE commands injected before wave 0), job k completed by the canonical
+harness with payload {"step": k}; every completion runs the default output merge. One "step" =
+inject the staged 1M CREATE batch (already resident in HBM) and run every lockstep wave until the
+partition is quiescent (~148 waves, ~169M records, 108M WORKFLOW_INSTANCE transitions).
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process and one partition
+per GPU, each with its own 1M instances (partitions never communicate for this workload:
+weak scaling, no collective on the data path; the barrier + max-over-ranks timing use torch.distributed).
+
+Prints ONE JSON line on rank 0 (contract in the task statement) with "roofline" and "cpu_baseline".
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+BYTES_PER_TRANSITION = 96  # 32 B row read + 32 B row write + 32 B record descriptor
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--instances", type=int, default=1_000_000)
+    ap.add_argument("--tasks", type=int, default=20)
+    ap.add_argument("--cpu-sample", type=int, default=30_000, help="instances in the oracle CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(n_inst, tasks):
+    """The oracle (sequential C++ restatement, 1 thread) on a bounded sample of the same workload."""
+    from oracle import zbref
+    from zeebe_amd import bpmn, workloads
+
+    xml = bpmn.chain_workflow(tasks).to_xml()
+    o = zbref.Oracle()
+    o.deploy(xml, 100, 1)
+    for k in range(1, tasks + 1):
+        o.set_job_payload(100, "t%d" % k, b"\x81" + workloads.mp_str("step") + workloads.mp_int(k))
+    blob, offs = workloads.order_payloads(n_inst)
+    for p in workloads.split(blob, offs):
+        o.create("chain", p)
+    n, secs = o.run_timed()
+    transitions = (8 + 5 * tasks) * n_inst
+    return {"value": transitions / secs, "unit": "transitions/s", "cores": 1, "kind": "port",
+            "sample": "C2 chain of %d tasks, %d instances, %d records processed in %.2f s by oracle/zbref "
+                      "(1 thread, sequential FIFO, canonical job harness)" % (tasks, n_inst, n, secs),
+            "completed_instances_per_s": n_inst / secs}
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+
+    from zeebe_amd import bpmn, workloads
+    from zeebe_amd.engine import Engine
+
+    n = a.instances
+    recs_per_inst = 1 + (8 + 5 * a.tasks) + 3 * a.tasks  # CREATE + WF events + JOB CREATE/CREATED/COMPLETED
+    eng = Engine(device=local_rank, partition_id=rank, partition_count=world,
+                 log_capacity=int(n * (recs_per_inst + 2)), row_capacity=int(n * (a.tasks + 2)),
+                 arena_bytes=int(n * (48 + 32 * a.tasks)) + (64 << 20))
+    xml = bpmn.chain_workflow(a.tasks).to_xml()
+    eng.deploy(xml, 100, 1)
+    for k in range(1, a.tasks + 1):
+        eng.set_job_payload(100, "t%d" % k, b"\x81" + workloads.mp_str("step") + workloads.mp_int(k))
+    # instance i of this partition: global instance id = rank * n + i (round-robin over partitions)
+    blob, offs = workloads.order_payloads(n, start=rank * n)
+    eng.create_packed("chain", blob, offs)
+
+    def one_step():
+        eng.reset(keep_staged=True)
+        st = eng.step()
+        assert st["quiescent"], st
+        return st
+
+    for _ in range(a.warmup):
+        one_step()
+
+    def barrier():
+        if dist is not None:
+            import torch
+
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    tot = dict(transitions=0, completed=0, kernel_ms=0.0, launches=0, waves=0, merge_bytes=0, cond_bytes=0,
+               records=0)
+    for _ in range(a.steps):
+        st = one_step()
+        tot["transitions"] += st["transitions"]
+        tot["completed"] += st["completed_instances"]
+        tot["kernel_ms"] += st["wave_kernel_ms"]
+        tot["launches"] += st["launches"]
+        tot["waves"] += st["waves"]
+        tot["merge_bytes"] += st["merge_bytes"]
+        tot["cond_bytes"] += st["condition_payload_bytes"]
+        tot["records"] += st["records_processed"]
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([tot["transitions"], tot["completed"]], dtype=torch.float64, device="cuda")
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        all_transitions, all_completed = float(c[0]), float(c[1])
+    else:
+        all_transitions, all_completed = float(tot["transitions"]), float(tot["completed"])
+
+    if rank == 0:
+        alg_bytes = BYTES_PER_TRANSITION * tot["transitions"] + tot["merge_bytes"] + tot["cond_bytes"]
+        kernel_s = tot["kernel_ms"] / 1e3
+        achieved = alg_bytes / kernel_s / 1e9 if kernel_s > 0 else 0.0
+        out = {
+            "metric": "BPMN element transitions/sec (+ completed instances/sec) per node; % HBM roofline",
+            "value": all_transitions / elapsed,
+            "unit": "transitions/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed * 1e3 / a.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (SURVEY §8d C2: {\"orderId\": i} create payloads, {\"step\": k} job payloads)",
+            "config": {"workload": "C2: 20-service-task chain, %d concurrent instances per GPU, canonical job "
+                                   "harness, default output merges" % n,
+                       "instances_per_gpu": n, "tasks": a.tasks, "partitions": world,
+                       "parallelism": "partition-per-gpu"},
+            "completed_instances_per_s": all_completed / elapsed,
+            "records_processed_per_step_rank0": tot["records"] / a.steps,
+            "wave_launches_per_step": tot["launches"] / a.steps,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "zbg::k_wave", "launches": tot["launches"],
+                         "avg_launch_us": tot["kernel_ms"] * 1e3 / max(tot["launches"], 1),
+                         "alg_bytes_per_transition": BYTES_PER_TRANSITION,
+                         "alg_bytes_total": alg_bytes},
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(a.cpu_sample, a.tasks)
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

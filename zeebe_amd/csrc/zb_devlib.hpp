@@ -134,7 +134,7 @@ __device__ inline bool query_fast(const uint8_t* d, uint32_t n, const uint8_t* k
 
 // General executor (literal state machine of MsgPackQueryExecutor.visitElement), depth <= 30.
 constexpr int JP_MAX_DEPTH = 30;
-__device__ inline bool query_general(const uint8_t* d, uint32_t n, const DevFilter* f, uint32_t nf,
+__device__ __noinline__ bool query_general(const uint8_t* d, uint32_t n, const DevFilter* f, uint32_t nf,
                                      const uint8_t* pool, QueryResult& r) {
   r.count = 0; r.pos = 0; r.len = 0;
   int cur[JP_MAX_DEPTH], num[JP_MAX_DEPTH], app[JP_MAX_DEPTH], dyn[JP_MAX_DEPTH];
@@ -256,7 +256,7 @@ __device__ __forceinline__ bool same_type(Operand& x, Operand& y, CondOut& out) 
 }
 
 // Evaluates one compiled condition; returns result (valid when out.err == 0 && !unsupported).
-__device__ inline bool eval_condition(uint32_t pc, const uint32_t* code, const uint8_t* doc, uint32_t n,
+__device__ __noinline__ bool eval_condition(uint32_t pc, const uint32_t* code, const uint8_t* doc, uint32_t n,
                                       const DevConst* consts, const DevQuery* queries, const DevFilter* filters,
                                       const uint8_t* pool, CondOut& out, bool& unsupported) {
   bool r = false;
@@ -415,7 +415,7 @@ __device__ inline uint32_t child_of(const uint8_t* d, uint32_t n, uint32_t cpos,
 // shadows a container of `d` (stale leafMap entry wins isLeaf); otherwise `d`'s structure is
 // written with minimal headers / re-encoded keys and its leaves copied raw.
 // Returns false when malformed (unsupported set separately).
-__device__ inline bool write_node(const uint8_t* d, uint32_t n, uint32_t spos, const uint8_t* t, uint32_t tn,
+__device__ __noinline__ bool write_node(const uint8_t* d, uint32_t n, uint32_t spos, const uint8_t* t, uint32_t tn,
                                   uint32_t tpos, Out& o, bool& unsupported) {
   struct Frame {
     uint32_t next, remaining, tcont, idx;
@@ -548,7 +548,7 @@ __device__ inline bool check_root(const uint8_t* d, uint32_t n, uint32_t first, 
 }
 
 // Performs the merge into o (size pass when o.dst == nullptr). Returns false when malformed.
-__device__ inline bool merge_docs(const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint32_t nt, Out& o,
+__device__ __noinline__ bool merge_docs(const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint32_t nt, Out& o,
                                   bool& unsupported) {
   Tok ts, tt;
   bool src_nil = ns == 0 || (ns >= 1 && src[0] == 0xc0);

@@ -43,7 +43,7 @@ struct Slot {
 };
 
 struct TState {
-  Slot s[MAX_SLOTS];
+  Slot* s;  // this thread's MAX_SLOTS output slots, staged in LDS (dynamic indexing stays out of scratch)
   int ns, nwf, njob, nrow;
   uint32_t bytes;
   // one merge and one incident detail per thread at most
@@ -364,29 +364,26 @@ __device__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t p
 }
 
 // ------------------------------------------------------------------------------ scan helpers
+// Tile counts packed like the status granules: a = rec << 28 | wf, b = job << 28 | row, c = bytes.
+// Sums of packed values never carry between fields (per-wave totals < 2^28, checked on the host).
 struct Cnt {
-  uint64_t rec, wf, job, row, bytes;
+  uint64_t a, b, c;
 };
-
-__device__ __forceinline__ Cnt cnt_add(const Cnt& a, const Cnt& b) {
-  return Cnt{a.rec + b.rec, a.wf + b.wf, a.job + b.job, a.row + b.row, a.bytes + b.bytes};
-}
-
+__device__ __forceinline__ Cnt cnt_add(const Cnt& x, const Cnt& y) { return Cnt{x.a + y.a, x.b + y.b, x.c + y.c}; }
 __device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int d) {
   return (uint64_t)__shfl_up((unsigned long long)v, d, 64);
 }
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int d) {
   return (uint64_t)__shfl_xor((unsigned long long)v, d, 64);
 }
+constexpr uint64_t F28 = 0xfffffffull;
+constexpr uint64_t F56 = 0xffffffffffffffull;
 
 __device__ __forceinline__ void publish(unsigned long long* st, int64_t tile, uint32_t tag, const Cnt& c) {
   const unsigned long long t8 = (unsigned long long)tag << 56;
-  unsigned long long g0 = t8 | ((c.rec & 0xfffffffull) << 28) | (c.wf & 0xfffffffull);
-  unsigned long long g1 = t8 | ((c.job & 0xfffffffull) << 28) | (c.row & 0xfffffffull);
-  unsigned long long g2 = t8 | (c.bytes & 0xffffffffffffffull);
-  __hip_atomic_store(st + 3 * tile + 0, g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(st + 3 * tile + 1, g1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(st + 3 * tile + 2, g2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(st + 3 * tile + 0, t8 | (c.a & F56), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(st + 3 * tile + 1, t8 | (c.b & F56), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(st + 3 * tile + 2, t8 | (c.c & F56), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------------------ the kernel
@@ -397,6 +394,7 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
   __shared__ int64_t s_tile;
   __shared__ uint32_t s_err;
   __shared__ uint32_t s_stats[6];
+  __shared__ Slot s_slots[WG * MAX_SLOTS];
 
   const WaveHdr* hin = P.hdr + (P.wave & 1);
   WaveHdr* hout = P.hdr + ((P.wave + 1) & 1);
@@ -423,6 +421,7 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
 
     // ---------------- 1. process
     TState t;
+    t.s = s_slots + threadIdx.x * MAX_SLOTS;
     t.ns = t.nwf = t.njob = t.nrow = 0;
     t.bytes = 0; t.merge = false; t.detail = false; t.err = 0; t.err_site = 0;
     t.transitions = t.completed = t.created = t.merges = 0;
@@ -461,11 +460,11 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
       ta += s_a[w]; tb += s_b[w];
     }
     const uint64_t ea = wa + ia - a, eb = wb + ib - b;  // thread-exclusive within the tile
-    const Cnt agg{ta & 0xffff, (ta >> 16) & 0xffff, (ta >> 32) & 0xffff, ta >> 48, tb};
+    const Cnt agg{((ta & 0xffff) << 28) | ((ta >> 16) & 0xffff), (((ta >> 32) & 0xffff) << 28) | (ta >> 48), tb};
 
     // ---------------- 3. decoupled look-back (wave 0)
     if (wv == 0) {
-      Cnt excl{0, 0, 0, 0, 0};
+      Cnt excl{0, 0, 0};
       if (tile == 0) {
         if (lane == 0) publish(P.status, 0, (epoch << 1) | 1, agg);
       } else {
@@ -475,7 +474,7 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
         bool timeout = false;
         for (;;) {
           const int64_t idx = base - lane;
-          Cnt v{0, 0, 0, 0, 0};
+          Cnt v{0, 0, 0};
           int st = 2;
           if (idx >= 0) {
             for (;;) {
@@ -486,8 +485,7 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
               uint32_t t0 = (uint32_t)(g0 >> 56), t1 = (uint32_t)(g1 >> 56), t2 = (uint32_t)(g2 >> 56);
               if (t0 == t1 && t1 == t2 && (t0 >> 1) == epoch) {
                 st = (t0 & 1) ? 2 : 1;
-                v = Cnt{(g0 >> 28) & 0xfffffffull, g0 & 0xfffffffull, (g1 >> 28) & 0xfffffffull, g1 & 0xfffffffull,
-                        g2 & 0xffffffffffffffull};
+                v = Cnt{g0 & F56, g1 & F56, g2 & F56};
                 break;
               }
               if (++spins > (1u << 24)) { timeout = true; st = 2; break; }
@@ -496,11 +494,10 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
           }
           const uint64_t pm = __ballot(st == 2);
           const int first = pm ? __ffsll((unsigned long long)pm) - 1 : 64;
-          Cnt c = lane <= first ? v : Cnt{0, 0, 0, 0, 0};
+          Cnt c = lane <= first ? v : Cnt{0, 0, 0};
 #pragma unroll
           for (int d = 32; d >= 1; d >>= 1) {
-            c.rec += shfl_xor64(c.rec, d); c.wf += shfl_xor64(c.wf, d); c.job += shfl_xor64(c.job, d);
-            c.row += shfl_xor64(c.row, d); c.bytes += shfl_xor64(c.bytes, d);
+            c.a += shfl_xor64(c.a, d); c.b += shfl_xor64(c.b, d); c.c += shfl_xor64(c.c, d);
           }
           excl = cnt_add(excl, c);
           if (pm) break;
@@ -515,11 +512,11 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
     const Cnt ex = s_excl;
 
     // ---------------- 4. write
-    uint64_t out_rec = (uint64_t)end + ex.rec + (ea & 0xffff);
-    const uint64_t wf0 = ex.wf + ((ea >> 16) & 0xffff);
-    const uint64_t job0 = ex.job + ((ea >> 32) & 0xffff);
-    const uint64_t row0 = (uint64_t)hin->rows_next + ex.row + (ea >> 48);
-    const uint64_t byte0 = (uint64_t)hin->arena_next + ex.bytes + eb;
+    uint64_t out_rec = (uint64_t)end + (ex.a >> 28) + (ea & 0xffff);
+    const uint64_t wf0 = (ex.a & F28) + ((ea >> 16) & 0xffff);
+    const uint64_t job0 = (ex.b >> 28) + ((ea >> 32) & 0xffff);
+    const uint64_t row0 = (uint64_t)hin->rows_next + (ex.b & F28) + (ea >> 48);
+    const uint64_t byte0 = (uint64_t)hin->arena_next + ex.c + eb;
     uint32_t err = t.err;
     uint64_t bump = byte0;
     uint32_t merged_ref = 0, detail_ref = 0;
@@ -596,11 +593,11 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
       const Cnt tot = cnt_add(ex, agg);
       WaveHdr h = *hin;
       h.begin = end;
-      h.end = end + (int64_t)tot.rec;
-      h.wf_next = hin->wf_next + 5 * (int64_t)tot.wf;
-      h.job_next = hin->job_next + 5 * (int64_t)tot.job;
-      h.rows_next = hin->rows_next + (int64_t)tot.row;
-      h.arena_next = hin->arena_next + (int64_t)tot.bytes;
+      h.end = end + (int64_t)(tot.a >> 28);
+      h.wf_next = hin->wf_next + 5 * (int64_t)(tot.a & F28);
+      h.job_next = hin->job_next + 5 * (int64_t)(tot.b >> 28);
+      h.rows_next = hin->rows_next + (int64_t)(tot.b & F28);
+      h.arena_next = hin->arena_next + (int64_t)tot.c;
       *hout = h;
     }
     __syncthreads();
