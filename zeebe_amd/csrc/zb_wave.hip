@@ -150,21 +150,19 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
     }
     case ST_APPLY_OUTPUT_MAPPING: {  // OutputMappingHandler :42-85, outputBehavior null -> merge
       if (!scope_alive) { fail_at(t, DE_PROCESSING, 4); return; }
-      uint32_t ns_, nt_;
-      const uint8_t* src = payload_ptr(P.arena, rec.payload, ns_);
+      // The merge itself runs once, in the write phase, into an arena blob sized by the upper bound
+      // |result| <= |source| + |target| + 3 (root header grows by <= 4, sub-headers / keys are
+      // re-encoded minimally so never grow): no size pass on the hot path.
       const uint32_t tref = P.rmeta[rscope].payload;
-      const uint8_t* tgt = payload_ptr(P.arena, tref, nt_);
-      Out o{nullptr, 0};
-      bool unsup = false;
-      if (!merge_docs(src, ns_, tgt, nt_, o, unsup)) { fail_at(t, DE_BAD_PAYLOAD, 5); return; }
-      if (unsup) { fail_at(t, DE_UNSUPPORTED, 6); return; }
+      const uint32_t ns_ = *(const uint32_t*)(P.arena + (uint64_t)rec.payload * 8);
+      const uint32_t nt_ = *(const uint32_t*)(P.arena + (uint64_t)tref * 8);
       if (t.merge) { fail_at(t, DE_UNSUPPORTED, 7); return; }
       t.merge = true;
-      t.m_src = rec.payload; t.m_tgt = tref; t.m_len = o.n;
-      t.m_bytes = blob_bytes(o.n);
+      t.m_src = rec.payload; t.m_tgt = tref; t.m_len = ns_ + nt_ + 8;
+      t.m_bytes = blob_bytes(t.m_len);
       t.bytes += t.m_bytes;
       t.merges += 1;
-      t.merge_bytes += ns_ + nt_ + o.n;
+      t.merge_bytes += ns_ + nt_;
       Slot& s = add_slot(t);
       s.d = rec;
       wf_event(t, s, WI_ELEMENT_COMPLETED, t.ns > 1);
@@ -528,10 +526,12 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
         const uint8_t* src = payload_ptr(P.arena, t.m_src, ns_);
         const uint8_t* tgt = payload_ptr(P.arena, t.m_tgt, nt_);
         uint8_t* dst = P.arena + bump;
-        *(uint32_t*)dst = t.m_len;
         Out o{dst + 4, 0};
         bool unsup = false;
-        merge_docs(src, ns_, tgt, nt_, o, unsup);
+        if (!merge_docs(src, ns_, tgt, nt_, o, unsup)) err |= DE_BAD_PAYLOAD;
+        else if (unsup || o.n > t.m_len) err |= DE_UNSUPPORTED;
+        *(uint32_t*)dst = o.n;
+        t.merge_bytes += o.n;
       }
       bump += t.m_bytes;
     }
