@@ -78,7 +78,7 @@ def main():
     recs_per_inst = 1 + (8 + 5 * a.tasks) + 3 * a.tasks  # CREATE + WF events + JOB CREATE/CREATED/COMPLETED
     eng = Engine(device=local_rank, partition_id=rank, partition_count=world,
                  log_capacity=int(n * (recs_per_inst + 2)), row_capacity=int(n * (a.tasks + 2)),
-                 arena_bytes=int(n * (48 + 32 * a.tasks)) + (64 << 20))
+                 arena_bytes=int(n * (48 + 48 * a.tasks)) + (64 << 20))
     xml = bpmn.chain_workflow(a.tasks).to_xml()
     eng.deploy(xml, 100, 1)
     for k in range(1, a.tasks + 1):

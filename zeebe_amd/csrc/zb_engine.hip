@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <string>
@@ -75,11 +76,16 @@ struct zb_engine {
   uint32_t* derr = nullptr;
   uint64_t* dstats = nullptr;
   uint64_t* derr_info = nullptr;
+  MergeJob* merge_jobs = nullptr;
+  uint64_t* cond_jobs = nullptr;
+  uint32_t* job_counts = nullptr;  // [0..1] merge counts, [2..3] cond counts
+  uint64_t job_cap = 0;
   WaveHdr* h_hdr_pinned = nullptr;  // pinned mirror for D2H polling
   uint32_t* h_err_pinned = nullptr;
 
   int64_t wave = 0;
   WaveHdr host_hdr{};
+  bool has_merges = false, has_splits = false;
   bool failed = false;
 
   // static arena region (ref 0 = {}, harness payloads)
@@ -168,6 +174,11 @@ WaveParams wave_params(zb_engine* e) {
   p.tickets = e->tickets;
   p.err = e->derr;
   p.err_info = e->derr_info;
+  p.merge_jobs = e->merge_jobs;
+  p.merge_count = e->job_counts;
+  p.cond_jobs = e->cond_jobs;
+  p.cond_count = e->job_counts + 2;
+  p.job_cap = e->job_cap;
   p.stats = e->dstats;
   p.log_cap = e->cfg.log_capacity;
   p.row_cap = e->cfg.row_capacity;
@@ -234,6 +245,10 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->derr, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->dstats, 8 * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->derr_info, sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  e->job_cap = std::min<uint64_t>(L, 1ull << 26);
+  if (hipMalloc(&e->merge_jobs, 2 * e->job_cap * sizeof(MergeJob)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->cond_jobs, 2 * e->job_cap * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->job_counts, 4 * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_hdr_pinned, 2 * sizeof(WaveHdr)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_err_pinned, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   e->ev.resize(2 * WAVES_PER_SYNC);
@@ -255,7 +270,7 @@ void zb_engine_destroy(zb_engine* e) {
   for (auto& x : e->ev)
     if (x) (void)hipEventDestroy(x);
   void* ps[] = {e->log, e->links, e->rmeta, e->rkeys, e->arena, e->hdr, e->status, e->tickets, e->derr, e->dstats,
-                e->derr_info};
+                e->derr_info, e->merge_jobs, e->cond_jobs, e->job_counts};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->h_hdr_pinned) (void)hipHostFree(e->h_hdr_pinned);
@@ -286,6 +301,7 @@ int zb_reset(zb_engine* e, int keep_staged) {
   HIPCHECK(e, hipMemsetAsync(e->tickets, 0, 128 * sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->derr, 0, sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->derr_info, 0xff, sizeof(uint64_t), e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->job_counts, 0, 4 * sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->dstats, 0, 8 * sizeof(uint64_t), e->stream));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
   e->ranges.clear();
@@ -305,6 +321,10 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
   std::string msg;
   int rc = compile_deployment(e->model, std::string((const char*)xml, len), workflow_key, version, msg);
   if (rc != ZB_OK) return fail(e, rc, msg);
+  for (const DevElem& el : e->model.elems) {
+    if (el.step[WI_ELEMENT_COMPLETING] == ST_APPLY_OUTPUT_MAPPING) e->has_merges = true;
+    if (el.step[WI_GATEWAY_ACTIVATED] == ST_EXCLUSIVE_SPLIT) e->has_splits = true;
+  }
   return upload_model(e);
 }
 
@@ -450,6 +470,9 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
       HIPCHECK(e, hipEventRecord(e->ev[2 * i], e->stream));
       launch_wave(p, grid, e->stream);
       HIPCHECK(e, hipEventRecord(e->ev[2 * i + 1], e->stream));
+      // payload kernels for this wave's deferred work (only when the model can produce any)
+      if (e->has_merges) launch_merge(p, e->stream);
+      if (e->has_splits) launch_cond(p, e->stream);
       e->wave++;
     }
     HIPCHECK(e, hipGetLastError());

@@ -6,6 +6,20 @@
 
 namespace zbg {
 
+// A deferred default output merge: k_wave reserves the result blob (upper-bound sized), k_merge fills it.
+struct MergeJob {
+  uint32_t dst;   // result blob ref (arena offset / 8)
+  uint32_t src;   // source (job / message payload) ref
+  uint32_t tgt;   // target (flow scope payload) ref
+  uint32_t cap;   // bytes reserved after the 4-byte length word
+};
+
+// k_cond decision word, stored in the row-self link of a GATEWAY_ACTIVATED record
+constexpr uint32_t COND_VALID = 1u << 31;
+constexpr uint32_t COND_INCIDENT = 1u << 30;
+constexpr uint32_t COND_UNSUPPORTED = 1u << 17;
+// flow: [15:0] chosen sequence flow elem; incident: [29:27] code [26:23] a [22:19] b [15:0] query
+
 struct WaveParams {
   zb_rec* log;
   uint64_t* links;        // per record: row_self | row_scope << 32
@@ -26,11 +40,18 @@ struct WaveParams {
   uint32_t* err;          // sticky DevErr flags
   uint64_t* err_info;     // min over failing records of (position << 8 | site)
   uint64_t* stats;        // [8] transitions, completed, created, merges, merge_bytes, cond_bytes, waves
+  MergeJob* merge_jobs;    // [2][job_cap], by wave parity
+  uint32_t* merge_count;   // [2]
+  uint64_t* cond_jobs;     // [2][job_cap] record indices of conditional GATEWAY_ACTIVATED records
+  uint32_t* cond_count;    // [2]
+  uint64_t job_cap;
   uint64_t log_cap, row_cap, arena_cap;
   int64_t wave;
 };
 
 void launch_wave(const WaveParams& p, int grid, hipStream_t stream);
+void launch_merge(const WaveParams& p, hipStream_t stream);
+void launch_cond(const WaveParams& p, hipStream_t stream);
 
 // submitted CREATE commands: one range per zb_submit_creates call (serialization of their values)
 struct CmdRange {

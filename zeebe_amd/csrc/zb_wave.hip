@@ -24,7 +24,9 @@
 namespace zbg {
 
 constexpr int WG = 256;
-constexpr int MAX_SLOTS = 4;
+constexpr int ITEMS = 2;           // records per thread per tile (item k of thread t = record k*WG + t)
+constexpr int TILE = WG * ITEMS;
+constexpr int MAX_SLOTS = 2;       // output records per item (one parent's batch emits <= 2 in every handler)
 
 enum SlotFlags : uint8_t {
   SF_KEY_WF = 1,       // key = new wf key #ord
@@ -34,6 +36,7 @@ enum SlotFlags : uint8_t {
   SF_ROW_INIT = 16,    // initialise that row as an ELEMENT_READY insert (ElementInstanceWriter.writeNewEvent)
   SF_PAY_MERGED = 32,  // payload = this thread's merge result
   SF_PAY_DETAIL = 64,  // payload = this thread's incident detail blob
+  SF_COND_JOB = 128,   // GATEWAY_ACTIVATED of a conditional split: k_cond evaluates it before the next wave
 };
 
 struct Slot {
@@ -114,7 +117,10 @@ __device__ void incident(TState& t, const zb_rec& rec, int64_t pos, uint8_t type
 __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, uint32_t rself, uint32_t rscope,
                           TState& t) {
   const uint8_t intent = rec.intent;
-  const bool self_alive = rself != NO_ROW && P.rmeta[rself].state != 0;
+  // stateless records (SFT/SEO/EEO/GA) never have an element instance; GA's link carries a decision
+  const bool stateless = intent == WI_SEQUENCE_FLOW_TAKEN || intent == WI_START_EVENT_OCCURRED ||
+                         intent == WI_END_EVENT_OCCURRED || intent == WI_GATEWAY_ACTIVATED;
+  const bool self_alive = !stateless && rself != NO_ROW && P.rmeta[rself].state != 0;
   const bool scope_alive = rscope != NO_ROW && P.rmeta[rscope].state != 0;
   if (!self_alive && !scope_alive) return;  // BpmnStepProcessor.java:244-247
   bool ok;
@@ -161,8 +167,6 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
       t.m_src = rec.payload; t.m_tgt = tref; t.m_len = ns_ + nt_ + 8;
       t.m_bytes = blob_bytes(t.m_len);
       t.bytes += t.m_bytes;
-      t.merges += 1;
-      t.merge_bytes += ns_ + nt_;
       Slot& s = add_slot(t);
       s.d = rec;
       wf_event(t, s, WI_ELEMENT_COMPLETED, t.ns > 1);
@@ -181,33 +185,19 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
       s.rself = rself; s.rscope = rscope;
       break;
     }
-    case ST_EXCLUSIVE_SPLIT: {  // ExclusiveSplitHandler :38-71
-      uint32_t n;
-      const uint8_t* doc = payload_ptr(P.arena, rec.payload, n);
-      uint16_t chosen = NO_ELEM;
-      CondOut co{0, 0, 0, 0};
-      bool unsup = false;
-      for (uint32_t i = 0; i < el.cond_count; i++) {
-        const uint16_t flow = P.cond_flows[el.cond_begin + i];
-        const bool r = eval_condition(P.elems[flow].cond_prog, P.code, doc, n, P.consts, P.queries, P.filters,
-                                      P.pool, co, unsup);
-        if (unsup) { fail_at(t, DE_UNSUPPORTED, 8); return; }
-        if (co.err) break;
-        if (r) { chosen = flow; break; }
-      }
-      t.cond_bytes += n;
-      if (co.err) {
-        incident(t, rec, pos, 3 /*CONDITION_ERROR*/, co.err, co.a, co.b, co.q);
-        break;
-      }
-      if (chosen == NO_ELEM) chosen = el.dflt;
-      if (chosen == NO_ELEM) {
-        incident(t, rec, pos, 3, EC_NO_FLOW, 0, 0, 0);
+    case ST_EXCLUSIVE_SPLIT: {  // ExclusiveSplitHandler :38-71, decision computed by k_cond (zb_aux.hip)
+      // the GATEWAY_ACTIVATED record is stateless, so its row-self link carries the decision
+      const uint32_t dec = rself;
+      if (!(dec & COND_VALID)) { fail_at(t, DE_PROCESSING, 20); return; }
+      if (dec & COND_UNSUPPORTED) { fail_at(t, DE_UNSUPPORTED, 21); return; }
+      if (dec & COND_INCIDENT) {
+        incident(t, rec, pos, 3 /*CONDITION_ERROR*/, (dec >> 27) & 7, (dec >> 23) & 15, (dec >> 19) & 15,
+                 (uint16_t)(dec & 0xffff));
         break;
       }
       Slot& s = add_slot(t);
       s.d = rec;
-      s.d.elem = chosen;
+      s.d.elem = (uint16_t)(dec & 0xffff);
       wf_event(t, s, WI_SEQUENCE_FLOW_TAKEN, t.ns > 1);
       s.flags |= SF_KEY_WF; s.ord = (uint8_t)t.nwf++;
       s.rself = NO_ROW; s.rscope = rscope;
@@ -385,14 +375,22 @@ __device__ __forceinline__ void publish(unsigned long long* st, int64_t tile, ui
 }
 
 // ------------------------------------------------------------------------------ the kernel
+struct ItemInfo {  // per (thread, item) write-phase inputs, staged in LDS (32 B)
+  uint32_t m_src, m_tgt, m_len, m_bytes;  // merge (m_bytes == 0: none)
+  int64_t d_pos;                          // incident detail
+  uint16_t d_q;
+  uint8_t d_type, d_code, d_a, d_b, has_detail, ns;
+};
+
 __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
-  __shared__ uint64_t s_a[WG / 64];     // packed rec|wf|job|row (16 bit each) wave totals
-  __shared__ uint64_t s_b[WG / 64];     // bytes wave totals
-  __shared__ Cnt s_excl;                // tile exclusive prefix
+  __shared__ uint64_t s_a[ITEMS][WG / 64];  // per-wave totals of packed rec|wf|job|row (16 bit each)
+  __shared__ uint64_t s_b[ITEMS][WG / 64];  // bytes
+  __shared__ Cnt s_excl;                    // tile exclusive prefix
   __shared__ int64_t s_tile;
   __shared__ uint32_t s_err;
   __shared__ uint32_t s_stats[6];
-  __shared__ Slot s_slots[WG * MAX_SLOTS];
+  __shared__ Slot s_slots[WG * ITEMS * MAX_SLOTS];
+  __shared__ ItemInfo s_info[WG * ITEMS];
 
   const WaveHdr* hin = P.hdr + (P.wave & 1);
   WaveHdr* hout = P.hdr + ((P.wave + 1) & 1);
@@ -401,15 +399,22 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t epoch = (uint32_t)(P.wave % 127) + 1;
 
-  if (blockIdx.x == 0 && threadIdx.x == 0) P.tickets[(P.wave + 1) & 127] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    P.tickets[(P.wave + 1) & 127] = 0;
+    // the other parity's job lists were consumed by the aux kernels of wave - 1 (stream order); clear
+    // them for wave + 1 (this wave's lists were cleared the same way by wave - 1 / zb_reset)
+    P.merge_count[(P.wave + 1) & 1] = 0;
+    P.cond_count[(P.wave + 1) & 1] = 0;
+  }
   if (n <= 0) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *hout = *hin;
     return;
   }
-  const int64_t ntiles = (n + WG - 1) / WG;
+  const int64_t ntiles = (n + TILE - 1) / TILE;
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd((unsigned long long*)&P.stats[6], 1ull);
   if (threadIdx.x < 6) s_stats[threadIdx.x] = 0;
   if (threadIdx.x == 0) s_err = 0;
+  uint32_t st_trans = 0, st_completed = 0, st_created = 0, st_merges = 0, st_mbytes = 0, st_cbytes = 0;
 
   for (;;) {
     if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(P.tickets + (P.wave & 127), 1u);
@@ -417,50 +422,78 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
     const int64_t tile = s_tile;
     if (tile >= ntiles) break;
 
-    // ---------------- 1. process
-    TState t;
-    t.s = s_slots + threadIdx.x * MAX_SLOTS;
-    t.ns = t.nwf = t.njob = t.nrow = 0;
-    t.bytes = 0; t.merge = false; t.detail = false; t.err = 0; t.err_site = 0;
-    t.transitions = t.completed = t.created = t.merges = 0;
-    t.merge_bytes = t.cond_bytes = 0;
-    const int64_t r = begin + tile * WG + threadIdx.x;
-    if (r < end) {
-      const zb_rec rec = P.log[r];
-      if (!kind_cont(rec.kind)) {
-        // a thread owns its record plus the continuation records that follow it (one parent's batch)
-        const uint64_t lk = P.links[r];
-        process_record(P, rec, r, (uint32_t)lk, (uint32_t)(lk >> 32), t);
-        for (int64_t q = r + 1; q < end && q < r + MAX_SLOTS; q++) {
-          const zb_rec rec2 = P.log[q];
-          if (!kind_cont(rec2.kind)) break;
-          const uint64_t lk2 = P.links[q];
-          process_record(P, rec2, q, (uint32_t)lk2, (uint32_t)(lk2 >> 32), t);
+    // ---------------- 1. process (item k of this thread = record tile*TILE + k*WG + tid)
+    uint64_t a[ITEMS], b[ITEMS];
+    uint32_t err = 0, err_site = 0;
+    int64_t err_pos = 0;
+#pragma unroll 1
+    for (int k = 0; k < ITEMS; k++) {
+      TState t;
+      t.s = s_slots + (threadIdx.x * ITEMS + k) * MAX_SLOTS;
+      t.ns = t.nwf = t.njob = t.nrow = 0;
+      t.bytes = 0; t.merge = false; t.detail = false; t.err = 0; t.err_site = 0;
+      t.transitions = t.completed = t.created = t.merges = 0;
+      t.merge_bytes = t.cond_bytes = 0;
+      const int64_t r = begin + tile * TILE + k * WG + threadIdx.x;
+      if (r < end) {
+        const zb_rec rec = P.log[r];
+        if (!kind_cont(rec.kind)) {
+          // a thread owns its record plus the continuation records that follow it (one parent's batch)
+          const uint64_t lk = P.links[r];
+          process_record(P, rec, r, (uint32_t)lk, (uint32_t)(lk >> 32), t);
+          for (int64_t q = r + 1; q < end && q < r + 4; q++) {
+            const zb_rec rec2 = P.log[q];
+            if (!kind_cont(rec2.kind)) break;
+            const uint64_t lk2 = P.links[q];
+            process_record(P, rec2, q, (uint32_t)lk2, (uint32_t)(lk2 >> 32), t);
+          }
         }
       }
+      ItemInfo inf;
+      inf.m_src = t.m_src; inf.m_tgt = t.m_tgt; inf.m_len = t.m_len; inf.m_bytes = t.merge ? t.m_bytes : 0;
+      inf.d_pos = t.d_pos; inf.d_q = t.d_q; inf.d_type = t.d_type; inf.d_code = t.d_code; inf.d_a = t.d_a;
+      inf.d_b = t.d_b; inf.has_detail = t.detail; inf.ns = (uint8_t)t.ns;
+      s_info[threadIdx.x * ITEMS + k] = inf;
+      a[k] = (uint64_t)t.ns | ((uint64_t)t.nwf << 16) | ((uint64_t)t.njob << 32) | ((uint64_t)t.nrow << 48);
+      b[k] = t.bytes;
+      if (t.err && !err) { err_site = t.err_site; err_pos = r; }
+      err |= t.err;
+      st_created += t.created; st_merges += t.merges; st_mbytes += t.merge_bytes; st_cbytes += t.cond_bytes;
+      st_completed += t.completed;
     }
 
-    // ---------------- 2. block scan of (rec, wf, job, row) packed 16-bit + bytes
-    uint64_t a = (uint64_t)t.ns | ((uint64_t)t.nwf << 16) | ((uint64_t)t.njob << 32) | ((uint64_t)t.nrow << 48);
-    uint64_t b = t.bytes;
-    uint64_t ia = a, ib = b;
+    // ---------------- 2. block scan, item-major order (all of item 0, then all of item 1)
+    uint64_t ea[ITEMS], eb[ITEMS];
+    uint64_t ta = 0, tb = 0;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      uint64_t ua = shfl_up64(ia, d), ub = shfl_up64(ib, d);
-      if (lane >= d) { ia += ua; ib += ub; }
+    for (int k = 0; k < ITEMS; k++) {
+      uint64_t ia = a[k], ib = b[k];
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        uint64_t ua = shfl_up64(ia, d), ub = shfl_up64(ib, d);
+        if (lane >= d) { ia += ua; ib += ub; }
+      }
+      if (lane == 63) { s_a[k][wv] = ia; s_b[k][wv] = ib; }
+      ea[k] = ia - a[k];
+      eb[k] = ib - b[k];
     }
-    if (lane == 63) { s_a[wv] = ia; s_b[wv] = ib; }
     __syncthreads();
-    uint64_t wa = 0, wb = 0, ta = 0, tb = 0;
 #pragma unroll
-    for (int w = 0; w < WG / 64; w++) {
-      if (w < wv) { wa += s_a[w]; wb += s_b[w]; }
-      ta += s_a[w]; tb += s_b[w];
+    for (int k = 0; k < ITEMS; k++) {
+      uint64_t wa = 0, wb = 0, ka = 0, kb = 0;
+#pragma unroll
+      for (int w = 0; w < WG / 64; w++) {
+        if (w < wv) { wa += s_a[k][w]; wb += s_b[k][w]; }
+        ka += s_a[k][w]; kb += s_b[k][w];
+      }
+      ea[k] += wa + ta;
+      eb[k] += wb + tb;
+      ta += ka;
+      tb += kb;
     }
-    const uint64_t ea = wa + ia - a, eb = wb + ib - b;  // thread-exclusive within the tile
     const Cnt agg{((ta & 0xffff) << 28) | ((ta >> 16) & 0xffff), (((ta >> 32) & 0xffff) << 28) | (ta >> 48), tb};
 
-    // ---------------- 3. decoupled look-back (wave 0)
+    // ---------------- 3. decoupled look-back (wave 0), 256 predecessors per round trip
     if (wv == 0) {
       Cnt excl{0, 0, 0};
       if (tile == 0) {
@@ -471,10 +504,14 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
         uint32_t spins = 0;
         bool timeout = false;
         for (;;) {
-          const int64_t idx = base - lane;
-          Cnt v{0, 0, 0};
-          int st = 2;
-          if (idx >= 0) {
+          Cnt v[4];
+          int first_local = 1 << 30;  // smallest window offset of a prefix this lane holds
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const int off = lane + 64 * j;
+            const int64_t idx = base - off;
+            v[j] = Cnt{0, 0, 0};
+            if (idx < 0) { if (off < first_local) first_local = off; continue; }
             for (;;) {
               unsigned long long* g = P.status + 3 * idx;
               unsigned long long g0 = __hip_atomic_load(g + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -482,24 +519,32 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
               unsigned long long g2 = __hip_atomic_load(g + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               uint32_t t0 = (uint32_t)(g0 >> 56), t1 = (uint32_t)(g1 >> 56), t2 = (uint32_t)(g2 >> 56);
               if (t0 == t1 && t1 == t2 && (t0 >> 1) == epoch) {
-                st = (t0 & 1) ? 2 : 1;
-                v = Cnt{g0 & F56, g1 & F56, g2 & F56};
+                v[j] = Cnt{g0 & F56, g1 & F56, g2 & F56};
+                if ((t0 & 1) && off < first_local) first_local = off;
                 break;
               }
-              if (++spins > (1u << 24)) { timeout = true; st = 2; break; }
+              if (++spins > (1u << 24)) { timeout = true; if (off < first_local) first_local = off; break; }
               __builtin_amdgcn_s_sleep(1);
             }
           }
-          const uint64_t pm = __ballot(st == 2);
-          const int first = pm ? __ffsll((unsigned long long)pm) - 1 : 64;
-          Cnt c = lane <= first ? v : Cnt{0, 0, 0};
+          // nearest predecessor holding an inclusive prefix (window offset), wave-wide minimum
+          int first = first_local;
+#pragma unroll
+          for (int d = 32; d >= 1; d >>= 1) {
+            int o = __shfl_xor(first, d, 64);
+            first = o < first ? o : first;
+          }
+          Cnt c{0, 0, 0};
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (lane + 64 * j <= first) c = cnt_add(c, v[j]);
 #pragma unroll
           for (int d = 32; d >= 1; d >>= 1) {
             c.a += shfl_xor64(c.a, d); c.b += shfl_xor64(c.b, d); c.c += shfl_xor64(c.c, d);
           }
           excl = cnt_add(excl, c);
-          if (pm) break;
-          base -= 64;
+          if (first < 256) break;
+          base -= 256;
         }
         if (__any(timeout) && lane == 0) atomicOr(&s_err, (uint32_t)DE_LOOKBACK_TIMEOUT);
         if (lane == 0) publish(P.status, tile, (epoch << 1) | 1, cnt_add(excl, agg));
@@ -510,85 +555,79 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
     const Cnt ex = s_excl;
 
     // ---------------- 4. write
-    uint64_t out_rec = (uint64_t)end + (ex.a >> 28) + (ea & 0xffff);
-    const uint64_t wf0 = (ex.a & F28) + ((ea >> 16) & 0xffff);
-    const uint64_t job0 = (ex.b >> 28) + ((ea >> 32) & 0xffff);
-    const uint64_t row0 = (uint64_t)hin->rows_next + (ex.b & F28) + (ea >> 48);
-    const uint64_t byte0 = (uint64_t)hin->arena_next + ex.c + eb;
-    uint32_t err = t.err;
-    uint64_t bump = byte0;
-    uint32_t merged_ref = 0, detail_ref = 0;
-    if (t.merge) {
-      if (bump + t.m_bytes > P.arena_cap) err |= DE_ARENA_FULL;
-      else {
-        merged_ref = (uint32_t)(bump >> 3);
-        uint32_t ns_, nt_;
-        const uint8_t* src = payload_ptr(P.arena, t.m_src, ns_);
-        const uint8_t* tgt = payload_ptr(P.arena, t.m_tgt, nt_);
-        uint8_t* dst = P.arena + bump;
-        Out o{dst + 4, 0};
-        bool unsup = false;
-        if (!merge_docs(src, ns_, tgt, nt_, o, unsup)) err |= DE_BAD_PAYLOAD;
-        else if (unsup || o.n > t.m_len) err |= DE_UNSUPPORTED;
-        *(uint32_t*)dst = o.n;
-        t.merge_bytes += o.n;
-      }
-      bump += t.m_bytes;
-    }
-    if (t.detail) {
-      if (bump + 24 > P.arena_cap) err |= DE_ARENA_FULL;
-      else {
-        detail_ref = (uint32_t)(bump >> 3);
-        uint8_t* dst = P.arena + bump;
-        *(uint32_t*)dst = 16;
-        dst[4] = t.d_type; dst[5] = t.d_code; dst[6] = t.d_a; dst[7] = t.d_b;
-        *(uint16_t*)(dst + 8) = t.d_q;
-        *(int64_t*)(dst + 16) = t.d_pos;
-      }
-      bump += 24;
-    }
-    for (int i = 0; i < t.ns; i++) {
-      Slot s = t.s[i];
-      if (s.flags & SF_KEY_WF) s.d.key = hin->wf_next + 5 * (int64_t)(wf0 + s.ord);
-      if (s.flags & SF_KEY_JOB) s.d.key = hin->job_next + 5 * (int64_t)(job0 + s.ord);
-      if (s.flags & SF_INST_WF) s.d.inst_key = hin->wf_next + 5 * (int64_t)(wf0 + s.ord);
-      if (s.flags & SF_PAY_MERGED) s.d.payload = merged_ref;
-      if (s.flags & SF_PAY_DETAIL) s.d.payload = detail_ref;
-      if (s.flags & SF_ROW_NEW) {
-        const uint64_t row = row0 + s.rord;
-        if (row >= P.row_cap) { err |= DE_ROWS_FULL; s.rself = NO_ROW; }
+#pragma unroll 1
+    for (int k = 0; k < ITEMS; k++) {
+      const ItemInfo inf = s_info[threadIdx.x * ITEMS + k];
+      uint64_t out_rec = (uint64_t)end + (ex.a >> 28) + (ea[k] & 0xffff);
+      const uint64_t wf0 = (ex.a & F28) + ((ea[k] >> 16) & 0xffff);
+      const uint64_t job0 = (ex.b >> 28) + ((ea[k] >> 32) & 0xffff);
+      const uint64_t row0 = (uint64_t)hin->rows_next + (ex.b & F28) + (ea[k] >> 48);
+      uint64_t bump = (uint64_t)hin->arena_next + ex.c + eb[k];
+      uint32_t merged_ref = 0, detail_ref = 0;
+      if (inf.m_bytes) {
+        // reserve the blob; k_merge (zb_aux.hip) fills it before the next wave reads any payload
+        if (bump + inf.m_bytes > P.arena_cap) err |= DE_ARENA_FULL;
         else {
-          s.rself = (uint32_t)row;
-          if (s.flags & SF_ROW_INIT) {
-            RowMeta m;
-            m.payload = s.d.payload; m.parent = s.rscope; m.elem = s.d.elem; m.state = WI_ELEMENT_READY;
-            m.flags = 0; m.nchild = 0;
-            P.rmeta[row] = m;
-            P.rkeys[row] = RowKeys{s.d.key, s.d.scope_key, s.d.inst_key, 0};
+          merged_ref = (uint32_t)(bump >> 3);
+          const uint32_t j = atomicAdd(P.merge_count + (P.wave & 1), 1u);
+          if (j >= P.job_cap) err |= DE_LOG_FULL;
+          else P.merge_jobs[(uint64_t)(P.wave & 1) * P.job_cap + j] = MergeJob{merged_ref, inf.m_src, inf.m_tgt, inf.m_len};
+        }
+        bump += inf.m_bytes;
+      }
+      if (inf.has_detail) {
+        if (bump + 24 > P.arena_cap) err |= DE_ARENA_FULL;
+        else {
+          detail_ref = (uint32_t)(bump >> 3);
+          uint8_t* dst = P.arena + bump;
+          *(uint32_t*)dst = 16;
+          dst[4] = inf.d_type; dst[5] = inf.d_code; dst[6] = inf.d_a; dst[7] = inf.d_b;
+          *(uint16_t*)(dst + 8) = inf.d_q;
+          *(int64_t*)(dst + 16) = inf.d_pos;
+        }
+        bump += 24;
+      }
+      const Slot* sl = s_slots + (threadIdx.x * ITEMS + k) * MAX_SLOTS;
+      for (int i = 0; i < inf.ns; i++) {
+        Slot s = sl[i];
+        if (s.flags & SF_KEY_WF) s.d.key = hin->wf_next + 5 * (int64_t)(wf0 + s.ord);
+        if (s.flags & SF_KEY_JOB) s.d.key = hin->job_next + 5 * (int64_t)(job0 + s.ord);
+        if (s.flags & SF_INST_WF) s.d.inst_key = hin->wf_next + 5 * (int64_t)(wf0 + s.ord);
+        if (s.flags & SF_PAY_MERGED) s.d.payload = merged_ref;
+        if (s.flags & SF_PAY_DETAIL) s.d.payload = detail_ref;
+        if (s.flags & SF_ROW_NEW) {
+          const uint64_t row = row0 + s.rord;
+          if (row >= P.row_cap) { err |= DE_ROWS_FULL; s.rself = NO_ROW; }
+          else {
+            s.rself = (uint32_t)row;
+            if (s.flags & SF_ROW_INIT) {
+              RowMeta m;
+              m.payload = s.d.payload; m.parent = s.rscope; m.elem = s.d.elem; m.state = WI_ELEMENT_READY;
+              m.flags = 0; m.nchild = 0;
+              P.rmeta[row] = m;
+              P.rkeys[row] = RowKeys{s.d.key, s.d.scope_key, s.d.inst_key, 0};
+            }
           }
         }
+        if (kind_vt(s.d.kind) == ZB_VT_WORKFLOW_INSTANCE && kind_rt(s.d.kind) == ZB_RT_EVENT) st_trans++;
+        if (out_rec >= P.log_cap) { err |= DE_LOG_FULL; }
+        else {
+          P.log[out_rec] = s.d;
+          P.links[out_rec] = (uint64_t)s.rself | ((uint64_t)s.rscope << 32);
+          if (s.flags & SF_COND_JOB) {
+            const uint32_t j = atomicAdd(P.cond_count + (P.wave & 1), 1u);
+            if (j >= P.job_cap) err |= DE_LOG_FULL;
+            else P.cond_jobs[(uint64_t)(P.wave & 1) * P.job_cap + j] = out_rec;
+          }
+        }
+        out_rec++;
       }
-      if (kind_vt(s.d.kind) == ZB_VT_WORKFLOW_INSTANCE && kind_rt(s.d.kind) == ZB_RT_EVENT) t.transitions++;
-      if (out_rec >= P.log_cap) { err |= DE_LOG_FULL; }
-      else {
-        P.log[out_rec] = s.d;
-        P.links[out_rec] = (uint64_t)s.rself | ((uint64_t)s.rscope << 32);
-      }
-      out_rec++;
     }
-
-    // ---------------- stats + header
     if (err) {
       atomicOr(&s_err, err);
       // first failing record (lowest position) and the code site that flagged it
-      atomicMin((unsigned long long*)P.err_info, ((unsigned long long)r << 8) | (t.err_site & 0xff));
+      atomicMin((unsigned long long*)P.err_info, ((unsigned long long)err_pos << 8) | (err_site & 0xff));
     }
-    if (t.transitions) atomicAdd(&s_stats[0], t.transitions);
-    if (t.completed) atomicAdd(&s_stats[1], t.completed);
-    if (t.created) atomicAdd(&s_stats[2], t.created);
-    if (t.merges) atomicAdd(&s_stats[3], t.merges);
-    if (t.merge_bytes) atomicAdd(&s_stats[4], t.merge_bytes);
-    if (t.cond_bytes) atomicAdd(&s_stats[5], t.cond_bytes);
     if (tile == ntiles - 1 && threadIdx.x == 0) {
       const Cnt tot = cnt_add(ex, agg);
       WaveHdr h = *hin;
@@ -602,7 +641,14 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
     }
     __syncthreads();
   }
-  // block-level stats -> device counters (one atomic per block per counter)
+  // stats: block reduce -> one atomic per block per counter
+  if (st_trans) atomicAdd(&s_stats[0], st_trans);
+  if (st_completed) atomicAdd(&s_stats[1], st_completed);
+  if (st_created) atomicAdd(&s_stats[2], st_created);
+  if (st_merges) atomicAdd(&s_stats[3], st_merges);
+  if (st_mbytes) atomicAdd(&s_stats[4], st_mbytes);
+  if (st_cbytes) atomicAdd(&s_stats[5], st_cbytes);
+  __syncthreads();
   if (threadIdx.x == 0) {
     if (s_err) atomicOr(P.err, s_err);
     for (int i = 0; i < 6; i++)
