@@ -6,6 +6,7 @@
 #define __device__
 #define __host__
 #define __forceinline__ inline
+#define __noinline__ __attribute__((noinline))
 #define __global__
 static inline float __uint_as_float(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 static inline double __longlong_as_double(long long u) { double d; std::memcpy(&d, &u, 8); return d; }
