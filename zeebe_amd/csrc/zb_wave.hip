@@ -231,6 +231,8 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
       if (s.d.elem == NO_ELEM) { fail_at(t, DE_PROCESSING, 10); return; }
       wf_event(t, s, out_intent, t.ns > 1);
       s.flags |= SF_KEY_WF; s.ord = (uint8_t)t.nwf++;
+      if (step == ST_ACTIVATE_GATEWAY && P.elems[s.d.elem].step[WI_GATEWAY_ACTIVATED] == ST_EXCLUSIVE_SPLIT)
+        s.flags |= SF_COND_JOB;
       s.rself = NO_ROW; s.rscope = rscope;
       break;
     }
