@@ -56,7 +56,7 @@ typedef struct zb_config {
   uint64_t log_capacity;    /* max records in the device log (32 B descriptor + 8 B row links each) */
   uint64_t row_capacity;    /* max element-instance rows (SoA state, 64 B each) */
   uint64_t arena_bytes;     /* payload arena (msgpack documents, 8-byte aligned blobs) */
-  uint64_t staging_records; /* max records staged by zb_submit_* between steps */
+  uint64_t wave_records;    /* max records processed per wave (chunk of a generation); 0 = min(log_capacity, 2^22) */
 } zb_config;
 
 /* The 32-byte record descriptor kept in HBM for every record of the log. */
@@ -94,8 +94,11 @@ typedef struct zb_step_stats {
   uint64_t merges;             /* default output merges performed */
   uint64_t merge_bytes;        /* sum of (job + scope + result) payload bytes of those merges */
   uint64_t condition_payload_bytes; /* payload bytes read by exclusive-gateway evaluations */
-  double wave_kernel_ms;       /* sum of per-launch wave kernel durations (HIP events on the engine stream) */
+  double wave_kernel_ms;       /* device time of all wave kernels (HIP events on the engine stream) */
   double wall_ms;              /* host wall time of the zb_step call */
+  double process_kernel_ms;    /* k_process share of wave_kernel_ms */
+  double emit_kernel_ms;       /* k_scan + k_emit share */
+  double aux_kernel_ms;        /* k_merge + k_cond share */
 } zb_step_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------- */

@@ -134,20 +134,21 @@ enum ErrCode : uint8_t {
 // device error flags (sticky, host checks after each batch of waves)
 enum DevErr : uint32_t {
   DE_LOG_FULL = 1u, DE_ROWS_FULL = 2u, DE_ARENA_FULL = 4u, DE_UNSUPPORTED = 8u, DE_PROCESSING = 16u,
-  DE_LOOKBACK_TIMEOUT = 32u, DE_BAD_PAYLOAD = 64u
+  DE_BAD_PAYLOAD = 64u
 };
 
-// Per-wave header (double buffered: wave w reads hdr[w&1], writes hdr[(w+1)&1])
+// Per-wave header (double buffered: wave w reads hdr[w&1], k_scan of wave w writes hdr[(w+1)&1]).
+// A wave processes the chunk [begin, min(gen_end, begin + wave_cap)) of the current breadth-first
+// generation [begin, gen_end) and appends its follow-ups at the log tail `end`. Processing a
+// generation in chunks is still FIFO order: every follow-up lands after the whole generation.
 struct WaveHdr {
-  int64_t begin, end;          // input range in the log
+  int64_t begin;               // first unprocessed record
+  int64_t end;                 // log tail (records [0, end) exist)
+  int64_t gen_end;             // end of the generation being processed (begin <= gen_end <= end)
   int64_t wf_next, job_next;   // key generators (next key)
   int64_t rows_next;           // row allocator
   int64_t arena_next;          // payload arena bump pointer (bytes)
-  int64_t transitions;         // cumulative WF events written
-  int64_t completed;           // cumulative process-level ELEMENT_COMPLETED
-  int64_t created;             // cumulative CREATED processed
-  int64_t merges, merge_bytes, cond_bytes;
-  int64_t pad[4];
+  int64_t pad[9];
 };
 static_assert(sizeof(WaveHdr) == 128, "WaveHdr is 128 bytes");
 

@@ -22,6 +22,7 @@ using namespace zbg;
 namespace {
 
 constexpr int WAVES_PER_SYNC = 16;
+constexpr int EV_PER_WAVE = 4;  // before k_process, after k_process, after k_emit, after the aux kernels
 constexpr uint64_t STATIC_ARENA_BYTES = 1ull << 20;  // {} at ref 0 + harness job completion payloads
 
 template <class T>
@@ -70,11 +71,15 @@ struct zb_engine {
   RowKeys* rkeys = nullptr;
   uint8_t* arena = nullptr;
   WaveHdr* hdr = nullptr;
-  unsigned long long* status = nullptr;
-  uint64_t status_tiles = 0;
-  uint32_t* tickets = nullptr;
   uint32_t* derr = nullptr;
   uint64_t* dstats = nullptr;
+  // wave staging (k_process -> k_scan -> k_emit), wave_cap records
+  uint64_t wave_cap = 0;
+  uint64_t* cw = nullptr;
+  Slot* stage = nullptr;
+  ItemInfo* info = nullptr;
+  BlockAgg* block_agg = nullptr;
+  BlockOff* block_off = nullptr;
   uint64_t* derr_info = nullptr;
   MergeJob* merge_jobs = nullptr;
   uint64_t* cond_jobs = nullptr;
@@ -170,8 +175,12 @@ WaveParams wave_params(zb_engine* e) {
   p.filters = e->d_filters.p;
   p.pool = e->d_pool.p;
   p.hdr = e->hdr;
-  p.status = e->status;
-  p.tickets = e->tickets;
+  p.cw = e->cw;
+  p.stage = e->stage;
+  p.info = e->info;
+  p.block_agg = e->block_agg;
+  p.block_off = e->block_off;
+  p.wave_cap = e->wave_cap;
   p.err = e->derr;
   p.err_info = e->derr_info;
   p.merge_jobs = e->merge_jobs;
@@ -196,7 +205,6 @@ int check_device_errors(zb_engine* e, uint32_t flags) {
   if (flags & DE_ARENA_FULL) m += " arena-capacity";
   if (flags & DE_UNSUPPORTED) m += " unsupported-shape";
   if (flags & DE_PROCESSING) m += " processing-failure";
-  if (flags & DE_LOOKBACK_TIMEOUT) m += " lookback-timeout";
   if (flags & DE_BAD_PAYLOAD) m += " malformed-payload";
   uint64_t info = ~0ull;
   if (hipMemcpy(&info, e->derr_info, sizeof(info), hipMemcpyDeviceToHost) == hipSuccess && info != ~0ull)
@@ -233,15 +241,19 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipSetDevice(cfg->device) != hipSuccess) return cleanup(ZB_EDEVICE);
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return cleanup(ZB_EDEVICE);
   const uint64_t L = e->cfg.log_capacity;
-  e->status_tiles = (L + 255) / 256 + 1;
+  e->wave_cap = e->cfg.wave_records ? e->cfg.wave_records : std::min<uint64_t>(L, 1ull << 22);
+  e->wave_cap = (e->wave_cap + WAVE_TILE - 1) / WAVE_TILE * WAVE_TILE;
   if (hipMalloc(&e->log, L * sizeof(zb_rec)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->links, L * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->rmeta, e->cfg.row_capacity * sizeof(RowMeta)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->rkeys, e->cfg.row_capacity * sizeof(RowKeys)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->arena, e->cfg.arena_bytes) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->hdr, 2 * sizeof(WaveHdr)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipMalloc(&e->status, e->status_tiles * 3 * sizeof(unsigned long long)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipMalloc(&e->tickets, 128 * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->cw, e->wave_cap * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->stage, e->wave_cap * 2 * sizeof(Slot)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->info, e->wave_cap * sizeof(ItemInfo)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->block_agg, WAVE_GRID * sizeof(BlockAgg)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->block_off, WAVE_GRID * sizeof(BlockOff)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->derr, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->dstats, 8 * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->derr_info, sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
@@ -251,7 +263,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->job_counts, 4 * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_hdr_pinned, 2 * sizeof(WaveHdr)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_err_pinned, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  e->ev.resize(2 * WAVES_PER_SYNC);
+  e->ev.resize(EV_PER_WAVE * WAVES_PER_SYNC);
   for (auto& x : e->ev)
     if (hipEventCreate(&x) != hipSuccess) return cleanup(ZB_EDEVICE);
   const uint8_t empty = 0x80;
@@ -269,8 +281,8 @@ void zb_engine_destroy(zb_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (auto& x : e->ev)
     if (x) (void)hipEventDestroy(x);
-  void* ps[] = {e->log, e->links, e->rmeta, e->rkeys, e->arena, e->hdr, e->status, e->tickets, e->derr, e->dstats,
-                e->derr_info, e->merge_jobs, e->cond_jobs, e->job_counts};
+  void* ps[] = {e->log, e->links, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
+                e->merge_jobs, e->cond_jobs, e->job_counts, e->cw, e->stage, e->info, e->block_agg, e->block_off};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->h_hdr_pinned) (void)hipHostFree(e->h_hdr_pinned);
@@ -290,15 +302,13 @@ int zb_reset(zb_engine* e, int keep_staged) {
   e->wave = 0;
   e->failed = false;
   WaveHdr h{};
-  h.begin = h.end = 0;
+  h.begin = h.end = h.gen_end = 0;
   h.wf_next = 1;   // KeyGenerator.createWorkflowInstanceKeyGenerator: (1, 5)
   h.job_next = 2;  // KeyGenerator.createJobKeyGenerator: (2, 5)
   h.rows_next = 0;
   h.arena_next = (int64_t)STATIC_ARENA_BYTES;
   e->host_hdr = h;
   HIPCHECK(e, hipMemcpyAsync(e->hdr, &h, sizeof(h), hipMemcpyHostToDevice, e->stream));
-  HIPCHECK(e, hipMemsetAsync(e->status, 0, e->status_tiles * 3 * sizeof(unsigned long long), e->stream));
-  HIPCHECK(e, hipMemsetAsync(e->tickets, 0, 128 * sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->derr, 0, sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->derr_info, 0xff, sizeof(uint64_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->job_counts, 0, 4 * sizeof(uint32_t), e->stream));
@@ -446,6 +456,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
       r.pid_len = pr.pid_len;
       e->ranges.push_back(r);
     }
+    if (e->host_hdr.begin == e->host_hdr.gen_end) e->host_hdr.gen_end = e->host_hdr.end + n;
     e->host_hdr.end += n;
     e->host_hdr.arena_next += (int64_t)e->staged_arena.size();
     HIPCHECK(e, hipMemcpyAsync(e->hdr + (e->wave & 1), &e->host_hdr, sizeof(WaveHdr), hipMemcpyHostToDevice,
@@ -455,24 +466,24 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   const int64_t written_from = e->host_hdr.end;
   uint64_t stats_before[8];
   HIPCHECK(e, hipMemcpy(stats_before, e->dstats, sizeof(stats_before), hipMemcpyDeviceToHost));
-  const int grid = 2048;
   uint32_t launched = 0;
   bool quiescent = e->host_hdr.begin == e->host_hdr.end;
   while (!quiescent && (max_waves == 0 || launched < max_waves)) {
     int batch = WAVES_PER_SYNC;
     if (max_waves) batch = std::min<int>(batch, (int)(max_waves - launched));
     for (int i = 0; i < batch; i++) {
-      if (e->wave % 127 == 0 && e->wave > 0) {
-        // tile-status epochs wrap every 127 waves: clear stale granules (stream ordered)
-        HIPCHECK(e, hipMemsetAsync(e->status, 0, e->status_tiles * 3 * sizeof(unsigned long long), e->stream));
-      }
       WaveParams p = wave_params(e);
-      HIPCHECK(e, hipEventRecord(e->ev[2 * i], e->stream));
-      launch_wave(p, grid, e->stream);
-      HIPCHECK(e, hipEventRecord(e->ev[2 * i + 1], e->stream));
+      hipEvent_t* ev = &e->ev[EV_PER_WAVE * i];
+      HIPCHECK(e, hipEventRecord(ev[0], e->stream));
+      launch_process(p, e->stream);
+      HIPCHECK(e, hipEventRecord(ev[1], e->stream));
+      launch_scan(p, e->stream);
+      launch_emit(p, e->stream);
+      HIPCHECK(e, hipEventRecord(ev[2], e->stream));
       // payload kernels for this wave's deferred work (only when the model can produce any)
       if (e->has_merges) launch_merge(p, e->stream);
       if (e->has_splits) launch_cond(p, e->stream);
+      HIPCHECK(e, hipEventRecord(ev[3], e->stream));
       e->wave++;
     }
     HIPCHECK(e, hipGetLastError());
@@ -481,9 +492,15 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     HIPCHECK(e, hipMemcpyAsync(e->h_err_pinned, e->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHECK(e, hipStreamSynchronize(e->stream));
     for (int i = 0; i < batch; i++) {
-      float ms = 0;
-      HIPCHECK(e, hipEventElapsedTime(&ms, e->ev[2 * i], e->ev[2 * i + 1]));
-      st.wave_kernel_ms += ms;
+      const hipEvent_t* ev = &e->ev[EV_PER_WAVE * i];
+      float ms0 = 0, ms1 = 0, ms2 = 0;
+      HIPCHECK(e, hipEventElapsedTime(&ms0, ev[0], ev[1]));
+      HIPCHECK(e, hipEventElapsedTime(&ms1, ev[1], ev[2]));
+      HIPCHECK(e, hipEventElapsedTime(&ms2, ev[2], ev[3]));
+      st.process_kernel_ms += ms0;
+      st.emit_kernel_ms += ms1;
+      st.aux_kernel_ms += ms2;
+      st.wave_kernel_ms += ms0 + ms1 + ms2;
     }
     launched += batch;
     st.launches += batch;

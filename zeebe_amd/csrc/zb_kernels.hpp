@@ -20,6 +20,45 @@ constexpr uint32_t COND_INCIDENT = 1u << 30;
 constexpr uint32_t COND_UNSUPPORTED = 1u << 17;
 // flow: [15:0] chosen sequence flow elem; incident: [29:27] code [26:23] a [22:19] b [15:0] query
 
+constexpr int WAVE_TILE = 256;   // records per tile (one per thread of a 256-thread workgroup)
+constexpr int WAVE_GRID = 1024;  // workgroups of k_process / k_emit; workgroup b owns tiles [b*T/G, (b+1)*T/G)
+
+// One staged output record of k_process (48 B): descriptor + row links + what k_emit fills in.
+struct Slot {
+  zb_rec d;
+  uint32_t rself, rscope;
+  uint8_t flags, ord, rord, pad;
+  uint32_t pad2;
+};
+static_assert(sizeof(Slot) == 48, "Slot is 48 bytes");
+
+// Per-record side information of k_process, written only when a merge or an incident detail exists.
+struct ItemInfo {
+  uint32_t m_src, m_tgt, m_len, m_bytes;  // merge (m_bytes == 0: none)
+  int64_t d_pos;                          // incident detail
+  uint16_t d_q;
+  uint8_t d_type, d_code, d_a, d_b, has_detail, ns;
+};
+static_assert(sizeof(ItemInfo) == 32, "ItemInfo is 32 bytes");
+
+// Per-workgroup totals of k_process (each workgroup owns one contiguous range of 256-record tiles,
+// the same range in k_emit), and their exclusive prefix computed by k_scan.
+struct BlockAgg {
+  uint64_t bytes;
+  uint32_t rec, wf, job, row, merges, conds;
+  uint32_t transitions, completed, created, pad;
+};
+static_assert(sizeof(BlockAgg) == 48, "BlockAgg is 48 bytes");
+struct BlockOff {
+  uint64_t rec, wf, job, row, bytes;
+  uint32_t merges, conds;
+};
+static_assert(sizeof(BlockOff) == 48, "BlockOff is 48 bytes");
+
+// Count word of one record (k_process -> k_emit): bits [0,3) outputs, [3,6) wf keys, [6,9) job keys,
+// [9,12) new rows, 12 merge, 13 incident detail, [14,17) condition jobs, [32,64) arena bytes.
+constexpr int CW_NWF = 3, CW_NJOB = 6, CW_NROW = 9, CW_MERGE = 12, CW_DETAIL = 13, CW_NCOND = 14;
+
 struct WaveParams {
   zb_rec* log;
   uint64_t* links;        // per record: row_self | row_scope << 32
@@ -34,22 +73,29 @@ struct WaveParams {
   const DevQuery* queries;
   const DevFilter* filters;
   const uint8_t* pool;
-  WaveHdr* hdr;           // [2], double buffered
-  unsigned long long* status;  // 3 granules per tile
-  uint32_t* tickets;      // [128]
-  uint32_t* err;          // sticky DevErr flags
-  uint64_t* err_info;     // min over failing records of (position << 8 | site)
-  uint64_t* stats;        // [8] transitions, completed, created, merges, merge_bytes, cond_bytes, waves
+  WaveHdr* hdr;            // [2], double buffered
+  uint32_t* err;           // sticky DevErr flags
+  uint64_t* err_info;      // min over failing records of (position << 8 | site)
+  uint64_t* stats;         // [8] transitions, completed, created, merges, merge_bytes, cond_bytes, waves
+  // wave staging (indexed by record - begin; wave_cap records)
+  uint64_t* cw;            // count words
+  Slot* stage;             // [wave_cap][2] output slots
+  ItemInfo* info;          // [wave_cap] side info (sparse)
+  BlockAgg* block_agg;     // [WAVE_GRID]
+  BlockOff* block_off;     // [WAVE_GRID]
   MergeJob* merge_jobs;    // [2][job_cap], by wave parity
   uint32_t* merge_count;   // [2]
   uint64_t* cond_jobs;     // [2][job_cap] record indices of conditional GATEWAY_ACTIVATED records
   uint32_t* cond_count;    // [2]
   uint64_t job_cap;
-  uint64_t log_cap, row_cap, arena_cap;
+  uint64_t log_cap, row_cap, arena_cap, wave_cap;
   int64_t wave;
 };
 
-void launch_wave(const WaveParams& p, int grid, hipStream_t stream);
+
+void launch_process(const WaveParams& p, hipStream_t stream);
+void launch_scan(const WaveParams& p, hipStream_t stream);
+void launch_emit(const WaveParams& p, hipStream_t stream);
 void launch_merge(const WaveParams& p, hipStream_t stream);
 void launch_cond(const WaveParams& p, hipStream_t stream);
 

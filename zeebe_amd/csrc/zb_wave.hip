@@ -1,21 +1,19 @@
-// zb_wave.hip — the lockstep wave kernel (one launch per breadth-first generation of the log).
+// zb_wave.hip — one breadth-first generation (or a chunk of one) of the log per wave, as three
+// launches with no inter-workgroup waiting anywhere:
 //
-// One launch processes every record of generation g (log[begin, end)) and appends generation g+1
-// at the log tail in exact reference log order: a record's follow-ups are contiguous and ordered
-// by emission index, and records of generation g+1 are ordered by their parent's position
-// (FIFO log processing == breadth-first waves). Keys come from an exclusive prefix
-// sum of per-record "new key" counts in that order (KeyGenerator(1,5) / job KeyGenerator(2,5)).
+//   k_process  per record: decode descriptor, guards (BpmnStepProcessor.java:128-150), step handler
+//              (BpmnStepProcessor.java:92-125 -> handlers); index mutations of existing rows; the
+//              follow-up records go to a staging slot pair, their counts (records, wf keys, job keys,
+//              new rows, arena bytes, merge / condition jobs) to a count word, and the workgroup's
+//              totals to block_agg (workgroup b owns one contiguous range of 256-record tiles).
+//   k_scan     one workgroup: exclusive prefix of the workgroup totals, the next wave header, counters.
+//   k_emit     per record: tile scan of the count words + the running workgroup prefix gives each follow-up its
+//              log position, keys (KeyGenerator(1,5) / job KeyGenerator(2,5) ordinals), new rows
+//              (ElementInstanceWriter.writeNewEvent inserts), reserved arena blobs and job-list entries.
 //
-// Structure (per workgroup of 256 threads, one record per thread, tiles claimed by a ticket):
-//   1. process: decode descriptor, guards (BpmnStepProcessor.java:128-150), step handler
-//      (BpmnStepProcessor.java:92-125 -> handlers) -> up to 4 output slots in registers, plus
-//      counts (records, wf keys, job keys, rows, arena bytes); index mutations of existing rows
-//   2. block scan of the 5 counts (wave64 shuffles + LDS)
-//   3. decoupled look-back over predecessor tiles (8-byte {tag,value} granules, agent-scope
-//      relaxed atomics: the granule IS the flag — cdna_hip_programming.md §6 G16 recipe R2)
-//   4. write: keys, new rows (READY inserts), merged payloads, descriptors + row links
-// The tile ticket makes every awaited predecessor a tile that a resident workgroup already owns,
-// so the look-back cannot deadlock whatever the dispatch order.
+// Follow-ups of a record are contiguous and ordered by emission index; follow-ups of the chunk are
+// ordered by their parent's position (FIFO log processing == breadth-first waves), so the
+// log, keys and rows come out exactly as the reference's sequential processor writes them.
 #include <hip/hip_runtime.h>
 
 #include "zb_devlib.hpp"
@@ -23,10 +21,8 @@
 
 namespace zbg {
 
-constexpr int WG = 256;
-constexpr int ITEMS = 2;           // records per thread per tile (item k of thread t = record k*WG + t)
-constexpr int TILE = WG * ITEMS;
-constexpr int MAX_SLOTS = 2;       // output records per item (one parent's batch emits <= 2 in every handler)
+constexpr int WG = WAVE_TILE;
+constexpr int MAX_SLOTS = 2;  // output records per item (one parent's batch emits <= 2 in every handler)
 
 enum SlotFlags : uint8_t {
   SF_KEY_WF = 1,       // key = new wf key #ord
@@ -34,15 +30,9 @@ enum SlotFlags : uint8_t {
   SF_INST_WF = 4,      // inst_key = new wf key #ord (CREATE)
   SF_ROW_NEW = 8,      // row_self = new row #rord
   SF_ROW_INIT = 16,    // initialise that row as an ELEMENT_READY insert (ElementInstanceWriter.writeNewEvent)
-  SF_PAY_MERGED = 32,  // payload = this thread's merge result
-  SF_PAY_DETAIL = 64,  // payload = this thread's incident detail blob
+  SF_PAY_MERGED = 32,  // payload = this item's merge result
+  SF_PAY_DETAIL = 64,  // payload = this item's incident detail blob
   SF_COND_JOB = 128,   // GATEWAY_ACTIVATED of a conditional split: k_cond evaluates it before the next wave
-};
-
-struct Slot {
-  zb_rec d;
-  uint32_t rself, rscope;
-  uint8_t flags, ord, rord, pad;
 };
 
 struct TState {
@@ -139,7 +129,7 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
   }
   if (!ok) return;
   if (rec.elem == NO_ELEM) { fail_at(t, DE_PROCESSING, 3); return; }
-  const DevElem el = P.elems[rec.elem];
+  const DevElem& el = P.elems[rec.elem];
   const uint8_t step = el.step[intent];
   if (step == ST_UNBOUND || step == ST_NONE) return;
 
@@ -353,227 +343,287 @@ __device__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t p
   }
 }
 
-// ------------------------------------------------------------------------------ scan helpers
-// Tile counts packed like the status granules: a = rec << 28 | wf, b = job << 28 | row, c = bytes.
-// Sums of packed values never carry between fields (per-wave totals < 2^28, checked on the host).
-struct Cnt {
-  uint64_t a, b, c;
-};
-__device__ __forceinline__ Cnt cnt_add(const Cnt& x, const Cnt& y) { return Cnt{x.a + y.a, x.b + y.b, x.c + y.c}; }
+// ------------------------------------------------------------------------------ helpers
 __device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int d) {
   return (uint64_t)__shfl_up((unsigned long long)v, d, 64);
 }
-__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int d) {
-  return (uint64_t)__shfl_xor((unsigned long long)v, d, 64);
-}
-constexpr uint64_t F28 = 0xfffffffull;
-constexpr uint64_t F56 = 0xffffffffffffffull;
-
-__device__ __forceinline__ void publish(unsigned long long* st, int64_t tile, uint32_t tag, const Cnt& c) {
-  const unsigned long long t8 = (unsigned long long)tag << 56;
-  __hip_atomic_store(st + 3 * tile + 0, t8 | (c.a & F56), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(st + 3 * tile + 1, t8 | (c.b & F56), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(st + 3 * tile + 2, t8 | (c.c & F56), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ uint64_t shfl_down64(uint64_t v, int d) {
+  return (uint64_t)__shfl_down((unsigned long long)v, d, 64);
 }
 
-// ------------------------------------------------------------------------------ the kernel
-struct ItemInfo {  // per (thread, item) write-phase inputs, staged in LDS (32 B)
-  uint32_t m_src, m_tgt, m_len, m_bytes;  // merge (m_bytes == 0: none)
-  int64_t d_pos;                          // incident detail
-  uint16_t d_q;
-  uint8_t d_type, d_code, d_a, d_b, has_detail, ns;
+struct Chunk {
+  int64_t begin, end, n;  // [begin, end) records processed by this wave
 };
+__device__ __forceinline__ Chunk wave_chunk(const WaveParams& P, const WaveHdr* h) {
+  const int64_t b = h->begin, g = h->gen_end;
+  const int64_t e = (g - b > (int64_t)P.wave_cap) ? b + (int64_t)P.wave_cap : g;
+  return Chunk{b, e, e - b};
+}
+// contiguous tile range of workgroup b (identical in k_process and k_emit)
+__device__ __forceinline__ void block_tiles(const Chunk& c, int64_t& t0, int64_t& t1) {
+  const int64_t ntiles = (c.n + WG - 1) / WG;
+  t0 = (int64_t)blockIdx.x * ntiles / gridDim.x;
+  t1 = (int64_t)(blockIdx.x + 1) * ntiles / gridDim.x;
+}
 
-__global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
-  __shared__ uint64_t s_a[ITEMS][WG / 64];  // per-wave totals of packed rec|wf|job|row (16 bit each)
-  __shared__ uint64_t s_b[ITEMS][WG / 64];  // bytes
-  __shared__ Cnt s_excl;                    // tile exclusive prefix
-  __shared__ int64_t s_tile;
-  __shared__ uint32_t s_err;
-  __shared__ uint32_t s_stats[6];
-  __shared__ Slot s_slots[WG * ITEMS * MAX_SLOTS];
-  __shared__ ItemInfo s_info[WG * ITEMS];
-
+// ------------------------------------------------------------------------------ k_process
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8))) k_process(WaveParams P) {
+  __shared__ Slot s_slots[WG * MAX_SLOTS];
+  __shared__ uint64_t s_red[WG / 64][6];
   const WaveHdr* hin = P.hdr + (P.wave & 1);
-  WaveHdr* hout = P.hdr + ((P.wave + 1) & 1);
-  const int64_t begin = hin->begin, end = hin->end;
-  const int64_t n = end - begin;
+  const Chunk c = wave_chunk(P, hin);
+  if (c.n <= 0) return;
+  const int64_t gen_end = hin->gen_end;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t epoch = (uint32_t)(P.wave % 127) + 1;
+  int64_t t0, t1;
+  block_tiles(c, t0, t1);
+  // this thread's totals over the workgroup's tiles: packed 16-bit fields (<= 2 per record per tile, and
+  // a workgroup owns at most wave_cap / WG / WAVE_GRID tiles), bytes separately
+  uint64_t acc_a = 0;  // rec | wf << 16 | job << 32 | row << 48
+  uint64_t acc_b = 0;  // merges | conds << 16 | transitions << 32 | completed << 48
+  uint64_t acc_bytes = 0;
+  uint32_t acc_created = 0;
 
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    P.tickets[(P.wave + 1) & 127] = 0;
-    // the other parity's job lists were consumed by the aux kernels of wave - 1 (stream order); clear
-    // them for wave + 1 (this wave's lists were cleared the same way by wave - 1 / zb_reset)
-    P.merge_count[(P.wave + 1) & 1] = 0;
-    P.cond_count[(P.wave + 1) & 1] = 0;
-  }
-  if (n <= 0) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *hout = *hin;
-    return;
-  }
-  const int64_t ntiles = (n + TILE - 1) / TILE;
-  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd((unsigned long long*)&P.stats[6], 1ull);
-  if (threadIdx.x < 6) s_stats[threadIdx.x] = 0;
-  if (threadIdx.x == 0) s_err = 0;
-  uint32_t st_trans = 0, st_completed = 0, st_created = 0, st_merges = 0, st_mbytes = 0, st_cbytes = 0;
-
-  for (;;) {
-    if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(P.tickets + (P.wave & 127), 1u);
-    __syncthreads();
-    const int64_t tile = s_tile;
-    if (tile >= ntiles) break;
-
-    // ---------------- 1. process (item k of this thread = record tile*TILE + k*WG + tid)
-    uint64_t a[ITEMS], b[ITEMS];
-    uint32_t err = 0, err_site = 0;
-    int64_t err_pos = 0;
-#pragma unroll 1
-    for (int k = 0; k < ITEMS; k++) {
-      TState t;
-      t.s = s_slots + (threadIdx.x * ITEMS + k) * MAX_SLOTS;
-      t.ns = t.nwf = t.njob = t.nrow = 0;
-      t.bytes = 0; t.merge = false; t.detail = false; t.err = 0; t.err_site = 0;
-      t.transitions = t.completed = t.created = t.merges = 0;
-      t.merge_bytes = t.cond_bytes = 0;
-      const int64_t r = begin + tile * TILE + k * WG + threadIdx.x;
-      if (r < end) {
-        const zb_rec rec = P.log[r];
-        if (!kind_cont(rec.kind)) {
-          // a thread owns its record plus the continuation records that follow it (one parent's batch)
-          const uint64_t lk = P.links[r];
-          process_record(P, rec, r, (uint32_t)lk, (uint32_t)(lk >> 32), t);
-          for (int64_t q = r + 1; q < end && q < r + 4; q++) {
-            const zb_rec rec2 = P.log[q];
-            if (!kind_cont(rec2.kind)) break;
-            const uint64_t lk2 = P.links[q];
-            process_record(P, rec2, q, (uint32_t)lk2, (uint32_t)(lk2 >> 32), t);
-          }
-        }
+  for (int64_t tile = t0; tile < t1; tile++) {
+    const int64_t i = tile * WG + threadIdx.x;  // wave-relative index
+    const int64_t r = c.begin + i;
+    if (r >= c.end) continue;
+    TState t;
+    t.s = s_slots + threadIdx.x * MAX_SLOTS;
+    t.ns = t.nwf = t.njob = t.nrow = 0;
+    t.bytes = 0; t.merge = false; t.detail = false; t.err = 0; t.err_site = 0;
+    t.transitions = t.completed = t.created = t.merges = 0;
+    t.merge_bytes = t.cond_bytes = 0;
+    uint32_t nconds = 0;
+    const zb_rec rec = P.log[r];
+    if (!kind_cont(rec.kind)) {
+      // a thread owns its record plus the continuation records that follow it (one parent's batch);
+      // a batch never spans generations, so its tail may lie past a chunk end (skipped there as cont)
+      const uint64_t lk = P.links[r];
+      process_record(P, rec, r, (uint32_t)lk, (uint32_t)(lk >> 32), t);
+      for (int64_t q = r + 1; q < gen_end && q < r + 4; q++) {
+        const zb_rec rec2 = P.log[q];
+        if (!kind_cont(rec2.kind)) break;
+        const uint64_t lk2 = P.links[q];
+        process_record(P, rec2, q, (uint32_t)lk2, (uint32_t)(lk2 >> 32), t);
       }
+    }
+    // stage the follow-ups and the count word
+    Slot* dst = P.stage + (uint64_t)i * MAX_SLOTS;
+    for (int k = 0; k < t.ns; k++) {
+      const Slot sl = t.s[k];
+      dst[k] = sl;
+      nconds += (sl.flags & SF_COND_JOB) ? 1 : 0;
+      if (kind_vt(sl.d.kind) == ZB_VT_WORKFLOW_INSTANCE && kind_rt(sl.d.kind) == ZB_RT_EVENT) t.transitions++;
+    }
+    if (t.merge || t.detail) {
       ItemInfo inf;
       inf.m_src = t.m_src; inf.m_tgt = t.m_tgt; inf.m_len = t.m_len; inf.m_bytes = t.merge ? t.m_bytes : 0;
       inf.d_pos = t.d_pos; inf.d_q = t.d_q; inf.d_type = t.d_type; inf.d_code = t.d_code; inf.d_a = t.d_a;
       inf.d_b = t.d_b; inf.has_detail = t.detail; inf.ns = (uint8_t)t.ns;
-      s_info[threadIdx.x * ITEMS + k] = inf;
-      a[k] = (uint64_t)t.ns | ((uint64_t)t.nwf << 16) | ((uint64_t)t.njob << 32) | ((uint64_t)t.nrow << 48);
-      b[k] = t.bytes;
-      if (t.err && !err) { err_site = t.err_site; err_pos = r; }
-      err |= t.err;
-      st_created += t.created; st_merges += t.merges; st_mbytes += t.merge_bytes; st_cbytes += t.cond_bytes;
-      st_completed += t.completed;
+      P.info[i] = inf;
     }
+    P.cw[i] = (uint64_t)t.ns | ((uint64_t)t.nwf << CW_NWF) | ((uint64_t)t.njob << CW_NJOB) |
+              ((uint64_t)t.nrow << CW_NROW) | ((uint64_t)(t.merge ? 1 : 0) << CW_MERGE) |
+              ((uint64_t)(t.detail ? 1 : 0) << CW_DETAIL) | ((uint64_t)nconds << CW_NCOND) |
+              ((uint64_t)t.bytes << 32);
+    acc_a += (uint64_t)t.ns | ((uint64_t)t.nwf << 16) | ((uint64_t)t.njob << 32) | ((uint64_t)t.nrow << 48);
+    acc_b += (uint64_t)(t.merge ? 1 : 0) | ((uint64_t)nconds << 16) | ((uint64_t)t.transitions << 32) |
+             ((uint64_t)t.completed << 48);
+    acc_bytes += t.bytes;
+    acc_created += t.created;
+    if (t.err) {
+      atomicOr(P.err, t.err);
+      // first failing record (lowest position) and the code site that flagged it
+      atomicMin((unsigned long long*)P.err_info, ((unsigned long long)r << 8) | (t.err_site & 0xff));
+    }
+  }
+  // workgroup totals: unpack to 32-bit lanes sums, wave reduction, 4 partials through LDS
+  uint64_t v[6] = {acc_a & 0xffffffffull, acc_a >> 32, acc_b & 0xffffffffull, acc_b >> 32, acc_bytes,
+                   (uint64_t)acc_created};
+  // 16-bit fields of a thread's totals never overflow (<= 2 * tiles per workgroup), but the sum over
+  // 256 threads can: widen each 16-bit pair into two 32-bit halves first
+  uint64_t w[10];
+  w[0] = v[0] & 0xffff; w[1] = v[0] >> 16; w[2] = v[1] & 0xffff; w[3] = v[1] >> 16;
+  w[4] = v[2] & 0xffff; w[5] = v[2] >> 16; w[6] = v[3] & 0xffff; w[7] = v[3] >> 16;
+  w[8] = v[4]; w[9] = v[5];
+  uint64_t pk[5] = {w[0] | (w[1] << 32), w[2] | (w[3] << 32), w[4] | (w[5] << 32), w[6] | (w[7] << 32),
+                    w[8] | (w[9] << 40)};
+#pragma unroll
+  for (int f = 0; f < 5; f++) {
+    uint64_t x = pk[f];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) x += shfl_down64(x, d);
+    pk[f] = x;
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int f = 0; f < 5; f++) s_red[wv][f] = pk[f];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t a[5];
+#pragma unroll
+    for (int f = 0; f < 5; f++) a[f] = s_red[0][f] + s_red[1][f] + s_red[2][f] + s_red[3][f];
+    BlockAgg g;
+    g.rec = (uint32_t)a[0]; g.wf = (uint32_t)(a[0] >> 32);
+    g.job = (uint32_t)a[1]; g.row = (uint32_t)(a[1] >> 32);
+    g.merges = (uint32_t)a[2]; g.conds = (uint32_t)(a[2] >> 32);
+    g.transitions = (uint32_t)a[3]; g.completed = (uint32_t)(a[3] >> 32);
+    g.bytes = a[4] & 0xffffffffffull; g.created = (uint32_t)(a[4] >> 40);
+    g.pad = 0;
+    P.block_agg[blockIdx.x] = g;
+  }
+}
 
-    // ---------------- 2. block scan, item-major order (all of item 0, then all of item 1)
-    uint64_t ea[ITEMS], eb[ITEMS];
+// ------------------------------------------------------------------------------ k_scan
+constexpr int SCAN_WG = 1024;
+constexpr int SCAN_PER = WAVE_GRID / SCAN_WG;  // workgroup aggregates per scan thread
+
+__global__ void __launch_bounds__(SCAN_WG) k_scan(WaveParams P) {
+  __shared__ uint64_t s_w[SCAN_WG / 64][10];
+  const WaveHdr* hin = P.hdr + (P.wave & 1);
+  WaveHdr* hout = P.hdr + ((P.wave + 1) & 1);
+  const Chunk c = wave_chunk(P, hin);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // fields: rec wf job row bytes merges conds | transitions completed created (reduced only)
+  BlockAgg g[SCAN_PER];
+  uint64_t x[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  if (c.n > 0) {
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) g[k] = P.block_agg[threadIdx.x * SCAN_PER + k];
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) {
+      x[0] += g[k].rec; x[1] += g[k].wf; x[2] += g[k].job; x[3] += g[k].row; x[4] += g[k].bytes;
+      x[5] += g[k].merges; x[6] += g[k].conds; x[7] += g[k].transitions; x[8] += g[k].completed;
+      x[9] += g[k].created;
+    }
+  }
+  uint64_t ex[10];
+#pragma unroll
+  for (int f = 0; f < 10; f++) {
+    uint64_t y = x[f];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t u = shfl_up64(y, d);
+      if (lane >= d) y += u;
+    }
+    ex[f] = y - x[f];
+    if (lane == 63) s_w[wv][f] = y;
+  }
+  __syncthreads();
+  if (c.n > 0) {
+#pragma unroll
+    for (int f = 0; f < 7; f++) {
+      uint64_t pre = 0;
+      for (int w = 0; w < wv; w++) pre += s_w[w][f];
+      ex[f] += pre;
+    }
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) {
+      P.block_off[threadIdx.x * SCAN_PER + k] =
+          BlockOff{ex[0], ex[1], ex[2], ex[3], ex[4], (uint32_t)ex[5], (uint32_t)ex[6]};
+      ex[0] += g[k].rec; ex[1] += g[k].wf; ex[2] += g[k].job; ex[3] += g[k].row; ex[4] += g[k].bytes;
+      ex[5] += g[k].merges; ex[6] += g[k].conds;
+    }
+  }
+  if (threadIdx.x == 0) {
+    uint64_t tot[10];
+    for (int f = 0; f < 10; f++) {
+      tot[f] = 0;
+      for (int w = 0; w < SCAN_WG / 64; w++) tot[f] += s_w[w][f];
+    }
+    WaveHdr h = *hin;
+    if (c.n > 0) {
+      h.begin = c.end;
+      h.end = hin->end + (int64_t)tot[0];
+      h.gen_end = (c.end == hin->gen_end) ? h.end : hin->gen_end;
+      h.wf_next = hin->wf_next + 5 * (int64_t)tot[1];
+      h.job_next = hin->job_next + 5 * (int64_t)tot[2];
+      h.rows_next = hin->rows_next + (int64_t)tot[3];
+      h.arena_next = hin->arena_next + (int64_t)tot[4];
+      P.stats[0] += tot[7];
+      P.stats[1] += tot[8];
+      P.stats[2] += tot[9];
+      P.stats[6] += 1;
+      uint32_t err = 0;
+      if ((uint64_t)h.end > P.log_cap) err |= DE_LOG_FULL;
+      if ((uint64_t)h.rows_next > P.row_cap) err |= DE_ROWS_FULL;
+      if ((uint64_t)h.arena_next > P.arena_cap) err |= DE_ARENA_FULL;
+      if (tot[5] > P.job_cap || tot[6] > P.job_cap) err |= DE_LOG_FULL;
+      if (err) atomicOr(P.err, err);
+    }
+    *hout = h;
+    P.merge_count[P.wave & 1] = c.n > 0 ? (uint32_t)tot[5] : 0;
+    P.cond_count[P.wave & 1] = c.n > 0 ? (uint32_t)tot[6] : 0;
+  }
+}
+
+// ------------------------------------------------------------------------------ k_emit
+__global__ void __launch_bounds__(WG) k_emit(WaveParams P) {
+  __shared__ uint64_t s_a[WG / 64], s_b[WG / 64];
+  const WaveHdr* hin = P.hdr + (P.wave & 1);
+  const Chunk c = wave_chunk(P, hin);
+  if (c.n <= 0) return;
+  int64_t t0, t1;
+  block_tiles(c, t0, t1);
+  if (t0 >= t1) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t end = hin->end, wf_next = hin->wf_next, job_next = hin->job_next;
+  const uint64_t rows_next = (uint64_t)hin->rows_next, arena_next = (uint64_t)hin->arena_next;
+  const uint64_t par = (uint64_t)(P.wave & 1) * P.job_cap;
+  const BlockOff bo = P.block_off[blockIdx.x];
+  // running workgroup offsets (tile prefix): outputs, wf keys, job keys, rows, bytes, merges, conds
+  uint64_t c_rec = bo.rec, c_wf = bo.wf, c_job = bo.job, c_row = bo.row, c_bytes = bo.bytes;
+  uint64_t c_merge = bo.merges, c_cond = bo.conds;
+
+  for (int64_t tile = t0; tile < t1; tile++) {
+    const int64_t i = tile * WG + threadIdx.x;
+    const uint64_t w = (c.begin + i < c.end) ? P.cw[i] : 0;
+    // packed block scan: a = outputs | wf << 16 | job << 32 | row << 48, b = bytes | merges << 40 | conds << 52
+    const uint64_t a0 = (w & 7) | (((w >> CW_NWF) & 7) << 16) | (((w >> CW_NJOB) & 7) << 32) |
+                        (((w >> CW_NROW) & 7) << 48);
+    const uint64_t b0 = (w >> 32) | (((w >> CW_MERGE) & 1) << 40) | (((w >> CW_NCOND) & 7) << 52);
+    uint64_t a = a0, b = b0;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t ua = shfl_up64(a, d), ub = shfl_up64(b, d);
+      if (lane >= d) { a += ua; b += ub; }
+    }
+    __syncthreads();  // s_a / s_b reuse across tiles
+    if (lane == 63) { s_a[wv] = a; s_b[wv] = b; }
+    __syncthreads();
     uint64_t ta = 0, tb = 0;
 #pragma unroll
-    for (int k = 0; k < ITEMS; k++) {
-      uint64_t ia = a[k], ib = b[k];
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        uint64_t ua = shfl_up64(ia, d), ub = shfl_up64(ib, d);
-        if (lane >= d) { ia += ua; ib += ub; }
-      }
-      if (lane == 63) { s_a[k][wv] = ia; s_b[k][wv] = ib; }
-      ea[k] = ia - a[k];
-      eb[k] = ib - b[k];
+    for (int k = 0; k < WG / 64; k++) {
+      if (k < wv) { a += s_a[k]; b += s_b[k]; }
+      ta += s_a[k]; tb += s_b[k];
     }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < ITEMS; k++) {
-      uint64_t wa = 0, wb = 0, ka = 0, kb = 0;
-#pragma unroll
-      for (int w = 0; w < WG / 64; w++) {
-        if (w < wv) { wa += s_a[k][w]; wb += s_b[k][w]; }
-        ka += s_a[k][w]; kb += s_b[k][w];
-      }
-      ea[k] += wa + ta;
-      eb[k] += wb + tb;
-      ta += ka;
-      tb += kb;
-    }
-    const Cnt agg{((ta & 0xffff) << 28) | ((ta >> 16) & 0xffff), (((ta >> 32) & 0xffff) << 28) | (ta >> 48), tb};
-
-    // ---------------- 3. decoupled look-back (wave 0), 256 predecessors per round trip
-    if (wv == 0) {
-      Cnt excl{0, 0, 0};
-      if (tile == 0) {
-        if (lane == 0) publish(P.status, 0, (epoch << 1) | 1, agg);
-      } else {
-        if (lane == 0) publish(P.status, tile, (epoch << 1) | 0, agg);
-        int64_t base = tile - 1;
-        uint32_t spins = 0;
-        bool timeout = false;
-        for (;;) {
-          Cnt v[4];
-          int first_local = 1 << 30;  // smallest window offset of a prefix this lane holds
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const int off = lane + 64 * j;
-            const int64_t idx = base - off;
-            v[j] = Cnt{0, 0, 0};
-            if (idx < 0) { if (off < first_local) first_local = off; continue; }
-            for (;;) {
-              unsigned long long* g = P.status + 3 * idx;
-              unsigned long long g0 = __hip_atomic_load(g + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              unsigned long long g1 = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              unsigned long long g2 = __hip_atomic_load(g + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              uint32_t t0 = (uint32_t)(g0 >> 56), t1 = (uint32_t)(g1 >> 56), t2 = (uint32_t)(g2 >> 56);
-              if (t0 == t1 && t1 == t2 && (t0 >> 1) == epoch) {
-                v[j] = Cnt{g0 & F56, g1 & F56, g2 & F56};
-                if ((t0 & 1) && off < first_local) first_local = off;
-                break;
-              }
-              if (++spins > (1u << 24)) { timeout = true; if (off < first_local) first_local = off; break; }
-              __builtin_amdgcn_s_sleep(1);
-            }
-          }
-          // nearest predecessor holding an inclusive prefix (window offset), wave-wide minimum
-          int first = first_local;
-#pragma unroll
-          for (int d = 32; d >= 1; d >>= 1) {
-            int o = __shfl_xor(first, d, 64);
-            first = o < first ? o : first;
-          }
-          Cnt c{0, 0, 0};
-#pragma unroll
-          for (int j = 0; j < 4; j++)
-            if (lane + 64 * j <= first) c = cnt_add(c, v[j]);
-#pragma unroll
-          for (int d = 32; d >= 1; d >>= 1) {
-            c.a += shfl_xor64(c.a, d); c.b += shfl_xor64(c.b, d); c.c += shfl_xor64(c.c, d);
-          }
-          excl = cnt_add(excl, c);
-          if (first < 256) break;
-          base -= 256;
-        }
-        if (__any(timeout) && lane == 0) atomicOr(&s_err, (uint32_t)DE_LOOKBACK_TIMEOUT);
-        if (lane == 0) publish(P.status, tile, (epoch << 1) | 1, cnt_add(excl, agg));
-      }
-      if (lane == 0) s_excl = excl;
-    }
-    __syncthreads();
-    const Cnt ex = s_excl;
-
-    // ---------------- 4. write
-#pragma unroll 1
-    for (int k = 0; k < ITEMS; k++) {
-      const ItemInfo inf = s_info[threadIdx.x * ITEMS + k];
-      uint64_t out_rec = (uint64_t)end + (ex.a >> 28) + (ea[k] & 0xffff);
-      const uint64_t wf0 = (ex.a & F28) + ((ea[k] >> 16) & 0xffff);
-      const uint64_t job0 = (ex.b >> 28) + ((ea[k] >> 32) & 0xffff);
-      const uint64_t row0 = (uint64_t)hin->rows_next + (ex.b & F28) + (ea[k] >> 48);
-      uint64_t bump = (uint64_t)hin->arena_next + ex.c + eb[k];
-      uint32_t merged_ref = 0, detail_ref = 0;
+    a -= a0;
+    b -= b0;
+    const uint64_t r_rec = c_rec, r_wf = c_wf, r_job = c_job, r_row = c_row, r_bytes = c_bytes;
+    const uint64_t r_merge = c_merge, r_cond = c_cond;
+    c_rec += ta & 0xffff; c_wf += (ta >> 16) & 0xffff; c_job += (ta >> 32) & 0xffff; c_row += ta >> 48;
+    c_bytes += tb & 0xffffffffffull; c_merge += (tb >> 40) & 0xfff; c_cond += tb >> 52;
+    const int ns = (int)(w & 7);
+    if (ns == 0 && !((w >> CW_DETAIL) & 1)) continue;
+    uint64_t out_rec = (uint64_t)end + r_rec + (a & 0xffff);
+    const uint64_t wf0 = r_wf + ((a >> 16) & 0xffff);
+    const uint64_t job0 = r_job + ((a >> 32) & 0xffff);
+    const uint64_t row0 = rows_next + r_row + (a >> 48);
+    uint64_t bump = arena_next + r_bytes + (b & 0xffffffffffull);
+    const uint64_t merge_j = r_merge + ((b >> 40) & 0xfff);
+    uint64_t cond_j = r_cond + (b >> 52);
+    uint32_t err = 0;
+    uint32_t merged_ref = 0, detail_ref = 0;
+    if (w & ((1ull << CW_MERGE) | (1ull << CW_DETAIL))) {
+      const ItemInfo inf = P.info[i];
       if (inf.m_bytes) {
         // reserve the blob; k_merge (zb_aux.hip) fills it before the next wave reads any payload
         if (bump + inf.m_bytes > P.arena_cap) err |= DE_ARENA_FULL;
         else {
           merged_ref = (uint32_t)(bump >> 3);
-          const uint32_t j = atomicAdd(P.merge_count + (P.wave & 1), 1u);
-          if (j >= P.job_cap) err |= DE_LOG_FULL;
-          else P.merge_jobs[(uint64_t)(P.wave & 1) * P.job_cap + j] = MergeJob{merged_ref, inf.m_src, inf.m_tgt, inf.m_len};
+          if (merge_j < P.job_cap) P.merge_jobs[par + merge_j] = MergeJob{merged_ref, inf.m_src, inf.m_tgt, inf.m_len};
         }
         bump += inf.m_bytes;
       }
@@ -589,77 +639,52 @@ __global__ void __launch_bounds__(WG) k_wave(WaveParams P) {
         }
         bump += 24;
       }
-      const Slot* sl = s_slots + (threadIdx.x * ITEMS + k) * MAX_SLOTS;
-      for (int i = 0; i < inf.ns; i++) {
-        Slot s = sl[i];
-        if (s.flags & SF_KEY_WF) s.d.key = hin->wf_next + 5 * (int64_t)(wf0 + s.ord);
-        if (s.flags & SF_KEY_JOB) s.d.key = hin->job_next + 5 * (int64_t)(job0 + s.ord);
-        if (s.flags & SF_INST_WF) s.d.inst_key = hin->wf_next + 5 * (int64_t)(wf0 + s.ord);
-        if (s.flags & SF_PAY_MERGED) s.d.payload = merged_ref;
-        if (s.flags & SF_PAY_DETAIL) s.d.payload = detail_ref;
-        if (s.flags & SF_ROW_NEW) {
-          const uint64_t row = row0 + s.rord;
-          if (row >= P.row_cap) { err |= DE_ROWS_FULL; s.rself = NO_ROW; }
-          else {
-            s.rself = (uint32_t)row;
-            if (s.flags & SF_ROW_INIT) {
-              RowMeta m;
-              m.payload = s.d.payload; m.parent = s.rscope; m.elem = s.d.elem; m.state = WI_ELEMENT_READY;
-              m.flags = 0; m.nchild = 0;
-              P.rmeta[row] = m;
-              P.rkeys[row] = RowKeys{s.d.key, s.d.scope_key, s.d.inst_key, 0};
-            }
-          }
-        }
-        if (kind_vt(s.d.kind) == ZB_VT_WORKFLOW_INSTANCE && kind_rt(s.d.kind) == ZB_RT_EVENT) st_trans++;
-        if (out_rec >= P.log_cap) { err |= DE_LOG_FULL; }
+    }
+    const Slot* sl = P.stage + (uint64_t)i * MAX_SLOTS;
+    for (int k = 0; k < ns; k++) {
+      Slot s = sl[k];
+      if (s.flags & SF_KEY_WF) s.d.key = wf_next + 5 * (int64_t)(wf0 + s.ord);
+      if (s.flags & SF_KEY_JOB) s.d.key = job_next + 5 * (int64_t)(job0 + s.ord);
+      if (s.flags & SF_INST_WF) s.d.inst_key = wf_next + 5 * (int64_t)(wf0 + s.ord);
+      if (s.flags & SF_PAY_MERGED) s.d.payload = merged_ref;
+      if (s.flags & SF_PAY_DETAIL) s.d.payload = detail_ref;
+      if (s.flags & SF_ROW_NEW) {
+        const uint64_t row = row0 + s.rord;
+        if (row >= P.row_cap) { err |= DE_ROWS_FULL; s.rself = NO_ROW; }
         else {
-          P.log[out_rec] = s.d;
-          P.links[out_rec] = (uint64_t)s.rself | ((uint64_t)s.rscope << 32);
-          if (s.flags & SF_COND_JOB) {
-            const uint32_t j = atomicAdd(P.cond_count + (P.wave & 1), 1u);
-            if (j >= P.job_cap) err |= DE_LOG_FULL;
-            else P.cond_jobs[(uint64_t)(P.wave & 1) * P.job_cap + j] = out_rec;
+          s.rself = (uint32_t)row;
+          if (s.flags & SF_ROW_INIT) {
+            RowMeta m;
+            m.payload = s.d.payload; m.parent = s.rscope; m.elem = s.d.elem; m.state = WI_ELEMENT_READY;
+            m.flags = 0; m.nchild = 0;
+            P.rmeta[row] = m;
+            P.rkeys[row] = RowKeys{s.d.key, s.d.scope_key, s.d.inst_key, 0};
           }
         }
-        out_rec++;
       }
+      if (out_rec >= P.log_cap) { err |= DE_LOG_FULL; }
+      else {
+        P.log[out_rec] = s.d;
+        P.links[out_rec] = (uint64_t)s.rself | ((uint64_t)s.rscope << 32);
+        if (s.flags & SF_COND_JOB) {
+          if (cond_j < P.job_cap) P.cond_jobs[par + cond_j] = out_rec;
+          cond_j++;
+        }
+      }
+      out_rec++;
     }
-    if (err) {
-      atomicOr(&s_err, err);
-      // first failing record (lowest position) and the code site that flagged it
-      atomicMin((unsigned long long*)P.err_info, ((unsigned long long)err_pos << 8) | (err_site & 0xff));
-    }
-    if (tile == ntiles - 1 && threadIdx.x == 0) {
-      const Cnt tot = cnt_add(ex, agg);
-      WaveHdr h = *hin;
-      h.begin = end;
-      h.end = end + (int64_t)(tot.a >> 28);
-      h.wf_next = hin->wf_next + 5 * (int64_t)(tot.a & F28);
-      h.job_next = hin->job_next + 5 * (int64_t)(tot.b >> 28);
-      h.rows_next = hin->rows_next + (int64_t)(tot.b & F28);
-      h.arena_next = hin->arena_next + (int64_t)tot.c;
-      *hout = h;
-    }
-    __syncthreads();
-  }
-  // stats: block reduce -> one atomic per block per counter
-  if (st_trans) atomicAdd(&s_stats[0], st_trans);
-  if (st_completed) atomicAdd(&s_stats[1], st_completed);
-  if (st_created) atomicAdd(&s_stats[2], st_created);
-  if (st_merges) atomicAdd(&s_stats[3], st_merges);
-  if (st_mbytes) atomicAdd(&s_stats[4], st_mbytes);
-  if (st_cbytes) atomicAdd(&s_stats[5], st_cbytes);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (s_err) atomicOr(P.err, s_err);
-    for (int i = 0; i < 6; i++)
-      if (s_stats[i]) atomicAdd((unsigned long long*)&P.stats[i], (unsigned long long)s_stats[i]);
+    if (err) atomicOr(P.err, err);  // capacity overflow: the wave's results are void, the host stops
   }
 }
 
-void launch_wave(const WaveParams& p, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(k_wave, dim3(grid), dim3(WG), 0, stream, p);
+void launch_process(const WaveParams& p, hipStream_t stream) {
+  hipLaunchKernelGGL(k_process, dim3(WAVE_GRID), dim3(WG), 0, stream, p);
+}
+void launch_scan(const WaveParams& p, hipStream_t stream) {
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(SCAN_WG), 0, stream, p);
+}
+void launch_emit(const WaveParams& p, hipStream_t stream) {
+  hipLaunchKernelGGL(k_emit, dim3(WAVE_GRID), dim3(WG), 0, stream, p);
 }
 
 }  // namespace zbg

@@ -29,7 +29,7 @@ class zb_config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("partition_id", ctypes.c_int32),
                 ("partition_count", ctypes.c_int32), ("reserved0", ctypes.c_int32),
                 ("log_capacity", ctypes.c_uint64), ("row_capacity", ctypes.c_uint64),
-                ("arena_bytes", ctypes.c_uint64), ("staging_records", ctypes.c_uint64)]
+                ("arena_bytes", ctypes.c_uint64), ("wave_records", ctypes.c_uint64)]
 
 
 class zb_rec(ctypes.Structure):
@@ -51,7 +51,8 @@ class zb_step_stats(ctypes.Structure):
                 ("transitions", ctypes.c_uint64), ("completed_instances", ctypes.c_uint64),
                 ("merges", ctypes.c_uint64), ("merge_bytes", ctypes.c_uint64),
                 ("condition_payload_bytes", ctypes.c_uint64), ("wave_kernel_ms", ctypes.c_double),
-                ("wall_ms", ctypes.c_double)]
+                ("wall_ms", ctypes.c_double), ("process_kernel_ms", ctypes.c_double),
+                ("emit_kernel_ms", ctypes.c_double), ("aux_kernel_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -108,9 +109,11 @@ class Engine:
     """One partition of the GPU stepping core (one HIP device + stream)."""
 
     def __init__(self, device: int = 0, partition_id: int = 0, partition_count: int = 1,
-                 log_capacity: int = 1 << 22, row_capacity: int = 1 << 20, arena_bytes: int = 64 << 20):
+                 log_capacity: int = 1 << 22, row_capacity: int = 1 << 20, arena_bytes: int = 64 << 20,
+                 wave_records: int = 0):
         self._L = lib()
-        cfg = zb_config(device, partition_id, partition_count, 0, log_capacity, row_capacity, arena_bytes, 0)
+        cfg = zb_config(device, partition_id, partition_count, 0, log_capacity, row_capacity, arena_bytes,
+                        wave_records)
         h = ctypes.c_void_p()
         rc = self._L.zb_engine_create(ctypes.byref(cfg), ctypes.byref(h))
         if rc != ZB_OK:
