@@ -34,6 +34,7 @@ def parse():
     ap.add_argument("--tasks", type=int, default=20)
     ap.add_argument("--cpu-sample", type=int, default=30_000, help="instances in the oracle CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--wave-only", action="store_true", help="force the general wave pipeline (no trajectory path)")
     return ap.parse_args()
 
 
@@ -78,7 +79,7 @@ def main():
     recs_per_inst = 1 + (8 + 5 * a.tasks) + 3 * a.tasks  # CREATE + WF events + JOB CREATE/CREATED/COMPLETED
     eng = Engine(device=local_rank, partition_id=rank, partition_count=world,
                  log_capacity=int(n * (recs_per_inst + 2)), row_capacity=int(n * (a.tasks + 2)),
-                 arena_bytes=int(n * (48 + 48 * a.tasks)) + (64 << 20))
+                 arena_bytes=int(n * (48 + 48 * a.tasks)) + (64 << 20), wave_only=a.wave_only)
     xml = bpmn.chain_workflow(a.tasks).to_xml()
     eng.deploy(xml, 100, 1)
     for k in range(1, a.tasks + 1):
@@ -106,7 +107,7 @@ def main():
     barrier()
     t0 = time.perf_counter()
     tot = dict(transitions=0, completed=0, kernel_ms=0.0, launches=0, waves=0, merge_bytes=0, cond_bytes=0,
-               records=0)
+               records=0, path=0)
     for _ in range(a.steps):
         st = one_step()
         tot["transitions"] += st["transitions"]
@@ -117,6 +118,7 @@ def main():
         tot["merge_bytes"] += st["merge_bytes"]
         tot["cond_bytes"] += st["condition_payload_bytes"]
         tot["records"] += st["records_processed"]
+        tot["path"] = st["path"]
     barrier()
     elapsed = time.perf_counter() - t0
 
@@ -158,7 +160,8 @@ def main():
             "wave_launches_per_step": tot["launches"] / a.steps,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "zbg::k_wave", "launches": tot["launches"],
+                         "kernel": "zbg::k_traj (count + emit passes)" if tot["path"] == 1 else
+                                   "zbg::k_process/k_scan/k_emit/k_merge", "launches": tot["launches"],
                          "avg_launch_us": tot["kernel_ms"] * 1e3 / max(tot["launches"], 1),
                          "alg_bytes_per_transition": BYTES_PER_TRANSITION,
                          "alg_bytes_total": alg_bytes},

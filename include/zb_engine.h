@@ -46,13 +46,16 @@ extern "C" {
 #define ZB_RT_COMMAND 1
 #define ZB_RT_COMMAND_REJECTION 2
 
+/* zb_config.flags */
+#define ZB_CFG_WAVE_ONLY 1    /* always use the general wave pipeline (never the trajectory path) */
+
 typedef struct zb_engine zb_engine;
 
 typedef struct zb_config {
   int32_t device;           /* HIP device ordinal */
   int32_t partition_id;
   int32_t partition_count;
-  int32_t reserved0;
+  int32_t flags;            /* ZB_CFG_* bits */
   uint64_t log_capacity;    /* max records in the device log (32 B descriptor + 8 B row links each) */
   uint64_t row_capacity;    /* max element-instance rows (SoA state, 64 B each) */
   uint64_t arena_bytes;     /* payload arena (msgpack documents, 8-byte aligned blobs) */
@@ -96,9 +99,10 @@ typedef struct zb_step_stats {
   uint64_t condition_payload_bytes; /* payload bytes read by exclusive-gateway evaluations */
   double wave_kernel_ms;       /* device time of all wave kernels (HIP events on the engine stream) */
   double wall_ms;              /* host wall time of the zb_step call */
-  double process_kernel_ms;    /* k_process share of wave_kernel_ms */
-  double emit_kernel_ms;       /* k_scan + k_emit share */
+  double process_kernel_ms;    /* k_process share of wave_kernel_ms (trajectory: count pass) */
+  double emit_kernel_ms;       /* k_scan + k_emit share (trajectory: scans + emit pass) */
   double aux_kernel_ms;        /* k_merge + k_cond share */
+  uint64_t path;               /* 0: wave pipeline, 1: trajectory path (zb_traj.hip) ran the step */
 } zb_step_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------- */

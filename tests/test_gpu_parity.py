@@ -13,6 +13,15 @@ from zeebe_amd import bpmn, workloads
 
 pytestmark = pytest.mark.gpu
 
+# Every case runs through both GPU pipelines: the trajectory path (zb_traj.hip, taken for a batch of
+# CREATEs on an idle partition) and the general wave pipeline (zb_wave.hip, forced by wave_only).
+PATHS = ["traj", "wave"]
+
+
+@pytest.fixture(params=PATHS)
+def path(request):
+    return request.param
+
 
 def _engine(**kw):
     from zeebe_amd.engine import Engine
@@ -20,10 +29,10 @@ def _engine(**kw):
     return Engine(**kw)
 
 
-def _run_both(xml, process, payloads, job_payloads=None, wf_key=100, **cap):
+def _run_both(xml, process, payloads, job_payloads=None, wf_key=100, path="traj", expect_traj=False, **cap):
     o = zbref.Oracle()
     o.deploy(xml, wf_key, 1)
-    e = _engine(**cap)
+    e = _engine(wave_only=(path == "wave"), **cap)
     e.deploy(xml, wf_key, 1)
     for act, p in (job_payloads or {}).items():
         o.set_job_payload(wf_key, act, p)
@@ -34,6 +43,10 @@ def _run_both(xml, process, payloads, job_payloads=None, wf_key=100, **cap):
     o.run()
     st = e.step()
     assert st["quiescent"]
+    if path == "wave":
+        assert st["path"] == 0
+    elif expect_traj:
+        assert st["path"] == 1, "trajectory path expected for this batch"
     return o, e, st
 
 
@@ -49,7 +62,7 @@ def _compare(o, e):
     return ref
 
 
-def test_golden_workflows(vectors):
+def test_golden_workflows(vectors, path):
     for spec in vectors["workflows"]:
         payloads = [bytes.fromhex(i["payload"]) for i in spec["instances"]]
         jp = {}
@@ -58,17 +71,18 @@ def test_golden_workflows(vectors):
             jp = {"service": bytes.fromhex(spec["instances"][0]["job_payload"])}
             payloads = payloads[:1]
         try:
-            o, e, st = _run_both(spec["xml"], spec["process"], payloads, jp)
+            o, e, st = _run_both(spec["xml"], spec["process"], payloads, jp, path=path)
         except Exception as ex:
             raise AssertionError("%s: %s" % (spec["name"], ex))
         _compare(o, e)
 
 
 @pytest.mark.parametrize("n", [1, 2, 7, 1000])
-def test_config1_shape(n):
+def test_config1_shape(n, path):
     cfg = workloads.CONFIGS["c1"]
     blob, offs = cfg["payloads"](n)
-    o, e, st = _run_both(cfg["workflow"]().to_xml(), cfg["process"], workloads.split(blob, offs), cfg["job_payloads"]())
+    o, e, st = _run_both(cfg["workflow"]().to_xml(), cfg["process"], workloads.split(blob, offs), cfg["job_payloads"](),
+                         path=path, expect_traj=True)
     ref = _compare(o, e)
     assert st["transitions"] == 13 * n
     assert st["completed_instances"] == n
@@ -76,34 +90,37 @@ def test_config1_shape(n):
 
 
 @pytest.mark.parametrize("n", [3, 300])
-def test_config2_shape(n):
+def test_config2_shape(n, path):
     cfg = workloads.CONFIGS["c2"]
     blob, offs = cfg["payloads"](n)
     o, e, st = _run_both(cfg["workflow"]().to_xml(), cfg["process"], workloads.split(blob, offs),
-                         cfg["job_payloads"](), log_capacity=1 << 20, row_capacity=1 << 18)
+                         cfg["job_payloads"](), log_capacity=1 << 20, row_capacity=1 << 18, path=path,
+                         expect_traj=True)
     _compare(o, e)
     assert st["transitions"] == 108 * n
     assert st["merges"] == 20 * n
 
 
 @pytest.mark.parametrize("n", [5, 3000])
-def test_config3_shape(n):
+def test_config3_shape(n, path):
     cfg = workloads.CONFIGS["c3"]
     blob, offs = cfg["payloads"](n)
-    o, e, st = _run_both(cfg["workflow"]().to_xml(), cfg["process"], workloads.split(blob, offs))
+    o, e, st = _run_both(cfg["workflow"]().to_xml(), cfg["process"], workloads.split(blob, offs), path=path,
+                         expect_traj=True)
     _compare(o, e)
     assert st["completed_instances"] == n
 
 
-def test_subprocess_chain():
+def test_subprocess_chain(path):
     cfg = workloads.CONFIGS["c4twin"]
     blob, offs = cfg["payloads"](200)
     o, e, st = _run_both(cfg["workflow"]().to_xml(), cfg["process"], workloads.split(blob, offs),
-                         cfg["job_payloads"](), log_capacity=1 << 20, row_capacity=1 << 18)
+                         cfg["job_payloads"](), log_capacity=1 << 20, row_capacity=1 << 18, path=path,
+                         expect_traj=True)
     _compare(o, e)
 
 
-def test_condition_incidents_and_rejections():
+def test_condition_incidents_and_rejections(path):
     # type errors, missing paths, NaN, no default flow -> IncidentIntent.CREATE commands (CONDITION_ERROR)
     m = (bpmn.Bpmn.create_executable_process("wf").start_event("s").exclusive_gateway("x")
          .sequence_flow_id("a").condition("$.foo < 5").end_event("ea").move_to_node("x")
@@ -111,15 +128,15 @@ def test_condition_incidents_and_rejections():
     payloads = [msgpack.packb(d) for d in
                 ({"foo": 1}, {"foo": 9}, {"foo": "x"}, {"bar": 3}, {"foo": None}, {"foo": float("nan")},
                  {"foo": 7, "bar": 2.5}, {"foo": [1, 2]}, {"foo": {"a": 1}}, {}, {"foo": 1, "foo2": True})]
-    o, e, st = _run_both(m.to_xml(), "wf", payloads)
+    o, e, st = _run_both(m.to_xml(), "wf", payloads, path=path, expect_traj=True)
     ref = _compare(o, e)
     assert any(r.value_type == 6 for r in ref)
     # unknown process -> CREATE rejection (key generated anyway)
-    o2, e2, _ = _run_both(m.to_xml(), "nope", [b"\x80", b"\x80"])
+    o2, e2, _ = _run_both(m.to_xml(), "nope", [b"\x80", b"\x80"], path=path, expect_traj=True)
     _compare(o2, e2)
 
 
-def test_merge_shapes():
+def test_merge_shapes(path):
     # payload shapes through the default output merge (nested maps/arrays, overwrite, new keys)
     m = (bpmn.Bpmn.create_executable_process("p").start_event("s").service_task("t", type="t")
          .end_event("e").done())
@@ -131,5 +148,59 @@ def test_merge_shapes():
         ({"s" * 40: "v" * 300}, {"q": b"\x00\x01"}),  # str8/str16/bin
     ]
     for tgt, src in cases:
-        o, e, st = _run_both(m.to_xml(), "p", [msgpack.packb(tgt)], {"t": msgpack.packb(src)})
+        o, e, st = _run_both(m.to_xml(), "p", [msgpack.packb(tgt)], {"t": msgpack.packb(src)}, path=path,
+                             expect_traj=True)
         _compare(o, e)
+
+
+def test_successive_batches(path):
+    """Two CREATE batches stepped one after the other: keys, positions and rows continue across steps."""
+    cfg = workloads.CONFIGS["c1"]
+    xml = cfg["workflow"]().to_xml()
+    o = zbref.Oracle()
+    o.deploy(xml, 100, 1)
+    e = _engine(wave_only=(path == "wave"))
+    e.deploy(xml, 100, 1)
+    for act, p in cfg["job_payloads"]().items():
+        o.set_job_payload(100, act, p)
+        e.set_job_payload(100, act, p)
+    for start, n in ((0, 37), (37, 300)):
+        blob, offs = workloads.order_payloads(n, start=start)
+        ps = workloads.split(blob, offs)
+        for p in ps:
+            o.create(cfg["process"], p)
+        e.create(cfg["process"], ps)
+        o.run()
+        st = e.step()
+        assert st["quiescent"]
+        assert st["path"] == (0 if path == "wave" else 1)
+        assert e.step()["records_processed"] == 0  # nothing is re-injected
+    _compare(o, e)
+    oc, ec = o.counters(), e.counters()
+    assert (ec["next_wf_key"], ec["next_job_key"], ec["completed"]) == \
+           (oc["next_wf_key"], oc["next_job_key"], oc["completed"])
+
+
+@pytest.mark.parametrize("cfg_name,n", [("c2", 20000), ("c3", 50000), ("c4twin", 5000)])
+def test_paths_agree_large(cfg_name, n):
+    """Trajectory path vs wave pipeline at sizes where every generation spans many workgroups."""
+    cfg = workloads.CONFIGS[cfg_name]
+    xml = cfg["workflow"]().to_xml()
+    blob, offs = cfg["payloads"](n)
+    logs = []
+    for wave_only in (False, True):
+        e = _engine(wave_only=wave_only, log_capacity=n * 200, row_capacity=n * 24, arena_bytes=(64 << 20) + n * 1200)
+        e.deploy(xml, 100, 1)
+        for act, p in cfg["job_payloads"]().items():
+            e.set_job_payload(100, act, p)
+        e.create_packed(cfg["process"], blob, offs)
+        st = e.step()
+        assert st["quiescent"] and st["path"] == (0 if wave_only else 1)
+        logs.append((e.records(), st))
+        e.close()
+    (ra, sa), (rb, sb) = logs
+    assert len(ra) == len(rb)
+    assert ra == rb
+    for k in ("transitions", "completed_instances", "merges", "merge_bytes", "condition_payload_bytes",
+              "records_written"):
+        assert sa[k] == sb[k], k

@@ -24,6 +24,9 @@ namespace {
 constexpr int WAVES_PER_SYNC = 16;
 constexpr int EV_PER_WAVE = 4;  // before k_process, after k_process, after k_emit, after the aux kernels
 constexpr uint64_t STATIC_ARENA_BYTES = 1ull << 20;  // {} at ref 0 + harness job completion payloads
+constexpr uint64_t TRAJ_BUDGET_BYTES = 256ull << 20;  // per-(generation, workgroup) counts of the trajectory path
+constexpr int TRAJ_MAX_GENERATIONS = 4096;
+constexpr int TRAJ_WAVE_CAP = 8192;                   // k_traj_scan grid bound (one workgroup per generation)
 
 template <class T>
 struct DevVec {
@@ -110,12 +113,25 @@ struct zb_engine {
   DevVec<zb_rec> d_staged;
   DevVec<uint8_t> d_staged_arena;
   bool staged_uploaded = false;
+  bool staged_pending = false;  // the staged batch has not been injected yet (zb_reset(keep) re-arms it)
 
   // submitted command ranges (serialization of CREATE commands / rejections)
   std::vector<CmdRange> ranges;
   std::vector<uint8_t> cmd_pool;
   DevVec<CmdRange> d_ranges;
   DevVec<uint8_t> d_cmd_pool;
+
+  // trajectory path buffers (zb_traj.hip), grown on demand
+  bool traj_model_ok = true;     // false when merges can precede condition evaluation (see zb_traj.hip)
+  uint64_t traj_entries = 0;     // capacity of agg / woff in (generation, workgroup) entries
+  uint64_t* t_agg = nullptr;
+  uint4* t_woff = nullptr;
+  uint32_t* t_wcount = nullptr;
+  uint64_t t_nwg_cap = 0;
+  uint4* t_wtot = nullptr;
+  TrajBase* t_wbase = nullptr;
+  TrajCtl* t_ctl = nullptr;
+  TrajCtl* h_ctl_pinned = nullptr;
 
   // timing
   std::vector<hipEvent_t> ev;
@@ -215,6 +231,92 @@ int check_device_errors(zb_engine* e, uint32_t flags) {
   return fail(e, code, m);
 }
 
+// Trajectory path (zb_traj.hip) for a batch of n CREATE commands injected at log_base on an idle
+// partition. Returns 1 when the batch ran to quiescence, 0 when the count pass asked for the wave
+// pipeline (nothing but scratch counts was written), <0 on a device error.
+int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st) {
+  const uint64_t nwg = (uint64_t)((n + TRAJ_WG - 1) / TRAJ_WG);
+  const uint64_t per_entry = sizeof(uint64_t) + sizeof(uint4);
+  uint64_t wcap = std::min<uint64_t>(TRAJ_MAX_GENERATIONS, (TRAJ_BUDGET_BYTES / per_entry) / nwg);
+  if (wcap < 8 || nwg > 0x7fffffffull) return 0;
+  if (wcap * nwg > e->traj_entries) {
+    if (e->t_agg) (void)hipFree(e->t_agg);
+    if (e->t_woff) (void)hipFree(e->t_woff);
+    e->t_agg = nullptr; e->t_woff = nullptr; e->traj_entries = 0;
+    const uint64_t ent = TRAJ_BUDGET_BYTES / per_entry;
+    HIPCHECK(e, hipMalloc(&e->t_agg, ent * sizeof(uint64_t)));
+    HIPCHECK(e, hipMalloc(&e->t_woff, ent * sizeof(uint4)));
+    e->traj_entries = ent;
+  }
+  if (nwg > e->t_nwg_cap) {
+    if (e->t_wcount) (void)hipFree(e->t_wcount);
+    e->t_wcount = nullptr;
+    HIPCHECK(e, hipMalloc(&e->t_wcount, nwg * sizeof(uint32_t)));
+    e->t_nwg_cap = nwg;
+  }
+  TrajCtl c{};
+  c.arena_next = (uint64_t)e->host_hdr.arena_next;
+  c.rows_next = (uint64_t)e->host_hdr.rows_next;
+  *e->h_ctl_pinned = c;
+  HIPCHECK(e, hipMemcpyAsync(e->t_ctl, e->h_ctl_pinned, sizeof(TrajCtl), hipMemcpyHostToDevice, e->stream));
+  TrajParams p{};
+  p.log = e->log;
+  p.arena = e->arena;
+  p.rmeta = e->rmeta;
+  p.rkeys = e->rkeys;
+  p.elems = e->d_elems.p;
+  p.cond_flows = e->d_cond.p;
+  p.code = e->d_code.p;
+  p.consts = e->d_consts.p;
+  p.queries = e->d_queries.p;
+  p.filters = e->d_filters.p;
+  p.pool = e->d_pool.p;
+  p.log_base = log_base;
+  p.n = n;
+  p.wf_start = e->host_hdr.wf_next;
+  p.job_start = e->host_hdr.job_next;
+  p.nwg = (int32_t)nwg;
+  p.wcap = (int32_t)wcap;
+  p.agg = e->t_agg;
+  p.wcount = e->t_wcount;
+  p.woff = e->t_woff;
+  p.wtot = e->t_wtot;
+  p.wbase = e->t_wbase;
+  p.ctl = e->t_ctl;
+  p.hdr = e->hdr + (e->wave & 1);
+  p.err = e->derr;
+  p.stats = e->dstats;
+  p.log_cap = e->cfg.log_capacity;
+  p.row_cap = e->cfg.row_capacity;
+  p.arena_cap = e->cfg.arena_bytes;
+  hipEvent_t* ev = e->ev.data();
+  HIPCHECK(e, hipEventRecord(ev[0], e->stream));
+  launch_traj_count(p, e->stream);
+  HIPCHECK(e, hipEventRecord(ev[1], e->stream));
+  launch_traj_scan(p, e->stream);
+  launch_traj_emit(p, e->stream);
+  HIPCHECK(e, hipEventRecord(ev[2], e->stream));
+  HIPCHECK(e, hipGetLastError());
+  HIPCHECK(e, hipMemcpyAsync(e->h_ctl_pinned, e->t_ctl, sizeof(TrajCtl), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipMemcpyAsync(e->h_hdr_pinned, e->hdr + (e->wave & 1), sizeof(WaveHdr), hipMemcpyDeviceToHost,
+                             e->stream));
+  HIPCHECK(e, hipMemcpyAsync(e->h_err_pinned, e->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  float ms0 = 0, ms1 = 0;
+  HIPCHECK(e, hipEventElapsedTime(&ms0, ev[0], ev[1]));
+  HIPCHECK(e, hipEventElapsedTime(&ms1, ev[1], ev[2]));
+  st.process_kernel_ms += ms0;
+  st.emit_kernel_ms += ms1;
+  st.wave_kernel_ms += ms0 + ms1;
+  st.launches += 6;
+  if (e->h_ctl_pinned->flag) return 0;
+  e->host_hdr = e->h_hdr_pinned[0];
+  int rc = check_device_errors(e, *e->h_err_pinned);
+  if (rc != ZB_OK) return rc;
+  st.path = 1;
+  return 1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -263,6 +365,10 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->job_counts, 4 * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_hdr_pinned, 2 * sizeof(WaveHdr)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_err_pinned, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipHostMalloc(&e->h_ctl_pinned, sizeof(TrajCtl)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->t_ctl, sizeof(TrajCtl)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->t_wtot, TRAJ_WAVE_CAP * sizeof(uint4)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->t_wbase, TRAJ_WAVE_CAP * sizeof(TrajBase)) != hipSuccess) return cleanup(ZB_ENOMEM);
   e->ev.resize(EV_PER_WAVE * WAVES_PER_SYNC);
   for (auto& x : e->ev)
     if (hipEventCreate(&x) != hipSuccess) return cleanup(ZB_EDEVICE);
@@ -282,11 +388,13 @@ void zb_engine_destroy(zb_engine* e) {
   for (auto& x : e->ev)
     if (x) (void)hipEventDestroy(x);
   void* ps[] = {e->log, e->links, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
-                e->merge_jobs, e->cond_jobs, e->job_counts, e->cw, e->stage, e->info, e->block_agg, e->block_off};
+                e->merge_jobs, e->cond_jobs, e->job_counts, e->cw, e->stage, e->info, e->block_agg, e->block_off,
+                e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->h_hdr_pinned) (void)hipHostFree(e->h_hdr_pinned);
   if (e->h_err_pinned) (void)hipHostFree(e->h_err_pinned);
+  if (e->h_ctl_pinned) (void)hipHostFree(e->h_ctl_pinned);
   e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_consts.free();
   e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
   e->d_ranges.free(); e->d_cmd_pool.free();
@@ -322,6 +430,7 @@ int zb_reset(zb_engine* e, int keep_staged) {
     e->pending_ranges.clear();
     e->staged_uploaded = false;
   }
+  e->staged_pending = !e->staged.empty();
   return ZB_OK;
 }
 
@@ -335,6 +444,8 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
     if (el.step[WI_ELEMENT_COMPLETING] == ST_APPLY_OUTPUT_MAPPING) e->has_merges = true;
     if (el.step[WI_GATEWAY_ACTIVATED] == ST_EXCLUSIVE_SPLIT) e->has_splits = true;
   }
+  // the trajectory count pass skips payload merges, so conditions must never read a merge result
+  e->traj_model_ok = !(e->has_merges && e->has_splits);
   return upload_model(e);
 }
 
@@ -381,6 +492,12 @@ int zb_submit_creates(zb_engine* e, const char* pid, int32_t version, int64_t wo
     for (auto& w : W)
       if (e->model.str(w.pid_off, w.pid_len) == spid && w.version > best) { best = w.version; pelem = w.process_elem; }
   }
+  if (!e->staged_pending) {  // the previous batch was injected: start a new one
+    e->staged.clear();
+    e->staged_arena.clear();
+    e->pending_ranges.clear();
+    e->staged_uploaded = false;
+  }
   zb_engine::PendingRange pr;
   pr.first = (int64_t)e->staged.size();
   pr.last = pr.first + (int64_t)n;
@@ -415,6 +532,7 @@ int zb_submit_creates(zb_engine* e, const char* pid, int32_t version, int64_t wo
   }
   e->pending_ranges.push_back(pr);
   e->staged_uploaded = false;
+  e->staged_pending = true;
   return ZB_OK;
 }
 
@@ -424,8 +542,15 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   HIPCHECK(e, hipSetDevice(e->cfg.device));
   auto t0 = std::chrono::steady_clock::now();
   zb_step_stats st{};
+  bool try_traj = false;
+  int64_t traj_base = 0, traj_n = 0;
   // ---- inject staged input at the log tail (engine is quiescent between steps)
-  if (!e->staged.empty()) {
+  if (e->staged_pending && !e->staged.empty()) {
+    // an idle partition fed only CREATE commands runs as independent trajectories (zb_traj.hip)
+    try_traj = !(e->cfg.flags & ZB_CFG_WAVE_ONLY) && max_waves == 0 && e->traj_model_ok &&
+               e->host_hdr.begin == e->host_hdr.end;
+    traj_base = e->host_hdr.end;
+    traj_n = (int64_t)e->staged.size();
     const int64_t n = (int64_t)e->staged.size();
     if ((uint64_t)(e->host_hdr.end + n) > e->cfg.log_capacity) return fail(e, ZB_ENOMEM, "log capacity");
     if ((uint64_t)e->host_hdr.arena_next + e->staged_arena.size() > e->cfg.arena_bytes)
@@ -461,6 +586,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     e->host_hdr.arena_next += (int64_t)e->staged_arena.size();
     HIPCHECK(e, hipMemcpyAsync(e->hdr + (e->wave & 1), &e->host_hdr, sizeof(WaveHdr), hipMemcpyHostToDevice,
                                e->stream));
+    e->staged_pending = false;
   }
   const int64_t processed_from = e->host_hdr.begin;
   const int64_t written_from = e->host_hdr.end;
@@ -468,6 +594,11 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   HIPCHECK(e, hipMemcpy(stats_before, e->dstats, sizeof(stats_before), hipMemcpyDeviceToHost));
   uint32_t launched = 0;
   bool quiescent = e->host_hdr.begin == e->host_hdr.end;
+  if (try_traj && !quiescent) {
+    int rc = run_trajectory(e, traj_base, traj_n, st);
+    if (rc < 0) return rc;
+    quiescent = e->host_hdr.begin == e->host_hdr.end;
+  }
   while (!quiescent && (max_waves == 0 || launched < max_waves)) {
     int batch = WAVES_PER_SYNC;
     if (max_waves) batch = std::min<int>(batch, (int)(max_waves - launched));

@@ -144,4 +144,52 @@ struct InjectParams {
 
 void launch_inject(const InjectParams& p, hipStream_t stream);
 
+// ---- trajectory path (zb_traj.hip): a batch of CREATEs on an idle partition, run to quiescence
+constexpr int TRAJ_WG = 256;  // instances per workgroup (one per thread)
+constexpr int TR = 4;         // element instances per workflow instance held in registers
+constexpr int TF = 2;         // records per workflow instance per generation
+
+struct TrajCtl {
+  uint32_t flag;       // != 0: the count pass met something this path does not do -> wave path
+  uint32_t wmax;       // generations of the batch
+  uint64_t arena_next; // payload arena bump pointer (emit pass)
+  uint64_t rows_next;  // row allocator (live element instances at the end)
+  int64_t end, wf_next, job_next;  // log end and key generators after the batch (k_traj_base)
+  int64_t pad;
+};
+struct TrajBase {      // generation w: log position of its follow-ups, key generator values
+  int64_t pos, wf, job, pad;
+};
+
+struct TrajParams {
+  zb_rec* log;
+  uint8_t* arena;
+  RowMeta* rmeta;
+  RowKeys* rkeys;
+  const DevElem* elems;
+  const uint16_t* cond_flows;
+  const uint32_t* code;
+  const DevConst* consts;
+  const DevQuery* queries;
+  const DevFilter* filters;
+  const uint8_t* pool;
+  int64_t log_base, n;   // the batch: CREATE commands at [log_base, log_base + n)
+  int64_t wf_start, job_start;
+  int32_t nwg, wcap;     // workgroups, generations the count buffers hold
+  uint64_t* agg;         // [wcap][nwg] workgroup totals: records | wf keys << 16 | job keys << 32
+  uint32_t* wcount;      // [nwg] generations processed by each workgroup
+  uint4* woff;           // [wcap][nwg] exclusive prefix of agg over workgroups
+  uint4* wtot;           // [wcap] generation totals
+  TrajBase* wbase;       // [wcap]
+  TrajCtl* ctl;
+  WaveHdr* hdr;          // the partition's current wave header (committed at the end)
+  uint32_t* err;
+  uint64_t* stats;
+  uint64_t log_cap, row_cap, arena_cap;
+};
+
+void launch_traj_count(const TrajParams& p, hipStream_t stream);
+void launch_traj_scan(const TrajParams& p, hipStream_t stream);
+void launch_traj_emit(const TrajParams& p, hipStream_t stream);
+
 }  // namespace zbg

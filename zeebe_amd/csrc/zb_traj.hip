@@ -1,0 +1,761 @@
+// zb_traj.hip — run-to-quiescence of a batch of independent workflow instances ("trajectory" path).
+//
+// Why this is exact. The reference processes its log FIFO, one record at a time
+// (StreamProcessorController.java:296-414), so a batch of CREATE commands written to an idle
+// partition is processed in breadth-first generations, and inside a generation records are ordered
+// by their parent's position. By induction from generation 0 (the CREATEs, in instance order) every
+// generation is instance-major: instance i's records of generation g are contiguous and come after
+// those of instances < i. Workflow instances without message correlation never read each other's
+// state, so instance i's sequence of generations ("trajectory") depends only on its own records and
+// element instances. What couples instances is the log position and the keys: the partition's
+// KeyGenerator(1, 5) / job KeyGenerator(2, 5) (KeyGenerator.java:28-60) hand out keys in processing
+// order, so the key and position of a follow-up emitted while processing generation g are
+//     base(g) + (follow-ups emitted by instances < i in generation g) + (emission index).
+//
+// So one thread owns one instance and keeps its element instances and its current generation in
+// registers; the only cross-instance quantity is a per-(generation, workgroup) count:
+//   k_traj<false>   (count)  step every instance to quiescence; per generation write the
+//                            workgroup's (records, wf keys, job keys) totals.
+//   k_traj_scan              per generation: exclusive prefix of the workgroup totals.
+//   k_traj_base              prefix of the generation totals: absolute position / key bases.
+//   k_traj<true>    (emit)   step again; per generation a workgroup scan places every follow-up at
+//                            its final log position with its final keys; merges and condition
+//                            incidents write their payload blobs; live element instances are
+//                            written to the partition's SoA rows at the end.
+//   k_traj_commit            new wave header (log end, key generators, allocators).
+// The count pass writes nothing but the totals, so when an instance needs something this path does
+// not implement (more than TR element instances or TF records per generation, message
+// subscriptions, a processing failure) it raises a flag and the host runs the general wave path
+// (zb_wave.hip) on the same injected log instead — both are gfx950 kernels, nothing runs on the CPU.
+//
+// Handlers mirror bpmn_step/process_record in zb_wave.hip (same reference citations); the two paths
+// are checked against each other and the oracle by tests/test_gpu_parity.py.
+#include <hip/hip_runtime.h>
+
+#include "zb_devlib.hpp"
+#include "zb_kernels.hpp"
+
+namespace zbg {
+
+constexpr int TWG = TRAJ_WG;
+constexpr uint8_t LN = 0xff;  // no local row
+
+enum TrajFlags : uint8_t {
+  TK_WF = 1,         // key := new wf key #ord
+  TK_JOB = 2,        // key := new job key #ord
+  TK_INST = 4,       // the instance key := new wf key #ord (CREATE)
+  TK_ROW_INIT = 8,   // initialise rself as an ELEMENT_READY insert (ElementInstanceWriter.writeNewEvent)
+  TK_MERGED = 16,    // payload := this generation's merge result
+  TK_DETAIL = 32,    // payload := this generation's incident detail blob
+};
+
+// trajectory-path error bits (count pass -> host falls back to the wave path)
+enum TrajErr : uint32_t { TE_FALLBACK = 1u };
+
+struct TRec {
+  int64_t key, scope_key;
+  uint32_t payload;
+  uint16_t elem;
+  uint8_t intent, kind;
+  uint8_t rself, rscope, flags, ord;
+};
+
+template <class T, int N>
+__device__ __forceinline__ T sel(const T (&a)[N], int i) {
+  T v = a[0];
+#pragma unroll
+  for (int k = 1; k < N; k++)
+    if (i == k) v = a[k];
+  return v;
+}
+template <class T, int N>
+__device__ __forceinline__ void put(T (&a)[N], int i, T v) {
+#pragma unroll
+  for (int k = 0; k < N; k++)
+    if (i == k) a[k] = v;
+}
+
+// One workflow instance: its element instances (local rows) and its current generation.
+struct Inst {
+  int64_t rkey[TR], rsk[TR], rjob[TR];
+  uint32_t rpay[TR];
+  uint32_t rmeta[TR];  // elem | state << 16 | parent << 24
+  int32_t rnch[TR];
+  uint32_t used, to_free;
+  int64_t inst_key;
+  TRec cur[TF], nx[TF];
+  int nc, nn, nwf, njob;
+  // this generation's payload work: one merge and one incident detail at most
+  bool merge, detail;
+  uint32_t m_src, m_tgt, m_len;
+  uint8_t d_code, d_a, d_b;
+  uint16_t d_q;
+  int64_t d_pos;
+  uint32_t err;
+  // stats (emit pass)
+  uint32_t transitions, completed, created, merges, cond_bytes;
+  uint64_t merge_bytes;
+
+  __device__ __forceinline__ uint8_t state(int r) const { return (uint8_t)(sel(rmeta, r) >> 16); }
+  __device__ __forceinline__ uint16_t elem(int r) const { return (uint16_t)sel(rmeta, r); }
+  __device__ __forceinline__ uint8_t parent(int r) const { return (uint8_t)(sel(rmeta, r) >> 24); }
+  __device__ __forceinline__ bool alive(int r) const { return r != LN && state(r) != 0; }
+  __device__ __forceinline__ void set_state(int r, uint8_t s) {
+    put(rmeta, r, (sel(rmeta, r) & 0xff00ffffu) | ((uint32_t)s << 16));
+  }
+  __device__ __forceinline__ void set_meta(int r, uint16_t el, uint8_t st, uint8_t par) {
+    put(rmeta, r, (uint32_t)el | ((uint32_t)st << 16) | ((uint32_t)par << 24));
+  }
+  __device__ __forceinline__ int alloc() {
+    const uint32_t freebits = ~used & ((1u << TR) - 1);
+    if (!freebits) { err |= TE_FALLBACK; return LN; }
+    const int r = __builtin_ctz(freebits);
+    used |= 1u << r;
+    set_meta(r, NO_ELEM, 0, LN);
+    put(rnch, r, 0);
+    return r;
+  }
+  // ElementInstanceWriter: remove on a final state; the slot is reused from the next generation on
+  __device__ __forceinline__ void remove(int r) {
+    const int p = parent(r);
+    set_state(r, 0);
+    if (p != LN) put(rnch, p, sel(rnch, p) - 1);
+    to_free |= 1u << r;
+  }
+  __device__ __forceinline__ void push(const TRec& s) {
+    if (nn >= TF) { err |= TE_FALLBACK; return; }
+    put(nx, nn, s);
+    nn++;
+  }
+};
+
+__device__ __forceinline__ uint32_t arena_len(const uint8_t* arena, uint32_t ref) {
+  return *(const uint32_t*)(arena + (uint64_t)ref * 8);
+}
+__device__ __forceinline__ uint32_t tblob_bytes(uint32_t len) { return (4 + len + 7) & ~7u; }
+
+template <bool EMIT>
+__device__ void t_incident(Inst& I, const TRec& rec, int64_t pos, uint8_t code, uint8_t a, uint8_t b, uint16_t q) {
+  // BpmnStepContext.raiseIncident: IncidentIntent.CREATE command, key null, CONDITION_ERROR
+  TRec s;
+  s.key = -1;
+  s.scope_key = rec.key;  // activityInstanceKey = failing record's key
+  s.payload = 0;
+  s.elem = rec.elem;
+  s.intent = 0;
+  s.kind = make_kind(ZB_VT_INCIDENT, ZB_RT_COMMAND, I.nn > 0);
+  s.rself = LN; s.rscope = LN; s.flags = TK_DETAIL; s.ord = 0;
+  if (I.detail) { I.err |= TE_FALLBACK; return; }
+  I.detail = true;
+  I.d_code = code; I.d_a = a; I.d_b = b; I.d_q = q; I.d_pos = pos;
+  I.push(s);
+}
+
+// bpmn_step (zb_wave.hip) on local rows: BpmnStepProcessor.java:92-251 guards + step handlers
+template <bool EMIT>
+__device__ void t_step(const TrajParams& P, Inst& I, const TRec& rec, int64_t pos) {
+  const uint8_t intent = rec.intent;
+  const bool stateless = intent == WI_SEQUENCE_FLOW_TAKEN || intent == WI_START_EVENT_OCCURRED ||
+                         intent == WI_END_EVENT_OCCURRED || intent == WI_GATEWAY_ACTIVATED;
+  const int rself = rec.rself, rscope = rec.rscope;
+  const bool self_alive = !stateless && I.alive(rself);
+  const bool scope_alive = I.alive(rscope);
+  if (!self_alive && !scope_alive) return;  // BpmnStepProcessor.java:244-247
+  bool ok;
+  switch (intent) {
+    case WI_ELEMENT_READY: case WI_ELEMENT_ACTIVATED: case WI_ELEMENT_COMPLETING:
+      if (!self_alive) { I.err |= TE_FALLBACK; return; }
+      ok = I.state(rself) == intent;
+      break;
+    case WI_ELEMENT_COMPLETED: case WI_END_EVENT_OCCURRED: case WI_GATEWAY_ACTIVATED:
+    case WI_START_EVENT_OCCURRED: case WI_SEQUENCE_FLOW_TAKEN:
+      ok = scope_alive && I.state(rscope) == WI_ELEMENT_ACTIVATED;
+      break;
+    case WI_ELEMENT_TERMINATING: ok = true; break;
+    case WI_ELEMENT_TERMINATED: ok = scope_alive && I.state(rscope) == WI_ELEMENT_TERMINATING; break;
+    default: ok = false;
+  }
+  if (!ok) return;
+  if (rec.elem == NO_ELEM) { I.err |= TE_FALLBACK; return; }
+  const DevElem& el = P.elems[rec.elem];
+  const uint8_t step = el.step[intent];
+  if (step == ST_UNBOUND || step == ST_NONE) return;
+
+  TRec s = rec;
+  s.flags = 0; s.ord = 0;
+  switch (step) {
+    case ST_APPLY_INPUT_MAPPING: {  // InputMappingHandler (no io mappings)
+      s.intent = WI_ELEMENT_ACTIVATED;
+      s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
+      I.set_state(rself, WI_ELEMENT_ACTIVATED);
+      put(I.rpay, rself, rec.payload);
+      I.push(s);
+      break;
+    }
+    case ST_APPLY_OUTPUT_MAPPING: {  // OutputMappingHandler :42-85, outputBehavior null -> merge
+      if (!scope_alive || I.merge) { I.err |= TE_FALLBACK; return; }
+      I.merge = true;
+      I.m_src = rec.payload;
+      I.m_tgt = sel(I.rpay, rscope);
+      if (EMIT) I.m_len = arena_len(P.arena, I.m_src) + arena_len(P.arena, I.m_tgt) + 8;
+      s.intent = WI_ELEMENT_COMPLETED;
+      s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
+      s.flags = TK_MERGED;
+      s.rself = LN;
+      I.remove(rself);
+      I.push(s);
+      break;
+    }
+    case ST_CREATE_JOB: {  // CreateJobHandler :33-56 -> JOB CREATE command, key null
+      s.key = -1;
+      s.scope_key = rec.key;  // headers.activityInstanceKey
+      s.intent = JI_CREATE;
+      s.kind = make_kind(ZB_VT_JOB, ZB_RT_COMMAND, I.nn > 0);
+      I.push(s);
+      break;
+    }
+    case ST_EXCLUSIVE_SPLIT: {  // ExclusiveSplitHandler :38-71 (first true condition, else default)
+      const uint8_t* pp = P.arena + (uint64_t)rec.payload * 8;
+      const uint32_t len = *(const uint32_t*)pp;
+      uint16_t chosen = NO_ELEM;
+      CondOut co{0, 0, 0, 0};
+      bool unsup = false;
+      for (uint32_t c = 0; c < el.cond_count; c++) {
+        const uint16_t flow = P.cond_flows[el.cond_begin + c];
+        const bool res = eval_condition(P.elems[flow].cond_prog, P.code, pp + 4, len, P.consts, P.queries,
+                                        P.filters, P.pool, co, unsup);
+        if (unsup || co.err) break;
+        if (res) { chosen = flow; break; }
+      }
+      I.cond_bytes += len;
+      if (unsup) { I.err |= TE_FALLBACK; return; }
+      if (co.err) { t_incident<EMIT>(I, rec, pos, co.err & 7, co.a & 15, co.b & 15, co.q); break; }
+      if (chosen == NO_ELEM) chosen = el.dflt;
+      if (chosen == NO_ELEM) { t_incident<EMIT>(I, rec, pos, EC_NO_FLOW, 0, 0, 0); break; }
+      s.elem = chosen;
+      s.intent = WI_SEQUENCE_FLOW_TAKEN;
+      s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
+      s.flags = TK_WF; s.ord = (uint8_t)I.nwf++;
+      s.rself = LN;
+      I.push(s);
+      break;
+    }
+    case ST_CONSUME_TOKEN: {  // ConsumeTokenHandler :30-43
+      if (!scope_alive) { I.err |= TE_FALLBACK; return; }
+      s.key = sel(I.rkey, rscope);
+      s.scope_key = sel(I.rsk, rscope);
+      s.elem = I.elem(rscope);
+      s.payload = rec.payload;
+      s.intent = WI_ELEMENT_COMPLETING;
+      s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
+      s.rself = (uint8_t)rscope;
+      s.rscope = I.parent(rscope);
+      I.set_state(rscope, WI_ELEMENT_COMPLETING);
+      put(I.rpay, rscope, rec.payload);
+      I.push(s);
+      break;
+    }
+    case ST_TAKE_SEQUENCE_FLOW:
+    case ST_ACTIVATE_GATEWAY:
+    case ST_TRIGGER_END_EVENT: {
+      uint8_t out_intent;
+      if (step == ST_TAKE_SEQUENCE_FLOW) { s.elem = el.out0; out_intent = WI_SEQUENCE_FLOW_TAKEN; }
+      else if (step == ST_ACTIVATE_GATEWAY) { s.elem = el.target; out_intent = WI_GATEWAY_ACTIVATED; }
+      else { s.elem = el.target; out_intent = WI_END_EVENT_OCCURRED; }
+      if (s.elem == NO_ELEM) { I.err |= TE_FALLBACK; return; }
+      s.intent = out_intent;
+      s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
+      s.flags = TK_WF; s.ord = (uint8_t)I.nwf++;
+      s.rself = LN;
+      I.push(s);
+      break;
+    }
+    case ST_START_STATEFUL_ELEMENT: {  // -> ELEMENT_READY(new key), index insert with parent = scope
+      const int row = I.alloc();
+      if (row == LN) return;
+      s.elem = el.target;
+      s.intent = WI_ELEMENT_READY;
+      s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
+      s.flags = TK_WF | TK_ROW_INIT; s.ord = (uint8_t)I.nwf++;
+      s.rself = (uint8_t)row;
+      s.rscope = scope_alive ? (uint8_t)rscope : LN;
+      if (scope_alive) put(I.rnch, rscope, sel(I.rnch, rscope) + 1);
+      I.push(s);
+      break;
+    }
+    case ST_TRIGGER_START_EVENT: {  // TriggerStartEventHandler :30-39
+      if (el.start == NO_ELEM) { I.err |= TE_FALLBACK; return; }
+      s.elem = el.start;
+      s.scope_key = rec.key;
+      s.intent = WI_START_EVENT_OCCURRED;
+      s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
+      s.flags = TK_WF; s.ord = (uint8_t)I.nwf++;
+      s.rscope = (uint8_t)rself;
+      s.rself = LN;
+      I.push(s);
+      break;
+    }
+    case ST_COMPLETE_PROCESS: {  // CompleteProcessHandler :28-35
+      s.intent = WI_ELEMENT_COMPLETED;
+      s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
+      s.rself = LN;
+      I.remove(rself);
+      if (EMIT && rec.key == I.inst_key) I.completed += 1;
+      I.push(s);
+      break;
+    }
+    default:  // message subscriptions, termination: general wave path
+      I.err |= TE_FALLBACK;
+      break;
+  }
+}
+
+// process_record (zb_wave.hip) on local rows
+template <bool EMIT>
+__device__ void t_record(const TrajParams& P, Inst& I, const TRec& rec, int64_t pos) {
+  const uint8_t vt = kind_vt(rec.kind), rt = kind_rt(rec.kind);
+  if (vt == ZB_VT_WORKFLOW_INSTANCE) {
+    if (rt == ZB_RT_COMMAND) {
+      if (rec.intent != WI_CREATE) { I.err |= TE_FALLBACK; return; }
+      // CreateWorkflowInstanceEventProcessor :233-368: key first, then resolve (done at submit)
+      const uint8_t ord = (uint8_t)I.nwf++;
+      TRec s = rec;
+      s.ord = ord;
+      if (rec.elem == NO_ELEM) {
+        s.scope_key = pos;  // command position -> the serializer finds the submitted command value
+        s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_COMMAND_REJECTION, I.nn > 0);
+        s.flags = TK_INST;
+        s.rself = LN; s.rscope = LN;
+        I.push(s);
+        return;
+      }
+      const int row = I.alloc();  // inserted when CREATED is processed
+      if (row == LN) return;
+      s.scope_key = -1;
+      s.flags = TK_WF | TK_INST;
+      s.rself = (uint8_t)row; s.rscope = LN;
+      s.intent = WI_CREATED;
+      s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
+      I.push(s);
+      s.intent = WI_ELEMENT_READY;
+      s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
+      I.push(s);
+    } else if (rt == ZB_RT_EVENT) {
+      if (rec.intent == WI_CREATED) {  // WorkflowInstanceCreatedEventProcessor: index insert (READY)
+        const int r = rec.rself;
+        if (r == LN) { I.err |= TE_FALLBACK; return; }
+        I.set_meta(r, rec.elem, WI_ELEMENT_READY, LN);
+        put(I.rpay, r, rec.payload);
+        put(I.rkey, r, rec.key);
+        put(I.rsk, r, rec.scope_key);
+        put(I.rjob, r, (int64_t)0);
+        put(I.rnch, r, 0);
+        I.created += 1;
+      } else if (rec.intent <= WI_ELEMENT_TERMINATED && rec.intent >= WI_START_EVENT_OCCURRED) {
+        t_step<EMIT>(P, I, rec, pos);
+      }
+    }
+  } else if (vt == ZB_VT_JOB) {
+    if (rt == ZB_RT_COMMAND && rec.intent == JI_CREATE) {
+      // canonical harness: JOB CREATED(k), JOB COMPLETED(k), k from the job key generator
+      const uint8_t ord = (uint8_t)I.njob++;
+      TRec s = rec;
+      s.flags = TK_JOB; s.ord = ord;
+      s.intent = JI_CREATED;
+      s.kind = make_kind(ZB_VT_JOB, ZB_RT_EVENT, I.nn > 0);
+      I.push(s);
+      s.intent = JI_COMPLETED;
+      s.kind = make_kind(ZB_VT_JOB, ZB_RT_EVENT, I.nn > 0);
+      s.payload = P.elems[rec.elem].job_payload;
+      I.push(s);
+    } else if (rt == ZB_RT_EVENT && rec.intent == JI_CREATED) {  // JobCreatedProcessor :408-426
+      if (rec.scope_key > 0 && I.alive(rec.rself)) put(I.rjob, (int)rec.rself, rec.key);
+    } else if (rt == ZB_RT_EVENT && rec.intent == JI_COMPLETED) {  // JobCompletedEventProcessor :428-453
+      const int r = rec.rself;
+      if (!I.alive(r)) return;
+      TRec s;
+      s.key = rec.scope_key;
+      s.scope_key = sel(I.rsk, r);
+      s.elem = I.elem(r);
+      s.payload = rec.payload;
+      s.intent = WI_ELEMENT_COMPLETING;
+      s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
+      s.rself = (uint8_t)r;
+      s.rscope = I.parent(r);
+      s.flags = 0; s.ord = 0;
+      I.set_state(r, WI_ELEMENT_COMPLETING);
+      put(I.rpay, r, rec.payload);
+      put(I.rjob, r, (int64_t)-1);
+      I.push(s);
+    }
+  }
+  // other value types (incident commands): not registered on the workflow stream processor
+}
+
+// ------------------------------------------------------------------------------ workgroup scans
+__device__ __forceinline__ uint64_t tshfl_up(uint64_t v, int d) {
+  return (uint64_t)__shfl_up((unsigned long long)v, d, 64);
+}
+
+// exclusive scan of (a, b) over the 256 threads of the workgroup; returns the totals in ta / tb
+__device__ __forceinline__ void block_scan2(uint64_t& a, uint64_t& b, uint64_t& ta, uint64_t& tb,
+                                            uint64_t (*s)[2]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t a0 = a, b0 = b;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t ua = tshfl_up(a, d), ub = tshfl_up(b, d);
+    if (lane >= d) { a += ua; b += ub; }
+  }
+  if (lane == 63) { s[wv][0] = a; s[wv][1] = b; }
+  __syncthreads();
+  ta = 0; tb = 0;
+#pragma unroll
+  for (int k = 0; k < TWG / 64; k++) {
+    const uint64_t xa = s[k][0], xb = s[k][1];
+    if (k < wv) { a += xa; b += xb; }
+    ta += xa; tb += xb;
+  }
+  a -= a0;
+  b -= b0;
+  __syncthreads();  // s reused by the next call
+}
+
+// ------------------------------------------------------------------------------ k_traj
+template <bool EMIT>
+__global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
+  __shared__ uint64_t s_scan[TWG / 64][2];
+  __shared__ uint64_t s_abase;
+  TrajCtl* ctl = P.ctl;
+  if (EMIT && ctl->flag) return;
+  const int64_t inst = (int64_t)blockIdx.x * TWG + threadIdx.x;
+  const int nwg = gridDim.x;
+
+  Inst I;
+  I.used = 0; I.to_free = 0;
+#pragma unroll
+  for (int k = 0; k < TR; k++) {
+    I.rkey[k] = 0; I.rsk[k] = 0; I.rjob[k] = 0; I.rpay[k] = 0; I.rmeta[k] = 0; I.rnch[k] = 0;
+  }
+  I.inst_key = -1;
+  I.nc = 0; I.nn = 0; I.nwf = 0; I.njob = 0;
+  I.merge = false; I.detail = false; I.m_src = I.m_tgt = I.m_len = 0;
+  I.d_code = I.d_a = I.d_b = 0; I.d_q = 0; I.d_pos = 0;
+  I.err = 0;
+  I.transitions = I.completed = I.created = I.merges = I.cond_bytes = 0;
+  I.merge_bytes = 0;
+  int64_t fpos = P.log_base + inst;  // log position of the first record of the current generation
+  if (inst < P.n) {
+    const zb_rec d = P.log[fpos];
+    TRec r;
+    r.key = d.key; r.scope_key = d.scope_key; r.payload = d.payload; r.elem = d.elem; r.intent = d.intent;
+    r.kind = d.kind; r.rself = LN; r.rscope = LN; r.flags = 0; r.ord = 0;
+    I.cur[0] = r;
+    I.nc = 1;
+  }
+#pragma unroll
+  for (int k = 1; k < TF; k++) I.cur[k] = I.cur[0];
+
+  int w = 0;
+  while (__syncthreads_or(I.nc > 0)) {
+    if (w >= P.wcap) {  // more generations than the count buffers hold
+      if (!EMIT && threadIdx.x == 0) atomicOr(&ctl->flag, TE_FALLBACK);
+      return;
+    }
+    // ---- process this generation (log order inside the instance)
+#pragma unroll
+    for (int k = 0; k < TF; k++)
+      if (k < I.nc) t_record<EMIT>(P, I, I.cur[k], fpos + k);
+    // ---- place the follow-ups
+    uint64_t a = (uint64_t)I.nn | ((uint64_t)I.nwf << 16) | ((uint64_t)I.njob << 32);
+    uint64_t bytes = 0;
+    if (EMIT) bytes = (I.merge ? tblob_bytes(I.m_len) : 0) + (I.detail ? 24 : 0);
+    uint64_t ta, tb;
+    block_scan2(a, bytes, ta, tb, s_scan);
+    int64_t pos0, kwf, kjob;
+    if (!EMIT) {
+      if (threadIdx.x == 0) P.agg[(uint64_t)w * nwg + blockIdx.x] = ta;
+      pos0 = 0;
+      kwf = 1 + 5 * (int64_t)((a >> 16) & 0xffff);
+      kjob = 2 + 5 * (int64_t)(a >> 32);
+    } else {
+      const TrajBase wb = P.wbase[w];
+      const uint4 off = P.woff[(uint64_t)w * nwg + blockIdx.x];
+      pos0 = wb.pos + off.x + (int64_t)(a & 0xffff);
+      kwf = wb.wf + 5 * ((int64_t)off.y + (int64_t)((a >> 16) & 0xffff));
+      kjob = wb.job + 5 * ((int64_t)off.z + (int64_t)(a >> 32));
+      if (tb) {
+        if (threadIdx.x == 0) s_abase = atomicAdd((unsigned long long*)&ctl->arena_next, (unsigned long long)tb);
+        __syncthreads();
+      }
+    }
+    uint32_t merged_ref = 0, detail_ref = 0;
+    if (EMIT && (I.merge || I.detail)) {
+      uint64_t at = s_abase + bytes;
+      if (I.merge) {
+        const uint32_t mb = tblob_bytes(I.m_len);
+        if (at + mb > P.arena_cap) I.err |= DE_ARENA_FULL;
+        else {
+          const uint8_t* sp = P.arena + (uint64_t)I.m_src * 8;
+          const uint8_t* tp = P.arena + (uint64_t)I.m_tgt * 8;
+          const uint32_t ns = *(const uint32_t*)sp, nt = *(const uint32_t*)tp;
+          uint8_t* dst = P.arena + at;
+          Out o{dst + 4, 0};
+          bool unsup = false;
+          if (!merge_docs(sp + 4, ns, tp + 4, nt, o, unsup)) I.err |= DE_BAD_PAYLOAD;
+          else if (unsup || o.n > I.m_len) I.err |= DE_UNSUPPORTED;
+          *(uint32_t*)dst = o.n;
+          merged_ref = (uint32_t)(at >> 3);
+          I.merges += 1;
+          I.merge_bytes += ns + nt + o.n;
+        }
+        at += mb;
+      }
+      if (I.detail) {
+        if (at + 24 > P.arena_cap) I.err |= DE_ARENA_FULL;
+        else {
+          detail_ref = (uint32_t)(at >> 3);
+          uint8_t* dst = P.arena + at;
+          *(uint32_t*)dst = 16;
+          dst[4] = 3;  // CONDITION_ERROR
+          dst[5] = I.d_code; dst[6] = I.d_a; dst[7] = I.d_b;
+          *(uint16_t*)(dst + 8) = I.d_q;
+          *(int64_t*)(dst + 16) = I.d_pos;
+        }
+      }
+    }
+    // keys, row inserts, log writes
+#pragma unroll
+    for (int k = 0; k < TF; k++) {
+      if (k < I.nn) {
+        TRec s = I.nx[k];
+        if (s.flags & TK_WF) s.key = kwf + 5 * (int64_t)s.ord;
+        if (s.flags & TK_JOB) s.key = kjob + 5 * (int64_t)s.ord;
+        if (s.flags & TK_INST) I.inst_key = kwf + 5 * (int64_t)s.ord;
+        if (s.flags & TK_MERGED) s.payload = merged_ref;
+        if (s.flags & TK_DETAIL) s.payload = detail_ref;
+        if (s.flags & TK_ROW_INIT) {
+          const int r = s.rself;
+          I.set_meta(r, s.elem, WI_ELEMENT_READY, s.rscope);
+          put(I.rpay, r, s.payload);
+          put(I.rkey, r, s.key);
+          put(I.rsk, r, s.scope_key);
+          put(I.rjob, r, (int64_t)0);
+          put(I.rnch, r, 0);
+        }
+        s.flags = 0;
+        I.cur[k] = s;
+        if (EMIT) {
+          zb_rec d;
+          d.key = s.key; d.scope_key = s.scope_key; d.inst_key = I.inst_key; d.payload = s.payload;
+          d.elem = s.elem; d.intent = s.intent; d.kind = s.kind;
+          if (pos0 + k < (int64_t)P.log_cap) P.log[pos0 + k] = d;
+          else I.err |= DE_LOG_FULL;
+          if (kind_vt(s.kind) == ZB_VT_WORKFLOW_INSTANCE && kind_rt(s.kind) == ZB_RT_EVENT) I.transitions++;
+        }
+      }
+    }
+    fpos = pos0;
+    I.nc = I.nn;
+    I.nn = 0; I.nwf = 0; I.njob = 0;
+    I.merge = false; I.detail = false;
+    I.used &= ~I.to_free;
+    I.to_free = 0;
+    w++;
+  }
+
+  if (!EMIT) {
+    if (threadIdx.x == 0) {
+      P.wcount[blockIdx.x] = (uint32_t)w;
+      atomicMax(&ctl->wmax, (uint32_t)w);
+    }
+    if (I.err) atomicOr(&ctl->flag, TE_FALLBACK);
+    return;
+  }
+
+  // ---- live element instances -> partition rows (instances stopped by an incident keep theirs)
+  uint32_t live = 0;
+#pragma unroll
+  for (int k = 0; k < TR; k++)
+    if (((I.used >> k) & 1) && I.alive(k)) live |= 1u << k;
+  uint64_t a = (uint64_t)__builtin_popcount(live), bz = 0, ta, tb;
+  block_scan2(a, bz, ta, tb, s_scan);
+  if (ta) {
+    if (threadIdx.x == 0) s_abase = atomicAdd((unsigned long long*)&ctl->rows_next, (unsigned long long)ta);
+    __syncthreads();
+    const uint64_t r0 = s_abase + a;
+    uint32_t gid[TR];
+    uint32_t n = 0;
+#pragma unroll
+    for (int k = 0; k < TR; k++) {
+      gid[k] = NO_ROW;
+      if ((live >> k) & 1) gid[k] = (uint32_t)(r0 + n++);
+    }
+#pragma unroll
+    for (int k = 0; k < TR; k++) {
+      if (!((live >> k) & 1)) continue;
+      if (gid[k] >= P.row_cap) { I.err |= DE_ROWS_FULL; continue; }
+      const uint32_t meta = I.rmeta[k];
+      const int par = (int)(meta >> 24);
+      RowMeta m;
+      m.payload = I.rpay[k];
+      m.parent = par == LN ? NO_ROW : sel(gid, par);
+      m.elem = (uint16_t)meta;
+      m.state = (uint8_t)(meta >> 16);
+      m.flags = 0;
+      m.nchild = I.rnch[k];
+      P.rmeta[gid[k]] = m;
+      P.rkeys[gid[k]] = RowKeys{I.rkey[k], I.rsk[k], I.inst_key, I.rjob[k]};
+    }
+  }
+  // ---- statistics
+  uint64_t s0 = (uint64_t)I.transitions | ((uint64_t)I.completed << 32);
+  uint64_t s1 = (uint64_t)I.created | ((uint64_t)I.merges << 32);
+  block_scan2(s0, s1, ta, tb, s_scan);
+  uint64_t s2 = I.merge_bytes, s3 = I.cond_bytes, tc, td;
+  block_scan2(s2, s3, tc, td, s_scan);
+  if (threadIdx.x == 0) {
+    atomicAdd((unsigned long long*)&P.stats[0], (unsigned long long)(ta & 0xffffffffu));
+    atomicAdd((unsigned long long*)&P.stats[1], (unsigned long long)(ta >> 32));
+    atomicAdd((unsigned long long*)&P.stats[2], (unsigned long long)(tb & 0xffffffffu));
+    atomicAdd((unsigned long long*)&P.stats[3], (unsigned long long)(tb >> 32));
+    atomicAdd((unsigned long long*)&P.stats[4], (unsigned long long)tc);
+    atomicAdd((unsigned long long*)&P.stats[5], (unsigned long long)td);
+  }
+  const uint32_t derr = I.err & ~(uint32_t)TE_FALLBACK;
+  if (I.err & TE_FALLBACK) atomicOr(P.err, DE_PROCESSING);  // count and emit passes disagree: cannot happen
+  if (derr) atomicOr(P.err, derr);
+}
+
+// ------------------------------------------------------------------------------ scans
+// one workgroup per generation w: exclusive prefix over workgroups of agg[w][.]
+__global__ void __launch_bounds__(1024) k_traj_scan(TrajParams P) {
+  __shared__ uint64_t s_w[16][3];
+  const TrajCtl* ctl = P.ctl;
+  const uint32_t w = blockIdx.x;
+  if (ctl->flag || w >= ctl->wmax) return;
+  const int nwg = P.nwg;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t carry[3] = {0, 0, 0};
+  for (int base = 0; base < nwg; base += 1024) {
+    const int b = base + threadIdx.x;
+    uint64_t v = 0;
+    if (b < nwg && w < P.wcount[b]) v = P.agg[(uint64_t)w * nwg + b];
+    uint64_t x[3] = {v & 0xffff, (v >> 16) & 0xffff, v >> 32};
+    uint64_t ex[3];
+#pragma unroll
+    for (int f = 0; f < 3; f++) {
+      uint64_t y = x[f];
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t u = tshfl_up(y, d);
+        if (lane >= d) y += u;
+      }
+      ex[f] = y - x[f];
+      if (lane == 63) s_w[wv][f] = y;
+    }
+    __syncthreads();
+    uint64_t tot[3] = {0, 0, 0};
+#pragma unroll
+    for (int f = 0; f < 3; f++) {
+      for (int k = 0; k < 16; k++) {
+        if (k < wv) ex[f] += s_w[k][f];
+        tot[f] += s_w[k][f];
+      }
+      ex[f] += carry[f];
+    }
+    if (b < nwg) P.woff[(uint64_t)w * nwg + b] = make_uint4((uint32_t)ex[0], (uint32_t)ex[1], (uint32_t)ex[2], 0);
+#pragma unroll
+    for (int f = 0; f < 3; f++) carry[f] += tot[f];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) P.wtot[w] = make_uint4((uint32_t)carry[0], (uint32_t)carry[1], (uint32_t)carry[2], 0);
+}
+
+// one workgroup: generation bases (log position of generation w+1, key generator values at w)
+__global__ void __launch_bounds__(1024) k_traj_base(TrajParams P) {
+  __shared__ uint64_t s_w[16][3];
+  __shared__ uint64_t s_carry[3];
+  TrajCtl* ctl = P.ctl;
+  if (ctl->flag) return;
+  const uint32_t W = ctl->wmax;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x < 3) s_carry[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < W; base += 1024) {
+    const uint32_t w = base + threadIdx.x;
+    uint64_t x[3] = {0, 0, 0};
+    if (w < W) {
+      const uint4 t = P.wtot[w];
+      x[0] = t.x; x[1] = t.y; x[2] = t.z;
+    }
+    uint64_t ex[3];
+#pragma unroll
+    for (int f = 0; f < 3; f++) {
+      uint64_t y = x[f];
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t u = tshfl_up(y, d);
+        if (lane >= d) y += u;
+      }
+      ex[f] = y - x[f];
+      if (lane == 63) s_w[wv][f] = y;
+    }
+    __syncthreads();
+    uint64_t tot[3] = {0, 0, 0};
+#pragma unroll
+    for (int f = 0; f < 3; f++) {
+      for (int k = 0; k < 16; k++) {
+        if (k < wv) ex[f] += s_w[k][f];
+        tot[f] += s_w[k][f];
+      }
+      ex[f] += s_carry[f];
+    }
+    if (w < W) {
+      TrajBase b;
+      b.pos = P.log_base + P.n + (int64_t)ex[0];
+      b.wf = P.wf_start + 5 * (int64_t)ex[1];
+      b.job = P.job_start + 5 * (int64_t)ex[2];
+      b.pad = 0;
+      P.wbase[w] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) s_carry[threadIdx.x] += tot[threadIdx.x];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    ctl->end = P.log_base + P.n + (int64_t)s_carry[0];
+    ctl->wf_next = P.wf_start + 5 * (int64_t)s_carry[1];
+    ctl->job_next = P.job_start + 5 * (int64_t)s_carry[2];
+    if ((uint64_t)ctl->end > P.log_cap) ctl->flag |= TE_FALLBACK;  // the wave path reports the capacity error
+  }
+}
+
+__global__ void k_traj_commit(TrajParams P) {
+  const TrajCtl* ctl = P.ctl;
+  if (ctl->flag) return;
+  WaveHdr h = *P.hdr;
+  h.begin = h.end = h.gen_end = ctl->end;
+  h.wf_next = ctl->wf_next;
+  h.job_next = ctl->job_next;
+  h.rows_next = (int64_t)ctl->rows_next;
+  h.arena_next = (int64_t)ctl->arena_next;
+  *P.hdr = h;
+  P.stats[6] += ctl->wmax;
+  if ((uint64_t)ctl->rows_next > P.row_cap) atomicOr(P.err, (uint32_t)DE_ROWS_FULL);
+  if ((uint64_t)ctl->arena_next > P.arena_cap) atomicOr(P.err, (uint32_t)DE_ARENA_FULL);
+}
+
+void launch_traj_count(const TrajParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_traj<false>, dim3(p.nwg), dim3(TWG), 0, s, p);
+}
+void launch_traj_scan(const TrajParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_traj_scan, dim3(p.wcap), dim3(1024), 0, s, p);
+  hipLaunchKernelGGL(k_traj_base, dim3(1), dim3(1024), 0, s, p);
+}
+void launch_traj_emit(const TrajParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_traj<true>, dim3(p.nwg), dim3(TWG), 0, s, p);
+  hipLaunchKernelGGL(k_traj_commit, dim3(1), dim3(1), 0, s, p);
+}
+
+}  // namespace zbg

@@ -13,6 +13,8 @@ from typing import List, NamedTuple, Optional, Sequence
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libzbgpu.so")
 
+CFG_WAVE_ONLY = 1  # zb_config.flags: never take the trajectory path
+
 ZB_OK, ZB_EINVAL, ZB_ENOMEM, ZB_EUNSUPPORTED, ZB_EDEPLOY, ZB_EDEVICE, ZB_EAGAIN, ZB_EPROCESSING = \
     0, -1, -2, -3, -4, -5, -6, -7
 _NAMES = {0: "ZB_OK", -1: "ZB_EINVAL", -2: "ZB_ENOMEM", -3: "ZB_EUNSUPPORTED", -4: "ZB_EDEPLOY",
@@ -27,7 +29,7 @@ class ZbError(RuntimeError):
 
 class zb_config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("partition_id", ctypes.c_int32),
-                ("partition_count", ctypes.c_int32), ("reserved0", ctypes.c_int32),
+                ("partition_count", ctypes.c_int32), ("flags", ctypes.c_int32),
                 ("log_capacity", ctypes.c_uint64), ("row_capacity", ctypes.c_uint64),
                 ("arena_bytes", ctypes.c_uint64), ("wave_records", ctypes.c_uint64)]
 
@@ -52,7 +54,8 @@ class zb_step_stats(ctypes.Structure):
                 ("merges", ctypes.c_uint64), ("merge_bytes", ctypes.c_uint64),
                 ("condition_payload_bytes", ctypes.c_uint64), ("wave_kernel_ms", ctypes.c_double),
                 ("wall_ms", ctypes.c_double), ("process_kernel_ms", ctypes.c_double),
-                ("emit_kernel_ms", ctypes.c_double), ("aux_kernel_ms", ctypes.c_double)]
+                ("emit_kernel_ms", ctypes.c_double), ("aux_kernel_ms", ctypes.c_double),
+                ("path", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -110,10 +113,10 @@ class Engine:
 
     def __init__(self, device: int = 0, partition_id: int = 0, partition_count: int = 1,
                  log_capacity: int = 1 << 22, row_capacity: int = 1 << 20, arena_bytes: int = 64 << 20,
-                 wave_records: int = 0):
+                 wave_records: int = 0, wave_only: bool = False):
         self._L = lib()
-        cfg = zb_config(device, partition_id, partition_count, 0, log_capacity, row_capacity, arena_bytes,
-                        wave_records)
+        cfg = zb_config(device, partition_id, partition_count, CFG_WAVE_ONLY if wave_only else 0, log_capacity,
+                        row_capacity, arena_bytes, wave_records)
         h = ctypes.c_void_p()
         rc = self._L.zb_engine_create(ctypes.byref(cfg), ctypes.byref(h))
         if rc != ZB_OK:
