@@ -106,13 +106,16 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    tot = dict(transitions=0, completed=0, kernel_ms=0.0, launches=0, waves=0, merge_bytes=0, cond_bytes=0,
+    tot = dict(transitions=0, completed=0, kernel_ms=0.0, process_ms=0.0, emit_ms=0.0, aux_ms=0.0, launches=0, waves=0, merge_bytes=0, cond_bytes=0,
                records=0, path=0)
     for _ in range(a.steps):
         st = one_step()
         tot["transitions"] += st["transitions"]
         tot["completed"] += st["completed_instances"]
         tot["kernel_ms"] += st["wave_kernel_ms"]
+        tot["process_ms"] += st["process_kernel_ms"]
+        tot["emit_ms"] += st["emit_kernel_ms"]
+        tot["aux_ms"] += st["aux_kernel_ms"]
         tot["launches"] += st["launches"]
         tot["waves"] += st["waves"]
         tot["merge_bytes"] += st["merge_bytes"]
@@ -158,6 +161,8 @@ def main():
             "completed_instances_per_s": all_completed / elapsed,
             "records_processed_per_step_rank0": tot["records"] / a.steps,
             "wave_launches_per_step": tot["launches"] / a.steps,
+            "kernel_ms_per_step": {"total": tot["kernel_ms"] / a.steps, "process_or_count": tot["process_ms"] / a.steps,
+                                   "scan_emit": tot["emit_ms"] / a.steps, "aux": tot["aux_ms"] / a.steps},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": "zbg::k_traj (count + emit passes)" if tot["path"] == 1 else

@@ -60,30 +60,44 @@ struct TRec {
   uint8_t rself, rscope, flags, ord;
 };
 
-template <class T, int N>
-__device__ __forceinline__ T sel(const T (&a)[N], int i) {
-  T v = a[0];
-#pragma unroll
-  for (int k = 1; k < N; k++)
-    if (i == k) v = a[k];
-  return v;
-}
-template <class T, int N>
-__device__ __forceinline__ void put(T (&a)[N], int i, T v) {
-#pragma unroll
-  for (int k = 0; k < N; k++)
-    if (i == k) a[k] = v;
-}
+// Per-instance state lives in ext-vector registers: a dynamic index becomes an extract / insert
+// element (selects), never an address, so nothing is spilled to scratch.
+typedef int64_t i64x4 __attribute__((ext_vector_type(TR)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(TR)));
+typedef int32_t i32x4 __attribute__((ext_vector_type(TR)));
+typedef int64_t i64x2 __attribute__((ext_vector_type(TF)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(TF)));
+
+// One generation of one instance (<= TF records), structure of vectors
+struct Gen {
+  i64x2 key, sk;
+  u32x2 pay;
+  u32x2 m0;  // elem | intent << 16 | kind << 24
+  u32x2 m1;  // rself | rscope << 8 | flags << 16 | ord << 24
+  __device__ __forceinline__ TRec get(int k) const {
+    TRec r;
+    r.key = key[k]; r.scope_key = sk[k]; r.payload = pay[k];
+    const uint32_t a = m0[k], b = m1[k];
+    r.elem = (uint16_t)a; r.intent = (uint8_t)(a >> 16); r.kind = (uint8_t)(a >> 24);
+    r.rself = (uint8_t)b; r.rscope = (uint8_t)(b >> 8); r.flags = (uint8_t)(b >> 16); r.ord = (uint8_t)(b >> 24);
+    return r;
+  }
+  __device__ __forceinline__ void set(int k, const TRec& r) {
+    key[k] = r.key; sk[k] = r.scope_key; pay[k] = r.payload;
+    m0[k] = (uint32_t)r.elem | ((uint32_t)r.intent << 16) | ((uint32_t)r.kind << 24);
+    m1[k] = (uint32_t)r.rself | ((uint32_t)r.rscope << 8) | ((uint32_t)r.flags << 16) | ((uint32_t)r.ord << 24);
+  }
+};
 
 // One workflow instance: its element instances (local rows) and its current generation.
 struct Inst {
-  int64_t rkey[TR], rsk[TR], rjob[TR];
-  uint32_t rpay[TR];
-  uint32_t rmeta[TR];  // elem | state << 16 | parent << 24
-  int32_t rnch[TR];
+  i64x4 rkey, rsk, rjob;
+  u32x4 rpay;
+  u32x4 rmeta;  // elem | state << 16 | parent << 24
+  i32x4 rnch;
   uint32_t used, to_free;
   int64_t inst_key;
-  TRec cur[TF], nx[TF];
+  Gen cur, nx;
   int nc, nn, nwf, njob;
   // this generation's payload work: one merge and one incident detail at most
   bool merge, detail;
@@ -96,15 +110,15 @@ struct Inst {
   uint32_t transitions, completed, created, merges, cond_bytes;
   uint64_t merge_bytes;
 
-  __device__ __forceinline__ uint8_t state(int r) const { return (uint8_t)(sel(rmeta, r) >> 16); }
-  __device__ __forceinline__ uint16_t elem(int r) const { return (uint16_t)sel(rmeta, r); }
-  __device__ __forceinline__ uint8_t parent(int r) const { return (uint8_t)(sel(rmeta, r) >> 24); }
+  __device__ __forceinline__ uint8_t state(int r) const { return (uint8_t)(rmeta[r] >> 16); }
+  __device__ __forceinline__ uint16_t elem(int r) const { return (uint16_t)rmeta[r]; }
+  __device__ __forceinline__ uint8_t parent(int r) const { return (uint8_t)(rmeta[r] >> 24); }
   __device__ __forceinline__ bool alive(int r) const { return r != LN && state(r) != 0; }
   __device__ __forceinline__ void set_state(int r, uint8_t s) {
-    put(rmeta, r, (sel(rmeta, r) & 0xff00ffffu) | ((uint32_t)s << 16));
+    rmeta[r] = (rmeta[r] & 0xff00ffffu) | ((uint32_t)s << 16);
   }
   __device__ __forceinline__ void set_meta(int r, uint16_t el, uint8_t st, uint8_t par) {
-    put(rmeta, r, (uint32_t)el | ((uint32_t)st << 16) | ((uint32_t)par << 24));
+    rmeta[r] = (uint32_t)el | ((uint32_t)st << 16) | ((uint32_t)par << 24);
   }
   __device__ __forceinline__ int alloc() {
     const uint32_t freebits = ~used & ((1u << TR) - 1);
@@ -112,19 +126,19 @@ struct Inst {
     const int r = __builtin_ctz(freebits);
     used |= 1u << r;
     set_meta(r, NO_ELEM, 0, LN);
-    put(rnch, r, 0);
+    rnch[r] = 0;
     return r;
   }
   // ElementInstanceWriter: remove on a final state; the slot is reused from the next generation on
   __device__ __forceinline__ void remove(int r) {
     const int p = parent(r);
     set_state(r, 0);
-    if (p != LN) put(rnch, p, sel(rnch, p) - 1);
+    if (p != LN) rnch[p] -= 1;
     to_free |= 1u << r;
   }
   __device__ __forceinline__ void push(const TRec& s) {
     if (nn >= TF) { err |= TE_FALLBACK; return; }
-    put(nx, nn, s);
+    nx.set(nn, s);
     nn++;
   }
 };
@@ -188,7 +202,7 @@ __device__ void t_step(const TrajParams& P, Inst& I, const TRec& rec, int64_t po
       s.intent = WI_ELEMENT_ACTIVATED;
       s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
       I.set_state(rself, WI_ELEMENT_ACTIVATED);
-      put(I.rpay, rself, rec.payload);
+      I.rpay[rself] = rec.payload;
       I.push(s);
       break;
     }
@@ -196,7 +210,7 @@ __device__ void t_step(const TrajParams& P, Inst& I, const TRec& rec, int64_t po
       if (!scope_alive || I.merge) { I.err |= TE_FALLBACK; return; }
       I.merge = true;
       I.m_src = rec.payload;
-      I.m_tgt = sel(I.rpay, rscope);
+      I.m_tgt = I.rpay[rscope];
       if (EMIT) I.m_len = arena_len(P.arena, I.m_src) + arena_len(P.arena, I.m_tgt) + 8;
       s.intent = WI_ELEMENT_COMPLETED;
       s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
@@ -242,8 +256,8 @@ __device__ void t_step(const TrajParams& P, Inst& I, const TRec& rec, int64_t po
     }
     case ST_CONSUME_TOKEN: {  // ConsumeTokenHandler :30-43
       if (!scope_alive) { I.err |= TE_FALLBACK; return; }
-      s.key = sel(I.rkey, rscope);
-      s.scope_key = sel(I.rsk, rscope);
+      s.key = I.rkey[rscope];
+      s.scope_key = I.rsk[rscope];
       s.elem = I.elem(rscope);
       s.payload = rec.payload;
       s.intent = WI_ELEMENT_COMPLETING;
@@ -251,7 +265,7 @@ __device__ void t_step(const TrajParams& P, Inst& I, const TRec& rec, int64_t po
       s.rself = (uint8_t)rscope;
       s.rscope = I.parent(rscope);
       I.set_state(rscope, WI_ELEMENT_COMPLETING);
-      put(I.rpay, rscope, rec.payload);
+      I.rpay[rscope] = rec.payload;
       I.push(s);
       break;
     }
@@ -279,7 +293,7 @@ __device__ void t_step(const TrajParams& P, Inst& I, const TRec& rec, int64_t po
       s.flags = TK_WF | TK_ROW_INIT; s.ord = (uint8_t)I.nwf++;
       s.rself = (uint8_t)row;
       s.rscope = scope_alive ? (uint8_t)rscope : LN;
-      if (scope_alive) put(I.rnch, rscope, sel(I.rnch, rscope) + 1);
+      if (scope_alive) I.rnch[rscope] += 1;
       I.push(s);
       break;
     }
@@ -345,11 +359,11 @@ __device__ void t_record(const TrajParams& P, Inst& I, const TRec& rec, int64_t 
         const int r = rec.rself;
         if (r == LN) { I.err |= TE_FALLBACK; return; }
         I.set_meta(r, rec.elem, WI_ELEMENT_READY, LN);
-        put(I.rpay, r, rec.payload);
-        put(I.rkey, r, rec.key);
-        put(I.rsk, r, rec.scope_key);
-        put(I.rjob, r, (int64_t)0);
-        put(I.rnch, r, 0);
+        I.rpay[r] = rec.payload;
+        I.rkey[r] = rec.key;
+        I.rsk[r] = rec.scope_key;
+        I.rjob[r] = 0;
+        I.rnch[r] = 0;
         I.created += 1;
       } else if (rec.intent <= WI_ELEMENT_TERMINATED && rec.intent >= WI_START_EVENT_OCCURRED) {
         t_step<EMIT>(P, I, rec, pos);
@@ -369,13 +383,13 @@ __device__ void t_record(const TrajParams& P, Inst& I, const TRec& rec, int64_t 
       s.payload = P.elems[rec.elem].job_payload;
       I.push(s);
     } else if (rt == ZB_RT_EVENT && rec.intent == JI_CREATED) {  // JobCreatedProcessor :408-426
-      if (rec.scope_key > 0 && I.alive(rec.rself)) put(I.rjob, (int)rec.rself, rec.key);
+      if (rec.scope_key > 0 && I.alive(rec.rself)) I.rjob[rec.rself] = rec.key;
     } else if (rt == ZB_RT_EVENT && rec.intent == JI_COMPLETED) {  // JobCompletedEventProcessor :428-453
       const int r = rec.rself;
       if (!I.alive(r)) return;
       TRec s;
       s.key = rec.scope_key;
-      s.scope_key = sel(I.rsk, r);
+      s.scope_key = I.rsk[r];
       s.elem = I.elem(r);
       s.payload = rec.payload;
       s.intent = WI_ELEMENT_COMPLETING;
@@ -384,8 +398,8 @@ __device__ void t_record(const TrajParams& P, Inst& I, const TRec& rec, int64_t 
       s.rscope = I.parent(r);
       s.flags = 0; s.ord = 0;
       I.set_state(r, WI_ELEMENT_COMPLETING);
-      put(I.rpay, r, rec.payload);
-      put(I.rjob, r, (int64_t)-1);
+      I.rpay[r] = rec.payload;
+      I.rjob[r] = -1;
       I.push(s);
     }
   }
@@ -433,10 +447,9 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
 
   Inst I;
   I.used = 0; I.to_free = 0;
-#pragma unroll
-  for (int k = 0; k < TR; k++) {
-    I.rkey[k] = 0; I.rsk[k] = 0; I.rjob[k] = 0; I.rpay[k] = 0; I.rmeta[k] = 0; I.rnch[k] = 0;
-  }
+  I.rkey = 0; I.rsk = 0; I.rjob = 0; I.rpay = 0; I.rmeta = 0; I.rnch = 0;
+  I.cur.key = 0; I.cur.sk = 0; I.cur.pay = 0; I.cur.m0 = 0; I.cur.m1 = 0;
+  I.nx = I.cur;
   I.inst_key = -1;
   I.nc = 0; I.nn = 0; I.nwf = 0; I.njob = 0;
   I.merge = false; I.detail = false; I.m_src = I.m_tgt = I.m_len = 0;
@@ -450,11 +463,9 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
     TRec r;
     r.key = d.key; r.scope_key = d.scope_key; r.payload = d.payload; r.elem = d.elem; r.intent = d.intent;
     r.kind = d.kind; r.rself = LN; r.rscope = LN; r.flags = 0; r.ord = 0;
-    I.cur[0] = r;
+    I.cur.set(0, r);
     I.nc = 1;
   }
-#pragma unroll
-  for (int k = 1; k < TF; k++) I.cur[k] = I.cur[0];
 
   int w = 0;
   while (__syncthreads_or(I.nc > 0)) {
@@ -463,9 +474,8 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
       return;
     }
     // ---- process this generation (log order inside the instance)
-#pragma unroll
-    for (int k = 0; k < TF; k++)
-      if (k < I.nc) t_record<EMIT>(P, I, I.cur[k], fpos + k);
+#pragma unroll 1
+    for (int k = 0; k < I.nc; k++) t_record<EMIT>(P, I, I.cur.get(k), fpos + k);
     // ---- place the follow-ups
     uint64_t a = (uint64_t)I.nn | ((uint64_t)I.nwf << 16) | ((uint64_t)I.njob << 32);
     uint64_t bytes = 0;
@@ -528,7 +538,7 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
 #pragma unroll
     for (int k = 0; k < TF; k++) {
       if (k < I.nn) {
-        TRec s = I.nx[k];
+        TRec s = I.nx.get(k);
         if (s.flags & TK_WF) s.key = kwf + 5 * (int64_t)s.ord;
         if (s.flags & TK_JOB) s.key = kjob + 5 * (int64_t)s.ord;
         if (s.flags & TK_INST) I.inst_key = kwf + 5 * (int64_t)s.ord;
@@ -537,14 +547,14 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
         if (s.flags & TK_ROW_INIT) {
           const int r = s.rself;
           I.set_meta(r, s.elem, WI_ELEMENT_READY, s.rscope);
-          put(I.rpay, r, s.payload);
-          put(I.rkey, r, s.key);
-          put(I.rsk, r, s.scope_key);
-          put(I.rjob, r, (int64_t)0);
-          put(I.rnch, r, 0);
+          I.rpay[r] = s.payload;
+          I.rkey[r] = s.key;
+          I.rsk[r] = s.scope_key;
+          I.rjob[r] = 0;
+          I.rnch[r] = 0;
         }
         s.flags = 0;
-        I.cur[k] = s;
+        I.cur.set(k, s);
         if (EMIT) {
           zb_rec d;
           d.key = s.key; d.scope_key = s.scope_key; d.inst_key = I.inst_key; d.payload = s.payload;
@@ -584,13 +594,11 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
     if (threadIdx.x == 0) s_abase = atomicAdd((unsigned long long*)&ctl->rows_next, (unsigned long long)ta);
     __syncthreads();
     const uint64_t r0 = s_abase + a;
-    uint32_t gid[TR];
+    u32x4 gid = NO_ROW;
     uint32_t n = 0;
 #pragma unroll
-    for (int k = 0; k < TR; k++) {
-      gid[k] = NO_ROW;
+    for (int k = 0; k < TR; k++)
       if ((live >> k) & 1) gid[k] = (uint32_t)(r0 + n++);
-    }
 #pragma unroll
     for (int k = 0; k < TR; k++) {
       if (!((live >> k) & 1)) continue;
@@ -599,7 +607,7 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
       const int par = (int)(meta >> 24);
       RowMeta m;
       m.payload = I.rpay[k];
-      m.parent = par == LN ? NO_ROW : sel(gid, par);
+      m.parent = par == LN ? NO_ROW : gid[par];
       m.elem = (uint16_t)meta;
       m.state = (uint8_t)(meta >> 16);
       m.flags = 0;
