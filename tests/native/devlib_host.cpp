@@ -29,6 +29,12 @@ long devlib_merge(const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint32_t 
   if (w.n != o.n) return -4;
   return (long)w.n;
 }
+// flat fast path: returns length, -5 when the documents are not flat (caller would use merge_docs)
+long devlib_merge_flat(const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint32_t nt, uint8_t* out, uint32_t cap) {
+  uint32_t n = 0;
+  if (!merge_flat(src, ns, tgt, nt, out, cap, n)) return -5;
+  return (long)n;
+}
 // returns count of results; first result pos/len in out[0..1]; -1 unsupported
 long devlib_query(const uint8_t* doc, uint32_t n, const uint8_t* f_ids, const int32_t* f_idx,
                   const uint8_t* keys, const uint32_t* key_off, const uint32_t* key_len, uint32_t nf, int fast,

@@ -120,3 +120,39 @@ def test_query_fuzz_vs_oracle(devlib):
                 assert cnt == len(ref), (p, msgpack.unpackb(doc, raw=False), cnt, len(ref), use_fast)
                 if cnt:
                     assert doc[out[0]:out[0] + out[1]] == ref[0], (p, doc.hex())
+
+
+def _flat_doc(r):
+    keys = ["a", "b", "c", "orderId", "step", "done", "k" * 31, "0", ""]
+    vals = [None, True, False, 0, 1, -1, 127, 128, -33, 255, 256, 65535, 65536, -129, -40000, 2 ** 31, -2 ** 31 - 1,
+            2 ** 40, -2 ** 40, 0.5, 1e300, "", "x", "y" * 31, "z" * 32, "w" * 200, b"\x00", b"\x01" * 40]
+    return {r.choice(keys): r.choice(vals) for _ in range(r.randint(0, 6))}
+
+
+def test_flat_merge_matches_general(devlib):
+    """merge_flat (the kernels' fast path) is byte-identical to merge_docs wherever it accepts the input."""
+    devlib.devlib_merge_flat.restype = ctypes.c_long
+    devlib.devlib_merge_flat.argtypes = devlib.devlib_merge.argtypes
+    r = random.Random(7)
+    accepted = 0
+    for it in range(6000):
+        src, tgt = _flat_doc(r), _flat_doc(r)
+        if it % 10 == 0:
+            tgt = r.choice([{}, None])
+        if it % 13 == 0:
+            src = r.choice([{}, None])
+        sb = b"" if src is None and it % 2 else msgpack.packb(src)
+        tb = msgpack.packb(tgt)
+        if it % 17 == 0:  # non-flat shapes must be declined
+            sb = msgpack.packb({"n": {"x": 1}})
+        cap = len(sb) + len(tb) + 8
+        out_f = ctypes.create_string_buffer(cap + 1)
+        out_g = ctypes.create_string_buffer(cap + 1)
+        nf = devlib.devlib_merge_flat(sb, len(sb), tb, len(tb), out_f, cap)
+        ng = devlib.devlib_merge(sb, len(sb), tb, len(tb), out_g, cap)
+        if nf == -5:
+            continue
+        accepted += 1
+        assert ng >= 0, (src, tgt, ng)
+        assert out_f.raw[:nf] == out_g.raw[:ng], (src, tgt)
+    assert accepted > 3000

@@ -616,4 +616,128 @@ __device__ __noinline__ bool merge_docs(const uint8_t* src, uint32_t ns, const u
   return true;
 }
 
+// ------------------------------------------------------------------------------ flat merge
+// Fast path of merge_docs for the common payload shape: both documents are fixmaps of at most
+// FLAT_MAX_KEYS entries, every key a fixstr without '[' / ']', every value a scalar (nil, bool, int,
+// float, fixstr / str8, bin8), no duplicate keys. For such documents MappingProcessor.merge reduces
+// to: target keys in document order, each with the source value when the source has that key,
+// then the source keys the target lacks; leaves are copied raw and fixstr keys are already minimal
+// (MsgPackDocumentTreeWriter.writeNode), so the output is exactly merge_docs'. Anything else returns
+// false with nothing written and the caller runs merge_docs. The byte accesses go through plain
+// pointers, so the kernels point them at LDS copies of the documents (zb_traj.hip).
+constexpr int FLAT_MAX_KEYS = 8;
+
+// length of the scalar value at d[p] (n bytes in the document), 0 = not a supported scalar
+__device__ __forceinline__ uint32_t flat_scalar_len(const uint8_t* d, uint32_t n, uint32_t p) {
+  if (p >= n) return 0;
+  const uint32_t b = d[p];
+  uint32_t len;
+  if (b <= 0x7f || b >= 0xe0 || b == 0xc0 || b == 0xc2 || b == 0xc3) len = 1;
+  else if ((b & 0xe0) == 0xa0) len = 1 + (b & 0x1f);
+  else if (b == 0xcc || b == 0xd0) len = 2;
+  else if (b == 0xcd || b == 0xd1) len = 3;
+  else if (b == 0xce || b == 0xd2 || b == 0xca) len = 5;
+  else if (b == 0xd3 || b == 0xcb) len = 9;  // 0xcf (uint64) needs the ensurePositive check: general path
+  else if (b == 0xd9 || b == 0xc4) { if (p + 1 >= n) return 0; len = 2 + d[p + 1]; }
+  else return 0;
+  return p + len <= n ? len : 0;
+}
+
+// entries of a flat fixmap: e[i] = key offset | key length << 8 | value length << 16 (offsets < 256)
+__device__ __forceinline__ bool flat_entries(const uint8_t* d, uint32_t n, uint32_t (&e)[FLAT_MAX_KEYS], uint32_t& cnt) {
+  cnt = 0;
+  if (n == 0 || (n == 1 && d[0] == 0xc0)) return true;  // nil document = empty tree
+  const uint32_t h = d[0];
+  if ((h & 0xf0) != 0x80 || (h & 0x0f) > FLAT_MAX_KEYS || n > 255) return false;
+  cnt = h & 0x0f;
+  uint32_t p = 1;
+#pragma unroll
+  for (int i = 0; i < FLAT_MAX_KEYS; i++) {
+    if (i < (int)cnt) {
+      if (p >= n) return false;
+      const uint32_t kb = d[p];
+      if ((kb & 0xe0) != 0xa0) return false;
+      const uint32_t kl = kb & 0x1f;
+      if (p + 1 + kl > n) return false;
+      for (uint32_t j = 0; j < kl; j++) {
+        const uint8_t c = d[p + 1 + j];
+        if (c == '[' || c == ']') return false;
+      }
+      const uint32_t vl = flat_scalar_len(d, n, p + 1 + kl);
+      if (!vl) return false;
+      e[i] = p | (kl << 8) | (vl << 16);
+      p += 1 + kl + vl;
+    }
+  }
+  return p == n;
+}
+
+__device__ __forceinline__ bool flat_key_eq(const uint8_t* a, uint32_t ea, const uint8_t* b, uint32_t eb) {
+  const uint32_t la = (ea >> 8) & 0xff, lb = (eb >> 8) & 0xff;
+  if (la != lb) return false;
+  const uint8_t* pa = a + (ea & 0xff) + 1;
+  const uint8_t* pb = b + (eb & 0xff) + 1;
+  for (uint32_t j = 0; j < la; j++)
+    if (pa[j] != pb[j]) return false;
+  return true;
+}
+
+// Writes merge(src -> tgt) to out (capacity cap) and its length to *olen; false = not flat.
+__device__ __forceinline__ bool merge_flat(const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint32_t nt,
+                                           uint8_t* out, uint32_t cap, uint32_t& olen) {
+  uint32_t se[FLAT_MAX_KEYS], te[FLAT_MAX_KEYS], sc, tc;
+  if (!flat_entries(src, ns, se, sc) || !flat_entries(tgt, nt, te, tc)) return false;
+  // duplicate keys inside one document are left to merge_docs (it flags them unsupported)
+  uint32_t smatch = 0;  // source entries present in the target
+  uint32_t tsrc = 0;    // per target entry: 1 + index of the source entry with the same key (4 bits each)
+#pragma unroll
+  for (int i = 0; i < FLAT_MAX_KEYS; i++) {
+#pragma unroll
+    for (int j = i + 1; j < FLAT_MAX_KEYS; j++) {
+      if (j < (int)sc && flat_key_eq(src, se[i], src, se[j])) return false;
+      if (j < (int)tc && flat_key_eq(tgt, te[i], tgt, te[j])) return false;
+    }
+    if (i < (int)tc) {
+#pragma unroll
+      for (int j = 0; j < FLAT_MAX_KEYS; j++) {
+        if (j < (int)sc && flat_key_eq(tgt, te[i], src, se[j])) {
+          tsrc |= (uint32_t)(j + 1) << (4 * i);
+          smatch |= 1u << j;
+        }
+      }
+    }
+  }
+  // (an empty result is the fixmap header alone, 0x80, as merge_docs writes for an empty tree)
+  const uint32_t total = tc + (uint32_t)__builtin_popcount(~smatch & ((1u << sc) - 1));
+  if (ns + nt + 3 > cap) return false;
+  uint32_t o = 0;
+  if (total < 16) out[o++] = (uint8_t)(0x80 | total);
+  else { out[o++] = 0xde; out[o++] = 0; out[o++] = (uint8_t)total; }
+#pragma unroll
+  for (int i = 0; i < FLAT_MAX_KEYS; i++) {
+    if (i < (int)tc) {
+      const uint32_t e = te[i];
+      const uint32_t kp = e & 0xff, kl = (e >> 8) & 0xff;
+      for (uint32_t j = 0; j < 1 + kl; j++) out[o++] = tgt[kp + j];
+      const uint32_t m = (tsrc >> (4 * i)) & 0xf;
+      const uint8_t* vd = tgt;
+      uint32_t vp = kp + 1 + kl, vl = (e >> 16) & 0xff;
+      for (int j = 0; j < FLAT_MAX_KEYS; j++) {  // source value wins
+        if (m == (uint32_t)(j + 1)) { vd = src; vp = (se[j] & 0xff) + 1 + ((se[j] >> 8) & 0xff); vl = (se[j] >> 16) & 0xff; }
+      }
+      for (uint32_t j = 0; j < vl; j++) out[o++] = vd[vp + j];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < FLAT_MAX_KEYS; i++) {
+    if (i < (int)sc && !((smatch >> i) & 1)) {
+      const uint32_t e = se[i];
+      const uint32_t kp = e & 0xff, len = 1 + ((e >> 8) & 0xff) + ((e >> 16) & 0xff);
+      for (uint32_t j = 0; j < len; j++) out[o++] = src[kp + j];
+    }
+  }
+  olen = o;
+  return true;
+}
+
 }  // namespace zbg

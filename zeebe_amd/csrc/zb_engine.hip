@@ -114,6 +114,8 @@ struct zb_engine {
   DevVec<uint8_t> d_staged_arena;
   bool staged_uploaded = false;
   bool staged_pending = false;  // the staged batch has not been injected yet (zb_reset(keep) re-arms it)
+  uint16_t staged_elem = NO_ELEM;  // process element of the staged CREATEs ...
+  bool staged_uniform = true;      // ... when they all address the same one
 
   // submitted command ranges (serialization of CREATE commands / rejections)
   std::vector<CmdRange> ranges;
@@ -255,8 +257,8 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st)
     e->t_nwg_cap = nwg;
   }
   TrajCtl c{};
-  c.arena_next = (uint64_t)e->host_hdr.arena_next;
-  c.rows_next = (uint64_t)e->host_hdr.rows_next;
+  c.arena_next = c.arena_start = (uint64_t)e->host_hdr.arena_next;
+  c.rows_next = c.rows_start = (uint64_t)e->host_hdr.rows_next;
   *e->h_ctl_pinned = c;
   HIPCHECK(e, hipMemcpyAsync(e->t_ctl, e->h_ctl_pinned, sizeof(TrajCtl), hipMemcpyHostToDevice, e->stream));
   TrajParams p{};
@@ -277,6 +279,10 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st)
   p.job_start = e->host_hdr.job_next;
   p.nwg = (int32_t)nwg;
   p.wcap = (int32_t)wcap;
+  // Without exclusive splits nothing in a trajectory depends on payload values, so a batch whose
+  // CREATEs all address one process has one trajectory shape: count it on the first instance.
+  p.uni = (!e->has_splits && e->staged_uniform) ? n : 0;
+  p.cond = e->has_splits ? 1 : 0;
   p.agg = e->t_agg;
   p.wcount = e->t_wcount;
   p.woff = e->t_woff;
@@ -291,7 +297,8 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st)
   p.arena_cap = e->cfg.arena_bytes;
   hipEvent_t* ev = e->ev.data();
   HIPCHECK(e, hipEventRecord(ev[0], e->stream));
-  launch_traj_count(p, e->stream);
+  if (p.uni) launch_traj_count_uniform(p, e->stream);
+  else launch_traj_count(p, e->stream);
   HIPCHECK(e, hipEventRecord(ev[1], e->stream));
   launch_traj_scan(p, e->stream);
   launch_traj_emit(p, e->stream);
@@ -308,7 +315,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st)
   st.process_kernel_ms += ms0;
   st.emit_kernel_ms += ms1;
   st.wave_kernel_ms += ms0 + ms1;
-  st.launches += 6;
+  st.launches += p.uni ? 6 : 7;
   if (e->h_ctl_pinned->flag) return 0;
   e->host_hdr = e->h_hdr_pinned[0];
   int rc = check_device_errors(e, *e->h_err_pinned);
@@ -497,6 +504,12 @@ int zb_submit_creates(zb_engine* e, const char* pid, int32_t version, int64_t wo
     e->staged_arena.clear();
     e->pending_ranges.clear();
     e->staged_uploaded = false;
+  }
+  if (e->staged.empty()) {
+    e->staged_elem = pelem;
+    e->staged_uniform = true;
+  } else if (n > 0 && pelem != e->staged_elem) {
+    e->staged_uniform = false;
   }
   zb_engine::PendingRange pr;
   pr.first = (int64_t)e->staged.size();

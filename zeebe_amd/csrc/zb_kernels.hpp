@@ -155,7 +155,10 @@ struct TrajCtl {
   uint64_t arena_next; // payload arena bump pointer (emit pass)
   uint64_t rows_next;  // row allocator (live element instances at the end)
   int64_t end, wf_next, job_next;  // log end and key generators after the batch (k_traj_base)
-  int64_t pad;
+  uint64_t arena_start, rows_start;  // allocator values before the emit pass (a rerun restarts there)
+  uint32_t regen;      // the emit pass met a non-flat merge: rerun it with the general merge
+  uint32_t derr;       // DevErr flags of the (last) emit pass
+  uint64_t st[6];      // emit pass statistics: transitions, completed, created, merges, merge bytes, cond bytes
 };
 struct TrajBase {      // generation w: log position of its follow-ups, key generator values
   int64_t pos, wf, job, pad;
@@ -175,6 +178,9 @@ struct TrajParams {
   const uint8_t* pool;
   int64_t log_base, n;   // the batch: CREATE commands at [log_base, log_base + n)
   int64_t wf_start, job_start;
+  int32_t cond, pad0;    // the model has exclusive splits (condition VM compiled into the kernels)
+  int64_t uni;           // > 0: uniform batch of `uni` instances whose trajectories are data-independent;
+                         // agg[w] holds one instance's counts (count pass over instance 0 only)
   int32_t nwg, wcap;     // workgroups, generations the count buffers hold
   uint64_t* agg;         // [wcap][nwg] workgroup totals: records | wf keys << 16 | job keys << 32
   uint32_t* wcount;      // [nwg] generations processed by each workgroup
@@ -189,6 +195,7 @@ struct TrajParams {
 };
 
 void launch_traj_count(const TrajParams& p, hipStream_t stream);
+void launch_traj_count_uniform(const TrajParams& p, hipStream_t stream);
 void launch_traj_scan(const TrajParams& p, hipStream_t stream);
 void launch_traj_emit(const TrajParams& p, hipStream_t stream);
 

@@ -50,7 +50,12 @@ enum TrajFlags : uint8_t {
 };
 
 // trajectory-path error bits (count pass -> host falls back to the wave path)
-enum TrajErr : uint32_t { TE_FALLBACK = 1u };
+enum TrajErr : uint32_t { TE_FALLBACK = 1u, TE_REGEN = 1u << 30 };
+
+// flat-merge staging in LDS (emit pass): per thread the two input blobs and the output blob
+constexpr int FM_WORDS = 16;                  // 64-byte blob slots: documents of <= 60 bytes
+constexpr int FM_BYTES = FM_WORDS * 4;
+constexpr int FM_STRIDE = 3 * FM_WORDS + 1;   // odd stride: lanes at the same offset hit distinct banks
 
 struct TRec {
   int64_t key, scope_key;
@@ -148,8 +153,7 @@ __device__ __forceinline__ uint32_t arena_len(const uint8_t* arena, uint32_t ref
 }
 __device__ __forceinline__ uint32_t tblob_bytes(uint32_t len) { return (4 + len + 7) & ~7u; }
 
-template <bool EMIT>
-__device__ void t_incident(Inst& I, const TRec& rec, int64_t pos, uint8_t code, uint8_t a, uint8_t b, uint16_t q) {
+__device__ __forceinline__ void t_incident(Inst& I, const TRec& rec, int64_t pos, uint8_t code, uint8_t a, uint8_t b, uint16_t q) {
   // BpmnStepContext.raiseIncident: IncidentIntent.CREATE command, key null, CONDITION_ERROR
   TRec s;
   s.key = -1;
@@ -165,9 +169,10 @@ __device__ void t_incident(Inst& I, const TRec& rec, int64_t pos, uint8_t code, 
   I.push(s);
 }
 
-// bpmn_step (zb_wave.hip) on local rows: BpmnStepProcessor.java:92-251 guards + step handlers
-template <bool EMIT>
-__device__ void t_step(const TrajParams& P, Inst& I, const TRec& rec, int64_t pos) {
+// bpmn_step (zb_wave.hip) on local rows: BpmnStepProcessor.java:92-251 guards + step handlers.
+// COND: exclusive splits are evaluated here (else they send the batch to the wave pipeline).
+template <bool EMIT, bool COND>
+__device__ __forceinline__ void t_step(const TrajParams& P, Inst& I, const TRec& rec, int64_t pos) {
   const uint8_t intent = rec.intent;
   const bool stateless = intent == WI_SEQUENCE_FLOW_TAKEN || intent == WI_START_EVENT_OCCURRED ||
                          intent == WI_END_EVENT_OCCURRED || intent == WI_GATEWAY_ACTIVATED;
@@ -229,30 +234,35 @@ __device__ void t_step(const TrajParams& P, Inst& I, const TRec& rec, int64_t po
       break;
     }
     case ST_EXCLUSIVE_SPLIT: {  // ExclusiveSplitHandler :38-71 (first true condition, else default)
-      const uint8_t* pp = P.arena + (uint64_t)rec.payload * 8;
-      const uint32_t len = *(const uint32_t*)pp;
-      uint16_t chosen = NO_ELEM;
-      CondOut co{0, 0, 0, 0};
-      bool unsup = false;
-      for (uint32_t c = 0; c < el.cond_count; c++) {
-        const uint16_t flow = P.cond_flows[el.cond_begin + c];
-        const bool res = eval_condition(P.elems[flow].cond_prog, P.code, pp + 4, len, P.consts, P.queries,
-                                        P.filters, P.pool, co, unsup);
-        if (unsup || co.err) break;
-        if (res) { chosen = flow; break; }
+      if constexpr (!COND) {
+        I.err |= TE_FALLBACK;
+        return;
+      } else {
+        const uint8_t* pp = P.arena + (uint64_t)rec.payload * 8;
+        const uint32_t len = *(const uint32_t*)pp;
+        uint16_t chosen = NO_ELEM;
+        CondOut co{0, 0, 0, 0};
+        bool unsup = false;
+        for (uint32_t c = 0; c < el.cond_count; c++) {
+          const uint16_t flow = P.cond_flows[el.cond_begin + c];
+          const bool res = eval_condition(P.elems[flow].cond_prog, P.code, pp + 4, len, P.consts, P.queries,
+                                          P.filters, P.pool, co, unsup);
+          if (unsup || co.err) break;
+          if (res) { chosen = flow; break; }
+        }
+        I.cond_bytes += len;
+        if (unsup) { I.err |= TE_FALLBACK; return; }
+        if (co.err) { t_incident(I, rec, pos, co.err & 7, co.a & 15, co.b & 15, co.q); break; }
+        if (chosen == NO_ELEM) chosen = el.dflt;
+        if (chosen == NO_ELEM) { t_incident(I, rec, pos, EC_NO_FLOW, 0, 0, 0); break; }
+        s.elem = chosen;
+        s.intent = WI_SEQUENCE_FLOW_TAKEN;
+        s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
+        s.flags = TK_WF; s.ord = (uint8_t)I.nwf++;
+        s.rself = LN;
+        I.push(s);
+        break;
       }
-      I.cond_bytes += len;
-      if (unsup) { I.err |= TE_FALLBACK; return; }
-      if (co.err) { t_incident<EMIT>(I, rec, pos, co.err & 7, co.a & 15, co.b & 15, co.q); break; }
-      if (chosen == NO_ELEM) chosen = el.dflt;
-      if (chosen == NO_ELEM) { t_incident<EMIT>(I, rec, pos, EC_NO_FLOW, 0, 0, 0); break; }
-      s.elem = chosen;
-      s.intent = WI_SEQUENCE_FLOW_TAKEN;
-      s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
-      s.flags = TK_WF; s.ord = (uint8_t)I.nwf++;
-      s.rself = LN;
-      I.push(s);
-      break;
     }
     case ST_CONSUME_TOKEN: {  // ConsumeTokenHandler :30-43
       if (!scope_alive) { I.err |= TE_FALLBACK; return; }
@@ -325,8 +335,8 @@ __device__ void t_step(const TrajParams& P, Inst& I, const TRec& rec, int64_t po
 }
 
 // process_record (zb_wave.hip) on local rows
-template <bool EMIT>
-__device__ void t_record(const TrajParams& P, Inst& I, const TRec& rec, int64_t pos) {
+template <bool EMIT, bool COND>
+__device__ __forceinline__ void t_record(const TrajParams& P, Inst& I, const TRec& rec, int64_t pos) {
   const uint8_t vt = kind_vt(rec.kind), rt = kind_rt(rec.kind);
   if (vt == ZB_VT_WORKFLOW_INSTANCE) {
     if (rt == ZB_RT_COMMAND) {
@@ -366,7 +376,7 @@ __device__ void t_record(const TrajParams& P, Inst& I, const TRec& rec, int64_t 
         I.rnch[r] = 0;
         I.created += 1;
       } else if (rec.intent <= WI_ELEMENT_TERMINATED && rec.intent >= WI_START_EVENT_OCCURRED) {
-        t_step<EMIT>(P, I, rec, pos);
+        t_step<EMIT, COND>(P, I, rec, pos);
       }
     }
   } else if (vt == ZB_VT_JOB) {
@@ -435,13 +445,31 @@ __device__ __forceinline__ void block_scan2(uint64_t& a, uint64_t& b, uint64_t& 
   __syncthreads();  // s reused by the next call
 }
 
+// inclusive scan over the 64 lanes of a wave
+__device__ __forceinline__ uint64_t wave_scan(uint64_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t u = tshfl_up(v, d);
+    if (lane >= d) v += u;
+  }
+  return v;
+}
+
 // ------------------------------------------------------------------------------ k_traj
-template <bool EMIT>
+// EMIT: emit pass (else count pass). UNI: uniform batch (see TrajParams::uni): every instance has the
+// same per-generation counts, so positions and keys are affine in the instance index and the
+// generation loop needs no workgroup synchronisation at all. COND: exclusive splits supported.
+// GEN: the general merge (merge_docs) backs up the flat fast path; without it a non-flat merge
+// makes the pass set ctl->regen and the host-side launch sequence reruns the pass with GEN.
+template <bool EMIT, bool UNI, bool COND, bool GEN>
 __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
   __shared__ uint64_t s_scan[TWG / 64][2];
   __shared__ uint64_t s_abase;
+  __shared__ uint32_t s_merge[EMIT ? TWG * FM_STRIDE : 1];
   TrajCtl* ctl = P.ctl;
   if (EMIT && ctl->flag) return;
+  if (EMIT && GEN && !ctl->regen) return;
   const int64_t inst = (int64_t)blockIdx.x * TWG + threadIdx.x;
   const int nwg = gridDim.x;
 
@@ -468,22 +496,38 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
   }
 
   int w = 0;
-  while (__syncthreads_or(I.nc > 0)) {
-    if (w >= P.wcap) {  // more generations than the count buffers hold
+  const int W = UNI ? (int)P.wcount[0] : 0;
+  while (UNI ? (w < W) : __syncthreads_or(I.nc > 0)) {
+    if (!UNI && w >= P.wcap) {  // more generations than the count buffers hold
       if (!EMIT && threadIdx.x == 0) atomicOr(&ctl->flag, TE_FALLBACK);
       return;
     }
     // ---- process this generation (log order inside the instance)
 #pragma unroll 1
-    for (int k = 0; k < I.nc; k++) t_record<EMIT>(P, I, I.cur.get(k), fpos + k);
+    for (int k = 0; k < I.nc; k++) t_record<EMIT, COND>(P, I, I.cur.get(k), fpos + k);
     // ---- place the follow-ups
     uint64_t a = (uint64_t)I.nn | ((uint64_t)I.nwf << 16) | ((uint64_t)I.njob << 32);
     uint64_t bytes = 0;
     if (EMIT) bytes = (I.merge ? tblob_bytes(I.m_len) : 0) + (I.detail ? 24 : 0);
-    uint64_t ta, tb;
-    block_scan2(a, bytes, ta, tb, s_scan);
+    uint64_t ta = 0, tb = 0;
+    if (!UNI) block_scan2(a, bytes, ta, tb, s_scan);
     int64_t pos0, kwf, kjob;
-    if (!EMIT) {
+    if (UNI) {
+      // positions and keys are affine in the instance index; the arena is allocated per wave
+      const uint64_t c = P.agg[w];
+      const TrajBase wb = P.wbase[w];
+      pos0 = wb.pos + inst * (int64_t)(c & 0xffff);
+      kwf = wb.wf + 5 * inst * (int64_t)((c >> 16) & 0xffff);
+      kjob = wb.job + 5 * inst * (int64_t)(c >> 32);
+      if (EMIT && __any(bytes != 0)) {
+        const uint64_t incl = wave_scan(bytes);
+        uint64_t base = 0;
+        if ((threadIdx.x & 63) == 63) base = atomicAdd((unsigned long long*)&ctl->arena_next, (unsigned long long)incl);
+        base = (uint64_t)__shfl((unsigned long long)base, 63, 64);
+        bytes = incl - bytes;
+        tb = base;  // per-wave arena base (s_abase below is per workgroup)
+      }
+    } else if (!EMIT) {
       if (threadIdx.x == 0) P.agg[(uint64_t)w * nwg + blockIdx.x] = ta;
       pos0 = 0;
       kwf = 1 + 5 * (int64_t)((a >> 16) & 0xffff);
@@ -501,23 +545,45 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
     }
     uint32_t merged_ref = 0, detail_ref = 0;
     if (EMIT && (I.merge || I.detail)) {
-      uint64_t at = s_abase + bytes;
+      uint64_t at = (UNI ? tb : s_abase) + bytes;
       if (I.merge) {
         const uint32_t mb = tblob_bytes(I.m_len);
         if (at + mb > P.arena_cap) I.err |= DE_ARENA_FULL;
         else {
-          const uint8_t* sp = P.arena + (uint64_t)I.m_src * 8;
-          const uint8_t* tp = P.arena + (uint64_t)I.m_tgt * 8;
-          const uint32_t ns = *(const uint32_t*)sp, nt = *(const uint32_t*)tp;
-          uint8_t* dst = P.arena + at;
-          Out o{dst + 4, 0};
-          bool unsup = false;
-          if (!merge_docs(sp + 4, ns, tp + 4, nt, o, unsup)) I.err |= DE_BAD_PAYLOAD;
-          else if (unsup || o.n > I.m_len) I.err |= DE_UNSUPPORTED;
-          *(uint32_t*)dst = o.n;
+          const uint32_t* gs = (const uint32_t*)(P.arena + (uint64_t)I.m_src * 8);
+          const uint32_t* gt = (const uint32_t*)(P.arena + (uint64_t)I.m_tgt * 8);
+          const uint32_t ns = gs[0], nt = gt[0];
+          uint32_t* gd = (uint32_t*)(P.arena + at);
+          uint32_t olen = 0;
+          bool done = false;
+          if (ns + nt + 3 <= FM_BYTES - 4) {
+            // flat fast path on LDS copies of the two documents
+            uint32_t* reg = s_merge + threadIdx.x * FM_STRIDE;
+            for (uint32_t k = 0; k < (ns + 7) / 4; k++) reg[k] = gs[k];
+            for (uint32_t k = 0; k < (nt + 7) / 4; k++) reg[FM_WORDS + k] = gt[k];
+            uint8_t* lo = (uint8_t*)(reg + 2 * FM_WORDS);
+            done = merge_flat((const uint8_t*)reg + 4, ns, (const uint8_t*)(reg + FM_WORDS) + 4, nt, lo + 4,
+                              FM_BYTES - 4, olen);
+            if (done) {
+              reg[2 * FM_WORDS] = olen;
+              for (uint32_t k = 0; k < (olen + 7) / 4; k++) gd[k] = reg[2 * FM_WORDS + k];
+            }
+          }
+          if (!done) {
+            if constexpr (GEN) {
+              Out o{(uint8_t*)gd + 4, 0};
+              bool unsup = false;
+              if (!merge_docs((const uint8_t*)gs + 4, ns, (const uint8_t*)gt + 4, nt, o, unsup)) I.err |= DE_BAD_PAYLOAD;
+              else if (unsup || o.n > I.m_len) I.err |= DE_UNSUPPORTED;
+              olen = o.n;
+              gd[0] = olen;
+            } else {
+              I.err |= TE_REGEN;
+            }
+          }
           merged_ref = (uint32_t)(at >> 3);
           I.merges += 1;
-          I.merge_bytes += ns + nt + o.n;
+          I.merge_bytes += ns + nt + olen;
         }
         at += mb;
       }
@@ -623,16 +689,17 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
   uint64_t s2 = I.merge_bytes, s3 = I.cond_bytes, tc, td;
   block_scan2(s2, s3, tc, td, s_scan);
   if (threadIdx.x == 0) {
-    atomicAdd((unsigned long long*)&P.stats[0], (unsigned long long)(ta & 0xffffffffu));
-    atomicAdd((unsigned long long*)&P.stats[1], (unsigned long long)(ta >> 32));
-    atomicAdd((unsigned long long*)&P.stats[2], (unsigned long long)(tb & 0xffffffffu));
-    atomicAdd((unsigned long long*)&P.stats[3], (unsigned long long)(tb >> 32));
-    atomicAdd((unsigned long long*)&P.stats[4], (unsigned long long)tc);
-    atomicAdd((unsigned long long*)&P.stats[5], (unsigned long long)td);
+    atomicAdd((unsigned long long*)&ctl->st[0], (unsigned long long)(ta & 0xffffffffu));
+    atomicAdd((unsigned long long*)&ctl->st[1], (unsigned long long)(ta >> 32));
+    atomicAdd((unsigned long long*)&ctl->st[2], (unsigned long long)(tb & 0xffffffffu));
+    atomicAdd((unsigned long long*)&ctl->st[3], (unsigned long long)(tb >> 32));
+    atomicAdd((unsigned long long*)&ctl->st[4], (unsigned long long)tc);
+    atomicAdd((unsigned long long*)&ctl->st[5], (unsigned long long)td);
   }
-  const uint32_t derr = I.err & ~(uint32_t)TE_FALLBACK;
-  if (I.err & TE_FALLBACK) atomicOr(P.err, DE_PROCESSING);  // count and emit passes disagree: cannot happen
-  if (derr) atomicOr(P.err, derr);
+  if (I.err & TE_REGEN) atomicOr(&ctl->regen, 1u);
+  const uint32_t derr = I.err & ~(uint32_t)(TE_FALLBACK | TE_REGEN);
+  if (I.err & TE_FALLBACK) atomicOr(&ctl->derr, (uint32_t)DE_PROCESSING);  // count and emit passes disagree
+  if (derr) atomicOr(&ctl->derr, derr);
 }
 
 // ------------------------------------------------------------------------------ scans
@@ -694,8 +761,14 @@ __global__ void __launch_bounds__(1024) k_traj_base(TrajParams P) {
     const uint32_t w = base + threadIdx.x;
     uint64_t x[3] = {0, 0, 0};
     if (w < W) {
-      const uint4 t = P.wtot[w];
-      x[0] = t.x; x[1] = t.y; x[2] = t.z;
+      if (P.uni) {
+        const uint64_t c = P.agg[w];
+        x[0] = (c & 0xffff) * (uint64_t)P.uni; x[1] = ((c >> 16) & 0xffff) * (uint64_t)P.uni;
+        x[2] = (c >> 32) * (uint64_t)P.uni;
+      } else {
+        const uint4 t = P.wtot[w];
+        x[0] = t.x; x[1] = t.y; x[2] = t.z;
+      }
     }
     uint64_t ex[3];
 #pragma unroll
@@ -739,9 +812,21 @@ __global__ void __launch_bounds__(1024) k_traj_base(TrajParams P) {
   }
 }
 
+// a non-flat merge stopped the first emit pass: restart the allocators and statistics for the rerun
+__global__ void k_traj_regen(TrajParams P) {
+  TrajCtl* ctl = P.ctl;
+  if (ctl->flag || !ctl->regen) return;
+  ctl->arena_next = ctl->arena_start;
+  ctl->rows_next = ctl->rows_start;
+  ctl->derr = 0;
+  for (int i = 0; i < 6; i++) ctl->st[i] = 0;
+}
+
 __global__ void k_traj_commit(TrajParams P) {
   const TrajCtl* ctl = P.ctl;
   if (ctl->flag) return;
+  for (int i = 0; i < 6; i++) P.stats[i] += ctl->st[i];
+  if (ctl->derr) atomicOr(P.err, ctl->derr);
   WaveHdr h = *P.hdr;
   h.begin = h.end = h.gen_end = ctl->end;
   h.wf_next = ctl->wf_next;
@@ -754,15 +839,38 @@ __global__ void k_traj_commit(TrajParams P) {
   if ((uint64_t)ctl->arena_next > P.arena_cap) atomicOr(P.err, (uint32_t)DE_ARENA_FULL);
 }
 
+// conditions are compiled into the count / emit kernels only when the model has exclusive splits
+// (a uniform batch never has any), keeping the condition VM's call frame out of the other variants
 void launch_traj_count(const TrajParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_traj<false>, dim3(p.nwg), dim3(TWG), 0, s, p);
+  if (p.cond) hipLaunchKernelGGL((k_traj<false, false, true, false>), dim3(p.nwg), dim3(TWG), 0, s, p);
+  else hipLaunchKernelGGL((k_traj<false, false, false, false>), dim3(p.nwg), dim3(TWG), 0, s, p);
+}
+// uniform batch: count one representative instance (the first CREATE), one workgroup
+void launch_traj_count_uniform(const TrajParams& p, hipStream_t s) {
+  TrajParams q = p;
+  q.n = 1;
+  q.nwg = 1;
+  hipLaunchKernelGGL((k_traj<false, false, false, false>), dim3(1), dim3(TWG), 0, s, q);
 }
 void launch_traj_scan(const TrajParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_traj_scan, dim3(p.wcap), dim3(1024), 0, s, p);
+  if (!p.uni) hipLaunchKernelGGL(k_traj_scan, dim3(p.wcap), dim3(1024), 0, s, p);
   hipLaunchKernelGGL(k_traj_base, dim3(1), dim3(1024), 0, s, p);
 }
 void launch_traj_emit(const TrajParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_traj<true>, dim3(p.nwg), dim3(TWG), 0, s, p);
+  const dim3 g(p.nwg), b(TWG);
+  if (p.uni) {
+    hipLaunchKernelGGL((k_traj<true, true, false, false>), g, b, 0, s, p);
+    hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
+    hipLaunchKernelGGL((k_traj<true, true, false, true>), g, b, 0, s, p);
+  } else if (p.cond) {
+    hipLaunchKernelGGL((k_traj<true, false, true, false>), g, b, 0, s, p);
+    hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
+    hipLaunchKernelGGL((k_traj<true, false, true, true>), g, b, 0, s, p);
+  } else {
+    hipLaunchKernelGGL((k_traj<true, false, false, false>), g, b, 0, s, p);
+    hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
+    hipLaunchKernelGGL((k_traj<true, false, false, true>), g, b, 0, s, p);
+  }
   hipLaunchKernelGGL(k_traj_commit, dim3(1), dim3(1), 0, s, p);
 }
 
