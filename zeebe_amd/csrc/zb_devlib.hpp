@@ -617,15 +617,15 @@ __device__ __noinline__ bool merge_docs(const uint8_t* src, uint32_t ns, const u
 }
 
 // ------------------------------------------------------------------------------ flat merge
-// Fast path of merge_docs for the common payload shape: both documents are fixmaps of at most
-// FLAT_MAX_KEYS entries, every key a fixstr without '[' / ']', every value a scalar (nil, bool, int,
-// float, fixstr / str8, bin8), no duplicate keys. For such documents MappingProcessor.merge reduces
-// to: target keys in document order, each with the source value when the source has that key,
-// then the source keys the target lacks; leaves are copied raw and fixstr keys are already minimal
+// Fast path of merge_docs for the common payload shape: both documents are fixmaps, every key a
+// fixstr without '[' / ']', every value a scalar (nil, bool, int, float, fixstr / str8, bin8), no
+// duplicate keys. For such documents MappingProcessor.merge reduces to: target keys in document
+// order, each with the source value when the source has that key, then the source keys the
+// target lacks; leaves are copied raw and fixstr keys are already minimal
 // (MsgPackDocumentTreeWriter.writeNode), so the output is exactly merge_docs'. Anything else returns
-// false with nothing written and the caller runs merge_docs. The byte accesses go through plain
+// false and the caller runs merge_docs. Written as rolled loops that re-parse entries on the fly:
+// no per-entry tables, so it stays small in code and registers. The byte accesses go through plain
 // pointers, so the kernels point them at LDS copies of the documents (zb_traj.hip).
-constexpr int FLAT_MAX_KEYS = 8;
 
 // length of the scalar value at d[p] (n bytes in the document), 0 = not a supported scalar
 __device__ __forceinline__ uint32_t flat_scalar_len(const uint8_t* d, uint32_t n, uint32_t p) {
@@ -643,98 +643,99 @@ __device__ __forceinline__ uint32_t flat_scalar_len(const uint8_t* d, uint32_t n
   return p + len <= n ? len : 0;
 }
 
-// entries of a flat fixmap: e[i] = key offset | key length << 8 | value length << 16 (offsets < 256)
-__device__ __forceinline__ bool flat_entries(const uint8_t* d, uint32_t n, uint32_t (&e)[FLAT_MAX_KEYS], uint32_t& cnt) {
+// entry at p: fixstr key of kl bytes at p + 1, scalar value of vl bytes at p + 1 + kl
+__device__ __forceinline__ bool flat_entry(const uint8_t* d, uint32_t n, uint32_t p, uint32_t& kl, uint32_t& vl) {
+  if (p >= n) return false;
+  const uint32_t kb = d[p];
+  if ((kb & 0xe0) != 0xa0) return false;
+  kl = kb & 0x1f;
+  if (p + 1 + kl > n) return false;
+  vl = flat_scalar_len(d, n, p + 1 + kl);
+  return vl != 0;
+}
+
+__device__ __forceinline__ bool flat_bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
+  for (uint32_t j = 0; j < n; j++)
+    if (a[j] != b[j]) return false;
+  return true;
+}
+
+// Value (position | length << 16) of key k in the flat map d with cnt entries; 0 when absent.
+__device__ __forceinline__ uint32_t flat_find(const uint8_t* d, uint32_t n, uint32_t cnt, const uint8_t* k,
+                                              uint32_t klen) {
+  uint32_t p = 1, found = 0;
+  for (uint32_t i = 0; i < cnt; i++) {
+    uint32_t kl, vl;
+    flat_entry(d, n, p, kl, vl);
+    if (!found && kl == klen && flat_bytes_eq(d + p + 1, k, kl)) found = (p + 1 + kl) | (vl << 16);
+    p += 1 + kl + vl;
+  }
+  return found;
+}
+
+// Checks the document is a flat map (or nil: cnt = 0) without duplicate or '['/']' keys.
+__device__ __forceinline__ bool flat_check(const uint8_t* d, uint32_t n, uint32_t& cnt) {
   cnt = 0;
   if (n == 0 || (n == 1 && d[0] == 0xc0)) return true;  // nil document = empty tree
   const uint32_t h = d[0];
-  if ((h & 0xf0) != 0x80 || (h & 0x0f) > FLAT_MAX_KEYS || n > 255) return false;
+  if ((h & 0xf0) != 0x80 || n > 0xffff) return false;
   cnt = h & 0x0f;
   uint32_t p = 1;
-#pragma unroll
-  for (int i = 0; i < FLAT_MAX_KEYS; i++) {
-    if (i < (int)cnt) {
-      if (p >= n) return false;
-      const uint32_t kb = d[p];
-      if ((kb & 0xe0) != 0xa0) return false;
-      const uint32_t kl = kb & 0x1f;
-      if (p + 1 + kl > n) return false;
-      for (uint32_t j = 0; j < kl; j++) {
-        const uint8_t c = d[p + 1 + j];
-        if (c == '[' || c == ']') return false;
-      }
-      const uint32_t vl = flat_scalar_len(d, n, p + 1 + kl);
-      if (!vl) return false;
-      e[i] = p | (kl << 8) | (vl << 16);
-      p += 1 + kl + vl;
+  for (uint32_t i = 0; i < cnt; i++) {
+    uint32_t kl, vl;
+    if (!flat_entry(d, n, p, kl, vl)) return false;
+    for (uint32_t j = 0; j < kl; j++) {
+      const uint8_t c = d[p + 1 + j];
+      if (c == '[' || c == ']') return false;
     }
+    // duplicates among the later entries (merge_docs flags them unsupported)
+    uint32_t q = p + 1 + kl + vl;
+    for (uint32_t j = i + 1; j < cnt; j++) {
+      uint32_t kl2, vl2;
+      if (!flat_entry(d, n, q, kl2, vl2)) return false;
+      if (kl2 == kl && flat_bytes_eq(d + q + 1, d + p + 1, kl)) return false;
+      q += 1 + kl2 + vl2;
+    }
+    p += 1 + kl + vl;
   }
   return p == n;
 }
 
-__device__ __forceinline__ bool flat_key_eq(const uint8_t* a, uint32_t ea, const uint8_t* b, uint32_t eb) {
-  const uint32_t la = (ea >> 8) & 0xff, lb = (eb >> 8) & 0xff;
-  if (la != lb) return false;
-  const uint8_t* pa = a + (ea & 0xff) + 1;
-  const uint8_t* pb = b + (eb & 0xff) + 1;
-  for (uint32_t j = 0; j < la; j++)
-    if (pa[j] != pb[j]) return false;
-  return true;
-}
-
-// Writes merge(src -> tgt) to out (capacity cap) and its length to *olen; false = not flat.
+// Writes merge(src -> tgt) to out (capacity cap) and its length to olen; false = not flat.
 __device__ __forceinline__ bool merge_flat(const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint32_t nt,
                                            uint8_t* out, uint32_t cap, uint32_t& olen) {
-  uint32_t se[FLAT_MAX_KEYS], te[FLAT_MAX_KEYS], sc, tc;
-  if (!flat_entries(src, ns, se, sc) || !flat_entries(tgt, nt, te, tc)) return false;
-  // duplicate keys inside one document are left to merge_docs (it flags them unsupported)
-  uint32_t smatch = 0;  // source entries present in the target
-  uint32_t tsrc = 0;    // per target entry: 1 + index of the source entry with the same key (4 bits each)
-#pragma unroll
-  for (int i = 0; i < FLAT_MAX_KEYS; i++) {
-#pragma unroll
-    for (int j = i + 1; j < FLAT_MAX_KEYS; j++) {
-      if (j < (int)sc && flat_key_eq(src, se[i], src, se[j])) return false;
-      if (j < (int)tc && flat_key_eq(tgt, te[i], tgt, te[j])) return false;
-    }
-    if (i < (int)tc) {
-#pragma unroll
-      for (int j = 0; j < FLAT_MAX_KEYS; j++) {
-        if (j < (int)sc && flat_key_eq(tgt, te[i], src, se[j])) {
-          tsrc |= (uint32_t)(j + 1) << (4 * i);
-          smatch |= 1u << j;
-        }
-      }
-    }
+  uint32_t sc, tc;
+  if (ns + nt + 3 > cap || !flat_check(src, ns, sc) || !flat_check(tgt, nt, tc)) return false;
+  // result keys: the target's, then the source's the target lacks
+  uint32_t total = tc, p = 1;
+  for (uint32_t i = 0; i < sc; i++) {
+    uint32_t kl, vl;
+    flat_entry(src, ns, p, kl, vl);
+    if (!flat_find(tgt, nt, tc, src + p + 1, kl)) total++;
+    p += 1 + kl + vl;
   }
   // (an empty result is the fixmap header alone, 0x80, as merge_docs writes for an empty tree)
-  const uint32_t total = tc + (uint32_t)__builtin_popcount(~smatch & ((1u << sc) - 1));
-  if (ns + nt + 3 > cap) return false;
   uint32_t o = 0;
   if (total < 16) out[o++] = (uint8_t)(0x80 | total);
   else { out[o++] = 0xde; out[o++] = 0; out[o++] = (uint8_t)total; }
-#pragma unroll
-  for (int i = 0; i < FLAT_MAX_KEYS; i++) {
-    if (i < (int)tc) {
-      const uint32_t e = te[i];
-      const uint32_t kp = e & 0xff, kl = (e >> 8) & 0xff;
-      for (uint32_t j = 0; j < 1 + kl; j++) out[o++] = tgt[kp + j];
-      const uint32_t m = (tsrc >> (4 * i)) & 0xf;
-      const uint8_t* vd = tgt;
-      uint32_t vp = kp + 1 + kl, vl = (e >> 16) & 0xff;
-      for (int j = 0; j < FLAT_MAX_KEYS; j++) {  // source value wins
-        if (m == (uint32_t)(j + 1)) { vd = src; vp = (se[j] & 0xff) + 1 + ((se[j] >> 8) & 0xff); vl = (se[j] >> 16) & 0xff; }
-      }
-      for (uint32_t j = 0; j < vl; j++) out[o++] = vd[vp + j];
-    }
+  p = 1;
+  for (uint32_t i = 0; i < tc; i++) {
+    uint32_t kl, vl;
+    flat_entry(tgt, nt, p, kl, vl);
+    for (uint32_t j = 0; j < 1 + kl; j++) out[o++] = tgt[p + j];
+    const uint32_t f = flat_find(src, ns, sc, tgt + p + 1, kl);  // the source value wins
+    const uint8_t* v = f ? src + (f & 0xffff) : tgt + p + 1 + kl;
+    const uint32_t len = f ? (f >> 16) : vl;
+    for (uint32_t j = 0; j < len; j++) out[o++] = v[j];
+    p += 1 + kl + vl;
   }
-#pragma unroll
-  for (int i = 0; i < FLAT_MAX_KEYS; i++) {
-    if (i < (int)sc && !((smatch >> i) & 1)) {
-      const uint32_t e = se[i];
-      const uint32_t kp = e & 0xff, len = 1 + ((e >> 8) & 0xff) + ((e >> 16) & 0xff);
-      for (uint32_t j = 0; j < len; j++) out[o++] = src[kp + j];
-    }
+  p = 1;
+  for (uint32_t i = 0; i < sc; i++) {
+    uint32_t kl, vl;
+    flat_entry(src, ns, p, kl, vl);
+    if (!flat_find(tgt, nt, tc, src + p + 1, kl))
+      for (uint32_t j = 0; j < 1 + kl + vl; j++) out[o++] = src[p + j];
+    p += 1 + kl + vl;
   }
   olen = o;
   return true;

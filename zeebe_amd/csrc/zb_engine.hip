@@ -116,6 +116,7 @@ struct zb_engine {
   bool staged_pending = false;  // the staged batch has not been injected yet (zb_reset(keep) re-arms it)
   uint16_t staged_elem = NO_ELEM;  // process element of the staged CREATEs ...
   bool staged_uniform = true;      // ... when they all address the same one
+  uint32_t staged_max_len = 1;     // longest staged CREATE payload (uniform batch merge bounds)
 
   // submitted command ranges (serialization of CREATE commands / rejections)
   std::vector<CmdRange> ranges;
@@ -133,6 +134,8 @@ struct zb_engine {
   uint4* t_wtot = nullptr;
   TrajBase* t_wbase = nullptr;
   TrajCtl* t_ctl = nullptr;
+  MergeGen* t_mgen = nullptr;     // [TRAJ_MAX_GENERATIONS] uniform batch merge slots
+  uint64_t* t_wstats = nullptr;   // [t_nwg_cap][6] emit statistics per workgroup
   TrajCtl* h_ctl_pinned = nullptr;
 
   // timing
@@ -252,8 +255,11 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st)
   }
   if (nwg > e->t_nwg_cap) {
     if (e->t_wcount) (void)hipFree(e->t_wcount);
+    if (e->t_wstats) (void)hipFree(e->t_wstats);
     e->t_wcount = nullptr;
+    e->t_wstats = nullptr;
     HIPCHECK(e, hipMalloc(&e->t_wcount, nwg * sizeof(uint32_t)));
+    HIPCHECK(e, hipMalloc(&e->t_wstats, nwg * 6 * sizeof(uint64_t)));
     e->t_nwg_cap = nwg;
   }
   TrajCtl c{};
@@ -289,6 +295,9 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st)
   p.wtot = e->t_wtot;
   p.wbase = e->t_wbase;
   p.ctl = e->t_ctl;
+  p.mgen = e->t_mgen;
+  p.wstats = e->t_wstats;
+  p.max_create = e->staged_max_len;
   p.hdr = e->hdr + (e->wave & 1);
   p.err = e->derr;
   p.stats = e->dstats;
@@ -376,6 +385,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->t_ctl, sizeof(TrajCtl)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_wtot, TRAJ_WAVE_CAP * sizeof(uint4)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_wbase, TRAJ_WAVE_CAP * sizeof(TrajBase)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->t_mgen, TRAJ_MAX_GENERATIONS * sizeof(MergeGen)) != hipSuccess) return cleanup(ZB_ENOMEM);
   e->ev.resize(EV_PER_WAVE * WAVES_PER_SYNC);
   for (auto& x : e->ev)
     if (hipEventCreate(&x) != hipSuccess) return cleanup(ZB_EDEVICE);
@@ -396,7 +406,7 @@ void zb_engine_destroy(zb_engine* e) {
     if (x) (void)hipEventDestroy(x);
   void* ps[] = {e->log, e->links, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
                 e->merge_jobs, e->cond_jobs, e->job_counts, e->cw, e->stage, e->info, e->block_agg, e->block_off,
-                e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl};
+                e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->h_hdr_pinned) (void)hipHostFree(e->h_hdr_pinned);
@@ -508,6 +518,7 @@ int zb_submit_creates(zb_engine* e, const char* pid, int32_t version, int64_t wo
   if (e->staged.empty()) {
     e->staged_elem = pelem;
     e->staged_uniform = true;
+    e->staged_max_len = 1;
   } else if (n > 0 && pelem != e->staged_elem) {
     e->staged_uniform = false;
   }
@@ -532,6 +543,7 @@ int zb_submit_creates(zb_engine* e, const char* pid, int32_t version, int64_t wo
       if (!((b & 0xf0) == 0x80 || b == 0xde || b == 0xdf))
         return fail(e, ZB_EINVAL, "Document has invalid format. On root level an object is only allowed.");
       ref = add_blob(e->staged_arena, p, (uint32_t)len);
+      e->staged_max_len = std::max<uint32_t>(e->staged_max_len, (uint32_t)len);
     }
     zb_rec d;
     d.key = -1;

@@ -161,7 +161,15 @@ struct TrajCtl {
   uint64_t st[6];      // emit pass statistics: transitions, completed, created, merges, merge bytes, cond bytes
 };
 struct TrajBase {      // generation w: log position of its follow-ups, key generator values
-  int64_t pos, wf, job, pad;
+  int64_t pos, wf, job, mbase;  // mbase: arena byte offset of the batch's merge results of generation w
+};
+
+// Uniform batch (zb_traj.hip): the representative instance's default output merge of generation w,
+// with symbolic source / target payloads (PAY_CREATE, PAY_MERGE | w', literal refs) and the slot
+// stride that bounds every instance's result. The emit pass writes instance i's merge result of
+// generation w at wbase[w].mbase + i * stride: no arena allocation (no atomic) on the hot path.
+struct MergeGen {
+  uint32_t src, tgt, stride, has;
 };
 
 struct TrajParams {
@@ -192,6 +200,10 @@ struct TrajParams {
   uint32_t* err;
   uint64_t* stats;
   uint64_t log_cap, row_cap, arena_cap;
+  MergeGen* mgen;        // [wcap] uniform batch: per-generation merge slots (written by the count pass)
+  uint64_t* wstats;      // [nwg][6] emit-pass statistics per workgroup (reduced by k_traj_commit)
+  uint32_t max_create;   // longest CREATE payload of the batch (merge result bounds)
+  uint32_t pad2;
 };
 
 void launch_traj_count(const TrajParams& p, hipStream_t stream);

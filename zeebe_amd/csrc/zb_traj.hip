@@ -53,12 +53,18 @@ enum TrajFlags : uint8_t {
 enum TrajErr : uint32_t { TE_FALLBACK = 1u, TE_REGEN = 1u << 30 };
 
 // flat-merge staging in LDS (emit pass): per thread the two input blobs and the output blob
-constexpr int FM_WORDS = 16;                  // 64-byte blob slots: documents of <= 60 bytes
+constexpr int FM_WORDS = 12;                  // 48-byte blob slots: documents of <= 44 bytes
 constexpr int FM_BYTES = FM_WORDS * 4;
 constexpr int FM_STRIDE = 3 * FM_WORDS + 1;   // odd stride: lanes at the same offset hit distinct banks
 
+// Keys inside a trajectory are 32-bit ordinals of the partition's generators within the batch:
+// wf key = wf_start + 5 * ordinal, job key = job_start + 5 * ordinal (every key a batch record
+// carries is created by the batch); NOK stands for the null key -1.
+constexpr uint32_t NOK = 0xffffffffu;
+constexpr uint32_t JOB_ZERO = 0xfffffffeu;  // row job key 0 (no job created yet)
+
 struct TRec {
-  int64_t key, scope_key;
+  uint32_t key, scope_key;
   uint32_t payload;
   uint16_t elem;
   uint8_t intent, kind;
@@ -67,15 +73,13 @@ struct TRec {
 
 // Per-instance state lives in ext-vector registers: a dynamic index becomes an extract / insert
 // element (selects), never an address, so nothing is spilled to scratch.
-typedef int64_t i64x4 __attribute__((ext_vector_type(TR)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(TR)));
 typedef int32_t i32x4 __attribute__((ext_vector_type(TR)));
-typedef int64_t i64x2 __attribute__((ext_vector_type(TF)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(TF)));
 
 // One generation of one instance (<= TF records), structure of vectors
 struct Gen {
-  i64x2 key, sk;
+  u32x2 key, sk;
   u32x2 pay;
   u32x2 m0;  // elem | intent << 16 | kind << 24
   u32x2 m1;  // rself | rscope << 8 | flags << 16 | ord << 24
@@ -96,12 +100,12 @@ struct Gen {
 
 // One workflow instance: its element instances (local rows) and its current generation.
 struct Inst {
-  i64x4 rkey, rsk, rjob;
+  u32x4 rkey, rjob;  // key ordinals (the row's scope key is its parent's key)
   u32x4 rpay;
   u32x4 rmeta;  // elem | state << 16 | parent << 24
   i32x4 rnch;
   uint32_t used, to_free;
-  int64_t inst_key;
+  uint32_t inst_key;
   Gen cur, nx;
   int nc, nn, nwf, njob;
   // this generation's payload work: one merge and one incident detail at most
@@ -119,6 +123,10 @@ struct Inst {
   __device__ __forceinline__ uint16_t elem(int r) const { return (uint16_t)rmeta[r]; }
   __device__ __forceinline__ uint8_t parent(int r) const { return (uint8_t)(rmeta[r] >> 24); }
   __device__ __forceinline__ bool alive(int r) const { return r != LN && state(r) != 0; }
+  __device__ __forceinline__ uint32_t scope_of(int r) const {
+    const int p = parent(r);
+    return p == LN ? NOK : rkey[p];
+  }
   __device__ __forceinline__ void set_state(int r, uint8_t s) {
     rmeta[r] = (rmeta[r] & 0xff00ffffu) | ((uint32_t)s << 16);
   }
@@ -148,15 +156,34 @@ struct Inst {
   }
 };
 
+__device__ __forceinline__ int64_t wf_key(const TrajParams& P, uint32_t o) {
+  return o == NOK ? -1 : P.wf_start + 5 * (int64_t)o;
+}
+__device__ __forceinline__ int64_t job_key(const TrajParams& P, uint32_t o) {
+  return o == NOK ? -1 : P.job_start + 5 * (int64_t)o;
+}
+
 __device__ __forceinline__ uint32_t arena_len(const uint8_t* arena, uint32_t ref) {
   return *(const uint32_t*)(arena + (uint64_t)ref * 8);
 }
+
+// symbolic payload refs of a trace (literal refs are static blobs below 2^28)
+constexpr uint32_t PAY_MERGE = 0x80000000u;   // | generation: that generation's merge result
+constexpr uint32_t PAY_CREATE = 0xC0000000u;  // the instance's CREATE payload
+__device__ __forceinline__ uint32_t sym_bound(const TrajParams& P, uint32_t sym);
 __device__ __forceinline__ uint32_t tblob_bytes(uint32_t len) { return (4 + len + 7) & ~7u; }
+
+// upper bound of the length of the document behind a symbolic payload ref (trace count pass)
+__device__ __forceinline__ uint32_t sym_bound(const TrajParams& P, uint32_t sym) {
+  if (sym == PAY_CREATE) return P.max_create;
+  if (sym & PAY_MERGE) return P.mgen[sym & 0xffff].stride - 4;
+  return arena_len(P.arena, sym);
+}
 
 __device__ __forceinline__ void t_incident(Inst& I, const TRec& rec, int64_t pos, uint8_t code, uint8_t a, uint8_t b, uint16_t q) {
   // BpmnStepContext.raiseIncident: IncidentIntent.CREATE command, key null, CONDITION_ERROR
   TRec s;
-  s.key = -1;
+  s.key = NOK;
   s.scope_key = rec.key;  // activityInstanceKey = failing record's key
   s.payload = 0;
   s.elem = rec.elem;
@@ -226,7 +253,7 @@ __device__ __forceinline__ void t_step(const TrajParams& P, Inst& I, const TRec&
       break;
     }
     case ST_CREATE_JOB: {  // CreateJobHandler :33-56 -> JOB CREATE command, key null
-      s.key = -1;
+      s.key = NOK;
       s.scope_key = rec.key;  // headers.activityInstanceKey
       s.intent = JI_CREATE;
       s.kind = make_kind(ZB_VT_JOB, ZB_RT_COMMAND, I.nn > 0);
@@ -267,7 +294,7 @@ __device__ __forceinline__ void t_step(const TrajParams& P, Inst& I, const TRec&
     case ST_CONSUME_TOKEN: {  // ConsumeTokenHandler :30-43
       if (!scope_alive) { I.err |= TE_FALLBACK; return; }
       s.key = I.rkey[rscope];
-      s.scope_key = I.rsk[rscope];
+      s.scope_key = I.scope_of(rscope);
       s.elem = I.elem(rscope);
       s.payload = rec.payload;
       s.intent = WI_ELEMENT_COMPLETING;
@@ -324,7 +351,7 @@ __device__ __forceinline__ void t_step(const TrajParams& P, Inst& I, const TRec&
       s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
       s.rself = LN;
       I.remove(rself);
-      if (EMIT && rec.key == I.inst_key) I.completed += 1;
+      if (rec.key == I.inst_key) I.completed += 1;  // (statistics: emit pass / trace)
       I.push(s);
       break;
     }
@@ -346,7 +373,7 @@ __device__ __forceinline__ void t_record(const TrajParams& P, Inst& I, const TRe
       TRec s = rec;
       s.ord = ord;
       if (rec.elem == NO_ELEM) {
-        s.scope_key = pos;  // command position -> the serializer finds the submitted command value
+        s.scope_key = NOK;  // written as the command position (the serializer finds the command value)
         s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_COMMAND_REJECTION, I.nn > 0);
         s.flags = TK_INST;
         s.rself = LN; s.rscope = LN;
@@ -355,7 +382,7 @@ __device__ __forceinline__ void t_record(const TrajParams& P, Inst& I, const TRe
       }
       const int row = I.alloc();  // inserted when CREATED is processed
       if (row == LN) return;
-      s.scope_key = -1;
+      s.scope_key = NOK;
       s.flags = TK_WF | TK_INST;
       s.rself = (uint8_t)row; s.rscope = LN;
       s.intent = WI_CREATED;
@@ -371,8 +398,7 @@ __device__ __forceinline__ void t_record(const TrajParams& P, Inst& I, const TRe
         I.set_meta(r, rec.elem, WI_ELEMENT_READY, LN);
         I.rpay[r] = rec.payload;
         I.rkey[r] = rec.key;
-        I.rsk[r] = rec.scope_key;
-        I.rjob[r] = 0;
+        I.rjob[r] = JOB_ZERO;
         I.rnch[r] = 0;
         I.created += 1;
       } else if (rec.intent <= WI_ELEMENT_TERMINATED && rec.intent >= WI_START_EVENT_OCCURRED) {
@@ -393,13 +419,13 @@ __device__ __forceinline__ void t_record(const TrajParams& P, Inst& I, const TRe
       s.payload = P.elems[rec.elem].job_payload;
       I.push(s);
     } else if (rt == ZB_RT_EVENT && rec.intent == JI_CREATED) {  // JobCreatedProcessor :408-426
-      if (rec.scope_key > 0 && I.alive(rec.rself)) I.rjob[rec.rself] = rec.key;
+      if (rec.scope_key != NOK && I.alive(rec.rself)) I.rjob[rec.rself] = rec.key;
     } else if (rt == ZB_RT_EVENT && rec.intent == JI_COMPLETED) {  // JobCompletedEventProcessor :428-453
       const int r = rec.rself;
       if (!I.alive(r)) return;
       TRec s;
       s.key = rec.scope_key;
-      s.scope_key = I.rsk[r];
+      s.scope_key = I.scope_of(r);
       s.elem = I.elem(r);
       s.payload = rec.payload;
       s.intent = WI_ELEMENT_COMPLETING;
@@ -409,7 +435,7 @@ __device__ __forceinline__ void t_record(const TrajParams& P, Inst& I, const TRe
       s.flags = 0; s.ord = 0;
       I.set_state(r, WI_ELEMENT_COMPLETING);
       I.rpay[r] = rec.payload;
-      I.rjob[r] = -1;
+      I.rjob[r] = NOK;
       I.push(s);
     }
   }
@@ -462,7 +488,10 @@ __device__ __forceinline__ uint64_t wave_scan(uint64_t v) {
 // generation loop needs no workgroup synchronisation at all. COND: exclusive splits supported.
 // GEN: the general merge (merge_docs) backs up the flat fast path; without it a non-flat merge
 // makes the pass set ctl->regen and the host-side launch sequence reruns the pass with GEN.
-template <bool EMIT, bool UNI, bool COND, bool GEN>
+// TRACE (count pass of a uniform batch, one instance): payload refs are symbolic (PAY_CREATE, PAY_MERGE | w,
+// literal refs) so that each generation's merge gets a result bound valid for every instance of the
+// batch (MergeGen); the emit pass then places instance i's result at mbase(w) + i * stride(w).
+template <bool EMIT, bool UNI, bool COND, bool GEN, bool TRACE>
 __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
   __shared__ uint64_t s_scan[TWG / 64][2];
   __shared__ uint64_t s_abase;
@@ -475,21 +504,24 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
 
   Inst I;
   I.used = 0; I.to_free = 0;
-  I.rkey = 0; I.rsk = 0; I.rjob = 0; I.rpay = 0; I.rmeta = 0; I.rnch = 0;
+  I.rkey = 0; I.rjob = 0; I.rpay = 0; I.rmeta = 0; I.rnch = 0;
   I.cur.key = 0; I.cur.sk = 0; I.cur.pay = 0; I.cur.m0 = 0; I.cur.m1 = 0;
   I.nx = I.cur;
-  I.inst_key = -1;
+  I.inst_key = NOK;
   I.nc = 0; I.nn = 0; I.nwf = 0; I.njob = 0;
   I.merge = false; I.detail = false; I.m_src = I.m_tgt = I.m_len = 0;
   I.d_code = I.d_a = I.d_b = 0; I.d_q = 0; I.d_pos = 0;
   I.err = 0;
   I.transitions = I.completed = I.created = I.merges = I.cond_bytes = 0;
   I.merge_bytes = 0;
+  // lanes past the batch follow lane 0's control in a uniform batch: they must not write anything
+  const bool active = inst < P.n;
   int64_t fpos = P.log_base + inst;  // log position of the first record of the current generation
   if (inst < P.n) {
     const zb_rec d = P.log[fpos];
     TRec r;
-    r.key = d.key; r.scope_key = d.scope_key; r.payload = d.payload; r.elem = d.elem; r.intent = d.intent;
+    r.key = NOK; r.scope_key = NOK; r.payload = TRACE ? PAY_CREATE : d.payload; r.elem = d.elem;  // a CREATE
+    r.intent = d.intent;
     r.kind = d.kind; r.rself = LN; r.rscope = LN; r.flags = 0; r.ord = 0;
     I.cur.set(0, r);
     I.nc = 1;
@@ -502,49 +534,78 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
       if (!EMIT && threadIdx.x == 0) atomicOr(&ctl->flag, TE_FALLBACK);
       return;
     }
+    // ---- uniform batch: every lane of the wave follows the same trajectory, so the control half of the
+    // state (record kinds, intents, elements, row links, row states) is the same in all lanes; read it
+    // from the first lane so that the compiler keeps it in SGPRs and every branch below is scalar.
+    // Per-lane data (keys, payload refs) stays in VGPRs.
+    if (UNI) {
+#pragma unroll
+      for (int k = 0; k < TF; k++) {
+        I.cur.m0[k] = __builtin_amdgcn_readfirstlane(I.cur.m0[k]);
+        I.cur.m1[k] = __builtin_amdgcn_readfirstlane(I.cur.m1[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < TR; k++) {
+        I.rmeta[k] = __builtin_amdgcn_readfirstlane(I.rmeta[k]);
+        I.rnch[k] = __builtin_amdgcn_readfirstlane(I.rnch[k]);
+      }
+      I.nc = __builtin_amdgcn_readfirstlane(I.nc);
+      I.used = __builtin_amdgcn_readfirstlane(I.used);
+    }
     // ---- process this generation (log order inside the instance)
 #pragma unroll 1
     for (int k = 0; k < I.nc; k++) t_record<EMIT, COND>(P, I, I.cur.get(k), fpos + k);
     // ---- place the follow-ups
     uint64_t a = (uint64_t)I.nn | ((uint64_t)I.nwf << 16) | ((uint64_t)I.njob << 32);
     uint64_t bytes = 0;
-    if (EMIT) bytes = (I.merge ? tblob_bytes(I.m_len) : 0) + (I.detail ? 24 : 0);
+    if (EMIT && active) bytes = (I.merge ? tblob_bytes(I.m_len) : 0) + (I.detail ? 24 : 0);
     uint64_t ta = 0, tb = 0;
     if (!UNI) block_scan2(a, bytes, ta, tb, s_scan);
-    int64_t pos0, kwf, kjob;
+    int64_t pos0;
+    uint32_t kwf, kjob;  // key ordinals of this instance's first new wf / job key
     if (UNI) {
       // positions and keys are affine in the instance index; the arena is allocated per wave
       const uint64_t c = P.agg[w];
       const TrajBase wb = P.wbase[w];
       pos0 = wb.pos + inst * (int64_t)(c & 0xffff);
-      kwf = wb.wf + 5 * inst * (int64_t)((c >> 16) & 0xffff);
-      kjob = wb.job + 5 * inst * (int64_t)(c >> 32);
-      if (EMIT && __any(bytes != 0)) {
-        const uint64_t incl = wave_scan(bytes);
-        uint64_t base = 0;
-        if ((threadIdx.x & 63) == 63) base = atomicAdd((unsigned long long*)&ctl->arena_next, (unsigned long long)incl);
-        base = (uint64_t)__shfl((unsigned long long)base, 63, 64);
-        bytes = incl - bytes;
-        tb = base;  // per-wave arena base (s_abase below is per workgroup)
+      kwf = (uint32_t)(wb.wf + inst * (int64_t)((c >> 16) & 0xffff));
+      kjob = (uint32_t)(wb.job + inst * (int64_t)(c >> 32));
+      if (EMIT && I.merge) {
+        // this instance's merge slot of generation w (MergeGen: the stride bounds every instance's result)
+        const MergeGen g = P.mgen[w];
+        tb = (uint64_t)wb.mbase + (uint64_t)inst * g.stride;
+        bytes = 0;
+        if (!g.has || tblob_bytes(I.m_len) > g.stride) { I.err |= DE_UNSUPPORTED; tb = P.arena_cap; }
       }
     } else if (!EMIT) {
       if (threadIdx.x == 0) P.agg[(uint64_t)w * nwg + blockIdx.x] = ta;
       pos0 = 0;
-      kwf = 1 + 5 * (int64_t)((a >> 16) & 0xffff);
-      kjob = 2 + 5 * (int64_t)(a >> 32);
+      kwf = (uint32_t)((a >> 16) & 0xffff);  // placeholder ordinals: nothing in the count depends on key values
+      kjob = (uint32_t)(a >> 32);
     } else {
       const TrajBase wb = P.wbase[w];
       const uint4 off = P.woff[(uint64_t)w * nwg + blockIdx.x];
       pos0 = wb.pos + off.x + (int64_t)(a & 0xffff);
-      kwf = wb.wf + 5 * ((int64_t)off.y + (int64_t)((a >> 16) & 0xffff));
-      kjob = wb.job + 5 * ((int64_t)off.z + (int64_t)(a >> 32));
+      kwf = (uint32_t)(wb.wf + off.y + ((a >> 16) & 0xffff));
+      kjob = (uint32_t)(wb.job + off.z + (a >> 32));
       if (tb) {
         if (threadIdx.x == 0) s_abase = atomicAdd((unsigned long long*)&ctl->arena_next, (unsigned long long)tb);
         __syncthreads();
       }
     }
     uint32_t merged_ref = 0, detail_ref = 0;
-    if (EMIT && (I.merge || I.detail)) {
+    if (TRACE && inst == 0) {
+      MergeGen g{0, 0, 0, 0};
+      if (I.merge) {
+        g.src = I.m_src; g.tgt = I.m_tgt; g.has = 1;
+        const uint32_t bound = sym_bound(P, I.m_src) + sym_bound(P, I.m_tgt) + 8;  // emit reserves |s| + |t| + 8
+        g.stride = tblob_bytes(bound);
+        merged_ref = PAY_MERGE | (uint32_t)w;
+        I.merges += 1;
+      }
+      P.mgen[w] = g;
+    }
+    if (EMIT && active && (I.merge || I.detail)) {
       uint64_t at = (UNI ? tb : s_abase) + bytes;
       if (I.merge) {
         const uint32_t mb = tblob_bytes(I.m_len);
@@ -568,6 +629,10 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
               reg[2 * FM_WORDS] = olen;
               for (uint32_t k = 0; k < (olen + 7) / 4; k++) gd[k] = reg[2 * FM_WORDS + k];
             }
+          } else {
+            // larger flat documents: the same fast path straight on the arena
+            done = merge_flat((const uint8_t*)gs + 4, ns, (const uint8_t*)gt + 4, nt, (uint8_t*)gd + 4, I.m_len, olen);
+            if (done) gd[0] = olen;
           }
           if (!done) {
             if constexpr (GEN) {
@@ -605,9 +670,9 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
     for (int k = 0; k < TF; k++) {
       if (k < I.nn) {
         TRec s = I.nx.get(k);
-        if (s.flags & TK_WF) s.key = kwf + 5 * (int64_t)s.ord;
-        if (s.flags & TK_JOB) s.key = kjob + 5 * (int64_t)s.ord;
-        if (s.flags & TK_INST) I.inst_key = kwf + 5 * (int64_t)s.ord;
+        if (s.flags & TK_WF) s.key = kwf + s.ord;
+        if (s.flags & TK_JOB) s.key = kjob + s.ord;
+        if (s.flags & TK_INST) I.inst_key = kwf + s.ord;
         if (s.flags & TK_MERGED) s.payload = merged_ref;
         if (s.flags & TK_DETAIL) s.payload = detail_ref;
         if (s.flags & TK_ROW_INIT) {
@@ -615,15 +680,18 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
           I.set_meta(r, s.elem, WI_ELEMENT_READY, s.rscope);
           I.rpay[r] = s.payload;
           I.rkey[r] = s.key;
-          I.rsk[r] = s.scope_key;
-          I.rjob[r] = 0;
+          I.rjob[r] = JOB_ZERO;
           I.rnch[r] = 0;
         }
         s.flags = 0;
         I.cur.set(k, s);
-        if (EMIT) {
+        if (EMIT && active) {
           zb_rec d;
-          d.key = s.key; d.scope_key = s.scope_key; d.inst_key = I.inst_key; d.payload = s.payload;
+          const bool job_event = kind_vt(s.kind) == ZB_VT_JOB && kind_rt(s.kind) == ZB_RT_EVENT;
+          d.key = job_event ? job_key(P, s.key) : wf_key(P, s.key);
+          d.scope_key = kind_rt(s.kind) == ZB_RT_COMMAND_REJECTION ? P.log_base + inst : wf_key(P, s.scope_key);
+          d.inst_key = wf_key(P, I.inst_key);
+          d.payload = s.payload;
           d.elem = s.elem; d.intent = s.intent; d.kind = s.kind;
           if (pos0 + k < (int64_t)P.log_cap) P.log[pos0 + k] = d;
           else I.err |= DE_LOG_FULL;
@@ -650,6 +718,7 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
   }
 
   // ---- live element instances -> partition rows (instances stopped by an incident keep theirs)
+  if (!active) I.used = 0;
   uint32_t live = 0;
 #pragma unroll
   for (int k = 0; k < TR; k++)
@@ -679,23 +748,23 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
       m.flags = 0;
       m.nchild = I.rnch[k];
       P.rmeta[gid[k]] = m;
-      P.rkeys[gid[k]] = RowKeys{I.rkey[k], I.rsk[k], I.inst_key, I.rjob[k]};
+      const uint32_t jk = I.rjob[k];
+      P.rkeys[gid[k]] = RowKeys{wf_key(P, I.rkey[k]), wf_key(P, I.scope_of(k)), wf_key(P, I.inst_key),
+                                jk == JOB_ZERO ? 0 : job_key(P, jk)};
     }
   }
   // ---- statistics
+  if (!active) I.transitions = I.completed = I.created = I.merges = I.cond_bytes = 0, I.merge_bytes = 0;
   uint64_t s0 = (uint64_t)I.transitions | ((uint64_t)I.completed << 32);
   uint64_t s1 = (uint64_t)I.created | ((uint64_t)I.merges << 32);
   block_scan2(s0, s1, ta, tb, s_scan);
   uint64_t s2 = I.merge_bytes, s3 = I.cond_bytes, tc, td;
   block_scan2(s2, s3, tc, td, s_scan);
-  if (threadIdx.x == 0) {
-    atomicAdd((unsigned long long*)&ctl->st[0], (unsigned long long)(ta & 0xffffffffu));
-    atomicAdd((unsigned long long*)&ctl->st[1], (unsigned long long)(ta >> 32));
-    atomicAdd((unsigned long long*)&ctl->st[2], (unsigned long long)(tb & 0xffffffffu));
-    atomicAdd((unsigned long long*)&ctl->st[3], (unsigned long long)(tb >> 32));
-    atomicAdd((unsigned long long*)&ctl->st[4], (unsigned long long)tc);
-    atomicAdd((unsigned long long*)&ctl->st[5], (unsigned long long)td);
+  if (threadIdx.x == 0) {  // per-workgroup partials (no same-address atomics): k_traj_commit reduces them
+    uint64_t* ws = P.wstats + (uint64_t)blockIdx.x * 6;
+    ws[0] = ta & 0xffffffffu; ws[1] = ta >> 32; ws[2] = tb & 0xffffffffu; ws[3] = tb >> 32; ws[4] = tc; ws[5] = td;
   }
+  if (!active) I.err = 0;
   if (I.err & TE_REGEN) atomicOr(&ctl->regen, 1u);
   const uint32_t derr = I.err & ~(uint32_t)(TE_FALLBACK | TE_REGEN);
   if (I.err & TE_FALLBACK) atomicOr(&ctl->derr, (uint32_t)DE_PROCESSING);  // count and emit passes disagree
@@ -749,18 +818,23 @@ __global__ void __launch_bounds__(1024) k_traj_scan(TrajParams P) {
 
 // one workgroup: generation bases (log position of generation w+1, key generator values at w)
 __global__ void __launch_bounds__(1024) k_traj_base(TrajParams P) {
-  __shared__ uint64_t s_w[16][3];
-  __shared__ uint64_t s_carry[3];
+  __shared__ uint64_t s_w[16][4];
+  __shared__ uint64_t s_carry[4];
   TrajCtl* ctl = P.ctl;
   if (ctl->flag) return;
   const uint32_t W = ctl->wmax;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (threadIdx.x < 3) s_carry[threadIdx.x] = 0;
+  const bool uni = P.uni != 0;
+  if (threadIdx.x < 4) s_carry[threadIdx.x] = 0;
   __syncthreads();
   for (uint32_t base = 0; base < W; base += 1024) {
     const uint32_t w = base + threadIdx.x;
-    uint64_t x[3] = {0, 0, 0};
+    uint64_t x[4] = {0, 0, 0, 0};
     if (w < W) {
+      if (uni) {  // merge slots of the generation: stride x instances
+        const MergeGen g = P.mgen[w];
+        if (g.has) x[3] = (uint64_t)g.stride * (uint64_t)P.uni;
+      }
       if (P.uni) {
         const uint64_t c = P.agg[w];
         x[0] = (c & 0xffff) * (uint64_t)P.uni; x[1] = ((c >> 16) & 0xffff) * (uint64_t)P.uni;
@@ -770,9 +844,9 @@ __global__ void __launch_bounds__(1024) k_traj_base(TrajParams P) {
         x[0] = t.x; x[1] = t.y; x[2] = t.z;
       }
     }
-    uint64_t ex[3];
+    uint64_t ex[4];
 #pragma unroll
-    for (int f = 0; f < 3; f++) {
+    for (int f = 0; f < 4; f++) {
       uint64_t y = x[f];
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
@@ -783,9 +857,9 @@ __global__ void __launch_bounds__(1024) k_traj_base(TrajParams P) {
       if (lane == 63) s_w[wv][f] = y;
     }
     __syncthreads();
-    uint64_t tot[3] = {0, 0, 0};
+    uint64_t tot[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int f = 0; f < 3; f++) {
+    for (int f = 0; f < 4; f++) {
       for (int k = 0; k < 16; k++) {
         if (k < wv) ex[f] += s_w[k][f];
         tot[f] += s_w[k][f];
@@ -795,16 +869,17 @@ __global__ void __launch_bounds__(1024) k_traj_base(TrajParams P) {
     if (w < W) {
       TrajBase b;
       b.pos = P.log_base + P.n + (int64_t)ex[0];
-      b.wf = P.wf_start + 5 * (int64_t)ex[1];
-      b.job = P.job_start + 5 * (int64_t)ex[2];
-      b.pad = 0;
+      b.wf = (int64_t)ex[1];  // key ordinals (zb_traj.hip keys are wf_start / job_start + 5 * ordinal)
+      b.job = (int64_t)ex[2];
+      b.mbase = (int64_t)(ctl->arena_start + ex[3]);
       P.wbase[w] = b;
     }
     __syncthreads();
-    if (threadIdx.x < 3) s_carry[threadIdx.x] += tot[threadIdx.x];
+    if (threadIdx.x < 4) s_carry[threadIdx.x] += tot[threadIdx.x];
     __syncthreads();
   }
   if (threadIdx.x == 0) {
+    if (uni) ctl->arena_next = ctl->arena_start + s_carry[3];  // every merge slot of the batch
     ctl->end = P.log_base + P.n + (int64_t)s_carry[0];
     ctl->wf_next = P.wf_start + 5 * (int64_t)s_carry[1];
     ctl->job_next = P.job_start + 5 * (int64_t)s_carry[2];
@@ -816,16 +891,28 @@ __global__ void __launch_bounds__(1024) k_traj_base(TrajParams P) {
 __global__ void k_traj_regen(TrajParams P) {
   TrajCtl* ctl = P.ctl;
   if (ctl->flag || !ctl->regen) return;
-  ctl->arena_next = ctl->arena_start;
+  if (!P.uni) ctl->arena_next = ctl->arena_start;  // (uniform batch: merge slots fixed by k_traj_base)
   ctl->rows_next = ctl->rows_start;
   ctl->derr = 0;
-  for (int i = 0; i < 6; i++) ctl->st[i] = 0;
 }
 
-__global__ void k_traj_commit(TrajParams P) {
+__global__ void __launch_bounds__(256) k_traj_commit(TrajParams P) {
+  __shared__ uint64_t s_st[256 / 64][6];
   const TrajCtl* ctl = P.ctl;
   if (ctl->flag) return;
-  for (int i = 0; i < 6; i++) P.stats[i] += ctl->st[i];
+  uint64_t st[6] = {0, 0, 0, 0, 0, 0};
+  for (int b = threadIdx.x; b < P.nwg; b += blockDim.x)
+#pragma unroll
+    for (int f = 0; f < 6; f++) st[f] += P.wstats[(uint64_t)b * 6 + f];
+#pragma unroll
+  for (int f = 0; f < 6; f++) {
+    uint64_t x = st[f];
+    for (int d = 32; d >= 1; d >>= 1) x += (uint64_t)__shfl_down((unsigned long long)x, d, 64);
+    if ((threadIdx.x & 63) == 0) s_st[threadIdx.x >> 6][f] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  for (int f = 0; f < 6; f++) P.stats[f] += s_st[0][f] + s_st[1][f] + s_st[2][f] + s_st[3][f];
   if (ctl->derr) atomicOr(P.err, ctl->derr);
   WaveHdr h = *P.hdr;
   h.begin = h.end = h.gen_end = ctl->end;
@@ -842,15 +929,15 @@ __global__ void k_traj_commit(TrajParams P) {
 // conditions are compiled into the count / emit kernels only when the model has exclusive splits
 // (a uniform batch never has any), keeping the condition VM's call frame out of the other variants
 void launch_traj_count(const TrajParams& p, hipStream_t s) {
-  if (p.cond) hipLaunchKernelGGL((k_traj<false, false, true, false>), dim3(p.nwg), dim3(TWG), 0, s, p);
-  else hipLaunchKernelGGL((k_traj<false, false, false, false>), dim3(p.nwg), dim3(TWG), 0, s, p);
+  if (p.cond) hipLaunchKernelGGL((k_traj<false, false, true, false, false>), dim3(p.nwg), dim3(TWG), 0, s, p);
+  else hipLaunchKernelGGL((k_traj<false, false, false, false, false>), dim3(p.nwg), dim3(TWG), 0, s, p);
 }
 // uniform batch: count one representative instance (the first CREATE), one workgroup
 void launch_traj_count_uniform(const TrajParams& p, hipStream_t s) {
   TrajParams q = p;
   q.n = 1;
   q.nwg = 1;
-  hipLaunchKernelGGL((k_traj<false, false, false, false>), dim3(1), dim3(TWG), 0, s, q);
+  hipLaunchKernelGGL((k_traj<false, false, false, false, true>), dim3(1), dim3(TWG), 0, s, q);
 }
 void launch_traj_scan(const TrajParams& p, hipStream_t s) {
   if (!p.uni) hipLaunchKernelGGL(k_traj_scan, dim3(p.wcap), dim3(1024), 0, s, p);
@@ -859,19 +946,19 @@ void launch_traj_scan(const TrajParams& p, hipStream_t s) {
 void launch_traj_emit(const TrajParams& p, hipStream_t s) {
   const dim3 g(p.nwg), b(TWG);
   if (p.uni) {
-    hipLaunchKernelGGL((k_traj<true, true, false, false>), g, b, 0, s, p);
+    hipLaunchKernelGGL((k_traj<true, true, false, false, false>), g, b, 0, s, p);
     hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
-    hipLaunchKernelGGL((k_traj<true, true, false, true>), g, b, 0, s, p);
+    hipLaunchKernelGGL((k_traj<true, true, false, true, false>), g, b, 0, s, p);
   } else if (p.cond) {
-    hipLaunchKernelGGL((k_traj<true, false, true, false>), g, b, 0, s, p);
+    hipLaunchKernelGGL((k_traj<true, false, true, false, false>), g, b, 0, s, p);
     hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
-    hipLaunchKernelGGL((k_traj<true, false, true, true>), g, b, 0, s, p);
+    hipLaunchKernelGGL((k_traj<true, false, true, true, false>), g, b, 0, s, p);
   } else {
-    hipLaunchKernelGGL((k_traj<true, false, false, false>), g, b, 0, s, p);
+    hipLaunchKernelGGL((k_traj<true, false, false, false, false>), g, b, 0, s, p);
     hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
-    hipLaunchKernelGGL((k_traj<true, false, false, true>), g, b, 0, s, p);
+    hipLaunchKernelGGL((k_traj<true, false, false, true, false>), g, b, 0, s, p);
   }
-  hipLaunchKernelGGL(k_traj_commit, dim3(1), dim3(1), 0, s, p);
+  hipLaunchKernelGGL(k_traj_commit, dim3(1), dim3(256), 0, s, p);
 }
 
 }  // namespace zbg
