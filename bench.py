@@ -23,6 +23,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BYTES_PER_TRANSITION = 96  # 32 B row read + 32 B row write + 32 B record descriptor
+# HBM bytes of the emit kernel from the committed rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE: separate
+# runs of this script with --steps 1; see profiles/r01/pmc_v4.json for the command and the gfx950 correction)
+PMC_FILE = os.path.join(ROOT, "profiles", "r01", "pmc_v4.json")
 
 
 def parse():
@@ -137,6 +140,11 @@ def main():
     else:
         all_transitions, all_completed = float(tot["transitions"]), float(tot["completed"])
 
+    traffic = None
+    if n == 1_000_000 and a.tasks == 20 and os.path.exists(PMC_FILE):
+        with open(PMC_FILE) as f:
+            traffic = json.load(f)["emit_traffic_bytes"]
+
     if rank == 0:
         alg_bytes = BYTES_PER_TRANSITION * tot["transitions"] + tot["merge_bytes"] + tot["cond_bytes"]
         kernel_s = tot["kernel_ms"] / 1e3
@@ -164,7 +172,10 @@ def main():
             "kernel_ms_per_step": {"total": tot["kernel_ms"] / a.steps, "process_or_count": tot["process_ms"] / a.steps,
                                    "scan_emit": tot["emit_ms"] / a.steps, "aux": tot["aux_ms"] / a.steps},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_note": "HBM bytes per launch of the emit kernel (FETCH_SIZE x2 + WRITE_SIZE, "
+                                         "profiles/r01/pmc_v4.json); below the algorithmic bytes because element "
+                                         "instances stay in registers instead of SoA rows",
                          "kernel": "zbg::k_traj (count + emit passes)" if tot["path"] == 1 else
                                    "zbg::k_process/k_scan/k_emit/k_merge", "launches": tot["launches"],
                          "avg_launch_us": tot["kernel_ms"] * 1e3 / max(tot["launches"], 1),

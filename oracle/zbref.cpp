@@ -52,7 +52,9 @@ enum WfIntent : uint8_t {
 };
 enum JobIntentE : uint8_t { JOB_CREATE = 0, JOB_CREATED = 1, JOB_COMPLETED = 5, JOB_CANCEL = 12 };
 enum IncidentIntentE : uint8_t { INCIDENT_CREATE = 0 };
-enum WisIntent : uint8_t { WIS_CORRELATE = 2, WIS_CORRELATED = 3 };
+enum WisIntent : uint8_t { WIS_CORRELATE = 0, WIS_CORRELATED = 1 };  // WorkflowInstanceSubscriptionIntent.java:19-20
+enum MsgIntent : uint8_t { MSG_PUBLISH = 0, MSG_PUBLISHED = 1, MSG_DELETE = 2, MSG_DELETED = 3 };  // MessageIntent.java:19-23
+enum MsgSubIntent : uint8_t { MSUB_OPEN = 0, MSUB_OPENED = 1 };  // MessageSubscriptionIntent.java:19-20
 enum RejectionTypeE : uint8_t { REJ_BAD_VALUE = 0, REJ_NOT_APPLICABLE = 1, REJ_PROCESSING_ERROR = 2, REJ_NULL = 255 };
 enum ErrorTypeE : uint8_t { ERR_UNKNOWN = 0, ERR_IO_MAPPING = 1, ERR_JOB_NO_RETRIES = 2, ERR_CONDITION = 3 };
 
@@ -159,20 +161,58 @@ struct IncidentValue {  // IncidentRecord.java
   }
 };
 
-struct WisValue {  // WorkflowInstanceSubscriptionRecord (subscription/message/data)
-  int32_t partition_id = 0;
+// WorkflowInstanceSubscriptionRecord.java:26-38: four properties, no partition id (pinned by
+// IntermediateMessageCatchEventTest.java:357-362, containsExactly)
+struct WisValue {
   int64_t workflow_instance_key = -1;
   int64_t activity_instance_key = -1;
   bytes message_name;
   bytes payload = EMPTY_DOCUMENT;
   bytes encode() const {
     MpWriter w;
-    w.map_header(5);
-    w.str("partitionId"); w.integer(partition_id);
+    w.map_header(4);
     w.str("workflowInstanceKey"); w.integer(workflow_instance_key);
     w.str("activityInstanceKey"); w.integer(activity_instance_key);
     w.str("messageName"); w.str(message_name);
     w.str("payload"); w.bin(payload);
+    return w.b;
+  }
+};
+
+// MessageSubscriptionRecord.java:26-41 (pinned by IntermediateMessageCatchEventTest.java:132-138)
+struct MsgSubValue {
+  int32_t wf_partition = 0;
+  int64_t workflow_instance_key = -1;
+  int64_t activity_instance_key = -1;
+  bytes message_name;
+  bytes correlation_key;
+  bytes encode() const {
+    MpWriter w;
+    w.map_header(5);
+    w.str("workflowInstancePartitionId"); w.integer(wf_partition);
+    w.str("workflowInstanceKey"); w.integer(workflow_instance_key);
+    w.str("activityInstanceKey"); w.integer(activity_instance_key);
+    w.str("messageName"); w.str(message_name);
+    w.str("correlationKey"); w.str(correlation_key);
+    return w.b;
+  }
+};
+
+// MessageRecord.java:26-42 (payload is a DocumentProperty: binary, {} by default; messageId "" by default)
+struct MessageValue {
+  bytes name;
+  bytes correlation_key;
+  int64_t ttl = 0;
+  bytes payload = EMPTY_DOCUMENT;
+  bytes message_id;
+  bytes encode() const {
+    MpWriter w;
+    w.map_header(5);
+    w.str("name"); w.str(name);
+    w.str("correlationKey"); w.str(correlation_key);
+    w.str("timeToLive"); w.integer(ttl);
+    w.str("payload"); w.bin(payload);
+    w.str("messageId"); w.str(message_id);
     return w.b;
   }
 };
@@ -190,12 +230,16 @@ struct Record {
   JobValue job;
   IncidentValue inc;
   WisValue wis;
+  MsgSubValue msub;
+  MessageValue msg;
   bytes encode_value() const {
     switch (value_type) {
       case VT_WORKFLOW_INSTANCE: return wf.encode();
       case VT_JOB: return job.encode();
       case VT_INCIDENT: return inc.encode();
       case VT_WORKFLOW_INSTANCE_SUBSCRIPTION: return wis.encode();
+      case VT_MESSAGE_SUBSCRIPTION: return msub.encode();
+      case VT_MESSAGE: return msg.encode();
     }
     return bytes();
   }
@@ -513,14 +557,17 @@ struct KeyGenerator {  // KeyGenerator.java:28-56
   int64_t next_key() { int64_t k = next; next += step; return k; }
 };
 
-// A side effect emitted by the engine (response / message-subscription open).
+// A side effect the processors hand to the subscription transport (SubscriptionCommandSender.java:83-128)
 struct SideEffect {
-  int kind;  // 1 = open message subscription
+  int kind;                 // 1 = open message subscription, 2 = correlate workflow instance subscription
   int64_t workflow_instance_key;
   int64_t activity_instance_key;
   bytes message_name;
-  bytes correlation_key;
-  int32_t partition;  // target partition (abs(hash % P))
+  bytes correlation_key;    // kind 1
+  int32_t partition;        // target: kind 1 abs(hash % P) (SubscriptionCommandSender.java:105-109), kind 2 the
+                            // workflow instance partition (:111-128)
+  int32_t wf_partition;     // kind 1: the sending (workflow) partition
+  bytes payload;            // kind 2: the message payload
 };
 
 // ------------------------------------------------------------------------------ engine
@@ -532,6 +579,12 @@ class Engine {
   std::vector<SideEffect> side_effects;
   KeyGenerator wf_keys{1, 5};
   KeyGenerator job_keys{2, 5};
+  KeyGenerator msg_keys{0, 1};  // message stream processor (MessageService.java:91)
+  // MessageSubscriptionDataStore / MessageDataStore: insertion-ordered lists, linear scans
+  struct StoredSub { int32_t wfp; int64_t wik, aik; bytes name, ck; };
+  struct StoredMsg { bytes name, ck, payload, id; int64_t ttl, key; };
+  std::vector<StoredSub> subs;
+  std::vector<StoredMsg> msgs;
   ElementInstanceIndex index;
   std::vector<std::unique_ptr<Workflow>> workflows;
   std::map<std::pair<int64_t, bytes>, bytes> job_payloads;  // (workflow key, activity id) -> completion payload
@@ -603,12 +656,40 @@ class Engine {
     r.record_type = RT_COMMAND;
     r.value_type = VT_WORKFLOW_INSTANCE_SUBSCRIPTION;
     r.intent = WIS_CORRELATE;
-    r.key = -1;
-    r.wis.partition_id = partition_id;
+    r.key = (int64_t)log.size();  // positionAsKey (SubscriptionApiCommandMessageHandler.java:131-151)
     r.wis.workflow_instance_key = wf_instance_key;
     r.wis.activity_instance_key = activity_instance_key;
     r.wis.message_name = name;
     r.wis.payload = payload.empty() ? EMPTY_DOCUMENT : payload;
+    append(std::move(r));
+  }
+
+  // SubscriptionApiCommandMessageHandler.onOpenMessageSubscription :94-110 (command key = position)
+  void submit_open(int32_t wfp, int64_t wik, int64_t aik, const bytes& name, const bytes& ck) {
+    Record r;
+    r.record_type = RT_COMMAND;
+    r.value_type = VT_MESSAGE_SUBSCRIPTION;
+    r.intent = MSUB_OPEN;
+    r.key = (int64_t)log.size();
+    r.msub.wf_partition = wfp;
+    r.msub.workflow_instance_key = wik;
+    r.msub.activity_instance_key = aik;
+    r.msub.message_name = name;
+    r.msub.correlation_key = ck;
+    append(std::move(r));
+  }
+  // ClientApiMessageHandler.handleExecuteCommandRequest :90-162: MESSAGE PUBLISH command, null key
+  void submit_publish(const bytes& name, const bytes& ck, int64_t ttl, const bytes& payload, const bytes& id) {
+    Record r;
+    r.record_type = RT_COMMAND;
+    r.value_type = VT_MESSAGE;
+    r.intent = MSG_PUBLISH;
+    r.key = -1;
+    r.msg.name = name;
+    r.msg.correlation_key = ck;
+    r.msg.ttl = ttl;
+    r.msg.payload = (payload.empty() || (payload.size() == 1 && (uint8_t)payload[0] == 0xc0)) ? EMPTY_DOCUMENT : payload;
+    r.msg.message_id = id;
     append(std::move(r));
   }
 
@@ -741,6 +822,11 @@ class Engine {
       else if (rec.record_type == RT_EVENT && rec.intent == JOB_COMPLETED) process_job_completed(rec);
     } else if (rec.value_type == VT_WORKFLOW_INSTANCE_SUBSCRIPTION) {
       if (rec.record_type == RT_COMMAND && rec.intent == WIS_CORRELATE) process_correlate(rec);
+    } else if (rec.value_type == VT_MESSAGE_SUBSCRIPTION) {  // message stream processor (MessageService.java:90-129)
+      if (rec.record_type == RT_COMMAND && rec.intent == MSUB_OPEN) process_open_subscription(rec);
+    } else if (rec.value_type == VT_MESSAGE) {
+      if (rec.record_type == RT_COMMAND && rec.intent == MSG_PUBLISH) process_publish(rec);
+      else if (rec.record_type == RT_COMMAND && rec.intent == MSG_DELETE) process_delete_message(rec);
     }
   }
 
@@ -840,6 +926,54 @@ class Engine {
     w_->stage(b);
     ei->state = ELEMENT_COMPLETING;
     ei->value = v;
+  }
+
+  // OpenMessageSubscriptionProcessor.processRecord :56-83
+  void process_open_subscription(const Record& rec) {
+    const MsgSubValue& v = rec.msub;
+    for (const StoredMsg& m : msgs) {  // MessageDataStore.findMessage: first match in insertion order
+      if (m.name == v.message_name && m.ck == v.correlation_key) {
+        side_effects.push_back({2, v.workflow_instance_key, v.activity_instance_key, v.message_name, bytes(),
+                                v.wf_partition, v.wf_partition, m.payload});
+        break;
+      }
+    }
+    stage_event(rec.key, VT_MESSAGE_SUBSCRIPTION, MSUB_OPENED, rec);
+    subs.push_back({v.wf_partition, v.workflow_instance_key, v.activity_instance_key, v.message_name,
+                    v.correlation_key});
+  }
+  // PublishMessageProcessor.processRecord :58-105 + correlateMessage :107-124
+  void process_publish(const Record& rec) {
+    const MessageValue& v = rec.msg;
+    if (!v.message_id.empty()) {  // MessageDataStore.hasMessage
+      for (const StoredMsg& m : msgs) {
+        if (!m.id.empty() && m.id == v.message_id && m.name == v.name && m.ck == v.correlation_key) {
+          write_rejection(rec, REJ_BAD_VALUE, "message with id '" + v.message_id + "' is already published");
+          return;
+        }
+      }
+    }
+    w_->new_batch();
+    const int64_t key = msg_keys.next_key();
+    Record a = rec;
+    a.key = key; a.record_type = RT_EVENT; a.intent = MSG_PUBLISHED;
+    w_->stage(a);
+    for (const StoredSub& sb : subs)  // MessageSubscriptionDataStore.findSubscriptions (insertion order)
+      if (sb.name == v.name && sb.ck == v.correlation_key)
+        side_effects.push_back({2, sb.wik, sb.aik, v.name, bytes(), sb.wfp, sb.wfp, v.payload});
+    if (v.ttl > 0) {
+      msgs.push_back({v.name, v.correlation_key, v.payload, v.message_id, v.ttl, key});
+    } else {
+      Record d = rec;
+      d.key = key; d.record_type = RT_EVENT; d.intent = MSG_DELETED;
+      w_->stage(d);
+    }
+  }
+  // DeleteMessageProcessor.processRecord :36-45
+  void process_delete_message(const Record& rec) {
+    stage_event(rec.key, VT_MESSAGE, MSG_DELETED, rec);
+    for (size_t i = 0; i < msgs.size(); i++)
+      if (msgs[i].key == rec.key) { msgs.erase(msgs.begin() + i); break; }
   }
 
   // canonical harness: the job processor as a deterministic FIFO participant
@@ -986,7 +1120,7 @@ class Engine {
         for (char c : ck) h = (int32_t)((uint32_t)h * 31u + (uint32_t)(int32_t)(int8_t)c);
         int32_t part = h % partition_count;
         if (part < 0) part = -part;
-        side_effects.push_back({1, v.workflow_instance_key, rec.key, el->message_name, ck, part});
+        side_effects.push_back({1, v.workflow_instance_key, rec.key, el->message_name, ck, part, partition_id, bytes()});
         break;
       }
       case S_TERMINATE_ELEMENT:
@@ -1087,6 +1221,38 @@ int zbref_submit_cancel(void* h, int64_t key) {
   ((Engine*)h)->submit_cancel(key);
   return 0;
 }
+
+int zbref_submit_open(void* h, int32_t wfp, int64_t wik, int64_t aik, const uint8_t* name, size_t nn,
+                      const uint8_t* ck, size_t nck) {
+  ((Engine*)h)->submit_open(wfp, wik, aik, bytes((const char*)name, nn), bytes((const char*)ck, nck));
+  return 0;
+}
+
+int zbref_submit_publish(void* h, const uint8_t* name, size_t nn, const uint8_t* ck, size_t nck, int64_t ttl,
+                         const uint8_t* p, size_t np, const uint8_t* id, size_t nid) {
+  ((Engine*)h)->submit_publish(bytes((const char*)name, nn), bytes((const char*)ck, nck), ttl,
+                               bytes((const char*)p, np), bytes((const char*)id, nid));
+  return 0;
+}
+
+int64_t zbref_side_effect_count(void* h) { return (int64_t)((Engine*)h)->side_effects.size(); }
+
+// kind/partition/wf_partition + keys; byte fields copied when their capacity (4096 each) suffices
+int zbref_side_effect_get(void* h, int64_t i, int32_t* ints, int64_t* keys, uint8_t* name, uint8_t* ck,
+                          uint8_t* payload, uint64_t* lens) {
+  const SideEffect& s = ((Engine*)h)->side_effects.at((size_t)i);
+  ints[0] = s.kind; ints[1] = s.partition; ints[2] = s.wf_partition;
+  keys[0] = s.workflow_instance_key; keys[1] = s.activity_instance_key;
+  const bytes* f[3] = {&s.message_name, &s.correlation_key, &s.payload};
+  uint8_t* d[3] = {name, ck, payload};
+  for (int k = 0; k < 3; k++) {
+    lens[k] = f[k]->size();
+    if (f[k]->size() <= 4096) std::memcpy(d[k], f[k]->data(), f[k]->size());
+  }
+  return 0;
+}
+
+void zbref_clear_side_effects(void* h) { ((Engine*)h)->side_effects.clear(); }
 
 int zbref_submit_correlate(void* h, int64_t wik, int64_t aik, const char* name, const uint8_t* p, size_t n) {
   ((Engine*)h)->submit_correlate(wik, aik, bytes(name), bytes((const char*)p, n));

@@ -41,6 +41,13 @@ def lib():
         L.zbref_submit_create.argtypes = [vp, cp, i32, i64, u8p, sz]
         L.zbref_submit_cancel.argtypes = [vp, i64]
         L.zbref_submit_correlate.argtypes = [vp, i64, i64, cp, u8p, sz]
+        L.zbref_submit_open.argtypes = [vp, i32, i64, i64, u8p, sz, u8p, sz]
+        L.zbref_submit_publish.argtypes = [vp, u8p, sz, u8p, sz, i64, u8p, sz, u8p, sz]
+        L.zbref_side_effect_count.restype = i64
+        L.zbref_side_effect_count.argtypes = [vp]
+        L.zbref_side_effect_get.argtypes = [vp, i64, ctypes.POINTER(i32), ctypes.POINTER(i64), ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
+        L.zbref_clear_side_effects.argtypes = [vp]
         L.zbref_run.restype = i64
         L.zbref_run.argtypes = [vp, i64]
         L.zbref_log_size.restype = i64
@@ -134,9 +141,40 @@ class Oracle:
     def cancel(self, key: int):
         self._L.zbref_submit_cancel(self._h, key)
 
-    def correlate(self, wf_instance_key: int, activity_instance_key: int, message_name: str, payload: bytes):
-        self._L.zbref_submit_correlate(self._h, wf_instance_key, activity_instance_key, message_name.encode(),
-                                       payload, len(payload))
+    def correlate(self, wf_instance_key: int, activity_instance_key: int, message_name, payload: bytes):
+        """WORKFLOW_INSTANCE_SUBSCRIPTION CORRELATE command (key = its log position)."""
+        if isinstance(message_name, str):
+            message_name = message_name.encode()
+        self._L.zbref_submit_correlate(self._h, wf_instance_key, activity_instance_key, message_name, payload,
+                                       len(payload))
+
+    def open_subscription(self, wf_partition: int, wf_instance_key: int, activity_instance_key: int,
+                          message_name: bytes, correlation_key: bytes):
+        """MESSAGE_SUBSCRIPTION OPEN command (key = its log position)."""
+        self._L.zbref_submit_open(self._h, wf_partition, wf_instance_key, activity_instance_key, message_name,
+                                  len(message_name), correlation_key, len(correlation_key))
+
+    def publish(self, name: bytes, correlation_key: bytes, payload: bytes = b"\x80", ttl: int = 0,
+                message_id: bytes = b""):
+        """MESSAGE PUBLISH command (null key)."""
+        self._L.zbref_submit_publish(self._h, name, len(name), correlation_key, len(correlation_key), ttl, payload,
+                                     len(payload), message_id, len(message_id))
+
+    def take_side_effects(self):
+        """Side effects since the last call, in emission order, as dicts (kind 1 open, 2 correlate)."""
+        n = self._L.zbref_side_effect_count(self._h)
+        out = []
+        ints = (ctypes.c_int32 * 3)()
+        keys = (ctypes.c_int64 * 2)()
+        lens = (ctypes.c_uint64 * 3)()
+        bufs = [ctypes.create_string_buffer(4096) for _ in range(3)]
+        for i in range(n):
+            self._L.zbref_side_effect_get(self._h, i, ints, keys, bufs[0], bufs[1], bufs[2], lens)
+            name, ck, payload = (bufs[k].raw[:lens[k]] for k in range(3))
+            out.append(dict(kind=ints[0], partition=ints[1], wf_partition=ints[2], wik=keys[0], aik=keys[1],
+                            name=name, ck=ck, payload=payload))
+        self._L.zbref_clear_side_effects(self._h)
+        return out
 
     def run(self, max_records: int = -1) -> int:
         n = self._L.zbref_run(self._h, max_records)
