@@ -265,3 +265,52 @@ def encode_float(v: float) -> bytes:
     buf = ctypes.create_string_buffer(16)
     n = lib().zbref_encode_float(v, buf)
     return buf.raw[:n]
+
+
+class OraclePartition(Oracle):
+    """An oracle partition with the partition interface of zeebe_amd.cluster (LocalCluster / DistCluster):
+    side effects become exchange records (zb_exchange_rec layout) sorted by target partition, stable in
+    emission order."""
+
+    def __init__(self, partition_id: int = 0, partition_count: int = 1):
+        super().__init__(partition_id, partition_count)
+        self.partition_id, self.partition_count = partition_id, partition_count
+        self._fx = []
+
+    def _harvest(self):
+        self._fx.extend(self.take_side_effects())
+
+    def pending(self, kind: int) -> int:
+        self._harvest()
+        return sum(1 for f in self._fx if f["kind"] == kind)
+
+    def outbox(self, kind: int):
+        from zeebe_amd import cluster
+
+        self._harvest()
+        mine = [f for f in self._fx if f["kind"] == kind]
+        self._fx = [f for f in self._fx if f["kind"] != kind]
+        mine.sort(key=lambda f: f["partition"])  # stable: emission order within a target
+        counts = [0] * self.partition_count
+        for f in mine:
+            counts[f["partition"]] += 1
+        return cluster.pack(mine), counts
+
+    def inbox(self, kind: int, buf):
+        from zeebe_amd import cluster
+
+        for r in cluster.unpack(buf.cpu().numpy() if hasattr(buf, "cpu") else buf):
+            if kind == cluster.KIND_OPEN:
+                self.open_subscription(r["wf_partition"], r["wik"], r["aik"], r["name"], r["ck"])
+            else:
+                self.correlate(r["wik"], r["aik"], r["name"], r["payload"])
+
+    def publish_batch(self, name: bytes, cks, payloads, ttl: int):
+        for ck, pl in zip(cks, payloads):
+            Oracle.publish(self, name, ck, pl, ttl)
+
+    def publish(self, name, cks, payloads=None, ttl: int = 3600000, message_id: bytes = b""):
+        """Cluster form: publish(name, [ck...], [payload...], ttl); single form: publish(name, ck, payload, ttl)."""
+        if isinstance(cks, (bytes, bytearray)):
+            return Oracle.publish(self, name, cks, payloads if payloads is not None else b"\x80", ttl, message_id)
+        self.publish_batch(name, cks, payloads, ttl)
