@@ -41,6 +41,8 @@ extern "C" {
 #define ZB_VT_JOB 0
 #define ZB_VT_WORKFLOW_INSTANCE 5
 #define ZB_VT_INCIDENT 6
+#define ZB_VT_MESSAGE 10
+#define ZB_VT_MESSAGE_SUBSCRIPTION 11
 #define ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION 12
 #define ZB_RT_EVENT 0
 #define ZB_RT_COMMAND 1
@@ -105,6 +107,33 @@ typedef struct zb_step_stats {
   uint64_t path;               /* 0: wave pipeline, 1: trajectory path (zb_traj.hip) ran the step */
 } zb_step_stats;
 
+/* One partition-to-partition command (SubscriptionCommandSender.java:83-128), 256 bytes, exchanged
+ * between partitions by all-to-all (zeebe_amd/cluster.py; RCCL over xGMI between GPUs):
+ *   ZB_XCHG_OPEN:      OpenMessageSubscriptionCommand, workflow partition -> abs(hash(ck) % P)
+ *   ZB_XCHG_CORRELATE: CorrelateWorkflowInstanceSubscriptionCommand, message partition -> workflow partition
+ * token / elem are the workflow partition's element-instance row and catch element (opaque to others). */
+#define ZB_XCHG_OPEN 1
+#define ZB_XCHG_CORRELATE 2
+#define ZB_XCHG_NAME_MAX 48
+#define ZB_XCHG_CK_MAX 48
+#define ZB_XCHG_PAYLOAD_MAX 112
+typedef struct zb_exchange_rec {
+  int32_t kind;
+  int32_t target_partition;
+  int32_t wf_partition;          /* workflowInstancePartitionId */
+  uint32_t token;                /* element-instance row on the workflow partition (0xffffffff = none) */
+  int64_t workflow_instance_key;
+  int64_t activity_instance_key;
+  int64_t source_position;       /* log position of the record whose processing produced it */
+  uint16_t elem;                 /* catch element (workflow partition's model) */
+  uint8_t name_len, ck_len;
+  uint16_t payload_len;
+  uint16_t pad;
+  uint8_t name[ZB_XCHG_NAME_MAX];       /* messageName */
+  uint8_t ck[ZB_XCHG_CK_MAX];           /* correlationKey (ZB_XCHG_OPEN) */
+  uint8_t payload[ZB_XCHG_PAYLOAD_MAX]; /* message payload document (ZB_XCHG_CORRELATE) */
+} zb_exchange_rec;
+
 /* ---- lifecycle ------------------------------------------------------------------------- */
 int zb_engine_create(const zb_config* cfg, zb_engine** out);
 void zb_engine_destroy(zb_engine* e);
@@ -133,6 +162,27 @@ int zb_submit_creates(zb_engine* e, const char* bpmn_process_id, int32_t version
 /* Injects staged input at the log tail and runs lockstep waves until quiescence (ZB_OK) or
  * max_waves (ZB_EAGAIN). stats may be NULL. */
 int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats);
+
+/* ---- message correlation (config 5) ------------------------------------------------------ */
+/* MESSAGE PUBLISH commands (ClientApiMessageHandler.java:90-162), all with one message name and
+ * time-to-live and no message id; correlation keys / payloads concatenated, n+1 offsets each.
+ * Appended and processed by the message stream processor at once (PublishMessageProcessor.java:58-124);
+ * the partition must be quiescent with nothing staged. Correlations found go to the outbox. */
+int zb_submit_publishes(zb_engine* e, const char* message_name, int64_t ttl, size_t n, const uint8_t* cks,
+                        const uint64_t* ck_offsets, const uint8_t* payloads, const uint64_t* payload_offsets);
+/* Commands from other partitions, in delivery order (zeebe_amd/cluster.py schedule); src is a device
+ * pointer when src_on_device != 0. ZB_XCHG_OPEN records are appended as MESSAGE_SUBSCRIPTION OPEN
+ * commands and processed at once (OpenMessageSubscriptionProcessor.java:56-92); ZB_XCHG_CORRELATE
+ * records are appended as WORKFLOW_INSTANCE_SUBSCRIPTION CORRELATE commands (key = log position,
+ * SubscriptionApiCommandMessageHandler.java:131-151), processed by the next zb_step
+ * (WorkflowInstanceStreamProcessor.java:455-509). The partition must be quiescent with nothing staged. */
+int zb_inbox_submit(zb_engine* e, int kind, const zb_exchange_rec* src, size_t n, int src_on_device);
+/* Pending outgoing commands of a kind (side effects of processed records). */
+int zb_outbox_count(zb_engine* e, int kind, uint64_t* n);
+/* Takes every pending command of a kind, sorted by (target partition, source position, emission order),
+ * into dst (cap records; device pointer when dst_on_device != 0); counts[partition_count] per target. */
+int zb_outbox_take(zb_engine* e, int kind, zb_exchange_rec* dst, size_t cap, int dst_on_device, uint64_t* counts,
+                   uint64_t* n_out);
 
 /* ---- output -------------------------------------------------------------------------- */
 int64_t zb_log_size(zb_engine* e);

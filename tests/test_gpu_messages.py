@@ -1,0 +1,136 @@
+"""Message correlation on the GPU (config 5 shape): GPU partitions vs oracle partitions, record for record.
+
+Both clusters run the same canonical schedule (zeebe_amd.cluster.LocalCluster): several GPU engines
+share cuda:0 here (one per partition); the oracle partitions are the checker. Every record of every
+partition's log is compared: position, key, record / value type, intent, rejection type and the full
+msgpack value bytes.
+"""
+import msgpack
+import pytest
+
+from oracle import zbref
+from zeebe_amd import bpmn, cluster
+
+pytestmark = pytest.mark.gpu
+
+
+def catch_workflow():
+    # IntermediateMessageCatchEventTest.java:59-66
+    return (bpmn.Bpmn.create_executable_process("wf").start_event()
+            .intermediate_catch_event("catch-event", message="order canceled", correlation_key="$.orderId")
+            .sequence_flow_id("to-end").end_event().done().to_xml())
+
+
+def clusters(P, xml, n_log=1 << 20):
+    from zeebe_amd.engine import Engine
+
+    gpu = [Engine(device=0, partition_id=p, partition_count=P, log_capacity=n_log, row_capacity=1 << 18,
+                  arena_bytes=256 << 20) for p in range(P)]
+    ref = [zbref.OraclePartition(p, P) for p in range(P)]
+    for x in gpu + ref:
+        x.deploy(xml, 100, 1)
+    return gpu, ref, cluster.LocalCluster(gpu), cluster.LocalCluster(ref)
+
+
+def compare(gpu, ref):
+    for p, (g, o) in enumerate(zip(gpu, ref)):
+        a, b = o.records(), g.records()
+        assert len(a) == len(b), (p, len(a), len(b))
+        for x, y in zip(a, b):
+            assert (x.position, x.key, x.record_type, x.value_type, x.intent) == \
+                   (y.position, y.key, y.record_type, y.value_type, y.intent), (p, x, y)
+            if x.record_type == 2:
+                assert x.rejection_type == y.rejection_type, (p, x, y)
+            assert x.value == y.value, (p, x.position, msgpack.unpackb(x.value, raw=False),
+                                        msgpack.unpackb(y.value, raw=False))
+
+
+def both(fn, gpu, ref):
+    fn(gpu)
+    fn(ref)
+
+
+@pytest.mark.parametrize("P", [1, 3])
+def test_correlation_round_trip(P):
+    gpu, ref, cg, co = clusters(P, catch_workflow())
+    n = 60
+    for i in range(n):
+        gpu[i % P].create("wf", [msgpack.packb({"orderId": "order-%d" % i})])
+        ref[i % P].create("wf", msgpack.packb({"orderId": "order-%d" % i}))
+    cg.settle()
+    co.settle()
+    compare(gpu, ref)
+    cks = [b"order-%d" % i for i in range(n)]
+    pls = [msgpack.packb({"foo": i}) for i in range(n)]
+    cg.publish(b"order canceled", cks, pls)
+    co.publish(b"order canceled", cks, pls)
+    compare(gpu, ref)
+    assert sum(g.counters()["completed"] for g in gpu) == n
+
+
+def test_published_first_ttl_duplicates_and_rejections():
+    P = 3
+    gpu, ref, cg, co = clusters(P, catch_workflow())
+    for c in (cg, co):
+        # shouldNotCorrelateMessageAfterTTL :264-279 shape, then a stored message for order-1
+        c.publish(b"order canceled", [b"order-0"], [msgpack.packb({"nr": "first"})], ttl=0)
+        c.publish(b"order canceled", [b"order-0", b"order-1"],
+                  [msgpack.packb({"nr": "second"}), msgpack.packb({"nr": "x"})], ttl=10000)
+    for i, key in enumerate(["order-0", "order-1", "order-2", "order-2", "order-3"]):
+        gpu[i % P].create("wf", [msgpack.packb({"orderId": key})])
+        ref[i % P].create("wf", msgpack.packb({"orderId": key}))
+    cg.settle()
+    co.settle()
+    compare(gpu, ref)
+    # correlate to all subscriptions of order-2; order-2 again -> CORRELATE rejections (activity gone)
+    for c in (cg, co):
+        c.publish(b"order canceled", [b"order-2", b"order-3"], [b"\x80", msgpack.packb({"a": [1, 2]})])
+        c.publish(b"order canceled", [b"order-2"], [msgpack.packb({"again": True})], ttl=0)
+    compare(gpu, ref)
+    recs = [r for p in ref for r in p.records() if r.value_type == 12 and r.record_type == 2]
+    assert recs, "expected CORRELATE rejections"
+
+
+def test_integer_correlation_key():
+    # extractCorrelationKey: a long becomes its 8 little-endian bytes (hash routing and store key)
+    P = 3
+    xml = (bpmn.Bpmn.create_executable_process("wf").start_event()
+           .intermediate_catch_event("catch-event", message="paid", correlation_key="$.id")
+           .end_event().done().to_xml())
+    gpu, ref, cg, co = clusters(P, xml)
+    for i in range(12):
+        gpu[i % P].create("wf", [msgpack.packb({"id": 1000 + i})])
+        ref[i % P].create("wf", msgpack.packb({"id": 1000 + i}))
+    cg.settle()
+    co.settle()
+    compare(gpu, ref)
+    cks = [int(1000 + i).to_bytes(8, "little", signed=True) for i in range(12)]
+    for c in (cg, co):
+        c.publish(b"paid", cks, [msgpack.packb({"ok": i}) for i in range(12)])
+    compare(gpu, ref)
+    assert sum(g.counters()["completed"] for g in gpu) == 12
+
+
+def test_c5_scale_properties():
+    """4 partitions on one GPU, 200k instances: every instance completes, every log has the C5 shape."""
+    from zeebe_amd.engine import Engine
+
+    P, n = 4, 200_000
+    xml = bpmn.message_workflow().to_xml()
+    gpu = [Engine(device=0, partition_id=p, partition_count=P, log_capacity=n * 8, row_capacity=n,
+                  arena_bytes=(n // P) * 1024 + (64 << 20)) for p in range(P)]
+    for g in gpu:
+        g.deploy(xml, 100, 1)
+    for p in range(P):
+        payloads = [msgpack.packb({"orderId": "order-%d" % i}) for i in range(p, n, P)]
+        gpu[p].create("msg", payloads)
+    c = cluster.LocalCluster(gpu)
+    c.settle()
+    assert sum(g.pending(1) + g.pending(2) for g in gpu) == 0
+    cks = [b"order-%d" % i for i in range(n)]
+    c.publish(b"order", cks, [msgpack.packb({"paid": True})] * n)
+    assert sum(g.counters()["completed"] for g in gpu) == n
+    # per instance: CREATE + 13 WORKFLOW_INSTANCE events + WIS CORRELATE / CORRELATED;
+    # per message PUBLISH + PUBLISHED; per subscription OPEN + OPENED
+    total = sum(g.log_size() for g in gpu)
+    assert total == n * (1 + 13 + 2) + n * 2 + n * 2, total

@@ -16,6 +16,7 @@
 
 #include "zb_kernels.hpp"
 #include "zb_model.hpp"
+#include "zb_msg.hpp"
 
 using namespace zbg;
 
@@ -138,6 +139,20 @@ struct zb_engine {
   uint64_t* t_wstats = nullptr;   // [t_nwg_cap][6] emit statistics per workgroup
   TrajCtl* h_ctl_pinned = nullptr;
 
+  // message correlation (zb_msg.hip): outboxes [0] open-subscription, [1] correlate
+  zb_exchange_rec* obox[2] = {nullptr, nullptr};
+  uint64_t* okeys[2] = {nullptr, nullptr};
+  uint32_t* on = nullptr;  // [2] device counters
+  uint64_t ocap = 0;
+  // message stores (MessageSubscriptionDataStore / MessageDataStore), allocated on first use
+  SubEntry* subs = nullptr;
+  uint32_t *sub_head = nullptr, *sub_next = nullptr;
+  MsgEntry* msgs = nullptr;
+  uint32_t *msg_head = nullptr, *msg_next = nullptr;
+  uint64_t store_cap = 0, head_mask = 0, sub_count = 0, msg_count = 0;
+  int64_t msg_key_next = 0;  // message KeyGenerator(0, 1) (MessageService.java:91)
+  bool has_catch = false;
+
   // timing
   std::vector<hipEvent_t> ev;
 };
@@ -214,6 +229,12 @@ WaveParams wave_params(zb_engine* e) {
   p.row_cap = e->cfg.row_capacity;
   p.arena_cap = e->cfg.arena_bytes;
   p.wave = e->wave;
+  p.obox = e->obox[0];
+  p.okeys = e->okeys[0];
+  p.on = e->on;
+  p.ocap = e->ocap;
+  p.partition_id = e->cfg.partition_id;
+  p.partition_count = e->cfg.partition_count;
   return p;
 }
 
@@ -333,6 +354,69 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st)
   return 1;
 }
 
+// outboxes: one record per element-instance row at most (a subscription per catch event instance;
+// a correlation per subscription and publish)
+int ensure_outbox(zb_engine* e) {
+  if (e->on) return ZB_OK;
+  e->ocap = std::max<uint64_t>(e->cfg.row_capacity, 1024);
+  for (int k = 0; k < 2; k++) {
+    HIPCHECK(e, hipMalloc(&e->obox[k], e->ocap * sizeof(zb_exchange_rec)));
+    HIPCHECK(e, hipMalloc(&e->okeys[k], e->ocap * sizeof(uint64_t)));
+  }
+  HIPCHECK(e, hipMalloc(&e->on, 2 * sizeof(uint32_t)));
+  HIPCHECK(e, hipMemsetAsync(e->on, 0, 2 * sizeof(uint32_t), e->stream));
+  return ZB_OK;
+}
+
+int ensure_stores(zb_engine* e) {
+  int rc = ensure_outbox(e);
+  if (rc != ZB_OK) return rc;
+  if (e->subs) return ZB_OK;
+  e->store_cap = std::max<uint64_t>(e->cfg.row_capacity, 1024);
+  uint64_t heads = 1;
+  while (heads < 2 * e->store_cap) heads <<= 1;
+  e->head_mask = heads - 1;
+  HIPCHECK(e, hipMalloc(&e->subs, e->store_cap * sizeof(SubEntry)));
+  HIPCHECK(e, hipMalloc(&e->sub_next, e->store_cap * sizeof(uint32_t)));
+  HIPCHECK(e, hipMalloc(&e->sub_head, heads * sizeof(uint32_t)));
+  HIPCHECK(e, hipMalloc(&e->msgs, e->store_cap * sizeof(MsgEntry)));
+  HIPCHECK(e, hipMalloc(&e->msg_next, e->store_cap * sizeof(uint32_t)));
+  HIPCHECK(e, hipMalloc(&e->msg_head, heads * sizeof(uint32_t)));
+  HIPCHECK(e, hipMemsetAsync(e->sub_head, 0xff, heads * sizeof(uint32_t), e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->msg_head, 0xff, heads * sizeof(uint32_t), e->stream));
+  return ZB_OK;
+}
+
+MsgParams msg_params(zb_engine* e) {
+  MsgParams p{};
+  p.log = e->log;
+  p.links = e->links;
+  p.arena = e->arena;
+  p.subs = e->subs; p.sub_head = e->sub_head; p.sub_next = e->sub_next;
+  p.sub_mask = e->head_mask; p.sub_count = e->sub_count; p.sub_cap = e->store_cap;
+  p.msgs = e->msgs; p.msg_head = e->msg_head; p.msg_next = e->msg_next;
+  p.msg_mask = e->head_mask; p.msg_count = e->msg_count; p.msg_cap = e->store_cap;
+  p.obox = e->obox[1]; p.okeys = e->okeys[1]; p.on = e->on + 1; p.ocap = e->ocap;
+  p.err = e->derr;
+  return p;
+}
+
+// the partition must be idle for a message-side batch (canonical schedule, zeebe_amd/cluster.py)
+int require_idle(zb_engine* e) {
+  if (e->failed) return fail(e, ZB_EPROCESSING, "partition stopped after a processing failure: " + e->err);
+  if (e->host_hdr.begin != e->host_hdr.end || (e->staged_pending && !e->staged.empty()))
+    return fail(e, ZB_EINVAL, "partition not quiescent: step it before delivering or publishing");
+  return ZB_OK;
+}
+
+int finish_batch(zb_engine* e) {
+  HIPCHECK(e, hipMemcpyAsync(e->hdr + (e->wave & 1), &e->host_hdr, sizeof(WaveHdr), hipMemcpyHostToDevice, e->stream));
+  HIPCHECK(e, hipGetLastError());
+  HIPCHECK(e, hipMemcpyAsync(e->h_err_pinned, e->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  return check_device_errors(e, *e->h_err_pinned);
+}
+
 }  // namespace
 
 extern "C" {
@@ -409,6 +493,10 @@ void zb_engine_destroy(zb_engine* e) {
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats};
   for (void* p : ps)
     if (p) (void)hipFree(p);
+  void* ms[] = {e->obox[0], e->obox[1], e->okeys[0], e->okeys[1], e->on, e->subs, e->sub_head, e->sub_next,
+                e->msgs, e->msg_head, e->msg_next};
+  for (void* p : ms)
+    if (p) (void)hipFree(p);
   if (e->h_hdr_pinned) (void)hipHostFree(e->h_hdr_pinned);
   if (e->h_err_pinned) (void)hipHostFree(e->h_err_pinned);
   if (e->h_ctl_pinned) (void)hipHostFree(e->h_ctl_pinned);
@@ -448,6 +536,14 @@ int zb_reset(zb_engine* e, int keep_staged) {
     e->staged_uploaded = false;
   }
   e->staged_pending = !e->staged.empty();
+  e->sub_count = e->msg_count = 0;
+  e->msg_key_next = 0;
+  if (e->on) HIPCHECK(e, hipMemsetAsync(e->on, 0, 2 * sizeof(uint32_t), e->stream));
+  if (e->subs) {
+    HIPCHECK(e, hipMemsetAsync(e->sub_head, 0xff, (e->head_mask + 1) * sizeof(uint32_t), e->stream));
+    HIPCHECK(e, hipMemsetAsync(e->msg_head, 0xff, (e->head_mask + 1) * sizeof(uint32_t), e->stream));
+  }
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
   return ZB_OK;
 }
 
@@ -460,6 +556,11 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
   for (const DevElem& el : e->model.elems) {
     if (el.step[WI_ELEMENT_COMPLETING] == ST_APPLY_OUTPUT_MAPPING) e->has_merges = true;
     if (el.step[WI_GATEWAY_ACTIVATED] == ST_EXCLUSIVE_SPLIT) e->has_splits = true;
+    if (el.kind == EK_CATCH) e->has_catch = true;
+  }
+  if (e->has_catch) {
+    int orc = ensure_outbox(e);
+    if (orc != ZB_OK) return orc;
   }
   // the trajectory count pass skips payload merges, so conditions must never read a merge result
   e->traj_model_ok = !(e->has_merges && e->has_splits);
@@ -769,6 +870,193 @@ int zb_drain(zb_engine* e, int64_t start, int64_t count, zb_record_header* heade
         hipMemcpyAsync(headers, d_hdrs, count * sizeof(zb_record_header), hipMemcpyDeviceToHost, e->stream) !=
             hipSuccess ||
         hipStreamSynchronize(e->stream) != hipSuccess) { rc = fail(e, ZB_EDEVICE, "drain copy"); break; }
+  } while (0);
+  cleanup();
+  return rc;
+}
+
+int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, const uint8_t* cks,
+                        const uint64_t* ck_offsets, const uint8_t* payloads, const uint64_t* payload_offsets) {
+  if (!e || !name || (n > 0 && (!cks || !ck_offsets || !payloads || !payload_offsets))) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  int rc = require_idle(e);
+  if (rc != ZB_OK) return rc;
+  if (n == 0) return ZB_OK;
+  rc = ensure_stores(e);
+  if (rc != ZB_OK) return rc;
+  const uint64_t nn = std::strlen(name);
+  if (nn > 0xffff) return fail(e, ZB_EINVAL, "message name too long");
+  const int per = ttl > 0 ? 1 : 2;
+  const int64_t base = e->host_hdr.end;
+  if ((uint64_t)(base + (int64_t)n * (1 + per)) > e->cfg.log_capacity) return fail(e, ZB_ENOMEM, "log capacity");
+  if ((uint64_t)base + n * (1 + per) >= (1ull << 34)) return fail(e, ZB_EUNSUPPORTED, "log position beyond the outbox order key");
+  if (e->msg_count + (ttl > 0 ? n : 0) > e->store_cap) return fail(e, ZB_ENOMEM, "message store capacity");
+  // PUBLISH commands (null key) and their message blobs, built on the host and uploaded once
+  std::vector<zb_rec> recs(n);
+  std::vector<uint8_t> blobs;
+  const uint64_t arena0 = (uint64_t)e->host_hdr.arena_next;
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t* ck = cks + ck_offsets[i];
+    const uint64_t nc = ck_offsets[i + 1] - ck_offsets[i];
+    const uint8_t* pl = payloads + payload_offsets[i];
+    uint64_t np = payload_offsets[i + 1] - payload_offsets[i];
+    static const uint8_t EMPTY = 0x80;
+    if (np == 0 || (np == 1 && pl[0] == 0xc0)) { pl = &EMPTY; np = 1; }  // DocumentValue: nil / empty -> {}
+    else if (!((pl[0] & 0xf0) == 0x80 || pl[0] == 0xde || pl[0] == 0xdf))
+      return fail(e, ZB_EINVAL, "Document has invalid format. On root level an object is only allowed.");
+    if (nc > 0xffff) return fail(e, ZB_EINVAL, "correlation key too long");
+    const size_t off = blobs.size();
+    const uint32_t len = (uint32_t)(16 + nn + nc + np);
+    blobs.resize(off + ((4 + len + 7) & ~(size_t)7), 0);
+    uint8_t* b = blobs.data() + off;
+    std::memcpy(b, &len, 4);
+    std::memcpy(b + 4, &ttl, 8);
+    const uint16_t n16 = (uint16_t)nn, c16 = (uint16_t)nc;
+    const uint32_t p32 = (uint32_t)np;
+    std::memcpy(b + 12, &n16, 2);
+    std::memcpy(b + 14, &c16, 2);
+    std::memcpy(b + 16, &p32, 4);
+    std::memcpy(b + 20, name, nn);
+    std::memcpy(b + 20 + nn, ck, nc);
+    std::memcpy(b + 20 + nn + nc, pl, np);
+    zb_rec& d = recs[i];
+    d.key = -1; d.scope_key = -1; d.inst_key = -1;
+    d.payload = (uint32_t)((arena0 + off) >> 3);
+    d.elem = NO_ELEM; d.intent = 0;  // PUBLISH
+    d.kind = make_kind(ZB_VT_MESSAGE, ZB_RT_COMMAND, false);
+  }
+  if (arena0 + blobs.size() > e->cfg.arena_bytes) return fail(e, ZB_ENOMEM, "arena capacity");
+  HIPCHECK(e, hipMemcpyAsync(e->log + base, recs.data(), n * sizeof(zb_rec), hipMemcpyHostToDevice, e->stream));
+  HIPCHECK(e, hipMemcpyAsync(e->arena + arena0, blobs.data(), blobs.size(), hipMemcpyHostToDevice, e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->links + base, 0xff, n * sizeof(uint64_t), e->stream));
+  MsgParams p = msg_params(e);
+  p.n = (int64_t)n;
+  p.base = base;
+  p.ttl = ttl;
+  p.key_base = e->msg_key_next;
+  launch_msg_publish(p, e->stream);
+  e->msg_key_next += (int64_t)n;
+  if (ttl > 0) e->msg_count += n;
+  e->host_hdr.end = base + (int64_t)n * (1 + per);
+  e->host_hdr.begin = e->host_hdr.gen_end = e->host_hdr.end;
+  e->host_hdr.arena_next += (int64_t)blobs.size();
+  return finish_batch(e);
+}
+
+int zb_inbox_submit(zb_engine* e, int kind, const zb_exchange_rec* src, size_t n, int src_on_device) {
+  if (!e || (n > 0 && !src) || (kind != ZB_XCHG_OPEN && kind != ZB_XCHG_CORRELATE)) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  int rc = require_idle(e);
+  if (rc != ZB_OK) return rc;
+  if (n == 0) return ZB_OK;
+  rc = ensure_stores(e);
+  if (rc != ZB_OK) return rc;
+  const int64_t base = e->host_hdr.end;
+  const uint64_t recs = kind == ZB_XCHG_OPEN ? 2 * n : n;
+  const uint64_t stride = kind == ZB_XCHG_OPEN ? SUB_BLOB : WIS_BLOB;
+  if ((uint64_t)base + recs > e->cfg.log_capacity) return fail(e, ZB_ENOMEM, "log capacity");
+  if ((uint64_t)base + recs >= (1ull << 34)) return fail(e, ZB_EUNSUPPORTED, "log position beyond the outbox order key");
+  if ((uint64_t)e->host_hdr.arena_next + n * stride > e->cfg.arena_bytes) return fail(e, ZB_ENOMEM, "arena capacity");
+  if (kind == ZB_XCHG_OPEN && (e->sub_count + n > e->store_cap || e->sub_count + n >= (1ull << 24)))
+    return fail(e, ZB_ENOMEM, "subscription store capacity");
+  const zb_exchange_rec* dsrc = src;
+  zb_exchange_rec* tmp = nullptr;
+  if (!src_on_device) {
+    HIPCHECK(e, hipMalloc(&tmp, n * sizeof(zb_exchange_rec)));
+    HIPCHECK(e, hipMemcpyAsync(tmp, src, n * sizeof(zb_exchange_rec), hipMemcpyHostToDevice, e->stream));
+    dsrc = tmp;
+  }
+  MsgParams p = msg_params(e);
+  p.in = dsrc;
+  p.n = (int64_t)n;
+  p.base = base;
+  p.arena_base = (uint64_t)e->host_hdr.arena_next;
+  if (kind == ZB_XCHG_OPEN) {
+    launch_msg_open(p, e->stream);  // processed at once: OPEN commands + OPENED events
+    e->sub_count += n;
+    e->host_hdr.end = base + (int64_t)recs;
+    e->host_hdr.begin = e->host_hdr.gen_end = e->host_hdr.end;
+  } else {
+    launch_wis_inject(p, e->stream);  // CORRELATE commands: the next zb_step processes them
+    e->host_hdr.end = base + (int64_t)recs;
+    e->host_hdr.gen_end = e->host_hdr.end;
+  }
+  e->host_hdr.arena_next += (int64_t)(n * stride);
+  rc = finish_batch(e);
+  if (tmp) (void)hipFree(tmp);
+  return rc;
+}
+
+int zb_outbox_count(zb_engine* e, int kind, uint64_t* n) {
+  if (!e || !n || (kind != ZB_XCHG_OPEN && kind != ZB_XCHG_CORRELATE)) return ZB_EINVAL;
+  *n = 0;
+  if (!e->on) return ZB_OK;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  uint32_t c = 0;
+  HIPCHECK(e, hipMemcpyAsync(&c, e->on + (kind - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  *n = c;
+  return ZB_OK;
+}
+
+int zb_outbox_take(zb_engine* e, int kind, zb_exchange_rec* dst, size_t cap, int dst_on_device, uint64_t* counts,
+                   uint64_t* n_out) {
+  if (!e || !counts || !n_out || (kind != ZB_XCHG_OPEN && kind != ZB_XCHG_CORRELATE)) return ZB_EINVAL;
+  const int P = e->cfg.partition_count;
+  if (P > 64) return fail(e, ZB_EUNSUPPORTED, "more than 64 partitions");
+  for (int q = 0; q < P; q++) counts[q] = 0;
+  uint64_t n = 0;
+  int rc = zb_outbox_count(e, kind, &n);
+  if (rc != ZB_OK) return rc;
+  *n_out = n;
+  if (n == 0) return ZB_OK;
+  if (n > cap || !dst) return fail(e, ZB_ENOMEM, "outbox destination too small");
+  if (n > e->ocap) return fail(e, ZB_ENOMEM, "outbox overflow");
+  const int k = kind - 1;
+  // sort (key, index) pairs: target partition, source position, emission order
+  uint64_t* keys_out = nullptr;
+  uint32_t *idx_in = nullptr, *idx_out = nullptr;
+  uint64_t* first = nullptr;
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  zb_exchange_rec* staging = nullptr;
+  auto cleanup = [&]() {
+    void* ps[] = {keys_out, idx_in, idx_out, first, tmp, staging};
+    for (void* q : ps)
+      if (q) (void)hipFree(q);
+  };
+  do {
+    if (hipMalloc(&keys_out, n * 8) != hipSuccess || hipMalloc(&idx_in, n * 4) != hipSuccess ||
+        hipMalloc(&idx_out, n * 4) != hipSuccess || hipMalloc(&first, (P + 1) * 8) != hipSuccess) {
+      rc = fail(e, ZB_ENOMEM, "outbox sort buffers");
+      break;
+    }
+    launch_iota(idx_in, n, e->stream);
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, e->okeys[k], keys_out, idx_in, idx_out, (int)n, 0, 64,
+                                           e->stream) != hipSuccess ||
+        hipMalloc(&tmp, tmp_bytes + 16) != hipSuccess ||
+        hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, e->okeys[k], keys_out, idx_in, idx_out, (int)n, 0, 64,
+                                           e->stream) != hipSuccess) {
+      rc = fail(e, ZB_EDEVICE, "outbox sort");
+      break;
+    }
+    zb_exchange_rec* out = dst;
+    if (!dst_on_device) {
+      if (hipMalloc(&staging, n * sizeof(zb_exchange_rec)) != hipSuccess) { rc = fail(e, ZB_ENOMEM, "outbox staging"); break; }
+      out = staging;
+    }
+    launch_outbox_gather(e->obox[k], idx_out, out, n, e->stream);
+    launch_outbox_bounds(keys_out, n, first, P, e->stream);
+    std::vector<uint64_t> h_first(P, 0);
+    if (hipMemcpyAsync(h_first.data(), first, P * 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+        (!dst_on_device && hipMemcpyAsync(dst, staging, n * sizeof(zb_exchange_rec), hipMemcpyDeviceToHost, e->stream) !=
+                               hipSuccess) ||
+        hipMemsetAsync(e->on + k, 0, sizeof(uint32_t), e->stream) != hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess) {
+      rc = fail(e, ZB_EDEVICE, "outbox copy");
+      break;
+    }
+    for (int q = 0; q < P; q++) counts[q] = (q + 1 < P ? h_first[q + 1] : n) - h_first[q];
   } while (0);
   cleanup();
   return rc;

@@ -90,7 +90,57 @@ struct WaveParams {
   uint64_t job_cap;
   uint64_t log_cap, row_cap, arena_cap, wave_cap;
   int64_t wave;
+  // open-subscription outbox (SUBSCRIBE_TO_INTERMEDIATE_MESSAGE side effects), zb_msg.hpp
+  zb_exchange_rec* obox;
+  uint64_t* okeys;
+  uint32_t* on;
+  uint64_t ocap;
+  int32_t partition_id, partition_count;
 };
+
+// message stores (zb_msg.hip): MessageSubscriptionDataStore / MessageDataStore entries
+struct SubEntry {   // 48 B
+  uint64_t h;       // name_ck_hash(messageName, correlationKey)
+  int64_t wik, aik;
+  int64_t pos;      // log position of the OPEN command
+  uint32_t blob;    // subscription blob ref (wfp, elem, token, name, correlation key)
+  uint32_t idx;     // insertion index
+};
+struct MsgEntry {   // 32 B, messages stored with ttl > 0
+  uint64_t h;
+  int64_t key;
+  int64_t pos;      // log position of the PUBLISH command
+  uint32_t blob;    // message blob ref
+  uint32_t pad;
+};
+struct MsgParams {
+  zb_rec* log;
+  uint64_t* links;
+  uint8_t* arena;
+  const zb_exchange_rec* in;  // delivered commands (k_msg_open, k_wis_inject)
+  int64_t n, base;            // batch size, log position of its first command
+  uint64_t arena_base;        // byte offset of the batch's blobs
+  SubEntry* subs;
+  uint32_t *sub_head, *sub_next;
+  uint64_t sub_mask, sub_count, sub_cap;
+  MsgEntry* msgs;
+  uint32_t *msg_head, *msg_next;
+  uint64_t msg_mask, msg_count, msg_cap;
+  int64_t ttl, key_base;      // publish batch
+  zb_exchange_rec* obox;      // correlate outbox
+  uint64_t* okeys;
+  uint32_t* on;
+  uint64_t ocap;
+  uint32_t* err;
+};
+
+void launch_msg_open(const MsgParams& p, hipStream_t stream);
+void launch_msg_publish(const MsgParams& p, hipStream_t stream);
+void launch_wis_inject(const MsgParams& p, hipStream_t stream);
+void launch_outbox_gather(const zb_exchange_rec* src, const uint32_t* idx, zb_exchange_rec* dst, uint64_t n,
+                          hipStream_t stream);
+void launch_outbox_bounds(const uint64_t* keys, uint64_t n, uint64_t* first, int parts, hipStream_t stream);
+void launch_iota(uint32_t* p, uint64_t n, hipStream_t stream);
 
 
 void launch_process(const WaveParams& p, hipStream_t stream);

@@ -183,6 +183,30 @@ __device__ inline void encode_value(const SerParams& P, int64_t pos, const zb_re
     w.key("activityInstanceKey"); w.integer(d.scope_key);
     w.key("jobKey"); w.integer(-1);
     w.key("payload"); w.bin((const uint8_t*)"\x80", 1);
+  } else if (vt == ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION) {  // WorkflowInstanceSubscriptionRecord.java:26-38
+    const DevElem& e = P.elems[d.elem];
+    w.map_hdr(4);
+    w.key("workflowInstanceKey"); w.integer(d.inst_key);
+    w.key("activityInstanceKey"); w.integer(d.scope_key);
+    w.key("messageName"); w.str(P.pool + e.msg_off, e.msg_len);
+    w.key("payload"); w.bin(pl, plen);
+  } else if (vt == ZB_VT_MESSAGE_SUBSCRIPTION) {  // MessageSubscriptionRecord.java:26-41 (blob: zb_msg.hpp SUB_BLOB)
+    const uint8_t* b = P.arena + (uint64_t)d.payload * 8;
+    w.map_hdr(5);
+    w.key("workflowInstancePartitionId"); w.integer(*(const int32_t*)(b + 4));
+    w.key("workflowInstanceKey"); w.integer(d.inst_key);
+    w.key("activityInstanceKey"); w.integer(d.scope_key);
+    w.key("messageName"); w.str(b + 16, b[8]);
+    w.key("correlationKey"); w.str(b + 64, b[9]);
+  } else if (vt == ZB_VT_MESSAGE) {  // MessageRecord.java:26-42 (blob: ttl, lengths, name, ck, payload)
+    const uint8_t* b = P.arena + (uint64_t)d.payload * 8 + 4;
+    const uint32_t nn = *(const uint16_t*)(b + 8), nc = *(const uint16_t*)(b + 10), np = *(const uint32_t*)(b + 12);
+    w.map_hdr(5);
+    w.key("name"); w.str(b + 16, nn);
+    w.key("correlationKey"); w.str(b + 16 + nn, nc);
+    w.key("timeToLive"); w.integer(*(const int64_t*)b);
+    w.key("payload"); w.bin(b + 16 + nn + nc, np);
+    w.key("messageId"); w.str(nullptr, 0);
   }
 }
 
@@ -214,7 +238,10 @@ __global__ void k_ser_write(SerParams P) {
   h.record_type = kind_rt(d.kind);
   h.value_type = kind_vt(d.kind);
   h.intent = d.intent;
-  h.rejection_type = kind_rt(d.kind) == ZB_RT_COMMAND_REJECTION ? 0 /*BAD_VALUE*/ : 255;
+  // RejectionType: CREATE of an unknown workflow -> BAD_VALUE (0); CORRELATE of an absent activity ->
+  // NOT_APPLICABLE (1) (WorkflowInstanceStreamProcessor.java:477-479)
+  h.rejection_type = kind_rt(d.kind) == ZB_RT_COMMAND_REJECTION
+                         ? (kind_vt(d.kind) == ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION ? 1 : 0) : 255;
   h.value_length = w.n;
   h.value_offset = P.offsets[i];
   P.headers[i] = h;

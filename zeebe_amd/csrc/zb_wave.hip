@@ -18,6 +18,7 @@
 
 #include "zb_devlib.hpp"
 #include "zb_kernels.hpp"
+#include "zb_msg.hpp"
 
 namespace zbg {
 
@@ -50,6 +51,13 @@ struct TState {
   // stats
   uint32_t transitions, completed, created, merges;
   uint32_t merge_bytes, cond_bytes;
+  // open-subscription side effect (SubscribeMessageHandler), written to the outbox after processing
+  bool fx, fx_int;
+  uint8_t fx_ck_len;
+  uint16_t fx_elem;
+  uint32_t fx_row;
+  uint64_t fx_ck_at;  // arena byte offset of the correlation key string
+  int64_t fx_ival, fx_pos, fx_wik, fx_aik;
 };
 
 __device__ __forceinline__ void fail_at(TState& t, uint32_t flag, uint32_t site) {
@@ -258,8 +266,35 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
       if (rec.key == rec.inst_key) t.completed += 1;
       break;
     }
+    case ST_SUBSCRIBE_TO_INTERMEDIATE_MESSAGE: {  // SubscribeMessageHandler :77-141: a side effect, no record
+      const uint8_t* pp = P.arena + (uint64_t)rec.payload * 8;
+      const uint32_t len = *(const uint32_t*)pp;
+      QueryResult q;
+      if (!run_query(pp + 4, len, P.queries[el.ck_query], P.filters, P.pool, q)) { fail_at(t, DE_UNSUPPORTED, 30); return; }
+      // extractCorrelationKey :121-141: exactly one result, a string or a long, else the processor fails
+      if (q.count != 1) { fail_at(t, DE_PROCESSING, 31); return; }
+      Tok tk;
+      if (!read_tok(pp + 4 + q.pos, q.len, tk)) { fail_at(t, DE_PROCESSING, 32); return; }
+      if (tk.type == TT_STRING) {
+        t.fx_int = false;
+        t.fx_ck_at = (uint64_t)rec.payload * 8 + 4 + q.pos + tk.hdr;
+        t.fx_ck_len = tk.len > 255 ? 255 : (uint8_t)tk.len;
+        if (tk.len > ZB_XCHG_CK_MAX) { fail_at(t, DE_UNSUPPORTED, 33); return; }
+      } else if (tk.type == TT_INTEGER) {
+        t.fx_int = true;  // QueryResult.getLongAsBuffer: 8 bytes, native (little-endian) order
+        t.fx_ival = tk.ival;
+        t.fx_ck_len = 8;
+      } else {
+        fail_at(t, DE_PROCESSING, 34);  // "Failed to extract correlation-key: wrong type"
+        return;
+      }
+      if (el.msg_len > ZB_XCHG_NAME_MAX || t.fx) { fail_at(t, DE_UNSUPPORTED, 35); return; }
+      t.fx = true;
+      t.fx_pos = pos; t.fx_wik = rec.inst_key; t.fx_aik = rec.key; t.fx_elem = rec.elem; t.fx_row = rself;
+      break;
+    }
     default:
-      // message subscription, termination: not on the GPU path yet (flagged, never silently skipped)
+      // termination: not on the GPU path yet (flagged, never silently skipped)
       fail_at(t, DE_UNSUPPORTED, 12);
       break;
   }
@@ -340,7 +375,60 @@ __device__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t p
       m.payload = rec.payload;
       k.job_key = -1;
     }
+  } else if (vt == ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION) {
+    if (rt != ZB_RT_COMMAND || rec.intent != 0) return;  // CORRELATE
+    // CorrelateWorkflowInstanceSubscription :463-508: the element instance by activityInstanceKey; the
+    // delivered command carries the catch event's row (rows are never reused: row + key identify it)
+    const bool found = rself != NO_ROW && rself < P.row_cap && P.rmeta[rself].state != 0 &&
+                       P.rkeys[rself].key == rec.scope_key;
+    if (!found) {  // writeRejection(record, NOT_APPLICABLE, "activity is not active anymore")
+      Slot& s = add_slot(t);
+      s.d = rec;
+      s.d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION, ZB_RT_COMMAND_REJECTION, t.ns > 1);
+      s.rself = NO_ROW; s.rscope = NO_ROW;
+      return;
+    }
+    RowMeta& m = P.rmeta[rself];
+    const RowKeys k = P.rkeys[rself];
+    Slot& a = add_slot(t);  // batch: CORRELATED(record key), ELEMENT_COMPLETING(activityInstanceKey)
+    a.d = rec;
+    a.d.intent = 1;
+    a.d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION, ZB_RT_EVENT, t.ns > 1);
+    a.rself = NO_ROW; a.rscope = NO_ROW;
+    Slot& b = add_slot(t);
+    b.d.key = rec.scope_key;
+    b.d.scope_key = k.scope_key;
+    b.d.inst_key = k.inst_key;
+    b.d.elem = m.elem;
+    b.d.payload = rec.payload;  // value.setPayload(subscription.getPayload())
+    wf_event(t, b, WI_ELEMENT_COMPLETING, t.ns > 1);
+    b.rself = rself; b.rscope = m.parent;
+    m.state = WI_ELEMENT_COMPLETING;
+    m.payload = rec.payload;
   }
+}
+
+// The open-subscription command of a SUBSCRIBE step (SubscriptionCommandSender.openMessageSubscription
+// :83-103): routed to abs(hash(correlationKey) % P), ordered by the catch event's log position.
+__device__ void write_open(const WaveParams& P, const TState& t, uint32_t slot) {
+  if (slot >= P.ocap) { atomicOr(P.err, (uint32_t)DE_LOG_FULL); return; }
+  uint8_t ck[ZB_XCHG_CK_MAX];
+  if (t.fx_int) {
+    for (int i = 0; i < 8; i++) ck[i] = (uint8_t)((uint64_t)t.fx_ival >> (8 * i));
+  } else {
+    for (uint32_t i = 0; i < t.fx_ck_len; i++) ck[i] = P.arena[t.fx_ck_at + i];
+  }
+  const int32_t target = subscription_partition(ck, t.fx_ck_len, P.partition_count);
+  const DevElem& el = P.elems[t.fx_elem];
+  zb_exchange_rec r;
+  r.kind = ZB_XCHG_OPEN; r.target_partition = target; r.wf_partition = P.partition_id; r.token = t.fx_row;
+  r.workflow_instance_key = t.fx_wik; r.activity_instance_key = t.fx_aik; r.source_position = t.fx_pos;
+  r.elem = t.fx_elem; r.name_len = (uint8_t)el.msg_len; r.ck_len = t.fx_ck_len; r.payload_len = 0; r.pad = 0;
+  for (uint32_t i = 0; i < ZB_XCHG_NAME_MAX; i++) r.name[i] = i < el.msg_len ? P.pool[el.msg_off + i] : 0;
+  for (uint32_t i = 0; i < ZB_XCHG_CK_MAX; i++) r.ck[i] = i < t.fx_ck_len ? ck[i] : 0;
+  for (uint32_t i = 0; i < ZB_XCHG_PAYLOAD_MAX; i++) r.payload[i] = 0;
+  P.obox[slot] = r;
+  P.okeys[slot] = outbox_key(target, t.fx_pos, 0);
 }
 
 // ------------------------------------------------------------------------------ helpers
@@ -394,6 +482,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
     t.bytes = 0; t.merge = false; t.detail = false; t.err = 0; t.err_site = 0;
     t.transitions = t.completed = t.created = t.merges = 0;
     t.merge_bytes = t.cond_bytes = 0;
+    t.fx = false;
     uint32_t nconds = 0;
     const zb_rec rec = P.log[r];
     if (!kind_cont(rec.kind)) {
@@ -432,6 +521,10 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
              ((uint64_t)t.completed << 48);
     acc_bytes += t.bytes;
     acc_created += t.created;
+    if (__ballot(t.fx)) {  // wave-uniform: open-subscription side effects of this tile
+      const uint32_t slot = wave_alloc(P.on, t.fx ? 1u : 0u);
+      if (t.fx) write_open(P, t, slot);
+    }
     if (t.err) {
       atomicOr(P.err, t.err);
       // first failing record (lowest position) and the code site that flagged it

@@ -99,13 +99,20 @@ def lib():
         L.zb_drain.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
         L.zb_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        L.zb_submit_publishes.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.zb_inbox_submit.argtypes = [vp, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        L.zb_outbox_count.argtypes = [vp, ctypes.c_int, u64p]
+        L.zb_outbox_take.argtypes = [vp, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, u64p, u64p]
         _lib = L
     return _lib
 
 
 EXPORTED_SYMBOLS = ["zb_engine_create", "zb_engine_destroy", "zb_last_error", "zb_reset", "zb_deploy",
                     "zb_set_job_completion_payload", "zb_submit_creates", "zb_step", "zb_log_size",
-                    "zb_read_descriptors", "zb_drain", "zb_counters"]
+                    "zb_read_descriptors", "zb_drain", "zb_counters", "zb_submit_publishes", "zb_inbox_submit",
+                    "zb_outbox_count", "zb_outbox_take"]
 
 
 class Engine:
@@ -118,6 +125,7 @@ class Engine:
         cfg = zb_config(device, partition_id, partition_count, CFG_WAVE_ONLY if wave_only else 0, log_capacity,
                         row_capacity, arena_bytes, wave_records)
         h = ctypes.c_void_p()
+        self._device, self._parts = device, partition_count
         rc = self._L.zb_engine_create(ctypes.byref(cfg), ctypes.byref(h))
         if rc != ZB_OK:
             raise ZbError(rc, "zb_engine_create failed")
@@ -212,6 +220,65 @@ class Engine:
             out.append(Record(h.position, h.source_position, h.key, h.record_type, h.value_type, h.intent,
                               h.rejection_type, v))
         return out
+
+    # ---- partition interface of zeebe_amd.cluster (message correlation, config 5)
+    def run(self) -> dict:
+        """Step to quiescence (StreamProcessorController loop until no unprocessed record is left)."""
+        st = self.step()
+        assert st["quiescent"]
+        return st
+
+    def pending(self, kind: int) -> int:
+        n = ctypes.c_uint64(0)
+        self._check(self._L.zb_outbox_count(self._h, kind, ctypes.byref(n)))
+        return n.value
+
+    def outbox(self, kind: int):
+        """All pending commands of a kind, sorted by (target, source position, emission), as a uint8 tensor
+        on this engine's device (ready for all_to_all) + counts per target partition."""
+        import torch
+
+        n = self.pending(kind)
+        dev = torch.device("cuda", self._device)
+        buf = torch.empty(max(n, 1) * 256, dtype=torch.uint8, device=dev)
+        counts = (ctypes.c_uint64 * max(self._parts, 1))()
+        got = ctypes.c_uint64(0)
+        torch.cuda.synchronize(dev)
+        self._check(self._L.zb_outbox_take(self._h, kind, ctypes.c_void_p(buf.data_ptr()), max(n, 1), 1, counts,
+                                           ctypes.byref(got)))
+        return buf[:got.value * 256], [int(counts[q]) for q in range(self._parts)]
+
+    def inbox(self, kind: int, buf):
+        """Commands delivered by other partitions (uint8 tensor / array of 256-byte records, delivery order)."""
+        import numpy as np
+        import torch
+
+        n = (buf.numel() if isinstance(buf, torch.Tensor) else len(buf)) // 256
+        if n == 0:
+            return
+        if isinstance(buf, torch.Tensor) and buf.is_cuda:
+            torch.cuda.synchronize(buf.device)
+            self._check(self._L.zb_inbox_submit(self._h, kind, ctypes.c_void_p(buf.data_ptr()), n, 1))
+        else:
+            a = np.ascontiguousarray(buf.numpy() if isinstance(buf, torch.Tensor) else np.asarray(buf, dtype=np.uint8))
+            self._check(self._L.zb_inbox_submit(self._h, kind, a.ctypes.data, n, 0))
+
+    def publish(self, name: bytes, correlation_keys, payloads, ttl: int = 3600000):
+        """MESSAGE PUBLISH commands, one message name and time-to-live for the batch."""
+        import numpy as np
+
+        if isinstance(name, str):
+            name = name.encode()
+        n = len(correlation_keys)
+        ck_off = np.zeros(n + 1, dtype=np.uint64)
+        pl_off = np.zeros(n + 1, dtype=np.uint64)
+        if n:
+            ck_off[1:] = np.cumsum([len(c) for c in correlation_keys])
+            pl_off[1:] = np.cumsum([len(p) for p in payloads])
+        ckb = ctypes.create_string_buffer(b"".join(correlation_keys), max(int(ck_off[-1]), 1))
+        plb = ctypes.create_string_buffer(b"".join(payloads), max(int(pl_off[-1]), 1))
+        self._check(self._L.zb_submit_publishes(self._h, name, ttl, n, ckb, ck_off.ctypes.data, plb,
+                                                pl_off.ctypes.data))
 
     def counters(self) -> dict:
         arr = (ctypes.c_int64 * 8)()
