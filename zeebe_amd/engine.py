@@ -234,33 +234,25 @@ class Engine:
         return n.value
 
     def outbox(self, kind: int):
-        """All pending commands of a kind, sorted by (target, source position, emission), as a uint8 tensor
-        on this engine's device (ready for all_to_all) + counts per target partition."""
-        import torch
+        """All pending commands of a kind, sorted by (target, source position, emission), as a host uint8
+        array of 256-byte records + counts per target partition. (Between GPUs the engines exchange
+        device-resident outboxes over RCCL themselves: exchange().)"""
+        import numpy as np
 
         n = self.pending(kind)
-        dev = torch.device("cuda", self._device)
-        buf = torch.empty(max(n, 1) * 256, dtype=torch.uint8, device=dev)
+        buf = np.zeros(max(n, 1) * 256, dtype=np.uint8)
         counts = (ctypes.c_uint64 * max(self._parts, 1))()
         got = ctypes.c_uint64(0)
-        torch.cuda.synchronize(dev)
-        self._check(self._L.zb_outbox_take(self._h, kind, ctypes.c_void_p(buf.data_ptr()), max(n, 1), 1, counts,
-                                           ctypes.byref(got)))
+        self._check(self._L.zb_outbox_take(self._h, kind, buf.ctypes.data, max(n, 1), 0, counts, ctypes.byref(got)))
         return buf[:got.value * 256], [int(counts[q]) for q in range(self._parts)]
 
     def inbox(self, kind: int, buf):
-        """Commands delivered by other partitions (uint8 tensor / array of 256-byte records, delivery order)."""
+        """Commands delivered by other partitions (host array of 256-byte records, delivery order)."""
         import numpy as np
-        import torch
 
-        n = (buf.numel() if isinstance(buf, torch.Tensor) else len(buf)) // 256
-        if n == 0:
-            return
-        if isinstance(buf, torch.Tensor) and buf.is_cuda:
-            torch.cuda.synchronize(buf.device)
-            self._check(self._L.zb_inbox_submit(self._h, kind, ctypes.c_void_p(buf.data_ptr()), n, 1))
-        else:
-            a = np.ascontiguousarray(buf.numpy() if isinstance(buf, torch.Tensor) else np.asarray(buf, dtype=np.uint8))
+        a = np.ascontiguousarray(np.asarray(buf, dtype=np.uint8))
+        n = len(a) // 256
+        if n:
             self._check(self._L.zb_inbox_submit(self._h, kind, a.ctypes.data, n, 0))
 
     def publish(self, name: bytes, correlation_keys, payloads, ttl: int = 3600000):
