@@ -38,6 +38,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=30_000, help="instances in the oracle CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--wave-only", action="store_true", help="force the general wave pipeline (no trajectory path)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on GPU 0 (multi-rank rehearsal on a one-GPU box; not a scaling run)")
     return ap.parse_args()
 
 
@@ -69,18 +71,20 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
-        import torch
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        # Control plane only (barrier, max-over-ranks, sums): the C2 partitions never exchange data, so
+        # there is no data-path collective (weak scaling). gloo keeps torch's own HIP runtime out of the
+        # process: the engine (libzbgpu.so) drives its GPU through the system ROCm runtime and
+        # synchronizes its own stream at the end of every zb_step.
+        dist.init_process_group("gloo")
 
     from zeebe_amd import bpmn, workloads
     from zeebe_amd.engine import Engine
 
     n = a.instances
     recs_per_inst = 1 + (8 + 5 * a.tasks) + 3 * a.tasks  # CREATE + WF events + JOB CREATE/CREATED/COMPLETED
-    eng = Engine(device=local_rank, partition_id=rank, partition_count=world,
+    eng = Engine(device=0 if a.same_device else local_rank, partition_id=rank, partition_count=world,
                  log_capacity=int(n * (recs_per_inst + 2)), row_capacity=int(n * (a.tasks + 2)),
                  arena_bytes=int(n * (48 + 48 * a.tasks)) + (64 << 20), wave_only=a.wave_only)
     xml = bpmn.chain_workflow(a.tasks).to_xml()
@@ -102,10 +106,7 @@ def main():
 
     def barrier():
         if dist is not None:
-            import torch
-
-            dist.barrier()
-            torch.cuda.synchronize()
+            dist.barrier()  # every rank's zb_step has returned: its stream is drained
 
     barrier()
     t0 = time.perf_counter()
@@ -131,10 +132,10 @@ def main():
     if dist is not None:
         import torch
 
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        c = torch.tensor([tot["transitions"], tot["completed"]], dtype=torch.float64, device="cuda")
+        c = torch.tensor([tot["transitions"], tot["completed"]], dtype=torch.float64)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         all_transitions, all_completed = float(c[0]), float(c[1])
     else:
