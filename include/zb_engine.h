@@ -184,6 +184,18 @@ int zb_outbox_count(zb_engine* e, int kind, uint64_t* n);
 int zb_outbox_take(zb_engine* e, int kind, zb_exchange_rec* dst, size_t cap, int dst_on_device, uint64_t* counts,
                    uint64_t* n_out);
 
+/* Partition-to-partition exchange over RCCL (xGMI between the GPUs of a node): one communicator
+ * per engine, rank = partition id. zb_comm_unique_id on one rank; the 128-byte id travels to the
+ * others out of band (zeebe_amd/cluster.py uses the torch.distributed control plane). */
+int zb_comm_unique_id(uint8_t id[128]);
+int zb_comm_init(zb_engine* e, const uint8_t id[128], int nranks, int rank);
+/* Collective: global[k] = sum over ranks of the pending commands of kind k+1 (ZB_XCHG_OPEN, _CORRELATE). */
+int zb_comm_pending(zb_engine* e, uint64_t global[2]);
+/* Collective: every rank takes its pending commands of `kind` (zb_outbox_take order), sends each target
+ * its slice (ncclSend / ncclRecv in one group), and delivers what it receives in source-rank order
+ * (zb_inbox_submit). *received = commands delivered to this rank. */
+int zb_comm_exchange(zb_engine* e, int kind, uint64_t* received);
+
 /* ---- output -------------------------------------------------------------------------- */
 int64_t zb_log_size(zb_engine* e);
 /* Copies raw descriptors [start, start+count) to host. */

@@ -134,3 +134,43 @@ def test_c5_scale_properties():
     # per message PUBLISH + PUBLISHED; per subscription OPEN + OPENED
     total = sum(g.log_size() for g in gpu)
     assert total == n * (1 + 13 + 2) + n * 2 + n * 2, total
+
+
+def test_rccl_exchange_single_rank():
+    """DistCluster with the engine's own RCCL communicator (world size 1 here: the one-GPU box; the
+    exchange still goes through ncclSend / ncclRecv to self) against the oracle."""
+    import os
+    import socket
+
+    import torch.distributed as dist
+    from zeebe_amd.engine import Engine
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        e = Engine(device=0, partition_id=0, partition_count=1, log_capacity=1 << 20, row_capacity=1 << 18)
+        o = zbref.OraclePartition(0, 1)
+        for x in (e, o):
+            x.deploy(catch_workflow(), 100, 1)
+        n = 50
+        e.create("wf", [msgpack.packb({"orderId": "order-%d" % i}) for i in range(n)])
+        for i in range(n):
+            o.create("wf", msgpack.packb({"orderId": "order-%d" % i}))
+        dc = cluster.DistCluster(e)
+        assert dc.rccl
+        co = cluster.LocalCluster([o])
+        dc.settle()
+        co.settle()
+        cks = [b"order-%d" % i for i in range(n)]
+        pls = [msgpack.packb({"n": i}) for i in range(n)]
+        dc.publish(b"order canceled", cks, pls)
+        co.publish(b"order canceled", cks, pls)
+        compare([e], [o])
+        assert e.counters()["completed"] == n
+    finally:
+        dist.destroy_process_group()

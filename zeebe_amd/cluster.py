@@ -158,7 +158,9 @@ class DistCluster:
     (RCCL over xGMI with backend "nccl" and device buffers; gloo with host buffers in the CPU tests).
     """
 
-    def __init__(self, partition, group=None, device=None):
+    def __init__(self, partition, group=None, device=None, rccl=None):
+        """rccl: exchange through the engine's own RCCL communicator (GPU engines: default), else through
+        torch.distributed on host buffers (oracle partitions, gloo)."""
         import torch
         import torch.distributed as dist
 
@@ -169,6 +171,12 @@ class DistCluster:
         self.rank = dist.get_rank(group)
         self.device = device if device is not None else torch.device("cpu")
         self.rounds = 0
+        self.rccl = hasattr(partition, "comm_exchange") if rccl is None else rccl
+        if self.rccl:
+            # the 128-byte RCCL id travels over the control plane; the data path is RCCL (xGMI)
+            obj = [partition.comm_unique_id() if self.rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0, group=group)
+            partition.comm_init(obj[0], self.world, self.rank)
 
     def _tensor(self, x):
         import torch
@@ -204,6 +212,15 @@ class DistCluster:
         for _ in range(max_rounds):
             self.p.run()
             self.rounds += 1
+            if self.rccl:
+                g_open, g_corr = self.p.comm_pending()
+                if g_open:
+                    self.p.comm_exchange(KIND_OPEN)
+                    continue
+                if g_corr:
+                    self.p.comm_exchange(KIND_CORRELATE)
+                    continue
+                return
             if self._any_pending(KIND_OPEN):
                 self._exchange(KIND_OPEN)
                 continue

@@ -7,6 +7,7 @@
 // reported as ZB_EUNSUPPORTED.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -152,6 +153,9 @@ struct zb_engine {
   uint64_t store_cap = 0, head_mask = 0, sub_count = 0, msg_count = 0;
   int64_t msg_key_next = 0;  // message KeyGenerator(0, 1) (MessageService.java:91)
   bool has_catch = false;
+  // RCCL communicator over the partitions of the node (zb_comm_*)
+  ncclComm_t comm = nullptr;
+  uint64_t* d_xcounts = nullptr;  // [2 * 64] send / receive counts
 
   // timing
   std::vector<hipEvent_t> ev;
@@ -493,8 +497,9 @@ void zb_engine_destroy(zb_engine* e) {
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats};
   for (void* p : ps)
     if (p) (void)hipFree(p);
+  if (e->comm) (void)ncclCommDestroy(e->comm);
   void* ms[] = {e->obox[0], e->obox[1], e->okeys[0], e->okeys[1], e->on, e->subs, e->sub_head, e->sub_next,
-                e->msgs, e->msg_head, e->msg_next};
+                e->msgs, e->msg_head, e->msg_next, e->d_xcounts};
   for (void* p : ms)
     if (p) (void)hipFree(p);
   if (e->h_hdr_pinned) (void)hipHostFree(e->h_hdr_pinned);
@@ -1059,6 +1064,108 @@ int zb_outbox_take(zb_engine* e, int kind, zb_exchange_rec* dst, size_t cap, int
     for (int q = 0; q < P; q++) counts[q] = (q + 1 < P ? h_first[q + 1] : n) - h_first[q];
   } while (0);
   cleanup();
+  return rc;
+}
+
+#define NCCLCHECK(e, call)                                                                      \
+  do {                                                                                          \
+    ncclResult_t _r = (call);                                                                   \
+    if (_r != ncclSuccess) return fail((e), ZB_EDEVICE, std::string(#call) + ": " + ncclGetErrorString(_r)); \
+  } while (0)
+
+int zb_comm_unique_id(uint8_t id[128]) {
+  if (!id) return ZB_EINVAL;
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return ZB_EDEVICE;
+  std::memcpy(id, &u, sizeof(u));
+  return ZB_OK;
+}
+
+int zb_comm_init(zb_engine* e, const uint8_t id[128], int nranks, int rank) {
+  if (!e || !id || nranks != e->cfg.partition_count || rank != e->cfg.partition_id || nranks > 64) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  NCCLCHECK(e, ncclCommInitRank(&e->comm, nranks, u, rank));
+  HIPCHECK(e, hipMalloc(&e->d_xcounts, 2 * 64 * sizeof(uint64_t)));
+  return ensure_outbox(e);
+}
+
+int zb_comm_pending(zb_engine* e, uint64_t global[2]) {
+  if (!e || !global || !e->comm) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  uint64_t local[2] = {0, 0};
+  for (int k = 0; k < 2; k++) {
+    int rc = zb_outbox_count(e, k + 1, &local[k]);
+    if (rc != ZB_OK) return rc;
+  }
+  HIPCHECK(e, hipMemcpyAsync(e->d_xcounts, local, sizeof(local), hipMemcpyHostToDevice, e->stream));
+  NCCLCHECK(e, ncclAllReduce(e->d_xcounts, e->d_xcounts, 2, ncclUint64, ncclSum, e->comm, e->stream));
+  HIPCHECK(e, hipMemcpyAsync(global, e->d_xcounts, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  return ZB_OK;
+}
+
+int zb_comm_exchange(zb_engine* e, int kind, uint64_t* received) {
+  if (!e || !received || !e->comm || (kind != ZB_XCHG_OPEN && kind != ZB_XCHG_CORRELATE)) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  const int P = e->cfg.partition_count;
+  *received = 0;
+  uint64_t n = 0;
+  int rc = zb_outbox_count(e, kind, &n);
+  if (rc != ZB_OK) return rc;
+  zb_exchange_rec* send = nullptr;
+  zb_exchange_rec* recv = nullptr;
+  auto cleanup = [&]() {
+    if (send) (void)hipFree(send);
+    if (recv) (void)hipFree(recv);
+  };
+  std::vector<uint64_t> sc(P, 0), rcv(P, 0);
+  if (hipMalloc(&send, std::max<uint64_t>(n, 1) * sizeof(zb_exchange_rec)) != hipSuccess) {
+    cleanup();
+    return fail(e, ZB_ENOMEM, "exchange send buffer");
+  }
+  uint64_t got = 0;
+  rc = zb_outbox_take(e, kind, send, std::max<uint64_t>(n, 1), 1, sc.data(), &got);
+  if (rc != ZB_OK) { cleanup(); return rc; }
+  // 1. counts: every rank learns how many commands each source sends it
+  if (hipMemcpyAsync(e->d_xcounts, sc.data(), P * 8, hipMemcpyHostToDevice, e->stream) != hipSuccess) {
+    cleanup();
+    return fail(e, ZB_EDEVICE, "exchange counts upload");
+  }
+  ncclResult_t nr = ncclGroupStart();
+  for (int q = 0; q < P && nr == ncclSuccess; q++) {
+    nr = ncclSend(e->d_xcounts + q, 1, ncclUint64, q, e->comm, e->stream);
+    if (nr == ncclSuccess) nr = ncclRecv(e->d_xcounts + 64 + q, 1, ncclUint64, q, e->comm, e->stream);
+  }
+  if (nr == ncclSuccess) nr = ncclGroupEnd();
+  if (nr != ncclSuccess) { cleanup(); return fail(e, ZB_EDEVICE, std::string("exchange counts: ") + ncclGetErrorString(nr)); }
+  if (hipMemcpyAsync(rcv.data(), e->d_xcounts + 64, P * 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+      hipStreamSynchronize(e->stream) != hipSuccess) {
+    cleanup();
+    return fail(e, ZB_EDEVICE, "exchange counts download");
+  }
+  uint64_t total = 0;
+  for (int q = 0; q < P; q++) total += rcv[q];
+  if (hipMalloc(&recv, std::max<uint64_t>(total, 1) * sizeof(zb_exchange_rec)) != hipSuccess) {
+    cleanup();
+    return fail(e, ZB_ENOMEM, "exchange receive buffer");
+  }
+  // 2. records: slices by target out, by source in (source-rank order = canonical delivery order)
+  nr = ncclGroupStart();
+  uint64_t so = 0, ro = 0;
+  for (int q = 0; q < P && nr == ncclSuccess; q++) {
+    if (sc[q]) nr = ncclSend(send + so, sc[q] * sizeof(zb_exchange_rec), ncclUint8, q, e->comm, e->stream);
+    if (nr == ncclSuccess && rcv[q]) nr = ncclRecv(recv + ro, rcv[q] * sizeof(zb_exchange_rec), ncclUint8, q, e->comm, e->stream);
+    so += sc[q];
+    ro += rcv[q];
+  }
+  if (nr == ncclSuccess) nr = ncclGroupEnd();
+  if (nr != ncclSuccess) { cleanup(); return fail(e, ZB_EDEVICE, std::string("exchange records: ") + ncclGetErrorString(nr)); }
+  if (hipStreamSynchronize(e->stream) != hipSuccess) { cleanup(); return fail(e, ZB_EDEVICE, "exchange sync"); }
+  rc = total ? zb_inbox_submit(e, kind, recv, total, 1) : ZB_OK;
+  cleanup();
+  if (rc == ZB_OK) *received = total;
   return rc;
 }
 

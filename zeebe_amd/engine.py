@@ -105,6 +105,10 @@ def lib():
         L.zb_inbox_submit.argtypes = [vp, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         L.zb_outbox_count.argtypes = [vp, ctypes.c_int, u64p]
         L.zb_outbox_take.argtypes = [vp, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, u64p, u64p]
+        L.zb_comm_unique_id.argtypes = [ctypes.c_char_p]
+        L.zb_comm_init.argtypes = [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+        L.zb_comm_pending.argtypes = [vp, u64p]
+        L.zb_comm_exchange.argtypes = [vp, ctypes.c_int, u64p]
         _lib = L
     return _lib
 
@@ -112,7 +116,8 @@ def lib():
 EXPORTED_SYMBOLS = ["zb_engine_create", "zb_engine_destroy", "zb_last_error", "zb_reset", "zb_deploy",
                     "zb_set_job_completion_payload", "zb_submit_creates", "zb_step", "zb_log_size",
                     "zb_read_descriptors", "zb_drain", "zb_counters", "zb_submit_publishes", "zb_inbox_submit",
-                    "zb_outbox_count", "zb_outbox_take"]
+                    "zb_outbox_count", "zb_outbox_take", "zb_comm_unique_id", "zb_comm_init", "zb_comm_pending",
+                    "zb_comm_exchange"]
 
 
 class Engine:
@@ -254,6 +259,28 @@ class Engine:
         n = len(a) // 256
         if n:
             self._check(self._L.zb_inbox_submit(self._h, kind, a.ctypes.data, n, 0))
+
+    # ---- RCCL exchange between engines of different processes (one partition per GPU)
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        rc = lib().zb_comm_unique_id(buf)
+        if rc != ZB_OK:
+            raise ZbError(rc, "zb_comm_unique_id failed")
+        return buf.raw
+
+    def comm_init(self, unique_id: bytes, nranks: int, rank: int):
+        self._check(self._L.zb_comm_init(self._h, unique_id, nranks, rank))
+
+    def comm_pending(self):
+        g = (ctypes.c_uint64 * 2)()
+        self._check(self._L.zb_comm_pending(self._h, g))
+        return int(g[0]), int(g[1])
+
+    def comm_exchange(self, kind: int) -> int:
+        n = ctypes.c_uint64(0)
+        self._check(self._L.zb_comm_exchange(self._h, kind, ctypes.byref(n)))
+        return n.value
 
     def publish(self, name: bytes, correlation_keys, payloads, ttl: int = 3600000):
         """MESSAGE PUBLISH commands, one message name and time-to-live for the batch."""
