@@ -31,9 +31,11 @@ PMC_FILE = os.path.join(ROOT, "profiles", "r01", "pmc_v4.json")
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", choices=("c2", "c3", "c5"), default="c2",
+                    help="BASELINE.json configuration (default: C2, the headline metric); c3 / c5: bench_extra.py")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--instances", type=int, default=1_000_000)
+    ap.add_argument("--instances", type=int, default=0, help="per GPU (default: C2/C5 1,000,000, C3 10,000,000)")
     ap.add_argument("--tasks", type=int, default=20)
     ap.add_argument("--cpu-sample", type=int, default=30_000, help="instances in the oracle CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -78,6 +80,11 @@ def main():
         # process: the engine (libzbgpu.so) drives its GPU through the system ROCm runtime and
         # synchronizes its own stream at the end of every zb_step.
         dist.init_process_group("gloo")
+
+    if a.instances == 0:
+        a.instances = 10_000_000 if a.config == "c3" else 1_000_000
+    if a.config != "c2":
+        return run_other(a, rank, world, local_rank, dist)
 
     from zeebe_amd import bpmn, workloads
     from zeebe_amd.engine import Engine
@@ -186,6 +193,41 @@ def main():
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.cpu_sample, a.tasks)
         print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def run_other(a, rank, world, local_rank, dist):
+    import socket
+
+    import torch
+    import torch.distributed as tdist
+
+    import bench_extra
+
+    if dist is None and a.config == "c5":  # the exchange driver needs a (one-rank) control plane
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(s.getsockname()[1]))
+        s.close()
+        tdist.init_process_group("gloo", rank=0, world_size=1)
+        dist = tdist
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def reduce(v, op):
+        if dist is None:
+            return v
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    fn = bench_extra.run_c3 if a.config == "c3" else bench_extra.run_c5
+    fn(a, rank, world, local_rank, dist, barrier, lambda v: reduce(v, tdist.ReduceOp.MAX),
+       lambda v: reduce(v, tdist.ReduceOp.SUM))
     if dist is not None:
         dist.destroy_process_group()
 

@@ -1,0 +1,135 @@
+"""bench.py --config c3 | c5: the other BASELINE.json configurations (the default run is C2).
+
+C3: two exclusive gateways with json-el conditions over msgpack payloads
+    {"amount": U[0,2000), "region": EU|US|APAC, "score": U[0,1)} (Philox, seed 42), 10M instances on one GPU.
+C5: start -> message catch ("order", $.orderId) -> end, instances round-robin over the
+    partitions (one per GPU); phase 1 runs the CREATEs to quiescence (subscriptions opened on partition
+    abs(hash % P)), phase 2 publishes one message per orderId (TTL 1 h, payload {"paid": true}) and runs
+    to quiescence. The engines exchange the subscription / correlation commands over RCCL
+    (zeebe_amd.cluster.DistCluster). One step = both phases; transitions = WORKFLOW_INSTANCE events.
+"""
+import json
+import os
+import time
+
+import numpy as np
+
+HBM_PEAK_GBS = 8000.0
+BYTES_PER_TRANSITION = 96
+
+
+def _routing(cks, world):
+    """abs(javaHash(ck) % P) for many keys at once (SubscriptionUtil.java:30-38), vectorized by length."""
+    out = np.zeros(len(cks), dtype=np.int64)
+    by_len = {}
+    for i, c in enumerate(cks):
+        by_len.setdefault(len(c), []).append(i)
+    for L, idx in by_len.items():
+        a = np.frombuffer(b"".join(cks[i] for i in idx), dtype=np.int8).reshape(len(idx), L).astype(np.int64)
+        h = np.zeros(len(idx), dtype=np.int64)
+        for j in range(L):
+            h = (h * 31 + a[:, j]) & 0xFFFFFFFF
+        h = np.where(h >= (1 << 31), h - (1 << 32), h)
+        out[np.asarray(idx)] = np.abs(np.fmod(h, world))
+    return out
+
+
+def _emit(out, rank):
+    if rank == 0:
+        print(json.dumps(out))
+
+
+def run_c3(a, rank, world, local_rank, dist, barrier, reduce_max, reduce_sum):
+    from zeebe_amd import bpmn, workloads
+    from zeebe_amd.engine import Engine
+
+    n = a.instances
+    eng = Engine(device=0 if a.same_device else local_rank, partition_id=rank, partition_count=world,
+                 log_capacity=n * 16, row_capacity=1 << 20, arena_bytes=n * 64 + (64 << 20), wave_only=a.wave_only)
+    eng.deploy(bpmn.xor_workflow().to_xml(), 100, 1)
+    blob, offs = workloads.xor_payloads(n, start=rank * n)
+    eng.create_packed("xor", blob, offs)
+
+    def step():
+        eng.reset(keep_staged=True)
+        st = eng.step()
+        assert st["quiescent"], st
+        return st
+
+    for _ in range(a.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    tr = comp = cond = 0
+    kms = 0.0
+    for _ in range(a.steps):
+        st = step()
+        tr += st["transitions"]; comp += st["completed_instances"]; cond += st["condition_payload_bytes"]
+        kms += st["wave_kernel_ms"]
+    barrier()
+    el = reduce_max(time.perf_counter() - t0)
+    all_tr, all_comp = reduce_sum(tr), reduce_sum(comp)
+    alg = BYTES_PER_TRANSITION * tr + cond
+    ach = alg / (kms / 1e3) / 1e9 if kms else 0.0
+    _emit({"metric": "BPMN element transitions/sec (+ completed instances/sec) per node; % HBM roofline",
+           "value": all_tr / el, "unit": "transitions/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+           "ms_per_step": el * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "int64/f64", "data": "synthetic (SURVEY §8d C3 payloads, Philox seed 42)",
+           "config": {"workload": "C3: exclusive gateways + json-el over msgpack, %d instances per GPU" % n,
+                      "instances_per_gpu": n, "partitions": world, "parallelism": "partition-per-gpu"},
+           "completed_instances_per_s": all_comp / el,
+           "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": ach / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_transition": BYTES_PER_TRANSITION,
+                        "condition_payload_bytes_per_step": cond / a.steps}}, rank)
+
+
+def run_c5(a, rank, world, local_rank, dist, barrier, reduce_max, reduce_sum):
+    import msgpack
+
+    from zeebe_amd import bpmn, cluster
+    from zeebe_amd.engine import Engine
+
+    n = a.instances  # per partition
+    N = n * world
+    eng = Engine(device=0 if a.same_device else local_rank, partition_id=rank, partition_count=world,
+                 log_capacity=n * 24, row_capacity=n + 1024, arena_bytes=n * 640 + (64 << 20))
+    eng.deploy(bpmn.message_workflow().to_xml(), 100, 1)
+    # instance i -> partition i % P (round-robin CREATE dispatch)
+    mine = range(rank, N, world)
+    create_payloads = [msgpack.packb({"orderId": "order-%d" % i}) for i in mine]
+    cks = [b"order-%d" % i for i in range(N)]
+    route = _routing(cks, world)
+    my_msgs = [cks[i] for i in np.nonzero(route == rank)[0]]
+    paid = msgpack.packb({"paid": True})
+    dc = cluster.DistCluster(eng)
+
+    def step():
+        eng.reset()
+        eng.create("msg", create_payloads)
+        t = time.perf_counter()
+        dc.settle()
+        if my_msgs:
+            eng.publish(b"order", my_msgs, [paid] * len(my_msgs), 3600000)
+        dc.settle()
+        return time.perf_counter() - t
+
+    for _ in range(a.warmup):
+        step()
+    barrier()
+    el = 0.0
+    for _ in range(a.steps):
+        barrier()
+        el += reduce_max(step())
+    completed = reduce_sum(eng.counters()["completed"])
+    assert completed == N, (completed, N)
+    tr = 13 * N * a.steps  # 13 WORKFLOW_INSTANCE events per instance
+    _emit({"metric": "BPMN element transitions/sec (+ completed instances/sec) per node; % HBM roofline",
+           "value": tr / el, "unit": "transitions/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+           "ms_per_step": el * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "int64", "data": "synthetic (SURVEY §8d C5: orderId 'order-<i>', payload {paid: true})",
+           "config": {"workload": "C5: message catch correlated across partitions (RCCL exchange), "
+                                  "%d instances per GPU" % n, "instances_per_gpu": n, "partitions": world,
+                      "parallelism": "partition-per-gpu", "exchange": "RCCL ncclSend/ncclRecv (engine)"},
+           "completed_instances_per_s": N * a.steps / el,
+           "note": "timed region: CREATE injection to quiescence, exchange rounds, publish to quiescence; "
+                   "excludes payload generation and hash routing of the published keys"}, rank)
