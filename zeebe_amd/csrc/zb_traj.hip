@@ -38,7 +38,61 @@
 namespace zbg {
 
 constexpr int TWG = TRAJ_WG;
+
+// Read-only tables (the deployed model; per-generation bases written by earlier launches) accessed
+// through the constant address space: with a wave-uniform index (every control decision of a
+// uniform batch) the backend emits scalar loads (s_load, scalar cache) instead of vector loads on
+// the generation loop's dependence chain.
+template <class T>
+using cptr = const T __attribute__((address_space(4)))*;
+template <class T>
+__device__ __forceinline__ cptr<T> K(const T* p) { return (cptr<T>)p; }
+// element i of a read-only array of dword-multiple structs through the constant address space
+template <class T>
+__device__ __forceinline__ T kload(const T* p, uint64_t i) {
+  static_assert(sizeof(T) % 4 == 0, "dword-multiple struct");
+  T out;
+  const cptr<uint32_t> src = (cptr<uint32_t>)(p + i);
+  uint32_t* d = (uint32_t*)&out;
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(T) / 4); k++) d[k] = src[k];
+  return out;
+}
 constexpr uint8_t LN = 0xff;  // no local row
+
+// The control fields of a DevElem (zb_device.hpp layout), as dword loads through the constant
+// address space: seven independent s_load_dword with a uniform element index, no byte loads, no
+// stack copy for the dynamically indexed step table.
+struct ElemCtl {
+  uint32_t st[3];  // step[0..11]                                   (dwords 1..3)
+  uint32_t ot;     // out0 | target << 16                           (dword 4)
+  uint32_t sd;     // start | dflt << 16                            (dword 5)
+  uint32_t cc;     // cond_begin | cond_count << 16                 (dword 6)
+  __device__ __forceinline__ uint8_t step(uint32_t intent) const {
+    const uint32_t w = intent < 4 ? st[0] : (intent < 8 ? st[1] : st[2]);
+    return (uint8_t)(w >> ((intent & 3) * 8));
+  }
+  __device__ __forceinline__ uint16_t out0() const { return (uint16_t)ot; }
+  __device__ __forceinline__ uint16_t target() const { return (uint16_t)(ot >> 16); }
+  __device__ __forceinline__ uint16_t start() const { return (uint16_t)sd; }
+  __device__ __forceinline__ uint16_t dflt() const { return (uint16_t)(sd >> 16); }
+  __device__ __forceinline__ uint16_t cond_begin() const { return (uint16_t)cc; }
+  __device__ __forceinline__ uint16_t cond_count() const { return (uint16_t)(cc >> 16); }
+};
+static_assert(offsetof(DevElem, step) == 4 && offsetof(DevElem, out0) == 16 && offsetof(DevElem, target) == 18 &&
+                  offsetof(DevElem, start) == 20 && offsetof(DevElem, dflt) == 22 &&
+                  offsetof(DevElem, cond_begin) == 24 && offsetof(DevElem, cond_count) == 26 &&
+                  offsetof(DevElem, job_payload) == 40 && sizeof(DevElem) == 72,
+              "ElemCtl mirrors the DevElem layout");
+__device__ __forceinline__ uint32_t elem_dword(const TrajParams& P, uint32_t e, uint32_t d) {
+  return K((const uint32_t*)P.elems)[(uint64_t)e * (sizeof(DevElem) / 4) + d];
+}
+__device__ __forceinline__ ElemCtl elem_ctl(const TrajParams& P, uint32_t e) {
+  ElemCtl c;
+  c.st[0] = elem_dword(P, e, 1); c.st[1] = elem_dword(P, e, 2); c.st[2] = elem_dword(P, e, 3);
+  c.ot = elem_dword(P, e, 4); c.sd = elem_dword(P, e, 5); c.cc = elem_dword(P, e, 6);
+  return c;
+}
 
 enum TrajFlags : uint8_t {
   TK_WF = 1,         // key := new wf key #ord
@@ -200,6 +254,7 @@ __device__ __forceinline__ void t_incident(Inst& I, const TRec& rec, int64_t pos
 // COND: exclusive splits are evaluated here (else they send the batch to the wave pipeline).
 template <bool EMIT, bool COND>
 __device__ __forceinline__ void t_step(const TrajParams& P, Inst& I, const TRec& rec, int64_t pos) {
+  // (rec's control fields are wave-uniform in a uniform batch: t_record scalarized them)
   const uint8_t intent = rec.intent;
   const bool stateless = intent == WI_SEQUENCE_FLOW_TAKEN || intent == WI_START_EVENT_OCCURRED ||
                          intent == WI_END_EVENT_OCCURRED || intent == WI_GATEWAY_ACTIVATED;
@@ -223,8 +278,8 @@ __device__ __forceinline__ void t_step(const TrajParams& P, Inst& I, const TRec&
   }
   if (!ok) return;
   if (rec.elem == NO_ELEM) { I.err |= TE_FALLBACK; return; }
-  const DevElem& el = P.elems[rec.elem];
-  const uint8_t step = el.step[intent];
+  const ElemCtl el = elem_ctl(P, rec.elem);  // scalar loads when rec.elem is wave-uniform
+  const uint8_t step = el.step(intent);
   if (step == ST_UNBOUND || step == ST_NONE) return;
 
   TRec s = rec;
@@ -270,9 +325,9 @@ __device__ __forceinline__ void t_step(const TrajParams& P, Inst& I, const TRec&
         uint16_t chosen = NO_ELEM;
         CondOut co{0, 0, 0, 0};
         bool unsup = false;
-        for (uint32_t c = 0; c < el.cond_count; c++) {
-          const uint16_t flow = P.cond_flows[el.cond_begin + c];
-          const bool res = eval_condition(P.elems[flow].cond_prog, P.code, pp + 4, len, P.consts, P.queries,
+        for (uint32_t c = 0; c < el.cond_count(); c++) {
+          const uint16_t flow = K(P.cond_flows)[el.cond_begin() + c];
+          const bool res = eval_condition(K(P.elems)[flow].cond_prog, P.code, pp + 4, len, P.consts, P.queries,
                                           P.filters, P.pool, co, unsup);
           if (unsup || co.err) break;
           if (res) { chosen = flow; break; }
@@ -280,7 +335,7 @@ __device__ __forceinline__ void t_step(const TrajParams& P, Inst& I, const TRec&
         I.cond_bytes += len;
         if (unsup) { I.err |= TE_FALLBACK; return; }
         if (co.err) { t_incident(I, rec, pos, co.err & 7, co.a & 15, co.b & 15, co.q); break; }
-        if (chosen == NO_ELEM) chosen = el.dflt;
+        if (chosen == NO_ELEM) chosen = el.dflt();
         if (chosen == NO_ELEM) { t_incident(I, rec, pos, EC_NO_FLOW, 0, 0, 0); break; }
         s.elem = chosen;
         s.intent = WI_SEQUENCE_FLOW_TAKEN;
@@ -310,9 +365,9 @@ __device__ __forceinline__ void t_step(const TrajParams& P, Inst& I, const TRec&
     case ST_ACTIVATE_GATEWAY:
     case ST_TRIGGER_END_EVENT: {
       uint8_t out_intent;
-      if (step == ST_TAKE_SEQUENCE_FLOW) { s.elem = el.out0; out_intent = WI_SEQUENCE_FLOW_TAKEN; }
-      else if (step == ST_ACTIVATE_GATEWAY) { s.elem = el.target; out_intent = WI_GATEWAY_ACTIVATED; }
-      else { s.elem = el.target; out_intent = WI_END_EVENT_OCCURRED; }
+      if (step == ST_TAKE_SEQUENCE_FLOW) { s.elem = el.out0(); out_intent = WI_SEQUENCE_FLOW_TAKEN; }
+      else if (step == ST_ACTIVATE_GATEWAY) { s.elem = el.target(); out_intent = WI_GATEWAY_ACTIVATED; }
+      else { s.elem = el.target(); out_intent = WI_END_EVENT_OCCURRED; }
       if (s.elem == NO_ELEM) { I.err |= TE_FALLBACK; return; }
       s.intent = out_intent;
       s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
@@ -324,7 +379,7 @@ __device__ __forceinline__ void t_step(const TrajParams& P, Inst& I, const TRec&
     case ST_START_STATEFUL_ELEMENT: {  // -> ELEMENT_READY(new key), index insert with parent = scope
       const int row = I.alloc();
       if (row == LN) return;
-      s.elem = el.target;
+      s.elem = el.target();
       s.intent = WI_ELEMENT_READY;
       s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
       s.flags = TK_WF | TK_ROW_INIT; s.ord = (uint8_t)I.nwf++;
@@ -335,8 +390,8 @@ __device__ __forceinline__ void t_step(const TrajParams& P, Inst& I, const TRec&
       break;
     }
     case ST_TRIGGER_START_EVENT: {  // TriggerStartEventHandler :30-39
-      if (el.start == NO_ELEM) { I.err |= TE_FALLBACK; return; }
-      s.elem = el.start;
+      if (el.start() == NO_ELEM) { I.err |= TE_FALLBACK; return; }
+      s.elem = el.start();
       s.scope_key = rec.key;
       s.intent = WI_START_EVENT_OCCURRED;
       s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
@@ -362,8 +417,18 @@ __device__ __forceinline__ void t_step(const TrajParams& P, Inst& I, const TRec&
 }
 
 // process_record (zb_wave.hip) on local rows
-template <bool EMIT, bool COND>
-__device__ __forceinline__ void t_record(const TrajParams& P, Inst& I, const TRec& rec, int64_t pos) {
+template <bool EMIT, bool COND, bool UNI>
+__device__ __forceinline__ void t_record(const TrajParams& P, Inst& I, const TRec& rec_in, int64_t pos) {
+  TRec rec = rec_in;
+  if (UNI) {  // control fields are the same in every lane: keep them in SGPRs (scalar branches, s_load)
+    rec.elem = (uint16_t)__builtin_amdgcn_readfirstlane(rec.elem);
+    rec.intent = (uint8_t)__builtin_amdgcn_readfirstlane(rec.intent);
+    rec.kind = (uint8_t)__builtin_amdgcn_readfirstlane(rec.kind);
+    rec.rself = (uint8_t)__builtin_amdgcn_readfirstlane(rec.rself);
+    rec.rscope = (uint8_t)__builtin_amdgcn_readfirstlane(rec.rscope);
+    rec.flags = (uint8_t)__builtin_amdgcn_readfirstlane(rec.flags);
+    rec.ord = (uint8_t)__builtin_amdgcn_readfirstlane(rec.ord);
+  }
   const uint8_t vt = kind_vt(rec.kind), rt = kind_rt(rec.kind);
   if (vt == ZB_VT_WORKFLOW_INSTANCE) {
     if (rt == ZB_RT_COMMAND) {
@@ -416,7 +481,7 @@ __device__ __forceinline__ void t_record(const TrajParams& P, Inst& I, const TRe
       I.push(s);
       s.intent = JI_COMPLETED;
       s.kind = make_kind(ZB_VT_JOB, ZB_RT_EVENT, I.nn > 0);
-      s.payload = P.elems[rec.elem].job_payload;
+      s.payload = elem_dword(P, rec.elem, 10);  // DevElem.job_payload
       I.push(s);
     } else if (rt == ZB_RT_EVENT && rec.intent == JI_CREATED) {  // JobCreatedProcessor :408-426
       if (rec.scope_key != NOK && I.alive(rec.rself)) I.rjob[rec.rself] = rec.key;
@@ -554,7 +619,7 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
     }
     // ---- process this generation (log order inside the instance)
 #pragma unroll 1
-    for (int k = 0; k < I.nc; k++) t_record<EMIT, COND>(P, I, I.cur.get(k), fpos + k);
+    for (int k = 0; k < I.nc; k++) t_record<EMIT, COND, UNI>(P, I, I.cur.get(k), fpos + k);
     // ---- place the follow-ups
     uint64_t a = (uint64_t)I.nn | ((uint64_t)I.nwf << 16) | ((uint64_t)I.njob << 32);
     uint64_t bytes = 0;
@@ -565,14 +630,14 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
     uint32_t kwf, kjob;  // key ordinals of this instance's first new wf / job key
     if (UNI) {
       // positions and keys are affine in the instance index; the arena is allocated per wave
-      const uint64_t c = P.agg[w];
-      const TrajBase wb = P.wbase[w];
+      const uint64_t c = kload(P.agg, (uint64_t)w);
+      const TrajBase wb = kload(P.wbase, (uint64_t)w);
       pos0 = wb.pos + inst * (int64_t)(c & 0xffff);
       kwf = (uint32_t)(wb.wf + inst * (int64_t)((c >> 16) & 0xffff));
       kjob = (uint32_t)(wb.job + inst * (int64_t)(c >> 32));
       if (EMIT && I.merge) {
         // this instance's merge slot of generation w (MergeGen: the stride bounds every instance's result)
-        const MergeGen g = P.mgen[w];
+        const MergeGen g = kload(P.mgen, (uint64_t)w);
         tb = (uint64_t)wb.mbase + (uint64_t)inst * g.stride;
         bytes = 0;
         if (!g.has || tblob_bytes(I.m_len) > g.stride) { I.err |= DE_UNSUPPORTED; tb = P.arena_cap; }
