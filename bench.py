@@ -184,7 +184,7 @@ def main():
                          "traffic_note": "HBM bytes per launch of the emit kernel (FETCH_SIZE x2 + WRITE_SIZE, "
                                          "profiles/r01/pmc_v4.json); below the algorithmic bytes because element "
                                          "instances stay in registers instead of SoA rows",
-                         "kernel": "zbg::k_traj (count + emit passes)" if tot["path"] == 1 else
+                         "kernel": "zbg::k_traj (count + emit passes)" if tot["path"] in (1, 2) else
                                    "zbg::k_process/k_scan/k_emit/k_merge", "launches": tot["launches"],
                          "avg_launch_us": tot["kernel_ms"] * 1e3 / max(tot["launches"], 1),
                          "alg_bytes_per_transition": BYTES_PER_TRANSITION,

@@ -104,7 +104,8 @@ typedef struct zb_step_stats {
   double process_kernel_ms;    /* k_process share of wave_kernel_ms (trajectory: count pass) */
   double emit_kernel_ms;       /* k_scan + k_emit share (trajectory: scans + emit pass) */
   double aux_kernel_ms;        /* k_merge + k_cond share */
-  uint64_t path;               /* 0: wave pipeline, 1: trajectory path (zb_traj.hip) ran the step */
+  uint64_t path;               /* 0: wave pipeline, 1: trajectory path (zb_traj.hip) ran the step,
+                                  2: trajectory path as a class batch (k_cls_*: split outcomes fixed at creation) */
 } zb_step_stats;
 
 /* One partition-to-partition command (SubscriptionCommandSender.java:83-128), 256 bytes, exchanged

@@ -1,0 +1,128 @@
+"""Class batches (zb_traj.hip k_cls_*) vs the oracle, record for record.
+
+A batch of CREATEs for one process whose exclusive splits read only the CREATE payload is split into
+trajectory classes by the outcome of every split, and each class runs like a uniform batch. These
+cases check the class path itself (stat path == 2) and each way out of it: more classes than CLS_MAX
+and incidents go to the per-instance trajectory path (path == 1), a split that reads a merge result goes
+to the wave pipeline (path == 0). Every case is compared with the oracle bit for bit.
+"""
+import random
+
+import msgpack
+import pytest
+
+from oracle import zbref
+from zeebe_amd import bpmn, workloads
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(xml, process, payloads, job_payloads=None, wave_only=False, **cap):
+    from zeebe_amd.engine import Engine
+
+    o = zbref.Oracle()
+    o.deploy(xml, 100, 1)
+    e = Engine(wave_only=wave_only, **cap)
+    e.deploy(xml, 100, 1)
+    for act, p in (job_payloads or {}).items():
+        o.set_job_payload(100, act, p)
+        e.set_job_payload(100, act, p)
+    for p in payloads:
+        o.create(process, p)
+    e.create(process, payloads)
+    o.run()
+    st = e.step()
+    assert st["quiescent"]
+    ref, got = o.records(), e.records()
+    assert len(got) == len(ref), (len(got), len(ref))
+    for a, b in zip(ref, got):
+        assert (a.position, a.key, a.record_type, a.value_type, a.intent) == \
+               (b.position, b.key, b.record_type, b.value_type, b.intent), (a, b)
+        assert a.value == b.value, (a.position, msgpack.unpackb(a.value, raw=False),
+                                    msgpack.unpackb(b.value, raw=False))
+    oc, ec = o.counters(), e.counters()
+    assert (ec["next_wf_key"], ec["next_job_key"], ec["completed"]) == \
+           (oc["next_wf_key"], oc["next_job_key"], oc["completed"])
+    e.close()
+    return st
+
+
+@pytest.mark.parametrize("n", [1, 5, 63, 64, 65, 3000])
+def test_c3_classes(n):
+    cfg = workloads.CONFIGS["c3"]
+    blob, offs = cfg["payloads"](n)
+    st = _run(cfg["workflow"]().to_xml(), cfg["process"], workloads.split(blob, offs))
+    assert st["path"] == 2
+    assert st["completed_instances"] == n
+
+
+def _xor_tasks():
+    # split first, then a service task on every branch: merges follow the split (class batch)
+    b = bpmn.Bpmn.create_executable_process("xt").start_event("s").exclusive_gateway("x")
+    b.sequence_flow_id("fa").condition("$.v < 10").service_task("ta", type="a").end_event("ea")
+    b.move_to_node("x").sequence_flow_id("fb").condition("$.v >= 10 && $.w == true").service_task(
+        "tb", type="b").service_task("tb2", type="b2").end_event("eb")
+    return b.move_to_node("x").default_flow().sequence_flow_id("fc").end_event("ec").done()
+
+
+def test_split_then_tasks():
+    rng = random.Random(7)
+    payloads = [msgpack.packb({"v": rng.randrange(20), "w": rng.random() < 0.5, "id": i}) for i in range(700)]
+    jp = {"ta": msgpack.packb({"a": 1}), "tb": msgpack.packb({"b": "x" * 9}), "tb2": msgpack.packb({"v": -1})}
+    st = _run(_xor_tasks().to_xml(), "xt", payloads, jp)
+    assert st["path"] == 2
+    st_w = _run(_xor_tasks().to_xml(), "xt", payloads, jp, wave_only=True)
+    assert st_w["path"] == 0
+    for k in ("transitions", "completed_instances", "merges", "merge_bytes", "condition_payload_bytes"):
+        assert st[k] == st_w[k], k
+
+
+def test_merge_before_split():
+    # a task's merge result feeds the split: the class trace refuses it, the wave pipeline runs the batch
+    b = bpmn.Bpmn.create_executable_process("ms").start_event("s").service_task("t", type="t").exclusive_gateway("x")
+    b.sequence_flow_id("f1").condition("$.k > 3").end_event("e1")
+    m = b.move_to_node("x").default_flow().sequence_flow_id("f2").end_event("e2").done()
+    payloads = [msgpack.packb({"k": i % 7}) for i in range(200)]
+    st = _run(m.to_xml(), "ms", payloads, {"t": msgpack.packb({"j": 1})})
+    assert st["path"] == 0
+
+
+def test_more_classes_than_cls_max():
+    # four splits on four keys (radix 4 each -> 256 keys): random payloads give far more than 8 classes
+    b = bpmn.Bpmn.create_executable_process("many").start_event("s")
+    for k in range(4):
+        g = b.exclusive_gateway("g%d" % k)
+        g.sequence_flow_id("c%da" % k).condition("$.k%d < 3" % k).end_event("e%da" % k)
+        g.move_to_node("g%d" % k).sequence_flow_id("c%db" % k).condition("$.k%d < 6" % k).end_event("e%db" % k)
+        b = g.move_to_node("g%d" % k).default_flow().sequence_flow_id("d%d" % k)
+    m = b.end_event("end").done()
+    rng = random.Random(3)
+    payloads = [msgpack.packb({"k%d" % k: rng.randrange(9) for k in range(4)}) for _ in range(1500)]
+    st = _run(m.to_xml(), "many", payloads)
+    assert st["path"] == 1
+
+
+def test_few_of_many_keys():
+    # the same model with payloads that only ever produce 3 distinct keys stays on the class path
+    b = bpmn.Bpmn.create_executable_process("many").start_event("s")
+    for k in range(4):
+        g = b.exclusive_gateway("g%d" % k)
+        g.sequence_flow_id("c%da" % k).condition("$.k%d < 3" % k).end_event("e%da" % k)
+        g.move_to_node("g%d" % k).sequence_flow_id("c%db" % k).condition("$.k%d < 6" % k).end_event("e%db" % k)
+        b = g.move_to_node("g%d" % k).default_flow().sequence_flow_id("d%d" % k)
+    m = b.end_event("end").done()
+    shapes = [{"k0": 1, "k1": 0, "k2": 0, "k3": 0}, {"k0": 8, "k1": 8, "k2": 4, "k3": 0},
+              {"k0": 7, "k1": 7, "k2": 7, "k3": 7}]
+    payloads = [msgpack.packb(shapes[(i * 7) % 3]) for i in range(999)]
+    st = _run(m.to_xml(), "many", payloads)
+    assert st["path"] == 2
+
+
+def test_incident_class_falls_back():
+    # no default flow: payloads where every condition is false raise an incident (per-instance path)
+    b = bpmn.Bpmn.create_executable_process("inc").start_event("s").exclusive_gateway("x")
+    b.sequence_flow_id("f1").condition("$.a == 1").end_event("e1")
+    m = b.move_to_node("x").sequence_flow_id("f2").condition("$.a == 2").end_event("e2").done()
+    payloads = [msgpack.packb({"a": i % 3}) for i in range(300)]
+    st = _run(m.to_xml(), "inc", payloads)
+    assert st["path"] == 1

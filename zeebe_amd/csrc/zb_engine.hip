@@ -27,7 +27,7 @@ constexpr int WAVES_PER_SYNC = 16;
 constexpr int EV_PER_WAVE = 4;  // before k_process, after k_process, after k_emit, after the aux kernels
 constexpr uint64_t STATIC_ARENA_BYTES = 1ull << 20;  // {} at ref 0 + harness job completion payloads
 constexpr uint64_t TRAJ_BUDGET_BYTES = 256ull << 20;  // per-(generation, workgroup) counts of the trajectory path
-constexpr int TRAJ_MAX_GENERATIONS = 4096;
+constexpr int TRAJ_MAX_GENERATIONS = CLS_ROW;
 constexpr int TRAJ_WAVE_CAP = 8192;                   // k_traj_scan grid bound (one workgroup per generation)
 
 template <class T>
@@ -137,8 +137,18 @@ struct zb_engine {
   TrajBase* t_wbase = nullptr;
   TrajCtl* t_ctl = nullptr;
   MergeGen* t_mgen = nullptr;     // [TRAJ_MAX_GENERATIONS] uniform batch merge slots
-  uint64_t* t_wstats = nullptr;   // [t_nwg_cap][6] emit statistics per workgroup
+  uint64_t* t_wstats = nullptr;   // [t_nwg_cap + CLS_MAX][6] emit statistics per workgroup
   TrajCtl* h_ctl_pinned = nullptr;
+  // class batches (zb_traj.hip k_cls_*): the model's exclusive splits as outcome-key digits
+  bool cls_ok = false;            // split outcome keys fit 8 bits and CLS_MAX_SPLITS splits
+  int nsplits = 0;
+  uint32_t split_elem[CLS_MAX_SPLITS] = {}, split_stride[CLS_MAX_SPLITS] = {};
+  ClsPlan* c_plan = nullptr;
+  uint64_t cls_cap = 0;           // instances the class buffers hold
+  uint8_t* c_ikey = nullptr;
+  uint32_t *c_khist = nullptr, *c_krep = nullptr;  // [256] each (one allocation)
+  uint64_t* c_mask = nullptr;
+  uint32_t *c_woffw = nullptr, *c_wgcnt = nullptr, *c_wgoff = nullptr, *c_perm = nullptr;
 
   // message correlation (zb_msg.hip): outboxes [0] open-subscription, [1] correlate
   zb_exchange_rec* obox[2] = {nullptr, nullptr};
@@ -264,7 +274,29 @@ int check_device_errors(zb_engine* e, uint32_t flags) {
 // Trajectory path (zb_traj.hip) for a batch of n CREATE commands injected at log_base on an idle
 // partition. Returns 1 when the batch ran to quiescence, 0 when the count pass asked for the wave
 // pipeline (nothing but scratch counts was written), <0 on a device error.
-int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st) {
+int grow_class_buffers(zb_engine* e, uint64_t n, uint64_t nwg) {
+  if (n <= e->cls_cap) return ZB_OK;
+  void* ps[] = {e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm};
+  for (void* q : ps)
+    if (q) (void)hipFree(q);
+  e->c_ikey = nullptr; e->c_khist = e->c_krep = nullptr; e->c_mask = nullptr;
+  e->c_woffw = e->c_wgcnt = e->c_wgoff = e->c_perm = nullptr;
+  e->cls_cap = 0;
+  const uint64_t groups = nwg * (TRAJ_WG / 64);
+  HIPCHECK(e, hipMalloc(&e->c_ikey, n));
+  HIPCHECK(e, hipMalloc(&e->c_khist, 512 * sizeof(uint32_t)));
+  e->c_krep = e->c_khist + 256;
+  HIPCHECK(e, hipMalloc(&e->c_mask, groups * CLS_MAX * sizeof(uint64_t)));
+  HIPCHECK(e, hipMalloc(&e->c_woffw, groups * CLS_MAX * sizeof(uint32_t)));
+  HIPCHECK(e, hipMalloc(&e->c_wgcnt, nwg * CLS_MAX * sizeof(uint32_t)));
+  HIPCHECK(e, hipMalloc(&e->c_wgoff, nwg * CLS_MAX * sizeof(uint32_t)));
+  HIPCHECK(e, hipMalloc(&e->c_perm, (n + 64 * CLS_MAX) * sizeof(uint32_t)));
+  if (!e->c_plan) HIPCHECK(e, hipMalloc(&e->c_plan, sizeof(ClsPlan)));
+  e->cls_cap = nwg * TRAJ_WG;
+  return ZB_OK;
+}
+
+int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st, bool allow_cls) {
   const uint64_t nwg = (uint64_t)((n + TRAJ_WG - 1) / TRAJ_WG);
   const uint64_t per_entry = sizeof(uint64_t) + sizeof(uint4);
   uint64_t wcap = std::min<uint64_t>(TRAJ_MAX_GENERATIONS, (TRAJ_BUDGET_BYTES / per_entry) / nwg);
@@ -283,8 +315,8 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st)
     if (e->t_wstats) (void)hipFree(e->t_wstats);
     e->t_wcount = nullptr;
     e->t_wstats = nullptr;
-    HIPCHECK(e, hipMalloc(&e->t_wcount, nwg * sizeof(uint32_t)));
-    HIPCHECK(e, hipMalloc(&e->t_wstats, nwg * 6 * sizeof(uint64_t)));
+    HIPCHECK(e, hipMalloc(&e->t_wcount, (nwg + CLS_MAX) * sizeof(uint32_t)));
+    HIPCHECK(e, hipMalloc(&e->t_wstats, (nwg + CLS_MAX) * 6 * sizeof(uint64_t)));
     e->t_nwg_cap = nwg;
   }
   TrajCtl c{};
@@ -314,6 +346,32 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st)
   // CREATEs all address one process has one trajectory shape: count it on the first instance.
   p.uni = (!e->has_splits && e->staged_uniform) ? n : 0;
   p.cond = e->has_splits ? 1 : 0;
+  // With exclusive splits whose conditions only ever read the CREATE payload, the batch splits into a
+  // few trajectory classes (k_cls_*); each runs like a uniform batch. More classes than CLS_MAX, or a
+  // class whose trajectory raises an incident, sends the batch to the per-instance count pass below.
+  p.cls = (allow_cls && e->has_splits && e->staged_uniform && e->cls_ok) ? 1 : 0;
+  p.nwg_e = (int32_t)nwg;
+  if (p.cls) {
+    int grc = grow_class_buffers(e, (uint64_t)n, nwg);
+    if (grc != ZB_OK) return grc;
+    p.nwg_e = (int32_t)(nwg + CLS_MAX / (TRAJ_WG / 64));  // + the padding of every class segment
+    p.nsplits = e->nsplits;
+    for (int k = 0; k < CLS_MAX_SPLITS; k++) {
+      p.split_elem[k] = e->split_elem[k];
+      p.split_stride[k] = e->split_stride[k];
+    }
+    p.plan = e->c_plan;
+    p.ikey = e->c_ikey;
+    p.khist = e->c_khist;
+    p.krep = e->c_krep;
+    p.cmask = e->c_mask;
+    p.woffw = e->c_woffw;
+    p.wgcnt = e->c_wgcnt;
+    p.wgoff = e->c_wgoff;
+    p.perm = e->c_perm;
+    HIPCHECK(e, hipMemsetAsync(e->c_khist, 0, 256 * sizeof(uint32_t), e->stream));
+    HIPCHECK(e, hipMemsetAsync(e->c_krep, 0xff, 256 * sizeof(uint32_t), e->stream));
+  }
   p.agg = e->t_agg;
   p.wcount = e->t_wcount;
   p.woff = e->t_woff;
@@ -331,7 +389,8 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st)
   p.arena_cap = e->cfg.arena_bytes;
   hipEvent_t* ev = e->ev.data();
   HIPCHECK(e, hipEventRecord(ev[0], e->stream));
-  if (p.uni) launch_traj_count_uniform(p, e->stream);
+  if (p.cls) launch_traj_count_classes(p, e->stream);
+  else if (p.uni) launch_traj_count_uniform(p, e->stream);
   else launch_traj_count(p, e->stream);
   HIPCHECK(e, hipEventRecord(ev[1], e->stream));
   launch_traj_scan(p, e->stream);
@@ -349,12 +408,31 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st)
   st.process_kernel_ms += ms0;
   st.emit_kernel_ms += ms1;
   st.wave_kernel_ms += ms0 + ms1;
-  st.launches += p.uni ? 6 : 7;
-  if (e->h_ctl_pinned->flag) return 0;
+  st.launches += p.cls ? 11 : p.uni ? 6 : 7;
+  if (p.cls && getenv("ZB_DEBUG_CLS")) {  // class batch internals (debugging aid)
+    ClsPlan pl;
+    uint32_t wc[CLS_MAX];
+    (void)hipMemcpy(&pl, e->c_plan, sizeof(pl), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(wc, e->t_wcount, sizeof(wc), hipMemcpyDeviceToHost);
+    const TrajCtl& c2 = *e->h_ctl_pinned;
+    fprintf(stderr, "zb cls: flag=%u wmax=%u end=%ld nc=%u slots=%u\n", c2.flag, c2.wmax, (long)c2.end, pl.nc, pl.slots);
+    for (uint32_t c = 0; c < pl.nc && c < CLS_MAX; c++) {
+      std::vector<uint64_t> a(c2.wmax);
+      if (c2.wmax) (void)hipMemcpy(a.data(), e->t_agg + (uint64_t)c * CLS_ROW, c2.wmax * 8, hipMemcpyDeviceToHost);
+      fprintf(stderr, "  class %u key=%u n=%u base=%u rep=%u W=%u agg:", c, pl.key[c], pl.n[c], pl.base[c], pl.rep[c], wc[c]);
+      for (auto x : a) fprintf(stderr, " %lx", (unsigned long)x);
+      fprintf(stderr, "\n");
+    }
+  }
+  if (e->h_ctl_pinned->flag) {
+    // nothing but scratch counts was written: run the batch per instance (or on the wave pipeline)
+    if (p.cls && e->traj_model_ok) return run_trajectory(e, log_base, n, st, false);
+    return 0;
+  }
   e->host_hdr = e->h_hdr_pinned[0];
   int rc = check_device_errors(e, *e->h_err_pinned);
   if (rc != ZB_OK) return rc;
-  st.path = 1;
+  st.path = p.cls ? 2 : 1;
   return 1;
 }
 
@@ -473,7 +551,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->t_ctl, sizeof(TrajCtl)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_wtot, TRAJ_WAVE_CAP * sizeof(uint4)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_wbase, TRAJ_WAVE_CAP * sizeof(TrajBase)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipMalloc(&e->t_mgen, TRAJ_MAX_GENERATIONS * sizeof(MergeGen)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->t_mgen, CLS_MAX * CLS_ROW * sizeof(MergeGen)) != hipSuccess) return cleanup(ZB_ENOMEM);
   e->ev.resize(EV_PER_WAVE * WAVES_PER_SYNC);
   for (auto& x : e->ev)
     if (hipEventCreate(&x) != hipSuccess) return cleanup(ZB_EDEVICE);
@@ -494,7 +572,8 @@ void zb_engine_destroy(zb_engine* e) {
     if (x) (void)hipEventDestroy(x);
   void* ps[] = {e->log, e->links, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
                 e->merge_jobs, e->cond_jobs, e->job_counts, e->cw, e->stage, e->info, e->block_agg, e->block_off,
-                e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats};
+                e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
+                e->c_plan, e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->comm) (void)ncclCommDestroy(e->comm);
@@ -569,6 +648,21 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
   }
   // the trajectory count pass skips payload merges, so conditions must never read a merge result
   e->traj_model_ok = !(e->has_merges && e->has_splits);
+  // class batches: every split of the model is one digit (radix conditions + 2) of an 8-bit outcome key
+  e->nsplits = 0;
+  e->cls_ok = true;
+  uint32_t stride = 1;
+  for (size_t i = 0; i < e->model.elems.size() && e->cls_ok; i++) {
+    const DevElem& el = e->model.elems[i];
+    if (el.step[WI_GATEWAY_ACTIVATED] != ST_EXCLUSIVE_SPLIT) continue;
+    const uint32_t radix = (uint32_t)el.cond_count + 2;
+    if (e->nsplits == CLS_MAX_SPLITS || (uint64_t)stride * radix > 256) { e->cls_ok = false; break; }
+    e->split_elem[e->nsplits] = (uint32_t)i;
+    e->split_stride[e->nsplits] = stride;
+    e->nsplits++;
+    stride *= radix;
+  }
+  if (!e->cls_ok) e->nsplits = 0;
   return upload_model(e);
 }
 
@@ -678,7 +772,8 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   // ---- inject staged input at the log tail (engine is quiescent between steps)
   if (e->staged_pending && !e->staged.empty()) {
     // an idle partition fed only CREATE commands runs as independent trajectories (zb_traj.hip)
-    try_traj = !(e->cfg.flags & ZB_CFG_WAVE_ONLY) && max_waves == 0 && e->traj_model_ok &&
+    try_traj = !(e->cfg.flags & ZB_CFG_WAVE_ONLY) && max_waves == 0 &&
+               (e->traj_model_ok || (e->cls_ok && e->staged_uniform)) &&
                e->host_hdr.begin == e->host_hdr.end;
     traj_base = e->host_hdr.end;
     traj_n = (int64_t)e->staged.size();
@@ -726,7 +821,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   uint32_t launched = 0;
   bool quiescent = e->host_hdr.begin == e->host_hdr.end;
   if (try_traj && !quiescent) {
-    int rc = run_trajectory(e, traj_base, traj_n, st);
+    int rc = run_trajectory(e, traj_base, traj_n, st, true);
     if (rc < 0) return rc;
     quiescent = e->host_hdr.begin == e->host_hdr.end;
   }

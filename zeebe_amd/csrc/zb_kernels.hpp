@@ -198,6 +198,19 @@ void launch_inject(const InjectParams& p, hipStream_t stream);
 constexpr int TRAJ_WG = 256;  // instances per workgroup (one per thread)
 constexpr int TR = 4;         // element instances per workflow instance held in registers
 constexpr int TF = 2;         // records per workflow instance per generation
+constexpr int CLS_MAX = 8;          // trajectory classes of a class batch
+constexpr int CLS_MAX_SPLITS = 8;   // exclusive splits a class key covers
+constexpr int CLS_ROW = 4096;       // agg / mgen row of one class (>= generations of a batch)
+
+// Class batch (zb_traj.hip): dense classes of the outcome keys present in the batch.
+struct ClsPlan {
+  uint32_t nc, slots;       // classes; emit slots (every class segment padded to a multiple of 64)
+  uint32_t key[CLS_MAX];    // outcome key of class c
+  uint32_t n[CLS_MAX];      // instances of class c
+  uint32_t base[CLS_MAX];   // first emit slot of class c
+  uint32_t rep[CLS_MAX];    // representative (first) instance of class c
+  uint8_t cid[256];         // key -> class (0xff: absent)
+};
 
 struct TrajCtl {
   uint32_t flag;       // != 0: the count pass met something this path does not do -> wave path
@@ -236,7 +249,8 @@ struct TrajParams {
   const uint8_t* pool;
   int64_t log_base, n;   // the batch: CREATE commands at [log_base, log_base + n)
   int64_t wf_start, job_start;
-  int32_t cond, pad0;    // the model has exclusive splits (condition VM compiled into the kernels)
+  int32_t cond;          // the model has exclusive splits (condition VM compiled into the kernels)
+  int32_t cls;           // class batch (uniform process, exclusive splits on CREATE payloads): see ClsPlan
   int64_t uni;           // > 0: uniform batch of `uni` instances whose trajectories are data-independent;
                          // agg[w] holds one instance's counts (count pass over instance 0 only)
   int32_t nwg, wcap;     // workgroups, generations the count buffers hold
@@ -253,11 +267,24 @@ struct TrajParams {
   MergeGen* mgen;        // [wcap] uniform batch: per-generation merge slots (written by the count pass)
   uint64_t* wstats;      // [nwg][6] emit-pass statistics per workgroup (reduced by k_traj_commit)
   uint32_t max_create;   // longest CREATE payload of the batch (merge result bounds)
-  uint32_t pad2;
+  int32_t nwg_e;         // emit-pass workgroups (class batch: class segments are padded)
+  // class batch: the model's exclusive splits (element, key stride, radix = conditions + 2)
+  int32_t nsplits, pad3;
+  uint32_t split_elem[CLS_MAX_SPLITS], split_stride[CLS_MAX_SPLITS];
+  ClsPlan* plan;
+  uint8_t* ikey;         // [n] outcome key of every instance
+  uint32_t* khist;       // [256] instances per key
+  uint32_t* krep;        // [256] first instance per key
+  uint64_t* cmask;       // [n / 64][CLS_MAX] per 64-instance group: ballot of the instances of class c
+  uint32_t* woffw;       // [n / 64][CLS_MAX] instances of class c before the group
+  uint32_t* wgcnt;       // [CLS_MAX][nwg] instances of class c in workgroup b
+  uint32_t* wgoff;       // [CLS_MAX][nwg] exclusive prefix of wgcnt over workgroups
+  uint32_t* perm;        // [slots] emit slot -> instance
 };
 
 void launch_traj_count(const TrajParams& p, hipStream_t stream);
 void launch_traj_count_uniform(const TrajParams& p, hipStream_t stream);
+void launch_traj_count_classes(const TrajParams& p, hipStream_t stream);
 void launch_traj_scan(const TrajParams& p, hipStream_t stream);
 void launch_traj_emit(const TrajParams& p, hipStream_t stream);
 

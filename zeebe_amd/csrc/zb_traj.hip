@@ -111,6 +111,27 @@ constexpr int FM_WORDS = 12;                  // 48-byte blob slots: documents o
 constexpr int FM_BYTES = FM_WORDS * 4;
 constexpr int FM_STRIDE = 3 * FM_WORDS + 1;   // odd stride: lanes at the same offset hit distinct banks
 
+// Condition documents are staged into the same per-thread LDS slot before the json-el VM runs: the
+// VM reads its document token by token (dependent byte loads), which from HBM costs a memory
+// latency per token; the staging copy issues all of its 8-byte loads back to back instead.
+constexpr int CD_BYTES = (FM_STRIDE - 1) * 4;  // [u32 len][document] of documents <= 140 bytes
+__device__ __forceinline__ const uint8_t* stage_doc(const uint8_t* pp, uint32_t len, uint32_t* slot) {
+  if (slot == nullptr || len + 4 > (uint32_t)CD_BYTES) return pp + 4;
+  const uint2* g = (const uint2*)pp;  // arena blobs are 8-aligned and padded to 8 bytes
+  const uint32_t n8 = (len + 4 + 7) / 8;
+#pragma unroll 1
+  for (uint32_t c = 0; c < n8; c += 8) {
+    uint2 v[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++)
+      if (c + k < n8) v[k] = g[c + k];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++)
+      if (c + k < n8) { slot[2 * (c + k)] = v[k].x; slot[2 * (c + k) + 1] = v[k].y; }
+  }
+  return (const uint8_t*)slot + 4;
+}
+
 // Keys inside a trajectory are 32-bit ordinals of the partition's generators within the batch:
 // wf key = wf_start + 5 * ordinal, job key = job_start + 5 * ordinal (every key a batch record
 // carries is created by the batch); NOK stands for the null key -1.
@@ -160,6 +181,7 @@ struct Inst {
   i32x4 rnch;
   uint32_t used, to_free;
   uint32_t inst_key;
+  uint32_t ckey, crow;  // class batch: outcome key of the instance's class, its agg / mgen row
   Gen cur, nx;
   int nc, nn, nwf, njob;
   // this generation's payload work: one merge and one incident detail at most
@@ -224,13 +246,12 @@ __device__ __forceinline__ uint32_t arena_len(const uint8_t* arena, uint32_t ref
 // symbolic payload refs of a trace (literal refs are static blobs below 2^28)
 constexpr uint32_t PAY_MERGE = 0x80000000u;   // | generation: that generation's merge result
 constexpr uint32_t PAY_CREATE = 0xC0000000u;  // the instance's CREATE payload
-__device__ __forceinline__ uint32_t sym_bound(const TrajParams& P, uint32_t sym);
 __device__ __forceinline__ uint32_t tblob_bytes(uint32_t len) { return (4 + len + 7) & ~7u; }
 
 // upper bound of the length of the document behind a symbolic payload ref (trace count pass)
-__device__ __forceinline__ uint32_t sym_bound(const TrajParams& P, uint32_t sym) {
+__device__ __forceinline__ uint32_t sym_bound(const TrajParams& P, uint32_t sym, uint32_t row) {
   if (sym == PAY_CREATE) return P.max_create;
-  if (sym & PAY_MERGE) return P.mgen[sym & 0xffff].stride - 4;
+  if (sym & PAY_MERGE) return P.mgen[row + (sym & 0xffff)].stride - 4;
   return arena_len(P.arena, sym);
 }
 
@@ -253,7 +274,7 @@ __device__ __forceinline__ void t_incident(Inst& I, const TRec& rec, int64_t pos
 // bpmn_step (zb_wave.hip) on local rows: BpmnStepProcessor.java:92-251 guards + step handlers.
 // COND: exclusive splits are evaluated here (else they send the batch to the wave pipeline).
 template <bool EMIT, bool COND>
-__device__ __forceinline__ void t_step(const TrajParams& P, Inst& I, const TRec& rec, int64_t pos) {
+__device__ __forceinline__ void t_step(const TrajParams& P, Inst& I, const TRec& rec, int64_t pos, uint32_t* slot) {
   // (rec's control fields are wave-uniform in a uniform batch: t_record scalarized them)
   const uint8_t intent = rec.intent;
   const bool stateless = intent == WI_SEQUENCE_FLOW_TAKEN || intent == WI_START_EVENT_OCCURRED ||
@@ -317,17 +338,38 @@ __device__ __forceinline__ void t_step(const TrajParams& P, Inst& I, const TRec&
     }
     case ST_EXCLUSIVE_SPLIT: {  // ExclusiveSplitHandler :38-71 (first true condition, else default)
       if constexpr (!COND) {
-        I.err |= TE_FALLBACK;
-        return;
+        // class batch: the outcome is a digit of the class key (k_cls_classify evaluated this split's
+        // conditions on the CREATE payload, which is the scope payload here: no merge precedes a split)
+        uint32_t o = 0xffffffffu;
+        const uint32_t cc = el.cond_count();
+        // (a class batch's count pass is its trace, with symbolic payloads: it checks that the split reads
+        // the CREATE payload, since k_cls_classify never saw a merge result)
+        if (P.cls && (EMIT || rec.payload == PAY_CREATE))
+          for (int k = 0; k < P.nsplits; k++)
+            if (P.split_elem[k] == rec.elem) o = (I.ckey / P.split_stride[k]) % (cc + 2);
+        uint16_t chosen = NO_ELEM;
+        if (o < cc) chosen = K(P.cond_flows)[el.cond_begin() + o];
+        else if (o == cc) chosen = el.dflt();
+        // errors and missing defaults raise incidents: those batches take the per-instance path
+        if (chosen == NO_ELEM) { I.err |= TE_FALLBACK; return; }
+        if (EMIT) I.cond_bytes += arena_len(P.arena, rec.payload);
+        s.elem = chosen;
+        s.intent = WI_SEQUENCE_FLOW_TAKEN;
+        s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
+        s.flags = TK_WF; s.ord = (uint8_t)I.nwf++;
+        s.rself = LN;
+        I.push(s);
+        break;
       } else {
         const uint8_t* pp = P.arena + (uint64_t)rec.payload * 8;
         const uint32_t len = *(const uint32_t*)pp;
+        const uint8_t* doc = stage_doc(pp, len, slot);
         uint16_t chosen = NO_ELEM;
         CondOut co{0, 0, 0, 0};
         bool unsup = false;
         for (uint32_t c = 0; c < el.cond_count(); c++) {
           const uint16_t flow = K(P.cond_flows)[el.cond_begin() + c];
-          const bool res = eval_condition(K(P.elems)[flow].cond_prog, P.code, pp + 4, len, P.consts, P.queries,
+          const bool res = eval_condition(K(P.elems)[flow].cond_prog, P.code, doc, len, P.consts, P.queries,
                                           P.filters, P.pool, co, unsup);
           if (unsup || co.err) break;
           if (res) { chosen = flow; break; }
@@ -418,7 +460,8 @@ __device__ __forceinline__ void t_step(const TrajParams& P, Inst& I, const TRec&
 
 // process_record (zb_wave.hip) on local rows
 template <bool EMIT, bool COND, bool UNI>
-__device__ __forceinline__ void t_record(const TrajParams& P, Inst& I, const TRec& rec_in, int64_t pos) {
+__device__ __forceinline__ void t_record(const TrajParams& P, Inst& I, const TRec& rec_in, int64_t pos,
+                                         uint32_t* slot) {
   TRec rec = rec_in;
   if (UNI) {  // control fields are the same in every lane: keep them in SGPRs (scalar branches, s_load)
     rec.elem = (uint16_t)__builtin_amdgcn_readfirstlane(rec.elem);
@@ -467,7 +510,7 @@ __device__ __forceinline__ void t_record(const TrajParams& P, Inst& I, const TRe
         I.rnch[r] = 0;
         I.created += 1;
       } else if (rec.intent <= WI_ELEMENT_TERMINATED && rec.intent >= WI_START_EVENT_OCCURRED) {
-        t_step<EMIT, COND>(P, I, rec, pos);
+        t_step<EMIT, COND>(P, I, rec, pos, slot);
       }
     }
   } else if (vt == ZB_VT_JOB) {
@@ -556,16 +599,48 @@ __device__ __forceinline__ uint64_t wave_scan(uint64_t v) {
 // TRACE (count pass of a uniform batch, one instance): payload refs are symbolic (PAY_CREATE, PAY_MERGE | w,
 // literal refs) so that each generation's merge gets a result bound valid for every instance of the
 // batch (MergeGen); the emit pass then places instance i's result at mbase(w) + i * stride(w).
-template <bool EMIT, bool UNI, bool COND, bool GEN, bool TRACE>
+// CLS (class batch, with UNI in the emit pass and with TRACE in the count pass): TRACE lane c traces the
+// representative of class c; emit slot s belongs to the class segment holding it, its instance is perm[s],
+// and its positions / keys / merge slots are linear in before_c(i) (instances of class c before it).
+template <bool EMIT, bool UNI, bool COND, bool GEN, bool TRACE, bool CLS>
 __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
   __shared__ uint64_t s_scan[TWG / 64][2];
   __shared__ uint64_t s_abase;
-  __shared__ uint32_t s_merge[EMIT ? TWG * FM_STRIDE : 1];
+  __shared__ uint32_t s_merge[(EMIT || COND) ? TWG * FM_STRIDE : 1];
+  uint32_t* const slot = COND ? s_merge + threadIdx.x * FM_STRIDE : nullptr;  // condition documents
   TrajCtl* ctl = P.ctl;
   if (EMIT && ctl->flag) return;
   if (EMIT && GEN && !ctl->regen) return;
-  const int64_t inst = (int64_t)blockIdx.x * TWG + threadIdx.x;
   const int nwg = gridDim.x;
+  int64_t inst = (int64_t)blockIdx.x * TWG + threadIdx.x;
+  // lanes past the batch follow lane 0's control in a uniform batch: they must not write anything
+  bool active = inst < P.n;
+  uint32_t cls = 0, ncls = 1;
+  uint32_t before[CLS_MAX];  // class batch emit: instances of each class before this one
+  if (CLS) {
+    const ClsPlan* pl = P.plan;
+    ncls = __builtin_amdgcn_readfirstlane(pl->nc);
+    if (TRACE) {
+      cls = threadIdx.x;
+      active = cls < ncls;
+      inst = active ? pl->rep[cls] : 0;
+    } else {
+      const uint32_t sl = (uint32_t)inst;
+      bool found = false;
+      for (uint32_t c = 0; c < ncls; c++) {
+        const uint32_t b = pl->base[c];
+        if (sl >= b && sl < b + ((pl->n[c] + 63) & ~63u)) { cls = c; found = true; }
+      }
+      cls = __builtin_amdgcn_readfirstlane(cls);  // class segments are whole waves
+      active = found && sl - pl->base[cls] < pl->n[cls];
+      inst = P.perm[active ? sl : pl->base[cls]];
+      const uint64_t grp = (uint64_t)(inst >> 6) * CLS_MAX;
+      const uint64_t lt = (1ull << (inst & 63)) - 1;
+#pragma unroll
+      for (int c = 0; c < CLS_MAX; c++)
+        before[c] = c < (int)ncls ? P.woffw[grp + c] + (uint32_t)__builtin_popcountll(P.cmask[grp + c] & lt) : 0;
+    }
+  }
 
   Inst I;
   I.used = 0; I.to_free = 0;
@@ -579,10 +654,10 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
   I.err = 0;
   I.transitions = I.completed = I.created = I.merges = I.cond_bytes = 0;
   I.merge_bytes = 0;
-  // lanes past the batch follow lane 0's control in a uniform batch: they must not write anything
-  const bool active = inst < P.n;
+  I.ckey = CLS ? P.plan->key[cls & (CLS_MAX - 1)] : 0;
+  I.crow = CLS ? cls * CLS_ROW : 0;
   int64_t fpos = P.log_base + inst;  // log position of the first record of the current generation
-  if (inst < P.n) {
+  if ((CLS && TRACE) ? active : inst < P.n) {
     const zb_rec d = P.log[fpos];
     TRec r;
     r.key = NOK; r.scope_key = NOK; r.payload = TRACE ? PAY_CREATE : d.payload; r.elem = d.elem;  // a CREATE
@@ -593,7 +668,8 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
   }
 
   int w = 0;
-  const int W = UNI ? (int)P.wcount[0] : 0;
+  const int W = UNI ? (int)P.wcount[cls] : 0;
+  int wl = 0;  // generations in which this instance had records (trace)
   while (UNI ? (w < W) : __syncthreads_or(I.nc > 0)) {
     if (!UNI && w >= P.wcap) {  // more generations than the count buffers hold
       if (!EMIT && threadIdx.x == 0) atomicOr(&ctl->flag, TE_FALLBACK);
@@ -617,18 +693,48 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
       I.nc = __builtin_amdgcn_readfirstlane(I.nc);
       I.used = __builtin_amdgcn_readfirstlane(I.used);
     }
+    if (I.nc > 0) wl = w + 1;
     // ---- process this generation (log order inside the instance)
 #pragma unroll 1
-    for (int k = 0; k < I.nc; k++) t_record<EMIT, COND, UNI>(P, I, I.cur.get(k), fpos + k);
+    for (int k = 0; k < I.nc; k++) t_record<EMIT, COND, UNI>(P, I, I.cur.get(k), fpos + k, slot);
     // ---- place the follow-ups
     uint64_t a = (uint64_t)I.nn | ((uint64_t)I.nwf << 16) | ((uint64_t)I.njob << 32);
     uint64_t bytes = 0;
     if (EMIT && active) bytes = (I.merge ? tblob_bytes(I.m_len) : 0) + (I.detail ? 24 : 0);
+    const uint64_t a_own = a;  // (block_scan2 turns a into the exclusive prefix)
     uint64_t ta = 0, tb = 0;
     if (!UNI) block_scan2(a, bytes, ta, tb, s_scan);
     int64_t pos0;
     uint32_t kwf, kjob;  // key ordinals of this instance's first new wf / job key
-    if (UNI) {
+    if (UNI && CLS) {
+      // class batch: linear in the per-class counts of the instances before this one
+      const TrajBase wb = kload(P.wbase, (uint64_t)w);
+      int64_t po = 0, pw = 0, pj = 0;
+#pragma unroll
+      for (int c = 0; c < CLS_MAX; c++) {
+        if (c >= (int)ncls) break;
+        const uint64_t n = kload(P.agg, (uint64_t)c * CLS_ROW + w);
+        po += (int64_t)before[c] * (int64_t)(n & 0xffff);
+        pw += (int64_t)before[c] * (int64_t)((n >> 16) & 0xffff);
+        pj += (int64_t)before[c] * (int64_t)(n >> 32);
+      }
+      pos0 = wb.pos + po;
+      kwf = (uint32_t)(wb.wf + pw);
+      kjob = (uint32_t)(wb.job + pj);
+      if (EMIT && I.merge) {
+        int64_t pm = 0;
+#pragma unroll
+        for (int c = 0; c < CLS_MAX; c++) {
+          if (c >= (int)ncls) break;
+          const MergeGen g = kload(P.mgen, (uint64_t)c * CLS_ROW + w);
+          if (g.has) pm += (int64_t)before[c] * (int64_t)g.stride;
+        }
+        const MergeGen g = kload(P.mgen, (uint64_t)I.crow + w);
+        tb = (uint64_t)(wb.mbase + pm);
+        bytes = 0;
+        if (!g.has || tblob_bytes(I.m_len) > g.stride) { I.err |= DE_UNSUPPORTED; tb = P.arena_cap; }
+      }
+    } else if (UNI) {
       // positions and keys are affine in the instance index; the arena is allocated per wave
       const uint64_t c = kload(P.agg, (uint64_t)w);
       const TrajBase wb = kload(P.wbase, (uint64_t)w);
@@ -643,7 +749,11 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
         if (!g.has || tblob_bytes(I.m_len) > g.stride) { I.err |= DE_UNSUPPORTED; tb = P.arena_cap; }
       }
     } else if (!EMIT) {
-      if (threadIdx.x == 0) P.agg[(uint64_t)w * nwg + blockIdx.x] = ta;
+      if (TRACE) {  // one traced instance per lane (lane = class): its own counts
+        if (active) P.agg[(uint64_t)I.crow + w] = a_own;
+      } else if (threadIdx.x == 0) {
+        P.agg[(uint64_t)w * nwg + blockIdx.x] = ta;
+      }
       pos0 = 0;
       kwf = (uint32_t)((a >> 16) & 0xffff);  // placeholder ordinals: nothing in the count depends on key values
       kjob = (uint32_t)(a >> 32);
@@ -659,16 +769,16 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
       }
     }
     uint32_t merged_ref = 0, detail_ref = 0;
-    if (TRACE && inst == 0) {
+    if (TRACE && active) {
       MergeGen g{0, 0, 0, 0};
       if (I.merge) {
         g.src = I.m_src; g.tgt = I.m_tgt; g.has = 1;
-        const uint32_t bound = sym_bound(P, I.m_src) + sym_bound(P, I.m_tgt) + 8;  // emit reserves |s| + |t| + 8
+        const uint32_t bound = sym_bound(P, I.m_src, I.crow) + sym_bound(P, I.m_tgt, I.crow) + 8;  // emit reserves |s| + |t| + 8
         g.stride = tblob_bytes(bound);
         merged_ref = PAY_MERGE | (uint32_t)w;
         I.merges += 1;
       }
-      P.mgen[w] = g;
+      P.mgen[I.crow + w] = g;
     }
     if (EMIT && active && (I.merge || I.detail)) {
       uint64_t at = (UNI ? tb : s_abase) + bytes;
@@ -774,7 +884,10 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
   }
 
   if (!EMIT) {
-    if (threadIdx.x == 0) {
+    if (TRACE) {
+      if (active) P.wcount[cls] = (uint32_t)wl;
+      if (threadIdx.x == 0) atomicMax(&ctl->wmax, (uint32_t)w);
+    } else if (threadIdx.x == 0) {
       P.wcount[blockIdx.x] = (uint32_t)w;
       atomicMax(&ctl->wmax, (uint32_t)w);
     }
@@ -889,21 +1002,22 @@ __global__ void __launch_bounds__(1024) k_traj_base(TrajParams P) {
   if (ctl->flag) return;
   const uint32_t W = ctl->wmax;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const bool uni = P.uni != 0;
+  const bool uni = P.uni != 0 || P.cls != 0;  // per-class counts (one class: uniform batch)
+  const uint32_t ncls = P.cls ? P.plan->nc : 1;
   if (threadIdx.x < 4) s_carry[threadIdx.x] = 0;
   __syncthreads();
   for (uint32_t base = 0; base < W; base += 1024) {
     const uint32_t w = base + threadIdx.x;
     uint64_t x[4] = {0, 0, 0, 0};
     if (w < W) {
-      if (uni) {  // merge slots of the generation: stride x instances
-        const MergeGen g = P.mgen[w];
-        if (g.has) x[3] = (uint64_t)g.stride * (uint64_t)P.uni;
-      }
-      if (P.uni) {
-        const uint64_t c = P.agg[w];
-        x[0] = (c & 0xffff) * (uint64_t)P.uni; x[1] = ((c >> 16) & 0xffff) * (uint64_t)P.uni;
-        x[2] = (c >> 32) * (uint64_t)P.uni;
+      if (uni) {  // generation totals: class counts x class sizes; merge slots: stride x class size
+        for (uint32_t c = 0; c < ncls; c++) {
+          const uint64_t m = P.cls ? (uint64_t)P.plan->n[c] : (uint64_t)P.uni;
+          const MergeGen g = P.mgen[(uint64_t)c * CLS_ROW + w];
+          if (g.has) x[3] += (uint64_t)g.stride * m;
+          const uint64_t a = P.agg[(uint64_t)c * CLS_ROW + w];
+          x[0] += (a & 0xffff) * m; x[1] += ((a >> 16) & 0xffff) * m; x[2] += (a >> 32) * m;
+        }
       } else {
         const uint4 t = P.wtot[w];
         x[0] = t.x; x[1] = t.y; x[2] = t.z;
@@ -956,7 +1070,7 @@ __global__ void __launch_bounds__(1024) k_traj_base(TrajParams P) {
 __global__ void k_traj_regen(TrajParams P) {
   TrajCtl* ctl = P.ctl;
   if (ctl->flag || !ctl->regen) return;
-  if (!P.uni) ctl->arena_next = ctl->arena_start;  // (uniform batch: merge slots fixed by k_traj_base)
+  if (!P.uni && !P.cls) ctl->arena_next = ctl->arena_start;  // (uniform batch: merge slots fixed by k_traj_base)
   ctl->rows_next = ctl->rows_start;
   ctl->derr = 0;
 }
@@ -966,7 +1080,7 @@ __global__ void __launch_bounds__(256) k_traj_commit(TrajParams P) {
   const TrajCtl* ctl = P.ctl;
   if (ctl->flag) return;
   uint64_t st[6] = {0, 0, 0, 0, 0, 0};
-  for (int b = threadIdx.x; b < P.nwg; b += blockDim.x)
+  for (int b = threadIdx.x; b < P.nwg_e; b += blockDim.x)
 #pragma unroll
     for (int f = 0; f < 6; f++) st[f] += P.wstats[(uint64_t)b * 6 + f];
 #pragma unroll
@@ -991,37 +1105,215 @@ __global__ void __launch_bounds__(256) k_traj_commit(TrajParams P) {
   if ((uint64_t)ctl->arena_next > P.arena_cap) atomicOr(P.err, (uint32_t)DE_ARENA_FULL);
 }
 
+// ------------------------------------------------------------------------------ class batches
+// A batch whose CREATEs all address one process, in a model whose exclusive splits never read a merge
+// result (zb_engine: traj_model_ok), evaluates every condition on the instance's CREATE payload, so
+// the outcome of every split is fixed when the instance is created. The outcome key is the mixed-radix
+// vector of the outcomes of all the model's splits (digit: index of the first true condition,
+// cond_count = none -> default flow, cond_count + 1 = evaluation error); instances with equal keys
+// follow the same trajectory. Each class runs like a uniform batch: one traced representative, emit
+// waves holding a single class (scalar control), and positions, keys and merge slots linear in
+// before_c(i), the number of class-c instances that precede instance i.
+//   k_cls_classify  key of every instance (conditions on an LDS copy of the CREATE payload), key histogram
+//   k_cls_plan      dense classes of the keys present (more than CLS_MAX: per-instance path)
+//   k_cls_masks     per 64-instance group and class: ballot; per workgroup and class: count
+//   k_cls_scan      per class: exclusive prefix of the workgroup counts
+//   k_cls_perm      per group and class: instances before the group; emit slot -> instance
+//   k_traj<TRACE, CLS> one lane per class: per-generation counts and merge bounds of its representative
+__global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
+  __shared__ uint32_t s_doc[TWG * FM_STRIDE];
+  __shared__ uint32_t s_hist[256], s_rep[256];
+  const int t = threadIdx.x;
+  s_hist[t] = 0;
+  s_rep[t] = 0xffffffffu;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * TWG + t;
+  if (i < P.n) {
+    const uint32_t ref = P.log[P.log_base + i].payload;
+    const uint8_t* pp = P.arena + (uint64_t)ref * 8;
+    const uint32_t len = *(const uint32_t*)pp;
+    const uint8_t* doc = stage_doc(pp, len, s_doc + t * FM_STRIDE);
+    uint32_t key = 0;
+    for (int k = 0; k < P.nsplits; k++) {
+      const ElemCtl el = elem_ctl(P, P.split_elem[k]);
+      const uint32_t cc = el.cond_count();
+      uint32_t o = cc;
+      for (uint32_t c = 0; c < cc; c++) {
+        CondOut co{0, 0, 0, 0};
+        bool unsup = false;
+        const uint16_t flow = K(P.cond_flows)[el.cond_begin() + c];
+        const bool res = eval_condition(K(P.elems)[flow].cond_prog, P.code, doc, len, P.consts, P.queries,
+                                        P.filters, P.pool, co, unsup);
+        if (unsup || co.err) { o = cc + 1; break; }
+        if (res) { o = c; break; }
+      }
+      key += o * P.split_stride[k];
+    }
+    P.ikey[i] = (uint8_t)key;
+    atomicAdd(&s_hist[key & 255], 1u);
+    atomicMin(&s_rep[key & 255], (uint32_t)i);
+  }
+  __syncthreads();
+  if (s_hist[t]) {
+    atomicAdd(&P.khist[t], s_hist[t]);
+    atomicMin(&P.krep[t], s_rep[t]);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_cls_plan(TrajParams P) {
+  __shared__ uint32_t s_w[4];
+  ClsPlan* pl = P.plan;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t cnt = P.khist[t];
+  const uint64_t m = __ballot(cnt > 0);
+  if (lane == 0) s_w[wv] = (uint32_t)__builtin_popcountll(m);
+  __syncthreads();
+  uint32_t cid = (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1));
+  for (int k = 0; k < wv; k++) cid += s_w[k];
+  const uint32_t nc = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+  pl->cid[t] = (cnt > 0 && cid < CLS_MAX) ? (uint8_t)cid : 0xff;
+  if (cnt > 0 && cid < CLS_MAX) {
+    pl->key[cid] = (uint32_t)t;
+    pl->n[cid] = cnt;
+    pl->rep[cid] = P.krep[t];
+  }
+  __syncthreads();
+  if (t == 0) {
+    if (nc == 0 || nc > CLS_MAX) {
+      atomicOr(&P.ctl->flag, TE_FALLBACK);
+      pl->nc = 0;
+      return;
+    }
+    uint32_t b = 0;
+    for (uint32_t c = 0; c < nc; c++) {
+      pl->base[c] = b;
+      b += (pl->n[c] + 63) & ~63u;
+    }
+    pl->nc = nc;
+    pl->slots = b;
+  }
+}
+
+__global__ void __launch_bounds__(TWG) k_cls_masks(TrajParams P) {
+  __shared__ uint32_t s_cnt[TWG / 64][CLS_MAX];
+  if (P.ctl->flag) return;
+  const ClsPlan* pl = P.plan;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t nc = __builtin_amdgcn_readfirstlane(pl->nc);
+  const int64_t i = (int64_t)blockIdx.x * TWG + t;
+  const uint32_t c = i < P.n ? pl->cid[P.ikey[i]] : 0xffu;
+  const uint64_t grp = ((uint64_t)blockIdx.x * (TWG / 64) + wv) * CLS_MAX;
+  for (uint32_t k = 0; k < nc; k++) {
+    const uint64_t m = __ballot(c == k);
+    if (lane == 0) {
+      P.cmask[grp + k] = m;
+      s_cnt[wv][k] = (uint32_t)__builtin_popcountll(m);
+    }
+  }
+  __syncthreads();
+  if ((uint32_t)t < nc) {
+    uint32_t sum = 0;
+    for (int v = 0; v < TWG / 64; v++) sum += s_cnt[v][t];
+    P.wgcnt[(uint64_t)t * P.nwg + blockIdx.x] = sum;
+  }
+}
+
+// one workgroup per class: exclusive prefix over workgroups of wgcnt[c][.]
+__global__ void __launch_bounds__(1024) k_cls_scan(TrajParams P) {
+  __shared__ uint32_t s_w[16];
+  const uint32_t c = blockIdx.x;
+  if (P.ctl->flag || c >= P.plan->nc) return;
+  const int nwg = P.nwg;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t carry = 0;
+  const uint32_t* in = P.wgcnt + (uint64_t)c * nwg;
+  uint32_t* out = P.wgoff + (uint64_t)c * nwg;
+  for (int base = 0; base < nwg; base += 1024) {
+    const int b = base + threadIdx.x;
+    const uint32_t x = b < nwg ? in[b] : 0;
+    uint32_t y = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t u = __shfl_up(y, d, 64);
+      if (lane >= d) y += u;
+    }
+    if (lane == 63) s_w[wv] = y;
+    __syncthreads();
+    uint32_t ex = y - x + carry, tot = 0;
+    for (int k = 0; k < 16; k++) {
+      if (k < wv) ex += s_w[k];
+      tot += s_w[k];
+    }
+    if (b < nwg) out[b] = ex;
+    carry += tot;
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(TWG) k_cls_perm(TrajParams P) {
+  if (P.ctl->flag) return;
+  const ClsPlan* pl = P.plan;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t nc = __builtin_amdgcn_readfirstlane(pl->nc);
+  const uint64_t grp0 = (uint64_t)blockIdx.x * (TWG / 64) * CLS_MAX;
+  const uint64_t grp = grp0 + (uint64_t)wv * CLS_MAX;
+  const int64_t i = (int64_t)blockIdx.x * TWG + t;
+  const uint32_t c = i < P.n ? pl->cid[P.ikey[i]] : 0xffu;
+  uint32_t mine = 0;
+  for (uint32_t k = 0; k < nc; k++) {
+    uint32_t off = P.wgoff[(uint64_t)k * P.nwg + blockIdx.x];
+    for (int v = 0; v < wv; v++) off += (uint32_t)__builtin_popcountll(P.cmask[grp0 + (uint64_t)v * CLS_MAX + k]);
+    if (lane == 0) P.woffw[grp + k] = off;
+    if (k == c) mine = off + (uint32_t)__builtin_popcountll(P.cmask[grp + k] & ((1ull << lane) - 1));
+  }
+  if (c < nc) P.perm[pl->base[c] + mine] = (uint32_t)i;
+}
+
 // conditions are compiled into the count / emit kernels only when the model has exclusive splits
 // (a uniform batch never has any), keeping the condition VM's call frame out of the other variants
 void launch_traj_count(const TrajParams& p, hipStream_t s) {
-  if (p.cond) hipLaunchKernelGGL((k_traj<false, false, true, false, false>), dim3(p.nwg), dim3(TWG), 0, s, p);
-  else hipLaunchKernelGGL((k_traj<false, false, false, false, false>), dim3(p.nwg), dim3(TWG), 0, s, p);
+  if (p.cond) hipLaunchKernelGGL((k_traj<false, false, true, false, false, false>), dim3(p.nwg), dim3(TWG), 0, s, p);
+  else hipLaunchKernelGGL((k_traj<false, false, false, false, false, false>), dim3(p.nwg), dim3(TWG), 0, s, p);
 }
 // uniform batch: count one representative instance (the first CREATE), one workgroup
 void launch_traj_count_uniform(const TrajParams& p, hipStream_t s) {
   TrajParams q = p;
   q.n = 1;
   q.nwg = 1;
-  hipLaunchKernelGGL((k_traj<false, false, false, false, true>), dim3(1), dim3(TWG), 0, s, q);
+  hipLaunchKernelGGL((k_traj<false, false, false, false, true, false>), dim3(1), dim3(TWG), 0, s, q);
+}
+// class batch: classify, plan, group masks, offsets, emit permutation, one traced representative per class
+void launch_traj_count_classes(const TrajParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_cls_classify, dim3(p.nwg), dim3(TWG), 0, s, p);
+  hipLaunchKernelGGL(k_cls_plan, dim3(1), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(k_cls_masks, dim3(p.nwg), dim3(TWG), 0, s, p);
+  hipLaunchKernelGGL(k_cls_scan, dim3(CLS_MAX), dim3(1024), 0, s, p);
+  hipLaunchKernelGGL(k_cls_perm, dim3(p.nwg), dim3(TWG), 0, s, p);
+  hipLaunchKernelGGL((k_traj<false, false, false, false, true, true>), dim3(1), dim3(TWG), 0, s, p);
 }
 void launch_traj_scan(const TrajParams& p, hipStream_t s) {
-  if (!p.uni) hipLaunchKernelGGL(k_traj_scan, dim3(p.wcap), dim3(1024), 0, s, p);
+  if (!p.uni && !p.cls) hipLaunchKernelGGL(k_traj_scan, dim3(p.wcap), dim3(1024), 0, s, p);
   hipLaunchKernelGGL(k_traj_base, dim3(1), dim3(1024), 0, s, p);
 }
 void launch_traj_emit(const TrajParams& p, hipStream_t s) {
   const dim3 g(p.nwg), b(TWG);
-  if (p.uni) {
-    hipLaunchKernelGGL((k_traj<true, true, false, false, false>), g, b, 0, s, p);
+  if (p.cls) {
+    const dim3 ge(p.nwg_e);
+    hipLaunchKernelGGL((k_traj<true, true, false, false, false, true>), ge, b, 0, s, p);
     hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
-    hipLaunchKernelGGL((k_traj<true, true, false, true, false>), g, b, 0, s, p);
+    hipLaunchKernelGGL((k_traj<true, true, false, true, false, true>), ge, b, 0, s, p);
+  } else if (p.uni) {
+    hipLaunchKernelGGL((k_traj<true, true, false, false, false, false>), g, b, 0, s, p);
+    hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
+    hipLaunchKernelGGL((k_traj<true, true, false, true, false, false>), g, b, 0, s, p);
   } else if (p.cond) {
-    hipLaunchKernelGGL((k_traj<true, false, true, false, false>), g, b, 0, s, p);
+    hipLaunchKernelGGL((k_traj<true, false, true, false, false, false>), g, b, 0, s, p);
     hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
-    hipLaunchKernelGGL((k_traj<true, false, true, true, false>), g, b, 0, s, p);
+    hipLaunchKernelGGL((k_traj<true, false, true, true, false, false>), g, b, 0, s, p);
   } else {
-    hipLaunchKernelGGL((k_traj<true, false, false, false, false>), g, b, 0, s, p);
+    hipLaunchKernelGGL((k_traj<true, false, false, false, false, false>), g, b, 0, s, p);
     hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
-    hipLaunchKernelGGL((k_traj<true, false, false, true, false>), g, b, 0, s, p);
+    hipLaunchKernelGGL((k_traj<true, false, false, true, false, false>), g, b, 0, s, p);
   }
   hipLaunchKernelGGL(k_traj_commit, dim3(1), dim3(256), 0, s, p);
 }
