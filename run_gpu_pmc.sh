@@ -10,6 +10,6 @@ IFS=';' read -ra SETS <<< "${PMC_SETS:-FETCH_SIZE;WRITE_SIZE}"
 i=0
 for s in "${SETS[@]}"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $s --kernel-trace -d gpurun_out/pmc/p$i -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --instances $INST --no-cpu-baseline > gpurun_out/pmc/p$i.json 2> gpurun_out/pmc/p$i.err || { echo "pmc pass $i ($s) failed rc=$?"; tail -5 gpurun_out/pmc/p$i.err; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $s --kernel-trace -d gpurun_out/pmc/p$i -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --instances $INST --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/pmc/p$i.json 2> gpurun_out/pmc/p$i.err || { echo "pmc pass $i ($s) failed rc=$?"; tail -5 gpurun_out/pmc/p$i.err; exit 1; }
   echo "pass $i done: $s"
 done

@@ -146,7 +146,10 @@ struct zb_engine {
   ClsPlan* c_plan = nullptr;
   uint64_t cls_cap = 0;           // instances the class buffers hold
   uint8_t* c_ikey = nullptr;
-  uint32_t *c_khist = nullptr, *c_krep = nullptr;  // [256] each (one allocation)
+  uint32_t *c_khist = nullptr, *c_krep = nullptr;  // [256] each (one allocation with c_klen)
+  uint64_t* c_klen = nullptr;                       // [256]
+  TmplRec* t_tmpl = nullptr;     // [CLS_MAX][CLS_ROW][TF] traced records (uniform / class batches)
+  uint32_t* t_cstat = nullptr;   // [CLS_MAX][TSTAT]
   uint64_t* c_mask = nullptr;
   uint32_t *c_woffw = nullptr, *c_wgcnt = nullptr, *c_wgoff = nullptr, *c_perm = nullptr;
 
@@ -279,13 +282,14 @@ int grow_class_buffers(zb_engine* e, uint64_t n, uint64_t nwg) {
   void* ps[] = {e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm};
   for (void* q : ps)
     if (q) (void)hipFree(q);
-  e->c_ikey = nullptr; e->c_khist = e->c_krep = nullptr; e->c_mask = nullptr;
+  e->c_ikey = nullptr; e->c_khist = e->c_krep = nullptr; e->c_klen = nullptr; e->c_mask = nullptr;
   e->c_woffw = e->c_wgcnt = e->c_wgoff = e->c_perm = nullptr;
   e->cls_cap = 0;
   const uint64_t groups = nwg * (TRAJ_WG / 64);
   HIPCHECK(e, hipMalloc(&e->c_ikey, n));
-  HIPCHECK(e, hipMalloc(&e->c_khist, 512 * sizeof(uint32_t)));
+  HIPCHECK(e, hipMalloc(&e->c_khist, 512 * sizeof(uint32_t) + 256 * sizeof(uint64_t)));
   e->c_krep = e->c_khist + 256;
+  e->c_klen = (uint64_t*)(e->c_khist + 512);
   HIPCHECK(e, hipMalloc(&e->c_mask, groups * CLS_MAX * sizeof(uint64_t)));
   HIPCHECK(e, hipMalloc(&e->c_woffw, groups * CLS_MAX * sizeof(uint32_t)));
   HIPCHECK(e, hipMalloc(&e->c_wgcnt, nwg * CLS_MAX * sizeof(uint32_t)));
@@ -296,7 +300,7 @@ int grow_class_buffers(zb_engine* e, uint64_t n, uint64_t nwg) {
   return ZB_OK;
 }
 
-int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st, bool allow_cls) {
+int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st, bool allow_tmpl) {
   const uint64_t nwg = (uint64_t)((n + TRAJ_WG - 1) / TRAJ_WG);
   const uint64_t per_entry = sizeof(uint64_t) + sizeof(uint4);
   uint64_t wcap = std::min<uint64_t>(TRAJ_MAX_GENERATIONS, (TRAJ_BUDGET_BYTES / per_entry) / nwg);
@@ -344,12 +348,12 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   p.wcap = (int32_t)wcap;
   // Without exclusive splits nothing in a trajectory depends on payload values, so a batch whose
   // CREATEs all address one process has one trajectory shape: count it on the first instance.
-  p.uni = (!e->has_splits && e->staged_uniform) ? n : 0;
+  p.uni = (allow_tmpl && !e->has_splits && e->staged_uniform) ? n : 0;
   p.cond = e->has_splits ? 1 : 0;
   // With exclusive splits whose conditions only ever read the CREATE payload, the batch splits into a
   // few trajectory classes (k_cls_*); each runs like a uniform batch. More classes than CLS_MAX, or a
   // class whose trajectory raises an incident, sends the batch to the per-instance count pass below.
-  p.cls = (allow_cls && e->has_splits && e->staged_uniform && e->cls_ok) ? 1 : 0;
+  p.cls = (allow_tmpl && e->has_splits && e->staged_uniform && e->cls_ok) ? 1 : 0;
   p.nwg_e = (int32_t)nwg;
   if (p.cls) {
     int grc = grow_class_buffers(e, (uint64_t)n, nwg);
@@ -363,6 +367,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
     p.plan = e->c_plan;
     p.ikey = e->c_ikey;
     p.khist = e->c_khist;
+    p.klen = e->c_klen;
     p.krep = e->c_krep;
     p.cmask = e->c_mask;
     p.woffw = e->c_woffw;
@@ -370,6 +375,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
     p.wgoff = e->c_wgoff;
     p.perm = e->c_perm;
     HIPCHECK(e, hipMemsetAsync(e->c_khist, 0, 256 * sizeof(uint32_t), e->stream));
+    HIPCHECK(e, hipMemsetAsync(e->c_klen, 0, 256 * sizeof(uint64_t), e->stream));
     HIPCHECK(e, hipMemsetAsync(e->c_krep, 0xff, 256 * sizeof(uint32_t), e->stream));
   }
   p.agg = e->t_agg;
@@ -379,6 +385,8 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   p.wbase = e->t_wbase;
   p.ctl = e->t_ctl;
   p.mgen = e->t_mgen;
+  p.tmpl = e->t_tmpl;
+  p.cstat = e->t_cstat;
   p.wstats = e->t_wstats;
   p.max_create = e->staged_max_len;
   p.hdr = e->hdr + (e->wave & 1);
@@ -426,7 +434,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   }
   if (e->h_ctl_pinned->flag) {
     // nothing but scratch counts was written: run the batch per instance (or on the wave pipeline)
-    if (p.cls && e->traj_model_ok) return run_trajectory(e, log_base, n, st, false);
+    if ((p.cls || p.uni) && e->traj_model_ok) return run_trajectory(e, log_base, n, st, false);
     return 0;
   }
   e->host_hdr = e->h_hdr_pinned[0];
@@ -552,6 +560,8 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->t_wtot, TRAJ_WAVE_CAP * sizeof(uint4)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_wbase, TRAJ_WAVE_CAP * sizeof(TrajBase)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_mgen, CLS_MAX * CLS_ROW * sizeof(MergeGen)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->t_tmpl, (size_t)CLS_MAX * CLS_ROW * TF * sizeof(TmplRec)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->t_cstat, CLS_MAX * TSTAT * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   e->ev.resize(EV_PER_WAVE * WAVES_PER_SYNC);
   for (auto& x : e->ev)
     if (hipEventCreate(&x) != hipSuccess) return cleanup(ZB_EDEVICE);
@@ -573,7 +583,8 @@ void zb_engine_destroy(zb_engine* e) {
   void* ps[] = {e->log, e->links, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
                 e->merge_jobs, e->cond_jobs, e->job_counts, e->cw, e->stage, e->info, e->block_agg, e->block_off,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
-                e->c_plan, e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm};
+                e->c_plan, e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
+                e->t_tmpl, e->t_cstat};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->comm) (void)ncclCommDestroy(e->comm);

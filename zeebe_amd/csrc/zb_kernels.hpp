@@ -202,6 +202,18 @@ constexpr int CLS_MAX = 8;          // trajectory classes of a class batch
 constexpr int CLS_MAX_SPLITS = 8;   // exclusive splits a class key covers
 constexpr int CLS_ROW = 4096;       // agg / mgen row of one class (>= generations of a batch)
 
+// One record of a traced trajectory (uniform / class batch), with symbolic keys and payload refs that
+// the template emit pass (k_tmpl) resolves per instance: keys SYMK_WF / SYMK_JOB | generation << 4 |
+// ordinal (the ordinal-th key the instance creates in that generation), NOK, or SYM_CMDPOS (the CREATE
+// command's log position); payloads PAY_CREATE, PAY_MERGE | generation, or a literal (static) ref.
+struct TmplRec {
+  uint32_t key, scope, inst, payload;
+  uint16_t elem;
+  uint8_t intent, kind;
+  uint32_t pad[3];
+};
+constexpr int TSTAT = 8;  // per-class trace statistics: transitions, completed, created, merges, split visits
+
 // Class batch (zb_traj.hip): dense classes of the outcome keys present in the batch.
 struct ClsPlan {
   uint32_t nc, slots;       // classes; emit slots (every class segment padded to a multiple of 64)
@@ -209,6 +221,7 @@ struct ClsPlan {
   uint32_t n[CLS_MAX];      // instances of class c
   uint32_t base[CLS_MAX];   // first emit slot of class c
   uint32_t rep[CLS_MAX];    // representative (first) instance of class c
+  uint64_t lensum[CLS_MAX]; // CREATE payload bytes of the instances of class c (condition statistics)
   uint8_t cid[256];         // key -> class (0xff: absent)
 };
 
@@ -280,6 +293,9 @@ struct TrajParams {
   uint32_t* wgcnt;       // [CLS_MAX][nwg] instances of class c in workgroup b
   uint32_t* wgoff;       // [CLS_MAX][nwg] exclusive prefix of wgcnt over workgroups
   uint32_t* perm;        // [slots] emit slot -> instance
+  uint64_t* klen;        // [256] CREATE payload bytes per key
+  TmplRec* tmpl;         // [CLS_MAX][CLS_ROW][TF] traced records per class and generation
+  uint32_t* cstat;       // [CLS_MAX][TSTAT] traced statistics per class
 };
 
 void launch_traj_count(const TrajParams& p, hipStream_t stream);

@@ -137,6 +137,9 @@ __device__ __forceinline__ const uint8_t* stage_doc(const uint8_t* pp, uint32_t 
 // carries is created by the batch); NOK stands for the null key -1.
 constexpr uint32_t NOK = 0xffffffffu;
 constexpr uint32_t JOB_ZERO = 0xfffffffeu;  // row job key 0 (no job created yet)
+// symbolic keys of a trace (TmplRec): tag | generation << 4 | ordinal
+constexpr uint32_t SYMK_WF = 0x80000000u, SYMK_JOB = 0x40000000u;
+constexpr uint32_t SYM_CMDPOS = 0xfffffffdu;
 
 struct TRec {
   uint32_t key, scope_key;
@@ -352,7 +355,7 @@ __device__ __forceinline__ void t_step(const TrajParams& P, Inst& I, const TRec&
         else if (o == cc) chosen = el.dflt();
         // errors and missing defaults raise incidents: those batches take the per-instance path
         if (chosen == NO_ELEM) { I.err |= TE_FALLBACK; return; }
-        if (EMIT) I.cond_bytes += arena_len(P.arena, rec.payload);
+        I.cond_bytes += 1;  // trace: split visits (k_traj_commit: x CREATE payload bytes of the class)
         s.elem = chosen;
         s.intent = WI_SEQUENCE_FLOW_TAKEN;
         s.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, I.nn > 0);
@@ -579,6 +582,49 @@ __device__ __forceinline__ void block_scan2(uint64_t& a, uint64_t& b, uint64_t& 
   __syncthreads();  // s reused by the next call
 }
 
+// Default output merge of the documents behind refs src (job / message payload) and tgt (scope payload)
+// into the blob at arena byte offset at (capacity m_len): LDS-staged flat-map fast path; a non-flat
+// document sets TE_REGEN (first pass) or runs the general indexer / merger (GEN rerun).
+template <bool GEN>
+__device__ __forceinline__ void merge_into(const TrajParams& P, uint32_t src, uint32_t tgt, uint32_t m_len, uint64_t at,
+                                           uint32_t* reg, uint32_t& err, uint32_t& ns, uint32_t& nt, uint32_t& olen) {
+  const uint32_t* gs = (const uint32_t*)(P.arena + (uint64_t)src * 8);
+  const uint32_t* gt = (const uint32_t*)(P.arena + (uint64_t)tgt * 8);
+  ns = gs[0];
+  nt = gt[0];
+  uint32_t* gd = (uint32_t*)(P.arena + at);
+  olen = 0;
+  bool done = false;
+  if (ns + nt + 3 <= FM_BYTES - 4) {
+    // flat fast path on LDS copies of the two documents
+    for (uint32_t k = 0; k < (ns + 7) / 4; k++) reg[k] = gs[k];
+    for (uint32_t k = 0; k < (nt + 7) / 4; k++) reg[FM_WORDS + k] = gt[k];
+    uint8_t* lo = (uint8_t*)(reg + 2 * FM_WORDS);
+    done = merge_flat((const uint8_t*)reg + 4, ns, (const uint8_t*)(reg + FM_WORDS) + 4, nt, lo + 4, FM_BYTES - 4,
+                      olen);
+    if (done) {
+      reg[2 * FM_WORDS] = olen;
+      for (uint32_t k = 0; k < (olen + 7) / 4; k++) gd[k] = reg[2 * FM_WORDS + k];
+    }
+  } else {
+    // larger flat documents: the same fast path straight on the arena
+    done = merge_flat((const uint8_t*)gs + 4, ns, (const uint8_t*)gt + 4, nt, (uint8_t*)gd + 4, m_len, olen);
+    if (done) gd[0] = olen;
+  }
+  if (!done) {
+    if constexpr (GEN) {
+      Out o{(uint8_t*)gd + 4, 0};
+      bool unsup = false;
+      if (!merge_docs((const uint8_t*)gs + 4, ns, (const uint8_t*)gt + 4, nt, o, unsup)) err |= DE_BAD_PAYLOAD;
+      else if (unsup || o.n > m_len) err |= DE_UNSUPPORTED;
+      olen = o.n;
+      gd[0] = olen;
+    } else {
+      err |= TE_REGEN;
+    }
+  }
+}
+
 // inclusive scan over the 64 lanes of a wave
 __device__ __forceinline__ uint64_t wave_scan(uint64_t v) {
   const int lane = threadIdx.x & 63;
@@ -755,8 +801,13 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
         P.agg[(uint64_t)w * nwg + blockIdx.x] = ta;
       }
       pos0 = 0;
-      kwf = (uint32_t)((a >> 16) & 0xffff);  // placeholder ordinals: nothing in the count depends on key values
-      kjob = (uint32_t)(a >> 32);
+      if (TRACE) {  // symbolic keys: resolved per instance by the template emit pass
+        kwf = SYMK_WF | ((uint32_t)w << 4);
+        kjob = SYMK_JOB | ((uint32_t)w << 4);
+      } else {
+        kwf = (uint32_t)((a >> 16) & 0xffff);  // placeholder ordinals: nothing in the count depends on key values
+        kjob = (uint32_t)(a >> 32);
+      }
     } else {
       const TrajBase wb = P.wbase[w];
       const uint4 off = P.woff[(uint64_t)w * nwg + blockIdx.x];
@@ -786,41 +837,8 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
         const uint32_t mb = tblob_bytes(I.m_len);
         if (at + mb > P.arena_cap) I.err |= DE_ARENA_FULL;
         else {
-          const uint32_t* gs = (const uint32_t*)(P.arena + (uint64_t)I.m_src * 8);
-          const uint32_t* gt = (const uint32_t*)(P.arena + (uint64_t)I.m_tgt * 8);
-          const uint32_t ns = gs[0], nt = gt[0];
-          uint32_t* gd = (uint32_t*)(P.arena + at);
-          uint32_t olen = 0;
-          bool done = false;
-          if (ns + nt + 3 <= FM_BYTES - 4) {
-            // flat fast path on LDS copies of the two documents
-            uint32_t* reg = s_merge + threadIdx.x * FM_STRIDE;
-            for (uint32_t k = 0; k < (ns + 7) / 4; k++) reg[k] = gs[k];
-            for (uint32_t k = 0; k < (nt + 7) / 4; k++) reg[FM_WORDS + k] = gt[k];
-            uint8_t* lo = (uint8_t*)(reg + 2 * FM_WORDS);
-            done = merge_flat((const uint8_t*)reg + 4, ns, (const uint8_t*)(reg + FM_WORDS) + 4, nt, lo + 4,
-                              FM_BYTES - 4, olen);
-            if (done) {
-              reg[2 * FM_WORDS] = olen;
-              for (uint32_t k = 0; k < (olen + 7) / 4; k++) gd[k] = reg[2 * FM_WORDS + k];
-            }
-          } else {
-            // larger flat documents: the same fast path straight on the arena
-            done = merge_flat((const uint8_t*)gs + 4, ns, (const uint8_t*)gt + 4, nt, (uint8_t*)gd + 4, I.m_len, olen);
-            if (done) gd[0] = olen;
-          }
-          if (!done) {
-            if constexpr (GEN) {
-              Out o{(uint8_t*)gd + 4, 0};
-              bool unsup = false;
-              if (!merge_docs((const uint8_t*)gs + 4, ns, (const uint8_t*)gt + 4, nt, o, unsup)) I.err |= DE_BAD_PAYLOAD;
-              else if (unsup || o.n > I.m_len) I.err |= DE_UNSUPPORTED;
-              olen = o.n;
-              gd[0] = olen;
-            } else {
-              I.err |= TE_REGEN;
-            }
-          }
+          uint32_t ns = 0, nt = 0, olen = 0;
+          merge_into<GEN>(P, I.m_src, I.m_tgt, I.m_len, at, s_merge + threadIdx.x * FM_STRIDE, I.err, ns, nt, olen);
           merged_ref = (uint32_t)(at >> 3);
           I.merges += 1;
           I.merge_bytes += ns + nt + olen;
@@ -858,6 +876,18 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
           I.rjob[r] = JOB_ZERO;
           I.rnch[r] = 0;
         }
+        if (TRACE && active) {  // the trajectory's record, symbolic
+          if (s.flags & TK_DETAIL) I.err |= TE_FALLBACK;  // incidents are never templated
+          TmplRec t;
+          t.key = s.key;
+          t.scope = kind_rt(s.kind) == ZB_RT_COMMAND_REJECTION ? SYM_CMDPOS : s.scope_key;
+          t.inst = I.inst_key;
+          t.payload = s.payload;
+          t.elem = s.elem; t.intent = s.intent; t.kind = s.kind;
+          t.pad[0] = t.pad[1] = t.pad[2] = 0;
+          P.tmpl[((uint64_t)I.crow + w) * TF + k] = t;
+          if (kind_vt(s.kind) == ZB_VT_WORKFLOW_INSTANCE && kind_rt(s.kind) == ZB_RT_EVENT) I.transitions++;
+        }
         s.flags = 0;
         I.cur.set(k, s);
         if (EMIT && active) {
@@ -885,7 +915,15 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
 
   if (!EMIT) {
     if (TRACE) {
-      if (active) P.wcount[cls] = (uint32_t)wl;
+      if (active) {
+        P.wcount[cls] = (uint32_t)wl;
+        // the template emit writes no element-instance rows: every traced instance must end
+#pragma unroll
+        for (int k = 0; k < TR; k++)
+          if (((I.used >> k) & 1) && I.alive(k)) I.err |= TE_FALLBACK;
+        uint32_t* cs = P.cstat + (uint64_t)cls * TSTAT;
+        cs[0] = I.transitions; cs[1] = I.completed; cs[2] = I.created; cs[3] = I.merges; cs[4] = I.cond_bytes;
+      }
       if (threadIdx.x == 0) atomicMax(&ctl->wmax, (uint32_t)w);
     } else if (threadIdx.x == 0) {
       P.wcount[blockIdx.x] = (uint32_t)w;
@@ -1092,6 +1130,18 @@ __global__ void __launch_bounds__(256) k_traj_commit(TrajParams P) {
   __syncthreads();
   if (threadIdx.x != 0) return;
   for (int f = 0; f < 6; f++) P.stats[f] += s_st[0][f] + s_st[1][f] + s_st[2][f] + s_st[3][f];
+  if (P.uni || P.cls) {  // template emit: per-class traced statistics x class sizes
+    const uint32_t nc = P.cls ? P.plan->nc : 1;
+    for (uint32_t c = 0; c < nc; c++) {
+      const uint64_t m = P.cls ? (uint64_t)P.plan->n[c] : (uint64_t)P.uni;
+      const uint32_t* cs = P.cstat + (uint64_t)c * TSTAT;
+      P.stats[0] += m * cs[0];  // transitions
+      P.stats[1] += m * cs[1];  // completed instances
+      P.stats[2] += m * cs[2];  // created
+      P.stats[3] += m * cs[3];  // merges
+      if (P.cls) P.stats[5] += (uint64_t)cs[4] * P.plan->lensum[c];  // condition payload bytes
+    }
+  }
   if (ctl->derr) atomicOr(P.err, ctl->derr);
   WaveHdr h = *P.hdr;
   h.begin = h.end = h.gen_end = ctl->end;
@@ -1123,9 +1173,11 @@ __global__ void __launch_bounds__(256) k_traj_commit(TrajParams P) {
 __global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
   __shared__ uint32_t s_doc[TWG * FM_STRIDE];
   __shared__ uint32_t s_hist[256], s_rep[256];
+  __shared__ unsigned long long s_len[256];
   const int t = threadIdx.x;
   s_hist[t] = 0;
   s_rep[t] = 0xffffffffu;
+  s_len[t] = 0;
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * TWG + t;
   if (i < P.n) {
@@ -1152,11 +1204,13 @@ __global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
     P.ikey[i] = (uint8_t)key;
     atomicAdd(&s_hist[key & 255], 1u);
     atomicMin(&s_rep[key & 255], (uint32_t)i);
+    atomicAdd(&s_len[key & 255], (unsigned long long)len);
   }
   __syncthreads();
   if (s_hist[t]) {
     atomicAdd(&P.khist[t], s_hist[t]);
     atomicMin(&P.krep[t], s_rep[t]);
+    atomicAdd((unsigned long long*)&P.klen[t], s_len[t]);
   }
 }
 
@@ -1176,6 +1230,7 @@ __global__ void __launch_bounds__(256) k_cls_plan(TrajParams P) {
     pl->key[cid] = (uint32_t)t;
     pl->n[cid] = cnt;
     pl->rep[cid] = P.krep[t];
+    pl->lensum[cid] = P.klen[t];
   }
   __syncthreads();
   if (t == 0) {
@@ -1269,6 +1324,168 @@ __global__ void __launch_bounds__(TWG) k_cls_perm(TrajParams P) {
   if (c < nc) P.perm[pl->base[c] + mine] = (uint32_t)i;
 }
 
+// ------------------------------------------------------------------------------ template emit
+// Uniform and class batches: every instance of class c follows the traced trajectory of c (TmplRec,
+// symbolic), so the emit pass instantiates it instead of stepping the state machine again: per
+// generation (a scalar loop) the instance's log position and key bases are linear in before_c(i),
+// the merge of that generation (if any) runs on its own slot, and each traced record is written with
+// its keys and payload refs resolved. No per-instance control flow: every branch is scalar.
+struct TmplLane {
+  uint32_t before[CLS_MAX];
+  uint32_t ncls;
+};
+// key ordinal base of generation g for this instance: wf (f = 1) or job (f = 2) counter
+__device__ __forceinline__ int64_t tmpl_kbase(const TrajParams& P, const TmplLane& L, uint32_t g, int f) {
+  const TrajBase wb = kload(P.wbase, (uint64_t)g);
+  int64_t k = f == 1 ? wb.wf : wb.job;
+#pragma unroll
+  for (int c = 0; c < CLS_MAX; c++) {
+    if (c >= (int)L.ncls) break;
+    const uint64_t n = kload(P.agg, (uint64_t)c * CLS_ROW + g);
+    k += (int64_t)L.before[c] * (int64_t)(f == 1 ? ((n >> 16) & 0xffff) : (n >> 32));
+  }
+  return k;
+}
+// arena byte offset of this instance's merge slot of generation g
+__device__ __forceinline__ uint64_t tmpl_mslot(const TrajParams& P, const TmplLane& L, uint32_t g) {
+  int64_t pm = kload(P.wbase, (uint64_t)g).mbase;
+#pragma unroll
+  for (int c = 0; c < CLS_MAX; c++) {
+    if (c >= (int)L.ncls) break;
+    const MergeGen m = kload(P.mgen, (uint64_t)c * CLS_ROW + g);
+    if (m.has) pm += (int64_t)L.before[c] * (int64_t)m.stride;
+  }
+  return (uint64_t)pm;
+}
+// a symbolic key: -1, or the partition key of the ordinal-th key created in its generation
+__device__ __forceinline__ int64_t tmpl_key(const TrajParams& P, const TmplLane& L, uint32_t sym, uint32_t w,
+                                            int64_t kwf, int64_t kjob) {
+  if (sym == NOK) return -1;
+  if (sym == JOB_ZERO) return 0;
+  const uint32_t g = (sym >> 4) & 0xfff, ord = sym & 15;
+  if (sym & SYMK_WF) return P.wf_start + 5 * ((g == w ? kwf : tmpl_kbase(P, L, g, 1)) + ord);
+  return P.job_start + 5 * ((g == w ? kjob : tmpl_kbase(P, L, g, 2)) + ord);
+}
+
+template <bool CLS, bool GEN>
+__global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
+  __shared__ uint32_t s_merge[TWG * FM_STRIDE];
+  __shared__ uint64_t s_scan[TWG / 64][2];
+  TrajCtl* ctl = P.ctl;
+  if (ctl->flag) return;
+  if (GEN && !ctl->regen) return;
+  int64_t inst = (int64_t)blockIdx.x * TWG + threadIdx.x;
+  bool active = inst < P.n;
+  uint32_t cls = 0;
+  TmplLane L;
+  L.ncls = 1;
+  if (CLS) {
+    const ClsPlan* pl = P.plan;
+    L.ncls = __builtin_amdgcn_readfirstlane(pl->nc);
+    const uint32_t sl = (uint32_t)inst;
+    bool found = false;
+    for (uint32_t c = 0; c < L.ncls; c++) {
+      const uint32_t b = pl->base[c];
+      if (sl >= b && sl < b + ((pl->n[c] + 63) & ~63u)) { cls = c; found = true; }
+    }
+    cls = __builtin_amdgcn_readfirstlane(cls);  // class segments are whole waves
+    active = found && sl - pl->base[cls] < pl->n[cls];
+    inst = P.perm[active ? sl : pl->base[cls]];
+    const uint64_t grp = (uint64_t)(inst >> 6) * CLS_MAX;
+    const uint64_t lt = (1ull << (inst & 63)) - 1;
+#pragma unroll
+    for (int c = 0; c < CLS_MAX; c++)
+      L.before[c] = c < (int)L.ncls ? P.woffw[grp + c] + (uint32_t)__builtin_popcountll(P.cmask[grp + c] & lt) : 0;
+  } else {
+    if (!active) inst = 0;  // (follows instance 0, writes nothing)
+#pragma unroll
+    for (int c = 0; c < CLS_MAX; c++) L.before[c] = c == 0 ? (uint32_t)inst : 0;
+  }
+  const uint32_t crow = cls * CLS_ROW;
+  const int W = (int)P.wcount[cls];
+  const uint32_t create_ref = P.log[P.log_base + inst].payload;
+  uint32_t err = 0;
+  uint64_t merge_bytes = 0;
+  uint32_t pc_sym = PAY_CREATE, pc_ref = create_ref;  // last resolved payload symbol
+  uint32_t* reg = s_merge + threadIdx.x * FM_STRIDE;
+
+#pragma unroll 1
+  for (int w = 0; w < W; w++) {
+    const TrajBase wb = kload(P.wbase, (uint64_t)w);
+    int64_t po = 0, pw = 0, pj = 0;
+#pragma unroll
+    for (int c = 0; c < CLS_MAX; c++) {
+      if (c >= (int)L.ncls) break;
+      const uint64_t n = kload(P.agg, (uint64_t)c * CLS_ROW + w);
+      po += (int64_t)L.before[c] * (int64_t)(n & 0xffff);
+      pw += (int64_t)L.before[c] * (int64_t)((n >> 16) & 0xffff);
+      pj += (int64_t)L.before[c] * (int64_t)(n >> 32);
+    }
+    const int64_t pos0 = wb.pos + po, kwf = wb.wf + pw, kjob = wb.job + pj;
+    const uint32_t nrec = (uint32_t)(kload(P.agg, (uint64_t)crow + w) & 0xffff);
+    // this generation's merge: source / target resolved, result into the instance's slot
+    const MergeGen g = kload(P.mgen, (uint64_t)crow + w);
+    uint32_t merged_ref = 0;
+    if (g.has) {
+      uint32_t src = g.src, tgt = g.tgt;
+      if (src == PAY_CREATE) src = create_ref;
+      else if (src & PAY_MERGE) src = (uint32_t)(tmpl_mslot(P, L, src & 0xffff) >> 3);
+      if (tgt == pc_sym) tgt = pc_ref;
+      else if (tgt == PAY_CREATE) tgt = create_ref;
+      else if (tgt & PAY_MERGE) tgt = (uint32_t)(tmpl_mslot(P, L, tgt & 0xffff) >> 3);
+      const uint64_t at = tmpl_mslot(P, L, (uint32_t)w);
+      merged_ref = (uint32_t)(at >> 3);
+      if (active) {
+        const uint32_t m_len = arena_len(P.arena, src) + arena_len(P.arena, tgt) + 8;
+        if (tblob_bytes(m_len) > g.stride) err |= DE_UNSUPPORTED;
+        else if (at + g.stride > P.arena_cap) err |= DE_ARENA_FULL;
+        else {
+          uint32_t ns = 0, nt = 0, olen = 0;
+          merge_into<GEN>(P, src, tgt, m_len, at, reg, err, ns, nt, olen);
+          merge_bytes += ns + nt + olen;
+        }
+      }
+    }
+#pragma unroll 1
+    for (uint32_t k = 0; k < nrec; k++) {
+      const TmplRec t = kload(P.tmpl, ((uint64_t)crow + w) * TF + k);
+      zb_rec d;
+      d.key = tmpl_key(P, L, t.key, (uint32_t)w, kwf, kjob);
+      d.scope_key = t.scope == SYM_CMDPOS ? P.log_base + inst : tmpl_key(P, L, t.scope, (uint32_t)w, kwf, kjob);
+      d.inst_key = tmpl_key(P, L, t.inst, (uint32_t)w, kwf, kjob);
+      uint32_t pay = t.payload;
+      if (pay == (PAY_MERGE | (uint32_t)w)) pay = merged_ref;
+      else if (pay == pc_sym) pay = pc_ref;
+      else if (pay == PAY_CREATE) pay = create_ref;
+      else if (pay & PAY_MERGE) {
+        const uint32_t r = (uint32_t)(tmpl_mslot(P, L, pay & 0xffff) >> 3);
+        pc_sym = pay;
+        pc_ref = r;
+        pay = r;
+      }
+      if (t.payload & PAY_MERGE) { pc_sym = t.payload; pc_ref = pay; }
+      d.payload = pay;
+      d.elem = t.elem; d.intent = t.intent; d.kind = t.kind;
+      if (active) {
+        if (pos0 + k < (int64_t)P.log_cap) P.log[pos0 + k] = d;
+        else err |= DE_LOG_FULL;
+      }
+    }
+  }
+  // statistics: everything but the merge bytes is a per-class constant (k_traj_commit)
+  uint64_t s0 = active ? merge_bytes : 0, s1 = 0, t0, t1;
+  block_scan2(s0, s1, t0, t1, s_scan);
+  if (threadIdx.x == 0) {
+    uint64_t* ws = P.wstats + (uint64_t)blockIdx.x * 6;
+    ws[0] = ws[1] = ws[2] = ws[3] = ws[5] = 0;
+    ws[4] = t0;
+  }
+  if (!active) err = 0;
+  if (err & TE_REGEN) atomicOr(&ctl->regen, 1u);
+  const uint32_t derr = err & ~(uint32_t)(TE_FALLBACK | TE_REGEN);
+  if (derr) atomicOr(&ctl->derr, derr);
+}
+
 // conditions are compiled into the count / emit kernels only when the model has exclusive splits
 // (a uniform batch never has any), keeping the condition VM's call frame out of the other variants
 void launch_traj_count(const TrajParams& p, hipStream_t s) {
@@ -1299,13 +1516,13 @@ void launch_traj_emit(const TrajParams& p, hipStream_t s) {
   const dim3 g(p.nwg), b(TWG);
   if (p.cls) {
     const dim3 ge(p.nwg_e);
-    hipLaunchKernelGGL((k_traj<true, true, false, false, false, true>), ge, b, 0, s, p);
+    hipLaunchKernelGGL((k_tmpl<true, false>), ge, b, 0, s, p);
     hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
-    hipLaunchKernelGGL((k_traj<true, true, false, true, false, true>), ge, b, 0, s, p);
+    hipLaunchKernelGGL((k_tmpl<true, true>), ge, b, 0, s, p);
   } else if (p.uni) {
-    hipLaunchKernelGGL((k_traj<true, true, false, false, false, false>), g, b, 0, s, p);
+    hipLaunchKernelGGL((k_tmpl<false, false>), g, b, 0, s, p);
     hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
-    hipLaunchKernelGGL((k_traj<true, true, false, true, false, false>), g, b, 0, s, p);
+    hipLaunchKernelGGL((k_tmpl<false, true>), g, b, 0, s, p);
   } else if (p.cond) {
     hipLaunchKernelGGL((k_traj<true, false, true, false, false, false>), g, b, 0, s, p);
     hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
