@@ -152,6 +152,7 @@ struct zb_engine {
   uint32_t* t_cstat = nullptr;   // [CLS_MAX][TSTAT]
   uint64_t* c_mask = nullptr;
   uint32_t *c_woffw = nullptr, *c_wgcnt = nullptr, *c_wgoff = nullptr, *c_perm = nullptr;
+  uint32_t *c_segs = nullptr, *c_wcls = nullptr;
 
   // message correlation (zb_msg.hip): outboxes [0] open-subscription, [1] correlate
   zb_exchange_rec* obox[2] = {nullptr, nullptr};
@@ -277,13 +278,19 @@ int check_device_errors(zb_engine* e, uint32_t flags) {
 // Trajectory path (zb_traj.hip) for a batch of n CREATE commands injected at log_base on an idle
 // partition. Returns 1 when the batch ran to quiescence, 0 when the count pass asked for the wave
 // pipeline (nothing but scratch counts was written), <0 on a device error.
+// emit slots of a class batch: instances + the padding of every (block, class) segment
+uint64_t cls_slot_bound(uint64_t n, uint64_t nwg) {
+  const uint64_t nblk = (nwg + CLS_BLK_WG - 1) / CLS_BLK_WG;
+  return n + 64 * CLS_MAX * nblk;
+}
+
 int grow_class_buffers(zb_engine* e, uint64_t n, uint64_t nwg) {
   if (n <= e->cls_cap) return ZB_OK;
-  void* ps[] = {e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm};
+  void* ps[] = {e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm, e->c_segs, e->c_wcls};
   for (void* q : ps)
     if (q) (void)hipFree(q);
   e->c_ikey = nullptr; e->c_khist = e->c_krep = nullptr; e->c_klen = nullptr; e->c_mask = nullptr;
-  e->c_woffw = e->c_wgcnt = e->c_wgoff = e->c_perm = nullptr;
+  e->c_woffw = e->c_wgcnt = e->c_wgoff = e->c_perm = e->c_segs = e->c_wcls = nullptr;
   e->cls_cap = 0;
   const uint64_t groups = nwg * (TRAJ_WG / 64);
   HIPCHECK(e, hipMalloc(&e->c_ikey, n));
@@ -294,7 +301,11 @@ int grow_class_buffers(zb_engine* e, uint64_t n, uint64_t nwg) {
   HIPCHECK(e, hipMalloc(&e->c_woffw, groups * CLS_MAX * sizeof(uint32_t)));
   HIPCHECK(e, hipMalloc(&e->c_wgcnt, nwg * CLS_MAX * sizeof(uint32_t)));
   HIPCHECK(e, hipMalloc(&e->c_wgoff, nwg * CLS_MAX * sizeof(uint32_t)));
-  HIPCHECK(e, hipMalloc(&e->c_perm, (n + 64 * CLS_MAX) * sizeof(uint32_t)));
+  const uint64_t nblk = (nwg + CLS_BLK_WG - 1) / CLS_BLK_WG;
+  const uint64_t slots = cls_slot_bound(n, nwg);
+  HIPCHECK(e, hipMalloc(&e->c_perm, slots * sizeof(uint32_t)));
+  HIPCHECK(e, hipMalloc(&e->c_segs, nblk * CLS_MAX * sizeof(uint32_t)));
+  HIPCHECK(e, hipMalloc(&e->c_wcls, (slots / 64 + 1) * sizeof(uint32_t)));
   if (!e->c_plan) HIPCHECK(e, hipMalloc(&e->c_plan, sizeof(ClsPlan)));
   e->cls_cap = nwg * TRAJ_WG;
   return ZB_OK;
@@ -320,7 +331,8 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
     e->t_wcount = nullptr;
     e->t_wstats = nullptr;
     HIPCHECK(e, hipMalloc(&e->t_wcount, (nwg + CLS_MAX) * sizeof(uint32_t)));
-    HIPCHECK(e, hipMalloc(&e->t_wstats, (nwg + CLS_MAX) * 6 * sizeof(uint64_t)));
+    // (class batches emit over up to nwg + nwg / 8 + 8 workgroups)
+    HIPCHECK(e, hipMalloc(&e->t_wstats, (2 * nwg + 64) * 6 * sizeof(uint64_t)));
     e->t_nwg_cap = nwg;
   }
   TrajCtl c{};
@@ -358,7 +370,12 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   if (p.cls) {
     int grc = grow_class_buffers(e, (uint64_t)n, nwg);
     if (grc != ZB_OK) return grc;
-    p.nwg_e = (int32_t)(nwg + CLS_MAX / (TRAJ_WG / 64));  // + the padding of every class segment
+    // every (block, class) segment padded to whole waves; a multiple of 8 workgroups (XCD mapping)
+    p.nwg_e = (int32_t)(((cls_slot_bound((uint64_t)n, nwg) + TRAJ_WG - 1) / TRAJ_WG + 7) & ~7ull);
+    p.nblk = (int32_t)((nwg + CLS_BLK_WG - 1) / CLS_BLK_WG);
+    p.segs = e->c_segs;
+    p.wcls = e->c_wcls;
+    HIPCHECK(e, hipMemsetAsync(e->c_perm, 0xff, cls_slot_bound((uint64_t)n, nwg) * sizeof(uint32_t), e->stream));
     p.nsplits = e->nsplits;
     for (int k = 0; k < CLS_MAX_SPLITS; k++) {
       p.split_elem[k] = e->split_elem[k];
@@ -427,7 +444,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
     for (uint32_t c = 0; c < pl.nc && c < CLS_MAX; c++) {
       std::vector<uint64_t> a(c2.wmax);
       if (c2.wmax) (void)hipMemcpy(a.data(), e->t_agg + (uint64_t)c * CLS_ROW, c2.wmax * 8, hipMemcpyDeviceToHost);
-      fprintf(stderr, "  class %u key=%u n=%u base=%u rep=%u W=%u agg:", c, pl.key[c], pl.n[c], pl.base[c], pl.rep[c], wc[c]);
+      fprintf(stderr, "  class %u key=%u n=%u rep=%u W=%u agg:", c, pl.key[c], pl.n[c], pl.rep[c], wc[c]);
       for (auto x : a) fprintf(stderr, " %lx", (unsigned long)x);
       fprintf(stderr, "\n");
     }
@@ -584,7 +601,7 @@ void zb_engine_destroy(zb_engine* e) {
                 e->merge_jobs, e->cond_jobs, e->job_counts, e->cw, e->stage, e->info, e->block_agg, e->block_off,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
-                e->t_tmpl, e->t_cstat};
+                e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->comm) (void)ncclCommDestroy(e->comm);

@@ -201,6 +201,7 @@ constexpr int TF = 2;         // records per workflow instance per generation
 constexpr int CLS_MAX = 8;          // trajectory classes of a class batch
 constexpr int CLS_MAX_SPLITS = 8;   // exclusive splits a class key covers
 constexpr int CLS_ROW = 4096;       // agg / mgen row of one class (>= generations of a batch)
+constexpr int CLS_BLK_WG = 16;      // instance workgroups per emit block (class segments per block)
 
 // One record of a traced trajectory (uniform / class batch), with symbolic keys and payload refs that
 // the template emit pass (k_tmpl) resolves per instance: keys SYMK_WF / SYMK_JOB | generation << 4 |
@@ -216,10 +217,9 @@ constexpr int TSTAT = 8;  // per-class trace statistics: transitions, completed,
 
 // Class batch (zb_traj.hip): dense classes of the outcome keys present in the batch.
 struct ClsPlan {
-  uint32_t nc, slots;       // classes; emit slots (every class segment padded to a multiple of 64)
+  uint32_t nc, slots;       // classes; emit slots (every (block, class) segment padded to a multiple of 64)
   uint32_t key[CLS_MAX];    // outcome key of class c
   uint32_t n[CLS_MAX];      // instances of class c
-  uint32_t base[CLS_MAX];   // first emit slot of class c
   uint32_t rep[CLS_MAX];    // representative (first) instance of class c
   uint64_t lensum[CLS_MAX]; // CREATE payload bytes of the instances of class c (condition statistics)
   uint8_t cid[256];         // key -> class (0xff: absent)
@@ -292,7 +292,10 @@ struct TrajParams {
   uint32_t* woffw;       // [n / 64][CLS_MAX] instances of class c before the group
   uint32_t* wgcnt;       // [CLS_MAX][nwg] instances of class c in workgroup b
   uint32_t* wgoff;       // [CLS_MAX][nwg] exclusive prefix of wgcnt over workgroups
-  uint32_t* perm;        // [slots] emit slot -> instance
+  uint32_t* perm;        // [slots] emit slot -> instance (~0: padding)
+  uint32_t* segs;        // [nblk][CLS_MAX] first emit slot of the class-c segment of block b
+  uint32_t* wcls;        // [slots / 64] class of every emit wave
+  int32_t nblk, pad4;    // blocks of CLS_BLK_WG instance workgroups
   uint64_t* klen;        // [256] CREATE payload bytes per key
   TmplRec* tmpl;         // [CLS_MAX][CLS_ROW][TF] traced records per class and generation
   uint32_t* cstat;       // [CLS_MAX][TSTAT] traced statistics per class

@@ -645,9 +645,7 @@ __device__ __forceinline__ uint64_t wave_scan(uint64_t v) {
 // TRACE (count pass of a uniform batch, one instance): payload refs are symbolic (PAY_CREATE, PAY_MERGE | w,
 // literal refs) so that each generation's merge gets a result bound valid for every instance of the
 // batch (MergeGen); the emit pass then places instance i's result at mbase(w) + i * stride(w).
-// CLS (class batch, with UNI in the emit pass and with TRACE in the count pass): TRACE lane c traces the
-// representative of class c; emit slot s belongs to the class segment holding it, its instance is perm[s],
-// and its positions / keys / merge slots are linear in before_c(i) (instances of class c before it).
+// CLS (with TRACE): class batch trace, lane c traces the representative of class c.
 template <bool EMIT, bool UNI, bool COND, bool GEN, bool TRACE, bool CLS>
 __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
   __shared__ uint64_t s_scan[TWG / 64][2];
@@ -661,31 +659,13 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
   int64_t inst = (int64_t)blockIdx.x * TWG + threadIdx.x;
   // lanes past the batch follow lane 0's control in a uniform batch: they must not write anything
   bool active = inst < P.n;
-  uint32_t cls = 0, ncls = 1;
-  uint32_t before[CLS_MAX];  // class batch emit: instances of each class before this one
-  if (CLS) {
+  uint32_t cls = 0;
+  if (CLS) {  // class trace: lane c traces the representative of class c
     const ClsPlan* pl = P.plan;
-    ncls = __builtin_amdgcn_readfirstlane(pl->nc);
-    if (TRACE) {
-      cls = threadIdx.x;
-      active = cls < ncls;
-      inst = active ? pl->rep[cls] : 0;
-    } else {
-      const uint32_t sl = (uint32_t)inst;
-      bool found = false;
-      for (uint32_t c = 0; c < ncls; c++) {
-        const uint32_t b = pl->base[c];
-        if (sl >= b && sl < b + ((pl->n[c] + 63) & ~63u)) { cls = c; found = true; }
-      }
-      cls = __builtin_amdgcn_readfirstlane(cls);  // class segments are whole waves
-      active = found && sl - pl->base[cls] < pl->n[cls];
-      inst = P.perm[active ? sl : pl->base[cls]];
-      const uint64_t grp = (uint64_t)(inst >> 6) * CLS_MAX;
-      const uint64_t lt = (1ull << (inst & 63)) - 1;
-#pragma unroll
-      for (int c = 0; c < CLS_MAX; c++)
-        before[c] = c < (int)ncls ? P.woffw[grp + c] + (uint32_t)__builtin_popcountll(P.cmask[grp + c] & lt) : 0;
-    }
+    const uint32_t ncls = __builtin_amdgcn_readfirstlane(pl->nc);
+    cls = threadIdx.x;
+    active = cls < ncls;
+    inst = active ? pl->rep[cls] : 0;
   }
 
   Inst I;
@@ -752,35 +732,7 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
     if (!UNI) block_scan2(a, bytes, ta, tb, s_scan);
     int64_t pos0;
     uint32_t kwf, kjob;  // key ordinals of this instance's first new wf / job key
-    if (UNI && CLS) {
-      // class batch: linear in the per-class counts of the instances before this one
-      const TrajBase wb = kload(P.wbase, (uint64_t)w);
-      int64_t po = 0, pw = 0, pj = 0;
-#pragma unroll
-      for (int c = 0; c < CLS_MAX; c++) {
-        if (c >= (int)ncls) break;
-        const uint64_t n = kload(P.agg, (uint64_t)c * CLS_ROW + w);
-        po += (int64_t)before[c] * (int64_t)(n & 0xffff);
-        pw += (int64_t)before[c] * (int64_t)((n >> 16) & 0xffff);
-        pj += (int64_t)before[c] * (int64_t)(n >> 32);
-      }
-      pos0 = wb.pos + po;
-      kwf = (uint32_t)(wb.wf + pw);
-      kjob = (uint32_t)(wb.job + pj);
-      if (EMIT && I.merge) {
-        int64_t pm = 0;
-#pragma unroll
-        for (int c = 0; c < CLS_MAX; c++) {
-          if (c >= (int)ncls) break;
-          const MergeGen g = kload(P.mgen, (uint64_t)c * CLS_ROW + w);
-          if (g.has) pm += (int64_t)before[c] * (int64_t)g.stride;
-        }
-        const MergeGen g = kload(P.mgen, (uint64_t)I.crow + w);
-        tb = (uint64_t)(wb.mbase + pm);
-        bytes = 0;
-        if (!g.has || tblob_bytes(I.m_len) > g.stride) { I.err |= DE_UNSUPPORTED; tb = P.arena_cap; }
-      }
-    } else if (UNI) {
+    if (UNI) {
       // positions and keys are affine in the instance index; the arena is allocated per wave
       const uint64_t c = kload(P.agg, (uint64_t)w);
       const TrajBase wb = kload(P.wbase, (uint64_t)w);
@@ -1239,13 +1191,7 @@ __global__ void __launch_bounds__(256) k_cls_plan(TrajParams P) {
       pl->nc = 0;
       return;
     }
-    uint32_t b = 0;
-    for (uint32_t c = 0; c < nc; c++) {
-      pl->base[c] = b;
-      b += (pl->n[c] + 63) & ~63u;
-    }
     pl->nc = nc;
-    pl->slots = b;
   }
 }
 
@@ -1321,7 +1267,57 @@ __global__ void __launch_bounds__(TWG) k_cls_perm(TrajParams P) {
     if (lane == 0) P.woffw[grp + k] = off;
     if (k == c) mine = off + (uint32_t)__builtin_popcountll(P.cmask[grp + k] & ((1ull << lane) - 1));
   }
-  if (c < nc) P.perm[pl->base[c] + mine] = (uint32_t)i;
+  if (c < nc) {  // slot in the (block, class) segment: rank among the block's class-c instances
+    const uint32_t blk = blockIdx.x / CLS_BLK_WG;
+    const uint32_t first = P.wgoff[(uint64_t)c * P.nwg + (uint64_t)blk * CLS_BLK_WG];
+    P.perm[P.segs[(uint64_t)blk * CLS_MAX + c] + mine - first] = (uint32_t)i;
+  }
+}
+
+// Emit slots are laid out block by block (CLS_BLK_WG instance workgroups), and inside a block class by
+// class, each (block, class) segment padded to whole waves: a wave holds one class, and the waves that
+// write one region of the log run close together in time (k_tmpl maps blocks to XCDs contiguously).
+// One workgroup: exclusive prefix of the padded segment sizes; class of every emit wave.
+__global__ void __launch_bounds__(1024) k_cls_segs(TrajParams P) {
+  __shared__ uint32_t s_w[16];
+  ClsPlan* pl = P.plan;
+  if (P.ctl->flag) return;
+  const uint32_t nc = pl->nc, nwg = (uint32_t)P.nwg;
+  const uint32_t E = (uint32_t)P.nblk * nc;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < E; base += 1024) {
+    const uint32_t e = base + threadIdx.x;
+    uint32_t x = 0, b = 0, c = 0;
+    if (e < E) {
+      b = e / nc;
+      c = e % nc;
+      const uint32_t w0 = b * CLS_BLK_WG, w1 = w0 + CLS_BLK_WG;
+      const uint32_t lo = P.wgoff[(uint64_t)c * nwg + w0];
+      const uint32_t hi = w1 < nwg ? P.wgoff[(uint64_t)c * nwg + w1] : pl->n[c];
+      x = (hi - lo + 63) & ~63u;
+    }
+    uint32_t y = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t u = __shfl_up(y, d, 64);
+      if (lane >= d) y += u;
+    }
+    if (lane == 63) s_w[wv] = y;
+    __syncthreads();
+    uint32_t ex = y - x + carry, tot = 0;
+    for (int k = 0; k < 16; k++) {
+      if (k < wv) ex += s_w[k];
+      tot += s_w[k];
+    }
+    if (e < E) {
+      P.segs[(uint64_t)b * CLS_MAX + c] = ex;
+      for (uint32_t j = 0; j < x / 64; j++) P.wcls[ex / 64 + j] = c;
+    }
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) pl->slots = carry;
 }
 
 // ------------------------------------------------------------------------------ template emit
@@ -1382,15 +1378,21 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
   if (CLS) {
     const ClsPlan* pl = P.plan;
     L.ncls = __builtin_amdgcn_readfirstlane(pl->nc);
-    const uint32_t sl = (uint32_t)inst;
-    bool found = false;
-    for (uint32_t c = 0; c < L.ncls; c++) {
-      const uint32_t b = pl->base[c];
-      if (sl >= b && sl < b + ((pl->n[c] + 63) & ~63u)) { cls = c; found = true; }
+    // XCD-aware: workgroups are dispatched round-robin over the 8 XCDs; give each XCD a contiguous
+    // range of emit slots (blocks), so that the partial lines of one log region meet in one L2
+    const uint32_t G = gridDim.x;  // a multiple of 8
+    const uint32_t lwg = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+    const uint32_t sl = lwg * TWG + threadIdx.x;
+    const uint32_t slots = __builtin_amdgcn_readfirstlane(pl->slots);
+    uint32_t pi = 0xffffffffu;
+    cls = 0;
+    if (__builtin_amdgcn_readfirstlane(sl) < slots) {  // (slots come in whole waves)
+      cls = __builtin_amdgcn_readfirstlane(P.wcls[sl >> 6]);
+      pi = P.perm[sl];
     }
-    cls = __builtin_amdgcn_readfirstlane(cls);  // class segments are whole waves
-    active = found && sl - pl->base[cls] < pl->n[cls];
-    inst = P.perm[active ? sl : pl->base[cls]];
+    active = pi != 0xffffffffu;
+    const uint32_t p0 = __builtin_amdgcn_readfirstlane(pi);  // lane 0 of a segment wave is never padding
+    inst = active ? pi : (p0 != 0xffffffffu ? p0 : pl->rep[0]);
     const uint64_t grp = (uint64_t)(inst >> 6) * CLS_MAX;
     const uint64_t lt = (1ull << (inst & 63)) - 1;
 #pragma unroll
@@ -1505,6 +1507,7 @@ void launch_traj_count_classes(const TrajParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_cls_plan, dim3(1), dim3(256), 0, s, p);
   hipLaunchKernelGGL(k_cls_masks, dim3(p.nwg), dim3(TWG), 0, s, p);
   hipLaunchKernelGGL(k_cls_scan, dim3(CLS_MAX), dim3(1024), 0, s, p);
+  hipLaunchKernelGGL(k_cls_segs, dim3(1), dim3(1024), 0, s, p);
   hipLaunchKernelGGL(k_cls_perm, dim3(p.nwg), dim3(TWG), 0, s, p);
   hipLaunchKernelGGL((k_traj<false, false, false, false, true, true>), dim3(1), dim3(TWG), 0, s, p);
 }
