@@ -256,9 +256,12 @@ __device__ __forceinline__ bool same_type(Operand& x, Operand& y, CondOut& out) 
 }
 
 // Evaluates one compiled condition; returns result (valid when out.err == 0 && !unsupported).
-__device__ __noinline__ bool eval_condition(uint32_t pc, const uint32_t* code, const uint8_t* doc, uint32_t n,
-                                      const DevConst* consts, const DevQuery* queries, const DevFilter* filters,
-                                      const uint8_t* pool, CondOut& out, bool& unsupported) {
+// Inlined form: a caller whose document is in LDS gets LDS loads (address-space inference).
+template <typename DocPtr>
+__device__ __forceinline__ bool eval_condition_inl(uint32_t pc, const uint32_t* code, DocPtr doc, uint32_t n,
+                                                   const DevConst* consts, const DevQuery* queries,
+                                                   const DevFilter* filters, const uint8_t* pool, CondOut& out,
+                                                   bool& unsupported) {
   bool r = false;
   out.err = 0;
   for (int guard = 0; guard < 4096; guard++) {
@@ -304,6 +307,11 @@ __device__ __noinline__ bool eval_condition(uint32_t pc, const uint32_t* code, c
   }
   unsupported = true;
   return false;
+}
+__device__ __noinline__ bool eval_condition(uint32_t pc, const uint32_t* code, const uint8_t* doc, uint32_t n,
+                                            const DevConst* consts, const DevQuery* queries, const DevFilter* filters,
+                                            const uint8_t* pool, CondOut& out, bool& unsupported) {
+  return eval_condition_inl(pc, code, doc, n, consts, queries, filters, pool, out, unsupported);
 }
 
 // ------------------------------------------------------------------------------ merge

@@ -115,8 +115,7 @@ constexpr int FM_STRIDE = 3 * FM_WORDS + 1;   // odd stride: lanes at the same o
 // VM reads its document token by token (dependent byte loads), which from HBM costs a memory
 // latency per token; the staging copy issues all of its 8-byte loads back to back instead.
 constexpr int CD_BYTES = (FM_STRIDE - 1) * 4;  // [u32 len][document] of documents <= 140 bytes
-__device__ __forceinline__ const uint8_t* stage_doc(const uint8_t* pp, uint32_t len, uint32_t* slot) {
-  if (slot == nullptr || len + 4 > (uint32_t)CD_BYTES) return pp + 4;
+__device__ __forceinline__ void stage_copy(const uint8_t* pp, uint32_t len, uint32_t* slot) {
   const uint2* g = (const uint2*)pp;  // arena blobs are 8-aligned and padded to 8 bytes
   const uint32_t n8 = (len + 4 + 7) / 8;
 #pragma unroll 1
@@ -129,6 +128,10 @@ __device__ __forceinline__ const uint8_t* stage_doc(const uint8_t* pp, uint32_t 
     for (uint32_t k = 0; k < 8; k++)
       if (c + k < n8) { slot[2 * (c + k)] = v[k].x; slot[2 * (c + k) + 1] = v[k].y; }
   }
+}
+__device__ __forceinline__ const uint8_t* stage_doc(const uint8_t* pp, uint32_t len, uint32_t* slot) {
+  if (slot == nullptr || len + 4 > (uint32_t)CD_BYTES) return pp + 4;
+  stage_copy(pp, len, slot);
   return (const uint8_t*)slot + 4;
 }
 
@@ -1122,6 +1125,29 @@ __global__ void __launch_bounds__(256) k_traj_commit(TrajParams P) {
 //   k_cls_scan      per class: exclusive prefix of the workgroup counts
 //   k_cls_perm      per group and class: instances before the group; emit slot -> instance
 //   k_traj<TRACE, CLS> one lane per class: per-generation counts and merge bounds of its representative
+// outcome key of one CREATE payload: every split of the model, digit = first true condition / none / error
+template <bool INL>
+__device__ __forceinline__ uint32_t outcome_key(const TrajParams& P, const uint8_t* doc, uint32_t len) {
+  uint32_t key = 0;
+  for (int k = 0; k < P.nsplits; k++) {
+    const ElemCtl el = elem_ctl(P, P.split_elem[k]);
+    const uint32_t cc = el.cond_count();
+    uint32_t o = cc;
+    for (uint32_t c = 0; c < cc; c++) {
+      CondOut co{0, 0, 0, 0};
+      bool unsup = false;
+      const uint16_t flow = K(P.cond_flows)[el.cond_begin() + c];
+      const uint32_t prog = K(P.elems)[flow].cond_prog;
+      const bool res = INL ? eval_condition_inl(prog, P.code, doc, len, P.consts, P.queries, P.filters, P.pool, co, unsup)
+                           : eval_condition(prog, P.code, doc, len, P.consts, P.queries, P.filters, P.pool, co, unsup);
+      if (unsup || co.err) { o = cc + 1; break; }
+      if (res) { o = c; break; }
+    }
+    key += o * P.split_stride[k];
+  }
+  return key;
+}
+
 __global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
   __shared__ uint32_t s_doc[TWG * FM_STRIDE];
   __shared__ uint32_t s_hist[256], s_rep[256];
@@ -1136,22 +1162,12 @@ __global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
     const uint32_t ref = P.log[P.log_base + i].payload;
     const uint8_t* pp = P.arena + (uint64_t)ref * 8;
     const uint32_t len = *(const uint32_t*)pp;
-    const uint8_t* doc = stage_doc(pp, len, s_doc + t * FM_STRIDE);
-    uint32_t key = 0;
-    for (int k = 0; k < P.nsplits; k++) {
-      const ElemCtl el = elem_ctl(P, P.split_elem[k]);
-      const uint32_t cc = el.cond_count();
-      uint32_t o = cc;
-      for (uint32_t c = 0; c < cc; c++) {
-        CondOut co{0, 0, 0, 0};
-        bool unsup = false;
-        const uint16_t flow = K(P.cond_flows)[el.cond_begin() + c];
-        const bool res = eval_condition(K(P.elems)[flow].cond_prog, P.code, doc, len, P.consts, P.queries,
-                                        P.filters, P.pool, co, unsup);
-        if (unsup || co.err) { o = cc + 1; break; }
-        if (res) { o = c; break; }
-      }
-      key += o * P.split_stride[k];
+    uint32_t key;
+    if (len + 4 <= (uint32_t)CD_BYTES) {  // the VM inlined on the LDS copy (LDS loads per token)
+      stage_copy(pp, len, s_doc + t * FM_STRIDE);
+      key = outcome_key<true>(P, (const uint8_t*)(s_doc + t * FM_STRIDE) + 4, len);
+    } else {
+      key = outcome_key<false>(P, pp + 4, len);
     }
     P.ikey[i] = (uint8_t)key;
     atomicAdd(&s_hist[key & 255], 1u);
