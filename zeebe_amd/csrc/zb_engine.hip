@@ -146,8 +146,8 @@ struct zb_engine {
   ClsPlan* c_plan = nullptr;
   uint64_t cls_cap = 0;           // instances the class buffers hold
   uint8_t* c_ikey = nullptr;
-  uint32_t *c_khist = nullptr, *c_krep = nullptr;  // [256] each (one allocation with c_klen)
-  uint64_t* c_klen = nullptr;                       // [256]
+  uint32_t *c_khist = nullptr, *c_krep = nullptr;  // [CLS_HB][256] each (one allocation with c_klen)
+  uint64_t* c_klen = nullptr;                       // [CLS_HB][256]
   TmplRec* t_tmpl = nullptr;     // [CLS_MAX][CLS_ROW][TF] traced records (uniform / class batches)
   uint32_t* t_cstat = nullptr;   // [CLS_MAX][TSTAT]
   uint64_t* c_mask = nullptr;
@@ -294,9 +294,9 @@ int grow_class_buffers(zb_engine* e, uint64_t n, uint64_t nwg) {
   e->cls_cap = 0;
   const uint64_t groups = nwg * (TRAJ_WG / 64);
   HIPCHECK(e, hipMalloc(&e->c_ikey, n));
-  HIPCHECK(e, hipMalloc(&e->c_khist, 512 * sizeof(uint32_t) + 256 * sizeof(uint64_t)));
-  e->c_krep = e->c_khist + 256;
-  e->c_klen = (uint64_t*)(e->c_khist + 512);
+  HIPCHECK(e, hipMalloc(&e->c_khist, CLS_HB * 256 * (2 * sizeof(uint32_t) + sizeof(uint64_t))));
+  e->c_krep = e->c_khist + CLS_HB * 256;
+  e->c_klen = (uint64_t*)(e->c_khist + 2 * CLS_HB * 256);
   HIPCHECK(e, hipMalloc(&e->c_mask, groups * CLS_MAX * sizeof(uint64_t)));
   HIPCHECK(e, hipMalloc(&e->c_woffw, groups * CLS_MAX * sizeof(uint32_t)));
   HIPCHECK(e, hipMalloc(&e->c_wgcnt, nwg * CLS_MAX * sizeof(uint32_t)));
@@ -391,9 +391,9 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
     p.wgcnt = e->c_wgcnt;
     p.wgoff = e->c_wgoff;
     p.perm = e->c_perm;
-    HIPCHECK(e, hipMemsetAsync(e->c_khist, 0, 256 * sizeof(uint32_t), e->stream));
-    HIPCHECK(e, hipMemsetAsync(e->c_klen, 0, 256 * sizeof(uint64_t), e->stream));
-    HIPCHECK(e, hipMemsetAsync(e->c_krep, 0xff, 256 * sizeof(uint32_t), e->stream));
+    HIPCHECK(e, hipMemsetAsync(e->c_khist, 0, CLS_HB * 256 * sizeof(uint32_t), e->stream));
+    HIPCHECK(e, hipMemsetAsync(e->c_klen, 0, CLS_HB * 256 * sizeof(uint64_t), e->stream));
+    HIPCHECK(e, hipMemsetAsync(e->c_krep, 0xff, CLS_HB * 256 * sizeof(uint32_t), e->stream));
   }
   p.agg = e->t_agg;
   p.wcount = e->t_wcount;

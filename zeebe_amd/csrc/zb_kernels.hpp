@@ -202,6 +202,7 @@ constexpr int CLS_MAX = 8;          // trajectory classes of a class batch
 constexpr int CLS_MAX_SPLITS = 8;   // exclusive splits a class key covers
 constexpr int CLS_ROW = 4096;       // agg / mgen row of one class (>= generations of a batch)
 constexpr int CLS_BLK_WG = 16;      // instance workgroups per emit block (class segments per block)
+constexpr int CLS_HB = 64;          // key histogram banks (workgroup b adds into bank b % CLS_HB)
 
 // One record of a traced trajectory (uniform / class batch), with symbolic keys and payload refs that
 // the template emit pass (k_tmpl) resolves per instance: keys SYMK_WF / SYMK_JOB | generation << 4 |
@@ -286,8 +287,8 @@ struct TrajParams {
   uint32_t split_elem[CLS_MAX_SPLITS], split_stride[CLS_MAX_SPLITS];
   ClsPlan* plan;
   uint8_t* ikey;         // [n] outcome key of every instance
-  uint32_t* khist;       // [256] instances per key
-  uint32_t* krep;        // [256] first instance per key
+  uint32_t* khist;       // [CLS_HB][256] instances per key
+  uint32_t* krep;        // [CLS_HB][256] first instance per key
   uint64_t* cmask;       // [n / 64][CLS_MAX] per 64-instance group: ballot of the instances of class c
   uint32_t* woffw;       // [n / 64][CLS_MAX] instances of class c before the group
   uint32_t* wgcnt;       // [CLS_MAX][nwg] instances of class c in workgroup b
@@ -296,7 +297,7 @@ struct TrajParams {
   uint32_t* segs;        // [nblk][CLS_MAX] first emit slot of the class-c segment of block b
   uint32_t* wcls;        // [slots / 64] class of every emit wave
   int32_t nblk, pad4;    // blocks of CLS_BLK_WG instance workgroups
-  uint64_t* klen;        // [256] CREATE payload bytes per key
+  uint64_t* klen;        // [CLS_HB][256] CREATE payload bytes per key
   TmplRec* tmpl;         // [CLS_MAX][CLS_ROW][TF] traced records per class and generation
   uint32_t* cstat;       // [CLS_MAX][TSTAT] traced statistics per class
 };

@@ -1125,8 +1125,88 @@ __global__ void __launch_bounds__(256) k_traj_commit(TrajParams P) {
 //   k_cls_scan      per class: exclusive prefix of the workgroup counts
 //   k_cls_perm      per group and class: instances before the group; emit slot -> instance
 //   k_traj<TRACE, CLS> one lane per class: per-generation counts and merge bounds of its representative
+// load_operand (zb_devlib.hpp) for the sweep below: constants and query descriptors through the scalar
+// cache; only the [ROOT, MAP_KEY] fast query form (any other path -> unsupported: the batch takes the
+// per-instance path, which runs the general json-path executor).
+__device__ __forceinline__ bool load_operand_k(const TrajParams& P, bool is_path, uint32_t idx, const uint8_t* doc,
+                                               uint32_t n, Operand& o, CondOut& out, bool& unsupported) {
+  if (!is_path) {
+    const DevConst c = kload(P.consts, idx);
+    o.type = c.type; o.bval = c.bval; o.ival = c.ival; o.fval = c.fval; o.s = P.pool + c.str_off; o.slen = c.str_len;
+    return true;
+  }
+  const DevQuery q = kload(P.queries, idx);
+  if (!q.fast) { unsupported = true; return false; }
+  const DevFilter f = kload(P.filters, q.first + 1);
+  QueryResult r;
+  if (!query_fast(doc, n, P.pool + f.key_off, f.key_len, r)) { unsupported = true; return false; }
+  if (r.count == 0) { out.err = EC_PATH_NO_RESULT; out.q = (uint16_t)idx; return false; }
+  if (r.count > 1) { out.err = EC_PATH_MULTI; out.q = (uint16_t)idx; return false; }
+  Tok t;
+  if (!read_tok(doc + r.pos, r.len, t)) { unsupported = true; return false; }
+  o.type = t.type; o.bval = t.bval; o.ival = t.ival; o.fval = t.fval;
+  o.s = doc + r.pos + t.hdr; o.slen = t.len;
+  return true;
+}
+
+// The json-el VM (eval_condition, zb_devlib.hpp) as one wave-uniform sweep over the program: every lane
+// runs the same program and its jumps only go forward (zb_model.cpp emit), so instruction pc is
+// fetched once per wave through the scalar cache and executed by the lanes whose own pc is there.
+// Same results, errors and short-circuit behaviour as eval_condition.
+__device__ __forceinline__ bool eval_condition_sweep(const TrajParams& P, uint32_t pc0, const uint8_t* doc, uint32_t n,
+                                                     CondOut& out, bool& unsupported) {
+  bool r = false, done = false;
+  uint32_t mine = pc0;
+  out.err = 0;
+  for (uint32_t pc = pc0; pc < pc0 + 4096; pc++) {
+    const uint32_t w0 = K(P.code)[2 * pc], w1 = K(P.code)[2 * pc + 1];
+    const uint32_t opc = w0 & 0xff;
+    if (opc == PC_END) return done ? false : r;
+    if (done || mine != pc) continue;
+    if (opc == PC_JF || opc == PC_JT) {
+      mine = (opc == PC_JF ? !r : r) ? (w0 >> 16) : pc + 1;
+      continue;
+    }
+    mine = pc + 1;
+    const uint32_t op = (w0 >> 8) & 0xf;
+    Operand x, y;
+    if (!load_operand_k(P, (w0 >> 12) & 1, w1 & 0xffff, doc, n, x, out, unsupported) ||
+        !load_operand_k(P, (w0 >> 13) & 1, w1 >> 16, doc, n, y, out, unsupported)) {
+      done = true;
+      continue;
+    }
+    if (op == OP_EQ || op == OP_NE) {
+      bool eq = false;
+      if (x.type == TT_NIL) eq = y.type == TT_NIL;
+      else if (y.type == TT_NIL) eq = false;
+      else {
+        if (!same_type(x, y, out)) { done = true; continue; }
+        switch (x.type) {
+          case TT_STRING: eq = x.slen == y.slen && bytes_eq(x.s, y.s, x.slen); break;
+          case TT_BOOLEAN: eq = x.bval == y.bval; break;
+          case TT_INTEGER: eq = x.ival == y.ival; break;
+          case TT_FLOAT: eq = x.fval == y.fval; break;
+          default: out.err = EC_CMP_TYPE; out.a = x.type; done = true; continue;
+        }
+      }
+      r = (op == OP_EQ) ? eq : !eq;
+    } else {
+      if (!same_type(x, y, out)) { done = true; continue; }
+      if (x.type != TT_INTEGER && x.type != TT_FLOAT) { out.err = EC_NOT_NUMBER; out.a = x.type; done = true; continue; }
+      if (x.type == TT_INTEGER) {
+        r = op == OP_LT ? x.ival < y.ival : op == OP_LE ? x.ival <= y.ival : op == OP_GT ? x.ival > y.ival
+                                                                                       : x.ival >= y.ival;
+      } else {
+        r = op == OP_LT ? x.fval < y.fval : op == OP_LE ? x.fval <= y.fval : op == OP_GT ? x.fval > y.fval
+                                                                                       : x.fval >= y.fval;
+      }
+    }
+  }
+  unsupported = true;
+  return false;
+}
+
 // outcome key of one CREATE payload: every split of the model, digit = first true condition / none / error
-template <bool INL>
 __device__ __forceinline__ uint32_t outcome_key(const TrajParams& P, const uint8_t* doc, uint32_t len) {
   uint32_t key = 0;
   for (int k = 0; k < P.nsplits; k++) {
@@ -1138,8 +1218,7 @@ __device__ __forceinline__ uint32_t outcome_key(const TrajParams& P, const uint8
       bool unsup = false;
       const uint16_t flow = K(P.cond_flows)[el.cond_begin() + c];
       const uint32_t prog = K(P.elems)[flow].cond_prog;
-      const bool res = INL ? eval_condition_inl(prog, P.code, doc, len, P.consts, P.queries, P.filters, P.pool, co, unsup)
-                           : eval_condition(prog, P.code, doc, len, P.consts, P.queries, P.filters, P.pool, co, unsup);
+      const bool res = eval_condition_sweep(P, prog, doc, len, co, unsup);
       if (unsup || co.err) { o = cc + 1; break; }
       if (res) { o = c; break; }
     }
@@ -1148,8 +1227,9 @@ __device__ __forceinline__ uint32_t outcome_key(const TrajParams& P, const uint8
   return key;
 }
 
+constexpr int CL_STRIDE = 25;  // classify: per-thread document slot, [u32 len][document <= 96 bytes], odd stride
 __global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
-  __shared__ uint32_t s_doc[TWG * FM_STRIDE];
+  __shared__ uint32_t s_doc[TWG * CL_STRIDE];
   __shared__ uint32_t s_hist[256], s_rep[256];
   __shared__ unsigned long long s_len[256];
   const int t = threadIdx.x;
@@ -1162,12 +1242,14 @@ __global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
     const uint32_t ref = P.log[P.log_base + i].payload;
     const uint8_t* pp = P.arena + (uint64_t)ref * 8;
     const uint32_t len = *(const uint32_t*)pp;
-    uint32_t key;
-    if (len + 4 <= (uint32_t)CD_BYTES) {  // the VM inlined on the LDS copy (LDS loads per token)
-      stage_copy(pp, len, s_doc + t * FM_STRIDE);
-      key = outcome_key<true>(P, (const uint8_t*)(s_doc + t * FM_STRIDE) + 4, len);
+    // the VM inlined on the LDS copy (LDS loads per token); a document too large for the copy gets the
+    // error outcome at every split (its class, when it reaches one, sends the batch to the per-instance path)
+    uint32_t key = 0;
+    if (((len + 11) & ~7u) <= CL_STRIDE * 4) {  // (stage_copy writes whole 8-byte words)
+      stage_copy(pp, len, s_doc + t * CL_STRIDE);
+      key = outcome_key(P, (const uint8_t*)(s_doc + t * CL_STRIDE) + 4, len);
     } else {
-      key = outcome_key<false>(P, pp + 4, len);
+      for (int k = 0; k < P.nsplits; k++) key += (elem_ctl(P, P.split_elem[k]).cond_count() + 1) * P.split_stride[k];
     }
     P.ikey[i] = (uint8_t)key;
     atomicAdd(&s_hist[key & 255], 1u);
@@ -1176,9 +1258,11 @@ __global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
   }
   __syncthreads();
   if (s_hist[t]) {
-    atomicAdd(&P.khist[t], s_hist[t]);
-    atomicMin(&P.krep[t], s_rep[t]);
-    atomicAdd((unsigned long long*)&P.klen[t], s_len[t]);
+    // banked: same-address atomics from every workgroup would serialize at the memory side
+    const uint32_t hb = (blockIdx.x % CLS_HB) * 256 + t;
+    atomicAdd(&P.khist[hb], s_hist[t]);
+    atomicMin(&P.krep[hb], s_rep[t]);
+    atomicAdd((unsigned long long*)&P.klen[hb], s_len[t]);
   }
 }
 
@@ -1186,7 +1270,13 @@ __global__ void __launch_bounds__(256) k_cls_plan(TrajParams P) {
   __shared__ uint32_t s_w[4];
   ClsPlan* pl = P.plan;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const uint32_t cnt = P.khist[t];
+  uint32_t cnt = 0, rep = 0xffffffffu;
+  uint64_t lsum = 0;
+  for (int b = 0; b < CLS_HB; b++) {
+    cnt += P.khist[b * 256 + t];
+    rep = min(rep, P.krep[b * 256 + t]);
+    lsum += P.klen[b * 256 + t];
+  }
   const uint64_t m = __ballot(cnt > 0);
   if (lane == 0) s_w[wv] = (uint32_t)__builtin_popcountll(m);
   __syncthreads();
@@ -1197,8 +1287,8 @@ __global__ void __launch_bounds__(256) k_cls_plan(TrajParams P) {
   if (cnt > 0 && cid < CLS_MAX) {
     pl->key[cid] = (uint32_t)t;
     pl->n[cid] = cnt;
-    pl->rep[cid] = P.krep[t];
-    pl->lensum[cid] = P.klen[t];
+    pl->rep[cid] = rep;
+    pl->lensum[cid] = lsum;
   }
   __syncthreads();
   if (t == 0) {
