@@ -23,9 +23,10 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BYTES_PER_TRANSITION = 96  # 32 B row read + 32 B row write + 32 B record descriptor
-# HBM bytes of the emit kernel from the committed rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE: separate
-# runs of this script with --steps 1; see profiles/r01/pmc_v4.json for the command and the gfx950 correction)
-PMC_FILE = os.path.join(ROOT, "profiles", "r01", "pmc_v4.json")
+DESC_BYTES = 32  # one zb_rec descriptor written per log record
+# HBM bytes of the main emit kernel from the committed rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE: separate
+# runs of this script with --steps 1; tools/pmc_summary.py writes the file with the gfx950 correction)
+PMC_FILE = os.path.join(ROOT, "profiles", "r01", "pmc_v5.json")
 
 
 def parse():
@@ -117,13 +118,15 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    tot = dict(transitions=0, completed=0, kernel_ms=0.0, process_ms=0.0, emit_ms=0.0, aux_ms=0.0, launches=0, waves=0, merge_bytes=0, cond_bytes=0,
+    tot = dict(main_ms=0.0, written=0, transitions=0, completed=0, kernel_ms=0.0, process_ms=0.0, emit_ms=0.0, aux_ms=0.0, launches=0, waves=0, merge_bytes=0, cond_bytes=0,
                records=0, path=0)
     for _ in range(a.steps):
         st = one_step()
         tot["transitions"] += st["transitions"]
         tot["completed"] += st["completed_instances"]
         tot["kernel_ms"] += st["wave_kernel_ms"]
+        tot["main_ms"] += st["main_emit_kernel_ms"]
+        tot["written"] += st["records_written"]
         tot["process_ms"] += st["process_kernel_ms"]
         tot["emit_ms"] += st["emit_kernel_ms"]
         tot["aux_ms"] += st["aux_kernel_ms"]
@@ -148,15 +151,23 @@ def main():
     else:
         all_transitions, all_completed = float(tot["transitions"]), float(tot["completed"])
 
-    traffic = None
+    traffic, pmc_kernel = None, None
     if n == 1_000_000 and a.tasks == 20 and os.path.exists(PMC_FILE):
         with open(PMC_FILE) as f:
-            traffic = json.load(f)["emit_traffic_bytes"]
+            pmc = json.load(f)
+        traffic, pmc_kernel = pmc["main_traffic_bytes"], pmc["main_kernel"]
 
     if rank == 0:
+        # path level (SURVEY §8d model): 96 B per transition + merge + condition bytes over every kernel of a step
         alg_bytes = BYTES_PER_TRANSITION * tot["transitions"] + tot["merge_bytes"] + tot["cond_bytes"]
         kernel_s = tot["kernel_ms"] / 1e3
-        achieved = alg_bytes / kernel_s / 1e9 if kernel_s > 0 else 0.0
+        path_achieved = alg_bytes / kernel_s / 1e9 if kernel_s > 0 else 0.0
+        # dominant kernel (the main emit launch, ~80% of device time): per launch it writes every record
+        # descriptor of the batch and performs every output merge (reads job + scope documents, writes the
+        # result) and condition evaluation; one launch per step
+        main_bytes = DESC_BYTES * tot["written"] + tot["merge_bytes"] + tot["cond_bytes"]
+        main_s = tot["main_ms"] / 1e3
+        achieved = main_bytes / main_s / 1e9 if main_s > 0 else path_achieved
         out = {
             "metric": "BPMN element transitions/sec (+ completed instances/sec) per node; % HBM roofline",
             "value": all_transitions / elapsed,
@@ -180,15 +191,20 @@ def main():
             "kernel_ms_per_step": {"total": tot["kernel_ms"] / a.steps, "process_or_count": tot["process_ms"] / a.steps,
                                    "scan_emit": tot["emit_ms"] / a.steps, "aux": tot["aux_ms"] / a.steps},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_note": "HBM bytes per launch of the emit kernel (FETCH_SIZE x2 + WRITE_SIZE, "
-                                         "profiles/r01/pmc_v4.json); below the algorithmic bytes because element "
-                                         "instances stay in registers instead of SoA rows",
-                         "kernel": "zbg::k_traj (count + emit passes)" if tot["path"] in (1, 2) else
-                                   "zbg::k_process/k_scan/k_emit/k_merge", "launches": tot["launches"],
-                         "avg_launch_us": tot["kernel_ms"] * 1e3 / max(tot["launches"], 1),
-                         "alg_bytes_per_transition": BYTES_PER_TRANSITION,
-                         "alg_bytes_total": alg_bytes},
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic,
+                         "traffic_note": "HBM bytes per launch of %s (FETCH_SIZE x2 + WRITE_SIZE, separate "
+                                         "rocprofv3 --pmc passes, profiles/r01/pmc_v5.json)" % pmc_kernel,
+                         "kernel": {0: "zbg::k_emit (wave pipeline)", 1: "zbg::k_tmpl<false,false> (template emit)",
+                                    2: "zbg::k_tmpl<true,false> (class-batch emit)"}.get(tot["path"], "?"),
+                         "launches": a.steps, "avg_launch_us": tot["main_ms"] * 1e3 / a.steps,
+                         "alg_bytes_per_launch": main_bytes / a.steps,
+                         "alg_bytes_model": "32 B descriptor per record written + merge (job+scope+result) bytes "
+                                            "+ condition payload bytes"},
+            "path_roofline": {"achieved": path_achieved, "frac": path_achieved / HBM_PEAK_GBS, "unit": "GB/s",
+                              "kernels": "every kernel of a step (count, scan, emit, commit)",
+                              "kernel_launches": tot["launches"],
+                              "alg_bytes_per_transition": BYTES_PER_TRANSITION, "alg_bytes_total": alg_bytes},
         }
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.cpu_sample, a.tasks)

@@ -106,6 +106,8 @@ typedef struct zb_step_stats {
   double aux_kernel_ms;        /* k_merge + k_cond share */
   uint64_t path;               /* 0: wave pipeline, 1: trajectory path (zb_traj.hip) ran the step,
                                   2: trajectory path as a class batch (k_cls_*: split outcomes fixed at creation) */
+  double main_emit_kernel_ms;  /* trajectory path: the main emit launch alone (k_tmpl / k_traj<emit>), the
+                                  dominant kernel priced by bench.py's roofline; 0 on the wave pipeline */
 } zb_step_stats;
 
 /* One partition-to-partition command (SubscriptionCommandSender.java:83-128), 256 bytes, exchanged

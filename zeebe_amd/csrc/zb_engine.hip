@@ -419,7 +419,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   else launch_traj_count(p, e->stream);
   HIPCHECK(e, hipEventRecord(ev[1], e->stream));
   launch_traj_scan(p, e->stream);
-  launch_traj_emit(p, e->stream);
+  launch_traj_emit(p, e->stream, &ev[3]);
   HIPCHECK(e, hipEventRecord(ev[2], e->stream));
   HIPCHECK(e, hipGetLastError());
   HIPCHECK(e, hipMemcpyAsync(e->h_ctl_pinned, e->t_ctl, sizeof(TrajCtl), hipMemcpyDeviceToHost, e->stream));
@@ -427,9 +427,11 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
                              e->stream));
   HIPCHECK(e, hipMemcpyAsync(e->h_err_pinned, e->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
-  float ms0 = 0, ms1 = 0;
+  float ms0 = 0, ms1 = 0, ms_main = 0;
   HIPCHECK(e, hipEventElapsedTime(&ms0, ev[0], ev[1]));
   HIPCHECK(e, hipEventElapsedTime(&ms1, ev[1], ev[2]));
+  HIPCHECK(e, hipEventElapsedTime(&ms_main, ev[3], ev[4]));
+  st.main_emit_kernel_ms += ms_main;
   st.process_kernel_ms += ms0;
   st.emit_kernel_ms += ms1;
   st.wave_kernel_ms += ms0 + ms1;

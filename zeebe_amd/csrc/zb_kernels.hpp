@@ -306,6 +306,7 @@ void launch_traj_count(const TrajParams& p, hipStream_t stream);
 void launch_traj_count_uniform(const TrajParams& p, hipStream_t stream);
 void launch_traj_count_classes(const TrajParams& p, hipStream_t stream);
 void launch_traj_scan(const TrajParams& p, hipStream_t stream);
-void launch_traj_emit(const TrajParams& p, hipStream_t stream);
+// ev_main (optional, 2 events): recorded around the main emit launch only
+void launch_traj_emit(const TrajParams& p, hipStream_t stream, hipEvent_t* ev_main = nullptr);
 
 }  // namespace zbg

@@ -1621,23 +1621,34 @@ void launch_traj_scan(const TrajParams& p, hipStream_t s) {
   if (!p.uni && !p.cls) hipLaunchKernelGGL(k_traj_scan, dim3(p.wcap), dim3(1024), 0, s, p);
   hipLaunchKernelGGL(k_traj_base, dim3(1), dim3(1024), 0, s, p);
 }
-void launch_traj_emit(const TrajParams& p, hipStream_t s) {
+void launch_traj_emit(const TrajParams& p, hipStream_t s, hipEvent_t* ev_main) {
   const dim3 g(p.nwg), b(TWG);
+  auto mark = [&](int i) {
+    if (ev_main) (void)hipEventRecord(ev_main[i], s);
+  };
   if (p.cls) {
     const dim3 ge(p.nwg_e);
+    mark(0);
     hipLaunchKernelGGL((k_tmpl<true, false>), ge, b, 0, s, p);
+    mark(1);
     hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
     hipLaunchKernelGGL((k_tmpl<true, true>), ge, b, 0, s, p);
   } else if (p.uni) {
+    mark(0);
     hipLaunchKernelGGL((k_tmpl<false, false>), g, b, 0, s, p);
+    mark(1);
     hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
     hipLaunchKernelGGL((k_tmpl<false, true>), g, b, 0, s, p);
   } else if (p.cond) {
+    mark(0);
     hipLaunchKernelGGL((k_traj<true, false, true, false, false, false>), g, b, 0, s, p);
+    mark(1);
     hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
     hipLaunchKernelGGL((k_traj<true, false, true, true, false, false>), g, b, 0, s, p);
   } else {
+    mark(0);
     hipLaunchKernelGGL((k_traj<true, false, false, false, false, false>), g, b, 0, s, p);
+    mark(1);
     hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
     hipLaunchKernelGGL((k_traj<true, false, false, true, false, false>), g, b, 0, s, p);
   }

@@ -55,7 +55,7 @@ class zb_step_stats(ctypes.Structure):
                 ("condition_payload_bytes", ctypes.c_uint64), ("wave_kernel_ms", ctypes.c_double),
                 ("wall_ms", ctypes.c_double), ("process_kernel_ms", ctypes.c_double),
                 ("emit_kernel_ms", ctypes.c_double), ("aux_kernel_ms", ctypes.c_double),
-                ("path", ctypes.c_uint64)]
+                ("path", ctypes.c_uint64), ("main_emit_kernel_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
