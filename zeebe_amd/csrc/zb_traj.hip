@@ -107,9 +107,9 @@ enum TrajFlags : uint8_t {
 enum TrajErr : uint32_t { TE_FALLBACK = 1u, TE_REGEN = 1u << 30 };
 
 // flat-merge staging in LDS (emit pass): per thread the two input blobs and the output blob
-constexpr int FM_WORDS = 12;                  // 48-byte blob slots: documents of <= 44 bytes
+constexpr int FM_WORDS = 9;                   // 36-byte blob slots (LDS per workgroup sets occupancy: 5 workgroups per CU)
 constexpr int FM_BYTES = FM_WORDS * 4;
-constexpr int FM_STRIDE = 3 * FM_WORDS + 1;   // odd stride: lanes at the same offset hit distinct banks
+constexpr int FM_STRIDE = 3 * FM_WORDS + 2;   // odd stride: lanes at the same offset hit distinct banks
 
 // Condition documents are staged into the same per-thread LDS slot before the json-el VM runs: the
 // VM reads its document token by token (dependent byte loads), which from HBM costs a memory
