@@ -107,9 +107,18 @@ enum TrajFlags : uint8_t {
 enum TrajErr : uint32_t { TE_FALLBACK = 1u, TE_REGEN = 1u << 30 };
 
 // flat-merge staging in LDS (emit pass): per thread the two input blobs and the output blob
-constexpr int FM_WORDS = 9;                   // 36-byte blob slots (LDS per workgroup sets occupancy: 5 workgroups per CU)
+constexpr int FM_WORDS = 12;                  // 48-byte blob slots: documents of <= 44 bytes
 constexpr int FM_BYTES = FM_WORDS * 4;
-constexpr int FM_STRIDE = 3 * FM_WORDS + 2;   // odd stride: lanes at the same offset hit distinct banks
+constexpr int FM_STRIDE = 3 * FM_WORDS + 1;   // odd stride: lanes at the same offset hit distinct banks
+// Template emit (k_tmpl) packs the two inputs back to back: with ns + nt <= 4 * OUT_WORDS - 7 they take
+// <= (ns + nt + 14) / 4 words. Uniform batches keep a 36-byte output blob (10 + 9 = 19 words per thread,
+// odd: distinct banks; 19.5 KB per workgroup, eight workgroups per CU); class batches, whose CREATE
+// payloads are larger, keep the 48-byte blob (13 + 12 = 25 words, six workgroups per CU).
+template <bool CLS> struct TmLayout {
+  static constexpr int OUT_WORDS = CLS ? 12 : 9;
+  static constexpr int IN_WORDS = (4 * OUT_WORDS - 7 + 14) / 4;
+  static constexpr int STRIDE = IN_WORDS + OUT_WORDS;
+};
 
 // Condition documents are staged into the same per-thread LDS slot before the json-el VM runs: the
 // VM reads its document token by token (dependent byte loads), which from HBM costs a memory
@@ -588,9 +597,13 @@ __device__ __forceinline__ void block_scan2(uint64_t& a, uint64_t& b, uint64_t& 
 // Default output merge of the documents behind refs src (job / message payload) and tgt (scope payload)
 // into the blob at arena byte offset at (capacity m_len): LDS-staged flat-map fast path; a non-flat
 // document sets TE_REGEN (first pass) or runs the general indexer / merger (GEN rerun).
-template <bool GEN>
+// PK_OUT / PK_IN != 0: packed layout (inputs back to back in PK_IN words, output blob of PK_OUT words)
+template <bool GEN, int PK_OUT = 0, int PK_IN = 0>
 __device__ __forceinline__ void merge_into(const TrajParams& P, uint32_t src, uint32_t tgt, uint32_t m_len, uint64_t at,
                                            uint32_t* reg, uint32_t& err, uint32_t& ns, uint32_t& nt, uint32_t& olen) {
+  constexpr bool PACKED = PK_OUT != 0;
+  constexpr uint32_t OUT_BYTES = PACKED ? 4 * PK_OUT : FM_BYTES;
+  constexpr uint32_t OUT_OFF = PACKED ? PK_IN : 2 * FM_WORDS;
   const uint32_t* gs = (const uint32_t*)(P.arena + (uint64_t)src * 8);
   const uint32_t* gt = (const uint32_t*)(P.arena + (uint64_t)tgt * 8);
   ns = gs[0];
@@ -598,16 +611,16 @@ __device__ __forceinline__ void merge_into(const TrajParams& P, uint32_t src, ui
   uint32_t* gd = (uint32_t*)(P.arena + at);
   olen = 0;
   bool done = false;
-  if (ns + nt + 3 <= FM_BYTES - 4) {
+  if (ns + nt + 3 <= OUT_BYTES - 4) {
     // flat fast path on LDS copies of the two documents
+    const uint32_t ws = PACKED ? (ns + 7) / 4 : FM_WORDS;
     for (uint32_t k = 0; k < (ns + 7) / 4; k++) reg[k] = gs[k];
-    for (uint32_t k = 0; k < (nt + 7) / 4; k++) reg[FM_WORDS + k] = gt[k];
-    uint8_t* lo = (uint8_t*)(reg + 2 * FM_WORDS);
-    done = merge_flat((const uint8_t*)reg + 4, ns, (const uint8_t*)(reg + FM_WORDS) + 4, nt, lo + 4, FM_BYTES - 4,
-                      olen);
+    for (uint32_t k = 0; k < (nt + 7) / 4; k++) reg[ws + k] = gt[k];
+    uint8_t* lo = (uint8_t*)(reg + OUT_OFF);
+    done = merge_flat((const uint8_t*)reg + 4, ns, (const uint8_t*)(reg + ws) + 4, nt, lo + 4, OUT_BYTES - 4, olen);
     if (done) {
-      reg[2 * FM_WORDS] = olen;
-      for (uint32_t k = 0; k < (olen + 7) / 4; k++) gd[k] = reg[2 * FM_WORDS + k];
+      reg[OUT_OFF] = olen;
+      for (uint32_t k = 0; k < (olen + 7) / 4; k++) gd[k] = reg[OUT_OFF + k];
     }
   } else {
     // larger flat documents: the same fast path straight on the arena
@@ -1471,7 +1484,8 @@ __device__ __forceinline__ int64_t tmpl_key(const TrajParams& P, const TmplLane&
 
 template <bool CLS, bool GEN>
 __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
-  __shared__ uint32_t s_merge[TWG * FM_STRIDE];
+  using TL = TmLayout<CLS>;
+  __shared__ uint32_t s_merge[TWG * TL::STRIDE];
   __shared__ uint64_t s_scan[TWG / 64][2];
   TrajCtl* ctl = P.ctl;
   if (ctl->flag) return;
@@ -1515,7 +1529,7 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
   uint32_t err = 0;
   uint64_t merge_bytes = 0;
   uint32_t pc_sym = PAY_CREATE, pc_ref = create_ref;  // last resolved payload symbol
-  uint32_t* reg = s_merge + threadIdx.x * FM_STRIDE;
+  uint32_t* reg = s_merge + threadIdx.x * TL::STRIDE;
 
 #pragma unroll 1
   for (int w = 0; w < W; w++) {
@@ -1549,7 +1563,7 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
         else if (at + g.stride > P.arena_cap) err |= DE_ARENA_FULL;
         else {
           uint32_t ns = 0, nt = 0, olen = 0;
-          merge_into<GEN>(P, src, tgt, m_len, at, reg, err, ns, nt, olen);
+          merge_into<GEN, TL::OUT_WORDS, TL::IN_WORDS>(P, src, tgt, m_len, at, reg, err, ns, nt, olen);
           merge_bytes += ns + nt + olen;
         }
       }
