@@ -26,7 +26,7 @@ BYTES_PER_TRANSITION = 96  # 32 B row read + 32 B row write + 32 B 
 DESC_BYTES = 32  # one zb_rec descriptor written per log record
 # HBM bytes of the main emit kernel from the committed rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE: separate
 # runs of this script with --steps 1; tools/pmc_summary.py writes the file with the gfx950 correction)
-PMC_FILE = os.path.join(ROOT, "profiles", "r01", "pmc_v5.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r01", "pmc_v7.json")
 
 
 def parse():
@@ -194,7 +194,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
                          "traffic_note": "HBM bytes per launch of %s (FETCH_SIZE x2 + WRITE_SIZE, separate "
-                                         "rocprofv3 --pmc passes, profiles/r01/pmc_v5.json)" % pmc_kernel,
+                                         "rocprofv3 --pmc passes, profiles/r01/pmc_v7.json)" % pmc_kernel,
                          "kernel": {0: "zbg::k_emit (wave pipeline)", 1: "zbg::k_tmpl<false,false> (template emit)",
                                     2: "zbg::k_tmpl<true,false> (class-batch emit)"}.get(tot["path"], "?"),
                          "launches": a.steps, "avg_launch_us": tot["main_ms"] * 1e3 / a.steps,
