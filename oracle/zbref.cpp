@@ -25,6 +25,7 @@
 //                            (JOB CREATE command at its FIFO position -> JOB CREATED(k), JOB COMPLETED(k); job keys
 //                            from KeyGenerator(2, 5))
 // Positions are log sequence numbers (0-based record index); byte positions of the real log are out of scope.
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <functional>
@@ -65,7 +66,11 @@ enum Step : uint8_t {
   S_NONE = 0, S_TAKE_SEQUENCE_FLOW, S_CONSUME_TOKEN, S_EXCLUSIVE_SPLIT, S_CREATE_JOB, S_APPLY_INPUT_MAPPING,
   S_APPLY_OUTPUT_MAPPING, S_ACTIVATE_GATEWAY, S_SUBSCRIBE_TO_INTERMEDIATE_MESSAGE, S_START_STATEFUL_ELEMENT,
   S_TRIGGER_END_EVENT, S_TRIGGER_START_EVENT, S_TERMINATE_CONTAINED_INSTANCES, S_TERMINATE_JOB_TASK,
-  S_TERMINATE_ELEMENT, S_PROPAGATE_TERMINATION, S_CANCEL_PROCESS, S_COMPLETE_PROCESS, S_UNBOUND = 255
+  S_TERMINATE_ELEMENT, S_PROPAGATE_TERMINATION, S_CANCEL_PROCESS, S_COMPLETE_PROCESS,
+  // EXTENSION (parity unpinned): the reference rejects parallel gateways at deployment
+  // (bpmn-model/.../validation/zeebe/FlowElementValidator.java:36-58); DESIGN.md §C4 defines these two.
+  S_PARALLEL_SPLIT, S_PARALLEL_MERGE,
+  S_UNBOUND = 255
 };
 
 static const bytes EMPTY_DOCUMENT = bytes("\x80", 1);
@@ -232,7 +237,9 @@ struct Record {
   WisValue wis;
   MsgSubValue msub;
   MessageValue msg;
+  bytes raw_value;  // submitted from outside (zbref_submit_record): the log keeps the bytes as written
   bytes encode_value() const {
+    if (!raw_value.empty()) return raw_value;
     switch (value_type) {
       case VT_WORKFLOW_INSTANCE: return wf.encode();
       case VT_JOB: return job.encode();
@@ -247,7 +254,7 @@ struct Record {
 
 // ------------------------------------------------------------------------------ executable model
 enum ElemKind : uint8_t { K_PROCESS, K_START_EVENT, K_END_EVENT, K_SERVICE_TASK, K_SUB_PROCESS,
-                          K_EXCLUSIVE_GATEWAY, K_INTERMEDIATE_CATCH, K_SEQUENCE_FLOW };
+                          K_EXCLUSIVE_GATEWAY, K_INTERMEDIATE_CATCH, K_SEQUENCE_FLOW, K_PARALLEL_GATEWAY };
 
 struct Element {
   ElemKind kind;
@@ -265,6 +272,7 @@ struct Element {
   bytes message_name;
   JsonPathQuery correlation_key;
   bool has_io_mapping = false;
+  int incoming = 0;                  // parallel gateway: sequence flows targeting it (join arity)
   uint8_t get_step(uint8_t intent) const {
     auto it = steps.find(intent);
     return it == steps.end() ? S_UNBOUND : it->second;
@@ -278,6 +286,7 @@ struct Workflow {
   std::vector<std::unique_ptr<Element>> storage;
   std::unordered_map<bytes, Element*> by_id;
   Element* process = nullptr;
+  bool has_parallel = false;
   Element* get(const bytes& id) const {
     auto it = by_id.find(id);
     return it == by_id.end() ? nullptr : it->second;
@@ -372,6 +381,7 @@ class Transformer {
         else if (nm == "serviceTask") k = K_SERVICE_TASK;
         else if (nm == "startEvent") k = K_START_EVENT;
         else if (nm == "subProcess") k = K_SUB_PROCESS;
+        else if (nm == "parallelGateway") k = K_PARALLEL_GATEWAY;  // EXTENSION (C4)
         else throw ZbError("unsupported element type: " + nm);  // factory lookup returns null (NPE)
         auto e = std::make_unique<Element>();
         e->kind = k;
@@ -413,6 +423,11 @@ class Transformer {
         step = S_START_STATEFUL_ELEMENT;
       else if (tgt->kind == K_EXCLUSIVE_GATEWAY) step = S_ACTIVATE_GATEWAY;
       else if (tgt->kind == K_END_EVENT) step = S_TRIGGER_END_EVENT;
+      else if (tgt->kind == K_PARALLEL_GATEWAY) {
+        // EXTENSION: a flow into a join (>= 2 incoming flows) is an arrival, else it activates the gateway
+        tgt->incoming = count_incoming(defs_, *tref);
+        step = tgt->incoming >= 2 ? S_PARALLEL_MERGE : S_ACTIVATE_GATEWAY;
+      }
       else throw ZbError("Unsupported element");
       e->steps[SEQUENCE_FLOW_TAKEN] = step;
       return;
@@ -454,6 +469,11 @@ class Transformer {
         first_has_cond = flow && !kids(flow, "conditionExpression").empty();
       }
       e->steps[GATEWAY_ACTIVATED] = first_has_cond ? S_EXCLUSIVE_SPLIT : current_outgoing_step_;
+    } else if (nm == "parallelGateway") {
+      // EXTENSION: GATEWAY_ACTIVATED forks one token per outgoing flow (>= 1 required)
+      if (kids(n, "outgoing").empty()) throw ZbError("parallel gateway without outgoing sequence flow");
+      e->steps[GATEWAY_ACTIVATED] = S_PARALLEL_SPLIT;
+      current_->has_parallel = true;
     } else if (nm == "serviceTask") {
       const XmlNode* td = ext(n, "taskDefinition");
       if (td) {
@@ -498,6 +518,16 @@ class Transformer {
     }
   }
 
+  static int count_incoming(const XmlNode* n, const std::string& id) {
+    int c = 0;
+    if (n->name == "sequenceFlow") {
+      const std::string* t = n->attr("targetRef");
+      if (t && *t == id) c++;
+    }
+    for (auto& k : n->children) c += count_incoming(k.get(), id);
+    return c;
+  }
+
   static const XmlNode* find_by_id(const XmlNode* n, const std::string& id) {
     const std::string* a = n->attr("id");
     if (a && *a == id) return n;
@@ -515,6 +545,9 @@ struct ElementInstance {  // ElementInstance.java:30-111
   WfValue value;
   std::vector<ElementInstance*> children;
   int64_t job_key = 0;
+  // EXTENSION (C4): live tokens of a scope and arrivals per parallel join
+  int32_t tokens = 0;
+  std::map<const void*, int32_t> joins;
 };
 
 struct ElementInstanceIndex {  // ElementInstanceIndex.java:25-65
@@ -590,6 +623,9 @@ class Engine {
   std::map<std::pair<int64_t, bytes>, bytes> job_payloads;  // (workflow key, activity id) -> completion payload
   int64_t created = 0, completed = 0, canceled = 0;
   size_t processed = 0;
+  // canonical job harness on; off: JOB CREATE commands wait for job events submitted
+  // from outside (the job stream processor's JOB CREATED / JOB COMPLETED records, zbref_submit_record)
+  bool harness = true;
   std::string last_error;
 
   void deploy(const std::string& xml, int64_t key, int32_t version) {
@@ -662,6 +698,105 @@ class Engine {
     r.wis.message_name = name;
     r.wis.payload = payload.empty() ? EMPTY_DOCUMENT : payload;
     append(std::move(r));
+  }
+
+  // A record written to the partition log by another writer (client API, job stream processor,
+  // subscription API), given as its reference msgpack value: UnpackedObject.wrap reads the declared
+  // properties (ObjectValue.java:93-131); the log keeps the bytes as written.
+  void submit_record(uint8_t record_type, uint8_t value_type, uint8_t intent, int64_t key, const bytes& value) {
+    Record r;
+    r.record_type = record_type;
+    r.value_type = value_type;
+    r.intent = intent;
+    r.key = key;
+    r.raw_value = value;
+    if (value_type == VT_WORKFLOW_INSTANCE) decode_wf(value, r.wf);
+    else if (value_type == VT_JOB) decode_job(value, r.job);
+    else if (value_type == VT_WORKFLOW_INSTANCE_SUBSCRIPTION) decode_wis(value, r.wis);
+    else throw ZbError("unsupported value type for submit");
+    if (value.empty()) r.raw_value.clear();
+    if (record_type == RT_COMMAND && value_type == VT_WORKFLOW_INSTANCE_SUBSCRIPTION && intent == WIS_CORRELATE)
+      r.key = (int64_t)log.size();  // positionAsKey (SubscriptionApiCommandMessageHandler.java:131-151)
+    append(std::move(r));
+  }
+
+  static bytes read_str(MpReader& rd) {
+    uint32_t n = rd.read_string_length();
+    if (rd.off + n > rd.cap) throw ZbError("Index out of bounds");
+    bytes b((const char*)rd.buf + rd.off, n);
+    rd.off += n;
+    return b;
+  }
+  static bytes read_doc(MpReader& rd) {  // DocumentProperty: msgpack binary, nil / empty -> {}
+    uint32_t n = rd.read_binary_length();
+    if (rd.off + n > rd.cap) throw ZbError("Index out of bounds");
+    bytes b((const char*)rd.buf + rd.off, n);
+    rd.off += n;
+    if (b.empty() || (b.size() == 1 && (uint8_t)b[0] == 0xc0)) return EMPTY_DOCUMENT;
+    return b;
+  }
+  template <class F>
+  static void for_props(MpReader& rd, F f) {
+    uint32_t n = rd.read_map_header();
+    for (uint32_t i = 0; i < n; i++) {
+      bytes k = read_str(rd);
+      if (!f(k, rd)) rd.skip_values(1);
+    }
+  }
+  static void decode_wf(const bytes& b, WfValue& v) {  // WorkflowInstanceRecord.java:39-60
+    if (b.empty()) return;
+    MpReader rd(b);
+    for_props(rd, [&](const bytes& k, MpReader& r) {
+      if (k == "bpmnProcessId") v.bpmn_process_id = read_str(r);
+      else if (k == "version") v.version = (int32_t)r.read_integer();
+      else if (k == "workflowKey") v.workflow_key = r.read_integer();
+      else if (k == "workflowInstanceKey") v.workflow_instance_key = r.read_integer();
+      else if (k == "activityId") v.activity_id = read_str(r);
+      else if (k == "payload") v.payload = read_doc(r);
+      else if (k == "scopeInstanceKey") v.scope_instance_key = r.read_integer();
+      else return false;
+      return true;
+    });
+  }
+  static void decode_job(const bytes& b, JobValue& v) {  // JobRecord.java:35-53, JobHeaders.java:33-51
+    if (b.empty()) return;
+    MpReader rd(b);
+    for_props(rd, [&](const bytes& k, MpReader& r) {
+      if (k == "deadline") v.deadline = r.read_integer();
+      else if (k == "worker") v.worker = read_str(r);
+      else if (k == "retries") v.retries = (int32_t)r.read_integer();
+      else if (k == "type") v.type = read_str(r);
+      else if (k == "headers") {
+        for_props(r, [&](const bytes& hk, MpReader& hr) {
+          if (hk == "bpmnProcessId") v.h_bpmn_process_id = read_str(hr);
+          else if (hk == "workflowDefinitionVersion") v.h_version = (int32_t)hr.read_integer();
+          else if (hk == "workflowKey") v.h_workflow_key = hr.read_integer();
+          else if (hk == "workflowInstanceKey") v.h_workflow_instance_key = hr.read_integer();
+          else if (hk == "activityId") v.h_activity_id = read_str(hr);
+          else if (hk == "activityInstanceKey") v.h_activity_instance_key = hr.read_integer();
+          else return false;
+          return true;
+        });
+      } else if (k == "customHeaders") {
+        size_t st = r.off;
+        r.skip_values(1);
+        v.custom_headers = bytes((const char*)r.buf + st, r.off - st);
+      } else if (k == "payload") v.payload = read_doc(r);
+      else return false;
+      return true;
+    });
+  }
+  static void decode_wis(const bytes& b, WisValue& v) {  // WorkflowInstanceSubscriptionRecord.java:26-38
+    if (b.empty()) return;
+    MpReader rd(b);
+    for_props(rd, [&](const bytes& k, MpReader& r) {
+      if (k == "workflowInstanceKey") v.workflow_instance_key = r.read_integer();
+      else if (k == "activityInstanceKey") v.activity_instance_key = r.read_integer();
+      else if (k == "messageName") v.message_name = read_str(r);
+      else if (k == "payload") v.payload = read_doc(r);
+      else return false;
+      return true;
+    });
   }
 
   // SubscriptionApiCommandMessageHandler.onOpenMessageSubscription :94-110 (command key = position)
@@ -791,6 +926,7 @@ class Engine {
     }
     w_ = nullptr;
     for (auto& r : w.staged) {
+      r.raw_value.clear();  // follow-ups are encoded from their value objects
       r.source_position = rec.position;
       append(std::move(r));
     }
@@ -817,7 +953,7 @@ class Engine {
         }
       }
     } else if (rec.value_type == VT_JOB) {
-      if (rec.record_type == RT_COMMAND && rec.intent == JOB_CREATE) harness_job_create(rec);
+      if (rec.record_type == RT_COMMAND && rec.intent == JOB_CREATE) { if (harness) harness_job_create(rec); }
       else if (rec.record_type == RT_EVENT && rec.intent == JOB_CREATED) process_job_created(rec);
       else if (rec.record_type == RT_EVENT && rec.intent == JOB_COMPLETED) process_job_completed(rec);
     } else if (rec.value_type == VT_WORKFLOW_INSTANCE_SUBSCRIPTION) {
@@ -869,8 +1005,11 @@ class Engine {
       write_rejection(cmd, REJ_NOT_APPLICABLE, "Workflow instance is not running");
       return;
     }
+    // workflowInstance.getValue() is the live indexed object (ElementInstance.java:67-69): setPayload
+    // mutates the index too, so the instance's later TERMINATED (PropagateTerminationHandler :29-40)
+    // carries the emptied payload.
+    wi->value.payload = EMPTY_DOCUMENT;
     WfValue v = wi->value;
-    v.payload = EMPTY_DOCUMENT;
     w_->new_batch();
     Record a; a.key = cmd.key; a.record_type = RT_EVENT; a.value_type = VT_WORKFLOW_INSTANCE; a.wf = v;
     a.intent = CANCELING; w_->stage(a);
@@ -1074,9 +1213,33 @@ class Engine {
         break;
       }
       case S_CONSUME_TOKEN: {  // ConsumeTokenHandler :30-43
+        // EXTENSION (C4): with parallel gateways a scope holds several tokens and completes when its
+        // last token is consumed. Without them every scope holds exactly one token here (tokens == 1),
+        // so this is the reference's unconditional completion.
+        if (--scope->tokens > 0) break;
         WfValue sv = scope->value;
         sv.payload = v.payload;
         write_followup_wf_event(v.scope_instance_key, ELEMENT_COMPLETING, sv);
+        break;
+      }
+      case S_PARALLEL_SPLIT: {  // EXTENSION (C4): fork, one SEQUENCE_FLOW_TAKEN per outgoing flow
+        // executable (reverse document) order; the join arity merges incoming tokens into one
+        scope->tokens += (int32_t)el->outgoing.size() - std::max(el->incoming, 1);
+        w_->new_batch();
+        for (Element* f : el->outgoing) {
+          WfValue fv = v;
+          fv.activity_id = f->id;
+          write_new_wf_event(SEQUENCE_FLOW_TAKEN, fv);
+        }
+        break;
+      }
+      case S_PARALLEL_MERGE: {  // EXTENSION (C4): join, fires on the arrival that completes the arity
+        Element* gw = el->target;
+        int32_t& n = scope->joins[gw];
+        if (++n < gw->incoming) break;
+        n = 0;
+        v.activity_id = gw->id;
+        write_new_wf_event(GATEWAY_ACTIVATED, v);
         break;
       }
       case S_TAKE_SEQUENCE_FLOW:  // TakeSequenceFlowHandler :30-38
@@ -1099,6 +1262,7 @@ class Engine {
         if (!el->start_event) throw ZbError("NullPointerException: container without start event");
         v.activity_id = el->start_event->id;
         v.scope_instance_key = rec.key;
+        ei->tokens = 1;  // EXTENSION (C4): the start event's token
         write_new_wf_event(START_EVENT_OCCURRED, v);
         break;
       case S_COMPLETE_PROCESS:  // CompleteProcessHandler :28-35
@@ -1151,7 +1315,16 @@ class Engine {
         break;
       }
       case S_PROPAGATE_TERMINATION:  // PropagateTerminationHandler :29-40
-        if (scope->children.empty()) write_followup_wf_event(scope->key, ELEMENT_TERMINATED, scope->value);
+        if (scope->children.empty()) {
+          write_followup_wf_event(scope->key, ELEMENT_TERMINATED, scope->value);
+        } else {
+          // EXTENSION (C4, several live tokens in one scope; unreachable in the reference, where a
+          // scope has at most one child): terminate the next child, as TerminateContainedElementsHandler
+          // does for the first one.
+          ElementInstance* child = scope->children[0];
+          if (child->state == ELEMENT_READY || child->state == ELEMENT_ACTIVATED || child->state == ELEMENT_COMPLETING)
+            write_followup_wf_event(child->key, ELEMENT_TERMINATING, child->value);
+        }
         break;
       default:
         break;
@@ -1215,6 +1388,50 @@ int zbref_submit_create(void* h, const char* process_id, int32_t version, int64_
     e->last_error = ex.what();
     return -1;
   }
+}
+
+int zbref_set_harness(void* h, int on) {
+  ((Engine*)h)->harness = on != 0;
+  return 0;
+}
+
+int zbref_submit_record(void* h, uint8_t record_type, uint8_t value_type, uint8_t intent, int64_t key,
+                        const uint8_t* value, size_t n) {
+  Engine* e = (Engine*)h;
+  try {
+    e->submit_record(record_type, value_type, intent, key, bytes((const char*)value, n));
+    return 0;
+  } catch (const std::exception& ex) {
+    e->last_error = ex.what();
+    return -1;
+  }
+}
+
+// Live element instances sorted by key (ElementInstanceIndex.java:25-65): per instance
+// [i64 key][i64 parent key (-1)][i64 job key][u8 state][3 pad][u32 value length][value bytes].
+int64_t zbref_dump_instances(void* h, uint8_t* buf, size_t cap) {
+  Engine* e = (Engine*)h;
+  std::vector<const ElementInstance*> v;
+  for (auto& kv : e->index.instances) v.push_back(kv.second.get());
+  std::sort(v.begin(), v.end(), [](const ElementInstance* a, const ElementInstance* b) { return a->key < b->key; });
+  size_t off = 0;
+  for (const ElementInstance* ei : v) {
+    bytes val = ei->value.encode();
+    size_t need = 32 + val.size();
+    if (buf && off + need <= cap) {
+      int64_t pk = ei->parent ? ei->parent->key : -1;
+      std::memcpy(buf + off, &ei->key, 8);
+      std::memcpy(buf + off + 8, &pk, 8);
+      std::memcpy(buf + off + 16, &ei->job_key, 8);
+      buf[off + 24] = ei->state;
+      buf[off + 25] = buf[off + 26] = buf[off + 27] = 0;
+      uint32_t n = (uint32_t)val.size();
+      std::memcpy(buf + off + 28, &n, 4);
+      std::memcpy(buf + off + 32, val.data(), val.size());
+    }
+    off += need;
+  }
+  return (int64_t)off;
 }
 
 int zbref_submit_cancel(void* h, int64_t key) {

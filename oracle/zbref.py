@@ -40,6 +40,10 @@ def lib():
         L.zbref_set_job_payload.argtypes = [vp, i64, cp, u8p, sz]
         L.zbref_submit_create.argtypes = [vp, cp, i32, i64, u8p, sz]
         L.zbref_submit_cancel.argtypes = [vp, i64]
+        L.zbref_set_harness.argtypes = [vp, ctypes.c_int]
+        L.zbref_submit_record.argtypes = [vp, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, i64, u8p, sz]
+        L.zbref_dump_instances.restype = i64
+        L.zbref_dump_instances.argtypes = [vp, ctypes.c_void_p, sz]
         L.zbref_submit_correlate.argtypes = [vp, i64, i64, cp, u8p, sz]
         L.zbref_submit_open.argtypes = [vp, i32, i64, i64, u8p, sz, u8p, sz]
         L.zbref_submit_publish.argtypes = [vp, u8p, sz, u8p, sz, i64, u8p, sz, u8p, sz]
@@ -100,6 +104,20 @@ def parse_log(buf: bytes) -> List[Record]:
     return out
 
 
+_INST = struct.Struct("<qqqB3xI")
+
+
+def parse_instances(buf: bytes):
+    """[i64 key][i64 parent key][i64 job key][u8 state][3 pad][u32 n][value] records (zb_read_instances layout)."""
+    out, off = [], 0
+    while off < len(buf):
+        key, pk, jk, st, n = _INST.unpack_from(buf, off)
+        off += _INST.size
+        out.append((key, pk, jk, st, bytes(buf[off:off + n])))
+        off += n
+    return out
+
+
 class ZbrefError(RuntimeError):
     pass
 
@@ -140,6 +158,23 @@ class Oracle:
 
     def cancel(self, key: int):
         self._L.zbref_submit_cancel(self._h, key)
+
+    def set_harness(self, on: bool):
+        """Canonical job harness on (default) / off (JOB CREATE commands wait for submitted job events)."""
+        self._L.zbref_set_harness(self._h, 1 if on else 0)
+
+    def submit(self, record_type: int, value_type: int, intent: int, key: int, value: bytes):
+        """A record written by another writer, as its reference msgpack value (kept verbatim in the log)."""
+        if self._L.zbref_submit_record(self._h, record_type, value_type, intent, key, value, len(value)):
+            raise ZbrefError(self._err())
+
+    def instances(self):
+        """Live element instances (ElementInstanceIndex) sorted by key:
+        list of (key, parent_key, job_key, state, value bytes)."""
+        need = self._L.zbref_dump_instances(self._h, None, 0)
+        buf = ctypes.create_string_buffer(max(need, 1))
+        self._L.zbref_dump_instances(self._h, buf, need)
+        return parse_instances(buf.raw[:need])
 
     def correlate(self, wf_instance_key: int, activity_instance_key: int, message_name, payload: bytes):
         """WORKFLOW_INSTANCE_SUBSCRIPTION CORRELATE command (key = its log position)."""

@@ -184,7 +184,8 @@ def hashes():
 
 WF = {"CREATE": 0, "CREATED": 1, "START_EVENT_OCCURRED": 2, "END_EVENT_OCCURRED": 3, "SEQUENCE_FLOW_TAKEN": 4,
       "GATEWAY_ACTIVATED": 5, "ELEMENT_READY": 6, "ELEMENT_ACTIVATED": 7, "ELEMENT_COMPLETING": 8,
-      "ELEMENT_COMPLETED": 9, "ELEMENT_TERMINATING": 10, "ELEMENT_TERMINATED": 11, "CANCEL": 12, "CANCELING": 13}
+      "ELEMENT_COMPLETED": 9, "ELEMENT_TERMINATING": 10, "ELEMENT_TERMINATED": 11, "CANCEL": 12, "CANCELING": 13,
+      "UPDATE_PAYLOAD": 14, "PAYLOAD_UPDATED": 15}
 
 
 def workflows():
@@ -278,6 +279,51 @@ def workflows():
     return out
 
 
+def cancels():
+    """CancelWorkflowInstanceTest.java:49-260: workflow events from the CANCEL command on, as (activityId,
+    intent); activityId None for the command. The instance is cancelled while its task waits for a job
+    (job_created: the job stream processor has written JOB CREATED first) or its catch event waits."""
+    B = bpmn.Bpmn
+    wf = (B.create_executable_process("process").start_event().service_task("task", type="test", retries=5)
+          .end_event().done())
+    sp = B.create_executable_process("process").start_event().sub_process("subProcess")
+    sp.embedded_sub_process().start_event().service_task("task", type="test", retries=5).end_event()
+    sub = sp.end_event().done()
+    catch = (B.create_executable_process("wf").start_event()
+             .intermediate_catch_event("catch-event", message="msg", correlation_key="$.id").done())
+    C = "CANCEL"
+    return [
+        # shouldCancelWorkflowInstance :81-124
+        {"name": "cancel_workflow_instance", "xml": wf.to_xml(), "process": "process", "payload": "80",
+         "job_created": False,
+         "expect": [[None, C], ["process", "CANCELING"], ["process", "ELEMENT_TERMINATING"],
+                    ["task", "ELEMENT_TERMINATING"], ["task", "ELEMENT_TERMINATED"],
+                    ["process", "ELEMENT_TERMINATED"]]},
+        # shouldCancelWorkflowInstanceWithEmbeddedSubProcess :126-156
+        {"name": "cancel_with_embedded_sub_process", "xml": sub.to_xml(), "process": "process", "payload": "80",
+         "job_created": False,
+         "expect": [[None, C], ["process", "CANCELING"], ["process", "ELEMENT_TERMINATING"],
+                    ["subProcess", "ELEMENT_TERMINATING"], ["task", "ELEMENT_TERMINATING"],
+                    ["task", "ELEMENT_TERMINATED"], ["subProcess", "ELEMENT_TERMINATED"],
+                    ["process", "ELEMENT_TERMINATED"]]},
+        # shouldCancelIntermediateCatchEvent :184-214 (TERMINATED's source = TERMINATING's position)
+        {"name": "cancel_intermediate_catch_event", "xml": catch.to_xml(), "process": "wf",
+         "payload": mp({"id": "123"}), "job_created": False,
+         "expect": [[None, C], ["wf", "CANCELING"], ["wf", "ELEMENT_TERMINATING"],
+                    ["catch-event", "ELEMENT_TERMINATING"], ["catch-event", "ELEMENT_TERMINATED"],
+                    ["wf", "ELEMENT_TERMINATED"]]},
+        # shouldCancelJobForActivity :216-245: JOB CANCEL command (key = job key) written with the task's
+        # TERMINATED, source = the task's TERMINATING; headers carry the instance / process / version / activity
+        {"name": "cancel_job_for_activity", "xml": wf.to_xml(), "process": "process", "payload": "80",
+         "job_created": True,
+         "expect": [[None, C], ["process", "CANCELING"], ["process", "ELEMENT_TERMINATING"],
+                    ["task", "ELEMENT_TERMINATING"], ["task", "ELEMENT_TERMINATED"],
+                    ["process", "ELEMENT_TERMINATED"]],
+         "expect_job_cancel_headers": {"bpmnProcessId": "process", "workflowDefinitionVersion": 1,
+                                       "activityId": "task"}},
+    ]
+
+
 def main():
     data = {
         "conditions": conditions(),
@@ -288,6 +334,7 @@ def main():
         "writer": writer(),
         "hashes": hashes(),
         "workflows": workflows(),
+        "cancels": cancels(),
         "wf_intents": WF,
     }
     with open(os.path.join(HERE, "reference_vectors.json"), "w") as f:

@@ -1,10 +1,17 @@
-"""Summarise the rocprofv3 PMC passes of run_gpu_pmc.sh into profiles/<round>/pmc_<tag>.json.
+"""Summarise the rocprofv3 PMC passes of run_gpu_pmc.sh (one counter set per pass directory p<i>).
 
-Pass 1 collects FETCH_SIZE, pass 2 WRITE_SIZE (separate runs, kernel trace only). Both are reported
-in KB per dispatch; gfx950 tallies 128-B read requests at 64 B, so FETCH_SIZE is doubled
-(MI355X_MICROARCH.md, HBM/rocprofv3 section). WRITE_SIZE is taken as reported.
+Per kernel (averaged over its dispatches) every counter of every pass, plus derived figures:
+  hbm_bytes        2 * FETCH_SIZE + WRITE_SIZE (both reported in KB; gfx950 tallies 128-B read requests
+                   at 64 B, so FETCH_SIZE is doubled -- MI355X_MICROARCH.md, HBM / rocprofv3 section)
+  valu_busy        SQ_ACTIVE_INST_VALU * 4 / (#SIMD = 4 * 256 CUs) / GRBM_GUI_ACTIVE (gfx94x formula)
+  valu_lane_util   SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU): mean active lanes of a VALU
+                   instruction (1.0 = no divergence)
+  mean_waves_cu    SQ_ACCUM_PREV_HIRES / SQ_BUSY_CU_CYCLES... reported as SQ_ACCUM_PREV_HIRES / GRBM_GUI_ACTIVE / CUs
+                   (resident waves per CU, of 32; occupancy = mean_waves_cu / 32)
+  wait_frac        SQ_WAIT_ANY / SQ_WAVE_CYCLES (waves parked on s_waitcnt / barriers)
+  lds_conflict     SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
 
-usage: python tools/pmc_summary.py gpurun_out/pmc profiles/r01/pmc_v5.json
+usage: python tools/pmc_summary.py gpurun_out/pmc_<tag> profiles/r02/pmc_<tag>.json
 """
 import csv
 import glob
@@ -13,48 +20,67 @@ import os
 import sys
 from collections import defaultdict
 
-MAIN_PREFERENCE = ("zbg::k_tmpl<false, false>", "zbg::k_tmpl<true, false>")
+CUS = 256
 
 
-def per_kernel(pass_dir, counter):
-    acc, calls = defaultdict(float), defaultdict(set)
+def per_kernel(pass_dir):
+    acc = defaultdict(lambda: defaultdict(float))
+    calls = defaultdict(lambda: defaultdict(set))
     for f in glob.glob(os.path.join(pass_dir, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if row.get("Counter_Name") != counter:
-                    continue
                 k = row["Kernel_Name"]
-                acc[k] += float(row["Counter_Value"])
-                calls[k].add(row.get("Dispatch_Id") or row.get("Correlation_Id"))
-    return {k: acc[k] / max(len(calls[k]), 1) for k in acc}
+                c = row.get("Counter_Name")
+                acc[k][c] += float(row["Counter_Value"])
+                calls[k][c].add(row.get("Dispatch_Id") or row.get("Correlation_Id"))
+    return {k: {c: acc[k][c] / max(len(calls[k][c]), 1) for c in acc[k]} for k in acc}, \
+        {k: max(len(v) for v in calls[k].values()) for k in calls}
 
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
-    fetch = per_kernel(os.path.join(src, "p1"), "FETCH_SIZE")
-    write = per_kernel(os.path.join(src, "p2"), "WRITE_SIZE")
-    kernels = {k: {"FETCH_SIZE_KB": fetch.get(k, 0.0), "WRITE_SIZE_KB": write.get(k, 0.0)}
-               for k in sorted(set(fetch) | set(write)) if k.startswith(("zbg::", "void zbg::"))}
-    main_k = None
-    for pref in MAIN_PREFERENCE:
-        main_k = next((k for k in kernels if pref in k), None)
-        if main_k:
-            break
-    if main_k is None:
-        main_k = max(kernels, key=lambda k: kernels[k]["WRITE_SIZE_KB"])
-    fb = 2 * 1024 * kernels[main_k]["FETCH_SIZE_KB"]
-    wb = 1024 * kernels[main_k]["WRITE_SIZE_KB"]
-    out = {"command": "rocprofv3 --pmc <FETCH_SIZE | WRITE_SIZE> --kernel-trace -- python3 bench.py --steps 1 "
-                      "--warmup 0 --instances 1000000 --no-cpu-baseline (one pass per counter, run_gpu_pmc.sh)",
-           "workload": "C2: 20-task chain, 1,000,000 instances, one step",
-           "kernels": kernels,
+    kernels = defaultdict(dict)
+    dispatches = {}
+    sets = []
+    for d in sorted(glob.glob(os.path.join(src, "p*")), key=lambda p: int(''.join(ch for ch in os.path.basename(p) if ch.isdigit()) or 0)):
+        if not os.path.isdir(d):
+            continue
+        setf = d + ".set"
+        if os.path.exists(setf):
+            sets.append(open(setf).read().strip())
+        vals, n = per_kernel(d)
+        for k, cs in vals.items():
+            kernels[k].update(cs)
+            dispatches[k] = max(dispatches.get(k, 0), n[k])
+    out = {}
+    for k, c in kernels.items():
+        if "zbg::" not in k:
+            continue
+        d = dict(c)
+        d["dispatches"] = dispatches.get(k, 0)
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            d["hbm_bytes"] = 1024 * (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"])
+        if c.get("GRBM_GUI_ACTIVE") and "SQ_ACTIVE_INST_VALU" in c:
+            d["valu_busy"] = c["SQ_ACTIVE_INST_VALU"] * 4 / (4 * CUS) / c["GRBM_GUI_ACTIVE"]
+        if c.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in c:
+            d["valu_lane_util"] = c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"])
+        if c.get("GRBM_GUI_ACTIVE") and "SQ_ACCUM_PREV_HIRES" in c:
+            d["mean_waves_cu"] = c["SQ_ACCUM_PREV_HIRES"] / c["GRBM_GUI_ACTIVE"] / CUS
+            d["occupancy"] = d["mean_waves_cu"] / 32.0
+        if c.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in c:
+            d["wait_frac"] = c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
+        if c.get("SQ_LDS_IDX_ACTIVE") and "SQ_LDS_BANK_CONFLICT" in c:
+            d["lds_conflict"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]
+        out[k] = d
+    res = {"source": src, "passes": sets,
            "correction": "FETCH_SIZE doubled (gfx950 tallies 128-B requests at 64 B); WRITE_SIZE as reported",
-           "main_kernel": main_k, "main_traffic_bytes": fb + wb,
-           "main_fetch_bytes_corrected": fb, "main_write_bytes": wb}
+           "kernels": out}
+    os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
     with open(dst, "w") as f:
-        json.dump(out, f, indent=1)
-    print(json.dumps({k: out[k] for k in ("main_kernel", "main_traffic_bytes", "main_fetch_bytes_corrected",
-                                          "main_write_bytes")}))
+        json.dump(res, f, indent=1)
+    for k, d in sorted(out.items(), key=lambda kv: -kv[1].get("hbm_bytes", 0)):
+        print(k[:60], {x: round(d[x], 4) for x in ("hbm_bytes", "valu_busy", "valu_lane_util", "occupancy",
+                                                     "wait_frac", "lds_conflict", "dispatches") if x in d})
 
 
 if __name__ == "__main__":

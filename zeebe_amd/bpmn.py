@@ -408,3 +408,26 @@ def message_workflow(process_id: str = "msg") -> BpmnModel:
     return (Bpmn.create_executable_process(process_id).start_event("start")
             .intermediate_catch_event("wait", message="order", correlation_key="$.orderId")
             .end_event("end").done())
+
+
+def parallel_workflow(fanout: int = 8, process_id: str = "par", subprocesses: bool = True) -> BpmnModel:
+    """C4 (EXTENSION): start -> fork (parallel) -> fanout x [sub_k {start -> task_k -> end}] ->
+    join (parallel) -> end. With subprocesses=False each branch is the service task alone."""
+    fork = Bpmn.create_executable_process(process_id).start_event("start").sequence_flow_id("in").parallel_gateway("fork")
+    for k in range(1, fanout + 1):
+        b = fork.move_to_node("fork").sequence_flow_id("b%d" % k)
+        if subprocesses:
+            sp = b.sub_process("sub%d" % k)
+            inner = sp.embedded_sub_process().start_event("s%d_start" % k)
+            inner.sequence_flow_id("s%d_f1" % k).service_task("task%d" % k, type="task%d" % k) \
+                .sequence_flow_id("s%d_f2" % k).end_event("s%d_end" % k)
+            b = sp
+        else:
+            b = b.service_task("task%d" % k, type="task%d" % k)
+        b = b.sequence_flow_id("j%d" % k)
+        if k == 1:
+            join = b.parallel_gateway("join")
+            join.sequence_flow_id("out").end_event("end")
+        else:
+            b.connect_to("join")
+    return fork.done()

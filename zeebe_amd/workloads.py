@@ -89,6 +89,8 @@ CONFIGS = {
     "c2": dict(workflow=lambda: bpmn.chain_workflow(20), process="chain", payloads=order_payloads,
                job_payloads=lambda: {"t%d" % k: b"\x81" + mp_str("step") + mp_int(k) for k in range(1, 21)}),
     "c3": dict(workflow=bpmn.xor_workflow, process="xor", payloads=xor_payloads, job_payloads=lambda: {}),
+    "c4": dict(workflow=lambda: bpmn.parallel_workflow(8), process="par", payloads=order_payloads,
+               job_payloads=lambda: {"task%d" % k: b"\x81" + mp_str("sub") + mp_int(k) for k in range(1, 9)}),
     "c4twin": dict(workflow=lambda: bpmn.subprocess_chain_workflow(8), process="subs", payloads=order_payloads,
                    job_payloads=lambda: {"task%d" % k: b"\x81" + mp_str("sub") + mp_int(k) for k in range(1, 9)}),
 }
