@@ -3,11 +3,12 @@
 Per kernel (averaged over its dispatches) every counter of every pass, plus derived figures:
   hbm_bytes        2 * FETCH_SIZE + WRITE_SIZE (both reported in KB; gfx950 tallies 128-B read requests
                    at 64 B, so FETCH_SIZE is doubled -- MI355X_MICROARCH.md, HBM / rocprofv3 section)
-  valu_busy        SQ_ACTIVE_INST_VALU * 4 / (#SIMD = 4 * 256 CUs) / GRBM_GUI_ACTIVE (gfx94x formula)
+  kernel_cycles    GRBM_GUI_ACTIVE / 8 (the counter is summed over the 8 XCDs)
+  valu_busy        SQ_ACTIVE_INST_VALU * 4 / (#SIMD = 4 * 256 CUs) / kernel_cycles (gfx94x formula)
   valu_lane_util   SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU): mean active lanes of a VALU
                    instruction (1.0 = no divergence)
-  mean_waves_cu    SQ_ACCUM_PREV_HIRES / SQ_BUSY_CU_CYCLES... reported as SQ_ACCUM_PREV_HIRES / GRBM_GUI_ACTIVE / CUs
-                   (resident waves per CU, of 32; occupancy = mean_waves_cu / 32)
+  mean_waves_cu    SQ_WAVE_CYCLES / kernel_cycles / 256 CUs: resident waves per CU averaged over the kernel
+                   (of 32; occupancy = mean_waves_cu / 32). SQ_ACCUM_PREV_HIRES reads 0 on gfx950 / ROCm 7.2.
   wait_frac        SQ_WAIT_ANY / SQ_WAVE_CYCLES (waves parked on s_waitcnt / barriers)
   lds_conflict     SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
 
@@ -21,6 +22,7 @@ import sys
 from collections import defaultdict
 
 CUS = 256
+XCDS = 8
 
 
 def per_kernel(pass_dir):
@@ -60,13 +62,17 @@ def main():
         d["dispatches"] = dispatches.get(k, 0)
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             d["hbm_bytes"] = 1024 * (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"])
-        if c.get("GRBM_GUI_ACTIVE") and "SQ_ACTIVE_INST_VALU" in c:
-            d["valu_busy"] = c["SQ_ACTIVE_INST_VALU"] * 4 / (4 * CUS) / c["GRBM_GUI_ACTIVE"]
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs: one XCD's value is the kernel's duration in cycles
+        cyc = c.get("GRBM_GUI_ACTIVE", 0) / XCDS
+        if cyc:
+            d["kernel_cycles"] = cyc
+        if cyc and "SQ_ACTIVE_INST_VALU" in c:
+            d["valu_busy"] = c["SQ_ACTIVE_INST_VALU"] * 4 / (4 * CUS) / cyc
+        if cyc and "SQ_WAVE_CYCLES" in c:
+            d["mean_waves_cu"] = c["SQ_WAVE_CYCLES"] / cyc / CUS
+            d["occupancy"] = d["mean_waves_cu"] / 32.0
         if c.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in c:
             d["valu_lane_util"] = c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"])
-        if c.get("GRBM_GUI_ACTIVE") and "SQ_ACCUM_PREV_HIRES" in c:
-            d["mean_waves_cu"] = c["SQ_ACCUM_PREV_HIRES"] / c["GRBM_GUI_ACTIVE"] / CUS
-            d["occupancy"] = d["mean_waves_cu"] / 32.0
         if c.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in c:
             d["wait_frac"] = c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
         if c.get("SQ_LDS_IDX_ACTIVE") and "SQ_LDS_BANK_CONFLICT" in c:
@@ -80,7 +86,7 @@ def main():
         json.dump(res, f, indent=1)
     for k, d in sorted(out.items(), key=lambda kv: -kv[1].get("hbm_bytes", 0)):
         print(k[:60], {x: round(d[x], 4) for x in ("hbm_bytes", "valu_busy", "valu_lane_util", "occupancy",
-                                                     "wait_frac", "lds_conflict", "dispatches") if x in d})
+                                                     "wait_frac", "lds_conflict", "kernel_cycles", "dispatches") if x in d})
 
 
 if __name__ == "__main__":
