@@ -50,6 +50,8 @@ extern "C" {
 
 /* zb_config.flags */
 #define ZB_CFG_WAVE_ONLY 1    /* always use the general wave pipeline (never the trajectory path) */
+#define ZB_CFG_EXTERNAL_JOBS 2 /* no canonical job harness: JOB CREATE commands wait for the job stream
+                                  processor's JOB CREATED / JOB COMPLETED events, submitted with zb_submit */
 
 typedef struct zb_engine zb_engine;
 
@@ -161,6 +163,32 @@ int zb_set_job_completion_payload(zb_engine* e, int64_t workflow_key, const char
 int zb_submit_creates(zb_engine* e, const char* bpmn_process_id, int32_t version, int64_t workflow_key,
                       size_t n, const uint8_t* payloads, const uint64_t* offsets);
 
+/* General record input: the records a JNI shim forwards for the 18 (recordType, valueType, intent) keys
+ * WorkflowInstanceStreamProcessor registers (WorkflowInstanceStreamProcessor.java:103-169), as the log
+ * holds them: metadata + the reference msgpack value (UnpackedObject.write). The engine decodes each
+ * value, keeps its bytes verbatim for the log, and injects the batch at the log tail at the next
+ * zb_step, in submission order. Accepted:
+ *   COMMAND WORKFLOW_INSTANCE CREATE          (CreateWorkflowInstanceEventProcessor :224-368)
+ *   COMMAND WORKFLOW_INSTANCE CANCEL          (CancelWorkflowInstanceProcessor :511-555; key = instance key)
+ *   COMMAND WORKFLOW_INSTANCE UPDATE_PAYLOAD  (UpdatePayloadProcessor :557-576)
+ *   EVENT   JOB CREATED / COMPLETED           (JobCreatedProcessor :408-426, JobCompletedEventProcessor :428-453)
+ *   COMMAND WORKFLOW_INSTANCE_SUBSCRIPTION CORRELATE (:455-509; its key becomes its log position)
+ * A tick's records must not race inside one lockstep wave: per workflow instance at most one CANCEL /
+ * UPDATE_PAYLOAD and then nothing else, per activity instance at most one record, except a JOB CREATED
+ * directly followed by its JOB COMPLETED; anything else returns ZB_EUNSUPPORTED (split the tick:
+ * zb_step, then submit the rest). Records other than CREATE are injected only into a quiescent
+ * partition. All-or-nothing: on error nothing is staged. */
+typedef struct zb_rec_desc {
+  int64_t key;            /* record key (-1 = null) */
+  uint8_t record_type;    /* ZB_RT_* */
+  uint8_t value_type;     /* ZB_VT_* */
+  uint8_t intent;
+  uint8_t pad;
+  uint32_t value_length;
+  uint64_t value_offset;  /* into the values buffer */
+} zb_rec_desc;
+int zb_submit(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* values, size_t values_len);
+
 /* ---- stepping ------------------------------------------------------------------------ */
 /* Injects staged input at the log tail and runs lockstep waves until quiescence (ZB_OK) or
  * max_waves (ZB_EAGAIN). stats may be NULL. */
@@ -211,6 +239,21 @@ int zb_drain(zb_engine* e, int64_t start, int64_t count, zb_record_header* heade
 /* counters: [0] created [1] completed [2] canceled [3] next wf key [4] next job key
  *           [5] rows allocated [6] arena bytes used [7] log size */
 int zb_counters(zb_engine* e, int64_t out[8]);
+
+/* Live element instances (ElementInstanceIndex.java:25-65, ElementInstance.java:30-111) sorted by key,
+ * packed as [i64 key][i64 flow scope (parent) key, -1 for none][i64 job key][u8 state (intent)][3 pad]
+ * [u32 value length][value: the indexed WorkflowInstanceRecord]. *len = bytes needed; if cap is too
+ * small nothing is copied and ZB_ENOMEM is returned. */
+int zb_read_instances(zb_engine* e, uint8_t* buf, size_t cap, size_t* len, uint64_t* count);
+
+/* Snapshot of a quiescent partition's processing state (ComposeableSerializableSnapshot.java:27-48:
+ * element instances, key generators; plus payloads and message stores): element-instance rows, the
+ * payload arena, wave header / key generators, statistics and message stores. Deployments are not in
+ * it (the reference keeps them in the WorkflowCache): zb_restore requires the same deployments. The log
+ * is not in it either: after zb_restore positions continue from the snapshot's log end and earlier
+ * records cannot be drained. *len = bytes needed (ZB_ENOMEM if cap too small). */
+int zb_snapshot(zb_engine* e, uint8_t* buf, size_t cap, size_t* len);
+int zb_restore(zb_engine* e, const uint8_t* buf, size_t len);
 
 #ifdef __cplusplus
 }

@@ -1022,6 +1022,7 @@ class Engine {
     if (wi) {
       wi->value.set_payload(cmd.wf.payload);
       Record a = cmd; a.record_type = RT_EVENT; a.intent = PAYLOAD_UPDATED;
+      if (a.key < 0) a.key = wf_keys.next_key();  // CommandProcessorImpl.accept :77-84: null key -> new key
       w_->stage(a);
     } else {
       write_rejection(cmd, REJ_NOT_APPLICABLE, "Workflow instance is not running");

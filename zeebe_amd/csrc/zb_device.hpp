@@ -19,15 +19,21 @@ constexpr uint32_t NO_REF = 0xffffffffu;
 
 // element kinds (FlowElementHandler.java:46-57 factories + the process)
 enum Kind : uint8_t { EK_PROCESS = 0, EK_START = 1, EK_END = 2, EK_TASK = 3, EK_SUB = 4, EK_XOR = 5, EK_CATCH = 6,
-                      EK_FLOW = 7 };
+                      EK_FLOW = 7,
+                      EK_PAR = 8 };  // parallel gateway: EXTENSION (C4), rejected by the reference
 
 // BpmnStep.java:20-54 (same order)
 enum Step : uint8_t {
   ST_NONE = 0, ST_TAKE_SEQUENCE_FLOW, ST_CONSUME_TOKEN, ST_EXCLUSIVE_SPLIT, ST_CREATE_JOB, ST_APPLY_INPUT_MAPPING,
   ST_APPLY_OUTPUT_MAPPING, ST_ACTIVATE_GATEWAY, ST_SUBSCRIBE_TO_INTERMEDIATE_MESSAGE, ST_START_STATEFUL_ELEMENT,
   ST_TRIGGER_END_EVENT, ST_TRIGGER_START_EVENT, ST_TERMINATE_CONTAINED_INSTANCES, ST_TERMINATE_JOB_TASK,
-  ST_TERMINATE_ELEMENT, ST_PROPAGATE_TERMINATION, ST_CANCEL_PROCESS, ST_COMPLETE_PROCESS, ST_UNBOUND = 255
+  ST_TERMINATE_ELEMENT, ST_PROPAGATE_TERMINATION, ST_CANCEL_PROCESS, ST_COMPLETE_PROCESS,
+  // EXTENSION (C4): GATEWAY_ACTIVATED of a parallel gateway forks; a flow into a join is an arrival
+  ST_PARALLEL_SPLIT, ST_PARALLEL_MERGE,
+  ST_UNBOUND = 255
 };
+constexpr int MAX_FANOUT = 63;  // outgoing flows of a parallel gateway (count word field)
+constexpr int JOIN_SLOTS = 2;   // parallel joins directly inside one scope (RowAux counters)
 
 // WorkflowInstanceIntent.java:18-38
 enum WfIntent : uint8_t {
@@ -38,7 +44,10 @@ enum WfIntent : uint8_t {
 };
 enum JobIntentG : uint8_t { JI_CREATE = 0, JI_CREATED = 1, JI_COMPLETED = 5, JI_CANCEL = 12 };
 
-// record kind byte
+// record kind byte: [3:0] value type, [5:4] record type, 6 second record of a batch, 7 KIND_RAW: the value
+// is serialized verbatim from the blob that follows the payload document blob (records submitted through
+// zb_submit, and the follow-ups the reference writes as the re-encoded command value)
+constexpr uint8_t KIND_RAW = 0x80;
 __host__ __device__ inline uint8_t make_kind(uint8_t vt, uint8_t rt, bool cont) {
   return (uint8_t)(vt | (rt << 4) | (cont ? 0x40 : 0));
 }
@@ -70,9 +79,13 @@ struct DevElem {              // 72 bytes
   uint32_t headers_len;
   uint32_t msg_off;           // message name in pool
   uint16_t msg_len;
-  uint16_t pad0;
+  uint16_t out_begin;         // parallel gateway: its outgoing flows in executable order (flows[])
+  uint8_t m_in;               // parallel gateway: incoming sequence flows (join arity)
+  uint8_t join_slot;          // parallel join: its counter slot in the scope's RowAux
+  uint16_t pad1;
+  uint32_t pad2;
 };
-static_assert(sizeof(DevElem) == 72, "DevElem layout is 72 bytes");
+static_assert(sizeof(DevElem) == 80, "DevElem layout is 80 bytes");
 
 struct DevWorkflow {          // 32 bytes
   int64_t key;
@@ -164,5 +177,17 @@ struct RowMeta {
 struct RowKeys {
   int64_t key, scope_key, inst_key, job_key;
 };
+// Scope-wide state touched only by scope operations (never on the chain-stepping hot path):
+// EXTENSION token / join counters of a scope with parallel gateways, and the first
+// live child of a scope being terminated (TerminateContainedElementsHandler :31-53 children.get(0)).
+struct RowAux {
+  int32_t tokens;              // live tokens of the scope (+ merged arrivals pending their GATEWAY_ACTIVATED)
+  uint32_t first;              // min live child row (k_children), valid when mark == the wave's epoch
+  uint32_t join_cnt[JOIN_SLOTS];
+  int64_t consume_pos;         // max log position of a CONSUME_TOKEN on this scope (k_pre)
+  int64_t join_pos[JOIN_SLOTS];// max log position of an arrival per join slot (k_pre)
+  int64_t mark;                // epoch of the wave that asked for `first`
+};
+static_assert(sizeof(RowAux) == 48, "RowAux is 48 bytes");
 
 }  // namespace zbg

@@ -13,6 +13,8 @@
 #include <chrono>
 #include <cstring>
 #include <string>
+#include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "zb_kernels.hpp"
@@ -171,6 +173,22 @@ struct zb_engine {
   ncclComm_t comm = nullptr;
   uint64_t* d_xcounts = nullptr;  // [2 * 64] send / receive counts
 
+  // scope-wide row state (RowAux), first-live-child requests, wave epoch
+  RowAux* raux = nullptr;
+  uint32_t* need_children = nullptr;
+  int64_t epoch = 1;
+  bool has_parallel = false;
+  bool term = false;               // a CANCEL was injected: terminations may run until quiescence
+  int64_t log_floor = 0;           // records below were not restored (zb_restore): not readable
+  // zb_submit: per staged record, the key whose element-instance row it needs (INT64_MIN: none)
+  std::vector<int64_t> staged_lookup;
+  bool staged_only_creates = true;
+  bool staged_has_cancel = false;
+  // per-tick race rules of zb_submit (include/zb_engine.h)
+  std::unordered_map<int64_t, uint8_t> tick_inst;  // workflow instance -> 1: scope command, 2: other records
+  std::unordered_set<int64_t> tick_aik;
+  DevVec<int64_t> d_lookup_keys, d_lookup_pos;
+
   // timing
   std::vector<hipEvent_t> ev;
 };
@@ -253,6 +271,12 @@ WaveParams wave_params(zb_engine* e) {
   p.ocap = e->ocap;
   p.partition_id = e->cfg.partition_id;
   p.partition_count = e->cfg.partition_count;
+  p.raux = e->raux;
+  p.has_parallel = e->has_parallel ? 1 : 0;
+  p.harness = (e->cfg.flags & ZB_CFG_EXTERNAL_JOBS) ? 0 : 1;
+  p.term = e->term ? 1 : 0;
+  p.epoch = e->epoch;
+  p.need_children = e->need_children;
   return p;
 }
 
@@ -581,6 +605,10 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->t_mgen, CLS_MAX * CLS_ROW * sizeof(MergeGen)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_tmpl, (size_t)CLS_MAX * CLS_ROW * TF * sizeof(TmplRec)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_cstat, CLS_MAX * TSTAT * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->raux, e->cfg.row_capacity * sizeof(RowAux)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMemset(e->raux, 0, e->cfg.row_capacity * sizeof(RowAux)) != hipSuccess) return cleanup(ZB_EDEVICE);
+  if (hipMalloc(&e->need_children, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMemset(e->need_children, 0, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_EDEVICE);
   e->ev.resize(EV_PER_WAVE * WAVES_PER_SYNC);
   for (auto& x : e->ev)
     if (hipEventCreate(&x) != hipSuccess) return cleanup(ZB_EDEVICE);
@@ -603,7 +631,7 @@ void zb_engine_destroy(zb_engine* e) {
                 e->merge_jobs, e->cond_jobs, e->job_counts, e->cw, e->stage, e->info, e->block_agg, e->block_off,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
-                e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls};
+                e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->need_children};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->comm) (void)ncclCommDestroy(e->comm);
@@ -616,7 +644,7 @@ void zb_engine_destroy(zb_engine* e) {
   if (e->h_ctl_pinned) (void)hipHostFree(e->h_ctl_pinned);
   e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_consts.free();
   e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
-  e->d_ranges.free(); e->d_cmd_pool.free();
+  e->d_ranges.free(); e->d_cmd_pool.free(); e->d_lookup_keys.free(); e->d_lookup_pos.free();
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -647,8 +675,15 @@ int zb_reset(zb_engine* e, int keep_staged) {
     e->staged.clear();
     e->staged_arena.clear();
     e->pending_ranges.clear();
+    e->staged_lookup.clear();
+    e->staged_only_creates = true;
+    e->staged_has_cancel = false;
+    e->tick_inst.clear();
+    e->tick_aik.clear();
     e->staged_uploaded = false;
   }
+  e->term = false;
+  e->log_floor = 0;
   e->staged_pending = !e->staged.empty();
   e->sub_count = e->msg_count = 0;
   e->msg_key_next = 0;
@@ -671,6 +706,7 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
     if (el.step[WI_ELEMENT_COMPLETING] == ST_APPLY_OUTPUT_MAPPING) e->has_merges = true;
     if (el.step[WI_GATEWAY_ACTIVATED] == ST_EXCLUSIVE_SPLIT) e->has_splits = true;
     if (el.kind == EK_CATCH) e->has_catch = true;
+    if (el.kind == EK_PAR) e->has_parallel = true;
   }
   if (e->has_catch) {
     int orc = ensure_outbox(e);
@@ -721,12 +757,12 @@ int zb_set_job_completion_payload(zb_engine* e, int64_t workflow_key, const char
   return upload_model(e);
 }
 
-int zb_submit_creates(zb_engine* e, const char* pid, int32_t version, int64_t workflow_key, size_t n,
-                      const uint8_t* payloads, const uint64_t* offsets) {
-  if (!e || (n > 0 && (!payloads || !offsets)) || !pid) return ZB_EINVAL;
-  // resolve like CreateWorkflowInstanceEventProcessor (all workflows are deployed locally)
+}  // extern "C"
+
+// resolve a CREATE's workflow like CreateWorkflowInstanceEventProcessor (all workflows are deployed locally):
+// workflow_key > 0 by key, else version > 0 by (process id, version), else the latest version
+uint16_t resolve_process(const zb_engine* e, const std::string& spid, int32_t version, int64_t workflow_key) {
   uint16_t pelem = NO_ELEM;
-  const std::string spid(pid);
   const auto& W = e->model.workflows;
   if (workflow_key > 0) {
     for (auto& w : W)
@@ -739,12 +775,45 @@ int zb_submit_creates(zb_engine* e, const char* pid, int32_t version, int64_t wo
     for (auto& w : W)
       if (e->model.str(w.pid_off, w.pid_len) == spid && w.version > best) { best = w.version; pelem = w.process_elem; }
   }
-  if (!e->staged_pending) {  // the previous batch was injected: start a new one
-    e->staged.clear();
-    e->staged_arena.clear();
-    e->pending_ranges.clear();
-    e->staged_uploaded = false;
+  return pelem;
+}
+
+bool is_doc(const uint8_t* p, uint64_t len) {  // DocumentValue: nil / empty -> {}, else a map
+  if (len == 0 || (len == 1 && p[0] == 0xc0)) return true;
+  const uint8_t b = p[0];
+  return (b & 0xf0) == 0x80 || b == 0xde || b == 0xdf;
+}
+
+// the staged batch of the last zb_step was injected: start a new one
+void begin_staging(zb_engine* e) {
+  if (e->staged_pending) return;
+  e->staged.clear();
+  e->staged_arena.clear();
+  e->pending_ranges.clear();
+  e->staged_lookup.clear();
+  e->staged_only_creates = true;
+  e->staged_has_cancel = false;
+  e->tick_inst.clear();
+  e->tick_aik.clear();
+  e->staged_uploaded = false;
+}
+
+extern "C" {
+
+int zb_submit_creates(zb_engine* e, const char* pid, int32_t version, int64_t workflow_key, size_t n,
+                      const uint8_t* payloads, const uint64_t* offsets) {
+  if (!e || (n > 0 && (!payloads || !offsets)) || !pid) return ZB_EINVAL;
+  // validate everything before any staged state changes (all-or-nothing)
+  for (size_t i = 0; i < n; i++) {
+    if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 0xffffffffull) return fail(e, ZB_EINVAL, "bad payload offsets");
+    if (!is_doc(payloads + offsets[i], offsets[i + 1] - offsets[i]))
+      return fail(e, ZB_EINVAL, "Document has invalid format. On root level an object is only allowed.");
   }
+  const std::string spid(pid);
+  if (spid.size() > 0xffff) return fail(e, ZB_EINVAL, "bpmn process id too long");
+  const uint16_t pelem = resolve_process(e, spid, version, workflow_key);
+  begin_staging(e);
+  e->staged_uploaded = false;  // the device copy (if any) no longer matches
   if (e->staged.empty()) {
     e->staged_elem = pelem;
     e->staged_uniform = true;
@@ -761,6 +830,7 @@ int zb_submit_creates(zb_engine* e, const char* pid, int32_t version, int64_t wo
   pr.pid_len = (uint16_t)spid.size();
   e->cmd_pool.insert(e->cmd_pool.end(), spid.begin(), spid.end());
   e->staged.reserve(e->staged.size() + n);
+  e->staged_lookup.reserve(e->staged_lookup.size() + n);
   for (size_t i = 0; i < n; i++) {
     const uint8_t* p = payloads + offsets[i];
     uint64_t len = offsets[i + 1] - offsets[i];
@@ -769,9 +839,6 @@ int zb_submit_creates(zb_engine* e, const char* pid, int32_t version, int64_t wo
       const uint8_t empty = 0x80;  // DocumentValue: nil / empty -> {}
       ref = add_blob(e->staged_arena, &empty, 1);
     } else {
-      uint8_t b = p[0];
-      if (!((b & 0xf0) == 0x80 || b == 0xde || b == 0xdf))
-        return fail(e, ZB_EINVAL, "Document has invalid format. On root level an object is only allowed.");
       ref = add_blob(e->staged_arena, p, (uint32_t)len);
       e->staged_max_len = std::max<uint32_t>(e->staged_max_len, (uint32_t)len);
     }
@@ -784,10 +851,354 @@ int zb_submit_creates(zb_engine* e, const char* pid, int32_t version, int64_t wo
     d.intent = WI_CREATE;
     d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_COMMAND, false);
     e->staged.push_back(d);
+    e->staged_lookup.push_back(INT64_MIN);
   }
   e->pending_ranges.push_back(pr);
-  e->staged_uploaded = false;
   e->staged_pending = true;
+  return ZB_OK;
+}
+
+}  // extern "C"
+
+// ---- zb_submit: host-side decoding of reference record values (UnpackedObject.wrap, ObjectValue.java:93-131)
+namespace {
+
+struct MpIn {
+  const uint8_t* p;
+  size_t n, o = 0;
+  bool ok = true;
+  uint8_t u8() { if (o >= n) { ok = false; return 0; } return p[o++]; }
+  uint64_t be(int k) { uint64_t v = 0; for (int i = 0; i < k; i++) v = (v << 8) | u8(); return v; }
+  uint32_t map_hdr() {
+    uint8_t h = u8();
+    if ((h & 0xf0) == 0x80) return h & 0x0f;
+    if (h == 0xde) return (uint32_t)be(2);
+    if (h == 0xdf) return (uint32_t)be(4);
+    ok = false;
+    return 0;
+  }
+  bool str(const uint8_t*& s, uint32_t& len) {
+    uint8_t h = u8();
+    if ((h & 0xe0) == 0xa0) len = h & 0x1f;
+    else if (h == 0xd9) len = (uint32_t)be(1);
+    else if (h == 0xda) len = (uint32_t)be(2);
+    else if (h == 0xdb) len = (uint32_t)be(4);
+    else { ok = false; return false; }
+    if (o + len > n) { ok = false; return false; }
+    s = p + o; o += len;
+    return true;
+  }
+  bool bin(const uint8_t*& s, uint32_t& len) {
+    uint8_t h = u8();
+    if (h == 0xc4) len = (uint32_t)be(1);
+    else if (h == 0xc5) len = (uint32_t)be(2);
+    else if (h == 0xc6) len = (uint32_t)be(4);
+    else { ok = false; return false; }
+    if (o + len > n) { ok = false; return false; }
+    s = p + o; o += len;
+    return true;
+  }
+  int64_t integer() {
+    uint8_t h = u8();
+    if (h <= 0x7f) return h;
+    if (h >= 0xe0) return (int8_t)h;
+    switch (h) {
+      case 0xcc: return (int64_t)be(1);
+      case 0xcd: return (int64_t)be(2);
+      case 0xce: return (int64_t)be(4);
+      case 0xcf: return (int64_t)be(8);
+      case 0xd0: return (int8_t)be(1);
+      case 0xd1: return (int16_t)be(2);
+      case 0xd2: return (int32_t)be(4);
+      case 0xd3: return (int64_t)be(8);
+    }
+    ok = false;
+    return 0;
+  }
+  void skip(int64_t count = 1) {  // MsgPackReader.skipValues
+    while (count > 0 && ok) {
+      uint8_t b = u8();
+      if (b <= 0x7f || b >= 0xe0 || b == 0xc0 || b == 0xc2 || b == 0xc3) {
+      } else if ((b & 0xf0) == 0x80) count += (int64_t)(b & 0x0f) * 2;
+      else if ((b & 0xf0) == 0x90) count += (b & 0x0f);
+      else if ((b & 0xe0) == 0xa0) o += (b & 0x1f);
+      else switch (b) {
+        case 0xd0: case 0xcc: o += 1; break;
+        case 0xd1: case 0xcd: o += 2; break;
+        case 0xd2: case 0xce: case 0xca: o += 4; break;
+        case 0xd3: case 0xcf: case 0xcb: o += 8; break;
+        case 0xc4: case 0xd9: o += be(1); break;
+        case 0xc5: case 0xda: o += be(2); break;
+        case 0xc6: case 0xdb: o += be(4); break;
+        case 0xd4: o += 2; break;
+        case 0xd5: o += 3; break;
+        case 0xd6: o += 5; break;
+        case 0xd7: o += 9; break;
+        case 0xd8: o += 17; break;
+        case 0xc7: o += 1 + be(1); break;
+        case 0xc8: o += 1 + be(2); break;
+        case 0xc9: o += 1 + be(4); break;
+        case 0xdc: count += be(2); break;
+        case 0xdd: count += be(4); break;
+        case 0xde: count += (int64_t)be(2) * 2; break;
+        case 0xdf: count += (int64_t)be(4) * 2; break;
+        default: ok = false;
+      }
+      if (o > n) ok = false;
+      count--;
+    }
+  }
+  bool key_is(const uint8_t* k, uint32_t kl, const char* s) { return kl == strlen(s) && memcmp(k, s, kl) == 0; }
+};
+
+// the declared properties a submitted value carries (defaults as in the reference records)
+struct Decoded {
+  std::string bpmn_process_id, message_name, activity_id;
+  int64_t version = -1, workflow_key = -1, wik = -1, aik = -1, scope = -1;
+  const uint8_t* payload = nullptr;
+  uint32_t payload_len = 0;
+};
+
+bool decode_value(uint8_t vt, const uint8_t* v, size_t n, Decoded& d) {
+  if (n == 0) return true;
+  MpIn in{v, n};
+  const uint32_t props = in.map_hdr();
+  for (uint32_t i = 0; i < props && in.ok; i++) {
+    const uint8_t* k; uint32_t kl;
+    if (!in.str(k, kl)) return false;
+    const uint8_t* s; uint32_t sl;
+    if (in.key_is(k, kl, "payload")) {
+      if (!in.bin(d.payload, d.payload_len)) return false;
+    } else if (vt == ZB_VT_WORKFLOW_INSTANCE && in.key_is(k, kl, "bpmnProcessId")) {
+      if (!in.str(s, sl)) return false;
+      d.bpmn_process_id.assign((const char*)s, sl);
+    } else if (vt == ZB_VT_WORKFLOW_INSTANCE && in.key_is(k, kl, "version")) d.version = in.integer();
+    else if (vt == ZB_VT_WORKFLOW_INSTANCE && in.key_is(k, kl, "workflowKey")) d.workflow_key = in.integer();
+    else if (vt != ZB_VT_JOB && in.key_is(k, kl, "workflowInstanceKey")) d.wik = in.integer();
+    else if (vt == ZB_VT_WORKFLOW_INSTANCE && in.key_is(k, kl, "scopeInstanceKey")) d.scope = in.integer();
+    else if (vt == ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION && in.key_is(k, kl, "activityInstanceKey")) d.aik = in.integer();
+    else if (vt == ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION && in.key_is(k, kl, "messageName")) {
+      if (!in.str(s, sl)) return false;
+      d.message_name.assign((const char*)s, sl);
+    } else if (vt == ZB_VT_WORKFLOW_INSTANCE && in.key_is(k, kl, "activityId")) {
+      if (!in.str(s, sl)) return false;
+      d.activity_id.assign((const char*)s, sl);
+    } else if (vt == ZB_VT_JOB && in.key_is(k, kl, "headers")) {  // JobHeaders.java:33-51
+      const uint32_t hp = in.map_hdr();
+      for (uint32_t j = 0; j < hp && in.ok; j++) {
+        const uint8_t* hk; uint32_t hkl;
+        if (!in.str(hk, hkl)) return false;
+        if (in.key_is(hk, hkl, "workflowInstanceKey")) d.wik = in.integer();
+        else if (in.key_is(hk, hkl, "activityInstanceKey")) d.aik = in.integer();
+        else in.skip();
+      }
+    } else in.skip();
+  }
+  return in.ok && in.o == n;
+}
+
+// MsgPackWriter.writeInteger (MsgPackWriter.java:143-201)
+void put_int(std::vector<uint8_t>& b, int64_t v) {
+  auto be = [&](uint64_t x, int k) { for (int i = k - 1; i >= 0; i--) b.push_back((uint8_t)(x >> (8 * i))); };
+  if (v < -(1LL << 5)) {
+    if (v < -(1LL << 15)) { if (v < -(1LL << 31)) { b.push_back(0xd3); be((uint64_t)v, 8); } else { b.push_back(0xd2); be((uint64_t)v, 4); } }
+    else if (v < -(1 << 7)) { b.push_back(0xd1); be((uint64_t)v, 2); }
+    else { b.push_back(0xd0); be((uint64_t)v, 1); }
+  } else if (v < (1 << 7)) b.push_back((uint8_t)v);
+  else if (v < (1LL << 8)) { b.push_back(0xcc); be((uint64_t)v, 1); }
+  else if (v < (1LL << 16)) { b.push_back(0xcd); be((uint64_t)v, 2); }
+  else if (v < (1LL << 32)) { b.push_back(0xce); be((uint64_t)v, 4); }
+  else { b.push_back(0xcf); be((uint64_t)v, 8); }
+}
+void put_str(std::vector<uint8_t>& b, const std::string& s) {
+  const size_t n = s.size();
+  if (n < 32) b.push_back((uint8_t)(0xa0 | n));
+  else if (n < 256) { b.push_back(0xd9); b.push_back((uint8_t)n); }
+  else if (n < 65536) { b.push_back(0xda); b.push_back((uint8_t)(n >> 8)); b.push_back((uint8_t)n); }
+  else { b.push_back(0xdb); for (int i = 3; i >= 0; i--) b.push_back((uint8_t)(n >> (8 * i))); }
+  b.insert(b.end(), s.begin(), s.end());
+}
+void put_bin(std::vector<uint8_t>& b, const uint8_t* p, uint32_t n) {
+  if (n < 256) { b.push_back(0xc4); b.push_back((uint8_t)n); }
+  else if (n < 65536) { b.push_back(0xc5); b.push_back((uint8_t)(n >> 8)); b.push_back((uint8_t)n); }
+  else { b.push_back(0xc6); for (int i = 3; i >= 0; i--) b.push_back((uint8_t)(n >> (8 * i))); }
+  b.insert(b.end(), p, p + n);
+}
+
+// the command value as the reference writes it back (CommandProcessorImpl.accept / writeRejection:
+// record.getValue() re-encoded: declared properties in order, ObjectValue.java:140-153)
+std::vector<uint8_t> reencode(uint8_t vt, const Decoded& d, const uint8_t* doc, uint32_t doc_len) {
+  std::vector<uint8_t> b;
+  if (vt == ZB_VT_WORKFLOW_INSTANCE) {  // WorkflowInstanceRecord.java:39-60
+    b.push_back(0x87);
+    put_str(b, "bpmnProcessId"); put_str(b, d.bpmn_process_id);
+    put_str(b, "version"); put_int(b, d.version);
+    put_str(b, "workflowKey"); put_int(b, d.workflow_key);
+    put_str(b, "workflowInstanceKey"); put_int(b, d.wik);
+    put_str(b, "activityId"); put_str(b, d.activity_id);
+    put_str(b, "payload"); put_bin(b, doc, doc_len);
+    put_str(b, "scopeInstanceKey"); put_int(b, d.scope);
+  } else {  // WorkflowInstanceSubscriptionRecord.java:26-38
+    b.push_back(0x84);
+    put_str(b, "workflowInstanceKey"); put_int(b, d.wik);
+    put_str(b, "activityInstanceKey"); put_int(b, d.aik);
+    put_str(b, "messageName"); put_str(b, d.message_name);
+    put_str(b, "payload"); put_bin(b, doc, doc_len);
+  }
+  return b;
+}
+
+}  // namespace
+
+extern "C" {
+
+int zb_submit(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* values, size_t values_len) {
+  if (!e || (n > 0 && (!recs || (!values && values_len)))) return ZB_EINVAL;
+  if (e->failed) return fail(e, ZB_EPROCESSING, "partition stopped after a processing failure: " + e->err);
+  struct Prep {
+    zb_rec d;
+    int64_t lookup = INT64_MIN, inst = INT64_MIN, aik = INT64_MIN;
+    bool scope_cmd = false, pair = false, cancel = false, create = false;
+    uint16_t pelem = NO_ELEM;
+    std::string pid;
+    int64_t wkey = -1;
+    int32_t version = -1;
+    const uint8_t* raw = nullptr;
+    uint32_t raw_len = 0;
+    const uint8_t* doc = nullptr;
+    uint32_t doc_len = 0;
+    std::vector<uint8_t> canon;
+  };
+  std::vector<Prep> prep(n);
+  static const uint8_t EMPTY = 0x80;
+  // 1. decode + validate (nothing staged on any error)
+  for (size_t i = 0; i < n; i++) {
+    const zb_rec_desc& r = recs[i];
+    if (r.value_offset > values_len || r.value_length > values_len - r.value_offset)
+      return fail(e, ZB_EINVAL, "record " + std::to_string(i) + ": value out of range");
+    Prep& p = prep[i];
+    p.raw = values + r.value_offset;
+    p.raw_len = r.value_length;
+    Decoded dv;
+    const uint8_t vt = r.value_type, rt = r.record_type, it = r.intent;
+    const bool wf_cmd = vt == ZB_VT_WORKFLOW_INSTANCE && rt == ZB_RT_COMMAND;
+    const bool job_ev = vt == ZB_VT_JOB && rt == ZB_RT_EVENT && (it == JI_CREATED || it == JI_COMPLETED);
+    const bool corr = vt == ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION && rt == ZB_RT_COMMAND && it == 0;
+    if (!(wf_cmd && (it == WI_CREATE || it == WI_CANCEL || it == WI_UPDATE_PAYLOAD)) && !job_ev && !corr)
+      return fail(e, ZB_EUNSUPPORTED, "record " + std::to_string(i) + ": no workflow processor is registered for "
+                                      "(recordType, valueType, intent) = (" + std::to_string(rt) + ", " +
+                                      std::to_string(vt) + ", " + std::to_string(it) + ")");
+    if (!decode_value(vt, p.raw, p.raw_len, dv))
+      return fail(e, ZB_EINVAL, "record " + std::to_string(i) + ": malformed msgpack value");
+    p.doc = dv.payload ? dv.payload : &EMPTY;
+    p.doc_len = dv.payload ? dv.payload_len : 1;
+    if (p.doc_len == 0 || (p.doc_len == 1 && p.doc[0] == 0xc0)) { p.doc = &EMPTY; p.doc_len = 1; }
+    if (!is_doc(p.doc, p.doc_len))
+      return fail(e, ZB_EINVAL, "record " + std::to_string(i) + ": Document has invalid format. On root level an object is only allowed.");
+    zb_rec& d = p.d;
+    d.key = r.key;
+    d.scope_key = -1;
+    d.inst_key = -1;
+    d.payload = 0;
+    d.elem = NO_ELEM;
+    d.intent = it;
+    d.kind = (uint8_t)(make_kind(vt, rt, false) | KIND_RAW);
+    if (wf_cmd && it == WI_CREATE) {
+      p.create = true;
+      if (dv.bpmn_process_id.size() > 0xffff) return fail(e, ZB_EINVAL, "bpmn process id too long");
+      p.pid = dv.bpmn_process_id;
+      p.version = (int32_t)dv.version;
+      p.wkey = dv.workflow_key;
+      d.elem = resolve_process(e, p.pid, p.version, p.wkey);
+      d.key = -1;
+    } else if (wf_cmd) {
+      p.scope_cmd = true;
+      p.cancel = it == WI_CANCEL;
+      p.lookup = p.cancel ? r.key : dv.wik;
+      p.inst = p.lookup;
+      d.inst_key = dv.wik;
+      p.canon = reencode(vt, dv, p.doc, p.doc_len);
+    } else if (job_ev) {
+      p.lookup = dv.aik;
+      p.inst = dv.wik;
+      p.aik = dv.aik;
+      d.scope_key = dv.aik;  // headers.activityInstanceKey
+      d.inst_key = dv.wik;
+    } else {  // CORRELATE: key = its log position (positionAsKey)
+      p.lookup = dv.aik;
+      p.inst = dv.wik;
+      p.aik = dv.aik;
+      d.key = KEY_IS_POSITION;
+      d.scope_key = dv.aik;
+      d.inst_key = dv.wik;
+      p.canon = reencode(vt, dv, p.doc, p.doc_len);
+    }
+  }
+  // 2. race rules of one tick (include/zb_engine.h), against what is staged already
+  if (!e->staged_pending) { e->tick_inst.clear(); e->tick_aik.clear(); }
+  std::unordered_map<int64_t, uint8_t> inst = e->staged_pending ? e->tick_inst : std::unordered_map<int64_t, uint8_t>();
+  std::unordered_set<int64_t> aiks = e->staged_pending ? e->tick_aik : std::unordered_set<int64_t>();
+  const zb_rec* prev_staged = (e->staged_pending && !e->staged.empty()) ? &e->staged.back() : nullptr;
+  for (size_t i = 0; i < n; i++) {
+    Prep& p = prep[i];
+    if (p.create) continue;
+    const zb_rec* prev = i > 0 ? &prep[i - 1].d : prev_staged;
+    // JOB CREATED directly followed by its JOB COMPLETED: one batch, processed in order by one thread
+    if (recs[i].value_type == ZB_VT_JOB && recs[i].intent == JI_COMPLETED && prev && kind_vt(prev->kind) == ZB_VT_JOB &&
+        prev->intent == JI_CREATED && prev->key == recs[i].key && prev->scope_key == p.d.scope_key) {
+      p.pair = true;
+      p.d.kind |= 0x40;
+      continue;
+    }
+    uint8_t& f = inst[p.inst];
+    if ((f & 1) || (p.scope_cmd && f)) {
+      return fail(e, ZB_EUNSUPPORTED, "record " + std::to_string(i) + ": workflow instance " + std::to_string(p.inst) +
+                                          " already has a record in this tick next to a CANCEL / UPDATE_PAYLOAD "
+                                          "(split the tick: zb_step, then submit the rest)");
+    }
+    f |= p.scope_cmd ? 1 : 2;
+    if (p.aik != INT64_MIN) {
+      if (aiks.count(p.aik))
+        return fail(e, ZB_EUNSUPPORTED, "record " + std::to_string(i) + ": activity instance " + std::to_string(p.aik) +
+                                            " already has a record in this tick (split the tick)");
+      aiks.insert(p.aik);
+    }
+  }
+  // 3. stage
+  begin_staging(e);
+  e->staged_uploaded = false;
+  e->tick_inst.swap(inst);
+  e->tick_aik.swap(aiks);
+  for (size_t i = 0; i < n; i++) {
+    Prep& p = prep[i];
+    // arena: [payload document][verbatim value] (+ [document][re-encoded command value])
+    p.d.payload = add_blob(e->staged_arena, p.doc, p.doc_len);
+    add_blob(e->staged_arena, p.raw, p.raw_len);
+    if (!p.canon.empty()) {
+      add_blob(e->staged_arena, p.doc, p.doc_len);
+      add_blob(e->staged_arena, p.canon.data(), (uint32_t)p.canon.size());
+    }
+    if (p.create) {
+      if (e->staged.empty()) { e->staged_elem = p.d.elem; e->staged_uniform = true; e->staged_max_len = 1; }
+      else if (p.d.elem != e->staged_elem) e->staged_uniform = false;
+      e->staged_max_len = std::max<uint32_t>(e->staged_max_len, p.doc_len);
+      zb_engine::PendingRange pr;
+      pr.first = (int64_t)e->staged.size();
+      pr.last = pr.first + 1;
+      pr.workflow_key = p.wkey;
+      pr.version = p.version;
+      pr.pid_off = (uint32_t)e->cmd_pool.size();
+      pr.pid_len = (uint16_t)p.pid.size();
+      e->cmd_pool.insert(e->cmd_pool.end(), p.pid.begin(), p.pid.end());
+      e->pending_ranges.push_back(pr);
+    } else {
+      e->staged_only_creates = false;
+      if (p.cancel) e->staged_has_cancel = true;
+    }
+    e->staged.push_back(p.d);
+    e->staged_lookup.push_back(p.lookup == INT64_MIN ? INT64_MIN : p.lookup);
+  }
+  if (n) e->staged_pending = true;
   return ZB_OK;
 }
 
@@ -801,8 +1212,13 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   int64_t traj_base = 0, traj_n = 0;
   // ---- inject staged input at the log tail (engine is quiescent between steps)
   if (e->staged_pending && !e->staged.empty()) {
-    // an idle partition fed only CREATE commands runs as independent trajectories (zb_traj.hip)
-    try_traj = !(e->cfg.flags & ZB_CFG_WAVE_ONLY) && max_waves == 0 &&
+    if (!e->staged_only_creates && e->host_hdr.begin != e->host_hdr.end)
+      return fail(e, ZB_EINVAL, "records other than CREATE are injected into a quiescent partition only: "
+                                "step it to quiescence first");
+    // an idle partition fed only CREATE commands runs as independent trajectories (zb_traj.hip) -- with the
+    // canonical job harness and no parallel gateways (the general wave pipeline covers everything else)
+    try_traj = !(e->cfg.flags & (ZB_CFG_WAVE_ONLY | ZB_CFG_EXTERNAL_JOBS)) && max_waves == 0 &&
+               e->staged_only_creates && !e->has_parallel &&
                (e->traj_model_ok || (e->cls_ok && e->staged_uniform)) &&
                e->host_hdr.begin == e->host_hdr.end;
     traj_base = e->host_hdr.end;
@@ -827,6 +1243,24 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     ip.arena_base = (uint64_t)e->host_hdr.arena_next;
     ip.staged_bytes = e->staged_arena.size();
     launch_inject(ip, e->stream);
+    // records naming an element instance by key: its row (ElementInstanceIndex.getInstance)
+    std::vector<std::pair<int64_t, int64_t>> look;
+    for (int64_t i = 0; i < n; i++)
+      if (e->staged_lookup[i] != INT64_MIN) look.emplace_back(e->staged_lookup[i], ip.log_base + i);
+    if (!look.empty()) {
+      std::sort(look.begin(), look.end());
+      std::vector<int64_t> lk(look.size()), lp(look.size());
+      for (size_t i = 0; i < look.size(); i++) { lk[i] = look[i].first; lp[i] = look[i].second; }
+      HIPCHECK(e, e->d_lookup_keys.upload(lk, e->stream));
+      HIPCHECK(e, e->d_lookup_pos.upload(lp, e->stream));
+      ResolveParams rp{};
+      rp.rmeta = e->rmeta; rp.rkeys = e->rkeys; rp.rows = (uint64_t)e->host_hdr.rows_next;
+      rp.keys = e->d_lookup_keys.p; rp.pos = e->d_lookup_pos.p; rp.n = (int64_t)look.size();
+      rp.links = e->links;
+      launch_resolve(rp, e->stream);
+      HIPCHECK(e, hipStreamSynchronize(e->stream));  // the host vectors die at scope end
+    }
+    if (e->staged_has_cancel) e->term = true;
     for (auto& pr : e->pending_ranges) {
       CmdRange r{};
       r.pos_begin = ip.log_base + pr.first;
@@ -862,6 +1296,10 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
       WaveParams p = wave_params(e);
       hipEvent_t* ev = &e->ev[EV_PER_WAVE * i];
       HIPCHECK(e, hipEventRecord(ev[0], e->stream));
+      if (p.has_parallel || p.term) {  // scope-wide counters / first-child requests of the chunk
+        launch_pre(p, e->stream);
+        if (p.term) launch_children(p, e->stream);
+      }
       launch_process(p, e->stream);
       HIPCHECK(e, hipEventRecord(ev[1], e->stream));
       launch_scan(p, e->stream);
@@ -872,6 +1310,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
       if (e->has_splits) launch_cond(p, e->stream);
       HIPCHECK(e, hipEventRecord(ev[3], e->stream));
       e->wave++;
+      e->epoch++;
     }
     HIPCHECK(e, hipGetLastError());
     HIPCHECK(e, hipMemcpyAsync(e->h_hdr_pinned, e->hdr + (e->wave & 1), sizeof(WaveHdr), hipMemcpyDeviceToHost,
@@ -909,13 +1348,14 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (stats) *stats = st;
   if (!quiescent) return ZB_EAGAIN;
+  e->term = false;  // every termination chain has ended
   return ZB_OK;
 }
 
 int64_t zb_log_size(zb_engine* e) { return e ? e->host_hdr.end : -1; }
 
 int zb_read_descriptors(zb_engine* e, int64_t start, int64_t count, zb_rec* out) {
-  if (!e || start < 0 || count < 0 || start + count > e->host_hdr.end || (!out && count)) return ZB_EINVAL;
+  if (!e || start < e->log_floor || count < 0 || start + count > e->host_hdr.end || (!out && count)) return ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
   HIPCHECK(e, hipMemcpyAsync(out, e->log + start, count * sizeof(zb_rec), hipMemcpyDeviceToHost, e->stream));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
@@ -924,7 +1364,7 @@ int zb_read_descriptors(zb_engine* e, int64_t start, int64_t count, zb_rec* out)
 
 int zb_drain(zb_engine* e, int64_t start, int64_t count, zb_record_header* headers, uint8_t* values,
              size_t values_cap, size_t* values_len) {
-  if (!e || start < 0 || count < 0 || start + count > e->host_hdr.end) return ZB_EINVAL;
+  if (!e || start < e->log_floor || count < 0 || start + count > e->host_hdr.end) return ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
   if (count == 0) {
     if (values_len) *values_len = 0;
@@ -1301,12 +1741,247 @@ int zb_counters(zb_engine* e, int64_t out[8]) {
   HIPCHECK(e, hipMemcpy(s, e->dstats, sizeof(s), hipMemcpyDeviceToHost));
   out[0] = (int64_t)s[2];
   out[1] = (int64_t)s[1];
-  out[2] = 0;
+  out[2] = (int64_t)s[7];
   out[3] = e->host_hdr.wf_next;
   out[4] = e->host_hdr.job_next;
   out[5] = e->host_hdr.rows_next;
   out[6] = e->host_hdr.arena_next;
   out[7] = e->host_hdr.end;
+  return ZB_OK;
+}
+
+}  // extern "C"
+
+// ---- element-instance index read-back and snapshots
+namespace {
+
+int require_quiescent(zb_engine* e) {
+  if (e->failed) return fail(e, ZB_EPROCESSING, "partition stopped after a processing failure: " + e->err);
+  if (e->host_hdr.begin != e->host_hdr.end) return fail(e, ZB_EINVAL, "partition not quiescent");
+  return ZB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int zb_read_instances(zb_engine* e, uint8_t* buf, size_t cap, size_t* len, uint64_t* count) {
+  if (!e || !len) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  const uint64_t rows = (uint64_t)e->host_hdr.rows_next;
+  *len = 0;
+  if (count) *count = 0;
+  if (rows == 0) return ZB_OK;
+  uint32_t* d_count = nullptr;
+  int64_t* d_keys = nullptr;
+  uint32_t* d_rows = nullptr;
+  zb_rec* d_descs = nullptr;
+  InstHead* d_heads = nullptr;
+  uint64_t *d_len = nullptr, *d_off = nullptr;
+  uint8_t* d_out = nullptr;
+  zb_record_header* d_hdrs = nullptr;
+  void* d_tmp = nullptr;
+  int rc = ZB_OK;
+  auto cleanup = [&]() {
+    void* ps[] = {d_count, d_keys, d_rows, d_descs, d_heads, d_len, d_off, d_out, d_hdrs, d_tmp};
+    for (void* q : ps)
+      if (q) (void)hipFree(q);
+  };
+  do {
+    if (hipMalloc(&d_count, 4) != hipSuccess || hipMalloc(&d_keys, rows * 8) != hipSuccess ||
+        hipMalloc(&d_rows, rows * 4) != hipSuccess) { rc = fail(e, ZB_ENOMEM, "read_instances buffers"); break; }
+    if (hipMemsetAsync(d_count, 0, 4, e->stream) != hipSuccess) { rc = ZB_EDEVICE; break; }
+    LiveParams lp{};
+    lp.rmeta = e->rmeta; lp.rkeys = e->rkeys; lp.rows = rows; lp.count = d_count; lp.cap = rows;
+    lp.keys = d_keys; lp.row_of = d_rows;
+    launch_live_rows(lp, e->stream);
+    uint32_t live = 0;
+    if (hipMemcpyAsync(&live, d_count, 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess) { rc = fail(e, ZB_EDEVICE, "read_instances count"); break; }
+    if (count) *count = live;
+    if (live == 0) break;
+    // key order (ElementInstanceIndex is a hash map; the dump is canonicalised by key)
+    std::vector<int64_t> keys(live);
+    std::vector<uint32_t> rws(live);
+    if (hipMemcpy(keys.data(), d_keys, live * 8, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(rws.data(), d_rows, live * 4, hipMemcpyDeviceToHost) != hipSuccess) { rc = ZB_EDEVICE; break; }
+    std::vector<uint32_t> ord(live);
+    for (uint32_t i = 0; i < live; i++) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return keys[a] < keys[b]; });
+    std::vector<uint32_t> sorted_rows(live);
+    for (uint32_t i = 0; i < live; i++) sorted_rows[i] = rws[ord[i]];
+    if (hipMemcpy(d_rows, sorted_rows.data(), live * 4, hipMemcpyHostToDevice) != hipSuccess) { rc = ZB_EDEVICE; break; }
+    if (hipMalloc(&d_descs, live * sizeof(zb_rec)) != hipSuccess || hipMalloc(&d_heads, live * sizeof(InstHead)) != hipSuccess ||
+        hipMalloc(&d_len, (live + 1) * 8) != hipSuccess || hipMalloc(&d_off, (live + 1) * 8) != hipSuccess ||
+        hipMalloc(&d_hdrs, live * sizeof(zb_record_header)) != hipSuccess) { rc = fail(e, ZB_ENOMEM, "read_instances"); break; }
+    lp.n = live; lp.descs = d_descs; lp.heads = d_heads;
+    launch_row_descs(lp, e->stream);
+    // values: the serializer over the descriptors (size pass, scan, write pass)
+    SerParams sp{};
+    sp.log = d_descs; sp.arena = e->arena; sp.elems = e->d_elems.p; sp.wfs = e->d_wfs.p;
+    sp.queries = e->d_queries.p; sp.pool = e->d_pool.p; sp.ranges = nullptr; sp.nranges = 0;
+    sp.cmd_pool = nullptr; sp.start = 0; sp.count = live;
+    SerParams sz = sp;
+    sz.lengths = (uint32_t*)d_off;
+    launch_ser_size(sz, e->stream);
+    std::vector<uint32_t> lens(live);
+    if (hipMemcpyAsync(lens.data(), d_off, live * 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess) { rc = ZB_EDEVICE; break; }
+    std::vector<uint64_t> offs(live + 1, 0);
+    for (uint32_t i = 0; i < live; i++) offs[i + 1] = offs[i] + lens[i];
+    const uint64_t total = offs[live];
+    *len = (size_t)(total + (uint64_t)live * sizeof(InstHead));
+    if (!buf || cap < *len) { rc = ZB_ENOMEM; break; }
+    if (hipMalloc(&d_out, total + 1) != hipSuccess ||
+        hipMemcpy(d_len, offs.data(), (live + 1) * 8, hipMemcpyHostToDevice) != hipSuccess) { rc = ZB_ENOMEM; break; }
+    SerParams wr = sp;
+    wr.offsets = d_len; wr.out = d_out; wr.headers = d_hdrs;
+    launch_ser_write(wr, e->stream);
+    std::vector<InstHead> heads(live);
+    std::vector<uint8_t> vals(total);
+    if (hipMemcpyAsync(heads.data(), d_heads, live * sizeof(InstHead), hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+        (total && hipMemcpyAsync(vals.data(), d_out, total, hipMemcpyDeviceToHost, e->stream) != hipSuccess) ||
+        hipStreamSynchronize(e->stream) != hipSuccess) { rc = fail(e, ZB_EDEVICE, "read_instances copy"); break; }
+    size_t o = 0;
+    for (uint32_t i = 0; i < live; i++) {
+      InstHead h = heads[i];
+      h.value_len = lens[i];
+      std::memcpy(buf + o, &h, sizeof(h));
+      o += sizeof(h);
+      std::memcpy(buf + o, vals.data() + offs[i], lens[i]);
+      o += lens[i];
+    }
+  } while (0);
+  cleanup();
+  return rc;
+}
+
+}  // extern "C"
+
+namespace {
+constexpr uint64_t SNAP_MAGIC = 0x31504e53425a4755ull;  // "UGZBSNP1"
+struct SnapHead {
+  uint64_t magic;
+  uint64_t model_hash;    // deployments the snapshot was taken with (zb_restore checks)
+  WaveHdr hdr;
+  uint64_t stats[8];
+  int64_t epoch, msg_key_next;
+  uint64_t sub_count, msg_count, store_cap, head_mask;
+  uint64_t rows, arena_bytes;
+  uint64_t ranges, cmd_pool;
+};
+
+uint64_t model_hash(const zb_engine* e) {  // FNV-1a over the deployed tables
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](const void* p, size_t n) {
+    const uint8_t* b = (const uint8_t*)p;
+    for (size_t i = 0; i < n; i++) { h ^= b[i]; h *= 1099511628211ull; }
+  };
+  mix(e->model.elems.data(), e->model.elems.size() * sizeof(DevElem));
+  mix(e->model.workflows.data(), e->model.workflows.size() * sizeof(DevWorkflow));
+  mix(e->model.pool.data(), e->model.pool.size());
+  mix(e->static_blobs.data(), e->static_blobs.size());
+  return h;
+}
+}  // namespace
+
+extern "C" {
+
+int zb_snapshot(zb_engine* e, uint8_t* buf, size_t cap, size_t* len) {
+  if (!e || !len) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  int rc = require_quiescent(e);
+  if (rc != ZB_OK) return rc;
+  if (e->staged_pending && !e->staged.empty()) return fail(e, ZB_EINVAL, "staged input not injected yet");
+  SnapHead h{};
+  h.magic = SNAP_MAGIC;
+  h.model_hash = model_hash(e);
+  h.hdr = e->host_hdr;
+  HIPCHECK(e, hipMemcpy(h.stats, e->dstats, sizeof(h.stats), hipMemcpyDeviceToHost));
+  h.epoch = e->epoch;
+  h.msg_key_next = e->msg_key_next;
+  h.sub_count = e->sub_count; h.msg_count = e->msg_count;
+  h.store_cap = e->subs ? e->store_cap : 0;
+  h.head_mask = e->head_mask;
+  h.rows = (uint64_t)e->host_hdr.rows_next;
+  h.arena_bytes = (uint64_t)e->host_hdr.arena_next;
+  h.ranges = e->ranges.size();
+  h.cmd_pool = e->cmd_pool.size();
+  const uint64_t heads = h.store_cap ? h.head_mask + 1 : 0;
+  const size_t need = sizeof(h) + h.rows * (sizeof(RowMeta) + sizeof(RowKeys) + sizeof(RowAux)) + h.arena_bytes +
+                      h.ranges * sizeof(CmdRange) + h.cmd_pool +
+                      (h.store_cap ? h.store_cap * (sizeof(SubEntry) + sizeof(MsgEntry) + 8) + heads * 8 : 0);
+  *len = need;
+  if (!buf || cap < need) return ZB_ENOMEM;
+  uint8_t* o = buf;
+  std::memcpy(o, &h, sizeof(h)); o += sizeof(h);
+  auto get = [&](const void* src, size_t n) -> bool {
+    if (n && hipMemcpy(o, src, n, hipMemcpyDeviceToHost) != hipSuccess) return false;
+    o += n;
+    return true;
+  };
+  bool ok = get(e->rmeta, h.rows * sizeof(RowMeta)) && get(e->rkeys, h.rows * sizeof(RowKeys)) &&
+            get(e->raux, h.rows * sizeof(RowAux)) && get(e->arena, h.arena_bytes);
+  if (!ok) return fail(e, ZB_EDEVICE, "snapshot copy");
+  std::memcpy(o, e->ranges.data(), h.ranges * sizeof(CmdRange)); o += h.ranges * sizeof(CmdRange);
+  std::memcpy(o, e->cmd_pool.data(), h.cmd_pool); o += h.cmd_pool;
+  if (h.store_cap) {
+    ok = get(e->subs, h.store_cap * sizeof(SubEntry)) && get(e->sub_next, h.store_cap * 4) &&
+         get(e->msgs, h.store_cap * sizeof(MsgEntry)) && get(e->msg_next, h.store_cap * 4) &&
+         get(e->sub_head, heads * 4) && get(e->msg_head, heads * 4);
+    if (!ok) return fail(e, ZB_EDEVICE, "snapshot copy (message stores)");
+  }
+  return ZB_OK;
+}
+
+int zb_restore(zb_engine* e, const uint8_t* buf, size_t len) {
+  if (!e || !buf || len < sizeof(SnapHead)) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  SnapHead h;
+  std::memcpy(&h, buf, sizeof(h));
+  if (h.magic != SNAP_MAGIC) return fail(e, ZB_EINVAL, "not a zb snapshot");
+  if (h.model_hash != model_hash(e)) return fail(e, ZB_EINVAL, "snapshot was taken with other deployments");
+  if (h.rows > e->cfg.row_capacity || h.arena_bytes > e->cfg.arena_bytes || (uint64_t)h.hdr.end > e->cfg.log_capacity)
+    return fail(e, ZB_ENOMEM, "snapshot exceeds this engine's capacities");
+  const uint64_t heads = h.store_cap ? h.head_mask + 1 : 0;
+  const size_t need = sizeof(h) + h.rows * (sizeof(RowMeta) + sizeof(RowKeys) + sizeof(RowAux)) + h.arena_bytes +
+                      h.ranges * sizeof(CmdRange) + h.cmd_pool +
+                      (h.store_cap ? h.store_cap * (sizeof(SubEntry) + sizeof(MsgEntry) + 8) + heads * 8 : 0);
+  if (len < need) return fail(e, ZB_EINVAL, "truncated snapshot");
+  int rc = zb_reset(e, 0);
+  if (rc != ZB_OK) return rc;
+  if (h.store_cap) {
+    rc = ensure_stores(e);
+    if (rc != ZB_OK) return rc;
+    if (e->store_cap != h.store_cap || e->head_mask != h.head_mask)
+      return fail(e, ZB_EINVAL, "snapshot message stores need the same row capacity");
+  }
+  const uint8_t* o = buf + sizeof(h);
+  auto put = [&](void* dst, size_t n) -> bool {
+    if (n && hipMemcpy(dst, o, n, hipMemcpyHostToDevice) != hipSuccess) return false;
+    o += n;
+    return true;
+  };
+  bool ok = put(e->rmeta, h.rows * sizeof(RowMeta)) && put(e->rkeys, h.rows * sizeof(RowKeys)) &&
+            put(e->raux, h.rows * sizeof(RowAux)) && put(e->arena, h.arena_bytes);
+  if (!ok) return fail(e, ZB_EDEVICE, "restore copy");
+  e->ranges.assign((const CmdRange*)o, (const CmdRange*)o + h.ranges); o += h.ranges * sizeof(CmdRange);
+  e->cmd_pool.assign(o, o + h.cmd_pool); o += h.cmd_pool;
+  if (h.store_cap) {
+    ok = put(e->subs, h.store_cap * sizeof(SubEntry)) && put(e->sub_next, h.store_cap * 4) &&
+         put(e->msgs, h.store_cap * sizeof(MsgEntry)) && put(e->msg_next, h.store_cap * 4) &&
+         put(e->sub_head, heads * 4) && put(e->msg_head, heads * 4);
+    if (!ok) return fail(e, ZB_EDEVICE, "restore copy (message stores)");
+  }
+  e->host_hdr = h.hdr;
+  e->host_hdr.begin = e->host_hdr.gen_end = e->host_hdr.end;
+  e->log_floor = e->host_hdr.end;  // the log itself lives in the logstream, not in the snapshot
+  e->epoch = std::max(e->epoch, h.epoch);
+  e->msg_key_next = h.msg_key_next;
+  e->sub_count = h.sub_count; e->msg_count = h.msg_count;
+  e->wave = 0;
+  HIPCHECK(e, hipMemcpy(e->dstats, h.stats, sizeof(h.stats), hipMemcpyHostToDevice));
+  HIPCHECK(e, hipMemcpy(e->hdr, &e->host_hdr, sizeof(WaveHdr), hipMemcpyHostToDevice));
   return ZB_OK;
 }
 

@@ -532,8 +532,30 @@ struct Deployer {
       else if (g == "exclusiveGateway") k = EK_XOR;
       else if (g == "intermediateCatchEvent") k = EK_CATCH;
       else if (g == "sequenceFlow") k = EK_FLOW;
+      else if (g == "parallelGateway") k = EK_PAR;  // EXTENSION (C4)
       else { err = "unsupported element type '" + g + "'"; return ZB_EUNSUPPORTED; }
       new_elem(k, n->get("id") ? n->get("id") : "");
+    }
+    // parallel gateways: join arity (sequence flows targeting the gateway) and, for joins, a counter slot
+    // in the RowAux of their scope (the enclosing process / sub process)
+    std::unordered_map<std::string, int> joins_in_scope;
+    for (const Node* n : order) {
+      if (n->tag != "sequenceFlow" || !n->get("targetRef")) continue;
+      auto it = ids.find(n->get("targetRef"));
+      if (it != ids.end() && E(it->second).kind == EK_PAR) {
+        if (E(it->second).m_in == 255) { err = "parallel gateway with more than 254 incoming flows"; return ZB_EUNSUPPORTED; }
+        E(it->second).m_in++;
+      }
+    }
+    for (const Node* n : order) {
+      if (n->tag != "parallelGateway") continue;
+      DevElem& g = E(ids.at(n->get("id") ? n->get("id") : ""));
+      if (g.m_in < 2) continue;
+      const Node* sc = n->up;
+      while (sc && sc->tag != "subProcess" && sc != proc) sc = sc->up;
+      int& slot = joins_in_scope[sc && sc->get("id") ? sc->get("id") : ""];
+      if (slot >= JOIN_SLOTS) { err = "more than 2 parallel joins directly inside one scope"; return ZB_EUNSUPPORTED; }
+      g.join_slot = (uint8_t)slot++;
     }
     // pass 2: attributes, links, lifecycle bindings
     std::vector<std::vector<uint16_t>> outgoing(t.elems.size());
@@ -562,6 +584,7 @@ struct Deployer {
         if (tk == EK_TASK || tk == EK_SUB || tk == EK_CATCH) st = ST_START_STATEFUL_ELEMENT;
         else if (tk == EK_XOR) st = ST_ACTIVATE_GATEWAY;
         else if (tk == EK_END) st = ST_TRIGGER_END_EVENT;
+        else if (tk == EK_PAR) st = E(di).m_in >= 2 ? ST_PARALLEL_MERGE : ST_ACTIVATE_GATEWAY;
         else { err = "Unsupported element"; return ZB_EUNSUPPORTED; }
         E(ei).step[WI_SEQUENCE_FLOW_TAKEN] = st;
         continue;
@@ -642,6 +665,10 @@ struct Deployer {
           e.step[WI_ELEMENT_ACTIVATED] = ST_TRIGGER_START_EVENT;
           e.step[WI_ELEMENT_TERMINATING] = ST_TERMINATE_CONTAINED_INSTANCES;
           break;
+        case EK_PAR:
+          if (n_out_refs == 0) { err = "parallel gateway without outgoing sequence flow"; return ZB_EUNSUPPORTED; }
+          e.step[WI_GATEWAY_ACTIVATED] = ST_PARALLEL_SPLIT;
+          break;
         case EK_CATCH: {
           const Node* med = child(n, "messageEventDefinition");
           const char* mref = med ? med->get("messageRef") : nullptr;
@@ -674,7 +701,13 @@ struct Deployer {
       e.cond_begin = (uint16_t)t.cond_flows.size();
       e.cond_count = (uint16_t)conditioned[i].size();
       t.cond_flows.insert(t.cond_flows.end(), conditioned[i].begin(), conditioned[i].end());
+      if (e.kind == EK_PAR) {  // fork: every outgoing flow, executable order
+        if (outgoing[i].size() > (size_t)MAX_FANOUT) { err = "parallel gateway with more than 63 outgoing flows"; return ZB_EUNSUPPORTED; }
+        e.out_begin = (uint16_t)t.cond_flows.size();
+        t.cond_flows.insert(t.cond_flows.end(), outgoing[i].begin(), outgoing[i].end());
+      }
     }
+    if (t.cond_flows.size() >= 0xffff) { err = "too many sequence flows"; return ZB_EUNSUPPORTED; }
     return ZB_OK;
   }
   uint16_t& P_start(uint16_t pe) { return t.elems[pe].start; }

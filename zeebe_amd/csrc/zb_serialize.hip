@@ -118,6 +118,13 @@ __device__ inline const CmdRange* find_range(const SerParams& P, int64_t pos) {
 
 __device__ inline void encode_value(const SerParams& P, int64_t pos, const zb_rec& d, W& w) {
   const uint8_t vt = kind_vt(d.kind), rt = kind_rt(d.kind);
+  if (d.kind & KIND_RAW) {  // zb_submit: the value as written, or the command value as the reference re-encodes it
+    const uint8_t* doc = P.arena + (uint64_t)d.payload * 8;
+    const uint32_t dl = *(const uint32_t*)doc;
+    const uint8_t* raw = doc + ((4 + dl + 7) & ~7u);
+    w.put_bytes(raw + 4, *(const uint32_t*)raw);
+    return;
+  }
   uint32_t plen = 0;
   const uint8_t* pl = nullptr;
   if (vt != ZB_VT_INCIDENT) {
@@ -149,6 +156,25 @@ __device__ inline void encode_value(const SerParams& P, int64_t pos, const zb_re
     w.key("activityId"); w.str(P.pool + e.id_off, e.id_len);
     w.key("payload"); w.bin(pl, plen);
     w.key("scopeInstanceKey"); w.integer(d.scope_key);
+  } else if (vt == ZB_VT_JOB && d.intent == JI_CANCEL) {
+    // TerminateServiceTaskHandler :37-58: a reset JobRecord with type "", headers without workflowKey
+    const DevElem& e = P.elems[d.elem];
+    const DevWorkflow& wf = P.wfs[e.wf];
+    w.map_hdr(7);
+    w.key("deadline"); w.integer(INT64_MIN);
+    w.key("worker"); w.str(nullptr, 0);
+    w.key("retries"); w.integer(-1);
+    w.key("type"); w.str(nullptr, 0);
+    w.key("headers");
+    w.map_hdr(6);
+    w.key("bpmnProcessId"); w.str(P.pool + wf.pid_off, wf.pid_len);
+    w.key("workflowDefinitionVersion"); w.integer(wf.version);
+    w.key("workflowKey"); w.integer(-1);
+    w.key("workflowInstanceKey"); w.integer(d.inst_key);
+    w.key("activityId"); w.str(P.pool + e.id_off, e.id_len);
+    w.key("activityInstanceKey"); w.integer(d.scope_key);
+    w.key("customHeaders"); w.put(0x80);
+    w.key("payload"); w.bin((const uint8_t*)"\x80", 1);
   } else if (vt == ZB_VT_JOB) {
     const DevElem& e = P.elems[d.elem];
     const DevWorkflow& wf = P.wfs[e.wf];
@@ -240,8 +266,9 @@ __global__ void k_ser_write(SerParams P) {
   h.intent = d.intent;
   // RejectionType: CREATE of an unknown workflow -> BAD_VALUE (0); CORRELATE of an absent activity ->
   // NOT_APPLICABLE (1) (WorkflowInstanceStreamProcessor.java:477-479)
+  // CANCEL / UPDATE_PAYLOAD of an instance that is not running -> NOT_APPLICABLE (1) (:524-529, :571-573)
   h.rejection_type = kind_rt(d.kind) == ZB_RT_COMMAND_REJECTION
-                         ? (kind_vt(d.kind) == ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION ? 1 : 0) : 255;
+                         ? ((kind_vt(d.kind) == ZB_VT_WORKFLOW_INSTANCE && d.intent == WI_CREATE) ? 0 : 1) : 255;
   h.value_length = w.n;
   h.value_offset = P.offsets[i];
   P.headers[i] = h;
@@ -264,6 +291,7 @@ __global__ void k_inject(InjectParams P) {
   for (int64_t i = tid; i < P.n; i += stride) {
     zb_rec d = P.staged[i];
     d.payload += base_ref;
+    if (d.key == KEY_IS_POSITION) d.key = P.log_base + i;
     P.log[P.log_base + i] = d;
     P.links[P.log_base + i] = ~0ull;  // no rows yet
   }

@@ -82,7 +82,7 @@ struct ElemCtl {
 static_assert(offsetof(DevElem, step) == 4 && offsetof(DevElem, out0) == 16 && offsetof(DevElem, target) == 18 &&
                   offsetof(DevElem, start) == 20 && offsetof(DevElem, dflt) == 22 &&
                   offsetof(DevElem, cond_begin) == 24 && offsetof(DevElem, cond_count) == 26 &&
-                  offsetof(DevElem, job_payload) == 40 && sizeof(DevElem) == 72,
+                  offsetof(DevElem, job_payload) == 40 && sizeof(DevElem) == 80,
               "ElemCtl mirrors the DevElem layout");
 __device__ __forceinline__ uint32_t elem_dword(const TrajParams& P, uint32_t e, uint32_t d) {
   return K((const uint32_t*)P.elems)[(uint64_t)e * (sizeof(DevElem) / 4) + d];

@@ -48,8 +48,10 @@ struct TState {
   uint16_t d_q;
   int64_t d_pos;
   uint32_t err, err_site;
+  // a parallel fork's expanded outputs (k_emit writes them after the staged slots)
+  uint32_t nexp, exp_ord;
   // stats
-  uint32_t transitions, completed, created, merges;
+  uint32_t transitions, completed, created, merges, canceled;
   uint32_t merge_bytes, cond_bytes;
   // open-subscription side effect (SubscribeMessageHandler), written to the outbox after processing
   bool fx, fx_int;
@@ -86,11 +88,42 @@ __device__ __forceinline__ void wf_event(TState& t, Slot& s, uint8_t intent, uin
 }
 
 // ElementInstanceWriter.writeFollowUpEvent index side effects for a final state
+// (atomic: the tokens of a scope with parallel branches remove their children in the same wave)
 __device__ __forceinline__ void remove_row(const WaveParams& P, uint32_t row) {
   RowMeta& m = P.rmeta[row];
   uint32_t parent = m.parent;
   m.state = 0;
-  if (parent != NO_ROW) P.rmeta[parent].nchild -= 1;
+  if (parent != NO_ROW) atomicSub(&P.rmeta[parent].nchild, 1);
+}
+
+__device__ __forceinline__ bool can_terminate(uint8_t state) {  // WorkflowInstanceLifecycle.canTerminate
+  return state == WI_ELEMENT_READY || state == WI_ELEMENT_ACTIVATED || state == WI_ELEMENT_COMPLETING;
+}
+
+// the blob after a submitted record's payload document holds its verbatim value (KIND_RAW); the copy
+// of the document after that one is followed by the command value as the reference re-encodes it
+// (zb_submit arena layout: [doc][raw value][doc][re-encoded value], each [u32 len][bytes] 8-aligned)
+__device__ __forceinline__ uint32_t next_blob(const uint8_t* arena, uint32_t ref) {
+  const uint32_t len = *(const uint32_t*)(arena + (uint64_t)ref * 8);
+  return ref + ((4 + len + 7) >> 3);
+}
+__device__ __forceinline__ uint32_t derived_ref(const uint8_t* arena, uint32_t ref) {
+  return next_blob(arena, next_blob(arena, ref));
+}
+
+// a WORKFLOW_INSTANCE event carrying an indexed element instance's value (row) with the given intent
+__device__ __forceinline__ Slot& row_event(const WaveParams& P, TState& t, uint32_t row, uint8_t intent) {
+  const RowMeta m = P.rmeta[row];
+  const RowKeys k = P.rkeys[row];
+  Slot& s = add_slot(t);
+  s.d.key = k.key;
+  s.d.scope_key = k.scope_key;
+  s.d.inst_key = k.inst_key;
+  s.d.elem = m.elem;
+  s.d.payload = m.payload;
+  wf_event(t, s, intent, t.ns > 1);
+  s.rself = row; s.rscope = m.parent;
+  return s;
 }
 
 __device__ void incident(TState& t, const zb_rec& rec, int64_t pos, uint8_t type, uint8_t code, uint8_t a,
@@ -203,6 +236,13 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
     }
     case ST_CONSUME_TOKEN: {  // ConsumeTokenHandler :30-43
       if (!scope_alive) { fail_at(t, DE_PROCESSING, 9); return; }
+      if (P.has_parallel) {
+        // EXTENSION (C4): k_pre took this token off the scope; the scope completes on its last token, i.e.
+        // when the count reached 0 and this is the wave's last consumer in log order
+        const RowAux& a = P.raux[rscope];
+        if (a.tokens < 0) { fail_at(t, DE_PROCESSING, 40); return; }
+        if (a.tokens != 0 || a.consume_pos != pos) return;
+      }
       RowMeta& m = P.rmeta[rscope];
       const RowKeys k = P.rkeys[rscope];
       Slot& s = add_slot(t);
@@ -243,11 +283,17 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
       s.ord = (uint8_t)t.nwf++;
       s.rord = (uint8_t)t.nrow++;
       s.rself = NO_ROW; s.rscope = scope_alive ? rscope : NO_ROW;
-      if (scope_alive) P.rmeta[rscope].nchild += 1;
+      if (scope_alive) atomicAdd(&P.rmeta[rscope].nchild, 1);
       break;
     }
     case ST_TRIGGER_START_EVENT: {  // TriggerStartEventHandler :30-39
       if (el.start == NO_ELEM) { fail_at(t, DE_PROCESSING, 11); return; }
+      if (P.has_parallel && self_alive) {  // EXTENSION (C4): the start event's token
+        RowAux a;
+        a.tokens = 1; a.first = NO_ROW; a.join_cnt[0] = a.join_cnt[1] = 0;
+        a.consume_pos = 0; a.join_pos[0] = a.join_pos[1] = 0; a.mark = 0;
+        P.raux[rself] = a;
+      }
       Slot& s = add_slot(t);
       s.d = rec;
       s.d.elem = el.start;
@@ -293,9 +339,90 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
       t.fx_pos = pos; t.fx_wik = rec.inst_key; t.fx_aik = rec.key; t.fx_elem = rec.elem; t.fx_row = rself;
       break;
     }
+    case ST_PARALLEL_SPLIT: {  // EXTENSION (C4): one SEQUENCE_FLOW_TAKEN per outgoing flow (k_emit writes them)
+      if (el.n_out == 0 || el.n_out > MAX_FANOUT || t.nexp) { fail_at(t, DE_UNSUPPORTED, 41); return; }
+      t.nexp = el.n_out;
+      t.exp_ord = (uint32_t)t.nwf;
+      t.nwf += el.n_out;
+      break;
+    }
+    case ST_PARALLEL_MERGE: {  // EXTENSION (C4): the wave's last arrival (log order) that completes the arity fires
+      if (!scope_alive || el.target == NO_ELEM) { fail_at(t, DE_PROCESSING, 42); return; }
+      const DevElem& g = P.elems[el.target];
+      RowAux& a = P.raux[rscope];
+      if (a.join_pos[g.join_slot] != pos) return;
+      const uint32_t cnt = a.join_cnt[g.join_slot];
+      if (cnt < g.m_in) return;
+      if (cnt > g.m_in) { fail_at(t, DE_UNSUPPORTED, 43); return; }  // a flow taken twice before the join fired
+      a.join_cnt[g.join_slot] = 0;
+      Slot& s = add_slot(t);
+      s.d = rec;
+      s.d.elem = el.target;
+      wf_event(t, s, WI_GATEWAY_ACTIVATED, t.ns > 1);
+      s.flags |= SF_KEY_WF; s.ord = (uint8_t)t.nwf++;
+      s.rself = NO_ROW; s.rscope = rscope;
+      break;
+    }
+    case ST_TERMINATE_CONTAINED_INSTANCES: {  // TerminateContainedElementsHandler :31-53
+      if (!self_alive) { fail_at(t, DE_PROCESSING, 44); return; }
+      if (P.rmeta[rself].nchild == 0) {
+        Slot& s = add_slot(t);
+        s.d = rec;
+        wf_event(t, s, WI_ELEMENT_TERMINATED, t.ns > 1);
+        s.rself = rself; s.rscope = rscope;
+        remove_row(P, rself);
+        if (rec.key == rec.inst_key) t.canceled += 1;
+      } else {
+        const RowAux& a = P.raux[rself];
+        const uint32_t child = a.mark == P.epoch ? a.first : NO_ROW;
+        if (child == NO_ROW) { fail_at(t, DE_PROCESSING, 45); return; }
+        if (can_terminate(P.rmeta[child].state)) {
+          row_event(P, t, child, WI_ELEMENT_TERMINATING);
+          P.rmeta[child].state = WI_ELEMENT_TERMINATING;
+        }
+      }
+      break;
+    }
+    case ST_TERMINATE_JOB_TASK:  // TerminateServiceTaskHandler :37-58: JOB CANCEL (key = job key) first
+    case ST_TERMINATE_ELEMENT: {  // TerminateElementHandler :29-45
+      if (step == ST_TERMINATE_JOB_TASK && self_alive && P.rkeys[rself].job_key > 0) {
+        Slot& j = add_slot(t);
+        j.d.key = P.rkeys[rself].job_key;
+        j.d.scope_key = rec.key;  // headers.activityInstanceKey
+        j.d.inst_key = rec.inst_key;
+        j.d.elem = rec.elem;
+        j.d.payload = 0;
+        j.d.intent = JI_CANCEL;
+        j.d.kind = make_kind(ZB_VT_JOB, ZB_RT_COMMAND, t.ns > 1);
+        j.rself = NO_ROW; j.rscope = NO_ROW;
+      }
+      Slot& s = add_slot(t);
+      s.d = rec;
+      wf_event(t, s, WI_ELEMENT_TERMINATED, t.ns > 1);
+      s.rself = rself; s.rscope = rscope;
+      if (self_alive) remove_row(P, rself);
+      break;
+    }
+    case ST_PROPAGATE_TERMINATION: {  // PropagateTerminationHandler :29-40 (the guard saw the scope TERMINATING)
+      if (P.rmeta[rscope].nchild == 0) {
+        const int64_t sk = P.rkeys[rscope].key;
+        row_event(P, t, rscope, WI_ELEMENT_TERMINATED);
+        remove_row(P, rscope);
+        if (sk == P.rkeys[rscope].inst_key) t.canceled += 1;
+      } else {
+        // EXTENSION (several live tokens in the scope, C4): terminate the next child
+        const RowAux& a = P.raux[rscope];
+        const uint32_t child = a.mark == P.epoch ? a.first : NO_ROW;
+        if (child == NO_ROW) { fail_at(t, DE_PROCESSING, 46); return; }
+        if (can_terminate(P.rmeta[child].state)) {
+          row_event(P, t, child, WI_ELEMENT_TERMINATING);
+          P.rmeta[child].state = WI_ELEMENT_TERMINATING;
+        }
+      }
+      break;
+    }
     default:
-      // termination: not on the GPU path yet (flagged, never silently skipped)
-      fail_at(t, DE_UNSUPPORTED, 12);
+      fail_at(t, DE_UNSUPPORTED, 12);  // never silently skipped
       break;
   }
 }
@@ -305,7 +432,42 @@ __device__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t p
   const uint8_t vt = kind_vt(rec.kind), rt = kind_rt(rec.kind);
   if (vt == ZB_VT_WORKFLOW_INSTANCE) {
     if (rt == ZB_RT_COMMAND) {
-      if (rec.intent != WI_CREATE) { fail_at(t, DE_UNSUPPORTED, 13); return; }
+      if (rec.intent == WI_CANCEL) {  // CancelWorkflowInstanceProcessor :511-555 (instance by command key)
+        const bool can = rself != NO_ROW && can_terminate(P.rmeta[rself].state);
+        if (!can) {  // writeRejection(command, NOT_APPLICABLE, "Workflow instance is not running")
+          Slot& s = add_slot(t);
+          s.d = rec;
+          if (rec.kind & KIND_RAW) s.d.payload = derived_ref(P.arena, rec.payload);
+          s.d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_COMMAND_REJECTION, t.ns > 1) | (rec.kind & KIND_RAW);
+          s.rself = NO_ROW; s.rscope = NO_ROW;
+          return;
+        }
+        // getValue() is the live indexed object: setPayload(EMPTY) empties the index's copy too
+        RowMeta& m = P.rmeta[rself];
+        m.payload = 0;
+        Slot& a = row_event(P, t, rself, WI_CANCELING);  // batch: CANCELING, ELEMENT_TERMINATING (command key)
+        a.rself = NO_ROW; a.rscope = NO_ROW;
+        row_event(P, t, rself, WI_ELEMENT_TERMINATING);
+        m.state = WI_ELEMENT_TERMINATING;
+        return;
+      }
+      if (rec.intent == WI_UPDATE_PAYLOAD) {  // UpdatePayloadProcessor :557-576 (instance by value key)
+        const bool found = rself != NO_ROW && P.rmeta[rself].state != 0;
+        Slot& s = add_slot(t);
+        s.d = rec;
+        if (rec.kind & KIND_RAW) s.d.payload = derived_ref(P.arena, rec.payload);  // command value, re-encoded
+        s.rself = NO_ROW; s.rscope = NO_ROW;
+        if (!found) {  // reject(NOT_APPLICABLE, "Workflow instance is not running")
+          s.d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_COMMAND_REJECTION, t.ns > 1) | (rec.kind & KIND_RAW);
+          return;
+        }
+        P.rmeta[rself].payload = rec.payload;
+        s.d.intent = WI_PAYLOAD_UPDATED;
+        s.d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, t.ns > 1) | (rec.kind & KIND_RAW);
+        if (rec.key < 0) { s.flags |= SF_KEY_WF; s.ord = (uint8_t)t.nwf++; }  // CommandProcessorImpl.accept :77-84
+        return;
+      }
+      if (rec.intent != WI_CREATE) return;  // no processor registered for this key
       // CreateWorkflowInstanceEventProcessor :233-368: key first, then resolve (done at submit)
       const uint8_t ord = (uint8_t)t.nwf++;
       if (rec.elem == NO_ELEM) {
@@ -345,6 +507,7 @@ __device__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t p
     }
   } else if (vt == ZB_VT_JOB) {
     if (rt == ZB_RT_COMMAND && rec.intent == JI_CREATE) {
+      if (!P.harness) return;  // the job stream processor answers from outside (zb_submit)
       // canonical harness: JOB CREATED(k), JOB COMPLETED(k), k from the job key generator
       const uint8_t ord = (uint8_t)t.njob++;
       for (int k = 0; k < 2; k++) {
@@ -381,10 +544,12 @@ __device__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t p
     // delivered command carries the catch event's row (rows are never reused: row + key identify it)
     const bool found = rself != NO_ROW && rself < P.row_cap && P.rmeta[rself].state != 0 &&
                        P.rkeys[rself].key == rec.scope_key;
+    const uint8_t raw = rec.kind & KIND_RAW;  // submitted through zb_submit: follow-ups re-encode its value
     if (!found) {  // writeRejection(record, NOT_APPLICABLE, "activity is not active anymore")
       Slot& s = add_slot(t);
       s.d = rec;
-      s.d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION, ZB_RT_COMMAND_REJECTION, t.ns > 1);
+      if (raw) s.d.payload = derived_ref(P.arena, rec.payload);
+      s.d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION, ZB_RT_COMMAND_REJECTION, t.ns > 1) | raw;
       s.rself = NO_ROW; s.rscope = NO_ROW;
       return;
     }
@@ -392,8 +557,9 @@ __device__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t p
     const RowKeys k = P.rkeys[rself];
     Slot& a = add_slot(t);  // batch: CORRELATED(record key), ELEMENT_COMPLETING(activityInstanceKey)
     a.d = rec;
+    if (raw) a.d.payload = derived_ref(P.arena, rec.payload);
     a.d.intent = 1;
-    a.d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION, ZB_RT_EVENT, t.ns > 1);
+    a.d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION, ZB_RT_EVENT, t.ns > 1) | raw;
     a.rself = NO_ROW; a.rscope = NO_ROW;
     Slot& b = add_slot(t);
     b.d.key = rec.scope_key;
@@ -454,10 +620,18 @@ __device__ __forceinline__ void block_tiles(const Chunk& c, int64_t& t0, int64_t
   t1 = (int64_t)(blockIdx.x + 1) * ntiles / gridDim.x;
 }
 
+// A batch's records are processed by the thread of its first record, in order (the later ones may read
+// what the earlier ones wrote to the index: CREATED + READY, JOB CREATED + COMPLETED). A parallel fork's
+// SEQUENCE_FLOW_TAKEN batch is the exception: its flows touch only their own new element instances (and
+// the scope's counters, atomically), so each is a record of its own.
+__device__ __forceinline__ bool grouped(const zb_rec& r) {
+  return kind_cont(r.kind) && !(r.intent == WI_SEQUENCE_FLOW_TAKEN && kind_vt(r.kind) == ZB_VT_WORKFLOW_INSTANCE);
+}
+
 // ------------------------------------------------------------------------------ k_process
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8))) k_process(WaveParams P) {
   __shared__ Slot s_slots[WG * MAX_SLOTS];
-  __shared__ uint64_t s_red[WG / 64][6];
+  __shared__ uint64_t s_red[WG / 64][6];  // (6 packed totals)
   const WaveHdr* hin = P.hdr + (P.wave & 1);
   const Chunk c = wave_chunk(P, hin);
   if (c.n <= 0) return;
@@ -480,19 +654,20 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
     t.s = s_slots + threadIdx.x * MAX_SLOTS;
     t.ns = t.nwf = t.njob = t.nrow = 0;
     t.bytes = 0; t.merge = false; t.detail = false; t.err = 0; t.err_site = 0;
-    t.transitions = t.completed = t.created = t.merges = 0;
+    t.transitions = t.completed = t.created = t.merges = t.canceled = 0;
     t.merge_bytes = t.cond_bytes = 0;
     t.fx = false;
+    t.nexp = 0; t.exp_ord = 0;
     uint32_t nconds = 0;
     const zb_rec rec = P.log[r];
-    if (!kind_cont(rec.kind)) {
+    if (!grouped(rec)) {
       // a thread owns its record plus the continuation records that follow it (one parent's batch);
       // a batch never spans generations, so its tail may lie past a chunk end (skipped there as cont)
       const uint64_t lk = P.links[r];
       process_record(P, rec, r, (uint32_t)lk, (uint32_t)(lk >> 32), t);
       for (int64_t q = r + 1; q < gen_end && q < r + 4; q++) {
         const zb_rec rec2 = P.log[q];
-        if (!kind_cont(rec2.kind)) break;
+        if (!grouped(rec2)) break;
         const uint64_t lk2 = P.links[q];
         process_record(P, rec2, q, (uint32_t)lk2, (uint32_t)(lk2 >> 32), t);
       }
@@ -512,15 +687,18 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
       inf.d_b = t.d_b; inf.has_detail = t.detail; inf.ns = (uint8_t)t.ns;
       P.info[i] = inf;
     }
-    P.cw[i] = (uint64_t)t.ns | ((uint64_t)t.nwf << CW_NWF) | ((uint64_t)t.njob << CW_NJOB) |
+    t.transitions += t.nexp;  // a fork's SEQUENCE_FLOW_TAKEN events
+    const uint32_t nwf_staged = (uint32_t)t.nwf - t.nexp;
+    P.cw[i] = (uint64_t)t.ns | ((uint64_t)nwf_staged << CW_NWF) | ((uint64_t)t.njob << CW_NJOB) |
               ((uint64_t)t.nrow << CW_NROW) | ((uint64_t)(t.merge ? 1 : 0) << CW_MERGE) |
               ((uint64_t)(t.detail ? 1 : 0) << CW_DETAIL) | ((uint64_t)nconds << CW_NCOND) |
-              ((uint64_t)t.bytes << 32);
-    acc_a += (uint64_t)t.ns | ((uint64_t)t.nwf << 16) | ((uint64_t)t.njob << 32) | ((uint64_t)t.nrow << 48);
+              ((uint64_t)t.nexp << CW_NEXP) | ((uint64_t)t.bytes << 32);
+    acc_a += (uint64_t)(t.ns + t.nexp) | ((uint64_t)t.nwf << 16) | ((uint64_t)t.njob << 32) |
+             ((uint64_t)t.nrow << 48);
     acc_b += (uint64_t)(t.merge ? 1 : 0) | ((uint64_t)nconds << 16) | ((uint64_t)t.transitions << 32) |
              ((uint64_t)t.completed << 48);
     acc_bytes += t.bytes;
-    acc_created += t.created;
+    acc_created += t.created | (t.canceled << 16);
     if (__ballot(t.fx)) {  // wave-uniform: open-subscription side effects of this tile
       const uint32_t slot = wave_alloc(P.on, t.fx ? 1u : 0u);
       if (t.fx) write_open(P, t, slot);
@@ -534,16 +712,16 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
   // workgroup totals: unpack to 32-bit lanes sums, wave reduction, 4 partials through LDS
   uint64_t v[6] = {acc_a & 0xffffffffull, acc_a >> 32, acc_b & 0xffffffffull, acc_b >> 32, acc_bytes,
                    (uint64_t)acc_created};
-  // 16-bit fields of a thread's totals never overflow (<= 2 * tiles per workgroup), but the sum over
+  // 16-bit fields of a thread's totals never overflow (<= 65 * tiles per workgroup), but the sum over
   // 256 threads can: widen each 16-bit pair into two 32-bit halves first
-  uint64_t w[10];
+  uint64_t w[11];
   w[0] = v[0] & 0xffff; w[1] = v[0] >> 16; w[2] = v[1] & 0xffff; w[3] = v[1] >> 16;
   w[4] = v[2] & 0xffff; w[5] = v[2] >> 16; w[6] = v[3] & 0xffff; w[7] = v[3] >> 16;
-  w[8] = v[4]; w[9] = v[5];
-  uint64_t pk[5] = {w[0] | (w[1] << 32), w[2] | (w[3] << 32), w[4] | (w[5] << 32), w[6] | (w[7] << 32),
-                    w[8] | (w[9] << 40)};
+  w[8] = v[4]; w[9] = v[5] & 0xffff; w[10] = v[5] >> 16;
+  uint64_t pk[6] = {w[0] | (w[1] << 32), w[2] | (w[3] << 32), w[4] | (w[5] << 32), w[6] | (w[7] << 32),
+                    w[8], w[9] | (w[10] << 32)};
 #pragma unroll
-  for (int f = 0; f < 5; f++) {
+  for (int f = 0; f < 6; f++) {
     uint64_t x = pk[f];
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) x += shfl_down64(x, d);
@@ -551,21 +729,92 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
   }
   if (lane == 0) {
 #pragma unroll
-    for (int f = 0; f < 5; f++) s_red[wv][f] = pk[f];
+    for (int f = 0; f < 6; f++) s_red[wv][f] = pk[f];
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint64_t a[5];
+    uint64_t a[6];
 #pragma unroll
-    for (int f = 0; f < 5; f++) a[f] = s_red[0][f] + s_red[1][f] + s_red[2][f] + s_red[3][f];
+    for (int f = 0; f < 6; f++) a[f] = s_red[0][f] + s_red[1][f] + s_red[2][f] + s_red[3][f];
     BlockAgg g;
     g.rec = (uint32_t)a[0]; g.wf = (uint32_t)(a[0] >> 32);
     g.job = (uint32_t)a[1]; g.row = (uint32_t)(a[1] >> 32);
     g.merges = (uint32_t)a[2]; g.conds = (uint32_t)(a[2] >> 32);
     g.transitions = (uint32_t)a[3]; g.completed = (uint32_t)(a[3] >> 32);
-    g.bytes = a[4] & 0xffffffffffull; g.created = (uint32_t)(a[4] >> 40);
-    g.pad = 0;
+    g.bytes = a[4];
+    g.created = (uint32_t)a[5]; g.canceled = (uint32_t)(a[5] >> 32);
     P.block_agg[blockIdx.x] = g;
+  }
+}
+
+// ------------------------------------------------------------------------------ k_pre
+// Scope-wide counters of the chunk, before k_process decides anything (only when the model has parallel
+// gateways or a cancellation is in flight). Token effects are order-independent sums, so they are
+// applied here with atomics and every decision in k_process reads the chunk's final counts plus the
+// max log position of the records that touched them -- which reproduces the sequential outcome: a scope
+// completes / a join fires exactly at its last consumer / arrival in log order.
+// Guards are the BpmnStepProcessor ones (scope ACTIVATED); k_process has not run yet, so they read the
+// state every record of the chunk sees in the reference (no record of the chunk changes them first).
+__global__ void __launch_bounds__(WG) k_pre(WaveParams P) {
+  const WaveHdr* hin = P.hdr + (P.wave & 1);
+  const Chunk c = wave_chunk(P, hin);
+  const int64_t stride = (int64_t)gridDim.x * WG;
+  bool need = false;
+  for (int64_t r = c.begin + (int64_t)blockIdx.x * WG + threadIdx.x; r < c.end; r += stride) {
+    const zb_rec rec = P.log[r];
+    if (kind_vt(rec.kind) != ZB_VT_WORKFLOW_INSTANCE || kind_rt(rec.kind) != ZB_RT_EVENT) continue;
+    const uint8_t it = rec.intent;
+    if (it != WI_END_EVENT_OCCURRED && it != WI_ELEMENT_COMPLETED && it != WI_SEQUENCE_FLOW_TAKEN &&
+        it != WI_GATEWAY_ACTIVATED && it != WI_ELEMENT_TERMINATING && it != WI_ELEMENT_TERMINATED)
+      continue;
+    if (rec.elem == NO_ELEM) continue;
+    const uint64_t lk = P.links[r];
+    const uint32_t rself = (uint32_t)lk, rscope = (uint32_t)(lk >> 32);
+    const DevElem& el = P.elems[rec.elem];
+    const uint8_t step = el.step[it];
+    const bool scope_alive = rscope != NO_ROW && P.rmeta[rscope].state != 0;
+    const uint8_t sst = scope_alive ? P.rmeta[rscope].state : 0;
+    if (P.has_parallel && sst == WI_ELEMENT_ACTIVATED) {
+      RowAux& a = P.raux[rscope];
+      if (step == ST_CONSUME_TOKEN && (it == WI_END_EVENT_OCCURRED || it == WI_ELEMENT_COMPLETED)) {
+        atomicSub(&a.tokens, 1);
+        atomicMax((unsigned long long*)&a.consume_pos, (unsigned long long)r);
+      } else if (step == ST_PARALLEL_MERGE && it == WI_SEQUENCE_FLOW_TAKEN && el.target != NO_ELEM) {
+        const uint32_t slot = P.elems[el.target].join_slot;
+        atomicAdd(&a.join_cnt[slot], 1u);
+        atomicMax((unsigned long long*)&a.join_pos[slot], (unsigned long long)r);
+      } else if (step == ST_PARALLEL_SPLIT && it == WI_GATEWAY_ACTIVATED) {
+        atomicAdd(&a.tokens, (int32_t)el.n_out - (int32_t)(el.m_in > 1 ? el.m_in : 1));
+      }
+    }
+    if (P.term) {
+      // scopes that look up their first live child this chunk (k_children answers)
+      uint32_t row = NO_ROW;
+      if (it == WI_ELEMENT_TERMINATING && step == ST_TERMINATE_CONTAINED_INSTANCES && rself != NO_ROW &&
+          P.rmeta[rself].state != 0 && P.rmeta[rself].nchild > 0)
+        row = rself;
+      else if (it == WI_ELEMENT_TERMINATED && step == ST_PROPAGATE_TERMINATION && sst == WI_ELEMENT_TERMINATING &&
+               P.rmeta[rscope].nchild > 0)
+        row = rscope;
+      if (row != NO_ROW) {
+        P.raux[row].first = NO_ROW;
+        P.raux[row].mark = P.epoch;
+        need = true;
+      }
+    }
+  }
+  if (need) atomicOr(P.need_children, 1u);
+}
+
+// First live child (min row index = first in insertion order, ElementInstance.children.get(0)) of every
+// scope k_pre marked: one pass over the allocated rows, only in chunks of a cancellation that need it.
+__global__ void __launch_bounds__(256) k_children(WaveParams P) {
+  if (*(volatile uint32_t*)P.need_children == 0) return;
+  const uint64_t rows = (uint64_t)P.hdr[P.wave & 1].rows_next;
+  for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < rows; r += (uint64_t)gridDim.x * 256) {
+    const RowMeta m = P.rmeta[r];
+    if (m.state == 0 || m.parent == NO_ROW) continue;
+    if (P.raux[m.parent].mark == P.epoch) atomicMin(&P.raux[m.parent].first, (uint32_t)r);
   }
 }
 
@@ -574,14 +823,14 @@ constexpr int SCAN_WG = 1024;
 constexpr int SCAN_PER = WAVE_GRID / SCAN_WG;  // workgroup aggregates per scan thread
 
 __global__ void __launch_bounds__(SCAN_WG) k_scan(WaveParams P) {
-  __shared__ uint64_t s_w[SCAN_WG / 64][10];
+  __shared__ uint64_t s_w[SCAN_WG / 64][11];
   const WaveHdr* hin = P.hdr + (P.wave & 1);
   WaveHdr* hout = P.hdr + ((P.wave + 1) & 1);
   const Chunk c = wave_chunk(P, hin);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  // fields: rec wf job row bytes merges conds | transitions completed created (reduced only)
+  // fields: rec wf job row bytes merges conds | transitions completed created canceled (reduced only)
   BlockAgg g[SCAN_PER];
-  uint64_t x[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t x[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   if (c.n > 0) {
 #pragma unroll
     for (int k = 0; k < SCAN_PER; k++) g[k] = P.block_agg[threadIdx.x * SCAN_PER + k];
@@ -589,12 +838,12 @@ __global__ void __launch_bounds__(SCAN_WG) k_scan(WaveParams P) {
     for (int k = 0; k < SCAN_PER; k++) {
       x[0] += g[k].rec; x[1] += g[k].wf; x[2] += g[k].job; x[3] += g[k].row; x[4] += g[k].bytes;
       x[5] += g[k].merges; x[6] += g[k].conds; x[7] += g[k].transitions; x[8] += g[k].completed;
-      x[9] += g[k].created;
+      x[9] += g[k].created; x[10] += g[k].canceled;
     }
   }
-  uint64_t ex[10];
+  uint64_t ex[11];
 #pragma unroll
-  for (int f = 0; f < 10; f++) {
+  for (int f = 0; f < 11; f++) {
     uint64_t y = x[f];
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -621,8 +870,8 @@ __global__ void __launch_bounds__(SCAN_WG) k_scan(WaveParams P) {
     }
   }
   if (threadIdx.x == 0) {
-    uint64_t tot[10];
-    for (int f = 0; f < 10; f++) {
+    uint64_t tot[11];
+    for (int f = 0; f < 11; f++) {
       tot[f] = 0;
       for (int w = 0; w < SCAN_WG / 64; w++) tot[f] += s_w[w][f];
     }
@@ -639,6 +888,7 @@ __global__ void __launch_bounds__(SCAN_WG) k_scan(WaveParams P) {
       P.stats[1] += tot[8];
       P.stats[2] += tot[9];
       P.stats[6] += 1;
+      P.stats[7] += tot[10];
       uint32_t err = 0;
       if ((uint64_t)h.end > P.log_cap) err |= DE_LOG_FULL;
       if ((uint64_t)h.rows_next > P.row_cap) err |= DE_ROWS_FULL;
@@ -647,6 +897,7 @@ __global__ void __launch_bounds__(SCAN_WG) k_scan(WaveParams P) {
       if (err) atomicOr(P.err, err);
     }
     *hout = h;
+    if (P.need_children) *P.need_children = 0;  // k_pre of the next chunk sets it again
     P.merge_count[P.wave & 1] = c.n > 0 ? (uint32_t)tot[5] : 0;
     P.cond_count[P.wave & 1] = c.n > 0 ? (uint32_t)tot[6] : 0;
   }
@@ -674,7 +925,8 @@ __global__ void __launch_bounds__(WG) k_emit(WaveParams P) {
     const int64_t i = tile * WG + threadIdx.x;
     const uint64_t w = (c.begin + i < c.end) ? P.cw[i] : 0;
     // packed block scan: a = outputs | wf << 16 | job << 32 | row << 48, b = bytes | merges << 40 | conds << 52
-    const uint64_t a0 = (w & 7) | (((w >> CW_NWF) & 7) << 16) | (((w >> CW_NJOB) & 7) << 32) |
+    const uint64_t nexp = (w >> CW_NEXP) & 63;
+    const uint64_t a0 = ((w & 7) + nexp) | ((((w >> CW_NWF) & 7) + nexp) << 16) | (((w >> CW_NJOB) & 7) << 32) |
                         (((w >> CW_NROW) & 7) << 48);
     const uint64_t b0 = (w >> 32) | (((w >> CW_MERGE) & 1) << 40) | (((w >> CW_NCOND) & 7) << 52);
     uint64_t a = a0, b = b0;
@@ -699,7 +951,7 @@ __global__ void __launch_bounds__(WG) k_emit(WaveParams P) {
     c_rec += ta & 0xffff; c_wf += (ta >> 16) & 0xffff; c_job += (ta >> 32) & 0xffff; c_row += ta >> 48;
     c_bytes += tb & 0xffffffffffull; c_merge += (tb >> 40) & 0xfff; c_cond += tb >> 52;
     const int ns = (int)(w & 7);
-    if (ns == 0 && !((w >> CW_DETAIL) & 1)) continue;
+    if (ns == 0 && nexp == 0 && !((w >> CW_DETAIL) & 1)) continue;
     uint64_t out_rec = (uint64_t)end + r_rec + (a & 0xffff);
     const uint64_t wf0 = r_wf + ((a >> 16) & 0xffff);
     const uint64_t job0 = r_job + ((a >> 32) & 0xffff);
@@ -766,10 +1018,36 @@ __global__ void __launch_bounds__(WG) k_emit(WaveParams P) {
       }
       out_rec++;
     }
+    if (nexp) {  // EXTENSION (C4): a parallel fork, one SEQUENCE_FLOW_TAKEN per outgoing flow, keys in order
+      const int64_t r = c.begin + i;
+      const zb_rec g = P.log[r];
+      const uint32_t rscope = (uint32_t)(P.links[r] >> 32);
+      const DevElem& ge = P.elems[g.elem];
+      const uint64_t kord = wf0 + ((w >> CW_NWF) & 7);
+      for (uint32_t j = 0; j < (uint32_t)nexp; j++) {
+        zb_rec d = g;
+        d.elem = P.cond_flows[ge.out_begin + j];
+        d.key = wf_next + 5 * (int64_t)(kord + j);
+        d.intent = WI_SEQUENCE_FLOW_TAKEN;
+        d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, ns + j > 0);
+        if (out_rec >= P.log_cap) { err |= DE_LOG_FULL; }
+        else {
+          P.log[out_rec] = d;
+          P.links[out_rec] = (uint64_t)NO_ROW | ((uint64_t)rscope << 32);
+        }
+        out_rec++;
+      }
+    }
     if (err) atomicOr(P.err, err);  // capacity overflow: the wave's results are void, the host stops
   }
 }
 
+void launch_pre(const WaveParams& p, hipStream_t stream) {
+  hipLaunchKernelGGL(k_pre, dim3(WAVE_GRID), dim3(WG), 0, stream, p);
+}
+void launch_children(const WaveParams& p, hipStream_t stream) {
+  hipLaunchKernelGGL(k_children, dim3(1024), dim3(256), 0, stream, p);
+}
 void launch_process(const WaveParams& p, hipStream_t stream) {
   hipLaunchKernelGGL(k_process, dim3(WAVE_GRID), dim3(WG), 0, stream, p);
 }

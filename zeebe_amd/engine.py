@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libzbgpu.so")
 
 CFG_WAVE_ONLY = 1  # zb_config.flags: never take the trajectory path
+CFG_EXTERNAL_JOBS = 2  # zb_config.flags: no canonical job harness (job events come through zb_submit)
 
 ZB_OK, ZB_EINVAL, ZB_ENOMEM, ZB_EUNSUPPORTED, ZB_EDEPLOY, ZB_EDEVICE, ZB_EAGAIN, ZB_EPROCESSING = \
     0, -1, -2, -3, -4, -5, -6, -7
@@ -38,6 +39,12 @@ class zb_rec(ctypes.Structure):
     _fields_ = [("key", ctypes.c_int64), ("scope_key", ctypes.c_int64), ("inst_key", ctypes.c_int64),
                 ("payload", ctypes.c_uint32), ("elem", ctypes.c_uint16), ("intent", ctypes.c_uint8),
                 ("kind", ctypes.c_uint8)]
+
+
+class zb_rec_desc(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_int64), ("record_type", ctypes.c_uint8), ("value_type", ctypes.c_uint8),
+                ("intent", ctypes.c_uint8), ("pad", ctypes.c_uint8), ("value_length", ctypes.c_uint32),
+                ("value_offset", ctypes.c_uint64)]
 
 
 class zb_record_header(ctypes.Structure):
@@ -71,6 +78,8 @@ class Record(NamedTuple):
     rejection_type: int
     value: bytes
 
+
+_INST = struct.Struct("<qqqB3xI")  # zb_read_instances record header
 
 _lib = None
 
@@ -109,6 +118,11 @@ def lib():
         L.zb_comm_init.argtypes = [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
         L.zb_comm_pending.argtypes = [vp, u64p]
         L.zb_comm_exchange.argtypes = [vp, ctypes.c_int, u64p]
+        szp = ctypes.POINTER(ctypes.c_size_t)
+        L.zb_submit.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+        L.zb_read_instances.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t, szp, u64p]
+        L.zb_snapshot.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t, szp]
+        L.zb_restore.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t]
         _lib = L
     return _lib
 
@@ -117,7 +131,7 @@ EXPORTED_SYMBOLS = ["zb_engine_create", "zb_engine_destroy", "zb_last_error", "z
                     "zb_set_job_completion_payload", "zb_submit_creates", "zb_step", "zb_log_size",
                     "zb_read_descriptors", "zb_drain", "zb_counters", "zb_submit_publishes", "zb_inbox_submit",
                     "zb_outbox_count", "zb_outbox_take", "zb_comm_unique_id", "zb_comm_init", "zb_comm_pending",
-                    "zb_comm_exchange"]
+                    "zb_comm_exchange", "zb_submit", "zb_read_instances", "zb_snapshot", "zb_restore"]
 
 
 class Engine:
@@ -125,12 +139,14 @@ class Engine:
 
     def __init__(self, device: int = 0, partition_id: int = 0, partition_count: int = 1,
                  log_capacity: int = 1 << 22, row_capacity: int = 1 << 20, arena_bytes: int = 64 << 20,
-                 wave_records: int = 0, wave_only: bool = False):
+                 wave_records: int = 0, wave_only: bool = False, external_jobs: bool = False):
         self._L = lib()
-        cfg = zb_config(device, partition_id, partition_count, CFG_WAVE_ONLY if wave_only else 0, log_capacity,
-                        row_capacity, arena_bytes, wave_records)
+        flags = (CFG_WAVE_ONLY if wave_only else 0) | (CFG_EXTERNAL_JOBS if external_jobs else 0)
+        cfg = zb_config(device, partition_id, partition_count, flags, log_capacity, row_capacity, arena_bytes,
+                        wave_records)
         h = ctypes.c_void_p()
         self._device, self._parts = device, partition_count
+        self._external = external_jobs
         rc = self._L.zb_engine_create(ctypes.byref(cfg), ctypes.byref(h))
         if rc != ZB_OK:
             raise ZbError(rc, "zb_engine_create failed")
@@ -182,6 +198,58 @@ class Engine:
         n = len(offsets) - 1
         self._check(self._L.zb_submit_creates(self._h, process_id.encode(), version, workflow_key, n, buf,
                                               offsets.ctypes.data))
+
+    def submit_records(self, recs):
+        """zb_submit: recs = [(record_type, value_type, intent, key, value bytes), ...] in log order."""
+        n = len(recs)
+        arr = (zb_rec_desc * max(n, 1))()
+        blob = bytearray()
+        for i, (rt, vt, it, key, value) in enumerate(recs):
+            arr[i] = zb_rec_desc(key, rt, vt, it, 0, len(value), len(blob))
+            blob += value
+        buf = ctypes.create_string_buffer(bytes(blob), max(len(blob), 1))
+        self._check(self._L.zb_submit(self._h, arr, n, buf, len(blob)))
+
+    def set_harness(self, on: bool):
+        """The job harness is fixed at creation (external_jobs=...): only checks it matches."""
+        if bool(on) == self._external:
+            raise ValueError("the canonical job harness is chosen at engine creation (external_jobs)")
+
+    def submit(self, record_type: int, value_type: int, intent: int, key: int, value: bytes):
+        """One record (the oracle's submit signature)."""
+        self.submit_records([(record_type, value_type, intent, key, value)])
+
+    def instances(self):
+        """Live element instances sorted by key: [(key, parent_key, job_key, state, value bytes)]."""
+        need = ctypes.c_size_t(0)
+        cnt = ctypes.c_uint64(0)
+        rc = self._L.zb_read_instances(self._h, None, 0, ctypes.byref(need), ctypes.byref(cnt))
+        if rc not in (ZB_OK, ZB_ENOMEM):
+            self._check(rc)
+        if need.value == 0:
+            return []
+        buf = ctypes.create_string_buffer(need.value)
+        self._check(self._L.zb_read_instances(self._h, buf, need.value, ctypes.byref(need), ctypes.byref(cnt)))
+        raw, out, off = buf.raw, [], 0
+        while off < len(raw):
+            key, pk, jk, st, n = _INST.unpack_from(raw, off)
+            off += _INST.size
+            out.append((key, pk, jk, st, raw[off:off + n]))
+            off += n
+        return out
+
+    def snapshot(self) -> bytes:
+        need = ctypes.c_size_t(0)
+        rc = self._L.zb_snapshot(self._h, None, 0, ctypes.byref(need))
+        if rc not in (ZB_OK, ZB_ENOMEM):
+            self._check(rc)
+        buf = ctypes.create_string_buffer(max(need.value, 1))
+        self._check(self._L.zb_snapshot(self._h, buf, need.value, ctypes.byref(need)))
+        return buf.raw[:need.value]
+
+    def restore(self, snap: bytes):
+        buf = ctypes.create_string_buffer(snap, max(len(snap), 1))
+        self._check(self._L.zb_restore(self._h, buf, len(snap)))
 
     def step(self, max_waves: int = 0) -> dict:
         st = zb_step_stats()
