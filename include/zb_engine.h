@@ -148,6 +148,11 @@ const char* zb_last_error(const zb_engine* e);
 int zb_reset(zb_engine* e, int keep_staged);
 
 /* ---- deployment (WorkflowCache.addWorkflow + BpmnTransformer) -------------------------- */
+/* Host-only (no device, no engine): transforms a BPMN 2.0 XML resource exactly as zb_deploy would --
+ * BpmnTransformer + json-el / json-path compilation -- and reports why it would be rejected
+ * (DeploymentCreateEventProcessor.java:91-151 validation / transformation). Returns ZB_OK,
+ * ZB_EDEPLOY or ZB_EUNSUPPORTED; err (may be NULL) receives the message. */
+int zb_validate_deployment(const uint8_t* bpmn_xml, size_t len, char* err, size_t err_cap);
 /* Deploys every executable process of a BPMN 2.0 XML resource; process i gets workflow_key + i. */
 int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t* bpmn_xml, size_t len);
 /* Canonical job harness: payload of the JOB COMPLETED event appended for every

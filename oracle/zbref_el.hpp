@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <memory>
+#include <cctype>
 #include <string>
 #include <vector>
 
@@ -169,6 +170,11 @@ class ElParser {
     fail_pos = p;
     return false;
   }
+  bool hex4(size_t i) const {  // \\u[a-fA-F0-9]{4}
+    for (size_t k = i; k < i + 4; k++)
+      if (k >= s.size() || !std::isxdigit((unsigned char)s[k])) return false;
+    return true;
+  }
   // string: JavaTokenParsers.stringLiteral (kept raw, no unescaping) | '...'
   bool string_lit(size_t& pos, bytes& out) {
     size_t p = skip_ws(pos);
@@ -180,7 +186,7 @@ class ElParser {
         if (c == '"') { ok = true; break; }
         if (c == '\\') {
           if (i + 1 < s.size() && std::strchr("\\'\"bfnrt", s[i + 1])) { i += 2; continue; }
-          if (i + 5 < s.size() && s[i + 1] == 'u') { i += 6; continue; }
+          if (i + 5 < s.size() && s[i + 1] == 'u' && hex4(i + 2)) { i += 6; continue; }
           break;
         }
         if (c < 0x20 || c == 0x7f) break;
@@ -198,7 +204,7 @@ class ElParser {
         if (c == '\'' || c == '"' || c < 0x20 || c == 0x7f) break;
         if (c == '\\') {
           if (i + 1 < s.size() && std::strchr("\\'\"bfnrt", s[i + 1])) { i += 2; continue; }
-          if (i + 5 < s.size() && s[i + 1] == 'u') { i += 6; continue; }
+          if (i + 5 < s.size() && s[i + 1] == 'u' && hex4(i + 2)) { i += 6; continue; }
           break;
         }
         i++;

@@ -696,6 +696,19 @@ int zb_reset(zb_engine* e, int keep_staged) {
   return ZB_OK;
 }
 
+int zb_validate_deployment(const uint8_t* xml, size_t len, char* err, size_t err_cap) {
+  if (!xml) return ZB_EINVAL;
+  ModelTables t;
+  std::string msg;
+  const int rc = compile_deployment(t, std::string((const char*)xml, len), 1, 1, msg);
+  if (err && err_cap) {
+    const size_t n = std::min(msg.size(), err_cap - 1);
+    std::memcpy(err, msg.data(), n);
+    err[n] = 0;
+  }
+  return rc;
+}
+
 int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t* xml, size_t len) {
   if (!e || !xml) return ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));

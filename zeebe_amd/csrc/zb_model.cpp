@@ -226,12 +226,20 @@ struct CondAst {
 class CondParser {
  public:
   CondParser(const std::string& s, ModelTables& t) : s_(s), t_(t) {}
+  // JsonConditionParser.parse = parseAll(condition): a committed failure (after `~!`) is final; otherwise
+  // the message is the furthest failure recorded while parsing, the later one at equal positions
+  // (scala-parser-combinators 1.0.6 lastNoSuccessVar; RegexParsers.phrase appends opt("\z"))
   std::unique_ptr<CondAst> parse(std::string& err) {
     size_t p = 0;
-    auto c = disjunction(p);
-    if (!c) { err = err_.empty() ? "expected comparison, disjunction or conjunction." : err_; return nullptr; }
-    p = ws(p);
-    if (p != s_.size()) { err = err_.empty() ? "end of input expected" : err_; return nullptr; }
+    auto c = condition(p);
+    if (committed_) { err = err_; return nullptr; }
+    if (!c) { err = rec_msg_; return nullptr; }
+    const size_t q = ws(p);
+    if (q != s_.size()) {
+      record("string matching regex `\\z' expected but " + found(q) + " found", q);
+      err = (rec_set_ && rec_pos_ >= p) ? rec_msg_ : "end of input expected";
+      return nullptr;
+    }
     return c;
   }
 
@@ -240,6 +248,24 @@ class CondParser {
   ModelTables& t_;
   std::string err_;
   bool committed_ = false;
+  std::string rec_msg_;
+  size_t rec_pos_ = 0;
+  bool rec_set_ = false;
+
+  void record(const std::string& m, size_t pos) {  // NoSuccess: furthest wins, the later at a tie
+    if (!rec_set_ || pos >= rec_pos_) { rec_msg_ = m; rec_pos_ = pos; rec_set_ = true; }
+  }
+  std::string found(size_t p) const {
+    if (p >= s_.size()) return "end of source";
+    return std::string("`") + s_[p] + "'";
+  }
+  // condition = disjunction | failure("expected comparison, disjunction or conjunction.")
+  std::unique_ptr<CondAst> condition(size_t& p) {
+    const size_t p0 = p;
+    auto c = disjunction(p);
+    if (!c && !committed_) record("expected comparison, disjunction or conjunction.", p0);
+    return c;
+  }
 
   size_t ws(size_t p) const {
     while (p < s_.size() && strchr(" \t\r\n\f\v", s_[p]) && s_[p]) p++;
@@ -264,11 +290,20 @@ class CondParser {
     }
     DevConst c{};
     if (allow_all && q < s_.size() && (s_[q] == '"' || s_[q] == '\'')) {
-      char qc = s_[q];
+      // JsonConditionParser.string: JavaTokenParsers.stringLiteral "([^"\x00-\x1F\x7F\\]|\\[\\'"bfnrt]|
+      // \\u[a-fA-F0-9]{4})*" or the same between single quotes without '"'; the body is kept raw
+      const char qc = s_[q];
       size_t e = q + 1;
       while (e < s_.size() && s_[e] != qc) {
-        if (s_[e] == '\\') e++;
-        else if (qc == '\'' && s_[e] == '"') break;
+        const unsigned char ch = (unsigned char)s_[e];
+        if (ch < 0x20 || ch == 0x7f || (qc == '\'' && ch == '"')) break;
+        if (ch == '\\') {
+          if (e + 1 < s_.size() && strchr("\\'\"bfnrt", s_[e + 1]) && s_[e + 1] != 0) { e += 2; continue; }
+          if (e + 5 < s_.size() && s_[e + 1] == 'u' && isxdigit((unsigned char)s_[e + 2]) &&
+              isxdigit((unsigned char)s_[e + 3]) && isxdigit((unsigned char)s_[e + 4]) &&
+              isxdigit((unsigned char)s_[e + 5])) { e += 6; continue; }
+          break;
+        }
         e++;
       }
       if (e >= s_.size() || s_[e] != qc) return false;
@@ -321,9 +356,11 @@ class CondParser {
   }
   std::unique_ptr<CondAst> comparison(size_t& p) {
     size_t save = p;
+    size_t reach = ws(p);  // furthest position its alternatives got to (withFailureMessage keeps it)
     int lp, li;
     if (operand(p, true, lp, li)) {
       size_t q = p;
+      reach = ws(p);
       int op = -1;
       if (lit(q, "==")) op = OP_EQ;
       else if (lit(q, "!=")) op = OP_NE;
@@ -365,23 +402,34 @@ class CondParser {
     }
     if (committed_) return nullptr;
     size_t q = p;
-    if (lit(q, "(")) {
-      auto c = disjunction(q);
-      if (!c) { committed_ = true; return nullptr; }
-      if (!lit(q, ")")) { committed_ = true; if (err_.empty()) err_ = "`)' expected"; return nullptr; }
+    if (lit(q, "(")) {  // "(" ~! condition ~ ")": everything after "(" is committed
+      auto c = condition(q);
+      if (!c) { committed_ = true; if (err_.empty()) err_ = rec_msg_; return nullptr; }
+      if (!lit(q, ")")) {
+        committed_ = true;
+        if (err_.empty()) err_ = "`)' expected but " + found(ws(q)) + " found";
+        return nullptr;
+      }
       p = q;
       return c;
     }
-    if (err_.empty()) err_ = "expected comparison operator ('==', '!=', '<', '<=', '>', '>=')";
+    record("expected comparison operator ('==', '!=', '<', '<=', '>', '>=')", reach);
     return nullptr;
   }
+  // chainl1(comparison | failure("expected comparison"), "&&")
+  std::unique_ptr<CondAst> comparison_or_fail(size_t& p) {
+    const size_t p0 = p;
+    auto c = comparison(p);
+    if (!c && !committed_) record("expected comparison", p0);
+    return c;
+  }
   std::unique_ptr<CondAst> conjunction(size_t& p) {
-    auto l = comparison(p);
+    auto l = comparison_or_fail(p);
     if (!l) return nullptr;
     for (;;) {
       size_t q = p;
       if (!lit(q, "&&")) break;
-      auto r = comparison(q);
+      auto r = comparison_or_fail(q);
       if (!r) {
         if (committed_) return nullptr;
         break;

@@ -120,6 +120,7 @@ def lib():
         L.zb_comm_exchange.argtypes = [vp, ctypes.c_int, u64p]
         szp = ctypes.POINTER(ctypes.c_size_t)
         L.zb_submit.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+        L.zb_validate_deployment.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
         L.zb_read_instances.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t, szp, u64p]
         L.zb_snapshot.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t, szp]
         L.zb_restore.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t]
@@ -131,7 +132,17 @@ EXPORTED_SYMBOLS = ["zb_engine_create", "zb_engine_destroy", "zb_last_error", "z
                     "zb_set_job_completion_payload", "zb_submit_creates", "zb_step", "zb_log_size",
                     "zb_read_descriptors", "zb_drain", "zb_counters", "zb_submit_publishes", "zb_inbox_submit",
                     "zb_outbox_count", "zb_outbox_take", "zb_comm_unique_id", "zb_comm_init", "zb_comm_pending",
-                    "zb_comm_exchange", "zb_submit", "zb_read_instances", "zb_snapshot", "zb_restore"]
+                    "zb_comm_exchange", "zb_submit", "zb_read_instances", "zb_snapshot", "zb_restore",
+                    "zb_validate_deployment"]
+
+
+def validate_deployment(xml):
+    """Host-only: (status, message) of transforming a deployment resource as zb_deploy would."""
+    if isinstance(xml, str):
+        xml = xml.encode()
+    err = ctypes.create_string_buffer(4096)
+    rc = lib().zb_validate_deployment(xml, len(xml), err, 4096)
+    return rc, err.value.decode("utf-8", "replace")
 
 
 class Engine:
