@@ -1,21 +1,31 @@
 """bench.py — BPMN element transitions/s on MI355X (BASELINE.json metric), one partition per GPU.
 
-Workload (BASELINE.json configs[1]): a 20-service-task chain, 1,000,000 concurrent
-instances per GPU (all CREATE commands injected before wave 0), job k completed by the canonical
-harness with payload {"step": k}; every completion runs the default output merge. One "step" =
-inject the staged 1M CREATE batch (already resident in HBM) and run every lockstep wave until the
-partition is quiescent (~148 waves, ~169M records, 108M WORKFLOW_INSTANCE transitions).
+Default workload (BASELINE.json configs[2], the largest single-GPU configuration and the one north_star's
+">= 50 % of HBM roofline for 10M concurrent instances" target names): two exclusive
+gateways with json-el conditions over msgpack payloads {"amount", "region", "score"} (Philox, seed 42),
+10,000,000 concurrent instances per GPU. One step = one processing tick of the partition
+(GPU timing):
+  1. inject the staged 10M CREATE commands (resident in HBM) at the log tail,
+  2. run every lockstep wave to quiescence (~130M records, ~120M WORKFLOW_INSTANCE transitions),
+  3. drain: serialize every record the tick wrote into the exact reference record values + record
+     headers, in HBM (zb_serialize) -- the emitted record stream a JNI shim appends to the log.
+The D2H copy of that stream into pinned host memory crosses PCIe; per the task contract it is never
+`value` and is reported beside it (value_pcie_inclusive), measured on one extra step.
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process and one partition
-per GPU, each with its own 1M instances (partitions never communicate for this workload:
-weak scaling, no collective on the data path; the barrier + max-over-ranks timing use torch.distributed).
+--config c2 | c3 | c4 | c5 selects another BASELINE configuration (c5: bench_extra.py).
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process and one partition per GPU,
+each with its own instances (instance i of the node -> partition i mod P); partitions never communicate
+for C1-C4 (weak scaling, no data-path collective; barrier + max-over-ranks timing through
+torch.distributed gloo).
 
-Prints ONE JSON line on rank 0 (contract in the task statement) with "roofline" and "cpu_baseline".
+Prints ONE JSON line on rank 0 with "roofline" and "cpu_baseline".
 """
 import argparse
 import json
 import os
+import platform
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -23,50 +33,269 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BYTES_PER_TRANSITION = 96  # 32 B row read + 32 B row write + 32 B record descriptor
-DESC_BYTES = 32  # one zb_rec descriptor written per log record
-# HBM bytes of the main emit kernel from the committed rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE: separate
-# runs of this script with --steps 1; tools/pmc_summary.py writes the file with the gfx950 correction)
-PMC_FILE = os.path.join(ROOT, "profiles", "r01", "pmc_v7.json")
+DESC_BYTES = 32  # one zb_rec descriptor per log record
+HDR_BYTES = 40  # one zb_record_header per drained record
+PMC_DIR = os.path.join(ROOT, "profiles", "r02")
+METRIC = "BPMN element transitions/sec (+ completed instances/sec) per node; % HBM roofline"
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=("c2", "c3", "c5"), default="c2",
-                    help="BASELINE.json configuration (default: C2, the headline metric); c3 / c5: bench_extra.py")
+    ap.add_argument("--config", choices=("c2", "c3", "c4", "c5"), default="c3")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--instances", type=int, default=0, help="per GPU (default: C2/C5 1,000,000, C3 10,000,000)")
+    ap.add_argument("--instances", type=int, default=0, help="per GPU (default: C3 10,000,000, C2/C4/C5 1,000,000)")
     ap.add_argument("--tasks", type=int, default=20)
-    ap.add_argument("--cpu-sample", type=int, default=30_000, help="instances in the oracle CPU baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=0, help="instances in the 1-thread oracle sample (0: default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the extra C2 wave-only / C4 lines")
+    ap.add_argument("--no-drain", action="store_true", help="device stepping only (not the contract's step)")
     ap.add_argument("--wave-only", action="store_true", help="force the general wave pipeline (no trajectory path)")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on GPU 0 (multi-rank rehearsal on a one-GPU box; not a scaling run)")
     return ap.parse_args()
 
 
-def cpu_baseline(n_inst, tasks):
-    """The oracle (sequential C++ restatement, 1 thread) on a bounded sample of the same workload."""
-    from oracle import zbref
+# ------------------------------------------------------------------------------ workloads
+def workload(cfg, n, start, tasks=20):
+    """(xml, process id, payload blob, offsets, job payloads, description) for instances [start, start + n)."""
     from zeebe_amd import bpmn, workloads
 
-    xml = bpmn.chain_workflow(tasks).to_xml()
+    if cfg == "c3":
+        blob, offs = workloads.xor_payloads_np(n, start=start)
+        return (bpmn.xor_workflow().to_xml(), "xor", blob, offs, {},
+                "C3: exclusive gateways with json-el conditions over msgpack payloads, %d concurrent instances "
+                "per GPU" % n)
+    if cfg == "c2":
+        blob, offs = workloads.order_payloads(n, start=start)
+        jp = {"t%d" % k: b"\x81" + workloads.mp_str("step") + workloads.mp_int(k) for k in range(1, tasks + 1)}
+        return (bpmn.chain_workflow(tasks).to_xml(), "chain", blob, offs, jp,
+                "C2: %d-service-task chain, %d concurrent instances per GPU, canonical job harness, default "
+                "output merges" % (tasks, n))
+    if cfg == "c4":
+        blob, offs = workloads.order_payloads(n, start=start)
+        jp = {"task%d" % k: b"\x81" + workloads.mp_str("sub") + workloads.mp_int(k) for k in range(1, 9)}
+        return (bpmn.parallel_workflow(8).to_xml(), "par", blob, offs, jp,
+                "C4: parallel fork/join (fan-out 8) with embedded sub-process scopes, %d instances per GPU "
+                "(EXTENSION, parity unpinned)" % n)
+    raise ValueError(cfg)
+
+
+RECS_PER_INST = {"c2": lambda t: 2 + 8 + 5 * t + 3 * t, "c3": lambda t: 16, "c4": lambda t: 200}
+
+
+def make_engine(cfg, n, a, rank, world, local_rank):
+    from zeebe_amd.engine import Engine
+
+    recs = RECS_PER_INST[cfg](a.tasks)
+    rows = {"c2": n * (a.tasks + 2), "c3": 1 << 20, "c4": n * 20}[cfg]
+    arena = {"c2": n * (48 + 48 * a.tasks), "c3": n * 64, "c4": n * 1200}[cfg] + (64 << 20)
+    return Engine(device=0 if a.same_device else local_rank, partition_id=rank, partition_count=world,
+                  log_capacity=int(n * recs), row_capacity=int(rows), arena_bytes=int(arena), wave_only=a.wave_only)
+
+
+def run_workload(cfg, n, a, rank, world, local_rank, barrier, steps, warmup, drain=True, pcie=False):
+    xml, pid, blob, offs, jp, desc = workload(cfg, n, rank * n, a.tasks)
+    eng = make_engine(cfg, n, a, rank, world, local_rank)
+    eng.deploy(xml, 100, 1)
+    for act, p in jp.items():
+        eng.set_job_payload(100, act, p)
+    eng.create_packed(pid, blob, offs)
+    del blob
+
+    def one_step():
+        eng.reset(keep_staged=True)
+        t0 = time.perf_counter()
+        st = eng.step()
+        t1 = time.perf_counter()
+        assert st["quiescent"], st
+        ser = None
+        if drain:  # the tick's emitted records (everything after the n injected commands)
+            ser = eng.serialize(n, eng.log_size() - n)
+        t2 = time.perf_counter()
+        return st, ser, t1 - t0, t2 - t1
+
+    for _ in range(warmup):
+        one_step()
+    barrier()
+    tot = dict(transitions=0, completed=0, written=0, merges=0, merge_bytes=0, cond_bytes=0, kernel_ms=0.0,
+               process_ms=0.0, emit_ms=0.0, aux_ms=0.0, main_ms=0.0, launches=0, waves=0, step_s=0.0, drain_s=0.0,
+               ser_write_ms=0.0, ser_size_ms=0.0, value_bytes=0, payload_bytes=0, drained=0, path=0)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        st, ser, ts, td = one_step()
+        tot["transitions"] += st["transitions"]
+        tot["completed"] += st["completed_instances"]
+        tot["written"] += st["records_written"]
+        tot["merges"] += st["merges"]
+        tot["merge_bytes"] += st["merge_bytes"]
+        tot["cond_bytes"] += st["condition_payload_bytes"]
+        tot["kernel_ms"] += st["wave_kernel_ms"]
+        tot["process_ms"] += st["process_kernel_ms"]
+        tot["emit_ms"] += st["emit_kernel_ms"]
+        tot["aux_ms"] += st["aux_kernel_ms"]
+        tot["main_ms"] += st["main_emit_kernel_ms"]
+        tot["launches"] += st["launches"]
+        tot["waves"] += st["waves"]
+        tot["path"] = st["path"]
+        tot["step_s"] += ts
+        tot["drain_s"] += td
+        if ser:
+            tot["ser_write_ms"] += ser["write_kernel_ms"]
+            tot["ser_size_ms"] += ser["size_kernel_ms"]
+            tot["value_bytes"] += ser["value_bytes"]
+            tot["payload_bytes"] += ser["payload_bytes"]
+            tot["drained"] += ser["records"]
+    barrier()
+    tot["elapsed"] = time.perf_counter() - t0
+    tot["desc"] = desc
+    if pcie and drain:
+        tot["pcie"] = pcie_step(eng, n, one_step)
+    eng.close()
+    return tot
+
+
+def pcie_step(eng, n, one_step, chunk=256 << 20):
+    """One more tick with the drained stream copied to pinned host memory in 256 MiB chunks (double
+    buffered host-side; each chunk is consumed before its buffer is reused)."""
+    from zeebe_amd.engine import pinned_alloc, pinned_free
+
+    bufs = [pinned_alloc(chunk), pinned_alloc(chunk)]
+    try:
+        t0 = time.perf_counter()
+        st, ser, _, _ = one_step()
+        t1 = time.perf_counter()
+        total, off, k = ser["value_bytes"], 0, 0
+        while off < total:
+            m = min(chunk, total - off)
+            eng.drain_copy(bufs[k & 1], off, m)
+            off += m
+            k += 1
+        t2 = time.perf_counter()
+    finally:
+        for b in bufs:
+            pinned_free(b)
+    return {"transitions": st["transitions"], "tick_s": t1 - t0, "d2h_s": t2 - t1, "bytes": ser["value_bytes"],
+            "d2h_GBps": ser["value_bytes"] / (t2 - t1) / 1e9 if t2 > t1 else 0.0}
+
+
+# ------------------------------------------------------------------------------ CPU baseline
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def _oracle_partition(cfg, n, start, tasks):
+    from oracle import zbref
+
+    xml, pid, blob, offs, jp, _ = workload(cfg, n, start, tasks)
     o = zbref.Oracle()
     o.deploy(xml, 100, 1)
-    for k in range(1, tasks + 1):
-        o.set_job_payload(100, "t%d" % k, b"\x81" + workloads.mp_str("step") + workloads.mp_int(k))
-    blob, offs = workloads.order_payloads(n_inst)
-    for p in workloads.split(blob, offs):
-        o.create("chain", p)
-    n, secs = o.run_timed()
-    transitions = (8 + 5 * tasks) * n_inst
-    return {"value": transitions / secs, "unit": "transitions/s", "cores": 1, "kind": "port",
-            "sample": "C2 chain of %d tasks, %d instances, %d records processed in %.2f s by oracle/zbref "
-                      "(1 thread, sequential FIFO, canonical job harness)" % (tasks, n_inst, n, secs),
-            "completed_instances_per_s": n_inst / secs}
+    for act, p in jp.items():
+        o.set_job_payload(100, act, p)
+    o.create_packed(pid, blob, offs)
+    return o
 
 
+def cpu_baseline_line(cfg, tasks, sample):
+    """The oracle (sequential C++ restatement of the reference path, same canonical schedule) on a bounded
+    sample of the same workload: 1 partition on 1 core, and P = min(8, cores) partitions on P cores (one
+    thread per partition, as the reference runs one stream processor per partition)."""
+    import ctypes
+
+    threads = min(8, os.cpu_count() or 1)
+    res = {}
+    for k in sorted({1, threads}):
+        per = sample if k == 1 else max(sample // 2, 1)
+        parts = [_oracle_partition(cfg, per, i * per, tasks) for i in range(k)]
+        counts = [0] * k
+
+        def run(i):
+            nrec = ctypes.c_int64()
+            parts[i]._L.zbref_run_timed(parts[i]._h, ctypes.byref(nrec))
+            counts[i] = nrec.value
+
+        ths = [threading.Thread(target=run, args=(i,)) for i in range(k)]
+        t0 = time.perf_counter()
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        wall = time.perf_counter() - t0
+        cs = [p.counters() for p in parts]
+        res[k] = dict(instances=sum(c["created"] for c in cs), transitions=sum(c["transitions"] for c in cs),
+                      completed=sum(c["completed"] for c in cs), records=sum(counts), wall_s=wall)
+        for p in parts:
+            p.close()
+    one, many = res[1], res[threads]
+    return {"value": one["transitions"] / one["wall_s"], "unit": "transitions/s", "cores": 1, "kind": "port",
+            "sample": "%s workload, %d instances (%d records processed) run to quiescence by oracle/zbref, 1 thread, "
+                      "sequential FIFO, canonical job harness: %.2f s" % (cfg.upper(), one["instances"],
+                                                                          one["records"], one["wall_s"]),
+            "cpu_model": cpu_model(),
+            "completed_instances_per_s": one["completed"] / one["wall_s"],
+            "multi_partition": {"value": many["transitions"] / many["wall_s"], "cores": threads,
+                                "partitions": threads, "instances": many["instances"], "wall_s": many["wall_s"],
+                                "completed_instances_per_s": many["completed"] / many["wall_s"],
+                                "note": "one oracle partition per thread, run concurrently (SURVEY §8d: P partitions "
+                                        "on P cores, P = min(8, cores))"}}
+
+
+# ------------------------------------------------------------------------------ roofline
+def load_traffic(tag, kernel_prefix):
+    f = os.path.join(PMC_DIR, "pmc_%s.json" % tag)
+    if not os.path.exists(f):
+        return None, None
+    with open(f) as fh:
+        d = json.load(fh)
+    for k, v in d.get("kernels", {}).items():
+        if kernel_prefix in k and "hbm_bytes" in v:
+            return v["hbm_bytes"], k
+    return None, None
+
+
+def roofline(tot, steps, cfg, n):
+    """Dominant kernel of the step: the drain's write pass or the main emit launch, by device time."""
+    cands = []
+    if tot["ser_write_ms"] > 0:
+        # per launch: every drained record's descriptor read + header write, its value bytes written and the
+        # payload documents copied into them read (SURVEY §8d payload term)
+        b = (tot["drained"] * (DESC_BYTES + HDR_BYTES) + tot["value_bytes"] + tot["payload_bytes"]) / steps
+        cands.append(("zbg::k_ser_write", tot["ser_write_ms"] / steps, b,
+                      "32 B descriptor read + 40 B header write per drained record + value bytes written + payload "
+                      "bytes read"))
+    if tot["main_ms"] > 0:
+        b = (DESC_BYTES * tot["written"] + tot["merge_bytes"] + tot["cond_bytes"]) / steps
+        kname = {1: "zbg::k_tmpl<false, false>", 2: "zbg::k_tmpl<true, false>"}.get(tot["path"], "zbg::k_tmpl")
+        cands.append((kname, tot["main_ms"] / steps, b,
+                      "32 B descriptor per record written + merge (job + scope + result) bytes + condition payload "
+                      "bytes (the launch writes no element-instance rows per transition)"))
+    if tot["path"] == 0 and tot["process_ms"] > 0:
+        b = (BYTES_PER_TRANSITION * tot["transitions"] + tot["merge_bytes"] + tot["cond_bytes"]) / steps
+        cands.append(("zbg::k_process (+ k_scan, k_emit, k_merge, k_cond: every wave kernel)", tot["kernel_ms"] / steps, b,
+                      "SURVEY §8d: 96 B per transition + merge + condition bytes over all wave kernels"))
+    name, ms, b, model = max(cands, key=lambda c: c[1])
+    achieved = b / (ms / 1e3) / 1e9
+    traffic, pmc_kernel = load_traffic("%s_%d" % (cfg, n), name.split(" ")[0].split("<")[0])
+    r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+         "traffic": traffic, "kernel": name, "avg_launch_us": ms * 1e3, "alg_bytes_per_launch": b,
+         "alg_bytes_model": model,
+         "traffic_note": ("HBM bytes per launch of %s from rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (separate --pmc "
+                          "passes, profiles/r02/pmc_%s_%d.json)" % (pmc_kernel, cfg, n)) if traffic else
+                         "no committed PMC passes for this workload"}
+    r["other_kernels"] = [{"kernel": c[0], "avg_launch_us": c[1] * 1e3, "alg_bytes_per_launch": c[2],
+                           "achieved": c[2] / (c[1] / 1e3) / 1e9, "frac": c[2] / (c[1] / 1e3) / 1e9 / HBM_PEAK_GBS}
+                          for c in cands if c[0] != name]
+    return r
+
+
+# ------------------------------------------------------------------------------ main
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -76,144 +305,104 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        # Control plane only (barrier, max-over-ranks, sums): the C2 partitions never exchange data, so
-        # there is no data-path collective (weak scaling). gloo keeps torch's own HIP runtime out of the
-        # process: the engine (libzbgpu.so) drives its GPU through the system ROCm runtime and
-        # synchronizes its own stream at the end of every zb_step.
+        # Control plane only (barrier, max-over-ranks, sums): C1-C4 partitions never exchange data (weak
+        # scaling, no data-path collective). gloo keeps torch's own HIP runtime out of the process: the engine
+        # (libzbgpu.so) drives its GPU through the system ROCm runtime.
         dist.init_process_group("gloo")
-
     if a.instances == 0:
         a.instances = 10_000_000 if a.config == "c3" else 1_000_000
-    if a.config != "c2":
-        return run_other(a, rank, world, local_rank, dist)
-
-    from zeebe_amd import bpmn, workloads
-    from zeebe_amd.engine import Engine
-
-    n = a.instances
-    recs_per_inst = 1 + (8 + 5 * a.tasks) + 3 * a.tasks  # CREATE + WF events + JOB CREATE/CREATED/COMPLETED
-    eng = Engine(device=0 if a.same_device else local_rank, partition_id=rank, partition_count=world,
-                 log_capacity=int(n * (recs_per_inst + 2)), row_capacity=int(n * (a.tasks + 2)),
-                 arena_bytes=int(n * (48 + 48 * a.tasks)) + (64 << 20), wave_only=a.wave_only)
-    xml = bpmn.chain_workflow(a.tasks).to_xml()
-    eng.deploy(xml, 100, 1)
-    for k in range(1, a.tasks + 1):
-        eng.set_job_payload(100, "t%d" % k, b"\x81" + workloads.mp_str("step") + workloads.mp_int(k))
-    # instance i of this partition: global instance id = rank * n + i (round-robin over partitions)
-    blob, offs = workloads.order_payloads(n, start=rank * n)
-    eng.create_packed("chain", blob, offs)
-
-    def one_step():
-        eng.reset(keep_staged=True)
-        st = eng.step()
-        assert st["quiescent"], st
-        return st
-
-    for _ in range(a.warmup):
-        one_step()
+    if a.config == "c5":
+        return run_c5(a, rank, world, local_rank, dist)
 
     def barrier():
         if dist is not None:
-            dist.barrier()  # every rank's zb_step has returned: its stream is drained
+            dist.barrier()
 
-    barrier()
-    t0 = time.perf_counter()
-    tot = dict(main_ms=0.0, written=0, transitions=0, completed=0, kernel_ms=0.0, process_ms=0.0, emit_ms=0.0, aux_ms=0.0, launches=0, waves=0, merge_bytes=0, cond_bytes=0,
-               records=0, path=0)
-    for _ in range(a.steps):
-        st = one_step()
-        tot["transitions"] += st["transitions"]
-        tot["completed"] += st["completed_instances"]
-        tot["kernel_ms"] += st["wave_kernel_ms"]
-        tot["main_ms"] += st["main_emit_kernel_ms"]
-        tot["written"] += st["records_written"]
-        tot["process_ms"] += st["process_kernel_ms"]
-        tot["emit_ms"] += st["emit_kernel_ms"]
-        tot["aux_ms"] += st["aux_kernel_ms"]
-        tot["launches"] += st["launches"]
-        tot["waves"] += st["waves"]
-        tot["merge_bytes"] += st["merge_bytes"]
-        tot["cond_bytes"] += st["condition_payload_bytes"]
-        tot["records"] += st["records_processed"]
-        tot["path"] = st["path"]
-    barrier()
-    elapsed = time.perf_counter() - t0
-
-    if dist is not None:
+    def reduce(v, op):
+        if dist is None:
+            return v
         import torch
 
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor([tot["transitions"], tot["completed"]], dtype=torch.float64)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        all_transitions, all_completed = float(c[0]), float(c[1])
-    else:
-        all_transitions, all_completed = float(tot["transitions"]), float(tot["completed"])
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        dist.all_reduce(t, op=op)
+        return float(t.item())
 
-    traffic, pmc_kernel = None, None
-    if n == 1_000_000 and a.tasks == 20 and os.path.exists(PMC_FILE):
-        with open(PMC_FILE) as f:
-            pmc = json.load(f)
-        traffic, pmc_kernel = pmc["main_traffic_bytes"], pmc["main_kernel"]
-
+    n = a.instances
+    tot = run_workload(a.config, n, a, rank, world, local_rank, barrier, a.steps, a.warmup, drain=not a.no_drain,
+                       pcie=(rank == 0 and world == 1 and not a.no_drain))
+    elapsed = tot["elapsed"]
+    all_tr, all_comp = tot["transitions"], tot["completed"]
+    if dist is not None:
+        elapsed = reduce(elapsed, dist.ReduceOp.MAX)
+        all_tr = reduce(all_tr, dist.ReduceOp.SUM)
+        all_comp = reduce(all_comp, dist.ReduceOp.SUM)
     if rank == 0:
-        # path level (SURVEY §8d model): 96 B per transition + merge + condition bytes over every kernel of a step
-        alg_bytes = BYTES_PER_TRANSITION * tot["transitions"] + tot["merge_bytes"] + tot["cond_bytes"]
-        kernel_s = tot["kernel_ms"] / 1e3
-        path_achieved = alg_bytes / kernel_s / 1e9 if kernel_s > 0 else 0.0
-        # dominant kernel (the main emit launch, ~80% of device time): per launch it writes every record
-        # descriptor of the batch and performs every output merge (reads job + scope documents, writes the
-        # result) and condition evaluation; one launch per step
-        main_bytes = DESC_BYTES * tot["written"] + tot["merge_bytes"] + tot["cond_bytes"]
-        main_s = tot["main_ms"] / 1e3
-        achieved = main_bytes / main_s / 1e9 if main_s > 0 else path_achieved
+        steps = a.steps
         out = {
-            "metric": "BPMN element transitions/sec (+ completed instances/sec) per node; % HBM roofline",
-            "value": all_transitions / elapsed,
+            "metric": METRIC,
+            "value": all_tr / elapsed,
             "unit": "transitions/s",
             "n_gpus": world,
-            "steps": a.steps,
+            "steps": steps,
             "warmup": a.warmup,
-            "ms_per_step": elapsed * 1e3 / a.steps,
+            "ms_per_step": elapsed * 1e3 / steps,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int64",
-            "data": "synthetic (SURVEY §8d C2: {\"orderId\": i} create payloads, {\"step\": k} job payloads)",
-            "config": {"workload": "C2: 20-service-task chain, %d concurrent instances per GPU, canonical job "
-                                   "harness, default output merges" % n,
-                       "instances_per_gpu": n, "tasks": a.tasks, "partitions": world,
-                       "parallelism": "partition-per-gpu"},
-            "completed_instances_per_s": all_completed / elapsed,
-            "records_processed_per_step_rank0": tot["records"] / a.steps,
-            "wave_launches_per_step": tot["launches"] / a.steps,
-            "kernel_ms_per_step": {"total": tot["kernel_ms"] / a.steps, "process_or_count": tot["process_ms"] / a.steps,
-                                   "scan_emit": tot["emit_ms"] / a.steps, "aux": tot["aux_ms"] / a.steps},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic,
-                         "traffic_note": "HBM bytes per launch of %s (FETCH_SIZE x2 + WRITE_SIZE, separate "
-                                         "rocprofv3 --pmc passes, profiles/r01/pmc_v7.json)" % pmc_kernel,
-                         "kernel": {0: "zbg::k_emit (wave pipeline)", 1: "zbg::k_tmpl<false,false> (template emit)",
-                                    2: "zbg::k_tmpl<true,false> (class-batch emit)"}.get(tot["path"], "?"),
-                         "launches": a.steps, "avg_launch_us": tot["main_ms"] * 1e3 / a.steps,
-                         "alg_bytes_per_launch": main_bytes / a.steps,
-                         "alg_bytes_model": "32 B descriptor per record written + merge (job+scope+result) bytes "
-                                            "+ condition payload bytes"},
-            "path_roofline": {"achieved": path_achieved, "frac": path_achieved / HBM_PEAK_GBS, "unit": "GB/s",
-                              "kernels": "every kernel of a step (count, scan, emit, commit)",
-                              "kernel_launches": tot["launches"],
-                              "alg_bytes_per_transition": BYTES_PER_TRANSITION, "alg_bytes_total": alg_bytes},
+            "data": "synthetic (SURVEY §8d %s inputs, deterministic)" % a.config.upper(),
+            "config": {"workload": tot["desc"], "instances_per_gpu": n, "partitions": world,
+                       "parallelism": "partition-per-gpu",
+                       "timed_step": "inject staged CREATEs (in HBM) + lockstep waves to quiescence" +
+                                     ("" if a.no_drain else " + zb_serialize of every emitted record (values + "
+                                                              "headers, in HBM)")},
+            "completed_instances_per_s": all_comp / elapsed,
+            "records_written_per_step": tot["written"] / steps,
+            "wave_launches_per_step": tot["launches"] / steps,
+            "step_breakdown_ms": {"stepping": tot["step_s"] * 1e3 / steps, "drain": tot["drain_s"] * 1e3 / steps,
+                                  "stepping_kernels": tot["kernel_ms"] / steps,
+                                  "drain_size_kernel": tot["ser_size_ms"] / steps,
+                                  "drain_write_kernel": tot["ser_write_ms"] / steps},
+            "value_stepping_only": tot["transitions"] / tot["step_s"] if tot["step_s"] else None,
+            "drained_bytes_per_step": tot["value_bytes"] / steps + HDR_BYTES * tot["drained"] / steps,
+            "roofline": roofline(tot, steps, a.config, n),
         }
+        if "pcie" in tot:
+            p = tot["pcie"]
+            out["value_pcie_inclusive"] = p["transitions"] / (p["tick_s"] + p["d2h_s"])
+            out["pcie"] = {"d2h_GBps": p["d2h_GBps"], "bytes": p["bytes"], "tick_ms": p["tick_s"] * 1e3,
+                           "d2h_ms": p["d2h_s"] * 1e3,
+                           "note": "one extra tick whose drained values are copied to pinned host memory (256 MiB "
+                                   "chunks); PCIe-inclusive rate, never `value` (task contract)"}
+        if world == 1 and not a.no_extras and a.config == "c3":
+            out["extras"] = extras(a, barrier)
         if world == 1 and not a.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(a.cpu_sample, a.tasks)
+            sample = a.cpu_sample or {"c3": 400_000, "c2": 30_000, "c4": 20_000}[a.config]
+            out["cpu_baseline"] = cpu_baseline_line(a.config, a.tasks, sample)
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
 
 
-def run_other(a, rank, world, local_rank, dist):
+def extras(a, barrier):
+    """Shorter lines on the other single-GPU configurations (same step definition, 3 steps each)."""
+    out = {}
+    import copy
+
+    b = copy.copy(a)
+    b.wave_only = True
+    t = run_workload("c2", 1_000_000, b, 0, 1, 0, barrier, 3, 1)
+    out["c2_wave_only"] = {"value": t["transitions"] / t["elapsed"], "ms_per_step": t["elapsed"] * 1e3 / 3,
+                           "stepping_ms": t["step_s"] * 1e3 / 3, "drain_ms": t["drain_s"] * 1e3 / 3,
+                           "roofline": roofline(t, 3, "c2w", 1_000_000), "workload": t["desc"] + " (wave pipeline)"}
+    t = run_workload("c4", 1_000_000, a, 0, 1, 0, barrier, 3, 1)
+    out["c4"] = {"value": t["transitions"] / t["elapsed"], "ms_per_step": t["elapsed"] * 1e3 / 3,
+                 "stepping_ms": t["step_s"] * 1e3 / 3, "drain_ms": t["drain_s"] * 1e3 / 3,
+                 "roofline": roofline(t, 3, "c4", 1_000_000), "workload": t["desc"]}
+    return out
+
+
+def run_c5(a, rank, world, local_rank, dist):
     import socket
 
     import torch
@@ -221,7 +410,7 @@ def run_other(a, rank, world, local_rank, dist):
 
     import bench_extra
 
-    if dist is None and a.config == "c5":  # the exchange driver needs a (one-rank) control plane
+    if dist is None:  # the exchange driver needs a (one-rank) control plane
         s = socket.socket()
         s.bind(("127.0.0.1", 0))
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -231,21 +420,16 @@ def run_other(a, rank, world, local_rank, dist):
         dist = tdist
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
+        dist.barrier()
 
     def reduce(v, op):
-        if dist is None:
-            return v
         t = torch.tensor([float(v)], dtype=torch.float64)
         dist.all_reduce(t, op=op)
         return float(t.item())
 
-    fn = bench_extra.run_c3 if a.config == "c3" else bench_extra.run_c5
-    fn(a, rank, world, local_rank, dist, barrier, lambda v: reduce(v, tdist.ReduceOp.MAX),
-       lambda v: reduce(v, tdist.ReduceOp.SUM))
-    if dist is not None:
-        dist.destroy_process_group()
+    bench_extra.run_c5(a, rank, world, local_rank, dist, barrier, lambda v: reduce(v, tdist.ReduceOp.MAX),
+                       lambda v: reduce(v, tdist.ReduceOp.SUM))
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -1,7 +1,5 @@
-"""bench.py --config c3 | c5: the other BASELINE.json configurations (the default run is C2).
+"""bench.py --config c5: message correlation across partitions (the default run is C3, bench.py).
 
-C3: two exclusive gateways with json-el conditions over msgpack payloads
-    {"amount": U[0,2000), "region": EU|US|APAC, "score": U[0,1)} (Philox, seed 42), 10M instances on one GPU.
 C5: start -> message catch ("order", $.orderId) -> end, instances round-robin over the
     partitions (one per GPU); phase 1 runs the CREATEs to quiescence (subscriptions opened on partition
     abs(hash % P)), phase 2 publishes one message per orderId (TTL 1 h, payload {"paid": true}) and runs
@@ -37,50 +35,6 @@ def _routing(cks, world):
 def _emit(out, rank):
     if rank == 0:
         print(json.dumps(out))
-
-
-def run_c3(a, rank, world, local_rank, dist, barrier, reduce_max, reduce_sum):
-    from zeebe_amd import bpmn, workloads
-    from zeebe_amd.engine import Engine
-
-    n = a.instances
-    eng = Engine(device=0 if a.same_device else local_rank, partition_id=rank, partition_count=world,
-                 log_capacity=n * 16, row_capacity=1 << 20, arena_bytes=n * 64 + (64 << 20), wave_only=a.wave_only)
-    eng.deploy(bpmn.xor_workflow().to_xml(), 100, 1)
-    blob, offs = workloads.xor_payloads(n, start=rank * n)
-    eng.create_packed("xor", blob, offs)
-
-    def step():
-        eng.reset(keep_staged=True)
-        st = eng.step()
-        assert st["quiescent"], st
-        return st
-
-    for _ in range(a.warmup):
-        step()
-    barrier()
-    t0 = time.perf_counter()
-    tr = comp = cond = 0
-    kms = 0.0
-    for _ in range(a.steps):
-        st = step()
-        tr += st["transitions"]; comp += st["completed_instances"]; cond += st["condition_payload_bytes"]
-        kms += st["wave_kernel_ms"]
-    barrier()
-    el = reduce_max(time.perf_counter() - t0)
-    all_tr, all_comp = reduce_sum(tr), reduce_sum(comp)
-    alg = BYTES_PER_TRANSITION * tr + cond
-    ach = alg / (kms / 1e3) / 1e9 if kms else 0.0
-    _emit({"metric": "BPMN element transitions/sec (+ completed instances/sec) per node; % HBM roofline",
-           "value": all_tr / el, "unit": "transitions/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-           "ms_per_step": el * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-           "dtype": "int64/f64", "data": "synthetic (SURVEY §8d C3 payloads, Philox seed 42)",
-           "config": {"workload": "C3: exclusive gateways + json-el over msgpack, %d instances per GPU" % n,
-                      "instances_per_gpu": n, "partitions": world, "parallelism": "partition-per-gpu"},
-           "completed_instances_per_s": all_comp / el,
-           "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": ach / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_transition": BYTES_PER_TRANSITION,
-                        "condition_payload_bytes_per_step": cond / a.steps}}, rank)
 
 
 def run_c5(a, rank, world, local_rank, dist, barrier, reduce_max, reduce_sum):

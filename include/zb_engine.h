@@ -238,9 +238,31 @@ int64_t zb_log_size(zb_engine* e);
 int zb_read_descriptors(zb_engine* e, int64_t start, int64_t count, zb_rec* out);
 /* Serializes records [start, start+count) on the GPU into reference value bytes and copies them
  * back: headers[count], value bytes into values (capacity values_cap); *values_len = bytes needed.
- * If values_cap is too small nothing is copied and ZB_ENOMEM is returned with *values_len set. */
+ * If values_cap is too small nothing is copied and ZB_ENOMEM is returned with *values_len set.
+ * = zb_serialize + zb_drain_copy. */
 int zb_drain(zb_engine* e, int64_t start, int64_t count, zb_record_header* headers, uint8_t* values,
              size_t values_cap, size_t* values_len);
+
+/* The two halves of zb_drain. zb_serialize writes the headers and value bytes of records
+ * [start, start+count) into the engine's device-resident drain buffers (reused between calls; the
+ * batch stays there until the next zb_serialize); zb_drain_copy copies that batch, or a byte range
+ * of its values, to host memory (pinned memory gives the full PCIe rate). */
+typedef struct zb_serialize_stats {
+  uint64_t records;
+  uint64_t value_bytes;        /* serialized record values */
+  uint64_t payload_bytes;      /* payload documents copied into them (msgpack bin) */
+  double size_kernel_ms;       /* size pass */
+  double scan_ms;              /* exclusive scan of the sizes */
+  double write_kernel_ms;      /* write pass (headers + values): the drain's dominant kernel */
+  double wall_ms;
+} zb_serialize_stats;
+int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats* stats);
+/* headers: NULL or room for the batch's headers; values: NULL or values_len bytes from value byte
+ * value_off of the batch. */
+int zb_drain_copy(zb_engine* e, zb_record_header* headers, uint8_t* values, uint64_t value_off, size_t values_len);
+/* Page-locked host memory for zb_drain_copy destinations (hipHostMalloc); NULL on failure. */
+void* zb_pinned_alloc(size_t bytes);
+void zb_pinned_free(void* p);
 /* counters: [0] created [1] completed [2] canceled [3] next wf key [4] next job key
  *           [5] rows allocated [6] arena bytes used [7] log size */
 int zb_counters(zb_engine* e, int64_t out[8]);

@@ -622,6 +622,7 @@ class Engine {
   std::vector<std::unique_ptr<Workflow>> workflows;
   std::map<std::pair<int64_t, bytes>, bytes> job_payloads;  // (workflow key, activity id) -> completion payload
   int64_t created = 0, completed = 0, canceled = 0;
+  int64_t transitions = 0;  // WORKFLOW_INSTANCE events written (streamprocessor_events_count{written}, WF)
   size_t processed = 0;
   // canonical job harness on; off: JOB CREATE commands wait for job events submitted
   // from outside (the job stream processor's JOB CREATED / JOB COMPLETED records, zbref_submit_record)
@@ -927,6 +928,7 @@ class Engine {
     w_ = nullptr;
     for (auto& r : w.staged) {
       r.raw_value.clear();  // follow-ups are encoded from their value objects
+      if (r.value_type == VT_WORKFLOW_INSTANCE && r.record_type == RT_EVENT) transitions++;
       r.source_position = rec.position;
       append(std::move(r));
     }
@@ -1435,6 +1437,21 @@ int64_t zbref_dump_instances(void* h, uint8_t* buf, size_t cap) {
   return (int64_t)off;
 }
 
+// bulk form of zbref_submit_create: n payloads, offsets[n + 1] into blob
+int zbref_submit_creates(void* h, const char* process_id, int32_t version, int64_t workflow_key, size_t n,
+                         const uint8_t* blob, const uint64_t* offsets) {
+  Engine* e = (Engine*)h;
+  try {
+    const bytes pid(process_id);
+    for (size_t i = 0; i < n; i++)
+      e->submit_create(pid, version, workflow_key, bytes((const char*)blob + offsets[i], offsets[i + 1] - offsets[i]));
+    return 0;
+  } catch (const std::exception& ex) {
+    e->last_error = ex.what();
+    return -1;
+  }
+}
+
 int zbref_submit_cancel(void* h, int64_t key) {
   ((Engine*)h)->submit_cancel(key);
   return 0;
@@ -1535,6 +1552,7 @@ void zbref_counters(void* h, int64_t* out) {
   out[3] = (int64_t)e->index.instances.size();
   out[4] = e->wf_keys.next;
   out[5] = e->job_keys.next;
+  out[6] = e->transitions;
 }
 
 int64_t zbref_side_effects(void* h, int64_t i, int64_t* keys, int32_t* partition, uint8_t* ck, size_t cap) {

@@ -40,6 +40,7 @@ def lib():
         L.zbref_set_job_payload.argtypes = [vp, i64, cp, u8p, sz]
         L.zbref_submit_create.argtypes = [vp, cp, i32, i64, u8p, sz]
         L.zbref_submit_cancel.argtypes = [vp, i64]
+        L.zbref_submit_creates.argtypes = [vp, cp, i32, i64, sz, ctypes.c_void_p, ctypes.c_void_p]
         L.zbref_set_harness.argtypes = [vp, ctypes.c_int]
         L.zbref_submit_record.argtypes = [vp, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, i64, u8p, sz]
         L.zbref_dump_instances.restype = i64
@@ -156,6 +157,13 @@ class Oracle:
         if self._L.zbref_submit_create(self._h, process_id.encode(), version, workflow_key, payload, len(payload)):
             raise ZbrefError(self._err())
 
+    def create_packed(self, process_id: str, blob: bytes, offsets, version: int = -1, workflow_key: int = -1):
+        """Bulk create: offsets is a uint64 numpy array of n+1 entries into blob."""
+        buf = ctypes.create_string_buffer(blob, max(len(blob), 1))
+        if self._L.zbref_submit_creates(self._h, process_id.encode(), version, workflow_key, len(offsets) - 1, buf,
+                                        offsets.ctypes.data):
+            raise ZbrefError(self._err())
+
     def cancel(self, key: int):
         self._L.zbref_submit_cancel(self._h, key)
 
@@ -240,10 +248,10 @@ class Oracle:
         return buf.raw[:need]
 
     def counters(self) -> dict:
-        arr = (ctypes.c_int64 * 6)()
+        arr = (ctypes.c_int64 * 7)()
         self._L.zbref_counters(self._h, arr)
         return dict(created=arr[0], completed=arr[1], canceled=arr[2], live_instances=arr[3],
-                    next_wf_key=arr[4], next_job_key=arr[5])
+                    next_wf_key=arr[4], next_job_key=arr[5], transitions=arr[6])
 
     def side_effects(self):
         n = self._L.zbref_side_effects(self._h, -1, None, None, None, 0)

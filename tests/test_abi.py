@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_symbols():
     src = open(os.path.join(ROOT, "include", "zb_engine.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|int64_t|void|const char\*)\s+(zb_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|void\*|void|const char\*)\s*(zb_\w+)\s*\(", src, re.M)))
 
 
 def test_header_declares_expected_api():

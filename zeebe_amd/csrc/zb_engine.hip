@@ -188,6 +188,17 @@ struct zb_engine {
   std::unordered_map<int64_t, uint8_t> tick_inst;  // workflow instance -> 1: scope command, 2: other records
   std::unordered_set<int64_t> tick_aik;
   DevVec<int64_t> d_lookup_keys, d_lookup_pos;
+  // drain buffers (zb_serialize), grown on demand and reused
+  uint64_t dr_cap = 0, dr_val_cap = 0, dr_tmp_cap = 0;
+  uint64_t *dr_len = nullptr, *dr_off = nullptr;
+  zb_record_header* dr_hdr = nullptr;
+  uint8_t* dr_val = nullptr;
+  void* dr_tmp = nullptr;
+  uint64_t* dr_total = nullptr;   // [0] value bytes, [1] payload bytes (device)
+  uint64_t* h_dr_total = nullptr; // pinned mirror
+  int64_t dr_count = 0;           // records of the batch in the drain buffers
+  uint64_t dr_bytes = 0;
+  hipEvent_t dr_ev[4] = {nullptr, nullptr, nullptr, nullptr};
 
   // timing
   std::vector<hipEvent_t> ev;
@@ -645,6 +656,12 @@ void zb_engine_destroy(zb_engine* e) {
   e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_consts.free();
   e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
   e->d_ranges.free(); e->d_cmd_pool.free(); e->d_lookup_keys.free(); e->d_lookup_pos.free();
+  void* dr[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_val, e->dr_tmp, e->dr_total};
+  for (void* p : dr)
+    if (p) (void)hipFree(p);
+  if (e->h_dr_total) (void)hipHostFree(e->h_dr_total);
+  for (auto& x : e->dr_ev)
+    if (x) (void)hipEventDestroy(x);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -1375,30 +1392,43 @@ int zb_read_descriptors(zb_engine* e, int64_t start, int64_t count, zb_rec* out)
   return ZB_OK;
 }
 
-int zb_drain(zb_engine* e, int64_t start, int64_t count, zb_record_header* headers, uint8_t* values,
-             size_t values_cap, size_t* values_len) {
+int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats* stats) {
   if (!e || start < e->log_floor || count < 0 || start + count > e->host_hdr.end) return ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
+  auto t0 = std::chrono::steady_clock::now();
+  zb_serialize_stats st{};
+  e->dr_count = 0;
+  e->dr_bytes = 0;
   if (count == 0) {
-    if (values_len) *values_len = 0;
+    if (stats) *stats = st;
     return ZB_OK;
   }
+  if (!e->dr_ev[0])
+    for (auto& x : e->dr_ev) HIPCHECK(e, hipEventCreate(&x));
+  if (!e->dr_total) {
+    HIPCHECK(e, hipMalloc(&e->dr_total, 2 * sizeof(uint64_t)));
+    HIPCHECK(e, hipHostMalloc(&e->h_dr_total, 2 * sizeof(uint64_t)));
+  }
+  if ((uint64_t)count > e->dr_cap) {
+    void* ps[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_tmp};
+    for (void* q : ps)
+      if (q) (void)hipFree(q);
+    e->dr_len = e->dr_off = nullptr; e->dr_hdr = nullptr; e->dr_tmp = nullptr; e->dr_cap = e->dr_tmp_cap = 0;
+    const uint64_t cap = (uint64_t)count + (uint64_t)count / 4 + 1024;
+    HIPCHECK(e, hipMalloc(&e->dr_len, (cap + 1) * sizeof(uint64_t)));
+    HIPCHECK(e, hipMalloc(&e->dr_off, (cap + 1) * sizeof(uint64_t)));
+    HIPCHECK(e, hipMalloc(&e->dr_hdr, cap * sizeof(zb_record_header)));
+    size_t tmp = 0;
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->dr_len, e->dr_off, (int)std::min<uint64_t>(cap + 1, INT32_MAX),
+                                         e->stream) != hipSuccess)
+      return fail(e, ZB_EDEVICE, "scan sizing");
+    HIPCHECK(e, hipMalloc(&e->dr_tmp, tmp + 16));
+    e->dr_tmp_cap = tmp;
+    e->dr_cap = cap;
+  }
+  if ((uint64_t)count + 1 > (uint64_t)INT32_MAX) return fail(e, ZB_EUNSUPPORTED, "more than 2^31 records in one drain");
   HIPCHECK(e, e->d_ranges.upload(e->ranges, e->stream));
   HIPCHECK(e, e->d_cmd_pool.upload(e->cmd_pool, e->stream));
-  uint64_t* d_len = nullptr;
-  uint64_t* d_off = nullptr;
-  void* d_tmp = nullptr;
-  size_t tmp_bytes = 0;
-  zb_record_header* d_hdrs = nullptr;
-  uint8_t* d_out = nullptr;
-  int rc = ZB_OK;
-  auto cleanup = [&]() {
-    if (d_len) (void)hipFree(d_len);
-    if (d_off) (void)hipFree(d_off);
-    if (d_tmp) (void)hipFree(d_tmp);
-    if (d_hdrs) (void)hipFree(d_hdrs);
-    if (d_out) (void)hipFree(d_out);
-  };
   SerParams sp{};
   sp.log = e->log;
   sp.arena = e->arena;
@@ -1411,51 +1441,81 @@ int zb_drain(zb_engine* e, int64_t start, int64_t count, zb_record_header* heade
   sp.cmd_pool = e->d_cmd_pool.p;
   sp.start = start;
   sp.count = count;
-  do {
-    if (hipMalloc(&d_len, (count + 1) * sizeof(uint64_t)) != hipSuccess ||
-        hipMalloc(&d_off, (count + 1) * sizeof(uint64_t)) != hipSuccess) { rc = fail(e, ZB_ENOMEM, "drain buffers"); break; }
-    if (hipMemsetAsync(d_len, 0, (count + 1) * sizeof(uint64_t), e->stream) != hipSuccess) { rc = ZB_EDEVICE; break; }
-    sp.lengths = (uint32_t*)nullptr;
-    // size pass writes 32-bit lengths into the low half of a 64-bit array
-    SerParams sz = sp;
-    sz.lengths = (uint32_t*)d_off;  // scratch
-    launch_ser_size(sz, e->stream);
-    // widen to 64-bit for the scan: reuse a tiny conversion via hipcub TransformInputIterator
-    hipcub::TransformInputIterator<uint64_t, hipcub::CastOp<uint64_t>, const uint32_t*> it(
-        (const uint32_t*)d_off, hipcub::CastOp<uint64_t>());
-    if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, it, d_len, (int)count, e->stream) != hipSuccess) {
-      rc = fail(e, ZB_EDEVICE, "scan sizing");
-      break;
-    }
-    if (hipMalloc(&d_tmp, tmp_bytes + 16) != hipSuccess) { rc = fail(e, ZB_ENOMEM, "scan temp"); break; }
-    if (hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_bytes, it, d_len, (int)count, e->stream) != hipSuccess) {
-      rc = fail(e, ZB_EDEVICE, "scan");
-      break;
-    }
-    uint64_t last_off = 0;
-    uint32_t last_len = 0;
-    if (hipMemcpyAsync(&last_off, d_len + count - 1, 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
-        hipMemcpyAsync(&last_len, ((uint32_t*)d_off) + count - 1, 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
-        hipStreamSynchronize(e->stream) != hipSuccess) { rc = fail(e, ZB_EDEVICE, "drain size"); break; }
-    const uint64_t total = last_off + last_len;
-    if (values_len) *values_len = total;
-    if (!values || !headers || values_cap < total) { rc = ZB_ENOMEM; break; }
-    if (hipMalloc(&d_out, total + 1) != hipSuccess || hipMalloc(&d_hdrs, count * sizeof(zb_record_header)) != hipSuccess) {
-      rc = fail(e, ZB_ENOMEM, "drain output");
-      break;
-    }
-    SerParams wr = sp;
-    wr.offsets = d_len;
-    wr.out = d_out;
-    wr.headers = d_hdrs;
-    launch_ser_write(wr, e->stream);
-    if (hipMemcpyAsync(values, d_out, total, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
-        hipMemcpyAsync(headers, d_hdrs, count * sizeof(zb_record_header), hipMemcpyDeviceToHost, e->stream) !=
-            hipSuccess ||
-        hipStreamSynchronize(e->stream) != hipSuccess) { rc = fail(e, ZB_EDEVICE, "drain copy"); break; }
-  } while (0);
-  cleanup();
-  return rc;
+  sp.totals = e->dr_total;
+  HIPCHECK(e, hipMemsetAsync(e->dr_total, 0, 2 * sizeof(uint64_t), e->stream));
+  HIPCHECK(e, hipEventRecord(e->dr_ev[0], e->stream));
+  SerParams sz = sp;
+  sz.lengths64 = e->dr_len;  // count + 1 entries, the last one 0: the scan's last output is the total
+  launch_ser_size(sz, e->stream);
+  HIPCHECK(e, hipEventRecord(e->dr_ev[1], e->stream));
+  size_t tmp = e->dr_tmp_cap;
+  if (hipcub::DeviceScan::ExclusiveSum(e->dr_tmp, tmp, e->dr_len, e->dr_off, (int)(count + 1), e->stream) != hipSuccess)
+    return fail(e, ZB_EDEVICE, "drain scan");
+  HIPCHECK(e, hipEventRecord(e->dr_ev[2], e->stream));
+  HIPCHECK(e, hipMemcpyAsync(e->h_dr_total, e->dr_off + count, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  const uint64_t total = e->h_dr_total[0];
+  if (total + 8 > e->dr_val_cap) {
+    if (e->dr_val) (void)hipFree(e->dr_val);
+    e->dr_val = nullptr;
+    e->dr_val_cap = 0;
+    const uint64_t cap = total + total / 4 + (1 << 20);
+    HIPCHECK(e, hipMalloc(&e->dr_val, cap));
+    e->dr_val_cap = cap;
+  }
+  SerParams wr = sp;
+  wr.offsets = e->dr_off;
+  wr.out = e->dr_val;
+  wr.headers = e->dr_hdr;
+  HIPCHECK(e, hipEventRecord(e->dr_ev[2], e->stream));
+  launch_ser_write(wr, e->stream);
+  HIPCHECK(e, hipEventRecord(e->dr_ev[3], e->stream));
+  HIPCHECK(e, hipMemcpyAsync(e->h_dr_total + 1, e->dr_total + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  float ms_size = 0, ms_write = 0;
+  HIPCHECK(e, hipEventElapsedTime(&ms_size, e->dr_ev[0], e->dr_ev[1]));
+  HIPCHECK(e, hipEventElapsedTime(&ms_write, e->dr_ev[2], e->dr_ev[3]));
+  e->dr_count = count;
+  e->dr_bytes = total;
+  st.records = (uint64_t)count;
+  st.value_bytes = total;
+  st.payload_bytes = e->h_dr_total[1];
+  st.size_kernel_ms = ms_size;
+  st.write_kernel_ms = ms_write;
+  st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  st.scan_ms = st.wall_ms - ms_size - ms_write;  // scan + the one host sync for the output size
+  if (stats) *stats = st;
+  return ZB_OK;
+}
+
+int zb_drain_copy(zb_engine* e, zb_record_header* headers, uint8_t* values, uint64_t value_off, size_t values_len) {
+  if (!e || value_off > e->dr_bytes || values_len > e->dr_bytes - value_off || (values_len && !values)) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  if (headers && e->dr_count)
+    HIPCHECK(e, hipMemcpyAsync(headers, e->dr_hdr, e->dr_count * sizeof(zb_record_header), hipMemcpyDeviceToHost, e->stream));
+  if (values_len) HIPCHECK(e, hipMemcpyAsync(values, e->dr_val + value_off, values_len, hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  return ZB_OK;
+}
+
+void* zb_pinned_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1) != hipSuccess) return nullptr;
+  return p;
+}
+void zb_pinned_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
+int zb_drain(zb_engine* e, int64_t start, int64_t count, zb_record_header* headers, uint8_t* values,
+             size_t values_cap, size_t* values_len) {
+  zb_serialize_stats st{};
+  int rc = zb_serialize(e, start, count, &st);
+  if (rc != ZB_OK) return rc;
+  if (values_len) *values_len = st.value_bytes;
+  if (count == 0) return ZB_OK;
+  if (!values || !headers || values_cap < st.value_bytes) return ZB_ENOMEM;
+  return zb_drain_copy(e, headers, values, 0, st.value_bytes);
 }
 
 int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, const uint8_t* cks,

@@ -42,7 +42,18 @@ struct W : Out {
     if (n < 256) { put(0xc4); put((uint8_t)n); }
     else if (n < 65536) { put(0xc5); put((uint8_t)(n >> 8)); put((uint8_t)n); }
     else { put(0xc6); for (int i = 3; i >= 0; i--) put((uint8_t)(n >> (8 * i))); }
-    put_bytes(s, n);
+    if (dst && (((uintptr_t)s) & 3) == 0) {
+      // arena documents: 4-byte aligned and padded to 8, so whole-word loads never leave the blob
+      const uint32_t* w = (const uint32_t*)s;
+      for (uint32_t k = 0; k < n; k += 4) {
+        const uint32_t v = w[k >> 2];
+        const uint32_t m = n - k < 4 ? n - k : 4;
+        for (uint32_t b = 0; b < m; b++) dst[this->n + k + b] = (uint8_t)(v >> (8 * b));
+      }
+      this->n += n;
+    } else {
+      put_bytes(s, n);
+    }
   }
   __device__ inline void cstr(const char* s) {  // append raw chars (message text)
     while (*s) put((uint8_t)*s++);
@@ -236,8 +247,9 @@ __device__ inline void encode_value(const SerParams& P, int64_t pos, const zb_re
   }
 }
 
-__global__ void k_ser_size(SerParams P) {
+__global__ void __launch_bounds__(256) k_ser_size(SerParams P) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (P.lengths64 && i == P.count) P.lengths64[i] = 0;  // the scan over count + 1 entries ends in the total
   if (i >= P.count) return;
   const int64_t pos = P.start + i;
   const zb_rec d = P.log[pos];
@@ -245,42 +257,88 @@ __global__ void k_ser_size(SerParams P) {
   w.dst = nullptr;
   w.n = 0;
   encode_value(P, pos, d, w);
-  P.lengths[i] = w.n;
+  if (P.lengths64) P.lengths64[i] = w.n;
+  else P.lengths[i] = w.n;
 }
 
-__global__ void k_ser_write(SerParams P) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P.count) return;
-  const int64_t pos = P.start + i;
-  const zb_rec d = P.log[pos];
-  W w;
-  w.dst = P.out + P.offsets[i];
-  w.n = 0;
-  encode_value(P, pos, d, w);
-  zb_record_header h;
-  h.position = pos;
-  h.source_position = -1;
-  h.key = d.key;
-  h.record_type = kind_rt(d.kind);
-  h.value_type = kind_vt(d.kind);
-  h.intent = d.intent;
-  // RejectionType: CREATE of an unknown workflow -> BAD_VALUE (0); CORRELATE of an absent activity ->
-  // NOT_APPLICABLE (1) (WorkflowInstanceStreamProcessor.java:477-479)
-  // CANCEL / UPDATE_PAYLOAD of an instance that is not running -> NOT_APPLICABLE (1) (:524-529, :571-573)
-  h.rejection_type = kind_rt(d.kind) == ZB_RT_COMMAND_REJECTION
-                         ? ((kind_vt(d.kind) == ZB_VT_WORKFLOW_INSTANCE && d.intent == WI_CREATE) ? 0 : 1) : 255;
-  h.value_length = w.n;
-  h.value_offset = P.offsets[i];
-  P.headers[i] = h;
+// Write pass. Record i's value goes to out[offsets[i], offsets[i + 1]); the workgroup's records are one
+// contiguous output range, so each thread encodes its value into an LDS image of that range (byte
+// stores stay on chip) and the workgroup then streams the image out with 16-byte stores, aligned to
+// the destination. A range larger than the image (large payloads) is encoded straight to HBM instead.
+constexpr int SER_WG = 256;
+constexpr int SER_IMG = 48 * 1024;  // three workgroups per CU
+
+__global__ void __launch_bounds__(SER_WG) k_ser_write(SerParams P) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[SER_IMG + 16];
+  __shared__ unsigned long long s_pay[SER_WG / 64];
+  const int64_t base = (int64_t)blockIdx.x * SER_WG;
+  const int64_t i = base + threadIdx.x;
+  const int64_t last = (base + SER_WG < P.count) ? base + SER_WG : P.count;
+  const uint64_t o0 = P.offsets[base], o1 = P.offsets[last];
+  const uint32_t shift = (uint32_t)(((uintptr_t)(P.out + o0)) & 15);
+  const bool staged = (o1 - o0) + shift <= (uint64_t)SER_IMG;
+  uint32_t pay = 0;
+  if (i < P.count) {
+    const int64_t pos = P.start + i;
+    const zb_rec d = P.log[pos];
+    const uint64_t off = P.offsets[i];
+    W w;
+    w.dst = staged ? img + shift + (off - o0) : P.out + off;
+    w.n = 0;
+    encode_value(P, pos, d, w);
+    if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay = *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
+    zb_record_header h;
+    h.position = pos;
+    h.source_position = -1;
+    h.key = d.key;
+    h.record_type = kind_rt(d.kind);
+    h.value_type = kind_vt(d.kind);
+    h.intent = d.intent;
+    // RejectionType: CREATE of an unknown workflow -> BAD_VALUE (0); CORRELATE of an absent activity, CANCEL /
+    // UPDATE_PAYLOAD of an instance that is not running -> NOT_APPLICABLE (1) (WorkflowInstanceStreamProcessor.java
+    // :477-479, :524-529, :571-573)
+    h.rejection_type = kind_rt(d.kind) == ZB_RT_COMMAND_REJECTION
+                           ? ((kind_vt(d.kind) == ZB_VT_WORKFLOW_INSTANCE && d.intent == WI_CREATE) ? 0 : 1) : 255;
+    h.value_length = w.n;
+    h.value_offset = off;
+    P.headers[i] = h;
+  }
+  if (P.totals) {
+    unsigned long long x = pay;
+    for (int dd = 32; dd >= 1; dd >>= 1) x += __shfl_down(x, dd, 64);
+    if ((threadIdx.x & 63) == 0) s_pay[threadIdx.x >> 6] = x;
+  }
+  __syncthreads();
+  if (P.totals && threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int k = 0; k < SER_WG / 64; k++) t += s_pay[k];
+    if (t) atomicAdd((unsigned long long*)&P.totals[1], t);
+  }
+  if (!staged) return;
+  // stream the image out: img[shift + k] -> out[o0 + k], k in [0, n); out + o0 - shift is 16-byte aligned
+  const uint64_t n = o1 - o0;
+  uint8_t* dst = P.out + o0 - shift;
+  const uint64_t lim = shift + n;  // image bytes [shift, lim) are ours
+  const uint64_t full_lo = (shift + 15) & ~15ull, full_hi = lim & ~15ull;
+  if (full_lo < full_hi) {
+    for (uint64_t c = full_lo + 16 * threadIdx.x; c < full_hi; c += 16 * SER_WG)
+      *(uint4*)(dst + c) = *(const uint4*)(img + c);
+  }
+  // partial head / tail bytes
+  const uint64_t head_end = full_lo < lim ? full_lo : lim;
+  for (uint64_t c = shift + threadIdx.x; c < head_end; c += SER_WG) dst[c] = img[c];
+  const uint64_t tail_lo = full_hi > head_end ? full_hi : head_end;
+  for (uint64_t c = tail_lo + threadIdx.x; c < lim; c += SER_WG) dst[c] = img[c];
 }
 
 void launch_ser_size(const SerParams& p, hipStream_t s) {
   if (p.count <= 0) return;
-  hipLaunchKernelGGL(k_ser_size, dim3((unsigned)((p.count + 255) / 256)), dim3(256), 0, s, p);
+  const int64_t work = p.count + (p.lengths64 ? 1 : 0);
+  hipLaunchKernelGGL(k_ser_size, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, p);
 }
 void launch_ser_write(const SerParams& p, hipStream_t s) {
   if (p.count <= 0) return;
-  hipLaunchKernelGGL(k_ser_write, dim3((unsigned)((p.count + 255) / 256)), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(k_ser_write, dim3((unsigned)((p.count + SER_WG - 1) / SER_WG)), dim3(SER_WG), 0, s, p);
 }
 
 // ------------------------------------------------------------------------------ input injection

@@ -68,6 +68,15 @@ class zb_step_stats(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class zb_serialize_stats(ctypes.Structure):
+    _fields_ = [("records", ctypes.c_uint64), ("value_bytes", ctypes.c_uint64), ("payload_bytes", ctypes.c_uint64),
+                ("size_kernel_ms", ctypes.c_double), ("scan_ms", ctypes.c_double),
+                ("write_kernel_ms", ctypes.c_double), ("wall_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class Record(NamedTuple):
     position: int
     source_position: int
@@ -121,6 +130,11 @@ def lib():
         szp = ctypes.POINTER(ctypes.c_size_t)
         L.zb_submit.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
         L.zb_validate_deployment.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
+        L.zb_serialize.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(zb_serialize_stats)]
+        L.zb_drain_copy.argtypes = [vp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t]
+        L.zb_pinned_alloc.restype = ctypes.c_void_p
+        L.zb_pinned_alloc.argtypes = [ctypes.c_size_t]
+        L.zb_pinned_free.argtypes = [ctypes.c_void_p]
         L.zb_read_instances.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t, szp, u64p]
         L.zb_snapshot.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t, szp]
         L.zb_restore.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t]
@@ -133,7 +147,7 @@ EXPORTED_SYMBOLS = ["zb_engine_create", "zb_engine_destroy", "zb_last_error", "z
                     "zb_read_descriptors", "zb_drain", "zb_counters", "zb_submit_publishes", "zb_inbox_submit",
                     "zb_outbox_count", "zb_outbox_take", "zb_comm_unique_id", "zb_comm_init", "zb_comm_pending",
                     "zb_comm_exchange", "zb_submit", "zb_read_instances", "zb_snapshot", "zb_restore",
-                    "zb_validate_deployment"]
+                    "zb_validate_deployment", "zb_serialize", "zb_drain_copy", "zb_pinned_alloc", "zb_pinned_free"]
 
 
 def validate_deployment(xml):
@@ -271,6 +285,16 @@ class Engine:
         d["quiescent"] = rc == ZB_OK
         return d
 
+    def serialize(self, start: int, count: int) -> dict:
+        """zb_serialize: records [start, start+count) -> the engine's device-resident drain buffers."""
+        st = zb_serialize_stats()
+        self._check(self._L.zb_serialize(self._h, start, count, ctypes.byref(st)))
+        return st.as_dict()
+
+    def drain_copy(self, dst_ptr: int, value_off: int, nbytes: int, headers_ptr=None):
+        """zb_drain_copy into caller memory (an address, e.g. from pinned_alloc)."""
+        self._check(self._L.zb_drain_copy(self._h, headers_ptr, dst_ptr, value_off, nbytes))
+
     def log_size(self) -> int:
         return self._L.zb_log_size(self._h)
 
@@ -383,3 +407,14 @@ class Engine:
         self._check(self._L.zb_counters(self._h, arr))
         return dict(created=arr[0], completed=arr[1], canceled=arr[2], next_wf_key=arr[3], next_job_key=arr[4],
                     rows=arr[5], arena_bytes=arr[6], log_size=arr[7])
+
+
+def pinned_alloc(nbytes: int) -> int:
+    p = lib().zb_pinned_alloc(nbytes)
+    if not p:
+        raise MemoryError("zb_pinned_alloc(%d) failed" % nbytes)
+    return p
+
+
+def pinned_free(p: int):
+    lib().zb_pinned_free(p)

@@ -78,6 +78,67 @@ def xor_payloads(n: int, seed: int = 42, start: int = 0) -> Tuple[bytes, np.ndar
     return b"".join(parts), offs
 
 
+def xor_payloads_np(n: int, seed: int = 42, start: int = 0) -> Tuple[bytes, np.ndarray]:
+    """xor_payloads, vectorized (same bytes): rows of at most 48 bytes assembled column-wise, then packed."""
+    g = np.random.Generator(np.random.Philox(key=seed))
+    if start:
+        g.bit_generator.advance(start)
+    amount = g.integers(0, 2000, size=n)
+    region = g.integers(0, 3, size=n)
+    score = g.random(size=n)
+    W = 48
+    buf = np.zeros((n, W), dtype=np.uint8)
+    ln = np.zeros(n, dtype=np.int64)
+
+    def put_const(b: bytes):
+        a = np.frombuffer(b, dtype=np.uint8)
+        cols = ln[:, None] + np.arange(len(a))[None, :]
+        buf[np.arange(n)[:, None], cols] = a[None, :]
+        ln[:] += len(a)
+
+    def put_rows(vals: np.ndarray, width: np.ndarray):
+        # vals: (n, k) bytes, width: per-row count used
+        k = vals.shape[1]
+        rows = np.repeat(np.arange(n), k)
+        cols = (ln[:, None] + np.arange(k)[None, :]).ravel()
+        keep = (np.arange(k)[None, :] < width[:, None]).ravel()
+        buf[rows[keep], cols[keep]] = vals.ravel()[keep]
+        ln[:] += width
+
+    put_const(b"\x83" + mp_str("amount"))
+    # mp_int for 0 <= a < 2000: fixint (<128), 0xcc uint8 (<256), 0xcd uint16
+    a = amount.astype(np.int64)
+    v = np.zeros((n, 3), dtype=np.uint8)
+    w = np.where(a < 128, 1, np.where(a < 256, 2, 3))
+    v[:, 0] = np.where(a < 128, a, np.where(a < 256, 0xcc, 0xcd))
+    v[:, 1] = np.where(a < 256, a & 0xff, a >> 8)
+    v[:, 2] = a & 0xff
+    put_rows(v, w)
+    put_const(mp_str("region"))
+    regs = [mp_str(r) for r in REGIONS]
+    rv = np.zeros((n, max(len(r) for r in regs)), dtype=np.uint8)
+    rw = np.zeros(n, dtype=np.int64)
+    for k, r in enumerate(regs):
+        m = region == k
+        rv[m, :len(r)] = np.frombuffer(r, dtype=np.uint8)
+        rw[m] = len(r)
+    put_rows(rv, rw)
+    put_const(mp_str("score"))
+    f32 = score.astype(np.float32)
+    exact = f32.astype(np.float64) == score
+    sv = np.zeros((n, 9), dtype=np.uint8)
+    sv[:, 0] = np.where(exact, 0xca, 0xcb)
+    b32 = f32.astype(">f4").view(np.uint8).reshape(n, 4)
+    b64 = score.astype(">f8").view(np.uint8).reshape(n, 8)
+    sv[:, 1:9] = b64
+    sv[exact, 1:5] = b32[exact]
+    put_rows(sv, np.where(exact, 5, 9))
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(ln, dtype=np.uint64)
+    mask = np.arange(W)[None, :] < ln[:, None]
+    return buf[mask].tobytes(), offs
+
+
 def split(blob: bytes, offs: np.ndarray) -> List[bytes]:
     o = offs.tolist()
     return [blob[o[i]:o[i + 1]] for i in range(len(o) - 1)]
