@@ -198,6 +198,7 @@ struct zb_engine {
   uint64_t* h_dr_total = nullptr; // pinned mirror
   int64_t dr_count = 0;           // records of the batch in the drain buffers
   uint64_t dr_bytes = 0;
+  uint64_t dr_epoch = 0;          // look-back tags of the single-pass serializer
   hipEvent_t dr_ev[4] = {nullptr, nullptr, nullptr, nullptr};
 
   // timing
@@ -656,7 +657,7 @@ void zb_engine_destroy(zb_engine* e) {
   e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_consts.free();
   e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
   e->d_ranges.free(); e->d_cmd_pool.free(); e->d_lookup_keys.free(); e->d_lookup_pos.free();
-  void* dr[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_val, e->dr_tmp, e->dr_total};
+  void* dr[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_val, e->dr_tmp, e->dr_total};  // dr_len: tile states
   for (void* p : dr)
     if (p) (void)hipFree(p);
   if (e->h_dr_total) (void)hipHostFree(e->h_dr_total);
@@ -1275,8 +1276,9 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     launch_inject(ip, e->stream);
     // records naming an element instance by key: its row (ElementInstanceIndex.getInstance)
     std::vector<std::pair<int64_t, int64_t>> look;
-    for (int64_t i = 0; i < n; i++)
-      if (e->staged_lookup[i] != INT64_MIN) look.emplace_back(e->staged_lookup[i], ip.log_base + i);
+    if (!e->staged_only_creates)  // (CREATE-only batches name no element instance: skip the scan)
+      for (int64_t i = 0; i < n; i++)
+        if (e->staged_lookup[i] != INT64_MIN) look.emplace_back(e->staged_lookup[i], ip.log_base + i);
     if (!look.empty()) {
       std::sort(look.begin(), look.end());
       std::vector<int64_t> lk(look.size()), lp(look.size());
@@ -1406,27 +1408,25 @@ int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats*
   if (!e->dr_ev[0])
     for (auto& x : e->dr_ev) HIPCHECK(e, hipEventCreate(&x));
   if (!e->dr_total) {
-    HIPCHECK(e, hipMalloc(&e->dr_total, 2 * sizeof(uint64_t)));
-    HIPCHECK(e, hipHostMalloc(&e->h_dr_total, 2 * sizeof(uint64_t)));
+    HIPCHECK(e, hipMalloc(&e->dr_total, 4 * sizeof(uint64_t)));  // [0] bytes [1] payload bytes [2] ctr|overflow
+    HIPCHECK(e, hipHostMalloc(&e->h_dr_total, 4 * sizeof(uint64_t)));
   }
+  const uint64_t tiles = ((uint64_t)count + 255) / 256;
   if ((uint64_t)count > e->dr_cap) {
-    void* ps[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_tmp};
-    for (void* q : ps)
-      if (q) (void)hipFree(q);
-    e->dr_len = e->dr_off = nullptr; e->dr_hdr = nullptr; e->dr_tmp = nullptr; e->dr_cap = e->dr_tmp_cap = 0;
+    if (e->dr_hdr) (void)hipFree(e->dr_hdr);
+    if (e->dr_len) (void)hipFree(e->dr_len);
+    e->dr_hdr = nullptr; e->dr_len = nullptr; e->dr_cap = 0;
     const uint64_t cap = (uint64_t)count + (uint64_t)count / 4 + 1024;
-    HIPCHECK(e, hipMalloc(&e->dr_len, (cap + 1) * sizeof(uint64_t)));
-    HIPCHECK(e, hipMalloc(&e->dr_off, (cap + 1) * sizeof(uint64_t)));
     HIPCHECK(e, hipMalloc(&e->dr_hdr, cap * sizeof(zb_record_header)));
-    size_t tmp = 0;
-    if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->dr_len, e->dr_off, (int)std::min<uint64_t>(cap + 1, INT32_MAX),
-                                         e->stream) != hipSuccess)
-      return fail(e, ZB_EDEVICE, "scan sizing");
-    HIPCHECK(e, hipMalloc(&e->dr_tmp, tmp + 16));
-    e->dr_tmp_cap = tmp;
+    HIPCHECK(e, hipMalloc(&e->dr_len, (cap / 256 + 2) * sizeof(uint64_t)));  // tile states
+    HIPCHECK(e, hipMemset(e->dr_len, 0, (cap / 256 + 2) * sizeof(uint64_t)));
     e->dr_cap = cap;
   }
-  if ((uint64_t)count + 1 > (uint64_t)INT32_MAX) return fail(e, ZB_EUNSUPPORTED, "more than 2^31 records in one drain");
+  if (e->dr_val_cap == 0) {  // first estimate; grown from the exact total if it overflows
+    const uint64_t cap = (uint64_t)count * 200 + (64ull << 20);
+    HIPCHECK(e, hipMalloc(&e->dr_val, cap));
+    e->dr_val_cap = cap;
+  }
   HIPCHECK(e, e->d_ranges.upload(e->ranges, e->stream));
   HIPCHECK(e, e->d_cmd_pool.upload(e->cmd_pool, e->stream));
   SerParams sp{};
@@ -1442,48 +1442,47 @@ int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats*
   sp.start = start;
   sp.count = count;
   sp.totals = e->dr_total;
-  HIPCHECK(e, hipMemsetAsync(e->dr_total, 0, 2 * sizeof(uint64_t), e->stream));
-  HIPCHECK(e, hipEventRecord(e->dr_ev[0], e->stream));
-  SerParams sz = sp;
-  sz.lengths64 = e->dr_len;  // count + 1 entries, the last one 0: the scan's last output is the total
-  launch_ser_size(sz, e->stream);
-  HIPCHECK(e, hipEventRecord(e->dr_ev[1], e->stream));
-  size_t tmp = e->dr_tmp_cap;
-  if (hipcub::DeviceScan::ExclusiveSum(e->dr_tmp, tmp, e->dr_len, e->dr_off, (int)(count + 1), e->stream) != hipSuccess)
-    return fail(e, ZB_EDEVICE, "drain scan");
-  HIPCHECK(e, hipEventRecord(e->dr_ev[2], e->stream));
-  HIPCHECK(e, hipMemcpyAsync(e->h_dr_total, e->dr_off + count, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
-  HIPCHECK(e, hipStreamSynchronize(e->stream));
-  const uint64_t total = e->h_dr_total[0];
-  if (total + 8 > e->dr_val_cap) {
-    if (e->dr_val) (void)hipFree(e->dr_val);
+  sp.tile_state = e->dr_len;
+  sp.tile_ctr = (uint32_t*)(e->dr_total + 2);
+  sp.overflow = (uint32_t*)(e->dr_total + 2) + 1;
+  sp.headers = e->dr_hdr;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    if ((++e->dr_epoch & 0x3ffff) == 0) {  // tile-state tags wrap: clear them once
+      HIPCHECK(e, hipMemsetAsync(e->dr_len, 0, (e->dr_cap / 256 + 2) * sizeof(uint64_t), e->stream));
+      ++e->dr_epoch;
+    }
+    sp.epoch = (uint32_t)e->dr_epoch;
+    sp.out = e->dr_val;
+    sp.out_cap = e->dr_val_cap;
+    HIPCHECK(e, hipMemsetAsync(e->dr_total, 0, 4 * sizeof(uint64_t), e->stream));
+    HIPCHECK(e, hipEventRecord(e->dr_ev[0], e->stream));
+    launch_ser_fused(sp, e->stream);
+    HIPCHECK(e, hipEventRecord(e->dr_ev[1], e->stream));
+    HIPCHECK(e, hipMemcpyAsync(e->h_dr_total, e->dr_total, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHECK(e, hipStreamSynchronize(e->stream));
+    HIPCHECK(e, hipGetLastError());
+    const uint32_t overflow = ((const uint32_t*)(e->h_dr_total + 2))[1];
+    if (!overflow) break;
+    if (attempt == 1) return fail(e, ZB_EDEVICE, "drain buffer overflow after growing it");
+    (void)hipFree(e->dr_val);
     e->dr_val = nullptr;
     e->dr_val_cap = 0;
-    const uint64_t cap = total + total / 4 + (1 << 20);
+    const uint64_t cap = e->h_dr_total[0] + e->h_dr_total[0] / 4 + (64ull << 20);
     HIPCHECK(e, hipMalloc(&e->dr_val, cap));
     e->dr_val_cap = cap;
   }
-  SerParams wr = sp;
-  wr.offsets = e->dr_off;
-  wr.out = e->dr_val;
-  wr.headers = e->dr_hdr;
-  HIPCHECK(e, hipEventRecord(e->dr_ev[2], e->stream));
-  launch_ser_write(wr, e->stream);
-  HIPCHECK(e, hipEventRecord(e->dr_ev[3], e->stream));
-  HIPCHECK(e, hipMemcpyAsync(e->h_dr_total + 1, e->dr_total + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
-  HIPCHECK(e, hipStreamSynchronize(e->stream));
-  float ms_size = 0, ms_write = 0;
-  HIPCHECK(e, hipEventElapsedTime(&ms_size, e->dr_ev[0], e->dr_ev[1]));
-  HIPCHECK(e, hipEventElapsedTime(&ms_write, e->dr_ev[2], e->dr_ev[3]));
+  (void)tiles;
+  float ms_write = 0;
+  HIPCHECK(e, hipEventElapsedTime(&ms_write, e->dr_ev[0], e->dr_ev[1]));
   e->dr_count = count;
-  e->dr_bytes = total;
+  e->dr_bytes = e->h_dr_total[0];
   st.records = (uint64_t)count;
-  st.value_bytes = total;
+  st.value_bytes = e->h_dr_total[0];
   st.payload_bytes = e->h_dr_total[1];
-  st.size_kernel_ms = ms_size;
+  st.size_kernel_ms = 0;  // sizes, offsets and values in one pass (k_ser_fused)
   st.write_kernel_ms = ms_write;
   st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  st.scan_ms = st.wall_ms - ms_size - ms_write;  // scan + the one host sync for the output size
+  st.scan_ms = 0;
   if (stats) *stats = st;
   return ZB_OK;
 }

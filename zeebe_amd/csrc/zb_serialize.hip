@@ -331,6 +331,150 @@ __global__ void __launch_bounds__(SER_WG) k_ser_write(SerParams P) {
   for (uint64_t c = tail_lo + threadIdx.x; c < lim; c += SER_WG) dst[c] = img[c];
 }
 
+// ------------------------------------------------------------------------------ single pass (zb_serialize)
+// Size, offset and write in one launch: each 256-record tile sizes its values, scans them in LDS, gets
+// its byte offset from its predecessors by decoupled look-back (tile ids in launch order from an atomic
+// counter, so a tile only waits for tiles already running; status words are 8-byte agent-scope atomics
+// on both sides, MI355X_MICROARCH.md "Valid forms"), then encodes into the LDS image and streams it out.
+constexpr uint64_t TS_AGG = 1ull << 62, TS_INC = 2ull << 62, TS_VAL = (1ull << 44) - 1;
+
+__device__ __forceinline__ uint64_t ts_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ts_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(SER_WG) k_ser_fused(SerParams P) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[SER_IMG + 16];
+  __shared__ uint64_t s_wsum[SER_WG / 64];
+  __shared__ unsigned long long s_pay[SER_WG / 64];
+  __shared__ uint32_t s_tile;
+  __shared__ uint64_t s_base;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_tile = atomicAdd(P.tile_ctr, 1u);
+  __syncthreads();
+  const uint32_t t = s_tile;
+  const int64_t base = (int64_t)t * SER_WG;
+  const int64_t i = base + threadIdx.x;
+  zb_rec d{};
+  uint32_t len = 0;
+  if (i < P.count) {
+    d = P.log[P.start + i];
+    W w;
+    w.dst = nullptr;
+    w.n = 0;
+    encode_value(P, P.start + i, d, w);
+    len = w.n;
+  }
+  // block exclusive scan of the lengths
+  uint64_t x = len;
+#pragma unroll
+  for (int k = 1; k < 64; k <<= 1) {
+    const uint64_t y = (uint64_t)__shfl_up((unsigned long long)x, k, 64);
+    if (lane >= k) x += y;
+  }
+  if (lane == 63) s_wsum[wv] = x;
+  __syncthreads();
+  uint64_t pre = 0, agg = 0;
+#pragma unroll
+  for (int k = 0; k < SER_WG / 64; k++) {
+    if (k < wv) pre += s_wsum[k];
+    agg += s_wsum[k];
+  }
+  const uint64_t lo = pre + x - len;  // offset inside the tile
+  const uint64_t tag = (uint64_t)(P.epoch & 0x3ffff) << 44;
+  if (wv == 0) {  // decoupled look-back by the first wave
+    uint64_t excl = 0;
+    if (t == 0) {
+      if (lane == 0) ts_store(P.tile_state, TS_INC | tag | agg);
+    } else {
+      if (lane == 0) ts_store(P.tile_state + t, TS_AGG | tag | agg);
+      int64_t p = (int64_t)t - 1;
+      for (;;) {
+        const int64_t q = p - lane;
+        uint64_t v = 0;
+        bool inc = true;
+        if (q >= 0) {
+          uint64_t wd;
+          do { wd = ts_load(P.tile_state + q); } while ((wd & ~(3ull << 62)) >> 44 != (tag >> 44) || !(wd >> 62));
+          inc = (wd >> 62) == 2;
+          v = wd & TS_VAL;
+        }
+        const uint64_t m = __ballot(inc);
+        const int first = m ? __ffsll((unsigned long long)m) - 1 : 64;
+        uint64_t s = lane <= first ? v : 0;
+#pragma unroll
+        for (int k = 32; k >= 1; k >>= 1) s += (uint64_t)__shfl_xor((unsigned long long)s, k, 64);
+        excl += s;
+        if (first < 64) break;
+        p -= 64;
+      }
+      if (lane == 0) ts_store(P.tile_state + t, TS_INC | tag | (excl + agg));
+    }
+    if (lane == 0) {
+      s_base = excl;
+      if ((int64_t)(base + SER_WG) >= P.count && P.totals) P.totals[0] = excl + agg;  // the last tile
+    }
+  }
+  __syncthreads();
+  const uint64_t o0 = s_base;
+  if (o0 + agg > P.out_cap) {  // does not fit: the host grows the buffer and runs the pass again
+    if (threadIdx.x == 0) atomicOr(P.overflow, 1u);
+    return;
+  }
+  const uint32_t shift = (uint32_t)(((uintptr_t)(P.out + o0)) & 15);
+  const bool staged = agg + shift <= (uint64_t)SER_IMG;
+  uint32_t pay = 0;
+  if (i < P.count) {
+    const int64_t pos = P.start + i;
+    const uint64_t off = o0 + lo;
+    W w;
+    w.dst = staged ? img + shift + lo : P.out + off;
+    w.n = 0;
+    encode_value(P, pos, d, w);
+    if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay = *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
+    zb_record_header h;
+    h.position = pos;
+    h.source_position = -1;
+    h.key = d.key;
+    h.record_type = kind_rt(d.kind);
+    h.value_type = kind_vt(d.kind);
+    h.intent = d.intent;
+    h.rejection_type = kind_rt(d.kind) == ZB_RT_COMMAND_REJECTION
+                           ? ((kind_vt(d.kind) == ZB_VT_WORKFLOW_INSTANCE && d.intent == WI_CREATE) ? 0 : 1) : 255;
+    h.value_length = len;
+    h.value_offset = off;
+    P.headers[i] = h;
+  }
+  if (P.totals) {
+    unsigned long long y = pay;
+    for (int dd = 32; dd >= 1; dd >>= 1) y += __shfl_down(y, dd, 64);
+    if (lane == 0) s_pay[wv] = y;
+  }
+  __syncthreads();
+  if (P.totals && threadIdx.x == 0) {
+    unsigned long long tt = 0;
+    for (int k = 0; k < SER_WG / 64; k++) tt += s_pay[k];
+    if (tt) atomicAdd((unsigned long long*)&P.totals[1], tt);
+  }
+  if (!staged) return;
+  uint8_t* dst = P.out + o0 - shift;
+  const uint64_t lim = shift + agg;
+  const uint64_t full_lo = (shift + 15) & ~15ull, full_hi = lim & ~15ull;
+  for (uint64_t c = full_lo + 16 * threadIdx.x; c < full_hi; c += 16 * SER_WG)
+    *(uint4*)(dst + c) = *(const uint4*)(img + c);
+  const uint64_t head_end = full_lo < lim ? full_lo : lim;
+  for (uint64_t c = shift + threadIdx.x; c < head_end; c += SER_WG) dst[c] = img[c];
+  const uint64_t tail_lo = full_hi > head_end ? full_hi : head_end;
+  for (uint64_t c = tail_lo + threadIdx.x; c < lim; c += SER_WG) dst[c] = img[c];
+}
+
+void launch_ser_fused(const SerParams& p, hipStream_t s) {
+  if (p.count <= 0) return;
+  hipLaunchKernelGGL(k_ser_fused, dim3((unsigned)((p.count + SER_WG - 1) / SER_WG)), dim3(SER_WG), 0, s, p);
+}
+
 void launch_ser_size(const SerParams& p, hipStream_t s) {
   if (p.count <= 0) return;
   const int64_t work = p.count + (p.lengths64 ? 1 : 0);
