@@ -267,7 +267,8 @@ def roofline(tot, steps, cfg, n):
         # per launch: every drained record's descriptor read + header write, its value bytes written and the
         # payload documents copied into them read (SURVEY §8d payload term)
         b = (tot["drained"] * (DESC_BYTES + HDR_BYTES) + tot["value_bytes"] + tot["payload_bytes"]) / steps
-        cands.append(("zbg::k_ser_write", tot["ser_write_ms"] / steps, b,
+        kname = "zbg::k_ser_write" if tot["ser_size_ms"] > 0 else "zbg::k_ser_fused"  # two-pass / single-pass
+        cands.append((kname, tot["ser_write_ms"] / steps, b,
                       "32 B descriptor read + 40 B header write per drained record + value bytes written + payload "
                       "bytes read"))
     if tot["main_ms"] > 0:

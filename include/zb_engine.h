@@ -251,9 +251,9 @@ typedef struct zb_serialize_stats {
   uint64_t records;
   uint64_t value_bytes;        /* serialized record values */
   uint64_t payload_bytes;      /* payload documents copied into them (msgpack bin) */
-  double size_kernel_ms;       /* size pass */
-  double scan_ms;              /* exclusive scan of the sizes */
-  double write_kernel_ms;      /* write pass (headers + values): the drain's dominant kernel */
+  double size_kernel_ms;       /* size pass (0: sizes, offsets and values in one pass) */
+  double scan_ms;              /* exclusive scan of the sizes (0 in the single-pass serializer) */
+  double write_kernel_ms;      /* write pass (headers + values; the whole single pass): the drain's kernel */
   double wall_ms;
 } zb_serialize_stats;
 int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats* stats);

@@ -83,10 +83,12 @@ def _c3_expected_end(n):
     region = g.integers(0, 3, size=n)
     score = g.random(size=n)
     # json-el compares the msgpack values: score travels as float32 when exactly representable, else float64,
-    # and either way compares as the double it denotes
+    # and either way compares as the double it denotes. g1's conditioned flows are tried in the order the
+    # transformer collects them (ExclusiveSplitHandler.java:38-71 over ExecutableExclusiveGateway's outgoing
+    # list): f2 ($.score >= 0.5) before f1, so an instance satisfying both takes endB (the oracle's order).
     eu = region == 0
     a_branch = (amount < 1000) & eu
-    end = np.where(a_branch, np.where(amount < 100, 0, 1), np.where(score >= 0.5, 2, 3))
+    end = np.where(score >= 0.5, 2, np.where(a_branch, np.where(amount < 100, 0, 1), 3))
     return end  # 0 endA1, 1 endA2, 2 endB, 3 endC
 
 

@@ -289,6 +289,14 @@ WaveParams wave_params(zb_engine* e) {
   p.term = e->term ? 1 : 0;
   p.epoch = e->epoch;
   p.need_children = e->need_children;
+  // one 256-record tile per workgroup for the generation last seen by the host (x2 headroom for a generation
+  // that grows inside the batch; a larger one is still covered, with several tiles per workgroup)
+  {
+    const int64_t gen = std::max<int64_t>(e->host_hdr.gen_end - e->host_hdr.begin, e->host_hdr.end - e->host_hdr.begin);
+    const int64_t chunk = std::min<int64_t>(gen, (int64_t)e->wave_cap);
+    const int64_t g = 2 * ((chunk + WAVE_TILE - 1) / WAVE_TILE);
+    p.grid = (int32_t)std::max<int64_t>(256, std::min<int64_t>(g, WAVE_GRID_MAX));
+  }
   return p;
 }
 
@@ -599,8 +607,8 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->cw, e->wave_cap * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->stage, e->wave_cap * 2 * sizeof(Slot)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->info, e->wave_cap * sizeof(ItemInfo)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipMalloc(&e->block_agg, WAVE_GRID * sizeof(BlockAgg)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipMalloc(&e->block_off, WAVE_GRID * sizeof(BlockOff)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->block_agg, WAVE_GRID_MAX * sizeof(BlockAgg)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->block_off, WAVE_GRID_MAX * sizeof(BlockOff)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->derr, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->dstats, 8 * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->derr_info, sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);

@@ -640,7 +640,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
   int64_t t0, t1;
   block_tiles(c, t0, t1);
   // this thread's totals over the workgroup's tiles: packed 16-bit fields (<= 2 per record per tile, and
-  // a workgroup owns at most wave_cap / WG / WAVE_GRID tiles), bytes separately
+  // a workgroup owns at most wave_cap / WG / grid tiles), bytes separately
   uint64_t acc_a = 0;  // rec | wf << 16 | job << 32 | row << 48
   uint64_t acc_b = 0;  // merges | conds << 16 | transitions << 32 | completed << 48
   uint64_t acc_bytes = 0;
@@ -820,7 +820,12 @@ __global__ void __launch_bounds__(256) k_children(WaveParams P) {
 
 // ------------------------------------------------------------------------------ k_scan
 constexpr int SCAN_WG = 1024;
-constexpr int SCAN_PER = WAVE_GRID / SCAN_WG;  // workgroup aggregates per scan thread
+
+__device__ __forceinline__ void agg_fields(const BlockAgg& g, uint64_t* x) {
+  x[0] += g.rec; x[1] += g.wf; x[2] += g.job; x[3] += g.row; x[4] += g.bytes;
+  x[5] += g.merges; x[6] += g.conds; x[7] += g.transitions; x[8] += g.completed;
+  x[9] += g.created; x[10] += g.canceled;
+}
 
 __global__ void __launch_bounds__(SCAN_WG) k_scan(WaveParams P) {
   __shared__ uint64_t s_w[SCAN_WG / 64][11];
@@ -828,19 +833,13 @@ __global__ void __launch_bounds__(SCAN_WG) k_scan(WaveParams P) {
   WaveHdr* hout = P.hdr + ((P.wave + 1) & 1);
   const Chunk c = wave_chunk(P, hin);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // workgroup aggregates [k0, k1) per scan thread
+  const int per = (P.grid + SCAN_WG - 1) / SCAN_WG;
+  const int k0 = threadIdx.x * per, k1 = k0 + per < P.grid ? k0 + per : P.grid;
   // fields: rec wf job row bytes merges conds | transitions completed created canceled (reduced only)
-  BlockAgg g[SCAN_PER];
   uint64_t x[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  if (c.n > 0) {
-#pragma unroll
-    for (int k = 0; k < SCAN_PER; k++) g[k] = P.block_agg[threadIdx.x * SCAN_PER + k];
-#pragma unroll
-    for (int k = 0; k < SCAN_PER; k++) {
-      x[0] += g[k].rec; x[1] += g[k].wf; x[2] += g[k].job; x[3] += g[k].row; x[4] += g[k].bytes;
-      x[5] += g[k].merges; x[6] += g[k].conds; x[7] += g[k].transitions; x[8] += g[k].completed;
-      x[9] += g[k].created; x[10] += g[k].canceled;
-    }
-  }
+  if (c.n > 0)
+    for (int k = k0; k < k1; k++) agg_fields(P.block_agg[k], x);
   uint64_t ex[11];
 #pragma unroll
   for (int f = 0; f < 11; f++) {
@@ -861,12 +860,11 @@ __global__ void __launch_bounds__(SCAN_WG) k_scan(WaveParams P) {
       for (int w = 0; w < wv; w++) pre += s_w[w][f];
       ex[f] += pre;
     }
-#pragma unroll
-    for (int k = 0; k < SCAN_PER; k++) {
-      P.block_off[threadIdx.x * SCAN_PER + k] =
-          BlockOff{ex[0], ex[1], ex[2], ex[3], ex[4], (uint32_t)ex[5], (uint32_t)ex[6]};
-      ex[0] += g[k].rec; ex[1] += g[k].wf; ex[2] += g[k].job; ex[3] += g[k].row; ex[4] += g[k].bytes;
-      ex[5] += g[k].merges; ex[6] += g[k].conds;
+    for (int k = k0; k < k1; k++) {
+      const BlockAgg g = P.block_agg[k];
+      P.block_off[k] = BlockOff{ex[0], ex[1], ex[2], ex[3], ex[4], (uint32_t)ex[5], (uint32_t)ex[6]};
+      ex[0] += g.rec; ex[1] += g.wf; ex[2] += g.job; ex[3] += g.row; ex[4] += g.bytes;
+      ex[5] += g.merges; ex[6] += g.conds;
     }
   }
   if (threadIdx.x == 0) {
@@ -1043,19 +1041,19 @@ __global__ void __launch_bounds__(WG) k_emit(WaveParams P) {
 }
 
 void launch_pre(const WaveParams& p, hipStream_t stream) {
-  hipLaunchKernelGGL(k_pre, dim3(WAVE_GRID), dim3(WG), 0, stream, p);
+  hipLaunchKernelGGL(k_pre, dim3(p.grid), dim3(WG), 0, stream, p);
 }
 void launch_children(const WaveParams& p, hipStream_t stream) {
   hipLaunchKernelGGL(k_children, dim3(1024), dim3(256), 0, stream, p);
 }
 void launch_process(const WaveParams& p, hipStream_t stream) {
-  hipLaunchKernelGGL(k_process, dim3(WAVE_GRID), dim3(WG), 0, stream, p);
+  hipLaunchKernelGGL(k_process, dim3(p.grid), dim3(WG), 0, stream, p);
 }
 void launch_scan(const WaveParams& p, hipStream_t stream) {
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(SCAN_WG), 0, stream, p);
 }
 void launch_emit(const WaveParams& p, hipStream_t stream) {
-  hipLaunchKernelGGL(k_emit, dim3(WAVE_GRID), dim3(WG), 0, stream, p);
+  hipLaunchKernelGGL(k_emit, dim3(p.grid), dim3(WG), 0, stream, p);
 }
 
 }  // namespace zbg
