@@ -229,7 +229,12 @@ int zb_comm_init(zb_engine* e, const uint8_t id[128], int nranks, int rank);
 int zb_comm_pending(zb_engine* e, uint64_t global[2]);
 /* Collective: every rank takes its pending commands of `kind` (zb_outbox_take order), sends each target
  * its slice (ncclSend / ncclRecv in one group), and delivers what it receives in source-rank order
- * (zb_inbox_submit). *received = commands delivered to this rank. */
+ * (zb_inbox_submit). *received = commands delivered to this rank.
+ * Failure protocol: a rank whose local work fails (outbox read, buffer growth) still takes part in the
+ * (count, status) all-to-all and the status all-reduce that precede the record exchange, so every rank
+ * returns an error in the same call and none is left blocking in ncclSend / ncclRecv. A failing RCCL
+ * call aborts the communicator (ncclCommAbort); later exchanges on the engine fail with ZB_EDEVICE.
+ * Exchange and sort buffers persist across calls (no allocation per round in the steady state). */
 int zb_comm_exchange(zb_engine* e, int kind, uint64_t* received);
 
 /* ---- output -------------------------------------------------------------------------- */

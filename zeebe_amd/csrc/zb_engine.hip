@@ -59,6 +59,7 @@ struct DevVec {
 struct zb_engine {
   zb_config cfg{};
   hipStream_t stream = nullptr;
+  int32_t wave_grid_fixed = 0;  // ZB_WAVE_GRID (tuning experiments): fixed wave grid instead of the sized one
   std::string err;
 
   ModelTables model;
@@ -70,6 +71,11 @@ struct zb_engine {
   DevVec<DevQuery> d_queries;
   DevVec<DevFilter> d_filters;
   DevVec<uint8_t> d_pool;
+  DevVec<ValTmpl> d_tmpl;        // record value templates (zb_model.cpp build_value_templates)
+  DevVec<uint8_t> d_tpool;
+  int ser_mode = 0;              // ZB_SER_MODE: 0 = two passes (size, scan, write), 1 = single pass (look-back)
+  int ser_tmpl = 1;              // ZB_SER_TMPL=0: generic encoder only (A/B)
+  int32_t ntmpl_elems = 0;
 
   // device state
   zb_rec* log = nullptr;
@@ -90,7 +96,8 @@ struct zb_engine {
   uint64_t* derr_info = nullptr;
   MergeJob* merge_jobs = nullptr;
   uint64_t* cond_jobs = nullptr;
-  uint32_t* job_counts = nullptr;  // [0..1] merge counts, [2..3] cond counts
+  uint32_t* job_counts = nullptr;  // [0..1] merge counts, [2..3] cond counts, [4..5] subscribe counts
+  uint64_t* sub_jobs = nullptr;    // [job_cap] subscribe steps of a wave (models with message catch events)
   uint64_t job_cap = 0;
   WaveHdr* h_hdr_pinned = nullptr;  // pinned mirror for D2H polling
   uint32_t* h_err_pinned = nullptr;
@@ -171,7 +178,20 @@ struct zb_engine {
   bool has_catch = false;
   // RCCL communicator over the partitions of the node (zb_comm_*)
   ncclComm_t comm = nullptr;
-  uint64_t* d_xcounts = nullptr;  // [2 * 64] send / receive counts
+  bool comm_broken = false;       // an RCCL call failed: the communicator is not used again
+  uint64_t* d_xcounts = nullptr;  // [4 * 64]: (count, status) pairs sent to / received from every rank
+  // persistent exchange buffers (grown geometrically, never freed per round)
+  zb_exchange_rec* xsend = nullptr;
+  zb_exchange_rec* xrecv = nullptr;
+  uint64_t xsend_cap = 0, xrecv_cap = 0;
+  // outbox sort buffers, sized to the outbox capacity once
+  uint64_t* ob_keys = nullptr;
+  uint32_t *ob_idx_in = nullptr, *ob_idx_out = nullptr;
+  uint64_t* ob_first = nullptr;
+  void* ob_tmp = nullptr;
+  size_t ob_tmp_bytes = 0;
+  zb_exchange_rec* ob_staging = nullptr;
+  uint64_t ob_staging_cap = 0;
 
   // scope-wide row state (RowAux), first-live-child requests, wave epoch
   RowAux* raux = nullptr;
@@ -190,7 +210,7 @@ struct zb_engine {
   DevVec<int64_t> d_lookup_keys, d_lookup_pos;
   // drain buffers (zb_serialize), grown on demand and reused
   uint64_t dr_cap = 0, dr_val_cap = 0, dr_tmp_cap = 0;
-  uint64_t *dr_len = nullptr, *dr_off = nullptr;
+  uint64_t *dr_len = nullptr, *dr_off = nullptr, *dr_tiles = nullptr;
   zb_record_header* dr_hdr = nullptr;
   uint8_t* dr_val = nullptr;
   void* dr_tmp = nullptr;
@@ -236,6 +256,14 @@ int upload_model(zb_engine* e) {
   HIPCHECK(e, e->d_queries.upload(e->model.queries, e->stream));
   HIPCHECK(e, e->d_filters.upload(e->model.filters, e->stream));
   HIPCHECK(e, e->d_pool.upload(e->model.pool, e->stream));
+  {
+    std::vector<ValTmpl> tm;
+    std::vector<uint8_t> tp;
+    build_value_templates(e->model, tm, tp);
+    HIPCHECK(e, e->d_tmpl.upload(tm, e->stream));
+    HIPCHECK(e, e->d_tpool.upload(tp, e->stream));
+    e->ntmpl_elems = (int32_t)e->model.elems.size();
+  }
   if (e->static_blobs.size() > STATIC_ARENA_BYTES) return fail(e, ZB_ENOMEM, "static payload region full");
   HIPCHECK(e, hipMemcpyAsync(e->arena, e->static_blobs.data(), e->static_blobs.size(), hipMemcpyHostToDevice,
                              e->stream));
@@ -271,6 +299,8 @@ WaveParams wave_params(zb_engine* e) {
   p.merge_count = e->job_counts;
   p.cond_jobs = e->cond_jobs;
   p.cond_count = e->job_counts + 2;
+  p.sub_jobs = e->sub_jobs;
+  p.sub_count = e->job_counts + 4;
   p.job_cap = e->job_cap;
   p.stats = e->dstats;
   p.log_cap = e->cfg.log_capacity;
@@ -289,13 +319,16 @@ WaveParams wave_params(zb_engine* e) {
   p.term = e->term ? 1 : 0;
   p.epoch = e->epoch;
   p.need_children = e->need_children;
-  // one 256-record tile per workgroup for the generation last seen by the host (x2 headroom for a generation
-  // that grows inside the batch; a larger one is still covered, with several tiles per workgroup)
+  // about four 256-record tiles per workgroup for the generation last seen by the host, 256..1024 workgroups
+  // (C2 wave-only, 1M records per wave: 1024 workgroups 32.5 ms/step, 2048 33.0, 512 34.3, one tile per
+  // workgroup 44.6 -- per-workgroup fixed costs; profiles/r02/grid_sweep.txt); a generation that grows inside
+  // the batch is still covered, with more tiles per workgroup
   {
     const int64_t gen = std::max<int64_t>(e->host_hdr.gen_end - e->host_hdr.begin, e->host_hdr.end - e->host_hdr.begin);
     const int64_t chunk = std::min<int64_t>(gen, (int64_t)e->wave_cap);
-    const int64_t g = 2 * ((chunk + WAVE_TILE - 1) / WAVE_TILE);
-    p.grid = (int32_t)std::max<int64_t>(256, std::min<int64_t>(g, WAVE_GRID_MAX));
+    const int64_t g = ((chunk + WAVE_TILE - 1) / WAVE_TILE + 3) / 4;
+    p.grid = (int32_t)std::max<int64_t>(256, std::min<int64_t>(g, 1024));
+    if (e->wave_grid_fixed) p.grid = e->wave_grid_fixed;
   }
   return p;
 }
@@ -518,6 +551,7 @@ int ensure_outbox(zb_engine* e) {
   }
   HIPCHECK(e, hipMalloc(&e->on, 2 * sizeof(uint32_t)));
   HIPCHECK(e, hipMemsetAsync(e->on, 0, 2 * sizeof(uint32_t), e->stream));
+  if (!e->sub_jobs) HIPCHECK(e, hipMalloc(&e->sub_jobs, e->job_cap * sizeof(uint64_t)));
   return ZB_OK;
 }
 
@@ -579,6 +613,9 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   *out = nullptr;
   auto* e = new zb_engine();
   e->cfg = *cfg;
+  if (const char* m = std::getenv("ZB_SER_MODE")) e->ser_mode = std::strcmp(m, "fused") == 0 ? 1 : 0;
+  if (const char* m = std::getenv("ZB_SER_TMPL")) e->ser_tmpl = atoi(m) != 0;
+  if (const char* g = std::getenv("ZB_WAVE_GRID")) e->wave_grid_fixed = std::max(0, std::min(atoi(g), (int)WAVE_GRID_MAX));
   if (e->cfg.log_capacity == 0) e->cfg.log_capacity = 1ull << 22;
   if (e->cfg.row_capacity == 0) e->cfg.row_capacity = 1ull << 20;
   if (e->cfg.arena_bytes == 0) e->cfg.arena_bytes = 64ull << 20;
@@ -615,7 +652,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   e->job_cap = std::min<uint64_t>(L, 1ull << 26);
   if (hipMalloc(&e->merge_jobs, 2 * e->job_cap * sizeof(MergeJob)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->cond_jobs, 2 * e->job_cap * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipMalloc(&e->job_counts, 4 * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->job_counts, 6 * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_hdr_pinned, 2 * sizeof(WaveHdr)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_err_pinned, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_ctl_pinned, sizeof(TrajCtl)) != hipSuccess) return cleanup(ZB_ENOMEM);
@@ -648,7 +685,7 @@ void zb_engine_destroy(zb_engine* e) {
   for (auto& x : e->ev)
     if (x) (void)hipEventDestroy(x);
   void* ps[] = {e->log, e->links, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
-                e->merge_jobs, e->cond_jobs, e->job_counts, e->cw, e->stage, e->info, e->block_agg, e->block_off,
+                e->merge_jobs, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
                 e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->need_children};
@@ -656,16 +693,17 @@ void zb_engine_destroy(zb_engine* e) {
     if (p) (void)hipFree(p);
   if (e->comm) (void)ncclCommDestroy(e->comm);
   void* ms[] = {e->obox[0], e->obox[1], e->okeys[0], e->okeys[1], e->on, e->subs, e->sub_head, e->sub_next,
-                e->msgs, e->msg_head, e->msg_next, e->d_xcounts};
+                e->msgs, e->msg_head, e->msg_next, e->d_xcounts, e->xsend, e->xrecv, e->ob_keys, e->ob_idx_in,
+                e->ob_idx_out, e->ob_first, e->ob_tmp, e->ob_staging};
   for (void* p : ms)
     if (p) (void)hipFree(p);
   if (e->h_hdr_pinned) (void)hipHostFree(e->h_hdr_pinned);
   if (e->h_err_pinned) (void)hipHostFree(e->h_err_pinned);
   if (e->h_ctl_pinned) (void)hipHostFree(e->h_ctl_pinned);
   e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_consts.free();
-  e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
+  e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_tmpl.free(); e->d_tpool.free(); e->d_staged.free(); e->d_staged_arena.free();
   e->d_ranges.free(); e->d_cmd_pool.free(); e->d_lookup_keys.free(); e->d_lookup_pos.free();
-  void* dr[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_val, e->dr_tmp, e->dr_total};  // dr_len: tile states
+  void* dr[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_val, e->dr_tmp, e->dr_total, e->dr_tiles};
   for (void* p : dr)
     if (p) (void)hipFree(p);
   if (e->h_dr_total) (void)hipHostFree(e->h_dr_total);
@@ -692,7 +730,7 @@ int zb_reset(zb_engine* e, int keep_staged) {
   HIPCHECK(e, hipMemcpyAsync(e->hdr, &h, sizeof(h), hipMemcpyHostToDevice, e->stream));
   HIPCHECK(e, hipMemsetAsync(e->derr, 0, sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->derr_info, 0xff, sizeof(uint64_t), e->stream));
-  HIPCHECK(e, hipMemsetAsync(e->job_counts, 0, 4 * sizeof(uint32_t), e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->job_counts, 0, 6 * sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->dstats, 0, 8 * sizeof(uint64_t), e->stream));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
   e->ranges.clear();
@@ -1346,6 +1384,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
       launch_emit(p, e->stream);
       HIPCHECK(e, hipEventRecord(ev[2], e->stream));
       // payload kernels for this wave's deferred work (only when the model can produce any)
+      if (e->has_catch) launch_subscribe(p, e->stream);  // this wave's subscribe steps (outbox)
       if (e->has_merges) launch_merge(p, e->stream);
       if (e->has_splits) launch_cond(p, e->stream);
       HIPCHECK(e, hipEventRecord(ev[3], e->stream));
@@ -1419,15 +1458,24 @@ int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats*
     HIPCHECK(e, hipMalloc(&e->dr_total, 4 * sizeof(uint64_t)));  // [0] bytes [1] payload bytes [2] ctr|overflow
     HIPCHECK(e, hipHostMalloc(&e->h_dr_total, 4 * sizeof(uint64_t)));
   }
-  const uint64_t tiles = ((uint64_t)count + 255) / 256;
   if ((uint64_t)count > e->dr_cap) {
-    if (e->dr_hdr) (void)hipFree(e->dr_hdr);
-    if (e->dr_len) (void)hipFree(e->dr_len);
-    e->dr_hdr = nullptr; e->dr_len = nullptr; e->dr_cap = 0;
+    void* ps[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_tmp, e->dr_tiles};
+    for (void* q : ps)
+      if (q) (void)hipFree(q);
+    e->dr_len = e->dr_off = e->dr_tiles = nullptr; e->dr_hdr = nullptr; e->dr_tmp = nullptr;
+    e->dr_cap = e->dr_tmp_cap = 0;
     const uint64_t cap = (uint64_t)count + (uint64_t)count / 4 + 1024;
+    if (cap + 1 > (uint64_t)INT32_MAX) return fail(e, ZB_EUNSUPPORTED, "more than 2^31 records in one drain");
     HIPCHECK(e, hipMalloc(&e->dr_hdr, cap * sizeof(zb_record_header)));
-    HIPCHECK(e, hipMalloc(&e->dr_len, (cap / 256 + 2) * sizeof(uint64_t)));  // tile states
-    HIPCHECK(e, hipMemset(e->dr_len, 0, (cap / 256 + 2) * sizeof(uint64_t)));
+    HIPCHECK(e, hipMalloc(&e->dr_tiles, (cap / 256 + 2) * sizeof(uint64_t)));  // single pass: tile states
+    HIPCHECK(e, hipMemset(e->dr_tiles, 0, (cap / 256 + 2) * sizeof(uint64_t)));
+    HIPCHECK(e, hipMalloc(&e->dr_len, (cap + 1) * sizeof(uint64_t)));  // two passes: sizes, offsets
+    HIPCHECK(e, hipMalloc(&e->dr_off, (cap + 1) * sizeof(uint64_t)));
+    size_t tmp = 0;
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->dr_len, e->dr_off, (int)(cap + 1), e->stream) != hipSuccess)
+      return fail(e, ZB_EDEVICE, "scan sizing");
+    HIPCHECK(e, hipMalloc(&e->dr_tmp, tmp + 16));
+    e->dr_tmp_cap = tmp;
     e->dr_cap = cap;
   }
   if (e->dr_val_cap == 0) {  // first estimate; grown from the exact total if it overflows
@@ -1440,6 +1488,10 @@ int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats*
   SerParams sp{};
   sp.log = e->log;
   sp.arena = e->arena;
+  sp.tmpl = e->d_tmpl.p;
+  sp.tpool = (const uint32_t*)e->d_tpool.p;
+  sp.nelems = e->d_tmpl.p ? e->ntmpl_elems : 0;
+  sp.use_tmpl = e->ser_tmpl && e->d_tmpl.p ? 1 : 0;
   sp.elems = e->d_elems.p;
   sp.wfs = e->d_wfs.p;
   sp.queries = e->d_queries.p;
@@ -1450,22 +1502,42 @@ int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats*
   sp.start = start;
   sp.count = count;
   sp.totals = e->dr_total;
-  sp.tile_state = e->dr_len;
+  sp.tile_state = e->dr_tiles;
   sp.tile_ctr = (uint32_t*)(e->dr_total + 2);
   sp.overflow = (uint32_t*)(e->dr_total + 2) + 1;
   sp.headers = e->dr_hdr;
+  float ms_size = 0, ms_scan = 0, ms_write = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
-    if ((++e->dr_epoch & 0x3ffff) == 0) {  // tile-state tags wrap: clear them once
-      HIPCHECK(e, hipMemsetAsync(e->dr_len, 0, (e->dr_cap / 256 + 2) * sizeof(uint64_t), e->stream));
-      ++e->dr_epoch;
-    }
-    sp.epoch = (uint32_t)e->dr_epoch;
     sp.out = e->dr_val;
     sp.out_cap = e->dr_val_cap;
     HIPCHECK(e, hipMemsetAsync(e->dr_total, 0, 4 * sizeof(uint64_t), e->stream));
-    HIPCHECK(e, hipEventRecord(e->dr_ev[0], e->stream));
-    launch_ser_fused(sp, e->stream);
-    HIPCHECK(e, hipEventRecord(e->dr_ev[1], e->stream));
+    if (e->ser_mode == 1) {  // one pass: decoupled look-back over 256-record tiles
+      if ((++e->dr_epoch & 0x3ffff) == 0) {  // tile-state tags wrap: clear them once
+        HIPCHECK(e, hipMemsetAsync(e->dr_tiles, 0, (e->dr_cap / 256 + 2) * sizeof(uint64_t), e->stream));
+        ++e->dr_epoch;
+      }
+      sp.epoch = (uint32_t)e->dr_epoch;
+      HIPCHECK(e, hipEventRecord(e->dr_ev[0], e->stream));
+      HIPCHECK(e, hipEventRecord(e->dr_ev[1], e->stream));
+      HIPCHECK(e, hipEventRecord(e->dr_ev[2], e->stream));
+      launch_ser_fused(sp, e->stream);
+      HIPCHECK(e, hipEventRecord(e->dr_ev[3], e->stream));
+    } else {  // two passes: sizes -> exclusive scan -> write (no host round trip: capacity checked on the device)
+      SerParams sz = sp;
+      sz.lengths64 = e->dr_len;  // count + 1 entries, the last one 0: the scan's last output is the total
+      HIPCHECK(e, hipEventRecord(e->dr_ev[0], e->stream));
+      launch_ser_size(sz, e->stream);
+      HIPCHECK(e, hipEventRecord(e->dr_ev[1], e->stream));
+      size_t tmp = e->dr_tmp_cap;
+      if (hipcub::DeviceScan::ExclusiveSum(e->dr_tmp, tmp, e->dr_len, e->dr_off, (int)(count + 1), e->stream) != hipSuccess)
+        return fail(e, ZB_EDEVICE, "drain scan");
+      HIPCHECK(e, hipMemcpyAsync(e->dr_total, e->dr_off + count, sizeof(uint64_t), hipMemcpyDeviceToDevice, e->stream));
+      HIPCHECK(e, hipEventRecord(e->dr_ev[2], e->stream));
+      SerParams wr = sp;
+      wr.offsets = e->dr_off;
+      launch_ser_write(wr, e->stream);
+      HIPCHECK(e, hipEventRecord(e->dr_ev[3], e->stream));
+    }
     HIPCHECK(e, hipMemcpyAsync(e->h_dr_total, e->dr_total, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHECK(e, hipStreamSynchronize(e->stream));
     HIPCHECK(e, hipGetLastError());
@@ -1479,18 +1551,18 @@ int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats*
     HIPCHECK(e, hipMalloc(&e->dr_val, cap));
     e->dr_val_cap = cap;
   }
-  (void)tiles;
-  float ms_write = 0;
-  HIPCHECK(e, hipEventElapsedTime(&ms_write, e->dr_ev[0], e->dr_ev[1]));
+  HIPCHECK(e, hipEventElapsedTime(&ms_size, e->dr_ev[0], e->dr_ev[1]));
+  HIPCHECK(e, hipEventElapsedTime(&ms_scan, e->dr_ev[1], e->dr_ev[2]));
+  HIPCHECK(e, hipEventElapsedTime(&ms_write, e->dr_ev[2], e->dr_ev[3]));
   e->dr_count = count;
   e->dr_bytes = e->h_dr_total[0];
   st.records = (uint64_t)count;
   st.value_bytes = e->h_dr_total[0];
   st.payload_bytes = e->h_dr_total[1];
-  st.size_kernel_ms = 0;  // sizes, offsets and values in one pass (k_ser_fused)
+  st.size_kernel_ms = ms_size;
+  st.scan_ms = ms_scan;
   st.write_kernel_ms = ms_write;
   st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  st.scan_ms = 0;
   if (stats) *stats = st;
   return ZB_OK;
 }
@@ -1663,53 +1735,46 @@ int zb_outbox_take(zb_engine* e, int kind, zb_exchange_rec* dst, size_t cap, int
   if (n > cap || !dst) return fail(e, ZB_ENOMEM, "outbox destination too small");
   if (n > e->ocap) return fail(e, ZB_ENOMEM, "outbox overflow");
   const int k = kind - 1;
-  // sort (key, index) pairs: target partition, source position, emission order
-  uint64_t* keys_out = nullptr;
-  uint32_t *idx_in = nullptr, *idx_out = nullptr;
-  uint64_t* first = nullptr;
-  void* tmp = nullptr;
-  size_t tmp_bytes = 0;
-  zb_exchange_rec* staging = nullptr;
-  auto cleanup = [&]() {
-    void* ps[] = {keys_out, idx_in, idx_out, first, tmp, staging};
-    for (void* q : ps)
-      if (q) (void)hipFree(q);
-  };
-  do {
-    if (hipMalloc(&keys_out, n * 8) != hipSuccess || hipMalloc(&idx_in, n * 4) != hipSuccess ||
-        hipMalloc(&idx_out, n * 4) != hipSuccess || hipMalloc(&first, (P + 1) * 8) != hipSuccess) {
-      rc = fail(e, ZB_ENOMEM, "outbox sort buffers");
-      break;
+  // sort (key, index) pairs: target partition, source position, emission order; the sort buffers are
+  // allocated once, at the outbox capacity
+  if (!e->ob_keys) {
+    const uint64_t c = e->ocap;
+    if (hipMalloc(&e->ob_keys, c * 8) != hipSuccess || hipMalloc(&e->ob_idx_in, c * 4) != hipSuccess ||
+        hipMalloc(&e->ob_idx_out, c * 4) != hipSuccess || hipMalloc(&e->ob_first, 65 * 8) != hipSuccess)
+      return fail(e, ZB_ENOMEM, "outbox sort buffers");
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, e->ob_tmp_bytes, e->okeys[0], e->ob_keys, e->ob_idx_in,
+                                           e->ob_idx_out, (int)c, 0, 64, e->stream) != hipSuccess ||
+        hipMalloc(&e->ob_tmp, e->ob_tmp_bytes + 16) != hipSuccess)
+      return fail(e, ZB_ENOMEM, "outbox sort scratch");
+  }
+  launch_iota(e->ob_idx_in, n, e->stream);
+  size_t tmp_bytes = e->ob_tmp_bytes;
+  if (hipcub::DeviceRadixSort::SortPairs(e->ob_tmp, tmp_bytes, e->okeys[k], e->ob_keys, e->ob_idx_in, e->ob_idx_out,
+                                         (int)n, 0, 64, e->stream) != hipSuccess)
+    return fail(e, ZB_EDEVICE, "outbox sort");
+  zb_exchange_rec* out = dst;
+  if (!dst_on_device) {
+    if (n > e->ob_staging_cap) {
+      if (e->ob_staging) (void)hipFree(e->ob_staging);
+      e->ob_staging = nullptr;
+      e->ob_staging_cap = 0;
+      const uint64_t c = std::max<uint64_t>(n, 2 * e->ob_staging_cap);
+      if (hipMalloc(&e->ob_staging, c * sizeof(zb_exchange_rec)) != hipSuccess) return fail(e, ZB_ENOMEM, "outbox staging");
+      e->ob_staging_cap = c;
     }
-    launch_iota(idx_in, n, e->stream);
-    if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, e->okeys[k], keys_out, idx_in, idx_out, (int)n, 0, 64,
-                                           e->stream) != hipSuccess ||
-        hipMalloc(&tmp, tmp_bytes + 16) != hipSuccess ||
-        hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, e->okeys[k], keys_out, idx_in, idx_out, (int)n, 0, 64,
-                                           e->stream) != hipSuccess) {
-      rc = fail(e, ZB_EDEVICE, "outbox sort");
-      break;
-    }
-    zb_exchange_rec* out = dst;
-    if (!dst_on_device) {
-      if (hipMalloc(&staging, n * sizeof(zb_exchange_rec)) != hipSuccess) { rc = fail(e, ZB_ENOMEM, "outbox staging"); break; }
-      out = staging;
-    }
-    launch_outbox_gather(e->obox[k], idx_out, out, n, e->stream);
-    launch_outbox_bounds(keys_out, n, first, P, e->stream);
-    std::vector<uint64_t> h_first(P, 0);
-    if (hipMemcpyAsync(h_first.data(), first, P * 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
-        (!dst_on_device && hipMemcpyAsync(dst, staging, n * sizeof(zb_exchange_rec), hipMemcpyDeviceToHost, e->stream) !=
-                               hipSuccess) ||
-        hipMemsetAsync(e->on + k, 0, sizeof(uint32_t), e->stream) != hipSuccess ||
-        hipStreamSynchronize(e->stream) != hipSuccess) {
-      rc = fail(e, ZB_EDEVICE, "outbox copy");
-      break;
-    }
-    for (int q = 0; q < P; q++) counts[q] = (q + 1 < P ? h_first[q + 1] : n) - h_first[q];
-  } while (0);
-  cleanup();
-  return rc;
+    out = e->ob_staging;
+  }
+  launch_outbox_gather(e->obox[k], e->ob_idx_out, out, n, e->stream);
+  launch_outbox_bounds(e->ob_keys, n, e->ob_first, P, e->stream);
+  std::vector<uint64_t> h_first(P, 0);
+  if (hipMemcpyAsync(h_first.data(), e->ob_first, P * 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+      (!dst_on_device && hipMemcpyAsync(dst, e->ob_staging, n * sizeof(zb_exchange_rec), hipMemcpyDeviceToHost,
+                                        e->stream) != hipSuccess) ||
+      hipMemsetAsync(e->on + k, 0, sizeof(uint32_t), e->stream) != hipSuccess ||
+      hipStreamSynchronize(e->stream) != hipSuccess)
+    return fail(e, ZB_EDEVICE, "outbox copy");
+  for (int q = 0; q < P; q++) counts[q] = (q + 1 < P ? h_first[q + 1] : n) - h_first[q];
+  return ZB_OK;
 }
 
 #define NCCLCHECK(e, call)                                                                      \
@@ -1732,12 +1797,43 @@ int zb_comm_init(zb_engine* e, const uint8_t id[128], int nranks, int rank) {
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof(u));
   NCCLCHECK(e, ncclCommInitRank(&e->comm, nranks, u, rank));
-  HIPCHECK(e, hipMalloc(&e->d_xcounts, 2 * 64 * sizeof(uint64_t)));
-  return ensure_outbox(e);
+  e->comm_broken = false;
+  HIPCHECK(e, hipMalloc(&e->d_xcounts, 4 * 64 * sizeof(uint64_t)));
+  int rc = ensure_outbox(e);
+  if (rc != ZB_OK) return rc;
+  // exchange buffers for the common case up front (grown later only if a round needs more)
+  const uint64_t c = std::min<uint64_t>(e->ocap, 1ull << 16);
+  HIPCHECK(e, hipMalloc(&e->xsend, c * sizeof(zb_exchange_rec)));
+  HIPCHECK(e, hipMalloc(&e->xrecv, c * sizeof(zb_exchange_rec)));
+  e->xsend_cap = e->xrecv_cap = c;
+  return ZB_OK;
 }
 
+namespace {
+// an RCCL failure leaves the communicator unusable (peers may be inside the same collective): abort it so
+// that no later call blocks on it, and fail this and every later exchange on this engine
+int comm_fail(zb_engine* e, const std::string& what, ncclResult_t r) {
+  e->comm_broken = true;
+  if (e->comm) (void)ncclCommAbort(e->comm);
+  e->comm = nullptr;
+  return fail(e, ZB_EDEVICE, what + ": " + ncclGetErrorString(r));
+}
+// grows a persistent exchange buffer to hold n records (local: the caller agrees on the outcome with its peers)
+int grow_xbuf(zb_exchange_rec** p, uint64_t* cap, uint64_t n) {
+  if (n <= *cap) return ZB_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  const uint64_t c = std::max<uint64_t>(n, 1024) + n / 2;
+  if (hipMalloc(p, c * sizeof(zb_exchange_rec)) != hipSuccess) return ZB_ENOMEM;
+  *cap = c;
+  return ZB_OK;
+}
+}  // namespace
+
 int zb_comm_pending(zb_engine* e, uint64_t global[2]) {
-  if (!e || !global || !e->comm) return ZB_EINVAL;
+  if (!e || !global) return ZB_EINVAL;
+  if (!e->comm) return e->comm_broken ? fail(e, ZB_EDEVICE, "communicator aborted after an earlier failure") : ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
   uint64_t local[2] = {0, 0};
   for (int k = 0; k < 2; k++) {
@@ -1745,71 +1841,86 @@ int zb_comm_pending(zb_engine* e, uint64_t global[2]) {
     if (rc != ZB_OK) return rc;
   }
   HIPCHECK(e, hipMemcpyAsync(e->d_xcounts, local, sizeof(local), hipMemcpyHostToDevice, e->stream));
-  NCCLCHECK(e, ncclAllReduce(e->d_xcounts, e->d_xcounts, 2, ncclUint64, ncclSum, e->comm, e->stream));
+  ncclResult_t nr = ncclAllReduce(e->d_xcounts, e->d_xcounts, 2, ncclUint64, ncclSum, e->comm, e->stream);
+  if (nr != ncclSuccess) return comm_fail(e, "pending counts", nr);
   HIPCHECK(e, hipMemcpyAsync(global, e->d_xcounts, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
   return ZB_OK;
 }
 
+// Collective on every rank, whatever happens locally: a rank whose local work fails still takes part in
+// both agreement steps (sending zero counts and its status), so every rank returns the same error instead
+// of one rank leaving the collective and its peers blocking in ncclSend / ncclRecv.
 int zb_comm_exchange(zb_engine* e, int kind, uint64_t* received) {
-  if (!e || !received || !e->comm || (kind != ZB_XCHG_OPEN && kind != ZB_XCHG_CORRELATE)) return ZB_EINVAL;
+  if (!e || !received || (kind != ZB_XCHG_OPEN && kind != ZB_XCHG_CORRELATE)) return ZB_EINVAL;
+  if (!e->comm) return e->comm_broken ? fail(e, ZB_EDEVICE, "communicator aborted after an earlier failure") : ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
   const int P = e->cfg.partition_count;
   *received = 0;
-  uint64_t n = 0;
-  int rc = zb_outbox_count(e, kind, &n);
-  if (rc != ZB_OK) return rc;
-  zb_exchange_rec* send = nullptr;
-  zb_exchange_rec* recv = nullptr;
-  auto cleanup = [&]() {
-    if (send) (void)hipFree(send);
-    if (recv) (void)hipFree(recv);
-  };
+  // 0. local: take the outbox (sorted by target) into the persistent send buffer
   std::vector<uint64_t> sc(P, 0), rcv(P, 0);
-  if (hipMalloc(&send, std::max<uint64_t>(n, 1) * sizeof(zb_exchange_rec)) != hipSuccess) {
-    cleanup();
-    return fail(e, ZB_ENOMEM, "exchange send buffer");
+  uint64_t n = 0;
+  int local = zb_outbox_count(e, kind, &n);
+  if (local == ZB_OK) local = grow_xbuf(&e->xsend, &e->xsend_cap, n);
+  if (local == ZB_OK) {
+    uint64_t got = 0;
+    local = zb_outbox_take(e, kind, e->xsend, e->xsend_cap, 1, sc.data(), &got);
   }
-  uint64_t got = 0;
-  rc = zb_outbox_take(e, kind, send, std::max<uint64_t>(n, 1), 1, sc.data(), &got);
-  if (rc != ZB_OK) { cleanup(); return rc; }
-  // 1. counts: every rank learns how many commands each source sends it
-  if (hipMemcpyAsync(e->d_xcounts, sc.data(), P * 8, hipMemcpyHostToDevice, e->stream) != hipSuccess) {
-    cleanup();
-    return fail(e, ZB_EDEVICE, "exchange counts upload");
-  }
+  if (local != ZB_OK) std::fill(sc.begin(), sc.end(), 0);
+  const std::string local_err = local != ZB_OK ? e->err : std::string();
+  // 1. agreement + counts: every rank sends every peer (count for it, its status); always posted
+  std::vector<uint64_t> pairs(2 * 64, 0);
+  for (int q = 0; q < P; q++) { pairs[2 * q] = sc[q]; pairs[2 * q + 1] = (uint64_t)(uint32_t)local; }
+  if (hipMemcpyAsync(e->d_xcounts, pairs.data(), 2 * P * 8, hipMemcpyHostToDevice, e->stream) != hipSuccess)
+    local = local != ZB_OK ? local : ZB_EDEVICE;  // the pairs may be stale: the status still travels below
   ncclResult_t nr = ncclGroupStart();
   for (int q = 0; q < P && nr == ncclSuccess; q++) {
-    nr = ncclSend(e->d_xcounts + q, 1, ncclUint64, q, e->comm, e->stream);
-    if (nr == ncclSuccess) nr = ncclRecv(e->d_xcounts + 64 + q, 1, ncclUint64, q, e->comm, e->stream);
+    nr = ncclSend(e->d_xcounts + 2 * q, 2, ncclUint64, q, e->comm, e->stream);
+    if (nr == ncclSuccess) nr = ncclRecv(e->d_xcounts + 128 + 2 * q, 2, ncclUint64, q, e->comm, e->stream);
   }
   if (nr == ncclSuccess) nr = ncclGroupEnd();
-  if (nr != ncclSuccess) { cleanup(); return fail(e, ZB_EDEVICE, std::string("exchange counts: ") + ncclGetErrorString(nr)); }
-  if (hipMemcpyAsync(rcv.data(), e->d_xcounts + 64, P * 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
-      hipStreamSynchronize(e->stream) != hipSuccess) {
-    cleanup();
-    return fail(e, ZB_EDEVICE, "exchange counts download");
-  }
+  if (nr != ncclSuccess) return comm_fail(e, "exchange counts", nr);
+  std::vector<uint64_t> rpairs(2 * 64, 0);
+  if (hipMemcpyAsync(rpairs.data(), e->d_xcounts + 128, 2 * P * 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+      hipStreamSynchronize(e->stream) != hipSuccess)
+    return comm_fail(e, "exchange counts download", ncclSystemError);
+  int peer_failed = -1;
   uint64_t total = 0;
-  for (int q = 0; q < P; q++) total += rcv[q];
-  if (hipMalloc(&recv, std::max<uint64_t>(total, 1) * sizeof(zb_exchange_rec)) != hipSuccess) {
-    cleanup();
-    return fail(e, ZB_ENOMEM, "exchange receive buffer");
+  for (int q = 0; q < P; q++) {
+    rcv[q] = rpairs[2 * q];
+    if (rpairs[2 * q + 1] != 0 && peer_failed < 0) peer_failed = q;
+    total += rcv[q];
   }
-  // 2. records: slices by target out, by source in (source-rank order = canonical delivery order)
+  // 2. the receive side may fail locally too: agree once more (max of the statuses) before any record moves
+  if (peer_failed < 0 && local == ZB_OK) local = grow_xbuf(&e->xrecv, &e->xrecv_cap, total);
+  uint64_t st = (local != ZB_OK || peer_failed >= 0) ? 1 : 0;
+  if (hipMemcpyAsync(e->d_xcounts + 192, &st, 8, hipMemcpyHostToDevice, e->stream) != hipSuccess)
+    return comm_fail(e, "exchange status upload", ncclSystemError);
+  nr = ncclAllReduce(e->d_xcounts + 192, e->d_xcounts + 192, 1, ncclUint64, ncclMax, e->comm, e->stream);
+  if (nr != ncclSuccess) return comm_fail(e, "exchange status", nr);
+  if (hipMemcpyAsync(&st, e->d_xcounts + 192, 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+      hipStreamSynchronize(e->stream) != hipSuccess)
+    return comm_fail(e, "exchange status download", ncclSystemError);
+  if (st != 0) {
+    if (local != ZB_OK) return fail(e, local, "exchange: " + (local_err.empty() ? std::string("receive buffer") : local_err));
+    if (peer_failed >= 0)
+      return fail(e, ZB_EDEVICE, "exchange: partition " + std::to_string(peer_failed) + " failed locally");
+    return fail(e, ZB_EDEVICE, "exchange: a peer failed to size its receive buffer");
+  }
+  // 3. records: slices by target out, by source in (source-rank order = canonical delivery order)
   nr = ncclGroupStart();
   uint64_t so = 0, ro = 0;
   for (int q = 0; q < P && nr == ncclSuccess; q++) {
-    if (sc[q]) nr = ncclSend(send + so, sc[q] * sizeof(zb_exchange_rec), ncclUint8, q, e->comm, e->stream);
-    if (nr == ncclSuccess && rcv[q]) nr = ncclRecv(recv + ro, rcv[q] * sizeof(zb_exchange_rec), ncclUint8, q, e->comm, e->stream);
+    if (sc[q]) nr = ncclSend(e->xsend + so, sc[q] * sizeof(zb_exchange_rec), ncclUint8, q, e->comm, e->stream);
+    if (nr == ncclSuccess && rcv[q]) nr = ncclRecv(e->xrecv + ro, rcv[q] * sizeof(zb_exchange_rec), ncclUint8, q, e->comm, e->stream);
     so += sc[q];
     ro += rcv[q];
   }
   if (nr == ncclSuccess) nr = ncclGroupEnd();
-  if (nr != ncclSuccess) { cleanup(); return fail(e, ZB_EDEVICE, std::string("exchange records: ") + ncclGetErrorString(nr)); }
-  if (hipStreamSynchronize(e->stream) != hipSuccess) { cleanup(); return fail(e, ZB_EDEVICE, "exchange sync"); }
-  rc = total ? zb_inbox_submit(e, kind, recv, total, 1) : ZB_OK;
-  cleanup();
+  if (nr != ncclSuccess) return comm_fail(e, "exchange records", nr);
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return comm_fail(e, "exchange sync", ncclSystemError);
+  // 4. delivery is local (no further collective in this call)
+  int rc = total ? zb_inbox_submit(e, kind, e->xrecv, total, 1) : ZB_OK;
   if (rc == ZB_OK) *received = total;
   return rc;
 }

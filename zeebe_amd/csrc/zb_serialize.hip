@@ -1,4 +1,4 @@
-// zb_serialize.hip — descriptor -> exact reference record value bytes (two passes: size, write).
+// zb_serialize.hip — descriptor -> exact reference record value bytes (size, offsets, write; one pass or two).
 //
 // Value layouts (UnpackedObject.write: declared properties in declaration order, ObjectValue.java:140-153):
 //   WorkflowInstanceRecord  broker-core/.../workflow/data/WorkflowInstanceRecord.java:39-60
@@ -247,18 +247,163 @@ __device__ inline void encode_value(const SerParams& P, int64_t pos, const zb_re
   }
 }
 
+// ------------------------------------------------------------------------------ template encoder
+// The common records (WORKFLOW_INSTANCE, JOB, WORKFLOW_INSTANCE_SUBSCRIPTION of a deployed element) are a
+// constant template with three variable fields (ValTmpl). Sizing is a handful of integer ops; writing
+// assembles whole 32-bit words in a register and stores them to the zeroed LDS image: interior words of a
+// value belong to one thread (plain ds_write_b32), the first and last words may be shared with the
+// neighbouring values and are merged with ds_or_b32.
+__device__ __forceinline__ uint32_t bmask(uint32_t k) { return k >= 4 ? 0xffffffffu : ((1u << (8 * k)) - 1u); }
+
+// MsgPackWriter.writeInteger (W::integer above) as up to 9 stream-order bytes: lo = bytes 0..7, hi = byte 8
+__device__ __forceinline__ uint32_t int_enc(int64_t v, uint64_t& lo, uint32_t& hi) {
+  hi = 0;
+  if (v < -(1LL << 5)) {
+    if (v < -(1LL << 15)) {
+      if (v < -(1LL << 31)) {
+        const uint64_t b = __builtin_bswap64((uint64_t)v);
+        lo = 0xd3ull | (b << 8); hi = (uint32_t)(b >> 56); return 9;
+      }
+      lo = 0xd2ull | ((uint64_t)__builtin_bswap32((uint32_t)v) << 8); return 5;
+    }
+    if (v < -(1 << 7)) { lo = 0xd1ull | ((uint64_t)__builtin_bswap16((uint16_t)v) << 8); return 3; }
+    lo = 0xd0ull | ((uint64_t)(uint8_t)v << 8); return 2;
+  }
+  if (v < (1 << 7)) { lo = (uint64_t)(uint8_t)v; return 1; }
+  if (v < (1LL << 16)) {
+    if (v < (1 << 8)) { lo = 0xccull | ((uint64_t)v << 8); return 2; }
+    lo = 0xcdull | ((uint64_t)__builtin_bswap16((uint16_t)v) << 8); return 3;
+  }
+  if (v < (1LL << 32)) { lo = 0xceull | ((uint64_t)__builtin_bswap32((uint32_t)v) << 8); return 5; }
+  const uint64_t b = __builtin_bswap64((uint64_t)v);
+  lo = 0xcfull | (b << 8); hi = (uint32_t)(b >> 56); return 9;
+}
+__device__ __forceinline__ uint32_t int_len(int64_t v) {
+  if (v < -(1LL << 5)) return v < -(1LL << 15) ? (v < -(1LL << 31) ? 9 : 5) : (v < -(1 << 7) ? 3 : 2);
+  if (v < (1 << 7)) return 1;
+  if (v < (1LL << 16)) return v < (1 << 8) ? 2 : 3;
+  return v < (1LL << 32) ? 5 : 9;
+}
+__device__ __forceinline__ uint32_t bin_hdr_len(uint32_t n) { return n < 256 ? 2 : (n < 65536 ? 3 : 5); }
+
+// template index of a record, or -1 (generic encoder)
+__device__ __forceinline__ int tmpl_index(const SerParams& P, const zb_rec& d) {
+  if (!P.use_tmpl || (d.kind & KIND_RAW) || d.elem >= (uint32_t)P.nelems) return -1;
+  const uint8_t vt = kind_vt(d.kind), rt = kind_rt(d.kind);
+  int cls;
+  if (vt == ZB_VT_WORKFLOW_INSTANCE) {
+    if (d.intent == WI_CREATE && (rt == ZB_RT_COMMAND || rt == ZB_RT_COMMAND_REJECTION)) return -1;
+    cls = TC_WI;
+  } else if (vt == ZB_VT_JOB) {
+    cls = d.intent == JI_CANCEL ? TC_JOB_CANCEL : TC_JOB;
+  } else if (vt == ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION) {
+    cls = TC_WIS;
+  } else {
+    return -1;
+  }
+  const int idx = (int)d.elem * TC_COUNT + cls;
+  return P.tmpl[idx].valid ? idx : -1;
+}
+
+__device__ __forceinline__ uint32_t tmpl_size(const ValTmpl& T, const zb_rec& d, uint32_t plen) {
+  uint32_t n = T.const_len;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const uint8_t v = T.var[k];
+    if (v == TV_INST) n += int_len(d.inst_key);
+    else if (v == TV_SCOPE) n += int_len(d.scope_key);
+    else if (v == TV_PAYLOAD) n += bin_hdr_len(plen) + plen;
+  }
+  return n;
+}
+
+struct TW {
+  uint32_t* img;  // LDS image (zeroed), word addressed
+  uint32_t w;     // word the pending bytes belong to
+  uint32_t nb;    // pending bytes (< 4)
+  uint64_t acc;
+  bool first;
+  __device__ __forceinline__ void init(uint32_t* base, uint32_t byte_off) {
+    img = base; w = byte_off >> 2; nb = byte_off & 3; acc = 0; first = true;
+  }
+  __device__ __forceinline__ void flush(uint32_t x) {
+    if (first) { atomicOr(img + w, x); first = false; }
+    else img[w] = x;
+    w++;
+  }
+  // k in 1..4 bytes of v (bytes above k zero)
+  __device__ __forceinline__ void app(uint32_t v, uint32_t k) {
+    acc |= (uint64_t)v << (8 * nb);
+    nb += k;
+    if (nb >= 4) { flush((uint32_t)acc); acc >>= 32; nb -= 4; }
+  }
+  __device__ __forceinline__ void app_int(int64_t v) {
+    uint64_t lo; uint32_t hi;
+    const uint32_t k = int_enc(v, lo, hi);
+    if (k <= 4) { app((uint32_t)lo, k); return; }
+    app((uint32_t)lo, 4);
+    app((uint32_t)(lo >> 32), 4 < k - 4 ? 4 : k - 4);
+    if (k == 9) app(hi, 1);
+  }
+  // len bytes from a 4-byte aligned source that may be read in whole words
+  __device__ __forceinline__ void app_words(const uint32_t* src, uint32_t len) {
+    uint32_t k = 0;
+    for (; k + 4 <= len; k += 4) app(src[k >> 2], 4);
+    if (k < len) app(src[k >> 2] & bmask(len - k), len - k);
+  }
+  __device__ __forceinline__ void finish() {
+    if (nb) atomicOr(img + w, (uint32_t)acc);
+  }
+};
+
+// writes a template record's value at image byte offset off (image zeroed beforehand)
+__device__ __forceinline__ void tmpl_write(const SerParams& P, const ValTmpl& T, const zb_rec& d, const uint8_t* pl,
+                                           uint32_t plen, uint32_t* img, uint32_t off) {
+  TW o;
+  o.init(img, off);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    o.app_words(P.tpool + (T.seg_off[k] >> 2), T.seg_len[k]);
+    const uint8_t v = T.var[k];
+    if (v == TV_INST) o.app_int(d.inst_key);
+    else if (v == TV_SCOPE) o.app_int(d.scope_key);
+    else if (v == TV_PAYLOAD) {
+      if (plen < 256) o.app(0xc4u | (plen << 8), 2);
+      else if (plen < 65536) o.app(0xc5u | ((uint32_t)__builtin_bswap16((uint16_t)plen) << 8), 3);
+      else { o.app(0xc6u, 1); o.app(__builtin_bswap32(plen), 4); }
+      o.app_words((const uint32_t*)pl, plen);  // arena blobs: 4-byte aligned data, padded to 8
+    }
+  }
+  o.finish();
+}
+
+// value size of record d (template or generic)
+__device__ __forceinline__ uint32_t value_size(const SerParams& P, int64_t pos, const zb_rec& d) {
+  const int ti = tmpl_index(P, d);
+  if (ti >= 0) return tmpl_size(P.tmpl[ti], d, *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8));
+  W w;
+  w.dst = nullptr;
+  w.n = 0;
+  encode_value(P, pos, d, w);
+  return w.n;
+}
+
+// zero image bytes [0, n) (n rounded up to 16) with 16-byte stores
+template <int NT>
+__device__ __forceinline__ void zero_image(uint8_t* img, uint64_t n) {
+  const uint64_t n16 = (n + 15) >> 4;
+  for (uint64_t c = threadIdx.x; c < n16; c += NT) *(uint4*)(img + 16 * c) = make_uint4(0, 0, 0, 0);
+}
+
 __global__ void __launch_bounds__(256) k_ser_size(SerParams P) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (P.lengths64 && i == P.count) P.lengths64[i] = 0;  // the scan over count + 1 entries ends in the total
   if (i >= P.count) return;
   const int64_t pos = P.start + i;
   const zb_rec d = P.log[pos];
-  W w;
-  w.dst = nullptr;
-  w.n = 0;
-  encode_value(P, pos, d, w);
-  if (P.lengths64) P.lengths64[i] = w.n;
-  else P.lengths[i] = w.n;
+  const uint32_t n = value_size(P, pos, d);
+  if (P.lengths64) P.lengths64[i] = n;
+  else P.lengths[i] = n;
 }
 
 // Write pass. Record i's value goes to out[offsets[i], offsets[i + 1]); the workgroup's records are one
@@ -275,17 +420,31 @@ __global__ void __launch_bounds__(SER_WG) k_ser_write(SerParams P) {
   const int64_t i = base + threadIdx.x;
   const int64_t last = (base + SER_WG < P.count) ? base + SER_WG : P.count;
   const uint64_t o0 = P.offsets[base], o1 = P.offsets[last];
+  if (P.out_cap && o1 > P.out_cap) {  // does not fit: the host grows the buffer and runs the pass again
+    if (threadIdx.x == 0) atomicOr(P.overflow, 1u);
+    return;
+  }
   const uint32_t shift = (uint32_t)(((uintptr_t)(P.out + o0)) & 15);
   const bool staged = (o1 - o0) + shift <= (uint64_t)SER_IMG;
+  if (staged) {  // template values merge their edge words into the image with OR: start from zero
+    zero_image<SER_WG>(img, shift + (o1 - o0) + 4);
+    __syncthreads();
+  }
   uint32_t pay = 0;
   if (i < P.count) {
     const int64_t pos = P.start + i;
     const zb_rec d = P.log[pos];
     const uint64_t off = P.offsets[i];
-    W w;
-    w.dst = staged ? img + shift + (off - o0) : P.out + off;
-    w.n = 0;
-    encode_value(P, pos, d, w);
+    const int ti = staged ? tmpl_index(P, d) : -1;
+    if (ti >= 0) {
+      const uint8_t* pp = P.arena + (uint64_t)d.payload * 8;
+      tmpl_write(P, P.tmpl[ti], d, pp + 4, *(const uint32_t*)pp, (uint32_t*)img, (uint32_t)(shift + (off - o0)));
+    } else {
+      W w;
+      w.dst = staged ? img + shift + (off - o0) : P.out + off;
+      w.n = 0;
+      encode_value(P, pos, d, w);
+    }
     if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay = *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
     zb_record_header h;
     h.position = pos;
@@ -299,7 +458,7 @@ __global__ void __launch_bounds__(SER_WG) k_ser_write(SerParams P) {
     // :477-479, :524-529, :571-573)
     h.rejection_type = kind_rt(d.kind) == ZB_RT_COMMAND_REJECTION
                            ? ((kind_vt(d.kind) == ZB_VT_WORKFLOW_INSTANCE && d.intent == WI_CREATE) ? 0 : 1) : 255;
-    h.value_length = w.n;
+    h.value_length = (uint32_t)(P.offsets[i + 1] - off);
     h.value_offset = off;
     P.headers[i] = h;
   }
@@ -361,11 +520,7 @@ __global__ void __launch_bounds__(SER_WG) k_ser_fused(SerParams P) {
   uint32_t len = 0;
   if (i < P.count) {
     d = P.log[P.start + i];
-    W w;
-    w.dst = nullptr;
-    w.n = 0;
-    encode_value(P, P.start + i, d, w);
-    len = w.n;
+    len = value_size(P, P.start + i, d);
   }
   // block exclusive scan of the lengths
   uint64_t x = len;
@@ -425,14 +580,24 @@ __global__ void __launch_bounds__(SER_WG) k_ser_fused(SerParams P) {
   }
   const uint32_t shift = (uint32_t)(((uintptr_t)(P.out + o0)) & 15);
   const bool staged = agg + shift <= (uint64_t)SER_IMG;
+  if (staged) {
+    zero_image<SER_WG>(img, shift + agg + 4);
+    __syncthreads();
+  }
   uint32_t pay = 0;
   if (i < P.count) {
     const int64_t pos = P.start + i;
     const uint64_t off = o0 + lo;
-    W w;
-    w.dst = staged ? img + shift + lo : P.out + off;
-    w.n = 0;
-    encode_value(P, pos, d, w);
+    const int ti = staged ? tmpl_index(P, d) : -1;
+    if (ti >= 0) {
+      const uint8_t* pp = P.arena + (uint64_t)d.payload * 8;
+      tmpl_write(P, P.tmpl[ti], d, pp + 4, *(const uint32_t*)pp, (uint32_t*)img, (uint32_t)(shift + lo));
+    } else {
+      W w;
+      w.dst = staged ? img + shift + lo : P.out + off;
+      w.n = 0;
+      encode_value(P, pos, d, w);
+    }
     if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay = *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
     zb_record_header h;
     h.position = pos;

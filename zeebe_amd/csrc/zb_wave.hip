@@ -53,13 +53,9 @@ struct TState {
   // stats
   uint32_t transitions, completed, created, merges, canceled;
   uint32_t merge_bytes, cond_bytes;
-  // open-subscription side effect (SubscribeMessageHandler), written to the outbox after processing
-  bool fx, fx_int;
-  uint8_t fx_ck_len;
-  uint16_t fx_elem;
-  uint32_t fx_row;
-  uint64_t fx_ck_at;  // arena byte offset of the correlation key string
-  int64_t fx_ival, fx_pos, fx_wik, fx_aik;
+  // a SUBSCRIBE_TO_INTERMEDIATE_MESSAGE step (SubscribeMessageHandler): k_subscribe does its side effect
+  bool sub;
+  int64_t sub_pos;
 };
 
 __device__ __forceinline__ void fail_at(TState& t, uint32_t flag, uint32_t site) {
@@ -313,30 +309,11 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
       break;
     }
     case ST_SUBSCRIBE_TO_INTERMEDIATE_MESSAGE: {  // SubscribeMessageHandler :77-141: a side effect, no record
-      const uint8_t* pp = P.arena + (uint64_t)rec.payload * 8;
-      const uint32_t len = *(const uint32_t*)pp;
-      QueryResult q;
-      if (!run_query(pp + 4, len, P.queries[el.ck_query], P.filters, P.pool, q)) { fail_at(t, DE_UNSUPPORTED, 30); return; }
-      // extractCorrelationKey :121-141: exactly one result, a string or a long, else the processor fails
-      if (q.count != 1) { fail_at(t, DE_PROCESSING, 31); return; }
-      Tok tk;
-      if (!read_tok(pp + 4 + q.pos, q.len, tk)) { fail_at(t, DE_PROCESSING, 32); return; }
-      if (tk.type == TT_STRING) {
-        t.fx_int = false;
-        t.fx_ck_at = (uint64_t)rec.payload * 8 + 4 + q.pos + tk.hdr;
-        t.fx_ck_len = tk.len > 255 ? 255 : (uint8_t)tk.len;
-        if (tk.len > ZB_XCHG_CK_MAX) { fail_at(t, DE_UNSUPPORTED, 33); return; }
-      } else if (tk.type == TT_INTEGER) {
-        t.fx_int = true;  // QueryResult.getLongAsBuffer: 8 bytes, native (little-endian) order
-        t.fx_ival = tk.ival;
-        t.fx_ck_len = 8;
-      } else {
-        fail_at(t, DE_PROCESSING, 34);  // "Failed to extract correlation-key: wrong type"
-        return;
-      }
-      if (el.msg_len > ZB_XCHG_NAME_MAX || t.fx) { fail_at(t, DE_UNSUPPORTED, 35); return; }
-      t.fx = true;
-      t.fx_pos = pos; t.fx_wik = rec.inst_key; t.fx_aik = rec.key; t.fx_elem = rec.elem; t.fx_row = rself;
+      // the correlation-key query and the open-subscription command run in k_subscribe, after this wave's
+      // k_process (no record of this step depends on them; a failure stops the partition either way)
+      if (t.sub) { fail_at(t, DE_UNSUPPORTED, 35); return; }
+      t.sub = true;
+      t.sub_pos = pos;
       break;
     }
     case ST_PARALLEL_SPLIT: {  // EXTENSION (C4): one SEQUENCE_FLOW_TAKEN per outgoing flow (k_emit writes them)
@@ -574,27 +551,59 @@ __device__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t p
   }
 }
 
-// The open-subscription command of a SUBSCRIBE step (SubscriptionCommandSender.openMessageSubscription
-// :83-103): routed to abs(hash(correlationKey) % P), ordered by the catch event's log position.
-__device__ void write_open(const WaveParams& P, const TState& t, uint32_t slot) {
-  if (slot >= P.ocap) { atomicOr(P.err, (uint32_t)DE_LOG_FULL); return; }
-  uint8_t ck[ZB_XCHG_CK_MAX];
-  if (t.fx_int) {
-    for (int i = 0; i < 8; i++) ck[i] = (uint8_t)((uint64_t)t.fx_ival >> (8 * i));
-  } else {
-    for (uint32_t i = 0; i < t.fx_ck_len; i++) ck[i] = P.arena[t.fx_ck_at + i];
+// The open-subscription command of a SUBSCRIBE step (SubscribeMessageHandler :77-141,
+// SubscriptionCommandSender.openMessageSubscription :83-103): the correlation key extracted from the
+// element instance's payload, routed to abs(hash(correlationKey) % P), ordered by the catch event's log
+// position. One thread per subscribe step of the wave (k_process listed them).
+__global__ void __launch_bounds__(256) k_subscribe(WaveParams P) {
+  const uint32_t n = P.sub_count[P.wave & 1];
+  for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < n && j < P.job_cap; j += (uint64_t)gridDim.x * 256) {
+    const int64_t pos = (int64_t)P.sub_jobs[j];
+    const zb_rec rec = P.log[pos];
+    const uint32_t rself = (uint32_t)P.links[pos];
+    const DevElem& el = P.elems[rec.elem];
+    uint32_t err = 0, site = 0;
+    const uint8_t* pp = P.arena + (uint64_t)rec.payload * 8;
+    const uint32_t len = *(const uint32_t*)pp;
+    QueryResult q;
+    Tok tk;
+    uint8_t ck[ZB_XCHG_CK_MAX];
+    uint32_t ck_len = 0;
+    if (!run_query(pp + 4, len, P.queries[el.ck_query], P.filters, P.pool, q)) { err = DE_UNSUPPORTED; site = 30; }
+    // extractCorrelationKey :121-141: exactly one result, a string or a long, else the processor fails
+    else if (q.count != 1) { err = DE_PROCESSING; site = 31; }
+    else if (!read_tok(pp + 4 + q.pos, q.len, tk)) { err = DE_PROCESSING; site = 32; }
+    else if (tk.type == TT_STRING) {
+      if (tk.len > ZB_XCHG_CK_MAX) { err = DE_UNSUPPORTED; site = 33; }
+      else {
+        ck_len = tk.len;
+        const uint8_t* src = pp + 4 + q.pos + tk.hdr;
+        for (uint32_t i = 0; i < ck_len; i++) ck[i] = src[i];
+      }
+    } else if (tk.type == TT_INTEGER) {  // QueryResult.getLongAsBuffer: 8 bytes, native (little-endian) order
+      ck_len = 8;
+      for (int i = 0; i < 8; i++) ck[i] = (uint8_t)((uint64_t)tk.ival >> (8 * i));
+    } else {
+      err = DE_PROCESSING; site = 34;  // "Failed to extract correlation-key: wrong type"
+    }
+    if (!err && el.msg_len > ZB_XCHG_NAME_MAX) { err = DE_UNSUPPORTED; site = 35; }
+    if (err) {
+      atomicOr(P.err, err);
+      atomicMin((unsigned long long*)P.err_info, ((unsigned long long)pos << 8) | site);
+      continue;
+    }
+    const uint32_t slot = atomicAdd(P.on, 1u);
+    if (slot >= P.ocap) { atomicOr(P.err, (uint32_t)DE_LOG_FULL); continue; }
+    const int32_t target = subscription_partition(ck, ck_len, P.partition_count);
+    zb_exchange_rec& r = P.obox[slot];
+    r.kind = ZB_XCHG_OPEN; r.target_partition = target; r.wf_partition = P.partition_id; r.token = rself;
+    r.workflow_instance_key = rec.inst_key; r.activity_instance_key = rec.key; r.source_position = pos;
+    r.elem = rec.elem; r.name_len = (uint8_t)el.msg_len; r.ck_len = (uint8_t)ck_len; r.payload_len = 0; r.pad = 0;
+    for (uint32_t i = 0; i < ZB_XCHG_NAME_MAX; i++) r.name[i] = i < el.msg_len ? P.pool[el.msg_off + i] : 0;
+    for (uint32_t i = 0; i < ZB_XCHG_CK_MAX; i++) r.ck[i] = i < ck_len ? ck[i] : 0;
+    for (uint32_t i = 0; i < ZB_XCHG_PAYLOAD_MAX; i++) r.payload[i] = 0;
+    P.okeys[slot] = outbox_key(target, pos, 0);
   }
-  const int32_t target = subscription_partition(ck, t.fx_ck_len, P.partition_count);
-  const DevElem& el = P.elems[t.fx_elem];
-  zb_exchange_rec r;
-  r.kind = ZB_XCHG_OPEN; r.target_partition = target; r.wf_partition = P.partition_id; r.token = t.fx_row;
-  r.workflow_instance_key = t.fx_wik; r.activity_instance_key = t.fx_aik; r.source_position = t.fx_pos;
-  r.elem = t.fx_elem; r.name_len = (uint8_t)el.msg_len; r.ck_len = t.fx_ck_len; r.payload_len = 0; r.pad = 0;
-  for (uint32_t i = 0; i < ZB_XCHG_NAME_MAX; i++) r.name[i] = i < el.msg_len ? P.pool[el.msg_off + i] : 0;
-  for (uint32_t i = 0; i < ZB_XCHG_CK_MAX; i++) r.ck[i] = i < t.fx_ck_len ? ck[i] : 0;
-  for (uint32_t i = 0; i < ZB_XCHG_PAYLOAD_MAX; i++) r.payload[i] = 0;
-  P.obox[slot] = r;
-  P.okeys[slot] = outbox_key(target, t.fx_pos, 0);
 }
 
 // ------------------------------------------------------------------------------ helpers
@@ -656,7 +665,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
     t.bytes = 0; t.merge = false; t.detail = false; t.err = 0; t.err_site = 0;
     t.transitions = t.completed = t.created = t.merges = t.canceled = 0;
     t.merge_bytes = t.cond_bytes = 0;
-    t.fx = false;
+    t.sub = false;
     t.nexp = 0; t.exp_ord = 0;
     uint32_t nconds = 0;
     const zb_rec rec = P.log[r];
@@ -699,9 +708,12 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
              ((uint64_t)t.completed << 48);
     acc_bytes += t.bytes;
     acc_created += t.created | (t.canceled << 16);
-    if (__ballot(t.fx)) {  // wave-uniform: open-subscription side effects of this tile
-      const uint32_t slot = wave_alloc(P.on, t.fx ? 1u : 0u);
-      if (t.fx) write_open(P, t, slot);
+    if (__ballot(t.sub)) {  // wave-uniform: this tile's subscribe steps, in the wave's job list
+      const uint32_t slot = wave_alloc(P.sub_count + (P.wave & 1), t.sub ? 1u : 0u);
+      if (t.sub) {
+        if (slot < P.job_cap) P.sub_jobs[slot] = (uint64_t)t.sub_pos;
+        else fail_at(t, DE_LOG_FULL, 36);
+      }
     }
     if (t.err) {
       atomicOr(P.err, t.err);
@@ -897,6 +909,7 @@ __global__ void __launch_bounds__(SCAN_WG) k_scan(WaveParams P) {
     *hout = h;
     if (P.need_children) *P.need_children = 0;  // k_pre of the next chunk sets it again
     P.merge_count[P.wave & 1] = c.n > 0 ? (uint32_t)tot[5] : 0;
+    if (P.sub_count) P.sub_count[(P.wave + 1) & 1] = 0;  // the next wave's subscribe list
     P.cond_count[P.wave & 1] = c.n > 0 ? (uint32_t)tot[6] : 0;
   }
 }
@@ -1054,6 +1067,9 @@ void launch_scan(const WaveParams& p, hipStream_t stream) {
 }
 void launch_emit(const WaveParams& p, hipStream_t stream) {
   hipLaunchKernelGGL(k_emit, dim3(p.grid), dim3(WG), 0, stream, p);
+}
+void launch_subscribe(const WaveParams& p, hipStream_t stream) {
+  hipLaunchKernelGGL(k_subscribe, dim3(256), dim3(256), 0, stream, p);
 }
 
 }  // namespace zbg
