@@ -14,7 +14,20 @@
 
 namespace zbg {
 
+// sum over the 256 threads of a workgroup, valid in thread 0 (statistics: one device atomic per workgroup
+// instead of one per thread -- same-address device atomics serialise)
+__device__ __forceinline__ unsigned long long wg_sum256(unsigned long long x, unsigned long long* s4) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_down(x, d, 64);
+  if ((threadIdx.x & 63) == 0) s4[threadIdx.x >> 6] = x;
+  __syncthreads();
+  const unsigned long long t = s4[0] + s4[1] + s4[2] + s4[3];
+  __syncthreads();
+  return t;
+}
+
 __global__ void __launch_bounds__(256) k_merge(WaveParams P) {
+  __shared__ unsigned long long s4[4];
   const uint32_t n = P.merge_count[P.wave & 1];
   const MergeJob* jobs = P.merge_jobs + (uint64_t)(P.wave & 1) * P.job_cap;
   uint32_t err = 0;
@@ -34,13 +47,16 @@ __global__ void __launch_bounds__(256) k_merge(WaveParams P) {
     bytes += ns + nt + o.n;
   }
   if (err) atomicOr(P.err, err);
-  if (merges) {
+  merges = wg_sum256(merges, s4);
+  bytes = wg_sum256(bytes, s4);
+  if (threadIdx.x == 0 && merges) {
     atomicAdd((unsigned long long*)&P.stats[3], merges);
     atomicAdd((unsigned long long*)&P.stats[4], bytes);
   }
 }
 
 __global__ void __launch_bounds__(256) k_cond(WaveParams P) {
+  __shared__ unsigned long long s4[4];
   const uint32_t n = P.cond_count[P.wave & 1];
   const uint64_t* jobs = P.cond_jobs + (uint64_t)(P.wave & 1) * P.job_cap;
   unsigned long long bytes = 0;
@@ -75,7 +91,8 @@ __global__ void __launch_bounds__(256) k_cond(WaveParams P) {
     uint32_t* link = (uint32_t*)(P.links + r);
     link[0] = dec;  // row-self half of the link; the scope half stays
   }
-  if (bytes) atomicAdd((unsigned long long*)&P.stats[5], bytes);
+  bytes = wg_sum256(bytes, s4);
+  if (threadIdx.x == 0 && bytes) atomicAdd((unsigned long long*)&P.stats[5], bytes);
 }
 
 void launch_merge(const WaveParams& p, hipStream_t s) {

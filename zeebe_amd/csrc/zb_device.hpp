@@ -190,22 +190,4 @@ struct RowAux {
 };
 static_assert(sizeof(RowAux) == 48, "RowAux is 48 bytes");
 
-// ---- record value templates (zb_serialize.hip) ----
-// The value of a WORKFLOW_INSTANCE / JOB / WORKFLOW_INSTANCE_SUBSCRIPTION record of one element is a
-// constant byte string with up to three variable fields (UnpackedObject.write over a fixed property set,
-// ObjectValue.java:140-153): segment 0, var 0, segment 1, var 1, segment 2, var 2. Built on the host at
-// deploy (zb_model.cpp build_value_templates), one per (element, template class).
-enum TmplClass : uint8_t { TC_WI = 0, TC_JOB = 1, TC_JOB_CANCEL = 2, TC_WIS = 3, TC_COUNT = 4 };
-enum TmplVar : uint8_t { TV_NONE = 0, TV_INST = 1, TV_SCOPE = 2, TV_PAYLOAD = 3 };
-struct ValTmpl {              // 40 bytes
-  uint32_t seg_off[3];        // in the template pool, 4-byte aligned, padded to a whole word
-  uint16_t seg_len[3];
-  uint8_t var[3];
-  uint8_t valid;
-  uint16_t pad0;
-  uint32_t const_len;         // sum of the segment lengths
-  uint32_t pad[3];
-};
-static_assert(sizeof(ValTmpl) == 40, "ValTmpl layout");
-
 }  // namespace zbg

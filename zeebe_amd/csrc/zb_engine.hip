@@ -59,7 +59,10 @@ struct DevVec {
 struct zb_engine {
   zb_config cfg{};
   hipStream_t stream = nullptr;
-  int32_t wave_grid_fixed = 0;  // ZB_WAVE_GRID (tuning experiments): fixed wave grid instead of the sized one
+  int32_t ncu = 256;            // compute units of the device
+  int32_t ser_grid = 0;         // drain write pass workgroups (ZB_SER_GRID; 0 = one per tile)
+  int32_t wave_grid_fixed = 0;
+  int32_t ser_exp = 0;          // ZB_SER_EXP: drain experiments (bit 0 no encode, 1 no value stores, 2 no headers)  // ZB_WAVE_GRID (tuning experiments): fixed wave grid instead of the sized one
   std::string err;
 
   ModelTables model;
@@ -71,11 +74,7 @@ struct zb_engine {
   DevVec<DevQuery> d_queries;
   DevVec<DevFilter> d_filters;
   DevVec<uint8_t> d_pool;
-  DevVec<ValTmpl> d_tmpl;        // record value templates (zb_model.cpp build_value_templates)
-  DevVec<uint8_t> d_tpool;
   int ser_mode = 0;              // ZB_SER_MODE: 0 = two passes (size, scan, write), 1 = single pass (look-back)
-  int ser_tmpl = 1;              // ZB_SER_TMPL=0: generic encoder only (A/B)
-  int32_t ntmpl_elems = 0;
 
   // device state
   zb_rec* log = nullptr;
@@ -210,7 +209,7 @@ struct zb_engine {
   DevVec<int64_t> d_lookup_keys, d_lookup_pos;
   // drain buffers (zb_serialize), grown on demand and reused
   uint64_t dr_cap = 0, dr_val_cap = 0, dr_tmp_cap = 0;
-  uint64_t *dr_len = nullptr, *dr_off = nullptr, *dr_tiles = nullptr;
+  uint64_t *dr_len = nullptr, *dr_off = nullptr, *dr_tiles = nullptr, *dr_pay = nullptr;
   zb_record_header* dr_hdr = nullptr;
   uint8_t* dr_val = nullptr;
   void* dr_tmp = nullptr;
@@ -256,14 +255,6 @@ int upload_model(zb_engine* e) {
   HIPCHECK(e, e->d_queries.upload(e->model.queries, e->stream));
   HIPCHECK(e, e->d_filters.upload(e->model.filters, e->stream));
   HIPCHECK(e, e->d_pool.upload(e->model.pool, e->stream));
-  {
-    std::vector<ValTmpl> tm;
-    std::vector<uint8_t> tp;
-    build_value_templates(e->model, tm, tp);
-    HIPCHECK(e, e->d_tmpl.upload(tm, e->stream));
-    HIPCHECK(e, e->d_tpool.upload(tp, e->stream));
-    e->ntmpl_elems = (int32_t)e->model.elems.size();
-  }
   if (e->static_blobs.size() > STATIC_ARENA_BYTES) return fail(e, ZB_ENOMEM, "static payload region full");
   HIPCHECK(e, hipMemcpyAsync(e->arena, e->static_blobs.data(), e->static_blobs.size(), hipMemcpyHostToDevice,
                              e->stream));
@@ -614,7 +605,8 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   auto* e = new zb_engine();
   e->cfg = *cfg;
   if (const char* m = std::getenv("ZB_SER_MODE")) e->ser_mode = std::strcmp(m, "fused") == 0 ? 1 : 0;
-  if (const char* m = std::getenv("ZB_SER_TMPL")) e->ser_tmpl = atoi(m) != 0;
+  if (const char* g = std::getenv("ZB_SER_GRID")) e->ser_grid = std::max(0, atoi(g));
+  if (const char* g = std::getenv("ZB_SER_EXP")) e->ser_exp = atoi(g);
   if (const char* g = std::getenv("ZB_WAVE_GRID")) e->wave_grid_fixed = std::max(0, std::min(atoi(g), (int)WAVE_GRID_MAX));
   if (e->cfg.log_capacity == 0) e->cfg.log_capacity = 1ull << 22;
   if (e->cfg.row_capacity == 0) e->cfg.row_capacity = 1ull << 20;
@@ -632,6 +624,11 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   };
   if (hipSetDevice(cfg->device) != hipSuccess) return cleanup(ZB_EDEVICE);
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return cleanup(ZB_EDEVICE);
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess && ncu > 0)
+      e->ncu = ncu;
+  }
   const uint64_t L = e->cfg.log_capacity;
   e->wave_cap = e->cfg.wave_records ? e->cfg.wave_records : std::min<uint64_t>(L, 1ull << 22);
   e->wave_cap = (e->wave_cap + WAVE_TILE - 1) / WAVE_TILE * WAVE_TILE;
@@ -701,9 +698,9 @@ void zb_engine_destroy(zb_engine* e) {
   if (e->h_err_pinned) (void)hipHostFree(e->h_err_pinned);
   if (e->h_ctl_pinned) (void)hipHostFree(e->h_ctl_pinned);
   e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_consts.free();
-  e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_tmpl.free(); e->d_tpool.free(); e->d_staged.free(); e->d_staged_arena.free();
+  e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
   e->d_ranges.free(); e->d_cmd_pool.free(); e->d_lookup_keys.free(); e->d_lookup_pos.free();
-  void* dr[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_val, e->dr_tmp, e->dr_total, e->dr_tiles};
+  void* dr[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_val, e->dr_tmp, e->dr_total, e->dr_tiles, e->dr_pay};
   for (void* p : dr)
     if (p) (void)hipFree(p);
   if (e->h_dr_total) (void)hipHostFree(e->h_dr_total);
@@ -1459,15 +1456,16 @@ int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats*
     HIPCHECK(e, hipHostMalloc(&e->h_dr_total, 4 * sizeof(uint64_t)));
   }
   if ((uint64_t)count > e->dr_cap) {
-    void* ps[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_tmp, e->dr_tiles};
+    void* ps[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_tmp, e->dr_tiles, e->dr_pay};
     for (void* q : ps)
       if (q) (void)hipFree(q);
-    e->dr_len = e->dr_off = e->dr_tiles = nullptr; e->dr_hdr = nullptr; e->dr_tmp = nullptr;
+    e->dr_len = e->dr_off = e->dr_tiles = e->dr_pay = nullptr; e->dr_hdr = nullptr; e->dr_tmp = nullptr;
     e->dr_cap = e->dr_tmp_cap = 0;
     const uint64_t cap = (uint64_t)count + (uint64_t)count / 4 + 1024;
     if (cap + 1 > (uint64_t)INT32_MAX) return fail(e, ZB_EUNSUPPORTED, "more than 2^31 records in one drain");
     HIPCHECK(e, hipMalloc(&e->dr_hdr, cap * sizeof(zb_record_header)));
     HIPCHECK(e, hipMalloc(&e->dr_tiles, (cap / 256 + 2) * sizeof(uint64_t)));  // single pass: tile states
+    HIPCHECK(e, hipMalloc(&e->dr_pay, (cap / 256 + 2) * sizeof(uint64_t)));    // payload bytes per tile
     HIPCHECK(e, hipMemset(e->dr_tiles, 0, (cap / 256 + 2) * sizeof(uint64_t)));
     HIPCHECK(e, hipMalloc(&e->dr_len, (cap + 1) * sizeof(uint64_t)));  // two passes: sizes, offsets
     HIPCHECK(e, hipMalloc(&e->dr_off, (cap + 1) * sizeof(uint64_t)));
@@ -1488,10 +1486,6 @@ int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats*
   SerParams sp{};
   sp.log = e->log;
   sp.arena = e->arena;
-  sp.tmpl = e->d_tmpl.p;
-  sp.tpool = (const uint32_t*)e->d_tpool.p;
-  sp.nelems = e->d_tmpl.p ? e->ntmpl_elems : 0;
-  sp.use_tmpl = e->ser_tmpl && e->d_tmpl.p ? 1 : 0;
   sp.elems = e->d_elems.p;
   sp.wfs = e->d_wfs.p;
   sp.queries = e->d_queries.p;
@@ -1503,6 +1497,7 @@ int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats*
   sp.count = count;
   sp.totals = e->dr_total;
   sp.tile_state = e->dr_tiles;
+  sp.pay_part = e->dr_pay;
   sp.tile_ctr = (uint32_t*)(e->dr_total + 2);
   sp.overflow = (uint32_t*)(e->dr_total + 2) + 1;
   sp.headers = e->dr_hdr;
@@ -1535,6 +1530,9 @@ int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats*
       HIPCHECK(e, hipEventRecord(e->dr_ev[2], e->stream));
       SerParams wr = sp;
       wr.offsets = e->dr_off;
+      wr.grid = e->ser_grid;
+      wr.exp = e->ser_exp;  // default one workgroup per tile (8.32 ms on C3 10M; 3 per CU persistent 11.2 ms,
+                              // 512 / 1024 workgroups 9.07 / 9.05 ms: profiles/r02/ser_grid_sweep.txt)
       launch_ser_write(wr, e->stream);
       HIPCHECK(e, hipEventRecord(e->dr_ev[3], e->stream));
     }

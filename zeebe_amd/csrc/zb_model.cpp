@@ -832,121 +832,4 @@ int compile_deployment(ModelTables& t, const std::string& xml, int64_t workflow_
   return rc;
 }
 
-// ------------------------------------------------------------------------------ value templates
-// Host mirror of the device writer (zb_serialize.hip W / MsgPackWriter.java:94-305); the GPU parity tests
-// compare every serialized value with the oracle's, so a divergence here fails them bit for bit.
-namespace {
-struct HostW {
-  std::vector<uint8_t> b;
-  void put(uint8_t x) { b.push_back(x); }
-  void map_hdr(uint32_t c) {
-    if (c < 16) put((uint8_t)(0x80 | c));
-    else { put(0xde); put((uint8_t)(c >> 8)); put((uint8_t)c); }
-  }
-  void str(const uint8_t* s, uint32_t c) {
-    if (c < 32) put((uint8_t)(0xa0 | c));
-    else if (c < 256) { put(0xd9); put((uint8_t)c); }
-    else if (c < 65536) { put(0xda); put((uint8_t)(c >> 8)); put((uint8_t)c); }
-    else { put(0xdb); for (int i = 3; i >= 0; i--) put((uint8_t)(c >> (8 * i))); }
-    b.insert(b.end(), s, s + c);
-  }
-  void key(const char* s) { str((const uint8_t*)s, (uint32_t)std::strlen(s)); }
-  void integer(int64_t v) {
-    if (v < -(1LL << 5)) {
-      if (v < -(1LL << 15)) {
-        if (v < -(1LL << 31)) { put(0xd3); for (int i = 7; i >= 0; i--) put((uint8_t)((uint64_t)v >> (8 * i))); }
-        else { put(0xd2); for (int i = 3; i >= 0; i--) put((uint8_t)((uint32_t)v >> (8 * i))); }
-      } else {
-        if (v < -(1 << 7)) { put(0xd1); put((uint8_t)((uint16_t)v >> 8)); put((uint8_t)v); }
-        else { put(0xd0); put((uint8_t)v); }
-      }
-    } else if (v < (1 << 7)) {
-      put((uint8_t)v);
-    } else if (v < (1LL << 16)) {
-      if (v < (1 << 8)) { put(0xcc); put((uint8_t)v); }
-      else { put(0xcd); put((uint8_t)(v >> 8)); put((uint8_t)v); }
-    } else if (v < (1LL << 32)) {
-      put(0xce); for (int i = 3; i >= 0; i--) put((uint8_t)(v >> (8 * i)));
-    } else {
-      put(0xcf); for (int i = 7; i >= 0; i--) put((uint8_t)((uint64_t)v >> (8 * i)));
-    }
-  }
-};
-}  // namespace
-
-void build_value_templates(const ModelTables& t, std::vector<ValTmpl>& tmpl, std::vector<uint8_t>& tpool) {
-  tmpl.assign(t.elems.size() * TC_COUNT, ValTmpl{});
-  tpool.clear();
-  const uint8_t* pool = t.pool.data();
-  for (size_t ei = 0; ei < t.elems.size(); ei++) {
-    const DevElem& e = t.elems[ei];
-    if (e.wf >= t.workflows.size()) continue;
-    const DevWorkflow& wf = t.workflows[e.wf];
-    for (int cls = 0; cls < TC_COUNT; cls++) {
-      HostW seg[3];
-      uint8_t var[3] = {TV_NONE, TV_NONE, TV_NONE};
-      if (cls == TC_WI) {  // WorkflowInstanceRecord.java:39-60
-        seg[0].map_hdr(7);
-        seg[0].key("bpmnProcessId"); seg[0].str(pool + wf.pid_off, wf.pid_len);
-        seg[0].key("version"); seg[0].integer(wf.version);
-        seg[0].key("workflowKey"); seg[0].integer(wf.key);
-        seg[0].key("workflowInstanceKey");
-        var[0] = TV_INST;
-        seg[1].key("activityId"); seg[1].str(pool + e.id_off, e.id_len);
-        seg[1].key("payload");
-        var[1] = TV_PAYLOAD;
-        seg[2].key("scopeInstanceKey");
-        var[2] = TV_SCOPE;
-      } else if (cls == TC_JOB || cls == TC_JOB_CANCEL) {  // JobRecord.java:35-53, JobHeaders.java:33-51
-        const bool cancel = cls == TC_JOB_CANCEL;  // TerminateServiceTaskHandler :37-58: a reset JobRecord
-        seg[0].map_hdr(7);
-        seg[0].key("deadline"); seg[0].integer(INT64_MIN);
-        seg[0].key("worker"); seg[0].str(nullptr, 0);
-        seg[0].key("retries"); seg[0].integer(cancel ? -1 : e.retries);
-        seg[0].key("type");
-        if (cancel) seg[0].str(nullptr, 0); else seg[0].str(pool + e.type_off, e.type_len);
-        seg[0].key("headers");
-        seg[0].map_hdr(6);
-        seg[0].key("bpmnProcessId"); seg[0].str(pool + wf.pid_off, wf.pid_len);
-        seg[0].key("workflowDefinitionVersion"); seg[0].integer(wf.version);
-        seg[0].key("workflowKey"); seg[0].integer(cancel ? -1 : wf.key);
-        seg[0].key("workflowInstanceKey");
-        var[0] = TV_INST;
-        seg[1].key("activityId"); seg[1].str(pool + e.id_off, e.id_len);
-        seg[1].key("activityInstanceKey");
-        var[1] = TV_SCOPE;
-        seg[2].key("customHeaders");
-        if (cancel || e.headers_off == NO_REF) seg[2].put(0x80);  // JobRecord.NO_HEADERS
-        else seg[2].b.insert(seg[2].b.end(), pool + e.headers_off, pool + e.headers_off + e.headers_len);
-        seg[2].key("payload");
-        if (cancel) { seg[2].put(0xc4); seg[2].put(1); seg[2].put(0x80); }
-        else var[2] = TV_PAYLOAD;
-      } else {  // TC_WIS: WorkflowInstanceSubscriptionRecord.java:26-38
-        seg[0].map_hdr(4);
-        seg[0].key("workflowInstanceKey");
-        var[0] = TV_INST;
-        seg[1].key("activityInstanceKey");
-        var[1] = TV_SCOPE;
-        seg[2].key("messageName"); seg[2].str(pool + e.msg_off, e.msg_len);
-        seg[2].key("payload");
-        var[2] = TV_PAYLOAD;
-      }
-      ValTmpl& v = tmpl[ei * TC_COUNT + cls];
-      v.const_len = 0;
-      bool ok = true;
-      for (int k = 0; k < 3; k++) {
-        if (seg[k].b.size() > 0xffff) ok = false;
-        v.seg_off[k] = (uint32_t)tpool.size();
-        v.seg_len[k] = (uint16_t)seg[k].b.size();
-        v.var[k] = var[k];
-        v.const_len += (uint32_t)seg[k].b.size();
-        tpool.insert(tpool.end(), seg[k].b.begin(), seg[k].b.end());
-        tpool.resize((tpool.size() + 7) & ~(size_t)3, 0);  // 4-aligned, at least one spare word
-      }
-      v.valid = ok ? 1 : 0;
-    }
-  }
-  if (tpool.empty()) tpool.resize(8, 0);
-}
-
 }  // namespace zbg

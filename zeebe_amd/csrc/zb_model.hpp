@@ -46,7 +46,4 @@ int compile_query(ModelTables& t, const std::string& expr, std::string& err);
 // json-el compilation; returns program offset in t.code or -1 (err set)
 int compile_condition(ModelTables& t, const std::string& expr, std::string& err);
 
-// Record value templates of every element (ValTmpl, zb_device.hpp): index elem * TC_COUNT + class.
-void build_value_templates(const ModelTables& t, std::vector<ValTmpl>& tmpl, std::vector<uint8_t>& tpool);
-
 }  // namespace zbg

@@ -7,6 +7,8 @@
 // Integer encoding is MsgPackWriter.writeInteger (msgpack-core/.../spec/MsgPackWriter.java:143-201).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "zb_devlib.hpp"
 #include "zb_kernels.hpp"
 
@@ -247,152 +249,15 @@ __device__ inline void encode_value(const SerParams& P, int64_t pos, const zb_re
   }
 }
 
-// ------------------------------------------------------------------------------ template encoder
-// The common records (WORKFLOW_INSTANCE, JOB, WORKFLOW_INSTANCE_SUBSCRIPTION of a deployed element) are a
-// constant template with three variable fields (ValTmpl). Sizing is a handful of integer ops; writing
-// assembles whole 32-bit words in a register and stores them to the zeroed LDS image: interior words of a
-// value belong to one thread (plain ds_write_b32), the first and last words may be shared with the
-// neighbouring values and are merged with ds_or_b32.
-__device__ __forceinline__ uint32_t bmask(uint32_t k) { return k >= 4 ? 0xffffffffu : ((1u << (8 * k)) - 1u); }
-
-// MsgPackWriter.writeInteger (W::integer above) as up to 9 stream-order bytes: lo = bytes 0..7, hi = byte 8
-__device__ __forceinline__ uint32_t int_enc(int64_t v, uint64_t& lo, uint32_t& hi) {
-  hi = 0;
-  if (v < -(1LL << 5)) {
-    if (v < -(1LL << 15)) {
-      if (v < -(1LL << 31)) {
-        const uint64_t b = __builtin_bswap64((uint64_t)v);
-        lo = 0xd3ull | (b << 8); hi = (uint32_t)(b >> 56); return 9;
-      }
-      lo = 0xd2ull | ((uint64_t)__builtin_bswap32((uint32_t)v) << 8); return 5;
-    }
-    if (v < -(1 << 7)) { lo = 0xd1ull | ((uint64_t)__builtin_bswap16((uint16_t)v) << 8); return 3; }
-    lo = 0xd0ull | ((uint64_t)(uint8_t)v << 8); return 2;
-  }
-  if (v < (1 << 7)) { lo = (uint64_t)(uint8_t)v; return 1; }
-  if (v < (1LL << 16)) {
-    if (v < (1 << 8)) { lo = 0xccull | ((uint64_t)v << 8); return 2; }
-    lo = 0xcdull | ((uint64_t)__builtin_bswap16((uint16_t)v) << 8); return 3;
-  }
-  if (v < (1LL << 32)) { lo = 0xceull | ((uint64_t)__builtin_bswap32((uint32_t)v) << 8); return 5; }
-  const uint64_t b = __builtin_bswap64((uint64_t)v);
-  lo = 0xcfull | (b << 8); hi = (uint32_t)(b >> 56); return 9;
-}
-__device__ __forceinline__ uint32_t int_len(int64_t v) {
-  if (v < -(1LL << 5)) return v < -(1LL << 15) ? (v < -(1LL << 31) ? 9 : 5) : (v < -(1 << 7) ? 3 : 2);
-  if (v < (1 << 7)) return 1;
-  if (v < (1LL << 16)) return v < (1 << 8) ? 2 : 3;
-  return v < (1LL << 32) ? 5 : 9;
-}
-__device__ __forceinline__ uint32_t bin_hdr_len(uint32_t n) { return n < 256 ? 2 : (n < 65536 ? 3 : 5); }
-
-// template index of a record, or -1 (generic encoder)
-__device__ __forceinline__ int tmpl_index(const SerParams& P, const zb_rec& d) {
-  if (!P.use_tmpl || (d.kind & KIND_RAW) || d.elem >= (uint32_t)P.nelems) return -1;
-  const uint8_t vt = kind_vt(d.kind), rt = kind_rt(d.kind);
-  int cls;
-  if (vt == ZB_VT_WORKFLOW_INSTANCE) {
-    if (d.intent == WI_CREATE && (rt == ZB_RT_COMMAND || rt == ZB_RT_COMMAND_REJECTION)) return -1;
-    cls = TC_WI;
-  } else if (vt == ZB_VT_JOB) {
-    cls = d.intent == JI_CANCEL ? TC_JOB_CANCEL : TC_JOB;
-  } else if (vt == ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION) {
-    cls = TC_WIS;
-  } else {
-    return -1;
-  }
-  const int idx = (int)d.elem * TC_COUNT + cls;
-  return P.tmpl[idx].valid ? idx : -1;
-}
-
-__device__ __forceinline__ uint32_t tmpl_size(const ValTmpl& T, const zb_rec& d, uint32_t plen) {
-  uint32_t n = T.const_len;
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    const uint8_t v = T.var[k];
-    if (v == TV_INST) n += int_len(d.inst_key);
-    else if (v == TV_SCOPE) n += int_len(d.scope_key);
-    else if (v == TV_PAYLOAD) n += bin_hdr_len(plen) + plen;
-  }
-  return n;
-}
-
-struct TW {
-  uint32_t* img;  // LDS image (zeroed), word addressed
-  uint32_t w;     // word the pending bytes belong to
-  uint32_t nb;    // pending bytes (< 4)
-  uint64_t acc;
-  bool first;
-  __device__ __forceinline__ void init(uint32_t* base, uint32_t byte_off) {
-    img = base; w = byte_off >> 2; nb = byte_off & 3; acc = 0; first = true;
-  }
-  __device__ __forceinline__ void flush(uint32_t x) {
-    if (first) { atomicOr(img + w, x); first = false; }
-    else img[w] = x;
-    w++;
-  }
-  // k in 1..4 bytes of v (bytes above k zero)
-  __device__ __forceinline__ void app(uint32_t v, uint32_t k) {
-    acc |= (uint64_t)v << (8 * nb);
-    nb += k;
-    if (nb >= 4) { flush((uint32_t)acc); acc >>= 32; nb -= 4; }
-  }
-  __device__ __forceinline__ void app_int(int64_t v) {
-    uint64_t lo; uint32_t hi;
-    const uint32_t k = int_enc(v, lo, hi);
-    if (k <= 4) { app((uint32_t)lo, k); return; }
-    app((uint32_t)lo, 4);
-    app((uint32_t)(lo >> 32), 4 < k - 4 ? 4 : k - 4);
-    if (k == 9) app(hi, 1);
-  }
-  // len bytes from a 4-byte aligned source that may be read in whole words
-  __device__ __forceinline__ void app_words(const uint32_t* src, uint32_t len) {
-    uint32_t k = 0;
-    for (; k + 4 <= len; k += 4) app(src[k >> 2], 4);
-    if (k < len) app(src[k >> 2] & bmask(len - k), len - k);
-  }
-  __device__ __forceinline__ void finish() {
-    if (nb) atomicOr(img + w, (uint32_t)acc);
-  }
-};
-
-// writes a template record's value at image byte offset off (image zeroed beforehand)
-__device__ __forceinline__ void tmpl_write(const SerParams& P, const ValTmpl& T, const zb_rec& d, const uint8_t* pl,
-                                           uint32_t plen, uint32_t* img, uint32_t off) {
-  TW o;
-  o.init(img, off);
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    o.app_words(P.tpool + (T.seg_off[k] >> 2), T.seg_len[k]);
-    const uint8_t v = T.var[k];
-    if (v == TV_INST) o.app_int(d.inst_key);
-    else if (v == TV_SCOPE) o.app_int(d.scope_key);
-    else if (v == TV_PAYLOAD) {
-      if (plen < 256) o.app(0xc4u | (plen << 8), 2);
-      else if (plen < 65536) o.app(0xc5u | ((uint32_t)__builtin_bswap16((uint16_t)plen) << 8), 3);
-      else { o.app(0xc6u, 1); o.app(__builtin_bswap32(plen), 4); }
-      o.app_words((const uint32_t*)pl, plen);  // arena blobs: 4-byte aligned data, padded to 8
-    }
-  }
-  o.finish();
-}
-
-// value size of record d (template or generic)
+// value size of record d. (Host-built value templates -- constant segments copied as whole words into the
+// image -- were measured slower than this encoder on C3 10M: 8.9 vs 8.3 ms write pass, 1.40 G vs 1.06 G VALU
+// instructions; the constant keys here compile to immediate stores. profiles/r02/pmc_c3g.json)
 __device__ __forceinline__ uint32_t value_size(const SerParams& P, int64_t pos, const zb_rec& d) {
-  const int ti = tmpl_index(P, d);
-  if (ti >= 0) return tmpl_size(P.tmpl[ti], d, *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8));
   W w;
   w.dst = nullptr;
   w.n = 0;
   encode_value(P, pos, d, w);
   return w.n;
-}
-
-// zero image bytes [0, n) (n rounded up to 16) with 16-byte stores
-template <int NT>
-__device__ __forceinline__ void zero_image(uint8_t* img, uint64_t n) {
-  const uint64_t n16 = (n + 15) >> 4;
-  for (uint64_t c = threadIdx.x; c < n16; c += NT) *(uint4*)(img + 16 * c) = make_uint4(0, 0, 0, 0);
 }
 
 __global__ void __launch_bounds__(256) k_ser_size(SerParams P) {
@@ -413,81 +278,122 @@ __global__ void __launch_bounds__(256) k_ser_size(SerParams P) {
 constexpr int SER_WG = 256;
 constexpr int SER_IMG = 48 * 1024;  // three workgroups per CU
 
+__device__ __forceinline__ zb_record_header record_header(const zb_rec& d, int64_t pos, uint32_t len, uint64_t off) {
+  zb_record_header h;
+  h.position = pos;
+  h.source_position = -1;
+  h.key = d.key;
+  h.record_type = kind_rt(d.kind);
+  h.value_type = kind_vt(d.kind);
+  h.intent = d.intent;
+  // RejectionType: CREATE of an unknown workflow -> BAD_VALUE (0); CORRELATE of an absent activity, CANCEL /
+  // UPDATE_PAYLOAD of an instance that is not running -> NOT_APPLICABLE (1) (WorkflowInstanceStreamProcessor.java
+  // :477-479, :524-529, :571-573)
+  h.rejection_type = kind_rt(d.kind) == ZB_RT_COMMAND_REJECTION
+                         ? ((kind_vt(d.kind) == ZB_VT_WORKFLOW_INSTANCE && d.intent == WI_CREATE) ? 0 : 1) : 255;
+  h.value_length = len;
+  h.value_offset = off;
+  return h;
+}
+
+// Write pass, persistent: SER_WG-record tiles are dealt round-robin to a grid sized to the resident
+// workgroups (the LDS image allows three per CU), so workgroup launch never paces the pass (one short-lived
+// workgroup per tile kept the CUs at ~2.8 resident waves: profiles/r02/pmc_c3_10000000.json). While a tile is
+// encoded, the next tile's descriptors and offsets are already in flight, and its payload headers are touched
+// once they have arrived.
 __global__ void __launch_bounds__(SER_WG) k_ser_write(SerParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t img[SER_IMG + 16];
   __shared__ unsigned long long s_pay[SER_WG / 64];
-  const int64_t base = (int64_t)blockIdx.x * SER_WG;
-  const int64_t i = base + threadIdx.x;
-  const int64_t last = (base + SER_WG < P.count) ? base + SER_WG : P.count;
-  const uint64_t o0 = P.offsets[base], o1 = P.offsets[last];
-  if (P.out_cap && o1 > P.out_cap) {  // does not fit: the host grows the buffer and runs the pass again
-    if (threadIdx.x == 0) atomicOr(P.overflow, 1u);
-    return;
-  }
-  const uint32_t shift = (uint32_t)(((uintptr_t)(P.out + o0)) & 15);
-  const bool staged = (o1 - o0) + shift <= (uint64_t)SER_IMG;
-  if (staged) {  // template values merge their edge words into the image with OR: start from zero
-    zero_image<SER_WG>(img, shift + (o1 - o0) + 4);
-    __syncthreads();
-  }
-  uint32_t pay = 0;
-  if (i < P.count) {
-    const int64_t pos = P.start + i;
-    const zb_rec d = P.log[pos];
-    const uint64_t off = P.offsets[i];
-    const int ti = staged ? tmpl_index(P, d) : -1;
-    if (ti >= 0) {
-      const uint8_t* pp = P.arena + (uint64_t)d.payload * 8;
-      tmpl_write(P, P.tmpl[ti], d, pp + 4, *(const uint32_t*)pp, (uint32_t*)img, (uint32_t)(shift + (off - o0)));
-    } else {
+  const int64_t ntiles = (P.count + SER_WG - 1) / SER_WG;
+  int64_t tile = blockIdx.x;
+  // prefetched state of the next tile
+  zb_rec nd{};
+  uint64_t noff = 0, no0 = 0, no1 = 0;
+  auto fetch = [&](int64_t t) {
+    const int64_t base = t * SER_WG;
+    const int64_t last = (base + SER_WG < P.count) ? base + SER_WG : P.count;
+    const int64_t i = base + threadIdx.x;
+    no0 = P.offsets[base];
+    no1 = P.offsets[last];
+    if (i < P.count) {
+      nd = P.log[P.start + i];
+      noff = P.offsets[i];
+    }
+  };
+  if (tile < ntiles) fetch(tile);
+  unsigned long long pay_acc = 0;
+  for (; tile < ntiles; tile += gridDim.x) {
+    const zb_rec d = nd;
+    const uint64_t off = noff, o0 = no0, o1 = no1;
+    const int64_t base = tile * SER_WG;
+    const int64_t i = base + threadIdx.x;
+    const bool live = i < P.count;
+    const bool more = tile + gridDim.x < ntiles;
+    if (more) fetch(tile + gridDim.x);
+    if (P.out_cap && o1 > P.out_cap) {  // does not fit: the host grows the buffer and runs the pass again
+      if (threadIdx.x == 0) atomicOr(P.overflow, 1u);
+      continue;  // uniform over the workgroup
+    }
+    const uint32_t shift = (uint32_t)(((uintptr_t)(P.out + o0)) & 15);
+    const bool staged = (o1 - o0) + shift <= (uint64_t)SER_IMG;
+    if (live) {
+      const int64_t pos = P.start + i;
       W w;
       w.dst = staged ? img + shift + (off - o0) : P.out + off;
       w.n = 0;
-      encode_value(P, pos, d, w);
+      if (!(P.exp & 1)) encode_value(P, pos, d, w);
+      if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay_acc += *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
+      if (!(P.exp & 4)) P.headers[i] = record_header(d, pos, (uint32_t)(P.offsets[i + 1] - off), off);
     }
-    if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay = *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
-    zb_record_header h;
-    h.position = pos;
-    h.source_position = -1;
-    h.key = d.key;
-    h.record_type = kind_rt(d.kind);
-    h.value_type = kind_vt(d.kind);
-    h.intent = d.intent;
-    // RejectionType: CREATE of an unknown workflow -> BAD_VALUE (0); CORRELATE of an absent activity, CANCEL /
-    // UPDATE_PAYLOAD of an instance that is not running -> NOT_APPLICABLE (1) (WorkflowInstanceStreamProcessor.java
-    // :477-479, :524-529, :571-573)
-    h.rejection_type = kind_rt(d.kind) == ZB_RT_COMMAND_REJECTION
-                           ? ((kind_vt(d.kind) == ZB_VT_WORKFLOW_INSTANCE && d.intent == WI_CREATE) ? 0 : 1) : 255;
-    h.value_length = (uint32_t)(P.offsets[i + 1] - off);
-    h.value_offset = off;
-    P.headers[i] = h;
+    // touch the next tile's payload header (its descriptor has arrived by now): the encode finds it cached
+    if (more && base + (int64_t)gridDim.x * SER_WG + threadIdx.x < P.count) {
+      const uint32_t t = *(const volatile uint32_t*)(P.arena + (uint64_t)nd.payload * 8);
+      (void)t;
+    }
+    __syncthreads();
+    if (staged && !(P.exp & 2)) {
+      // stream the image out: img[shift + k] -> out[o0 + k], k in [0, n); out + o0 - shift is 16-byte aligned
+      const uint64_t n = o1 - o0;
+      uint8_t* dst = P.out + o0 - shift;
+      const uint64_t lim = shift + n;  // image bytes [shift, lim) are ours
+      const uint64_t full_lo = (shift + 15) & ~15ull, full_hi = lim & ~15ull;
+      for (uint64_t c = full_lo + 16 * threadIdx.x; c < full_hi; c += 16 * SER_WG)
+        *(uint4*)(dst + c) = *(const uint4*)(img + c);
+      const uint64_t head_end = full_lo < lim ? full_lo : lim;
+      for (uint64_t c = shift + threadIdx.x; c < head_end; c += SER_WG) dst[c] = img[c];
+      const uint64_t tail_lo = full_hi > head_end ? full_hi : head_end;
+      for (uint64_t c = tail_lo + threadIdx.x; c < lim; c += SER_WG) dst[c] = img[c];
+      __syncthreads();  // the image is reused by the next tile
+    }
   }
   if (P.totals) {
-    unsigned long long x = pay;
-    for (int dd = 32; dd >= 1; dd >>= 1) x += __shfl_down(x, dd, 64);
-    if ((threadIdx.x & 63) == 0) s_pay[threadIdx.x >> 6] = x;
+    unsigned long long y = pay_acc;
+    for (int dd = 32; dd >= 1; dd >>= 1) y += __shfl_down(y, dd, 64);
+    if ((threadIdx.x & 63) == 0) s_pay[threadIdx.x >> 6] = y;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long tt = 0;
+      for (int k = 0; k < SER_WG / 64; k++) tt += s_pay[k];
+      // one partial per workgroup, reduced by k_ser_sum: 400k same-address device atomics serialised the
+      // pass (~3 ms of an 8.8 ms write pass on C3 10M, profiles/r02/ser_grid_sweep.txt)
+      P.pay_part[blockIdx.x] = tt;
+    }
   }
+}
+
+// payload-byte total of the write pass (one workgroup)
+__global__ void __launch_bounds__(1024) k_ser_sum(SerParams P, int64_t nparts) {
+  __shared__ unsigned long long s[16];
+  unsigned long long x = 0;
+  for (int64_t k = threadIdx.x; k < nparts; k += 1024) x += P.pay_part[k];
+  for (int dd = 32; dd >= 1; dd >>= 1) x += __shfl_down(x, dd, 64);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = x;
   __syncthreads();
-  if (P.totals && threadIdx.x == 0) {
+  if (threadIdx.x == 0) {
     unsigned long long t = 0;
-    for (int k = 0; k < SER_WG / 64; k++) t += s_pay[k];
-    if (t) atomicAdd((unsigned long long*)&P.totals[1], t);
+    for (int k = 0; k < 16; k++) t += s[k];
+    P.totals[1] = t;
   }
-  if (!staged) return;
-  // stream the image out: img[shift + k] -> out[o0 + k], k in [0, n); out + o0 - shift is 16-byte aligned
-  const uint64_t n = o1 - o0;
-  uint8_t* dst = P.out + o0 - shift;
-  const uint64_t lim = shift + n;  // image bytes [shift, lim) are ours
-  const uint64_t full_lo = (shift + 15) & ~15ull, full_hi = lim & ~15ull;
-  if (full_lo < full_hi) {
-    for (uint64_t c = full_lo + 16 * threadIdx.x; c < full_hi; c += 16 * SER_WG)
-      *(uint4*)(dst + c) = *(const uint4*)(img + c);
-  }
-  // partial head / tail bytes
-  const uint64_t head_end = full_lo < lim ? full_lo : lim;
-  for (uint64_t c = shift + threadIdx.x; c < head_end; c += SER_WG) dst[c] = img[c];
-  const uint64_t tail_lo = full_hi > head_end ? full_hi : head_end;
-  for (uint64_t c = tail_lo + threadIdx.x; c < lim; c += SER_WG) dst[c] = img[c];
 }
 
 // ------------------------------------------------------------------------------ single pass (zb_serialize)
@@ -580,37 +486,16 @@ __global__ void __launch_bounds__(SER_WG) k_ser_fused(SerParams P) {
   }
   const uint32_t shift = (uint32_t)(((uintptr_t)(P.out + o0)) & 15);
   const bool staged = agg + shift <= (uint64_t)SER_IMG;
-  if (staged) {
-    zero_image<SER_WG>(img, shift + agg + 4);
-    __syncthreads();
-  }
   uint32_t pay = 0;
   if (i < P.count) {
     const int64_t pos = P.start + i;
     const uint64_t off = o0 + lo;
-    const int ti = staged ? tmpl_index(P, d) : -1;
-    if (ti >= 0) {
-      const uint8_t* pp = P.arena + (uint64_t)d.payload * 8;
-      tmpl_write(P, P.tmpl[ti], d, pp + 4, *(const uint32_t*)pp, (uint32_t*)img, (uint32_t)(shift + lo));
-    } else {
-      W w;
-      w.dst = staged ? img + shift + lo : P.out + off;
-      w.n = 0;
-      encode_value(P, pos, d, w);
-    }
+    W w;
+    w.dst = staged ? img + shift + lo : P.out + off;
+    w.n = 0;
+    encode_value(P, pos, d, w);
     if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay = *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
-    zb_record_header h;
-    h.position = pos;
-    h.source_position = -1;
-    h.key = d.key;
-    h.record_type = kind_rt(d.kind);
-    h.value_type = kind_vt(d.kind);
-    h.intent = d.intent;
-    h.rejection_type = kind_rt(d.kind) == ZB_RT_COMMAND_REJECTION
-                           ? ((kind_vt(d.kind) == ZB_VT_WORKFLOW_INSTANCE && d.intent == WI_CREATE) ? 0 : 1) : 255;
-    h.value_length = len;
-    h.value_offset = off;
-    P.headers[i] = h;
+    P.headers[i] = record_header(d, pos, len, off);
   }
   if (P.totals) {
     unsigned long long y = pay;
@@ -621,7 +506,7 @@ __global__ void __launch_bounds__(SER_WG) k_ser_fused(SerParams P) {
   if (P.totals && threadIdx.x == 0) {
     unsigned long long tt = 0;
     for (int k = 0; k < SER_WG / 64; k++) tt += s_pay[k];
-    if (tt) atomicAdd((unsigned long long*)&P.totals[1], tt);
+    P.pay_part[t] = tt;  // reduced by k_ser_sum
   }
   if (!staged) return;
   uint8_t* dst = P.out + o0 - shift;
@@ -637,7 +522,9 @@ __global__ void __launch_bounds__(SER_WG) k_ser_fused(SerParams P) {
 
 void launch_ser_fused(const SerParams& p, hipStream_t s) {
   if (p.count <= 0) return;
-  hipLaunchKernelGGL(k_ser_fused, dim3((unsigned)((p.count + SER_WG - 1) / SER_WG)), dim3(SER_WG), 0, s, p);
+  const int64_t tiles = (p.count + SER_WG - 1) / SER_WG;
+  hipLaunchKernelGGL(k_ser_fused, dim3((unsigned)tiles), dim3(SER_WG), 0, s, p);
+  if (p.totals) hipLaunchKernelGGL(k_ser_sum, dim3(1), dim3(1024), 0, s, p, tiles);
 }
 
 void launch_ser_size(const SerParams& p, hipStream_t s) {
@@ -647,7 +534,10 @@ void launch_ser_size(const SerParams& p, hipStream_t s) {
 }
 void launch_ser_write(const SerParams& p, hipStream_t s) {
   if (p.count <= 0) return;
-  hipLaunchKernelGGL(k_ser_write, dim3((unsigned)((p.count + SER_WG - 1) / SER_WG)), dim3(SER_WG), 0, s, p);
+  const int64_t tiles = (p.count + SER_WG - 1) / SER_WG;
+  const int64_t grid = p.grid > 0 ? std::min<int64_t>(tiles, p.grid) : tiles;
+  hipLaunchKernelGGL(k_ser_write, dim3((unsigned)grid), dim3(SER_WG), 0, s, p);
+  if (p.totals) hipLaunchKernelGGL(k_ser_sum, dim3(1), dim3(1024), 0, s, p, grid);
 }
 
 // ------------------------------------------------------------------------------ input injection

@@ -592,7 +592,7 @@ __global__ void __launch_bounds__(256) k_subscribe(WaveParams P) {
       atomicMin((unsigned long long*)P.err_info, ((unsigned long long)pos << 8) | site);
       continue;
     }
-    const uint32_t slot = atomicAdd(P.on, 1u);
+    const uint32_t slot = wave_alloc(P.on, 1u);  // one device atomic per wave
     if (slot >= P.ocap) { atomicOr(P.err, (uint32_t)DE_LOG_FULL); continue; }
     const int32_t target = subscription_partition(ck, ck_len, P.partition_count);
     zb_exchange_rec& r = P.obox[slot];
