@@ -60,9 +60,7 @@ struct zb_engine {
   zb_config cfg{};
   hipStream_t stream = nullptr;
   int32_t ncu = 256;            // compute units of the device
-  int32_t ser_grid = 0;         // drain write pass workgroups (ZB_SER_GRID; 0 = one per tile)
-  int32_t wave_grid_fixed = 0;
-  int32_t ser_exp = 0;          // ZB_SER_EXP: drain experiments (bit 0 no encode, 1 no value stores, 2 no headers)  // ZB_WAVE_GRID (tuning experiments): fixed wave grid instead of the sized one
+  int32_t wave_grid_fixed = 0;  // ZB_WAVE_GRID (tuning experiments): fixed wave grid instead of the sized one
   std::string err;
 
   ModelTables model;
@@ -605,8 +603,6 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   auto* e = new zb_engine();
   e->cfg = *cfg;
   if (const char* m = std::getenv("ZB_SER_MODE")) e->ser_mode = std::strcmp(m, "fused") == 0 ? 1 : 0;
-  if (const char* g = std::getenv("ZB_SER_GRID")) e->ser_grid = std::max(0, atoi(g));
-  if (const char* g = std::getenv("ZB_SER_EXP")) e->ser_exp = atoi(g);
   if (const char* g = std::getenv("ZB_WAVE_GRID")) e->wave_grid_fixed = std::max(0, std::min(atoi(g), (int)WAVE_GRID_MAX));
   if (e->cfg.log_capacity == 0) e->cfg.log_capacity = 1ull << 22;
   if (e->cfg.row_capacity == 0) e->cfg.row_capacity = 1ull << 20;
@@ -1498,6 +1494,14 @@ int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats*
   sp.totals = e->dr_total;
   sp.tile_state = e->dr_tiles;
   sp.pay_part = e->dr_pay;
+  sp.n_elems = (int32_t)e->model.elems.size();
+  sp.n_wfs = (int32_t)e->model.workflows.size();
+  sp.pool_len = (uint32_t)e->model.pool.size();
+  {
+    const uint64_t need = ((sp.n_elems * sizeof(DevElem) + 15) & ~15ull) + ((sp.n_wfs * sizeof(DevWorkflow) + 15) & ~15ull) +
+                          sp.pool_len;
+    sp.model_lds = (need <= 4096 && e->d_elems.p && e->d_wfs.p && e->d_pool.p) ? 1 : 0;
+  }
   sp.tile_ctr = (uint32_t*)(e->dr_total + 2);
   sp.overflow = (uint32_t*)(e->dr_total + 2) + 1;
   sp.headers = e->dr_hdr;
@@ -1530,9 +1534,6 @@ int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats*
       HIPCHECK(e, hipEventRecord(e->dr_ev[2], e->stream));
       SerParams wr = sp;
       wr.offsets = e->dr_off;
-      wr.grid = e->ser_grid;
-      wr.exp = e->ser_exp;  // default one workgroup per tile (8.32 ms on C3 10M; 3 per CU persistent 11.2 ms,
-                              // 512 / 1024 workgroups 9.07 / 9.05 ms: profiles/r02/ser_grid_sweep.txt)
       launch_ser_write(wr, e->stream);
       HIPCHECK(e, hipEventRecord(e->dr_ev[3], e->stream));
     }

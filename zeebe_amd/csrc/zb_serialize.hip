@@ -252,6 +252,25 @@ __device__ inline void encode_value(const SerParams& P, int64_t pos, const zb_re
 // value size of record d. (Host-built value templates -- constant segments copied as whole words into the
 // image -- were measured slower than this encoder on C3 10M: 8.9 vs 8.3 ms write pass, 1.40 G vs 1.06 G VALU
 // instructions; the constant keys here compile to immediate stores. profiles/r02/pmc_c3g.json)
+// The model tables the encoder reads per record (elements, workflows, the string pool) are a few hundred
+// bytes for a typical deployment: every workgroup copies them into LDS once, which turns the
+// descriptor -> element -> workflow -> string chain of dependent global loads into LDS reads.
+constexpr uint32_t SER_MODEL_LDS = 4096;
+__device__ __forceinline__ SerParams model_in_lds(const SerParams& P, uint8_t* sm, int nt) {
+  if (!P.model_lds) return P;
+  const uint32_t eb = (uint32_t)P.n_elems * (uint32_t)sizeof(DevElem), wb = (uint32_t)P.n_wfs * (uint32_t)sizeof(DevWorkflow);
+  const uint32_t wo = (eb + 15) & ~15u, po = wo + ((wb + 15) & ~15u);
+  for (uint32_t c = threadIdx.x; c < eb / 16; c += nt) ((uint4*)sm)[c] = ((const uint4*)P.elems)[c];
+  for (uint32_t c = threadIdx.x; c < wb / 16; c += nt) ((uint4*)(sm + wo))[c] = ((const uint4*)P.wfs)[c];
+  for (uint32_t c = threadIdx.x; c < P.pool_len; c += nt) sm[po + c] = P.pool[c];
+  __syncthreads();
+  SerParams Q = P;
+  Q.elems = (const DevElem*)sm;
+  Q.wfs = (const DevWorkflow*)(sm + wo);
+  Q.pool = sm + po;
+  return Q;
+}
+
 __device__ __forceinline__ uint32_t value_size(const SerParams& P, int64_t pos, const zb_rec& d) {
   W w;
   w.dst = nullptr;
@@ -260,7 +279,9 @@ __device__ __forceinline__ uint32_t value_size(const SerParams& P, int64_t pos, 
   return w.n;
 }
 
-__global__ void __launch_bounds__(256) k_ser_size(SerParams P) {
+__global__ void __launch_bounds__(256) k_ser_size(SerParams P0) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_model[SER_MODEL_LDS];
+  const SerParams P = model_in_lds(P0, s_model, 256);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (P.lengths64 && i == P.count) P.lengths64[i] = 0;  // the scan over count + 1 entries ends in the total
   if (i >= P.count) return;
@@ -296,89 +317,68 @@ __device__ __forceinline__ zb_record_header record_header(const zb_rec& d, int64
   return h;
 }
 
-// Write pass, persistent: SER_WG-record tiles are dealt round-robin to a grid sized to the resident
-// workgroups (the LDS image allows three per CU), so workgroup launch never paces the pass (one short-lived
-// workgroup per tile kept the CUs at ~2.8 resident waves: profiles/r02/pmc_c3_10000000.json). While a tile is
-// encoded, the next tile's descriptors and offsets are already in flight, and its payload headers are touched
-// once they have arrived.
-__global__ void __launch_bounds__(SER_WG) k_ser_write(SerParams P) {
+// Write pass: one workgroup per SER_WG-record tile. (A persistent grid with the next tile prefetched was
+// measured slower -- 9.05 ms vs 8.32 ms on C3 10M, profiles/r02/ser_grid_sweep.txt -- and its loop cost the
+// compiler 248 VGPRs.)
+__global__ void __launch_bounds__(SER_WG) k_ser_write(SerParams P0) {
   __shared__ __attribute__((aligned(16))) uint8_t img[SER_IMG + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_model[SER_MODEL_LDS];
   __shared__ unsigned long long s_pay[SER_WG / 64];
-  const int64_t ntiles = (P.count + SER_WG - 1) / SER_WG;
-  int64_t tile = blockIdx.x;
-  // prefetched state of the next tile
-  zb_rec nd{};
-  uint64_t noff = 0, no0 = 0, no1 = 0;
-  auto fetch = [&](int64_t t) {
-    const int64_t base = t * SER_WG;
-    const int64_t last = (base + SER_WG < P.count) ? base + SER_WG : P.count;
-    const int64_t i = base + threadIdx.x;
-    no0 = P.offsets[base];
-    no1 = P.offsets[last];
-    if (i < P.count) {
-      nd = P.log[P.start + i];
-      noff = P.offsets[i];
-    }
-  };
-  if (tile < ntiles) fetch(tile);
-  unsigned long long pay_acc = 0;
-  for (; tile < ntiles; tile += gridDim.x) {
-    const zb_rec d = nd;
-    const uint64_t off = noff, o0 = no0, o1 = no1;
-    const int64_t base = tile * SER_WG;
-    const int64_t i = base + threadIdx.x;
-    const bool live = i < P.count;
-    const bool more = tile + gridDim.x < ntiles;
-    if (more) fetch(tile + gridDim.x);
-    if (P.out_cap && o1 > P.out_cap) {  // does not fit: the host grows the buffer and runs the pass again
-      if (threadIdx.x == 0) atomicOr(P.overflow, 1u);
-      continue;  // uniform over the workgroup
-    }
-    const uint32_t shift = (uint32_t)(((uintptr_t)(P.out + o0)) & 15);
-    const bool staged = (o1 - o0) + shift <= (uint64_t)SER_IMG;
-    if (live) {
-      const int64_t pos = P.start + i;
-      W w;
-      w.dst = staged ? img + shift + (off - o0) : P.out + off;
-      w.n = 0;
-      if (!(P.exp & 1)) encode_value(P, pos, d, w);
-      if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay_acc += *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
-      if (!(P.exp & 4)) P.headers[i] = record_header(d, pos, (uint32_t)(P.offsets[i + 1] - off), off);
-    }
-    // touch the next tile's payload header (its descriptor has arrived by now): the encode finds it cached
-    if (more && base + (int64_t)gridDim.x * SER_WG + threadIdx.x < P.count) {
-      const uint32_t t = *(const volatile uint32_t*)(P.arena + (uint64_t)nd.payload * 8);
-      (void)t;
-    }
-    __syncthreads();
-    if (staged && !(P.exp & 2)) {
-      // stream the image out: img[shift + k] -> out[o0 + k], k in [0, n); out + o0 - shift is 16-byte aligned
-      const uint64_t n = o1 - o0;
-      uint8_t* dst = P.out + o0 - shift;
-      const uint64_t lim = shift + n;  // image bytes [shift, lim) are ours
-      const uint64_t full_lo = (shift + 15) & ~15ull, full_hi = lim & ~15ull;
-      for (uint64_t c = full_lo + 16 * threadIdx.x; c < full_hi; c += 16 * SER_WG)
-        *(uint4*)(dst + c) = *(const uint4*)(img + c);
-      const uint64_t head_end = full_lo < lim ? full_lo : lim;
-      for (uint64_t c = shift + threadIdx.x; c < head_end; c += SER_WG) dst[c] = img[c];
-      const uint64_t tail_lo = full_hi > head_end ? full_hi : head_end;
-      for (uint64_t c = tail_lo + threadIdx.x; c < lim; c += SER_WG) dst[c] = img[c];
-      __syncthreads();  // the image is reused by the next tile
-    }
+  const int64_t base = (int64_t)blockIdx.x * SER_WG;
+  const int64_t i = base + threadIdx.x;
+  const bool live = i < P0.count;
+  // independent loads first; the model copy to LDS overlaps them
+  const int64_t last = (base + SER_WG < P0.count) ? base + SER_WG : P0.count;
+  const uint64_t o0 = P0.offsets[base], o1 = P0.offsets[last];
+  zb_rec d{};
+  uint64_t off = 0, nxt = 0;
+  if (live) {
+    d = P0.log[P0.start + i];
+    off = P0.offsets[i];
+    nxt = P0.offsets[i + 1];
+  }
+  const SerParams P = model_in_lds(P0, s_model, SER_WG);
+  if (P.out_cap && o1 > P.out_cap) {  // does not fit: the host grows the buffer and runs the pass again
+    if (threadIdx.x == 0) atomicOr(P.overflow, 1u);
+    return;
+  }
+  const uint32_t shift = (uint32_t)(((uintptr_t)(P.out + o0)) & 15);
+  const bool staged = (o1 - o0) + shift <= (uint64_t)SER_IMG;
+  uint32_t pay = 0;
+  if (live) {
+    const int64_t pos = P.start + i;
+    W w;
+    w.dst = staged ? img + shift + (off - o0) : P.out + off;
+    w.n = 0;
+    encode_value(P, pos, d, w);
+    if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay = *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
+    P.headers[i] = record_header(d, pos, (uint32_t)(nxt - off), off);
   }
   if (P.totals) {
-    unsigned long long y = pay_acc;
+    unsigned long long y = pay;
     for (int dd = 32; dd >= 1; dd >>= 1) y += __shfl_down(y, dd, 64);
     if ((threadIdx.x & 63) == 0) s_pay[threadIdx.x >> 6] = y;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      unsigned long long tt = 0;
-      for (int k = 0; k < SER_WG / 64; k++) tt += s_pay[k];
-      // one partial per workgroup, reduced by k_ser_sum: 400k same-address device atomics serialised the
-      // pass (~3 ms of an 8.8 ms write pass on C3 10M, profiles/r02/ser_grid_sweep.txt)
-      P.pay_part[blockIdx.x] = tt;
-    }
   }
+  __syncthreads();
+  if (P.totals && threadIdx.x == 0) {
+    unsigned long long tt = 0;
+    for (int k = 0; k < SER_WG / 64; k++) tt += s_pay[k];
+    // one partial per workgroup, reduced by k_ser_sum: 400k same-address device atomics serialised the pass
+    // (~2.4 ms of the empty pass on C3 10M, profiles/r02/ser_grid_sweep.txt)
+    P.pay_part[blockIdx.x] = tt;
+  }
+  if (!staged) return;
+  // stream the image out: img[shift + k] -> out[o0 + k], k in [0, n); out + o0 - shift is 16-byte aligned
+  const uint64_t n = o1 - o0;
+  uint8_t* dst = P.out + o0 - shift;
+  const uint64_t lim = shift + n;  // image bytes [shift, lim) are ours
+  const uint64_t full_lo = (shift + 15) & ~15ull, full_hi = lim & ~15ull;
+  for (uint64_t c = full_lo + 16 * threadIdx.x; c < full_hi; c += 16 * SER_WG)
+    *(uint4*)(dst + c) = *(const uint4*)(img + c);
+  const uint64_t head_end = full_lo < lim ? full_lo : lim;
+  for (uint64_t c = shift + threadIdx.x; c < head_end; c += SER_WG) dst[c] = img[c];
+  const uint64_t tail_lo = full_hi > head_end ? full_hi : head_end;
+  for (uint64_t c = tail_lo + threadIdx.x; c < lim; c += SER_WG) dst[c] = img[c];
 }
 
 // payload-byte total of the write pass (one workgroup)
@@ -410,8 +410,10 @@ __device__ __forceinline__ void ts_store(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ void __launch_bounds__(SER_WG) k_ser_fused(SerParams P) {
+__global__ void __launch_bounds__(SER_WG) k_ser_fused(SerParams P0) {
   __shared__ __attribute__((aligned(16))) uint8_t img[SER_IMG + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_model[SER_MODEL_LDS];
+  const SerParams P = model_in_lds(P0, s_model, SER_WG);
   __shared__ uint64_t s_wsum[SER_WG / 64];
   __shared__ unsigned long long s_pay[SER_WG / 64];
   __shared__ uint32_t s_tile;
@@ -535,9 +537,8 @@ void launch_ser_size(const SerParams& p, hipStream_t s) {
 void launch_ser_write(const SerParams& p, hipStream_t s) {
   if (p.count <= 0) return;
   const int64_t tiles = (p.count + SER_WG - 1) / SER_WG;
-  const int64_t grid = p.grid > 0 ? std::min<int64_t>(tiles, p.grid) : tiles;
-  hipLaunchKernelGGL(k_ser_write, dim3((unsigned)grid), dim3(SER_WG), 0, s, p);
-  if (p.totals) hipLaunchKernelGGL(k_ser_sum, dim3(1), dim3(1024), 0, s, p, grid);
+  hipLaunchKernelGGL(k_ser_write, dim3((unsigned)tiles), dim3(SER_WG), 0, s, p);
+  if (p.totals) hipLaunchKernelGGL(k_ser_sum, dim3(1), dim3(1024), 0, s, p, tiles);
 }
 
 // ------------------------------------------------------------------------------ input injection
