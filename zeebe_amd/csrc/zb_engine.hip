@@ -61,6 +61,8 @@ struct zb_engine {
   hipStream_t stream = nullptr;
   int32_t ncu = 256;            // compute units of the device
   int32_t wave_grid_fixed = 0;  // ZB_WAVE_GRID (tuning experiments): fixed wave grid instead of the sized one
+  int32_t wave_fused_grid = 0;  // k_wave: resident workgroups (0 = three-kernel pipeline; ZB_WAVE_FUSED=0 forces it)
+  uint64_t* lookback = nullptr; // k_wave look-back granules
   std::string err;
 
   ModelTables model;
@@ -281,6 +283,7 @@ WaveParams wave_params(zb_engine* e) {
   p.info = e->info;
   p.block_agg = e->block_agg;
   p.block_off = e->block_off;
+  p.lookback = e->lookback;
   p.wave_cap = e->wave_cap;
   p.err = e->derr;
   p.err_info = e->derr_info;
@@ -332,12 +335,14 @@ int check_device_errors(zb_engine* e, uint32_t flags) {
   if (flags & DE_UNSUPPORTED) m += " unsupported-shape";
   if (flags & DE_PROCESSING) m += " processing-failure";
   if (flags & DE_BAD_PAYLOAD) m += " malformed-payload";
+  if (flags & DE_TIMEOUT) m += " hand-off-timeout";
   uint64_t info = ~0ull;
   if (hipMemcpy(&info, e->derr_info, sizeof(info), hipMemcpyDeviceToHost) == hipSuccess && info != ~0ull)
     m += " (first at log position " + std::to_string(info >> 8) + ", site " + std::to_string(info & 0xff) + ")";
   int code = ZB_EPROCESSING;
   if (flags & (DE_LOG_FULL | DE_ROWS_FULL | DE_ARENA_FULL)) code = ZB_ENOMEM;
   else if (flags & DE_UNSUPPORTED) code = ZB_EUNSUPPORTED;
+  if (flags & DE_TIMEOUT) code = ZB_EDEVICE;
   return fail(e, code, m);
 }
 
@@ -625,6 +630,13 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess && ncu > 0)
       e->ncu = ncu;
   }
+  {
+    const char* f = std::getenv("ZB_WAVE_FUSED");
+    const int per_cu = (f && atoi(f) == 0) ? 0 : wave_resident_per_cu();
+    // one workgroup per CU below the occupancy limit: every workgroup of the persistent grid is resident with
+    // room to spare, so no tile waits on a workgroup that is not running
+    e->wave_fused_grid = per_cu > 1 ? (per_cu - 1) * e->ncu : (per_cu == 1 ? e->ncu : 0);
+  }
   const uint64_t L = e->cfg.log_capacity;
   e->wave_cap = e->cfg.wave_records ? e->cfg.wave_records : std::min<uint64_t>(L, 1ull << 22);
   e->wave_cap = (e->wave_cap + WAVE_TILE - 1) / WAVE_TILE * WAVE_TILE;
@@ -639,6 +651,11 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->info, e->wave_cap * sizeof(ItemInfo)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->block_agg, WAVE_GRID_MAX * sizeof(BlockAgg)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->block_off, WAVE_GRID_MAX * sizeof(BlockOff)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  {
+    const size_t lb = (e->wave_cap / WAVE_TILE + 1) * 16 * sizeof(uint64_t);
+    if (hipMalloc(&e->lookback, lb) != hipSuccess) return cleanup(ZB_ENOMEM);
+    if (hipMemset(e->lookback, 0, lb) != hipSuccess) return cleanup(ZB_EDEVICE);
+  }
   if (hipMalloc(&e->derr, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->dstats, 8 * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->derr_info, sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
@@ -678,7 +695,7 @@ void zb_engine_destroy(zb_engine* e) {
   for (auto& x : e->ev)
     if (x) (void)hipEventDestroy(x);
   void* ps[] = {e->log, e->links, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
-                e->merge_jobs, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off,
+                e->merge_jobs, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
                 e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->need_children};
@@ -1371,11 +1388,17 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
         launch_pre(p, e->stream);
         if (p.term) launch_children(p, e->stream);
       }
-      launch_process(p, e->stream);
-      HIPCHECK(e, hipEventRecord(ev[1], e->stream));
-      launch_scan(p, e->stream);
-      launch_emit(p, e->stream);
-      HIPCHECK(e, hipEventRecord(ev[2], e->stream));
+      if (e->wave_fused_grid) {  // process + scan + emit in one launch (k_wave)
+        launch_wave(p, e->wave_fused_grid, e->stream);
+        HIPCHECK(e, hipEventRecord(ev[1], e->stream));
+        HIPCHECK(e, hipEventRecord(ev[2], e->stream));
+      } else {
+        launch_process(p, e->stream);
+        HIPCHECK(e, hipEventRecord(ev[1], e->stream));
+        launch_scan(p, e->stream);
+        launch_emit(p, e->stream);
+        HIPCHECK(e, hipEventRecord(ev[2], e->stream));
+      }
       // payload kernels for this wave's deferred work (only when the model can produce any)
       if (e->has_catch) launch_subscribe(p, e->stream);  // this wave's subscribe steps (outbox)
       if (e->has_merges) launch_merge(p, e->stream);

@@ -914,6 +914,97 @@ __global__ void __launch_bounds__(SCAN_WG) k_scan(WaveParams P) {
   }
 }
 
+// ------------------------------------------------------------------------------ emit (k_emit, k_wave)
+// Writes the follow-ups of wave item i at their final positions: staged slots sl[0, ns) get their keys
+// (KeyGenerator ordinals wf0 / job0 + slot ordinal), rows (row0 + ordinal; ELEMENT_READY inserts initialise the
+// row), merge result / incident detail blobs (reserved at bump) and job-list entries; a parallel fork's
+// SEQUENCE_FLOW_TAKEN records follow (EXTENSION, C4). Every base already includes the item's exclusive offset.
+__device__ __forceinline__ void emit_item(const WaveParams& P, const Chunk& c, int64_t i, uint64_t w, const Slot* sl,
+                                          const ItemInfo& inf, uint64_t out_rec, uint64_t wf0, uint64_t job0,
+                                          uint64_t row0, uint64_t bump, uint64_t merge_j, uint64_t cond_j,
+                                          int64_t wf_next, int64_t job_next, uint64_t par) {
+  const int ns = (int)(w & 7);
+  const uint64_t nexp = (w >> CW_NEXP) & 63;
+  uint32_t err = 0;
+  uint32_t merged_ref = 0, detail_ref = 0;
+  if (w & ((1ull << CW_MERGE) | (1ull << CW_DETAIL))) {
+    if (inf.m_bytes) {
+      // reserve the blob; k_merge (zb_aux.hip) fills it before the next wave reads any payload
+      if (bump + inf.m_bytes > P.arena_cap) err |= DE_ARENA_FULL;
+      else {
+        merged_ref = (uint32_t)(bump >> 3);
+        if (merge_j < P.job_cap) P.merge_jobs[par + merge_j] = MergeJob{merged_ref, inf.m_src, inf.m_tgt, inf.m_len};
+      }
+      bump += inf.m_bytes;
+    }
+    if (inf.has_detail) {
+      if (bump + 24 > P.arena_cap) err |= DE_ARENA_FULL;
+      else {
+        detail_ref = (uint32_t)(bump >> 3);
+        uint8_t* dst = P.arena + bump;
+        *(uint32_t*)dst = 16;
+        dst[4] = inf.d_type; dst[5] = inf.d_code; dst[6] = inf.d_a; dst[7] = inf.d_b;
+        *(uint16_t*)(dst + 8) = inf.d_q;
+        *(int64_t*)(dst + 16) = inf.d_pos;
+      }
+      bump += 24;
+    }
+  }
+  for (int k = 0; k < ns; k++) {
+    Slot s = sl[k];
+    if (s.flags & SF_KEY_WF) s.d.key = wf_next + 5 * (int64_t)(wf0 + s.ord);
+    if (s.flags & SF_KEY_JOB) s.d.key = job_next + 5 * (int64_t)(job0 + s.ord);
+    if (s.flags & SF_INST_WF) s.d.inst_key = wf_next + 5 * (int64_t)(wf0 + s.ord);
+    if (s.flags & SF_PAY_MERGED) s.d.payload = merged_ref;
+    if (s.flags & SF_PAY_DETAIL) s.d.payload = detail_ref;
+    if (s.flags & SF_ROW_NEW) {
+      const uint64_t row = row0 + s.rord;
+      if (row >= P.row_cap) { err |= DE_ROWS_FULL; s.rself = NO_ROW; }
+      else {
+        s.rself = (uint32_t)row;
+        if (s.flags & SF_ROW_INIT) {
+          RowMeta m;
+          m.payload = s.d.payload; m.parent = s.rscope; m.elem = s.d.elem; m.state = WI_ELEMENT_READY;
+          m.flags = 0; m.nchild = 0;
+          P.rmeta[row] = m;
+          P.rkeys[row] = RowKeys{s.d.key, s.d.scope_key, s.d.inst_key, 0};
+        }
+      }
+    }
+    if (out_rec >= P.log_cap) { err |= DE_LOG_FULL; }
+    else {
+      P.log[out_rec] = s.d;
+      P.links[out_rec] = (uint64_t)s.rself | ((uint64_t)s.rscope << 32);
+      if (s.flags & SF_COND_JOB) {
+        if (cond_j < P.job_cap) P.cond_jobs[par + cond_j] = out_rec;
+        cond_j++;
+      }
+    }
+    out_rec++;
+  }
+  if (nexp) {  // EXTENSION (C4): a parallel fork, one SEQUENCE_FLOW_TAKEN per outgoing flow, keys in order
+    const int64_t r = c.begin + i;
+    const zb_rec g = P.log[r];
+    const uint32_t rscope = (uint32_t)(P.links[r] >> 32);
+    const DevElem& ge = P.elems[g.elem];
+    const uint64_t kord = wf0 + ((w >> CW_NWF) & 7);
+    for (uint32_t j = 0; j < (uint32_t)nexp; j++) {
+      zb_rec d = g;
+      d.elem = P.cond_flows[ge.out_begin + j];
+      d.key = wf_next + 5 * (int64_t)(kord + j);
+      d.intent = WI_SEQUENCE_FLOW_TAKEN;
+      d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, ns + j > 0);
+      if (out_rec >= P.log_cap) { err |= DE_LOG_FULL; }
+      else {
+        P.log[out_rec] = d;
+        P.links[out_rec] = (uint64_t)NO_ROW | ((uint64_t)rscope << 32);
+      }
+      out_rec++;
+    }
+  }
+  if (err) atomicOr(P.err, err);  // capacity overflow: the wave's results are void, the host stops
+}
+
 // ------------------------------------------------------------------------------ k_emit
 __global__ void __launch_bounds__(WG) k_emit(WaveParams P) {
   __shared__ uint64_t s_a[WG / 64], s_b[WG / 64];
@@ -970,87 +1061,281 @@ __global__ void __launch_bounds__(WG) k_emit(WaveParams P) {
     uint64_t bump = arena_next + r_bytes + (b & 0xffffffffffull);
     const uint64_t merge_j = r_merge + ((b >> 40) & 0xfff);
     uint64_t cond_j = r_cond + (b >> 52);
-    uint32_t err = 0;
-    uint32_t merged_ref = 0, detail_ref = 0;
-    if (w & ((1ull << CW_MERGE) | (1ull << CW_DETAIL))) {
-      const ItemInfo inf = P.info[i];
-      if (inf.m_bytes) {
-        // reserve the blob; k_merge (zb_aux.hip) fills it before the next wave reads any payload
-        if (bump + inf.m_bytes > P.arena_cap) err |= DE_ARENA_FULL;
-        else {
-          merged_ref = (uint32_t)(bump >> 3);
-          if (merge_j < P.job_cap) P.merge_jobs[par + merge_j] = MergeJob{merged_ref, inf.m_src, inf.m_tgt, inf.m_len};
-        }
-        bump += inf.m_bytes;
-      }
-      if (inf.has_detail) {
-        if (bump + 24 > P.arena_cap) err |= DE_ARENA_FULL;
-        else {
-          detail_ref = (uint32_t)(bump >> 3);
-          uint8_t* dst = P.arena + bump;
-          *(uint32_t*)dst = 16;
-          dst[4] = inf.d_type; dst[5] = inf.d_code; dst[6] = inf.d_a; dst[7] = inf.d_b;
-          *(uint16_t*)(dst + 8) = inf.d_q;
-          *(int64_t*)(dst + 16) = inf.d_pos;
-        }
-        bump += 24;
-      }
-    }
-    const Slot* sl = P.stage + (uint64_t)i * MAX_SLOTS;
-    for (int k = 0; k < ns; k++) {
-      Slot s = sl[k];
-      if (s.flags & SF_KEY_WF) s.d.key = wf_next + 5 * (int64_t)(wf0 + s.ord);
-      if (s.flags & SF_KEY_JOB) s.d.key = job_next + 5 * (int64_t)(job0 + s.ord);
-      if (s.flags & SF_INST_WF) s.d.inst_key = wf_next + 5 * (int64_t)(wf0 + s.ord);
-      if (s.flags & SF_PAY_MERGED) s.d.payload = merged_ref;
-      if (s.flags & SF_PAY_DETAIL) s.d.payload = detail_ref;
-      if (s.flags & SF_ROW_NEW) {
-        const uint64_t row = row0 + s.rord;
-        if (row >= P.row_cap) { err |= DE_ROWS_FULL; s.rself = NO_ROW; }
-        else {
-          s.rself = (uint32_t)row;
-          if (s.flags & SF_ROW_INIT) {
-            RowMeta m;
-            m.payload = s.d.payload; m.parent = s.rscope; m.elem = s.d.elem; m.state = WI_ELEMENT_READY;
-            m.flags = 0; m.nchild = 0;
-            P.rmeta[row] = m;
-            P.rkeys[row] = RowKeys{s.d.key, s.d.scope_key, s.d.inst_key, 0};
-          }
-        }
-      }
-      if (out_rec >= P.log_cap) { err |= DE_LOG_FULL; }
-      else {
-        P.log[out_rec] = s.d;
-        P.links[out_rec] = (uint64_t)s.rself | ((uint64_t)s.rscope << 32);
-        if (s.flags & SF_COND_JOB) {
-          if (cond_j < P.job_cap) P.cond_jobs[par + cond_j] = out_rec;
-          cond_j++;
-        }
-      }
-      out_rec++;
-    }
-    if (nexp) {  // EXTENSION (C4): a parallel fork, one SEQUENCE_FLOW_TAKEN per outgoing flow, keys in order
-      const int64_t r = c.begin + i;
-      const zb_rec g = P.log[r];
-      const uint32_t rscope = (uint32_t)(P.links[r] >> 32);
-      const DevElem& ge = P.elems[g.elem];
-      const uint64_t kord = wf0 + ((w >> CW_NWF) & 7);
-      for (uint32_t j = 0; j < (uint32_t)nexp; j++) {
-        zb_rec d = g;
-        d.elem = P.cond_flows[ge.out_begin + j];
-        d.key = wf_next + 5 * (int64_t)(kord + j);
-        d.intent = WI_SEQUENCE_FLOW_TAKEN;
-        d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_EVENT, ns + j > 0);
-        if (out_rec >= P.log_cap) { err |= DE_LOG_FULL; }
-        else {
-          P.log[out_rec] = d;
-          P.links[out_rec] = (uint64_t)NO_ROW | ((uint64_t)rscope << 32);
-        }
-        out_rec++;
-      }
-    }
-    if (err) atomicOr(P.err, err);  // capacity overflow: the wave's results are void, the host stops
+    ItemInfo inf{};
+    if (w & ((1ull << CW_MERGE) | (1ull << CW_DETAIL))) inf = P.info[i];
+    emit_item(P, c, i, w, P.stage + (uint64_t)i * MAX_SLOTS, inf, out_rec, wf0, job0, row0, bump, merge_j, cond_j,
+              wf_next, job_next, par);
   }
+}
+
+// ------------------------------------------------------------------------------ k_wave (fused)
+// k_process + k_scan + k_emit in one launch: each 256-record tile is processed (follow-ups staged in LDS),
+// scanned in LDS, gets its offsets from its predecessors by decoupled look-back, and writes its follow-ups
+// straight from LDS -- no count words, staging slots or side information round-trip through HBM, and no
+// single-workgroup scan between the passes. The grid is persistent (every workgroup resident, tiles dealt
+// round-robin in increasing order), so a tile only ever waits for tiles that are already running.
+//
+// Look-back state: per tile LB_FIELDS 8-byte granules {tag, value} (agent-scope atomic stores and loads; the
+// data is its own flag, cdna_hip_programming.md Guideline 16 R2). A tile first publishes its aggregate
+// (tag = epoch:AGG), then its inclusive prefix (tag = epoch:INC); a reader accepts a tile's granules only when
+// all of them carry the same tag. Spins are bounded: a hand-off that never arrives sets DE_TIMEOUT, the wave's
+// results are void and the host stops the partition -- it never hangs the device.
+constexpr int LB_FIELDS = 12;  // rec wf job row bytes_lo bytes_hi merges conds | transitions completed created canceled
+constexpr int LB_STRIDE = 16;  // granules per tile (128 B)
+constexpr uint32_t LB_SPIN_LIMIT = 1u << 16;  // ~0.1 s per granule; then DE_TIMEOUT and every waiter gives up
+
+__device__ __forceinline__ uint32_t lb_tag(int64_t epoch, uint32_t inc) {
+  return (uint32_t)((((uint64_t)epoch + 1) << 1) | inc);
+}
+
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8))) k_wave(WaveParams P) {
+  __shared__ Slot s_slots[WG * MAX_SLOTS];
+  __shared__ uint64_t s_a[WG / 64], s_b[WG / 64];
+  __shared__ uint64_t s_st[WG / 64][2];  // transitions | completed << 32, created | canceled << 32
+  __shared__ uint64_t s_ex[LB_FIELDS];   // the tile's exclusive prefix
+  __shared__ uint64_t s_tot[LB_FIELDS];  // and its inclusive prefix (the chunk totals on the last tile)
+  __shared__ uint32_t s_agg[LB_FIELDS];  // the tile's aggregate
+  __shared__ ItemInfo s_inf[WG];         // per item: merge / incident detail (k_emit's P.info, kept on chip)
+  __shared__ uint64_t s_w[WG];           // per item: count word
+  const WaveHdr* hin = P.hdr + (P.wave & 1);
+  WaveHdr* hout = P.hdr + ((P.wave + 1) & 1);
+  const Chunk c = wave_chunk(P, hin);
+  if (c.n <= 0) {  // nothing in this wave (the batch outran quiescence): carry the header forward
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      *hout = *hin;
+      if (P.need_children) *P.need_children = 0;
+      P.merge_count[P.wave & 1] = 0;
+      P.cond_count[P.wave & 1] = 0;
+      if (P.sub_count) P.sub_count[(P.wave + 1) & 1] = 0;
+    }
+    return;
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t ntiles = (c.n + WG - 1) / WG;
+  const int64_t gen_end = hin->gen_end;
+  const int64_t end = hin->end, wf_next = hin->wf_next, job_next = hin->job_next;
+  const uint64_t rows_next = (uint64_t)hin->rows_next, arena_next = (uint64_t)hin->arena_next;
+  const uint64_t par = (uint64_t)(P.wave & 1) * P.job_cap;
+  const uint32_t tag_agg = lb_tag(P.epoch, 0), tag_inc = lb_tag(P.epoch, 1);
+
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t i = tile * WG + threadIdx.x;  // wave-relative index
+    const int64_t r = c.begin + i;
+    // ---- process (k_process)
+    TState t;
+    t.s = s_slots + threadIdx.x * MAX_SLOTS;
+    t.ns = t.nwf = t.njob = t.nrow = 0;
+    t.bytes = 0; t.merge = false; t.detail = false; t.err = 0; t.err_site = 0;
+    t.transitions = t.completed = t.created = t.merges = t.canceled = 0;
+    t.merge_bytes = t.cond_bytes = 0;
+    t.sub = false;
+    t.nexp = 0; t.exp_ord = 0;
+    uint32_t nconds = 0;
+    if (r < c.end) {
+      const zb_rec rec = P.log[r];
+      if (!grouped(rec)) {
+        const uint64_t lk = P.links[r];
+        process_record(P, rec, r, (uint32_t)lk, (uint32_t)(lk >> 32), t);
+        for (int64_t q = r + 1; q < gen_end && q < r + 4; q++) {
+          const zb_rec rec2 = P.log[q];
+          if (!grouped(rec2)) break;
+          const uint64_t lk2 = P.links[q];
+          process_record(P, rec2, q, (uint32_t)lk2, (uint32_t)(lk2 >> 32), t);
+        }
+      }
+    }
+    for (int k = 0; k < t.ns; k++) {
+      const Slot& sl = t.s[k];
+      nconds += (sl.flags & SF_COND_JOB) ? 1 : 0;
+      if (kind_vt(sl.d.kind) == ZB_VT_WORKFLOW_INSTANCE && kind_rt(sl.d.kind) == ZB_RT_EVENT) t.transitions++;
+    }
+    t.transitions += t.nexp;  // a fork's SEQUENCE_FLOW_TAKEN events
+    const uint64_t nwf_staged = (uint64_t)t.nwf - t.nexp;
+    const uint64_t w = (uint64_t)t.ns | (nwf_staged << CW_NWF) | ((uint64_t)t.njob << CW_NJOB) |
+                       ((uint64_t)t.nrow << CW_NROW) | ((uint64_t)(t.merge ? 1 : 0) << CW_MERGE) |
+                       ((uint64_t)(t.detail ? 1 : 0) << CW_DETAIL) | ((uint64_t)nconds << CW_NCOND) |
+                       ((uint64_t)t.nexp << CW_NEXP) | ((uint64_t)t.bytes << 32);
+    s_w[threadIdx.x] = w;
+    if (t.merge || t.detail) {
+      ItemInfo inf;
+      inf.m_src = t.m_src; inf.m_tgt = t.m_tgt; inf.m_len = t.m_len; inf.m_bytes = t.merge ? t.m_bytes : 0;
+      inf.d_pos = t.d_pos; inf.d_q = t.d_q; inf.d_type = t.d_type; inf.d_code = t.d_code; inf.d_a = t.d_a;
+      inf.d_b = t.d_b; inf.has_detail = t.detail; inf.ns = (uint8_t)t.ns;
+      s_inf[threadIdx.x] = inf;
+    }
+    if (__ballot(t.sub)) {  // wave-uniform: this tile's subscribe steps, in the wave's job list
+      const uint32_t slot = wave_alloc(P.sub_count + (P.wave & 1), t.sub ? 1u : 0u);
+      if (t.sub) {
+        if (slot < P.job_cap) P.sub_jobs[slot] = (uint64_t)t.sub_pos;
+        else fail_at(t, DE_LOG_FULL, 36);
+      }
+    }
+    if (t.err) {
+      atomicOr(P.err, t.err);
+      atomicMin((unsigned long long*)P.err_info, ((unsigned long long)r << 8) | (t.err_site & 0xff));
+    }
+    // ---- tile scan (packed as in k_emit): a = outputs | wf << 16 | job << 32 | row << 48,
+    //      b = bytes | merges << 40 | conds << 52
+    const uint64_t nexp = (w >> CW_NEXP) & 63;
+    const uint64_t a0 = ((w & 7) + nexp) | ((((w >> CW_NWF) & 7) + nexp) << 16) | (((w >> CW_NJOB) & 7) << 32) |
+                        (((w >> CW_NROW) & 7) << 48);
+    const uint64_t b0 = (w >> 32) | (((w >> CW_MERGE) & 1) << 40) | (((w >> CW_NCOND) & 7) << 52);
+    uint64_t a = a0, b = b0;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t ua = shfl_up64(a, d), ub = shfl_up64(b, d);
+      if (lane >= d) { a += ua; b += ub; }
+    }
+    uint64_t st0 = (uint64_t)t.transitions | ((uint64_t)t.completed << 32);
+    uint64_t st1 = (uint64_t)t.created | ((uint64_t)t.canceled << 32);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) { st0 += shfl_down64(st0, d); st1 += shfl_down64(st1, d); }
+    if (lane == 63) { s_a[wv] = a; s_b[wv] = b; }
+    if (lane == 0) { s_st[wv][0] = st0; s_st[wv][1] = st1; }
+    __syncthreads();
+    uint64_t ta = 0, tb = 0;
+#pragma unroll
+    for (int k = 0; k < WG / 64; k++) {
+      if (k < wv) { a += s_a[k]; b += s_b[k]; }
+      ta += s_a[k]; tb += s_b[k];
+    }
+    a -= a0;
+    b -= b0;
+    // ---- decoupled look-back (first wave): lane L < 60 reads granule L % 12 of predecessor tile p - L / 12,
+    // so a round covers 5 predecessors and every lane keeps one running sum (field L % 12)
+    if (threadIdx.x == 0) {
+      const uint64_t sa = s_st[0][0] + s_st[1][0] + s_st[2][0] + s_st[3][0];
+      const uint64_t sb = s_st[0][1] + s_st[1][1] + s_st[2][1] + s_st[3][1];
+      const uint64_t tbytes = tb & 0xffffffffffull;
+      s_agg[0] = (uint32_t)(ta & 0xffff); s_agg[1] = (uint32_t)((ta >> 16) & 0xffff);
+      s_agg[2] = (uint32_t)((ta >> 32) & 0xffff); s_agg[3] = (uint32_t)(ta >> 48);
+      s_agg[4] = (uint32_t)tbytes; s_agg[5] = (uint32_t)(tbytes >> 32);
+      s_agg[6] = (uint32_t)((tb >> 40) & 0xfff); s_agg[7] = (uint32_t)(tb >> 52);
+      s_agg[8] = (uint32_t)sa; s_agg[9] = (uint32_t)(sa >> 32); s_agg[10] = (uint32_t)sb; s_agg[11] = (uint32_t)(sb >> 32);
+    }
+    if (wv == 0) {
+      const int f = lane % LB_FIELDS, j = lane / LB_FIELDS;  // field, predecessor distance - 1 (j < 5 for lane < 60)
+      const bool lb_lane = lane < 5 * LB_FIELDS;
+      const uint32_t my_agg = lane < LB_FIELDS ? s_agg[lane] : 0;
+      uint64_t* lb = P.lookback + (uint64_t)tile * LB_STRIDE;
+      if (lane < LB_FIELDS)
+        __hip_atomic_store(lb + lane, ((uint64_t)(tile == 0 ? tag_inc : tag_agg) << 32) | my_agg, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      uint64_t acc = 0;  // lanes < 12: exclusive prefix of field `lane`
+      if (tile > 0) {
+        bool timeout = false;
+        for (int64_t p = tile - 1;;) {
+          const int64_t q = p - j;
+          uint32_t v = 0, tg = tag_inc;  // predecessors before tile 0 count as the (empty) inclusive start
+          if (lb_lane && q >= 0) {
+            const uint64_t* g = P.lookback + (uint64_t)q * LB_STRIDE + f;
+            for (uint32_t spins = 0;; spins++) {
+              const uint64_t x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              tg = (uint32_t)(x >> 32);
+              v = (uint32_t)x;
+              if (tg == tag_agg || tg == tag_inc) break;
+              if (spins >= LB_SPIN_LIMIT ||
+                  ((spins & 255) == 255 && (__hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & DE_TIMEOUT))) {
+                timeout = true;
+                break;
+              }
+              __builtin_amdgcn_s_sleep(1);
+            }
+          }
+          // a predecessor is usable when its 12 granules carry one tag (a reader can catch it between its
+          // aggregate and inclusive publication): re-read the round otherwise
+          const uint64_t m_agg = __ballot(lb_lane && tg == tag_agg), m_inc = __ballot(!lb_lane || tg == tag_inc);
+          bool consistent = true, found = false;
+          int first = 5;
+#pragma unroll
+          for (int k = 0; k < 5; k++) {
+            const uint64_t gm = 0xfffull << (LB_FIELDS * k);
+            const bool inc_k = (m_inc & gm) == gm, agg_k = (m_agg & gm) == gm;
+            if (!found) {
+              if (!inc_k && !agg_k) consistent = false;
+              if (inc_k) { first = k; found = true; }
+            }
+          }
+          if (__ballot(timeout)) { timeout = true; break; }
+          if (!consistent) continue;  // same p again (bounded by the per-granule spins above)
+          // sum field f over predecessors j <= first: lanes f, f + 12, ..., f + 48
+          uint64_t x = (lb_lane && j <= first) ? (uint64_t)v : 0;
+          const uint64_t x12 = __shfl(x, (lane + 12) & 63, 64), x24 = __shfl(x, (lane + 24) & 63, 64);
+          const uint64_t x36 = __shfl(x, (lane + 36) & 63, 64), x48 = __shfl(x, (lane + 48) & 63, 64);
+          if (lane < LB_FIELDS) acc += x + x12 + x24 + x36 + x48;
+          if (first < 5) break;
+          p -= 5;
+        }
+        if (__ballot(timeout) && lane == 0) atomicOr(P.err, (uint32_t)DE_TIMEOUT);  // the others stop waiting too
+      }
+      // bytes travel as two 32-bit granules (fields 4, 5): recombine the carry
+      const uint64_t ex_lo = __shfl(acc, 4, 64), ex_hi = __shfl(acc, 5, 64);
+      const uint64_t exb = ex_lo + (ex_hi << 32);
+      const uint64_t tbytes = (uint64_t)s_agg[4] | ((uint64_t)s_agg[5] << 32);
+      if (tile > 0 && lane < LB_FIELDS) {
+        const uint64_t incb = exb + tbytes;
+        const uint32_t val = lane == 4 ? (uint32_t)incb : lane == 5 ? (uint32_t)(incb >> 32) : (uint32_t)(acc + my_agg);
+        __hip_atomic_store(lb + lane, ((uint64_t)tag_inc << 32) | val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (lane < LB_FIELDS) {
+        s_ex[lane] = lane == 4 ? exb : lane == 5 ? 0 : acc;
+        s_tot[lane] = lane == 4 ? exb + tbytes : lane == 5 ? 0 : acc + my_agg;
+      }
+      // the chunk's last tile: totals -> next wave header, counters, job counts (k_scan's job)
+      if (tile == ntiles - 1 && lane == 0) {
+        WaveHdr h = *hin;
+        h.begin = c.end;
+        h.end = hin->end + (int64_t)s_tot[0];
+        h.gen_end = (c.end == hin->gen_end) ? h.end : hin->gen_end;
+        h.wf_next = hin->wf_next + 5 * (int64_t)s_tot[1];
+        h.job_next = hin->job_next + 5 * (int64_t)s_tot[2];
+        h.rows_next = hin->rows_next + (int64_t)s_tot[3];
+        h.arena_next = hin->arena_next + (int64_t)s_tot[4];
+        P.stats[0] += s_tot[8];
+        P.stats[1] += s_tot[9];
+        P.stats[2] += s_tot[10];
+        P.stats[6] += 1;
+        P.stats[7] += s_tot[11];
+        uint32_t err = 0;
+        if ((uint64_t)h.end > P.log_cap) err |= DE_LOG_FULL;
+        if ((uint64_t)h.rows_next > P.row_cap) err |= DE_ROWS_FULL;
+        if ((uint64_t)h.arena_next > P.arena_cap) err |= DE_ARENA_FULL;
+        if (s_tot[6] > P.job_cap || s_tot[7] > P.job_cap) err |= DE_LOG_FULL;
+        if (err) atomicOr(P.err, err);
+        *hout = h;
+        if (P.need_children) *P.need_children = 0;  // k_pre of the next chunk sets it again
+        P.merge_count[P.wave & 1] = (uint32_t)s_tot[6];
+        P.cond_count[P.wave & 1] = (uint32_t)s_tot[7];
+        if (P.sub_count) P.sub_count[(P.wave + 1) & 1] = 0;  // the next wave's subscribe list
+      }
+    }
+    __syncthreads();
+    // ---- emit (k_emit) straight from the LDS slots
+    const uint64_t we = s_w[threadIdx.x];
+    const int ns = (int)(we & 7);
+    if (r < c.end && (ns || ((we >> CW_NEXP) & 63) || ((we >> CW_DETAIL) & 1))) {
+      const uint64_t out_rec = (uint64_t)end + s_ex[0] + (a & 0xffff);
+      const uint64_t wf0 = s_ex[1] + ((a >> 16) & 0xffff);
+      const uint64_t job0 = s_ex[2] + ((a >> 32) & 0xffff);
+      const uint64_t row0 = rows_next + s_ex[3] + (a >> 48);
+      const uint64_t bump = arena_next + s_ex[4] + (b & 0xffffffffffull);
+      const uint64_t merge_j = s_ex[6] + ((b >> 40) & 0xfff);
+      const uint64_t cond_j = s_ex[7] + (b >> 52);
+      const ItemInfo inf = s_inf[threadIdx.x];
+      emit_item(P, c, i, we, s_slots + threadIdx.x * MAX_SLOTS, inf, out_rec, wf0, job0, row0, bump, merge_j, cond_j,
+                wf_next, job_next, par);
+    }
+    __syncthreads();  // LDS slots and scan scratch are reused by the next tile
+  }
+}
+
+void launch_wave(const WaveParams& p, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(k_wave, dim3(grid), dim3(WG), 0, stream, p);
+}
+int wave_resident_per_cu() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_wave, WG, 0) != hipSuccess) return 0;
+  return n;
 }
 
 void launch_pre(const WaveParams& p, hipStream_t stream) {
