@@ -317,13 +317,33 @@ __device__ __forceinline__ zb_record_header record_header(const zb_rec& d, int64
   return h;
 }
 
+// streams image bytes [shift, shift + n) to out[o .. o + n) with 16-byte stores aligned to the destination
+// (out + o - shift is 16-byte aligned)
+__device__ __forceinline__ void stream_image(const uint8_t* img, uint8_t* out, uint64_t o, uint32_t shift, uint64_t n) {
+  uint8_t* dst = out + o - shift;
+  const uint64_t lim = shift + n;  // image bytes [shift, lim) are ours
+  const uint64_t full_lo = (shift + 15) & ~15ull, full_hi = lim & ~15ull;
+  for (uint64_t c = full_lo + 16 * threadIdx.x; c < full_hi; c += 16 * SER_WG)
+    *(uint4*)(dst + c) = *(const uint4*)(img + c);
+  const uint64_t head_end = full_lo < lim ? full_lo : lim;
+  for (uint64_t c = shift + threadIdx.x; c < head_end; c += SER_WG) dst[c] = img[c];
+  const uint64_t tail_lo = full_hi > head_end ? full_hi : head_end;
+  for (uint64_t c = tail_lo + threadIdx.x; c < lim; c += SER_WG) dst[c] = img[c];
+}
+
 // Write pass: one workgroup per SER_WG-record tile. (A persistent grid with the next tile prefetched was
 // measured slower -- 9.05 ms vs 8.32 ms on C3 10M, profiles/r02/ser_grid_sweep.txt -- and its loop cost the
-// compiler 248 VGPRs.)
-__global__ void __launch_bounds__(SER_WG) k_ser_write(SerParams P0) {
+// compiler 248 VGPRs.) A tile whose values exceed the image is written in windows: record k goes to window
+// (off_k - o0) / ws with ws = image - longest value, so every window's records fit the image; the windows are
+// encoded and streamed one after another (large values, e.g. C2's job records: 64 KB per tile). The phase loop
+// lets the compiler spend 255 VGPRs unless told the LDS-bound occupancy (3 workgroups per CU): 168, no spills.
+constexpr int SER_WINDOWS = 16;
+__global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 3))) k_ser_write(SerParams P0) {
   __shared__ __attribute__((aligned(16))) uint8_t img[SER_IMG + 16];
   __shared__ __attribute__((aligned(16))) uint8_t s_model[SER_MODEL_LDS];
   __shared__ unsigned long long s_pay[SER_WG / 64];
+  __shared__ uint32_t s_maxlen;
+  __shared__ unsigned long long s_wlo[SER_WINDOWS], s_whi[SER_WINDOWS];
   const int64_t base = (int64_t)blockIdx.x * SER_WG;
   const int64_t i = base + threadIdx.x;
   const bool live = i < P0.count;
@@ -337,48 +357,83 @@ __global__ void __launch_bounds__(SER_WG) k_ser_write(SerParams P0) {
     off = P0.offsets[i];
     nxt = P0.offsets[i + 1];
   }
-  const SerParams P = model_in_lds(P0, s_model, SER_WG);
+  if (threadIdx.x == 0) s_maxlen = 0;
+  const SerParams P = model_in_lds(P0, s_model, SER_WG);  // (ends in a barrier)
   if (P.out_cap && o1 > P.out_cap) {  // does not fit: the host grows the buffer and runs the pass again
     if (threadIdx.x == 0) atomicOr(P.overflow, 1u);
     return;
   }
+  const uint32_t len = (uint32_t)(nxt - off);
   const uint32_t shift = (uint32_t)(((uintptr_t)(P.out + o0)) & 15);
   const bool staged = (o1 - o0) + shift <= (uint64_t)SER_IMG;
+  uint64_t ws = 0;
+  int nwin = 0;
+  if (!staged) {
+    if (live) atomicMax(&s_maxlen, len);
+    if (threadIdx.x < SER_WINDOWS) { s_wlo[threadIdx.x] = ~0ull; s_whi[threadIdx.x] = 0; }
+    __syncthreads();
+    const uint32_t maxlen = s_maxlen;
+    if (maxlen + 32 < (uint32_t)SER_IMG) {
+      ws = (uint64_t)SER_IMG - 32 - maxlen;
+      const uint64_t nw = (o1 - o0 + ws - 1) / ws;
+      nwin = nw <= SER_WINDOWS ? (int)nw : 0;
+    }
+    if (nwin && live) {
+      const int wk = (int)((off - o0) / ws);
+      atomicMin(&s_wlo[wk], (unsigned long long)off);
+      atomicMax(&s_whi[wk], (unsigned long long)nxt);
+    }
+    __syncthreads();
+  }
   uint32_t pay = 0;
+  const int64_t pos = P.start + i;
   if (live) {
-    const int64_t pos = P.start + i;
-    W w;
-    w.dst = staged ? img + shift + (off - o0) : P.out + off;
-    w.n = 0;
-    encode_value(P, pos, d, w);
     if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay = *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
-    P.headers[i] = record_header(d, pos, (uint32_t)(nxt - off), off);
+    P.headers[i] = record_header(d, pos, len, off);
   }
   if (P.totals) {
     unsigned long long y = pay;
     for (int dd = 32; dd >= 1; dd >>= 1) y += __shfl_down(y, dd, 64);
     if ((threadIdx.x & 63) == 0) s_pay[threadIdx.x >> 6] = y;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long tt = 0;
+      for (int k = 0; k < SER_WG / 64; k++) tt += s_pay[k];
+      // one partial per workgroup, reduced by k_ser_sum: 400k same-address device atomics serialised the pass
+      // (~2.4 ms of the empty pass on C3 10M, profiles/r02/ser_grid_sweep.txt)
+      P.pay_part[blockIdx.x] = tt;
+    }
   }
-  __syncthreads();
-  if (P.totals && threadIdx.x == 0) {
-    unsigned long long tt = 0;
-    for (int k = 0; k < SER_WG / 64; k++) tt += s_pay[k];
-    // one partial per workgroup, reduced by k_ser_sum: 400k same-address device atomics serialised the pass
-    // (~2.4 ms of the empty pass on C3 10M, profiles/r02/ser_grid_sweep.txt)
-    P.pay_part[blockIdx.x] = tt;
+  // phases (one encode site keeps the encoder inlined once): the whole tile staged, straight to HBM, or one
+  // phase per window
+  const int mywin = (nwin && live) ? (int)((off - o0) / ws) : -1;
+  const int nph = nwin ? nwin : 1;
+#pragma unroll 1
+  for (int ph = 0; ph < nph; ph++) {
+    uint64_t wlo = o0, whi = o1;
+    uint32_t sh = shift;
+    bool go = live;
+    uint8_t* dst = staged ? img + shift + (off - o0) : P.out + off;
+    if (nwin) {
+      wlo = s_wlo[ph];
+      whi = s_whi[ph];
+      if (wlo >= whi) continue;  // no value starts in this window (uniform)
+      sh = (uint32_t)(((uintptr_t)(P.out + wlo)) & 15);
+      go = mywin == ph;
+      dst = img + sh + (off - wlo);
+    }
+    if (go) {
+      W w;
+      w.dst = dst;
+      w.n = 0;
+      encode_value(P, pos, d, w);
+    }
+    if (staged || nwin) {
+      __syncthreads();
+      stream_image(img, P.out, wlo, sh, whi - wlo);
+      __syncthreads();  // the image is reused by the next window
+    }
   }
-  if (!staged) return;
-  // stream the image out: img[shift + k] -> out[o0 + k], k in [0, n); out + o0 - shift is 16-byte aligned
-  const uint64_t n = o1 - o0;
-  uint8_t* dst = P.out + o0 - shift;
-  const uint64_t lim = shift + n;  // image bytes [shift, lim) are ours
-  const uint64_t full_lo = (shift + 15) & ~15ull, full_hi = lim & ~15ull;
-  for (uint64_t c = full_lo + 16 * threadIdx.x; c < full_hi; c += 16 * SER_WG)
-    *(uint4*)(dst + c) = *(const uint4*)(img + c);
-  const uint64_t head_end = full_lo < lim ? full_lo : lim;
-  for (uint64_t c = shift + threadIdx.x; c < head_end; c += SER_WG) dst[c] = img[c];
-  const uint64_t tail_lo = full_hi > head_end ? full_hi : head_end;
-  for (uint64_t c = tail_lo + threadIdx.x; c < lim; c += SER_WG) dst[c] = img[c];
 }
 
 // payload-byte total of the write pass (one workgroup)
