@@ -271,7 +271,10 @@ struct Element {
   bytes encoded_headers = EMPTY_DOCUMENT;  // JobRecord.NO_HEADERS
   bytes message_name;
   JsonPathQuery correlation_key;
+  // zeebe:ioMapping (FlowNodeHandler.transformIoMappings, broker-core/.../transformation/handler/FlowNodeHandler.java:62-88)
   bool has_io_mapping = false;
+  std::vector<Mapping> input_mappings, output_mappings;
+  enum OutputBehavior : uint8_t { OB_UNSET = 0, OB_NONE, OB_MERGE, OB_OVERWRITE } output_behavior = OB_UNSET;
   int incoming = 0;                  // parallel gateway: sequence flows targeting it (join arity)
   uint8_t get_step(uint8_t intent) const {
     auto it = steps.find(intent);
@@ -435,7 +438,22 @@ class Transformer {
     // FlowNodeHandler (supertype first)
     {
       const XmlNode* io = ext(n, "ioMapping");
-      if (io) e->has_io_mapping = true;
+      if (io) {
+        e->has_io_mapping = true;
+        JsonPathCompiler jc;
+        for (const XmlNode* m : kids(io, "input"))
+          e->input_mappings.push_back({jc.compile(m->attr("source") ? *m->attr("source") : std::string()),
+                                       m->attr("target") ? *m->attr("target") : std::string()});
+        for (const XmlNode* m : kids(io, "output"))
+          e->output_mappings.push_back({jc.compile(m->attr("source") ? *m->attr("source") : std::string()),
+                                        m->attr("target") ? *m->attr("target") : std::string()});
+        if (const std::string* b = io->attr("outputBehavior")) {
+          if (*b == "none") e->output_behavior = Element::OB_NONE;
+          else if (*b == "merge") e->output_behavior = Element::OB_MERGE;
+          else if (*b == "overwrite") e->output_behavior = Element::OB_OVERWRITE;
+          else throw ZbError("invalid outputBehavior: " + *b);
+        }
+      }
       size_t n_out = kids(n, "outgoing").size();  // FlowNode.getOutgoing(): <outgoing> references
       current_outgoing_step_ = n_out == 0 ? S_CONSUME_TOKEN : S_TAKE_SEQUENCE_FLOW;
     }
@@ -629,6 +647,39 @@ class Engine {
   bool harness = true;
   std::string last_error;
 
+  // ZeebeIoMappingValidator (broker-core/.../validation/ZeebeIoMappingValidator.java:36-57), the model's
+  // ZeebeIoMappingValidator (bpmn-model/.../validation/zeebe/ZeebeIoMappingValidator.java:31-39) and
+  // ZeebeExpressionValidator.validateJsonPath (:42-54) for every source and target
+  static void validate_io_mapping(const Element& e) {
+    auto root_target = [](const std::vector<Mapping>& ms) {
+      for (auto& m : ms)
+        if (m.target == "$") return true;
+      return false;
+    };
+    if (e.input_mappings.size() > 1 && root_target(e.input_mappings))
+      throw ZbError("Invalid inputs: When using $ as target, no other input can be defined");
+    if (e.output_mappings.size() > 1 && root_target(e.output_mappings))
+      throw ZbError("Invalid outputs: When using $ as target, no other output can be defined");
+    if (e.output_behavior == Element::OB_NONE && !e.output_mappings.empty())
+      throw ZbError("Output behavior 'none' cannot be used in combination without zeebe:output elements");
+    JsonPathCompiler jc;
+    for (const auto* ms : {&e.input_mappings, &e.output_mappings})
+      for (auto& m : *ms) {
+        for (const bytes& path : {m.source.expression, m.target}) {
+          JsonPathQuery q = jc.compile(path);
+          if (!q.valid()) throw ZbError("JSON path query is invalid: " + q.error);
+          // PROHIBITED_PATHS_REGEX "(\\.\\*)|(\\[.*,.*\\])"
+          if (path.find(".*") != std::string::npos) throw ZbError("This JSON path query is not supported");
+          const size_t lb = path.find('[');
+          if (lb != std::string::npos) {
+            const size_t comma = path.find(',', lb + 1);
+            if (comma != std::string::npos && path.find(']', comma + 1) != std::string::npos)
+              throw ZbError("This JSON path query is not supported");
+          }
+        }
+      }
+  }
+
   void deploy(const std::string& xml, int64_t key, int32_t version) {
     XmlReader xr;
     auto doc = xr.parse(xml);
@@ -637,7 +688,7 @@ class Engine {
     int64_t k = key;
     for (auto& w : wfs) {
       for (auto& e : w->storage) {
-        if (e->has_io_mapping) throw ZbError("io mappings are not supported by the oracle yet");
+        if (e->has_io_mapping) validate_io_mapping(*e);
         if (e->condition && !e->condition->valid) throw ZbError("invalid condition: " + e->condition->error);
       }
       w->key = k++;
@@ -1163,16 +1214,28 @@ class Engine {
   void handle(uint8_t step, const Record& rec, Element* el, ElementInstance* ei, ElementInstance* scope, Workflow* wf) {
     WfValue v = rec.wf;
     switch (step) {
-      case S_APPLY_INPUT_MAPPING:  // InputMappingHandler (no mappings)
+      case S_APPLY_INPUT_MAPPING:  // InputMappingHandler :39-70
+        if (!el->input_mappings.empty()) {
+          try {
+            v.set_payload(map_extract(v.payload, el->input_mappings));
+          } catch (const MappingError& e) {
+            raise_incident(rec, ERR_IO_MAPPING, e.what());
+            break;
+          }
+        }
         write_followup_wf_event(rec.key, ELEMENT_ACTIVATED, v);
         break;
       case S_APPLY_OUTPUT_MAPPING: {  // OutputMappingHandler :42-85 (outputBehavior null => merge)
-        try {
-          bytes merged = merge_documents(v.payload, scope->value.payload);
-          v.set_payload(merged);
-        } catch (const MappingError& e) {
-          raise_incident(rec, ERR_IO_MAPPING, e.what());
-          break;
+        if (el->output_behavior == Element::OB_NONE) {
+          v.set_payload(scope->value.payload);
+        } else {
+          const bytes target = el->output_behavior == Element::OB_OVERWRITE ? EMPTY_DOCUMENT : scope->value.payload;
+          try {
+            v.set_payload(map_merge(v.payload, target, el->output_mappings));
+          } catch (const MappingError& e) {
+            raise_incident(rec, ERR_IO_MAPPING, e.what());
+            break;
+          }
         }
         write_followup_wf_event(rec.key, ELEMENT_COMPLETED, v);
         break;
@@ -1609,6 +1672,36 @@ int64_t zbref_merge(const uint8_t* src, size_t ns, const uint8_t* tgt, size_t nt
   } catch (const std::exception& ex) {
     std::snprintf(err, errcap, "%s", ex.what());
     return -1;
+  }
+}
+
+// MappingProcessor.extract (tgt == nullptr) / merge with explicit mappings; mappings = "source\ttarget\n"...
+// returns the result length, -1 MappingException (err has its message), -2 any other failure
+int64_t zbref_map(const uint8_t* src, size_t ns, const uint8_t* tgt, size_t nt, const char* mappings, uint8_t* out,
+                  size_t cap, char* err, size_t errcap) {
+  try {
+    std::vector<Mapping> ms;
+    JsonPathCompiler jc;
+    std::string all(mappings);
+    size_t p = 0;
+    while (p < all.size()) {
+      size_t nl = all.find('\n', p);
+      if (nl == std::string::npos) nl = all.size();
+      std::string line = all.substr(p, nl - p);
+      size_t tab = line.find('\t');
+      if (tab != std::string::npos) ms.push_back({jc.compile(line.substr(0, tab)), line.substr(tab + 1)});
+      p = nl + 1;
+    }
+    bytes s((const char*)src, ns);
+    bytes r = tgt ? map_merge(s, bytes((const char*)tgt, nt), ms) : map_extract(s, ms);
+    if (r.size() <= cap) std::memcpy(out, r.data(), r.size());
+    return (int64_t)r.size();
+  } catch (const MappingError& ex) {
+    std::snprintf(err, errcap, "%s", ex.what());
+    return -1;
+  } catch (const std::exception& ex) {
+    std::snprintf(err, errcap, "%s", ex.what());
+    return -2;
   }
 }
 

@@ -67,6 +67,8 @@ def lib():
                                                ctypes.POINTER(ctypes.c_int)]
         L.zbref_merge.restype = i64
         L.zbref_merge.argtypes = [u8p, sz, u8p, sz, ctypes.c_void_p, sz, ctypes.c_char_p, sz]
+        L.zbref_map.restype = i64
+        L.zbref_map.argtypes = [u8p, sz, u8p, sz, ctypes.c_char_p, ctypes.c_void_p, sz, ctypes.c_char_p, sz]
         L.zbref_query.argtypes = [cp, u8p, sz, ctypes.POINTER(i32), ctypes.c_int, ctypes.c_char_p, sz]
         L.zbref_subscription_hash.restype = i32
         L.zbref_subscription_hash.argtypes = [u8p, sz]
@@ -280,6 +282,24 @@ def merge(source: bytes, target: bytes) -> bytes:
     out = ctypes.create_string_buffer(65536)
     err = ctypes.create_string_buffer(4096)
     n = lib().zbref_merge(source, len(source), target, len(target), out, 65536, err, 4096)
+    if n < 0:
+        raise RuntimeError(err.value.decode())
+    return out.raw[:n]
+
+
+class MappingError(Exception):
+    """MappingException (json-path/.../mapping/MappingException.java): becomes an IO_MAPPING_ERROR incident."""
+
+
+def map_documents(source: bytes, mappings, target: Optional[bytes] = None) -> bytes:
+    """MappingProcessor.extract(source, mappings) (target None) or .merge(source, target, mappings)."""
+    spec = "".join("%s\t%s\n" % (a, b) for a, b in mappings).encode()
+    out = ctypes.create_string_buffer(1 << 20)
+    err = ctypes.create_string_buffer(4096)
+    n = lib().zbref_map(source, len(source), target, len(target) if target is not None else 0, spec, out, 1 << 20,
+                        err, 4096)
+    if n == -1:
+        raise MappingError(err.value.decode())
     if n < 0:
         raise RuntimeError(err.value.decode())
     return out.raw[:n]

@@ -44,6 +44,39 @@ inline const char* jp_token_name(JpToken t) {
   }
 }
 
+// JsonPathTokenizer.tokenize (json-path/.../jsonpath/JsonPathTokenizer.java:67-116): static tokens matched in
+// table order, everything between them a LITERAL; after "['" only "']" is recognised.
+template <class F>
+inline void jp_tokenize(const bytes& expr, F&& visit) {
+  static const struct { JpToken t; const char* rep; } ALL[8] = {
+      {JpToken::ROOT_OBJECT, "$"}, {JpToken::RECURSION_OPERATOR, ".."}, {JpToken::CHILD_OPERATOR, "."},
+      {JpToken::WILDCARD, "*"}, {JpToken::CHILD_BRACKET_OPERATOR_BEGIN, "['"},
+      {JpToken::CHILD_BRACKET_OPERATOR_END, "']"}, {JpToken::SUBSCRIPT_OPERATOR_BEGIN, "["},
+      {JpToken::SUBSCRIPT_OPERATOR_END, "]"}};
+  const int length = (int)expr.size();
+  int position = 0, last_end = 0;
+  bool child_bracket = false;
+  visit(JpToken::START_INPUT, 0, length);
+  while (position < length) {
+    bool matched = false;
+    for (int i = 0; i < 8 && !matched; i++) {
+      if (child_bracket && ALL[i].t != JpToken::CHILD_BRACKET_OPERATOR_END) continue;
+      const size_t rl = std::strlen(ALL[i].rep);
+      if (position + rl <= expr.size() && expr.compare(position, rl, ALL[i].rep) == 0) {
+        if (last_end < position) visit(JpToken::LITERAL, last_end, position - last_end);
+        child_bracket = ALL[i].t == JpToken::CHILD_BRACKET_OPERATOR_BEGIN;
+        visit(ALL[i].t, position, (int)rl);
+        position += (int)rl;
+        last_end = position;
+        matched = true;
+      }
+    }
+    if (!matched) position++;
+  }
+  if (last_end < position) visit(JpToken::LITERAL, last_end, position - last_end);
+  visit(JpToken::END_INPUT, 0, length);
+}
+
 struct JsonPathQuery {
   bytes expression;
   std::vector<JpFilter> filters;
@@ -108,33 +141,7 @@ struct JsonPathCompiler {
     query.expression = expr;
     q = &query;
     mode = DEFAULT;
-    static const struct { JpToken t; const char* rep; } ALL[8] = {
-        {JpToken::ROOT_OBJECT, "$"}, {JpToken::RECURSION_OPERATOR, ".."}, {JpToken::CHILD_OPERATOR, "."},
-        {JpToken::WILDCARD, "*"}, {JpToken::CHILD_BRACKET_OPERATOR_BEGIN, "['"},
-        {JpToken::CHILD_BRACKET_OPERATOR_END, "']"}, {JpToken::SUBSCRIPT_OPERATOR_BEGIN, "["},
-        {JpToken::SUBSCRIPT_OPERATOR_END, "]"}};
-    const int length = (int)expr.size();
-    int position = 0, last_end = 0;
-    bool child_bracket = false;
-    visit(JpToken::START_INPUT, expr, 0, length);
-    while (position < length) {
-      bool matched = false;
-      for (int i = 0; i < 8 && !matched; i++) {
-        if (child_bracket && ALL[i].t != JpToken::CHILD_BRACKET_OPERATOR_END) continue;
-        const size_t rl = std::strlen(ALL[i].rep);
-        if (position + rl <= expr.size() && expr.compare(position, rl, ALL[i].rep) == 0) {
-          if (last_end < position) visit(JpToken::LITERAL, expr, last_end, position - last_end);
-          child_bracket = ALL[i].t == JpToken::CHILD_BRACKET_OPERATOR_BEGIN;
-          visit(ALL[i].t, expr, position, (int)rl);
-          position += (int)rl;
-          last_end = position;
-          matched = true;
-        }
-      }
-      if (!matched) position++;
-    }
-    if (last_end < position) visit(JpToken::LITERAL, expr, last_end, position - last_end);
-    visit(JpToken::END_INPUT, expr, 0, length);
+    jp_tokenize(expr, [&](JpToken t, int off, int len) { visit(t, expr, off, len); });
     q = nullptr;
     return query;
   }

@@ -14,6 +14,7 @@
 #include <unordered_set>
 #include <vector>
 
+#include "zbref_jsonpath.hpp"
 #include "zbref_msgpack.hpp"
 
 namespace zbref {
@@ -59,6 +60,10 @@ struct MsgPackTree {
   bool is_array(const std::string& id) const {
     auto it = node_type.find(id);
     return it != node_type.end() && it->second == NodeType::ARRAY;
+  }
+  bool is_map(const std::string& id) const {
+    auto it = node_type.find(id);
+    return it != node_type.end() && it->second == NodeType::MAP;
   }
 
   // MsgPackTree.merge :141-166 (top-level merge: only the root child set is unioned)
@@ -249,6 +254,86 @@ inline bytes merge_documents(const bytes& source, const bytes& target) {
   MpType ty = mp_format_type((uint8_t)out[0]);
   if (ty != MpType::MAP && ty != MpType::NIL)
     throw MappingError("Processing failed, since mapping will result in a non map object (json object).");
+  return out;
+}
+
+// ------------------------------------------------------------------------------ explicit mappings
+// Mapping (json-path/.../mapping/Mapping.java): a compiled source query and a target path.
+struct Mapping {
+  JsonPathQuery source;
+  bytes target;
+};
+
+inline void ensure_map_result(const bytes& out) {  // MappingProcessor.ensureDocumentIsAMsgPackMap :206-213
+  MpType ty = mp_format_type((uint8_t)out[0]);
+  if (ty != MpType::MAP && ty != MpType::NIL)
+    throw MappingError("Processing failed, since mapping will result in a non map object (json object).");
+}
+
+// MsgPackDocumentExtractor.createParentRelation :146-166
+inline std::string create_parent_relation(MsgPackTree& t, const std::string& parent, const std::string& name) {
+  if (parent.empty()) return name;
+  bool is_index = true;  // isIndex :168-177 (an empty name counts as an index)
+  for (char c : name)
+    if (c < '0' || c > '9') { is_index = false; break; }
+  if (is_index) {
+    if (!t.is_map(parent)) t.add_array(parent);
+  } else {
+    t.add_map(parent);
+  }
+  std::string id = node_id(parent, name);
+  t.add_child(name, parent);
+  return id;
+}
+
+// MsgPackDocumentExtractor.extract :121-128 with TargetPathVisitor :205-228 and executeLeafMapping :185-203
+inline void extract_mappings(MsgPackTree& t, const bytes& doc, const std::vector<Mapping>& mappings) {
+  t.extract = &doc;  // setExtractDocument
+  for (const Mapping& m : mappings) {
+    std::string node, parent;
+    jp_tokenize(m.target, [&](JpToken type, int off, int len) {
+      if (type == JpToken::LITERAL || type == JpToken::ROOT_OBJECT) {
+        node = create_parent_relation(t, parent, m.target.substr(off, len));
+        parent = node;
+      } else if (type == JpToken::END_INPUT) {
+        JsonPathExecutor ex;
+        ex.run(m.source.filters, (const uint8_t*)doc.data(), doc.size());
+        if (ex.results.empty())
+          throw MappingError("No data found for query " + m.source.expression + ".");
+        if (ex.results.size() > 1)  // IllegalStateException: not a MappingException, the processor fails
+          throw ZbError("JSON path mapping has more than one matching source.");
+        t.add_leaf(node, (uint32_t)ex.results[0].position, (uint32_t)ex.results[0].length);
+      }
+    });
+  }
+}
+
+// MappingProcessor.extract :179-190
+inline bytes map_extract(const bytes& source, const std::vector<Mapping>& mappings) {
+  MsgPackTree t;
+  if (mappings.empty()) {
+    DocumentIndexer ix;
+    ix.index(t, source);
+  } else {
+    extract_mappings(t, source, mappings);
+  }
+  TreeWriter tw;
+  bytes out = tw.write(t);
+  ensure_map_result(out);
+  return out;
+}
+
+// MappingProcessor.merge :143-170 (the target is indexed, then the mappings extract into its tree)
+inline bytes map_merge(const bytes& source, const bytes& target, const std::vector<Mapping>& mappings) {
+  if (mappings.empty()) return merge_documents(source, target);
+  if (target.empty()) return map_extract(source, mappings);
+  MsgPackTree t;
+  DocumentIndexer ix;
+  ix.index(t, target);
+  extract_mappings(t, source, mappings);
+  TreeWriter tw;
+  bytes out = tw.write(t);
+  ensure_map_result(out);
   return out;
 }
 

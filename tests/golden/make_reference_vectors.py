@@ -324,6 +324,217 @@ def cancels():
     ]
 
 
+
+# ------------------------------------------------------------------------------ explicit io-mappings
+REF = "/root/reference"
+MAPPING_TESTS = "json-path/src/test/java/io/zeebe/msgpack/mapping"
+
+
+class _JavaRows:
+    """Reads the rows of a JUnit `parameters()` table (`new Object[][] { {...}, ... }`) from the reference
+    test source: Java string literals (concatenated with +), null, createMapping(src, tgt),
+    createMappings().mapping(src, tgt)...build(), and the largeJsonDocument.json resource."""
+
+    def __init__(self, text, res_dir):
+        self.s = text
+        self.i = text.index("new Object[][]")
+        self.i = text.index("{", self.i) + 1
+        self.res_dir = res_dir
+
+    def ws(self):
+        while self.i < len(self.s):
+            if self.s[self.i].isspace():
+                self.i += 1
+            elif self.s.startswith("//", self.i):
+                self.i = self.s.index("\n", self.i)
+            else:
+                break
+
+    def string(self):
+        assert self.s[self.i] == '"'
+        j = self.i + 1
+        out = []
+        while self.s[j] != '"':
+            if self.s[j] == "\\":
+                out.append(self.s[j + 1])
+                j += 2
+            else:
+                out.append(self.s[j])
+                j += 1
+        self.i = j + 1
+        return "".join(out)
+
+    def value(self):
+        self.ws()
+        if self.s.startswith("null", self.i):
+            self.i += 4
+            return None
+        if self.s[self.i] == '"':
+            v = self.string()
+            while True:
+                self.ws()
+                if self.s[self.i] == "+":
+                    self.i += 1
+                    self.ws()
+                    v += self.string()
+                else:
+                    return v
+        if self.s.startswith("createMappings()", self.i):
+            self.i += len("createMappings()")
+            ms = []
+            while True:
+                self.ws()
+                if self.s.startswith(".mapping(", self.i):
+                    self.i += len(".mapping(")
+                    self.ws()
+                    a = self.string()
+                    self.ws(); assert self.s[self.i] == ","; self.i += 1; self.ws()
+                    b = self.string()
+                    self.ws(); assert self.s[self.i] == ")"; self.i += 1
+                    ms.append([a, b])
+                elif self.s.startswith(".build()", self.i):
+                    self.i += len(".build()")
+                    return ms
+                else:
+                    raise ValueError(self.s[self.i:self.i + 40])
+        if self.s.startswith("createMapping(", self.i):
+            self.i += len("createMapping(")
+            self.ws()
+            a = self.string()
+            self.ws(); assert self.s[self.i] == ","; self.i += 1; self.ws()
+            b = self.string()
+            self.ws(); assert self.s[self.i] == ")"; self.i += 1
+            return [[a, b]]
+        if self.s.startswith("new String(", self.i):
+            k = self.s.index('getResource("', self.i) + len('getResource("')
+            name = self.s[k:self.s.index('"', k)]
+            self.i = self.s.index(".toURI())))", self.i) + len(".toURI())))")
+            with open(os.path.join(self.res_dir, name)) as f:
+                return f.read()
+        raise ValueError(self.s[self.i:self.i + 60])
+
+    def rows(self):
+        out = []
+        while True:
+            self.ws()
+            if self.s[self.i] == "}":
+                return out
+            assert self.s[self.i] == "{", self.s[self.i:self.i + 40]
+            self.i += 1
+            row = []
+            while True:
+                row.append(self.value())
+                self.ws()
+                if self.s[self.i] == ",":
+                    self.i += 1
+                    self.ws()
+                    if self.s[self.i] == "}":
+                        self.i += 1
+                        break
+                    continue
+                assert self.s[self.i] == "}", self.s[self.i:self.i + 40]
+                self.i += 1
+                break
+            out.append(row)
+            self.ws()
+            if self.s[self.i] == ",":
+                self.i += 1
+
+
+def _java_rows(name):
+    with open(os.path.join(REF, MAPPING_TESTS, name)) as f:
+        text = f.read()
+    return _JavaRows(text, os.path.join(REF, "json-path/src/test/resources/io/zeebe/msgpack/mapping")).rows()
+
+
+def _tree(s):
+    """JSON_MAPPER.readTree with ALLOW_SINGLE_QUOTES; Jackson ignores a trailing '}' after the root value."""
+    return json.JSONDecoder().raw_decode(s.replace("'", '"'))[0]
+
+
+def mapping_extracts():
+    # json-path/src/test/java/io/zeebe/msgpack/mapping/MappingExtractParameterizedTest.java:40-230 (all rows),
+    # MappingExtractTest.java:51-79 (exceptions), :81-113 (extract twice); compared as JSON trees
+    out = [{"source": mp(_tree(src)), "mappings": ms or [], "expected_json": _tree(exp)}
+           for src, ms, exp in _java_rows("MappingExtractParameterizedTest.java")]
+    out += [
+        {"source": "80", "mappings": [["$.foo", "$"]], "error": "No data found for query $.foo."},
+        {"source": mp({"foo": "bar"}), "mappings": [["$.foo", "$"]],
+         "error": "Processing failed, since mapping will result in a non map object (json object)."},
+        {"source": mp(_tree("{'arr':[{'deepObj':{'value':123}}, 1], 'obj':{'int':1}, 'test':'value'}")),
+         "mappings": [["$.arr[0]", "$"]], "expected_json": {"deepObj": {"value": 123}}},
+        {"source": mp({"deepObj": {"value": 123}}), "mappings": [["$.deepObj", "$"]], "expected_json": {"value": 123}},
+    ]
+    return out
+
+
+def mapping_merges():
+    # json-path/src/test/java/io/zeebe/msgpack/mapping/MappingMergeParameterizedTest.java:40-420 (all rows;
+    # the mapping-less ones are also in `merges`), MappingMergeTest.java:70-100 (exceptions)
+    out = [{"source": mp(_tree(src)), "target": mp(_tree(tgt)), "mappings": ms or [], "expected_json": _tree(exp)}
+           for src, tgt, ms, exp in _java_rows("MappingMergeParameterizedTest.java")]
+    out += [
+        {"source": "80", "target": "80", "mappings": [["$.foo", "$"]], "error": "No data found for query $.foo."},
+        {"source": mp({"foo": "bar"}), "target": mp({"foo": "bar"}), "mappings": [["$.foo", "$"]],
+         "error": "Processing failed, since mapping will result in a non map object (json object)."},
+    ]
+    return out
+
+
+def io_workflows():
+    # broker-core/src/test/java/io/zeebe/broker/workflow/WorkflowTaskIOMappingTest.java: start -> service task
+    # "service" (type "external") -> end. create / complete payloads: MsgPackUtil.JSON_DOCUMENT (MSGPACK_PAYLOAD),
+    # OTHER_DOCUMENT (OTHER_PAYLOAD); a completion without payload completes with {} . Expected: the JOB CREATE
+    # payload, the task's ELEMENT_COMPLETED payload, or the incident's errorMessage (IO_MAPPING_ERROR).
+    jd = "{'string':'value', 'jsonObject':{'testAttr':'test'}}"
+    od = "{'string':'bar', 'otherObject':{'testAttr':'test'}}"
+    merged = "{'string':'bar', 'jsonObject':{'testAttr':'test'}, 'otherObject':{'testAttr':'test'}}"
+    rows = [
+        # name, inputs, outputs, behavior, create, complete, job payload, completed payload, incident
+        ("shouldCreateTwoNewObjectsViaInputMapping :90-113", [["$.string", "$.newFoo"], ["$.jsonObject", "$.newObj"]],
+         [], None, jd, None, "{'newFoo':'value', 'newObj':{'testAttr':'test'}}", None, None),
+        ("shouldCreateIncidentForNoMatchOnInputMapping :134-156", [["$.notExisting", "$"]], [], None, jd, None, None,
+         None, "No data found for query $.notExisting."),
+        ("shouldCreateIncidentForNonMatchingAndMatchingValueOnInputMapping :158-183",
+         [["$.notExisting", "$.nullVal"], ["$.string", "$.existing"]], [], None, jd, None, None, None,
+         "No data found for query $.notExisting."),
+        ("shouldUseOutputMappingWithNoWorkflowPayload :232-254", [], [["$.string", "$.foo"]], None, None, od, None,
+         "{'foo':'bar'}", None),
+        ("shouldUseNoneOutputBehaviorWithoutCompletePayload :256-279", [], [], "none", jd, None, None, jd, None),
+        ("shouldUseNoneOutputBehaviorAndCompletePayload :281-304", [], [], "none", jd, od, None, jd, None),
+        ("shouldUseOverwriteOutputBehaviorWithoutCompletePayload :306-329", [], [], "overwrite", jd, None, None,
+         "{}", None),
+        ("shouldUseOverwriteOutputBehaviorAndCompletePayload :331-354", [], [], "overwrite", jd, od, None, od, None),
+        ("shouldUseOverwriteOutputBehaviorWithOutputMappingAndCompletePayload :356-383", [], [["$.string", "$.foo"]],
+         "overwrite", jd, od, None, "{'foo':'bar'}", None),
+        ("shouldCreateIncidentOnOverwriteOutputBehaviorWithOutputMappingAndWithoutCompletedPayload :385-414", [],
+         [["$.string", "$.foo"]], "overwrite", jd, None, None, None, "No data found for query $.string."),
+        ("shouldNotSeePayloadOfWorkflowInstanceBeforeOnOutputMapping :497-538 (first instance)", [],
+         [["$", "$.taskPayload"]], None, jd, jd, None,
+         "{'string':'value', 'jsonObject':{'testAttr':'test'},'taskPayload':{'string':'value', "
+         "'jsonObject':{'testAttr':'test'}}}", None),
+        ("shouldUseDefaultOutputMappingIfOnlyInputMappingSpecified :540-566", [["$", "$"]], [], None, jd, od, None,
+         merged, None),
+        ("shouldUseOutputMappingToAddObjectsToWorkflowPayload :591-620", [],
+         [["$.string", "$.newFoo"], ["$.jsonObject", "$.newObj"]], None, jd, jd, None,
+         "{'newFoo':'value', 'newObj':{'testAttr':'test'}, 'string':'value', 'jsonObject':{'testAttr':'test'}}",
+         None),
+        ("shouldCreateIncidentForNotMatchingOnOutputMapping :622-648", [], [["$.notExisting", "$.notExist"]], None,
+         jd, jd, None, None, "No data found for query $.notExisting."),
+        ("shouldUseInOutMapping :650-690", [["$.jsonObject", "$"]], [["$.testAttr", "$.result"]], None, jd,
+         "{'testAttr':123}", "{'testAttr':'test'}",
+         "{'string':'value', 'jsonObject':{'testAttr':'test'}, 'result':123}", None),
+    ]
+    out = []
+    for name, ins, outs, beh, create, complete, job, done, inc in rows:
+        out.append({"name": name, "inputs": ins, "outputs": outs, "behavior": beh,
+                    "create": mp(_tree(create)) if create else None,
+                    "complete": mp(_tree(complete)) if complete else "80",
+                    "job_payload_json": _tree(job) if job else None,
+                    "completed_payload_json": _tree(done) if done else None,
+                    "incident": inc})
+    return out
+
 def main():
     data = {
         "conditions": conditions(),
@@ -335,6 +546,9 @@ def main():
         "hashes": hashes(),
         "workflows": workflows(),
         "cancels": cancels(),
+        "mapping_extracts": mapping_extracts(),
+        "mapping_merges": mapping_merges(),
+        "io_workflows": io_workflows(),
         "wf_intents": WF,
     }
     with open(os.path.join(HERE, "reference_vectors.json"), "w") as f:
