@@ -231,6 +231,11 @@ struct Record {
   uint8_t intent = 0;
   uint8_t rejection_type = REJ_NULL;
   std::string rejection_reason;
+  // log frame fields (LogStreamBatchWriterImpl.java:232-268, RecordMetadata.java:236-249 reset values)
+  uint64_t request_id = UINT64_MAX;       // RecordMetadataEncoder.requestIdNullValue
+  int32_t request_stream_id = INT32_MIN;  // RecordMetadataEncoder.requestStreamIdNullValue
+  int32_t producer_id = -1;               // LogStreamBatchWriterImpl.reset :280 (client / external writers)
+  uint8_t batch_flags = 0;                // DataFrameDescriptor BEGIN 0x80 / END 0x40 (ClaimedFragmentBatch.commit)
   WfValue wf;
   JobValue job;
   IncidentValue inc;
@@ -977,10 +982,26 @@ class Engine {
       throw;
     }
     w_ = nullptr;
-    for (auto& r : w.staged) {
+    // TypedStreamProcessor: writer.configureSourceContext(streamProcessorId, position) (StreamProcessorIds.java:23-39):
+    // the job processor (harness) 10, the message processor 90, the workflow instance processor 70
+    const int32_t producer = rec.value_type == VT_JOB && rec.record_type == RT_COMMAND ? 10
+                           : (rec.value_type == VT_MESSAGE || rec.value_type == VT_MESSAGE_SUBSCRIPTION) ? 90 : 70;
+    const size_t nst = w.staged.size();
+    for (size_t k = 0; k < nst; k++) {
+      Record& r = w.staged[k];
       r.raw_value.clear();  // follow-ups are encoded from their value objects
       if (r.value_type == VT_WORKFLOW_INSTANCE && r.record_type == RT_EVENT) transitions++;
       r.source_position = rec.position;
+      r.producer_id = producer;
+      // ClaimedFragmentBatch.commit :130-147: batch flags only when the batch holds more than one fragment
+      r.batch_flags = nst > 1 ? (k == 0 ? 0x80 : (k + 1 == nst ? 0x40 : 0)) : 0;
+      // RecordMetadata.reset on every write; only the CREATE processor copies the command's request
+      // metadata, onto CREATED and onto its rejection (WorkflowInstanceStreamProcessor.java:254-257, :370-377)
+      const bool keeps = r.value_type == VT_WORKFLOW_INSTANCE &&
+                         ((r.record_type == RT_EVENT && r.intent == CREATED) ||
+                          (r.record_type == RT_REJECTION && r.intent == CREATE));
+      r.request_id = keeps ? rec.request_id : UINT64_MAX;
+      r.request_stream_id = keeps ? rec.request_stream_id : INT32_MIN;
       append(std::move(r));
     }
   }
@@ -1401,8 +1422,62 @@ class Engine {
 
 }  // namespace zbref
 
+
 // =============================================================================== C API (ctypes)
 using namespace zbref;
+
+// ------------------------------------------------------------------------------ log frames (§8f rank 1)
+// One record as LogStreamBatchWriterImpl.writeEventsToBuffer (:222-268) / LogStreamWriterImpl.tryWrite lay it
+// into the dispatcher buffer: DataFrameDescriptor header (:53-96, 12 B: framed length, version, flags, type
+// TYPE_MESSAGE, stream id = partition id), LogEntryDescriptor header (:28-121, 48 B), RecordMetadata
+// (RecordMetadata.java:96-128: SBE message header + 34-byte block + varData rejectionReason, protocol.xml:135-146),
+// the value, zero padding to FRAME_ALIGNMENT 8. Position: the record's log position (the dispatcher would
+// derive it from the byte offset of the claim; the caller maps it).
+static void put_le(bytes& b, uint64_t v, int n) {
+  for (int i = 0; i < n; i++) b.push_back((char)(uint8_t)(v >> (8 * i)));
+}
+bytes encode_frame(const Record& r, int32_t stream_id, int32_t raft_term, int64_t timestamp) {
+  const bytes v = r.encode_value();
+  const std::string& reason = r.record_type == RT_REJECTION ? r.rejection_reason : std::string();
+  const uint32_t meta_len = 8 + 34 + 2 + (uint32_t)reason.size();
+  const uint32_t framed = 12 + 48 + meta_len + (uint32_t)v.size();
+  bytes b;
+  b.reserve((framed + 7) & ~7u);
+  put_le(b, framed, 4);
+  put_le(b, 0, 1);                 // version
+  put_le(b, r.batch_flags, 1);
+  put_le(b, 0, 2);                 // TYPE_MESSAGE
+  put_le(b, (uint32_t)stream_id, 4);
+  put_le(b, 0, 2);                 // LogEntryDescriptor version
+  put_le(b, 0, 2);                 // reserved
+  put_le(b, (uint64_t)r.position, 8);
+  put_le(b, (uint32_t)raft_term, 4);
+  put_le(b, (uint32_t)r.producer_id, 4);
+  put_le(b, (uint64_t)r.source_position, 8);
+  put_le(b, (uint64_t)r.key, 8);
+  put_le(b, (uint64_t)timestamp, 8);
+  put_le(b, meta_len, 2);
+  put_le(b, 0, 2);                 // unused
+  put_le(b, 34, 2);                // SBE header: blockLength, templateId 200, schemaId 0, version 1
+  put_le(b, 200, 2);
+  put_le(b, 0, 2);
+  put_le(b, 1, 2);
+  put_le(b, r.record_type, 1);
+  put_le(b, (uint32_t)r.request_stream_id, 4);
+  put_le(b, r.request_id, 8);
+  put_le(b, UINT64_MAX, 8);        // subscriptionId (null)
+  put_le(b, 1, 2);                 // protocolVersion = Protocol.PROTOCOL_VERSION
+  put_le(b, r.value_type, 1);
+  put_le(b, r.intent, 1);
+  put_le(b, UINT64_MAX, 8);        // incidentKey (null)
+  put_le(b, r.rejection_type, 1);
+  put_le(b, reason.size(), 2);
+  b.append(reason);
+  b.append(v);
+  while (b.size() & 7) b.push_back(0);
+  return b;
+}
+
 
 struct zbref_record {
   int64_t position;
@@ -1566,6 +1641,29 @@ int64_t zbref_run(void* h, int64_t max_records) {
     if (e->last_error.empty()) e->last_error = ex.what();
     return -1;
   }
+}
+
+// request metadata of a submitted command (the client API's requestId / requestStreamId)
+int zbref_set_request(void* h, int64_t position, uint64_t request_id, int32_t request_stream_id) {
+  Engine* e = (Engine*)h;
+  if (position < 0 || position >= (int64_t)e->log.size()) return -1;
+  e->log[(size_t)position].request_id = request_id;
+  e->log[(size_t)position].request_stream_id = request_stream_id;
+  return 0;
+}
+
+// log frames of records [from, to), contiguous; returns the byte count (written when it fits cap)
+int64_t zbref_frames(void* h, int64_t from, int64_t to, int32_t stream_id, int32_t raft_term, int64_t timestamp,
+                     uint8_t* buf, size_t cap) {
+  Engine* e = (Engine*)h;
+  if (to < 0 || to > (int64_t)e->log.size()) to = (int64_t)e->log.size();
+  size_t off = 0;
+  for (int64_t i = from; i < to; i++) {
+    const bytes f = encode_frame(e->log[(size_t)i], stream_id, raft_term, timestamp);
+    if (buf && off + f.size() <= cap) std::memcpy(buf + off, f.data(), f.size());
+    off += f.size();
+  }
+  return (int64_t)off;
 }
 
 int64_t zbref_log_size(void* h) { return (int64_t)((Engine*)h)->log.size(); }

@@ -76,6 +76,9 @@ def lib():
         L.zbref_encode_int.argtypes = [i64, ctypes.c_void_p]
         L.zbref_encode_float.restype = i64
         L.zbref_encode_float.argtypes = [ctypes.c_double, ctypes.c_void_p]
+        L.zbref_set_request.argtypes = [vp, i64, ctypes.c_uint64, i32]
+        L.zbref_frames.restype = i64
+        L.zbref_frames.argtypes = [vp, i64, i64, i32, i32, i64, ctypes.c_void_p, sz]
         L.zbref_run_timed.restype = ctypes.c_double
         L.zbref_run_timed.argtypes = [vp, ctypes.POINTER(i64)]
         _lib = L
@@ -247,6 +250,20 @@ class Oracle:
         need = self._L.zbref_dump_log(self._h, start, end, None, 0)
         buf = ctypes.create_string_buffer(max(need, 1))
         self._L.zbref_dump_log(self._h, start, end, buf, need)
+        return buf.raw[:need]
+
+    def set_request(self, position: int, request_id: int, request_stream_id: int):
+        """Request metadata (requestId, requestStreamId) of the submitted command at `position`."""
+        if self._L.zbref_set_request(self._h, position, request_id, request_stream_id):
+            raise ZbrefError("no record at position %d" % position)
+
+    def frames(self, start: int = 0, end: int = -1, stream_id: int = 0, raft_term: int = 0,
+               timestamp: int = 0) -> bytes:
+        """Log frames of records [start, end) as the reference's log writers lay them into the dispatcher
+        buffer (DataFrameDescriptor + LogEntryDescriptor + RecordMetadata + value, 8-aligned)."""
+        need = self._L.zbref_frames(self._h, start, end, stream_id, raft_term, timestamp, None, 0)
+        buf = ctypes.create_string_buffer(max(need, 1))
+        self._L.zbref_frames(self._h, start, end, stream_id, raft_term, timestamp, buf, need)
         return buf.raw[:need]
 
     def counters(self) -> dict:

@@ -117,3 +117,38 @@ def job_event(create_value: bytes, payload=None) -> bytes:
     for k, raw in p.items():
         out += mp_str(k) + (mp_bin(_doc(payload)) if k == "payload" else raw)
     return out
+
+
+# ---- log frames (zb_serialize_frames): DataFrameDescriptor.java:53-96 + LogEntryDescriptor.java:28-121 +
+# RecordMetadata (protocol.xml:135-146; SBE message header + 34-byte block + varData rejectionReason)
+FRAME_ALIGNMENT = 8
+FLAG_BATCH_BEGIN, FLAG_BATCH_END = 0x80, 0x40
+_DF = struct.Struct("<iBBhi")                 # framed length, version, flags, type, stream id
+_LE = struct.Struct("<hhqiiqqqhh")            # version, reserved, position, raft term, producer id,
+                                              # source event position, key, timestamp, metadata length, unused
+_SBE = struct.Struct("<HHHHBiQQHBBQB")        # blockLength templateId schemaId version | recordType
+                                              # requestStreamId requestId subscriptionId protocolVersion
+                                              # valueType intent incidentKey rejectionType
+
+
+def parse_frames(buf) -> list:
+    """Log frames -> list of dicts (one per record), as a log reader (LoggedEventImpl) sees them."""
+    buf = bytes(buf)
+    out, off = [], 0
+    while off < len(buf):
+        framed, ver, flags, typ, stream = _DF.unpack_from(buf, off)
+        le = off + _DF.size
+        (_, _, pos, term, producer, src, key, ts, mlen, _) = _LE.unpack_from(buf, le)
+        mo = le + _LE.size
+        (blen, tmpl, schema, sver, rt, rsid, rid, sub, pver, vt, it, ik, rj) = _SBE.unpack_from(buf, mo)
+        rlen = struct.unpack_from("<H", buf, mo + 8 + blen)[0]
+        reason = buf[mo + 8 + blen + 2:mo + 8 + blen + 2 + rlen]
+        value = buf[mo + mlen:off + framed]
+        out.append(dict(framed_length=framed, version=ver, flags=flags, type=typ, stream_id=stream, position=pos,
+                        raft_term=term, producer_id=producer, source_position=src, key=key, timestamp=ts,
+                        metadata_length=mlen, block_length=blen, template_id=tmpl, schema_id=schema,
+                        schema_version=sver, record_type=rt, request_stream_id=rsid, request_id=rid,
+                        subscription_id=sub, protocol_version=pver, value_type=vt, intent=it, incident_key=ik,
+                        rejection_type=rj, rejection_reason=reason, value=value))
+        off += (framed + FRAME_ALIGNMENT - 1) & ~(FRAME_ALIGNMENT - 1)
+    return out
