@@ -265,6 +265,26 @@ int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats*
 /* headers: NULL or room for the batch's headers; values: NULL or values_len bytes from value byte
  * value_off of the batch. */
 int zb_drain_copy(zb_engine* e, zb_record_header* headers, uint8_t* values, uint64_t value_off, size_t values_len);
+/* Log frames: zb_serialize_frames serializes records [start, start+count) into the
+ * drain buffer as the byte stream the reference's log writers append to the dispatcher buffer
+ * (LogStreamBatchWriterImpl.java:222-268, LogStreamWriterImpl.java:150-205): per record a
+ * DataFrameDescriptor header (DataFrameDescriptor.java:53-96; batch begin / end flags per
+ * ClaimedFragmentBatch.commit), a LogEntryDescriptor header (LogEntryDescriptor.java:28-121), the SBE
+ * RecordMetadata (RecordMetadata.java:96-128, protocol.xml:135-146) with the rejection reason, the value
+ * and zero padding to 8 bytes. Positions are the engine's log positions (the dispatcher derives them from
+ * the claim offset: the caller maps them). stats->value_bytes = frame bytes; zb_drain_copy(e, NULL, buf,
+ * off, len) copies them. */
+typedef struct zb_frame_config {
+  int32_t stream_id;   /* dispatcher stream id = the log's partition id (LogStreamBatchWriterImpl.java:90) */
+  int32_t raft_term;   /* LogStream.getTerm() */
+  int64_t timestamp;   /* ActorClock.currentTimeMillis() of the tick, written into every frame */
+} zb_frame_config;
+int zb_serialize_frames(zb_engine* e, int64_t start, int64_t count, const zb_frame_config* fc,
+                        zb_serialize_stats* stats);
+/* Request metadata (RecordMetadata requestId / requestStreamId, ClientApiMessageHandler) of the last n
+ * records staged by zb_submit / zb_submit_creates; CREATED and the CREATE rejection copy it from their
+ * command (WorkflowInstanceStreamProcessor.java:254-257, :370-377). Frames only. */
+int zb_set_request_metadata(zb_engine* e, size_t n, const uint64_t* request_ids, const int32_t* request_stream_ids);
 /* Page-locked host memory for zb_drain_copy destinations (hipHostMalloc); NULL on failure. */
 void* zb_pinned_alloc(size_t bytes);
 void zb_pinned_free(void* p);

@@ -11,6 +11,8 @@ import random
 import msgpack
 import pytest
 
+from frames_check import assert_frames_equal
+
 from oracle import zbref
 from zeebe_amd import bpmn, workloads
 
@@ -40,6 +42,7 @@ def _run(xml, process, payloads, job_payloads=None, wave_only=False, **cap):
                (b.position, b.key, b.record_type, b.value_type, b.intent), (a, b)
         assert a.value == b.value, (a.position, msgpack.unpackb(a.value, raw=False),
                                     msgpack.unpackb(b.value, raw=False))
+    assert_frames_equal(o, e)
     oc, ec = o.counters(), e.counters()
     assert (ec["next_wf_key"], ec["next_job_key"], ec["completed"]) == \
            (oc["next_wf_key"], oc["next_job_key"], oc["completed"])

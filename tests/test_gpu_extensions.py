@@ -12,6 +12,7 @@ Every log record is compared bit-exact (position, key, record / value type, inte
 import msgpack
 import pytest
 
+from frames_check import assert_frames_equal
 from oracle import zbref
 from zeebe_amd import bpmn, records as R, workloads
 
@@ -35,6 +36,7 @@ def compare_logs(o, e, start=0):
         if b.record_type == R.RT_REJECTION:
             assert a.rejection_type == b.rejection_type, (a, b)
         assert a.value == b.value, (a.position, msgpack.unpackb(a.value, raw=False), msgpack.unpackb(b.value, raw=False))
+    assert_frames_equal(o, e, start)
     return ref
 
 

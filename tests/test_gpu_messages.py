@@ -8,6 +8,7 @@ msgpack value bytes.
 import msgpack
 import pytest
 
+from frames_check import assert_frames_equal
 from oracle import zbref
 from zeebe_amd import bpmn, cluster
 
@@ -43,6 +44,7 @@ def compare(gpu, ref):
                 assert x.rejection_type == y.rejection_type, (p, x, y)
             assert x.value == y.value, (p, x.position, msgpack.unpackb(x.value, raw=False),
                                         msgpack.unpackb(y.value, raw=False))
+        assert_frames_equal(o, g)
 
 
 def both(fn, gpu, ref):

@@ -8,6 +8,7 @@ properties (tests/test_gpu_properties.py).
 import msgpack
 import pytest
 
+from frames_check import assert_frames_equal
 from oracle import zbref
 from zeebe_amd import bpmn, workloads
 
@@ -59,6 +60,7 @@ def _compare(o, e):
                (b.position, b.key, b.record_type, b.value_type, b.intent), (a, b)
         assert a.value == b.value, (a.position, msgpack.unpackb(a.value, raw=False),
                                     msgpack.unpackb(b.value, raw=False))
+    assert_frames_equal(o, e)
     return ref
 
 

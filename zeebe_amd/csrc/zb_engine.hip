@@ -79,6 +79,7 @@ struct zb_engine {
   // device state
   zb_rec* log = nullptr;
   uint64_t* links = nullptr;
+  uint32_t* srcd = nullptr;     // per record: position - source position (0: none), for log frames
   RowMeta* rmeta = nullptr;
   RowKeys* rkeys = nullptr;
   uint8_t* arena = nullptr;
@@ -127,6 +128,12 @@ struct zb_engine {
   uint16_t staged_elem = NO_ELEM;  // process element of the staged CREATEs ...
   bool staged_uniform = true;      // ... when they all address the same one
   uint32_t staged_max_len = 1;     // longest staged CREATE payload (uniform batch merge bounds)
+
+  // request metadata: of staged records (staged index), then of injected ones (log position, sorted)
+  struct StagedReq { int64_t idx; uint64_t rid; int32_t sid; };
+  std::vector<StagedReq> staged_reqs;
+  std::vector<ReqMeta> reqs;
+  DevVec<ReqMeta> d_reqs;
 
   // submitted command ranges (serialization of CREATE commands / rejections)
   std::vector<CmdRange> ranges;
@@ -212,6 +219,7 @@ struct zb_engine {
   uint64_t *dr_len = nullptr, *dr_off = nullptr, *dr_tiles = nullptr, *dr_pay = nullptr;
   zb_record_header* dr_hdr = nullptr;
   uint8_t* dr_val = nullptr;
+  bool dr_frames = false;       // the drain batch holds log frames (no headers)
   void* dr_tmp = nullptr;
   uint64_t* dr_total = nullptr;   // [0] value bytes, [1] payload bytes (device)
   uint64_t* h_dr_total = nullptr; // pinned mirror
@@ -266,6 +274,7 @@ WaveParams wave_params(zb_engine* e) {
   WaveParams p;
   p.log = e->log;
   p.links = e->links;
+  p.srcd = e->srcd;
   p.rmeta = e->rmeta;
   p.rkeys = e->rkeys;
   p.arena = e->arena;
@@ -413,6 +422,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   HIPCHECK(e, hipMemcpyAsync(e->t_ctl, e->h_ctl_pinned, sizeof(TrajCtl), hipMemcpyHostToDevice, e->stream));
   TrajParams p{};
   p.log = e->log;
+  p.srcd = e->srcd;
   p.arena = e->arena;
   p.rmeta = e->rmeta;
   p.rkeys = e->rkeys;
@@ -572,6 +582,7 @@ MsgParams msg_params(zb_engine* e) {
   MsgParams p{};
   p.log = e->log;
   p.links = e->links;
+  p.srcd = e->srcd;
   p.arena = e->arena;
   p.subs = e->subs; p.sub_head = e->sub_head; p.sub_next = e->sub_next;
   p.sub_mask = e->head_mask; p.sub_count = e->sub_count; p.sub_cap = e->store_cap;
@@ -642,6 +653,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   e->wave_cap = (e->wave_cap + WAVE_TILE - 1) / WAVE_TILE * WAVE_TILE;
   if (hipMalloc(&e->log, L * sizeof(zb_rec)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->links, L * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->srcd, L * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->rmeta, e->cfg.row_capacity * sizeof(RowMeta)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->rkeys, e->cfg.row_capacity * sizeof(RowKeys)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->arena, e->cfg.arena_bytes) != hipSuccess) return cleanup(ZB_ENOMEM);
@@ -694,7 +706,7 @@ void zb_engine_destroy(zb_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (auto& x : e->ev)
     if (x) (void)hipEventDestroy(x);
-  void* ps[] = {e->log, e->links, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
+  void* ps[] = {e->log, e->links, e->srcd, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
                 e->merge_jobs, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
@@ -745,7 +757,9 @@ int zb_reset(zb_engine* e, int keep_staged) {
   HIPCHECK(e, hipStreamSynchronize(e->stream));
   e->ranges.clear();
   e->cmd_pool.clear();
+  e->reqs.clear();
   if (!keep_staged) {
+    e->staged_reqs.clear();
     e->staged.clear();
     e->staged_arena.clear();
     e->pending_ranges.clear();
@@ -874,6 +888,7 @@ bool is_doc(const uint8_t* p, uint64_t len) {  // DocumentValue: nil / empty -> 
 // the staged batch of the last zb_step was injected: start a new one
 void begin_staging(zb_engine* e) {
   if (e->staged_pending) return;
+  e->staged_reqs.clear();
   e->staged.clear();
   e->staged_arena.clear();
   e->pending_ranges.clear();
@@ -1322,6 +1337,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     InjectParams ip;
     ip.log = e->log;
     ip.links = e->links;
+    ip.srcd = e->srcd;
     ip.arena = e->arena;
     ip.staged = e->d_staged.p;
     ip.staged_arena = e->d_staged_arena.p;
@@ -1349,6 +1365,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
       HIPCHECK(e, hipStreamSynchronize(e->stream));  // the host vectors die at scope end
     }
     if (e->staged_has_cancel) e->term = true;
+    for (const auto& q : e->staged_reqs) e->reqs.push_back(ReqMeta{ip.log_base + q.idx, q.rid, q.sid, 0});
     for (auto& pr : e->pending_ranges) {
       CmdRange r{};
       r.pos_begin = ip.log_base + pr.first;
@@ -1457,7 +1474,32 @@ int zb_read_descriptors(zb_engine* e, int64_t start, int64_t count, zb_rec* out)
   return ZB_OK;
 }
 
+static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_config* fc, zb_serialize_stats* stats);
+
 int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats* stats) {
+  return serialize(e, start, count, nullptr, stats);
+}
+
+int zb_serialize_frames(zb_engine* e, int64_t start, int64_t count, const zb_frame_config* fc,
+                        zb_serialize_stats* stats) {
+  if (!fc) return ZB_EINVAL;
+  return serialize(e, start, count, fc, stats);
+}
+
+int zb_set_request_metadata(zb_engine* e, size_t n, const uint64_t* request_ids, const int32_t* request_stream_ids) {
+  if (!e || (n && (!request_ids || !request_stream_ids)) || n > e->staged.size()) return ZB_EINVAL;
+  const int64_t first = (int64_t)(e->staged.size() - n);
+  // (staged indices only grow between injections: the list stays sorted unless a range is set twice)
+  for (size_t i = 0; i < n; i++) {
+    const int64_t idx = first + (int64_t)i;
+    if (!e->staged_reqs.empty() && e->staged_reqs.back().idx >= idx)
+      return fail(e, ZB_EINVAL, "request metadata already set for these records");
+    e->staged_reqs.push_back(zb_engine::StagedReq{idx, request_ids[i], request_stream_ids[i]});
+  }
+  return ZB_OK;
+}
+
+static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_config* fc, zb_serialize_stats* stats) {
   if (!e || start < e->log_floor || count < 0 || start + count > e->host_hdr.end) return ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
   auto t0 = std::chrono::steady_clock::now();
@@ -1502,8 +1544,20 @@ int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats*
   }
   HIPCHECK(e, e->d_ranges.upload(e->ranges, e->stream));
   HIPCHECK(e, e->d_cmd_pool.upload(e->cmd_pool, e->stream));
+  if (fc && !e->reqs.empty()) HIPCHECK(e, e->d_reqs.upload(e->reqs, e->stream));
   SerParams sp{};
+  if (fc) {
+    sp.frames = 1;
+    sp.stream_id = fc->stream_id;
+    sp.raft_term = fc->raft_term;
+    sp.timestamp = fc->timestamp;
+    sp.log_begin = e->log_floor;
+    sp.log_end = e->host_hdr.end;
+    sp.reqs = e->reqs.empty() ? nullptr : e->d_reqs.p;
+    sp.nreqs = (int64_t)e->reqs.size();
+  }
   sp.log = e->log;
+  sp.srcd = e->srcd;
   sp.arena = e->arena;
   sp.elems = e->d_elems.p;
   sp.wfs = e->d_wfs.p;
@@ -1533,7 +1587,7 @@ int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats*
     sp.out = e->dr_val;
     sp.out_cap = e->dr_val_cap;
     HIPCHECK(e, hipMemsetAsync(e->dr_total, 0, 4 * sizeof(uint64_t), e->stream));
-    if (e->ser_mode == 1) {  // one pass: decoupled look-back over 256-record tiles
+    if (e->ser_mode == 1 && !fc) {  // one pass: decoupled look-back over 256-record tiles (values only)
       if ((++e->dr_epoch & 0x3ffff) == 0) {  // tile-state tags wrap: clear them once
         HIPCHECK(e, hipMemsetAsync(e->dr_tiles, 0, (e->dr_cap / 256 + 2) * sizeof(uint64_t), e->stream));
         ++e->dr_epoch;
@@ -1578,6 +1632,7 @@ int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats*
   HIPCHECK(e, hipEventElapsedTime(&ms_write, e->dr_ev[2], e->dr_ev[3]));
   e->dr_count = count;
   e->dr_bytes = e->h_dr_total[0];
+  e->dr_frames = fc != nullptr;
   st.records = (uint64_t)count;
   st.value_bytes = e->h_dr_total[0];
   st.payload_bytes = e->h_dr_total[1];
@@ -1592,6 +1647,7 @@ int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats*
 int zb_drain_copy(zb_engine* e, zb_record_header* headers, uint8_t* values, uint64_t value_off, size_t values_len) {
   if (!e || value_off > e->dr_bytes || values_len > e->dr_bytes - value_off || (values_len && !values)) return ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
+  if (headers && e->dr_frames) return fail(e, ZB_EINVAL, "the drain batch holds log frames: no headers");
   if (headers && e->dr_count)
     HIPCHECK(e, hipMemcpyAsync(headers, e->dr_hdr, e->dr_count * sizeof(zb_record_header), hipMemcpyDeviceToHost, e->stream));
   if (values_len) HIPCHECK(e, hipMemcpyAsync(values, e->dr_val + value_off, values_len, hipMemcpyDeviceToHost, e->stream));
@@ -1673,6 +1729,7 @@ int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, c
   HIPCHECK(e, hipMemcpyAsync(e->log + base, recs.data(), n * sizeof(zb_rec), hipMemcpyHostToDevice, e->stream));
   HIPCHECK(e, hipMemcpyAsync(e->arena + arena0, blobs.data(), blobs.size(), hipMemcpyHostToDevice, e->stream));
   HIPCHECK(e, hipMemsetAsync(e->links + base, 0xff, n * sizeof(uint64_t), e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->srcd + base, 0, n * sizeof(uint32_t), e->stream));  // client API commands
   MsgParams p = msg_params(e);
   p.n = (int64_t)n;
   p.base = base;

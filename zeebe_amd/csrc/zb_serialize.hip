@@ -279,6 +279,108 @@ __device__ __forceinline__ uint32_t value_size(const SerParams& P, int64_t pos, 
   return w.n;
 }
 
+// ------------------------------------------------------------------------------ log frames (§8f rank 1)
+// A record as LogStreamBatchWriterImpl.writeEventsToBuffer (:222-268) / LogStreamWriterImpl lay it into the
+// dispatcher buffer: DataFrameDescriptor header (DataFrameDescriptor.java:53-96: framed length, version 0,
+// batch flags, TYPE_MESSAGE, stream id), LogEntryDescriptor header (LogEntryDescriptor.java:28-121: version,
+// position, raft term, producer id, source event position, key, timestamp, metadata length), RecordMetadata
+// (RecordMetadata.java:96-128: SBE header {34, 200, 0, 1} + block + varData rejectionReason), the value, and
+// zero padding to FRAME_ALIGNMENT 8. The 104-byte prefix goes out as 13 aligned 8-byte words (frames start
+// 8-aligned in the image and in HBM).
+constexpr uint32_t FRAME_PREFIX = 12 + 48 + 8 + 34 + 2;
+
+// rejection reasons of the commands this path rejects (WorkflowInstanceStreamProcessor.java:346-347, :527-529,
+// :573, :478-479)
+__device__ __forceinline__ uint32_t reason_of(const zb_rec& d) {
+  if (kind_rt(d.kind) != ZB_RT_COMMAND_REJECTION) return 0;
+  const uint8_t vt = kind_vt(d.kind);
+  if (vt == ZB_VT_WORKFLOW_INSTANCE) return d.intent == WI_CREATE ? 1 : 2;
+  return vt == ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION ? 3 : 0;
+}
+__device__ __forceinline__ uint32_t reason_len(uint32_t r) { return r == 1 ? 24 : r == 2 ? 32 : r == 3 ? 30 : 0; }
+
+__device__ __forceinline__ const ReqMeta* find_req(const SerParams& P, int64_t pos) {
+  int64_t lo = 0, hi = P.nreqs - 1;
+  while (lo <= hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    const int64_t p = P.reqs[mid].pos;
+    if (p == pos) return &P.reqs[mid];
+    if (p < pos) lo = mid + 1; else hi = mid - 1;
+  }
+  return nullptr;
+}
+
+__device__ __forceinline__ int64_t source_of(const SerParams& P, int64_t pos) {
+  const uint32_t s = P.srcd[pos];
+  return s ? pos - (int64_t)s : -1;
+}
+
+// frame of record d at log position pos into dst (8-aligned), or only its size (dst == nullptr); returns the
+// aligned frame length
+__device__ inline uint32_t encode_frame(const SerParams& P, int64_t pos, const zb_rec& d, uint8_t* dst) {
+  const uint32_t rs = reason_of(d), rlen = reason_len(rs);
+  W w;
+  w.dst = dst ? dst + FRAME_PREFIX + rlen : nullptr;
+  w.n = 0;
+  encode_value(P, pos, d, w);
+  const uint32_t framed = FRAME_PREFIX + rlen + w.n, fsize = (framed + 7) & ~7u;
+  if (!dst) return fsize;
+  const uint8_t vt = kind_vt(d.kind), rt = kind_rt(d.kind);
+  const int64_t src = source_of(P, pos);
+  // ClaimedFragmentBatch.commit :130-147: BEGIN on the first and END on the last fragment of a batch with more
+  // than one; a batch is the records one processed record wrote (contiguous, same source)
+  uint32_t flags = 0;
+  if (src >= 0) {
+    const bool first = pos - 1 < P.log_begin || source_of(P, pos - 1) != src;
+    const bool last = pos + 1 >= P.log_end || source_of(P, pos + 1) != src;
+    if (!(first && last)) flags = first ? 0x80 : (last ? 0x40 : 0);
+  }
+  // TypedStreamProcessor producer ids (StreamProcessorIds.java:23-39): harness job events 10 (the job
+  // processor), message partition records 90, everything else the workflow instance processor 70; records
+  // other writers appended keep the writer's default -1
+  const int32_t producer = src < 0 ? -1 : (vt == ZB_VT_JOB && rt == ZB_RT_EVENT) ? 10
+                         : (vt == ZB_VT_MESSAGE || vt == ZB_VT_MESSAGE_SUBSCRIPTION) ? 90 : 70;
+  uint64_t rid = ~0ull;
+  uint32_t sid = 0x80000000u;
+  if (P.nreqs) {
+    int64_t q = -1;
+    if (src < 0) q = pos;
+    else if (vt == ZB_VT_WORKFLOW_INSTANCE && ((rt == ZB_RT_EVENT && d.intent == WI_CREATED) ||
+                                               (rt == ZB_RT_COMMAND_REJECTION && d.intent == WI_CREATE)))
+      q = src;
+    if (q >= 0) {
+      const ReqMeta* m = find_req(P, q);
+      if (m) { rid = m->request_id; sid = (uint32_t)m->request_stream_id; }
+    }
+  }
+  const uint64_t rej = rt == ZB_RT_COMMAND_REJECTION
+                           ? ((vt == ZB_VT_WORKFLOW_INSTANCE && d.intent == WI_CREATE) ? 0 : 1) : 255;
+  const uint64_t mlen = 8 + 34 + 2 + rlen;
+  uint64_t* h = (uint64_t*)dst;
+  h[0] = (uint64_t)framed | (uint64_t)flags << 40;                          // length, version 0, flags, type 0
+  h[1] = (uint64_t)(uint32_t)P.stream_id;                                    // stream id, entry version, reserved
+  h[2] = (uint64_t)pos;
+  h[3] = (uint64_t)(uint32_t)P.raft_term | (uint64_t)(uint32_t)producer << 32;
+  h[4] = (uint64_t)src;
+  h[5] = (uint64_t)d.key;
+  h[6] = (uint64_t)P.timestamp;
+  h[7] = mlen | 34ull << 32 | 200ull << 48;                                   // metadata length | blockLength, templateId
+  h[8] = 1ull << 16 | (uint64_t)rt << 32 | (uint64_t)(sid & 0xffffffu) << 40; // schemaId 0, version 1 | recordType
+  h[9] = (uint64_t)(sid >> 24) | rid << 8;                                    // requestStreamId | requestId
+  h[10] = (rid >> 56) | 0xffffffffffffff00ull;                                // | subscriptionId (null)
+  h[11] = 0xffull | 1ull << 8 | (uint64_t)vt << 24 | (uint64_t)d.intent << 32 | 0xffffffull << 40;  // protocolVersion 1
+  h[12] = 0xffffffffffull | rej << 40 | (uint64_t)rlen << 48;                  // incidentKey (null) | rejectionType
+  W r;
+  r.dst = dst + FRAME_PREFIX;
+  r.n = 0;
+  if (rs == 1) r.cstr("Workflow is not deployed");
+  else if (rs == 2) r.cstr("Workflow instance is not running");
+  else if (rs == 3) r.cstr("activity is not active anymore");
+  for (uint32_t k = framed; k < fsize; k++) dst[k] = 0;
+  return fsize;
+}
+
+template <bool FRAMES>
 __global__ void __launch_bounds__(256) k_ser_size(SerParams P0) {
   __shared__ __attribute__((aligned(16))) uint8_t s_model[SER_MODEL_LDS];
   const SerParams P = model_in_lds(P0, s_model, 256);
@@ -287,7 +389,7 @@ __global__ void __launch_bounds__(256) k_ser_size(SerParams P0) {
   if (i >= P.count) return;
   const int64_t pos = P.start + i;
   const zb_rec d = P.log[pos];
-  const uint32_t n = value_size(P, pos, d);
+  const uint32_t n = FRAMES ? encode_frame(P, pos, d, nullptr) : value_size(P, pos, d);
   if (P.lengths64) P.lengths64[i] = n;
   else P.lengths[i] = n;
 }
@@ -338,6 +440,7 @@ __device__ __forceinline__ void stream_image(const uint8_t* img, uint8_t* out, u
 // encoded and streamed one after another (large values, e.g. C2's job records: 64 KB per tile). The phase loop
 // lets the compiler spend 255 VGPRs unless told the LDS-bound occupancy (3 workgroups per CU): 168, no spills.
 constexpr int SER_WINDOWS = 16;
+template <bool FRAMES>
 __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 3))) k_ser_write(SerParams P0) {
   __shared__ __attribute__((aligned(16))) uint8_t img[SER_IMG + 16];
   __shared__ __attribute__((aligned(16))) uint8_t s_model[SER_MODEL_LDS];
@@ -389,7 +492,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
   const int64_t pos = P.start + i;
   if (live) {
     if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay = *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
-    P.headers[i] = record_header(d, pos, len, off);
+    if (!FRAMES) P.headers[i] = record_header(d, pos, len, off);
   }
   if (P.totals) {
     unsigned long long y = pay;
@@ -423,10 +526,14 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
       dst = img + sh + (off - wlo);
     }
     if (go) {
-      W w;
-      w.dst = dst;
-      w.n = 0;
-      encode_value(P, pos, d, w);
+      if (FRAMES) {
+        (void)encode_frame(P, pos, d, dst);
+      } else {
+        W w;
+        w.dst = dst;
+        w.n = 0;
+        encode_value(P, pos, d, w);
+      }
     }
     if (staged || nwin) {
       __syncthreads();
@@ -587,12 +694,14 @@ void launch_ser_fused(const SerParams& p, hipStream_t s) {
 void launch_ser_size(const SerParams& p, hipStream_t s) {
   if (p.count <= 0) return;
   const int64_t work = p.count + (p.lengths64 ? 1 : 0);
-  hipLaunchKernelGGL(k_ser_size, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, p);
+  if (p.frames) hipLaunchKernelGGL(k_ser_size<true>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(k_ser_size<false>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, p);
 }
 void launch_ser_write(const SerParams& p, hipStream_t s) {
   if (p.count <= 0) return;
   const int64_t tiles = (p.count + SER_WG - 1) / SER_WG;
-  hipLaunchKernelGGL(k_ser_write, dim3((unsigned)tiles), dim3(SER_WG), 0, s, p);
+  if (p.frames) hipLaunchKernelGGL(k_ser_write<true>, dim3((unsigned)tiles), dim3(SER_WG), 0, s, p);
+  else hipLaunchKernelGGL(k_ser_write<false>, dim3((unsigned)tiles), dim3(SER_WG), 0, s, p);
   if (p.totals) hipLaunchKernelGGL(k_ser_sum, dim3(1), dim3(1024), 0, s, p, tiles);
 }
 
@@ -607,6 +716,7 @@ __global__ void k_inject(InjectParams P) {
     if (d.key == KEY_IS_POSITION) d.key = P.log_base + i;
     P.log[P.log_base + i] = d;
     P.links[P.log_base + i] = ~0ull;  // no rows yet
+    P.srcd[P.log_base + i] = 0;       // written by another writer (client API, job processor, ...)
   }
   const uint64_t nw = P.staged_bytes / 8;
   const uint64_t* src = (const uint64_t*)P.staged_arena;

@@ -737,8 +737,12 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
     }
     if (I.nc > 0) wl = w + 1;
     // ---- process this generation (log order inside the instance)
+    int cut = 0;  // follow-ups [0, cut) come from the generation's first record, the rest from its second
 #pragma unroll 1
-    for (int k = 0; k < I.nc; k++) t_record<EMIT, COND, UNI>(P, I, I.cur.get(k), fpos + k, slot);
+    for (int k = 0; k < I.nc; k++) {
+      t_record<EMIT, COND, UNI>(P, I, I.cur.get(k), fpos + k, slot);
+      if (k == 0) cut = I.nn;
+    }
     // ---- place the follow-ups
     uint64_t a = (uint64_t)I.nn | ((uint64_t)I.nwf << 16) | ((uint64_t)I.njob << 32);
     uint64_t bytes = 0;
@@ -852,7 +856,8 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
           t.inst = I.inst_key;
           t.payload = s.payload;
           t.elem = s.elem; t.intent = s.intent; t.kind = s.kind;
-          t.pad[0] = t.pad[1] = t.pad[2] = 0;
+          t.pad[0] = k < cut ? 0 : 1;  // source: the instance's record of the previous generation
+          t.pad[1] = t.pad[2] = 0;
           P.tmpl[((uint64_t)I.crow + w) * TF + k] = t;
           if (kind_vt(s.kind) == ZB_VT_WORKFLOW_INSTANCE && kind_rt(s.kind) == ZB_RT_EVENT) I.transitions++;
         }
@@ -866,8 +871,10 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
           d.inst_key = wf_key(P, I.inst_key);
           d.payload = s.payload;
           d.elem = s.elem; d.intent = s.intent; d.kind = s.kind;
-          if (pos0 + k < (int64_t)P.log_cap) P.log[pos0 + k] = d;
-          else I.err |= DE_LOG_FULL;
+          if (pos0 + k < (int64_t)P.log_cap) {
+            P.log[pos0 + k] = d;
+            P.srcd[pos0 + k] = (uint32_t)(pos0 + k - (fpos + (k < cut ? 0 : 1)));
+          } else I.err |= DE_LOG_FULL;
           if (kind_vt(s.kind) == ZB_VT_WORKFLOW_INSTANCE && kind_rt(s.kind) == ZB_RT_EVENT) I.transitions++;
         }
       }
@@ -1530,6 +1537,7 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
   uint64_t merge_bytes = 0;
   uint32_t pc_sym = PAY_CREATE, pc_ref = create_ref;  // last resolved payload symbol
   uint32_t* reg = s_merge + threadIdx.x * TL::STRIDE;
+  int64_t prev0 = P.log_base + inst;  // the instance's first record of the previous generation (the CREATE)
 
 #pragma unroll 1
   for (int w = 0; w < W; w++) {
@@ -1589,10 +1597,13 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
       d.payload = pay;
       d.elem = t.elem; d.intent = t.intent; d.kind = t.kind;
       if (active) {
-        if (pos0 + k < (int64_t)P.log_cap) P.log[pos0 + k] = d;
-        else err |= DE_LOG_FULL;
+        if (pos0 + k < (int64_t)P.log_cap) {
+          P.log[pos0 + k] = d;
+          P.srcd[pos0 + k] = (uint32_t)(pos0 + k - (prev0 + t.pad[0]));
+        } else err |= DE_LOG_FULL;
       }
     }
+    prev0 = pos0;
   }
   // statistics: everything but the merge bytes is a per-class constant (k_traj_commit)
   uint64_t s0 = active ? merge_bytes : 0, s1 = 0, t0, t1;

@@ -50,6 +50,7 @@ struct TState {
   uint32_t err, err_site;
   // a parallel fork's expanded outputs (k_emit writes them after the staged slots)
   uint32_t nexp, exp_ord;
+  uint32_t src_off;  // the record being processed, relative to the thread's first (the slots' source)
   // stats
   uint32_t transitions, completed, created, merges, canceled;
   uint32_t merge_bytes, cond_bytes;
@@ -75,6 +76,7 @@ __device__ __forceinline__ Slot& add_slot(TState& t) {
   if (t.ns >= MAX_SLOTS) { fail_at(t, DE_PROCESSING, 1); return t.s[MAX_SLOTS - 1]; }
   Slot& s = t.s[t.ns++];
   s.flags = 0; s.ord = 0; s.rord = 0;
+  s.pad = (uint8_t)t.src_off;
   return s;
 }
 
@@ -666,7 +668,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
     t.transitions = t.completed = t.created = t.merges = t.canceled = 0;
     t.merge_bytes = t.cond_bytes = 0;
     t.sub = false;
-    t.nexp = 0; t.exp_ord = 0;
+    t.nexp = 0; t.exp_ord = 0; t.src_off = 0;
     uint32_t nconds = 0;
     const zb_rec rec = P.log[r];
     if (!grouped(rec)) {
@@ -678,6 +680,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
         const zb_rec rec2 = P.log[q];
         if (!grouped(rec2)) break;
         const uint64_t lk2 = P.links[q];
+        t.src_off = (uint32_t)(q - r);
         process_record(P, rec2, q, (uint32_t)lk2, (uint32_t)(lk2 >> 32), t);
       }
     }
@@ -975,6 +978,7 @@ __device__ __forceinline__ void emit_item(const WaveParams& P, const Chunk& c, i
     else {
       P.log[out_rec] = s.d;
       P.links[out_rec] = (uint64_t)s.rself | ((uint64_t)s.rscope << 32);
+      P.srcd[out_rec] = (uint32_t)(out_rec - (uint64_t)(c.begin + i + s.pad));
       if (s.flags & SF_COND_JOB) {
         if (cond_j < P.job_cap) P.cond_jobs[par + cond_j] = out_rec;
         cond_j++;
@@ -998,6 +1002,7 @@ __device__ __forceinline__ void emit_item(const WaveParams& P, const Chunk& c, i
       else {
         P.log[out_rec] = d;
         P.links[out_rec] = (uint64_t)NO_ROW | ((uint64_t)rscope << 32);
+        P.srcd[out_rec] = (uint32_t)(out_rec - (uint64_t)r);
       }
       out_rec++;
     }
@@ -1129,7 +1134,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
     t.transitions = t.completed = t.created = t.merges = t.canceled = 0;
     t.merge_bytes = t.cond_bytes = 0;
     t.sub = false;
-    t.nexp = 0; t.exp_ord = 0;
+    t.nexp = 0; t.exp_ord = 0; t.src_off = 0;
     uint32_t nconds = 0;
     if (r < c.end) {
       const zb_rec rec = P.log[r];
@@ -1140,6 +1145,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
           const zb_rec rec2 = P.log[q];
           if (!grouped(rec2)) break;
           const uint64_t lk2 = P.links[q];
+          t.src_off = (uint32_t)(q - r);
           process_record(P, rec2, q, (uint32_t)lk2, (uint32_t)(lk2 >> 32), t);
         }
       }

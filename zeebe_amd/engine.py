@@ -68,6 +68,10 @@ class zb_step_stats(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class zb_frame_config(ctypes.Structure):
+    _fields_ = [("stream_id", ctypes.c_int32), ("raft_term", ctypes.c_int32), ("timestamp", ctypes.c_int64)]
+
+
 class zb_serialize_stats(ctypes.Structure):
     _fields_ = [("records", ctypes.c_uint64), ("value_bytes", ctypes.c_uint64), ("payload_bytes", ctypes.c_uint64),
                 ("size_kernel_ms", ctypes.c_double), ("scan_ms", ctypes.c_double),
@@ -132,6 +136,9 @@ def lib():
         L.zb_validate_deployment.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
         L.zb_serialize.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(zb_serialize_stats)]
         L.zb_drain_copy.argtypes = [vp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_size_t]
+        L.zb_serialize_frames.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(zb_frame_config),
+                                          ctypes.POINTER(zb_serialize_stats)]
+        L.zb_set_request_metadata.argtypes = [vp, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
         L.zb_pinned_alloc.restype = ctypes.c_void_p
         L.zb_pinned_alloc.argtypes = [ctypes.c_size_t]
         L.zb_pinned_free.argtypes = [ctypes.c_void_p]
@@ -147,7 +154,8 @@ EXPORTED_SYMBOLS = ["zb_engine_create", "zb_engine_destroy", "zb_last_error", "z
                     "zb_read_descriptors", "zb_drain", "zb_counters", "zb_submit_publishes", "zb_inbox_submit",
                     "zb_outbox_count", "zb_outbox_take", "zb_comm_unique_id", "zb_comm_init", "zb_comm_pending",
                     "zb_comm_exchange", "zb_submit", "zb_read_instances", "zb_snapshot", "zb_restore",
-                    "zb_validate_deployment", "zb_serialize", "zb_drain_copy", "zb_pinned_alloc", "zb_pinned_free"]
+                    "zb_validate_deployment", "zb_serialize", "zb_drain_copy", "zb_pinned_alloc", "zb_pinned_free",
+                    "zb_serialize_frames", "zb_set_request_metadata"]
 
 
 def validate_deployment(xml):
@@ -290,6 +298,33 @@ class Engine:
         st = zb_serialize_stats()
         self._check(self._L.zb_serialize(self._h, start, count, ctypes.byref(st)))
         return st.as_dict()
+
+    def serialize_frames(self, start: int, count: int, stream_id: int = 0, raft_term: int = 0,
+                         timestamp: int = 0) -> dict:
+        """zb_serialize_frames: records [start, start+count) -> log frames in the device-resident drain buffer."""
+        fc = zb_frame_config(stream_id, raft_term, timestamp)
+        st = zb_serialize_stats()
+        self._check(self._L.zb_serialize_frames(self._h, start, count, ctypes.byref(fc), ctypes.byref(st)))
+        return st.as_dict()
+
+    def frames(self, start: int = 0, count: Optional[int] = None, stream_id: int = 0, raft_term: int = 0,
+               timestamp: int = 0) -> bytes:
+        """The log frames of records [start, start+count), copied to host memory."""
+        if count is None:
+            count = self.log_size() - start
+        st = self.serialize_frames(start, count, stream_id, raft_term, timestamp)
+        n = st["value_bytes"]
+        buf = ctypes.create_string_buffer(max(n, 1))
+        if n:
+            self._check(self._L.zb_drain_copy(self._h, None, buf, 0, n))
+        return buf.raw[:n]
+
+    def set_request_metadata(self, request_ids, request_stream_ids):
+        """Request metadata of the last len(request_ids) staged records (zb_set_request_metadata)."""
+        n = len(request_ids)
+        ids = (ctypes.c_uint64 * max(n, 1))(*request_ids)
+        sids = (ctypes.c_int32 * max(n, 1))(*request_stream_ids)
+        self._check(self._L.zb_set_request_metadata(self._h, n, ids, sids))
 
     def drain_copy(self, dst_ptr: int, value_off: int, nbytes: int, headers_ptr=None):
         """zb_drain_copy into caller memory (an address, e.g. from pinned_alloc)."""
