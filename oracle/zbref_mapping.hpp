@@ -210,6 +210,9 @@ struct TreeWriter {
       uint32_t pos = (uint32_t)(m >> 32), len = (uint32_t)m;
       NodeType nt = t->node_type.at(id);
       const bytes& buf = (nt == NodeType::EXTRACTED_LEAF) ? *t->extract : t->underlying;
+      // the buffer follows the node type (an extracted leaf whose node addArrayNode retyped is read from the
+      // indexed document); UnsafeBuffer bounds checks throw outside it
+      if ((size_t)pos + len > buf.size()) throw ZbError("IndexOutOfBoundsException in tree writer");
       w.raw(buf.data() + pos, len);
     } else {
       bool arr = t->is_array(id);

@@ -2,6 +2,7 @@
 // that their byte-level logic can be fuzzed against the oracle on CPU (tests/test_devlib_host.py).
 // Nothing here is part of the product; the product runs these routines only inside the HIP kernels.
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #define __device__
 #define __host__
@@ -12,6 +13,9 @@ static inline float __uint_as_float(uint32_t u) { float f; std::memcpy(&f, &u, 4
 static inline double __longlong_as_double(long long u) { double d; std::memcpy(&d, &u, 8); return d; }
 #define HIP_INCLUDE_HIP_HIP_RUNTIME_H
 #include "../../zeebe_amd/csrc/zb_devlib.hpp"
+#include "../../zeebe_amd/csrc/zb_model.cpp"  // the product's deploy-time compilers (json-path, mapping targets)
+
+#include <string>
 
 using namespace zbg;
 
@@ -34,6 +38,42 @@ long devlib_merge_flat(const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint
   uint32_t n = 0;
   if (!merge_flat(src, ns, tgt, nt, out, cap, n)) return -5;
   return (long)n;
+}
+// explicit io-mappings: map_documents over caller-built tables (tgt == nullptr: extract). Returns the
+// output length, or -(10 + status) for a MAP_* status other than MAP_OK (fail_query in *fq).
+long devlib_map(const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint32_t nt, const DevMapping* maps,
+                uint32_t nmaps, const DevSeg* segs, const DevQuery* queries, const DevFilter* filters,
+                const uint8_t* pool, uint8_t* out, uint32_t cap, uint32_t* fq) {
+  static MNode ws[MAP_NODES];
+  uint16_t q = 0xffff;
+  Out o{nullptr, 0};
+  int st = map_documents(src, ns, tgt, nt, maps, nmaps, segs, queries, filters, pool, ws, o, q);
+  *fq = q;
+  if (st != MAP_OK) return -(10 + st);
+  if (o.n > cap) return -3;
+  Out w{out, 0};
+  st = map_documents(src, ns, tgt, nt, maps, nmaps, segs, queries, filters, pool, ws, w, q);
+  if (st != MAP_OK || w.n != o.n) return -4;
+  return (long)w.n;
+}
+// the same through the product's deploy-time compilers: spec = "source\ttarget\n"...; -20 = compile error (err)
+long devlib_map_text(const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint32_t nt, const char* spec, uint8_t* out,
+                     uint32_t cap, uint32_t* fq, char* err, uint32_t errcap) {
+  ModelTables t;
+  std::string sp(spec), e;
+  size_t p = 0;
+  while (p < sp.size()) {
+    size_t tab = sp.find('\t', p), nl = sp.find('\n', p);
+    if (tab == std::string::npos || nl == std::string::npos || tab > nl) return -21;
+    if (compile_mapping(t, sp.substr(p, tab - p), sp.substr(tab + 1, nl - tab - 1), e) < 0) {
+      snprintf(err, errcap, "%s", e.c_str());
+      return -20;
+    }
+    p = nl + 1;
+  }
+  if (t.pool.empty()) t.pool.push_back(0);
+  return devlib_map(src, ns, tgt, nt, t.maps.data(), (uint32_t)t.maps.size(), t.segs.data(), t.queries.data(),
+                    t.filters.data(), t.pool.data(), out, cap, fq);
 }
 // returns count of results; first result pos/len in out[0..1]; -1 unsupported
 long devlib_query(const uint8_t* doc, uint32_t n, const uint8_t* f_ids, const int32_t* f_idx,

@@ -6,6 +6,7 @@ same source runs inside the HIP kernels, so logic bugs show up here without a GP
 import ctypes
 import os
 import random
+import struct
 import subprocess
 
 import msgpack
@@ -21,8 +22,9 @@ NATIVE = os.path.join(HERE, "native")
 def devlib():
     src = os.path.join(NATIVE, "devlib_host.cpp")
     so = os.path.join(NATIVE, "libdevlib_host.so")
-    hdr = os.path.join(HERE, "..", "zeebe_amd", "csrc", "zb_devlib.hpp")
-    if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(src), os.path.getmtime(hdr)):
+    hdrs = [os.path.join(HERE, "..", "zeebe_amd", "csrc", f) for f in ("zb_devlib.hpp", "zb_model.cpp", "zb_model.hpp",
+                                                                        "zb_device.hpp")]
+    if not os.path.exists(so) or os.path.getmtime(so) < max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in hdrs]):
         subprocess.check_call(["g++", "-O1", "-std=c++17", "-fPIC", "-shared", "-I/opt/rocm/include", "-o", so, src])
     L = ctypes.CDLL(so)
     L.devlib_merge.restype = ctypes.c_long
@@ -156,3 +158,88 @@ def test_flat_merge_matches_general(devlib):
         assert ng >= 0, (src, tgt, ng)
         assert out_f.raw[:nf] == out_g.raw[:ng], (src, tgt)
     assert accepted > 3000
+
+
+# ---- explicit io-mappings (map_documents) vs the oracle's MappingProcessor restatement, with the tables built by
+# the product's deploy-time compilers (zb_model.cpp compile_mapping)
+def dev_map(L, src, tgt, mappings):
+    spec = "".join("%s\t%s\n" % m for m in mappings).encode()
+    out = ctypes.create_string_buffer(1 << 16)
+    err = ctypes.create_string_buffer(512)
+    fq = ctypes.c_uint32()
+    n = L.devlib_map_text(src, len(src), tgt, len(tgt) if tgt is not None else 0, spec, out, 1 << 16,
+                          ctypes.byref(fq), err, 512)
+    return n, out.raw[:max(n, 0)], fq.value
+
+
+def _oracle_map(src, tgt, mappings):
+    try:
+        return 0, zbref.map_documents(src, mappings, tgt)
+    except zbref.MappingError as e:
+        return 1, str(e)
+    except RuntimeError as e:
+        return 2, str(e)
+
+
+def test_mapping_fuzz_vs_oracle(devlib):
+    devlib.devlib_map_text.restype = ctypes.c_long
+    r = random.Random(23)
+    sources = ["$", "$.a", "$.b", "$.key", "$.a.b", "$.a.c", "$.a[1]", "$.b[0]", "$.0", "$.c"]
+    targets = ["$", "$.a", "$.b", "$.n", "$.a.b", "$.a.x", "$.n.m", "$.a[0]", "$.n[1]", "$.a.0", "$.b.c.d",
+               "$.x[0].y"]
+    checked = {0: 0, 1: 0, 2: 0}
+    unsupported = 0
+    for it in range(4000):
+        s = rand_doc(r)
+        t = rand_doc(r) if it % 4 else None
+        present = ["$." + k for k in s if k.isalnum() and not k.isdigit()] + ["$"]
+        ms = [(r.choice(present) if r.random() < 0.7 else r.choice(sources), r.choice(targets))
+              for _ in range(r.randint(1, 3))]
+        sb = msgpack.packb(s)
+        tb = msgpack.packb(t) if t is not None else None
+        n, got, fq = dev_map(devlib, sb, tb, ms)
+        kind, ref = _oracle_map(sb, tb, ms)
+        if n == -14:
+            unsupported += 1
+            continue
+        ctx = (s, t, ms, n, kind, ref)
+        if kind == 0:
+            assert n >= 0 and got == ref, ctx
+        elif kind == 1:
+            if ref.startswith("No data found for query "):
+                assert n == -11 and ref == "No data found for query %s." % ms[fq][0], ctx
+            else:
+                assert n == -12 and ref.startswith("Processing failed, since mapping"), ctx
+        else:
+            assert n == -13, ctx
+        checked[kind] += 1
+    assert unsupported < 40, unsupported
+    assert checked[0] > 1000 and checked[1] > 200 and checked[2] > 0, checked
+
+
+def test_mapping_reference_vectors(devlib, vectors):
+    """Every MappingExtractParameterizedTest / MappingMergeParameterizedTest row (transcribed into
+    reference_vectors.json) through the kernels' engine: the same document or the same failure as the oracle,
+    which test_oracle_iomapping.py pins on the rows' expected JSON."""
+    devlib.devlib_map_text.restype = ctypes.c_long
+    ran = unsupported = 0
+    for kind in ("mapping_extracts", "mapping_merges"):
+        for row in vectors[kind]:
+            ms = [tuple(m) for m in row["mappings"]]
+            if not ms:  # no mappings: the kernels run the default merge (test_merge_* above)
+                continue
+            src = bytes.fromhex(row["source"])
+            tgt = bytes.fromhex(row["target"]) if "target" in row else None
+            n, got, _ = dev_map(devlib, src, tgt, ms)
+            if n == -20:  # the deploy-time compiler rejects the path (the reference's would too)
+                continue
+            if n == -14:
+                unsupported += 1
+                continue
+            okind, ref = _oracle_map(src, tgt, ms)
+            if okind == 0:
+                assert n >= 0 and got == ref, (row, n)
+            else:
+                assert n in (-11, -12, -13), (row, n, ref)
+            ran += 1
+    assert ran >= 90 and unsupported <= 6, (ran, unsupported)

@@ -1,4 +1,5 @@
-// zb_aux.hip — the two payload kernels that run between waves, off the state-machine kernel:
+// zb_aux.hip — the payload kernels that run around a wave, off the state-machine kernel:
+//   k_map:   explicit io-mappings of the records a wave is about to process (below)
 //   k_merge: default output merges reserved by k_wave (OutputMappingHandler :42-85 ->
 //            MappingProcessor.merge, json-path/.../mapping/MappingProcessor.java:143-170)
 //   k_cond:  exclusive-gateway condition evaluation for GATEWAY_ACTIVATED records emitted by the
@@ -93,6 +94,82 @@ __global__ void __launch_bounds__(256) k_cond(WaveParams P) {
   }
   bytes = wg_sum256(bytes, s4);
   if (threadIdx.x == 0 && bytes) atomicAdd((unsigned long long*)&P.stats[5], bytes);
+}
+
+// k_map: explicit io-mappings of the chunk's records, before the wave processes them (InputMappingHandler
+// :39-70 -> MappingProcessor.extract; OutputMappingHandler :42-85 -> MappingProcessor.merge with the element's
+// output mappings, or with none into {} for outputBehavior overwrite). One thread per record of the chunk (plus
+// the batch tails that reach past its end); a READY / COMPLETING record of a mapped element that will pass its
+// guard gets its result document in a fresh arena blob (size pass, one 8-byte atomic on the wave header's
+// arena pointer, write pass) or the MappingException that becomes its IO_MAPPING_ERROR incident; k_process
+// reads the outcome from mapres. The guard and the flow scope's payload are read before the wave changes
+// anything, which is what the record's own turn in log order sees: only the record's own thread changes its
+// row, and a flow scope's value changes only with records of the scope itself.
+__global__ void __launch_bounds__(256) k_map(WaveParams P) {
+  WaveHdr* hin = P.hdr + (P.wave & 1);
+  const int64_t b = hin->begin, g = hin->gen_end;
+  const int64_t cend = (g - b > (int64_t)P.wave_cap) ? b + (int64_t)P.wave_cap : g;
+  const int64_t lim = cend + 3 < g ? cend + 3 : g;  // a batch's tail may lie past the chunk end
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  MNode* ws = P.map_ws + tid * MAP_NODES;
+  uint32_t err = 0;
+  for (int64_t r = b + (int64_t)tid; r < lim; r += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t res = 0;
+    const zb_rec rec = P.log[r];
+    if (kind_vt(rec.kind) == ZB_VT_WORKFLOW_INSTANCE && kind_rt(rec.kind) == ZB_RT_EVENT && rec.elem != NO_ELEM) {
+      const DevElem& el = P.elems[rec.elem];
+      const uint8_t ob = (el.flags >> OB_SHIFT) & 3;
+      const bool in = rec.intent == WI_ELEMENT_READY && el.n_in && el.step[WI_ELEMENT_READY] == ST_APPLY_INPUT_MAPPING;
+      const bool out = rec.intent == WI_ELEMENT_COMPLETING && el.step[WI_ELEMENT_COMPLETING] == ST_APPLY_OUTPUT_MAPPING &&
+                       (el.n_out_map || ob == OB_OVERWRITE);
+      const uint64_t lk = P.links[r];
+      const uint32_t rself = (uint32_t)lk, rscope = (uint32_t)(lk >> 32);
+      if ((in || out) && rself != NO_ROW && P.rmeta[rself].state == rec.intent && (in || rscope != NO_ROW)) {
+        const uint8_t* sp = P.arena + (uint64_t)rec.payload * 8;
+        const uint32_t ns = *(const uint32_t*)sp;
+        const uint8_t* tp = nullptr;
+        uint32_t nt = 0;
+        if (out) {
+          tp = P.arena + (ob == OB_OVERWRITE ? 0 : (uint64_t)P.rmeta[rscope].payload * 8);  // ref 0: {}
+          nt = *(const uint32_t*)tp;
+          tp += 4;
+        }
+        const uint16_t first = in ? el.map_in : el.map_out;
+        const uint32_t nm = in ? el.n_in : el.n_out_map;
+        uint16_t fq = 0;
+        int st;
+        Out o{nullptr, 0};
+        bool unsup = false;
+        if (nm) st = map_documents(sp + 4, ns, tp, nt, P.maps + first, nm, P.segs, P.queries, P.filters, P.pool, ws, o, fq);
+        else st = !merge_docs(sp + 4, ns, tp, nt, o, unsup) ? MAP_FAIL : (unsup ? MAP_UNSUPPORTED : MAP_OK);
+        if (st == MAP_OK) {
+          const uint64_t bytes = (4 + o.n + 7) & ~7ull;
+          const uint64_t at = atomicAdd((unsigned long long*)&hin->arena_next, (unsigned long long)bytes);
+          if (at + bytes > P.arena_cap) {
+            err |= DE_ARENA_FULL;
+          } else {
+            Out w{P.arena + at + 4, 0};
+            if (nm) st = map_documents(sp + 4, ns, tp, nt, P.maps + first, nm, P.segs, P.queries, P.filters, P.pool, ws, w, fq);
+            else (void)merge_docs(sp + 4, ns, tp, nt, w, unsup);
+            *(uint32_t*)(P.arena + at) = w.n;
+            res = MR_OK | (at >> 3);
+          }
+        } else if (st == MAP_ERR_NO_DATA) {
+          res = MR_INCIDENT | ((uint64_t)EC_MAPPING_NO_DATA << 48) | ((uint64_t)fq << 32);
+        } else if (st == MAP_ERR_NOT_MAP) {
+          res = MR_INCIDENT | ((uint64_t)EC_MAPPING_NOT_MAP << 48);
+        } else {
+          res = st == MAP_FAIL ? MR_FAIL : MR_UNSUPPORTED;
+        }
+      }
+    }
+    P.mapres[r - b] = res;
+  }
+  if (err) atomicOr(P.err, err);
+}
+
+void launch_map(const WaveParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_map, dim3(MAP_GRID), dim3(256), 0, s, p);
 }
 
 void launch_merge(const WaveParams& p, hipStream_t s) {

@@ -82,8 +82,9 @@ struct DevElem {              // 72 bytes
   uint16_t out_begin;         // parallel gateway: its outgoing flows in executable order (flows[])
   uint8_t m_in;               // parallel gateway: incoming sequence flows (join arity)
   uint8_t join_slot;          // parallel join: its counter slot in the scope's RowAux
-  uint16_t pad1;
-  uint32_t pad2;
+  uint16_t map_in;            // first input mapping (DevMapping) of the element's zeebe:ioMapping
+  uint16_t map_out;           // first output mapping
+  uint8_t n_in, n_out_map;    // input / output mappings
 };
 static_assert(sizeof(DevElem) == 80, "DevElem layout is 80 bytes");
 
@@ -116,6 +117,18 @@ struct DevQuery {             // 16 bytes
   uint32_t pad;
 };
 
+// ---- explicit io-mappings (Mapping.java: source query -> target path) ----
+struct DevMapping {           // 8 bytes
+  uint16_t query;             // DevQuery of the source expression
+  uint16_t nseg;              // target path segments: the LITERAL / ROOT_OBJECT tokens of JsonPathTokenizer
+  uint32_t seg;               // first segment in segs[]
+};
+struct DevSeg {               // 8 bytes: segment text in the pool
+  uint32_t off, len;
+};
+// DevElem.flags: bit 0 has io mapping; bits 1-2 output behaviour (ZeebeOutputBehavior; 0 = unset = merge)
+constexpr uint8_t EF_IO = 1, OB_SHIFT = 1, OB_UNSET = 0, OB_NONE = 1, OB_MERGE = 2, OB_OVERWRITE = 3;
+
 // ---- json-el constants / program ----
 enum TokType : uint8_t { TT_INTEGER = 0, TT_FLOAT = 1, TT_BOOLEAN = 2, TT_NIL = 3, TT_MAP = 4, TT_ARRAY = 5,
                          TT_BINARY = 6, TT_STRING = 7, TT_EXTENSION = 8 };
@@ -141,7 +154,8 @@ enum ErrCode : uint8_t {
   EC_DIFF_TYPES = 4,     // "Cannot compare values of different types: %s and %s"
   EC_CMP_TYPE = 5,       // "Cannot compare value of type: %s"
   EC_NOT_NUMBER = 6,     // "Cannot compare values. Expected number but found: %s"
-  EC_MAPPING_NOT_MAP = 7 // "Processing failed, since mapping will result in a non map object (json object)."
+  EC_MAPPING_NOT_MAP = 7, // "Processing failed, since mapping will result in a non map object (json object)."
+  EC_MAPPING_NO_DATA = 8  // "No data found for query %s." (MsgPackDocumentExtractor.executeLeafMapping)
 };
 
 // device error flags (sticky, host checks after each batch of waves)

@@ -749,4 +749,248 @@ __device__ __forceinline__ bool merge_flat(const uint8_t* src, uint32_t ns, cons
   return true;
 }
 
+// ------------------------------------------------------------------------------ explicit io-mappings
+// MappingProcessor.extract / merge with mappings (json-path/.../mapping/MappingProcessor.java:143-190): the
+// target document is indexed into a MsgPackTree (MsgPackDocumentIndexer.java:136-283), every mapping puts its
+// source query's single result at its target path (MsgPackDocumentExtractor.java:121-230: createParentRelation,
+// executeLeafMapping), and the tree is written out (MsgPackDocumentTreeWriter.java:53-104). The tree lives in a
+// caller-provided workspace as nodes identified by (parent, name) -- what the reference's string node ids
+// "$[a][b]" identify -- with names taken from the target document's keys, the target path literals (pool) or
+// array indices. MsgPackTree keeps node types and leaves apart from the child sets, so a node can carry a leaf
+// and a type at once (addArrayNode keeps a leaf, addMapNode drops it); the writer looks at the leaf first.
+// Names holding '[' or ']' (where the reference's string ids collide) are flagged unsupported.
+constexpr uint32_t MAP_NODES = 256;
+constexpr int MAP_DEPTH = 32;
+constexpr uint16_t MN_NONE = 0xffff;
+enum : uint8_t { MN_UNTYPED = 0, MN_LEAF_T = 1, MN_LEAF_S = 2, MN_MAP = 3, MN_ARRAY = 4 };
+enum : uint8_t { NS_TDOC = 0, NS_POOL = 1, NS_INDEX = 2 };
+// outcome of map_documents
+enum : int { MAP_OK = 0, MAP_ERR_NO_DATA = 1, MAP_ERR_NOT_MAP = 2, MAP_FAIL = 3, MAP_UNSUPPORTED = 4 };
+
+struct MNode {
+  uint32_t name;        // name bytes offset (NS_TDOC: target document, NS_POOL: pool) or array index (NS_INDEX)
+  uint16_t nlen;
+  uint8_t nsrc, type;
+  uint32_t lpos, llen;  // leaf value in the target (MN_LEAF_T) or source document; llen 0 = no leaf
+  uint16_t first, last, next, pad;
+};
+static_assert(sizeof(MNode) == 24, "MNode is 24 bytes");
+
+__device__ __forceinline__ bool has_bracket(const uint8_t* p, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++)
+    if (p[i] == '[' || p[i] == ']') return true;
+  return false;
+}
+
+struct MapTree {
+  MNode* n;
+  uint32_t cnt;
+  const uint8_t* t;  // indexed (target) document
+  uint32_t tn;
+  const uint8_t* s;  // extract (source) document
+  uint32_t sn;
+  const uint8_t* pool;
+  int status;
+
+  __device__ const uint8_t* name_of(uint8_t src, uint32_t off, uint32_t len, uint8_t* tmp, uint32_t& l) const {
+    if (src == NS_TDOC) { l = len; return t + off; }
+    if (src == NS_POOL) { l = len; return pool + off; }
+    uint8_t d[10];
+    int k = 0;
+    uint32_t v = off;
+    do { d[k++] = (uint8_t)('0' + v % 10); v /= 10; } while (v);
+    for (int i = 0; i < k; i++) tmp[i] = d[k - 1 - i];
+    l = (uint32_t)k;
+    return tmp;
+  }
+  __device__ uint16_t add_node(uint8_t src, uint32_t off, uint32_t len) {
+    if (cnt >= MAP_NODES || len > 0xffff) { status = MAP_UNSUPPORTED; return MN_NONE; }
+    MNode& m = n[cnt];
+    m.name = off; m.nlen = (uint16_t)len; m.nsrc = src; m.type = MN_UNTYPED; m.lpos = 0; m.llen = 0;
+    m.first = m.last = m.next = MN_NONE; m.pad = 0;
+    return (uint16_t)cnt++;
+  }
+  // MsgPackTree.addChildToNode: the parent's child set keeps insertion order and no duplicates
+  __device__ uint16_t child(uint16_t parent, uint8_t src, uint32_t off, uint32_t len) {
+    uint8_t ta[12], tb[12];
+    uint32_t la, lb;
+    const uint8_t* a = name_of(src, off, len, ta, la);
+    for (uint16_t c = n[parent].first; c != MN_NONE; c = n[c].next) {
+      const uint8_t* b = name_of(n[c].nsrc, n[c].name, n[c].nlen, tb, lb);
+      if (la == lb && bytes_eq(a, b, la)) return c;
+    }
+    const uint16_t c = add_node(src, off, len);
+    if (c == MN_NONE) return c;
+    if (n[parent].last == MN_NONE) n[parent].first = c;
+    else n[n[parent].last].next = c;
+    n[parent].last = c;
+    return c;
+  }
+  __device__ void add_map(uint16_t x) { n[x].llen = 0; n[x].type = MN_MAP; }    // addMapNode: leaf removed
+  __device__ void add_array(uint16_t x) { n[x].type = MN_ARRAY; }               // addArrayNode: leaf kept
+  __device__ void add_leaf(uint16_t x, uint32_t pos, uint32_t len, bool extracted) {
+    n[x].lpos = pos; n[x].llen = len; n[x].type = extracted ? MN_LEAF_S : MN_LEAF_T;
+  }
+};
+
+// MsgPackDocumentIndexer.index of the target document into the tree (root node 0)
+__device__ inline void map_index(MapTree& T) {
+  Tok t;
+  if (T.tn == 0 || !read_tok(T.t, T.tn, t) || t.type == TT_NIL) return;  // empty tree
+  if (t.type != TT_MAP) { T.status = MAP_UNSUPPORTED; return; }
+  uint16_t fnode[MAP_DEPTH];
+  uint32_t frem[MAP_DEPTH], fidx[MAP_DEPTH];
+  bool farr[MAP_DEPTH];
+  int depth = 0;
+  T.add_map(0);
+  fnode[0] = 0; frem[0] = t.len; fidx[0] = 0; farr[0] = false;
+  depth = 1;
+  uint32_t pos = t.total;
+  while (depth > 0) {
+    const int L = depth - 1;
+    if (frem[L] == 0) { depth--; continue; }
+    frem[L]--;
+    uint16_t c;
+    if (!farr[L]) {
+      Tok k;
+      if (pos >= T.tn || !read_tok(T.t + pos, T.tn - pos, k)) { T.status = MAP_UNSUPPORTED; return; }
+      if (k.type != TT_STRING) { T.status = MAP_FAIL; return; }  // "non-string map key is not supported"
+      if (has_bracket(T.t + pos + k.hdr, k.len)) { T.status = MAP_UNSUPPORTED; return; }
+      c = T.child(fnode[L], NS_TDOC, pos + k.hdr, k.len);
+      pos += k.total;
+    } else {
+      c = T.child(fnode[L], NS_INDEX, fidx[L]++, 0);
+    }
+    if (c == MN_NONE) return;
+    Tok v;
+    if (pos >= T.tn || !read_tok(T.t + pos, T.tn - pos, v)) { T.status = MAP_UNSUPPORTED; return; }
+    if (v.type == TT_MAP || v.type == TT_ARRAY) {
+      if (v.type == TT_MAP) T.add_map(c); else T.add_array(c);
+      if (depth >= MAP_DEPTH) { T.status = MAP_UNSUPPORTED; return; }
+      fnode[depth] = c; frem[depth] = v.len; fidx[depth] = 0; farr[depth] = v.type == TT_ARRAY;
+      depth++;
+    } else {
+      T.add_leaf(c, pos, v.total, false);
+    }
+    pos += v.total;
+  }
+}
+
+// MsgPackDocumentExtractor.extract: every mapping's target path, then its source query's result as the leaf
+__device__ inline void map_extract(MapTree& T, const DevMapping* maps, uint32_t nmaps, const DevSeg* segs,
+                                   const DevQuery* queries, const DevFilter* filters, uint16_t& fail_query) {
+  for (uint32_t mi = 0; mi < nmaps; mi++) {
+    const DevMapping m = maps[mi];
+    uint16_t node = MN_NONE;
+    for (uint32_t k = 0; k < m.nseg; k++) {
+      const DevSeg sg = segs[m.seg + k];
+      const uint8_t* nm = T.pool + sg.off;
+      if (has_bracket(nm, sg.len)) { T.status = MAP_UNSUPPORTED; return; }
+      if (node == MN_NONE) {  // createParentRelation("", "$") is the root's id
+        node = 0;
+        continue;
+      }
+      bool index = true;  // isIndex :168-177 (an empty name counts as an index)
+      for (uint32_t i = 0; i < sg.len; i++)
+        if (nm[i] < '0' || nm[i] > '9') { index = false; break; }
+      if (index) {
+        if (T.n[node].type != MN_MAP) T.add_array(node);
+      } else {
+        T.add_map(node);
+      }
+      node = T.child(node, NS_POOL, sg.off, sg.len);
+      if (node == MN_NONE) return;
+    }
+    if (node == MN_NONE) { T.status = MAP_UNSUPPORTED; return; }
+    QueryResult r;
+    if (!run_query(T.s, T.sn, queries[m.query], filters, T.pool, r)) { T.status = MAP_UNSUPPORTED; return; }
+    if (r.count == 0) { T.status = MAP_ERR_NO_DATA; fail_query = m.query; return; }
+    if (r.count > 1) { T.status = MAP_FAIL; return; }  // IllegalStateException: more than one matching source
+    T.add_leaf(node, r.pos, r.len, true);
+  }
+}
+
+// MsgPackDocumentTreeWriter.write
+__device__ inline void map_write(MapTree& T, Out& o) {
+  if (T.n[0].type == MN_UNTYPED && T.n[0].llen == 0) { o.put(0xc0); return; }  // empty tree: nil
+  uint16_t fnode[MAP_DEPTH + 1];
+  bool farr[MAP_DEPTH + 1];
+  int depth = 0;
+  uint16_t x = 0;
+  bool key = false;
+  bool arr_parent = false;
+  for (;;) {
+    // write node x (its key first, unless the parent is an array or x is the root)
+    const MNode m = T.n[x];
+    if (key && !arr_parent) {
+      uint8_t tmp[12];
+      uint32_t l;
+      const uint8_t* nm = T.name_of(m.nsrc, m.name, m.nlen, tmp, l);
+      o.str(nm, l);
+    }
+    if (m.llen) {
+      // the buffer follows the node type, not where the leaf came from (an extracted leaf under a node that
+      // addArrayNode retyped is read from the indexed document): out of its bounds the reference's buffer
+      // access throws
+      const bool from_s = m.type == MN_LEAF_S;
+      if ((uint64_t)m.lpos + m.llen > (from_s ? T.sn : T.tn)) { T.status = MAP_FAIL; return; }
+      o.put_bytes((from_s ? T.s : T.t) + m.lpos, m.llen);
+    } else if (m.type == MN_MAP || m.type == MN_ARRAY) {
+      uint32_t nc = 0;
+      for (uint16_t c = m.first; c != MN_NONE; c = T.n[c].next) nc++;
+      if (m.type == MN_ARRAY) o.arr_hdr(nc); else o.map_hdr(nc);
+      if (m.first != MN_NONE) {
+        if (depth > MAP_DEPTH) { T.status = MAP_UNSUPPORTED; return; }
+        fnode[depth] = m.first;
+        farr[depth] = m.type == MN_ARRAY;
+        depth++;
+        x = m.first; key = true; arr_parent = m.type == MN_ARRAY;
+        continue;
+      }
+    } else {
+      T.status = MAP_FAIL;  // a child without node type: NullPointerException in the writer
+      return;
+    }
+    // next sibling, or climb
+    for (;;) {
+      if (depth == 0) return;
+      const uint16_t nx = T.n[fnode[depth - 1]].next;
+      if (nx != MN_NONE) {
+        fnode[depth - 1] = nx;
+        x = nx; key = true; arr_parent = farr[depth - 1];
+        break;
+      }
+      depth--;
+    }
+  }
+}
+
+// The result document of MappingProcessor.extract(src, mappings) (tgt == nullptr) or .merge(src, tgt,
+// mappings), nmaps >= 1; the size pass when o.dst == nullptr. Returns MAP_OK, MAP_ERR_NO_DATA (fail_query set)
+// or MAP_ERR_NOT_MAP (MappingException -> IO_MAPPING_ERROR incident), MAP_FAIL (any other exception: the
+// processor fails) or MAP_UNSUPPORTED. ws: MAP_NODES nodes.
+__device__ __noinline__ int map_documents(const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint32_t nt,
+                                          const DevMapping* maps, uint32_t nmaps, const DevSeg* segs,
+                                          const DevQuery* queries, const DevFilter* filters, const uint8_t* pool,
+                                          MNode* ws, Out& o, uint16_t& fail_query) {
+  MapTree T;
+  T.n = ws; T.cnt = 0; T.t = tgt; T.tn = tgt ? nt : 0; T.s = src; T.sn = ns; T.pool = pool; T.status = MAP_OK;
+  T.add_node(NS_INDEX, 0, 0);  // "$"
+  if (tgt) map_index(T);
+  if (T.status != MAP_OK) return T.status;
+  map_extract(T, maps, nmaps, segs, queries, filters, fail_query);
+  if (T.status != MAP_OK) return T.status;
+  map_write(T, o);
+  if (T.status != MAP_OK) return T.status;
+  // ensureDocumentIsAMsgPackMap :206-213: the written document must be a map (or nil)
+  const MNode r = T.n[0];
+  if (r.llen) {
+    const uint8_t b = (r.type == MN_LEAF_S ? src : tgt)[r.lpos];
+    if (!((b & 0xf0) == 0x80 || b == 0xde || b == 0xdf || b == 0xc0)) return MAP_ERR_NOT_MAP;
+  } else if (r.type == MN_ARRAY) {
+    return MAP_ERR_NOT_MAP;
+  }
+  return MAP_OK;
+}
+
 }  // namespace zbg

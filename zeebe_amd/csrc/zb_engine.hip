@@ -17,6 +17,7 @@
 #include <unordered_set>
 #include <vector>
 
+#include "zb_devlib.hpp"
 #include "zb_kernels.hpp"
 #include "zb_model.hpp"
 #include "zb_msg.hpp"
@@ -74,6 +75,11 @@ struct zb_engine {
   DevVec<DevQuery> d_queries;
   DevVec<DevFilter> d_filters;
   DevVec<uint8_t> d_pool;
+  DevVec<DevMapping> d_maps;
+  DevVec<DevSeg> d_segs;
+  bool has_io = false;          // some element has a zeebe:ioMapping (k_map runs, no trajectory path)
+  uint64_t* mapres = nullptr;   // k_map outcomes [wave_cap + 8]
+  MNode* map_ws = nullptr;      // k_map tree workspaces
   int ser_mode = 0;              // ZB_SER_MODE: 0 = two passes (size, scan, write), 1 = single pass (look-back)
 
   // device state
@@ -263,6 +269,8 @@ int upload_model(zb_engine* e) {
   HIPCHECK(e, e->d_queries.upload(e->model.queries, e->stream));
   HIPCHECK(e, e->d_filters.upload(e->model.filters, e->stream));
   HIPCHECK(e, e->d_pool.upload(e->model.pool, e->stream));
+  HIPCHECK(e, e->d_maps.upload(e->model.maps, e->stream));
+  HIPCHECK(e, e->d_segs.upload(e->model.segs, e->stream));
   if (e->static_blobs.size() > STATIC_ARENA_BYTES) return fail(e, ZB_ENOMEM, "static payload region full");
   HIPCHECK(e, hipMemcpyAsync(e->arena, e->static_blobs.data(), e->static_blobs.size(), hipMemcpyHostToDevice,
                              e->stream));
@@ -286,6 +294,10 @@ WaveParams wave_params(zb_engine* e) {
   p.queries = e->d_queries.p;
   p.filters = e->d_filters.p;
   p.pool = e->d_pool.p;
+  p.maps = e->d_maps.p;
+  p.segs = e->d_segs.p;
+  p.mapres = e->mapres;
+  p.map_ws = e->map_ws;
   p.hdr = e->hdr;
   p.cw = e->cw;
   p.stage = e->stage;
@@ -706,7 +718,7 @@ void zb_engine_destroy(zb_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (auto& x : e->ev)
     if (x) (void)hipEventDestroy(x);
-  void* ps[] = {e->log, e->links, e->srcd, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
+  void* ps[] = {e->mapres, e->map_ws, e->log, e->links, e->srcd, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
                 e->merge_jobs, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
@@ -808,13 +820,18 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
     if (el.step[WI_GATEWAY_ACTIVATED] == ST_EXCLUSIVE_SPLIT) e->has_splits = true;
     if (el.kind == EK_CATCH) e->has_catch = true;
     if (el.kind == EK_PAR) e->has_parallel = true;
+    if (el.flags & EF_IO) e->has_io = true;
+  }
+  if (e->has_io && !e->mapres) {
+    HIPCHECK(e, hipMalloc(&e->mapres, (e->wave_cap + 8) * sizeof(uint64_t)));
+    HIPCHECK(e, hipMalloc(&e->map_ws, (size_t)MAP_GRID * 256 * MAP_NODES * sizeof(MNode)));
   }
   if (e->has_catch) {
     int orc = ensure_outbox(e);
     if (orc != ZB_OK) return orc;
   }
   // the trajectory count pass skips payload merges, so conditions must never read a merge result
-  e->traj_model_ok = !(e->has_merges && e->has_splits);
+  e->traj_model_ok = !(e->has_merges && e->has_splits) && !e->has_io;
   // class batches: every split of the model is one digit (radix conditions + 2) of an 8-bit outcome key
   e->nsplits = 0;
   e->cls_ok = true;
@@ -1320,7 +1337,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     // an idle partition fed only CREATE commands runs as independent trajectories (zb_traj.hip) -- with the
     // canonical job harness and no parallel gateways (the general wave pipeline covers everything else)
     try_traj = !(e->cfg.flags & (ZB_CFG_WAVE_ONLY | ZB_CFG_EXTERNAL_JOBS)) && max_waves == 0 &&
-               e->staged_only_creates && !e->has_parallel &&
+               e->staged_only_creates && !e->has_parallel && !e->has_io &&
                (e->traj_model_ok || (e->cls_ok && e->staged_uniform)) &&
                e->host_hdr.begin == e->host_hdr.end;
     traj_base = e->host_hdr.end;
@@ -1405,6 +1422,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
         launch_pre(p, e->stream);
         if (p.term) launch_children(p, e->stream);
       }
+      if (e->has_io) launch_map(p, e->stream);  // io-mapping results of the chunk's records
       if (e->wave_fused_grid) {  // process + scan + emit in one launch (k_wave)
         launch_wave(p, e->wave_fused_grid, e->stream);
         HIPCHECK(e, hipEventRecord(ev[1], e->stream));

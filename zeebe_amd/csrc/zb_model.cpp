@@ -548,6 +548,66 @@ struct Deployer {
     return idx;
   }
 
+  // FlowNodeHandler (transformation/handler/FlowNodeHandler.java): zeebe:ioMapping inputs / outputs / output
+  // behaviour, validated as ZeebeIoMappingValidator (broker-core/.../validation/ZeebeIoMappingValidator.java:36-57,
+  // bpmn-model/.../validation/zeebe/ZeebeIoMappingValidator.java:31-39) and ZeebeExpressionValidator
+  // (.validateJsonPath :42-54) validate them at deployment
+  int io_mapping(DevElem& e, const Node* io) {
+    std::vector<std::pair<std::string, std::string>> ins, outs;
+    for (auto& k : io->kids) {
+      if (k->tag != "input" && k->tag != "output") continue;
+      const char* src = k->get("source");
+      const char* tgt = k->get("target");
+      (k->tag == "input" ? ins : outs).emplace_back(src ? src : "", tgt ? tgt : "");
+    }
+    uint8_t ob = OB_UNSET;
+    if (const char* b = io->get("outputBehavior")) {
+      const std::string bs(b);
+      if (bs == "none") ob = OB_NONE;
+      else if (bs == "merge") ob = OB_MERGE;
+      else if (bs == "overwrite") ob = OB_OVERWRITE;
+      else { err = "invalid outputBehavior: " + bs; return ZB_EDEPLOY; }
+    }
+    auto root_target = [](const std::vector<std::pair<std::string, std::string>>& ms) {
+      for (auto& m : ms)
+        if (m.second == "$") return true;
+      return false;
+    };
+    if (ins.size() > 1 && root_target(ins)) { err = "Invalid inputs: When using $ as target, no other input can be defined"; return ZB_EDEPLOY; }
+    if (outs.size() > 1 && root_target(outs)) { err = "Invalid outputs: When using $ as target, no other output can be defined"; return ZB_EDEPLOY; }
+    if (ob == OB_NONE && !outs.empty()) {
+      err = "Output behavior 'none' cannot be used in combination without zeebe:output elements";
+      return ZB_EDEPLOY;
+    }
+    for (const auto* ms : {&ins, &outs})
+      for (auto& m : *ms)
+        for (const std::string& path : {m.first, m.second}) {
+          ModelTables scratch;
+          std::string qerr;
+          if (compile_query(scratch, path, qerr) < 0) { err = "JSON path query is invalid: " + qerr; return ZB_EDEPLOY; }
+          // PROHIBITED_PATHS_REGEX "(\\.\\*)|(\\[.*,.*\\])"
+          const size_t lb = path.find('[');
+          const size_t comma = lb == std::string::npos ? std::string::npos : path.find(',', lb + 1);
+          if (path.find(".*") != std::string::npos ||
+              (comma != std::string::npos && path.find(']', comma + 1) != std::string::npos)) {
+            err = "This JSON path query is not supported";
+            return ZB_EDEPLOY;
+          }
+        }
+    if (ins.size() > 255 || outs.size() > 255) { err = "more than 255 io mappings on one element"; return ZB_EUNSUPPORTED; }
+    e.flags |= EF_IO | (uint8_t)(ob << OB_SHIFT);
+    e.map_in = (uint16_t)t.maps.size();
+    e.n_in = (uint8_t)ins.size();
+    for (auto& m : ins)
+      if (compile_mapping(t, m.first, m.second, err) < 0) return ZB_EDEPLOY;
+    e.map_out = (uint16_t)t.maps.size();
+    e.n_out_map = (uint8_t)outs.size();
+    for (auto& m : outs)
+      if (compile_mapping(t, m.first, m.second, err) < 0) return ZB_EDEPLOY;
+    if (t.maps.size() >= 0xffff) { err = "too many io mappings"; return ZB_EUNSUPPORTED; }
+    return ZB_OK;
+  }
+
   int process(const Node* proc, int64_t key, int32_t version) {
     ids.clear();
     order.clear();
@@ -639,9 +699,9 @@ struct Deployer {
       }
       DevElem& e = E(ei);
       // FlowNodeHandler: io mapping + outgoing behaviour from <outgoing> references
-      if (extension(n, "ioMapping")) {
-        err = "io mappings are not implemented on the GPU path yet (element '" + std::string(n->get("id")) + "')";
-        return ZB_EUNSUPPORTED;
+      if (const Node* io = extension(n, "ioMapping")) {
+        const int rc = io_mapping(e, io);
+        if (rc != ZB_OK) return rc;
       }
       int n_out_refs = 0;
       for (auto& k : n->kids)
@@ -775,6 +835,47 @@ int compile_query(ModelTables& t, const std::string& expr, std::string& err) {
   t.filters.insert(t.filters.end(), fs.begin(), fs.end());
   t.queries.push_back(q);
   return (int)t.queries.size() - 1;
+}
+
+// JsonPathTokenizer (json-path/.../jsonpath/JsonPathTokenizer.java): operators in table order ("$", "..", ".",
+// "*", "['", "']", "[", "]"), everything between them a LITERAL; after "['" only "']" is recognised
+static void path_literals(const std::string& e, std::vector<std::pair<uint32_t, uint32_t>>& out) {
+  static const char* OPS[8] = {"$", "..", ".", "*", "['", "']", "[", "]"};
+  size_t pos = 0, last = 0;
+  bool bracket = false;
+  while (pos < e.size()) {
+    bool hit = false;
+    for (int i = 0; i < 8 && !hit; i++) {
+      if (bracket && i != 5) continue;
+      const size_t l = strlen(OPS[i]);
+      if (e.compare(pos, l, OPS[i]) == 0) {
+        if (last < pos) out.emplace_back((uint32_t)last, (uint32_t)(pos - last));
+        if (i == 0) out.emplace_back((uint32_t)pos, 1u);  // ROOT_OBJECT
+        bracket = i == 4;
+        pos += l;
+        last = pos;
+        hit = true;
+      }
+    }
+    if (!hit) pos++;
+  }
+  if (last < pos) out.emplace_back((uint32_t)last, (uint32_t)(pos - last));
+}
+
+int compile_mapping(ModelTables& t, const std::string& source, const std::string& target, std::string& err) {
+  const int q = compile_query(t, source, err);
+  if (q < 0) return -1;
+  std::vector<std::pair<uint32_t, uint32_t>> lits;
+  path_literals(target, lits);
+  if (lits.empty() || lits.size() > 0xffff || t.maps.size() >= 0xffff) { err = "invalid mapping target"; return -1; }
+  DevMapping m{};
+  m.query = (uint16_t)q;
+  m.nseg = (uint16_t)lits.size();
+  m.seg = (uint32_t)t.segs.size();
+  const uint32_t base = t.add_bytes(target);
+  for (auto& l : lits) t.segs.push_back(DevSeg{base + l.first, l.second});
+  t.maps.push_back(m);
+  return (int)t.maps.size() - 1;
 }
 
 static bool has_large_int_const(const ModelTables& t, const CondAst* n) {

@@ -27,6 +27,8 @@ struct ModelTables {
   std::vector<DevQuery> queries;
   std::vector<DevFilter> filters;
   std::vector<uint8_t> pool;
+  std::vector<DevMapping> maps;  // explicit io-mappings (DevElem.map_in / map_out ranges)
+  std::vector<DevSeg> segs;      // their target path segments
   // host-only
   std::vector<std::string> elem_ids;
 
@@ -42,6 +44,11 @@ int compile_deployment(ModelTables& t, const std::string& xml, int64_t workflow_
 
 // json-path compilation into t.queries/t.filters; returns query index or -1 (invalid, err set)
 int compile_query(ModelTables& t, const std::string& expr, std::string& err);
+
+// one io-mapping (Mapping.java): the source compiled as a json-path query, the target split into the
+// LITERAL / ROOT_OBJECT tokens of JsonPathTokenizer (MsgPackDocumentExtractor.extract walks them); appended
+// to t.maps / t.segs, returns its index or -1 (err set)
+int compile_mapping(ModelTables& t, const std::string& source, const std::string& target, std::string& err);
 
 // json-el compilation; returns program offset in t.code or -1 (err set)
 int compile_condition(ModelTables& t, const std::string& expr, std::string& err);

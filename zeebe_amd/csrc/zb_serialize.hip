@@ -112,6 +112,13 @@ __device__ inline void message(W& w, const SerParams& P, const uint8_t* det, boo
       case EC_MAPPING_NOT_MAP:
         o.cstr("Processing failed, since mapping will result in a non map object (json object).");
         break;
+      case EC_MAPPING_NO_DATA: {  // MsgPackDocumentExtractor.executeLeafMapping :185-203
+        const DevQuery& qq = P.queries[q];
+        o.cstr("No data found for query ");
+        o.put_bytes(P.pool + qq.expr_off, qq.expr_len);
+        o.cstr(".");
+        break;
+      }
     }
   }
   (void)size_only_hdr;

@@ -143,6 +143,21 @@ __device__ void incident(TState& t, const zb_rec& rec, int64_t pos, uint8_t type
   t.bytes += 24;  // [u32 len=16][type code a b][u16 q][pad][i64 position]
 }
 
+// k_map's outcome for the record at pos (zb_aux.hip)
+__device__ __forceinline__ uint64_t map_outcome(const WaveParams& P, int64_t pos) {
+  return P.mapres[pos - P.hdr[P.wave & 1].begin];
+}
+// true: a result document (ref in the low bits); otherwise the IO_MAPPING_ERROR incident is raised
+// (BpmnStepContext.raiseIncident) or the processor fails
+__device__ bool map_ok(TState& t, const zb_rec& rec, int64_t pos, uint64_t mr) {
+  const uint64_t st = mr & (15ull << 60);
+  if (st == MR_OK) return true;
+  if (st == MR_INCIDENT) incident(t, rec, pos, 1 /*IO_MAPPING_ERROR*/, (uint8_t)(mr >> 48), 0, 0, (uint16_t)(mr >> 32));
+  else if (st == MR_UNSUPPORTED) fail_at(t, DE_UNSUPPORTED, 30);
+  else fail_at(t, DE_PROCESSING, 31);  // MappingProcessor threw something else (or no outcome)
+  return false;
+}
+
 __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, uint32_t rself, uint32_t rscope,
                           TState& t) {
   const uint8_t intent = rec.intent;
@@ -173,18 +188,42 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
   if (step == ST_UNBOUND || step == ST_NONE) return;
 
   switch (step) {
-    case ST_APPLY_INPUT_MAPPING: {  // InputMappingHandler (no mappings: io mappings are rejected at deploy)
+    case ST_APPLY_INPUT_MAPPING: {  // InputMappingHandler :39-70 (mappings: extract, done by k_map)
+      uint32_t pay = rec.payload;
+      if (el.n_in) {
+        const uint64_t mr = map_outcome(P, pos);
+        if (!map_ok(t, rec, pos, mr)) return;
+        pay = (uint32_t)mr;
+      }
       Slot& s = add_slot(t);
       s.d = rec;
+      s.d.payload = pay;
       wf_event(t, s, WI_ELEMENT_ACTIVATED, t.ns > 1);
       s.rself = rself; s.rscope = rscope;
       RowMeta& m = P.rmeta[rself];
       m.state = WI_ELEMENT_ACTIVATED;
-      m.payload = rec.payload;
+      m.payload = pay;
       break;
     }
     case ST_APPLY_OUTPUT_MAPPING: {  // OutputMappingHandler :42-85, outputBehavior null -> merge
       if (!scope_alive) { fail_at(t, DE_PROCESSING, 4); return; }
+      const uint8_t ob = (el.flags >> OB_SHIFT) & 3;
+      if (ob == OB_NONE || el.n_out_map || ob == OB_OVERWRITE) {
+        // none: the flow scope's payload; mappings / overwrite: the document k_map produced
+        uint32_t pay = P.rmeta[rscope].payload;
+        if (ob != OB_NONE) {
+          const uint64_t mr = map_outcome(P, pos);
+          if (!map_ok(t, rec, pos, mr)) return;
+          pay = (uint32_t)mr;
+        }
+        Slot& s = add_slot(t);
+        s.d = rec;
+        s.d.payload = pay;
+        wf_event(t, s, WI_ELEMENT_COMPLETED, t.ns > 1);
+        s.rself = rself; s.rscope = rscope;
+        remove_row(P, rself);
+        break;
+      }
       // The merge itself runs once, in the write phase, into an arena blob sized by the upper bound
       // |result| <= |source| + |target| + 3 (root header grows by <= 4, sub-headers / keys are
       // re-encoded minimally so never grow): no size pass on the hot path.
