@@ -51,7 +51,9 @@ enum WfIntent : uint8_t {
   ELEMENT_TERMINATING = 10, ELEMENT_TERMINATED = 11, CANCEL = 12, CANCELING = 13, UPDATE_PAYLOAD = 14,
   PAYLOAD_UPDATED = 15
 };
-enum JobIntentE : uint8_t { JOB_CREATE = 0, JOB_CREATED = 1, JOB_COMPLETED = 5, JOB_CANCEL = 12 };
+enum JobIntentE : uint8_t { JOB_CREATE = 0, JOB_CREATED = 1, JOB_ACTIVATE = 2, JOB_ACTIVATED = 3, JOB_COMPLETE = 4,
+                            JOB_COMPLETED = 5, JOB_TIME_OUT = 6, JOB_TIMED_OUT = 7, JOB_FAIL = 8, JOB_FAILED = 9,
+                            JOB_UPDATE_RETRIES = 10, JOB_RETRIES_UPDATED = 11, JOB_CANCEL = 12, JOB_CANCELED = 13 };
 enum IncidentIntentE : uint8_t { INCIDENT_CREATE = 0 };
 enum WisIntent : uint8_t { WIS_CORRELATE = 0, WIS_CORRELATED = 1 };  // WorkflowInstanceSubscriptionIntent.java:19-20
 enum MsgIntent : uint8_t { MSG_PUBLISH = 0, MSG_PUBLISHED = 1, MSG_DELETE = 2, MSG_DELETED = 3 };  // MessageIntent.java:19-23
@@ -650,6 +652,11 @@ class Engine {
   // canonical job harness on; off: JOB CREATE commands wait for job events submitted
   // from outside (the job stream processor's JOB CREATED / JOB COMPLETED records, zbref_submit_record)
   bool harness = true;
+  // the job stream processor (JobInstanceStreamProcessor.java:70-242) on the same log, as a FIFO participant:
+  // JOB commands are processed at their log position; job states by key (JobStateController)
+  bool job_processor = false;
+  enum JobState : uint8_t { JS_NONE = 0, JS_CREATED, JS_ACTIVATED, JS_FAILED, JS_TIMED_OUT };
+  std::unordered_map<int64_t, uint8_t> job_states;
   std::string last_error;
 
   // ZeebeIoMappingValidator (broker-core/.../validation/ZeebeIoMappingValidator.java:36-57), the model's
@@ -1027,7 +1034,8 @@ class Engine {
         }
       }
     } else if (rec.value_type == VT_JOB) {
-      if (rec.record_type == RT_COMMAND && rec.intent == JOB_CREATE) { if (harness) harness_job_create(rec); }
+      if (rec.record_type == RT_COMMAND && job_processor) process_job_command(rec);
+      else if (rec.record_type == RT_COMMAND && rec.intent == JOB_CREATE) { if (harness) harness_job_create(rec); }
       else if (rec.record_type == RT_EVENT && rec.intent == JOB_CREATED) process_job_created(rec);
       else if (rec.record_type == RT_EVENT && rec.intent == JOB_COMPLETED) process_job_completed(rec);
     } else if (rec.value_type == VT_WORKFLOW_INSTANCE_SUBSCRIPTION) {
@@ -1188,6 +1196,67 @@ class Engine {
     stage_event(rec.key, VT_MESSAGE, MSG_DELETED, rec);
     for (size_t i = 0; i < msgs.size(); i++)
       if (msgs[i].key == rec.key) { msgs.erase(msgs.begin() + i); break; }
+  }
+
+  // JobInstanceStreamProcessor :98-242. CommandProcessorImpl: accept -> writeFollowUpEvent(key, intent, command
+  // value) with a new key for a null command key (:73-82); reject -> writeRejection(command, type, reason)
+  void process_job_command(const Record& cmd) {
+    auto st = [&]() -> uint8_t {
+      auto it = job_states.find(cmd.key);
+      return it == job_states.end() ? JS_NONE : it->second;
+    };
+    auto accept = [&](uint8_t intent, int64_t key) {
+      Record a = cmd;
+      a.key = key; a.record_type = RT_EVENT; a.intent = intent;
+      w_->stage(std::move(a));
+    };
+    const uint8_t s0 = st();
+    switch (cmd.intent) {
+      case JOB_CREATE: {  // CreateJobProcessor :98-106
+        const int64_t key = cmd.key < 0 ? job_keys.next_key() : cmd.key;
+        job_states[key] = JS_CREATED;
+        accept(JOB_CREATED, key);
+        break;
+      }
+      case JOB_ACTIVATE:  // ActivateJobProcessor :108-160 (the push to the subscriber is a side effect)
+        if (s0 == JS_CREATED || s0 == JS_FAILED || s0 == JS_TIMED_OUT) {
+          job_states[cmd.key] = JS_ACTIVATED;
+          accept(JOB_ACTIVATED, cmd.key);
+        } else {
+          write_rejection(cmd, REJ_NOT_APPLICABLE, "Job is not in one of these states: CREATED, FAILED, TIMED_OUT");
+        }
+        break;
+      case JOB_COMPLETE:  // CompleteJobProcessor :162-175
+        if (s0 == JS_ACTIVATED || s0 == JS_TIMED_OUT) {
+          job_states.erase(cmd.key);
+          accept(JOB_COMPLETED, cmd.key);
+        } else {
+          write_rejection(cmd, REJ_NOT_APPLICABLE, "Job is not in state: ACTIVATED, TIMED_OUT");
+        }
+        break;
+      case JOB_FAIL:  // FailJobProcessor :177-189
+        if (s0 == JS_ACTIVATED) { job_states[cmd.key] = JS_FAILED; accept(JOB_FAILED, cmd.key); }
+        else write_rejection(cmd, REJ_NOT_APPLICABLE, "Job is not in state ACTIVATED");
+        break;
+      case JOB_TIME_OUT:  // TimeOutJobProcessor :191-204
+        if (s0 == JS_ACTIVATED) { job_states[cmd.key] = JS_TIMED_OUT; accept(JOB_TIMED_OUT, cmd.key); }
+        else write_rejection(cmd, REJ_NOT_APPLICABLE, "Job is not in state ACTIVATED");
+        break;
+      case JOB_UPDATE_RETRIES:  // UpdateRetriesJobProcessor :206-222
+        if (s0 == JS_FAILED) {
+          if (cmd.job.retries > 0) accept(JOB_RETRIES_UPDATED, cmd.key);
+          else write_rejection(cmd, REJ_BAD_VALUE, "Retries must be greater than 0");
+        } else {
+          write_rejection(cmd, REJ_NOT_APPLICABLE, "Job is not in state FAILED");
+        }
+        break;
+      case JOB_CANCEL:  // CancelJobProcessor :224-240
+        if (s0 != JS_NONE) { job_states.erase(cmd.key); accept(JOB_CANCELED, cmd.key); }
+        else write_rejection(cmd, REJ_NOT_APPLICABLE, "Job does not exist");
+        break;
+      default:
+        break;
+    }
   }
 
   // canonical harness: the job processor as a deterministic FIFO participant
@@ -1533,6 +1602,14 @@ int zbref_submit_create(void* h, const char* process_id, int32_t version, int64_
 
 int zbref_set_harness(void* h, int on) {
   ((Engine*)h)->harness = on != 0;
+  return 0;
+}
+
+// the job stream processor on (harness off): JOB commands go through JobInstanceStreamProcessor
+int zbref_set_job_processor(void* h, int on) {
+  Engine* e = (Engine*)h;
+  e->job_processor = on != 0;
+  if (on) e->harness = false;
   return 0;
 }
 

@@ -42,6 +42,7 @@ def lib():
         L.zbref_submit_cancel.argtypes = [vp, i64]
         L.zbref_submit_creates.argtypes = [vp, cp, i32, i64, sz, ctypes.c_void_p, ctypes.c_void_p]
         L.zbref_set_harness.argtypes = [vp, ctypes.c_int]
+        L.zbref_set_job_processor.argtypes = [vp, ctypes.c_int]
         L.zbref_submit_record.argtypes = [vp, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, i64, u8p, sz]
         L.zbref_dump_instances.restype = i64
         L.zbref_dump_instances.argtypes = [vp, ctypes.c_void_p, sz]
@@ -175,6 +176,10 @@ class Oracle:
     def set_harness(self, on: bool):
         """Canonical job harness on (default) / off (JOB CREATE commands wait for submitted job events)."""
         self._L.zbref_set_harness(self._h, 1 if on else 0)
+
+    def set_job_processor(self, on: bool):
+        """The job stream processor (JobInstanceStreamProcessor) processes JOB commands on this log (harness off)."""
+        self._L.zbref_set_job_processor(self._h, 1 if on else 0)
 
     def submit(self, record_type: int, value_type: int, intent: int, key: int, value: bytes):
         """A record written by another writer, as its reference msgpack value (kept verbatim in the log)."""

@@ -535,6 +535,50 @@ def io_workflows():
                     "incident": inc})
     return out
 
+def job_sequences():
+    """JobInstanceStreamProcessorTest.java:59-462: commands written to the job stream processor, in batches
+    that reach the log before the processor sees any of them (the tests' blockAfterJobEvent / unblock), and
+    the job records the log ends up with as (recordType, intent). Values: job() = JobRecord{type "foo"},
+    activated = JobRecord{type "foo", worker "bar", deadline} (:481-497). Key 1 for every command."""
+    C, E, R = "COMMAND", "EVENT", "COMMAND_REJECTION"
+
+    def seq(name, batches, expect):
+        return {"name": name, "key": 1, "batches": batches, "expect": [[t, i] for t, i in expect]}
+
+    return [
+        seq("complete_expired_job", [["CREATE"], ["ACTIVATE"], ["TIME_OUT"], ["COMPLETE"]],   # :59-97
+            [(C, "CREATE"), (E, "CREATED"), (C, "ACTIVATE"), (E, "ACTIVATED"), (C, "TIME_OUT"), (E, "TIMED_OUT"),
+             (C, "COMPLETE"), (E, "COMPLETED")]),
+        seq("activate_only_once", [["CREATE"], ["ACTIVATE", "ACTIVATE"]],                     # :99-131
+            [(C, "CREATE"), (E, "CREATED"), (C, "ACTIVATE"), (C, "ACTIVATE"), (E, "ACTIVATED"), (R, "ACTIVATE")]),
+        seq("reject_activation_job_not_found", [["ACTIVATE"]],                                # :133-155
+            [(C, "ACTIVATE"), (R, "ACTIVATE")]),
+        seq("expire_activation_only_once", [["CREATE"], ["ACTIVATE"], ["TIME_OUT", "TIME_OUT"]],  # :157-194
+            [(C, "CREATE"), (E, "CREATED"), (C, "ACTIVATE"), (E, "ACTIVATED"), (C, "TIME_OUT"), (C, "TIME_OUT"),
+             (E, "TIMED_OUT"), (R, "TIME_OUT")]),
+        seq("reject_expire_if_created", [["CREATE"], ["TIME_OUT"]],                           # :200-226
+            [(C, "CREATE"), (E, "CREATED"), (C, "TIME_OUT"), (R, "TIME_OUT")]),
+        seq("reject_expire_if_completed", [["CREATE"], ["ACTIVATE"], ["COMPLETE", "TIME_OUT"]],  # :228-265
+            [(C, "CREATE"), (E, "CREATED"), (C, "ACTIVATE"), (E, "ACTIVATED"), (C, "COMPLETE"), (C, "TIME_OUT"),
+             (E, "COMPLETED"), (R, "TIME_OUT")]),
+        seq("reject_expire_if_failed", [["CREATE"], ["ACTIVATE"], ["FAIL", "TIME_OUT"]],      # :267-304
+            [(C, "CREATE"), (E, "CREATED"), (C, "ACTIVATE"), (E, "ACTIVATED"), (C, "FAIL"), (C, "TIME_OUT"),
+             (E, "FAILED"), (R, "TIME_OUT")]),
+        seq("reject_expire_job_not_found", [["TIME_OUT"]],                                    # :306-326
+            [(C, "TIME_OUT"), (R, "TIME_OUT")]),
+        seq("cancel_created_job", [["CREATE"], ["CANCEL"]],                                   # :328-353
+            [(C, "CREATE"), (E, "CREATED"), (C, "CANCEL"), (E, "CANCELED")]),
+        seq("cancel_activated_job", [["CREATE"], ["ACTIVATE"], ["CANCEL"]],                   # :355-386
+            [(C, "CREATE"), (E, "CREATED"), (C, "ACTIVATE"), (E, "ACTIVATED"), (C, "CANCEL"), (E, "CANCELED")]),
+        seq("cancel_failed_job", [["CREATE"], ["ACTIVATE"], ["FAIL"], ["CANCEL"]],            # :388-424
+            [(C, "CREATE"), (E, "CREATED"), (C, "ACTIVATE"), (E, "ACTIVATED"), (C, "FAIL"), (E, "FAILED"),
+             (C, "CANCEL"), (E, "CANCELED")]),
+        seq("reject_cancel_if_completed", [["CREATE"], ["ACTIVATE"], ["COMPLETE"], ["CANCEL"]],  # :426-462
+            [(C, "CREATE"), (E, "CREATED"), (C, "ACTIVATE"), (E, "ACTIVATED"), (C, "COMPLETE"), (E, "COMPLETED"),
+             (C, "CANCEL"), (R, "CANCEL")]),
+    ]
+
+
 def main():
     data = {
         "conditions": conditions(),
@@ -549,6 +593,7 @@ def main():
         "mapping_extracts": mapping_extracts(),
         "mapping_merges": mapping_merges(),
         "io_workflows": io_workflows(),
+        "job_sequences": job_sequences(),
         "wf_intents": WF,
     }
     with open(os.path.join(HERE, "reference_vectors.json"), "w") as f:

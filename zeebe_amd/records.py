@@ -29,7 +29,11 @@ WI_NAMES = ["CREATE", "CREATED", "START_EVENT_OCCURRED", "END_EVENT_OCCURRED", "
             "ELEMENT_TERMINATING", "ELEMENT_TERMINATED", "CANCEL", "CANCELING", "UPDATE_PAYLOAD", "PAYLOAD_UPDATED"]
 # JobIntent.java:18-37
 JI_CREATE, JI_CREATED, JI_ACTIVATE, JI_ACTIVATED, JI_COMPLETE, JI_COMPLETED = 0, 1, 2, 3, 4, 5
+JI_TIME_OUT, JI_TIMED_OUT, JI_FAIL, JI_FAILED, JI_UPDATE_RETRIES, JI_RETRIES_UPDATED = 6, 7, 8, 9, 10, 11
 JI_CANCEL, JI_CANCELED = 12, 13
+JI_NAMES = ["CREATE", "CREATED", "ACTIVATE", "ACTIVATED", "COMPLETE", "COMPLETED", "TIME_OUT", "TIMED_OUT", "FAIL",
+            "FAILED", "UPDATE_RETRIES", "RETRIES_UPDATED", "CANCEL", "CANCELED"]
+RT_NAMES = ["EVENT", "COMMAND", "COMMAND_REJECTION"]
 # WorkflowInstanceSubscriptionIntent.java:19-20
 WIS_CORRELATE, WIS_CORRELATED = 0, 1
 
