@@ -52,6 +52,10 @@ extern "C" {
 #define ZB_CFG_WAVE_ONLY 1    /* always use the general wave pipeline (never the trajectory path) */
 #define ZB_CFG_EXTERNAL_JOBS 2 /* no canonical job harness: JOB CREATE commands wait for the job stream
                                   processor's JOB CREATED / JOB COMPLETED events, submitted with zb_submit */
+#define ZB_CFG_JOB_PROCESSOR 4 /* the job stream processor runs on the GPU too (JobInstanceStreamProcessor.java:70-242):
+                                 JOB commands (the workflow's CREATE / CANCEL, a worker's ACTIVATE / COMPLETE /
+                                 FAIL / TIME_OUT / UPDATE_RETRIES through zb_submit) are processed at their log
+                                 position with per-job states; implies no harness (as ZB_CFG_EXTERNAL_JOBS) */
 
 typedef struct zb_engine zb_engine;
 

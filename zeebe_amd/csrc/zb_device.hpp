@@ -42,7 +42,11 @@ enum WfIntent : uint8_t {
   WI_ELEMENT_COMPLETED = 9, WI_ELEMENT_TERMINATING = 10, WI_ELEMENT_TERMINATED = 11, WI_CANCEL = 12,
   WI_CANCELING = 13, WI_UPDATE_PAYLOAD = 14, WI_PAYLOAD_UPDATED = 15
 };
-enum JobIntentG : uint8_t { JI_CREATE = 0, JI_CREATED = 1, JI_COMPLETED = 5, JI_CANCEL = 12 };
+enum JobIntentG : uint8_t { JI_CREATE = 0, JI_CREATED = 1, JI_ACTIVATE = 2, JI_ACTIVATED = 3, JI_COMPLETE = 4,
+                           JI_COMPLETED = 5, JI_TIME_OUT = 6, JI_TIMED_OUT = 7, JI_FAIL = 8, JI_FAILED = 9,
+                           JI_UPDATE_RETRIES = 10, JI_RETRIES_UPDATED = 11, JI_CANCEL = 12, JI_CANCELED = 13 };
+// job states of the job stream processor (JobStateController), one byte per job key ordinal ((key - 2) / 5)
+enum JobStateG : uint8_t { JS_NONE = 0, JS_CREATED = 1, JS_ACTIVATED = 2, JS_FAILED = 3, JS_TIMED_OUT = 4 };
 
 // record kind byte: [3:0] value type, [5:4] record type, 6 second record of a batch, 7 KIND_RAW: the value
 // is serialized verbatim from the blob that follows the payload document blob (records submitted through

@@ -219,6 +219,8 @@ struct zb_engine {
   // per-tick race rules of zb_submit (include/zb_engine.h)
   std::unordered_map<int64_t, uint8_t> tick_inst;  // workflow instance -> 1: scope command, 2: other records
   std::unordered_set<int64_t> tick_aik;
+  std::unordered_set<int64_t> tick_jobs;   // job keys with commands in the staged tick (one group each)
+  uint8_t* jstate = nullptr;               // ZB_CFG_JOB_PROCESSOR: JobStateG per job key ordinal [row_capacity]
   DevVec<int64_t> d_lookup_keys, d_lookup_pos;
   // drain buffers (zb_serialize), grown on demand and reused
   uint64_t dr_cap = 0, dr_val_cap = 0, dr_tmp_cap = 0;
@@ -328,7 +330,10 @@ WaveParams wave_params(zb_engine* e) {
   p.partition_count = e->cfg.partition_count;
   p.raux = e->raux;
   p.has_parallel = e->has_parallel ? 1 : 0;
-  p.harness = (e->cfg.flags & ZB_CFG_EXTERNAL_JOBS) ? 0 : 1;
+  p.harness = (e->cfg.flags & (ZB_CFG_EXTERNAL_JOBS | ZB_CFG_JOB_PROCESSOR)) ? 0 : 1;
+  p.jobproc = (e->cfg.flags & ZB_CFG_JOB_PROCESSOR) ? 1 : 0;
+  p.jstate = e->jstate;
+  p.jstate_cap = e->jstate ? e->cfg.row_capacity : 0;
   p.term = e->term ? 1 : 0;
   p.epoch = e->epoch;
   p.need_children = e->need_children;
@@ -666,6 +671,10 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->log, L * sizeof(zb_rec)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->links, L * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->srcd, L * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  // job states: a job belongs to one service-task instance and rows are never reused, so job ordinals stay
+  // below the row capacity
+  if ((e->cfg.flags & ZB_CFG_JOB_PROCESSOR) && hipMalloc(&e->jstate, e->cfg.row_capacity) != hipSuccess)
+    return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->rmeta, e->cfg.row_capacity * sizeof(RowMeta)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->rkeys, e->cfg.row_capacity * sizeof(RowKeys)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->arena, e->cfg.arena_bytes) != hipSuccess) return cleanup(ZB_ENOMEM);
@@ -718,7 +727,7 @@ void zb_engine_destroy(zb_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (auto& x : e->ev)
     if (x) (void)hipEventDestroy(x);
-  void* ps[] = {e->mapres, e->map_ws, e->log, e->links, e->srcd, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
+  void* ps[] = {e->jstate, e->mapres, e->map_ws, e->log, e->links, e->srcd, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
                 e->merge_jobs, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
@@ -766,6 +775,7 @@ int zb_reset(zb_engine* e, int keep_staged) {
   HIPCHECK(e, hipMemsetAsync(e->derr_info, 0xff, sizeof(uint64_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->job_counts, 0, 6 * sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->dstats, 0, 8 * sizeof(uint64_t), e->stream));
+  if (e->jstate) HIPCHECK(e, hipMemsetAsync(e->jstate, 0, e->cfg.row_capacity, e->stream));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
   e->ranges.clear();
   e->cmd_pool.clear();
@@ -780,6 +790,7 @@ int zb_reset(zb_engine* e, int keep_staged) {
     e->staged_has_cancel = false;
     e->tick_inst.clear();
     e->tick_aik.clear();
+    e->tick_jobs.clear();
     e->staged_uploaded = false;
   }
   e->term = false;
@@ -914,6 +925,7 @@ void begin_staging(zb_engine* e) {
   e->staged_has_cancel = false;
   e->tick_inst.clear();
   e->tick_aik.clear();
+  e->tick_jobs.clear();
   e->staged_uploaded = false;
 }
 
@@ -1076,6 +1088,11 @@ struct Decoded {
   int64_t version = -1, workflow_key = -1, wik = -1, aik = -1, scope = -1;
   const uint8_t* payload = nullptr;
   uint32_t payload_len = 0;
+  // JobRecord / JobHeaders (JobRecord.java:35-53, JobHeaders.java:33-51)
+  int64_t deadline = INT64_MIN, retries = -1;
+  std::string worker, type;
+  const uint8_t* custom_headers = nullptr;  // PackedProperty, raw
+  uint32_t custom_headers_len = 0;
 };
 
 bool decode_value(uint8_t vt, const uint8_t* v, size_t n, Decoded& d) {
@@ -1109,8 +1126,27 @@ bool decode_value(uint8_t vt, const uint8_t* v, size_t n, Decoded& d) {
         if (!in.str(hk, hkl)) return false;
         if (in.key_is(hk, hkl, "workflowInstanceKey")) d.wik = in.integer();
         else if (in.key_is(hk, hkl, "activityInstanceKey")) d.aik = in.integer();
-        else in.skip();
+        else if (in.key_is(hk, hkl, "workflowKey")) d.workflow_key = in.integer();
+        else if (in.key_is(hk, hkl, "workflowDefinitionVersion")) d.version = in.integer();
+        else if (in.key_is(hk, hkl, "bpmnProcessId")) {
+          if (!in.str(s, sl)) return false;
+          d.bpmn_process_id.assign((const char*)s, sl);
+        } else if (in.key_is(hk, hkl, "activityId")) {
+          if (!in.str(s, sl)) return false;
+          d.activity_id.assign((const char*)s, sl);
+        } else in.skip();
       }
+    } else if (vt == ZB_VT_JOB && in.key_is(k, kl, "deadline")) d.deadline = in.integer();
+    else if (vt == ZB_VT_JOB && in.key_is(k, kl, "retries")) d.retries = in.integer();
+    else if (vt == ZB_VT_JOB && (in.key_is(k, kl, "worker") || in.key_is(k, kl, "type"))) {
+      const bool w = in.key_is(k, kl, "worker");
+      if (!in.str(s, sl)) return false;
+      (w ? d.worker : d.type).assign((const char*)s, sl);
+    } else if (vt == ZB_VT_JOB && in.key_is(k, kl, "customHeaders")) {
+      const size_t st = in.o;
+      in.skip();
+      d.custom_headers = v + st;
+      d.custom_headers_len = (uint32_t)(in.o - st);
     } else in.skip();
   }
   return in.ok && in.o == n;
@@ -1157,6 +1193,24 @@ std::vector<uint8_t> reencode(uint8_t vt, const Decoded& d, const uint8_t* doc, 
     put_str(b, "activityId"); put_str(b, d.activity_id);
     put_str(b, "payload"); put_bin(b, doc, doc_len);
     put_str(b, "scopeInstanceKey"); put_int(b, d.scope);
+  } else if (vt == ZB_VT_JOB) {  // JobRecord.java:35-53 with JobHeaders.java:33-51
+    b.push_back(0x87);
+    put_str(b, "deadline"); put_int(b, d.deadline);
+    put_str(b, "worker"); put_str(b, d.worker);
+    put_str(b, "retries"); put_int(b, d.retries);
+    put_str(b, "type"); put_str(b, d.type);
+    put_str(b, "headers");
+    b.push_back(0x86);
+    put_str(b, "bpmnProcessId"); put_str(b, d.bpmn_process_id);
+    put_str(b, "workflowDefinitionVersion"); put_int(b, d.version);
+    put_str(b, "workflowKey"); put_int(b, d.workflow_key);
+    put_str(b, "workflowInstanceKey"); put_int(b, d.wik);
+    put_str(b, "activityId"); put_str(b, d.activity_id);
+    put_str(b, "activityInstanceKey"); put_int(b, d.aik);
+    put_str(b, "customHeaders");
+    if (d.custom_headers) b.insert(b.end(), d.custom_headers, d.custom_headers + d.custom_headers_len);
+    else b.push_back(0x80);  // JobRecord.NO_HEADERS
+    put_str(b, "payload"); put_bin(b, doc, doc_len);
   } else {  // WorkflowInstanceSubscriptionRecord.java:26-38
     b.push_back(0x84);
     put_str(b, "workflowInstanceKey"); put_int(b, d.wik);
@@ -1177,7 +1231,7 @@ int zb_submit(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* va
   struct Prep {
     zb_rec d;
     int64_t lookup = INT64_MIN, inst = INT64_MIN, aik = INT64_MIN;
-    bool scope_cmd = false, pair = false, cancel = false, create = false;
+    bool scope_cmd = false, pair = false, cancel = false, create = false, job_cmd = false;
     uint16_t pelem = NO_ELEM;
     std::string pid;
     int64_t wkey = -1;
@@ -1203,7 +1257,11 @@ int zb_submit(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* va
     const bool wf_cmd = vt == ZB_VT_WORKFLOW_INSTANCE && rt == ZB_RT_COMMAND;
     const bool job_ev = vt == ZB_VT_JOB && rt == ZB_RT_EVENT && (it == JI_CREATED || it == JI_COMPLETED);
     const bool corr = vt == ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION && rt == ZB_RT_COMMAND && it == 0;
-    if (!(wf_cmd && (it == WI_CREATE || it == WI_CANCEL || it == WI_UPDATE_PAYLOAD)) && !job_ev && !corr)
+    // the job stream processor's commands (JobInstanceStreamProcessor.java:76-84), with ZB_CFG_JOB_PROCESSOR
+    const bool job_cmd = vt == ZB_VT_JOB && rt == ZB_RT_COMMAND && (e->cfg.flags & ZB_CFG_JOB_PROCESSOR) &&
+                         (it == JI_CREATE || it == JI_ACTIVATE || it == JI_COMPLETE || it == JI_FAIL ||
+                          it == JI_TIME_OUT || it == JI_UPDATE_RETRIES || it == JI_CANCEL);
+    if (!(wf_cmd && (it == WI_CREATE || it == WI_CANCEL || it == WI_UPDATE_PAYLOAD)) && !job_ev && !corr && !job_cmd)
       return fail(e, ZB_EUNSUPPORTED, "record " + std::to_string(i) + ": no workflow processor is registered for "
                                       "(recordType, valueType, intent) = (" + std::to_string(rt) + ", " +
                                       std::to_string(vt) + ", " + std::to_string(it) + ")");
@@ -1237,6 +1295,17 @@ int zb_submit(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* va
       p.inst = p.lookup;
       d.inst_key = dv.wik;
       p.canon = reencode(vt, dv, p.doc, p.doc_len);
+    } else if (job_cmd) {
+      if (it == JI_CREATE && r.key >= 0)
+        return fail(e, ZB_EUNSUPPORTED, "record " + std::to_string(i) + ": JOB CREATE with a key (job keys come from "
+                                        "the partition's job key generator)");
+      p.job_cmd = true;
+      p.lookup = dv.aik;
+      p.inst = dv.wik;
+      d.scope_key = dv.aik;
+      d.inst_key = dv.wik;
+      if (it == JI_UPDATE_RETRIES) d.elem = dv.retries > 0 ? 1 : 0;  // (job_command reads it)
+      p.canon = reencode(vt, dv, p.doc, p.doc_len);
     } else if (job_ev) {
       p.lookup = dv.aik;
       p.inst = dv.wik;
@@ -1254,9 +1323,10 @@ int zb_submit(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* va
     }
   }
   // 2. race rules of one tick (include/zb_engine.h), against what is staged already
-  if (!e->staged_pending) { e->tick_inst.clear(); e->tick_aik.clear(); }
+  if (!e->staged_pending) { e->tick_inst.clear(); e->tick_aik.clear(); e->tick_jobs.clear(); }
   std::unordered_map<int64_t, uint8_t> inst = e->staged_pending ? e->tick_inst : std::unordered_map<int64_t, uint8_t>();
   std::unordered_set<int64_t> aiks = e->staged_pending ? e->tick_aik : std::unordered_set<int64_t>();
+  std::unordered_set<int64_t> tick_jobs = e->staged_pending ? e->tick_jobs : std::unordered_set<int64_t>();
   const zb_rec* prev_staged = (e->staged_pending && !e->staged.empty()) ? &e->staged.back() : nullptr;
   for (size_t i = 0; i < n; i++) {
     Prep& p = prep[i];
@@ -1268,6 +1338,24 @@ int zb_submit(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* va
       p.pair = true;
       p.d.kind |= 0x40;
       continue;
+    }
+    // a job's commands of one tick: consecutive ones form one group, processed in order by one thread
+    if (p.job_cmd) {
+      if (prev && kind_vt(prev->kind) == ZB_VT_JOB && kind_rt(prev->kind) == ZB_RT_COMMAND && prev->key == p.d.key &&
+          p.d.key >= 0) {
+        // a group's records share one thread's MAX_SLOTS (2) output slots, one per job command: two commands
+        // for a job per tick
+        const bool second = !(prev->kind & 0x40);
+        if (!second)
+          return fail(e, ZB_EUNSUPPORTED, "record " + std::to_string(i) + ": more than 2 commands for job " +
+                                              std::to_string(p.d.key) + " in one tick (split the tick)");
+        p.d.kind |= 0x40;
+        continue;
+      }
+      if (p.d.key >= 0 && !tick_jobs.insert(p.d.key).second)
+        return fail(e, ZB_EUNSUPPORTED, "record " + std::to_string(i) + ": job " + std::to_string(p.d.key) +
+                                            " already has commands in this tick that are not next to this one "
+                                            "(submit a job's commands together, or split the tick)");
     }
     uint8_t& f = inst[p.inst];
     if ((f & 1) || (p.scope_cmd && f)) {
@@ -1288,6 +1376,7 @@ int zb_submit(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* va
   e->staged_uploaded = false;
   e->tick_inst.swap(inst);
   e->tick_aik.swap(aiks);
+  e->tick_jobs.swap(tick_jobs);
   for (size_t i = 0; i < n; i++) {
     Prep& p = prep[i];
     // arena: [payload document][verbatim value] (+ [document][re-encoded command value])
@@ -1336,7 +1425,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
                                 "step it to quiescence first");
     // an idle partition fed only CREATE commands runs as independent trajectories (zb_traj.hip) -- with the
     // canonical job harness and no parallel gateways (the general wave pipeline covers everything else)
-    try_traj = !(e->cfg.flags & (ZB_CFG_WAVE_ONLY | ZB_CFG_EXTERNAL_JOBS)) && max_waves == 0 &&
+    try_traj = !(e->cfg.flags & (ZB_CFG_WAVE_ONLY | ZB_CFG_EXTERNAL_JOBS | ZB_CFG_JOB_PROCESSOR)) && max_waves == 0 &&
                e->staged_only_creates && !e->has_parallel && !e->has_io &&
                (e->traj_model_ok || (e->cls_ok && e->staged_uniform)) &&
                e->host_hdr.begin == e->host_hdr.end;
@@ -2157,6 +2246,7 @@ struct SnapHead {
   uint64_t sub_count, msg_count, store_cap, head_mask;
   uint64_t rows, arena_bytes;
   uint64_t ranges, cmd_pool;
+  uint64_t jobs;          // job states (ZB_CFG_JOB_PROCESSOR: JobStateController), one byte per job key ordinal
 };
 
 uint64_t model_hash(const zb_engine* e) {  // FNV-1a over the deployed tables
@@ -2195,10 +2285,11 @@ int zb_snapshot(zb_engine* e, uint8_t* buf, size_t cap, size_t* len) {
   h.arena_bytes = (uint64_t)e->host_hdr.arena_next;
   h.ranges = e->ranges.size();
   h.cmd_pool = e->cmd_pool.size();
+  h.jobs = e->jstate ? (uint64_t)std::max<int64_t>(0, (e->host_hdr.job_next - 2) / 5) : 0;
   const uint64_t heads = h.store_cap ? h.head_mask + 1 : 0;
   const size_t need = sizeof(h) + h.rows * (sizeof(RowMeta) + sizeof(RowKeys) + sizeof(RowAux)) + h.arena_bytes +
                       h.ranges * sizeof(CmdRange) + h.cmd_pool +
-                      (h.store_cap ? h.store_cap * (sizeof(SubEntry) + sizeof(MsgEntry) + 8) + heads * 8 : 0);
+                      (h.store_cap ? h.store_cap * (sizeof(SubEntry) + sizeof(MsgEntry) + 8) + heads * 8 : 0) + h.jobs;
   *len = need;
   if (!buf || cap < need) return ZB_ENOMEM;
   uint8_t* o = buf;
@@ -2219,6 +2310,7 @@ int zb_snapshot(zb_engine* e, uint8_t* buf, size_t cap, size_t* len) {
          get(e->sub_head, heads * 4) && get(e->msg_head, heads * 4);
     if (!ok) return fail(e, ZB_EDEVICE, "snapshot copy (message stores)");
   }
+  if (h.jobs && !get(e->jstate, h.jobs)) return fail(e, ZB_EDEVICE, "snapshot copy (job states)");
   return ZB_OK;
 }
 
@@ -2234,8 +2326,10 @@ int zb_restore(zb_engine* e, const uint8_t* buf, size_t len) {
   const uint64_t heads = h.store_cap ? h.head_mask + 1 : 0;
   const size_t need = sizeof(h) + h.rows * (sizeof(RowMeta) + sizeof(RowKeys) + sizeof(RowAux)) + h.arena_bytes +
                       h.ranges * sizeof(CmdRange) + h.cmd_pool +
-                      (h.store_cap ? h.store_cap * (sizeof(SubEntry) + sizeof(MsgEntry) + 8) + heads * 8 : 0);
+                      (h.store_cap ? h.store_cap * (sizeof(SubEntry) + sizeof(MsgEntry) + 8) + heads * 8 : 0) + h.jobs;
   if (len < need) return fail(e, ZB_EINVAL, "truncated snapshot");
+  if (h.jobs && (!e->jstate || h.jobs > e->cfg.row_capacity))
+    return fail(e, ZB_EINVAL, "snapshot holds job states: restore into an engine with ZB_CFG_JOB_PROCESSOR");
   int rc = zb_reset(e, 0);
   if (rc != ZB_OK) return rc;
   if (h.store_cap) {
@@ -2261,6 +2355,7 @@ int zb_restore(zb_engine* e, const uint8_t* buf, size_t len) {
          put(e->sub_head, heads * 4) && put(e->msg_head, heads * 4);
     if (!ok) return fail(e, ZB_EDEVICE, "restore copy (message stores)");
   }
+  if (h.jobs && !put(e->jstate, h.jobs)) return fail(e, ZB_EDEVICE, "restore copy (job states)");
   e->host_hdr = h.hdr;
   e->host_hdr.begin = e->host_hdr.gen_end = e->host_hdr.end;
   e->log_floor = e->host_hdr.end;  // the log itself lives in the logstream, not in the snapshot

@@ -176,7 +176,7 @@ __device__ inline void encode_value(const SerParams& P, int64_t pos, const zb_re
     w.key("activityId"); w.str(P.pool + e.id_off, e.id_len);
     w.key("payload"); w.bin(pl, plen);
     w.key("scopeInstanceKey"); w.integer(d.scope_key);
-  } else if (vt == ZB_VT_JOB && d.intent == JI_CANCEL) {
+  } else if (vt == ZB_VT_JOB && (d.intent == JI_CANCEL || d.intent == JI_CANCELED)) {
     // TerminateServiceTaskHandler :37-58: a reset JobRecord with type "", headers without workflowKey
     const DevElem& e = P.elems[d.elem];
     const DevWorkflow& wf = P.wfs[e.wf];
@@ -286,6 +286,18 @@ __device__ __forceinline__ uint32_t value_size(const SerParams& P, int64_t pos, 
   return w.n;
 }
 
+// RejectionType: CREATE of an unknown workflow -> BAD_VALUE (0); CORRELATE of an absent activity, CANCEL /
+// UPDATE_PAYLOAD of an instance that is not running -> NOT_APPLICABLE (1) (WorkflowInstanceStreamProcessor.java
+// :477-479, :524-529, :571-573); job commands NOT_APPLICABLE but UPDATE_RETRIES with retries <= 0 BAD_VALUE
+// (JobInstanceStreamProcessor.java:206-222; job_command keeps it in elem)
+__device__ __forceinline__ uint8_t rejection_type(const zb_rec& d) {
+  if (kind_rt(d.kind) != ZB_RT_COMMAND_REJECTION) return 255;
+  const uint8_t vt = kind_vt(d.kind);
+  if (vt == ZB_VT_WORKFLOW_INSTANCE && d.intent == WI_CREATE) return 0;
+  if (vt == ZB_VT_JOB && d.intent == JI_UPDATE_RETRIES && (d.kind & KIND_RAW) && d.elem == 1) return 0;
+  return 1;
+}
+
 // ------------------------------------------------------------------------------ log frames (§8f rank 1)
 // A record as LogStreamBatchWriterImpl.writeEventsToBuffer (:222-268) / LogStreamWriterImpl lay it into the
 // dispatcher buffer: DataFrameDescriptor header (DataFrameDescriptor.java:53-96: framed length, version 0,
@@ -298,13 +310,29 @@ constexpr uint32_t FRAME_PREFIX = 12 + 48 + 8 + 34 + 2;
 
 // rejection reasons of the commands this path rejects (WorkflowInstanceStreamProcessor.java:346-347, :527-529,
 // :573, :478-479)
+// and of the job commands (JobInstanceStreamProcessor.java:155-158, :172-173, :186-187, :193, :215-220, :238)
+__device__ const char* const REASONS[11] = {
+    "", "Workflow is not deployed", "Workflow instance is not running", "activity is not active anymore",
+    "Job is not in one of these states: CREATED, FAILED, TIMED_OUT", "Job is not in state: ACTIVATED, TIMED_OUT",
+    "Job is not in state ACTIVATED", "Retries must be greater than 0", "Job is not in state FAILED",
+    "Job does not exist", ""};
 __device__ __forceinline__ uint32_t reason_of(const zb_rec& d) {
   if (kind_rt(d.kind) != ZB_RT_COMMAND_REJECTION) return 0;
   const uint8_t vt = kind_vt(d.kind);
   if (vt == ZB_VT_WORKFLOW_INSTANCE) return d.intent == WI_CREATE ? 1 : 2;
-  return vt == ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION ? 3 : 0;
+  if (vt == ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION) return 3;
+  if (vt == ZB_VT_JOB) {
+    switch (d.intent) {
+      case JI_ACTIVATE: return 4;
+      case JI_COMPLETE: return 5;
+      case JI_FAIL: case JI_TIME_OUT: return 6;
+      case JI_UPDATE_RETRIES: return rejection_type(d) == 0 ? 7 : 8;
+      case JI_CANCEL: return 9;
+    }
+  }
+  return 0;
 }
-__device__ __forceinline__ uint32_t reason_len(uint32_t r) { return r == 1 ? 24 : r == 2 ? 32 : r == 3 ? 30 : 0; }
+__device__ __forceinline__ uint32_t reason_len(uint32_t r) { return dstrlen(REASONS[r < 11 ? r : 0]); }
 
 __device__ __forceinline__ const ReqMeta* find_req(const SerParams& P, int64_t pos) {
   int64_t lo = 0, hi = P.nreqs - 1;
@@ -345,7 +373,7 @@ __device__ inline uint32_t encode_frame(const SerParams& P, int64_t pos, const z
   // TypedStreamProcessor producer ids (StreamProcessorIds.java:23-39): harness job events 10 (the job
   // processor), message partition records 90, everything else the workflow instance processor 70; records
   // other writers appended keep the writer's default -1
-  const int32_t producer = src < 0 ? -1 : (vt == ZB_VT_JOB && rt == ZB_RT_EVENT) ? 10
+  const int32_t producer = src < 0 ? -1 : (vt == ZB_VT_JOB && rt != ZB_RT_COMMAND) ? 10
                          : (vt == ZB_VT_MESSAGE || vt == ZB_VT_MESSAGE_SUBSCRIPTION) ? 90 : 70;
   uint64_t rid = ~0ull;
   uint32_t sid = 0x80000000u;
@@ -360,8 +388,7 @@ __device__ inline uint32_t encode_frame(const SerParams& P, int64_t pos, const z
       if (m) { rid = m->request_id; sid = (uint32_t)m->request_stream_id; }
     }
   }
-  const uint64_t rej = rt == ZB_RT_COMMAND_REJECTION
-                           ? ((vt == ZB_VT_WORKFLOW_INSTANCE && d.intent == WI_CREATE) ? 0 : 1) : 255;
+  const uint64_t rej = rejection_type(d);
   const uint64_t mlen = 8 + 34 + 2 + rlen;
   uint64_t* h = (uint64_t*)dst;
   h[0] = (uint64_t)framed | (uint64_t)flags << 40;                          // length, version 0, flags, type 0
@@ -380,9 +407,7 @@ __device__ inline uint32_t encode_frame(const SerParams& P, int64_t pos, const z
   W r;
   r.dst = dst + FRAME_PREFIX;
   r.n = 0;
-  if (rs == 1) r.cstr("Workflow is not deployed");
-  else if (rs == 2) r.cstr("Workflow instance is not running");
-  else if (rs == 3) r.cstr("activity is not active anymore");
+  if (rs) r.cstr(REASONS[rs < 11 ? rs : 0]);
   for (uint32_t k = framed; k < fsize; k++) dst[k] = 0;
   return fsize;
 }
@@ -416,11 +441,7 @@ __device__ __forceinline__ zb_record_header record_header(const zb_rec& d, int64
   h.record_type = kind_rt(d.kind);
   h.value_type = kind_vt(d.kind);
   h.intent = d.intent;
-  // RejectionType: CREATE of an unknown workflow -> BAD_VALUE (0); CORRELATE of an absent activity, CANCEL /
-  // UPDATE_PAYLOAD of an instance that is not running -> NOT_APPLICABLE (1) (WorkflowInstanceStreamProcessor.java
-  // :477-479, :524-529, :571-573)
-  h.rejection_type = kind_rt(d.kind) == ZB_RT_COMMAND_REJECTION
-                         ? ((kind_vt(d.kind) == ZB_VT_WORKFLOW_INSTANCE && d.intent == WI_CREATE) ? 0 : 1) : 255;
+  h.rejection_type = rejection_type(d);
   h.value_length = len;
   h.value_offset = off;
   return h;

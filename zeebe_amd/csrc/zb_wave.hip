@@ -445,6 +445,69 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
   }
 }
 
+// ---- the job stream processor (ZB_CFG_JOB_PROCESSOR): JobInstanceStreamProcessor.java:98-242 through
+// CommandProcessorImpl (accept -> follow-up event with the command's value, a new key for a null command key;
+// reject -> the command's value with its rejection). Job states live in P.jstate by key ordinal; all commands
+// for one job in a tick arrive as one group (zb_submit), so the owning thread is the only one touching it.
+__device__ __forceinline__ int64_t job_ordinal(const WaveParams& P, int64_t key) {
+  if (key < 2 || (key - 2) % 5 != 0) return -1;
+  const int64_t j = (key - 2) / 5;
+  return (uint64_t)j < P.jstate_cap && key < P.hdr[P.wave & 1].job_next ? j : -1;
+}
+
+__device__ void job_command(const WaveParams& P, const zb_rec& rec, uint32_t rself, uint32_t rscope, TState& t) {
+  const uint8_t raw = rec.kind & KIND_RAW;
+  Slot& s = add_slot(t);
+  s.d = rec;
+  if (raw) s.d.payload = derived_ref(P.arena, rec.payload);  // the command's value, as the reference re-encodes it
+  s.rself = rself; s.rscope = rscope;  // (JOB events find the element instance through the activity key)
+  if (rec.intent == JI_CREATE) {  // CreateJobProcessor :98-106 (a null key: the job key generator's next)
+    s.d.intent = JI_CREATED;
+    s.d.kind = make_kind(ZB_VT_JOB, ZB_RT_EVENT, t.ns > 1) | raw;
+    s.flags = SF_KEY_JOB;  // k_emit assigns the key and marks the job CREATED
+    s.ord = (uint8_t)t.njob++;
+    return;
+  }
+  const int64_t j = job_ordinal(P, rec.key);
+  const uint8_t st = j >= 0 ? P.jstate[j] : JS_NONE;
+  uint8_t ev = 0xff, next = st;
+  bool bad_value = false;
+  switch (rec.intent) {
+    case JI_ACTIVATE:  // ActivateJobProcessor :108-160
+      if (st == JS_CREATED || st == JS_FAILED || st == JS_TIMED_OUT) { ev = JI_ACTIVATED; next = JS_ACTIVATED; }
+      break;
+    case JI_COMPLETE:  // CompleteJobProcessor :162-175 (the state is deleted)
+      if (st == JS_ACTIVATED || st == JS_TIMED_OUT) { ev = JI_COMPLETED; next = JS_NONE; }
+      break;
+    case JI_FAIL:      // FailJobProcessor :177-189
+      if (st == JS_ACTIVATED) { ev = JI_FAILED; next = JS_FAILED; }
+      break;
+    case JI_TIME_OUT:  // TimeOutJobProcessor :191-204
+      if (st == JS_ACTIVATED) { ev = JI_TIMED_OUT; next = JS_TIMED_OUT; }
+      break;
+    case JI_UPDATE_RETRIES:  // UpdateRetriesJobProcessor :206-222 (zb_submit: elem = value.retries > 0)
+      if (st == JS_FAILED) {
+        if (rec.elem == 1) ev = JI_RETRIES_UPDATED;
+        else bad_value = true;
+      }
+      break;
+    case JI_CANCEL:    // CancelJobProcessor :224-240
+      if (st != JS_NONE) { ev = JI_CANCELED; next = JS_NONE; }
+      break;
+    default:  // no processor for this command
+      t.ns--;
+      return;
+  }
+  if (ev == 0xff) {  // reject: the reason follows the intent (and BAD_VALUE, kept in elem, for UPDATE_RETRIES)
+    s.d.kind = make_kind(ZB_VT_JOB, ZB_RT_COMMAND_REJECTION, t.ns > 1) | raw;
+    if (raw) s.d.elem = bad_value ? 1 : 0;
+    return;
+  }
+  s.d.intent = ev;
+  s.d.kind = make_kind(ZB_VT_JOB, ZB_RT_EVENT, t.ns > 1) | raw;
+  if (j >= 0 && next != st) P.jstate[j] = next;
+}
+
 __device__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t pos, uint32_t rself,
                                uint32_t rscope, TState& t) {
   const uint8_t vt = kind_vt(rec.kind), rt = kind_rt(rec.kind);
@@ -524,7 +587,9 @@ __device__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t p
       }
     }
   } else if (vt == ZB_VT_JOB) {
-    if (rt == ZB_RT_COMMAND && rec.intent == JI_CREATE) {
+    if (rt == ZB_RT_COMMAND && P.jobproc) {
+      job_command(P, rec, rself, rscope, t);
+    } else if (rt == ZB_RT_COMMAND && rec.intent == JI_CREATE) {
       if (!P.harness) return;  // the job stream processor answers from outside (zb_submit)
       // canonical harness: JOB CREATED(k), JOB COMPLETED(k), k from the job key generator
       const uint8_t ord = (uint8_t)t.njob++;
@@ -995,7 +1060,15 @@ __device__ __forceinline__ void emit_item(const WaveParams& P, const Chunk& c, i
   for (int k = 0; k < ns; k++) {
     Slot s = sl[k];
     if (s.flags & SF_KEY_WF) s.d.key = wf_next + 5 * (int64_t)(wf0 + s.ord);
-    if (s.flags & SF_KEY_JOB) s.d.key = job_next + 5 * (int64_t)(job0 + s.ord);
+    if (s.flags & SF_KEY_JOB) {
+      s.d.key = job_next + 5 * (int64_t)(job0 + s.ord);
+      // the job stream processor's CREATED: the job exists from here on (JobStateController.putJobState)
+      if (P.jobproc && s.d.intent == JI_CREATED) {
+        const uint64_t j = (uint64_t)(s.d.key - 2) / 5;
+        if (j < P.jstate_cap) P.jstate[j] = JS_CREATED;
+        else err |= DE_ROWS_FULL;
+      }
+    }
     if (s.flags & SF_INST_WF) s.d.inst_key = wf_next + 5 * (int64_t)(wf0 + s.ord);
     if (s.flags & SF_PAY_MERGED) s.d.payload = merged_ref;
     if (s.flags & SF_PAY_DETAIL) s.d.payload = detail_ref;

@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(_HERE, "libzbgpu.so")
 
 CFG_WAVE_ONLY = 1  # zb_config.flags: never take the trajectory path
 CFG_EXTERNAL_JOBS = 2  # zb_config.flags: no canonical job harness (job events come through zb_submit)
+CFG_JOB_PROCESSOR = 4  # zb_config.flags: the job stream processor runs on the GPU (job commands through zb_submit)
 
 ZB_OK, ZB_EINVAL, ZB_ENOMEM, ZB_EUNSUPPORTED, ZB_EDEPLOY, ZB_EDEVICE, ZB_EAGAIN, ZB_EPROCESSING = \
     0, -1, -2, -3, -4, -5, -6, -7
@@ -172,14 +173,18 @@ class Engine:
 
     def __init__(self, device: int = 0, partition_id: int = 0, partition_count: int = 1,
                  log_capacity: int = 1 << 22, row_capacity: int = 1 << 20, arena_bytes: int = 64 << 20,
-                 wave_records: int = 0, wave_only: bool = False, external_jobs: bool = False):
+                 wave_records: int = 0, wave_only: bool = False, external_jobs: bool = False,
+                 job_processor: bool = False):
         self._L = lib()
-        flags = (CFG_WAVE_ONLY if wave_only else 0) | (CFG_EXTERNAL_JOBS if external_jobs else 0)
+        flags = (CFG_WAVE_ONLY if wave_only else 0) | (CFG_EXTERNAL_JOBS if external_jobs else 0) | \
+            (CFG_JOB_PROCESSOR if job_processor else 0)
+        external_jobs = external_jobs or job_processor
         cfg = zb_config(device, partition_id, partition_count, flags, log_capacity, row_capacity, arena_bytes,
                         wave_records)
         h = ctypes.c_void_p()
         self._device, self._parts = device, partition_count
         self._external = external_jobs
+        self._flags = flags
         rc = self._L.zb_engine_create(ctypes.byref(cfg), ctypes.byref(h))
         if rc != ZB_OK:
             raise ZbError(rc, "zb_engine_create failed")
@@ -242,6 +247,11 @@ class Engine:
             blob += value
         buf = ctypes.create_string_buffer(bytes(blob), max(len(blob), 1))
         self._check(self._L.zb_submit(self._h, arr, n, buf, len(blob)))
+
+    def set_job_processor(self, on: bool):
+        """The job stream processor is fixed at creation (job_processor=...): only checks it matches."""
+        if bool(on) != bool(self._flags & CFG_JOB_PROCESSOR):
+            raise ValueError("the job stream processor is chosen at engine creation (job_processor)")
 
     def set_harness(self, on: bool):
         """The job harness is fixed at creation (external_jobs=...): only checks it matches."""
