@@ -81,6 +81,7 @@ struct zb_engine {
   uint64_t* mapres = nullptr;   // k_map outcomes [wave_cap + 8]
   MNode* map_ws = nullptr;      // k_map tree workspaces
   int ser_mode = 0;              // ZB_SER_MODE: 0 = two passes (size, scan, write), 1 = single pass (look-back)
+  int ser_nt = 0;                // ZB_SER_NT=1: non-temporal stores in the drain write pass
 
   // device state
   zb_rec* log = nullptr;
@@ -636,6 +637,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   auto* e = new zb_engine();
   e->cfg = *cfg;
   if (const char* m = std::getenv("ZB_SER_MODE")) e->ser_mode = std::strcmp(m, "fused") == 0 ? 1 : 0;
+  if (const char* m = std::getenv("ZB_SER_NT")) e->ser_nt = atoi(m);
   if (const char* g = std::getenv("ZB_WAVE_GRID")) e->wave_grid_fixed = std::max(0, std::min(atoi(g), (int)WAVE_GRID_MAX));
   if (e->cfg.log_capacity == 0) e->cfg.log_capacity = 1ull << 22;
   if (e->cfg.row_capacity == 0) e->cfg.row_capacity = 1ull << 20;
@@ -1653,6 +1655,7 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
   HIPCHECK(e, e->d_cmd_pool.upload(e->cmd_pool, e->stream));
   if (fc && !e->reqs.empty()) HIPCHECK(e, e->d_reqs.upload(e->reqs, e->stream));
   SerParams sp{};
+  sp.nt = e->ser_nt;
   if (fc) {
     sp.frames = 1;
     sp.stream_id = fc->stream_id;

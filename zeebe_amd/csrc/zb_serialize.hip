@@ -136,7 +136,7 @@ __device__ inline const CmdRange* find_range(const SerParams& P, int64_t pos) {
   return nullptr;
 }
 
-__device__ inline void encode_value(const SerParams& P, int64_t pos, const zb_rec& d, W& w) {
+__device__ __forceinline__ void encode_value(const SerParams& P, int64_t pos, const zb_rec& d, W& w) {
   const uint8_t vt = kind_vt(d.kind), rt = kind_rt(d.kind);
   if (d.kind & KIND_RAW) {  // zb_submit: the value as written, or the command value as the reference re-encodes it
     const uint8_t* doc = P.arena + (uint64_t)d.payload * 8;
@@ -176,7 +176,7 @@ __device__ inline void encode_value(const SerParams& P, int64_t pos, const zb_re
     w.key("activityId"); w.str(P.pool + e.id_off, e.id_len);
     w.key("payload"); w.bin(pl, plen);
     w.key("scopeInstanceKey"); w.integer(d.scope_key);
-  } else if (vt == ZB_VT_JOB && (d.intent == JI_CANCEL || d.intent == JI_CANCELED)) {
+  } else if (vt == ZB_VT_JOB && (d.intent | 1) == JI_CANCELED) {  // CANCEL (12) or CANCELED (13)
     // TerminateServiceTaskHandler :37-58: a reset JobRecord with type "", headers without workflowKey
     const DevElem& e = P.elems[d.elem];
     const DevWorkflow& wf = P.wfs[e.wf];
@@ -449,12 +449,23 @@ __device__ __forceinline__ zb_record_header record_header(const zb_rec& d, int64
 
 // streams image bytes [shift, shift + n) to out[o .. o + n) with 16-byte stores aligned to the destination
 // (out + o - shift is 16-byte aligned)
-__device__ __forceinline__ void stream_image(const uint8_t* img, uint8_t* out, uint64_t o, uint32_t shift, uint64_t n) {
+__device__ __forceinline__ void stream_image(const uint8_t* img, uint8_t* out, uint64_t o, uint32_t shift, uint64_t n,
+                                             bool nt) {
   uint8_t* dst = out + o - shift;
   const uint64_t lim = shift + n;  // image bytes [shift, lim) are ours
   const uint64_t full_lo = (shift + 15) & ~15ull, full_hi = lim & ~15ull;
-  for (uint64_t c = full_lo + 16 * threadIdx.x; c < full_hi; c += 16 * SER_WG)
-    *(uint4*)(dst + c) = *(const uint4*)(img + c);
+  if (nt) {
+    for (uint64_t c = full_lo + 16 * threadIdx.x; c < full_hi; c += 16 * SER_WG) {
+      const uint4 v = *(const uint4*)(img + c);
+      __builtin_nontemporal_store(v.x, (uint32_t*)(dst + c));
+      __builtin_nontemporal_store(v.y, (uint32_t*)(dst + c) + 1);
+      __builtin_nontemporal_store(v.z, (uint32_t*)(dst + c) + 2);
+      __builtin_nontemporal_store(v.w, (uint32_t*)(dst + c) + 3);
+    }
+  } else {
+    for (uint64_t c = full_lo + 16 * threadIdx.x; c < full_hi; c += 16 * SER_WG)
+      *(uint4*)(dst + c) = *(const uint4*)(img + c);
+  }
   const uint64_t head_end = full_lo < lim ? full_lo : lim;
   for (uint64_t c = shift + threadIdx.x; c < head_end; c += SER_WG) dst[c] = img[c];
   const uint64_t tail_lo = full_hi > head_end ? full_hi : head_end;
@@ -520,7 +531,16 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
   const int64_t pos = P.start + i;
   if (live) {
     if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay = *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
-    if (!FRAMES) P.headers[i] = record_header(d, pos, len, off);
+    if (!FRAMES) {
+      const zb_record_header h = record_header(d, pos, len, off);
+      if (P.nt) {
+        const uint64_t* hw = (const uint64_t*)&h;
+        uint64_t* dw = (uint64_t*)(P.headers + i);
+        for (int k = 0; k < 5; k++) __builtin_nontemporal_store(hw[k], dw + k);
+      } else {
+        P.headers[i] = h;
+      }
+    }
   }
   if (P.totals) {
     unsigned long long y = pay;
@@ -565,7 +585,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
     }
     if (staged || nwin) {
       __syncthreads();
-      stream_image(img, P.out, wlo, sh, whi - wlo);
+      stream_image(img, P.out, wlo, sh, whi - wlo, P.nt != 0);
       __syncthreads();  // the image is reused by the next window
     }
   }
