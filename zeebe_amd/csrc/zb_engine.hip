@@ -81,7 +81,7 @@ struct zb_engine {
   uint64_t* mapres = nullptr;   // k_map outcomes [wave_cap + 8]
   MNode* map_ws = nullptr;      // k_map tree workspaces
   int ser_mode = 0;              // ZB_SER_MODE: 0 = two passes (size, scan, write), 1 = single pass (look-back)
-  int ser_nt = 0;                // ZB_SER_NT=1: non-temporal stores in the drain write pass
+  int ser_nt = 1;                // ZB_SER_NT=0: plain (not non-temporal) stores in the drain write pass
 
   // device state
   zb_rec* log = nullptr;

@@ -479,7 +479,7 @@ __device__ __forceinline__ void stream_image(const uint8_t* img, uint8_t* out, u
 // encoded and streamed one after another (large values, e.g. C2's job records: 64 KB per tile). The phase loop
 // lets the compiler spend 255 VGPRs unless told the LDS-bound occupancy (3 workgroups per CU): 168, no spills.
 constexpr int SER_WINDOWS = 16;
-template <bool FRAMES>
+template <bool FRAMES, bool NT>
 __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 3))) k_ser_write(SerParams P0) {
   __shared__ __attribute__((aligned(16))) uint8_t img[SER_IMG + 16];
   __shared__ __attribute__((aligned(16))) uint8_t s_model[SER_MODEL_LDS];
@@ -533,7 +533,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
     if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay = *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
     if (!FRAMES) {
       const zb_record_header h = record_header(d, pos, len, off);
-      if (P.nt) {
+      if (NT) {
         const uint64_t* hw = (const uint64_t*)&h;
         uint64_t* dw = (uint64_t*)(P.headers + i);
         for (int k = 0; k < 5; k++) __builtin_nontemporal_store(hw[k], dw + k);
@@ -585,7 +585,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
     }
     if (staged || nwin) {
       __syncthreads();
-      stream_image(img, P.out, wlo, sh, whi - wlo, P.nt != 0);
+      stream_image(img, P.out, wlo, sh, whi - wlo, NT);
       __syncthreads();  // the image is reused by the next window
     }
   }
@@ -748,8 +748,9 @@ void launch_ser_size(const SerParams& p, hipStream_t s) {
 void launch_ser_write(const SerParams& p, hipStream_t s) {
   if (p.count <= 0) return;
   const int64_t tiles = (p.count + SER_WG - 1) / SER_WG;
-  if (p.frames) hipLaunchKernelGGL(k_ser_write<true>, dim3((unsigned)tiles), dim3(SER_WG), 0, s, p);
-  else hipLaunchKernelGGL(k_ser_write<false>, dim3((unsigned)tiles), dim3(SER_WG), 0, s, p);
+  if (p.frames) hipLaunchKernelGGL((k_ser_write<true, true>), dim3((unsigned)tiles), dim3(SER_WG), 0, s, p);
+  else if (p.nt) hipLaunchKernelGGL((k_ser_write<false, true>), dim3((unsigned)tiles), dim3(SER_WG), 0, s, p);
+  else hipLaunchKernelGGL((k_ser_write<false, false>), dim3((unsigned)tiles), dim3(SER_WG), 0, s, p);
   if (p.totals) hipLaunchKernelGGL(k_ser_sum, dim3(1), dim3(1024), 0, s, p, tiles);
 }
 
