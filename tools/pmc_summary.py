@@ -7,8 +7,9 @@ Per kernel (averaged over its dispatches) every counter of every pass, plus deri
   valu_busy        SQ_ACTIVE_INST_VALU * 4 / (#SIMD = 4 * 256 CUs) / kernel_cycles (gfx94x formula)
   valu_lane_util   SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU): mean active lanes of a VALU
                    instruction (1.0 = no divergence)
-  mean_waves_cu    SQ_WAVE_CYCLES / kernel_cycles / 256 CUs: resident waves per CU averaged over the kernel
-                   (of 32; occupancy = mean_waves_cu / 32). SQ_ACCUM_PREV_HIRES reads 0 on gfx950 / ROCm 7.2.
+  mean_waves_cu    4 * SQ_WAVE_CYCLES / kernel_cycles / 256 CUs: resident waves per CU averaged over the
+                   kernel (SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles, MI355X_MICROARCH.md;
+                   of 32; occupancy = mean_waves_cu / 32). SQ_ACCUM_PREV_HIRES reads 0 on gfx950 / ROCm 7.2.
   wait_frac        SQ_WAIT_ANY / SQ_WAVE_CYCLES (waves parked on s_waitcnt / barriers)
   lds_conflict     SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
 
@@ -69,7 +70,7 @@ def main():
         if cyc and "SQ_ACTIVE_INST_VALU" in c:
             d["valu_busy"] = c["SQ_ACTIVE_INST_VALU"] * 4 / (4 * CUS) / cyc
         if cyc and "SQ_WAVE_CYCLES" in c:
-            d["mean_waves_cu"] = c["SQ_WAVE_CYCLES"] / cyc / CUS
+            d["mean_waves_cu"] = 4 * c["SQ_WAVE_CYCLES"] / cyc / CUS  # quad-cycles
             d["occupancy"] = d["mean_waves_cu"] / 32.0
         if c.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in c:
             d["valu_lane_util"] = c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"])
@@ -78,7 +79,7 @@ def main():
         if c.get("SQ_LDS_IDX_ACTIVE") and "SQ_LDS_BANK_CONFLICT" in c:
             d["lds_conflict"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]
         out[k] = d
-    res = {"source": src, "passes": sets,
+    res = {"source": src, "passes": sets, "occupancy_units": "quad-cycle corrected",
            "correction": "FETCH_SIZE doubled (gfx950 tallies 128-B requests at 64 B); WRITE_SIZE as reported",
            "kernels": out}
     os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
@@ -89,5 +90,24 @@ def main():
                                                      "wait_frac", "lds_conflict", "kernel_cycles", "dispatches") if x in d})
 
 
+def rederive(path):
+    """Recompute mean_waves_cu / occupancy of a summary written before the quad-cycle correction."""
+    with open(path) as f:
+        res = json.load(f)
+    if res.get("occupancy_units") == "quad-cycle corrected":
+        return
+    for d in res["kernels"].values():
+        if d.get("kernel_cycles") and "SQ_WAVE_CYCLES" in d:
+            d["mean_waves_cu"] = 4 * d["SQ_WAVE_CYCLES"] / d["kernel_cycles"] / CUS
+            d["occupancy"] = d["mean_waves_cu"] / 32.0
+    res["occupancy_units"] = "quad-cycle corrected"
+    with open(path, "w") as f:
+        json.dump(res, f, indent=1)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1] == "--rederive":
+        for p in sys.argv[2:]:
+            rederive(p)
+    else:
+        main()
