@@ -4,6 +4,8 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# GPU tests: the drain's size pass checks every value length an emitting kernel supplied against the encoder
+os.environ.setdefault("ZB_VLEN_CHECK", "1")
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 

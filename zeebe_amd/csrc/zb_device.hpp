@@ -121,6 +121,26 @@ struct DevQuery {             // 16 bytes
   uint32_t pad;
 };
 
+// ---- value lengths (msgpack sizes of MsgPackWriter.writeInteger / writeString / writeBinary) ----
+// The emit kernels that know a record's payload length write the length of its serialized value (vlen),
+// so that the drain's size pass does not re-read every payload from HBM (VLEN_UNKNOWN: the size pass
+// encodes the value to measure it).
+constexpr uint32_t VLEN_UNKNOWN = 0xffffffffu;
+__host__ __device__ inline uint32_t mp_int_len(int64_t v) {
+  if (v < -(1LL << 5)) return v < -(1LL << 15) ? (v < -(1LL << 31) ? 9 : 5) : (v < -(1LL << 7) ? 3 : 2);
+  if (v < (1LL << 7)) return 1;
+  if (v < (1LL << 16)) return v < (1LL << 8) ? 2 : 3;
+  return v < (1LL << 32) ? 5 : 9;
+}
+__host__ __device__ inline uint32_t mp_str_len(uint32_t n) { return (n < 32 ? 1 : n < 256 ? 2 : n < 65536 ? 3 : 5) + n; }
+__host__ __device__ inline uint32_t mp_bin_len(uint32_t n) { return (n < 256 ? 2 : n < 65536 ? 3 : 5) + n; }
+// per element: the constant part of a WORKFLOW_INSTANCE event value and of a JOB record value it writes
+// (zb_serialize.hip encode_value); + mp_int_len(workflowInstanceKey) + mp_int_len(scope / activity instance
+// key) + mp_bin_len(payload length)
+struct ValueConst {
+  uint32_t wf, job;
+};
+
 // ---- explicit io-mappings (Mapping.java: source query -> target path) ----
 struct DevMapping {           // 8 bytes
   uint16_t query;             // DevQuery of the source expression

@@ -87,6 +87,9 @@ struct zb_engine {
   zb_rec* log = nullptr;
   uint64_t* links = nullptr;
   uint32_t* srcd = nullptr;     // per record: position - source position (0: none), for log frames
+  uint32_t* vlen = nullptr;     // per record: serialized value length if the emitting kernel knew it
+  DevVec<ValueConst> d_vconst;  // per element: constant parts of its WORKFLOW_INSTANCE / JOB values
+  uint32_t* vlen_bad = nullptr; // ZB_VLEN_CHECK=1: the size pass checks every known length (device flag)
   RowMeta* rmeta = nullptr;
   RowKeys* rkeys = nullptr;
   uint8_t* arena = nullptr;
@@ -119,6 +122,8 @@ struct zb_engine {
 
   // staged input
   std::vector<zb_rec> staged;
+  std::vector<uint32_t> staged_vlen;   // value length of each staged record (VLEN_UNKNOWN: measured at drain)
+  DevVec<uint32_t> d_staged_vlen;
   std::vector<uint8_t> staged_arena;
   struct PendingRange {
     int64_t first, last;  // staged indices
@@ -273,6 +278,19 @@ int upload_model(zb_engine* e) {
   HIPCHECK(e, e->d_filters.upload(e->model.filters, e->stream));
   HIPCHECK(e, e->d_pool.upload(e->model.pool, e->stream));
   HIPCHECK(e, e->d_maps.upload(e->model.maps, e->stream));
+  {  // constant parts of the values an element's records carry (zb_serialize.hip encode_value)
+    std::vector<ValueConst> vc(e->model.elems.size());
+    for (size_t i = 0; i < vc.size(); i++) {
+      const DevElem& el = e->model.elems[i];
+      const DevWorkflow& wf = e->model.workflows[el.wf];
+      const uint32_t pid = mp_str_len(wf.pid_len), id = mp_str_len(el.id_len);
+      vc[i].wf = 1 + 14 + pid + 8 + mp_int_len(wf.version) + 12 + mp_int_len(wf.key) + 20 + 11 + id + 8 + 17;
+      vc[i].job = 1 + 9 + 9 + 7 + 1 + 8 + mp_int_len(el.retries) + 5 + mp_str_len(el.type_len) + 8 + 1 + 14 + pid +
+                  26 + mp_int_len(wf.version) + 12 + mp_int_len(wf.key) + 20 + 11 + id + 20 + 14 +
+                  (el.headers_off == NO_REF ? 1 : el.headers_len) + 8;
+    }
+    HIPCHECK(e, e->d_vconst.upload(vc, e->stream));
+  }
   HIPCHECK(e, e->d_segs.upload(e->model.segs, e->stream));
   if (e->static_blobs.size() > STATIC_ARENA_BYTES) return fail(e, ZB_ENOMEM, "static payload region full");
   HIPCHECK(e, hipMemcpyAsync(e->arena, e->static_blobs.data(), e->static_blobs.size(), hipMemcpyHostToDevice,
@@ -286,6 +304,7 @@ WaveParams wave_params(zb_engine* e) {
   p.log = e->log;
   p.links = e->links;
   p.srcd = e->srcd;
+  p.vlen = e->vlen;
   p.rmeta = e->rmeta;
   p.rkeys = e->rkeys;
   p.arena = e->arena;
@@ -440,7 +459,9 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   HIPCHECK(e, hipMemcpyAsync(e->t_ctl, e->h_ctl_pinned, sizeof(TrajCtl), hipMemcpyHostToDevice, e->stream));
   TrajParams p{};
   p.log = e->log;
+  p.vconst = e->d_vconst.p;
   p.srcd = e->srcd;
+  p.vlen = e->vlen;
   p.arena = e->arena;
   p.rmeta = e->rmeta;
   p.rkeys = e->rkeys;
@@ -601,6 +622,7 @@ MsgParams msg_params(zb_engine* e) {
   p.log = e->log;
   p.links = e->links;
   p.srcd = e->srcd;
+  p.vlen = e->vlen;
   p.arena = e->arena;
   p.subs = e->subs; p.sub_head = e->sub_head; p.sub_next = e->sub_next;
   p.sub_mask = e->head_mask; p.sub_count = e->sub_count; p.sub_cap = e->store_cap;
@@ -673,6 +695,9 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->log, L * sizeof(zb_rec)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->links, L * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->srcd, L * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->vlen, L * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (const char* c = std::getenv("ZB_VLEN_CHECK"))
+    if (atoi(c) && hipMalloc(&e->vlen_bad, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   // job states: a job belongs to one service-task instance and rows are never reused, so job ordinals stay
   // below the row capacity
   if ((e->cfg.flags & ZB_CFG_JOB_PROCESSOR) && hipMalloc(&e->jstate, e->cfg.row_capacity) != hipSuccess)
@@ -729,7 +754,7 @@ void zb_engine_destroy(zb_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (auto& x : e->ev)
     if (x) (void)hipEventDestroy(x);
-  void* ps[] = {e->jstate, e->mapres, e->map_ws, e->log, e->links, e->srcd, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
+  void* ps[] = {e->vlen, e->vlen_bad, e->jstate, e->mapres, e->map_ws, e->log, e->links, e->srcd, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
                 e->merge_jobs, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
@@ -785,6 +810,7 @@ int zb_reset(zb_engine* e, int keep_staged) {
   if (!keep_staged) {
     e->staged_reqs.clear();
     e->staged.clear();
+    e->staged_vlen.clear();
     e->staged_arena.clear();
     e->pending_ranges.clear();
     e->staged_lookup.clear();
@@ -920,6 +946,7 @@ void begin_staging(zb_engine* e) {
   if (e->staged_pending) return;
   e->staged_reqs.clear();
   e->staged.clear();
+  e->staged_vlen.clear();
   e->staged_arena.clear();
   e->pending_ranges.clear();
   e->staged_lookup.clear();
@@ -984,6 +1011,11 @@ int zb_submit_creates(zb_engine* e, const char* pid, int32_t version, int64_t wo
     d.intent = WI_CREATE;
     d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE, ZB_RT_COMMAND, false);
     e->staged.push_back(d);
+    // the command's value (zb_serialize.hip encode_value, submitted CREATE): pid / version / workflowKey of
+    // the call, instance / scope keys -1, activityId ""
+    const uint32_t plen = (len == 0 || (len == 1 && p[0] == 0xc0)) ? 1u : (uint32_t)len;
+    e->staged_vlen.push_back(1 + 14 + mp_str_len((uint32_t)spid.size()) + 8 + mp_int_len(version) + 12 +
+                             mp_int_len(workflow_key) + 20 + 1 + 11 + 1 + 8 + mp_bin_len(plen) + 17 + 1);
     e->staged_lookup.push_back(INT64_MIN);
   }
   e->pending_ranges.push_back(pr);
@@ -1406,6 +1438,7 @@ int zb_submit(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* va
       if (p.cancel) e->staged_has_cancel = true;
     }
     e->staged.push_back(p.d);
+    e->staged_vlen.push_back(p.raw_len);  // KIND_RAW: the value as written
     e->staged_lookup.push_back(p.lookup == INT64_MIN ? INT64_MIN : p.lookup);
   }
   if (n) e->staged_pending = true;
@@ -1439,6 +1472,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
       return fail(e, ZB_ENOMEM, "arena capacity");
     if (!e->staged_uploaded) {
       HIPCHECK(e, e->d_staged.upload(e->staged, e->stream));
+      HIPCHECK(e, e->d_staged_vlen.upload(e->staged_vlen, e->stream));
       HIPCHECK(e, e->d_staged_arena.upload(e->staged_arena, e->stream));
       e->staged_uploaded = true;
     }
@@ -1446,6 +1480,8 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     ip.log = e->log;
     ip.links = e->links;
     ip.srcd = e->srcd;
+    ip.vlen = e->vlen;
+    ip.staged_vlen = e->d_staged_vlen.p;
     ip.arena = e->arena;
     ip.staged = e->d_staged.p;
     ip.staged_arena = e->d_staged_arena.p;
@@ -1668,6 +1704,8 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
   }
   sp.log = e->log;
   sp.srcd = e->srcd;
+  sp.vlen = e->vlen;
+  sp.vlen_bad = e->vlen_bad;
   sp.arena = e->arena;
   sp.elems = e->d_elems.p;
   sp.wfs = e->d_wfs.p;
@@ -1709,6 +1747,7 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
       launch_ser_fused(sp, e->stream);
       HIPCHECK(e, hipEventRecord(e->dr_ev[3], e->stream));
     } else {  // two passes: sizes -> exclusive scan -> write (no host round trip: capacity checked on the device)
+      if (e->vlen_bad) HIPCHECK(e, hipMemsetAsync(e->vlen_bad, 0, sizeof(uint32_t), e->stream));
       SerParams sz = sp;
       sz.lengths64 = e->dr_len;  // count + 1 entries, the last one 0: the scan's last output is the total
       HIPCHECK(e, hipEventRecord(e->dr_ev[0], e->stream));
@@ -1727,6 +1766,11 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
     HIPCHECK(e, hipMemcpyAsync(e->h_dr_total, e->dr_total, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHECK(e, hipStreamSynchronize(e->stream));
     HIPCHECK(e, hipGetLastError());
+    if (e->vlen_bad) {  // ZB_VLEN_CHECK: an emitting kernel's value length disagreed with the encoder
+      uint32_t bad = 0;
+      HIPCHECK(e, hipMemcpy(&bad, e->vlen_bad, sizeof(bad), hipMemcpyDeviceToHost));
+      if (bad) return fail(e, ZB_EDEVICE, "value length hint differs from the serialized value (ZB_VLEN_CHECK)");
+    }
     const uint32_t overflow = ((const uint32_t*)(e->h_dr_total + 2))[1];
     if (!overflow) break;
     if (attempt == 1) return fail(e, ZB_EDEVICE, "drain buffer overflow after growing it");
@@ -1840,6 +1884,7 @@ int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, c
   HIPCHECK(e, hipMemcpyAsync(e->arena + arena0, blobs.data(), blobs.size(), hipMemcpyHostToDevice, e->stream));
   HIPCHECK(e, hipMemsetAsync(e->links + base, 0xff, n * sizeof(uint64_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->srcd + base, 0, n * sizeof(uint32_t), e->stream));  // client API commands
+  HIPCHECK(e, hipMemsetAsync(e->vlen + base, 0xff, n * sizeof(uint32_t), e->stream));
   MsgParams p = msg_params(e);
   p.n = (int64_t)n;
   p.base = base;

@@ -94,11 +94,13 @@ __global__ void __launch_bounds__(256) k_msg_open(MsgParams P) {
     P.log[pos] = d;
     P.links[pos] = ~0ull;
     P.srcd[pos] = 0;  // delivered from another partition
+    P.vlen[pos] = VLEN_UNKNOWN;
     d.intent = 1;  // OPENED: writeFollowUpEvent(record.getKey(), OPENED, subscriptionRecord)
     d.kind = make_kind(ZB_VT_MESSAGE_SUBSCRIPTION, ZB_RT_EVENT, false);
     P.log[pos + P.n] = d;
     P.links[pos + P.n] = ~0ull;
     P.srcd[pos + P.n] = (uint32_t)P.n;
+    P.vlen[pos + P.n] = VLEN_UNKNOWN;
     // MessageDataStore.findMessage(name, correlationKey): the first stored message that matches
     h = name_ck_hash(r.name, r.name_len, r.ck, r.ck_len);
     int64_t best = -1;
@@ -162,12 +164,14 @@ __global__ void __launch_bounds__(256) k_msg_publish(MsgParams P) {
     P.log[fpos] = d;
     P.links[fpos] = ~0ull;
     P.srcd[fpos] = (uint32_t)(fpos - pos);
+    P.vlen[fpos] = VLEN_UNKNOWN;
     if (per == 2) {  // ttl <= 0: addFollowUpEvent(key, DELETED, messageRecord)
       d.intent = 3;
       d.kind = make_kind(ZB_VT_MESSAGE, ZB_RT_EVENT, true);
       P.log[fpos + 1] = d;
       P.links[fpos + 1] = ~0ull;
       P.srcd[fpos + 1] = (uint32_t)(fpos + 1 - pos);
+      P.vlen[fpos + 1] = VLEN_UNKNOWN;
     }
     for (uint32_t e = P.sub_head[h & P.sub_mask]; e != NO_ENTRY; e = P.sub_next[e]) {
       const SubEntry s = P.subs[e];
@@ -231,6 +235,7 @@ __global__ void __launch_bounds__(256) k_wis_inject(MsgParams P) {
   P.log[pos] = d;
   P.links[pos] = (uint64_t)r.token | ((uint64_t)NO_ROW << 32);  // row_self = the catch event's row
   P.srcd[pos] = 0;
+  P.vlen[pos] = VLEN_UNKNOWN;
 }
 
 // ------------------------------------------------------------------------------ outbox

@@ -420,8 +420,16 @@ __global__ void __launch_bounds__(256) k_ser_size(SerParams P0) {
   if (P.lengths64 && i == P.count) P.lengths64[i] = 0;  // the scan over count + 1 entries ends in the total
   if (i >= P.count) return;
   const int64_t pos = P.start + i;
-  const zb_rec d = P.log[pos];
-  const uint32_t n = FRAMES ? encode_frame(P, pos, d, nullptr) : value_size(P, pos, d);
+  // the value length the emitting kernel knew, else the encoder's dry run (reads the record and its payload)
+  uint32_t n = P.vlen ? P.vlen[pos] : VLEN_UNKNOWN;
+  if (n == VLEN_UNKNOWN || P.vlen_bad) {  // (ZB_VLEN_CHECK: measure every record and compare)
+    const zb_rec d = P.log[pos];
+    const uint32_t m = value_size(P, pos, d);
+    if (n != VLEN_UNKNOWN && n != m) atomicOr(P.vlen_bad, 1u);
+    n = FRAMES ? (FRAME_PREFIX + reason_len(reason_of(d)) + m + 7) & ~7u : m;
+  } else if (FRAMES) {
+    n = (FRAME_PREFIX + n + 7) & ~7u;  // (a known length is never a rejection's: no reason)
+  }
   if (P.lengths64) P.lengths64[i] = n;
   else P.lengths[i] = n;
 }
@@ -766,6 +774,7 @@ __global__ void k_inject(InjectParams P) {
     P.log[P.log_base + i] = d;
     P.links[P.log_base + i] = ~0ull;  // no rows yet
     P.srcd[P.log_base + i] = 0;       // written by another writer (client API, job processor, ...)
+    P.vlen[P.log_base + i] = P.staged_vlen[i];
   }
   const uint64_t nw = P.staged_bytes / 8;
   const uint64_t* src = (const uint64_t*)P.staged_arena;

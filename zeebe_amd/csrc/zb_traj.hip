@@ -874,6 +874,7 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
           if (pos0 + k < (int64_t)P.log_cap) {
             P.log[pos0 + k] = d;
             P.srcd[pos0 + k] = (uint32_t)(pos0 + k - (fpos + (k < cut ? 0 : 1)));
+            P.vlen[pos0 + k] = VLEN_UNKNOWN;
           } else I.err |= DE_LOG_FULL;
           if (kind_vt(s.kind) == ZB_VT_WORKFLOW_INSTANCE && kind_rt(s.kind) == ZB_RT_EVENT) I.transitions++;
         }
@@ -1536,6 +1537,9 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
   uint32_t err = 0;
   uint64_t merge_bytes = 0;
   uint32_t pc_sym = PAY_CREATE, pc_ref = create_ref;  // last resolved payload symbol
+  // payload lengths for the value lengths (vlen): the CREATE payload's is read once per instance
+  const uint32_t create_len = arena_len(P.arena, create_ref);
+  uint32_t pc_len = create_len;
   uint32_t* reg = s_merge + threadIdx.x * TL::STRIDE;
   int64_t prev0 = P.log_base + inst;  // the instance's first record of the previous generation (the CREATE)
 
@@ -1555,7 +1559,7 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
     const uint32_t nrec = (uint32_t)(kload(P.agg, (uint64_t)crow + w) & 0xffff);
     // this generation's merge: source / target resolved, result into the instance's slot
     const MergeGen g = kload(P.mgen, (uint64_t)crow + w);
-    uint32_t merged_ref = 0;
+    uint32_t merged_ref = 0, merged_len = 0;
     if (g.has) {
       uint32_t src = g.src, tgt = g.tgt;
       if (src == PAY_CREATE) src = create_ref;
@@ -1565,6 +1569,7 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
       else if (tgt & PAY_MERGE) tgt = (uint32_t)(tmpl_mslot(P, L, tgt & 0xffff) >> 3);
       const uint64_t at = tmpl_mslot(P, L, (uint32_t)w);
       merged_ref = (uint32_t)(at >> 3);
+      merged_len = 0;
       if (active) {
         const uint32_t m_len = arena_len(P.arena, src) + arena_len(P.arena, tgt) + 8;
         if (tblob_bytes(m_len) > g.stride) err |= DE_UNSUPPORTED;
@@ -1573,6 +1578,7 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
           uint32_t ns = 0, nt = 0, olen = 0;
           merge_into<GEN, TL::OUT_WORDS, TL::IN_WORDS>(P, src, tgt, m_len, at, reg, err, ns, nt, olen);
           merge_bytes += ns + nt + olen;
+          merged_len = olen;
         }
       }
     }
@@ -1583,23 +1589,36 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
       d.key = tmpl_key(P, L, t.key, (uint32_t)w, kwf, kjob);
       d.scope_key = t.scope == SYM_CMDPOS ? P.log_base + inst : tmpl_key(P, L, t.scope, (uint32_t)w, kwf, kjob);
       d.inst_key = tmpl_key(P, L, t.inst, (uint32_t)w, kwf, kjob);
-      uint32_t pay = t.payload;
-      if (pay == (PAY_MERGE | (uint32_t)w)) pay = merged_ref;
-      else if (pay == pc_sym) pay = pc_ref;
-      else if (pay == PAY_CREATE) pay = create_ref;
+      uint32_t pay = t.payload, plen;
+      if (pay == (PAY_MERGE | (uint32_t)w)) { pay = merged_ref; plen = merged_len; }
+      else if (pay == pc_sym) { pay = pc_ref; plen = pc_len; }
+      else if (pay == PAY_CREATE) { pay = create_ref; plen = create_len; }
       else if (pay & PAY_MERGE) {
         const uint32_t r = (uint32_t)(tmpl_mslot(P, L, pay & 0xffff) >> 3);
+        plen = active ? arena_len(P.arena, r) : 0;
         pc_sym = pay;
         pc_ref = r;
+        pc_len = plen;
         pay = r;
+      } else {
+        plen = arena_len(P.arena, pay);  // a static blob (shared by every instance: cached)
       }
-      if (t.payload & PAY_MERGE) { pc_sym = t.payload; pc_ref = pay; }
+      if (t.payload & PAY_MERGE) { pc_sym = t.payload; pc_ref = pay; pc_len = plen; }
       d.payload = pay;
       d.elem = t.elem; d.intent = t.intent; d.kind = t.kind;
       if (active) {
         if (pos0 + k < (int64_t)P.log_cap) {
           P.log[pos0 + k] = d;
           P.srcd[pos0 + k] = (uint32_t)(pos0 + k - (prev0 + t.pad[0]));
+          // the value's length (zb_serialize.hip encode_value) from the element's constants and the variable fields
+          const uint8_t vt = kind_vt(d.kind), rt = kind_rt(d.kind);
+          uint32_t vl = VLEN_UNKNOWN;
+          if (!(d.kind & KIND_RAW) && ((vt == ZB_VT_WORKFLOW_INSTANCE && rt == ZB_RT_EVENT) ||
+                                       (vt == ZB_VT_JOB && (d.intent | 1) != JI_CANCELED))) {
+            const ValueConst vc = kload(P.vconst, (uint64_t)d.elem);
+            vl = (vt == ZB_VT_JOB ? vc.job : vc.wf) + mp_int_len(d.inst_key) + mp_int_len(d.scope_key) + mp_bin_len(plen);
+          }
+          P.vlen[pos0 + k] = vl;
         } else err |= DE_LOG_FULL;
       }
     }

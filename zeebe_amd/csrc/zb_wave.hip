@@ -1091,6 +1091,7 @@ __device__ __forceinline__ void emit_item(const WaveParams& P, const Chunk& c, i
       P.log[out_rec] = s.d;
       P.links[out_rec] = (uint64_t)s.rself | ((uint64_t)s.rscope << 32);
       P.srcd[out_rec] = (uint32_t)(out_rec - (uint64_t)(c.begin + i + s.pad));
+      P.vlen[out_rec] = VLEN_UNKNOWN;
       if (s.flags & SF_COND_JOB) {
         if (cond_j < P.job_cap) P.cond_jobs[par + cond_j] = out_rec;
         cond_j++;
@@ -1115,6 +1116,7 @@ __device__ __forceinline__ void emit_item(const WaveParams& P, const Chunk& c, i
         P.log[out_rec] = d;
         P.links[out_rec] = (uint64_t)NO_ROW | ((uint64_t)rscope << 32);
         P.srcd[out_rec] = (uint32_t)(out_rec - (uint64_t)r);
+        P.vlen[out_rec] = VLEN_UNKNOWN;
       }
       out_rec++;
     }
