@@ -1,0 +1,54 @@
+// TEST ONLY: compiles the drain write pass's fast value encoder (zeebe_amd/csrc/zb_fastenc.hpp) for the host
+// so that its bytes -- and that it never stores past the value -- can be fuzzed on CPU
+// (tests/test_fastenc_host.py). Nothing here is part of the product.
+#include <cstdint>
+#include <cstring>
+#define __device__
+#define __host__
+#define __forceinline__ inline
+#include "../../zeebe_amd/csrc/zb_fastenc.hpp"
+
+using namespace zbg;
+
+extern "C" {
+// Encodes one record with fast_encode into out (cap bytes, pre-filled by the caller with guard bytes).
+// pool: element id / type / process id / headers bytes (offsets below); doc: [u32 len][payload], 8-aligned,
+// padded to 8. Returns the encoded length (the caller checks out[n..cap) is still guard).
+long fastenc(int vt, int intent, int64_t inst_key, int64_t scope_key, int64_t wf_key, int32_t version,
+             int32_t retries, const uint8_t* pool_in, uint32_t pool_len, uint32_t pid_off, uint32_t pid_len,
+             uint32_t id_off, uint32_t id_len, uint32_t type_off, uint32_t type_len, uint32_t hdr_off, uint32_t hdr_len,
+             const uint64_t* doc, uint8_t* out) {
+  static uint8_t pool[1 << 16];
+  std::memset(pool, 0xcd, sizeof(pool));
+  std::memcpy(pool, pool_in, pool_len);
+  DevElem e{};
+  e.wf = 0;
+  e.id_off = id_off;
+  e.id_len = (uint16_t)id_len;
+  e.type_off = type_off;
+  e.type_len = (uint16_t)type_len;
+  e.headers_off = hdr_off;
+  e.headers_len = hdr_len;
+  e.retries = retries;
+  DevWorkflow wf{};
+  wf.key = wf_key;
+  wf.version = version;
+  wf.pid_off = pid_off;
+  wf.pid_len = (uint16_t)pid_len;
+  zb_rec d{};
+  d.inst_key = inst_key;
+  d.scope_key = scope_key;
+  d.elem = 0;
+  d.intent = (uint8_t)intent;
+  d.kind = make_kind((uint8_t)vt, ZB_RT_EVENT, false);
+  if (!fast_kind(d)) return -1;
+  uint64_t pre[SER_PRE];
+  const uint32_t words = (4 + (uint32_t)doc[0] + 7) / 8;  // (doc[0] low half: the payload length)
+  for (int j = 0; j < SER_PRE; j++) pre[j] = (uint32_t)j < words ? doc[j] : 0xa5a5a5a5a5a5a5a5ull;  // (next doc)
+  FastW w;
+  w.p = out;
+  w.n = 0;
+  fast_encode(w, d, &e, &wf, pool, doc, pre);
+  return w.n;
+}
+}

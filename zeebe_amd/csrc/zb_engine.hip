@@ -230,7 +230,8 @@ struct zb_engine {
   DevVec<int64_t> d_lookup_keys, d_lookup_pos;
   // drain buffers (zb_serialize), grown on demand and reused
   uint64_t dr_cap = 0, dr_val_cap = 0, dr_tmp_cap = 0;
-  uint64_t *dr_len = nullptr, *dr_off = nullptr, *dr_tiles = nullptr, *dr_pay = nullptr;
+  uint32_t* dr_len = nullptr;  // value lengths
+  uint64_t *dr_off = nullptr, *dr_tiles = nullptr, *dr_pay = nullptr, *dr_tsum = nullptr;  // tile offsets / states / ...
   zb_record_header* dr_hdr = nullptr;
   uint8_t* dr_val = nullptr;
   bool dr_frames = false;       // the drain batch holds log frames (no headers)
@@ -773,7 +774,7 @@ void zb_engine_destroy(zb_engine* e) {
   e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_consts.free();
   e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
   e->d_ranges.free(); e->d_cmd_pool.free(); e->d_lookup_keys.free(); e->d_lookup_pos.free();
-  void* dr[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_val, e->dr_tmp, e->dr_total, e->dr_tiles, e->dr_pay};
+  void* dr[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_val, e->dr_tmp, e->dr_total, e->dr_tiles, e->dr_pay, e->dr_tsum};
   for (void* p : dr)
     if (p) (void)hipFree(p);
   if (e->h_dr_total) (void)hipHostFree(e->h_dr_total);
@@ -1662,10 +1663,11 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
     HIPCHECK(e, hipHostMalloc(&e->h_dr_total, 4 * sizeof(uint64_t)));
   }
   if ((uint64_t)count > e->dr_cap) {
-    void* ps[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_tmp, e->dr_tiles, e->dr_pay};
+    void* ps[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_tmp, e->dr_tiles, e->dr_pay, e->dr_tsum};
     for (void* q : ps)
       if (q) (void)hipFree(q);
-    e->dr_len = e->dr_off = e->dr_tiles = e->dr_pay = nullptr; e->dr_hdr = nullptr; e->dr_tmp = nullptr;
+    e->dr_off = e->dr_tiles = e->dr_pay = e->dr_tsum = nullptr; e->dr_len = nullptr; e->dr_hdr = nullptr;
+    e->dr_tmp = nullptr;
     e->dr_cap = e->dr_tmp_cap = 0;
     const uint64_t cap = (uint64_t)count + (uint64_t)count / 4 + 1024;
     if (cap + 1 > (uint64_t)INT32_MAX) return fail(e, ZB_EUNSUPPORTED, "more than 2^31 records in one drain");
@@ -1673,10 +1675,12 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
     HIPCHECK(e, hipMalloc(&e->dr_tiles, (cap / 256 + 2) * sizeof(uint64_t)));  // single pass: tile states
     HIPCHECK(e, hipMalloc(&e->dr_pay, (cap / 256 + 2) * sizeof(uint64_t)));    // payload bytes per tile
     HIPCHECK(e, hipMemset(e->dr_tiles, 0, (cap / 256 + 2) * sizeof(uint64_t)));
-    HIPCHECK(e, hipMalloc(&e->dr_len, (cap + 1) * sizeof(uint64_t)));  // two passes: sizes, offsets
-    HIPCHECK(e, hipMalloc(&e->dr_off, (cap + 1) * sizeof(uint64_t)));
+    // two passes: value lengths (u32 per record) and byte totals per 256-record tile -> tile offsets
+    HIPCHECK(e, hipMalloc(&e->dr_len, cap * sizeof(uint32_t)));
+    HIPCHECK(e, hipMalloc(&e->dr_tsum, (cap / 256 + 2) * sizeof(uint64_t)));
+    HIPCHECK(e, hipMalloc(&e->dr_off, (cap / 256 + 2) * sizeof(uint64_t)));
     size_t tmp = 0;
-    if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->dr_len, e->dr_off, (int)(cap + 1), e->stream) != hipSuccess)
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->dr_tsum, e->dr_off, (int)(cap / 256 + 2), e->stream) != hipSuccess)
       return fail(e, ZB_EDEVICE, "scan sizing");
     HIPCHECK(e, hipMalloc(&e->dr_tmp, tmp + 16));
     e->dr_tmp_cap = tmp;
@@ -1707,6 +1711,7 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
   sp.vlen = e->vlen;
   sp.vlen_bad = e->vlen_bad;
   sp.arena = e->arena;
+  sp.arena_bytes = e->cfg.arena_bytes;
   sp.elems = e->d_elems.p;
   sp.wfs = e->d_wfs.p;
   sp.queries = e->d_queries.p;
@@ -1748,18 +1753,21 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
       HIPCHECK(e, hipEventRecord(e->dr_ev[3], e->stream));
     } else {  // two passes: sizes -> exclusive scan -> write (no host round trip: capacity checked on the device)
       if (e->vlen_bad) HIPCHECK(e, hipMemsetAsync(e->vlen_bad, 0, sizeof(uint32_t), e->stream));
+      const int64_t tiles = (count + 255) / 256;
       SerParams sz = sp;
-      sz.lengths64 = e->dr_len;  // count + 1 entries, the last one 0: the scan's last output is the total
+      sz.lengths = e->dr_len;
+      sz.tile_sums = e->dr_tsum;  // tiles + 1 entries, the last one 0: the scan's last output is the total
       HIPCHECK(e, hipEventRecord(e->dr_ev[0], e->stream));
       launch_ser_size(sz, e->stream);
       HIPCHECK(e, hipEventRecord(e->dr_ev[1], e->stream));
       size_t tmp = e->dr_tmp_cap;
-      if (hipcub::DeviceScan::ExclusiveSum(e->dr_tmp, tmp, e->dr_len, e->dr_off, (int)(count + 1), e->stream) != hipSuccess)
+      if (hipcub::DeviceScan::ExclusiveSum(e->dr_tmp, tmp, e->dr_tsum, e->dr_off, (int)(tiles + 1), e->stream) != hipSuccess)
         return fail(e, ZB_EDEVICE, "drain scan");
-      HIPCHECK(e, hipMemcpyAsync(e->dr_total, e->dr_off + count, sizeof(uint64_t), hipMemcpyDeviceToDevice, e->stream));
+      HIPCHECK(e, hipMemcpyAsync(e->dr_total, e->dr_off + tiles, sizeof(uint64_t), hipMemcpyDeviceToDevice, e->stream));
       HIPCHECK(e, hipEventRecord(e->dr_ev[2], e->stream));
       SerParams wr = sp;
-      wr.offsets = e->dr_off;
+      wr.lengths = e->dr_len;
+      wr.tile_offs = e->dr_off;
       launch_ser_write(wr, e->stream);
       HIPCHECK(e, hipEventRecord(e->dr_ev[3], e->stream));
     }
@@ -2243,7 +2251,7 @@ int zb_read_instances(zb_engine* e, uint8_t* buf, size_t cap, size_t* len, uint6
     launch_row_descs(lp, e->stream);
     // values: the serializer over the descriptors (size pass, scan, write pass)
     SerParams sp{};
-    sp.log = d_descs; sp.arena = e->arena; sp.elems = e->d_elems.p; sp.wfs = e->d_wfs.p;
+    sp.log = d_descs; sp.arena = e->arena; sp.arena_bytes = e->cfg.arena_bytes; sp.elems = e->d_elems.p; sp.wfs = e->d_wfs.p;
     sp.queries = e->d_queries.p; sp.pool = e->d_pool.p; sp.ranges = nullptr; sp.nranges = 0;
     sp.cmd_pool = nullptr; sp.start = 0; sp.count = live;
     SerParams sz = sp;

@@ -10,6 +10,7 @@
 #include <algorithm>
 
 #include "zb_devlib.hpp"
+#include "zb_fastenc.hpp"
 #include "zb_kernels.hpp"
 
 namespace zbg {
@@ -412,26 +413,40 @@ __device__ inline uint32_t encode_frame(const SerParams& P, int64_t pos, const z
   return fsize;
 }
 
+// Size pass: value (or frame) length per record and the byte total of every 256-record tile (the write
+// pass's tiles); the tile totals are scanned, each write-pass tile scans its own lengths.
 template <bool FRAMES>
 __global__ void __launch_bounds__(256) k_ser_size(SerParams P0) {
   __shared__ __attribute__((aligned(16))) uint8_t s_model[SER_MODEL_LDS];
-  const SerParams P = model_in_lds(P0, s_model, 256);
+  __shared__ unsigned long long s_sum[4];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (P.lengths64 && i == P.count) P.lengths64[i] = 0;  // the scan over count + 1 entries ends in the total
-  if (i >= P.count) return;
-  const int64_t pos = P.start + i;
+  const bool live = i < P0.count;
+  const int64_t pos = P0.start + i;
   // the value length the emitting kernel knew, else the encoder's dry run (reads the record and its payload)
-  uint32_t n = P.vlen ? P.vlen[pos] : VLEN_UNKNOWN;
-  if (n == VLEN_UNKNOWN || P.vlen_bad) {  // (ZB_VLEN_CHECK: measure every record and compare)
-    const zb_rec d = P.log[pos];
-    const uint32_t m = value_size(P, pos, d);
-    if (n != VLEN_UNKNOWN && n != m) atomicOr(P.vlen_bad, 1u);
-    n = FRAMES ? (FRAME_PREFIX + reason_len(reason_of(d)) + m + 7) & ~7u : m;
-  } else if (FRAMES) {
-    n = (FRAME_PREFIX + n + 7) & ~7u;  // (a known length is never a rejection's: no reason)
+  uint32_t n = (live && P0.vlen) ? P0.vlen[pos] : VLEN_UNKNOWN;
+  const bool measure = live && (n == VLEN_UNKNOWN || P0.vlen_bad);  // (ZB_VLEN_CHECK: measure every record)
+  if (__syncthreads_or(measure)) {  // the model tables go to LDS only for tiles that encode
+    const SerParams P = model_in_lds(P0, s_model, 256);
+    if (measure) {
+      const zb_rec d = P.log[pos];
+      const uint32_t m = value_size(P, pos, d);
+      if (n != VLEN_UNKNOWN && n != m) atomicOr(P.vlen_bad, 1u);
+      n = FRAMES ? (FRAME_PREFIX + reason_len(reason_of(d)) + m + 7) & ~7u : m;
+    }
   }
-  if (P.lengths64) P.lengths64[i] = n;
-  else P.lengths[i] = n;
+  if (live && !measure && FRAMES) n = (FRAME_PREFIX + n + 7) & ~7u;  // (a known length is never a rejection's)
+  if (!live) n = 0;
+  if (live) P0.lengths[i] = n;
+  if (P0.tile_sums) {
+    unsigned long long y = n;
+    for (int dd = 32; dd >= 1; dd >>= 1) y += __shfl_down(y, dd, 64);
+    if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = y;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      P0.tile_sums[blockIdx.x] = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+      if (blockIdx.x == 0) P0.tile_sums[gridDim.x] = 0;  // the scan over tiles + 1 entries ends in the total
+    }
+  }
 }
 
 // Write pass. Record i's value goes to out[offsets[i], offsets[i + 1]); the workgroup's records are one
@@ -490,30 +505,65 @@ constexpr int SER_WINDOWS = 16;
 template <bool FRAMES, bool NT>
 __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 3))) k_ser_write(SerParams P0) {
   __shared__ __attribute__((aligned(16))) uint8_t img[SER_IMG + 16];
-  __shared__ __attribute__((aligned(16))) uint8_t s_model[SER_MODEL_LDS];
+  __shared__ __attribute__((aligned(16))) uint8_t s_model[SER_MODEL_LDS + 16];  // (+16: 8-byte reads past the pool)
   __shared__ unsigned long long s_pay[SER_WG / 64];
+  __shared__ unsigned long long s_wsum[SER_WG / 64];
   __shared__ uint32_t s_maxlen;
   __shared__ unsigned long long s_wlo[SER_WINDOWS], s_whi[SER_WINDOWS];
   const int64_t base = (int64_t)blockIdx.x * SER_WG;
   const int64_t i = base + threadIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool live = i < P0.count;
   // independent loads first; the model copy to LDS overlaps them
-  const int64_t last = (base + SER_WG < P0.count) ? base + SER_WG : P0.count;
-  const uint64_t o0 = P0.offsets[base], o1 = P0.offsets[last];
   zb_rec d{};
-  uint64_t off = 0, nxt = 0;
-  if (live) {
-    d = P0.log[P0.start + i];
-    off = P0.offsets[i];
-    nxt = P0.offsets[i + 1];
+  uint64_t o0, o1, off = 0, nxt = 0, x = 0;
+  uint32_t len = 0;
+  if (P0.tile_offs) {  // tile offsets + lengths: this tile's exclusive scan in registers / LDS
+    o0 = P0.tile_offs[blockIdx.x];
+    o1 = P0.tile_offs[blockIdx.x + 1];
+    if (live) len = P0.lengths[i];
+  } else {
+    const int64_t last = (base + SER_WG < P0.count) ? base + SER_WG : P0.count;
+    o0 = P0.offsets[base];
+    o1 = P0.offsets[last];
+    if (live) {
+      off = P0.offsets[i];
+      nxt = P0.offsets[i + 1];
+    }
+  }
+  if (live) d = P0.log[P0.start + i];
+  // payload document words of the fast records, loaded before the model copy's barrier
+  const bool fast = live && P0.model_lds && P0.arena_bytes && fast_kind(d);
+  const uint64_t* dw = (const uint64_t*)(P0.arena + (uint64_t)d.payload * 8);
+  uint64_t pre[SER_PRE];
+#pragma unroll
+  for (int j = 0; j < SER_PRE; j++)
+    pre[j] = (fast && (uint64_t)d.payload * 8 + 8 * j + 8 <= P0.arena_bytes) ? dw[j] : 0;
+  if (P0.tile_offs) {
+    x = len;
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+      const uint64_t y = (uint64_t)__shfl_up((unsigned long long)x, k, 64);
+      if (lane >= k) x += y;
+    }
+    if (lane == 63) s_wsum[wv] = x;
   }
   if (threadIdx.x == 0) s_maxlen = 0;
-  const SerParams P = model_in_lds(P0, s_model, SER_WG);  // (ends in a barrier)
+  const SerParams P = model_in_lds(P0, s_model, SER_WG);  // (ends in a barrier when the model goes to LDS)
+  if (!P0.model_lds) __syncthreads();
+  if (P.tile_offs) {
+    uint64_t pre_w = 0;
+#pragma unroll
+    for (int k = 0; k < SER_WG / 64; k++)
+      if (k < wv) pre_w += s_wsum[k];
+    off = o0 + pre_w + x - len;
+    nxt = off + len;
+  }
   if (P.out_cap && o1 > P.out_cap) {  // does not fit: the host grows the buffer and runs the pass again
     if (threadIdx.x == 0) atomicOr(P.overflow, 1u);
     return;
   }
-  const uint32_t len = (uint32_t)(nxt - off);
+  if (!P.tile_offs) len = (uint32_t)(nxt - off);
   const uint32_t shift = (uint32_t)(((uintptr_t)(P.out + o0)) & 15);
   const bool staged = (o1 - o0) + shift <= (uint64_t)SER_IMG;
   uint64_t ws = 0;
@@ -538,13 +588,14 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
   uint32_t pay = 0;
   const int64_t pos = P.start + i;
   if (live) {
-    if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay = *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
+    if (fast) pay = (uint32_t)pre[0];
+    else if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay = *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
     if (!FRAMES) {
       const zb_record_header h = record_header(d, pos, len, off);
       if (NT) {
         const uint64_t* hw = (const uint64_t*)&h;
-        uint64_t* dw = (uint64_t*)(P.headers + i);
-        for (int k = 0; k < 5; k++) __builtin_nontemporal_store(hw[k], dw + k);
+        uint64_t* dh = (uint64_t*)(P.headers + i);
+        for (int k = 0; k < 5; k++) __builtin_nontemporal_store(hw[k], dh + k);
       } else {
         P.headers[i] = h;
       }
@@ -553,7 +604,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
   if (P.totals) {
     unsigned long long y = pay;
     for (int dd = 32; dd >= 1; dd >>= 1) y += __shfl_down(y, dd, 64);
-    if ((threadIdx.x & 63) == 0) s_pay[threadIdx.x >> 6] = y;
+    if (lane == 0) s_pay[wv] = y;
     __syncthreads();
     if (threadIdx.x == 0) {
       unsigned long long tt = 0;
@@ -563,8 +614,23 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
       P.pay_part[blockIdx.x] = tt;
     }
   }
-  // phases (one encode site keeps the encoder inlined once): the whole tile staged, straight to HBM, or one
-  // phase per window
+  // LDS offsets of the model tables (fast encoder: typed LDS reads)
+  const uint32_t eb = (uint32_t)P0.n_elems * (uint32_t)sizeof(DevElem), wb = (uint32_t)P0.n_wfs * (uint32_t)sizeof(DevWorkflow);
+  const uint32_t wo = (eb + 15) & ~15u, po = wo + ((wb + 15) & ~15u);
+  // the common case: a staged tile of fast records, encoded from the prefetched payload words
+  if (!FRAMES && staged && __syncthreads_and(fast || !live)) {
+    if (live) {
+      FastW w;
+      w.p = img + shift + (uint32_t)(off - o0);
+      w.n = 0;
+      fast_encode(w, d, (const DevElem*)s_model, (const DevWorkflow*)(s_model + wo), s_model + po, dw, pre);
+    }
+    __syncthreads();
+    stream_image(img, P.out, o0, shift, o1 - o0, NT);
+    return;
+  }
+  // otherwise the generic encoder in phases (one encode site keeps it inlined once): the whole tile staged,
+  // straight to HBM, or one phase per window (the fast encoder here too spills at the 3-workgroup register cap)
   const int mywin = (nwin && live) ? (int)((off - o0) / ws) : -1;
   const int nph = nwin ? nwin : 1;
 #pragma unroll 1
@@ -572,16 +638,17 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
     uint64_t wlo = o0, whi = o1;
     uint32_t sh = shift;
     bool go = live;
-    uint8_t* dst = staged ? img + shift + (off - o0) : P.out + off;
     if (nwin) {
       wlo = s_wlo[ph];
       whi = s_whi[ph];
       if (wlo >= whi) continue;  // no value starts in this window (uniform)
       sh = (uint32_t)(((uintptr_t)(P.out + wlo)) & 15);
       go = mywin == ph;
-      dst = img + sh + (off - wlo);
     }
+    const bool in_img = staged || nwin;
+    const uint32_t lo = (uint32_t)(sh + (off - wlo));  // the record's image offset (staged / windowed)
     if (go) {
+      uint8_t* dst = in_img ? img + lo : P.out + off;
       if (FRAMES) {
         (void)encode_frame(P, pos, d, dst);
       } else {
@@ -591,7 +658,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
         encode_value(P, pos, d, w);
       }
     }
-    if (staged || nwin) {
+    if (in_img) {
       __syncthreads();
       stream_image(img, P.out, wlo, sh, whi - wlo, NT);
       __syncthreads();  // the image is reused by the next window
@@ -599,19 +666,15 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
   }
 }
 
-// payload-byte total of the write pass (one workgroup)
-__global__ void __launch_bounds__(1024) k_ser_sum(SerParams P, int64_t nparts) {
-  __shared__ unsigned long long s[16];
+// payload-byte total of the write pass: every workgroup sums a slice of the per-tile partials, one atomic each
+__global__ void __launch_bounds__(256) k_ser_sum(SerParams P, int64_t nparts) {
+  __shared__ unsigned long long s[4];
   unsigned long long x = 0;
-  for (int64_t k = threadIdx.x; k < nparts; k += 1024) x += P.pay_part[k];
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < nparts; k += (int64_t)gridDim.x * 256) x += P.pay_part[k];
   for (int dd = 32; dd >= 1; dd >>= 1) x += __shfl_down(x, dd, 64);
   if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = x;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long t = 0;
-    for (int k = 0; k < 16; k++) t += s[k];
-    P.totals[1] = t;
-  }
+  if (threadIdx.x == 0) atomicAdd((unsigned long long*)&P.totals[1], s[0] + s[1] + s[2] + s[3]);
 }
 
 // ------------------------------------------------------------------------------ single pass (zb_serialize)
@@ -744,12 +807,12 @@ void launch_ser_fused(const SerParams& p, hipStream_t s) {
   if (p.count <= 0) return;
   const int64_t tiles = (p.count + SER_WG - 1) / SER_WG;
   hipLaunchKernelGGL(k_ser_fused, dim3((unsigned)tiles), dim3(SER_WG), 0, s, p);
-  if (p.totals) hipLaunchKernelGGL(k_ser_sum, dim3(1), dim3(1024), 0, s, p, tiles);
+  if (p.totals) hipLaunchKernelGGL(k_ser_sum, dim3((unsigned)std::min<int64_t>(256, (tiles + 255) / 256)), dim3(256), 0, s, p, tiles);
 }
 
 void launch_ser_size(const SerParams& p, hipStream_t s) {
   if (p.count <= 0) return;
-  const int64_t work = p.count + (p.lengths64 ? 1 : 0);
+  const int64_t work = p.count;
   if (p.frames) hipLaunchKernelGGL(k_ser_size<true>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, p);
   else hipLaunchKernelGGL(k_ser_size<false>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, p);
 }
@@ -759,7 +822,7 @@ void launch_ser_write(const SerParams& p, hipStream_t s) {
   if (p.frames) hipLaunchKernelGGL((k_ser_write<true, true>), dim3((unsigned)tiles), dim3(SER_WG), 0, s, p);
   else if (p.nt) hipLaunchKernelGGL((k_ser_write<false, true>), dim3((unsigned)tiles), dim3(SER_WG), 0, s, p);
   else hipLaunchKernelGGL((k_ser_write<false, false>), dim3((unsigned)tiles), dim3(SER_WG), 0, s, p);
-  if (p.totals) hipLaunchKernelGGL(k_ser_sum, dim3(1), dim3(1024), 0, s, p, tiles);
+  if (p.totals) hipLaunchKernelGGL(k_ser_sum, dim3((unsigned)std::min<int64_t>(256, (tiles + 255) / 256)), dim3(256), 0, s, p, tiles);
 }
 
 // ------------------------------------------------------------------------------ input injection
