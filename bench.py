@@ -121,7 +121,7 @@ def run_workload(cfg, n, a, rank, world, local_rank, barrier, steps, warmup, dra
     barrier()
     tot = dict(transitions=0, completed=0, written=0, merges=0, merge_bytes=0, cond_bytes=0, kernel_ms=0.0,
                process_ms=0.0, emit_ms=0.0, aux_ms=0.0, main_ms=0.0, launches=0, waves=0, step_s=0.0, drain_s=0.0,
-               ser_write_ms=0.0, ser_size_ms=0.0, value_bytes=0, payload_bytes=0, drained=0, path=0)
+               ser_write_ms=0.0, ser_size_ms=0.0, value_bytes=0, payload_bytes=0, drained=0, path=0, generic_tiles=0)
     t0 = time.perf_counter()
     for _ in range(steps):
         st, ser, ts, td = one_step()
@@ -147,6 +147,7 @@ def run_workload(cfg, n, a, rank, world, local_rank, barrier, steps, warmup, dra
             tot["value_bytes"] += ser["value_bytes"]
             tot["payload_bytes"] += ser["payload_bytes"]
             tot["drained"] += ser["records"]
+            tot["generic_tiles"] += ser["generic_tiles"]
     barrier()
     tot["elapsed"] = time.perf_counter() - t0
     tot["desc"] = desc
@@ -267,7 +268,9 @@ def roofline(tot, steps, cfg, n):
         # per launch: every drained record's descriptor read + header write, its value bytes written and the
         # payload documents copied into them read (SURVEY §8d payload term)
         b = (tot["drained"] * (DESC_BYTES + HDR_BYTES) + tot["value_bytes"] + tot["payload_bytes"]) / steps
-        kname = "zbg::k_ser_write" if tot["ser_size_ms"] > 0 else "zbg::k_ser_fused"  # two-pass / single-pass
+        # two passes: the fast write pass (k_ser_write over the tiles it leaves, if any) / single pass
+        kname = ("zbg::k_ser_fast" if tot["generic_tiles"] == 0 else "zbg::k_ser_fast (+ k_ser_write on %d tiles)"
+                 % (tot["generic_tiles"] // steps)) if tot["ser_size_ms"] > 0 else "zbg::k_ser_fused"
         cands.append((kname, tot["ser_write_ms"] / steps, b,
                       "32 B descriptor read + 40 B header write per drained record + value bytes written + payload "
                       "bytes read"))

@@ -264,6 +264,7 @@ typedef struct zb_serialize_stats {
   double scan_ms;              /* exclusive scan of the sizes (0 in the single-pass serializer) */
   double write_kernel_ms;      /* write pass (headers + values; the whole single pass): the drain's kernel */
   double wall_ms;
+  uint64_t generic_tiles;      /* 256-record tiles the generic write pass encoded (the rest: the fast pass) */
 } zb_serialize_stats;
 int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats* stats);
 /* headers: NULL or room for the batch's headers; values: NULL or values_len bytes from value byte

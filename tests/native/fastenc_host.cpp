@@ -11,13 +11,13 @@
 using namespace zbg;
 
 extern "C" {
-// Encodes one record with fast_encode into out (cap bytes, pre-filled by the caller with guard bytes).
+// Encodes one record with fast_encode into out + head (out 8-aligned, pre-filled by the caller with guard bytes).
 // pool: element id / type / process id / headers bytes (offsets below); doc: [u32 len][payload], 8-aligned,
 // padded to 8. Returns the encoded length (the caller checks out[n..cap) is still guard).
 long fastenc(int vt, int intent, int64_t inst_key, int64_t scope_key, int64_t wf_key, int32_t version,
              int32_t retries, const uint8_t* pool_in, uint32_t pool_len, uint32_t pid_off, uint32_t pid_len,
              uint32_t id_off, uint32_t id_len, uint32_t type_off, uint32_t type_len, uint32_t hdr_off, uint32_t hdr_len,
-             const uint64_t* doc, uint8_t* out) {
+             const uint64_t* doc, uint8_t* out, uint32_t head) {
   static uint8_t pool[1 << 16];
   std::memset(pool, 0xcd, sizeof(pool));
   std::memcpy(pool, pool_in, pool_len);
@@ -46,9 +46,8 @@ long fastenc(int vt, int intent, int64_t inst_key, int64_t scope_key, int64_t wf
   const uint32_t words = (4 + (uint32_t)doc[0] + 7) / 8;  // (doc[0] low half: the payload length)
   for (int j = 0; j < SER_PRE; j++) pre[j] = (uint32_t)j < words ? doc[j] : 0xa5a5a5a5a5a5a5a5ull;  // (next doc)
   FastW w;
-  w.p = out;
-  w.n = 0;
+  w.begin(out, head);  // (out: 8-aligned image; the value starts at byte head of it)
   fast_encode(w, d, &e, &wf, pool, doc, pre);
-  return w.n;
+  return w.n();
 }
 }

@@ -3,9 +3,9 @@
 tests/native/fastenc_host.cpp compiles the encoder for the host. Each value is checked two ways:
   * its bytes equal the reference layout (WorkflowInstanceRecord.java:39-60, JobRecord.java:35-53 +
     JobHeaders.java:33-51, MsgPackWriter integer / string / binary encodings), built here with msgpack;
-  * no store lands past the value: the output buffer is filled with guard bytes, and on the GPU the
-    bytes after a value belong to the next lane's record (the encoder writes 8-byte words that may run
-    past a field, never past the value).
+  * no store lands outside the value: the image is filled with guard bytes and the value starts at every
+    offset mod 8; on the GPU the bytes around a value belong to the neighbouring lanes' records (the
+    encoder stores whole aligned 8-byte slots inside the value, exact aligned pieces at its two ends).
 """
 import ctypes
 import os
@@ -33,7 +33,7 @@ def lib():
     L = ctypes.CDLL(so)
     L.fastenc.restype = ctypes.c_long
     L.fastenc.argtypes = ([ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
-                           ctypes.c_int32, ctypes.c_char_p] + [ctypes.c_uint32] * 9 + [ctypes.c_void_p, ctypes.c_void_p])
+                           ctypes.c_int32, ctypes.c_char_p] + [ctypes.c_uint32] * 9 + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32])
     return L
 
 
@@ -47,7 +47,7 @@ def rand_str(r):
     return "".join(r.choice("abcxyz_-0") for _ in range(r.choice([0, 1, 5, 7, 8, 9, 15, 31, 32, 33, 40, 255, 256, 300])))
 
 
-def encode(lib, vt, intent, inst, scope, wfkey, version, retries, pid, act, jtype, headers, payload):
+def encode(lib, vt, intent, inst, scope, wfkey, version, retries, pid, act, jtype, headers, payload, head=0):
     pool = b""
     offs = {}
     for name, v in (("pid", pid), ("act", act), ("type", jtype), ("hdr", headers or b"")):
@@ -56,15 +56,17 @@ def encode(lib, vt, intent, inst, scope, wfkey, version, retries, pid, act, jtyp
     doc = struct.pack("<I", len(payload)) + payload
     doc += b"\0" * (-len(doc) % 8) + b"\xa5" * 64  # padded to 8, then whatever follows in the arena
     dbuf = ctypes.create_string_buffer(doc, len(doc))
-    cap = 2048 + len(payload) + len(pool)
-    out = ctypes.create_string_buffer(bytes([GUARD]) * cap, cap)
+    cap = (2048 + len(payload) + len(pool) + 7) // 8 * 8
+    out = (ctypes.c_uint64 * (cap // 8))()  # 8-aligned image
+    ctypes.memset(out, GUARD, cap)
     n = lib.fastenc(vt, intent, inst, scope, wfkey, version, retries, pool, len(pool), offs["pid"], len(pid),
                     offs["act"], len(act), offs["type"], len(jtype), offs["hdr"] if headers else 0xFFFFFFFF,
-                    len(headers or b""), dbuf, out)
-    raw = out.raw
+                    len(headers or b""), dbuf, out, head)
+    raw = bytes(out)
     assert n > 0
-    assert all(b == GUARD for b in raw[n:]), "store past the value end"
-    return raw[:n]
+    assert all(b == GUARD for b in raw[:head]), "store before the value start (the previous lane's bytes)"
+    assert all(b == GUARD for b in raw[head + n:]), "store past the value end"
+    return raw[head:head + n]
 
 
 def expect_wi(pid, version, wfkey, inst, act, payload, scope):
@@ -95,10 +97,12 @@ def test_fast_encoder_fuzz(lib):
         version, retries = (max(-2 ** 31, min(2 ** 31 - 1, rand_int(r))) for _ in range(2))
         headers = r.choice([None, msgpack.packb({"k": "v" * r.randrange(20)})])
         if it % 2 == 0:
-            got = encode(lib, VT_WI, 4, inst, scope, wfkey, version, retries, pid, act, jtype, headers, payload)
+            got = encode(lib, VT_WI, 4, inst, scope, wfkey, version, retries, pid, act, jtype, headers, payload,
+                         head=r.randrange(24))
             assert got == expect_wi(pid, version, wfkey, inst, act, payload, scope), it
         else:
-            got = encode(lib, VT_JOB, 5, inst, scope, wfkey, version, retries, pid, act, jtype, headers, payload)
+            got = encode(lib, VT_JOB, 5, inst, scope, wfkey, version, retries, pid, act, jtype, headers, payload,
+                         head=r.randrange(24))
             assert got == expect_job(pid, version, wfkey, inst, act, payload, scope, retries, jtype, headers), it
 
 
@@ -106,5 +110,5 @@ def test_fast_kind_excludes_cancel(lib):
     # JOB CANCEL / CANCELED (a reset record) and submitted CREATEs stay on the generic encoder
     for intent in (12, 13):
         n = lib.fastenc(VT_JOB, intent, 1, 1, 1, 1, 3, b"x", 1, 0, 1, 0, 1, 0, 1, 0xFFFFFFFF, 0,
-                        ctypes.create_string_buffer(16), ctypes.create_string_buffer(256))
+                        ctypes.create_string_buffer(16), ctypes.create_string_buffer(256), 0)
         assert n == -1

@@ -1,0 +1,98 @@
+"""The drain's two write passes give the same bytes.
+
+zb_serialize runs the fast pass (k_ser_fast: per-wave LDS image, the fast WORKFLOW_INSTANCE / JOB encoder)
+over every 256-record tile and hands the tiles it cannot take (other record kinds, a wave's values over its
+image) to the generic pass (k_ser_write). ZB_SER_FAST=0 sends every tile through the generic pass, whose
+bytes every other GPU test compares with the oracle. Here the two drains of the same log must agree byte for
+byte -- values and the 40-byte record headers -- on logs that mix the cases: C3 (all tiles fast), C2 with
+job payloads large enough that tiles overflow the fast image, and the CREATE commands (generic records) at
+the head of every log.
+"""
+import ctypes
+import os
+
+import msgpack
+import pytest
+
+from zeebe_amd import bpmn, workloads
+
+pytestmark = pytest.mark.gpu
+
+
+def _drain(make, fast):
+    from zeebe_amd.engine import Engine, zb_record_header
+
+    old = os.environ.get("ZB_SER_FAST")
+    os.environ["ZB_SER_FAST"] = "1" if fast else "0"
+    try:
+        e = Engine()
+    finally:
+        if old is None:
+            del os.environ["ZB_SER_FAST"]
+        else:
+            os.environ["ZB_SER_FAST"] = old
+    make(e)
+    st = e.step()
+    assert st["quiescent"]
+    n = e.log_size()
+    ser = e.serialize(0, n)
+    vals = ctypes.create_string_buffer(max(ser["value_bytes"], 1))
+    hdrs = (zb_record_header * n)()
+    e.drain_copy(ctypes.addressof(vals), 0, ser["value_bytes"], ctypes.addressof(hdrs))
+    e.close()
+    return ser, vals.raw[:ser["value_bytes"]], bytes(hdrs)
+
+
+def _compare(make, expect_generic_all=False):
+    sf, vf, hf = _drain(make, True)
+    sg, vg, hg = _drain(make, False)
+    tiles = (sf["records"] + 255) // 256
+    assert sg["generic_tiles"] == tiles
+    assert sf["value_bytes"] == sg["value_bytes"] and sf["payload_bytes"] == sg["payload_bytes"]
+    assert vf == vg
+    assert hf == hg
+    if not expect_generic_all:
+        assert sf["generic_tiles"] < tiles
+    return sf
+
+
+def test_c3_fast_drain_matches_generic():
+    cfg = workloads.CONFIGS["c3"]
+    blob, offs = cfg["payloads"](20000)
+
+    def make(e):
+        e.deploy(cfg["workflow"]().to_xml(), 100, 1)
+        e.create_packed(cfg["process"], blob, offs)
+
+    sf = _compare(make)
+    assert sf["generic_tiles"] <= 79  # only the tiles holding the 20k CREATE commands (generic records)
+
+
+def test_c2_large_job_payloads_fast_drain_matches_generic():
+    # job payloads of 40..400 bytes: the merged instance payloads grow along the chain, so later tiles
+    # outgrow the one-wave image and go to the generic pass; JOB records take the fast JOB encoder
+    wf = bpmn.chain_workflow(6)
+    blob, offs = workloads.order_payloads(3000)
+    jp = {"t%d" % k: msgpack.packb({"k%d" % k: "x" * (40 * k * k // 3)}) for k in range(1, 7)}
+
+    def make(e):
+        e.deploy(wf.to_xml(), 100, 1)
+        for act, p in jp.items():
+            e.set_job_payload(100, act, p)
+        e.create_packed("chain", blob, offs)
+
+    _compare(make)
+
+
+def test_mixed_kinds_fast_drain_matches_generic():
+    # incidents (no default flow) interleave generic records with fast ones inside tiles
+    b = bpmn.Bpmn.create_executable_process("inc").start_event("s").exclusive_gateway("x")
+    b.sequence_flow_id("f1").condition("$.a == 1").end_event("e1")
+    m = b.move_to_node("x").sequence_flow_id("f2").condition("$.a == 2").end_event("e2").done()
+    payloads = [msgpack.packb({"a": i % 3, "pad": "p" * (i % 50)}) for i in range(3000)]
+
+    def make(e):
+        e.deploy(m.to_xml(), 100, 1)
+        e.create("inc", payloads)
+
+    _compare(make)

@@ -82,6 +82,8 @@ struct zb_engine {
   MNode* map_ws = nullptr;      // k_map tree workspaces
   int ser_mode = 0;              // ZB_SER_MODE: 0 = two passes (size, scan, write), 1 = single pass (look-back)
   int ser_nt = 1;                // ZB_SER_NT=0: plain (not non-temporal) stores in the drain write pass
+  int ser_exp = 0;               // ZB_SER_EXP: measurement knobs of the fast write path (1 no encode, 2 no stream-out,
+                                 // 4 no header stores) -- the output is wrong with any of them set
 
   // device state
   zb_rec* log = nullptr;
@@ -232,6 +234,10 @@ struct zb_engine {
   uint64_t dr_cap = 0, dr_val_cap = 0, dr_tmp_cap = 0;
   uint32_t* dr_len = nullptr;  // value lengths
   uint64_t *dr_off = nullptr, *dr_tiles = nullptr, *dr_pay = nullptr, *dr_tsum = nullptr;  // tile offsets / states / ...
+  uint32_t* dr_list = nullptr;   // tiles k_ser_fast leaves to k_ser_write
+  uint32_t dr_slow_tiles = 0;    // how many tiles the last drain ran through k_ser_write
+  bool dr_split = false;         // the last drain ran k_ser_fast + k_ser_write (events 2-4, 5-3)
+  int ser_fast = 1;              // ZB_SER_FAST=0: every tile through k_ser_write
   zb_record_header* dr_hdr = nullptr;
   uint8_t* dr_val = nullptr;
   bool dr_frames = false;       // the drain batch holds log frames (no headers)
@@ -241,7 +247,7 @@ struct zb_engine {
   int64_t dr_count = 0;           // records of the batch in the drain buffers
   uint64_t dr_bytes = 0;
   uint64_t dr_epoch = 0;          // look-back tags of the single-pass serializer
-  hipEvent_t dr_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t dr_ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
 
   // timing
   std::vector<hipEvent_t> ev;
@@ -661,6 +667,8 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   e->cfg = *cfg;
   if (const char* m = std::getenv("ZB_SER_MODE")) e->ser_mode = std::strcmp(m, "fused") == 0 ? 1 : 0;
   if (const char* m = std::getenv("ZB_SER_NT")) e->ser_nt = atoi(m);
+  if (const char* m = std::getenv("ZB_SER_EXP")) e->ser_exp = atoi(m);
+  if (const char* m = std::getenv("ZB_SER_FAST")) e->ser_fast = atoi(m);
   if (const char* g = std::getenv("ZB_WAVE_GRID")) e->wave_grid_fixed = std::max(0, std::min(atoi(g), (int)WAVE_GRID_MAX));
   if (e->cfg.log_capacity == 0) e->cfg.log_capacity = 1ull << 22;
   if (e->cfg.row_capacity == 0) e->cfg.row_capacity = 1ull << 20;
@@ -774,7 +782,8 @@ void zb_engine_destroy(zb_engine* e) {
   e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_consts.free();
   e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
   e->d_ranges.free(); e->d_cmd_pool.free(); e->d_lookup_keys.free(); e->d_lookup_pos.free();
-  void* dr[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_val, e->dr_tmp, e->dr_total, e->dr_tiles, e->dr_pay, e->dr_tsum};
+  void* dr[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_val, e->dr_tmp, e->dr_total, e->dr_tiles, e->dr_pay, e->dr_tsum,
+                e->dr_list};
   for (void* p : dr)
     if (p) (void)hipFree(p);
   if (e->h_dr_total) (void)hipHostFree(e->h_dr_total);
@@ -1663,10 +1672,10 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
     HIPCHECK(e, hipHostMalloc(&e->h_dr_total, 4 * sizeof(uint64_t)));
   }
   if ((uint64_t)count > e->dr_cap) {
-    void* ps[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_tmp, e->dr_tiles, e->dr_pay, e->dr_tsum};
+    void* ps[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_tmp, e->dr_tiles, e->dr_pay, e->dr_tsum, e->dr_list};
     for (void* q : ps)
       if (q) (void)hipFree(q);
-    e->dr_off = e->dr_tiles = e->dr_pay = e->dr_tsum = nullptr; e->dr_len = nullptr; e->dr_hdr = nullptr;
+    e->dr_off = e->dr_tiles = e->dr_pay = e->dr_tsum = nullptr; e->dr_len = e->dr_list = nullptr; e->dr_hdr = nullptr;
     e->dr_tmp = nullptr;
     e->dr_cap = e->dr_tmp_cap = 0;
     const uint64_t cap = (uint64_t)count + (uint64_t)count / 4 + 1024;
@@ -1679,6 +1688,7 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
     HIPCHECK(e, hipMalloc(&e->dr_len, cap * sizeof(uint32_t)));
     HIPCHECK(e, hipMalloc(&e->dr_tsum, (cap / 256 + 2) * sizeof(uint64_t)));
     HIPCHECK(e, hipMalloc(&e->dr_off, (cap / 256 + 2) * sizeof(uint64_t)));
+    HIPCHECK(e, hipMalloc(&e->dr_list, (cap / 256 + 2) * sizeof(uint32_t)));
     size_t tmp = 0;
     if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->dr_tsum, e->dr_off, (int)(cap / 256 + 2), e->stream) != hipSuccess)
       return fail(e, ZB_EDEVICE, "scan sizing");
@@ -1696,6 +1706,7 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
   if (fc && !e->reqs.empty()) HIPCHECK(e, e->d_reqs.upload(e->reqs, e->stream));
   SerParams sp{};
   sp.nt = e->ser_nt;
+  sp.exp = e->ser_exp;
   if (fc) {
     sp.frames = 1;
     sp.stream_id = fc->stream_id;
@@ -1740,6 +1751,7 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
     sp.out = e->dr_val;
     sp.out_cap = e->dr_val_cap;
     HIPCHECK(e, hipMemsetAsync(e->dr_total, 0, 4 * sizeof(uint64_t), e->stream));
+    e->dr_split = false;
     if (e->ser_mode == 1 && !fc) {  // one pass: decoupled look-back over 256-record tiles (values only)
       if ((++e->dr_epoch & 0x3ffff) == 0) {  // tile-state tags wrap: clear them once
         HIPCHECK(e, hipMemsetAsync(e->dr_tiles, 0, (e->dr_cap / 256 + 2) * sizeof(uint64_t), e->stream));
@@ -1768,7 +1780,22 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
       SerParams wr = sp;
       wr.lengths = e->dr_len;
       wr.tile_offs = e->dr_off;
-      launch_ser_write(wr, e->stream);
+      e->dr_split = e->ser_fast && !fc && sp.model_lds;
+      if (e->dr_split) {  // k_ser_fast, then k_ser_write over the tiles it left
+        wr.tile_list = e->dr_list;
+        wr.tile_list_n = (uint32_t*)(e->dr_total + 3);
+        launch_ser_fast(wr, e->stream);
+        HIPCHECK(e, hipEventRecord(e->dr_ev[4], e->stream));
+        HIPCHECK(e, hipMemcpyAsync(e->h_dr_total + 3, e->dr_total + 3, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+        HIPCHECK(e, hipStreamSynchronize(e->stream));
+        e->dr_slow_tiles = (uint32_t)e->h_dr_total[3];
+        HIPCHECK(e, hipEventRecord(e->dr_ev[5], e->stream));  // (the host round trip is not write-pass time)
+        launch_ser_write_list(wr, e->dr_slow_tiles, e->stream);
+        launch_ser_sum(wr, e->stream);
+      } else {
+        e->dr_slow_tiles = (uint32_t)tiles;
+        launch_ser_write(wr, e->stream);
+      }
       HIPCHECK(e, hipEventRecord(e->dr_ev[3], e->stream));
     }
     HIPCHECK(e, hipMemcpyAsync(e->h_dr_total, e->dr_total, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
@@ -1791,7 +1818,14 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
   }
   HIPCHECK(e, hipEventElapsedTime(&ms_size, e->dr_ev[0], e->dr_ev[1]));
   HIPCHECK(e, hipEventElapsedTime(&ms_scan, e->dr_ev[1], e->dr_ev[2]));
-  HIPCHECK(e, hipEventElapsedTime(&ms_write, e->dr_ev[2], e->dr_ev[3]));
+  if (e->dr_split) {  // fast pass + generic pass over its leftovers, without the host round trip between them
+    float a = 0, b = 0;
+    HIPCHECK(e, hipEventElapsedTime(&a, e->dr_ev[2], e->dr_ev[4]));
+    HIPCHECK(e, hipEventElapsedTime(&b, e->dr_ev[5], e->dr_ev[3]));
+    ms_write = a + b;
+  } else {
+    HIPCHECK(e, hipEventElapsedTime(&ms_write, e->dr_ev[2], e->dr_ev[3]));
+  }
   e->dr_count = count;
   e->dr_bytes = e->h_dr_total[0];
   e->dr_frames = fc != nullptr;
@@ -1801,6 +1835,7 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
   st.size_kernel_ms = ms_size;
   st.scan_ms = ms_scan;
   st.write_kernel_ms = ms_write;
+  st.generic_tiles = e->ser_mode == 1 && !fc ? 0 : e->dr_slow_tiles;
   st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (stats) *stats = st;
   return ZB_OK;

@@ -1,5 +1,5 @@
 // zb_fastenc.hpp — the drain write pass's fast value encoder (WORKFLOW_INSTANCE / JOB records into the LDS
-// image with 8-byte stores). Included by zb_serialize.hip; compiled for the host only by tests/native.
+// image). Included by zb_serialize.hip; compiled for the host only by tests/native.
 #pragma once
 #include <cstdint>
 
@@ -7,26 +7,63 @@
 
 namespace zbg {
 
-// The write pass's common records -- WORKFLOW_INSTANCE records of a deployed element and JOB records other
-// than CANCEL(ED) -- are encoded into the LDS image with 8-byte stores (gfx950 LDS takes unaligned
-// ds_write_b64): keys as immediates, integers assembled in a register, strings read from the LDS copy of the
-// pool, payload documents copied as 8-byte words. A store may run up to 7 bytes past the field it writes:
-// the fields after it (at least 8 bytes) overwrite them (same lane, LDS order). The value's trailing fields
-// are written exactly, so nothing lands past the value (the next lane's record). Same bytes as encode_value:
-// the GPU tests compare every value with the oracle's, tests/test_fastenc_host.py fuzzes this on the host
-// (guard bytes after each value).
+// The common records -- WORKFLOW_INSTANCE records of a deployed element and JOB records other than
+// CANCEL(ED) -- are encoded into the LDS image with ALIGNED stores only: a b64 / b32 DS access off its
+// natural alignment is replayed at 64 cycles per wave instruction on gfx950 (cdna_hip_programming.md, LDS
+// alignment), which made a byte-addressed 8-byte writer LDS-bound. The writer keeps the bytes of the
+// current 8-byte image slot in a register and stores the slot when it fills; the value's first slot (shared
+// with the previous lane's value) and its last one (shared with the next lane's) are written at the end with
+// naturally aligned b8 / b16 / b32 stores of exactly the value's bytes. Keys are immediates, integers are assembled in a register, strings are read
+// from the LDS copy of the pool with aligned b64 reads, payload documents are copied as 8-byte words.
+// Same bytes as encode_value: the GPU tests compare every value with the oracle's, and
+// tests/test_fastenc_host.py fuzzes this on the host with guard bytes around each value.
 struct FastW {
-  uint8_t* p;  // record start in the LDS image
-  uint32_t n;
-  __device__ __forceinline__ void st8(uint32_t o, uint64_t v) { __builtin_memcpy(p + o, &v, 8); }
-  __device__ __forceinline__ void exact(uint32_t o, uint64_t v, uint32_t L) {  // the low L <= 8 bytes of v
-    if (L == 8) { st8(o, v); return; }
-    if (L & 4) { const uint32_t x = (uint32_t)v; __builtin_memcpy(p + o, &x, 4); v >>= 32; o += 4; }
-    if (L & 2) { const uint16_t x = (uint16_t)v; __builtin_memcpy(p + o, &x, 2); v >>= 16; o += 2; }
-    if (L & 1) p[o] = (uint8_t)v;
+  uint8_t* img;   // LDS image base (8-aligned)
+  uint32_t pos;   // image offset of the next byte
+  uint32_t head;  // image offset of the value's first byte
+  uint64_t acc;   // the current slot's bytes below pos (low bytes first)
+  uint64_t first; // the first slot's word (stored by end(): its bytes below head are the previous value's)
+
+  __device__ __forceinline__ void begin(uint8_t* base, uint32_t at) {
+    img = base;
+    pos = head = at;
+    acc = 0;
+    first = 0;
   }
-  // N - 1 literal bytes (may hold NULs); EXACT: no store past them (the field after them may be 1 byte long)
-  template <bool EXACT = false, int N>
+  __device__ __forceinline__ uint32_t n() const { return pos - head; }
+  // bytes [b, e) of slot word v at image offset slot, with naturally aligned stores (0 <= b < e <= 8)
+  __device__ __forceinline__ void part(uint32_t slot, uint64_t v, uint32_t b, uint32_t e) {
+    if ((b & 1) && b < e) { img[slot + b] = (uint8_t)(v >> (8 * b)); b += 1; }
+    if ((b & 2) && b + 2 <= e) { *(uint16_t*)(img + slot + b) = (uint16_t)(v >> (8 * b)); b += 2; }
+    if ((b & 4) && b + 4 <= e) { *(uint32_t*)(img + slot + b) = (uint32_t)(v >> (8 * b)); b += 4; }
+    // b is now 0 / 4-aligned (head part done) or the tail remains: [b, e) from the low end
+    if (b + 4 <= e) { *(uint32_t*)(img + slot + b) = (uint32_t)(v >> (8 * b)); b += 4; }
+    if (b + 2 <= e) { *(uint16_t*)(img + slot + b) = (uint16_t)(v >> (8 * b)); b += 2; }
+    if (b < e) img[slot + b] = (uint8_t)(v >> (8 * b));
+  }
+  // append the low k bytes of v (1 <= k <= 8; v's other bytes zero)
+  __device__ __forceinline__ void put(uint64_t v, uint32_t k) {
+    const uint32_t f = pos & 7;
+    const uint64_t lo = acc | (v << (8 * f));
+    const uint64_t hi = f ? v >> (64 - 8 * f) : 0;
+    if (f + k >= 8) {
+      const uint32_t slot = pos - f;
+      if (slot < head) first = lo;  // the first slot: end() stores its bytes from head on
+      else *(uint64_t*)(img + slot) = lo;
+      acc = hi;
+    } else {
+      acc = lo;
+    }
+    pos += k;
+  }
+  // the first and the last slot's bytes (call once, after the last put; values of 16 bytes or more, so that
+  // the two are different slots -- WORKFLOW_INSTANCE and JOB values are over 80 bytes)
+  __device__ __forceinline__ void end() {
+    if (head & 7) part(head & ~7u, first, head & 7, 8);
+    if (pos & 7) part(pos & ~7u, acc, 0, pos & 7);
+  }
+  // N - 1 literal bytes (may hold NULs), as immediates
+  template <int N>
   __device__ __forceinline__ void lit(const char (&s)[N]) {
     constexpr int L = N - 1;
 #pragma unroll
@@ -35,45 +72,41 @@ struct FastW {
 #pragma unroll
       for (int k = 0; k < 8; k++)
         if (c + k < L) w |= (uint64_t)(uint8_t)s[c + k] << (8 * k);
-      if (EXACT && L - c < 8) exact(n + c, w, L - c);
-      else st8(n + c, w);
+      put(w, L - c < 8 ? L - c : 8);
     }
-    n += L;
   }
-  // MsgPackWriter.writeInteger (same ranges as W::integer)
-  __device__ __forceinline__ void ival(int64_t v, bool last = false) {
-    uint64_t w;
-    uint32_t L;
-    if (v >= -32 && v < 128) { w = (uint8_t)v; L = 1; }
-    else if (v >= 0) {
-      if (v < 256) { w = 0xcc | (uint64_t)v << 8; L = 2; }
-      else if (v < 65536) { w = 0xcd | (uint64_t)__builtin_bswap16((uint16_t)v) << 8; L = 3; }
-      else if (v < (1LL << 32)) { w = 0xce | (uint64_t)__builtin_bswap32((uint32_t)v) << 8; L = 5; }
-      else { w = 0xcf | __builtin_bswap64((uint64_t)v) << 8; L = 9; }
-    } else {
-      if (v >= -128) { w = 0xd0 | (uint64_t)(uint8_t)v << 8; L = 2; }
-      else if (v >= -32768) { w = 0xd1 | (uint64_t)__builtin_bswap16((uint16_t)v) << 8; L = 3; }
-      else if (v >= -(1LL << 31)) { w = 0xd2 | (uint64_t)__builtin_bswap32((uint32_t)v) << 8; L = 5; }
-      else { w = 0xd3 | __builtin_bswap64((uint64_t)v) << 8; L = 9; }
-    }
-    if (L == 9) { st8(n, w); p[n + 8] = (uint8_t)v; }
-    else if (last) exact(n, w, L);
-    else st8(n, w);
-    n += L;
+  // MsgPackWriter.writeInteger (same ranges as W::integer): a fixint, or a header byte (0xcc..0xcf unsigned,
+  // 0xd0..0xd3 signed, by width) and the low m = 1, 2, 4 or 8 bytes of v big-endian; one straight path
+  __device__ __forceinline__ void ival(int64_t v) {
+    const bool neg = v < 0;
+    const uint64_t mag = neg ? ~(uint64_t)v : (uint64_t)v;  // signed ranges are [-2^(8m-1), 2^(8m-1))
+    const bool fix = neg ? v >= -32 : v < 128;
+    const uint32_t lg = neg ? (mag < 0x80u ? 0 : mag < 0x8000u ? 1 : mag < 0x80000000ull ? 2 : 3)
+                            : (mag < 0x100u ? 0 : mag < 0x10000u ? 1 : mag < 0x100000000ull ? 2 : 3);
+    const uint32_t m = 1u << lg;
+    const uint64_t be = __builtin_bswap64((uint64_t)v << (64 - 8 * m));
+    if (fix) { put((uint8_t)v, 1); return; }
+    put(((neg ? 0xd0u : 0xccu) + lg) | be << 8, m < 8 ? m + 1 : 8);
+    if (m == 8) put((uint8_t)v, 1);
   }
-  __device__ __forceinline__ void raw(const uint8_t* s, uint32_t c) {  // s: LDS (reads may pass its end)
-    for (uint32_t k = 0; k < c; k += 8) {
-      uint64_t v;
-      __builtin_memcpy(&v, s + k, 8);
-      st8(n + k, v);
+  // c bytes at s (LDS, any alignment): aligned b64 reads (reads up to 7 bytes past the string)
+  __device__ __forceinline__ void raw(const uint8_t* s, uint32_t c) {
+    const uint32_t a = (uint32_t)((uintptr_t)s & 7);
+    const uint64_t* w = (const uint64_t*)(s - a);
+    uint64_t cur = w[0];
+    for (uint32_t k = 0, j = 1; k < c; k += 8, j++) {
+      const uint64_t nx = w[j];
+      const uint64_t v = a ? (cur >> (8 * a)) | (nx << (64 - 8 * a)) : cur;
+      const uint32_t r = c - k;
+      put(r < 8 ? v & (~0ull >> (64 - 8 * r)) : v, r < 8 ? r : 8);
+      cur = nx;
     }
-    n += c;
   }
   __device__ __forceinline__ void str(const uint8_t* s, uint32_t c) {  // MsgPackWriter.writeString
-    if (c < 32) { p[n] = (uint8_t)(0xa0 | c); n += 1; }
-    else if (c < 256) { st8(n, 0xd9 | (uint64_t)c << 8); n += 2; }
-    else if (c < 65536) { st8(n, 0xda | (uint64_t)__builtin_bswap16((uint16_t)c) << 8); n += 3; }
-    else { st8(n, 0xdb | (uint64_t)__builtin_bswap32(c) << 8); n += 5; }
+    if (c < 32) put(0xa0 | c, 1);
+    else if (c < 256) put(0xd9 | (uint64_t)c << 8, 2);
+    else if (c < 65536) put(0xda | (uint64_t)__builtin_bswap16((uint16_t)c) << 8, 3);
+    else put(0xdb | (uint64_t)__builtin_bswap32(c) << 8, 5);
     raw(s, c);
   }
 };
@@ -81,37 +114,32 @@ struct FastW {
 constexpr int SER_PRE = 6;  // payload document words prefetched per record (length + 44 bytes)
 
 // the payload document [u32 len][bytes] as binary (MsgPackWriter.writeBinary): doc words W_j (8-aligned), the
-// first SER_PRE already loaded; payload bytes [8k, 8k + 8) = W_k >> 32 | W_{k+1} << 32 (no read past the doc)
-__device__ __forceinline__ void fast_bin(FastW& w, const uint64_t* dw, const uint64_t (&pre)[SER_PRE], bool last) {
-  uint64_t cur = pre[0];
-  const uint32_t plen = (uint32_t)cur;
-  uint64_t h;
-  uint32_t hl;
-  if (plen < 256) { h = 0xc4 | (uint64_t)plen << 8; hl = 2; }
-  else if (plen < 65536) { h = 0xc5 | (uint64_t)__builtin_bswap16((uint16_t)plen) << 8; hl = 3; }
-  else { h = 0xc6 | (uint64_t)__builtin_bswap32(plen) << 8; hl = 5; }
-  if (last) w.exact(w.n, h, hl);  // (a short last payload ends within the 8 bytes after the header)
-  else w.st8(w.n, h);
-  w.n += hl;
+// first SER_PRE already loaded (words past the document hold whatever follows it: only bytes past the payload
+// come from them, and those are masked off); payload bytes [8k, 8k + 8) = W_k >> 32 | W_(k+1) << 32
+__device__ __forceinline__ void fast_bin(FastW& w, const uint64_t* dw, const uint64_t (&pre)[SER_PRE]) {
+  const uint32_t plen = (uint32_t)pre[0];
+  if (plen < 256) w.put(0xc4 | (uint64_t)plen << 8, 2);
+  else if (plen < 65536) w.put(0xc5 | (uint64_t)__builtin_bswap16((uint16_t)plen) << 8, 3);
+  else w.put(0xc6 | (uint64_t)__builtin_bswap32(plen) << 8, 5);
 #pragma unroll
   for (int j = 1; j < SER_PRE; j++) {
     const uint32_t k = 8 * (j - 1);
     if (k < plen) {
-      const uint64_t nx = k + 4 < plen ? pre[j] : 0;
+      const uint64_t v = (pre[j - 1] >> 32) | (pre[j] << 32);
+      const uint32_t r = plen - k;
+      w.put(r < 8 ? v & (~0ull >> (64 - 8 * r)) : v, r < 8 ? r : 8);
+    }
+  }
+  if (plen > 8 * (SER_PRE - 1)) {  // longer payloads: the rest from HBM (no load past the document)
+    uint64_t cur = pre[SER_PRE - 1];
+    for (uint32_t k = 8 * (SER_PRE - 1), j = SER_PRE; k < plen; k += 8, j++) {
+      const uint64_t nx = k + 4 < plen ? dw[j] : 0;
       const uint64_t v = (cur >> 32) | (nx << 32);
-      if (last && k + 8 > plen) w.exact(w.n + k, v, plen - k);
-      else w.st8(w.n + k, v);
+      const uint32_t r = plen - k;
+      w.put(r < 8 ? v & (~0ull >> (64 - 8 * r)) : v, r < 8 ? r : 8);
       cur = nx;
     }
   }
-  for (uint32_t k = 8 * (SER_PRE - 1), j = SER_PRE; k < plen; k += 8, j++) {
-    const uint64_t nx = k + 4 < plen ? dw[j] : 0;
-    const uint64_t v = (cur >> 32) | (nx << 32);
-    if (last && k + 8 > plen) w.exact(w.n + k, v, plen - k);
-    else w.st8(w.n + k, v);
-    cur = nx;
-  }
-  w.n += plen;
 }
 
 __device__ __forceinline__ bool fast_kind(const zb_rec& d) {
@@ -139,9 +167,9 @@ __device__ __forceinline__ void fast_encode(FastW& w, const zb_rec& d, const Dev
     w.lit("\xaa" "activityId");
     w.str(pool + e.id_off, e.id_len);
     w.lit("\xa7" "payload");
-    fast_bin(w, dw, pre, false);
-    w.lit<true>("\xb0" "scopeInstanceKey");  // (the value ends with a 1..9-byte integer)
-    w.ival(d.scope_key, true);
+    fast_bin(w, dw, pre);
+    w.lit("\xb0" "scopeInstanceKey");
+    w.ival(d.scope_key);
   } else {  // JobRecord.java:35-53 + JobHeaders.java:33-51
     w.lit("\x87\xa8" "deadline" "\xd3\x80\x00\x00\x00\x00\x00\x00\x00" "\xa6" "worker" "\xa0" "\xa7" "retries");
     w.ival(e.retries);
@@ -160,11 +188,12 @@ __device__ __forceinline__ void fast_encode(FastW& w, const zb_rec& d, const Dev
     w.lit("\xb3" "activityInstanceKey");
     w.ival(d.scope_key);
     w.lit("\xad" "customHeaders");
-    if (e.headers_off == NO_REF) { w.p[w.n] = 0x80; w.n += 1; }  // JobRecord.NO_HEADERS
+    if (e.headers_off == NO_REF) w.put(0x80, 1);  // JobRecord.NO_HEADERS
     else w.raw(pool + e.headers_off, e.headers_len);
     w.lit("\xa7" "payload");
-    fast_bin(w, dw, pre, true);
+    fast_bin(w, dw, pre);
   }
+  w.end();
 }
 
 }  // namespace zbg

@@ -510,7 +510,8 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
   __shared__ unsigned long long s_wsum[SER_WG / 64];
   __shared__ uint32_t s_maxlen;
   __shared__ unsigned long long s_wlo[SER_WINDOWS], s_whi[SER_WINDOWS];
-  const int64_t base = (int64_t)blockIdx.x * SER_WG;
+  const uint32_t tile = P0.tile_list ? P0.tile_list[blockIdx.x] : blockIdx.x;  // (the tiles k_ser_fast left)
+  const int64_t base = (int64_t)tile * SER_WG;
   const int64_t i = base + threadIdx.x;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool live = i < P0.count;
@@ -519,8 +520,8 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
   uint64_t o0, o1, off = 0, nxt = 0, x = 0;
   uint32_t len = 0;
   if (P0.tile_offs) {  // tile offsets + lengths: this tile's exclusive scan in registers / LDS
-    o0 = P0.tile_offs[blockIdx.x];
-    o1 = P0.tile_offs[blockIdx.x + 1];
+    o0 = P0.tile_offs[tile];
+    o1 = P0.tile_offs[tile + 1];
     if (live) len = P0.lengths[i];
   } else {
     const int64_t last = (base + SER_WG < P0.count) ? base + SER_WG : P0.count;
@@ -590,7 +591,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
   if (live) {
     if (fast) pay = (uint32_t)pre[0];
     else if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay = *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
-    if (!FRAMES) {
+    if (!FRAMES && !(P.exp & 4)) {
       const zb_record_header h = record_header(d, pos, len, off);
       if (NT) {
         const uint64_t* hw = (const uint64_t*)&h;
@@ -611,7 +612,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
       for (int k = 0; k < SER_WG / 64; k++) tt += s_pay[k];
       // one partial per workgroup, reduced by k_ser_sum: 400k same-address device atomics serialised the pass
       // (~2.4 ms of the empty pass on C3 10M, profiles/r02/ser_grid_sweep.txt)
-      P.pay_part[blockIdx.x] = tt;
+      P.pay_part[tile] = tt;
     }
   }
   // LDS offsets of the model tables (fast encoder: typed LDS reads)
@@ -619,14 +620,13 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
   const uint32_t wo = (eb + 15) & ~15u, po = wo + ((wb + 15) & ~15u);
   // the common case: a staged tile of fast records, encoded from the prefetched payload words
   if (!FRAMES && staged && __syncthreads_and(fast || !live)) {
-    if (live) {
+    if (live && !(P.exp & 1)) {
       FastW w;
-      w.p = img + shift + (uint32_t)(off - o0);
-      w.n = 0;
+      w.begin(img, shift + (uint32_t)(off - o0));
       fast_encode(w, d, (const DevElem*)s_model, (const DevWorkflow*)(s_model + wo), s_model + po, dw, pre);
     }
     __syncthreads();
-    stream_image(img, P.out, o0, shift, o1 - o0, NT);
+    if (!(P.exp & 2)) stream_image(img, P.out, o0, shift, o1 - o0, NT);
     return;
   }
   // otherwise the generic encoder in phases (one encode site keeps it inlined once): the whole tile staged,
@@ -675,6 +675,113 @@ __global__ void __launch_bounds__(256) k_ser_sum(SerParams P, int64_t nparts) {
   if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = x;
   __syncthreads();
   if (threadIdx.x == 0) atomicAdd((unsigned long long*)&P.totals[1], s[0] + s[1] + s[2] + s[3]);
+}
+
+
+// Fast write pass (values + headers, no frames): one workgroup per 256-record tile as k_ser_write, but the
+// LDS image holds ONE wave's records (64 values): the waves encode in turn and all four stream each wave's
+// range out. A workgroup then needs ~17 KB of LDS instead of 52 KB and a third of the registers, so several
+// times more tiles -- and their descriptor / payload loads -- are in flight per CU. Tiles with a record the
+// fast encoder does not take, or a wave range larger than the image, go to k_ser_write (tile_list).
+constexpr int SER_FIMG = 13 * 1024;
+__global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(6))) k_ser_fast(SerParams P0) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[SER_FIMG + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_model[SER_MODEL_LDS + 16];  // (+16: 8-byte reads past the pool)
+  __shared__ unsigned long long s_wsum[SER_WG / 64], s_pay[SER_WG / 64];
+  const uint32_t tile = blockIdx.x;
+  const int64_t base = (int64_t)tile * SER_WG;
+  const int64_t i = base + threadIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool live = i < P0.count;
+  const uint64_t o0 = P0.tile_offs[tile], o1 = P0.tile_offs[tile + 1];
+  const uint32_t len = live ? P0.lengths[i] : 0;
+  zb_rec d{};
+  if (live) d = P0.log[P0.start + i];
+  const bool fast = live && fast_kind(d);
+  const uint64_t* dw = (const uint64_t*)(P0.arena + (uint64_t)d.payload * 8);
+  uint64_t pre[SER_PRE];
+#pragma unroll
+  for (int j = 0; j < SER_PRE; j++)
+    pre[j] = (fast && (uint64_t)d.payload * 8 + 8 * j + 8 <= P0.arena_bytes) ? dw[j] : 0;
+  uint64_t x = len;
+#pragma unroll
+  for (int k = 1; k < 64; k <<= 1) {
+    const uint64_t y = (uint64_t)__shfl_up((unsigned long long)x, k, 64);
+    if (lane >= k) x += y;
+  }
+  if (lane == 63) s_wsum[wv] = x;
+  // the model tables into LDS (their barrier is the vote's)
+  const uint32_t eb = (uint32_t)P0.n_elems * (uint32_t)sizeof(DevElem), wb = (uint32_t)P0.n_wfs * (uint32_t)sizeof(DevWorkflow);
+  const uint32_t wo = (eb + 15) & ~15u, po = wo + ((wb + 15) & ~15u);
+  for (uint32_t c = threadIdx.x; c < eb / 16; c += SER_WG) ((uint4*)s_model)[c] = ((const uint4*)P0.elems)[c];
+  for (uint32_t c = threadIdx.x; c < wb / 16; c += SER_WG) ((uint4*)(s_model + wo))[c] = ((const uint4*)P0.wfs)[c];
+  for (uint32_t c = threadIdx.x; c < P0.pool_len; c += SER_WG) s_model[po + c] = P0.pool[c];
+  const bool all_fast = __syncthreads_and(fast || !live);
+  bool fits = true;
+#pragma unroll
+  for (int k = 0; k < SER_WG / 64; k++) fits = fits && s_wsum[k] + 16 <= (uint64_t)SER_FIMG;
+  if (P0.out_cap && o1 > P0.out_cap) {  // does not fit: the host grows the buffer and runs the pass again
+    if (threadIdx.x == 0) atomicOr(P0.overflow, 1u);
+    return;
+  }
+  if (!all_fast || !fits) {  // k_ser_write takes this tile
+    if (threadIdx.x == 0) P0.tile_list[atomicAdd(P0.tile_list_n, 1u)] = tile;
+    return;
+  }
+  uint64_t pw = 0;
+#pragma unroll
+  for (int k = 0; k < SER_WG / 64; k++)
+    if (k < wv) pw += s_wsum[k];
+  const uint64_t off = o0 + pw + x - len;
+  if (live && !(P0.exp & 4)) {
+    const zb_record_header h = record_header(d, P0.start + i, len, off);
+    const uint64_t* hw = (const uint64_t*)&h;
+    uint64_t* dh = (uint64_t*)(P0.headers + i);
+    for (int k = 0; k < 5; k++) __builtin_nontemporal_store(hw[k], dh + k);
+  }
+  if (P0.totals) {
+    unsigned long long y = live ? (uint32_t)pre[0] : 0;
+    for (int dd = 32; dd >= 1; dd >>= 1) y += __shfl_down(y, dd, 64);
+    if (lane == 0) s_pay[wv] = y;
+  }
+  // phase k: wave k encodes its values into the image, then all four waves stream them out. Each wave runs
+  // the phases before its own, its own (the encoder sits outside any loop: no constants hoisted into
+  // registers for the whole kernel), then the rest -- the same barriers in the same order for every wave.
+  auto stream_wave = [&](int k) {
+    uint64_t lo = o0;
+    for (int j = 0; j < k; j++) lo += s_wsum[j];
+    const uint32_t sh = (uint32_t)(((uintptr_t)(P0.out + lo)) & 15);
+    __syncthreads();
+    if (!(P0.exp & 2)) stream_image(img, P0.out, lo, sh, s_wsum[k], true);
+    __syncthreads();  // the image is reused by the next wave
+  };
+#pragma unroll 1
+  for (int k = 0; k < wv; k++) stream_wave(k);
+  if (live && !(P0.exp & 1)) {
+    const uint64_t lo = o0 + pw;  // this wave's range starts at the tile start + the waves before it
+    FastW w;
+    w.begin(img, (uint32_t)(((uintptr_t)(P0.out + lo)) & 15) + (uint32_t)(off - lo));
+    fast_encode(w, d, (const DevElem*)s_model, (const DevWorkflow*)(s_model + wo), s_model + po, dw, pre);
+  }
+  stream_wave(wv);
+#pragma unroll 1
+  for (int k = wv + 1; k < SER_WG / 64; k++) stream_wave(k);
+  if (P0.totals && threadIdx.x == 0) P0.pay_part[tile] = s_pay[0] + s_pay[1] + s_pay[2] + s_pay[3];
+}
+
+void launch_ser_fast(const SerParams& p, hipStream_t s) {
+  if (p.count <= 0) return;
+  hipLaunchKernelGGL(k_ser_fast, dim3((unsigned)((p.count + SER_WG - 1) / SER_WG)), dim3(SER_WG), 0, s, p);
+}
+void launch_ser_write_list(const SerParams& p, uint32_t n, hipStream_t s) {
+  if (n == 0) return;
+  if (p.nt) hipLaunchKernelGGL((k_ser_write<false, true>), dim3(n), dim3(SER_WG), 0, s, p);
+  else hipLaunchKernelGGL((k_ser_write<false, false>), dim3(n), dim3(SER_WG), 0, s, p);
+}
+void launch_ser_sum(const SerParams& p, hipStream_t s) {
+  const int64_t tiles = (p.count + SER_WG - 1) / SER_WG;
+  if (p.count > 0 && p.totals)
+    hipLaunchKernelGGL(k_ser_sum, dim3((unsigned)std::min<int64_t>(256, (tiles + 255) / 256)), dim3(256), 0, s, p, tiles);
 }
 
 // ------------------------------------------------------------------------------ single pass (zb_serialize)

@@ -76,7 +76,8 @@ class zb_frame_config(ctypes.Structure):
 class zb_serialize_stats(ctypes.Structure):
     _fields_ = [("records", ctypes.c_uint64), ("value_bytes", ctypes.c_uint64), ("payload_bytes", ctypes.c_uint64),
                 ("size_kernel_ms", ctypes.c_double), ("scan_ms", ctypes.c_double),
-                ("write_kernel_ms", ctypes.c_double), ("wall_ms", ctypes.c_double)]
+                ("write_kernel_ms", ctypes.c_double), ("wall_ms", ctypes.c_double),
+                ("generic_tiles", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
