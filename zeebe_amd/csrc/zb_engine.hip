@@ -238,6 +238,7 @@ struct zb_engine {
   uint32_t dr_slow_tiles = 0;    // how many tiles the last drain ran through k_ser_write
   bool dr_split = false;         // the last drain ran k_ser_fast + k_ser_write (events 2-4, 5-3)
   int ser_fast = 1;              // ZB_SER_FAST=0: every tile through k_ser_write
+  int ser_lenbuf = 0;            // ZB_SER_LENBUF=1: value lengths through their own buffer, not vlen
   zb_record_header* dr_hdr = nullptr;
   uint8_t* dr_val = nullptr;
   bool dr_frames = false;       // the drain batch holds log frames (no headers)
@@ -465,6 +466,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   *e->h_ctl_pinned = c;
   HIPCHECK(e, hipMemcpyAsync(e->t_ctl, e->h_ctl_pinned, sizeof(TrajCtl), hipMemcpyHostToDevice, e->stream));
   TrajParams p{};
+  if (const char* x = std::getenv("ZB_TMPL_EXP")) p.texp = atoi(x);  // (measurement only: wrong logs)
   p.log = e->log;
   p.vconst = e->d_vconst.p;
   p.srcd = e->srcd;
@@ -669,6 +671,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (const char* m = std::getenv("ZB_SER_NT")) e->ser_nt = atoi(m);
   if (const char* m = std::getenv("ZB_SER_EXP")) e->ser_exp = atoi(m);
   if (const char* m = std::getenv("ZB_SER_FAST")) e->ser_fast = atoi(m);
+  if (const char* m = std::getenv("ZB_SER_LENBUF")) e->ser_lenbuf = atoi(m);
   if (const char* g = std::getenv("ZB_WAVE_GRID")) e->wave_grid_fixed = std::max(0, std::min(atoi(g), (int)WAVE_GRID_MAX));
   if (e->cfg.log_capacity == 0) e->cfg.log_capacity = 1ull << 22;
   if (e->cfg.row_capacity == 0) e->cfg.row_capacity = 1ull << 20;
@@ -1768,6 +1771,9 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
       const int64_t tiles = (count + 255) / 256;
       SerParams sz = sp;
       sz.lengths = e->dr_len;
+      // values: lengths in vlen (measured ones filled in); frames (and ZB_SER_LENBUF=1): lengths[]
+      sz.len_in_vlen = (fc || e->ser_lenbuf) ? 0 : 1;
+      sz.vlen_out = e->vlen;
       sz.tile_sums = e->dr_tsum;  // tiles + 1 entries, the last one 0: the scan's last output is the total
       HIPCHECK(e, hipEventRecord(e->dr_ev[0], e->stream));
       launch_ser_size(sz, e->stream);
@@ -1779,6 +1785,7 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
       HIPCHECK(e, hipEventRecord(e->dr_ev[2], e->stream));
       SerParams wr = sp;
       wr.lengths = e->dr_len;
+      wr.len_in_vlen = sz.len_in_vlen;
       wr.tile_offs = e->dr_off;
       e->dr_split = e->ser_fast && !fc && sp.model_lds;
       if (e->dr_split) {  // k_ser_fast, then k_ser_write over the tiles it left
