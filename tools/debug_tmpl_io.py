@@ -1,0 +1,37 @@
+"""Debug aid: C3 with n instances through the instance-order and the class-uniform emit; prints the first
+descriptor / record differences."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from zeebe_amd import workloads  # noqa: E402
+
+
+def run(io, n):
+    os.environ["ZB_TMPL_IO"] = str(io)
+    os.environ["ZB_VLEN_CHECK"] = "0"
+    from zeebe_amd.engine import Engine
+    cfg = workloads.CONFIGS["c3"]
+    blob, offs = cfg["payloads"](n)
+    e = Engine()
+    e.deploy(cfg["workflow"]().to_xml(), 100, 1)
+    e.create(cfg["process"], workloads.split(blob, offs))
+    st = e.step()
+    d = e.descriptors()
+    recs = e.records()
+    e.close()
+    return st, d, recs
+
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+s1, d1, r1 = run(1, n)
+s0, d0, r0 = run(0, n)
+print("stats io", {k: s1[k] for k in ("transitions", "records_written", "path")}, "cls", {k: s0[k] for k in ("transitions", "records_written", "path")})
+bad = 0
+for i in range(min(len(d0), len(d1))):
+    if d0[i].tobytes() != d1[i].tobytes() or r0[i] != r1[i]:
+        print(i, "cls", d0[i], r0[i].value[:60], "\n   io ", d1[i], r1[i].value[:60], r1[i].source_position)
+        bad += 1
+        if bad > 6:
+            break
+print("len", len(d0), len(d1), "bad", bad)

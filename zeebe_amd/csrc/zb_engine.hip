@@ -238,6 +238,7 @@ struct zb_engine {
   uint32_t dr_slow_tiles = 0;    // how many tiles the last drain ran through k_ser_write
   bool dr_split = false;         // the last drain ran k_ser_fast + k_ser_write (events 2-4, 5-3)
   int ser_fast = 1;              // ZB_SER_FAST=0: every tile through k_ser_write
+  int tmpl_io = 0;               // ZB_TMPL_IO=1: class batches emitted in instance order (k_tmpl_io; in progress)
   int ser_lenbuf = 0;            // ZB_SER_LENBUF=1: value lengths through their own buffer, not vlen
   zb_record_header* dr_hdr = nullptr;
   uint8_t* dr_val = nullptr;
@@ -499,12 +500,14 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   if (p.cls) {
     int grc = grow_class_buffers(e, (uint64_t)n, nwg);
     if (grc != ZB_OK) return grc;
-    // every (block, class) segment padded to whole waves; a multiple of 8 workgroups (XCD mapping)
-    p.nwg_e = (int32_t)(((cls_slot_bound((uint64_t)n, nwg) + TRAJ_WG - 1) / TRAJ_WG + 7) & ~7ull);
+    // instance-order emit (k_tmpl_io) over the instance workgroups; ZB_TMPL_IO=0: class-uniform emit, every
+    // (block, class) segment padded to whole waves, a multiple of 8 workgroups (XCD mapping)
+    p.io = e->tmpl_io;
+    if (!p.io) p.nwg_e = (int32_t)(((cls_slot_bound((uint64_t)n, nwg) + TRAJ_WG - 1) / TRAJ_WG + 7) & ~7ull);
     p.nblk = (int32_t)((nwg + CLS_BLK_WG - 1) / CLS_BLK_WG);
     p.segs = e->c_segs;
     p.wcls = e->c_wcls;
-    HIPCHECK(e, hipMemsetAsync(e->c_perm, 0xff, cls_slot_bound((uint64_t)n, nwg) * sizeof(uint32_t), e->stream));
+    if (!p.io) HIPCHECK(e, hipMemsetAsync(e->c_perm, 0xff, cls_slot_bound((uint64_t)n, nwg) * sizeof(uint32_t), e->stream));
     p.nsplits = e->nsplits;
     for (int k = 0; k < CLS_MAX_SPLITS; k++) {
       p.split_elem[k] = e->split_elem[k];
@@ -671,6 +674,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (const char* m = std::getenv("ZB_SER_NT")) e->ser_nt = atoi(m);
   if (const char* m = std::getenv("ZB_SER_EXP")) e->ser_exp = atoi(m);
   if (const char* m = std::getenv("ZB_SER_FAST")) e->ser_fast = atoi(m);
+  if (const char* m = std::getenv("ZB_TMPL_IO")) e->tmpl_io = atoi(m);
   if (const char* m = std::getenv("ZB_SER_LENBUF")) e->ser_lenbuf = atoi(m);
   if (const char* g = std::getenv("ZB_WAVE_GRID")) e->wave_grid_fixed = std::max(0, std::min(atoi(g), (int)WAVE_GRID_MAX));
   if (e->cfg.log_capacity == 0) e->cfg.log_capacity = 1ull << 22;

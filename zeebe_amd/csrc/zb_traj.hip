@@ -1647,6 +1647,165 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
   if (derr) atomicOr(&ctl->derr, derr);
 }
 
+// Class batches in instance order (the default): lane = instance, as the log orders them, each lane
+// following its own class's trace (the loops run to the wave's longest class; lanes of other classes are
+// masked). In generation w the wave's 64 instances own ONE contiguous log range (pos0(i + 1) = pos0(i) +
+// records of i), so each lane stages its descriptors / source deltas / value lengths in the wave's slice of
+// the merge workspace and the wave writes the range out with whole-line 16-byte stores. The class-uniform
+// emit (k_tmpl<true>, ZB_TMPL_IO=0) wrote each record from its own lane: a wave's lanes sit among the
+// other classes' instances, every store instruction touched ~64 partly written lines, and the L2 write
+// requests, not HBM, bounded the launch (profiles/r02/tmpl_store_exp.txt).
+template <bool GEN>
+__global__ void __launch_bounds__(TWG) k_tmpl_io(TrajParams P) {
+  using TL = TmLayout<true>;
+  static_assert(64 * TL::STRIDE * 4 >= 64 * TF * (32 + 4 + 4), "staging fits the wave's merge workspace");
+  __shared__ uint32_t s_merge[TWG * TL::STRIDE];
+  __shared__ uint64_t s_scan[TWG / 64][2];
+  TrajCtl* ctl = P.ctl;
+  if (ctl->flag) return;
+  if (GEN && !ctl->regen) return;
+  const int lane = threadIdx.x & 63;
+  int64_t inst = (int64_t)blockIdx.x * TWG + threadIdx.x;
+  const bool active = inst < P.n;
+  if (!active) inst = P.n - 1;  // (follows the last instance, writes nothing)
+  TmplLane L;
+  L.ncls = __builtin_amdgcn_readfirstlane(P.plan->nc);
+  uint32_t cls = 0;
+  {
+    const uint64_t grp = (uint64_t)(inst >> 6) * CLS_MAX;
+    const uint32_t bit = (uint32_t)(inst & 63);
+    const uint64_t lt = (1ull << bit) - 1;
+#pragma unroll
+    for (int c = 0; c < CLS_MAX; c++) {
+      const uint64_t m = c < (int)L.ncls ? P.cmask[grp + c] : 0;
+      L.before[c] = c < (int)L.ncls ? P.woffw[grp + c] + (uint32_t)__builtin_popcountll(m & lt) : 0;
+      if ((m >> bit) & 1) cls = (uint32_t)c;
+    }
+  }
+  const uint32_t crow = cls * CLS_ROW;
+  const int W = active ? (int)P.wcount[cls] : 0;
+  int Wmax = W;
+  for (int d = 32; d >= 1; d >>= 1) Wmax = max(Wmax, __shfl_xor(Wmax, d, 64));
+  const uint32_t create_ref = P.log[P.log_base + inst].payload;
+  uint32_t err = 0;
+  uint64_t merge_bytes = 0;
+  uint32_t pc_sym = PAY_CREATE, pc_ref = create_ref;  // last resolved payload symbol
+  const uint32_t create_len = arena_len(P.arena, create_ref);
+  uint32_t pc_len = create_len;
+  uint32_t* reg = s_merge + threadIdx.x * TL::STRIDE;
+  uint8_t* stage = (uint8_t*)(s_merge + (threadIdx.x & ~63) * TL::STRIDE);  // the wave's slice
+  zb_rec* s_desc = (zb_rec*)stage;
+  uint32_t* s_srcd = (uint32_t*)(stage + 64 * TF * 32);
+  uint32_t* s_vlen = s_srcd + 64 * TF;
+  int64_t prev0 = P.log_base + inst;  // the instance's first record of the previous generation (the CREATE)
+
+#pragma unroll 1
+  for (int w = 0; w < Wmax; w++) {
+    const bool live = w < W;
+    const TrajBase wb = kload(P.wbase, (uint64_t)w);
+    int64_t po = 0, pw = 0, pj = 0;
+#pragma unroll
+    for (int c = 0; c < CLS_MAX; c++) {
+      if (c >= (int)L.ncls) break;
+      const uint64_t n = kload(P.agg, (uint64_t)c * CLS_ROW + w);
+      po += (int64_t)L.before[c] * (int64_t)(n & 0xffff);
+      pw += (int64_t)L.before[c] * (int64_t)((n >> 16) & 0xffff);
+      pj += (int64_t)L.before[c] * (int64_t)(n >> 32);
+    }
+    const int64_t pos0 = wb.pos + po, kwf = wb.wf + pw, kjob = wb.job + pj;
+    const uint32_t nrec = live ? (uint32_t)(P.agg[(uint64_t)crow + w] & 0xffff) : 0;
+    uint32_t merged_ref = 0, merged_len = 0;
+    const MergeGen g = live ? P.mgen[(uint64_t)crow + w] : MergeGen{};
+    if (g.has) {
+      uint32_t src = g.src, tgt = g.tgt;
+      if (src == PAY_CREATE) src = create_ref;
+      else if (src & PAY_MERGE) src = (uint32_t)(tmpl_mslot(P, L, src & 0xffff) >> 3);
+      if (tgt == pc_sym) tgt = pc_ref;
+      else if (tgt == PAY_CREATE) tgt = create_ref;
+      else if (tgt & PAY_MERGE) tgt = (uint32_t)(tmpl_mslot(P, L, tgt & 0xffff) >> 3);
+      const uint64_t at = tmpl_mslot(P, L, (uint32_t)w);
+      merged_ref = (uint32_t)(at >> 3);
+      const uint32_t m_len = arena_len(P.arena, src) + arena_len(P.arena, tgt) + 8;
+      if (tblob_bytes(m_len) > g.stride) err |= DE_UNSUPPORTED;
+      else if (at + g.stride > P.arena_cap) err |= DE_ARENA_FULL;
+      else {
+        uint32_t ns = 0, nt = 0, olen = 0;
+        merge_into<GEN, TL::OUT_WORDS, TL::IN_WORDS>(P, src, tgt, m_len, at, reg, err, ns, nt, olen);
+        merge_bytes += ns + nt + olen;
+        merged_len = olen;
+      }
+    }
+    // the wave's range of this generation: [base, base + span)
+    uint32_t span = nrec;
+    for (int d = 32; d >= 1; d >>= 1) span += __shfl_xor(span, d, 64);
+    const int64_t base = __shfl(pos0, 0, 64);  // lane 0 is an active instance whenever span > 0
+    const uint32_t rel = (uint32_t)(pos0 - base);
+#pragma unroll 1
+    for (uint32_t k = 0; k < nrec; k++) {
+      const TmplRec t = P.tmpl[((uint64_t)crow + w) * TF + k];
+      zb_rec d;
+      d.key = tmpl_key(P, L, t.key, (uint32_t)w, kwf, kjob);
+      d.scope_key = t.scope == SYM_CMDPOS ? P.log_base + inst : tmpl_key(P, L, t.scope, (uint32_t)w, kwf, kjob);
+      d.inst_key = tmpl_key(P, L, t.inst, (uint32_t)w, kwf, kjob);
+      uint32_t pay = t.payload, plen;
+      if (pay == (PAY_MERGE | (uint32_t)w)) { pay = merged_ref; plen = merged_len; }
+      else if (pay == pc_sym) { pay = pc_ref; plen = pc_len; }
+      else if (pay == PAY_CREATE) { pay = create_ref; plen = create_len; }
+      else if (pay & PAY_MERGE) {
+        const uint32_t r = (uint32_t)(tmpl_mslot(P, L, pay & 0xffff) >> 3);
+        plen = arena_len(P.arena, r);
+        pc_sym = pay;
+        pc_ref = r;
+        pc_len = plen;
+        pay = r;
+      } else {
+        plen = arena_len(P.arena, pay);  // a static blob (shared by every instance: cached)
+      }
+      if (t.payload & PAY_MERGE) { pc_sym = t.payload; pc_ref = pay; pc_len = plen; }
+      d.payload = pay;
+      d.elem = t.elem; d.intent = t.intent; d.kind = t.kind;
+      // the value's length (zb_serialize.hip encode_value) from the element's constants and the variable fields
+      const uint8_t vt = kind_vt(d.kind), rt = kind_rt(d.kind);
+      uint32_t vl = VLEN_UNKNOWN;
+      if (!(d.kind & KIND_RAW) && ((vt == ZB_VT_WORKFLOW_INSTANCE && rt == ZB_RT_EVENT) ||
+                                   (vt == ZB_VT_JOB && (d.intent | 1) != JI_CANCELED))) {
+        const ValueConst vc = kload(P.vconst, (uint64_t)d.elem);
+        vl = (vt == ZB_VT_JOB ? vc.job : vc.wf) + mp_int_len(d.inst_key) + mp_int_len(d.scope_key) + mp_bin_len(plen);
+      }
+      s_desc[rel + k] = d;
+      s_srcd[rel + k] = (uint32_t)(pos0 + k - (prev0 + t.pad[0]));
+      s_vlen[rel + k] = vl;
+    }
+    if (live) prev0 = pos0;
+    // the wave's range out in whole lines (records past the log's capacity are an error, not written)
+    if (span) {
+      uint32_t fit = span;
+      if (base + span > (int64_t)P.log_cap) {
+        fit = base < (int64_t)P.log_cap ? (uint32_t)((int64_t)P.log_cap - base) : 0;
+        err |= DE_LOG_FULL;
+      }
+      uint4* dst = (uint4*)(P.log + base);
+      for (uint32_t c = lane; c < 2 * fit; c += 64) dst[c] = ((const uint4*)s_desc)[c];
+      for (uint32_t c = lane; c < fit; c += 64) {
+        P.srcd[base + c] = s_srcd[c];
+        P.vlen[base + c] = s_vlen[c];
+      }
+    }
+  }
+  // statistics: everything but the merge bytes is a per-class constant (k_traj_commit)
+  uint64_t s0 = active ? merge_bytes : 0, s1 = 0, t0, t1;
+  block_scan2(s0, s1, t0, t1, s_scan);
+  if (threadIdx.x == 0) {
+    uint64_t* ws = P.wstats + (uint64_t)blockIdx.x * 6;
+    ws[0] = ws[1] = ws[2] = ws[3] = ws[5] = 0;
+    ws[4] = t0;
+  }
+  if (!active) err &= DE_LOG_FULL;  // (the range copy is the wave's: an inactive lane may see its overflow)
+  if (err & TE_REGEN) atomicOr(&ctl->regen, 1u);
+  const uint32_t derr = err & ~(uint32_t)(TE_FALLBACK | TE_REGEN);
+  if (derr) atomicOr(&ctl->derr, derr);
+}
+
 // conditions are compiled into the count / emit kernels only when the model has exclusive splits
 // (a uniform batch never has any), keeping the condition VM's call frame out of the other variants
 void launch_traj_count(const TrajParams& p, hipStream_t s) {
@@ -1666,8 +1825,10 @@ void launch_traj_count_classes(const TrajParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_cls_plan, dim3(1), dim3(256), 0, s, p);
   hipLaunchKernelGGL(k_cls_masks, dim3(p.nwg), dim3(TWG), 0, s, p);
   hipLaunchKernelGGL(k_cls_scan, dim3(CLS_MAX), dim3(1024), 0, s, p);
-  hipLaunchKernelGGL(k_cls_segs, dim3(1), dim3(1024), 0, s, p);
-  hipLaunchKernelGGL(k_cls_perm, dim3(p.nwg), dim3(TWG), 0, s, p);
+  if (!p.io) {  // the class-uniform emit's slot layout
+    hipLaunchKernelGGL(k_cls_segs, dim3(1), dim3(1024), 0, s, p);
+    hipLaunchKernelGGL(k_cls_perm, dim3(p.nwg), dim3(TWG), 0, s, p);
+  }
   hipLaunchKernelGGL((k_traj<false, false, false, false, true, true>), dim3(1), dim3(TWG), 0, s, p);
 }
 void launch_traj_scan(const TrajParams& p, hipStream_t s) {
@@ -1679,7 +1840,13 @@ void launch_traj_emit(const TrajParams& p, hipStream_t s, hipEvent_t* ev_main) {
   auto mark = [&](int i) {
     if (ev_main) (void)hipEventRecord(ev_main[i], s);
   };
-  if (p.cls) {
+  if (p.cls && p.io) {  // instance order (default)
+    mark(0);
+    hipLaunchKernelGGL((k_tmpl_io<false>), g, b, 0, s, p);
+    mark(1);
+    hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
+    hipLaunchKernelGGL((k_tmpl_io<true>), g, b, 0, s, p);
+  } else if (p.cls) {
     const dim3 ge(p.nwg_e);
     mark(0);
     hipLaunchKernelGGL((k_tmpl<true, false>), ge, b, 0, s, p);
