@@ -19,6 +19,7 @@ def run(io, n):
     st = e.step()
     d = e.descriptors()
     recs = e.records()
+    print("io", io, "counters", e.counters())
     e.close()
     return st, d, recs
 
@@ -35,3 +36,5 @@ for i in range(min(len(d0), len(d1))):
         if bad > 6:
             break
 print("len", len(d0), len(d1), "bad", bad)
+print("CREATE payload refs io", [int(x) for x in d1["payload"][:3]], "cls", [int(x) for x in d0["payload"][:3]])
+print("first emitted io", d1[n:n + 4], "\ncls", d0[n:n + 4])

@@ -443,9 +443,19 @@ class Engine:
         if n:
             ck_off[1:] = np.cumsum([len(c) for c in correlation_keys])
             pl_off[1:] = np.cumsum([len(p) for p in payloads])
-        ckb = ctypes.create_string_buffer(b"".join(correlation_keys), max(int(ck_off[-1]), 1))
-        plb = ctypes.create_string_buffer(b"".join(payloads), max(int(pl_off[-1]), 1))
-        self._check(self._L.zb_submit_publishes(self._h, name, ttl, n, ckb, ck_off.ctypes.data, plb,
+        self.publish_packed(name, b"".join(correlation_keys), ck_off, b"".join(payloads), pl_off, ttl)
+
+    def publish_packed(self, name: bytes, ck_blob: bytes, ck_off, pl_blob: bytes, pl_off, ttl: int = 3600000):
+        """publish() with the batch already packed: message i has correlation key ck_blob[ck_off[i]:ck_off[i+1]]
+        and payload pl_blob[pl_off[i]:pl_off[i+1]] (offsets: n + 1 uint64, numpy)."""
+        import numpy as np
+
+        if isinstance(name, str):
+            name = name.encode()
+        ck_off = np.ascontiguousarray(ck_off, dtype=np.uint64)
+        pl_off = np.ascontiguousarray(pl_off, dtype=np.uint64)
+        n = len(ck_off) - 1
+        self._check(self._L.zb_submit_publishes(self._h, name, ttl, n, ck_blob, ck_off.ctypes.data, pl_blob,
                                                 pl_off.ctypes.data))
 
     def counters(self) -> dict:
