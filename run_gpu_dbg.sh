@@ -1,4 +1,4 @@
 #!/bin/bash
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
 mkdir -p gpurun_out/dbg
-timeout -k 5 120 python3 tools/debug_tmpl_io.py 300 > gpurun_out/dbg/io300.txt 2>&1; echo "rc=$?"; head -30 gpurun_out/dbg/io300.txt
+timeout -k 5 200 python3 tools/debug_tmpl_io.py probe 65 > gpurun_out/dbg/survey.txt 2>&1; echo "rc=$?"; cat gpurun_out/dbg/survey.txt | tail -12

@@ -19,11 +19,17 @@ def run(io, n):
     st = e.step()
     d = e.descriptors()
     recs = e.records()
-    print("io", io, "counters", e.counters())
     e.close()
     return st, d, recs
 
 
+if len(sys.argv) > 2:  # survey: bad descriptor counts for several sizes
+    for n in map(int, sys.argv[1:]):
+        _, a, _ = run(1, n)
+        _, b, _ = run(0, n)
+        bad = [i for i in range(len(b)) if a[i].tobytes() != b[i].tobytes()]
+        print("n", n, "bad", len(bad), "first", bad[:3], "payload io/cls", [(int(a[i]["payload"]), int(b[i]["payload"])) for i in bad[:2]])
+    sys.exit(0)
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 s1, d1, r1 = run(1, n)
 s0, d0, r0 = run(0, n)

@@ -238,7 +238,7 @@ struct zb_engine {
   uint32_t dr_slow_tiles = 0;    // how many tiles the last drain ran through k_ser_write
   bool dr_split = false;         // the last drain ran k_ser_fast + k_ser_write (events 2-4, 5-3)
   int ser_fast = 1;              // ZB_SER_FAST=0: every tile through k_ser_write
-  int tmpl_io = 0;               // ZB_TMPL_IO=1: class batches emitted in instance order (k_tmpl_io; in progress)
+  int tmpl_io = 0;               // ZB_TMPL_IO=1: class batches emitted in instance order (k_tmpl_io)
   int ser_lenbuf = 0;            // ZB_SER_LENBUF=1: value lengths through their own buffer, not vlen
   zb_record_header* dr_hdr = nullptr;
   uint8_t* dr_val = nullptr;

@@ -41,15 +41,16 @@ struct FastW {
     if (b + 2 <= e) { *(uint16_t*)(img + slot + b) = (uint16_t)(v >> (8 * b)); b += 2; }
     if (b < e) img[slot + b] = (uint8_t)(v >> (8 * b));
   }
-  // append the low k bytes of v (1 <= k <= 8; v's other bytes zero)
+  // append the low k bytes of v (1 <= k <= 8; v's other bytes zero). FIRST: the value's first put (8 bytes):
+  // the slot it completes is the head slot, which end() stores; every later slot is the value's alone
+  template <bool FIRST = false>
   __device__ __forceinline__ void put(uint64_t v, uint32_t k) {
     const uint32_t f = pos & 7;
     const uint64_t lo = acc | (v << (8 * f));
-    const uint64_t hi = f ? v >> (64 - 8 * f) : 0;
+    const uint64_t hi = (v >> 1) >> (63 - 8 * f);  // the bytes past the slot (0 when f == 0)
     if (f + k >= 8) {
-      const uint32_t slot = pos - f;
-      if (slot < head) first = lo;  // the first slot: end() stores its bytes from head on
-      else *(uint64_t*)(img + slot) = lo;
+      if (FIRST && f) first = lo;
+      else *(uint64_t*)(img + (pos - f)) = lo;
       acc = hi;
     } else {
       acc = lo;
@@ -62,17 +63,19 @@ struct FastW {
     if (head & 7) part(head & ~7u, first, head & 7, 8);
     if (pos & 7) part(pos & ~7u, acc, 0, pos & 7);
   }
-  // N - 1 literal bytes (may hold NULs), as immediates
-  template <int N>
+  // N - 1 literal bytes (may hold NULs), as immediates; FIRST: the value starts with them (N - 1 >= 8)
+  template <bool FIRST = false, int N>
   __device__ __forceinline__ void lit(const char (&s)[N]) {
     constexpr int L = N - 1;
+    static_assert(!FIRST || L >= 8, "the first put is a whole 8-byte chunk");
 #pragma unroll
     for (int c = 0; c < L; c += 8) {
       uint64_t w = 0;
 #pragma unroll
       for (int k = 0; k < 8; k++)
         if (c + k < L) w |= (uint64_t)(uint8_t)s[c + k] << (8 * k);
-      put(w, L - c < 8 ? L - c : 8);
+      if (FIRST && c == 0) put<true>(w, 8);
+      else put(w, L - c < 8 ? L - c : 8);
     }
   }
   // MsgPackWriter.writeInteger (same ranges as W::integer): a fixint, or a header byte (0xcc..0xcf unsigned,
@@ -156,7 +159,7 @@ __device__ __forceinline__ void fast_encode(FastW& w, const zb_rec& d, const Dev
   const DevElem& e = elems[d.elem];
   const DevWorkflow& wf = wfs[e.wf];
   if (kind_vt(d.kind) == ZB_VT_WORKFLOW_INSTANCE) {  // WorkflowInstanceRecord.java:39-60
-    w.lit("\x87\xad" "bpmnProcessId");
+    w.lit<true>("\x87\xad" "bpmnProcessId");
     w.str(pool + wf.pid_off, wf.pid_len);
     w.lit("\xa7" "version");
     w.ival(wf.version);
@@ -171,7 +174,7 @@ __device__ __forceinline__ void fast_encode(FastW& w, const zb_rec& d, const Dev
     w.lit("\xb0" "scopeInstanceKey");
     w.ival(d.scope_key);
   } else {  // JobRecord.java:35-53 + JobHeaders.java:33-51
-    w.lit("\x87\xa8" "deadline" "\xd3\x80\x00\x00\x00\x00\x00\x00\x00" "\xa6" "worker" "\xa0" "\xa7" "retries");
+    w.lit<true>("\x87\xa8" "deadline" "\xd3\x80\x00\x00\x00\x00\x00\x00\x00" "\xa6" "worker" "\xa0" "\xa7" "retries");
     w.ival(e.retries);
     w.lit("\xa4" "type");
     w.str(pool + e.type_off, e.type_len);

@@ -1671,14 +1671,19 @@ __global__ void __launch_bounds__(TWG) k_tmpl_io(TrajParams P) {
   TmplLane L;
   L.ncls = __builtin_amdgcn_readfirstlane(P.plan->nc);
   uint32_t cls = 0;
-  {
+  {  // class-c instances before this one: its workgroup's offset (k_cls_scan), the waves before it, the lanes
     const uint64_t grp = (uint64_t)(inst >> 6) * CLS_MAX;
+    const uint64_t wg = (uint64_t)(inst / TWG), grp0 = wg * (TWG / 64) * CLS_MAX;
+    const int wvi = (int)((inst % TWG) >> 6);
     const uint32_t bit = (uint32_t)(inst & 63);
     const uint64_t lt = (1ull << bit) - 1;
 #pragma unroll
     for (int c = 0; c < CLS_MAX; c++) {
-      const uint64_t m = c < (int)L.ncls ? P.cmask[grp + c] : 0;
-      L.before[c] = c < (int)L.ncls ? P.woffw[grp + c] + (uint32_t)__builtin_popcountll(m & lt) : 0;
+      if (c >= (int)L.ncls) { L.before[c] = 0; continue; }
+      const uint64_t m = P.cmask[grp + c];
+      uint32_t off = P.wgoff[(uint64_t)c * P.nwg + wg];
+      for (int v = 0; v < wvi; v++) off += (uint32_t)__builtin_popcountll(P.cmask[grp0 + (uint64_t)v * CLS_MAX + c]);
+      L.before[c] = off + (uint32_t)__builtin_popcountll(m & lt);
       if ((m >> bit) & 1) cls = (uint32_t)c;
     }
   }
