@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BYTES_PER_TRANSITION = 96  # 32 B row read + 32 B row write + 32 B record descriptor
 DESC_BYTES = 32  # one zb_rec descriptor per log record
-HDR_BYTES = 40  # one zb_record_header per drained record
+HDR_BYTES = 24  # one zb_record_header per drained record
 PMC_DIR = os.path.join(ROOT, "profiles", "r02")
 METRIC = "BPMN element transitions/sec (+ completed instances/sec) per node; % HBM roofline"
 
@@ -272,7 +272,7 @@ def roofline(tot, steps, cfg, n):
         kname = ("zbg::k_ser_fast" if tot["generic_tiles"] == 0 else "zbg::k_ser_fast (+ k_ser_write on %d tiles)"
                  % (tot["generic_tiles"] // steps)) if tot["ser_size_ms"] > 0 else "zbg::k_ser_fused"
         cands.append((kname, tot["ser_write_ms"] / steps, b,
-                      "32 B descriptor read + 40 B header write per drained record + value bytes written + payload "
+                      "32 B descriptor read + 24 B header write per drained record + value bytes written + payload "
                       "bytes read"))
     if tot["main_ms"] > 0:
         b = (DESC_BYTES * tot["written"] + tot["merge_bytes"] + tot["cond_bytes"]) / steps

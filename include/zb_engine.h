@@ -81,11 +81,12 @@ typedef struct zb_rec {
   uint8_t kind;       /* bits 0-3 value type, bits 4-5 record type, bit 6 = 2nd record of a batch */
 } zb_rec;
 
-/* Serialized record as handed back for log append. value bytes are the exact msgpack value
- * (UnpackedObject.write) of the reference record; position = log sequence number. */
+/* Serialized record as handed back for log append (the layout of zb_rec_desc, the submit input, with the
+ * rejection type in its pad byte). value bytes are the exact msgpack value (UnpackedObject.write) of the
+ * reference record. Header i of a drained batch [start, start + count) is the record at log position
+ * start + i; source positions, batch flags and the SBE metadata are in the log frames
+ * (zb_serialize_frames). 24 bytes: the drain writes one per record, so every byte is HBM traffic. */
 typedef struct zb_record_header {
-  int64_t position;
-  int64_t source_position;
   int64_t key;
   uint8_t record_type;
   uint8_t value_type;

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 def test_config_struct_layout_matches_header():
     assert ctypes.sizeof(engine.zb_config) == 48
     assert ctypes.sizeof(engine.zb_rec) == 32
-    assert ctypes.sizeof(engine.zb_record_header) == 40
+    assert ctypes.sizeof(engine.zb_record_header) == 24
 
 
 def test_workloads_payload_encoding():

@@ -202,6 +202,7 @@ struct WaveHdr {
   int64_t pad[9];
 };
 static_assert(sizeof(WaveHdr) == 128, "WaveHdr is 128 bytes");
+static_assert(sizeof(zb_record_header) == 24, "zb_record_header is 24 bytes (the drain writes one per record)");
 
 // element-instance row hot fields (16 B); keys live in a separate 32 B array
 struct RowMeta {

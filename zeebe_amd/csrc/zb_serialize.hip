@@ -482,8 +482,7 @@ constexpr int SER_IMG = 48 * 1024;  // three workgroups per CU
 
 __device__ __forceinline__ zb_record_header record_header(const zb_rec& d, int64_t pos, uint32_t len, uint64_t off) {
   zb_record_header h;
-  h.position = pos;
-  h.source_position = -1;
+  (void)pos;  // (implicit: start + index)
   h.key = d.key;
   h.record_type = kind_rt(d.kind);
   h.value_type = kind_vt(d.kind);
@@ -620,7 +619,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
       if (NT) {
         const uint64_t* hw = (const uint64_t*)&h;
         uint64_t* dh = (uint64_t*)(P.headers + i);
-        for (int k = 0; k < 5; k++) __builtin_nontemporal_store(hw[k], dh + k);
+        for (int k = 0; k < (int)(sizeof(zb_record_header) / 8); k++) __builtin_nontemporal_store(hw[k], dh + k);
       } else {
         P.headers[i] = h;
       }
@@ -761,7 +760,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(6))
     const zb_record_header h = record_header(d, P0.start + i, len, off);
     const uint64_t* hw = (const uint64_t*)&h;
     uint64_t* dh = (uint64_t*)(P0.headers + i);
-    for (int k = 0; k < 5; k++) __builtin_nontemporal_store(hw[k], dh + k);
+    for (int k = 0; k < (int)(sizeof(zb_record_header) / 8); k++) __builtin_nontemporal_store(hw[k], dh + k);
   }
   if (P0.totals) {
     unsigned long long y = live ? (uint32_t)pre[0] : 0;

@@ -48,10 +48,9 @@ class zb_rec_desc(ctypes.Structure):
                 ("value_offset", ctypes.c_uint64)]
 
 
-class zb_record_header(ctypes.Structure):
-    _fields_ = [("position", ctypes.c_int64), ("source_position", ctypes.c_int64), ("key", ctypes.c_int64),
-                ("record_type", ctypes.c_uint8), ("value_type", ctypes.c_uint8), ("intent", ctypes.c_uint8),
-                ("rejection_type", ctypes.c_uint8), ("value_length", ctypes.c_uint32),
+class zb_record_header(ctypes.Structure):  # header i of a drained batch: the record at position start + i
+    _fields_ = [("key", ctypes.c_int64), ("record_type", ctypes.c_uint8), ("value_type", ctypes.c_uint8),
+                ("intent", ctypes.c_uint8), ("rejection_type", ctypes.c_uint8), ("value_length", ctypes.c_uint32),
                 ("value_offset", ctypes.c_uint64)]
 
 
@@ -369,10 +368,9 @@ class Engine:
         self._check(self._L.zb_drain(self._h, start, count, hdrs, buf, need.value, ctypes.byref(need)))
         raw = buf.raw
         out = []
-        for h in hdrs:
+        for i, h in enumerate(hdrs):
             v = raw[h.value_offset:h.value_offset + h.value_length]
-            out.append(Record(h.position, h.source_position, h.key, h.record_type, h.value_type, h.intent,
-                              h.rejection_type, v))
+            out.append(Record(start + i, -1, h.key, h.record_type, h.value_type, h.intent, h.rejection_type, v))
         return out
 
     # ---- partition interface of zeebe_amd.cluster (message correlation, config 5)
