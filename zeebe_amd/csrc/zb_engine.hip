@@ -234,7 +234,9 @@ struct zb_engine {
   uint64_t dr_cap = 0, dr_val_cap = 0, dr_tmp_cap = 0;
   uint32_t* dr_len = nullptr;  // value lengths
   uint64_t *dr_off = nullptr, *dr_tiles = nullptr, *dr_pay = nullptr, *dr_tsum = nullptr;  // tile offsets / states / ...
-  uint32_t* dr_list = nullptr;   // tiles k_ser_fast leaves to k_ser_write
+  uint32_t* dr_list = nullptr;   // tiles the first fast pass leaves to the wide one
+  uint32_t* dr_list2 = nullptr;  // tiles the wide fast pass leaves to k_ser_write
+  uint32_t dr_wide_tiles = 0;    // tiles the last drain's wide fast pass encoded
   uint32_t dr_slow_tiles = 0;    // how many tiles the last drain ran through k_ser_write
   bool dr_split = false;         // the last drain ran k_ser_fast + k_ser_write (events 2-4, 5-3)
   int ser_fast = 1;              // ZB_SER_FAST=0: every tile through k_ser_write
@@ -790,7 +792,7 @@ void zb_engine_destroy(zb_engine* e) {
   e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
   e->d_ranges.free(); e->d_cmd_pool.free(); e->d_lookup_keys.free(); e->d_lookup_pos.free();
   void* dr[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_val, e->dr_tmp, e->dr_total, e->dr_tiles, e->dr_pay, e->dr_tsum,
-                e->dr_list};
+                e->dr_list, e->dr_list2};
   for (void* p : dr)
     if (p) (void)hipFree(p);
   if (e->h_dr_total) (void)hipHostFree(e->h_dr_total);
@@ -1679,10 +1681,11 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
     HIPCHECK(e, hipHostMalloc(&e->h_dr_total, 4 * sizeof(uint64_t)));
   }
   if ((uint64_t)count > e->dr_cap) {
-    void* ps[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_tmp, e->dr_tiles, e->dr_pay, e->dr_tsum, e->dr_list};
+    void* ps[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_tmp, e->dr_tiles, e->dr_pay, e->dr_tsum, e->dr_list, e->dr_list2};
     for (void* q : ps)
       if (q) (void)hipFree(q);
-    e->dr_off = e->dr_tiles = e->dr_pay = e->dr_tsum = nullptr; e->dr_len = e->dr_list = nullptr; e->dr_hdr = nullptr;
+    e->dr_off = e->dr_tiles = e->dr_pay = e->dr_tsum = nullptr; e->dr_len = e->dr_list = e->dr_list2 = nullptr;
+    e->dr_hdr = nullptr;
     e->dr_tmp = nullptr;
     e->dr_cap = e->dr_tmp_cap = 0;
     const uint64_t cap = (uint64_t)count + (uint64_t)count / 4 + 1024;
@@ -1696,6 +1699,7 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
     HIPCHECK(e, hipMalloc(&e->dr_tsum, (cap / 256 + 2) * sizeof(uint64_t)));
     HIPCHECK(e, hipMalloc(&e->dr_off, (cap / 256 + 2) * sizeof(uint64_t)));
     HIPCHECK(e, hipMalloc(&e->dr_list, (cap / 256 + 2) * sizeof(uint32_t)));
+    HIPCHECK(e, hipMalloc(&e->dr_list2, (cap / 256 + 2) * sizeof(uint32_t)));
     size_t tmp = 0;
     if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->dr_tsum, e->dr_off, (int)(cap / 256 + 2), e->stream) != hipSuccess)
       return fail(e, ZB_EDEVICE, "scan sizing");
@@ -1793,15 +1797,31 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
       wr.tile_offs = e->dr_off;
       e->dr_split = e->ser_fast && !fc && sp.model_lds;
       if (e->dr_split) {  // k_ser_fast, then k_ser_write over the tiles it left
+        // pass 1 over every tile (13 KB wave image) -> list A; pass 2 over A (40 KB) -> list B; k_ser_write over B
+        uint32_t* cnt = (uint32_t*)(e->dr_total + 3);  // [0] list A, [1] list B (zeroed with dr_total)
         wr.tile_list = e->dr_list;
-        wr.tile_list_n = (uint32_t*)(e->dr_total + 3);
+        wr.tile_list_n = cnt;
         launch_ser_fast(wr, e->stream);
         HIPCHECK(e, hipEventRecord(e->dr_ev[4], e->stream));
         HIPCHECK(e, hipMemcpyAsync(e->h_dr_total + 3, e->dr_total + 3, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
         HIPCHECK(e, hipStreamSynchronize(e->stream));
-        e->dr_slow_tiles = (uint32_t)e->h_dr_total[3];
-        HIPCHECK(e, hipEventRecord(e->dr_ev[5], e->stream));  // (the host round trip is not write-pass time)
-        launch_ser_write_list(wr, e->dr_slow_tiles, e->stream);
+        uint32_t nA = ((const uint32_t*)(e->h_dr_total + 3))[0], nB = 0;
+        HIPCHECK(e, hipEventRecord(e->dr_ev[5], e->stream));  // (the host round trips are not write-pass time)
+        if (nA) {
+          SerParams w2 = wr;
+          w2.tile_list_in = e->dr_list;
+          w2.tile_list = e->dr_list2;
+          w2.tile_list_n = cnt + 1;
+          launch_ser_fast_wide(w2, nA, e->stream);
+          HIPCHECK(e, hipMemcpyAsync(e->h_dr_total + 3, e->dr_total + 3, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+          HIPCHECK(e, hipStreamSynchronize(e->stream));
+          nB = ((const uint32_t*)(e->h_dr_total + 3))[1];
+          SerParams w3 = wr;
+          w3.tile_list_in = e->dr_list2;
+          launch_ser_write_list(w3, nB, e->stream);
+        }
+        e->dr_slow_tiles = nB;
+        e->dr_wide_tiles = nA - nB;
         launch_ser_sum(wr, e->stream);
       } else {
         e->dr_slow_tiles = (uint32_t)tiles;

@@ -533,7 +533,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
   __shared__ unsigned long long s_wsum[SER_WG / 64];
   __shared__ uint32_t s_maxlen;
   __shared__ unsigned long long s_wlo[SER_WINDOWS], s_whi[SER_WINDOWS];
-  const uint32_t tile = P0.tile_list ? P0.tile_list[blockIdx.x] : blockIdx.x;  // (the tiles k_ser_fast left)
+  const uint32_t tile = P0.tile_list_in ? P0.tile_list_in[blockIdx.x] : blockIdx.x;  // (the tiles k_ser_fast left)
   const int64_t base = (int64_t)tile * SER_WG;
   const int64_t i = base + threadIdx.x;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -706,12 +706,15 @@ __global__ void __launch_bounds__(256) k_ser_sum(SerParams P, int64_t nparts) {
 // range out. A workgroup then needs ~17 KB of LDS instead of 52 KB and a third of the registers, so several
 // times more tiles -- and their descriptor / payload loads -- are in flight per CU. Tiles with a record the
 // fast encoder does not take, or a wave range larger than the image, go to k_ser_write (tile_list).
-constexpr int SER_FIMG = 13 * 1024;
-__global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(6))) k_ser_fast(SerParams P0) {
-  __shared__ __attribute__((aligned(16))) uint8_t img[SER_FIMG + 16];
+// A second instantiation with a 40 KB image (3 workgroups per CU) runs over the tiles the first one left when
+// their values are large (jobs and merged payloads, C2 / C4); only what neither takes reaches k_ser_write.
+constexpr int SER_FIMG = 13 * 1024, SER_FIMG_WIDE = 40 * 1024;
+template <int IMG, bool LISTED>
+__global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(IMG <= SER_FIMG ? 6 : 3))) k_ser_fast(SerParams P0) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[IMG + 16];
   __shared__ __attribute__((aligned(16))) uint8_t s_model[SER_MODEL_LDS + 16];  // (+16: 8-byte reads past the pool)
   __shared__ unsigned long long s_wsum[SER_WG / 64], s_pay[SER_WG / 64];
-  const uint32_t tile = blockIdx.x;
+  const uint32_t tile = LISTED ? P0.tile_list_in[blockIdx.x] : blockIdx.x;
   const int64_t base = (int64_t)tile * SER_WG;
   const int64_t i = base + threadIdx.x;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -742,7 +745,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(6))
   const bool all_fast = __syncthreads_and(fast || !live);
   bool fits = true;
 #pragma unroll
-  for (int k = 0; k < SER_WG / 64; k++) fits = fits && s_wsum[k] + 16 <= (uint64_t)SER_FIMG;
+  for (int k = 0; k < SER_WG / 64; k++) fits = fits && s_wsum[k] + 16 <= (uint64_t)IMG;
   if (P0.out_cap && o1 > P0.out_cap) {  // does not fit: the host grows the buffer and runs the pass again
     if (threadIdx.x == 0) atomicOr(P0.overflow, 1u);
     return;
@@ -794,7 +797,12 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(6))
 
 void launch_ser_fast(const SerParams& p, hipStream_t s) {
   if (p.count <= 0) return;
-  hipLaunchKernelGGL(k_ser_fast, dim3((unsigned)((p.count + SER_WG - 1) / SER_WG)), dim3(SER_WG), 0, s, p);
+  hipLaunchKernelGGL((k_ser_fast<SER_FIMG, false>), dim3((unsigned)((p.count + SER_WG - 1) / SER_WG)), dim3(SER_WG), 0,
+                     s, p);
+}
+void launch_ser_fast_wide(const SerParams& p, uint32_t n, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL((k_ser_fast<SER_FIMG_WIDE, true>), dim3(n), dim3(SER_WG), 0, s, p);
 }
 void launch_ser_write_list(const SerParams& p, uint32_t n, hipStream_t s) {
   if (n == 0) return;
