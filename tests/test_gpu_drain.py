@@ -19,18 +19,22 @@ from zeebe_amd import bpmn, workloads
 pytestmark = pytest.mark.gpu
 
 
-def _drain(make, fast):
+def _drain(make, fast, vlen_check=None, **engine_args):
     from zeebe_amd.engine import Engine, zb_record_header
 
-    old = os.environ.get("ZB_SER_FAST")
-    os.environ["ZB_SER_FAST"] = "1" if fast else "0"
+    env = {"ZB_SER_FAST": "1" if fast else "0"}
+    if vlen_check is not None:
+        env["ZB_VLEN_CHECK"] = "1" if vlen_check else "0"
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
-        e = Engine()
+        e = Engine(**engine_args)
     finally:
-        if old is None:
-            del os.environ["ZB_SER_FAST"]
-        else:
-            os.environ["ZB_SER_FAST"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     make(e)
     st = e.step()
     assert st["quiescent"]
@@ -96,3 +100,23 @@ def test_mixed_kinds_fast_drain_matches_generic():
         e.create("inc", payloads)
 
     _compare(make)
+
+
+def test_size_pass_formula_matches_encoder():
+    # records without a length from their emitting kernel (the wave pipeline writes none) are sized by the
+    # size pass: WORKFLOW_INSTANCE / JOB records by the emit kernels' formula, unless ZB_VLEN_CHECK=1, which
+    # runs the encoder's dry run on every record. Both must give the same drain, byte for byte.
+    wf = bpmn.chain_workflow(4)
+    blob, offs = workloads.order_payloads(2000)
+    jp = {"t%d" % k: msgpack.packb({"k%d" % k: "y" * (7 * k)}) for k in range(1, 5)}
+
+    def make(e):
+        e.deploy(wf.to_xml(), 100, 1)
+        for act, p in jp.items():
+            e.set_job_payload(100, act, p)
+        e.create_packed("chain", blob, offs)
+
+    a = _drain(make, True, vlen_check=False, wave_only=True)
+    b = _drain(make, True, vlen_check=True, wave_only=True)
+    assert a[0]["value_bytes"] == b[0]["value_bytes"]
+    assert a[1] == b[1] and a[2] == b[2]

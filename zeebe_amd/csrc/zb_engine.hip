@@ -1734,6 +1734,7 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
   sp.vlen_bad = e->vlen_bad;
   sp.arena = e->arena;
   sp.arena_bytes = e->cfg.arena_bytes;
+  sp.vconst = e->d_vconst.p;
   sp.elems = e->d_elems.p;
   sp.wfs = e->d_wfs.p;
   sp.queries = e->d_queries.p;

@@ -445,7 +445,12 @@ __global__ void __launch_bounds__(256) k_ser_size(SerParams P0) {
       const int64_t i = ((int64_t)blockIdx.x * SER_SIZE_TILES + j) * 256 + threadIdx.x;
       const int64_t pos = P.start + i;
       const zb_rec d = P.log[pos];
-      const uint32_t m = value_size(P, pos, d);
+      // the fast encoder's records: the emit kernels' formula (element constant + key lengths + binary
+      // payload); every other record, and every record under ZB_VLEN_CHECK, by the encoder's dry run
+      const uint32_t m = (P.vconst && !P.vlen_bad && fast_kind(d))
+          ? (kind_vt(d.kind) == ZB_VT_JOB ? P.vconst[d.elem].job : P.vconst[d.elem].wf) + mp_int_len(d.inst_key) +
+                mp_int_len(d.scope_key) + mp_bin_len(*(const uint32_t*)(P.arena + (uint64_t)d.payload * 8))
+          : value_size(P, pos, d);
       if (n[j] != VLEN_UNKNOWN && n[j] != m) atomicOr(P.vlen_bad, 1u);
       n[j] = FRAMES ? (FRAME_PREFIX + reason_len(reason_of(d)) + m + 7) & ~7u : m;
       if (P.len_in_vlen) P.vlen_out[pos] = n[j];
