@@ -3,6 +3,7 @@
 // (tests/test_fastenc_host.py). Nothing here is part of the product.
 #include <cstdint>
 #include <cstring>
+#include <vector>
 #define __device__
 #define __host__
 #define __forceinline__ inline
@@ -22,6 +23,7 @@ long fastenc(int vt, int intent, int64_t inst_key, int64_t scope_key, int64_t wf
   std::memset(pool, 0xcd, sizeof(pool));
   std::memcpy(pool, pool_in, pool_len);
   DevElem e{};
+  e.kind = EK_TASK;  // (its JOB runs are built only for service tasks)
   e.wf = 0;
   e.id_off = id_off;
   e.id_len = (uint16_t)id_len;
@@ -42,12 +44,18 @@ long fastenc(int vt, int intent, int64_t inst_key, int64_t scope_key, int64_t wf
   d.intent = (uint8_t)intent;
   d.kind = make_kind((uint8_t)vt, ZB_RT_EVENT, false);
   if (!fast_kind(d)) return -1;
+  // the element's constant runs, as zb_deploy builds them (8-aligned copy: the device reads them from LDS)
+  std::vector<DevValSeg> tab;
+  std::vector<uint8_t> segs;
+  if (!build_value_segments(&e, 1, &wf, 1, pool, tab, segs)) return -2;
+  std::vector<uint64_t> seg_words((segs.size() + 7) / 8);
+  std::memcpy(seg_words.data(), segs.data(), segs.size());
   uint64_t pre[SER_PRE];
   const uint32_t words = (4 + (uint32_t)doc[0] + 7) / 8;  // (doc[0] low half: the payload length)
   for (int j = 0; j < SER_PRE; j++) pre[j] = (uint32_t)j < words ? doc[j] : 0xa5a5a5a5a5a5a5a5ull;  // (next doc)
   FastW w;
   w.begin(out, head);  // (out: 8-aligned image; the value starts at byte head of it)
-  fast_encode(w, d, &e, &wf, pool, doc, pre);
+  fast_encode(w, d, tab.data(), (const uint8_t*)seg_words.data(), doc, pre);
   return w.n();
 }
 }

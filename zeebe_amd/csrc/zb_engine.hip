@@ -91,6 +91,10 @@ struct zb_engine {
   uint32_t* srcd = nullptr;     // per record: position - source position (0: none), for log frames
   uint32_t* vlen = nullptr;     // per record: serialized value length if the emitting kernel knew it
   DevVec<ValueConst> d_vconst;  // per element: constant parts of its WORKFLOW_INSTANCE / JOB values
+  DevVec<DevValSeg> d_vsegs;    // per element: its values' constant runs (fast drain passes)
+  DevVec<uint8_t> d_segpool;
+  uint32_t segpool_len = 0;
+  bool seg_ok = false;          // the runs fit the fast passes' LDS
   uint32_t* vlen_bad = nullptr; // ZB_VLEN_CHECK=1: the size pass checks every known length (device flag)
   RowMeta* rmeta = nullptr;
   RowKeys* rkeys = nullptr;
@@ -301,6 +305,16 @@ int upload_model(zb_engine* e) {
                   (el.headers_off == NO_REF ? 1 : el.headers_len) + 8;
     }
     HIPCHECK(e, e->d_vconst.upload(vc, e->stream));
+    // the fast drain passes' constant runs (zb_fastenc.hpp); the table padded to whole 16-byte LDS copies
+    std::vector<DevValSeg> tab;
+    std::vector<uint8_t> segs;
+    e->seg_ok = build_value_segments(e->model.elems.data(), e->model.elems.size(), e->model.workflows.data(),
+                                     e->model.workflows.size(), e->model.pool.data(), tab, segs);
+    tab.resize((tab.size() + 3) & ~(size_t)3, DevValSeg{});
+    e->seg_ok = e->seg_ok && tab.size() * sizeof(DevValSeg) + segs.size() <= SEG_LDS_MAX;
+    e->segpool_len = (uint32_t)segs.size();
+    HIPCHECK(e, e->d_vsegs.upload(tab, e->stream));
+    HIPCHECK(e, e->d_segpool.upload(segs, e->stream));
   }
   HIPCHECK(e, e->d_segs.upload(e->model.segs, e->stream));
   if (e->static_blobs.size() > STATIC_ARENA_BYTES) return fail(e, ZB_ENOMEM, "static payload region full");
@@ -791,6 +805,13 @@ void zb_engine_destroy(zb_engine* e) {
   e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_consts.free();
   e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
   e->d_ranges.free(); e->d_cmd_pool.free(); e->d_lookup_keys.free(); e->d_lookup_pos.free();
+  e->d_maps.free();
+  e->d_segs.free();
+  e->d_vconst.free();
+  e->d_vsegs.free();
+  e->d_segpool.free();
+  e->d_staged_vlen.free();
+  e->d_reqs.free();
   void* dr[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_val, e->dr_tmp, e->dr_total, e->dr_tiles, e->dr_pay, e->dr_tsum,
                 e->dr_list, e->dr_list2};
   for (void* p : dr)
@@ -1735,6 +1756,10 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
   sp.arena = e->arena;
   sp.arena_bytes = e->cfg.arena_bytes;
   sp.vconst = e->d_vconst.p;
+  sp.vsegs = e->d_vsegs.p;
+  sp.segpool = e->d_segpool.p;
+  sp.segpool_len = e->segpool_len;
+  sp.seg_lds = e->seg_ok ? 1 : 0;
   sp.elems = e->d_elems.p;
   sp.wfs = e->d_wfs.p;
   sp.queries = e->d_queries.p;
@@ -1796,7 +1821,7 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
       wr.lengths = e->dr_len;
       wr.len_in_vlen = sz.len_in_vlen;
       wr.tile_offs = e->dr_off;
-      e->dr_split = e->ser_fast && !fc && sp.model_lds;
+      e->dr_split = e->ser_fast && !fc && sp.seg_lds && sp.arena_bytes;
       if (e->dr_split) {  // k_ser_fast, then k_ser_write over the tiles it left
         // pass 1 over every tile (13 KB wave image) -> list A; pass 2 over A (40 KB) -> list B; k_ser_write over B
         uint32_t* cnt = (uint32_t*)(e->dr_total + 3);  // [0] list A, [1] list B (zeroed with dr_total)

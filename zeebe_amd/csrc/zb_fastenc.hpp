@@ -2,6 +2,7 @@
 // image). Included by zb_serialize.hip; compiled for the host only by tests/native.
 #pragma once
 #include <cstdint>
+#include <vector>
 
 #include "zb_device.hpp"
 
@@ -92,29 +93,33 @@ struct FastW {
     put(((neg ? 0xd0u : 0xccu) + lg) | be << 8, m < 8 ? m + 1 : 8);
     if (m == 8) put((uint8_t)v, 1);
   }
-  // c bytes at s (LDS, any alignment): aligned b64 reads (reads up to 7 bytes past the string)
-  __device__ __forceinline__ void raw(const uint8_t* s, uint32_t c) {
-    const uint32_t a = (uint32_t)((uintptr_t)s & 7);
-    const uint64_t* w = (const uint64_t*)(s - a);
-    uint64_t cur = w[0];
-    for (uint32_t k = 0, j = 1; k < c; k += 8, j++) {
-      const uint64_t nx = w[j];
-      const uint64_t v = a ? (cur >> (8 * a)) | (nx << (64 - 8 * a)) : cur;
-      const uint32_t r = c - k;
-      put(r < 8 ? v & (~0ull >> (64 - 8 * r)) : v, r < 8 ? r : 8);
-      cur = nx;
-    }
-  }
-  __device__ __forceinline__ void str(const uint8_t* s, uint32_t c) {  // MsgPackWriter.writeString
-    if (c < 32) put(0xa0 | c, 1);
-    else if (c < 256) put(0xd9 | (uint64_t)c << 8, 2);
-    else if (c < 65536) put(0xda | (uint64_t)__builtin_bswap16((uint16_t)c) << 8, 3);
-    else put(0xdb | (uint64_t)__builtin_bswap32(c) << 8, 5);
-    raw(s, c);
+  // a constant run: c bytes at s (LDS, 8-aligned, zero-padded to 8); FIRST as in put
+  template <bool FIRST = false>
+  __device__ __forceinline__ void seg(const uint8_t* s, uint32_t c) {
+    const uint64_t* w = (const uint64_t*)s;
+    uint32_t k = 0;
+    if (FIRST) { put<true>(w[0], 8); k = 8; }
+    for (; k < c; k += 8) put(w[k >> 3], c - k < 8 ? c - k : 8);
   }
 };
 
 constexpr int SER_PRE = 6;  // payload document words prefetched per record (length + 44 bytes)
+
+// The constant runs of an element's values, built at deploy time (build_value_segments) and copied into LDS
+// by the write pass: a run is appended 8 bytes at a time from aligned LDS words instead of key by key.
+//   WI_A  {0x87 "bpmnProcessId" pid "version" v "workflowKey" k "workflowInstanceKey"}   (per workflow)
+//   WI_B  {"activityId" id "payload"}
+//   JOB_A {0x87 "deadline" MIN "worker" "" "retries" r "type" t "headers" 0x86 "bpmnProcessId" pid
+//          "workflowDefinitionVersion" v "workflowKey" k "workflowInstanceKey"}
+//   JOB_B {"activityId" id "activityInstanceKey"}      JOB_C {"customHeaders" h "payload"}
+// Each run starts 8-aligned in the segment pool and is zero-padded to 8 bytes.
+enum { SEG_WI_A = 0, SEG_WI_B, SEG_JOB_A, SEG_JOB_B, SEG_JOB_C, SEG_N };
+struct DevValSeg {
+  uint16_t off8[SEG_N];  // offset / 8 in the segment pool
+  uint16_t len[SEG_N];
+};
+static_assert(sizeof(DevValSeg) == 20, "DevValSeg is 20 bytes");
+constexpr uint32_t SEG_LDS_MAX = 16384;  // table (padded to 4 entries) + pool the fast passes copy into LDS
 
 // the payload document [u32 len][bytes] as binary (MsgPackWriter.writeBinary): doc words W_j (8-aligned), the
 // first SER_PRE already loaded (words past the document hold whatever follows it: only bytes past the payload
@@ -153,50 +158,112 @@ __device__ __forceinline__ bool fast_kind(const zb_rec& d) {
   return vt == ZB_VT_JOB && (d.intent | 1) != JI_CANCELED;
 }
 
-// encode_value's WORKFLOW_INSTANCE (non-submitted) and JOB branches; elems / wfs / pool in LDS
-__device__ __forceinline__ void fast_encode(FastW& w, const zb_rec& d, const DevElem* elems, const DevWorkflow* wfs,
-                                            const uint8_t* pool, const uint64_t* dw, const uint64_t (&pre)[SER_PRE]) {
-  const DevElem& e = elems[d.elem];
-  const DevWorkflow& wf = wfs[e.wf];
+// encode_value's WORKFLOW_INSTANCE (non-submitted) and JOB branches from the constant runs of the record's
+// element (tab / pool in LDS) and its variable fields: keys, payload
+__device__ __forceinline__ void fast_encode(FastW& w, const zb_rec& d, const DevValSeg* tab, const uint8_t* segs,
+                                            const uint64_t* dw, const uint64_t (&pre)[SER_PRE]) {
+  const DevValSeg& t = tab[d.elem];
   if (kind_vt(d.kind) == ZB_VT_WORKFLOW_INSTANCE) {  // WorkflowInstanceRecord.java:39-60
-    w.lit<true>("\x87\xad" "bpmnProcessId");
-    w.str(pool + wf.pid_off, wf.pid_len);
-    w.lit("\xa7" "version");
-    w.ival(wf.version);
-    w.lit("\xab" "workflowKey");
-    w.ival(wf.key);
-    w.lit("\xb3" "workflowInstanceKey");
+    w.seg<true>(segs + 8 * t.off8[SEG_WI_A], t.len[SEG_WI_A]);
     w.ival(d.inst_key);
-    w.lit("\xaa" "activityId");
-    w.str(pool + e.id_off, e.id_len);
-    w.lit("\xa7" "payload");
+    w.seg(segs + 8 * t.off8[SEG_WI_B], t.len[SEG_WI_B]);
     fast_bin(w, dw, pre);
     w.lit("\xb0" "scopeInstanceKey");
     w.ival(d.scope_key);
   } else {  // JobRecord.java:35-53 + JobHeaders.java:33-51
-    w.lit<true>("\x87\xa8" "deadline" "\xd3\x80\x00\x00\x00\x00\x00\x00\x00" "\xa6" "worker" "\xa0" "\xa7" "retries");
-    w.ival(e.retries);
-    w.lit("\xa4" "type");
-    w.str(pool + e.type_off, e.type_len);
-    w.lit("\xa7" "headers" "\x86" "\xad" "bpmnProcessId");
-    w.str(pool + wf.pid_off, wf.pid_len);
-    w.lit("\xb9" "workflowDefinitionVersion");
-    w.ival(wf.version);
-    w.lit("\xab" "workflowKey");
-    w.ival(wf.key);
-    w.lit("\xb3" "workflowInstanceKey");
+    w.seg<true>(segs + 8 * t.off8[SEG_JOB_A], t.len[SEG_JOB_A]);
     w.ival(d.inst_key);
-    w.lit("\xaa" "activityId");
-    w.str(pool + e.id_off, e.id_len);
-    w.lit("\xb3" "activityInstanceKey");
+    w.seg(segs + 8 * t.off8[SEG_JOB_B], t.len[SEG_JOB_B]);
     w.ival(d.scope_key);
-    w.lit("\xad" "customHeaders");
-    if (e.headers_off == NO_REF) w.put(0x80, 1);  // JobRecord.NO_HEADERS
-    else w.raw(pool + e.headers_off, e.headers_len);
-    w.lit("\xa7" "payload");
+    w.seg(segs + 8 * t.off8[SEG_JOB_C], t.len[SEG_JOB_C]);
     fast_bin(w, dw, pre);
   }
   w.end();
+}
+
+// ---- host: the constant runs of every element's values (deploy time)
+inline void seg_int(std::vector<uint8_t>& b, int64_t v) {  // MsgPackWriter.writeInteger
+  auto be = [&](uint64_t x, int n) { for (int i = n - 1; i >= 0; i--) b.push_back((uint8_t)(x >> (8 * i))); };
+  if (v < -(1LL << 5)) {
+    if (v < -(1LL << 15)) {
+      if (v < -(1LL << 31)) { b.push_back(0xd3); be((uint64_t)v, 8); }
+      else { b.push_back(0xd2); be((uint64_t)v, 4); }
+    } else if (v < -(1 << 7)) { b.push_back(0xd1); be((uint64_t)v, 2); }
+    else { b.push_back(0xd0); be((uint64_t)v, 1); }
+  } else if (v < (1 << 7)) b.push_back((uint8_t)v);
+  else if (v < (1LL << 8)) { b.push_back(0xcc); be((uint64_t)v, 1); }
+  else if (v < (1LL << 16)) { b.push_back(0xcd); be((uint64_t)v, 2); }
+  else if (v < (1LL << 32)) { b.push_back(0xce); be((uint64_t)v, 4); }
+  else { b.push_back(0xcf); be((uint64_t)v, 8); }
+}
+inline void seg_str(std::vector<uint8_t>& b, const uint8_t* s, uint32_t n) {  // MsgPackWriter.writeString
+  if (n < 32) b.push_back((uint8_t)(0xa0 | n));
+  else if (n < 256) { b.push_back(0xd9); b.push_back((uint8_t)n); }
+  else if (n < 65536) { b.push_back(0xda); b.push_back((uint8_t)(n >> 8)); b.push_back((uint8_t)n); }
+  else { b.push_back(0xdb); for (int i = 3; i >= 0; i--) b.push_back((uint8_t)(n >> (8 * i))); }
+  b.insert(b.end(), s, s + n);
+}
+inline void seg_key(std::vector<uint8_t>& b, const char* k) {
+  uint32_t n = 0;
+  while (k[n]) n++;
+  seg_str(b, (const uint8_t*)k, n);
+}
+// false: a run or the pool does not fit the 16-bit table fields
+inline bool build_value_segments(const DevElem* elems, size_t n_elems, const DevWorkflow* wfs, size_t n_wfs,
+                                 const uint8_t* pool, std::vector<DevValSeg>& tab, std::vector<uint8_t>& segs) {
+  tab.assign(n_elems, DevValSeg{});
+  segs.clear();
+  auto add = [&](const std::vector<uint8_t>& b, uint16_t& off8, uint16_t& len) {
+    if (segs.size() / 8 > 0xffff || b.size() > 0xffff) return false;
+    off8 = (uint16_t)(segs.size() / 8);
+    len = (uint16_t)b.size();
+    segs.insert(segs.end(), b.begin(), b.end());
+    segs.resize((segs.size() + 7) & ~(size_t)7, 0);
+    return true;
+  };
+  std::vector<uint16_t> wf_off(n_wfs), wf_len(n_wfs);
+  for (size_t k = 0; k < n_wfs; k++) {  // WI_A, shared by a workflow's elements
+    const DevWorkflow& wf = wfs[k];
+    std::vector<uint8_t> b = {0x87};
+    seg_key(b, "bpmnProcessId"); seg_str(b, pool + wf.pid_off, wf.pid_len);
+    seg_key(b, "version"); seg_int(b, wf.version);
+    seg_key(b, "workflowKey"); seg_int(b, wf.key);
+    seg_key(b, "workflowInstanceKey");
+    if (!add(b, wf_off[k], wf_len[k])) return false;
+  }
+  for (size_t i = 0; i < n_elems; i++) {
+    const DevElem& e = elems[i];
+    const DevWorkflow& wf = wfs[e.wf];
+    DevValSeg& t = tab[i];
+    t.off8[SEG_WI_A] = wf_off[e.wf];
+    t.len[SEG_WI_A] = wf_len[e.wf];
+    std::vector<uint8_t> b;
+    seg_key(b, "activityId"); seg_str(b, pool + e.id_off, e.id_len); seg_key(b, "payload");
+    if (!add(b, t.off8[SEG_WI_B], t.len[SEG_WI_B])) return false;
+    if (e.kind != EK_TASK) continue;  // only service tasks write JOB records
+    b = {0x87};
+    seg_key(b, "deadline"); seg_int(b, INT64_MIN);
+    seg_key(b, "worker"); seg_str(b, nullptr, 0);
+    seg_key(b, "retries"); seg_int(b, e.retries);
+    seg_key(b, "type"); seg_str(b, pool + e.type_off, e.type_len);
+    seg_key(b, "headers"); b.push_back(0x86);
+    seg_key(b, "bpmnProcessId"); seg_str(b, pool + wf.pid_off, wf.pid_len);
+    seg_key(b, "workflowDefinitionVersion"); seg_int(b, wf.version);
+    seg_key(b, "workflowKey"); seg_int(b, wf.key);
+    seg_key(b, "workflowInstanceKey");
+    if (!add(b, t.off8[SEG_JOB_A], t.len[SEG_JOB_A])) return false;
+    b.clear();
+    seg_key(b, "activityId"); seg_str(b, pool + e.id_off, e.id_len); seg_key(b, "activityInstanceKey");
+    if (!add(b, t.off8[SEG_JOB_B], t.len[SEG_JOB_B])) return false;
+    b.clear();
+    seg_key(b, "customHeaders");
+    if (e.headers_off == NO_REF) b.push_back(0x80);  // JobRecord.NO_HEADERS
+    else b.insert(b.end(), pool + e.headers_off, pool + e.headers_off + e.headers_len);
+    seg_key(b, "payload");
+    if (!add(b, t.off8[SEG_JOB_C], t.len[SEG_JOB_C])) return false;
+  }
+  segs.resize(segs.size() + 8, 0);  // (a run's last word is read whole)
+  return true;
 }
 
 }  // namespace zbg

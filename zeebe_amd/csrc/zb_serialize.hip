@@ -561,13 +561,6 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
     }
   }
   if (live) d = P0.log[P0.start + i];
-  // payload document words of the fast records, loaded before the model copy's barrier
-  const bool fast = live && P0.model_lds && P0.arena_bytes && fast_kind(d);
-  const uint64_t* dw = (const uint64_t*)(P0.arena + (uint64_t)d.payload * 8);
-  uint64_t pre[SER_PRE];
-#pragma unroll
-  for (int j = 0; j < SER_PRE; j++)
-    pre[j] = (fast && (uint64_t)d.payload * 8 + 8 * j + 8 <= P0.arena_bytes) ? dw[j] : 0;
   if (P0.tile_offs) {
     x = len;
 #pragma unroll
@@ -617,8 +610,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
   uint32_t pay = 0;
   const int64_t pos = P.start + i;
   if (live) {
-    if (fast) pay = (uint32_t)pre[0];
-    else if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay = *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
+    if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay = *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
     if (!FRAMES && !(P.exp & 4)) {
       const zb_record_header h = record_header(d, pos, len, off);
       if (NT) {
@@ -643,22 +635,8 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
       P.pay_part[tile] = tt;
     }
   }
-  // LDS offsets of the model tables (fast encoder: typed LDS reads)
-  const uint32_t eb = (uint32_t)P0.n_elems * (uint32_t)sizeof(DevElem), wb = (uint32_t)P0.n_wfs * (uint32_t)sizeof(DevWorkflow);
-  const uint32_t wo = (eb + 15) & ~15u, po = wo + ((wb + 15) & ~15u);
-  // the common case: a staged tile of fast records, encoded from the prefetched payload words
-  if (!FRAMES && staged && __syncthreads_and(fast || !live)) {
-    if (live && !(P.exp & 1)) {
-      FastW w;
-      w.begin(img, shift + (uint32_t)(off - o0));
-      fast_encode(w, d, (const DevElem*)s_model, (const DevWorkflow*)(s_model + wo), s_model + po, dw, pre);
-    }
-    __syncthreads();
-    if (!(P.exp & 2)) stream_image(img, P.out, o0, shift, o1 - o0, NT);
-    return;
-  }
-  // otherwise the generic encoder in phases (one encode site keeps it inlined once): the whole tile staged,
-  // straight to HBM, or one phase per window (the fast encoder here too spills at the 3-workgroup register cap)
+  // the generic encoder in phases (one encode site keeps it inlined once): the whole tile staged, straight to
+  // HBM, or one phase per window
   const int mywin = (nwin && live) ? (int)((off - o0) / ws) : -1;
   const int nph = nwin ? nwin : 1;
 #pragma unroll 1
@@ -717,7 +695,7 @@ constexpr int SER_FIMG = 13 * 1024, SER_FIMG_WIDE = 40 * 1024;
 template <int IMG, bool LISTED>
 __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(IMG <= SER_FIMG ? 6 : 3))) k_ser_fast(SerParams P0) {
   __shared__ __attribute__((aligned(16))) uint8_t img[IMG + 16];
-  __shared__ __attribute__((aligned(16))) uint8_t s_model[SER_MODEL_LDS + 16];  // (+16: 8-byte reads past the pool)
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_model[];  // the constant runs (sized at launch)
   __shared__ unsigned long long s_wsum[SER_WG / 64], s_pay[SER_WG / 64];
   const uint32_t tile = LISTED ? P0.tile_list_in[blockIdx.x] : blockIdx.x;
   const int64_t base = (int64_t)tile * SER_WG;
@@ -741,12 +719,11 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(IMG
     if (lane >= k) x += y;
   }
   if (lane == 63) s_wsum[wv] = x;
-  // the model tables into LDS (their barrier is the vote's)
-  const uint32_t eb = (uint32_t)P0.n_elems * (uint32_t)sizeof(DevElem), wb = (uint32_t)P0.n_wfs * (uint32_t)sizeof(DevWorkflow);
-  const uint32_t wo = (eb + 15) & ~15u, po = wo + ((wb + 15) & ~15u);
-  for (uint32_t c = threadIdx.x; c < eb / 16; c += SER_WG) ((uint4*)s_model)[c] = ((const uint4*)P0.elems)[c];
-  for (uint32_t c = threadIdx.x; c < wb / 16; c += SER_WG) ((uint4*)(s_model + wo))[c] = ((const uint4*)P0.wfs)[c];
-  for (uint32_t c = threadIdx.x; c < P0.pool_len; c += SER_WG) s_model[po + c] = P0.pool[c];
+  // the elements' constant runs into LDS (their barrier is the vote's): table (4-byte words), pool (8-byte)
+  const uint32_t tb = ((uint32_t)P0.n_elems * (uint32_t)sizeof(DevValSeg) + 15) & ~15u;
+  for (uint32_t c = threadIdx.x; c < tb / 4; c += SER_WG) ((uint32_t*)s_model)[c] = ((const uint32_t*)P0.vsegs)[c];
+  for (uint32_t c = threadIdx.x; c < P0.segpool_len / 8; c += SER_WG)
+    ((uint64_t*)(s_model + tb))[c] = ((const uint64_t*)P0.segpool)[c];
   const bool all_fast = __syncthreads_and(fast || !live);
   bool fits = true;
 #pragma unroll
@@ -792,7 +769,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(IMG
     const uint64_t lo = o0 + pw;  // this wave's range starts at the tile start + the waves before it
     FastW w;
     w.begin(img, (uint32_t)(((uintptr_t)(P0.out + lo)) & 15) + (uint32_t)(off - lo));
-    fast_encode(w, d, (const DevElem*)s_model, (const DevWorkflow*)(s_model + wo), s_model + po, dw, pre);
+    fast_encode(w, d, (const DevValSeg*)s_model, s_model + tb, dw, pre);
   }
   stream_wave(wv);
 #pragma unroll 1
@@ -800,14 +777,18 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(IMG
   if (P0.totals && threadIdx.x == 0) P0.pay_part[tile] = s_pay[0] + s_pay[1] + s_pay[2] + s_pay[3];
 }
 
+// dynamic LDS of the fast passes: the segment table (whole 16-byte rows) + the segment pool
+static uint32_t seg_lds_bytes(const SerParams& p) {
+  return (((uint32_t)p.n_elems * (uint32_t)sizeof(DevValSeg) + 15) & ~15u) + p.segpool_len;
+}
 void launch_ser_fast(const SerParams& p, hipStream_t s) {
   if (p.count <= 0) return;
-  hipLaunchKernelGGL((k_ser_fast<SER_FIMG, false>), dim3((unsigned)((p.count + SER_WG - 1) / SER_WG)), dim3(SER_WG), 0,
-                     s, p);
+  hipLaunchKernelGGL((k_ser_fast<SER_FIMG, false>), dim3((unsigned)((p.count + SER_WG - 1) / SER_WG)), dim3(SER_WG),
+                     seg_lds_bytes(p), s, p);
 }
 void launch_ser_fast_wide(const SerParams& p, uint32_t n, hipStream_t s) {
   if (n == 0) return;
-  hipLaunchKernelGGL((k_ser_fast<SER_FIMG_WIDE, true>), dim3(n), dim3(SER_WG), 0, s, p);
+  hipLaunchKernelGGL((k_ser_fast<SER_FIMG_WIDE, true>), dim3(n), dim3(SER_WG), seg_lds_bytes(p), s, p);
 }
 void launch_ser_write_list(const SerParams& p, uint32_t n, hipStream_t s) {
   if (n == 0) return;
