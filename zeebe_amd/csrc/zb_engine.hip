@@ -238,6 +238,8 @@ struct zb_engine {
   uint64_t dr_cap = 0, dr_val_cap = 0, dr_tmp_cap = 0;
   uint32_t* dr_len = nullptr;  // value lengths
   uint64_t *dr_off = nullptr, *dr_tiles = nullptr, *dr_pay = nullptr, *dr_tsum = nullptr;  // tile offsets / states / ...
+  uint8_t* h_stage = nullptr;    // pinned staging of host-built uploads (zb_submit_publishes)
+  size_t h_stage_cap = 0;
   uint32_t* dr_list = nullptr;   // tiles the first fast pass leaves to the wide one
   uint32_t* dr_list2 = nullptr;  // tiles the wide fast pass leaves to k_ser_write
   uint32_t dr_wide_tiles = 0;    // tiles the last drain's wide fast pass encoded
@@ -817,6 +819,7 @@ void zb_engine_destroy(zb_engine* e) {
   for (void* p : dr)
     if (p) (void)hipFree(p);
   if (e->h_dr_total) (void)hipHostFree(e->h_dr_total);
+  if (e->h_stage) (void)hipHostFree(e->h_stage);
   for (auto& x : e->dr_ev)
     if (x) (void)hipEventDestroy(x);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -1929,6 +1932,20 @@ int zb_drain(zb_engine* e, int64_t start, int64_t count, zb_record_header* heade
   return zb_drain_copy(e, headers, values, 0, st.value_bytes);
 }
 
+// pinned host staging for uploads built on the host (grown on demand; the stream is drained before reuse)
+static uint8_t* host_stage(zb_engine* e, size_t bytes) {
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return nullptr;
+  if (bytes > e->h_stage_cap) {
+    if (e->h_stage) (void)hipHostFree(e->h_stage);
+    e->h_stage = nullptr;
+    e->h_stage_cap = 0;
+    const size_t cap = bytes + bytes / 4 + (1 << 20);
+    if (hipHostMalloc(&e->h_stage, cap) != hipSuccess) return nullptr;
+    e->h_stage_cap = cap;
+  }
+  return e->h_stage;
+}
+
 int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, const uint8_t* cks,
                         const uint64_t* ck_offsets, const uint8_t* payloads, const uint64_t* payload_offsets) {
   if (!e || !name || (n > 0 && (!cks || !ck_offsets || !payloads || !payload_offsets))) return ZB_EINVAL;
@@ -1945,24 +1962,37 @@ int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, c
   if ((uint64_t)(base + (int64_t)n * (1 + per)) > e->cfg.log_capacity) return fail(e, ZB_ENOMEM, "log capacity");
   if ((uint64_t)base + n * (1 + per) >= (1ull << 34)) return fail(e, ZB_EUNSUPPORTED, "log position beyond the outbox order key");
   if (e->msg_count + (ttl > 0 ? n : 0) > e->store_cap) return fail(e, ZB_ENOMEM, "message store capacity");
-  // PUBLISH commands (null key) and their message blobs, built on the host and uploaded once
-  std::vector<zb_rec> recs(n);
-  std::vector<uint8_t> blobs;
+  // PUBLISH commands (null key) and their message blobs, built on the host straight into pinned staging
+  // memory (validated and sized first, so a failure changes nothing) and uploaded once
+  static const uint8_t EMPTY = 0x80;
+  size_t blob_bytes = 0;
+  for (size_t i = 0; i < n; i++) {
+    const uint64_t nc = ck_offsets[i + 1] - ck_offsets[i];
+    const uint8_t* pl = payloads + payload_offsets[i];
+    uint64_t np = payload_offsets[i + 1] - payload_offsets[i];
+    if (np == 0 || (np == 1 && pl[0] == 0xc0)) np = 1;  // DocumentValue: nil / empty -> {}
+    else if (!((pl[0] & 0xf0) == 0x80 || pl[0] == 0xde || pl[0] == 0xdf))
+      return fail(e, ZB_EINVAL, "Document has invalid format. On root level an object is only allowed.");
+    if (nc > 0xffff) return fail(e, ZB_EINVAL, "correlation key too long");
+    blob_bytes += (4 + 16 + nn + nc + np + 7) & ~(size_t)7;
+  }
   const uint64_t arena0 = (uint64_t)e->host_hdr.arena_next;
+  if (arena0 + blob_bytes > e->cfg.arena_bytes) return fail(e, ZB_ENOMEM, "arena capacity");
+  uint8_t* stage = host_stage(e, n * sizeof(zb_rec) + blob_bytes);
+  if (!stage) return fail(e, ZB_ENOMEM, "pinned staging memory");
+  zb_rec* recs = (zb_rec*)stage;
+  uint8_t* blobs = stage + n * sizeof(zb_rec);
+  size_t off = 0;
   for (size_t i = 0; i < n; i++) {
     const uint8_t* ck = cks + ck_offsets[i];
     const uint64_t nc = ck_offsets[i + 1] - ck_offsets[i];
     const uint8_t* pl = payloads + payload_offsets[i];
     uint64_t np = payload_offsets[i + 1] - payload_offsets[i];
-    static const uint8_t EMPTY = 0x80;
-    if (np == 0 || (np == 1 && pl[0] == 0xc0)) { pl = &EMPTY; np = 1; }  // DocumentValue: nil / empty -> {}
-    else if (!((pl[0] & 0xf0) == 0x80 || pl[0] == 0xde || pl[0] == 0xdf))
-      return fail(e, ZB_EINVAL, "Document has invalid format. On root level an object is only allowed.");
-    if (nc > 0xffff) return fail(e, ZB_EINVAL, "correlation key too long");
-    const size_t off = blobs.size();
+    if (np == 0 || (np == 1 && pl[0] == 0xc0)) { pl = &EMPTY; np = 1; }
     const uint32_t len = (uint32_t)(16 + nn + nc + np);
-    blobs.resize(off + ((4 + len + 7) & ~(size_t)7), 0);
-    uint8_t* b = blobs.data() + off;
+    const size_t sz = (4 + len + 7) & ~(size_t)7;
+    uint8_t* b = blobs + off;
+    std::memset(b + 4 + len, 0, sz - 4 - len);
     std::memcpy(b, &len, 4);
     std::memcpy(b + 4, &ttl, 8);
     const uint16_t n16 = (uint16_t)nn, c16 = (uint16_t)nc;
@@ -1978,10 +2008,10 @@ int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, c
     d.payload = (uint32_t)((arena0 + off) >> 3);
     d.elem = NO_ELEM; d.intent = 0;  // PUBLISH
     d.kind = make_kind(ZB_VT_MESSAGE, ZB_RT_COMMAND, false);
+    off += sz;
   }
-  if (arena0 + blobs.size() > e->cfg.arena_bytes) return fail(e, ZB_ENOMEM, "arena capacity");
-  HIPCHECK(e, hipMemcpyAsync(e->log + base, recs.data(), n * sizeof(zb_rec), hipMemcpyHostToDevice, e->stream));
-  HIPCHECK(e, hipMemcpyAsync(e->arena + arena0, blobs.data(), blobs.size(), hipMemcpyHostToDevice, e->stream));
+  HIPCHECK(e, hipMemcpyAsync(e->log + base, recs, n * sizeof(zb_rec), hipMemcpyHostToDevice, e->stream));
+  HIPCHECK(e, hipMemcpyAsync(e->arena + arena0, blobs, blob_bytes, hipMemcpyHostToDevice, e->stream));
   HIPCHECK(e, hipMemsetAsync(e->links + base, 0xff, n * sizeof(uint64_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->srcd + base, 0, n * sizeof(uint32_t), e->stream));  // client API commands
   HIPCHECK(e, hipMemsetAsync(e->vlen + base, 0xff, n * sizeof(uint32_t), e->stream));
@@ -1995,7 +2025,7 @@ int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, c
   if (ttl > 0) e->msg_count += n;
   e->host_hdr.end = base + (int64_t)n * (1 + per);
   e->host_hdr.begin = e->host_hdr.gen_end = e->host_hdr.end;
-  e->host_hdr.arena_next += (int64_t)blobs.size();
+  e->host_hdr.arena_next += (int64_t)blob_bytes;
   return finish_batch(e);
 }
 
