@@ -13,6 +13,7 @@
 #include <chrono>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -1964,26 +1965,46 @@ int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, c
   if (e->msg_count + (ttl > 0 ? n : 0) > e->store_cap) return fail(e, ZB_ENOMEM, "message store capacity");
   // PUBLISH commands (null key) and their message blobs, built on the host straight into pinned staging
   // memory (validated and sized first, so a failure changes nothing) and uploaded once
+  // (large batches: sized and filled by up to 8 host threads over contiguous chunks)
   static const uint8_t EMPTY = 0x80;
-  size_t blob_bytes = 0;
-  for (size_t i = 0; i < n; i++) {
-    const uint64_t nc = ck_offsets[i + 1] - ck_offsets[i];
-    const uint8_t* pl = payloads + payload_offsets[i];
-    uint64_t np = payload_offsets[i + 1] - payload_offsets[i];
-    if (np == 0 || (np == 1 && pl[0] == 0xc0)) np = 1;  // DocumentValue: nil / empty -> {}
-    else if (!((pl[0] & 0xf0) == 0x80 || pl[0] == 0xde || pl[0] == 0xdf))
-      return fail(e, ZB_EINVAL, "Document has invalid format. On root level an object is only allowed.");
-    if (nc > 0xffff) return fail(e, ZB_EINVAL, "correlation key too long");
-    blob_bytes += (4 + 16 + nn + nc + np + 7) & ~(size_t)7;
+  const size_t nth = n >= 65536 ? std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency())) : 1;
+  const size_t chunk = (n + nth - 1) / nth;
+  std::vector<size_t> part_bytes(nth + 1, 0);
+  std::vector<int> part_err(nth, 0);
+  auto run_parts = [&](auto&& body) {
+    std::vector<std::thread> ths;
+    for (size_t t = 1; t < nth; t++) ths.emplace_back(body, t);
+    body((size_t)0);
+    for (auto& th : ths) th.join();
+  };
+  run_parts([&](size_t t) {
+    size_t bytes = 0;
+    for (size_t i = t * chunk; i < std::min(n, (t + 1) * chunk); i++) {
+      const uint64_t nc = ck_offsets[i + 1] - ck_offsets[i];
+      const uint8_t* pl = payloads + payload_offsets[i];
+      uint64_t np = payload_offsets[i + 1] - payload_offsets[i];
+      if (np == 0 || (np == 1 && pl[0] == 0xc0)) np = 1;  // DocumentValue: nil / empty -> {}
+      else if (!((pl[0] & 0xf0) == 0x80 || pl[0] == 0xde || pl[0] == 0xdf)) { part_err[t] = 1; return; }
+      if (nc > 0xffff) { part_err[t] = 2; return; }
+      bytes += (4 + 16 + nn + nc + np + 7) & ~(size_t)7;
+    }
+    part_bytes[t + 1] = bytes;
+  });
+  for (size_t t = 0; t < nth; t++) {  // (the first failing chunk's error, as the sequential check reports it)
+    if (part_err[t] == 1) return fail(e, ZB_EINVAL, "Document has invalid format. On root level an object is only allowed.");
+    if (part_err[t] == 2) return fail(e, ZB_EINVAL, "correlation key too long");
   }
+  for (size_t t = 0; t < nth; t++) part_bytes[t + 1] += part_bytes[t];
+  const size_t blob_bytes = part_bytes[nth];
   const uint64_t arena0 = (uint64_t)e->host_hdr.arena_next;
   if (arena0 + blob_bytes > e->cfg.arena_bytes) return fail(e, ZB_ENOMEM, "arena capacity");
   uint8_t* stage = host_stage(e, n * sizeof(zb_rec) + blob_bytes);
   if (!stage) return fail(e, ZB_ENOMEM, "pinned staging memory");
   zb_rec* recs = (zb_rec*)stage;
   uint8_t* blobs = stage + n * sizeof(zb_rec);
-  size_t off = 0;
-  for (size_t i = 0; i < n; i++) {
+  run_parts([&](size_t t) {
+  size_t off = part_bytes[t];
+  for (size_t i = t * chunk; i < std::min(n, (t + 1) * chunk); i++) {
     const uint8_t* ck = cks + ck_offsets[i];
     const uint64_t nc = ck_offsets[i + 1] - ck_offsets[i];
     const uint8_t* pl = payloads + payload_offsets[i];
@@ -2010,6 +2031,7 @@ int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, c
     d.kind = make_kind(ZB_VT_MESSAGE, ZB_RT_COMMAND, false);
     off += sz;
   }
+  });
   HIPCHECK(e, hipMemcpyAsync(e->log + base, recs, n * sizeof(zb_rec), hipMemcpyHostToDevice, e->stream));
   HIPCHECK(e, hipMemcpyAsync(e->arena + arena0, blobs, blob_bytes, hipMemcpyHostToDevice, e->stream));
   HIPCHECK(e, hipMemsetAsync(e->links + base, 0xff, n * sizeof(uint64_t), e->stream));
