@@ -27,7 +27,8 @@ using namespace zbg;
 
 namespace {
 
-constexpr int WAVES_PER_SYNC = 16;
+constexpr int WAVES_PER_SYNC = 16;      // the first batch; each later batch of the step doubles, up to
+constexpr int WAVES_PER_SYNC_MAX = 64;  // (long chains: fewer host round trips, at most one batch of empty waves)
 constexpr int EV_PER_WAVE = 4;  // before k_process, after k_process, after k_emit, after the aux kernels
 constexpr uint64_t STATIC_ARENA_BYTES = 1ull << 20;  // {} at ref 0 + harness job completion payloads
 constexpr uint64_t TRAJ_BUDGET_BYTES = 256ull << 20;  // per-(generation, workgroup) counts of the trajectory path
@@ -771,7 +772,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMemset(e->raux, 0, e->cfg.row_capacity * sizeof(RowAux)) != hipSuccess) return cleanup(ZB_EDEVICE);
   if (hipMalloc(&e->need_children, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMemset(e->need_children, 0, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_EDEVICE);
-  e->ev.resize(EV_PER_WAVE * WAVES_PER_SYNC);
+  e->ev.resize(EV_PER_WAVE * WAVES_PER_SYNC_MAX);
   for (auto& x : e->ev)
     if (hipEventCreate(&x) != hipSuccess) return cleanup(ZB_EDEVICE);
   const uint8_t empty = 0x80;
@@ -1582,8 +1583,10 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     if (rc < 0) return rc;
     quiescent = e->host_hdr.begin == e->host_hdr.end;
   }
+  int next_batch = WAVES_PER_SYNC;
   while (!quiescent && (max_waves == 0 || launched < max_waves)) {
-    int batch = WAVES_PER_SYNC;
+    int batch = next_batch;
+    next_batch = std::min(2 * next_batch, WAVES_PER_SYNC_MAX);
     if (max_waves) batch = std::min<int>(batch, (int)(max_waves - launched));
     for (int i = 0; i < batch; i++) {
       WaveParams p = wave_params(e);
