@@ -108,7 +108,8 @@ typedef struct zb_step_stats {
   uint64_t condition_payload_bytes; /* payload bytes read by exclusive-gateway evaluations */
   double wave_kernel_ms;       /* device time of all wave kernels (HIP events on the engine stream) */
   double wall_ms;              /* host wall time of the zb_step call */
-  double process_kernel_ms;    /* k_process share of wave_kernel_ms (trajectory: count pass) */
+  double process_kernel_ms;    /* k_process share of wave_kernel_ms (trajectory: count pass; wave pipeline without
+                                  ZB_WAVE_EVENTS=1: all of it, timed per batch of waves) */
   double emit_kernel_ms;       /* k_scan + k_emit share (trajectory: scans + emit pass) */
   double aux_kernel_ms;        /* k_merge + k_cond share */
   uint64_t path;               /* 0: wave pipeline, 1: trajectory path (zb_traj.hip) ran the step,

@@ -248,6 +248,7 @@ struct zb_engine {
   uint32_t dr_slow_tiles = 0;    // how many tiles the last drain ran through k_ser_write
   bool dr_split = false;         // the last drain ran k_ser_fast + k_ser_write (events 2-4, 5-3)
   int ser_fast = 1;              // ZB_SER_FAST=0: every tile through k_ser_write
+  bool wave_events = false;      // ZB_WAVE_EVENTS=1: timing events around every wave's kernels
   int tmpl_io = 0;               // ZB_TMPL_IO=1: class batches emitted in instance order (k_tmpl_io)
   int ser_lenbuf = 0;            // ZB_SER_LENBUF=1: value lengths through their own buffer, not vlen
   zb_record_header* dr_hdr = nullptr;
@@ -695,6 +696,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (const char* m = std::getenv("ZB_SER_EXP")) e->ser_exp = atoi(m);
   if (const char* m = std::getenv("ZB_SER_FAST")) e->ser_fast = atoi(m);
   if (const char* m = std::getenv("ZB_TMPL_IO")) e->tmpl_io = atoi(m);
+  if (const char* m = std::getenv("ZB_WAVE_EVENTS")) e->wave_events = atoi(m) != 0;
   if (const char* m = std::getenv("ZB_SER_LENBUF")) e->ser_lenbuf = atoi(m);
   if (const char* g = std::getenv("ZB_WAVE_GRID")) e->wave_grid_fixed = std::max(0, std::min(atoi(g), (int)WAVE_GRID_MAX));
   if (e->cfg.log_capacity == 0) e->cfg.log_capacity = 1ull << 22;
@@ -1588,10 +1590,14 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     int batch = next_batch;
     next_batch = std::min(2 * next_batch, WAVES_PER_SYNC_MAX);
     if (max_waves) batch = std::min<int>(batch, (int)(max_waves - launched));
+    // timing events cost ~5 us of stream time each between kernels (C2: 4 per wave = 2.9 ms of a 41 ms
+    // step): per wave only with ZB_WAVE_EVENTS=1 (process / emit / aux split), else one pair per batch
+    const bool per_wave = e->wave_events;
+    if (!per_wave) HIPCHECK(e, hipEventRecord(e->ev[0], e->stream));
     for (int i = 0; i < batch; i++) {
       WaveParams p = wave_params(e);
       hipEvent_t* ev = &e->ev[EV_PER_WAVE * i];
-      HIPCHECK(e, hipEventRecord(ev[0], e->stream));
+      if (per_wave) HIPCHECK(e, hipEventRecord(ev[0], e->stream));
       if (p.has_parallel || p.term) {  // scope-wide counters / first-child requests of the chunk
         launch_pre(p, e->stream);
         if (p.term) launch_children(p, e->stream);
@@ -1599,38 +1605,46 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
       if (e->has_io) launch_map(p, e->stream);  // io-mapping results of the chunk's records
       if (e->wave_fused_grid) {  // process + scan + emit in one launch (k_wave)
         launch_wave(p, e->wave_fused_grid, e->stream);
-        HIPCHECK(e, hipEventRecord(ev[1], e->stream));
-        HIPCHECK(e, hipEventRecord(ev[2], e->stream));
+        if (per_wave) HIPCHECK(e, hipEventRecord(ev[1], e->stream));
+        if (per_wave) HIPCHECK(e, hipEventRecord(ev[2], e->stream));
       } else {
         launch_process(p, e->stream);
-        HIPCHECK(e, hipEventRecord(ev[1], e->stream));
+        if (per_wave) HIPCHECK(e, hipEventRecord(ev[1], e->stream));
         launch_scan(p, e->stream);
         launch_emit(p, e->stream);
-        HIPCHECK(e, hipEventRecord(ev[2], e->stream));
+        if (per_wave) HIPCHECK(e, hipEventRecord(ev[2], e->stream));
       }
       // payload kernels for this wave's deferred work (only when the model can produce any)
       if (e->has_catch) launch_subscribe(p, e->stream);  // this wave's subscribe steps (outbox)
       if (e->has_merges) launch_merge(p, e->stream);
       if (e->has_splits) launch_cond(p, e->stream);
-      HIPCHECK(e, hipEventRecord(ev[3], e->stream));
+      if (per_wave) HIPCHECK(e, hipEventRecord(ev[3], e->stream));
       e->wave++;
       e->epoch++;
     }
+    if (!per_wave) HIPCHECK(e, hipEventRecord(e->ev[1], e->stream));
     HIPCHECK(e, hipGetLastError());
     HIPCHECK(e, hipMemcpyAsync(e->h_hdr_pinned, e->hdr + (e->wave & 1), sizeof(WaveHdr), hipMemcpyDeviceToHost,
                                e->stream));
     HIPCHECK(e, hipMemcpyAsync(e->h_err_pinned, e->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHECK(e, hipStreamSynchronize(e->stream));
-    for (int i = 0; i < batch; i++) {
-      const hipEvent_t* ev = &e->ev[EV_PER_WAVE * i];
-      float ms0 = 0, ms1 = 0, ms2 = 0;
-      HIPCHECK(e, hipEventElapsedTime(&ms0, ev[0], ev[1]));
-      HIPCHECK(e, hipEventElapsedTime(&ms1, ev[1], ev[2]));
-      HIPCHECK(e, hipEventElapsedTime(&ms2, ev[2], ev[3]));
-      st.process_kernel_ms += ms0;
-      st.emit_kernel_ms += ms1;
-      st.aux_kernel_ms += ms2;
-      st.wave_kernel_ms += ms0 + ms1 + ms2;
+    if (per_wave) {
+      for (int i = 0; i < batch; i++) {
+        const hipEvent_t* ev = &e->ev[EV_PER_WAVE * i];
+        float ms0 = 0, ms1 = 0, ms2 = 0;
+        HIPCHECK(e, hipEventElapsedTime(&ms0, ev[0], ev[1]));
+        HIPCHECK(e, hipEventElapsedTime(&ms1, ev[1], ev[2]));
+        HIPCHECK(e, hipEventElapsedTime(&ms2, ev[2], ev[3]));
+        st.process_kernel_ms += ms0;
+        st.emit_kernel_ms += ms1;
+        st.aux_kernel_ms += ms2;
+        st.wave_kernel_ms += ms0 + ms1 + ms2;
+      }
+    } else {  // the batch as a whole (kernel boundaries included), reported as the process share
+      float ms = 0;
+      HIPCHECK(e, hipEventElapsedTime(&ms, e->ev[0], e->ev[1]));
+      st.process_kernel_ms += ms;
+      st.wave_kernel_ms += ms;
     }
     launched += batch;
     st.launches += batch;
