@@ -9,7 +9,7 @@ S4="SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_LEVEL_WAVES SQ_INSTS_LDS SQ_LDS
 PMC_SETS="FETCH_SIZE;WRITE_SIZE;$S3;$S4" BENCH_ARGS="--no-extras" TAG=c3_10000000 ./run_gpu_pmc.sh || exit 1
 python3 tools/pmc_summary.py gpurun_out/pmc_c3_10000000 gpurun_out/pmc_c3_10000000.json | head -4
 cp gpurun_out/pmc_c3_10000000.json profiles/r02/pmc_c3_10000000.json
-O=gpurun_out/r02ag
+O=gpurun_out/${RUN_TAG:-r02ag}
 mkdir -p $O
 timeout -k 10 600 python3 bench.py > $O/bench_full.json 2> $O/bench_full.err || { echo "full bench failed"; tail -20 $O/bench_full.err; exit 1; }
 python3 -c "import json; d=json.load(open('$O/bench_full.json')); print(d['value']/1e9, d['ms_per_step'], d['roofline']['kernel'], d['roofline']['frac'], d['roofline']['traffic']); print({k: (v['value'] / 1e9, v['ms_per_step']) for k, v in d.get('extras', {}).items()}); print(d['cpu_baseline']['value'], d['cpu_baseline']['multi_partition']['value'])"
