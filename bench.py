@@ -6,16 +6,19 @@ gateways with json-el conditions over msgpack payloads {"amount", "region", "sco
 10,000,000 concurrent instances per GPU. One step = one processing tick of the partition
 (GPU timing):
   1. inject the staged 10M CREATE commands (resident in HBM) at the log tail,
-  2. run every lockstep wave to quiescence (~130M records, ~120M WORKFLOW_INSTANCE transitions),
+  2. run every lockstep wave to quiescence (~101.7M records written, all WORKFLOW_INSTANCE events: 11 or 13
+     transitions per instance),
   3. drain: serialize every record the tick wrote into the exact reference record values + record
      headers, in HBM (zb_serialize) -- the emitted record stream a JNI shim appends to the log.
 The D2H copy of that stream into pinned host memory crosses PCIe; per the task contract it is never
 `value` and is reported beside it (value_pcie_inclusive), measured on one extra step.
 
 --config c2 | c3 | c4 | c5 selects another BASELINE configuration (c5: bench_extra.py).
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process and one partition per GPU,
-each with its own instances (instance i of the node -> partition i mod P); partitions never communicate
-for C1-C4 (weak scaling, no data-path collective; barrier + max-over-ranks timing through
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process and one partition per GPU;
+rank r takes the contiguous block of instances [r*n, (r+1)*n) of the node (instances are independent, so this
+is the same per-partition load as the reference's round-robin dispatch; payloads are counter-based per
+instance index, so every instance's payload is the same whatever the partitioning). Partitions never
+communicate for C1-C4 (weak scaling, no data-path collective; barrier + max-over-ranks timing through
 torch.distributed gloo).
 
 Prints ONE JSON line on rank 0 with "roofline" and "cpu_baseline".

@@ -245,6 +245,10 @@ int zb_comm_exchange(zb_engine* e, int kind, uint64_t* received);
 
 /* ---- output -------------------------------------------------------------------------- */
 int64_t zb_log_size(zb_engine* e);
+/* Source event position of records [start, start+count) (LogEntryDescriptor sourceEventPosition: the record
+ * whose processing wrote it, TypedStreamWriterImpl / TypedCommandWriterImpl.configureSourceContext), -1 for
+ * records another writer appended (client commands, zb_submit). */
+int zb_read_source_positions(zb_engine* e, int64_t start, int64_t count, int64_t* out);
 /* Copies raw descriptors [start, start+count) to host. */
 int zb_read_descriptors(zb_engine* e, int64_t start, int64_t count, zb_rec* out);
 /* Serializes records [start, start+count) on the GPU into reference value bytes and copies them

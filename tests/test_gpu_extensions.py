@@ -31,8 +31,8 @@ def compare_logs(o, e, start=0):
     ref, got = o.records(start), e.records(start)
     assert len(got) == len(ref), (len(got), len(ref))
     for a, b in zip(ref, got):
-        assert (a.position, a.key, a.record_type, a.value_type, a.intent) == \
-               (b.position, b.key, b.record_type, b.value_type, b.intent), (a, b)
+        assert (a.position, a.source_position, a.key, a.record_type, a.value_type, a.intent) == \
+               (b.position, b.source_position, b.key, b.record_type, b.value_type, b.intent), (a, b)
         if b.record_type == R.RT_REJECTION:
             assert a.rejection_type == b.rejection_type, (a, b)
         assert a.value == b.value, (a.position, msgpack.unpackb(a.value, raw=False), msgpack.unpackb(b.value, raw=False))

@@ -75,7 +75,8 @@ def test_frames_c2_properties():
     assert len(fr) == total == 169 * n  # CREATE, 108 WF events, 20 JOB CREATE, 40 harness job events
     recs = e.records()
     for f, r in zip(fr, recs):
-        assert (f["position"], f["key"], f["value"]) == (r.position, r.key, r.value)
+        assert (f["position"], f["source_position"], f["key"], f["value"]) == \
+               (r.position, r.source_position, r.key, r.value)
     # sources: every non-submitted record's source precedes it; batches are runs of one source
     runs = {}
     for f in fr:
@@ -90,4 +91,45 @@ def test_frames_c2_properties():
             assert fs[0]["flags"] == 0
         else:
             assert fs[0]["flags"] == R.FLAG_BATCH_BEGIN and fs[-1]["flags"] == R.FLAG_BATCH_END
+    e.close()
+
+
+def test_frames_after_values_drain_with_rejections(monkeypatch):
+    """records() then frames() over one log holding rejections: the values drain writes the measured
+    value lengths back into the engine's length hints, and the frames size pass must still add each rejection's
+    reason. Product configuration (ZB_VLEN_CHECK=0): the size pass trusts the hints."""
+    from zeebe_amd.engine import Engine
+
+    monkeypatch.setenv("ZB_VLEN_CHECK", "0")
+    cfg = workloads.CONFIGS["c1"]
+    xml = cfg["workflow"]().to_xml()
+    o = zbref.Oracle()
+    e = Engine(external_jobs=True)
+    o.set_harness(False)
+    for x in (o, e):
+        x.deploy(xml, 100, 1)
+    payloads = workloads.split(*cfg["payloads"](30))
+    for p in payloads:
+        o.create(cfg["process"], p)
+    o.create("missing", b"\x80")  # CREATE rejection
+    e.create(cfg["process"], payloads)
+    e.create("missing", [b"\x80"])
+    o.run()
+    assert e.step()["quiescent"]
+    pos = o.log_size()
+    # CANCEL of instances that do not exist / UPDATE_PAYLOAD of one that does not: NOT_APPLICABLE rejections
+    recs = [(R.RT_COMMAND, R.VT_WORKFLOW_INSTANCE, R.WI_CANCEL, 7777 + 5 * i, b"\x80") for i in range(3)]
+    recs.append((R.RT_COMMAND, R.VT_WORKFLOW_INSTANCE, R.WI_UPDATE_PAYLOAD, -1, R.wf_record(workflow_instance_key=999)))
+    recs.append((R.RT_COMMAND, R.VT_WORKFLOW_INSTANCE, R.WI_CANCEL, 1, b"\x80"))
+    for r in recs:
+        o.submit(*r)
+    e.submit_records(recs)
+    o.run()
+    assert e.step()["quiescent"]
+    ref, got = o.records(), e.records()  # the values drain first (writes the measured lengths back)
+    assert [(r.key, r.record_type, r.intent, r.value) for r in ref] == [(r.key, r.record_type, r.intent, r.value)
+                                                                        for r in got]
+    assert sum(1 for r in got if r.record_type == R.RT_REJECTION) >= 5
+    assert_frames_equal(o, e)
+    assert_frames_equal(o, e, pos)
     e.close()

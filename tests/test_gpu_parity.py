@@ -15,13 +15,16 @@ from zeebe_amd import bpmn, workloads
 pytestmark = pytest.mark.gpu
 
 # Every case runs through both GPU pipelines: the trajectory path (zb_traj.hip, taken for a batch of
-# CREATEs on an idle partition) and the general wave pipeline (zb_wave.hip, forced by wave_only).
-PATHS = ["traj", "wave"]
+# CREATEs on an idle partition) and the general wave pipeline (zb_wave.hip, forced by wave_only), each in the
+# product configuration and with ZB_VLEN_CHECK=1 (the drain's size pass checks every value length an emitting
+# kernel wrote against the encoder's dry run, and fails the drain on a difference).
+PATHS = ["traj", "wave", "traj+vlencheck", "wave+vlencheck"]
 
 
 @pytest.fixture(params=PATHS)
-def path(request):
-    return request.param
+def path(request, monkeypatch):
+    monkeypatch.setenv("ZB_VLEN_CHECK", "1" if request.param.endswith("+vlencheck") else "0")
+    return request.param.split("+")[0]
 
 
 def _engine(**kw):
@@ -56,8 +59,8 @@ def _compare(o, e):
     got = e.records()
     assert len(got) == len(ref), (len(got), len(ref))
     for a, b in zip(ref, got):
-        assert (a.position, a.key, a.record_type, a.value_type, a.intent) == \
-               (b.position, b.key, b.record_type, b.value_type, b.intent), (a, b)
+        assert (a.position, a.source_position, a.key, a.record_type, a.value_type, a.intent) == \
+               (b.position, b.source_position, b.key, b.record_type, b.value_type, b.intent), (a, b)
         assert a.value == b.value, (a.position, msgpack.unpackb(a.value, raw=False),
                                     msgpack.unpackb(b.value, raw=False))
     assert_frames_equal(o, e)

@@ -84,8 +84,6 @@ struct zb_engine {
   MNode* map_ws = nullptr;      // k_map tree workspaces
   int ser_mode = 0;              // ZB_SER_MODE: 0 = two passes (size, scan, write), 1 = single pass (look-back)
   int ser_nt = 1;                // ZB_SER_NT=0: plain (not non-temporal) stores in the drain write pass
-  int ser_exp = 0;               // ZB_SER_EXP: measurement knobs of the fast write path (1 no encode, 2 no stream-out,
-                                 // 4 no header stores) -- the output is wrong with any of them set
 
   // device state
   zb_rec* log = nullptr;
@@ -488,7 +486,6 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   *e->h_ctl_pinned = c;
   HIPCHECK(e, hipMemcpyAsync(e->t_ctl, e->h_ctl_pinned, sizeof(TrajCtl), hipMemcpyHostToDevice, e->stream));
   TrajParams p{};
-  if (const char* x = std::getenv("ZB_TMPL_EXP")) p.texp = atoi(x);  // (measurement only: wrong logs)
   p.log = e->log;
   p.vconst = e->d_vconst.p;
   p.srcd = e->srcd;
@@ -693,7 +690,6 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   e->cfg = *cfg;
   if (const char* m = std::getenv("ZB_SER_MODE")) e->ser_mode = std::strcmp(m, "fused") == 0 ? 1 : 0;
   if (const char* m = std::getenv("ZB_SER_NT")) e->ser_nt = atoi(m);
-  if (const char* m = std::getenv("ZB_SER_EXP")) e->ser_exp = atoi(m);
   if (const char* m = std::getenv("ZB_SER_FAST")) e->ser_fast = atoi(m);
   if (const char* m = std::getenv("ZB_TMPL_IO")) e->tmpl_io = atoi(m);
   if (const char* m = std::getenv("ZB_WAVE_EVENTS")) e->wave_events = atoi(m) != 0;
@@ -1672,6 +1668,17 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
 
 int64_t zb_log_size(zb_engine* e) { return e ? e->host_hdr.end : -1; }
 
+int zb_read_source_positions(zb_engine* e, int64_t start, int64_t count, int64_t* out) {
+  if (!e || start < e->log_floor || count < 0 || start + count > e->host_hdr.end || (!out && count)) return ZB_EINVAL;
+  if (count == 0) return ZB_OK;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  std::vector<uint32_t> d((size_t)count);
+  HIPCHECK(e, hipMemcpyAsync(d.data(), e->srcd + start, count * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  for (int64_t i = 0; i < count; i++) out[i] = d[(size_t)i] ? start + i - (int64_t)d[(size_t)i] : -1;
+  return ZB_OK;
+}
+
 int zb_read_descriptors(zb_engine* e, int64_t start, int64_t count, zb_rec* out) {
   if (!e || start < e->log_floor || count < 0 || start + count > e->host_hdr.end || (!out && count)) return ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
@@ -1693,7 +1700,11 @@ int zb_serialize_frames(zb_engine* e, int64_t start, int64_t count, const zb_fra
 }
 
 int zb_set_request_metadata(zb_engine* e, size_t n, const uint64_t* request_ids, const int32_t* request_stream_ids) {
-  if (!e || (n && (!request_ids || !request_stream_ids)) || n > e->staged.size()) return ZB_EINVAL;
+  if (!e || (n && (!request_ids || !request_stream_ids))) return ZB_EINVAL;
+  // only records staged since the last injection (e->staged holds them while staged_pending): after zb_step the
+  // indices would name records of the batch already in the log
+  if (n && !e->staged_pending) return fail(e, ZB_EINVAL, "no staged records: request metadata goes with zb_submit*");
+  if (n > e->staged.size()) return fail(e, ZB_EINVAL, "more request metadata than staged records");
   const int64_t first = (int64_t)(e->staged.size() - n);
   // (staged indices only grow between injections: the list stays sorted unless a range is set twice)
   for (size_t i = 0; i < n; i++) {
@@ -1759,7 +1770,6 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
   if (fc && !e->reqs.empty()) HIPCHECK(e, e->d_reqs.upload(e->reqs, e->stream));
   SerParams sp{};
   sp.nt = e->ser_nt;
-  sp.exp = e->ser_exp;
   if (fc) {
     sp.frames = 1;
     sp.stream_id = fc->stream_id;

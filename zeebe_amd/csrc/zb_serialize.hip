@@ -461,7 +461,12 @@ __global__ void __launch_bounds__(256) k_ser_size(SerParams P0) {
   for (int j = 0; j < SER_SIZE_TILES; j++) {
     const int64_t i = ((int64_t)blockIdx.x * SER_SIZE_TILES + j) * 256 + threadIdx.x;
     const bool live = i < P0.count;
-    if (live && !measure[j] && FRAMES) n[j] = (FRAME_PREFIX + n[j] + 7) & ~7u;  // (a known length: no reason)
+    if (live && !measure[j] && FRAMES) {
+      // a known value length (an emitting kernel's, or one a values drain measured and wrote back -- which
+      // includes rejections): the frame adds the rejection reason of the record
+      const zb_rec d = P0.log[P0.start + i];
+      n[j] = (FRAME_PREFIX + reason_len(reason_of(d)) + n[j] + 7) & ~7u;
+    }
     if (live && !P0.len_in_vlen) P0.lengths[i] = n[j];
     unsigned long long y = n[j];
     for (int dd = 32; dd >= 1; dd >>= 1) y += __shfl_down(y, dd, 64);
@@ -611,7 +616,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
   const int64_t pos = P.start + i;
   if (live) {
     if (kind_vt(d.kind) != ZB_VT_INCIDENT && !(d.kind & KIND_RAW)) pay = *(const uint32_t*)(P.arena + (uint64_t)d.payload * 8);
-    if (!FRAMES && !(P.exp & 4)) {
+    if (!FRAMES) {
       const zb_record_header h = record_header(d, pos, len, off);
       if (NT) {
         const uint64_t* hw = (const uint64_t*)&h;
@@ -741,7 +746,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(IMG
   for (int k = 0; k < SER_WG / 64; k++)
     if (k < wv) pw += s_wsum[k];
   const uint64_t off = o0 + pw + x - len;
-  if (live && !(P0.exp & 4)) {
+  if (live) {
     const zb_record_header h = record_header(d, P0.start + i, len, off);
     const uint64_t* hw = (const uint64_t*)&h;
     uint64_t* dh = (uint64_t*)(P0.headers + i);
@@ -760,12 +765,12 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(IMG
     for (int j = 0; j < k; j++) lo += s_wsum[j];
     const uint32_t sh = (uint32_t)(((uintptr_t)(P0.out + lo)) & 15);
     __syncthreads();
-    if (!(P0.exp & 2)) stream_image(img, P0.out, lo, sh, s_wsum[k], true);
+    stream_image(img, P0.out, lo, sh, s_wsum[k], true);
     __syncthreads();  // the image is reused by the next wave
   };
 #pragma unroll 1
   for (int k = 0; k < wv; k++) stream_wave(k);
-  if (live && !(P0.exp & 1)) {
+  if (live) {
     const uint64_t lo = o0 + pw;  // this wave's range starts at the tile start + the waves before it
     FastW w;
     w.begin(img, (uint32_t)(((uintptr_t)(P0.out + lo)) & 15) + (uint32_t)(off - lo));

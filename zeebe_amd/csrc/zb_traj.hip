@@ -1608,16 +1608,8 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
       d.elem = t.elem; d.intent = t.intent; d.kind = t.kind;
       if (active) {
         if (pos0 + k < (int64_t)P.log_cap) {
-          const uint32_t sd = (uint32_t)(pos0 + k - (prev0 + t.pad[0]));
-          if (P.texp & 4) {  // (experiment: non-temporal stores)
-            const uint64_t* dw = (const uint64_t*)&d;
-            uint64_t* lw = (uint64_t*)(P.log + pos0 + k);
-            for (int q = 0; q < 4; q++) __builtin_nontemporal_store(dw[q], lw + q);
-            __builtin_nontemporal_store(sd, P.srcd + pos0 + k);
-          } else {
-            if (!(P.texp & 1)) P.log[pos0 + k] = d;
-            if (!(P.texp & 2)) P.srcd[pos0 + k] = sd;
-          }
+          P.log[pos0 + k] = d;
+          P.srcd[pos0 + k] = (uint32_t)(pos0 + k - (prev0 + t.pad[0]));
           // the value's length (zb_serialize.hip encode_value) from the element's constants and the variable fields
           const uint8_t vt = kind_vt(d.kind), rt = kind_rt(d.kind);
           uint32_t vl = VLEN_UNKNOWN;
@@ -1626,8 +1618,7 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
             const ValueConst vc = kload(P.vconst, (uint64_t)d.elem);
             vl = (vt == ZB_VT_JOB ? vc.job : vc.wf) + mp_int_len(d.inst_key) + mp_int_len(d.scope_key) + mp_bin_len(plen);
           }
-          if (P.texp & 4) __builtin_nontemporal_store(vl, P.vlen + pos0 + k);
-          else if (!(P.texp & 2)) P.vlen[pos0 + k] = vl;
+          P.vlen[pos0 + k] = vl;
         } else err |= DE_LOG_FULL;
       }
     }

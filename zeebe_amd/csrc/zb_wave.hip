@@ -1197,11 +1197,13 @@ __global__ void __launch_bounds__(WG) k_emit(WaveParams P) {
 // Look-back state: per tile LB_FIELDS 8-byte granules {tag, value} (agent-scope atomic stores and loads; the
 // data is its own flag, cdna_hip_programming.md Guideline 16 R2). A tile first publishes its aggregate
 // (tag = epoch:AGG), then its inclusive prefix (tag = epoch:INC); a reader accepts a tile's granules only when
-// all of them carry the same tag. Spins are bounded: a hand-off that never arrives sets DE_TIMEOUT, the wave's
-// results are void and the host stops the partition -- it never hangs the device.
+// all of them carry the same tag. Waiting is bounded in time (the constant-rate wall clock, not a spin count:
+// a resident predecessor that the scheduler time-slices out keeps its waiters spinning without progress for
+// as long as it is descheduled): a hand-off that has not arrived after LB_TIMEOUT_TICKS sets DE_TIMEOUT, the
+// wave's results are void and the host stops the partition -- it never hangs the device.
 constexpr int LB_FIELDS = 12;  // rec wf job row bytes_lo bytes_hi merges conds | transitions completed created canceled
 constexpr int LB_STRIDE = 16;  // granules per tile (128 B)
-constexpr uint32_t LB_SPIN_LIMIT = 1u << 16;  // ~0.1 s per granule; then DE_TIMEOUT and every waiter gives up
+constexpr uint64_t LB_TIMEOUT_TICKS = 400000000ull;  // 4 s of the 100 MHz wall clock per look-back, then DE_TIMEOUT
 
 __device__ __forceinline__ uint32_t lb_tag(int64_t epoch, uint32_t inc) {
   return (uint32_t)((((uint64_t)epoch + 1) << 1) | inc);
@@ -1344,6 +1346,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
       uint64_t acc = 0;  // lanes < 12: exclusive prefix of field `lane`
       if (tile > 0) {
         bool timeout = false;
+        const uint64_t t_start = wall_clock64();
         for (int64_t p = tile - 1;;) {
           const int64_t q = p - j;
           uint32_t v = 0, tg = tag_inc;  // predecessors before tile 0 count as the (empty) inclusive start
@@ -1354,8 +1357,9 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
               tg = (uint32_t)(x >> 32);
               v = (uint32_t)x;
               if (tg == tag_agg || tg == tag_inc) break;
-              if (spins >= LB_SPIN_LIMIT ||
-                  ((spins & 255) == 255 && (__hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & DE_TIMEOUT))) {
+              if ((spins & 255) == 255 &&
+                  (wall_clock64() - t_start > LB_TIMEOUT_TICKS ||
+                   (__hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & DE_TIMEOUT))) {
                 timeout = true;
                 break;
               }

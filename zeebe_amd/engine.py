@@ -119,6 +119,7 @@ def lib():
         L.zb_log_size.restype = ctypes.c_int64
         L.zb_log_size.argtypes = [vp]
         L.zb_read_descriptors.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
+        L.zb_read_source_positions.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
         L.zb_drain.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
         L.zb_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
@@ -156,7 +157,7 @@ EXPORTED_SYMBOLS = ["zb_engine_create", "zb_engine_destroy", "zb_last_error", "z
                     "zb_outbox_count", "zb_outbox_take", "zb_comm_unique_id", "zb_comm_init", "zb_comm_pending",
                     "zb_comm_exchange", "zb_submit", "zb_read_instances", "zb_snapshot", "zb_restore",
                     "zb_validate_deployment", "zb_serialize", "zb_drain_copy", "zb_pinned_alloc", "zb_pinned_free",
-                    "zb_serialize_frames", "zb_set_request_metadata"]
+                    "zb_serialize_frames", "zb_set_request_metadata", "zb_read_source_positions"]
 
 
 def validate_deployment(xml):
@@ -367,10 +368,12 @@ class Engine:
         buf = ctypes.create_string_buffer(max(need.value, 1))
         self._check(self._L.zb_drain(self._h, start, count, hdrs, buf, need.value, ctypes.byref(need)))
         raw = buf.raw
+        src = (ctypes.c_int64 * count)()
+        self._check(self._L.zb_read_source_positions(self._h, start, count, src))
         out = []
         for i, h in enumerate(hdrs):
             v = raw[h.value_offset:h.value_offset + h.value_length]
-            out.append(Record(start + i, -1, h.key, h.record_type, h.value_type, h.intent, h.rejection_type, v))
+            out.append(Record(start + i, src[i], h.key, h.record_type, h.value_type, h.intent, h.rejection_type, v))
         return out
 
     # ---- partition interface of zeebe_amd.cluster (message correlation, config 5)

@@ -2,7 +2,7 @@
 
 Shared by the parity tests and bench.py. Payloads are msgpack documents built with the
 reference writer's encoding rules (MsgPackWriter.java:143-305: minimal integers, fixstr keys);
-all generators are deterministic (seeded counter-based RNG, numpy Philox, seed 42).
+all generators are deterministic (counter-based Philox4x32-10, seed 42, counter = instance index).
 """
 from __future__ import annotations
 
@@ -58,14 +58,43 @@ def order_string_payloads(n: int, start: int = 0) -> Tuple[bytes, np.ndarray]:
 REGIONS = ("EU", "US", "APAC")
 
 
+def philox4x32(counter: np.ndarray, key: int) -> np.ndarray:
+    """Philox4x32-10 (Salmon et al., SC'11) of the 128-bit counters (i, 0, 0, 0), key (key, 0): (n, 4) uint32.
+    Counter-based: instance i's values depend on i alone, so any partitioning of the instances generates the
+    same payload for the same instance (stream = instance index)."""
+    m0, m1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+    mask = np.uint64(0xFFFFFFFF)
+    c0 = counter.astype(np.uint64) & mask
+    c1 = (counter.astype(np.uint64) >> np.uint64(32)) & mask
+    c2 = np.zeros_like(c0)
+    c3 = np.zeros_like(c0)
+    k0, k1 = np.uint64(key & 0xFFFFFFFF), np.uint64(0)
+    for _ in range(10):
+        p0 = m0 * c0
+        p1 = m1 * c2
+        hi0, lo0 = p0 >> np.uint64(32), p0 & mask
+        hi1, lo1 = p1 >> np.uint64(32), p1 & mask
+        c0, c1, c2, c3 = hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0
+        k0 = (k0 + np.uint64(0x9E3779B9)) & mask
+        k1 = (k1 + np.uint64(0xBB67AE85)) & mask
+    return np.stack([c0, c1, c2, c3], axis=1).astype(np.uint32)
+
+
+def xor_fields(n: int, seed: int = 42, start: int = 0):
+    """C3 payload fields of instances [start, start + n): amount U[0,2000), region index U{0,1,2}, score U[0,1)
+    (53-bit float64), from Philox4x32-10 with counter = instance index, key = seed."""
+    r = philox4x32(np.arange(start, start + n, dtype=np.uint64), seed).astype(np.uint64)
+    amount = (r[:, 0] % np.uint64(2000)).astype(np.int64)
+    region = (r[:, 1] % np.uint64(3)).astype(np.int64)
+    score = ((r[:, 2] >> np.uint64(11)) << np.uint64(32) | r[:, 3]).astype(np.float64)  # 21 + 32 bits
+    score = score / float(1 << 53)
+    return amount, region, score
+
+
 def xor_payloads(n: int, seed: int = 42, start: int = 0) -> Tuple[bytes, np.ndarray]:
-    """C3: {"amount": U[0,2000), "region": EU|US|APAC, "score": U[0,1) float64} (Philox, seed 42)."""
-    g = np.random.Generator(np.random.Philox(key=seed))
-    if start:
-        g.bit_generator.advance(start)
-    amount = g.integers(0, 2000, size=n)
-    region = g.integers(0, 3, size=n)
-    score = g.random(size=n)
+    """C3: {"amount": U[0,2000), "region": EU|US|APAC, "score": U[0,1) float64} (Philox4x32-10, seed 42, counter =
+    instance index), encoded with the reference writer's rules (float32 iff exactly representable)."""
+    amount, region, score = xor_fields(n, seed, start)
     ka, kr, ks = mp_str("amount"), mp_str("region"), mp_str("score")
     regs = [mp_str(r) for r in REGIONS]
     parts = []
@@ -80,12 +109,7 @@ def xor_payloads(n: int, seed: int = 42, start: int = 0) -> Tuple[bytes, np.ndar
 
 def xor_payloads_np(n: int, seed: int = 42, start: int = 0) -> Tuple[bytes, np.ndarray]:
     """xor_payloads, vectorized (same bytes): rows of at most 48 bytes assembled column-wise, then packed."""
-    g = np.random.Generator(np.random.Philox(key=seed))
-    if start:
-        g.bit_generator.advance(start)
-    amount = g.integers(0, 2000, size=n)
-    region = g.integers(0, 3, size=n)
-    score = g.random(size=n)
+    amount, region, score = xor_fields(n, seed, start)
     W = 48
     buf = np.zeros((n, W), dtype=np.uint8)
     ln = np.zeros(n, dtype=np.int64)
