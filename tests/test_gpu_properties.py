@@ -78,10 +78,7 @@ def test_c2_one_million_properties():
 
 
 def _c3_expected_end(n):
-    g = np.random.Generator(np.random.Philox(key=42))
-    amount = g.integers(0, 2000, size=n)
-    region = g.integers(0, 3, size=n)
-    score = g.random(size=n)
+    amount, region, score = workloads.xor_fields(n)  # the payload fields (Philox4x32-10, counter = instance)
     # json-el compares the msgpack values: score travels as float32 when exactly representable, else float64,
     # and either way compares as the double it denotes. g1's conditioned flows are tried in the order the
     # transformer collects them (ExclusiveSplitHandler.java:38-71 over ExecutableExclusiveGateway's outgoing
