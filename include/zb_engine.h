@@ -299,6 +299,28 @@ int zb_set_request_metadata(zb_engine* e, size_t n, const uint64_t* request_ids,
 /* Page-locked host memory for zb_drain_copy destinations (hipHostMalloc); NULL on failure. */
 void* zb_pinned_alloc(size_t bytes);
 void zb_pinned_free(void* p);
+/* ---- a partition that runs indefinitely ------------------------------------------------------ */
+/* The device log holds a window of log_capacity positions. The caller releases what it has appended to the
+ * logstream (records below position; only processed ones): at the next call that appends (zb_step,
+ * zb_submit_publishes, zb_inbox_submit) the window starts there, and released records can no longer be
+ * drained. Positions stay absolute (LogStream positions are the caller's). */
+int zb_log_release(zb_engine* e, int64_t position);
+/* Compaction of a quiescent partition (also run automatically between ticks when the element-instance rows,
+ * the payload arena or the job table are more than half full): element instances removed on COMPLETED /
+ * TERMINATED free their rows (ElementInstanceIndex.removeInstance, ElementInstanceIndex.java:54-64), payload
+ * blobs that no live row, unreleased record or stored message references are reclaimed, removed messages and
+ * job states are dropped. Order-preserving: logs and state read back identically. */
+int zb_compact(zb_engine* e);
+typedef struct zb_memory_stats {
+  int64_t log_window_begin, log_end;  /* positions [log_window_begin, log_end) are readable */
+  uint64_t log_capacity;
+  uint64_t rows_allocated, row_capacity;  /* rows in use (live + dead since the last compaction) */
+  uint64_t arena_used, arena_bytes;
+  uint64_t records_total, rows_total, arena_total;  /* lifetime totals written / allocated */
+  uint64_t compactions;
+} zb_memory_stats;
+int zb_read_memory_stats(zb_engine* e, zb_memory_stats* out);
+
 /* counters: [0] created [1] completed [2] canceled [3] next wf key [4] next job key
  *           [5] rows allocated [6] arena bytes used [7] log size */
 int zb_counters(zb_engine* e, int64_t out[8]);

@@ -1,0 +1,243 @@
+"""A partition that runs indefinitely: many ticks through device capacities far smaller than what
+the partition writes and allocates over its life, bit-exact vs the oracle at every tick.
+
+Every tick: new CREATE commands, job events for (some of) the pending jobs with per-job payloads, cancellations;
+the engine steps to quiescence, the tick's records are compared with the oracle's (positions, keys, values, log
+frames), the element-instance state is compared, and the caller releases the drained records
+(zb_log_release). The log window, the element-instance rows and the payload arena are sized so that the totals
+written over the run are >= 10x their capacities: the run only completes if the window moves, dead rows are
+reused (ElementInstanceIndex.removeInstance on COMPLETED / TERMINATED) and unreachable blobs are reclaimed. At
+the end the snapshot holds only live state, and a restored engine continues exactly like the original.
+"""
+import msgpack
+import pytest
+
+from frames_check import assert_frames_equal
+from oracle import zbref
+from zeebe_amd import records as R, workloads
+
+pytestmark = pytest.mark.gpu
+
+STATIC = 1 << 20  # the engine's static arena region (harness payloads, {}); never compacted
+
+
+def _compare_tick(o, e, start):
+    ref, got = o.records(start), e.records(start)
+    assert len(got) == len(ref), (len(got), len(ref))
+    for a, b in zip(ref, got):
+        assert (a.position, a.source_position, a.key, a.record_type, a.value_type, a.intent, a.rejection_type) == \
+               (b.position, b.source_position, b.key, b.record_type, b.value_type, b.intent, b.rejection_type), (a, b)
+        assert a.value == b.value, (a.position, msgpack.unpackb(a.value, raw=False), msgpack.unpackb(b.value, raw=False))
+    assert_frames_equal(o, e, start)
+    ri, gi = o.instances(), e.instances()
+    assert len(ri) == len(gi)
+    for a, b in zip(ri, gi):
+        assert a == b, (a[:4], b[:4])
+    oc, ec = o.counters(), e.counters()
+    assert (ec["created"], ec["completed"], ec["canceled"], ec["next_wf_key"], ec["next_job_key"]) == \
+           (oc["created"], oc["completed"], oc["canceled"], oc["next_wf_key"], oc["next_job_key"]), (oc, ec)
+    return len(ref)
+
+
+def _engine(**kw):
+    from zeebe_amd.engine import Engine
+
+    return Engine(**kw)
+
+
+class Driver:
+    """The oracle and the GPU engine fed the same ticks; external job stream processor emulated by the test
+    (job keys 2 + 5j in JOB CREATE order, as the job processor's KeyGenerator(2, 5) would give them)."""
+
+    def __init__(self, xmls, **cap):
+        self.o = zbref.Oracle()
+        self.o.set_harness(False)
+        self.e = _engine(external_jobs=True, **cap)
+        for k, xml in xmls.items():
+            self.o.deploy(xml, k, 1)
+            self.e.deploy(xml, k, 1)
+        self.scan_from = 0
+        self.pending = []  # (job key, JOB CREATE record) not completed yet
+        self.jobs_seen = 0
+        self.inst = 0
+
+    def collect_jobs(self):
+        for r in self.o.records(self.scan_from):
+            if r.value_type == R.VT_JOB and r.record_type == R.RT_COMMAND and r.intent == R.JI_CREATE:
+                self.pending.append((2 + 5 * self.jobs_seen, r))
+                self.jobs_seen += 1
+        self.scan_from = self.o.log_size()
+
+    def tick(self, creates, job_recs, cancels):
+        for process, payloads in creates:
+            for p in payloads:
+                self.o.create(process, p)
+            self.e.create(process, payloads)
+        recs = list(job_recs) + list(cancels)
+        if recs:
+            for r in recs:
+                self.o.submit(*r)
+            self.e.submit_records(recs)
+        start = self.e.log_size()
+        assert start == self.o.log_size()
+        self.o.run()
+        st = self.e.step()
+        assert st["quiescent"], st
+        n = _compare_tick(self.o, self.e, start)
+        self.e.release(self.e.log_size())  # appended to the logstream: the window may move on
+        self.collect_jobs()
+        return n
+
+
+def _job_events(items, tick):
+    recs = []
+    for key, rec in items:
+        pl = msgpack.packb({"tick": tick, "job": key, "note": "x" * (120 + key % 97)})
+        recs.append((R.RT_EVENT, R.VT_JOB, R.JI_CREATED, key, R.job_event(rec.value)))
+        recs.append((R.RT_EVENT, R.VT_JOB, R.JI_COMPLETED, key, R.job_event(rec.value, pl)))
+    return recs
+
+
+def _wik(rec):
+    return msgpack.unpackb(rec.value, raw=False)["headers"]["workflowInstanceKey"]
+
+
+def test_many_ticks_through_small_capacities():
+    c1, c4t = workloads.CONFIGS["c1"], workloads.CONFIGS["c4twin"]
+    log_cap, row_cap, arena = 4096, 1024, 2 * STATIC
+    d = Driver({100: c1["workflow"]().to_xml(), 200: c4t["workflow"]().to_xml()},
+               log_capacity=log_cap, row_capacity=row_cap, arena_bytes=arena)
+    ticks, total = 64, 0
+    live_instances = {}
+    canceled = set()
+    for t in range(ticks):
+        k = 20
+        base = d.inst
+        d.inst += k
+        pay = [msgpack.packb({"orderId": base + i, "blob": "p" * (20 + (base + i) % 60)}) for i in range(k)]
+        creates = [("process", pay[: k // 2]), ("subs", pay[k // 2:])]
+        # complete 3 of every 4 pending jobs (the rest wait a tick or more), skipping instances cancelled now
+        cancel_now = set()
+        if t % 3 == 2:  # cancel two running instances (their jobs are not completed in this tick: race rules)
+            for wik in sorted(live_instances)[:2]:
+                cancel_now.add(wik)
+        done, keep = [], []
+        for i, (key, rec) in enumerate(d.pending):
+            wik = _wik(rec)
+            if wik in canceled or wik in cancel_now:
+                continue  # the job's task was (or is being) terminated: never completed
+            (done if (i + t) % 4 else keep).append((key, rec))
+        d.pending = keep
+        cancels = [(R.RT_COMMAND, R.VT_WORKFLOW_INSTANCE, R.WI_CANCEL, wik, b"\x80") for wik in sorted(cancel_now)]
+        canceled |= cancel_now
+        total += d.tick(creates, _job_events(done, t), cancels)
+        live_instances = {key: 1 for key, parent, *_ in d.e.instances() if parent == -1}
+    m = d.e.memory_stats()
+    # the run wrote / allocated >= 10x what the device regions hold
+    assert m["records_total"] == total == d.o.log_size()
+    assert m["records_total"] >= 10 * log_cap, m
+    assert m["rows_total"] >= 10 * row_cap, m
+    assert m["arena_total"] >= 10 * (arena - STATIC), m
+    assert m["compactions"] > 0
+    assert d.e.counters()["completed"] > 0 and d.e.counters()["canceled"] > 0
+    # the snapshot holds live state only: live rows (96 B) + reachable blobs, not what was ever allocated
+    snap = d.e.snapshot()
+    live_rows = len(d.e.instances())
+    m2 = d.e.memory_stats()
+    assert m2["rows_allocated"] == live_rows
+    assert len(snap) <= 4096 + 96 * live_rows + (m2["arena_used"] - STATIC), (len(snap), live_rows, m2)
+    assert len(snap) * 10 < m["arena_total"] + 96 * m["rows_total"]
+    # restore into a fresh engine and continue: the same records as the original run
+    e2 = _engine(external_jobs=True, log_capacity=log_cap, row_capacity=row_cap, arena_bytes=arena)
+    e2.deploy(c1["workflow"]().to_xml(), 100, 1)
+    e2.deploy(c4t["workflow"]().to_xml(), 200, 1)
+    e2.restore(snap)
+    assert e2.log_size() == d.o.log_size()
+    d.e.close()
+    d.e = e2
+    for t in range(ticks, ticks + 10):
+        done, d.pending = d.pending, []
+        done = [(k, r) for k, r in done if _wik(r) not in canceled]
+        d.tick([("subs", [msgpack.packb({"orderId": 10 ** 6 + t})])], _job_events(done, t), [])
+    assert e2.instances() == d.o.instances()
+    e2.close()
+
+
+def test_trajectory_batches_reuse_arena():
+    """C2's chain (20 tasks, canonical harness, default output merges) as repeated CREATE batches on the trajectory
+    path, which writes each instance's merge results into per-batch arena slots; job payloads with a distinct key
+    per task make the merged payloads grow along the chain. After each tick every instance has completed (the
+    path allocates no rows for them), so compaction leaves only the static region, and 40 ticks run through a log
+    window and an arena far smaller than what they write."""
+    cfg = workloads.CONFIGS["c2"]
+    n = 60
+    recs_per_tick = 169 * n
+    log_cap, row_cap, arena = recs_per_tick + 1024, 1024, 2 * STATIC
+    o = zbref.Oracle()
+    e = _engine(log_capacity=log_cap, row_capacity=row_cap, arena_bytes=arena)
+    jp = {"t%d" % k: msgpack.packb({"t%d" % k: "v" * 24}) for k in range(1, 21)}
+    for x in (o, e):
+        x.deploy(cfg["workflow"]().to_xml(), 100, 1)
+        for act, p in jp.items():
+            x.set_job_payload(100, act, p)
+    ticks = 40
+    for t in range(ticks):
+        blob, offs = workloads.order_payloads(n, start=t * n)
+        ps = workloads.split(blob, offs)
+        for p in ps:
+            o.create(cfg["process"], p)
+        e.create(cfg["process"], ps)
+        start = e.log_size()
+        o.run()
+        st = e.step()
+        assert st["quiescent"] and st["path"] in (1, 2), st
+        if t % 8 == 0 or t == ticks - 1:
+            _compare_tick(o, e, start)
+        else:  # (the oracle's values are compared every 8 ticks; counters and instance state every tick)
+            assert e.log_size() == o.log_size()
+            assert e.counters()["completed"] == o.counters()["completed"] == (t + 1) * n
+            assert e.instances() == []
+        e.release(e.log_size())
+    m = e.memory_stats()
+    assert m["records_total"] >= 30 * log_cap
+    assert m["arena_total"] >= 10 * (arena - STATIC), m
+    assert m["compactions"] > 0
+    e.close()
+
+
+def test_job_processor_long_run():
+    """The job stream processor on the GPU over many ticks: worker commands ACTIVATE + COMPLETE for every new job,
+    job states removed on COMPLETE (tombstones), the job table rebuilt at compaction."""
+    cfg = workloads.CONFIGS["c1"]
+    o = zbref.Oracle()
+    o.set_job_processor(True)
+    e = _engine(job_processor=True, log_capacity=2048, row_capacity=512, arena_bytes=2 * STATIC)
+    for x in (o, e):
+        x.deploy(cfg["workflow"]().to_xml(), 100, 1)
+    seen = 0
+    for t in range(60):
+        payloads = [msgpack.packb({"orderId": t * 30 + i}) for i in range(30)]
+        for p in payloads:
+            o.create("process", p)
+        e.create("process", payloads)
+        created = [r for r in o.records() if r.value_type == R.VT_JOB and r.record_type == R.RT_EVENT
+                   and r.intent == R.JI_CREATED][seen:]
+        seen += len(created)
+        cmds = []
+        for r in created:
+            v = msgpack.unpackb(R.job_event(r.value), raw=False)
+            v.update(worker="w", deadline=10 ** 12)
+            cmds.append((R.RT_COMMAND, R.VT_JOB, R.JI_ACTIVATE, r.key, msgpack.packb(v)))
+            v2 = msgpack.unpackb(R.job_event(r.value, msgpack.packb({"done": t})), raw=False)
+            cmds.append((R.RT_COMMAND, R.VT_JOB, R.JI_COMPLETE, r.key, msgpack.packb(v2)))
+        for c in cmds:
+            o.submit(*c)
+        e.submit_records(cmds)
+        start = e.log_size()
+        o.run()
+        assert e.step()["quiescent"]
+        _compare_tick(o, e, start)
+        e.release(e.log_size())
+    m = e.memory_stats()
+    assert m["records_total"] >= 10 * 2048 and m["rows_total"] >= 2 * 512 and m["compactions"] > 0, m
+    e.close()

@@ -85,11 +85,19 @@ struct zb_engine {
   int ser_mode = 0;              // ZB_SER_MODE: 0 = two passes (size, scan, write), 1 = single pass (look-back)
   int ser_nt = 1;                // ZB_SER_NT=0: plain (not non-temporal) stores in the drain write pass
 
-  // device state
+  // device state. The log arrays hold the window [win_base, win_base + log_capacity) of absolute positions;
+  // log / links / srcd / vlen are biased pointers (index = absolute position) into the *_mem allocations, so
+  // every kernel indexes by position and the window moves by re-biasing (rebase_log)
   zb_rec* log = nullptr;
   uint64_t* links = nullptr;
   uint32_t* srcd = nullptr;     // per record: position - source position (0: none), for log frames
   uint32_t* vlen = nullptr;     // per record: serialized value length if the emitting kernel knew it
+  zb_rec* log_mem = nullptr;
+  uint64_t* links_mem = nullptr;
+  uint32_t* srcd_mem = nullptr;
+  uint32_t* vlen_mem = nullptr;
+  int64_t win_base = 0;         // first position the device log holds (earlier ones were released / not restored)
+  int64_t released = 0;         // zb_log_release: the caller appended everything below
   DevVec<ValueConst> d_vconst;  // per element: constant parts of its WORKFLOW_INSTANCE / JOB values
   DevVec<DevValSeg> d_vsegs;    // per element: its values' constant runs (fast drain passes)
   DevVec<uint8_t> d_segpool;
@@ -223,7 +231,6 @@ struct zb_engine {
   int64_t epoch = 1;
   bool has_parallel = false;
   bool term = false;               // a CANCEL was injected: terminations may run until quiescence
-  int64_t log_floor = 0;           // records below were not restored (zb_restore): not readable
   // zb_submit: per staged record, the key whose element-instance row it needs (INT64_MIN: none)
   std::vector<int64_t> staged_lookup;
   bool staged_only_creates = true;
@@ -232,7 +239,25 @@ struct zb_engine {
   std::unordered_map<int64_t, uint8_t> tick_inst;  // workflow instance -> 1: scope command, 2: other records
   std::unordered_set<int64_t> tick_aik;
   std::unordered_set<int64_t> tick_jobs;   // job keys with commands in the staged tick (one group each)
-  uint8_t* jstate = nullptr;               // ZB_CFG_JOB_PROCESSOR: JobStateG per job key ordinal [row_capacity]
+  JobTable jobs{};                         // ZB_CFG_JOB_PROCESSOR: job states by job key (open addressing)
+  // compaction (zb_compact.hip): scratch grown on demand, lifetime totals
+  uint32_t *c_flag = nullptr, *c_new = nullptr;  // scan input / output (live rows, live messages)
+  uint64_t c_flag_cap = 0, c_new_cap = 0;
+  void* c_tmp = nullptr;
+  size_t c_tmp_cap = 0;
+  uint8_t* c_scratch = nullptr;                  // live rows / live arena granules / live messages
+  uint64_t c_scratch_cap = 0;
+  uint64_t* c_bits = nullptr;                    // arena granule bitmap
+  uint64_t c_bits_cap = 0;
+  uint32_t *c_pop = nullptr, *c_off = nullptr;   // per-word popcounts and their scan
+  uint64_t c_pop_cap = 0, c_off_cap = 0;
+  uint32_t* c_count = nullptr;                   // device counter (job rebuild)
+  uint64_t rows_total = 0, arena_total = 0, records_total = 0, compactions = 0;  // lifetime allocation totals
+  // inbox CORRELATE resolution by activity instance key (zb_inbox_submit)
+  int64_t *x_keys = nullptr, *x_pos = nullptr, *x_keys2 = nullptr, *x_pos2 = nullptr;
+  uint64_t x_cap = 0;
+  void* x_tmp = nullptr;
+  size_t x_tmp_cap = 0;
   DevVec<int64_t> d_lookup_keys, d_lookup_pos;
   // drain buffers (zb_serialize), grown on demand and reused
   uint64_t dr_cap = 0, dr_val_cap = 0, dr_tmp_cap = 0;
@@ -366,7 +391,7 @@ WaveParams wave_params(zb_engine* e) {
   p.sub_count = e->job_counts + 4;
   p.job_cap = e->job_cap;
   p.stats = e->dstats;
-  p.log_cap = e->cfg.log_capacity;
+  p.log_cap = (uint64_t)e->win_base + e->cfg.log_capacity;  // absolute: the window's end
   p.row_cap = e->cfg.row_capacity;
   p.arena_cap = e->cfg.arena_bytes;
   p.wave = e->wave;
@@ -380,8 +405,7 @@ WaveParams wave_params(zb_engine* e) {
   p.has_parallel = e->has_parallel ? 1 : 0;
   p.harness = (e->cfg.flags & (ZB_CFG_EXTERNAL_JOBS | ZB_CFG_JOB_PROCESSOR)) ? 0 : 1;
   p.jobproc = (e->cfg.flags & ZB_CFG_JOB_PROCESSOR) ? 1 : 0;
-  p.jstate = e->jstate;
-  p.jstate_cap = e->jstate ? e->cfg.row_capacity : 0;
+  p.jobs = e->jobs;
   p.term = e->term ? 1 : 0;
   p.epoch = e->epoch;
   p.need_children = e->need_children;
@@ -559,7 +583,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   p.hdr = e->hdr + (e->wave & 1);
   p.err = e->derr;
   p.stats = e->dstats;
-  p.log_cap = e->cfg.log_capacity;
+  p.log_cap = (uint64_t)e->win_base + e->cfg.log_capacity;  // absolute: the window's end
   p.row_cap = e->cfg.row_capacity;
   p.arena_cap = e->cfg.arena_bytes;
   hipEvent_t* ev = e->ev.data();
@@ -679,6 +703,227 @@ int finish_batch(zb_engine* e) {
   return check_device_errors(e, *e->h_err_pinned);
 }
 
+// ---- the long-running partition: log window, compaction of rows / arena / stores / job states
+
+// biased views of the log arrays: element [pos] of the view is array index pos - win_base
+template <class T>
+T* biased(T* mem, int64_t base) {
+  return (T*)((uintptr_t)mem - (uintptr_t)base * sizeof(T));
+}
+void rebias(zb_engine* e) {
+  e->log = biased(e->log_mem, e->win_base);
+  e->links = biased(e->links_mem, e->win_base);
+  e->srcd = biased(e->srcd_mem, e->win_base);
+  e->vlen = biased(e->vlen_mem, e->win_base);
+}
+
+// Records the caller released move out of the window: [released, end) go to the front of the arrays (the
+// partition is quiescent: nothing below end is unprocessed). Chunks of at most (released - win_base) records,
+// front to back, never overlap a source not yet copied.
+int rebase_log(zb_engine* e) {
+  const int64_t from = std::min(e->released, e->host_hdr.end);
+  if (from <= e->win_base) return ZB_OK;
+  const int64_t keep = e->host_hdr.end - from, shift = from - e->win_base;
+  for (int64_t o = 0; o < keep; o += shift) {
+    const int64_t n = std::min(shift, keep - o);
+    HIPCHECK(e, hipMemcpyAsync(e->log_mem + o, e->log_mem + shift + o, n * sizeof(zb_rec), hipMemcpyDeviceToDevice, e->stream));
+    HIPCHECK(e, hipMemcpyAsync(e->links_mem + o, e->links_mem + shift + o, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, e->stream));
+    HIPCHECK(e, hipMemcpyAsync(e->srcd_mem + o, e->srcd_mem + shift + o, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream));
+    HIPCHECK(e, hipMemcpyAsync(e->vlen_mem + o, e->vlen_mem + shift + o, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream));
+  }
+  e->win_base = from;
+  rebias(e);
+  // submitted-command ranges and request metadata of released records are no longer needed by the drain
+  e->ranges.erase(std::remove_if(e->ranges.begin(), e->ranges.end(),
+                                 [&](const CmdRange& r) { return r.pos_end <= e->win_base; }), e->ranges.end());
+  e->reqs.erase(std::remove_if(e->reqs.begin(), e->reqs.end(), [&](const ReqMeta& r) { return r.pos < e->win_base; }),
+                e->reqs.end());
+  // the process-id strings they name: only those of the remaining (and the staged) ranges are kept
+  std::vector<uint8_t> pool;
+  auto keep_str = [&](uint32_t& off, uint16_t len) {
+    const uint32_t at = (uint32_t)pool.size();
+    pool.insert(pool.end(), e->cmd_pool.begin() + off, e->cmd_pool.begin() + off + len);
+    off = at;
+  };
+  for (auto& r : e->ranges) keep_str(r.pid_off, r.pid_len);
+  for (auto& r : e->pending_ranges) keep_str(r.pid_off, r.pid_len);
+  e->cmd_pool.swap(pool);
+  return ZB_OK;
+}
+
+template <class T>
+int grow(zb_engine* e, T** p, uint64_t* cap, uint64_t n) {
+  if (n <= *cap && *p) return ZB_OK;
+  HIPCHECK(e, hipStreamSynchronize(e->stream));  // (queued work may still use the old buffer)
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  const uint64_t c = std::max<uint64_t>(n + n / 4, 1024);
+  HIPCHECK(e, hipMalloc(p, c * sizeof(T)));
+  *cap = c;
+  return ZB_OK;
+}
+
+// exclusive scan of in[0, n] into out; returns the total (out[n], in[n] being 0)
+int scan_u32(zb_engine* e, const uint32_t* in, uint32_t* out, uint64_t n, uint64_t* total) {
+  if (n + 1 > (uint64_t)INT32_MAX) return fail(e, ZB_EUNSUPPORTED, "compaction over more than 2^31 entries");
+  size_t tmp = 0;
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (int)(n + 1), e->stream) != hipSuccess)
+    return fail(e, ZB_EDEVICE, "compaction scan sizing");
+  if (tmp > e->c_tmp_cap) {
+    if (e->c_tmp) (void)hipFree(e->c_tmp);
+    e->c_tmp = nullptr;
+    e->c_tmp_cap = 0;
+    HIPCHECK(e, hipMalloc(&e->c_tmp, tmp + 16));
+    e->c_tmp_cap = tmp;
+  }
+  tmp = e->c_tmp_cap;
+  if (hipcub::DeviceScan::ExclusiveSum(e->c_tmp, tmp, in, out, (int)(n + 1), e->stream) != hipSuccess)
+    return fail(e, ZB_EDEVICE, "compaction scan");
+  uint32_t t = 0;
+  HIPCHECK(e, hipMemcpyAsync(&t, out + n, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  *total = t;
+  return ZB_OK;
+}
+
+CompactParams compact_params(zb_engine* e) {
+  CompactParams c{};
+  c.rmeta = e->rmeta; c.rkeys = e->rkeys; c.raux = e->raux;
+  c.rows = (uint64_t)e->host_hdr.rows_next;
+  c.live_rows = c.rows;
+  c.row_flag = e->c_flag; c.row_new = e->c_new;
+  c.arena = e->arena;
+  c.static_refs = STATIC_ARENA_BYTES / 8;
+  c.arena_next = (uint64_t)e->host_hdr.arena_next;
+  c.log = e->log;
+  c.win_begin = e->win_base;
+  c.win_end = e->host_hdr.end;
+  c.msgs = e->msgs; c.msg_count = e->msgs ? e->msg_count : 0;
+  c.subs = e->subs; c.sub_count = e->subs ? e->sub_count : 0;
+  return c;
+}
+
+// Compaction of a quiescent partition: dead element-instance rows, removed messages, unreachable arena
+// blobs and job-table tombstones are dropped; everything live keeps its order (zb_compact.hip).
+int compact_state(zb_engine* e) {
+  const uint64_t rows = (uint64_t)e->host_hdr.rows_next;
+  const uint64_t nflag = std::max<uint64_t>(rows, e->msgs ? e->msg_count : 0) + 1;
+  int rc = grow(e, &e->c_flag, &e->c_flag_cap, nflag);
+  if (rc == ZB_OK) rc = grow(e, &e->c_new, &e->c_new_cap, nflag);
+  if (rc != ZB_OK) return rc;
+  // 1. rows: live ones to the front (index order kept), parents renamed
+  CompactParams c = compact_params(e);
+  uint64_t live = 0;
+  if (rows) {
+    launch_row_flags(c, e->stream);
+    rc = scan_u32(e, e->c_flag, e->c_new, rows, &live);
+    if (rc != ZB_OK) return rc;
+    const uint64_t row_bytes = sizeof(RowMeta) + sizeof(RowKeys) + sizeof(RowAux);
+    rc = grow(e, &e->c_scratch, &e->c_scratch_cap, std::max<uint64_t>(live, 1) * row_bytes);
+    if (rc != ZB_OK) return rc;
+    c.row_new = e->c_new;
+    c.m2 = (RowMeta*)e->c_scratch;
+    c.k2 = (RowKeys*)(e->c_scratch + live * sizeof(RowMeta));
+    c.a2 = (RowAux*)(e->c_scratch + live * (sizeof(RowMeta) + sizeof(RowKeys)));
+    launch_row_gather(c, e->stream);
+    if (live) {
+      HIPCHECK(e, hipMemcpyAsync(e->rmeta, c.m2, live * sizeof(RowMeta), hipMemcpyDeviceToDevice, e->stream));
+      HIPCHECK(e, hipMemcpyAsync(e->rkeys, c.k2, live * sizeof(RowKeys), hipMemcpyDeviceToDevice, e->stream));
+      HIPCHECK(e, hipMemcpyAsync(e->raux, c.a2, live * sizeof(RowAux), hipMemcpyDeviceToDevice, e->stream));
+    }
+  }
+  e->host_hdr.rows_next = (int64_t)live;
+  // 2. message store: removed messages dropped, chains rebuilt (subscriptions are never removed)
+  if (e->msgs && e->msg_count) {
+    c = compact_params(e);
+    launch_msg_flags(c, e->stream);
+    uint64_t live_msgs = 0;
+    rc = scan_u32(e, e->c_flag, e->c_new, e->msg_count, &live_msgs);
+    if (rc != ZB_OK) return rc;
+    if (live_msgs != e->msg_count) {
+      rc = grow(e, &e->c_scratch, &e->c_scratch_cap, std::max<uint64_t>(live_msgs, 1) * sizeof(MsgEntry));
+      if (rc != ZB_OK) return rc;
+      launch_msg_gather(c, (MsgEntry*)e->c_scratch, e->stream);
+      if (live_msgs)
+        HIPCHECK(e, hipMemcpyAsync(e->msgs, e->c_scratch, live_msgs * sizeof(MsgEntry), hipMemcpyDeviceToDevice, e->stream));
+      e->msg_count = live_msgs;
+      launch_chains(e->msgs, e->msg_count, e->msg_head, e->msg_next, e->subs, e->sub_count, e->sub_head, e->sub_next,
+                    e->head_mask, e->stream);
+    }
+  }
+  // 3. arena: blobs reachable from live rows, the unreleased log window and the stores
+  c = compact_params(e);
+  c.live_rows = live;
+  const uint64_t dyn = (uint64_t)e->host_hdr.arena_next - STATIC_ARENA_BYTES;
+  const uint64_t words = (dyn / 8 + 63) / 64;
+  if (words) {
+    rc = grow(e, &e->c_bits, &e->c_bits_cap, words);
+    if (rc == ZB_OK) rc = grow(e, &e->c_pop, &e->c_pop_cap, words + 1);
+    if (rc == ZB_OK) rc = grow(e, &e->c_off, &e->c_off_cap, words + 1);
+    if (rc != ZB_OK) return rc;
+    HIPCHECK(e, hipMemsetAsync(e->c_bits, 0, words * sizeof(uint64_t), e->stream));
+    c.bits = e->c_bits; c.word_pop = e->c_pop; c.word_off = e->c_off; c.words = words;
+    launch_mark(c, e->stream);
+    launch_word_pop(c, e->stream);
+    uint64_t granules = 0;
+    rc = scan_u32(e, e->c_pop, e->c_off, words, &granules);
+    if (rc != ZB_OK) return rc;
+    rc = grow(e, &e->c_scratch, &e->c_scratch_cap, std::max<uint64_t>(granules, 1) * 8);
+    if (rc != ZB_OK) return rc;
+    c.scratch = e->c_scratch;
+    launch_arena_gather(c, e->stream);
+    launch_rename(c, e->stream);
+    if (granules)
+      HIPCHECK(e, hipMemcpyAsync(e->arena + STATIC_ARENA_BYTES, e->c_scratch, granules * 8, hipMemcpyDeviceToDevice, e->stream));
+    e->host_hdr.arena_next = (int64_t)(STATIC_ARENA_BYTES + granules * 8);
+  }
+  // 4. job table: tombstones dropped (live entries collected, table cleared, refilled)
+  if (e->jobs.keys) {
+    uint32_t tombs = 0;
+    HIPCHECK(e, hipMemcpyAsync(&tombs, e->jobs.tombs, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHECK(e, hipStreamSynchronize(e->stream));
+    if (tombs) {
+      const uint64_t slots = e->jobs.mask + 1;
+      rc = grow(e, &e->c_scratch, &e->c_scratch_cap, slots * (sizeof(int64_t) + 1));
+      if (rc != ZB_OK) return rc;
+      if (!e->c_count) HIPCHECK(e, hipMalloc(&e->c_count, sizeof(uint32_t)));
+      HIPCHECK(e, hipMemsetAsync(e->c_count, 0, sizeof(uint32_t), e->stream));
+      int64_t* keys = (int64_t*)e->c_scratch;
+      uint8_t* st = e->c_scratch + slots * sizeof(int64_t);
+      launch_job_collect(e->jobs, keys, st, e->c_count, e->stream);
+      uint32_t n = 0;
+      HIPCHECK(e, hipMemcpyAsync(&n, e->c_count, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+      HIPCHECK(e, hipStreamSynchronize(e->stream));
+      launch_job_clear(e->jobs, e->stream);
+      launch_job_fill(e->jobs, keys, st, n, e->derr, e->stream);
+      HIPCHECK(e, hipMemsetAsync(e->jobs.tombs, 0, sizeof(uint32_t), e->stream));
+    }
+  }
+  e->compactions++;
+  return finish_batch(e);  // the device wave header takes the new allocators
+}
+
+// Between ticks: the released part of the log leaves the window, and the state is compacted when any region
+// is more than half full (or always, force) -- so a partition whose live state fits half its capacities runs
+// indefinitely.
+int maintain(zb_engine* e, bool force) {
+  if (e->failed || e->host_hdr.begin != e->host_hdr.end) return ZB_OK;  // only at quiescence
+  int rc = rebase_log(e);
+  if (rc != ZB_OK) return rc;
+  const bool rows_half = (uint64_t)e->host_hdr.rows_next > e->cfg.row_capacity / 2;
+  const bool arena_half = (uint64_t)e->host_hdr.arena_next - STATIC_ARENA_BYTES > (e->cfg.arena_bytes - STATIC_ARENA_BYTES) / 2;
+  bool jobs_half = false;
+  if (e->jobs.keys && !force && !rows_half && !arena_half) {
+    uint32_t tombs = 0;
+    HIPCHECK(e, hipMemcpyAsync(&tombs, e->jobs.tombs, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHECK(e, hipStreamSynchronize(e->stream));
+    jobs_half = tombs > (e->jobs.mask + 1) / 4;
+  }
+  if (force || rows_half || arena_half || jobs_half) return compact_state(e);
+  return ZB_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -726,16 +971,22 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   const uint64_t L = e->cfg.log_capacity;
   e->wave_cap = e->cfg.wave_records ? e->cfg.wave_records : std::min<uint64_t>(L, 1ull << 22);
   e->wave_cap = (e->wave_cap + WAVE_TILE - 1) / WAVE_TILE * WAVE_TILE;
-  if (hipMalloc(&e->log, L * sizeof(zb_rec)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipMalloc(&e->links, L * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipMalloc(&e->srcd, L * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipMalloc(&e->vlen, L * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->log_mem, L * sizeof(zb_rec)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->links_mem, L * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->srcd_mem, L * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->vlen_mem, L * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  rebias(e);
   if (const char* c = std::getenv("ZB_VLEN_CHECK"))
     if (atoi(c) && hipMalloc(&e->vlen_bad, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  // job states: a job belongs to one service-task instance and rows are never reused, so job ordinals stay
-  // below the row capacity
-  if ((e->cfg.flags & ZB_CFG_JOB_PROCESSOR) && hipMalloc(&e->jstate, e->cfg.row_capacity) != hipSuccess)
-    return cleanup(ZB_ENOMEM);
+  // job states: open addressing at load <= 1/2 for row_capacity live jobs
+  if (e->cfg.flags & ZB_CFG_JOB_PROCESSOR) {
+    uint64_t slots = 1024;
+    while (slots < 2 * e->cfg.row_capacity) slots <<= 1;
+    e->jobs.mask = slots - 1;
+    if (hipMalloc(&e->jobs.keys, slots * sizeof(int64_t)) != hipSuccess ||
+        hipMalloc(&e->jobs.state, slots) != hipSuccess || hipMalloc(&e->jobs.tombs, sizeof(uint32_t)) != hipSuccess)
+      return cleanup(ZB_ENOMEM);
+  }
   if (hipMalloc(&e->rmeta, e->cfg.row_capacity * sizeof(RowMeta)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->rkeys, e->cfg.row_capacity * sizeof(RowKeys)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->arena, e->cfg.arena_bytes) != hipSuccess) return cleanup(ZB_ENOMEM);
@@ -788,7 +1039,9 @@ void zb_engine_destroy(zb_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (auto& x : e->ev)
     if (x) (void)hipEventDestroy(x);
-  void* ps[] = {e->vlen, e->vlen_bad, e->jstate, e->mapres, e->map_ws, e->log, e->links, e->srcd, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
+  void* ps[] = {e->vlen_mem, e->vlen_bad, e->jobs.keys, e->jobs.state, e->jobs.tombs, e->c_flag, e->c_new, e->c_tmp,
+                e->c_scratch, e->c_bits, e->c_pop, e->c_off, e->c_count, e->x_keys, e->x_pos, e->x_keys2, e->x_pos2,
+                e->x_tmp, e->mapres, e->map_ws, e->log_mem, e->links_mem, e->srcd_mem, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
                 e->merge_jobs, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
@@ -845,7 +1098,14 @@ int zb_reset(zb_engine* e, int keep_staged) {
   HIPCHECK(e, hipMemsetAsync(e->derr_info, 0xff, sizeof(uint64_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->job_counts, 0, 6 * sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->dstats, 0, 8 * sizeof(uint64_t), e->stream));
-  if (e->jstate) HIPCHECK(e, hipMemsetAsync(e->jstate, 0, e->cfg.row_capacity, e->stream));
+  if (e->jobs.keys) {
+    HIPCHECK(e, hipMemsetAsync(e->jobs.keys, 0, (e->jobs.mask + 1) * sizeof(int64_t), e->stream));  // JOB_EMPTY
+    HIPCHECK(e, hipMemsetAsync(e->jobs.state, 0, e->jobs.mask + 1, e->stream));
+    HIPCHECK(e, hipMemsetAsync(e->jobs.tombs, 0, sizeof(uint32_t), e->stream));
+  }
+  e->win_base = e->released = 0;
+  rebias(e);
+  e->rows_total = e->arena_total = e->records_total = e->compactions = 0;
   HIPCHECK(e, hipStreamSynchronize(e->stream));
   e->ranges.clear();
   e->cmd_pool.clear();
@@ -865,7 +1125,6 @@ int zb_reset(zb_engine* e, int keep_staged) {
     e->staged_uploaded = false;
   }
   e->term = false;
-  e->log_floor = 0;
   e->staged_pending = !e->staged.empty();
   e->sub_count = e->msg_count = 0;
   e->msg_key_next = 0;
@@ -1495,6 +1754,11 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   auto t0 = std::chrono::steady_clock::now();
   zb_step_stats st{};
   bool try_traj = false;
+  {
+    int mrc = maintain(e, false);  // released records leave the window; compaction when a region is half full
+    if (mrc != ZB_OK) return mrc;
+  }
+  const int64_t rows_before = e->host_hdr.rows_next, arena_before = e->host_hdr.arena_next;
   int64_t traj_base = 0, traj_n = 0;
   // ---- inject staged input at the log tail (engine is quiescent between steps)
   if (e->staged_pending && !e->staged.empty()) {
@@ -1510,7 +1774,8 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     traj_base = e->host_hdr.end;
     traj_n = (int64_t)e->staged.size();
     const int64_t n = (int64_t)e->staged.size();
-    if ((uint64_t)(e->host_hdr.end + n) > e->cfg.log_capacity) return fail(e, ZB_ENOMEM, "log capacity");
+    if ((uint64_t)(e->host_hdr.end + n - e->win_base) > e->cfg.log_capacity)
+      return fail(e, ZB_ENOMEM, "log capacity (release drained records with zb_log_release)");
     if ((uint64_t)e->host_hdr.arena_next + e->staged_arena.size() > e->cfg.arena_bytes)
       return fail(e, ZB_ENOMEM, "arena capacity");
     if (!e->staged_uploaded) {
@@ -1659,6 +1924,9 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   st.merge_bytes = stats_after[4] - stats_before[4];
   st.condition_payload_bytes = stats_after[5] - stats_before[5];
   st.waves = stats_after[6] - stats_before[6];
+  e->rows_total += (uint64_t)std::max<int64_t>(0, e->host_hdr.rows_next - rows_before);
+  e->arena_total += (uint64_t)std::max<int64_t>(0, e->host_hdr.arena_next - arena_before);
+  e->records_total += (uint64_t)(e->host_hdr.end - written_from);
   st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (stats) *stats = st;
   if (!quiescent) return ZB_EAGAIN;
@@ -1669,7 +1937,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
 int64_t zb_log_size(zb_engine* e) { return e ? e->host_hdr.end : -1; }
 
 int zb_read_source_positions(zb_engine* e, int64_t start, int64_t count, int64_t* out) {
-  if (!e || start < e->log_floor || count < 0 || start + count > e->host_hdr.end || (!out && count)) return ZB_EINVAL;
+  if (!e || start < e->win_base || count < 0 || start + count > e->host_hdr.end || (!out && count)) return ZB_EINVAL;
   if (count == 0) return ZB_OK;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
   std::vector<uint32_t> d((size_t)count);
@@ -1680,7 +1948,7 @@ int zb_read_source_positions(zb_engine* e, int64_t start, int64_t count, int64_t
 }
 
 int zb_read_descriptors(zb_engine* e, int64_t start, int64_t count, zb_rec* out) {
-  if (!e || start < e->log_floor || count < 0 || start + count > e->host_hdr.end || (!out && count)) return ZB_EINVAL;
+  if (!e || start < e->win_base || count < 0 || start + count > e->host_hdr.end || (!out && count)) return ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
   HIPCHECK(e, hipMemcpyAsync(out, e->log + start, count * sizeof(zb_rec), hipMemcpyDeviceToHost, e->stream));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
@@ -1717,7 +1985,7 @@ int zb_set_request_metadata(zb_engine* e, size_t n, const uint64_t* request_ids,
 }
 
 static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_config* fc, zb_serialize_stats* stats) {
-  if (!e || start < e->log_floor || count < 0 || start + count > e->host_hdr.end) return ZB_EINVAL;
+  if (!e || start < e->win_base || count < 0 || start + count > e->host_hdr.end) return ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
   auto t0 = std::chrono::steady_clock::now();
   zb_serialize_stats st{};
@@ -1775,7 +2043,7 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
     sp.stream_id = fc->stream_id;
     sp.raft_term = fc->raft_term;
     sp.timestamp = fc->timestamp;
-    sp.log_begin = e->log_floor;
+    sp.log_begin = e->win_base;
     sp.log_end = e->host_hdr.end;
     sp.reqs = e->reqs.empty() ? nullptr : e->d_reqs.p;
     sp.nreqs = (int64_t)e->reqs.size();
@@ -1982,12 +2250,13 @@ int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, c
   if (rc != ZB_OK) return rc;
   if (n == 0) return ZB_OK;
   rc = ensure_stores(e);
+  if (rc == ZB_OK) rc = maintain(e, false);
   if (rc != ZB_OK) return rc;
   const uint64_t nn = std::strlen(name);
   if (nn > 0xffff) return fail(e, ZB_EINVAL, "message name too long");
   const int per = ttl > 0 ? 1 : 2;
   const int64_t base = e->host_hdr.end;
-  if ((uint64_t)(base + (int64_t)n * (1 + per)) > e->cfg.log_capacity) return fail(e, ZB_ENOMEM, "log capacity");
+  if ((uint64_t)(base + (int64_t)n * (1 + per) - e->win_base) > e->cfg.log_capacity) return fail(e, ZB_ENOMEM, "log capacity");
   if ((uint64_t)base + n * (1 + per) >= (1ull << 34)) return fail(e, ZB_EUNSUPPORTED, "log position beyond the outbox order key");
   if (e->msg_count + (ttl > 0 ? n : 0) > e->store_cap) return fail(e, ZB_ENOMEM, "message store capacity");
   // PUBLISH commands (null key) and their message blobs, built on the host straight into pinned staging
@@ -2075,6 +2344,8 @@ int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, c
   e->host_hdr.end = base + (int64_t)n * (1 + per);
   e->host_hdr.begin = e->host_hdr.gen_end = e->host_hdr.end;
   e->host_hdr.arena_next += (int64_t)blob_bytes;
+  e->records_total += n * (1 + per);
+  e->arena_total += blob_bytes;
   return finish_batch(e);
 }
 
@@ -2085,11 +2356,12 @@ int zb_inbox_submit(zb_engine* e, int kind, const zb_exchange_rec* src, size_t n
   if (rc != ZB_OK) return rc;
   if (n == 0) return ZB_OK;
   rc = ensure_stores(e);
+  if (rc == ZB_OK) rc = maintain(e, false);
   if (rc != ZB_OK) return rc;
   const int64_t base = e->host_hdr.end;
   const uint64_t recs = kind == ZB_XCHG_OPEN ? 2 * n : n;
   const uint64_t stride = kind == ZB_XCHG_OPEN ? SUB_BLOB : WIS_BLOB;
-  if ((uint64_t)base + recs > e->cfg.log_capacity) return fail(e, ZB_ENOMEM, "log capacity");
+  if ((uint64_t)(base - e->win_base) + recs > e->cfg.log_capacity) return fail(e, ZB_ENOMEM, "log capacity");
   if ((uint64_t)base + recs >= (1ull << 34)) return fail(e, ZB_EUNSUPPORTED, "log position beyond the outbox order key");
   if ((uint64_t)e->host_hdr.arena_next + n * stride > e->cfg.arena_bytes) return fail(e, ZB_ENOMEM, "arena capacity");
   if (kind == ZB_XCHG_OPEN && (e->sub_count + n > e->store_cap || e->sub_count + n >= (1ull << 24)))
@@ -2112,11 +2384,54 @@ int zb_inbox_submit(zb_engine* e, int kind, const zb_exchange_rec* src, size_t n
     e->host_hdr.end = base + (int64_t)recs;
     e->host_hdr.begin = e->host_hdr.gen_end = e->host_hdr.end;
   } else {
-    launch_wis_inject(p, e->stream);  // CORRELATE commands: the next zb_step processes them
+    // CORRELATE commands: the next zb_step processes them; the element instance each names is looked up by its
+    // activity instance key (ElementInstanceIndex.getInstance): keys sorted, then one pass over the rows
+    const uint64_t need = n;
+    if (need > e->x_cap) {
+      HIPCHECK(e, hipStreamSynchronize(e->stream));
+      void* xs[] = {e->x_keys, e->x_pos, e->x_keys2, e->x_pos2};
+      for (void* q : xs)
+        if (q) (void)hipFree(q);
+      e->x_keys = e->x_pos = e->x_keys2 = e->x_pos2 = nullptr;
+      e->x_cap = 0;
+      const uint64_t c = std::max<uint64_t>(need + need / 2, 1024);
+      HIPCHECK(e, hipMalloc(&e->x_keys, c * 8));
+      HIPCHECK(e, hipMalloc(&e->x_pos, c * 8));
+      HIPCHECK(e, hipMalloc(&e->x_keys2, c * 8));
+      HIPCHECK(e, hipMalloc(&e->x_pos2, c * 8));
+      e->x_cap = c;
+    }
+    if (n > (uint64_t)INT32_MAX) return fail(e, ZB_EUNSUPPORTED, "more than 2^31 delivered commands");
+    p.lookup_keys = e->x_keys;
+    p.lookup_pos = e->x_pos;
+    launch_wis_inject(p, e->stream);
+    size_t tmp = 0;
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, e->x_keys, e->x_keys2, e->x_pos, e->x_pos2, (int)n, 0, 64,
+                                           e->stream) != hipSuccess)
+      return fail(e, ZB_EDEVICE, "inbox sort sizing");
+    if (tmp > e->x_tmp_cap) {
+      HIPCHECK(e, hipStreamSynchronize(e->stream));
+      if (e->x_tmp) (void)hipFree(e->x_tmp);
+      e->x_tmp = nullptr;
+      e->x_tmp_cap = 0;
+      HIPCHECK(e, hipMalloc(&e->x_tmp, tmp + 16));
+      e->x_tmp_cap = tmp;
+    }
+    tmp = e->x_tmp_cap;
+    if (hipcub::DeviceRadixSort::SortPairs(e->x_tmp, tmp, e->x_keys, e->x_keys2, e->x_pos, e->x_pos2, (int)n, 0, 64,
+                                           e->stream) != hipSuccess)
+      return fail(e, ZB_EDEVICE, "inbox sort");
+    ResolveParams rp{};
+    rp.rmeta = e->rmeta; rp.rkeys = e->rkeys; rp.rows = (uint64_t)e->host_hdr.rows_next;
+    rp.keys = e->x_keys2; rp.pos = e->x_pos2; rp.n = (int64_t)n;
+    rp.links = e->links;
+    launch_resolve(rp, e->stream);
     e->host_hdr.end = base + (int64_t)recs;
     e->host_hdr.gen_end = e->host_hdr.end;
   }
   e->host_hdr.arena_next += (int64_t)(n * stride);
+  e->records_total += recs;
+  e->arena_total += n * stride;
   rc = finish_batch(e);
   if (tmp) (void)hipFree(tmp);
   return rc;
@@ -2338,6 +2653,40 @@ int zb_comm_exchange(zb_engine* e, int kind, uint64_t* received) {
   return rc;
 }
 
+int zb_log_release(zb_engine* e, int64_t position) {
+  if (!e) return ZB_EINVAL;
+  // only processed records can leave the window (the engine still reads the unprocessed ones)
+  if (position > e->host_hdr.begin) return fail(e, ZB_EINVAL, "cannot release unprocessed records");
+  e->released = std::max(e->released, position);
+  return ZB_OK;
+}
+
+int zb_compact(zb_engine* e) {
+  if (!e) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  if (e->failed) return fail(e, ZB_EPROCESSING, "partition stopped after a processing failure: " + e->err);
+  if (e->host_hdr.begin != e->host_hdr.end) return fail(e, ZB_EINVAL, "partition not quiescent");
+  return maintain(e, true);
+}
+
+int zb_read_memory_stats(zb_engine* e, zb_memory_stats* out) {
+  if (!e || !out) return ZB_EINVAL;
+  zb_memory_stats m{};
+  m.log_window_begin = e->win_base;
+  m.log_end = e->host_hdr.end;
+  m.log_capacity = e->cfg.log_capacity;
+  m.rows_allocated = (uint64_t)e->host_hdr.rows_next;
+  m.row_capacity = e->cfg.row_capacity;
+  m.arena_used = (uint64_t)e->host_hdr.arena_next;
+  m.arena_bytes = e->cfg.arena_bytes;
+  m.records_total = e->records_total;
+  m.rows_total = e->rows_total;
+  m.arena_total = e->arena_total;
+  m.compactions = e->compactions;
+  *out = m;
+  return ZB_OK;
+}
+
 int zb_counters(zb_engine* e, int64_t out[8]) {
   if (!e || !out) return ZB_EINVAL;
   uint64_t s[8];
@@ -2463,17 +2812,20 @@ int zb_read_instances(zb_engine* e, uint8_t* buf, size_t cap, size_t* len, uint6
 }  // extern "C"
 
 namespace {
-constexpr uint64_t SNAP_MAGIC = 0x31504e53425a4755ull;  // "UGZBSNP1"
+constexpr uint64_t SNAP_MAGIC = 0x32504e53425a4755ull;  // "UGZBSNP2"
+// A snapshot holds the live state only (taken right after a forced compaction): the element-instance rows
+// [0, live), the arena's dynamic region [STATIC, arena_next) (the static region comes with the deployments),
+// the live job states as (key, state) pairs, and the store entries (chains are rebuilt on restore).
 struct SnapHead {
   uint64_t magic;
   uint64_t model_hash;    // deployments the snapshot was taken with (zb_restore checks)
   WaveHdr hdr;
   uint64_t stats[8];
   int64_t epoch, msg_key_next;
-  uint64_t sub_count, msg_count, store_cap, head_mask;
-  uint64_t rows, arena_bytes;
-  uint64_t ranges, cmd_pool;
-  uint64_t jobs;          // job states (ZB_CFG_JOB_PROCESSOR: JobStateController), one byte per job key ordinal
+  uint64_t sub_count, msg_count;
+  uint64_t rows, arena_dyn;
+  uint64_t jobs;          // live job states (ZB_CFG_JOB_PROCESSOR)
+  uint64_t records_total, rows_total, arena_total;
 };
 
 uint64_t model_hash(const zb_engine* e) {  // FNV-1a over the deployed tables
@@ -2488,6 +2840,11 @@ uint64_t model_hash(const zb_engine* e) {  // FNV-1a over the deployed tables
   mix(e->static_blobs.data(), e->static_blobs.size());
   return h;
 }
+
+size_t snap_bytes(const SnapHead& h) {
+  return sizeof(h) + h.rows * (sizeof(RowMeta) + sizeof(RowKeys) + sizeof(RowAux)) + h.arena_dyn +
+         h.jobs * (sizeof(int64_t) + 1) + h.sub_count * sizeof(SubEntry) + h.msg_count * sizeof(MsgEntry);
+}
 }  // namespace
 
 extern "C" {
@@ -2498,6 +2855,8 @@ int zb_snapshot(zb_engine* e, uint8_t* buf, size_t cap, size_t* len) {
   int rc = require_quiescent(e);
   if (rc != ZB_OK) return rc;
   if (e->staged_pending && !e->staged.empty()) return fail(e, ZB_EINVAL, "staged input not injected yet");
+  rc = maintain(e, true);  // live state only
+  if (rc != ZB_OK) return rc;
   SnapHead h{};
   h.magic = SNAP_MAGIC;
   h.model_hash = model_hash(e);
@@ -2505,18 +2864,25 @@ int zb_snapshot(zb_engine* e, uint8_t* buf, size_t cap, size_t* len) {
   HIPCHECK(e, hipMemcpy(h.stats, e->dstats, sizeof(h.stats), hipMemcpyDeviceToHost));
   h.epoch = e->epoch;
   h.msg_key_next = e->msg_key_next;
-  h.sub_count = e->sub_count; h.msg_count = e->msg_count;
-  h.store_cap = e->subs ? e->store_cap : 0;
-  h.head_mask = e->head_mask;
+  h.sub_count = e->subs ? e->sub_count : 0;
+  h.msg_count = e->msgs ? e->msg_count : 0;
   h.rows = (uint64_t)e->host_hdr.rows_next;
-  h.arena_bytes = (uint64_t)e->host_hdr.arena_next;
-  h.ranges = e->ranges.size();
-  h.cmd_pool = e->cmd_pool.size();
-  h.jobs = e->jstate ? (uint64_t)std::max<int64_t>(0, (e->host_hdr.job_next - 2) / 5) : 0;
-  const uint64_t heads = h.store_cap ? h.head_mask + 1 : 0;
-  const size_t need = sizeof(h) + h.rows * (sizeof(RowMeta) + sizeof(RowKeys) + sizeof(RowAux)) + h.arena_bytes +
-                      h.ranges * sizeof(CmdRange) + h.cmd_pool +
-                      (h.store_cap ? h.store_cap * (sizeof(SubEntry) + sizeof(MsgEntry) + 8) + heads * 8 : 0) + h.jobs;
+  h.arena_dyn = (uint64_t)e->host_hdr.arena_next - STATIC_ARENA_BYTES;
+  h.records_total = e->records_total; h.rows_total = e->rows_total; h.arena_total = e->arena_total;
+  // live job states: collected on the device (the table itself is sized by capacity)
+  if (e->jobs.keys) {
+    const uint64_t slots = e->jobs.mask + 1;
+    rc = grow(e, &e->c_scratch, &e->c_scratch_cap, slots * (sizeof(int64_t) + 1));
+    if (rc != ZB_OK) return rc;
+    if (!e->c_count) HIPCHECK(e, hipMalloc(&e->c_count, sizeof(uint32_t)));
+    HIPCHECK(e, hipMemsetAsync(e->c_count, 0, sizeof(uint32_t), e->stream));
+    launch_job_collect(e->jobs, (int64_t*)e->c_scratch, e->c_scratch + slots * sizeof(int64_t), e->c_count, e->stream);
+    uint32_t n = 0;
+    HIPCHECK(e, hipMemcpyAsync(&n, e->c_count, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHECK(e, hipStreamSynchronize(e->stream));
+    h.jobs = n;
+  }
+  const size_t need = snap_bytes(h);
   *len = need;
   if (!buf || cap < need) return ZB_ENOMEM;
   uint8_t* o = buf;
@@ -2527,17 +2893,15 @@ int zb_snapshot(zb_engine* e, uint8_t* buf, size_t cap, size_t* len) {
     return true;
   };
   bool ok = get(e->rmeta, h.rows * sizeof(RowMeta)) && get(e->rkeys, h.rows * sizeof(RowKeys)) &&
-            get(e->raux, h.rows * sizeof(RowAux)) && get(e->arena, h.arena_bytes);
+            get(e->raux, h.rows * sizeof(RowAux)) && get(e->arena + STATIC_ARENA_BYTES, h.arena_dyn);
   if (!ok) return fail(e, ZB_EDEVICE, "snapshot copy");
-  std::memcpy(o, e->ranges.data(), h.ranges * sizeof(CmdRange)); o += h.ranges * sizeof(CmdRange);
-  std::memcpy(o, e->cmd_pool.data(), h.cmd_pool); o += h.cmd_pool;
-  if (h.store_cap) {
-    ok = get(e->subs, h.store_cap * sizeof(SubEntry)) && get(e->sub_next, h.store_cap * 4) &&
-         get(e->msgs, h.store_cap * sizeof(MsgEntry)) && get(e->msg_next, h.store_cap * 4) &&
-         get(e->sub_head, heads * 4) && get(e->msg_head, heads * 4);
-    if (!ok) return fail(e, ZB_EDEVICE, "snapshot copy (message stores)");
+  if (h.jobs) {
+    const uint64_t slots = e->jobs.mask + 1;
+    ok = get(e->c_scratch, h.jobs * sizeof(int64_t)) && get(e->c_scratch + slots * sizeof(int64_t), h.jobs);
+    if (!ok) return fail(e, ZB_EDEVICE, "snapshot copy (job states)");
   }
-  if (h.jobs && !get(e->jstate, h.jobs)) return fail(e, ZB_EDEVICE, "snapshot copy (job states)");
+  ok = get(e->subs, h.sub_count * sizeof(SubEntry)) && get(e->msgs, h.msg_count * sizeof(MsgEntry));
+  if (!ok) return fail(e, ZB_EDEVICE, "snapshot copy (message stores)");
   return ZB_OK;
 }
 
@@ -2548,22 +2912,19 @@ int zb_restore(zb_engine* e, const uint8_t* buf, size_t len) {
   std::memcpy(&h, buf, sizeof(h));
   if (h.magic != SNAP_MAGIC) return fail(e, ZB_EINVAL, "not a zb snapshot");
   if (h.model_hash != model_hash(e)) return fail(e, ZB_EINVAL, "snapshot was taken with other deployments");
-  if (h.rows > e->cfg.row_capacity || h.arena_bytes > e->cfg.arena_bytes || (uint64_t)h.hdr.end > e->cfg.log_capacity)
+  if (len < snap_bytes(h)) return fail(e, ZB_EINVAL, "truncated snapshot");
+  if (h.rows > e->cfg.row_capacity || STATIC_ARENA_BYTES + h.arena_dyn > e->cfg.arena_bytes)
     return fail(e, ZB_ENOMEM, "snapshot exceeds this engine's capacities");
-  const uint64_t heads = h.store_cap ? h.head_mask + 1 : 0;
-  const size_t need = sizeof(h) + h.rows * (sizeof(RowMeta) + sizeof(RowKeys) + sizeof(RowAux)) + h.arena_bytes +
-                      h.ranges * sizeof(CmdRange) + h.cmd_pool +
-                      (h.store_cap ? h.store_cap * (sizeof(SubEntry) + sizeof(MsgEntry) + 8) + heads * 8 : 0) + h.jobs;
-  if (len < need) return fail(e, ZB_EINVAL, "truncated snapshot");
-  if (h.jobs && (!e->jstate || h.jobs > e->cfg.row_capacity))
+  if (h.jobs && !e->jobs.keys)
     return fail(e, ZB_EINVAL, "snapshot holds job states: restore into an engine with ZB_CFG_JOB_PROCESSOR");
+  if (e->jobs.keys && h.jobs > (e->jobs.mask + 1) / 2) return fail(e, ZB_ENOMEM, "snapshot job states exceed the job table");
   int rc = zb_reset(e, 0);
   if (rc != ZB_OK) return rc;
-  if (h.store_cap) {
+  if (h.sub_count || h.msg_count) {
     rc = ensure_stores(e);
     if (rc != ZB_OK) return rc;
-    if (e->store_cap != h.store_cap || e->head_mask != h.head_mask)
-      return fail(e, ZB_EINVAL, "snapshot message stores need the same row capacity");
+    if (h.sub_count > e->store_cap || h.msg_count > e->store_cap)
+      return fail(e, ZB_ENOMEM, "snapshot message stores exceed this engine's store capacity");
   }
   const uint8_t* o = buf + sizeof(h);
   auto put = [&](void* dst, size_t n) -> bool {
@@ -2572,27 +2933,34 @@ int zb_restore(zb_engine* e, const uint8_t* buf, size_t len) {
     return true;
   };
   bool ok = put(e->rmeta, h.rows * sizeof(RowMeta)) && put(e->rkeys, h.rows * sizeof(RowKeys)) &&
-            put(e->raux, h.rows * sizeof(RowAux)) && put(e->arena, h.arena_bytes);
+            put(e->raux, h.rows * sizeof(RowAux)) && put(e->arena + STATIC_ARENA_BYTES, h.arena_dyn);
   if (!ok) return fail(e, ZB_EDEVICE, "restore copy");
-  e->ranges.assign((const CmdRange*)o, (const CmdRange*)o + h.ranges); o += h.ranges * sizeof(CmdRange);
-  e->cmd_pool.assign(o, o + h.cmd_pool); o += h.cmd_pool;
-  if (h.store_cap) {
-    ok = put(e->subs, h.store_cap * sizeof(SubEntry)) && put(e->sub_next, h.store_cap * 4) &&
-         put(e->msgs, h.store_cap * sizeof(MsgEntry)) && put(e->msg_next, h.store_cap * 4) &&
-         put(e->sub_head, heads * 4) && put(e->msg_head, heads * 4);
-    if (!ok) return fail(e, ZB_EDEVICE, "restore copy (message stores)");
+  if (h.jobs) {
+    rc = grow(e, &e->c_scratch, &e->c_scratch_cap, h.jobs * (sizeof(int64_t) + 1));
+    if (rc != ZB_OK) return rc;
+    ok = put(e->c_scratch, h.jobs * sizeof(int64_t)) && put(e->c_scratch + h.jobs * sizeof(int64_t), h.jobs);
+    if (!ok) return fail(e, ZB_EDEVICE, "restore copy (job states)");
+    launch_job_fill(e->jobs, (const int64_t*)e->c_scratch, e->c_scratch + h.jobs * sizeof(int64_t), (uint32_t)h.jobs,
+                    e->derr, e->stream);
   }
-  if (h.jobs && !put(e->jstate, h.jobs)) return fail(e, ZB_EDEVICE, "restore copy (job states)");
+  if (h.sub_count || h.msg_count) {
+    ok = put(e->subs, h.sub_count * sizeof(SubEntry)) && put(e->msgs, h.msg_count * sizeof(MsgEntry));
+    if (!ok) return fail(e, ZB_EDEVICE, "restore copy (message stores)");
+    launch_chains(e->msgs, h.msg_count, e->msg_head, e->msg_next, e->subs, h.sub_count, e->sub_head, e->sub_next,
+                  e->head_mask, e->stream);
+  }
   e->host_hdr = h.hdr;
   e->host_hdr.begin = e->host_hdr.gen_end = e->host_hdr.end;
-  e->log_floor = e->host_hdr.end;  // the log itself lives in the logstream, not in the snapshot
+  // the log itself lives in the logstream, not in the snapshot: the window starts empty at its end
+  e->win_base = e->released = e->host_hdr.end;
+  rebias(e);
   e->epoch = std::max(e->epoch, h.epoch);
   e->msg_key_next = h.msg_key_next;
   e->sub_count = h.sub_count; e->msg_count = h.msg_count;
+  e->records_total = h.records_total; e->rows_total = h.rows_total; e->arena_total = h.arena_total;
   e->wave = 0;
   HIPCHECK(e, hipMemcpy(e->dstats, h.stats, sizeof(h.stats), hipMemcpyHostToDevice));
-  HIPCHECK(e, hipMemcpy(e->hdr, &e->host_hdr, sizeof(WaveHdr), hipMemcpyHostToDevice));
-  return ZB_OK;
+  return finish_batch(e);
 }
 
 }  // extern "C"

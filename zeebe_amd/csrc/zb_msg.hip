@@ -107,7 +107,7 @@ __global__ void __launch_bounds__(256) k_msg_open(MsgParams P) {
     if (P.msg_cap) {
       for (uint32_t e = P.msg_head[h & P.msg_mask]; e != NO_ENTRY; e = P.msg_next[e]) {
         const MsgEntry m = P.msgs[e];
-        if (m.h != h) continue;
+        if (m.h != h || m.dead) continue;
         const MsgView v = msg_view(P.arena, m.blob);
         if (v.nn != r.name_len || v.nc != r.ck_len || !bytes_equal(v.name, r.name, v.nn) ||
             !bytes_equal(v.ck, r.ck, v.nc))
@@ -202,7 +202,7 @@ __global__ void __launch_bounds__(256) k_msg_publish(MsgParams P) {
   if (act && P.ttl > 0) {  // messageStore.addMessage
     const uint32_t idx = (uint32_t)(P.msg_count + i);
     MsgEntry m;
-    m.h = h; m.key = P.key_base + i; m.pos = pos; m.blob = ref; m.pad = 0;
+    m.h = h; m.key = P.key_base + i; m.pos = pos; m.blob = ref; m.dead = 0;
     P.msgs[idx] = m;
     P.msg_next[idx] = atomicExch(&P.msg_head[h & P.msg_mask], idx);
   }
@@ -233,9 +233,13 @@ __global__ void __launch_bounds__(256) k_wis_inject(MsgParams P) {
   d.intent = 0;  // CORRELATE
   d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION, ZB_RT_COMMAND, false);
   P.log[pos] = d;
-  P.links[pos] = (uint64_t)r.token | ((uint64_t)NO_ROW << 32);  // row_self = the catch event's row
+  // row_self: found by activity instance key (k_resolve after this kernel; the sender's row token can be stale
+  // once the workflow partition compacted its rows)
+  P.links[pos] = ~0ull;
   P.srcd[pos] = 0;
   P.vlen[pos] = VLEN_UNKNOWN;
+  P.lookup_keys[i] = r.activity_instance_key;
+  P.lookup_pos[i] = pos;
 }
 
 // ------------------------------------------------------------------------------ outbox

@@ -447,13 +447,8 @@ __device__ void bpmn_step(const WaveParams& P, const zb_rec& rec, int64_t pos, u
 
 // ---- the job stream processor (ZB_CFG_JOB_PROCESSOR): JobInstanceStreamProcessor.java:98-242 through
 // CommandProcessorImpl (accept -> follow-up event with the command's value, a new key for a null command key;
-// reject -> the command's value with its rejection). Job states live in P.jstate by key ordinal; all commands
-// for one job in a tick arrive as one group (zb_submit), so the owning thread is the only one touching it.
-__device__ __forceinline__ int64_t job_ordinal(const WaveParams& P, int64_t key) {
-  if (key < 2 || (key - 2) % 5 != 0) return -1;
-  const int64_t j = (key - 2) / 5;
-  return (uint64_t)j < P.jstate_cap && key < P.hdr[P.wave & 1].job_next ? j : -1;
-}
+// reject -> the command's value with its rejection). Job states live in the job table (P.jobs, by job key); all
+// commands for one job in a tick arrive as one group (zb_submit), so the owning thread is the only one touching it.
 
 __device__ void job_command(const WaveParams& P, const zb_rec& rec, uint32_t rself, uint32_t rscope, TState& t) {
   const uint8_t raw = rec.kind & KIND_RAW;
@@ -468,8 +463,8 @@ __device__ void job_command(const WaveParams& P, const zb_rec& rec, uint32_t rse
     s.ord = (uint8_t)t.njob++;
     return;
   }
-  const int64_t j = job_ordinal(P, rec.key);
-  const uint8_t st = j >= 0 ? P.jstate[j] : JS_NONE;
+  const int64_t j = job_find(P.jobs, rec.key);
+  const uint8_t st = j >= 0 ? P.jobs.state[j] : JS_NONE;
   uint8_t ev = 0xff, next = st;
   bool bad_value = false;
   switch (rec.intent) {
@@ -505,7 +500,15 @@ __device__ void job_command(const WaveParams& P, const zb_rec& rec, uint32_t rse
   }
   s.d.intent = ev;
   s.d.kind = make_kind(ZB_VT_JOB, ZB_RT_EVENT, t.ns > 1) | raw;
-  if (j >= 0 && next != st) P.jstate[j] = next;
+  if (j >= 0 && next != st) {
+    if (next == JS_NONE) {  // JobStateController.deleteJobState: the slot becomes a tombstone
+      P.jobs.state[j] = JS_NONE;
+      __hip_atomic_store(P.jobs.keys + j, JOB_TOMB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      atomicAdd(P.jobs.tombs, 1u);
+    } else {
+      P.jobs.state[j] = next;
+    }
+  }
 }
 
 __device__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t pos, uint32_t rself,
@@ -1064,9 +1067,9 @@ __device__ __forceinline__ void emit_item(const WaveParams& P, const Chunk& c, i
       s.d.key = job_next + 5 * (int64_t)(job0 + s.ord);
       // the job stream processor's CREATED: the job exists from here on (JobStateController.putJobState)
       if (P.jobproc && s.d.intent == JI_CREATED) {
-        const uint64_t j = (uint64_t)(s.d.key - 2) / 5;
-        if (j < P.jstate_cap) P.jstate[j] = JS_CREATED;
-        else err |= DE_ROWS_FULL;
+        const int64_t j = job_insert(P.jobs, s.d.key);
+        if (j >= 0) P.jobs.state[j] = JS_CREATED;
+        else err |= DE_ROWS_FULL;  // job table full
       }
     }
     if (s.flags & SF_INST_WF) s.d.inst_key = wf_next + 5 * (int64_t)(wf0 + s.ord);

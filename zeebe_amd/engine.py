@@ -82,6 +82,17 @@ class zb_serialize_stats(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class zb_memory_stats(ctypes.Structure):
+    _fields_ = [("log_window_begin", ctypes.c_int64), ("log_end", ctypes.c_int64), ("log_capacity", ctypes.c_uint64),
+                ("rows_allocated", ctypes.c_uint64), ("row_capacity", ctypes.c_uint64),
+                ("arena_used", ctypes.c_uint64), ("arena_bytes", ctypes.c_uint64),
+                ("records_total", ctypes.c_uint64), ("rows_total", ctypes.c_uint64), ("arena_total", ctypes.c_uint64),
+                ("compactions", ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class Record(NamedTuple):
     position: int
     source_position: int
@@ -146,6 +157,9 @@ def lib():
         L.zb_pinned_free.argtypes = [ctypes.c_void_p]
         L.zb_read_instances.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t, szp, u64p]
         L.zb_snapshot.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t, szp]
+        L.zb_log_release.argtypes = [vp, ctypes.c_int64]
+        L.zb_compact.argtypes = [vp]
+        L.zb_read_memory_stats.argtypes = [vp, ctypes.POINTER(zb_memory_stats)]
         L.zb_restore.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t]
         _lib = L
     return _lib
@@ -157,7 +171,8 @@ EXPORTED_SYMBOLS = ["zb_engine_create", "zb_engine_destroy", "zb_last_error", "z
                     "zb_outbox_count", "zb_outbox_take", "zb_comm_unique_id", "zb_comm_init", "zb_comm_pending",
                     "zb_comm_exchange", "zb_submit", "zb_read_instances", "zb_snapshot", "zb_restore",
                     "zb_validate_deployment", "zb_serialize", "zb_drain_copy", "zb_pinned_alloc", "zb_pinned_free",
-                    "zb_serialize_frames", "zb_set_request_metadata", "zb_read_source_positions"]
+                    "zb_serialize_frames", "zb_set_request_metadata", "zb_read_source_positions",
+                    "zb_log_release", "zb_compact", "zb_read_memory_stats"]
 
 
 def validate_deployment(xml):
@@ -343,6 +358,19 @@ class Engine:
 
     def log_size(self) -> int:
         return self._L.zb_log_size(self._h)
+
+    def release(self, position: int):
+        """zb_log_release: records below position were appended by the caller; they leave the device window."""
+        self._check(self._L.zb_log_release(self._h, position))
+
+    def compact(self):
+        """zb_compact: drop dead element-instance rows, unreachable payload blobs, removed messages / job states."""
+        self._check(self._L.zb_compact(self._h))
+
+    def memory_stats(self) -> dict:
+        m = zb_memory_stats()
+        self._check(self._L.zb_read_memory_stats(self._h, ctypes.byref(m)))
+        return m.as_dict()
 
     def descriptors(self, start: int = 0, count: Optional[int] = None):
         import numpy as np
