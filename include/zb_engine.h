@@ -118,32 +118,36 @@ typedef struct zb_step_stats {
                                   dominant kernel priced by bench.py's roofline; 0 on the wave pipeline */
 } zb_step_stats;
 
-/* One partition-to-partition command (SubscriptionCommandSender.java:83-128), 256 bytes, exchanged
- * between partitions by all-to-all (zeebe_amd/cluster.py; RCCL over xGMI between GPUs):
+/* One partition-to-partition command (SubscriptionCommandSender.java:83-128) exchanged between partitions
+ * (zeebe_amd/cluster.py; RCCL over xGMI between GPUs):
  *   ZB_XCHG_OPEN:      OpenMessageSubscriptionCommand, workflow partition -> abs(hash(ck) % P)
  *   ZB_XCHG_CORRELATE: CorrelateWorkflowInstanceSubscriptionCommand, message partition -> workflow partition
- * token / elem are the workflow partition's element-instance row and catch element (opaque to others). */
+ * A 64-byte header; its variable fields follow in the byte section of the batch that carries it, so message
+ * names, correlation keys and payload documents have no length limit. token / elem are the workflow partition's
+ * element-instance row (a hint: a delivered CORRELATE finds its element instance by activity instance key) and
+ * catch element. */
 #define ZB_XCHG_OPEN 1
 #define ZB_XCHG_CORRELATE 2
-#define ZB_XCHG_NAME_MAX 48
-#define ZB_XCHG_CK_MAX 48
-#define ZB_XCHG_PAYLOAD_MAX 112
 typedef struct zb_exchange_rec {
   int32_t kind;
   int32_t target_partition;
   int32_t wf_partition;          /* workflowInstancePartitionId */
-  uint32_t token;                /* element-instance row on the workflow partition (0xffffffff = none) */
+  uint32_t token;
   int64_t workflow_instance_key;
   int64_t activity_instance_key;
   int64_t source_position;       /* log position of the record whose processing produced it */
   uint16_t elem;                 /* catch element (workflow partition's model) */
-  uint8_t name_len, ck_len;
-  uint16_t payload_len;
   uint16_t pad;
-  uint8_t name[ZB_XCHG_NAME_MAX];       /* messageName */
-  uint8_t ck[ZB_XCHG_CK_MAX];           /* correlationKey (ZB_XCHG_OPEN) */
-  uint8_t payload[ZB_XCHG_PAYLOAD_MAX]; /* message payload document (ZB_XCHG_CORRELATE) */
+  uint32_t name_len;             /* messageName */
+  uint32_t ck_len;               /* correlationKey (ZB_XCHG_OPEN) */
+  uint32_t payload_len;          /* message payload document (ZB_XCHG_CORRELATE) */
+  uint64_t var_offset;           /* [name][correlation key][payload] at this offset of the batch's byte section */
 } zb_exchange_rec;
+/* An exchange batch -- the commands one partition sends one other partition in a round -- is one contiguous,
+ * 8-byte aligned block: [uint64 count][uint64 total bytes][count x zb_exchange_rec][byte section]; each
+ * record's variable bytes are padded to 8. A delivery is a sequence of batches (one per sending partition, in
+ * partition order). */
+#define ZB_XCHG_BATCH_HEADER 16
 
 /* ---- lifecycle ------------------------------------------------------------------------- */
 int zb_engine_create(const zb_config* cfg, zb_engine** out);
@@ -205,26 +209,43 @@ int zb_submit(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* va
  * max_waves (ZB_EAGAIN). stats may be NULL. */
 int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats);
 
-/* ---- message correlation (config 5) ------------------------------------------------------ */
-/* MESSAGE PUBLISH commands (ClientApiMessageHandler.java:90-162), all with one message name and
- * time-to-live and no message id; correlation keys / payloads concatenated, n+1 offsets each.
- * Appended and processed by the message stream processor at once (PublishMessageProcessor.java:58-124);
- * the partition must be quiescent with nothing staged. Correlations found go to the outbox. */
+/* ---- the message stream processor (config 5; MessageService.java:90-129) --------------------------- */
+/* ActorClock.currentTimeMillis() for the records processed from now on: a stored message's deadline is
+ * timeToLive + now (MessageDataStore.Message). */
+int zb_set_clock(zb_engine* e, int64_t now_ms);
+/* MESSAGE commands as the log holds them (ClientApiMessageHandler.java:90-162 for PUBLISH; the time-to-live
+ * checker's DELETE): metadata + the reference MessageRecord value (MessageRecord.java:26-42: name,
+ * correlationKey, timeToLive, payload, messageId), kept verbatim for the log. Appended and processed at once
+ * by the message stream processor, in order (runs of one intent are processed in lockstep):
+ *   COMMAND MESSAGE PUBLISH (key -1)  PublishMessageProcessor.java:58-124: a messageId already published with
+ *                                     the same name and correlation key -> BAD_VALUE rejection; else PUBLISHED
+ *                                     (+ DELETED when timeToLive <= 0, else stored) and a correlate command per
+ *                                     matching subscription in the outbox
+ *   COMMAND MESSAGE DELETE (key = message key)  DeleteMessageProcessor.java:36-45: DELETED, message removed
+ * The partition must be quiescent with nothing staged. */
+int zb_submit_messages(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* values, size_t values_len);
+/* Bulk PUBLISH commands with one message name and time-to-live and no message id, built by the engine
+ * (correlation keys / payloads concatenated, n+1 offsets each): same processing as zb_submit_messages. */
 int zb_submit_publishes(zb_engine* e, const char* message_name, int64_t ttl, size_t n, const uint8_t* cks,
                         const uint64_t* ck_offsets, const uint8_t* payloads, const uint64_t* payload_offsets);
-/* Commands from other partitions, in delivery order (zeebe_amd/cluster.py schedule); src is a device
- * pointer when src_on_device != 0. ZB_XCHG_OPEN records are appended as MESSAGE_SUBSCRIPTION OPEN
- * commands and processed at once (OpenMessageSubscriptionProcessor.java:56-92); ZB_XCHG_CORRELATE
- * records are appended as WORKFLOW_INSTANCE_SUBSCRIPTION CORRELATE commands (key = log position,
+/* MessageTimeToLiveChecker.run (MessageTimeToLiveChecker.java:44-68) at now_ms: a DELETE command for every
+ * stored message with deadline <= now_ms, in store order, then their processing. *n_deleted = commands written. */
+int zb_expire_messages(zb_engine* e, int64_t now_ms, uint64_t* n_deleted);
+/* Exchange batches from other partitions, in delivery order (zeebe_amd/cluster.py schedule); batches is a
+ * device pointer when on_device != 0. ZB_XCHG_OPEN commands are appended as MESSAGE_SUBSCRIPTION OPEN commands
+ * and processed at once (OpenMessageSubscriptionProcessor.java:56-92); ZB_XCHG_CORRELATE commands are appended
+ * as WORKFLOW_INSTANCE_SUBSCRIPTION CORRELATE commands (key = log position,
  * SubscriptionApiCommandMessageHandler.java:131-151), processed by the next zb_step
  * (WorkflowInstanceStreamProcessor.java:455-509). The partition must be quiescent with nothing staged. */
-int zb_inbox_submit(zb_engine* e, int kind, const zb_exchange_rec* src, size_t n, int src_on_device);
+int zb_inbox_submit(zb_engine* e, int kind, const uint8_t* batches, size_t bytes, int on_device);
 /* Pending outgoing commands of a kind (side effects of processed records). */
 int zb_outbox_count(zb_engine* e, int kind, uint64_t* n);
-/* Takes every pending command of a kind, sorted by (target partition, source position, emission order),
- * into dst (cap records; device pointer when dst_on_device != 0); counts[partition_count] per target. */
-int zb_outbox_take(zb_engine* e, int kind, zb_exchange_rec* dst, size_t cap, int dst_on_device, uint64_t* counts,
-                   uint64_t* n_out);
+/* Takes every pending command of a kind, ordered by (target partition, source position, emission order), as one
+ * exchange batch per target partition with commands, back to back in target order, into dst (cap bytes; device
+ * pointer when dst_on_device != 0). bytes_per_target[partition_count]: each target's batch size (0: none).
+ * *total = bytes needed; with dst NULL or cap too small nothing is taken (ZB_ENOMEM unless nothing is pending). */
+int zb_outbox_take(zb_engine* e, int kind, uint8_t* dst, size_t cap, int dst_on_device, uint64_t* bytes_per_target,
+                   uint64_t* n_out, uint64_t* total);
 
 /* Partition-to-partition exchange over RCCL (xGMI between the GPUs of a node): one communicator
  * per engine, rank = partition id. zb_comm_unique_id on one rank; the 128-byte id travels to the
@@ -234,7 +255,7 @@ int zb_comm_init(zb_engine* e, const uint8_t id[128], int nranks, int rank);
 /* Collective: global[k] = sum over ranks of the pending commands of kind k+1 (ZB_XCHG_OPEN, _CORRELATE). */
 int zb_comm_pending(zb_engine* e, uint64_t global[2]);
 /* Collective: every rank takes its pending commands of `kind` (zb_outbox_take order), sends each target
- * its slice (ncclSend / ncclRecv in one group), and delivers what it receives in source-rank order
+ * its batch (ncclSend / ncclRecv in one group), and delivers what it receives in source-rank order
  * (zb_inbox_submit). *received = commands delivered to this rank.
  * Failure protocol: a rank whose local work fails (outbox read, buffer growth) still takes part in the
  * (count, status) all-to-all and the status all-reduce that precede the record exchange, so every rank

@@ -640,7 +640,8 @@ class Engine {
   KeyGenerator msg_keys{0, 1};  // message stream processor (MessageService.java:91)
   // MessageSubscriptionDataStore / MessageDataStore: insertion-ordered lists, linear scans
   struct StoredSub { int32_t wfp; int64_t wik, aik; bytes name, ck; };
-  struct StoredMsg { bytes name, ck, payload, id; int64_t ttl, key; };
+  struct StoredMsg { bytes name, ck, payload, id; int64_t ttl, key, deadline; };  // MessageDataStore.Message
+  int64_t clock_ms = 0;  // ActorClock.currentTimeMillis() of the processing (MessageDataStore.Message deadline)
   std::vector<StoredSub> subs;
   std::vector<StoredMsg> msgs;
   ElementInstanceIndex index;
@@ -777,8 +778,11 @@ class Engine {
     if (value_type == VT_WORKFLOW_INSTANCE) decode_wf(value, r.wf);
     else if (value_type == VT_JOB) decode_job(value, r.job);
     else if (value_type == VT_WORKFLOW_INSTANCE_SUBSCRIPTION) decode_wis(value, r.wis);
+    else if (value_type == VT_MESSAGE) decode_msg(value, r.msg);
     else throw ZbError("unsupported value type for submit");
     if (value.empty()) r.raw_value.clear();
+    // a MESSAGE DELETE command is written by the time-to-live checker's own command writer (producer id 0)
+    if (record_type == RT_COMMAND && value_type == VT_MESSAGE && intent == MSG_DELETE) r.producer_id = 0;
     if (record_type == RT_COMMAND && value_type == VT_WORKFLOW_INSTANCE_SUBSCRIPTION && intent == WIS_CORRELATE)
       r.key = (int64_t)log.size();  // positionAsKey (SubscriptionApiCommandMessageHandler.java:131-151)
     append(std::move(r));
@@ -849,6 +853,42 @@ class Engine {
       else return false;
       return true;
     });
+  }
+  static void decode_msg(const bytes& b, MessageValue& v) {  // MessageRecord.java:26-42
+    if (b.empty()) return;
+    MpReader rd(b);
+    for_props(rd, [&](const bytes& k, MpReader& r) {
+      if (k == "name") v.name = read_str(r);
+      else if (k == "correlationKey") v.correlation_key = read_str(r);
+      else if (k == "timeToLive") v.ttl = r.read_integer();
+      else if (k == "payload") v.payload = read_doc(r);
+      else if (k == "messageId") v.message_id = read_str(r);
+      else return false;
+      return true;
+    });
+  }
+  // MessageTimeToLiveChecker.run :44-68 at `now`: a DELETE command (key = message key, the stored message's
+  // name / correlation key / ttl / payload / id) for every stored message whose deadline has passed, in store
+  // order, written by the checker's own command writer (no source event position, producer id 0)
+  size_t check_ttl(int64_t now) {
+    size_t n = 0;
+    for (const StoredMsg& m : msgs) {
+      if (m.deadline > now) continue;
+      Record r;
+      r.record_type = RT_COMMAND;
+      r.value_type = VT_MESSAGE;
+      r.intent = MSG_DELETE;
+      r.key = m.key;
+      r.msg.name = m.name;
+      r.msg.correlation_key = m.ck;
+      r.msg.ttl = m.ttl;
+      r.msg.payload = m.payload;
+      r.msg.message_id = m.id;
+      r.producer_id = 0;
+      append(std::move(r));
+      n++;
+    }
+    return n;
   }
   static void decode_wis(const bytes& b, WisValue& v) {  // WorkflowInstanceSubscriptionRecord.java:26-38
     if (b.empty()) return;
@@ -1184,7 +1224,7 @@ class Engine {
       if (sb.name == v.name && sb.ck == v.correlation_key)
         side_effects.push_back({2, sb.wik, sb.aik, v.name, bytes(), sb.wfp, sb.wfp, v.payload});
     if (v.ttl > 0) {
-      msgs.push_back({v.name, v.correlation_key, v.payload, v.message_id, v.ttl, key});
+      msgs.push_back({v.name, v.correlation_key, v.payload, v.message_id, v.ttl, key, v.ttl + clock_ms});
     } else {
       Record d = rec;
       d.key = key; d.record_type = RT_EVENT; d.intent = MSG_DELETED;
@@ -1684,6 +1724,14 @@ int zbref_submit_publish(void* h, const uint8_t* name, size_t nn, const uint8_t*
                                bytes((const char*)p, np), bytes((const char*)id, nid));
   return 0;
 }
+
+// ActorClock for the message stream processor (deadline = timeToLive + now, MessageDataStore.Message)
+int zbref_set_clock(void* h, int64_t now_ms) {
+  ((Engine*)h)->clock_ms = now_ms;
+  return 0;
+}
+// MessageTimeToLiveChecker.run at now_ms: appends the DELETE commands (processed by the next run)
+int64_t zbref_check_ttl(void* h, int64_t now_ms) { return (int64_t)((Engine*)h)->check_ttl(now_ms); }
 
 int64_t zbref_side_effect_count(void* h) { return (int64_t)((Engine*)h)->side_effects.size(); }
 

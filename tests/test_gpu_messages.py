@@ -176,3 +176,127 @@ def test_rccl_exchange_single_rank():
         assert e.counters()["completed"] == n
     finally:
         dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------------------ the whole message partition
+def _msg_value(name, ck, ttl, payload=b"\x80", message_id=b""):
+    """MessageRecord (MessageRecord.java:26-42) as the client API writes it."""
+    return msgpack.packb({"name": name, "correlationKey": ck, "timeToLive": ttl, "payload": payload,
+                          "messageId": message_id})
+
+
+def _submit_messages(gpu, ref, msgs, P):
+    """MESSAGE commands (intent, key, name, ck, ttl, payload, id) routed to abs(hash(ck) % P) as a client would."""
+    by = [[] for _ in range(P)]
+    for intent, key, name, ck, ttl, payload, mid in msgs:
+        q = cluster.subscription_partition(ck.encode(), P)
+        by[q].append((intent, key, _msg_value(name, ck, ttl, payload, mid)))
+    for q in range(P):
+        if by[q]:
+            gpu[q].submit_messages(by[q])
+            for intent, key, value in by[q]:
+                ref[q].submit(1, 10, intent, key, value)
+
+
+def test_message_ids_delete_ttl_and_large_fields():
+    """PublishMessageProcessor's messageId rejection (against the store and inside one batch), DELETE commands,
+    the time-to-live checker removing stored messages at a clock, per-command names and TTLs, 4 KB payloads and
+    200-byte correlation keys / message names through the variable-length exchange, at P = 1 and P = 3."""
+    for P in (1, 3):
+        name = "m" * 150
+        xml = (bpmn.Bpmn.create_executable_process("wf").start_event()
+               .intermediate_catch_event("catch", message=name, correlation_key="$.k").end_event().done().to_xml())
+        gpu, ref, cg, co = clusters(P, xml)
+        for x in gpu + ref:
+            x.set_clock(1000)
+        big = msgpack.packb({"blob": "z" * 4000, "n": 1})
+        cks = ["c%03d-" % i + "x" * 195 for i in range(12)]
+        # t=1000: stored messages (ttl 500 / 5000), a duplicate id in the batch, an empty id (never a duplicate),
+        # ttl 0 (deleted at once), another name
+        msgs = [(0, -1, name, cks[0], 500, big, "id-0"), (0, -1, name, cks[0], 500, big, "id-0"),
+                (0, -1, name, cks[1], 5000, msgpack.packb({"v": 1}), "id-1"), (0, -1, name, cks[2], 0, big, ""),
+                (0, -1, name, cks[2], 0, big, ""), (0, -1, "other", cks[3], 700, big, "id-0"),
+                (0, -1, name, cks[4], 5000, msgpack.packb({"v": 4}), "")]
+        _submit_messages(gpu, ref, msgs, P)
+        co.settle()
+        cg.settle()
+        compare(gpu, ref)
+        # the same ids again (rejected: already stored) and a DELETE of a stored message (key from the log)
+        stored = [r for p in ref for r in p.records() if r.value_type == 10 and r.intent == 1]
+        victim = [r for r in stored if msgpack.unpackb(r.value, raw=False)["correlationKey"] == cks[4]][0]
+        msgs = [(0, -1, name, cks[0], 500, big, "id-0"), (0, -1, name, cks[1], 10, big, "id-1"),
+                (2, victim.key, name, cks[4], 5000, msgpack.packb({"v": 4}), "")]
+        _submit_messages(gpu, ref, msgs, P)
+        co.settle()
+        cg.settle()
+        compare(gpu, ref)
+        # instances subscribe: cks[1] correlates with its stored message; cks[4]'s was deleted; cks[5] waits
+        for i, ck in enumerate([cks[1], cks[4], cks[5], cks[0]]):
+            gpu[i % P].create("wf", [msgpack.packb({"k": ck})])
+            ref[i % P].create("wf", msgpack.packb({"k": ck}))
+        cg.settle()
+        co.settle()
+        compare(gpu, ref)
+        # the time-to-live checker at t=1600: id-0 (deadline 1500) and "other" (1700? no: 1700 > 1600) expire
+        for q in range(P):
+            n_g = gpu[q].expire_messages(1600)
+            n_o = ref[q].check_ttl(1600)
+            assert n_g == n_o
+        co.settle()
+        cg.settle()
+        compare(gpu, ref)
+        # a message for the waiting instance, published after the clock moved on
+        for x in gpu + ref:
+            x.set_clock(9000)
+        _submit_messages(gpu, ref, [(0, -1, name, cks[5], 100, big, "late")], P)
+        co.settle()
+        cg.settle()
+        compare(gpu, ref)
+        for q in range(P):
+            assert gpu[q].expire_messages(20000) == ref[q].check_ttl(20000)
+        co.settle()
+        cg.settle()
+        compare(gpu, ref)
+        assert sum(g.counters()["completed"] for g in gpu) == sum(o.counters()["completed"] for o in ref) >= 3
+        rej = [r for p in ref for r in p.records() if r.value_type == 10 and r.record_type == 2]
+        assert len(rej) >= 3
+        for g in gpu:
+            g.close()
+
+
+def test_rccl_exchange_failure_protocol():
+    """A rank whose local part of zb_comm_exchange fails (ZB_FAIL_EXCHANGE, before its outbox is taken) returns an
+    error from the collective instead of hanging; the next exchange goes through and the run completes."""
+    import os
+    import socket
+
+    import torch.distributed as dist
+    from zeebe_amd.engine import Engine, ZbError
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        e = Engine(device=0, partition_id=0, partition_count=1, log_capacity=1 << 20, row_capacity=1 << 18)
+        e.deploy(catch_workflow(), 100, 1)
+        e.create("wf", [msgpack.packb({"orderId": "order-%d" % i}) for i in range(20)])
+        dc = cluster.DistCluster(e)
+        e.run()
+        assert e.comm_pending()[0] == 20
+        os.environ["ZB_FAIL_EXCHANGE"] = "0"
+        try:
+            with pytest.raises(ZbError, match="injected local failure"):
+                e.comm_exchange(cluster.KIND_OPEN)
+        finally:
+            del os.environ["ZB_FAIL_EXCHANGE"]
+        assert e.comm_pending()[0] == 20  # nothing was taken
+        dc.settle()
+        dc.publish(b"order canceled", [b"order-%d" % i for i in range(20)], [b"\x80"] * 20)
+        assert e.counters()["completed"] == 20
+        e.close()
+    finally:
+        dist.destroy_process_group()

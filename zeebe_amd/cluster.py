@@ -23,9 +23,12 @@ A delivery appends, on each target partition, the commands of source partition 0
 each source's in the order its processors produced them (log order of the records that produced
 them). Messages are published at a point of quiescence, routed by the same hash.
 
-Partitions are exchanged as fixed 256-byte records (`zb_exchange_rec` in include/zb_engine.h),
-so one `all_to_all_single` over RCCL (backend "nccl", xGMI) moves a whole round for every rank
-(`DistCluster`); `LocalCluster` runs several partitions in one process (tests, single GPU).
+Partitions exchange commands as batches (`zb_exchange_rec` in include/zb_engine.h): per (source, target) pair
+one contiguous block [count][total bytes][count 64-byte headers][variable bytes: name, correlation key, payload],
+so names, correlation keys and payloads have no length limit. GPU engines exchange their device-resident
+batches with grouped RCCL send / receive over xGMI (`DistCluster` with the engine's own communicator, the
+engine's zb_comm_exchange); torch.distributed (gloo) carries only the RCCL unique id and the control decisions.
+`LocalCluster` runs several partitions in one process (tests, single GPU).
 """
 from __future__ import annotations
 
@@ -34,16 +37,15 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
-REC_BYTES = 256
 KIND_OPEN = 1
 KIND_CORRELATE = 2
-NAME_MAX, CK_MAX, PAYLOAD_MAX = 48, 48, 112
 NO_TOKEN = 0xFFFFFFFF
+BATCH_HEADER = 16
 
-# int32 kind, target, wf_partition; u32 token; i64 wik, aik, source_position; u16 elem; u8 name_len, ck_len;
-# u16 payload_len, pad; name[48] ck[48] payload[112]
-_HDR = struct.Struct("<iiiIqqqHBBHH")
-assert _HDR.size == 48
+# int32 kind, target, wf_partition; u32 token; i64 wik, aik, source_position; u16 elem, pad; u32 name_len,
+# ck_len, payload_len; u64 var_offset
+_HDR = struct.Struct("<iiiIqqqHHIIIQ")
+assert _HDR.size == 64
 
 
 def java_hash(b: bytes) -> int:
@@ -61,32 +63,47 @@ def subscription_partition(correlation_key: bytes, partition_count: int) -> int:
     return r
 
 
-def pack(records: Sequence[dict]) -> np.ndarray:
-    """dicts (kind, partition, wf_partition, wik, aik, name, ck, payload[, token, elem, source_position])
-    -> uint8 array of len * 256."""
-    out = np.zeros(len(records) * REC_BYTES, dtype=np.uint8)
-    for i, r in enumerate(records):
+def pack_batch(records: Sequence[dict]) -> bytes:
+    """One exchange batch of dicts (kind, partition, wf_partition, wik, aik, name[, ck, payload, token, elem,
+    source_position])."""
+    if not records:
+        return b""
+    hdrs, var = [], bytearray()
+    for r in records:
         name, ck, payload = r["name"], r.get("ck", b""), r.get("payload", b"")
-        if len(name) > NAME_MAX or len(ck) > CK_MAX or len(payload) > PAYLOAD_MAX:
-            raise ValueError("exchange record field too long (name <= 48, correlation key <= 48, payload <= 112 B)")
-        hdr = _HDR.pack(r["kind"], r["partition"], r.get("wf_partition", 0), r.get("token", NO_TOKEN), r["wik"],
-                        r["aik"], r.get("source_position", -1), r.get("elem", 0xFFFF), len(name), len(ck),
-                        len(payload), 0)
-        row = hdr + name.ljust(NAME_MAX, b"\0") + ck.ljust(CK_MAX, b"\0") + payload.ljust(PAYLOAD_MAX, b"\0")
-        out[i * REC_BYTES:(i + 1) * REC_BYTES] = np.frombuffer(row, dtype=np.uint8)
-    return out
+        hdrs.append(_HDR.pack(r["kind"], r["partition"], r.get("wf_partition", 0), r.get("token", NO_TOKEN), r["wik"],
+                              r["aik"], r.get("source_position", -1), r.get("elem", 0xFFFF), 0, len(name), len(ck),
+                              len(payload), len(var)))
+        v = name + ck + payload
+        var += v + b"\0" * (-len(v) % 8)
+    body = b"".join(hdrs) + bytes(var)
+    return struct.pack("<QQ", len(records), BATCH_HEADER + len(body)) + body
+
+
+def pack(records: Sequence[dict], partition_count: int):
+    """Records in emission order -> (uint8 array of one batch per target partition, back to back in target order,
+    byte size of each target's batch)."""
+    by = [[] for _ in range(partition_count)]
+    for r in records:
+        by[r["partition"]].append(r)
+    parts = [pack_batch(b) for b in by]
+    return np.frombuffer(b"".join(parts), dtype=np.uint8).copy(), [len(p) for p in parts]
 
 
 def unpack(buf) -> List[dict]:
+    """Every command of a sequence of exchange batches, in order."""
     b = bytes(np.asarray(buf, dtype=np.uint8))
-    out = []
-    for i in range(len(b) // REC_BYTES):
-        row = b[i * REC_BYTES:(i + 1) * REC_BYTES]
-        kind, tgt, wfp, token, wik, aik, spos, elem, nl, cl, pl, _ = _HDR.unpack_from(row)
-        o = 48
-        out.append(dict(kind=kind, partition=tgt, wf_partition=wfp, token=token, wik=wik, aik=aik,
-                        source_position=spos, elem=elem, name=row[o:o + nl], ck=row[o + 48:o + 48 + cl],
-                        payload=row[o + 96:o + 96 + pl]))
+    out, o = [], 0
+    while o < len(b):
+        n, total = struct.unpack_from("<QQ", b, o)
+        var0 = o + BATCH_HEADER + 64 * n
+        for j in range(n):
+            kind, tgt, wfp, token, wik, aik, spos, elem, _, nl, cl, pl, vo = _HDR.unpack_from(b, o + BATCH_HEADER + 64 * j)
+            v = var0 + vo
+            out.append(dict(kind=kind, partition=tgt, wf_partition=wfp, token=token, wik=wik, aik=aik,
+                            source_position=spos, elem=elem, name=b[v:v + nl], ck=b[v + nl:v + nl + cl],
+                            payload=b[v + nl + cl:v + nl + cl + pl]))
+        o += total
     return out
 
 
@@ -104,11 +121,11 @@ class LocalCluster:
         boxes = [p.outbox(kind) for p in self.parts]
         for q in range(P):
             pieces = []
-            for buf, counts in boxes:
-                off = int(sum(counts[:q]))
-                n = int(counts[q])
+            for buf, sizes in boxes:  # source order: the canonical delivery order
+                off = int(sum(sizes[:q]))
+                n = int(sizes[q])
                 if n:
-                    pieces.append(buf[off * REC_BYTES:(off + n) * REC_BYTES])
+                    pieces.append(buf[off:off + n])
             if pieces:
                 self.parts[q].inbox(kind, _concat(pieces))
 
@@ -153,9 +170,11 @@ def _concat(pieces):
 class DistCluster:
     """One partition per rank of a torch.distributed process group (partition id = rank).
 
-    Each round: an all_reduce of the pending counts decides the step; an exchange is one
-    all_to_all_single of the per-target counts and one all_to_all_single of the 256-byte records
-    (RCCL over xGMI with backend "nccl" and device buffers; gloo with host buffers in the CPU tests).
+    GPU engines (rccl=True, the default for them): the engine's own RCCL communicator moves the batches
+    (zb_comm_pending / zb_comm_exchange: grouped ncclSend / ncclRecv over xGMI, with a failure protocol);
+    torch.distributed only broadcasts the RCCL unique id. Other partitions (the oracle, CPU tests): each round an
+    all_reduce of the pending counts decides the step, and an exchange is one all_to_all_single of the per-target
+    byte sizes and one of the batches (host buffers, gloo).
     """
 
     def __init__(self, partition, group=None, device=None, rccl=None):
@@ -188,18 +207,17 @@ class DistCluster:
     def _exchange(self, kind: int):
         import torch
 
-        buf, counts = self.p.outbox(kind)
-        send_counts = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=self.device)
-        recv_counts = torch.empty_like(send_counts)
-        self.dist.all_to_all_single(recv_counts, send_counts, group=self.group)
-        rc = [int(x) for x in recv_counts.tolist()]
-        sc = [int(x) for x in counts]
+        buf, sizes = self.p.outbox(kind)
+        send_sizes = torch.tensor([int(c) for c in sizes], dtype=torch.int64, device=self.device)
+        recv_sizes = torch.empty_like(send_sizes)
+        self.dist.all_to_all_single(recv_sizes, send_sizes, group=self.group)
+        rs = [int(x) for x in recv_sizes.tolist()]
+        ss = [int(x) for x in sizes]
         send = self._tensor(buf).to(torch.uint8).contiguous()
-        recv = torch.empty(sum(rc) * REC_BYTES, dtype=torch.uint8, device=self.device)
-        self.dist.all_to_all_single(recv, send, [c * REC_BYTES for c in rc], [c * REC_BYTES for c in sc],
-                                    group=self.group)
-        if sum(rc):
-            self.p.inbox(kind, recv)
+        recv = torch.empty(sum(rs), dtype=torch.uint8, device=self.device)
+        self.dist.all_to_all_single(recv, send, rs, ss, group=self.group)
+        if sum(rs):
+            self.p.inbox(kind, recv.cpu().numpy())
 
     def _any_pending(self, kind: int) -> bool:
         import torch

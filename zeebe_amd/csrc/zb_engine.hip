@@ -198,8 +198,20 @@ struct zb_engine {
   // message correlation (zb_msg.hip): outboxes [0] open-subscription, [1] correlate
   zb_exchange_rec* obox[2] = {nullptr, nullptr};
   uint64_t* okeys[2] = {nullptr, nullptr};
-  uint32_t* on = nullptr;  // [2] device counters
-  uint64_t ocap = 0;
+  uint8_t* ovar[2] = {nullptr, nullptr};  // their commands' variable bytes
+  uint32_t* on = nullptr;  // [4] device counters: commands of [0] / [1], byte-section granules of [0] / [1]
+  uint64_t ocap = 0, ovar_cap = 0;        // commands, granules
+  int64_t clock_ms = 0;                   // zb_set_clock (ActorClock of the message stream processor)
+  // message batches / delivered exchange batches
+  uint8_t* m_prior = nullptr;
+  uint64_t m_prior_cap = 0;
+  uint64_t* m_cnt = nullptr;
+  uint64_t m_cnt_cap = 0;
+  void* m_tmp = nullptr;
+  uint64_t m_tmp_cap = 0;
+  uint8_t* in_buf = nullptr;
+  uint64_t in_buf_cap = 0;
+  DevVec<uint64_t> d_slices;
   // message stores (MessageSubscriptionDataStore / MessageDataStore), allocated on first use
   SubEntry* subs = nullptr;
   uint32_t *sub_head = nullptr, *sub_next = nullptr;
@@ -212,17 +224,19 @@ struct zb_engine {
   ncclComm_t comm = nullptr;
   bool comm_broken = false;       // an RCCL call failed: the communicator is not used again
   uint64_t* d_xcounts = nullptr;  // [4 * 64]: (count, status) pairs sent to / received from every rank
-  // persistent exchange buffers (grown geometrically, never freed per round)
-  zb_exchange_rec* xsend = nullptr;
-  zb_exchange_rec* xrecv = nullptr;
+  // persistent exchange buffers, bytes (grown geometrically, never freed per round)
+  uint8_t* xsend = nullptr;
+  uint8_t* xrecv = nullptr;
   uint64_t xsend_cap = 0, xrecv_cap = 0;
   // outbox sort buffers, sized to the outbox capacity once
   uint64_t* ob_keys = nullptr;
   uint32_t *ob_idx_in = nullptr, *ob_idx_out = nullptr;
-  uint64_t* ob_first = nullptr;
+  uint64_t* ob_first = nullptr;  // [65]
+  uint32_t *ob_sizes = nullptr, *ob_goff = nullptr;
+  uint64_t *ob_table = nullptr, *ob_base = nullptr;
   void* ob_tmp = nullptr;
   size_t ob_tmp_bytes = 0;
-  zb_exchange_rec* ob_staging = nullptr;
+  uint8_t* ob_staging = nullptr;
   uint64_t ob_staging_cap = 0;
 
   // scope-wide row state (RowAux), first-live-child requests, wave epoch
@@ -352,6 +366,20 @@ int upload_model(zb_engine* e) {
   return ZB_OK;
 }
 
+// one outbox of the partition (kind ZB_XCHG_OPEN / _CORRELATE)
+Outbox outbox(zb_engine* e, int kind) {
+  Outbox o{};
+  const int k = kind - 1;
+  o.rec = e->obox[k];
+  o.keys = e->okeys[k];
+  o.n = e->on ? e->on + k : nullptr;
+  o.cap = e->ocap;
+  o.var = e->ovar[k];
+  o.var_n = e->on ? e->on + 2 + k : nullptr;
+  o.var_cap = e->ovar_cap;
+  return o;
+}
+
 WaveParams wave_params(zb_engine* e) {
   WaveParams p;
   p.log = e->log;
@@ -395,10 +423,7 @@ WaveParams wave_params(zb_engine* e) {
   p.row_cap = e->cfg.row_capacity;
   p.arena_cap = e->cfg.arena_bytes;
   p.wave = e->wave;
-  p.obox = e->obox[0];
-  p.okeys = e->okeys[0];
-  p.on = e->on;
-  p.ocap = e->ocap;
+  p.obx = outbox(e, ZB_XCHG_OPEN);
   p.partition_id = e->cfg.partition_id;
   p.partition_count = e->cfg.partition_count;
   p.raux = e->raux;
@@ -642,12 +667,15 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
 int ensure_outbox(zb_engine* e) {
   if (e->on) return ZB_OK;
   e->ocap = std::max<uint64_t>(e->cfg.row_capacity, 1024);
+  // byte sections: 192 bytes per command on average (name + correlation key or payload), at least 64 MiB
+  e->ovar_cap = std::max<uint64_t>(e->ocap * 24, 8ull << 20);
   for (int k = 0; k < 2; k++) {
     HIPCHECK(e, hipMalloc(&e->obox[k], e->ocap * sizeof(zb_exchange_rec)));
     HIPCHECK(e, hipMalloc(&e->okeys[k], e->ocap * sizeof(uint64_t)));
+    HIPCHECK(e, hipMalloc(&e->ovar[k], e->ovar_cap * 8));
   }
-  HIPCHECK(e, hipMalloc(&e->on, 2 * sizeof(uint32_t)));
-  HIPCHECK(e, hipMemsetAsync(e->on, 0, 2 * sizeof(uint32_t), e->stream));
+  HIPCHECK(e, hipMalloc(&e->on, 4 * sizeof(uint32_t)));
+  HIPCHECK(e, hipMemsetAsync(e->on, 0, 4 * sizeof(uint32_t), e->stream));
   if (!e->sub_jobs) HIPCHECK(e, hipMalloc(&e->sub_jobs, e->job_cap * sizeof(uint64_t)));
   return ZB_OK;
 }
@@ -671,21 +699,6 @@ int ensure_stores(zb_engine* e) {
   return ZB_OK;
 }
 
-MsgParams msg_params(zb_engine* e) {
-  MsgParams p{};
-  p.log = e->log;
-  p.links = e->links;
-  p.srcd = e->srcd;
-  p.vlen = e->vlen;
-  p.arena = e->arena;
-  p.subs = e->subs; p.sub_head = e->sub_head; p.sub_next = e->sub_next;
-  p.sub_mask = e->head_mask; p.sub_count = e->sub_count; p.sub_cap = e->store_cap;
-  p.msgs = e->msgs; p.msg_head = e->msg_head; p.msg_next = e->msg_next;
-  p.msg_mask = e->head_mask; p.msg_count = e->msg_count; p.msg_cap = e->store_cap;
-  p.obox = e->obox[1]; p.okeys = e->okeys[1]; p.on = e->on + 1; p.ocap = e->ocap;
-  p.err = e->derr;
-  return p;
-}
 
 // the partition must be idle for a message-side batch (canonical schedule, zeebe_amd/cluster.py)
 int require_idle(zb_engine* e) {
@@ -1049,9 +1062,10 @@ void zb_engine_destroy(zb_engine* e) {
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->comm) (void)ncclCommDestroy(e->comm);
-  void* ms[] = {e->obox[0], e->obox[1], e->okeys[0], e->okeys[1], e->on, e->subs, e->sub_head, e->sub_next,
-                e->msgs, e->msg_head, e->msg_next, e->d_xcounts, e->xsend, e->xrecv, e->ob_keys, e->ob_idx_in,
-                e->ob_idx_out, e->ob_first, e->ob_tmp, e->ob_staging};
+  void* ms[] = {e->obox[0], e->obox[1], e->okeys[0], e->okeys[1], e->ovar[0], e->ovar[1], e->on, e->subs, e->sub_head,
+                e->sub_next, e->msgs, e->msg_head, e->msg_next, e->d_xcounts, e->xsend, e->xrecv, e->ob_keys, e->ob_idx_in,
+                e->ob_idx_out, e->ob_first, e->ob_sizes, e->ob_goff, e->ob_table, e->ob_base, e->ob_tmp, e->ob_staging,
+                e->m_prior, e->m_cnt, e->m_tmp, e->in_buf};
   for (void* p : ms)
     if (p) (void)hipFree(p);
   if (e->h_hdr_pinned) (void)hipHostFree(e->h_hdr_pinned);
@@ -1067,6 +1081,7 @@ void zb_engine_destroy(zb_engine* e) {
   e->d_segpool.free();
   e->d_staged_vlen.free();
   e->d_reqs.free();
+  e->d_slices.free();
   void* dr[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_val, e->dr_tmp, e->dr_total, e->dr_tiles, e->dr_pay, e->dr_tsum,
                 e->dr_list, e->dr_list2};
   for (void* p : dr)
@@ -1128,7 +1143,8 @@ int zb_reset(zb_engine* e, int keep_staged) {
   e->staged_pending = !e->staged.empty();
   e->sub_count = e->msg_count = 0;
   e->msg_key_next = 0;
-  if (e->on) HIPCHECK(e, hipMemsetAsync(e->on, 0, 2 * sizeof(uint32_t), e->stream));
+  if (e->on) HIPCHECK(e, hipMemsetAsync(e->on, 0, 4 * sizeof(uint32_t), e->stream));
+  e->clock_ms = 0;
   if (e->subs) {
     HIPCHECK(e, hipMemsetAsync(e->sub_head, 0xff, (e->head_mask + 1) * sizeof(uint32_t), e->stream));
     HIPCHECK(e, hipMemsetAsync(e->msg_head, 0xff, (e->head_mask + 1) * sizeof(uint32_t), e->stream));
@@ -2242,6 +2258,362 @@ static uint8_t* host_stage(zb_engine* e, size_t bytes) {
   return e->h_stage;
 }
 
+}  // extern "C"
+
+// ---- the message stream processor and the partition exchange (host side; kernels in zb_msg.hip)
+namespace {
+
+// MESSAGE commands ready for the device: descriptors (payload = the message blob's ref relative to the batch's
+// blob area; KIND_RAW commands have their verbatim value blob right after it) and the blob area
+struct MsgBatch {
+  std::vector<zb_rec> recs;
+  std::vector<uint8_t> blobs;
+  std::vector<uint8_t> prior;  // PUBLISH: an earlier command of the batch has the same (name, ck, id) and ttl > 0
+};
+
+// message blob (zb_msg.hpp MsgView): [u32 len][u32 nn][i64 ttl][i64 deadline][u32 nc][u32 np][u32 nid][u32 pad]
+// [name][ck][payload][id]
+uint32_t add_msg_blob(std::vector<uint8_t>& a, const uint8_t* name, uint32_t nn, const uint8_t* ck, uint32_t nc,
+                      int64_t ttl, const uint8_t* pl, uint32_t np, const uint8_t* id, uint32_t nid) {
+  const size_t off = a.size();
+  const uint32_t len = MSG_HDR - 4 + nn + nc + np + nid;
+  a.resize(off + ((4 + (size_t)len + 7) & ~(size_t)7), 0);
+  uint8_t* b = a.data() + off;
+  const int64_t deadline = 0;  // set when the message is stored
+  std::memcpy(b, &len, 4);
+  std::memcpy(b + 4, &nn, 4);
+  std::memcpy(b + 8, &ttl, 8);
+  std::memcpy(b + 16, &deadline, 8);
+  std::memcpy(b + 24, &nc, 4);
+  std::memcpy(b + 28, &np, 4);
+  std::memcpy(b + 32, &nid, 4);
+  uint8_t* d = b + MSG_HDR;
+  if (nn) std::memcpy(d, name, nn);
+  if (nc) std::memcpy(d + nn, ck, nc);
+  if (np) std::memcpy(d + nn + nc, pl, np);
+  if (nid) std::memcpy(d + nn + nc + np, id, nid);
+  return (uint32_t)(off >> 3);
+}
+
+MsgParams msg_params(zb_engine* e) {
+  MsgParams p{};
+  p.log = e->log; p.links = e->links; p.srcd = e->srcd; p.vlen = e->vlen;
+  p.arena = e->arena;
+  p.hdr = e->hdr + (e->wave & 1);
+  p.arena_cap = e->cfg.arena_bytes;
+  p.subs = e->subs; p.sub_head = e->sub_head; p.sub_next = e->sub_next;
+  p.sub_mask = e->head_mask; p.sub_count = e->sub_count; p.sub_cap = e->store_cap;
+  p.msgs = e->msgs; p.msg_head = e->msg_head; p.msg_next = e->msg_next;
+  p.msg_mask = e->head_mask; p.msg_count = e->msg_count; p.msg_cap = e->store_cap;
+  p.ob = outbox(e, 1);
+  p.err = e->derr;
+  p.clock = e->clock_ms;
+  return p;
+}
+
+// the device header after message-side kernels that allocate blobs with atomics (arena_next)
+int pull_header(zb_engine* e) {
+  HIPCHECK(e, hipMemcpyAsync(e->h_hdr_pinned, e->hdr + (e->wave & 1), sizeof(WaveHdr), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  e->host_hdr.arena_next = e->h_hdr_pinned[0].arena_next;
+  return ZB_OK;
+}
+
+int grow_dev(zb_engine* e, uint8_t** p, uint64_t* cap, uint64_t bytes) {
+  if (bytes <= *cap && *p) return ZB_OK;
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  const uint64_t c = std::max<uint64_t>(bytes + bytes / 2, 1 << 20);
+  HIPCHECK(e, hipMalloc(p, c));
+  *cap = c;
+  return ZB_OK;
+}
+
+// exclusive scan of u64 in[0, n] into out (in[n] = 0); returns out[n]
+int scan_u64(zb_engine* e, uint64_t* in, uint64_t* out, uint64_t n, uint64_t* total) {
+  if (n + 1 > (uint64_t)INT32_MAX) return fail(e, ZB_EUNSUPPORTED, "more than 2^31 commands in one batch");
+  HIPCHECK(e, hipMemsetAsync(in + n, 0, sizeof(uint64_t), e->stream));
+  size_t tmp = 0;
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (int)(n + 1), e->stream) != hipSuccess)
+    return fail(e, ZB_EDEVICE, "scan sizing");
+  int rc = grow_dev(e, (uint8_t**)&e->m_tmp, &e->m_tmp_cap, tmp + 16);
+  if (rc != ZB_OK) return rc;
+  tmp = e->m_tmp_cap;
+  if (hipcub::DeviceScan::ExclusiveSum(e->m_tmp, tmp, in, out, (int)(n + 1), e->stream) != hipSuccess)
+    return fail(e, ZB_EDEVICE, "scan");
+  HIPCHECK(e, hipMemcpyAsync(total, out + n, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  return ZB_OK;
+}
+
+// Appends the batch's commands at the log tail and processes them in order, runs of one intent in lockstep
+// (PUBLISH: count, scan, emit; DELETE: emit). Follow-ups come after all the commands, in command order (FIFO).
+int process_messages(zb_engine* e, const MsgBatch& b) {
+  const uint64_t n = b.recs.size();
+  if (n == 0) return ZB_OK;
+  const int64_t base = e->host_hdr.end;
+  // upper bounds first: every command writes at most 3 records (itself, PUBLISHED, DELETED)
+  if ((uint64_t)(base - e->win_base) + 3 * n > e->cfg.log_capacity)
+    return fail(e, ZB_ENOMEM, "log capacity (release drained records with zb_log_release)");
+  if ((uint64_t)base + 3 * n >= (1ull << 34)) return fail(e, ZB_EUNSUPPORTED, "log position beyond the outbox order key");
+  uint64_t publishes = 0;
+  for (const zb_rec& r : b.recs) publishes += r.intent == 0 ? 1 : 0;
+  if (e->msg_count + publishes > e->store_cap) return fail(e, ZB_ENOMEM, "message store capacity");
+  const uint64_t arena0 = (uint64_t)e->host_hdr.arena_next;
+  if (arena0 + b.blobs.size() > e->cfg.arena_bytes) return fail(e, ZB_ENOMEM, "arena capacity");
+  // commands + blobs (refs made absolute on the host), one upload through pinned staging
+  uint8_t* stage = host_stage(e, n * sizeof(zb_rec) + b.blobs.size() + n);
+  if (!stage) return fail(e, ZB_ENOMEM, "pinned staging memory");
+  zb_rec* recs = (zb_rec*)stage;
+  for (uint64_t i = 0; i < n; i++) {
+    recs[i] = b.recs[i];
+    recs[i].payload += (uint32_t)(arena0 >> 3);
+  }
+  std::memcpy(stage + n * sizeof(zb_rec), b.blobs.data(), b.blobs.size());
+  std::memcpy(stage + n * sizeof(zb_rec) + b.blobs.size(), b.prior.data(), n);
+  int rc = grow_dev(e, &e->m_prior, &e->m_prior_cap, n);
+  if (rc == ZB_OK) rc = grow_dev(e, (uint8_t**)&e->m_cnt, &e->m_cnt_cap, 2 * (n + 1) * sizeof(uint64_t));
+  if (rc != ZB_OK) return rc;
+  HIPCHECK(e, hipMemcpyAsync(e->log + base, recs, n * sizeof(zb_rec), hipMemcpyHostToDevice, e->stream));
+  HIPCHECK(e, hipMemcpyAsync(e->arena + arena0, stage + n * sizeof(zb_rec), b.blobs.size(), hipMemcpyHostToDevice, e->stream));
+  HIPCHECK(e, hipMemcpyAsync(e->m_prior, stage + n * sizeof(zb_rec) + b.blobs.size(), n, hipMemcpyHostToDevice, e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->links + base, 0xff, n * sizeof(uint64_t), e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->srcd + base, 0, n * sizeof(uint32_t), e->stream));  // written by other writers
+  // (the verbatim value of a submitted command is its serialized length: the size pass measures the rest)
+  HIPCHECK(e, hipMemsetAsync(e->vlen + base, 0xff, n * sizeof(uint32_t), e->stream));
+  e->host_hdr.arena_next += (int64_t)b.blobs.size();
+  e->arena_total += b.blobs.size();
+  int64_t out = base + (int64_t)n;  // the next follow-up position
+  for (uint64_t i0 = 0; i0 < n;) {
+    const uint8_t intent = b.recs[i0].intent;
+    uint64_t i1 = i0 + 1;
+    while (i1 < n && b.recs[i1].intent == intent && i1 - i0 < (1u << 20)) i1++;
+    MsgParams p = msg_params(e);
+    p.base = base + (int64_t)i0;
+    p.n = (int64_t)(i1 - i0);
+    p.out_base = out;
+    if (intent == 0) {  // PUBLISH
+      p.prior = e->m_prior + i0;
+      p.cnt = e->m_cnt;
+      p.cnt_off = e->m_cnt + (n + 1);
+      p.key_base = e->msg_key_next;
+      launch_pub_count(p, e->stream);
+      uint64_t tot = 0;
+      rc = scan_u64(e, e->m_cnt, e->m_cnt + (n + 1), i1 - i0, &tot);
+      if (rc != ZB_OK) return rc;
+      launch_pub_emit(p, e->stream);
+      const uint64_t mask = (1ull << 21) - 1;
+      out += (int64_t)(tot & mask);
+      e->msg_key_next += (int64_t)((tot >> 21) & mask);
+      e->msg_count += (tot >> 42) & mask;
+    } else {  // DELETE
+      launch_msg_delete(p, e->stream);
+      out += (int64_t)(i1 - i0);
+    }
+    i0 = i1;
+  }
+  e->records_total += (uint64_t)(out - base);
+  e->host_hdr.end = out;
+  e->host_hdr.begin = e->host_hdr.gen_end = e->host_hdr.end;
+  return finish_batch(e);
+}
+
+// MessageRecord (MessageRecord.java:26-42) of a submitted MESSAGE command
+bool decode_message(const uint8_t* v, size_t n, std::string& name, std::string& ck, int64_t& ttl, const uint8_t*& pl,
+                    uint32_t& np, std::string& id) {
+  ttl = 0;
+  pl = nullptr;
+  np = 0;
+  if (n == 0) return true;
+  MpIn in{v, n};
+  const uint32_t props = in.map_hdr();
+  for (uint32_t i = 0; i < props && in.ok; i++) {
+    const uint8_t* k; uint32_t kl;
+    if (!in.str(k, kl)) return false;
+    const uint8_t* s; uint32_t sl;
+    if (in.key_is(k, kl, "name")) { if (!in.str(s, sl)) return false; name.assign((const char*)s, sl); }
+    else if (in.key_is(k, kl, "correlationKey")) { if (!in.str(s, sl)) return false; ck.assign((const char*)s, sl); }
+    else if (in.key_is(k, kl, "messageId")) { if (!in.str(s, sl)) return false; id.assign((const char*)s, sl); }
+    else if (in.key_is(k, kl, "timeToLive")) ttl = in.integer();
+    else if (in.key_is(k, kl, "payload")) { if (!in.bin(pl, np)) return false; }
+    else in.skip();
+  }
+  return in.ok && in.o == n;
+}
+
+// the intra-batch part of MessageDataStore.hasMessage: command i follows a command with the same (name,
+// correlation key, message id) and ttl > 0 (which stores it unless it is rejected itself -- then so is i)
+struct PriorIds {
+  std::unordered_set<std::string> seen;
+  uint8_t check(const std::string& name, const std::string& ck, const std::string& id, int64_t ttl) {
+    if (id.empty()) return 0;
+    std::string k;
+    k.reserve(name.size() + ck.size() + id.size() + 16);
+    auto put = [&](const std::string& s) { const uint64_t l = s.size(); k.append((const char*)&l, 8); k += s; };
+    put(name); put(ck); put(id);
+    const uint8_t hit = seen.count(k) ? 1 : 0;
+    if (ttl > 0) seen.insert(k);
+    return hit;
+  }
+};
+
+// delivered batches in device memory at buf (slices: command count and byte offset of each batch)
+int deliver(zb_engine* e, int kind, const uint8_t* buf, const std::vector<uint64_t>& counts,
+            const std::vector<uint64_t>& offs, uint64_t* delivered) {
+  uint64_t n = 0;
+  std::vector<uint64_t> first;
+  std::vector<uint64_t> off;
+  for (size_t s = 0; s < counts.size(); s++) {
+    if (!counts[s]) continue;
+    first.push_back(n);
+    off.push_back(offs[s]);
+    n += counts[s];
+  }
+  if (delivered) *delivered = n;
+  if (n == 0) return ZB_OK;
+  const int64_t base = e->host_hdr.end;
+  const uint64_t recs = kind == ZB_XCHG_OPEN ? 2 * n : n;
+  if ((uint64_t)(base - e->win_base) + recs > e->cfg.log_capacity) return fail(e, ZB_ENOMEM, "log capacity");
+  if ((uint64_t)base + recs >= (1ull << 34)) return fail(e, ZB_EUNSUPPORTED, "log position beyond the outbox order key");
+  if (kind == ZB_XCHG_OPEN && (e->sub_count + n > e->store_cap || e->sub_count + n >= (1ull << 32)))
+    return fail(e, ZB_ENOMEM, "subscription store capacity");
+  std::vector<uint64_t> table(first);
+  table.insert(table.end(), off.begin(), off.end());
+  HIPCHECK(e, e->d_slices.upload(table, e->stream));
+  MsgParams p = msg_params(e);
+  p.in = buf;
+  p.nslices = (int32_t)first.size();
+  p.slice_first = e->d_slices.p;
+  p.slice_off = e->d_slices.p + first.size();
+  p.n = (int64_t)n;
+  p.base = base;
+  const int64_t arena_before = e->host_hdr.arena_next;
+  if (kind == ZB_XCHG_OPEN) {
+    launch_msg_open(p, e->stream);  // processed at once: OPEN commands + OPENED events
+    e->sub_count += n;
+    e->host_hdr.end = base + (int64_t)recs;
+    e->host_hdr.begin = e->host_hdr.gen_end = e->host_hdr.end;
+  } else {
+    // CORRELATE commands: the next zb_step processes them; the element instance each names is looked up by its
+    // activity instance key (ElementInstanceIndex.getInstance): keys sorted, then one pass over the rows
+    if (n > e->x_cap) {
+      HIPCHECK(e, hipStreamSynchronize(e->stream));
+      void* xs[] = {e->x_keys, e->x_pos, e->x_keys2, e->x_pos2};
+      for (void* q : xs)
+        if (q) (void)hipFree(q);
+      e->x_keys = e->x_pos = e->x_keys2 = e->x_pos2 = nullptr;
+      e->x_cap = 0;
+      const uint64_t c = std::max<uint64_t>(n + n / 2, 1024);
+      HIPCHECK(e, hipMalloc(&e->x_keys, c * 8));
+      HIPCHECK(e, hipMalloc(&e->x_pos, c * 8));
+      HIPCHECK(e, hipMalloc(&e->x_keys2, c * 8));
+      HIPCHECK(e, hipMalloc(&e->x_pos2, c * 8));
+      e->x_cap = c;
+    }
+    if (n > (uint64_t)INT32_MAX) return fail(e, ZB_EUNSUPPORTED, "more than 2^31 delivered commands");
+    p.lookup_keys = e->x_keys;
+    p.lookup_pos = e->x_pos;
+    launch_wis_inject(p, e->stream);
+    size_t tmp = 0;
+    if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, e->x_keys, e->x_keys2, e->x_pos, e->x_pos2, (int)n, 0, 64,
+                                           e->stream) != hipSuccess)
+      return fail(e, ZB_EDEVICE, "inbox sort sizing");
+    int rc = grow_dev(e, (uint8_t**)&e->x_tmp, &e->x_tmp_cap, tmp + 16);
+    if (rc != ZB_OK) return rc;
+    tmp = e->x_tmp_cap;
+    if (hipcub::DeviceRadixSort::SortPairs(e->x_tmp, tmp, e->x_keys, e->x_keys2, e->x_pos, e->x_pos2, (int)n, 0, 64,
+                                           e->stream) != hipSuccess)
+      return fail(e, ZB_EDEVICE, "inbox sort");
+    ResolveParams rp{};
+    rp.rmeta = e->rmeta; rp.rkeys = e->rkeys; rp.rows = (uint64_t)e->host_hdr.rows_next;
+    rp.keys = e->x_keys2; rp.pos = e->x_pos2; rp.n = (int64_t)n;
+    rp.links = e->links;
+    launch_resolve(rp, e->stream);
+    e->host_hdr.end = base + (int64_t)recs;
+    e->host_hdr.gen_end = e->host_hdr.end;
+  }
+  int rc = pull_header(e);  // blobs were allocated on the device header
+  if (rc != ZB_OK) return rc;
+  e->records_total += recs;
+  e->arena_total += (uint64_t)(e->host_hdr.arena_next - arena_before);
+  return finish_batch(e);
+}
+
+// batches laid out back to back: (count, byte offset) of each, from their headers
+bool parse_batches(const uint8_t* p, size_t bytes, std::vector<uint64_t>& counts, std::vector<uint64_t>& offs) {
+  size_t o = 0;
+  while (o < bytes) {
+    if (bytes - o < ZB_XCHG_BATCH_HEADER) return false;
+    uint64_t h[2];
+    std::memcpy(h, p + o, sizeof(h));
+    if (h[1] < ZB_XCHG_BATCH_HEADER + h[0] * sizeof(zb_exchange_rec) || h[1] > bytes - o || (h[1] & 7)) return false;
+    counts.push_back(h[0]);
+    offs.push_back(o);
+    o += h[1];
+  }
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int zb_set_clock(zb_engine* e, int64_t now_ms) {
+  if (!e) return ZB_EINVAL;
+  e->clock_ms = now_ms;
+  return ZB_OK;
+}
+
+int zb_submit_messages(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* values, size_t values_len) {
+  if (!e || (n > 0 && (!recs || (!values && values_len)))) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  int rc = require_idle(e);
+  if (rc != ZB_OK) return rc;
+  if (n == 0) return ZB_OK;
+  MsgBatch b;
+  b.recs.reserve(n);
+  b.prior.reserve(n);
+  PriorIds prior;
+  static const uint8_t EMPTY = 0x80;
+  for (size_t i = 0; i < n; i++) {  // decode + validate everything first (nothing changes on an error)
+    const zb_rec_desc& r = recs[i];
+    if (r.value_offset > values_len || r.value_length > values_len - r.value_offset)
+      return fail(e, ZB_EINVAL, "record " + std::to_string(i) + ": value out of range");
+    if (r.value_type != ZB_VT_MESSAGE || r.record_type != ZB_RT_COMMAND || (r.intent != 0 && r.intent != 2))
+      return fail(e, ZB_EUNSUPPORTED, "record " + std::to_string(i) + ": no message processor is registered for "
+                                      "(recordType, valueType, intent) = (" + std::to_string(r.record_type) + ", " +
+                                      std::to_string(r.value_type) + ", " + std::to_string(r.intent) + ")");
+    const uint8_t* v = values + r.value_offset;
+    std::string name, ck, id;
+    int64_t ttl = 0;
+    const uint8_t* pl = nullptr;
+    uint32_t np = 0;
+    if (!decode_message(v, r.value_length, name, ck, ttl, pl, np, id))
+      return fail(e, ZB_EINVAL, "record " + std::to_string(i) + ": malformed msgpack value");
+    if (!pl || np == 0 || (np == 1 && pl[0] == 0xc0)) { pl = &EMPTY; np = 1; }  // DocumentValue: nil -> {}
+    if (!is_doc(pl, np))
+      return fail(e, ZB_EINVAL, "record " + std::to_string(i) + ": Document has invalid format. On root level an object is only allowed.");
+    zb_rec d{};
+    d.key = r.intent == 0 ? -1 : r.key;  // PUBLISH: a client command has no key
+    d.scope_key = -1;
+    d.inst_key = -1;
+    d.payload = add_msg_blob(b.blobs, (const uint8_t*)name.data(), (uint32_t)name.size(), (const uint8_t*)ck.data(),
+                             (uint32_t)ck.size(), ttl, pl, np, (const uint8_t*)id.data(), (uint32_t)id.size());
+    add_blob(b.blobs, v, (uint32_t)r.value_length);  // the verbatim value (KIND_RAW)
+    d.elem = NO_ELEM;
+    d.intent = r.intent;
+    d.kind = (uint8_t)(make_kind(ZB_VT_MESSAGE, ZB_RT_COMMAND, false) | KIND_RAW);
+    b.recs.push_back(d);
+    b.prior.push_back(r.intent == 0 ? prior.check(name, ck, id, ttl) : 0);
+  }
+  rc = ensure_stores(e);
+  if (rc == ZB_OK) rc = maintain(e, false);
+  if (rc != ZB_OK) return rc;
+  return process_messages(e, b);
+}
+
 int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, const uint8_t* cks,
                         const uint64_t* ck_offsets, const uint8_t* payloads, const uint64_t* payload_offsets) {
   if (!e || !name || (n > 0 && (!cks || !ck_offsets || !payloads || !payload_offsets))) return ZB_EINVAL;
@@ -2249,20 +2621,13 @@ int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, c
   int rc = require_idle(e);
   if (rc != ZB_OK) return rc;
   if (n == 0) return ZB_OK;
-  rc = ensure_stores(e);
-  if (rc == ZB_OK) rc = maintain(e, false);
-  if (rc != ZB_OK) return rc;
-  const uint64_t nn = std::strlen(name);
-  if (nn > 0xffff) return fail(e, ZB_EINVAL, "message name too long");
-  const int per = ttl > 0 ? 1 : 2;
-  const int64_t base = e->host_hdr.end;
-  if ((uint64_t)(base + (int64_t)n * (1 + per) - e->win_base) > e->cfg.log_capacity) return fail(e, ZB_ENOMEM, "log capacity");
-  if ((uint64_t)base + n * (1 + per) >= (1ull << 34)) return fail(e, ZB_EUNSUPPORTED, "log position beyond the outbox order key");
-  if (e->msg_count + (ttl > 0 ? n : 0) > e->store_cap) return fail(e, ZB_ENOMEM, "message store capacity");
-  // PUBLISH commands (null key) and their message blobs, built on the host straight into pinned staging
-  // memory (validated and sized first, so a failure changes nothing) and uploaded once
-  // (large batches: sized and filled by up to 8 host threads over contiguous chunks)
+  const uint32_t nn = (uint32_t)std::strlen(name);
   static const uint8_t EMPTY = 0x80;
+  MsgBatch b;
+  b.recs.resize(n);
+  b.prior.assign(n, 0);
+  // PUBLISH commands (null key, no message id) and their blobs; large batches are built by up to 8 host threads
+  // over contiguous chunks (sized first, then filled)
   const size_t nth = n >= 65536 ? std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency())) : 1;
   const size_t chunk = (n + nth - 1) / nth;
   std::vector<size_t> part_bytes(nth + 1, 0);
@@ -2279,162 +2644,115 @@ int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, c
       const uint64_t nc = ck_offsets[i + 1] - ck_offsets[i];
       const uint8_t* pl = payloads + payload_offsets[i];
       uint64_t np = payload_offsets[i + 1] - payload_offsets[i];
-      if (np == 0 || (np == 1 && pl[0] == 0xc0)) np = 1;  // DocumentValue: nil / empty -> {}
+      if (np == 0 || (np == 1 && pl[0] == 0xc0)) np = 1;
       else if (!((pl[0] & 0xf0) == 0x80 || pl[0] == 0xde || pl[0] == 0xdf)) { part_err[t] = 1; return; }
-      if (nc > 0xffff) { part_err[t] = 2; return; }
-      bytes += (4 + 16 + nn + nc + np + 7) & ~(size_t)7;
+      if (nc > 0xffffffffull || np > 0xffffffffull) { part_err[t] = 2; return; }
+      bytes += (MSG_HDR + nn + nc + np + 7) & ~(size_t)7;
     }
     part_bytes[t + 1] = bytes;
   });
-  for (size_t t = 0; t < nth; t++) {  // (the first failing chunk's error, as the sequential check reports it)
+  for (size_t t = 0; t < nth; t++) {
     if (part_err[t] == 1) return fail(e, ZB_EINVAL, "Document has invalid format. On root level an object is only allowed.");
-    if (part_err[t] == 2) return fail(e, ZB_EINVAL, "correlation key too long");
+    if (part_err[t] == 2) return fail(e, ZB_EINVAL, "correlation key or payload too long");
   }
   for (size_t t = 0; t < nth; t++) part_bytes[t + 1] += part_bytes[t];
-  const size_t blob_bytes = part_bytes[nth];
-  const uint64_t arena0 = (uint64_t)e->host_hdr.arena_next;
-  if (arena0 + blob_bytes > e->cfg.arena_bytes) return fail(e, ZB_ENOMEM, "arena capacity");
-  uint8_t* stage = host_stage(e, n * sizeof(zb_rec) + blob_bytes);
-  if (!stage) return fail(e, ZB_ENOMEM, "pinned staging memory");
-  zb_rec* recs = (zb_rec*)stage;
-  uint8_t* blobs = stage + n * sizeof(zb_rec);
+  b.blobs.resize(part_bytes[nth]);
   run_parts([&](size_t t) {
-  size_t off = part_bytes[t];
-  for (size_t i = t * chunk; i < std::min(n, (t + 1) * chunk); i++) {
-    const uint8_t* ck = cks + ck_offsets[i];
-    const uint64_t nc = ck_offsets[i + 1] - ck_offsets[i];
-    const uint8_t* pl = payloads + payload_offsets[i];
-    uint64_t np = payload_offsets[i + 1] - payload_offsets[i];
-    if (np == 0 || (np == 1 && pl[0] == 0xc0)) { pl = &EMPTY; np = 1; }
-    const uint32_t len = (uint32_t)(16 + nn + nc + np);
-    const size_t sz = (4 + len + 7) & ~(size_t)7;
-    uint8_t* b = blobs + off;
-    std::memset(b + 4 + len, 0, sz - 4 - len);
-    std::memcpy(b, &len, 4);
-    std::memcpy(b + 4, &ttl, 8);
-    const uint16_t n16 = (uint16_t)nn, c16 = (uint16_t)nc;
-    const uint32_t p32 = (uint32_t)np;
-    std::memcpy(b + 12, &n16, 2);
-    std::memcpy(b + 14, &c16, 2);
-    std::memcpy(b + 16, &p32, 4);
-    std::memcpy(b + 20, name, nn);
-    std::memcpy(b + 20 + nn, ck, nc);
-    std::memcpy(b + 20 + nn + nc, pl, np);
-    zb_rec& d = recs[i];
-    d.key = -1; d.scope_key = -1; d.inst_key = -1;
-    d.payload = (uint32_t)((arena0 + off) >> 3);
-    d.elem = NO_ELEM; d.intent = 0;  // PUBLISH
-    d.kind = make_kind(ZB_VT_MESSAGE, ZB_RT_COMMAND, false);
-    off += sz;
-  }
+    std::vector<uint8_t> tmp;
+    size_t off = part_bytes[t];
+    for (size_t i = t * chunk; i < std::min(n, (t + 1) * chunk); i++) {
+      const uint8_t* pl = payloads + payload_offsets[i];
+      uint64_t np = payload_offsets[i + 1] - payload_offsets[i];
+      if (np == 0 || (np == 1 && pl[0] == 0xc0)) { pl = &EMPTY; np = 1; }
+      tmp.clear();
+      add_msg_blob(tmp, (const uint8_t*)name, nn, cks + ck_offsets[i], (uint32_t)(ck_offsets[i + 1] - ck_offsets[i]),
+                   ttl, pl, (uint32_t)np, nullptr, 0);
+      std::memcpy(b.blobs.data() + off, tmp.data(), tmp.size());
+      zb_rec& d = b.recs[i];
+      d.key = -1; d.scope_key = -1; d.inst_key = -1;
+      d.payload = (uint32_t)(off >> 3);
+      d.elem = NO_ELEM; d.intent = 0;  // PUBLISH
+      d.kind = make_kind(ZB_VT_MESSAGE, ZB_RT_COMMAND, false);
+      off += tmp.size();
+    }
   });
-  HIPCHECK(e, hipMemcpyAsync(e->log + base, recs, n * sizeof(zb_rec), hipMemcpyHostToDevice, e->stream));
-  HIPCHECK(e, hipMemcpyAsync(e->arena + arena0, blobs, blob_bytes, hipMemcpyHostToDevice, e->stream));
-  HIPCHECK(e, hipMemsetAsync(e->links + base, 0xff, n * sizeof(uint64_t), e->stream));
-  HIPCHECK(e, hipMemsetAsync(e->srcd + base, 0, n * sizeof(uint32_t), e->stream));  // client API commands
-  HIPCHECK(e, hipMemsetAsync(e->vlen + base, 0xff, n * sizeof(uint32_t), e->stream));
-  MsgParams p = msg_params(e);
-  p.n = (int64_t)n;
-  p.base = base;
-  p.ttl = ttl;
-  p.key_base = e->msg_key_next;
-  launch_msg_publish(p, e->stream);
-  e->msg_key_next += (int64_t)n;
-  if (ttl > 0) e->msg_count += n;
-  e->host_hdr.end = base + (int64_t)n * (1 + per);
-  e->host_hdr.begin = e->host_hdr.gen_end = e->host_hdr.end;
-  e->host_hdr.arena_next += (int64_t)blob_bytes;
-  e->records_total += n * (1 + per);
-  e->arena_total += blob_bytes;
-  return finish_batch(e);
-}
-
-int zb_inbox_submit(zb_engine* e, int kind, const zb_exchange_rec* src, size_t n, int src_on_device) {
-  if (!e || (n > 0 && !src) || (kind != ZB_XCHG_OPEN && kind != ZB_XCHG_CORRELATE)) return ZB_EINVAL;
-  HIPCHECK(e, hipSetDevice(e->cfg.device));
-  int rc = require_idle(e);
-  if (rc != ZB_OK) return rc;
-  if (n == 0) return ZB_OK;
   rc = ensure_stores(e);
   if (rc == ZB_OK) rc = maintain(e, false);
   if (rc != ZB_OK) return rc;
-  const int64_t base = e->host_hdr.end;
-  const uint64_t recs = kind == ZB_XCHG_OPEN ? 2 * n : n;
-  const uint64_t stride = kind == ZB_XCHG_OPEN ? SUB_BLOB : WIS_BLOB;
-  if ((uint64_t)(base - e->win_base) + recs > e->cfg.log_capacity) return fail(e, ZB_ENOMEM, "log capacity");
-  if ((uint64_t)base + recs >= (1ull << 34)) return fail(e, ZB_EUNSUPPORTED, "log position beyond the outbox order key");
-  if ((uint64_t)e->host_hdr.arena_next + n * stride > e->cfg.arena_bytes) return fail(e, ZB_ENOMEM, "arena capacity");
-  if (kind == ZB_XCHG_OPEN && (e->sub_count + n > e->store_cap || e->sub_count + n >= (1ull << 24)))
-    return fail(e, ZB_ENOMEM, "subscription store capacity");
-  const zb_exchange_rec* dsrc = src;
-  zb_exchange_rec* tmp = nullptr;
-  if (!src_on_device) {
-    HIPCHECK(e, hipMalloc(&tmp, n * sizeof(zb_exchange_rec)));
-    HIPCHECK(e, hipMemcpyAsync(tmp, src, n * sizeof(zb_exchange_rec), hipMemcpyHostToDevice, e->stream));
-    dsrc = tmp;
-  }
+  return process_messages(e, b);
+}
+
+int zb_expire_messages(zb_engine* e, int64_t now_ms, uint64_t* n_deleted) {
+  if (!e) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  if (n_deleted) *n_deleted = 0;
+  int rc = require_idle(e);
+  if (rc != ZB_OK) return rc;
+  if (!e->msgs || e->msg_count == 0) return ZB_OK;
+  rc = maintain(e, false);
+  if (rc != ZB_OK) return rc;
+  const uint64_t m = e->msg_count;
+  rc = grow(e, &e->c_flag, &e->c_flag_cap, m + 1);
+  if (rc == ZB_OK) rc = grow(e, &e->c_new, &e->c_new_cap, m + 1);
+  if (rc != ZB_OK) return rc;
   MsgParams p = msg_params(e);
-  p.in = dsrc;
-  p.n = (int64_t)n;
+  p.now = now_ms;
+  p.flags = e->c_flag;
+  launch_ttl_flags(p, e->stream);
+  uint64_t k = 0;
+  rc = scan_u32(e, e->c_flag, e->c_new, m, &k);
+  if (rc != ZB_OK) return rc;
+  if (k == 0) return ZB_OK;
+  const int64_t base = e->host_hdr.end;
+  if ((uint64_t)(base - e->win_base) + 2 * k > e->cfg.log_capacity) return fail(e, ZB_ENOMEM, "log capacity");
   p.base = base;
-  p.arena_base = (uint64_t)e->host_hdr.arena_next;
-  if (kind == ZB_XCHG_OPEN) {
-    launch_msg_open(p, e->stream);  // processed at once: OPEN commands + OPENED events
-    e->sub_count += n;
-    e->host_hdr.end = base + (int64_t)recs;
-    e->host_hdr.begin = e->host_hdr.gen_end = e->host_hdr.end;
-  } else {
-    // CORRELATE commands: the next zb_step processes them; the element instance each names is looked up by its
-    // activity instance key (ElementInstanceIndex.getInstance): keys sorted, then one pass over the rows
-    const uint64_t need = n;
-    if (need > e->x_cap) {
-      HIPCHECK(e, hipStreamSynchronize(e->stream));
-      void* xs[] = {e->x_keys, e->x_pos, e->x_keys2, e->x_pos2};
-      for (void* q : xs)
-        if (q) (void)hipFree(q);
-      e->x_keys = e->x_pos = e->x_keys2 = e->x_pos2 = nullptr;
-      e->x_cap = 0;
-      const uint64_t c = std::max<uint64_t>(need + need / 2, 1024);
-      HIPCHECK(e, hipMalloc(&e->x_keys, c * 8));
-      HIPCHECK(e, hipMalloc(&e->x_pos, c * 8));
-      HIPCHECK(e, hipMalloc(&e->x_keys2, c * 8));
-      HIPCHECK(e, hipMalloc(&e->x_pos2, c * 8));
-      e->x_cap = c;
+  p.flag_off = e->c_new;
+  launch_ttl_write(p, e->stream);  // the checker's DELETE commands at [base, base + k)
+  MsgParams d = msg_params(e);
+  d.base = base;
+  d.n = (int64_t)k;
+  d.out_base = base + (int64_t)k;
+  launch_msg_delete(d, e->stream);  // ... and their processing
+  e->host_hdr.end = base + 2 * (int64_t)k;
+  e->host_hdr.begin = e->host_hdr.gen_end = e->host_hdr.end;
+  e->records_total += 2 * k;
+  if (n_deleted) *n_deleted = k;
+  return finish_batch(e);
+}
+
+int zb_inbox_submit(zb_engine* e, int kind, const uint8_t* batches, size_t bytes, int on_device) {
+  if (!e || (bytes > 0 && !batches) || (kind != ZB_XCHG_OPEN && kind != ZB_XCHG_CORRELATE)) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  int rc = require_idle(e);
+  if (rc != ZB_OK) return rc;
+  if (bytes == 0) return ZB_OK;
+  std::vector<uint64_t> counts, offs;
+  if (on_device) {  // batch headers read one after another
+    size_t o = 0;
+    while (o < bytes) {
+      uint64_t h[2];
+      if (bytes - o < sizeof(h)) return fail(e, ZB_EINVAL, "malformed exchange batches");
+      HIPCHECK(e, hipMemcpy(h, batches + o, sizeof(h), hipMemcpyDeviceToHost));
+      if (h[1] < ZB_XCHG_BATCH_HEADER + h[0] * sizeof(zb_exchange_rec) || h[1] > bytes - o || (h[1] & 7))
+        return fail(e, ZB_EINVAL, "malformed exchange batches");
+      counts.push_back(h[0]);
+      offs.push_back(o);
+      o += h[1];
     }
-    if (n > (uint64_t)INT32_MAX) return fail(e, ZB_EUNSUPPORTED, "more than 2^31 delivered commands");
-    p.lookup_keys = e->x_keys;
-    p.lookup_pos = e->x_pos;
-    launch_wis_inject(p, e->stream);
-    size_t tmp = 0;
-    if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, e->x_keys, e->x_keys2, e->x_pos, e->x_pos2, (int)n, 0, 64,
-                                           e->stream) != hipSuccess)
-      return fail(e, ZB_EDEVICE, "inbox sort sizing");
-    if (tmp > e->x_tmp_cap) {
-      HIPCHECK(e, hipStreamSynchronize(e->stream));
-      if (e->x_tmp) (void)hipFree(e->x_tmp);
-      e->x_tmp = nullptr;
-      e->x_tmp_cap = 0;
-      HIPCHECK(e, hipMalloc(&e->x_tmp, tmp + 16));
-      e->x_tmp_cap = tmp;
-    }
-    tmp = e->x_tmp_cap;
-    if (hipcub::DeviceRadixSort::SortPairs(e->x_tmp, tmp, e->x_keys, e->x_keys2, e->x_pos, e->x_pos2, (int)n, 0, 64,
-                                           e->stream) != hipSuccess)
-      return fail(e, ZB_EDEVICE, "inbox sort");
-    ResolveParams rp{};
-    rp.rmeta = e->rmeta; rp.rkeys = e->rkeys; rp.rows = (uint64_t)e->host_hdr.rows_next;
-    rp.keys = e->x_keys2; rp.pos = e->x_pos2; rp.n = (int64_t)n;
-    rp.links = e->links;
-    launch_resolve(rp, e->stream);
-    e->host_hdr.end = base + (int64_t)recs;
-    e->host_hdr.gen_end = e->host_hdr.end;
+  } else if (!parse_batches(batches, bytes, counts, offs)) {
+    return fail(e, ZB_EINVAL, "malformed exchange batches");
   }
-  e->host_hdr.arena_next += (int64_t)(n * stride);
-  e->records_total += recs;
-  e->arena_total += n * stride;
-  rc = finish_batch(e);
-  if (tmp) (void)hipFree(tmp);
-  return rc;
+  rc = ensure_stores(e);
+  if (rc == ZB_OK) rc = maintain(e, false);
+  if (rc != ZB_OK) return rc;
+  const uint8_t* dbuf = batches;
+  if (!on_device) {
+    rc = grow_dev(e, &e->in_buf, &e->in_buf_cap, bytes);
+    if (rc != ZB_OK) return rc;
+    HIPCHECK(e, hipMemcpyAsync(e->in_buf, batches, bytes, hipMemcpyHostToDevice, e->stream));
+    dbuf = e->in_buf;
+  }
+  return deliver(e, kind, dbuf, counts, offs, nullptr);
 }
 
 int zb_outbox_count(zb_engine* e, int kind, uint64_t* n) {
@@ -2442,66 +2760,106 @@ int zb_outbox_count(zb_engine* e, int kind, uint64_t* n) {
   *n = 0;
   if (!e->on) return ZB_OK;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
-  uint32_t c = 0;
-  HIPCHECK(e, hipMemcpyAsync(&c, e->on + (kind - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  uint32_t c[4] = {0, 0, 0, 0};
+  HIPCHECK(e, hipMemcpyAsync(c, e->on, sizeof(c), hipMemcpyDeviceToHost, e->stream));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
-  *n = c;
+  if ((uint64_t)c[kind - 1] > e->ocap || (uint64_t)c[kind + 1] > e->ovar_cap)
+    return fail(e, ZB_ENOMEM, "outbox overflow (commands or their variable bytes)");
+  *n = c[kind - 1];
   return ZB_OK;
 }
 
-int zb_outbox_take(zb_engine* e, int kind, zb_exchange_rec* dst, size_t cap, int dst_on_device, uint64_t* counts,
-                   uint64_t* n_out) {
-  if (!e || !counts || !n_out || (kind != ZB_XCHG_OPEN && kind != ZB_XCHG_CORRELATE)) return ZB_EINVAL;
+}  // extern "C"
+
+namespace {
+// Sorts the outbox of `kind` and lays it out as one exchange batch per target (target order) at dst (device):
+// per-target byte sizes into bytes_per_target, *total = their sum. With dst == nullptr only the sizes are
+// computed (the outbox is left as it is).
+int outbox_pack(zb_engine* e, int kind, uint8_t* dst, uint64_t cap, uint64_t* bytes_per_target, uint64_t* counts,
+                uint64_t* n_out, uint64_t* total) {
   const int P = e->cfg.partition_count;
   if (P > 64) return fail(e, ZB_EUNSUPPORTED, "more than 64 partitions");
-  for (int q = 0; q < P; q++) counts[q] = 0;
+  for (int q = 0; q < P; q++) bytes_per_target[q] = counts[q] = 0;
+  *total = 0;
   uint64_t n = 0;
   int rc = zb_outbox_count(e, kind, &n);
   if (rc != ZB_OK) return rc;
   *n_out = n;
   if (n == 0) return ZB_OK;
-  if (n > cap || !dst) return fail(e, ZB_ENOMEM, "outbox destination too small");
-  if (n > e->ocap) return fail(e, ZB_ENOMEM, "outbox overflow");
   const int k = kind - 1;
-  // sort (key, index) pairs: target partition, source position, emission order; the sort buffers are
-  // allocated once, at the outbox capacity
-  if (!e->ob_keys) {
+  if (!e->ob_keys) {  // sort buffers, allocated once at the outbox capacity
     const uint64_t c = e->ocap;
     if (hipMalloc(&e->ob_keys, c * 8) != hipSuccess || hipMalloc(&e->ob_idx_in, c * 4) != hipSuccess ||
-        hipMalloc(&e->ob_idx_out, c * 4) != hipSuccess || hipMalloc(&e->ob_first, 65 * 8) != hipSuccess)
+        hipMalloc(&e->ob_idx_out, c * 4) != hipSuccess || hipMalloc(&e->ob_first, 65 * 8) != hipSuccess ||
+        hipMalloc(&e->ob_sizes, (c + 1) * 4) != hipSuccess || hipMalloc(&e->ob_goff, (c + 1) * 4) != hipSuccess ||
+        hipMalloc(&e->ob_table, 2 * 64 * 8) != hipSuccess || hipMalloc(&e->ob_base, 64 * 8) != hipSuccess)
       return fail(e, ZB_ENOMEM, "outbox sort buffers");
     if (hipcub::DeviceRadixSort::SortPairs(nullptr, e->ob_tmp_bytes, e->okeys[0], e->ob_keys, e->ob_idx_in,
-                                           e->ob_idx_out, (int)c, 0, 64, e->stream) != hipSuccess ||
-        hipMalloc(&e->ob_tmp, e->ob_tmp_bytes + 16) != hipSuccess)
+                                           e->ob_idx_out, (int)c, 0, 64, e->stream) != hipSuccess)
       return fail(e, ZB_ENOMEM, "outbox sort scratch");
+    size_t scan_bytes = 0;
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, e->ob_sizes, e->ob_goff, (int)(c + 1), e->stream) != hipSuccess)
+      return fail(e, ZB_ENOMEM, "outbox scan scratch");
+    e->ob_tmp_bytes = std::max(e->ob_tmp_bytes, scan_bytes);
+    if (hipMalloc(&e->ob_tmp, e->ob_tmp_bytes + 16) != hipSuccess) return fail(e, ZB_ENOMEM, "outbox sort scratch");
   }
   launch_iota(e->ob_idx_in, n, e->stream);
   size_t tmp_bytes = e->ob_tmp_bytes;
   if (hipcub::DeviceRadixSort::SortPairs(e->ob_tmp, tmp_bytes, e->okeys[k], e->ob_keys, e->ob_idx_in, e->ob_idx_out,
                                          (int)n, 0, 64, e->stream) != hipSuccess)
     return fail(e, ZB_EDEVICE, "outbox sort");
-  zb_exchange_rec* out = dst;
+  const Outbox ob = outbox(e, kind);
+  launch_outbox_sizes(ob, e->ob_idx_out, n, e->ob_sizes, e->stream);
+  tmp_bytes = e->ob_tmp_bytes;
+  if (hipcub::DeviceScan::ExclusiveSum(e->ob_tmp, tmp_bytes, e->ob_sizes, e->ob_goff, (int)(n + 1), e->stream) != hipSuccess)
+    return fail(e, ZB_EDEVICE, "outbox scan");
+  launch_outbox_bounds(e->ob_keys, n, e->ob_first, P, e->stream);
+  launch_outbox_table(e->ob_first, e->ob_goff, P, e->ob_table, e->stream);
+  uint64_t table[128];
+  HIPCHECK(e, hipMemcpyAsync(table, e->ob_table, 2 * P * 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  uint64_t base[64], o = 0;
+  for (int q = 0; q < P; q++) {
+    counts[q] = table[2 * q];
+    bytes_per_target[q] = counts[q] ? ZB_XCHG_BATCH_HEADER + counts[q] * sizeof(zb_exchange_rec) + 8 * table[2 * q + 1] : 0;
+    base[q] = o;
+    o += bytes_per_target[q];
+  }
+  *total = o;
+  if (!dst) return ZB_OK;
+  if (o > cap) return fail(e, ZB_ENOMEM, "outbox destination too small");
+  HIPCHECK(e, hipMemcpyAsync(e->ob_base, base, P * 8, hipMemcpyHostToDevice, e->stream));
+  launch_outbox_pack(ob, e->ob_idx_out, e->ob_keys, n, e->ob_first, e->ob_goff, e->ob_base, dst, e->stream);
+  HIPCHECK(e, hipMemsetAsync(e->on + k, 0, sizeof(uint32_t), e->stream));      // the outbox is taken
+  HIPCHECK(e, hipMemsetAsync(e->on + 2 + k, 0, sizeof(uint32_t), e->stream));  // (and its byte section)
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  return ZB_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int zb_outbox_take(zb_engine* e, int kind, uint8_t* dst, size_t cap, int dst_on_device, uint64_t* bytes_per_target,
+                   uint64_t* n_out, uint64_t* total) {
+  if (!e || !bytes_per_target || !n_out || !total || (kind != ZB_XCHG_OPEN && kind != ZB_XCHG_CORRELATE))
+    return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  uint64_t counts[64];
+  int rc = outbox_pack(e, kind, nullptr, 0, bytes_per_target, counts, n_out, total);  // sizes only
+  if (rc != ZB_OK || *n_out == 0) return rc;
+  if (!dst || cap < *total) return ZB_ENOMEM;
+  uint8_t* out = dst;
   if (!dst_on_device) {
-    if (n > e->ob_staging_cap) {
-      if (e->ob_staging) (void)hipFree(e->ob_staging);
-      e->ob_staging = nullptr;
-      e->ob_staging_cap = 0;
-      const uint64_t c = std::max<uint64_t>(n, 2 * e->ob_staging_cap);
-      if (hipMalloc(&e->ob_staging, c * sizeof(zb_exchange_rec)) != hipSuccess) return fail(e, ZB_ENOMEM, "outbox staging");
-      e->ob_staging_cap = c;
-    }
+    rc = grow_dev(e, &e->ob_staging, &e->ob_staging_cap, *total);
+    if (rc != ZB_OK) return rc;
     out = e->ob_staging;
   }
-  launch_outbox_gather(e->obox[k], e->ob_idx_out, out, n, e->stream);
-  launch_outbox_bounds(e->ob_keys, n, e->ob_first, P, e->stream);
-  std::vector<uint64_t> h_first(P, 0);
-  if (hipMemcpyAsync(h_first.data(), e->ob_first, P * 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
-      (!dst_on_device && hipMemcpyAsync(dst, e->ob_staging, n * sizeof(zb_exchange_rec), hipMemcpyDeviceToHost,
-                                        e->stream) != hipSuccess) ||
-      hipMemsetAsync(e->on + k, 0, sizeof(uint32_t), e->stream) != hipSuccess ||
-      hipStreamSynchronize(e->stream) != hipSuccess)
-    return fail(e, ZB_EDEVICE, "outbox copy");
-  for (int q = 0; q < P; q++) counts[q] = (q + 1 < P ? h_first[q + 1] : n) - h_first[q];
+  rc = outbox_pack(e, kind, out, dst_on_device ? cap : e->ob_staging_cap, bytes_per_target, counts, n_out, total);
+  if (rc != ZB_OK) return rc;
+  if (!dst_on_device) {
+    HIPCHECK(e, hipMemcpyAsync(dst, e->ob_staging, *total, hipMemcpyDeviceToHost, e->stream));
+    HIPCHECK(e, hipStreamSynchronize(e->stream));
+  }
   return ZB_OK;
 }
 
@@ -2526,16 +2884,16 @@ int zb_comm_init(zb_engine* e, const uint8_t id[128], int nranks, int rank) {
   std::memcpy(&u, id, sizeof(u));
   NCCLCHECK(e, ncclCommInitRank(&e->comm, nranks, u, rank));
   e->comm_broken = false;
-  HIPCHECK(e, hipMalloc(&e->d_xcounts, 4 * 64 * sizeof(uint64_t)));
+  HIPCHECK(e, hipMalloc(&e->d_xcounts, 8 * 64 * sizeof(uint64_t)));
   int rc = ensure_outbox(e);
   if (rc != ZB_OK) return rc;
   // exchange buffers for the common case up front (grown later only if a round needs more)
-  const uint64_t c = std::min<uint64_t>(e->ocap, 1ull << 16);
-  HIPCHECK(e, hipMalloc(&e->xsend, c * sizeof(zb_exchange_rec)));
-  HIPCHECK(e, hipMalloc(&e->xrecv, c * sizeof(zb_exchange_rec)));
-  e->xsend_cap = e->xrecv_cap = c;
-  return ZB_OK;
+  rc = grow_dev(e, &e->xsend, &e->xsend_cap, 16ull << 20);
+  if (rc == ZB_OK) rc = grow_dev(e, &e->xrecv, &e->xrecv_cap, 16ull << 20);
+  return rc;
 }
+
+}  // extern "C"
 
 namespace {
 // an RCCL failure leaves the communicator unusable (peers may be inside the same collective): abort it so
@@ -2546,18 +2904,9 @@ int comm_fail(zb_engine* e, const std::string& what, ncclResult_t r) {
   e->comm = nullptr;
   return fail(e, ZB_EDEVICE, what + ": " + ncclGetErrorString(r));
 }
-// grows a persistent exchange buffer to hold n records (local: the caller agrees on the outcome with its peers)
-int grow_xbuf(zb_exchange_rec** p, uint64_t* cap, uint64_t n) {
-  if (n <= *cap) return ZB_OK;
-  if (*p) (void)hipFree(*p);
-  *p = nullptr;
-  *cap = 0;
-  const uint64_t c = std::max<uint64_t>(n, 1024) + n / 2;
-  if (hipMalloc(p, c * sizeof(zb_exchange_rec)) != hipSuccess) return ZB_ENOMEM;
-  *cap = c;
-  return ZB_OK;
-}
 }  // namespace
+
+extern "C" {
 
 int zb_comm_pending(zb_engine* e, uint64_t global[2]) {
   if (!e || !global) return ZB_EINVAL;
@@ -2577,56 +2926,58 @@ int zb_comm_pending(zb_engine* e, uint64_t global[2]) {
 }
 
 // Collective on every rank, whatever happens locally: a rank whose local work fails still takes part in
-// both agreement steps (sending zero counts and its status), so every rank returns the same error instead
-// of one rank leaving the collective and its peers blocking in ncclSend / ncclRecv.
+// both agreement steps (sending zero sizes and its status), so every rank returns the same error instead
+// of one rank leaving the collective and its peers blocking in ncclSend / ncclRecv. ZB_FAIL_EXCHANGE=<rank>
+// (tests) makes that rank's local step fail.
 int zb_comm_exchange(zb_engine* e, int kind, uint64_t* received) {
   if (!e || !received || (kind != ZB_XCHG_OPEN && kind != ZB_XCHG_CORRELATE)) return ZB_EINVAL;
   if (!e->comm) return e->comm_broken ? fail(e, ZB_EDEVICE, "communicator aborted after an earlier failure") : ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
   const int P = e->cfg.partition_count;
   *received = 0;
-  // 0. local: take the outbox (sorted by target) into the persistent send buffer
-  std::vector<uint64_t> sc(P, 0), rcv(P, 0);
-  uint64_t n = 0;
-  int local = zb_outbox_count(e, kind, &n);
-  if (local == ZB_OK) local = grow_xbuf(&e->xsend, &e->xsend_cap, n);
-  if (local == ZB_OK) {
-    uint64_t got = 0;
-    local = zb_outbox_take(e, kind, e->xsend, e->xsend_cap, 1, sc.data(), &got);
-  }
-  if (local != ZB_OK) std::fill(sc.begin(), sc.end(), 0);
+  // 0. local: the outbox as one batch per target into the persistent send buffer
+  uint64_t sb[64] = {}, sc[64] = {}, n = 0, total = 0;
+  int local = ZB_OK;
+  if (const char* f = std::getenv("ZB_FAIL_EXCHANGE"))  // (before the outbox is taken: a retry still has it)
+    if (*f && atoi(f) == e->cfg.partition_id) local = fail(e, ZB_EDEVICE, "injected local failure (ZB_FAIL_EXCHANGE)");
+  if (local == ZB_OK) local = outbox_pack(e, kind, nullptr, 0, sb, sc, &n, &total);
+  if (local == ZB_OK && n) local = grow_dev(e, &e->xsend, &e->xsend_cap, total);
+  if (local == ZB_OK && n) local = outbox_pack(e, kind, e->xsend, e->xsend_cap, sb, sc, &n, &total);
+  if (local != ZB_OK) for (int q = 0; q < P; q++) sb[q] = sc[q] = 0;
   const std::string local_err = local != ZB_OK ? e->err : std::string();
-  // 1. agreement + counts: every rank sends every peer (count for it, its status); always posted
-  std::vector<uint64_t> pairs(2 * 64, 0);
-  for (int q = 0; q < P; q++) { pairs[2 * q] = sc[q]; pairs[2 * q + 1] = (uint64_t)(uint32_t)local; }
-  if (hipMemcpyAsync(e->d_xcounts, pairs.data(), 2 * P * 8, hipMemcpyHostToDevice, e->stream) != hipSuccess)
-    local = local != ZB_OK ? local : ZB_EDEVICE;  // the pairs may be stale: the status still travels below
+  // 1. agreement + sizes: every rank sends every peer (bytes, commands, status) for it; always posted
+  std::vector<uint64_t> tri(4 * 64, 0);
+  for (int q = 0; q < P; q++) { tri[4 * q] = sb[q]; tri[4 * q + 1] = sc[q]; tri[4 * q + 2] = (uint64_t)(uint32_t)local; }
+  if (hipMemcpyAsync(e->d_xcounts, tri.data(), 4 * P * 8, hipMemcpyHostToDevice, e->stream) != hipSuccess)
+    local = local != ZB_OK ? local : ZB_EDEVICE;  // the sizes may be stale: the status still travels below
   ncclResult_t nr = ncclGroupStart();
   for (int q = 0; q < P && nr == ncclSuccess; q++) {
-    nr = ncclSend(e->d_xcounts + 2 * q, 2, ncclUint64, q, e->comm, e->stream);
-    if (nr == ncclSuccess) nr = ncclRecv(e->d_xcounts + 128 + 2 * q, 2, ncclUint64, q, e->comm, e->stream);
+    nr = ncclSend(e->d_xcounts + 4 * q, 4, ncclUint64, q, e->comm, e->stream);
+    if (nr == ncclSuccess) nr = ncclRecv(e->d_xcounts + 256 + 4 * q, 4, ncclUint64, q, e->comm, e->stream);
   }
   if (nr == ncclSuccess) nr = ncclGroupEnd();
-  if (nr != ncclSuccess) return comm_fail(e, "exchange counts", nr);
-  std::vector<uint64_t> rpairs(2 * 64, 0);
-  if (hipMemcpyAsync(rpairs.data(), e->d_xcounts + 128, 2 * P * 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+  if (nr != ncclSuccess) return comm_fail(e, "exchange sizes", nr);
+  std::vector<uint64_t> rtri(4 * 64, 0);
+  if (hipMemcpyAsync(rtri.data(), e->d_xcounts + 256, 4 * P * 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
       hipStreamSynchronize(e->stream) != hipSuccess)
-    return comm_fail(e, "exchange counts download", ncclSystemError);
+    return comm_fail(e, "exchange sizes download", ncclSystemError);
   int peer_failed = -1;
-  uint64_t total = 0;
+  uint64_t rbytes = 0;
+  std::vector<uint64_t> rcounts(P), roffs(P);
   for (int q = 0; q < P; q++) {
-    rcv[q] = rpairs[2 * q];
-    if (rpairs[2 * q + 1] != 0 && peer_failed < 0) peer_failed = q;
-    total += rcv[q];
+    roffs[q] = rbytes;
+    rcounts[q] = rtri[4 * q + 1];
+    rbytes += rtri[4 * q];
+    if (rtri[4 * q + 2] != 0 && peer_failed < 0) peer_failed = q;
   }
-  // 2. the receive side may fail locally too: agree once more (max of the statuses) before any record moves
-  if (peer_failed < 0 && local == ZB_OK) local = grow_xbuf(&e->xrecv, &e->xrecv_cap, total);
+  // 2. the receive side may fail locally too: agree once more (max of the statuses) before any byte moves
+  if (peer_failed < 0 && local == ZB_OK && rbytes) local = grow_dev(e, &e->xrecv, &e->xrecv_cap, rbytes);
   uint64_t st = (local != ZB_OK || peer_failed >= 0) ? 1 : 0;
-  if (hipMemcpyAsync(e->d_xcounts + 192, &st, 8, hipMemcpyHostToDevice, e->stream) != hipSuccess)
+  if (hipMemcpyAsync(e->d_xcounts + 448, &st, 8, hipMemcpyHostToDevice, e->stream) != hipSuccess)
     return comm_fail(e, "exchange status upload", ncclSystemError);
-  nr = ncclAllReduce(e->d_xcounts + 192, e->d_xcounts + 192, 1, ncclUint64, ncclMax, e->comm, e->stream);
+  nr = ncclAllReduce(e->d_xcounts + 448, e->d_xcounts + 448, 1, ncclUint64, ncclMax, e->comm, e->stream);
   if (nr != ncclSuccess) return comm_fail(e, "exchange status", nr);
-  if (hipMemcpyAsync(&st, e->d_xcounts + 192, 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+  if (hipMemcpyAsync(&st, e->d_xcounts + 448, 8, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
       hipStreamSynchronize(e->stream) != hipSuccess)
     return comm_fail(e, "exchange status download", ncclSystemError);
   if (st != 0) {
@@ -2635,21 +2986,25 @@ int zb_comm_exchange(zb_engine* e, int kind, uint64_t* received) {
       return fail(e, ZB_EDEVICE, "exchange: partition " + std::to_string(peer_failed) + " failed locally");
     return fail(e, ZB_EDEVICE, "exchange: a peer failed to size its receive buffer");
   }
-  // 3. records: slices by target out, by source in (source-rank order = canonical delivery order)
+  // 3. batches: one per (source, target) pair; received in source-rank order = canonical delivery order
   nr = ncclGroupStart();
-  uint64_t so = 0, ro = 0;
+  uint64_t so = 0;
   for (int q = 0; q < P && nr == ncclSuccess; q++) {
-    if (sc[q]) nr = ncclSend(e->xsend + so, sc[q] * sizeof(zb_exchange_rec), ncclUint8, q, e->comm, e->stream);
-    if (nr == ncclSuccess && rcv[q]) nr = ncclRecv(e->xrecv + ro, rcv[q] * sizeof(zb_exchange_rec), ncclUint8, q, e->comm, e->stream);
-    so += sc[q];
-    ro += rcv[q];
+    if (sb[q]) nr = ncclSend(e->xsend + so, sb[q], ncclUint8, q, e->comm, e->stream);
+    if (nr == ncclSuccess && rtri[4 * q]) nr = ncclRecv(e->xrecv + roffs[q], rtri[4 * q], ncclUint8, q, e->comm, e->stream);
+    so += sb[q];
   }
   if (nr == ncclSuccess) nr = ncclGroupEnd();
   if (nr != ncclSuccess) return comm_fail(e, "exchange records", nr);
   if (hipStreamSynchronize(e->stream) != hipSuccess) return comm_fail(e, "exchange sync", ncclSystemError);
   // 4. delivery is local (no further collective in this call)
-  int rc = total ? zb_inbox_submit(e, kind, e->xrecv, total, 1) : ZB_OK;
-  if (rc == ZB_OK) *received = total;
+  int rc = ZB_OK;
+  if (rbytes) {
+    rc = require_idle(e);
+    if (rc == ZB_OK) rc = ensure_stores(e);
+    if (rc == ZB_OK) rc = maintain(e, false);
+    if (rc == ZB_OK) rc = deliver(e, kind, e->xrecv, rcounts, roffs, received);
+  }
   return rc;
 }
 

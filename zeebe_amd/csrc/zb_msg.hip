@@ -1,21 +1,26 @@
-// zb_msg.hip — the message side of correlation and the partition
-// exchange (zb_exchange_rec, include/zb_engine.h).
+// zb_msg.hip — the message stream processor (MessageService.java:90-129) and
+// the partition exchange (zb_exchange_rec batches, include/zb_engine.h).
 //
-//   k_msg_open      MESSAGE_SUBSCRIPTION OPEN commands delivered by workflow partitions: append the
-//                   command (key = its log position) and its OPENED event, look for a stored message
-//                   (MessageDataStore.findMessage: the first one stored), insert the subscription
+//   k_msg_open      MESSAGE_SUBSCRIPTION OPEN commands delivered by workflow partitions: append the command
+//                   (key = its log position) and its OPENED event, look for a stored message
+//                   (MessageDataStore.findMessage: the first stored one), insert the subscription
 //                   (MessageSubscriptionDataStore.addSubscription) — OpenMessageSubscriptionProcessor.java:56-92
-//   k_msg_publish   MESSAGE PUBLISH commands: PUBLISHED (+ DELETED when ttl <= 0) keyed by the message
-//                   KeyGenerator(0, 1) (MessageService.java:91); every matching subscription becomes a
-//                   correlate command in the outbox; the message is stored when ttl > 0
-//                   — PublishMessageProcessor.java:58-124
+//   k_pub_count     a run of PUBLISH commands, per command: rejected (a message with its id, name and correlation
+//                   key is stored: MessageDataStore.hasMessage) or accepted; records written; stored
+//   k_pub_emit      PublishMessageProcessor.java:58-124 at the scanned offsets: the rejection (BAD_VALUE), or
+//                   PUBLISHED (+ DELETED when ttl <= 0) keyed by the message KeyGenerator(0, 1), a correlate command
+//                   per matching subscription (findSubscriptions, insertion order), the message stored when ttl > 0
+//   k_msg_delete    a run of DELETE commands: DELETED, the message removed (DeleteMessageProcessor.java:36-45)
+//   k_ttl_flags / k_ttl_write   MessageTimeToLiveChecker.run (:44-68): a DELETE command per stored message whose
+//                   deadline has passed, in store order
 //   k_wis_inject    CORRELATE commands delivered by message partitions -> WORKFLOW_INSTANCE_SUBSCRIPTION
 //                   CORRELATE commands at the log tail (processed by the wave pipeline, zb_wave.hip)
-//   k_outbox_gather / k_outbox_bounds   the outbox sorted by (target, source position, emission)
+//   k_outbox_*      the outbox sorted by (target, source position, emission) into one exchange batch per target
 //
-// The stores are hash tables of chains pushed lock-free (atomicExch on the bucket head) over
-// insertion-indexed entry arrays. The reference scans insertion-ordered lists; the entries carry
-// their log positions, and the outbox is sorted, so the order of any chain walk never shows.
+// The stores are hash tables of chains pushed lock-free (atomicExch on the bucket head) over insertion-indexed
+// entry arrays. The reference scans insertion-ordered lists; entries carry their log positions / insertion
+// indices and the outbox is sorted, so the order of a chain walk never shows. Stored messages are in key order
+// (keys are handed out in command order), so DELETE finds its message by binary search.
 #include <hip/hip_runtime.h>
 
 #include "zb_devlib.hpp"
@@ -30,181 +35,268 @@ __device__ __forceinline__ bool bytes_equal(const uint8_t* a, const uint8_t* b, 
   return true;
 }
 
-// message blob: [u32 len][i64 ttl][u16 name_len][u16 ck_len][u32 payload_len][name][ck][payload]
-struct MsgView {
-  int64_t ttl;
-  const uint8_t *name, *ck, *payload;
-  uint32_t nn, nc, np;
-};
-__device__ __forceinline__ MsgView msg_view(const uint8_t* arena, uint32_t ref) {
-  const uint8_t* b = arena + (uint64_t)ref * 8 + 4;
-  MsgView v;
-  v.ttl = *(const int64_t*)b;
-  v.nn = *(const uint16_t*)(b + 8);
-  v.nc = *(const uint16_t*)(b + 10);
-  v.np = *(const uint32_t*)(b + 12);
-  v.name = b + 16;
-  v.ck = v.name + v.nn;
-  v.payload = v.ck + v.nc;
-  return v;
+__device__ __forceinline__ void put_record(const MsgParams& P, int64_t pos, const zb_rec& d, uint32_t srcd) {
+  P.log[pos] = d;
+  P.links[pos] = ~0ull;
+  P.srcd[pos] = srcd;
+  P.vlen[pos] = VLEN_UNKNOWN;
 }
 
-__device__ __forceinline__ void write_xchg(zb_exchange_rec* dst, int32_t kind, int32_t target, int32_t wfp, uint32_t token,
-                                           int64_t wik, int64_t aik, int64_t spos, uint16_t elem, const uint8_t* name,
-                                           uint32_t nn, const uint8_t* ck, uint32_t nc, const uint8_t* payload, uint32_t np) {
-  zb_exchange_rec r;
-  r.kind = kind; r.target_partition = target; r.wf_partition = wfp; r.token = token;
-  r.workflow_instance_key = wik; r.activity_instance_key = aik; r.source_position = spos;
-  r.elem = elem; r.name_len = (uint8_t)nn; r.ck_len = (uint8_t)nc; r.payload_len = (uint16_t)np; r.pad = 0;
-  for (uint32_t i = 0; i < ZB_XCHG_NAME_MAX; i++) r.name[i] = i < nn ? name[i] : 0;
-  for (uint32_t i = 0; i < ZB_XCHG_CK_MAX; i++) r.ck[i] = i < nc ? ck[i] : 0;
-  for (uint32_t i = 0; i < ZB_XCHG_PAYLOAD_MAX; i++) r.payload[i] = i < np ? payload[i] : 0;
-  *dst = r;
+// an arena blob of `len` bytes after its length word, allocated on the wave header's bump pointer
+__device__ __forceinline__ uint8_t* alloc_blob(const MsgParams& P, uint32_t len, uint32_t& ref, uint32_t& err) {
+  const uint64_t bytes = (4 + (uint64_t)len + 7) & ~7ull;
+  const uint64_t at = atomicAdd((unsigned long long*)&P.hdr->arena_next, (unsigned long long)bytes);
+  if (at + bytes > P.arena_cap) {
+    err |= DE_ARENA_FULL;
+    return nullptr;
+  }
+  uint8_t* b = P.arena + at;
+  *(uint32_t*)b = len;
+  for (uint64_t k = 4 + len; k < bytes; k++) b[k] = 0;
+  ref = (uint32_t)(at >> 3);
+  return b;
+}
+
+// command i of the delivered batches: its header and its variable bytes
+__device__ __forceinline__ zb_exchange_rec delivered(const MsgParams& P, int64_t i, const uint8_t*& var) {
+  int lo = 0, hi = P.nslices - 1;
+  while (lo < hi) {  // last batch whose first command is <= i
+    const int mid = (lo + hi + 1) >> 1;
+    if ((int64_t)P.slice_first[mid] <= i) lo = mid;
+    else hi = mid - 1;
+  }
+  const uint8_t* bat = P.in + P.slice_off[lo];
+  const uint64_t cnt = *(const uint64_t*)bat;
+  const zb_exchange_rec r = ((const zb_exchange_rec*)(bat + ZB_XCHG_BATCH_HEADER))[i - (int64_t)P.slice_first[lo]];
+  var = bat + ZB_XCHG_BATCH_HEADER + cnt * sizeof(zb_exchange_rec) + r.var_offset;
+  return r;
+}
+
+__device__ __forceinline__ void flag_error(const MsgParams& P, uint32_t err) {
+  if (err) atomicOr(P.err, err);
 }
 
 // ------------------------------------------------------------------------------ OPEN
 __global__ void __launch_bounds__(256) k_msg_open(MsgParams P) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool act = i < P.n;
-  zb_exchange_rec r;
-  uint32_t ncorr = 0, best_blob = 0;
+  uint32_t err = 0, ncorr = 0, best_blob = 0, gran = 0;
   uint64_t h = 0;
-  int64_t pos = P.base + i;
+  const int64_t pos = P.base + i;
+  zb_exchange_rec r{};
+  const uint8_t* var = nullptr;
+  uint32_t sref = 0;
   if (act) {
-    r = P.in[i];
-    // subscription blob (the serializer reads wfp / name / ck from it)
-    const uint64_t at = P.arena_base + (uint64_t)i * SUB_BLOB;
-    uint8_t* b = P.arena + at;
-    *(uint32_t*)b = SUB_BLOB - 4;
-    *(int32_t*)(b + 4) = r.wf_partition;
-    b[8] = r.name_len; b[9] = r.ck_len;
-    *(uint16_t*)(b + 10) = r.elem;
-    *(uint32_t*)(b + 12) = r.token;
-    for (int k = 0; k < ZB_XCHG_NAME_MAX; k++) b[16 + k] = r.name[k];
-    for (int k = 0; k < ZB_XCHG_CK_MAX; k++) b[64 + k] = r.ck[k];
-    const uint32_t ref = (uint32_t)(at >> 3);
+    r = delivered(P, i, var);
+    const uint8_t* name = var;
+    const uint8_t* ck = var + r.name_len;
+    // the subscription blob (the serializer and the store read wf partition / name / correlation key from it)
+    uint8_t* b = alloc_blob(P, SUB_HDR - 4 + r.name_len + r.ck_len, sref, err);
+    if (b) {
+      *(int32_t*)(b + 4) = r.wf_partition;
+      *(uint32_t*)(b + 8) = r.token;
+      *(uint16_t*)(b + 12) = r.elem;
+      *(uint16_t*)(b + 14) = 0;
+      *(uint32_t*)(b + 16) = r.name_len;
+      *(uint32_t*)(b + 20) = r.ck_len;
+      copy_bytes(b + SUB_HDR, name, r.name_len);
+      copy_bytes(b + SUB_HDR + r.name_len, ck, r.ck_len);
+    }
     zb_rec d;
     d.key = pos;  // positionAsKey (SubscriptionApiCommandMessageHandler.java:144-149)
     d.scope_key = r.activity_instance_key;
     d.inst_key = r.workflow_instance_key;
-    d.payload = ref;
+    d.payload = sref;
     d.elem = r.elem;
     d.intent = 0;  // OPEN
     d.kind = make_kind(ZB_VT_MESSAGE_SUBSCRIPTION, ZB_RT_COMMAND, false);
-    P.log[pos] = d;
-    P.links[pos] = ~0ull;
-    P.srcd[pos] = 0;  // delivered from another partition
-    P.vlen[pos] = VLEN_UNKNOWN;
+    put_record(P, pos, d, 0);  // delivered from another partition
     d.intent = 1;  // OPENED: writeFollowUpEvent(record.getKey(), OPENED, subscriptionRecord)
     d.kind = make_kind(ZB_VT_MESSAGE_SUBSCRIPTION, ZB_RT_EVENT, false);
-    P.log[pos + P.n] = d;
-    P.links[pos + P.n] = ~0ull;
-    P.srcd[pos + P.n] = (uint32_t)P.n;
-    P.vlen[pos + P.n] = VLEN_UNKNOWN;
+    put_record(P, pos + P.n, d, (uint32_t)P.n);
     // MessageDataStore.findMessage(name, correlationKey): the first stored message that matches
-    h = name_ck_hash(r.name, r.name_len, r.ck, r.ck_len);
+    h = name_ck_hash(name, r.name_len, ck, r.ck_len);
     int64_t best = -1;
     if (P.msg_cap) {
       for (uint32_t e = P.msg_head[h & P.msg_mask]; e != NO_ENTRY; e = P.msg_next[e]) {
         const MsgEntry m = P.msgs[e];
         if (m.h != h || m.dead) continue;
         const MsgView v = msg_view(P.arena, m.blob);
-        if (v.nn != r.name_len || v.nc != r.ck_len || !bytes_equal(v.name, r.name, v.nn) ||
-            !bytes_equal(v.ck, r.ck, v.nc))
+        if (v.nn != r.name_len || v.nc != r.ck_len || !bytes_equal(v.name, name, v.nn) || !bytes_equal(v.ck, ck, v.nc))
           continue;
         if (best < 0 || m.pos < best) { best = m.pos; best_blob = m.blob; }
       }
     }
-    ncorr = best >= 0 ? 1 : 0;
-  }
-  const uint32_t slot = wave_alloc(P.on, ncorr);
-  if (act && ncorr) {
-    const MsgView v = msg_view(P.arena, best_blob);
-    if (slot >= P.ocap) atomicOr(P.err, (uint32_t)DE_LOG_FULL);
-    else if (v.np > ZB_XCHG_PAYLOAD_MAX) atomicOr(P.err, (uint32_t)DE_UNSUPPORTED);
-    else {
-      write_xchg(P.obox + slot, ZB_XCHG_CORRELATE, r.wf_partition, r.wf_partition, r.token, r.workflow_instance_key,
-                 r.activity_instance_key, pos, r.elem, r.name, r.name_len, nullptr, 0, v.payload, v.np);
-      P.okeys[slot] = outbox_key(r.wf_partition, pos, 0);
+    if (best >= 0) {
+      ncorr = 1;
+      gran = var_granules(r.name_len, 0, msg_view(P.arena, best_blob).np);
     }
   }
-  if (act) {
-    // MessageSubscriptionDataStore.addSubscription
+  const uint32_t slot = wave_alloc(P.ob.n, ncorr);
+  const uint32_t vat = wave_alloc(P.ob.var_n, gran);
+  if (act && ncorr) {
+    const MsgView v = msg_view(P.arena, best_blob);
+    if (slot >= P.ob.cap || (uint64_t)vat + gran > P.ob.var_cap) err |= DE_LOG_FULL;
+    else
+      outbox_write(P.ob, slot, vat, ZB_XCHG_CORRELATE, r.wf_partition, r.wf_partition, r.token, r.workflow_instance_key,
+                   r.activity_instance_key, pos, r.elem, var, r.name_len, nullptr, 0, v.payload, v.np, 0);
+  }
+  if (act) {  // MessageSubscriptionDataStore.addSubscription
     const uint32_t idx = (uint32_t)(P.sub_count + i);
     SubEntry s;
-    s.h = h; s.wik = r.workflow_instance_key; s.aik = r.activity_instance_key; s.pos = pos;
-    s.blob = (uint32_t)((P.arena_base + (uint64_t)i * SUB_BLOB) >> 3);
-    s.idx = idx;
+    s.h = h; s.wik = r.workflow_instance_key; s.aik = r.activity_instance_key; s.pos = pos; s.blob = sref; s.idx = idx;
     P.subs[idx] = s;
     P.sub_next[idx] = atomicExch(&P.sub_head[h & P.sub_mask], idx);
   }
+  flag_error(P, err);
 }
 
 // ------------------------------------------------------------------------------ PUBLISH
-// Publish i of the batch: command at base + i; uniform ttl, so its follow-ups are at
-// base + n + i * per (per = 1 PUBLISHED, or 2 with DELETED) and its key is key_base + i.
-__global__ void __launch_bounds__(256) k_msg_publish(MsgParams P) {
+// per command: [20:0] records written, [41:21] accepted (a message key), [62:42] stored (ttl > 0)
+constexpr int PC_ACC = 21, PC_STORED = 42;
+constexpr uint64_t PC_MASK = (1ull << 21) - 1;
+
+__global__ void __launch_bounds__(256) k_pub_count(MsgParams P) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P.n) return;
+  const zb_rec d = P.log[P.base + i];
+  const MsgView v = msg_view(P.arena, d.payload);
+  bool rejected = false;
+  if (v.nid) {  // messageRecord.hasMessageId() && messageStore.hasMessage(message) (PublishMessageProcessor :77-84)
+    rejected = P.prior[i] != 0;
+    if (!rejected && P.msg_cap) {
+      const uint64_t h = name_ck_hash(v.name, v.nn, v.ck, v.nc);
+      for (uint32_t e = P.msg_head[h & P.msg_mask]; e != NO_ENTRY && !rejected; e = P.msg_next[e]) {
+        const MsgEntry m = P.msgs[e];
+        if (m.h != h || m.dead) continue;
+        const MsgView s = msg_view(P.arena, m.blob);
+        rejected = s.nid == v.nid && s.nn == v.nn && s.nc == v.nc && bytes_equal(s.id, v.id, v.nid) &&
+                   bytes_equal(s.name, v.name, v.nn) && bytes_equal(s.ck, v.ck, v.nc);
+      }
+    }
+  }
+  const uint64_t out = rejected ? 1 : (v.ttl > 0 ? 1 : 2);
+  const uint64_t acc = rejected ? 0 : 1, stored = (!rejected && v.ttl > 0) ? 1 : 0;
+  P.cnt[i] = out | (acc << PC_ACC) | (stored << PC_STORED);
+}
+
+__device__ __forceinline__ bool sub_matches(const SubView& sb, const MsgView& v) {
+  return sb.nn == v.nn && sb.nc == v.nc && bytes_equal(sb.name, v.name, v.nn) && bytes_equal(sb.ck, v.ck, v.nc);
+}
+
+__global__ void __launch_bounds__(256) k_pub_emit(MsgParams P) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool act = i < P.n;
   const int64_t pos = P.base + i;
-  uint32_t ref = 0, nmatch = 0;
+  uint32_t err = 0, nmatch = 0, gran = 0;
   uint64_t h = 0;
+  zb_rec d{};
   MsgView v{};
+  bool acc = false;
+  uint64_t off = 0;
   if (act) {
-    zb_rec d = P.log[pos];  // injected PUBLISH command (payload = message blob)
-    ref = d.payload;
-    v = msg_view(P.arena, ref);
-    h = name_ck_hash(v.name, v.nn, v.ck, v.nc);
-    const int per = P.ttl > 0 ? 1 : 2;
-    const int64_t key = P.key_base + i;
-    const int64_t fpos = P.base + P.n + i * per;
-    d.key = key;
-    d.intent = 1;  // PUBLISHED (batchWriter.addNewEvent)
-    d.kind = make_kind(ZB_VT_MESSAGE, ZB_RT_EVENT, false);
-    P.log[fpos] = d;
-    P.links[fpos] = ~0ull;
-    P.srcd[fpos] = (uint32_t)(fpos - pos);
-    P.vlen[fpos] = VLEN_UNKNOWN;
-    if (per == 2) {  // ttl <= 0: addFollowUpEvent(key, DELETED, messageRecord)
-      d.intent = 3;
-      d.kind = make_kind(ZB_VT_MESSAGE, ZB_RT_EVENT, true);
-      P.log[fpos + 1] = d;
-      P.links[fpos + 1] = ~0ull;
-      P.srcd[fpos + 1] = (uint32_t)(fpos + 1 - pos);
-      P.vlen[fpos + 1] = VLEN_UNKNOWN;
+    d = P.log[pos];
+    v = msg_view(P.arena, d.payload);
+    acc = (P.cnt[i] >> PC_ACC) & 1;
+    off = P.cnt_off[i];
+    const int64_t fpos = P.out_base + (int64_t)(off & PC_MASK);
+    zb_rec f = d;  // follow-ups re-encode record.getValue(): the message blob, not the verbatim command value
+    if (!acc) {  // writeRejection(record, BAD_VALUE, "message with id '%s' is already published")
+      f.kind = make_kind(ZB_VT_MESSAGE, ZB_RT_COMMAND_REJECTION, false);
+      put_record(P, fpos, f, (uint32_t)(fpos - pos));
+    } else {
+      f.key = P.key_base + (int64_t)((off >> PC_ACC) & PC_MASK);
+      f.intent = 1;  // PUBLISHED (batchWriter.addNewEvent)
+      f.kind = make_kind(ZB_VT_MESSAGE, ZB_RT_EVENT, false);
+      put_record(P, fpos, f, (uint32_t)(fpos - pos));
+      if (v.ttl <= 0) {  // addFollowUpEvent(key, DELETED, messageRecord): never stored
+        f.intent = 3;
+        f.kind = make_kind(ZB_VT_MESSAGE, ZB_RT_EVENT, true);
+        put_record(P, fpos + 1, f, (uint32_t)(fpos + 1 - pos));
+      }
+      h = name_ck_hash(v.name, v.nn, v.ck, v.nc);
+      for (uint32_t e = P.sub_head[h & P.sub_mask]; e != NO_ENTRY; e = P.sub_next[e]) {
+        const SubEntry s = P.subs[e];
+        if (s.h == h && sub_matches(sub_view(P.arena, s.blob), v)) nmatch++;
+      }
+      gran = nmatch * var_granules(v.nn, 0, v.np);
     }
-    for (uint32_t e = P.sub_head[h & P.sub_mask]; e != NO_ENTRY; e = P.sub_next[e]) {
-      const SubEntry s = P.subs[e];
-      if (s.h != h) continue;
-      const uint8_t* sb = P.arena + (uint64_t)s.blob * 8;
-      if (sb[8] != v.nn || sb[9] != v.nc || !bytes_equal(sb + 16, v.name, v.nn) || !bytes_equal(sb + 64, v.ck, v.nc))
-        continue;
-      nmatch++;
-    }
-    if (nmatch && v.np > ZB_XCHG_PAYLOAD_MAX) { atomicOr(P.err, (uint32_t)DE_UNSUPPORTED); nmatch = 0; }
   }
-  uint32_t slot = wave_alloc(P.on, nmatch);
-  if (act && nmatch) {
+  uint32_t slot = wave_alloc(P.ob.n, nmatch);
+  uint32_t vat = wave_alloc(P.ob.var_n, gran);
+  if (act && nmatch) {  // correlateMessage :107-124: one command per matching subscription
+    const uint32_t g = var_granules(v.nn, 0, v.np);
     for (uint32_t e = P.sub_head[h & P.sub_mask]; e != NO_ENTRY; e = P.sub_next[e]) {
       const SubEntry s = P.subs[e];
       if (s.h != h) continue;
-      const uint8_t* sb = P.arena + (uint64_t)s.blob * 8;
-      if (sb[8] != v.nn || sb[9] != v.nc || !bytes_equal(sb + 16, v.name, v.nn) || !bytes_equal(sb + 64, v.ck, v.nc))
-        continue;
-      const int32_t wfp = *(const int32_t*)(sb + 4);
-      if (slot >= P.ocap) { atomicOr(P.err, (uint32_t)DE_LOG_FULL); break; }
-      write_xchg(P.obox + slot, ZB_XCHG_CORRELATE, wfp, wfp, *(const uint32_t*)(sb + 12), s.wik, s.aik, pos,
-                 *(const uint16_t*)(sb + 10), v.name, v.nn, nullptr, 0, v.payload, v.np);
-      P.okeys[slot] = outbox_key(wfp, pos, s.idx);  // findSubscriptions: insertion order
+      const SubView sb = sub_view(P.arena, s.blob);
+      if (!sub_matches(sb, v)) continue;
+      if (slot >= P.ob.cap || (uint64_t)vat + g > P.ob.var_cap) { err |= DE_LOG_FULL; break; }
+      outbox_write(P.ob, slot, vat, ZB_XCHG_CORRELATE, sb.wfp, sb.wfp, sb.token, s.wik, s.aik, pos, sb.elem, v.name, v.nn,
+                   nullptr, 0, v.payload, v.np, s.idx);  // findSubscriptions: insertion order
       slot++;
+      vat += g;
     }
   }
-  if (act && P.ttl > 0) {  // messageStore.addMessage
-    const uint32_t idx = (uint32_t)(P.msg_count + i);
-    MsgEntry m;
-    m.h = h; m.key = P.key_base + i; m.pos = pos; m.blob = ref; m.dead = 0;
-    P.msgs[idx] = m;
-    P.msg_next[idx] = atomicExch(&P.msg_head[h & P.msg_mask], idx);
+  if (act && acc && v.ttl > 0) {  // messageStore.addMessage (deadline = timeToLive + now)
+    const uint64_t idx = P.msg_count + ((off >> PC_STORED) & PC_MASK);
+    if (idx >= P.msg_cap) err |= DE_LOG_FULL;
+    else {
+      MsgEntry m;
+      m.h = h; m.key = P.key_base + (int64_t)((off >> PC_ACC) & PC_MASK); m.pos = pos; m.deadline = v.ttl + P.clock;
+      m.blob = d.payload; m.dead = 0;
+      *(int64_t*)(P.arena + (uint64_t)d.payload * 8 + 16) = m.deadline;
+      P.msgs[idx] = m;
+      P.msg_next[idx] = atomicExch(&P.msg_head[h & P.msg_mask], (uint32_t)idx);
+    }
+  }
+  flag_error(P, err);
+}
+
+// ------------------------------------------------------------------------------ DELETE
+__global__ void __launch_bounds__(256) k_msg_delete(MsgParams P) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= P.n) return;
+  const int64_t pos = P.base + j, fpos = P.out_base + j;
+  zb_rec f = P.log[pos];
+  f.kind = make_kind(ZB_VT_MESSAGE, ZB_RT_EVENT, false);  // writeFollowUpEvent(record.getKey(), DELETED, value)
+  f.intent = 3;
+  put_record(P, fpos, f, (uint32_t)(fpos - pos));
+  // messageStore.removeMessage(key): entries are in key order
+  int64_t lo = 0, hi = (int64_t)P.msg_count - 1;
+  while (lo <= hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    const int64_t k = P.msgs[mid].key;
+    if (k == f.key) {
+      P.msgs[mid].dead = 1;
+      break;
+    }
+    if (k < f.key) lo = mid + 1;
+    else hi = mid - 1;
+  }
+}
+
+// ------------------------------------------------------------------------------ time to live
+__global__ void __launch_bounds__(256) k_ttl_flags(MsgParams P) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i <= P.msg_count; i += stride)
+    P.flags[i] = (i < P.msg_count && !P.msgs[i].dead && P.msgs[i].deadline <= P.now) ? 1u : 0u;
+}
+// writeFollowUpCommand(message.getKey(), DELETE, command) by the checker's own command writer (no source)
+__global__ void __launch_bounds__(256) k_ttl_write(MsgParams P) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < P.msg_count; i += stride) {
+    const MsgEntry m = P.msgs[i];
+    if (m.dead || m.deadline > P.now) continue;
+    zb_rec d;
+    d.key = m.key;
+    d.scope_key = -1;
+    d.inst_key = -1;
+    d.payload = m.blob;
+    d.elem = NO_ELEM;
+    d.intent = 2;  // DELETE
+    d.kind = make_kind(ZB_VT_MESSAGE, ZB_RT_COMMAND, false);
+    put_record(P, P.base + (int64_t)P.flag_off[i], d, 0);
   }
 }
 
@@ -212,42 +304,43 @@ __global__ void __launch_bounds__(256) k_msg_publish(MsgParams P) {
 __global__ void __launch_bounds__(256) k_wis_inject(MsgParams P) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= P.n) return;
-  const zb_exchange_rec r = P.in[i];
-  const int64_t pos = P.base + i;
-  const uint64_t at = P.arena_base + (uint64_t)i * WIS_BLOB;
-  uint8_t* b = P.arena + at;
-  uint32_t np = r.payload_len;
-  if (np == 0 || (np == 1 && r.payload[0] == 0xc0)) {  // DocumentValue: nil / empty -> {}
-    np = 1;
-    b[4] = 0x80;
-  } else {
-    for (uint32_t k = 0; k < np && k < ZB_XCHG_PAYLOAD_MAX; k++) b[4 + k] = r.payload[k];
+  const uint8_t* var;
+  const zb_exchange_rec r = delivered(P, i, var);
+  const uint8_t* pl = var + r.name_len + r.ck_len;
+  const uint32_t np = r.payload_len;
+  const bool empty = np == 0 || (np == 1 && pl[0] == 0xc0);  // DocumentValue: nil / empty -> {}
+  uint32_t err = 0, ref = 0;
+  uint8_t* b = alloc_blob(P, empty ? 1 : np, ref, err);
+  if (b) {
+    if (empty) b[4] = 0x80;
+    else copy_bytes(b + 4, pl, np);
   }
-  *(uint32_t*)b = np;
+  const int64_t pos = P.base + i;
   zb_rec d;
   d.key = pos;  // positionAsKey (SubscriptionApiCommandMessageHandler.java:144-149)
   d.scope_key = r.activity_instance_key;
   d.inst_key = r.workflow_instance_key;
-  d.payload = (uint32_t)(at >> 3);
+  d.payload = ref;
   d.elem = r.elem;
   d.intent = 0;  // CORRELATE
   d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION, ZB_RT_COMMAND, false);
-  P.log[pos] = d;
   // row_self: found by activity instance key (k_resolve after this kernel; the sender's row token can be stale
   // once the workflow partition compacted its rows)
-  P.links[pos] = ~0ull;
-  P.srcd[pos] = 0;
-  P.vlen[pos] = VLEN_UNKNOWN;
+  put_record(P, pos, d, 0);
   P.lookup_keys[i] = r.activity_instance_key;
   P.lookup_pos[i] = pos;
+  flag_error(P, err);
 }
 
-// ------------------------------------------------------------------------------ outbox
-__global__ void k_outbox_gather(const zb_exchange_rec* src, const uint32_t* idx, zb_exchange_rec* dst, uint64_t n) {
+// ------------------------------------------------------------------------------ outbox take
+__global__ void k_outbox_sizes(Outbox ob, const uint32_t* idx, uint64_t n, uint32_t* sizes) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) dst[i] = src[idx[i]];
+  if (i > n) return;
+  if (i == n) { sizes[n] = 0; return; }
+  const zb_exchange_rec& r = ob.rec[idx[i]];
+  sizes[i] = var_granules(r.name_len, r.ck_len, r.payload_len);
 }
-// first sorted index of every target partition (targets are the key's top 6 bits)
+// first sorted index of every target partition (targets are the key's top 6 bits); first[parts] = n
 __global__ void k_outbox_bounds(const uint64_t* keys, uint64_t n, uint64_t* first, int parts) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -255,7 +348,35 @@ __global__ void k_outbox_bounds(const uint64_t* keys, uint64_t n, uint64_t* firs
   const int tp = i == 0 ? -1 : (int)(keys[i - 1] >> 58);
   for (int q = tp + 1; q <= t && q < parts; q++) first[q] = i;
   if (i == n - 1)
-    for (int q = t + 1; q < parts; q++) first[q] = n;
+    for (int q = t + 1; q <= parts; q++) first[q] = n;
+}
+// per target: (commands, variable granules)
+__global__ void k_outbox_table(const uint64_t* first, const uint32_t* goff, int parts, uint64_t* table) {
+  const int q = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (q >= parts) return;
+  table[2 * q] = first[q + 1] - first[q];
+  table[2 * q + 1] = (uint64_t)goff[first[q + 1]] - (uint64_t)goff[first[q]];
+}
+// sorted command i into its target's batch at dst + base[target]
+__global__ void k_outbox_pack(Outbox ob, const uint32_t* idx, const uint64_t* keys, uint64_t n, const uint64_t* first,
+                              const uint32_t* goff, const uint64_t* base, uint8_t* dst) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int q = (int)(keys[i] >> 58);
+  const uint64_t f = first[q], cnt = first[q + 1] - f;
+  uint8_t* bat = dst + base[q];
+  const uint64_t var_bytes = 8 * ((uint64_t)goff[first[q + 1]] - (uint64_t)goff[f]);
+  if (i == f) {
+    ((uint64_t*)bat)[0] = cnt;
+    ((uint64_t*)bat)[1] = ZB_XCHG_BATCH_HEADER + cnt * sizeof(zb_exchange_rec) + var_bytes;
+  }
+  zb_exchange_rec r = ob.rec[idx[i]];
+  const uint64_t* src = (const uint64_t*)(ob.var + r.var_offset);
+  r.var_offset = 8 * ((uint64_t)goff[i] - (uint64_t)goff[f]);
+  ((zb_exchange_rec*)(bat + ZB_XCHG_BATCH_HEADER))[i - f] = r;
+  uint64_t* vd = (uint64_t*)(bat + ZB_XCHG_BATCH_HEADER + cnt * sizeof(zb_exchange_rec) + r.var_offset);
+  const uint32_t g = var_granules(r.name_len, r.ck_len, r.payload_len);
+  for (uint32_t k = 0; k < g; k++) vd[k] = src[k];
 }
 __global__ void k_iota(uint32_t* p, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -263,22 +384,44 @@ __global__ void k_iota(uint32_t* p, uint64_t n) {
 }
 
 static unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
+static unsigned grid_cap(uint64_t n) {
+  const uint64_t g = (n + 255) / 256;
+  return (unsigned)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
+}
 
 void launch_msg_open(const MsgParams& p, hipStream_t s) {
   if (p.n > 0) hipLaunchKernelGGL(k_msg_open, dim3(blocks(p.n)), dim3(256), 0, s, p);
 }
-void launch_msg_publish(const MsgParams& p, hipStream_t s) {
-  if (p.n > 0) hipLaunchKernelGGL(k_msg_publish, dim3(blocks(p.n)), dim3(256), 0, s, p);
+void launch_pub_count(const MsgParams& p, hipStream_t s) {
+  if (p.n > 0) hipLaunchKernelGGL(k_pub_count, dim3(blocks(p.n)), dim3(256), 0, s, p);
+}
+void launch_pub_emit(const MsgParams& p, hipStream_t s) {
+  if (p.n > 0) hipLaunchKernelGGL(k_pub_emit, dim3(blocks(p.n)), dim3(256), 0, s, p);
+}
+void launch_msg_delete(const MsgParams& p, hipStream_t s) {
+  if (p.n > 0) hipLaunchKernelGGL(k_msg_delete, dim3(blocks(p.n)), dim3(256), 0, s, p);
+}
+void launch_ttl_flags(const MsgParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_ttl_flags, dim3(grid_cap(p.msg_count + 1)), dim3(256), 0, s, p);
+}
+void launch_ttl_write(const MsgParams& p, hipStream_t s) {
+  if (p.msg_count) hipLaunchKernelGGL(k_ttl_write, dim3(grid_cap(p.msg_count)), dim3(256), 0, s, p);
 }
 void launch_wis_inject(const MsgParams& p, hipStream_t s) {
   if (p.n > 0) hipLaunchKernelGGL(k_wis_inject, dim3(blocks(p.n)), dim3(256), 0, s, p);
 }
-void launch_outbox_gather(const zb_exchange_rec* src, const uint32_t* idx, zb_exchange_rec* dst, uint64_t n,
-                          hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_outbox_gather, dim3(blocks((int64_t)n)), dim3(256), 0, s, src, idx, dst, n);
+void launch_outbox_sizes(const Outbox& ob, const uint32_t* idx, uint64_t n, uint32_t* sizes, hipStream_t s) {
+  hipLaunchKernelGGL(k_outbox_sizes, dim3(blocks((int64_t)n + 1)), dim3(256), 0, s, ob, idx, n, sizes);
 }
 void launch_outbox_bounds(const uint64_t* keys, uint64_t n, uint64_t* first, int parts, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_outbox_bounds, dim3(blocks((int64_t)n)), dim3(256), 0, s, keys, n, first, parts);
+}
+void launch_outbox_table(const uint64_t* first, const uint32_t* goff, int parts, uint64_t* table, hipStream_t s) {
+  hipLaunchKernelGGL(k_outbox_table, dim3(1), dim3(64), 0, s, first, goff, parts, table);
+}
+void launch_outbox_pack(const Outbox& ob, const uint32_t* idx, const uint64_t* keys, uint64_t n, const uint64_t* first,
+                        const uint32_t* goff, const uint64_t* base, uint8_t* dst, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_outbox_pack, dim3(blocks((int64_t)n)), dim3(256), 0, s, ob, idx, keys, n, first, goff, base, dst);
 }
 void launch_iota(uint32_t* p, uint64_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_iota, dim3(blocks((int64_t)n)), dim3(256), 0, s, p, n);

@@ -1,5 +1,5 @@
 // zb_msg.hpp — message correlation helpers shared by the wave pipeline (workflow side) and the
-// message-side kernels (zb_msg.hip): partition routing, store hashing, outbox records.
+// message-side kernels (zb_msg.hip): partition routing, store hashing, arena blob layouts, outbox records.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -8,8 +8,54 @@
 namespace zbg {
 
 constexpr uint32_t NO_ENTRY = 0xffffffffu;
-constexpr uint32_t SUB_BLOB = 112;   // [u32 len][i32 wfp][u8 name_len][u8 ck_len][u16 elem][u32 token][name 48][ck 48]
-constexpr uint32_t WIS_BLOB = 120;   // [u32 len][payload document <= 112 B] (CORRELATE command payload)
+
+// ---- arena blobs of the message side ([u32 len][len bytes], 8-aligned; len counts the bytes after the word)
+// message (MessageRecord.java:26-42 as stored by MessageDataStore.Message): the PUBLISH command's decoded value
+//   [u32 len][u32 name_len][i64 ttl][i64 deadline][u32 ck_len][u32 payload_len][u32 id_len][u32 pad]
+//   [name][correlation key][payload document][message id]
+constexpr uint32_t MSG_HDR = 40;  // bytes before the name (incl. the length word)
+struct MsgView {
+  int64_t ttl, deadline;
+  const uint8_t *name, *ck, *payload, *id;
+  uint32_t nn, nc, np, nid;
+};
+__device__ __forceinline__ MsgView msg_view(const uint8_t* arena, uint32_t ref) {
+  const uint8_t* b = arena + (uint64_t)ref * 8;
+  MsgView v;
+  v.nn = *(const uint32_t*)(b + 4);
+  v.ttl = *(const int64_t*)(b + 8);
+  v.deadline = *(const int64_t*)(b + 16);
+  v.nc = *(const uint32_t*)(b + 24);
+  v.np = *(const uint32_t*)(b + 28);
+  v.nid = *(const uint32_t*)(b + 32);
+  v.name = b + MSG_HDR;
+  v.ck = v.name + v.nn;
+  v.payload = v.ck + v.nc;
+  v.id = v.payload + v.np;
+  return v;
+}
+// subscription (MessageSubscriptionRecord.java:26-41 as OPEN delivered it):
+//   [u32 len][i32 wf_partition][u32 token][u16 elem][u16 pad][u32 name_len][u32 ck_len][name][correlation key]
+constexpr uint32_t SUB_HDR = 24;
+struct SubView {
+  int32_t wfp;
+  uint32_t token;
+  uint16_t elem;
+  const uint8_t *name, *ck;
+  uint32_t nn, nc;
+};
+__device__ __forceinline__ SubView sub_view(const uint8_t* arena, uint32_t ref) {
+  const uint8_t* b = arena + (uint64_t)ref * 8;
+  SubView v;
+  v.wfp = *(const int32_t*)(b + 4);
+  v.token = *(const uint32_t*)(b + 8);
+  v.elem = *(const uint16_t*)(b + 12);
+  v.nn = *(const uint32_t*)(b + 16);
+  v.nc = *(const uint32_t*)(b + 20);
+  v.name = b + SUB_HDR;
+  v.ck = v.name + v.nn;
+  return v;
+}
 
 // SubscriptionUtil.getSubscriptionHashCode (SubscriptionUtil.java:30-38: 31-hash over SIGNED bytes,
 // int32 wraparound) -> abs(hash % P) (SubscriptionCommandSender.java:105-109, Java remainder)
@@ -59,6 +105,32 @@ __device__ __forceinline__ uint32_t wave_alloc(uint32_t* counter, uint32_t cnt) 
   if (lane == leader && total) base = atomicAdd(counter, total);
   base = __shfl(base, leader, 64);
   return base + excl;
+}
+
+__device__ __forceinline__ uint32_t var_granules(uint32_t nn, uint32_t nc, uint32_t np) {
+  return (nn + nc + np + 7) >> 3;
+}
+
+__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++) dst[i] = src[i];
+}
+__device__ __forceinline__ void outbox_write(const Outbox& ob, uint32_t slot, uint32_t var_at, int32_t kind, int32_t target,
+                                             int32_t wfp, uint32_t token, int64_t wik, int64_t aik, int64_t spos,
+                                             uint16_t elem, const uint8_t* name, uint32_t nn, const uint8_t* ck,
+                                             uint32_t nc, const uint8_t* payload, uint32_t np, uint32_t emission) {
+  zb_exchange_rec r;
+  r.kind = kind; r.target_partition = target; r.wf_partition = wfp; r.token = token;
+  r.workflow_instance_key = wik; r.activity_instance_key = aik; r.source_position = spos;
+  r.elem = elem; r.pad = 0;
+  r.name_len = nn; r.ck_len = nc; r.payload_len = np;
+  r.var_offset = (uint64_t)var_at * 8;
+  uint8_t* v = ob.var + (uint64_t)var_at * 8;
+  copy_bytes(v, name, nn);
+  copy_bytes(v + nn, ck, nc);
+  copy_bytes(v + nn + nc, payload, np);
+  for (uint32_t i = nn + nc + np; i < var_granules(nn, nc, np) * 8; i++) v[i] = 0;
+  ob.rec[slot] = r;
+  ob.keys[slot] = outbox_key(target, spos, emission);
 }
 
 }  // namespace zbg

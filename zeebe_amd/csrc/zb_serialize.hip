@@ -12,6 +12,7 @@
 #include "zb_devlib.hpp"
 #include "zb_fastenc.hpp"
 #include "zb_kernels.hpp"
+#include "zb_msg.hpp"
 
 namespace zbg {
 
@@ -237,23 +238,22 @@ __device__ __forceinline__ void encode_value(const SerParams& P, int64_t pos, co
     w.key("activityInstanceKey"); w.integer(d.scope_key);
     w.key("messageName"); w.str(P.pool + e.msg_off, e.msg_len);
     w.key("payload"); w.bin(pl, plen);
-  } else if (vt == ZB_VT_MESSAGE_SUBSCRIPTION) {  // MessageSubscriptionRecord.java:26-41 (blob: zb_msg.hpp SUB_BLOB)
-    const uint8_t* b = P.arena + (uint64_t)d.payload * 8;
+  } else if (vt == ZB_VT_MESSAGE_SUBSCRIPTION) {  // MessageSubscriptionRecord.java:26-41 (blob: zb_msg.hpp SubView)
+    const SubView v = sub_view(P.arena, d.payload);
     w.map_hdr(5);
-    w.key("workflowInstancePartitionId"); w.integer(*(const int32_t*)(b + 4));
+    w.key("workflowInstancePartitionId"); w.integer(v.wfp);
     w.key("workflowInstanceKey"); w.integer(d.inst_key);
     w.key("activityInstanceKey"); w.integer(d.scope_key);
-    w.key("messageName"); w.str(b + 16, b[8]);
-    w.key("correlationKey"); w.str(b + 64, b[9]);
-  } else if (vt == ZB_VT_MESSAGE) {  // MessageRecord.java:26-42 (blob: ttl, lengths, name, ck, payload)
-    const uint8_t* b = P.arena + (uint64_t)d.payload * 8 + 4;
-    const uint32_t nn = *(const uint16_t*)(b + 8), nc = *(const uint16_t*)(b + 10), np = *(const uint32_t*)(b + 12);
+    w.key("messageName"); w.str(v.name, v.nn);
+    w.key("correlationKey"); w.str(v.ck, v.nc);
+  } else if (vt == ZB_VT_MESSAGE) {  // MessageRecord.java:26-42 (blob: zb_msg.hpp MsgView)
+    const MsgView v = msg_view(P.arena, d.payload);
     w.map_hdr(5);
-    w.key("name"); w.str(b + 16, nn);
-    w.key("correlationKey"); w.str(b + 16 + nn, nc);
-    w.key("timeToLive"); w.integer(*(const int64_t*)b);
-    w.key("payload"); w.bin(b + 16 + nn + nc, np);
-    w.key("messageId"); w.str(nullptr, 0);
+    w.key("name"); w.str(v.name, v.nn);
+    w.key("correlationKey"); w.str(v.ck, v.nc);
+    w.key("timeToLive"); w.integer(v.ttl);
+    w.key("payload"); w.bin(v.payload, v.np);
+    w.key("messageId"); w.str(v.id, v.nid);
   }
 }
 
@@ -296,6 +296,7 @@ __device__ __forceinline__ uint8_t rejection_type(const zb_rec& d) {
   const uint8_t vt = kind_vt(d.kind);
   if (vt == ZB_VT_WORKFLOW_INSTANCE && d.intent == WI_CREATE) return 0;
   if (vt == ZB_VT_JOB && d.intent == JI_UPDATE_RETRIES && (d.kind & KIND_RAW) && d.elem == 1) return 0;
+  if (vt == ZB_VT_MESSAGE) return 0;  // a published message id (PublishMessageProcessor.java:77-84)
   return 1;
 }
 
@@ -310,13 +311,15 @@ __device__ __forceinline__ uint8_t rejection_type(const zb_rec& d) {
 constexpr uint32_t FRAME_PREFIX = 12 + 48 + 8 + 34 + 2;
 
 // rejection reasons of the commands this path rejects (WorkflowInstanceStreamProcessor.java:346-347, :527-529,
-// :573, :478-479)
-// and of the job commands (JobInstanceStreamProcessor.java:155-158, :172-173, :186-187, :193, :215-220, :238)
+// :573, :478-479), of the job commands (JobInstanceStreamProcessor.java:155-158, :172-173, :186-187, :193,
+// :215-220, :238) and of PUBLISH (PublishMessageProcessor.java:77-84: "message with id '%s' is already published",
+// built around the message's id, reason 10)
 __device__ const char* const REASONS[11] = {
     "", "Workflow is not deployed", "Workflow instance is not running", "activity is not active anymore",
     "Job is not in one of these states: CREATED, FAILED, TIMED_OUT", "Job is not in state: ACTIVATED, TIMED_OUT",
     "Job is not in state ACTIVATED", "Retries must be greater than 0", "Job is not in state FAILED",
-    "Job does not exist", ""};
+    "Job does not exist", "message with id '"};
+__device__ const char MSG_ID_TAIL[] = "' is already published";
 __device__ __forceinline__ uint32_t reason_of(const zb_rec& d) {
   if (kind_rt(d.kind) != ZB_RT_COMMAND_REJECTION) return 0;
   const uint8_t vt = kind_vt(d.kind);
@@ -331,9 +334,13 @@ __device__ __forceinline__ uint32_t reason_of(const zb_rec& d) {
       case JI_CANCEL: return 9;
     }
   }
+  if (vt == ZB_VT_MESSAGE) return 10;
   return 0;
 }
-__device__ __forceinline__ uint32_t reason_len(uint32_t r) { return dstrlen(REASONS[r < 11 ? r : 0]); }
+__device__ __forceinline__ uint32_t reason_len(const SerParams& P, const zb_rec& d, uint32_t r) {
+  if (r == 10) return dstrlen(REASONS[10]) + msg_view(P.arena, d.payload).nid + dstrlen(MSG_ID_TAIL);
+  return dstrlen(REASONS[r < 11 ? r : 0]);
+}
 
 __device__ __forceinline__ const ReqMeta* find_req(const SerParams& P, int64_t pos) {
   int64_t lo = 0, hi = P.nreqs - 1;
@@ -354,7 +361,7 @@ __device__ __forceinline__ int64_t source_of(const SerParams& P, int64_t pos) {
 // frame of record d at log position pos into dst (8-aligned), or only its size (dst == nullptr); returns the
 // aligned frame length
 __device__ inline uint32_t encode_frame(const SerParams& P, int64_t pos, const zb_rec& d, uint8_t* dst) {
-  const uint32_t rs = reason_of(d), rlen = reason_len(rs);
+  const uint32_t rs = reason_of(d), rlen = reason_len(P, d, rs);
   W w;
   w.dst = dst ? dst + FRAME_PREFIX + rlen : nullptr;
   w.n = 0;
@@ -374,7 +381,10 @@ __device__ inline uint32_t encode_frame(const SerParams& P, int64_t pos, const z
   // TypedStreamProcessor producer ids (StreamProcessorIds.java:23-39): harness job events 10 (the job
   // processor), message partition records 90, everything else the workflow instance processor 70; records
   // other writers appended keep the writer's default -1
-  const int32_t producer = src < 0 ? -1 : (vt == ZB_VT_JOB && rt != ZB_RT_COMMAND) ? 10
+  // (a MESSAGE DELETE command comes from the time-to-live checker's own command writer: producer id 0,
+  // TypedCommandWriterImpl never configured, MessageService.java:118-120)
+  const int32_t producer = src < 0 ? ((vt == ZB_VT_MESSAGE && rt == ZB_RT_COMMAND && d.intent == 2) ? 0 : -1)
+                         : (vt == ZB_VT_JOB && rt != ZB_RT_COMMAND) ? 10
                          : (vt == ZB_VT_MESSAGE || vt == ZB_VT_MESSAGE_SUBSCRIPTION) ? 90 : 70;
   uint64_t rid = ~0ull;
   uint32_t sid = 0x80000000u;
@@ -409,6 +419,11 @@ __device__ inline uint32_t encode_frame(const SerParams& P, int64_t pos, const z
   r.dst = dst + FRAME_PREFIX;
   r.n = 0;
   if (rs) r.cstr(REASONS[rs < 11 ? rs : 0]);
+  if (rs == 10) {
+    const MsgView v = msg_view(P.arena, d.payload);
+    r.put_bytes(v.id, v.nid);
+    r.cstr(MSG_ID_TAIL);
+  }
   for (uint32_t k = framed; k < fsize; k++) dst[k] = 0;
   return fsize;
 }
@@ -452,7 +467,7 @@ __global__ void __launch_bounds__(256) k_ser_size(SerParams P0) {
                 mp_int_len(d.scope_key) + mp_bin_len(*(const uint32_t*)(P.arena + (uint64_t)d.payload * 8))
           : value_size(P, pos, d);
       if (n[j] != VLEN_UNKNOWN && n[j] != m) atomicOr(P.vlen_bad, 1u);
-      n[j] = FRAMES ? (FRAME_PREFIX + reason_len(reason_of(d)) + m + 7) & ~7u : m;
+      n[j] = FRAMES ? (FRAME_PREFIX + reason_len(P, d, reason_of(d)) + m + 7) & ~7u : m;
       if (P.len_in_vlen) P.vlen_out[pos] = n[j];
     }
   }
@@ -465,7 +480,7 @@ __global__ void __launch_bounds__(256) k_ser_size(SerParams P0) {
       // a known value length (an emitting kernel's, or one a values drain measured and wrote back -- which
       // includes rejections): the frame adds the rejection reason of the record
       const zb_rec d = P0.log[P0.start + i];
-      n[j] = (FRAME_PREFIX + reason_len(reason_of(d)) + n[j] + 7) & ~7u;
+      n[j] = (FRAME_PREFIX + reason_len(P0, d, reason_of(d)) + n[j] + 7) & ~7u;
     }
     if (live && !P0.len_in_vlen) P0.lengths[i] = n[j];
     unsigned long long y = n[j];

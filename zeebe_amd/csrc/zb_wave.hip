@@ -666,52 +666,56 @@ __device__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t p
 // position. One thread per subscribe step of the wave (k_process listed them).
 __global__ void __launch_bounds__(256) k_subscribe(WaveParams P) {
   const uint32_t n = P.sub_count[P.wave & 1];
-  for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < n && j < P.job_cap; j += (uint64_t)gridDim.x * 256) {
-    const int64_t pos = (int64_t)P.sub_jobs[j];
-    const zb_rec rec = P.log[pos];
-    const uint32_t rself = (uint32_t)P.links[pos];
-    const DevElem& el = P.elems[rec.elem];
-    uint32_t err = 0, site = 0;
-    const uint8_t* pp = P.arena + (uint64_t)rec.payload * 8;
-    const uint32_t len = *(const uint32_t*)pp;
-    QueryResult q;
-    Tok tk;
-    uint8_t ck[ZB_XCHG_CK_MAX];
-    uint32_t ck_len = 0;
-    if (!run_query(pp + 4, len, P.queries[el.ck_query], P.filters, P.pool, q)) { err = DE_UNSUPPORTED; site = 30; }
-    // extractCorrelationKey :121-141: exactly one result, a string or a long, else the processor fails
-    else if (q.count != 1) { err = DE_PROCESSING; site = 31; }
-    else if (!read_tok(pp + 4 + q.pos, q.len, tk)) { err = DE_PROCESSING; site = 32; }
-    else if (tk.type == TT_STRING) {
-      if (tk.len > ZB_XCHG_CK_MAX) { err = DE_UNSUPPORTED; site = 33; }
-      else {
+  // (uniform trip count per wave: wave_alloc below is a wave-wide operation)
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t j0 = (uint64_t)blockIdx.x * 256; j0 < n && j0 < P.job_cap; j0 += stride) {
+    const uint64_t j = j0 + threadIdx.x;
+    const bool act = j < n && j < P.job_cap;
+    uint32_t err = 0, site = 0, ck_len = 0, gran = 0, rself = NO_ROW;
+    int64_t pos = 0;
+    zb_rec rec{};
+    const uint8_t* ck = nullptr;
+    uint8_t ckbuf[8];
+    const DevElem* el = nullptr;
+    if (act) {
+      pos = (int64_t)P.sub_jobs[j];
+      rec = P.log[pos];
+      rself = (uint32_t)P.links[pos];
+      el = &P.elems[rec.elem];
+      const uint8_t* pp = P.arena + (uint64_t)rec.payload * 8;
+      const uint32_t len = *(const uint32_t*)pp;
+      QueryResult q;
+      Tok tk;
+      if (!run_query(pp + 4, len, P.queries[el->ck_query], P.filters, P.pool, q)) { err = DE_UNSUPPORTED; site = 30; }
+      // extractCorrelationKey :121-141: exactly one result, a string or a long, else the processor fails
+      else if (q.count != 1) { err = DE_PROCESSING; site = 31; }
+      else if (!read_tok(pp + 4 + q.pos, q.len, tk)) { err = DE_PROCESSING; site = 32; }
+      else if (tk.type == TT_STRING) {
         ck_len = tk.len;
-        const uint8_t* src = pp + 4 + q.pos + tk.hdr;
-        for (uint32_t i = 0; i < ck_len; i++) ck[i] = src[i];
+        ck = pp + 4 + q.pos + tk.hdr;
+      } else if (tk.type == TT_INTEGER) {  // QueryResult.getLongAsBuffer: 8 bytes, native (little-endian) order
+        ck_len = 8;
+        for (int i = 0; i < 8; i++) ckbuf[i] = (uint8_t)((uint64_t)tk.ival >> (8 * i));
+        ck = ckbuf;
+      } else {
+        err = DE_PROCESSING; site = 34;  // "Failed to extract correlation-key: wrong type"
       }
-    } else if (tk.type == TT_INTEGER) {  // QueryResult.getLongAsBuffer: 8 bytes, native (little-endian) order
-      ck_len = 8;
-      for (int i = 0; i < 8; i++) ck[i] = (uint8_t)((uint64_t)tk.ival >> (8 * i));
-    } else {
-      err = DE_PROCESSING; site = 34;  // "Failed to extract correlation-key: wrong type"
+      if (!err) gran = var_granules(el->msg_len, ck_len, 0);
     }
-    if (!err && el.msg_len > ZB_XCHG_NAME_MAX) { err = DE_UNSUPPORTED; site = 35; }
+    const uint32_t slot = wave_alloc(P.obx.n, act && !err ? 1u : 0u);
+    const uint32_t vat = wave_alloc(P.obx.var_n, gran);
+    if (act && !err) {
+      if (slot >= P.obx.cap || (uint64_t)vat + gran > P.obx.var_cap) { err = DE_LOG_FULL; site = 36; }
+      else {
+        const int32_t target = subscription_partition(ck, ck_len, P.partition_count);
+        outbox_write(P.obx, slot, vat, ZB_XCHG_OPEN, target, P.partition_id, rself, rec.inst_key, rec.key, pos, rec.elem,
+                     P.pool + el->msg_off, el->msg_len, ck, ck_len, nullptr, 0, 0);
+      }
+    }
     if (err) {
       atomicOr(P.err, err);
       atomicMin((unsigned long long*)P.err_info, ((unsigned long long)pos << 8) | site);
-      continue;
     }
-    const uint32_t slot = wave_alloc(P.on, 1u);  // one device atomic per wave
-    if (slot >= P.ocap) { atomicOr(P.err, (uint32_t)DE_LOG_FULL); continue; }
-    const int32_t target = subscription_partition(ck, ck_len, P.partition_count);
-    zb_exchange_rec& r = P.obox[slot];
-    r.kind = ZB_XCHG_OPEN; r.target_partition = target; r.wf_partition = P.partition_id; r.token = rself;
-    r.workflow_instance_key = rec.inst_key; r.activity_instance_key = rec.key; r.source_position = pos;
-    r.elem = rec.elem; r.name_len = (uint8_t)el.msg_len; r.ck_len = (uint8_t)ck_len; r.payload_len = 0; r.pad = 0;
-    for (uint32_t i = 0; i < ZB_XCHG_NAME_MAX; i++) r.name[i] = i < el.msg_len ? P.pool[el.msg_off + i] : 0;
-    for (uint32_t i = 0; i < ZB_XCHG_CK_MAX; i++) r.ck[i] = i < ck_len ? ck[i] : 0;
-    for (uint32_t i = 0; i < ZB_XCHG_PAYLOAD_MAX; i++) r.payload[i] = 0;
-    P.okeys[slot] = outbox_key(target, pos, 0);
   }
 }
 

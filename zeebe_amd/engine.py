@@ -139,7 +139,10 @@ def lib():
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.zb_inbox_submit.argtypes = [vp, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         L.zb_outbox_count.argtypes = [vp, ctypes.c_int, u64p]
-        L.zb_outbox_take.argtypes = [vp, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, u64p, u64p]
+        L.zb_outbox_take.argtypes = [vp, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, u64p, u64p, u64p]
+        L.zb_submit_messages.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+        L.zb_set_clock.argtypes = [vp, ctypes.c_int64]
+        L.zb_expire_messages.argtypes = [vp, ctypes.c_int64, u64p]
         L.zb_comm_unique_id.argtypes = [ctypes.c_char_p]
         L.zb_comm_init.argtypes = [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
         L.zb_comm_pending.argtypes = [vp, u64p]
@@ -172,7 +175,8 @@ EXPORTED_SYMBOLS = ["zb_engine_create", "zb_engine_destroy", "zb_last_error", "z
                     "zb_comm_exchange", "zb_submit", "zb_read_instances", "zb_snapshot", "zb_restore",
                     "zb_validate_deployment", "zb_serialize", "zb_drain_copy", "zb_pinned_alloc", "zb_pinned_free",
                     "zb_serialize_frames", "zb_set_request_metadata", "zb_read_source_positions",
-                    "zb_log_release", "zb_compact", "zb_read_memory_stats"]
+                    "zb_log_release", "zb_compact", "zb_read_memory_stats", "zb_submit_messages", "zb_set_clock",
+                    "zb_expire_messages"]
 
 
 def validate_deployment(xml):
@@ -417,26 +421,31 @@ class Engine:
         return n.value
 
     def outbox(self, kind: int):
-        """All pending commands of a kind, sorted by (target, source position, emission), as a host uint8
-        array of 256-byte records + counts per target partition. (Between GPUs the engines exchange
-        device-resident outboxes over RCCL themselves: exchange().)"""
+        """All pending commands of a kind, sorted by (target, source position, emission), as exchange batches (one
+        per target partition with commands, back to back; include/zb_engine.h) in a host uint8 array + the byte
+        size of each target's batch. (Between GPUs the engines exchange device-resident outboxes over RCCL
+        themselves: comm_exchange().)"""
         import numpy as np
 
-        n = self.pending(kind)
-        buf = np.zeros(max(n, 1) * 256, dtype=np.uint8)
-        counts = (ctypes.c_uint64 * max(self._parts, 1))()
-        got = ctypes.c_uint64(0)
-        self._check(self._L.zb_outbox_take(self._h, kind, buf.ctypes.data, max(n, 1), 0, counts, ctypes.byref(got)))
-        return buf[:got.value * 256], [int(counts[q]) for q in range(self._parts)]
+        sizes = (ctypes.c_uint64 * max(self._parts, 1))()
+        got, total = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        rc = self._L.zb_outbox_take(self._h, kind, None, 0, 0, sizes, ctypes.byref(got), ctypes.byref(total))
+        if rc not in (ZB_OK, ZB_ENOMEM):
+            self._check(rc)
+        if got.value == 0:
+            return np.zeros(0, dtype=np.uint8), [0] * self._parts
+        buf = np.zeros(total.value, dtype=np.uint8)
+        self._check(self._L.zb_outbox_take(self._h, kind, buf.ctypes.data, total.value, 0, sizes, ctypes.byref(got),
+                                           ctypes.byref(total)))
+        return buf, [int(sizes[q]) for q in range(self._parts)]
 
     def inbox(self, kind: int, buf):
-        """Commands delivered by other partitions (host array of 256-byte records, delivery order)."""
+        """Exchange batches delivered by other partitions (host uint8 array, delivery order)."""
         import numpy as np
 
         a = np.ascontiguousarray(np.asarray(buf, dtype=np.uint8))
-        n = len(a) // 256
-        if n:
-            self._check(self._L.zb_inbox_submit(self._h, kind, a.ctypes.data, n, 0))
+        if len(a):
+            self._check(self._L.zb_inbox_submit(self._h, kind, a.ctypes.data, len(a), 0))
 
     # ---- RCCL exchange between engines of different processes (one partition per GPU)
     @staticmethod
@@ -486,6 +495,27 @@ class Engine:
         n = len(ck_off) - 1
         self._check(self._L.zb_submit_publishes(self._h, name, ttl, n, ck_blob, ck_off.ctypes.data, pl_blob,
                                                 pl_off.ctypes.data))
+
+    def submit_messages(self, recs):
+        """zb_submit_messages: recs = [(intent, key, MessageRecord value bytes), ...] (MESSAGE commands: PUBLISH 0,
+        DELETE 2), appended and processed at once."""
+        n = len(recs)
+        arr = (zb_rec_desc * max(n, 1))()
+        blob = bytearray()
+        for i, (intent, key, value) in enumerate(recs):
+            arr[i] = zb_rec_desc(key, 1, 10, intent, 0, len(value), len(blob))
+            blob += value
+        buf = ctypes.create_string_buffer(bytes(blob), max(len(blob), 1))
+        self._check(self._L.zb_submit_messages(self._h, arr, n, buf, len(blob)))
+
+    def set_clock(self, now_ms: int):
+        self._check(self._L.zb_set_clock(self._h, now_ms))
+
+    def expire_messages(self, now_ms: int) -> int:
+        """MessageTimeToLiveChecker at now_ms: DELETE commands for the expired messages, processed."""
+        n = ctypes.c_uint64(0)
+        self._check(self._L.zb_expire_messages(self._h, now_ms, ctypes.byref(n)))
+        return n.value
 
     def counters(self) -> dict:
         arr = (ctypes.c_int64 * 8)()
