@@ -38,7 +38,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BYTES_PER_TRANSITION = 96  # 32 B row read + 32 B row write + 32 B record descriptor
 DESC_BYTES = 32  # one zb_rec descriptor per log record
 HDR_BYTES = 24  # one zb_record_header per drained record
-PMC_DIR = os.path.join(ROOT, "profiles", "r02")
+PMC_DIR = os.path.join(ROOT, "profiles", "r03")
 METRIC = "BPMN element transitions/sec (+ completed instances/sec) per node; % HBM roofline"
 
 
@@ -285,8 +285,9 @@ def roofline(tot, steps, cfg, n):
                       "bytes (the launch writes no element-instance rows per transition)"))
     if tot["path"] == 0 and tot["process_ms"] > 0:
         b = (BYTES_PER_TRANSITION * tot["transitions"] + tot["merge_bytes"] + tot["cond_bytes"]) / steps
-        cands.append(("zbg::k_process (+ k_scan, k_emit, k_merge, k_cond: every wave kernel)", tot["kernel_ms"] / steps, b,
-                      "SURVEY §8d: 96 B per transition + merge + condition bytes over all wave kernels"))
+        cands.append(("zbg::k_wave (fused process / scan / emit, + k_merge / k_cond / k_subscribe: every wave kernel)",
+                      tot["kernel_ms"] / steps, b,
+                      "SURVEY §8d: 96 B per transition + merge + condition bytes over all wave kernels of the step"))
     name, ms, b, model = max(cands, key=lambda c: c[1])
     achieved = b / (ms / 1e3) / 1e9
     traffic, pmc_kernel = load_traffic("%s_%d" % (cfg, n), name.split(" ")[0].split("<")[0])
@@ -294,11 +295,21 @@ def roofline(tot, steps, cfg, n):
          "traffic": traffic, "kernel": name, "avg_launch_us": ms * 1e3, "alg_bytes_per_launch": b,
          "alg_bytes_model": model,
          "traffic_note": ("HBM bytes per launch of %s from rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (separate --pmc "
-                          "passes, profiles/r02/pmc_%s_%d.json)" % (pmc_kernel, cfg, n)) if traffic else
+                          "passes, profiles/r03/pmc_%s_%d.json)" % (pmc_kernel, cfg, n)) if traffic else
                          "no committed PMC passes for this workload"}
     r["other_kernels"] = [{"kernel": c[0], "avg_launch_us": c[1] * 1e3, "alg_bytes_per_launch": c[2],
                            "achieved": c[2] / (c[1] / 1e3) / 1e9, "frac": c[2] / (c[1] / 1e3) / 1e9 / HBM_PEAK_GBS}
                           for c in cands if c[0] != name]
+    # BASELINE.md §3 / SURVEY §8d: the whole path priced by its algorithmic bytes -- 96 B per transition + the
+    # payload terms (merges, condition payloads) -- over the step's wall time (drain included)
+    if tot.get("elapsed"):
+        pb = (BYTES_PER_TRANSITION * tot["transitions"] + tot["merge_bytes"] + tot["cond_bytes"]) / steps
+        pa = pb / (tot["elapsed"] / steps) / 1e9
+        r["path_bytes_per_step"] = pb
+        r["path_achieved"] = pa
+        r["path_frac"] = pa / HBM_PEAK_GBS
+        r["path_note"] = ("BASELINE.md §3: (96 B x transitions + merge + condition payload bytes) / step wall time / "
+                          "8 TB/s; the step also writes the serialized record stream, which this model does not price")
     return r
 
 
@@ -402,6 +413,11 @@ def extras(a, barrier):
     out["c2_wave_only"] = {"value": t["transitions"] / t["elapsed"], "ms_per_step": t["elapsed"] * 1e3 / 3,
                            "stepping_ms": t["step_s"] * 1e3 / 3, "drain_ms": t["drain_s"] * 1e3 / 3,
                            "roofline": roofline(t, 3, "c2w", 1_000_000), "workload": t["desc"] + " (wave pipeline)"}
+    t = run_workload("c3", 10_000_000, b, 0, 1, 0, barrier, 3, 1)
+    out["c3_wave_only"] = {"value": t["transitions"] / t["elapsed"], "ms_per_step": t["elapsed"] * 1e3 / 3,
+                           "stepping_ms": t["step_s"] * 1e3 / 3, "drain_ms": t["drain_s"] * 1e3 / 3,
+                           "roofline": roofline(t, 3, "c3w", 10_000_000),
+                           "workload": t["desc"] + " (general wave pipeline, no trajectory path)"}
     t = run_workload("c4", 1_000_000, a, 0, 1, 0, barrier, 3, 1)
     out["c4"] = {"value": t["transitions"] / t["elapsed"], "ms_per_step": t["elapsed"] * 1e3 / 3,
                  "stepping_ms": t["step_s"] * 1e3 / 3, "drain_ms": t["drain_s"] * 1e3 / 3,

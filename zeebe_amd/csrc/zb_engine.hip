@@ -183,6 +183,9 @@ struct zb_engine {
   // class batches (zb_traj.hip k_cls_*): the model's exclusive splits as outcome-key digits
   bool cls_ok = false;            // split outcome keys fit 8 bits and CLS_MAX_SPLITS splits
   int nsplits = 0;
+  int cls_nq = 0;                 // distinct fast queries of the split conditions (k_cls_classify extraction)
+  uint16_t cls_q[CLS_QMAX] = {};
+  uint32_t cls_key_off[CLS_QMAX] = {}, cls_key_len[CLS_QMAX] = {};
   uint32_t split_elem[CLS_MAX_SPLITS] = {}, split_stride[CLS_MAX_SPLITS] = {};
   ClsPlan* c_plan = nullptr;
   uint64_t cls_cap = 0;           // instances the class buffers hold
@@ -576,6 +579,12 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
     p.wcls = e->c_wcls;
     if (!p.io) HIPCHECK(e, hipMemsetAsync(e->c_perm, 0xff, cls_slot_bound((uint64_t)n, nwg) * sizeof(uint32_t), e->stream));
     p.nsplits = e->nsplits;
+    p.cls_nq = e->cls_nq;
+    for (int j = 0; j < CLS_QMAX; j++) {
+      p.cls_q[j] = e->cls_q[j];
+      p.cls_key_off[j] = e->cls_key_off[j];
+      p.cls_key_len[j] = e->cls_key_len[j];
+    }
     for (int k = 0; k < CLS_MAX_SPLITS; k++) {
       p.split_elem[k] = e->split_elem[k];
       p.split_stride[k] = e->split_stride[k];
@@ -1204,6 +1213,38 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
     stride *= radix;
   }
   if (!e->cls_ok) e->nsplits = 0;
+  // the condition queries the class path extracts in one scan: every path operand of every split's conditions,
+  // all of the [ROOT, MAP_KEY k] form, at most CLS_QMAX distinct (else each operand runs its own query)
+  e->cls_nq = 0;
+  bool ext_ok = e->cls_ok;
+  for (int k = 0; k < e->nsplits && ext_ok; k++) {
+    const DevElem& el = e->model.elems[e->split_elem[k]];
+    for (uint32_t c = 0; c < el.cond_count && ext_ok; c++) {
+      const DevElem& flow = e->model.elems[e->model.cond_flows[el.cond_begin + c]];
+      if (flow.cond_prog == NO_REF) continue;
+      for (uint32_t pc = flow.cond_prog; 2 * pc + 1 < e->model.code.size(); pc++) {
+        const uint32_t w0 = e->model.code[2 * pc], w1 = e->model.code[2 * pc + 1];
+        if ((w0 & 0xff) == PC_END) break;
+        if ((w0 & 0xff) != PC_CMP) continue;
+        for (int side = 0; side < 2 && ext_ok; side++) {
+          if (!((w0 >> (12 + side)) & 1)) continue;
+          const uint16_t q = (uint16_t)(side ? w1 >> 16 : w1 & 0xffff);
+          const DevQuery& dq = e->model.queries[q];
+          if (!dq.fast) { ext_ok = false; break; }
+          bool seen = false;
+          for (int j = 0; j < e->cls_nq; j++) seen = seen || e->cls_q[j] == q;
+          if (seen) continue;
+          if (e->cls_nq == CLS_QMAX) { ext_ok = false; break; }
+          const DevFilter& f = e->model.filters[dq.first + 1];
+          e->cls_q[e->cls_nq] = q;
+          e->cls_key_off[e->cls_nq] = f.key_off;
+          e->cls_key_len[e->cls_nq] = f.key_len;
+          e->cls_nq++;
+        }
+      }
+    }
+  }
+  if (!ext_ok) e->cls_nq = 0;
   return upload_model(e);
 }
 

@@ -1170,12 +1170,73 @@ __device__ __forceinline__ bool load_operand_k(const TrajParams& P, bool is_path
   return true;
 }
 
+// The operands of every split condition in one scan of the CREATE payload: query_fast ([ROOT, MAP_KEY k]: every
+// top-level value under key k) for all the model's condition keys at once. The scan (token walk, value skips,
+// the container-key check) does not depend on the key, so each key's (count, first result) -- and whether the
+// scan is unsupported -- is what query_fast gives for that key alone.
+struct Extract {
+  uint32_t cnt[CLS_QMAX], pos[CLS_QMAX], len[CLS_QMAX];
+  bool ok;
+};
+__device__ __forceinline__ void extract_fast(const TrajParams& P, const uint8_t* d, uint32_t n, Extract& x) {
+#pragma unroll
+  for (int j = 0; j < CLS_QMAX; j++) { x.cnt[j] = 0; x.pos[j] = 0; x.len[j] = 0; }
+  Tok t;
+  if (!read_tok(d, n, t)) { x.ok = n == 0; return; }
+  x.ok = true;
+  if (t.type != TT_MAP) return;  // root filter needs a container; arrays give no key matches
+  uint32_t pos = t.total;
+  for (uint32_t i = 0; i < t.len; i++) {
+    Tok k;
+    if (pos >= n || !read_tok(d + pos, n - pos, k)) { x.ok = false; return; }
+    const uint32_t kpos = pos;
+    pos += k.total;
+    const uint32_t vend = skip_value(d, n, pos);
+    if (vend == 0xffffffffu) { x.ok = false; return; }
+    if (k.type == TT_STRING) {
+#pragma unroll
+      for (int j = 0; j < CLS_QMAX; j++) {
+        if (j < P.cls_nq && k.len == P.cls_key_len[j] && bytes_eq(d + kpos + k.hdr, P.pool + P.cls_key_off[j], k.len)) {
+          if (x.cnt[j] == 0) { x.pos[j] = pos; x.len[j] = vend - pos; }
+          x.cnt[j]++;
+        }
+      }
+    } else if (k.type == TT_MAP || k.type == TT_ARRAY) {
+      x.ok = false;  // container map keys: the reference's traversal would descend; not supported here
+      return;
+    }
+    pos = vend;
+  }
+}
+// load_operand_k with the query results taken from the extraction
+__device__ __forceinline__ bool load_operand_x(const TrajParams& P, bool is_path, uint32_t idx, const uint8_t* doc,
+                                               const Extract& x, Operand& o, CondOut& out, bool& unsupported) {
+  if (!is_path) {
+    const DevConst c = kload(P.consts, idx);
+    o.type = c.type; o.bval = c.bval; o.ival = c.ival; o.fval = c.fval; o.s = P.pool + c.str_off; o.slen = c.str_len;
+    return true;
+  }
+  if (!x.ok) { unsupported = true; return false; }
+  uint32_t cnt = 0, rpos = 0, rlen = 0;
+#pragma unroll
+  for (int j = 0; j < CLS_QMAX; j++)
+    if (j < P.cls_nq && P.cls_q[j] == idx) { cnt = x.cnt[j]; rpos = x.pos[j]; rlen = x.len[j]; }
+  if (cnt == 0) { out.err = EC_PATH_NO_RESULT; out.q = (uint16_t)idx; return false; }
+  if (cnt > 1) { out.err = EC_PATH_MULTI; out.q = (uint16_t)idx; return false; }
+  Tok t;
+  if (!read_tok(doc + rpos, rlen, t)) { unsupported = true; return false; }
+  o.type = t.type; o.bval = t.bval; o.ival = t.ival; o.fval = t.fval;
+  o.s = doc + rpos + t.hdr; o.slen = t.len;
+  return true;
+}
+
 // The json-el VM (eval_condition, zb_devlib.hpp) as one wave-uniform sweep over the program: every lane
 // runs the same program and its jumps only go forward (zb_model.cpp emit), so instruction pc is
 // fetched once per wave through the scalar cache and executed by the lanes whose own pc is there.
 // Same results, errors and short-circuit behaviour as eval_condition.
+template <bool EXT>
 __device__ __forceinline__ bool eval_condition_sweep(const TrajParams& P, uint32_t pc0, const uint8_t* doc, uint32_t n,
-                                                     CondOut& out, bool& unsupported) {
+                                                     const Extract& ext, CondOut& out, bool& unsupported) {
   bool r = false, done = false;
   uint32_t mine = pc0;
   out.err = 0;
@@ -1191,8 +1252,11 @@ __device__ __forceinline__ bool eval_condition_sweep(const TrajParams& P, uint32
     mine = pc + 1;
     const uint32_t op = (w0 >> 8) & 0xf;
     Operand x, y;
-    if (!load_operand_k(P, (w0 >> 12) & 1, w1 & 0xffff, doc, n, x, out, unsupported) ||
-        !load_operand_k(P, (w0 >> 13) & 1, w1 >> 16, doc, n, y, out, unsupported)) {
+    const bool lx = EXT ? load_operand_x(P, (w0 >> 12) & 1, w1 & 0xffff, doc, ext, x, out, unsupported)
+                        : load_operand_k(P, (w0 >> 12) & 1, w1 & 0xffff, doc, n, x, out, unsupported);
+    const bool ly = lx && (EXT ? load_operand_x(P, (w0 >> 13) & 1, w1 >> 16, doc, ext, y, out, unsupported)
+                               : load_operand_k(P, (w0 >> 13) & 1, w1 >> 16, doc, n, y, out, unsupported));
+    if (!lx || !ly) {
       done = true;
       continue;
     }
@@ -1228,7 +1292,10 @@ __device__ __forceinline__ bool eval_condition_sweep(const TrajParams& P, uint32
 }
 
 // outcome key of one CREATE payload: every split of the model, digit = first true condition / none / error
+template <bool EXT>
 __device__ __forceinline__ uint32_t outcome_key(const TrajParams& P, const uint8_t* doc, uint32_t len) {
+  Extract ext;
+  if (EXT) extract_fast(P, doc, len, ext);
   uint32_t key = 0;
   for (int k = 0; k < P.nsplits; k++) {
     const ElemCtl el = elem_ctl(P, P.split_elem[k]);
@@ -1239,7 +1306,7 @@ __device__ __forceinline__ uint32_t outcome_key(const TrajParams& P, const uint8
       bool unsup = false;
       const uint16_t flow = K(P.cond_flows)[el.cond_begin() + c];
       const uint32_t prog = K(P.elems)[flow].cond_prog;
-      const bool res = eval_condition_sweep(P, prog, doc, len, co, unsup);
+      const bool res = eval_condition_sweep<EXT>(P, prog, doc, len, ext, co, unsup);
       if (unsup || co.err) { o = cc + 1; break; }
       if (res) { o = c; break; }
     }
@@ -1268,7 +1335,8 @@ __global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
     uint32_t key = 0;
     if (((len + 11) & ~7u) <= CL_STRIDE * 4) {  // (stage_copy writes whole 8-byte words)
       stage_copy(pp, len, s_doc + t * CL_STRIDE);
-      key = outcome_key(P, (const uint8_t*)(s_doc + t * CL_STRIDE) + 4, len);
+      const uint8_t* doc = (const uint8_t*)(s_doc + t * CL_STRIDE) + 4;
+      key = P.cls_nq ? outcome_key<true>(P, doc, len) : outcome_key<false>(P, doc, len);
     } else {
       for (int k = 0; k < P.nsplits; k++) key += (elem_ctl(P, P.split_elem[k]).cond_count() + 1) * P.split_stride[k];
     }
