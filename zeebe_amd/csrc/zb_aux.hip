@@ -44,6 +44,11 @@ __global__ void __launch_bounds__(256) k_merge(WaveParams P) {
     if (!merge_docs(sp + 4, ns, tp + 4, nt, o, unsup)) err |= DE_BAD_PAYLOAD;
     else if (unsup || o.n > j.cap) err |= DE_UNSUPPORTED;
     *(uint32_t*)dst = o.n;
+    if (j.pos >= 0 && P.vconst) {  // the ELEMENT_COMPLETED record carrying the result: its value length hint
+      const zb_rec d = P.log[j.pos];
+      const ValueConst vc = P.vconst[d.elem];
+      P.vlen[j.pos] = vc.wf + mp_int_len(d.inst_key) + mp_int_len(d.scope_key) + mp_bin_len(o.n);
+    }
     merges += 1;
     bytes += ns + nt + o.n;
   }

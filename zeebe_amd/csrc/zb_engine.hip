@@ -400,6 +400,7 @@ WaveParams wave_params(zb_engine* e) {
   p.queries = e->d_queries.p;
   p.filters = e->d_filters.p;
   p.pool = e->d_pool.p;
+  p.vconst = e->d_vconst.p;
   p.maps = e->d_maps.p;
   p.segs = e->d_segs.p;
   p.mapres = e->mapres;

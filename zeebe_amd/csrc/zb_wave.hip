@@ -77,7 +77,43 @@ __device__ __forceinline__ Slot& add_slot(TState& t) {
   Slot& s = t.s[t.ns++];
   s.flags = 0; s.ord = 0; s.rord = 0;
   s.pad = (uint8_t)t.src_off;
+  s.plen = VLEN_UNKNOWN;
   return s;
+}
+
+// ---- value length hints (vlen) of the records a wave writes, so that the drain's size pass reads 4 bytes per
+// record instead of every record's payload document: a follow-up carrying its source record's payload takes
+// the source's payload length, recovered from the source's own hint (the inverse of the emit formula, the
+// value's constant part + key lengths + bin header); the rest read the document's length word.
+__device__ __forceinline__ uint32_t formula_base(const WaveParams& P, const zb_rec& d) {
+  const ValueConst vc = P.vconst[d.elem];
+  return (kind_vt(d.kind) == ZB_VT_JOB ? vc.job : vc.wf) + mp_int_len(d.inst_key) + mp_int_len(d.scope_key);
+}
+__device__ __forceinline__ uint32_t payload_len_of(const WaveParams& P, const zb_rec& rec, int64_t pos) {
+  if (kind_vt(rec.kind) == ZB_VT_INCIDENT) return VLEN_UNKNOWN;  // (payload: an incident detail blob)
+  if (fast_kind(rec) && P.vconst) {
+    const uint32_t v = P.vlen[pos];
+    if (v != VLEN_UNKNOWN) {
+      const uint32_t x = v - formula_base(P, rec);  // mp_bin_len(plen)
+      return x <= 257 ? x - 2 : (x <= 65538 ? x - 3 : x - 5);
+    }
+  }
+  return *(const uint32_t*)(P.arena + (uint64_t)rec.payload * 8);
+}
+// after process_record(rec at pos) staged slots [ns0, t.ns): their payload lengths
+__device__ __forceinline__ void annotate_slots(const WaveParams& P, TState& t, int ns0, const zb_rec& rec, int64_t pos) {
+  uint32_t rl = VLEN_UNKNOWN;
+  bool have = false;
+  for (int k = ns0; k < t.ns; k++) {
+    Slot& s = t.s[k];
+    if (s.flags & (SF_PAY_MERGED | SF_PAY_DETAIL) || !fast_kind(s.d)) continue;
+    if (s.d.payload == rec.payload && !(rec.kind & KIND_RAW)) {
+      if (!have) { rl = payload_len_of(P, rec, pos); have = true; }
+      s.plen = rl;
+    } else {
+      s.plen = *(const uint32_t*)(P.arena + (uint64_t)s.d.payload * 8);
+    }
+  }
 }
 
 __device__ __forceinline__ void wf_event(TState& t, Slot& s, uint8_t intent, uint8_t cont) {
@@ -787,12 +823,15 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
       // a batch never spans generations, so its tail may lie past a chunk end (skipped there as cont)
       const uint64_t lk = P.links[r];
       process_record(P, rec, r, (uint32_t)lk, (uint32_t)(lk >> 32), t);
+      annotate_slots(P, t, 0, rec, r);
       for (int64_t q = r + 1; q < gen_end && q < r + 4; q++) {
         const zb_rec rec2 = P.log[q];
         if (!grouped(rec2)) break;
         const uint64_t lk2 = P.links[q];
         t.src_off = (uint32_t)(q - r);
+        const int ns0 = t.ns;
         process_record(P, rec2, q, (uint32_t)lk2, (uint32_t)(lk2 >> 32), t);
+        annotate_slots(P, t, ns0, rec2, q);
       }
     }
     // stage the follow-ups and the count word
@@ -1047,7 +1086,12 @@ __device__ __forceinline__ void emit_item(const WaveParams& P, const Chunk& c, i
       if (bump + inf.m_bytes > P.arena_cap) err |= DE_ARENA_FULL;
       else {
         merged_ref = (uint32_t)(bump >> 3);
-        if (merge_j < P.job_cap) P.merge_jobs[par + merge_j] = MergeJob{merged_ref, inf.m_src, inf.m_tgt, inf.m_len};
+        if (merge_j < P.job_cap) {
+          int64_t mpos = -1;  // the slot that carries the result
+          for (int k = 0; k < ns; k++)
+            if (sl[k].flags & SF_PAY_MERGED) mpos = (int64_t)out_rec + k;
+          P.merge_jobs[par + merge_j] = MergeJob{merged_ref, inf.m_src, inf.m_tgt, inf.m_len, mpos};
+        }
       }
       bump += inf.m_bytes;
     }
@@ -1098,7 +1142,7 @@ __device__ __forceinline__ void emit_item(const WaveParams& P, const Chunk& c, i
       P.log[out_rec] = s.d;
       P.links[out_rec] = (uint64_t)s.rself | ((uint64_t)s.rscope << 32);
       P.srcd[out_rec] = (uint32_t)(out_rec - (uint64_t)(c.begin + i + s.pad));
-      P.vlen[out_rec] = VLEN_UNKNOWN;
+      P.vlen[out_rec] = (s.plen != VLEN_UNKNOWN && P.vconst) ? formula_base(P, s.d) + mp_bin_len(s.plen) : VLEN_UNKNOWN;
       if (s.flags & SF_COND_JOB) {
         if (cond_j < P.job_cap) P.cond_jobs[par + cond_j] = out_rec;
         cond_j++;
@@ -1264,12 +1308,15 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
       if (!grouped(rec)) {
         const uint64_t lk = P.links[r];
         process_record(P, rec, r, (uint32_t)lk, (uint32_t)(lk >> 32), t);
+        annotate_slots(P, t, 0, rec, r);
         for (int64_t q = r + 1; q < gen_end && q < r + 4; q++) {
           const zb_rec rec2 = P.log[q];
           if (!grouped(rec2)) break;
           const uint64_t lk2 = P.links[q];
           t.src_off = (uint32_t)(q - r);
+          const int ns0 = t.ns;
           process_record(P, rec2, q, (uint32_t)lk2, (uint32_t)(lk2 >> 32), t);
+          annotate_slots(P, t, ns0, rec2, q);
         }
       }
     }
