@@ -45,12 +45,13 @@ METRIC = "BPMN element transitions/sec (+ completed instances/sec) per node; % H
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=("c2", "c3", "c4", "c5"), default="c3")
+    ap.add_argument("--config", choices=("c1", "c2", "c3", "c4", "c5"), default="c3")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--instances", type=int, default=0, help="per GPU (default: C3 10,000,000, C2/C4/C5 1,000,000)")
     ap.add_argument("--tasks", type=int, default=20)
     ap.add_argument("--cpu-sample", type=int, default=0, help="instances in the 1-thread oracle sample (0: default)")
+    ap.add_argument("--cpu-partitions", type=int, default=0, help="C5: oracle partitions of the CPU sample (0: 4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the extra C2 wave-only / C4 lines")
     ap.add_argument("--no-drain", action="store_true", help="device stepping only (not the contract's step)")
@@ -70,6 +71,12 @@ def workload(cfg, n, start, tasks=20):
         return (bpmn.xor_workflow().to_xml(), "xor", blob, offs, {},
                 "C3: exclusive gateways with json-el conditions over msgpack payloads, %d concurrent instances "
                 "per GPU" % n)
+    if cfg == "c1":
+        blob, offs = workloads.order_payloads(n, start=start)
+        return (bpmn.chain_workflow(1).to_xml(), "chain", blob, offs,
+                {"t1": b"\x81" + workloads.mp_str("step") + workloads.mp_int(1)},
+                "C1: start -> one service task -> end, %d instances, canonical job harness (BASELINE configs[0], "
+                "the reference's CPU-runnable case)" % n)
     if cfg == "c2":
         blob, offs = workloads.order_payloads(n, start=start)
         jp = {"t%d" % k: b"\x81" + workloads.mp_str("step") + workloads.mp_int(k) for k in range(1, tasks + 1)}
@@ -85,15 +92,15 @@ def workload(cfg, n, start, tasks=20):
     raise ValueError(cfg)
 
 
-RECS_PER_INST = {"c2": lambda t: 2 + 8 + 5 * t + 3 * t, "c3": lambda t: 16, "c4": lambda t: 200}
+RECS_PER_INST = {"c1": lambda t: 18, "c2": lambda t: 2 + 8 + 5 * t + 3 * t, "c3": lambda t: 16, "c4": lambda t: 200}
 
 
 def make_engine(cfg, n, a, rank, world, local_rank):
     from zeebe_amd.engine import Engine
 
     recs = RECS_PER_INST[cfg](a.tasks)
-    rows = {"c2": n * (a.tasks + 2), "c3": 1 << 20, "c4": n * 20}[cfg]
-    arena = {"c2": n * (48 + 48 * a.tasks), "c3": n * 64, "c4": n * 1200}[cfg] + (64 << 20)
+    rows = {"c1": n * 3, "c2": n * (a.tasks + 2), "c3": 1 << 20, "c4": n * 20}[cfg]
+    arena = {"c1": n * 96, "c2": n * (48 + 48 * a.tasks), "c3": n * 64, "c4": n * 1200}[cfg] + (64 << 20)
     return Engine(device=0 if a.same_device else local_rank, partition_id=rank, partition_count=world,
                   log_capacity=int(n * recs), row_capacity=int(rows), arena_bytes=int(arena), wave_only=a.wave_only)
 
@@ -105,6 +112,7 @@ def run_workload(cfg, n, a, rank, world, local_rank, barrier, steps, warmup, dra
     for act, p in jp.items():
         eng.set_job_payload(100, act, p)
     eng.create_packed(pid, blob, offs)
+    create_bytes = len(blob) + 4 * n  # the CREATE payload documents ([u32 len][bytes]) in the arena
     del blob
 
     def one_step():
@@ -124,7 +132,8 @@ def run_workload(cfg, n, a, rank, world, local_rank, barrier, steps, warmup, dra
     barrier()
     tot = dict(transitions=0, completed=0, written=0, merges=0, merge_bytes=0, cond_bytes=0, kernel_ms=0.0,
                process_ms=0.0, emit_ms=0.0, aux_ms=0.0, main_ms=0.0, launches=0, waves=0, step_s=0.0, drain_s=0.0,
-               ser_write_ms=0.0, ser_size_ms=0.0, value_bytes=0, payload_bytes=0, drained=0, path=0, generic_tiles=0)
+               ser_write_ms=0.0, ser_size_ms=0.0, value_bytes=0, payload_bytes=0, drained=0, path=0, generic_tiles=0,
+               template_drain=0, create_bytes=0, instances=n)
     t0 = time.perf_counter()
     for _ in range(steps):
         st, ser, ts, td = one_step()
@@ -151,9 +160,11 @@ def run_workload(cfg, n, a, rank, world, local_rank, barrier, steps, warmup, dra
             tot["payload_bytes"] += ser["payload_bytes"]
             tot["drained"] += ser["records"]
             tot["generic_tiles"] += ser["generic_tiles"]
+            tot["template_drain"] += ser["template_drain"]
     barrier()
     tot["elapsed"] = time.perf_counter() - t0
     tot["desc"] = desc
+    tot["create_bytes"] = create_bytes
     if pcie and drain:
         tot["pcie"] = pcie_step(eng, n, one_step)
     eng.close()
@@ -217,18 +228,27 @@ def cpu_baseline_line(cfg, tasks, sample):
     res = {}
     for k in sorted({1, threads}):
         per = sample if k == 1 else max(sample // 2, 1)
-        parts = [_oracle_partition(cfg, per, i * per, tasks) for i in range(k)]
+        parts = [None] * k
         counts = [0] * k
+        ready = threading.Barrier(k + 1)
 
         def run(i):
+            # each partition is built on its own thread, so its state lives in that thread's malloc arena (built
+            # on the main thread, every free from the workers went through the main arena's lock)
+            w = _oracle_partition(cfg, per, i * per, tasks)  # untimed warm-up: faults in the thread's arena
+            w._L.zbref_run_timed(w._h, ctypes.byref(ctypes.c_int64()))
+            w.close()
+            parts[i] = _oracle_partition(cfg, per, i * per, tasks)
+            ready.wait()
             nrec = ctypes.c_int64()
             parts[i]._L.zbref_run_timed(parts[i]._h, ctypes.byref(nrec))
             counts[i] = nrec.value
 
         ths = [threading.Thread(target=run, args=(i,)) for i in range(k)]
-        t0 = time.perf_counter()
         for t in ths:
             t.start()
+        ready.wait()
+        t0 = time.perf_counter()
         for t in ths:
             t.join()
         wall = time.perf_counter() - t0
@@ -267,7 +287,16 @@ def load_traffic(tag, kernel_prefix):
 def roofline(tot, steps, cfg, n):
     """Dominant kernel of the step: the drain's write pass or the main emit launch, by device time."""
     cands = []
-    if tot["ser_write_ms"] > 0:
+    if tot["ser_write_ms"] > 0 and tot["template_drain"] == steps:
+        # the template drain (zb_tdrain.hip): per launch every drained record's header and value written, and per
+        # instance its CREATE descriptor and CREATE payload document read once (the traces and generation bases
+        # are a few KB, read from the scalar cache)
+        b = (tot["drained"] * HDR_BYTES + tot["value_bytes"] + steps * (tot["instances"] * DESC_BYTES +
+                                                                          tot["create_bytes"])) / steps
+        cands.append(("zbg::k_tdrain_write", tot["ser_write_ms"] / steps, b,
+                      "24 B header + value bytes written per drained record + 32 B CREATE descriptor and the CREATE "
+                      "payload document read per instance"))
+    elif tot["ser_write_ms"] > 0:
         # per launch: every drained record's descriptor read + header write, its value bytes written and the
         # payload documents copied into them read (SURVEY §8d payload term)
         b = (tot["drained"] * (DESC_BYTES + HDR_BYTES) + tot["value_bytes"] + tot["payload_bytes"]) / steps
@@ -319,6 +348,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # Load libzbgpu.so before torch: its DT_NEEDED HIP runtime and RCCL (/opt/rocm/lib) are then the copies the
+    # process binds, so the engine's communicator runs on the system RCCL, not the one torch bundles
+    # (zb_rccl_library reports the file; C5 prints it).
+    from zeebe_amd.engine import lib
+
+    lib()
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -328,7 +363,7 @@ def main():
         # (libzbgpu.so) drives its GPU through the system ROCm runtime.
         dist.init_process_group("gloo")
     if a.instances == 0:
-        a.instances = 10_000_000 if a.config == "c3" else 1_000_000
+        a.instances = {"c3": 10_000_000, "c1": 10_000}.get(a.config, 1_000_000)
     if a.config == "c5":
         return run_c5(a, rank, world, local_rank, dist)
 
@@ -395,7 +430,7 @@ def main():
         if world == 1 and not a.no_extras and a.config == "c3":
             out["extras"] = extras(a, barrier)
         if world == 1 and not a.no_cpu_baseline:
-            sample = a.cpu_sample or {"c3": 400_000, "c2": 30_000, "c4": 20_000}[a.config]
+            sample = a.cpu_sample or {"c1": 10_000, "c3": 400_000, "c2": 30_000, "c4": 20_000}[a.config]
             out["cpu_baseline"] = cpu_baseline_line(a.config, a.tasks, sample)
         print(json.dumps(out))
     if dist is not None:

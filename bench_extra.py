@@ -37,11 +37,47 @@ def _emit(out, rank):
         print(json.dumps(out))
 
 
+def cpu_baseline_c5(world, n_sample):
+    """The oracle (C++ restatement) on a bounded C5 sample: `world` oracle partitions in one process on one
+    thread (zeebe_amd.cluster.LocalCluster: the same canonical schedule), timed from the first CREATE to the
+    quiescence after the publishes."""
+    import msgpack
+
+    from oracle import zbref
+    from zeebe_amd import bpmn, cluster
+
+    P = max(world, 1)
+    parts = [zbref.OraclePartition(p, P) for p in range(P)]
+    xml = bpmn.message_workflow().to_xml()
+    for p in parts:
+        p.deploy(xml, 100, 1)
+    N = n_sample * P
+    lc = cluster.LocalCluster(parts)
+    cks = [b"order-%d" % i for i in range(N)]
+    paid = msgpack.packb({"paid": True})
+    t0 = time.perf_counter()
+    for i in range(N):
+        parts[i % P].create("msg", msgpack.packb({"orderId": "order-%d" % i}))
+    lc.settle()
+    lc.publish(b"order", cks, [paid] * N)
+    wall = time.perf_counter() - t0
+    tr = sum(p.counters()["transitions"] for p in parts)
+    comp = sum(p.counters()["completed"] for p in parts)
+    for p in parts:
+        p.close()
+    from bench import cpu_model
+
+    return {"value": tr / wall, "unit": "transitions/s", "cores": 1, "kind": "port",
+            "sample": "C5, %d instances over %d oracle partitions in one process (LocalCluster schedule, one thread; "
+                      "includes the Python exchange driver): %.2f s" % (N, P, wall),
+            "cpu_model": cpu_model(), "completed_instances_per_s": comp / wall}
+
+
 def run_c5(a, rank, world, local_rank, dist, barrier, reduce_max, reduce_sum):
     import msgpack
 
     from zeebe_amd import bpmn, cluster
-    from zeebe_amd.engine import Engine
+    from zeebe_amd.engine import Engine, rccl_library
 
     n = a.instances  # per partition
     N = n * world
@@ -61,6 +97,7 @@ def run_c5(a, rank, world, local_rank, dist, barrier, reduce_max, reduce_sum):
     ck_off[1:] = np.cumsum([len(c) for c in my_msgs])
     pl_off = np.arange(len(my_msgs) + 1, dtype=np.uint64) * len(paid)
     ck_blob, pl_blob = b"".join(my_msgs), paid * len(my_msgs)
+    tot = dict(records=0, value_bytes=0, transitions=0, ser_ms=0.0)
 
     def step():
         eng.reset()
@@ -70,7 +107,9 @@ def run_c5(a, rank, world, local_rank, dist, barrier, reduce_max, reduce_sum):
         if my_msgs:
             eng.publish_packed(b"order", ck_blob, ck_off, pl_blob, pl_off, 3600000)
         dc.settle()
-        return time.perf_counter() - t
+        ser = eng.serialize(0, eng.log_size())  # the drain: every record the partition's log holds after the step
+        dt = time.perf_counter() - t
+        return dt, ser
 
     for _ in range(a.warmup):
         step()
@@ -78,17 +117,35 @@ def run_c5(a, rank, world, local_rank, dist, barrier, reduce_max, reduce_sum):
     el = 0.0
     for _ in range(a.steps):
         barrier()
-        el += reduce_max(step())
+        dt, ser = step()
+        el += reduce_max(dt)
+        tot["records"] += ser["records"]
+        tot["value_bytes"] += ser["value_bytes"]
+        tot["ser_ms"] += ser["write_kernel_ms"] + ser["size_kernel_ms"]
     completed = reduce_sum(eng.counters()["completed"])
     assert completed == N, (completed, N)
     tr = 13 * N * a.steps  # 13 WORKFLOW_INSTANCE events per instance
-    _emit({"metric": "BPMN element transitions/sec (+ completed instances/sec) per node; % HBM roofline",
+    path_bytes = (BYTES_PER_TRANSITION * 13 + 2 * len(paid)) * N  # + P per correlation-key extraction / merge (approx.)
+    ms = el * 1e3 / a.steps
+    out = {"metric": "BPMN element transitions/sec (+ completed instances/sec) per node; % HBM roofline",
            "value": tr / el, "unit": "transitions/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-           "ms_per_step": el * 1e3 / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
            "dtype": "int64", "data": "synthetic (SURVEY §8d C5: orderId 'order-<i>', payload {paid: true})",
            "config": {"workload": "C5: message catch correlated across partitions (RCCL exchange), "
                                   "%d instances per GPU" % n, "instances_per_gpu": n, "partitions": world,
-                      "parallelism": "partition-per-gpu", "exchange": "RCCL ncclSend/ncclRecv (engine)"},
+                      "parallelism": "partition-per-gpu", "exchange": "RCCL ncclSend/ncclRecv (engine)",
+                      "timed_step": "CREATE injection to quiescence, exchange rounds, publish to quiescence, "
+                                    "zb_serialize of every record of the partition's log (values + headers, in HBM)"},
            "completed_instances_per_s": N * a.steps / el,
-           "note": "timed region: CREATE injection to quiescence, exchange rounds, publish to quiescence; "
-                   "excludes payload generation and hash routing of the published keys"}, rank)
+           "drained_records_per_step_rank0": tot["records"] / a.steps,
+           "rccl_library": rccl_library(),
+           "roofline": {"bound": "hbm", "achieved": path_bytes / (ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": path_bytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                        "kernel": "whole step (host-driven exchange rounds; no single dominant kernel)",
+                        "alg_bytes_model": "SURVEY §8d: 96 B per transition + payload terms, all partitions",
+                        "path_frac": path_bytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS},
+           "note": "excludes payload generation and hash routing of the published keys (input preparation)"}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_c5(max(world, 4) if a.cpu_partitions == 0 else a.cpu_partitions,
+                                              a.cpu_sample or 5000)
+    _emit(out, rank)

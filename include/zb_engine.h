@@ -251,6 +251,9 @@ int zb_outbox_take(zb_engine* e, int kind, uint8_t* dst, size_t cap, int dst_on_
  * per engine, rank = partition id. zb_comm_unique_id on one rank; the 128-byte id travels to the
  * others out of band (zeebe_amd/cluster.py uses the torch.distributed control plane). */
 int zb_comm_unique_id(uint8_t id[128]);
+/* The RCCL library file the communicator runs on (the engine links /opt/rocm/lib/librccl.so; a process that
+ * loaded another copy of the library first -- e.g. torch's -- resolves to that one: load libzbgpu.so first). */
+const char* zb_rccl_library(void);
 int zb_comm_init(zb_engine* e, const uint8_t id[128], int nranks, int rank);
 /* Collective: global[k] = sum over ranks of the pending commands of kind k+1 (ZB_XCHG_OPEN, _CORRELATE). */
 int zb_comm_pending(zb_engine* e, uint64_t global[2]);
@@ -292,6 +295,7 @@ typedef struct zb_serialize_stats {
   double write_kernel_ms;      /* write pass (headers + values; the whole single pass): the drain's kernel */
   double wall_ms;
   uint64_t generic_tiles;      /* 256-record tiles the generic write pass encoded (the rest: the fast pass) */
+  uint64_t template_drain;     /* 1: a deferred trajectory batch, encoded from its traces (no descriptors) */
 } zb_serialize_stats;
 int zb_serialize(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats* stats);
 /* headers: NULL or room for the batch's headers; values: NULL or values_len bytes from value byte

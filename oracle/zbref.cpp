@@ -25,6 +25,8 @@
 //                            (JOB CREATE command at its FIFO position -> JOB CREATED(k), JOB COMPLETED(k); job keys
 //                            from KeyGenerator(2, 5))
 // Positions are log sequence numbers (0-based record index); byte positions of the real log are out of scope.
+#include <malloc.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -1598,6 +1600,16 @@ struct zbref_record {
   uint8_t rejection_type;
   uint32_t value_len;
 };
+
+// The CPU baseline runs one oracle partition per thread. glibc's defaults (arenas grown and trimmed in small
+// steps, large vectors from mmap) put every partition's page faults and mprotect / munmap calls under the
+// process-wide mmap lock: 8 threads ran C1 as slowly as 1.5 threads' worth. Large arena steps, no trimming and
+// large vectors from the arena (with an untimed warm-up run per thread, bench.py) let them scale.
+__attribute__((constructor)) static void zbref_malloc_tuning() {
+  mallopt(M_MMAP_THRESHOLD, 32 << 20);
+  mallopt(M_TRIM_THRESHOLD, 1 << 30);
+  mallopt(M_TOP_PAD, 64 << 20);
+}
 
 extern "C" {
 

@@ -120,3 +120,93 @@ def test_size_pass_formula_matches_encoder():
     b = _drain(make, True, vlen_check=True, wave_only=True)
     assert a[0]["value_bytes"] == b[0]["value_bytes"]
     assert a[1] == b[1] and a[2] == b[2]
+
+
+# ---- the template drain (zb_tdrain.hip): a uniform / class batch left without descriptors by zb_step, encoded
+# straight from its traces by zb_serialize of exactly its records; vs the descriptor path (ZB_TMPL_DEFER=0)
+def _template_drain(make, defer):
+    from zeebe_amd.engine import Engine, zb_record_header
+
+    old = os.environ.get("ZB_TMPL_DEFER")
+    os.environ["ZB_TMPL_DEFER"] = "1" if defer else "0"
+    try:
+        e = Engine(log_capacity=1 << 22, row_capacity=1 << 16, arena_bytes=64 << 20)
+    finally:
+        if old is None:
+            del os.environ["ZB_TMPL_DEFER"]
+        else:
+            os.environ["ZB_TMPL_DEFER"] = old
+    n = make(e)
+    st = e.step()
+    assert st["quiescent"] and st["path"] in (1, 2), st
+    L = e.log_size()
+    ser = e.serialize(n, L - n)
+    vals = ctypes.create_string_buffer(max(ser["value_bytes"], 1))
+    hdrs = (zb_record_header * (L - n))()
+    e.drain_copy(ctypes.addressof(vals), 0, ser["value_bytes"], ctypes.addressof(hdrs))
+    out = dict(ser=ser, values=vals.raw[:ser["value_bytes"]], headers=bytes(hdrs))
+    # then the descriptors (materialized on demand) and the records API
+    out["desc"] = bytes(e.descriptors(0, L))
+    out["records"] = e.records(n)
+    out["counters"] = e.counters()
+    e.close()
+    return out
+
+
+def _simple_workflow():
+    return bpmn.Bpmn.create_executable_process("simple").start_event().end_event().done().to_xml()
+
+
+@pytest.mark.parametrize("shape", ["c3", "uniform"])
+def test_template_drain_matches_descriptor_drain(shape):
+    if shape == "c3":
+        cfg = workloads.CONFIGS["c3"]
+        blob, offs = cfg["payloads"](30000)
+
+        def make(e):
+            e.deploy(cfg["workflow"]().to_xml(), 100, 1)
+            e.create_packed(cfg["process"], blob, offs)
+            return 30000
+    else:
+        blob, offs = workloads.order_payloads(7000)
+
+        def make(e):
+            e.deploy(_simple_workflow(), 100, 1)
+            e.create_packed("simple", blob, offs)
+            return 7000
+
+    a = _template_drain(make, True)
+    b = _template_drain(make, False)
+    assert a["ser"]["template_drain"] == 1 and b["ser"]["template_drain"] == 0
+    assert a["ser"]["value_bytes"] == b["ser"]["value_bytes"] and a["ser"]["payload_bytes"] == b["ser"]["payload_bytes"]
+    assert a["values"] == b["values"]
+    assert a["headers"] == b["headers"]
+    assert a["desc"] == b["desc"]
+    assert a["records"] == b["records"]
+    assert a["counters"] == b["counters"]
+
+
+def test_template_drain_not_taken_for_merges_or_partial_ranges():
+    """C1's canonical harness merges job payloads: the batch is not deferred. A deferred batch serialized from
+    another start, or as frames, is materialized first and drained from its descriptors."""
+    cfg = workloads.CONFIGS["c1"]
+    from zeebe_amd.engine import Engine
+
+    e = Engine(log_capacity=1 << 20, row_capacity=1 << 14, arena_bytes=32 << 20)
+    e.deploy(cfg["workflow"]().to_xml(), 100, 1)
+    blob, offs = workloads.order_payloads(2000)
+    e.create_packed(cfg["process"], blob, offs)
+    assert e.step()["quiescent"]
+    assert e.serialize(2000, e.log_size() - 2000)["template_drain"] == 0
+    e.close()
+    c3 = workloads.CONFIGS["c3"]
+    blob, offs = c3["payloads"](5000)
+    e = Engine(log_capacity=1 << 20, row_capacity=1 << 14, arena_bytes=32 << 20)
+    e.deploy(c3["workflow"]().to_xml(), 100, 1)
+    e.create_packed(c3["process"], blob, offs)
+    assert e.step()["quiescent"]
+    L = e.log_size()
+    whole = e.records(0)  # from 0: includes the CREATE commands -> materialized, descriptor drain
+    assert e.serialize(5000, L - 5000)["template_drain"] == 0  # (no longer deferred)
+    assert [r.position for r in whole] == list(range(L))
+    e.close()

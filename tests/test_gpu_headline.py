@@ -1,9 +1,10 @@
 """The bench's headline step (C3, 10M instances, BASELINE.json configs[2]) byte-checked in the configuration that
-produces the number: product build, no ZB_VLEN_CHECK, the fast drain (k_ser_fast) with the value lengths the
-emitting kernels wrote.
+produces the number: product build, no ZB_VLEN_CHECK, the batch left without descriptors by zb_step and drained
+from its traces (zb_tdrain.hip).
 
-  * the fast drain's values and record headers equal the generic encoder's (ZB_SER_FAST=0 sends every tile
-    through k_ser_write), byte for byte, for all ~101.7M records;
+  * the template drain's values and record headers equal the generic encoder's over the descriptors
+    (ZB_TMPL_DEFER=0: k_tmpl writes them; ZB_SER_FAST=0: every tile through k_ser_write), byte for byte, for all
+    ~101.7M records;
   * a strided sample of instances: every record's value equals the reference's bytes for that instance -- the
     oracle runs the instance alone, its keys are mapped onto the keys the 10M run gave the same records (in
     order), and the values re-encoded with those keys (msgpack's minimal encodings = MsgPackWriter's).
@@ -27,6 +28,7 @@ def _run(monkeypatch, fast):
 
     monkeypatch.setenv("ZB_VLEN_CHECK", "0")
     monkeypatch.setenv("ZB_SER_FAST", "1" if fast else "0")
+    monkeypatch.setenv("ZB_TMPL_DEFER", "1" if fast else "0")
     e = Engine(log_capacity=N * 16, row_capacity=1 << 20, arena_bytes=N * 64 + (64 << 20))
     e.deploy(bpmn.xor_workflow().to_xml(), 100, 1)
     blob, offs = workloads.xor_payloads_np(N)
@@ -48,12 +50,12 @@ def _copy(e, ser, count):
     return vals, np.frombuffer(hdrs, dtype=np.uint8).copy()
 
 
-def test_headline_drain_fast_equals_generic_and_reference(monkeypatch):
+def test_headline_template_drain_equals_generic_and_reference(monkeypatch):
     e, ser, L = _run(monkeypatch, True)
     count = L - N
-    assert ser["generic_tiles"] == 0  # every tile took the fast path
+    assert ser["template_drain"] == 1 and ser["generic_tiles"] == 0  # drained from the traces
     vals, hdrs = _copy(e, ser, count)
-    # per-instance check on a strided sample
+    # per-instance check on a strided sample (the descriptors: materialized on demand)
     from test_gpu_properties import descriptors
 
     d = descriptors(e, N, count)
@@ -87,6 +89,7 @@ def test_headline_drain_fast_equals_generic_and_reference(monkeypatch):
     del d
     # the generic encoder over the same log: identical bytes
     e2, ser2, L2 = _run(monkeypatch, False)
+    assert ser2["template_drain"] == 0
     assert L2 == L and ser2["value_bytes"] == ser["value_bytes"] and ser2["payload_bytes"] == ser["payload_bytes"]
     vals2, hdrs2 = _copy(e2, ser2, count)
     e2.close()

@@ -69,6 +69,8 @@ class Driver:
         self.scan_from = self.o.log_size()
 
     def tick(self, creates, job_recs, cancels):
+        start = self.e.log_size()  # staged input is injected at the log tail by zb_step
+        assert start == self.o.log_size()
         for process, payloads in creates:
             for p in payloads:
                 self.o.create(process, p)
@@ -78,8 +80,6 @@ class Driver:
             for r in recs:
                 self.o.submit(*r)
             self.e.submit_records(recs)
-        start = self.e.log_size()
-        assert start == self.o.log_size()
         self.o.run()
         st = self.e.step()
         assert st["quiescent"], st
@@ -92,7 +92,7 @@ class Driver:
 def _job_events(items, tick):
     recs = []
     for key, rec in items:
-        pl = msgpack.packb({"tick": tick, "job": key, "note": "x" * (120 + key % 97)})
+        pl = msgpack.packb({"tick": tick, "job": key, "note": "x" * (200 + key % 97)})
         recs.append((R.RT_EVENT, R.VT_JOB, R.JI_CREATED, key, R.job_event(rec.value)))
         recs.append((R.RT_EVENT, R.VT_JOB, R.JI_COMPLETED, key, R.job_event(rec.value, pl)))
     return recs
@@ -170,12 +170,12 @@ def test_trajectory_batches_reuse_arena():
     path allocates no rows for them), so compaction leaves only the static region, and 40 ticks run through a log
     window and an arena far smaller than what they write."""
     cfg = workloads.CONFIGS["c2"]
-    n = 60
+    n = 240
     recs_per_tick = 169 * n
-    log_cap, row_cap, arena = recs_per_tick + 1024, 1024, 2 * STATIC
+    log_cap, row_cap, arena = recs_per_tick + 1024, 1024, 2 * STATIC  # one tick merges ~350 KB
     o = zbref.Oracle()
     e = _engine(log_capacity=log_cap, row_capacity=row_cap, arena_bytes=arena)
-    jp = {"t%d" % k: msgpack.packb({"t%d" % k: "v" * 24}) for k in range(1, 21)}
+    jp = {"t%d" % k: msgpack.packb({"t%d" % k: "v" * 40}) for k in range(1, 21)}
     for x in (o, e):
         x.deploy(cfg["workflow"]().to_xml(), 100, 1)
         for act, p in jp.items():
@@ -186,8 +186,8 @@ def test_trajectory_batches_reuse_arena():
         ps = workloads.split(blob, offs)
         for p in ps:
             o.create(cfg["process"], p)
-        e.create(cfg["process"], ps)
         start = e.log_size()
+        e.create(cfg["process"], ps)
         o.run()
         st = e.step()
         assert st["quiescent"] and st["path"] in (1, 2), st
@@ -216,6 +216,7 @@ def test_job_processor_long_run():
         x.deploy(cfg["workflow"]().to_xml(), 100, 1)
     seen = 0
     for t in range(60):
+        start = e.log_size()
         payloads = [msgpack.packb({"orderId": t * 30 + i}) for i in range(30)]
         for p in payloads:
             o.create("process", p)
@@ -233,7 +234,6 @@ def test_job_processor_long_run():
         for c in cmds:
             o.submit(*c)
         e.submit_records(cmds)
-        start = e.log_size()
         o.run()
         assert e.step()["quiescent"]
         _compare_tick(o, e, start)

@@ -9,6 +9,8 @@
 #include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstring>
@@ -301,6 +303,22 @@ struct zb_engine {
   uint64_t dr_bytes = 0;
   uint64_t dr_epoch = 0;          // look-back tags of the single-pass serializer
   hipEvent_t dr_ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+
+  // deferred template batch (zb_tdrain.hip): a uniform / class batch whose descriptors k_tmpl has not written;
+  // zb_serialize of exactly [seg_begin, seg_end) encodes it from the traces, anything else materializes it
+  int tmpl_defer = 1;             // ZB_TMPL_DEFER=0: always write the descriptors in zb_step
+  bool seg_pending = false;
+  int64_t seg_begin = 0, seg_end = 0;
+  uint32_t seg_wmax = 0;
+  TrajParams seg_p{};
+  uint64_t* td_wbytes = nullptr;  // [wmax * nwave + 1] (u64: hipcub's scan accumulates in the input type)
+  uint64_t* td_woffs = nullptr;
+  uint64_t td_cap = 0;
+  void* td_tmp = nullptr;
+  size_t td_tmp_cap = 0;
+  uint64_t* td_pay = nullptr;     // [nwg]
+  uint64_t td_pay_cap = 0;
+  uint32_t* td_flags = nullptr;   // [2]
 
   // timing
   std::vector<hipEvent_t> ev;
@@ -621,6 +639,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   p.log_cap = (uint64_t)e->win_base + e->cfg.log_capacity;  // absolute: the window's end
   p.row_cap = e->cfg.row_capacity;
   p.arena_cap = e->cfg.arena_bytes;
+  p.defer_ok = (e->tmpl_defer && e->seg_ok && e->d_vsegs.p && e->d_vconst.p && (p.cls || p.uni)) ? 1 : 0;
   hipEvent_t* ev = e->ev.data();
   HIPCHECK(e, hipEventRecord(ev[0], e->stream));
   if (p.cls) launch_traj_count_classes(p, e->stream);
@@ -669,6 +688,13 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   int rc = check_device_errors(e, *e->h_err_pinned);
   if (rc != ZB_OK) return rc;
   st.path = p.cls ? 2 : 1;
+  if (e->h_ctl_pinned->defer) {  // descriptors not written: zb_serialize encodes the batch from its traces
+    e->seg_pending = true;
+    e->seg_begin = log_base + n;
+    e->seg_end = e->host_hdr.end;
+    e->seg_wmax = e->h_ctl_pinned->wmax;
+    e->seg_p = p;
+  }
   return 1;
 }
 
@@ -927,12 +953,39 @@ int compact_state(zb_engine* e) {
   return finish_batch(e);  // the device wave header takes the new allocators
 }
 
+// A deferred template batch gets its descriptors (+ source deltas, value-length hints) written by the emit
+// pass it skipped; the batch's buffers (traces, class plan, generation bases) are still those of the last
+// trajectory run (every zb_step settles the deferred batch before a new run).
+int materialize(zb_engine* e) {
+  if (!e->seg_pending) return ZB_OK;
+  e->seg_pending = false;
+  TrajParams p = e->seg_p;
+  p.materialize = 1;
+  launch_traj_emit(p, e->stream, nullptr);
+  HIPCHECK(e, hipGetLastError());
+  HIPCHECK(e, hipMemcpyAsync(e->h_ctl_pinned, e->t_ctl, sizeof(TrajCtl), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  return check_device_errors(e, e->h_ctl_pinned->derr);
+}
+// before anything reads the log window or reuses the trajectory buffers: a deferred batch that was released
+// (appended by the caller) is dropped, any other is materialized
+int settle_deferred(zb_engine* e) {
+  if (!e->seg_pending) return ZB_OK;
+  if (e->released >= e->seg_end) {
+    e->seg_pending = false;
+    return ZB_OK;
+  }
+  return materialize(e);
+}
+
 // Between ticks: the released part of the log leaves the window, and the state is compacted when any region
 // is more than half full (or always, force) -- so a partition whose live state fits half its capacities runs
 // indefinitely.
 int maintain(zb_engine* e, bool force) {
   if (e->failed || e->host_hdr.begin != e->host_hdr.end) return ZB_OK;  // only at quiescence
-  int rc = rebase_log(e);
+  int rc = settle_deferred(e);
+  if (rc != ZB_OK) return rc;
+  rc = rebase_log(e);
   if (rc != ZB_OK) return rc;
   const bool rows_half = (uint64_t)e->host_hdr.rows_next > e->cfg.row_capacity / 2;
   const bool arena_half = (uint64_t)e->host_hdr.arena_next - STATIC_ARENA_BYTES > (e->cfg.arena_bytes - STATIC_ARENA_BYTES) / 2;
@@ -960,6 +1013,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (const char* m = std::getenv("ZB_SER_NT")) e->ser_nt = atoi(m);
   if (const char* m = std::getenv("ZB_SER_FAST")) e->ser_fast = atoi(m);
   if (const char* m = std::getenv("ZB_TMPL_IO")) e->tmpl_io = atoi(m);
+  if (const char* m = std::getenv("ZB_TMPL_DEFER")) e->tmpl_defer = atoi(m);
   if (const char* m = std::getenv("ZB_WAVE_EVENTS")) e->wave_events = atoi(m) != 0;
   if (const char* m = std::getenv("ZB_SER_LENBUF")) e->ser_lenbuf = atoi(m);
   if (const char* g = std::getenv("ZB_WAVE_GRID")) e->wave_grid_fixed = std::max(0, std::min(atoi(g), (int)WAVE_GRID_MAX));
@@ -1129,6 +1183,7 @@ int zb_reset(zb_engine* e, int keep_staged) {
     HIPCHECK(e, hipMemsetAsync(e->jobs.tombs, 0, sizeof(uint32_t), e->stream));
   }
   e->win_base = e->released = 0;
+  e->seg_pending = false;  // (the log is empty again)
   rebias(e);
   e->rows_total = e->arena_total = e->records_total = e->compactions = 0;
   HIPCHECK(e, hipStreamSynchronize(e->stream));
@@ -1813,10 +1868,13 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   zb_step_stats st{};
   bool try_traj = false;
   {
-    int mrc = maintain(e, false);  // released records leave the window; compaction when a region is half full
+    int mrc = settle_deferred(e);  // (a new trajectory run reuses the deferred batch's buffers)
+    if (mrc != ZB_OK) return mrc;
+    mrc = maintain(e, false);  // released records leave the window; compaction when a region is half full
     if (mrc != ZB_OK) return mrc;
   }
   const int64_t rows_before = e->host_hdr.rows_next, arena_before = e->host_hdr.arena_next;
+  const int64_t end_before = e->host_hdr.end;  // records appended by this call: injected input + follow-ups
   int64_t traj_base = 0, traj_n = 0;
   // ---- inject staged input at the log tail (engine is quiescent between steps)
   if (e->staged_pending && !e->staged.empty()) {
@@ -1984,7 +2042,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   st.waves = stats_after[6] - stats_before[6];
   e->rows_total += (uint64_t)std::max<int64_t>(0, e->host_hdr.rows_next - rows_before);
   e->arena_total += (uint64_t)std::max<int64_t>(0, e->host_hdr.arena_next - arena_before);
-  e->records_total += (uint64_t)(e->host_hdr.end - written_from);
+  e->records_total += (uint64_t)(e->host_hdr.end - end_before);
   st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (stats) *stats = st;
   if (!quiescent) return ZB_EAGAIN;
@@ -1998,6 +2056,8 @@ int zb_read_source_positions(zb_engine* e, int64_t start, int64_t count, int64_t
   if (!e || start < e->win_base || count < 0 || start + count > e->host_hdr.end || (!out && count)) return ZB_EINVAL;
   if (count == 0) return ZB_OK;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
+  int rc = materialize(e);
+  if (rc != ZB_OK) return rc;
   std::vector<uint32_t> d((size_t)count);
   HIPCHECK(e, hipMemcpyAsync(d.data(), e->srcd + start, count * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
@@ -2008,6 +2068,8 @@ int zb_read_source_positions(zb_engine* e, int64_t start, int64_t count, int64_t
 int zb_read_descriptors(zb_engine* e, int64_t start, int64_t count, zb_rec* out) {
   if (!e || start < e->win_base || count < 0 || start + count > e->host_hdr.end || (!out && count)) return ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
+  int rc = materialize(e);
+  if (rc != ZB_OK) return rc;
   HIPCHECK(e, hipMemcpyAsync(out, e->log + start, count * sizeof(zb_rec), hipMemcpyDeviceToHost, e->stream));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
   return ZB_OK;
@@ -2039,6 +2101,99 @@ int zb_set_request_metadata(zb_engine* e, size_t n, const uint64_t* request_ids,
       return fail(e, ZB_EINVAL, "request metadata already set for these records");
     e->staged_reqs.push_back(zb_engine::StagedReq{idx, request_ids[i], request_stream_ids[i]});
   }
+  return ZB_OK;
+}
+
+// zb_serialize of exactly a deferred template batch: k_tdrain_size -> scan -> k_tdrain_write (zb_tdrain.hip).
+// ZB_EAGAIN: the batch needs the descriptor path (an instance's records exceed the wave image, or a value length
+// disagreed with the encoder -- never silently).
+static int serialize_deferred(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats& st) {
+  const TrajParams& p = e->seg_p;
+  const uint64_t nwave = (uint64_t)p.nwg * (TRAJ_WG / 64);
+  const uint64_t ent = (uint64_t)e->seg_wmax * nwave + 1;
+  if (ent > (uint64_t)INT32_MAX) return ZB_EAGAIN;
+  if (ent > e->td_cap) {
+    if (e->td_wbytes) (void)hipFree(e->td_wbytes);
+    if (e->td_woffs) (void)hipFree(e->td_woffs);
+    if (e->td_tmp) (void)hipFree(e->td_tmp);
+    e->td_wbytes = nullptr; e->td_woffs = nullptr; e->td_tmp = nullptr; e->td_cap = 0;
+    const uint64_t cap = ent + ent / 4 + 1024;
+    HIPCHECK(e, hipMalloc(&e->td_wbytes, cap * sizeof(uint64_t)));
+    HIPCHECK(e, hipMalloc(&e->td_woffs, cap * sizeof(uint64_t)));
+    size_t tmp = 0;
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->td_wbytes, e->td_woffs, (int)cap, e->stream) != hipSuccess)
+      return fail(e, ZB_EDEVICE, "template drain scan sizing");
+    HIPCHECK(e, hipMalloc(&e->td_tmp, tmp + 16));
+    e->td_tmp_cap = tmp;
+    e->td_cap = cap;
+  }
+  if ((uint64_t)p.nwg > e->td_pay_cap) {
+    if (e->td_pay) (void)hipFree(e->td_pay);
+    e->td_pay = nullptr;
+    HIPCHECK(e, hipMalloc(&e->td_pay, (uint64_t)p.nwg * sizeof(uint64_t)));
+    e->td_pay_cap = (uint64_t)p.nwg;
+  }
+  if (!e->td_flags) HIPCHECK(e, hipMalloc(&e->td_flags, 4 * sizeof(uint32_t)));
+  TDrainParams d{};
+  d.t = p;
+  d.headers = e->dr_hdr;
+  d.start = start;
+  d.wmax = e->seg_wmax;
+  d.nwave = (uint32_t)nwave;
+  d.wbytes = e->td_wbytes;
+  d.woffs = e->td_woffs;
+  d.pay_part = e->td_pay;
+  d.totals = e->dr_total;
+  d.flags = e->td_flags;
+  d.vsegs = e->d_vsegs.p;
+  d.segpool = e->d_segpool.p;
+  d.segpool_len = e->segpool_len;
+  d.n_elems = (int32_t)e->model.elems.size();
+  float ms_size = 0, ms_scan = 0, ms_write = 0;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    d.out = e->dr_val;
+    d.out_cap = e->dr_val_cap;
+    HIPCHECK(e, hipMemsetAsync(e->dr_total, 0, 4 * sizeof(uint64_t), e->stream));
+    HIPCHECK(e, hipMemsetAsync(e->td_flags, 0, 4 * sizeof(uint32_t), e->stream));
+    HIPCHECK(e, hipMemsetAsync(e->td_wbytes + (ent - 1), 0, sizeof(uint64_t), e->stream));
+    HIPCHECK(e, hipEventRecord(e->dr_ev[0], e->stream));
+    launch_tdrain_size(d, e->stream);
+    HIPCHECK(e, hipEventRecord(e->dr_ev[1], e->stream));
+    size_t tmp = e->td_tmp_cap;
+    if (hipcub::DeviceScan::ExclusiveSum(e->td_tmp, tmp, e->td_wbytes, e->td_woffs, (int)ent, e->stream) != hipSuccess)
+      return fail(e, ZB_EDEVICE, "template drain scan");
+    HIPCHECK(e, hipMemcpyAsync(e->dr_total, e->td_woffs + (ent - 1), sizeof(uint64_t), hipMemcpyDeviceToDevice, e->stream));
+    HIPCHECK(e, hipEventRecord(e->dr_ev[2], e->stream));
+    launch_tdrain_write(d, e->stream);
+    HIPCHECK(e, hipEventRecord(e->dr_ev[3], e->stream));
+    HIPCHECK(e, hipGetLastError());
+    HIPCHECK(e, hipMemcpyAsync(e->h_dr_total, e->dr_total, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHECK(e, hipMemcpyAsync(e->h_dr_total + 2, e->td_flags, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHECK(e, hipStreamSynchronize(e->stream));
+    const uint32_t* fl = (const uint32_t*)(e->h_dr_total + 2);
+    if (fl[1]) return ZB_EAGAIN;
+    if (!fl[0]) break;
+    if (attempt == 1) return fail(e, ZB_EDEVICE, "drain buffer overflow after growing it");
+    (void)hipFree(e->dr_val);
+    e->dr_val = nullptr;
+    e->dr_val_cap = 0;
+    const uint64_t cap = e->h_dr_total[0] + e->h_dr_total[0] / 4 + (64ull << 20);
+    HIPCHECK(e, hipMalloc(&e->dr_val, cap));
+    e->dr_val_cap = cap;
+  }
+  HIPCHECK(e, hipEventElapsedTime(&ms_size, e->dr_ev[0], e->dr_ev[1]));
+  HIPCHECK(e, hipEventElapsedTime(&ms_scan, e->dr_ev[1], e->dr_ev[2]));
+  HIPCHECK(e, hipEventElapsedTime(&ms_write, e->dr_ev[2], e->dr_ev[3]));
+  st.records = (uint64_t)count;
+  st.value_bytes = e->h_dr_total[0];
+  st.payload_bytes = e->h_dr_total[1];
+  st.size_kernel_ms = ms_size;
+  st.scan_ms = ms_scan;
+  st.write_kernel_ms = ms_write;
+  st.generic_tiles = 0;
+  st.template_drain = 1;
+  e->dr_slow_tiles = 0;
+  e->dr_split = false;
   return ZB_OK;
 }
 
@@ -2090,6 +2245,23 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
     const uint64_t cap = (uint64_t)count * 200 + (64ull << 20);
     HIPCHECK(e, hipMalloc(&e->dr_val, cap));
     e->dr_val_cap = cap;
+  }
+  if (e->seg_pending) {  // a deferred template batch: encoded from its traces, or materialized first
+    if (!fc && start == e->seg_begin && count == e->seg_end - e->seg_begin) {
+      const int rc = serialize_deferred(e, start, count, st);
+      if (rc == ZB_OK) {
+        e->dr_count = count;
+        e->dr_bytes = st.value_bytes;
+        e->dr_frames = false;
+        st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (stats) *stats = st;
+        return ZB_OK;
+      }
+      if (rc != ZB_EAGAIN) return rc;
+      st = zb_serialize_stats{};
+    }
+    const int rc = materialize(e);
+    if (rc != ZB_OK) return rc;
   }
   HIPCHECK(e, e->d_ranges.upload(e->ranges, e->stream));
   HIPCHECK(e, e->d_cmd_pool.upload(e->cmd_pool, e->stream));
@@ -2911,6 +3083,13 @@ int zb_outbox_take(zb_engine* e, int kind, uint8_t* dst, size_t cap, int dst_on_
     if (_r != ncclSuccess) return fail((e), ZB_EDEVICE, std::string(#call) + ": " + ncclGetErrorString(_r)); \
   } while (0)
 
+const char* zb_rccl_library(void) {
+  static std::string path;
+  Dl_info info{};
+  if (path.empty() && dladdr((void*)&ncclCommInitRank, &info) && info.dli_fname) path = info.dli_fname;
+  return path.c_str();
+}
+
 int zb_comm_unique_id(uint8_t id[128]) {
   if (!id) return ZB_EINVAL;
   ncclUniqueId u;
@@ -3308,6 +3487,7 @@ int zb_restore(zb_engine* e, const uint8_t* buf, size_t len) {
   SnapHead h;
   std::memcpy(&h, buf, sizeof(h));
   if (h.magic != SNAP_MAGIC) return fail(e, ZB_EINVAL, "not a zb snapshot");
+  e->seg_pending = false;  // (the restored log replaces it)
   if (h.model_hash != model_hash(e)) return fail(e, ZB_EINVAL, "snapshot was taken with other deployments");
   if (len < snap_bytes(h)) return fail(e, ZB_EINVAL, "truncated snapshot");
   if (h.rows > e->cfg.row_capacity || STATIC_ARENA_BYTES + h.arena_dyn > e->cfg.arena_bytes)

@@ -76,7 +76,7 @@ class zb_serialize_stats(ctypes.Structure):
     _fields_ = [("records", ctypes.c_uint64), ("value_bytes", ctypes.c_uint64), ("payload_bytes", ctypes.c_uint64),
                 ("size_kernel_ms", ctypes.c_double), ("scan_ms", ctypes.c_double),
                 ("write_kernel_ms", ctypes.c_double), ("wall_ms", ctypes.c_double),
-                ("generic_tiles", ctypes.c_uint64)]
+                ("generic_tiles", ctypes.c_uint64), ("template_drain", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -155,6 +155,8 @@ def lib():
         L.zb_serialize_frames.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(zb_frame_config),
                                           ctypes.POINTER(zb_serialize_stats)]
         L.zb_set_request_metadata.argtypes = [vp, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+        L.zb_rccl_library.restype = ctypes.c_char_p
+        L.zb_rccl_library.argtypes = []
         L.zb_pinned_alloc.restype = ctypes.c_void_p
         L.zb_pinned_alloc.argtypes = [ctypes.c_size_t]
         L.zb_pinned_free.argtypes = [ctypes.c_void_p]
@@ -176,7 +178,7 @@ EXPORTED_SYMBOLS = ["zb_engine_create", "zb_engine_destroy", "zb_last_error", "z
                     "zb_validate_deployment", "zb_serialize", "zb_drain_copy", "zb_pinned_alloc", "zb_pinned_free",
                     "zb_serialize_frames", "zb_set_request_metadata", "zb_read_source_positions",
                     "zb_log_release", "zb_compact", "zb_read_memory_stats", "zb_submit_messages", "zb_set_clock",
-                    "zb_expire_messages"]
+                    "zb_expire_messages", "zb_rccl_library"]
 
 
 def validate_deployment(xml):
@@ -522,6 +524,11 @@ class Engine:
         self._check(self._L.zb_counters(self._h, arr))
         return dict(created=arr[0], completed=arr[1], canceled=arr[2], next_wf_key=arr[3], next_job_key=arr[4],
                     rows=arr[5], arena_bytes=arr[6], log_size=arr[7])
+
+
+def rccl_library() -> str:
+    """The file of the RCCL library the engine's communicator runs on (zb_rccl_library: dladdr of ncclCommInitRank)."""
+    return lib().zb_rccl_library().decode("utf-8", "replace")
 
 
 def pinned_alloc(nbytes: int) -> int:
