@@ -99,7 +99,9 @@ def make_engine(cfg, n, a, rank, world, local_rank):
     from zeebe_amd.engine import Engine
 
     recs = RECS_PER_INST[cfg](a.tasks)
-    rows = {"c1": n * 3, "c2": n * (a.tasks + 2), "c3": 1 << 20, "c4": n * 20}[cfg]
+    # (the trajectory path allocates no rows for instances that complete in the tick; the wave pipeline holds a
+    # row per live element instance: C3 wave-only needs the process + gateway / task rows of every instance)
+    rows = {"c1": n * 3, "c2": n * (a.tasks + 2), "c3": n * 3 if a.wave_only else 1 << 20, "c4": n * 20}[cfg]
     arena = {"c1": n * 96, "c2": n * (48 + 48 * a.tasks), "c3": n * 64, "c4": n * 1200}[cfg] + (64 << 20)
     return Engine(device=0 if a.same_device else local_rank, partition_id=rank, partition_count=world,
                   log_capacity=int(n * recs), row_capacity=int(rows), arena_bytes=int(arena), wave_only=a.wave_only)

@@ -2519,7 +2519,7 @@ MsgParams msg_params(zb_engine* e) {
   p.sub_mask = e->head_mask; p.sub_count = e->sub_count; p.sub_cap = e->store_cap;
   p.msgs = e->msgs; p.msg_head = e->msg_head; p.msg_next = e->msg_next;
   p.msg_mask = e->head_mask; p.msg_count = e->msg_count; p.msg_cap = e->store_cap;
-  p.ob = outbox(e, 1);
+  p.ob = outbox(e, ZB_XCHG_CORRELATE);  // the message side sends correlations
   p.err = e->derr;
   p.clock = e->clock_ms;
   return p;
