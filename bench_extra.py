@@ -82,7 +82,7 @@ def run_c5(a, rank, world, local_rank, dist, barrier, reduce_max, reduce_sum):
     n = a.instances  # per partition
     N = n * world
     eng = Engine(device=0 if a.same_device else local_rank, partition_id=rank, partition_count=world,
-                 log_capacity=n * 24, row_capacity=2 * n + 1024, arena_bytes=n * 640 + (64 << 20))
+                 log_capacity=n * 24, row_capacity=4 * n + 1024, arena_bytes=n * 640 + (64 << 20))
     eng.deploy(bpmn.message_workflow().to_xml(), 100, 1)
     # instance i -> partition i % P (round-robin CREATE dispatch)
     mine = range(rank, N, world)

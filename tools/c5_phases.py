@@ -7,16 +7,18 @@ import time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import msgpack  # noqa: E402
 import numpy as np  # noqa: E402
+from zeebe_amd.engine import Engine, lib  # noqa: E402
+
+lib()  # (before torch: the engine's RCCL)
 import torch.distributed as tdist  # noqa: E402
 
 from zeebe_amd import bpmn, cluster  # noqa: E402
-from zeebe_amd.engine import Engine  # noqa: E402
 
 s = socket.socket(); s.bind(("127.0.0.1", 0))
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1"); os.environ.setdefault("MASTER_PORT", str(s.getsockname()[1])); s.close()
 tdist.init_process_group("gloo", rank=0, world_size=1)
 n = 1_000_000
-eng = Engine(log_capacity=n * 24, row_capacity=2 * n + 1024, arena_bytes=n * 640 + (64 << 20))
+eng = Engine(log_capacity=n * 24, row_capacity=4 * n + 1024, arena_bytes=n * 640 + (64 << 20))
 eng.deploy(bpmn.message_workflow().to_xml(), 100, 1)
 create_payloads = [msgpack.packb({"orderId": "order-%d" % i}) for i in range(n)]
 cks = [b"order-%d" % i for i in range(n)]
@@ -42,5 +44,6 @@ for it in range(3):
     tm("settle1", dc.settle)
     tm("publish", eng.publish_packed, b"order", ck_blob, ck_off, pl_blob, pl_off, 3600000)
     tm("settle2", dc.settle)
+    tm("serialize", eng.serialize, 0, eng.log_size())
     print("step %.2f ms" % ((time.perf_counter() - t0) * 1e3), {k: round(v * 1e3, 2) for k, v in T.items()}, "rounds", dc.rounds)
 tdist.destroy_process_group()

@@ -272,6 +272,7 @@ struct zb_engine {
   uint64_t c_pop_cap = 0, c_off_cap = 0;
   uint32_t* c_count = nullptr;                   // device counter (job rebuild)
   uint64_t rows_total = 0, arena_total = 0, records_total = 0, compactions = 0;  // lifetime allocation totals
+  uint64_t rows_mark = 0, arena_mark = 0;  // rows / arena bytes live after the last compaction (maintain)
   // inbox CORRELATE resolution by activity instance key (zb_inbox_submit)
   int64_t *x_keys = nullptr, *x_pos = nullptr, *x_keys2 = nullptr, *x_pos2 = nullptr;
   uint64_t x_cap = 0;
@@ -309,7 +310,7 @@ struct zb_engine {
   int tmpl_defer = 1;             // ZB_TMPL_DEFER=0: always write the descriptors in zb_step
   bool seg_pending = false;
   int64_t seg_begin = 0, seg_end = 0;
-  uint32_t seg_wmax = 0;
+  uint32_t seg_wmax = 0, seg_nc = 1;
   TrajParams seg_p{};
   uint64_t* td_wbytes = nullptr;  // [wmax * nwave + 1] (u64: hipcub's scan accumulates in the input type)
   uint64_t* td_woffs = nullptr;
@@ -694,6 +695,8 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
     e->seg_end = e->host_hdr.end;
     e->seg_wmax = e->h_ctl_pinned->wmax;
     e->seg_p = p;
+    e->seg_nc = 1;
+    if (p.cls) HIPCHECK(e, hipMemcpy(&e->seg_nc, e->c_plan, sizeof(uint32_t), hipMemcpyDeviceToHost));  // ClsPlan.nc
   }
   return 1;
 }
@@ -950,6 +953,8 @@ int compact_state(zb_engine* e) {
     }
   }
   e->compactions++;
+  e->rows_mark = (uint64_t)e->host_hdr.rows_next;  // what survived: the next trigger is relative to it
+  e->arena_mark = (uint64_t)e->host_hdr.arena_next;
   return finish_batch(e);  // the device wave header takes the new allocators
 }
 
@@ -978,17 +983,23 @@ int settle_deferred(zb_engine* e) {
   return materialize(e);
 }
 
-// Between ticks: the released part of the log leaves the window, and the state is compacted when any region
-// is more than half full (or always, force) -- so a partition whose live state fits half its capacities runs
-// indefinitely.
+// Between ticks: the released part of the log leaves the window, and the state is compacted when a region has
+// used half of the room the last compaction left it (or always, force) -- so a partition whose live state fits
+// its capacities runs indefinitely, and a compaction that frees little is not repeated at every tick (each one
+// is paid for by at least half the free room having been allocated since the last).
 int maintain(zb_engine* e, bool force) {
   if (e->failed || e->host_hdr.begin != e->host_hdr.end) return ZB_OK;  // only at quiescence
   int rc = settle_deferred(e);
   if (rc != ZB_OK) return rc;
   rc = rebase_log(e);
   if (rc != ZB_OK) return rc;
-  const bool rows_half = (uint64_t)e->host_hdr.rows_next > e->cfg.row_capacity / 2;
-  const bool arena_half = (uint64_t)e->host_hdr.arena_next - STATIC_ARENA_BYTES > (e->cfg.arena_bytes - STATIC_ARENA_BYTES) / 2;
+  const uint64_t rm = std::min<uint64_t>(e->rows_mark, e->cfg.row_capacity);
+  const uint64_t am = std::max<uint64_t>(std::min<uint64_t>(e->arena_mark, e->cfg.arena_bytes), STATIC_ARENA_BYTES);
+  const uint64_t ru = (uint64_t)e->host_hdr.rows_next, au = (uint64_t)e->host_hdr.arena_next;
+  const uint64_t rc_ = e->cfg.row_capacity, ac = e->cfg.arena_bytes;
+  // (and whenever less than an eighth is left: then compacting is the only way on)
+  const bool rows_half = ru > rm + (rc_ - rm) / 2 || rc_ - std::min(ru, rc_) < rc_ / 8;
+  const bool arena_half = au > am + (ac - am) / 2 || ac - std::min(au, ac) < (ac - STATIC_ARENA_BYTES) / 8;
   bool jobs_half = false;
   if (e->jobs.keys && !force && !rows_half && !arena_half) {
     uint32_t tombs = 0;
@@ -1186,6 +1197,8 @@ int zb_reset(zb_engine* e, int keep_staged) {
   e->seg_pending = false;  // (the log is empty again)
   rebias(e);
   e->rows_total = e->arena_total = e->records_total = e->compactions = 0;
+  e->rows_mark = 0;
+  e->arena_mark = STATIC_ARENA_BYTES;
   HIPCHECK(e, hipStreamSynchronize(e->stream));
   e->ranges.clear();
   e->cmd_pool.clear();
@@ -2149,6 +2162,7 @@ static int serialize_deferred(zb_engine* e, int64_t start, int64_t count, zb_ser
   d.segpool = e->d_segpool.p;
   d.segpool_len = e->segpool_len;
   d.n_elems = (int32_t)e->model.elems.size();
+  d.nc = e->seg_nc;
   float ms_size = 0, ms_scan = 0, ms_write = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     d.out = e->dr_val;
@@ -3535,6 +3549,8 @@ int zb_restore(zb_engine* e, const uint8_t* buf, size_t len) {
   e->msg_key_next = h.msg_key_next;
   e->sub_count = h.sub_count; e->msg_count = h.msg_count;
   e->records_total = h.records_total; e->rows_total = h.rows_total; e->arena_total = h.arena_total;
+  e->rows_mark = h.rows;  // (a snapshot holds live state only)
+  e->arena_mark = STATIC_ARENA_BYTES + h.arena_dyn;
   e->wave = 0;
   HIPCHECK(e, hipMemcpy(e->dstats, h.stats, sizeof(h.stats), hipMemcpyHostToDevice));
   return finish_batch(e);

@@ -11,8 +11,9 @@
 //   k_tdrain_size   one lane per instance (instance order = log order inside every generation): per generation
 //                   the value bytes of the wave's records -> wbytes[w][wave]
 //   (hipcub)        exclusive scan over wbytes, generation-major = log order -> byte offset of every wave range
-//   k_tdrain_write  the same lanes again: headers of the wave's records, values encoded with the fast encoder
-//                   (zb_fastenc.hpp) into the wave's LDS image and streamed out with 16-byte stores
+//   k_tdrain_write  the same lanes again: headers of the wave's records; per generation the four waves of a
+//                   workgroup take turns encoding their values with the fast encoder (zb_fastenc.hpp) into the
+//                   workgroup's LDS image, which all 256 lanes stream out with 16-byte stores
 // The CREATE payload -- the payload of every record the instance writes -- is read once per lane, not once per
 // record. Anything else (zb_step, frames, descriptors, a partial range, compaction) materializes the batch
 // first with k_tmpl, so every other API sees the descriptors it always saw.
@@ -24,20 +25,99 @@
 namespace zbg {
 
 constexpr int TD_WG = TRAJ_WG;  // 256 lanes = 256 instances, four waves
-constexpr uint32_t TD_IMG = 6 * 1024 - 16;  // per-wave image: 6 KB slices, four per workgroup (+ the model)
+// the workgroup's image holds one wave's values of one generation (64 instances x at most TF records); a range
+// larger than that sends the batch to the descriptor path (ZB_EAGAIN). 28 KB + the tables: four workgroups per CU
+constexpr uint32_t TD_IMG = 28 * 1024 - 16;
+
+// The batch's tables in LDS (every lookup of the generation loop is an LDS read, not a dependent global load):
+//   agg[c][w]  records | wf keys << 16 | job keys << 32 of class c in generation w (one instance)
+//   wbase[w]   generation bases (log position, key ordinals)
+//   tmpl[c][w][k] traced records,  vconst[e] value-length constants of element e
+struct TdTab {
+  const uint64_t* agg;
+  const TrajBase* wbase;
+  const TmplRec* tmpl;
+  const ValueConst* vconst;
+  uint32_t wmax;
+};
+struct TdLayout {
+  uint32_t tab, pool, agg, wbase, tmpl, vconst, total;  // byte offsets in dynamic LDS (16-aligned) and the size
+};
+__host__ __device__ __forceinline__ uint32_t td_r16(uint32_t x) { return (x + 15) & ~15u; }
+__host__ __device__ __forceinline__ TdLayout td_layout(const TDrainParams& d, bool model) {
+  TdLayout l;
+  l.tab = 0;
+  const uint32_t tb = model ? td_r16((uint32_t)d.n_elems * 20u) : 0u;  // DevValSeg table (20 B each)
+  l.pool = l.tab + tb;
+  l.agg = l.pool + (model ? td_r16(d.segpool_len) : 0u);
+  l.wbase = l.agg + td_r16(d.nc * d.wmax * 8u);
+  l.tmpl = l.wbase + td_r16(d.wmax * (uint32_t)sizeof(TrajBase));
+  l.vconst = l.tmpl + td_r16(d.nc * d.wmax * (uint32_t)TF * (uint32_t)sizeof(TmplRec));
+  l.total = l.vconst + td_r16((uint32_t)d.n_elems * (uint32_t)sizeof(ValueConst));
+  return l;
+}
+// copies the tables (and, for the write pass, the value segments) into LDS; ends in a barrier
+__device__ __forceinline__ TdTab td_load_tables(const TDrainParams& D, uint8_t* sm, bool model) {
+  const TdLayout l = td_layout(D, model);
+  const TrajParams& P = D.t;
+  const int t = threadIdx.x;
+  if (model) {
+    const uint32_t tb = td_r16((uint32_t)D.n_elems * 20u);  // (the table is padded to 4 entries at deploy)
+    for (uint32_t c = t; c < tb / 4; c += TD_WG) ((uint32_t*)(sm + l.tab))[c] = ((const uint32_t*)D.vsegs)[c];
+    for (uint32_t c = t; c < D.segpool_len / 8; c += TD_WG) ((uint64_t*)(sm + l.pool))[c] = ((const uint64_t*)D.segpool)[c];
+  }
+  uint64_t* agg = (uint64_t*)(sm + l.agg);
+  for (uint32_t c = t; c < D.nc * D.wmax; c += TD_WG)
+    agg[c] = P.agg[(uint64_t)(c / D.wmax) * CLS_ROW + c % D.wmax];
+  TrajBase* wb = (TrajBase*)(sm + l.wbase);
+  for (uint32_t c = t; c < D.wmax; c += TD_WG) wb[c] = P.wbase[c];
+  uint4* tm = (uint4*)(sm + l.tmpl);  // TmplRec: two 16-byte halves
+  for (uint32_t c = t; c < D.nc * D.wmax * TF * 2; c += TD_WG) {
+    const uint32_t r = c / 2, h = c & 1, k = r % TF, cw = r / TF;
+    const uint64_t src = ((uint64_t)(cw / D.wmax) * CLS_ROW + cw % D.wmax) * TF + k;
+    tm[c] = ((const uint4*)(P.tmpl + src))[h];
+  }
+  ValueConst* vc = (ValueConst*)(sm + l.vconst);
+  for (uint32_t c = t; c < (uint32_t)D.n_elems; c += TD_WG) vc[c] = P.vconst[c];
+  __syncthreads();
+  TdTab T;
+  T.agg = agg; T.wbase = wb; T.tmpl = (const TmplRec*)tm; T.vconst = vc; T.wmax = D.wmax;
+  return T;
+}
+
+// key ordinal base of generation g for this instance: wf (f = 1) or job (f = 2) counter (tmpl_kbase on the tables)
+__device__ __forceinline__ int64_t td_kbase(const TdTab& T, const TmplLane& L, uint32_t g, int f) {
+  const TrajBase wb = T.wbase[g];
+  int64_t k = f == 1 ? wb.wf : wb.job;
+#pragma unroll
+  for (int c = 0; c < CLS_MAX; c++) {
+    if (c >= (int)L.ncls) break;
+    const uint64_t n = T.agg[c * T.wmax + g];
+    k += (int64_t)L.before[c] * (int64_t)(f == 1 ? ((n >> 16) & 0xffff) : (n >> 32));
+  }
+  return k;
+}
+__device__ __forceinline__ int64_t td_key(const TrajParams& P, const TdTab& T, const TmplLane& L, uint32_t sym,
+                                          uint32_t w, int64_t kwf, int64_t kjob) {
+  if (sym == NOK) return -1;
+  if (sym == JOB_ZERO) return 0;
+  const uint32_t g = (sym >> 4) & 0xfff, ord = sym & 15;
+  if (sym & SYMK_WF) return P.wf_start + 5 * ((g == w ? kwf : td_kbase(T, L, g, 1)) + ord);
+  return P.job_start + 5 * ((g == w ? kjob : td_kbase(T, L, g, 2)) + ord);
+}
 
 // one instance's generation w: log position and key bases (linear in the class ranks), record count
 struct TdGen {
   int64_t pos0, kwf, kjob;
   uint32_t nrec;
 };
-__device__ __forceinline__ TdGen td_gen(const TrajParams& P, const TmplLane& L, uint32_t crow, int w, bool live) {
-  const TrajBase wb = kload(P.wbase, (uint64_t)w);
+__device__ __forceinline__ TdGen td_gen(const TdTab& T, const TmplLane& L, uint32_t cls, int w, bool live) {
+  const TrajBase wb = T.wbase[w];
   int64_t po = 0, pw = 0, pj = 0;
 #pragma unroll
   for (int c = 0; c < CLS_MAX; c++) {
     if (c >= (int)L.ncls) break;
-    const uint64_t n = kload(P.agg, (uint64_t)c * CLS_ROW + w);
+    const uint64_t n = T.agg[c * T.wmax + w];
     po += (int64_t)L.before[c] * (int64_t)(n & 0xffff);
     pw += (int64_t)L.before[c] * (int64_t)((n >> 16) & 0xffff);
     pj += (int64_t)L.before[c] * (int64_t)(n >> 32);
@@ -46,25 +126,25 @@ __device__ __forceinline__ TdGen td_gen(const TrajParams& P, const TmplLane& L, 
   G.pos0 = wb.pos + po;
   G.kwf = wb.wf + pw;
   G.kjob = wb.job + pj;
-  G.nrec = live ? (uint32_t)(P.agg[(uint64_t)crow + w] & 0xffff) : 0;
+  G.nrec = live ? (uint32_t)(T.agg[cls * T.wmax + w] & 0xffff) : 0;
   return G;
 }
-// record k of the instance's generation w, resolved from the class trace; *vl: its value length (the
-// encoder's, by the formula), *plen: its payload document's length
-__device__ __forceinline__ zb_rec td_record(const TrajParams& P, const TmplLane& L, uint32_t crow, int w, uint32_t k,
-                                            const TdGen& G, int64_t inst, uint32_t create_ref, uint32_t create_len,
-                                            uint32_t& vl, uint32_t& plen) {
-  const TmplRec t = P.tmpl[((uint64_t)crow + w) * TF + k];
+// record k of the instance's generation w, resolved from the class trace; vl: its value length (the
+// encoder's, by the formula), plen: its payload document's length
+__device__ __forceinline__ zb_rec td_record(const TrajParams& P, const TdTab& T, const TmplLane& L, uint32_t cls, int w,
+                                            uint32_t k, const TdGen& G, int64_t inst, uint32_t create_ref,
+                                            uint32_t create_len, uint32_t& vl, uint32_t& plen) {
+  const TmplRec t = T.tmpl[(cls * T.wmax + w) * TF + k];
   zb_rec d;
-  d.key = tmpl_key(P, L, t.key, (uint32_t)w, G.kwf, G.kjob);
-  d.scope_key = t.scope == SYM_CMDPOS ? P.log_base + inst : tmpl_key(P, L, t.scope, (uint32_t)w, G.kwf, G.kjob);
-  d.inst_key = tmpl_key(P, L, t.inst, (uint32_t)w, G.kwf, G.kjob);
+  d.key = td_key(P, T, L, t.key, (uint32_t)w, G.kwf, G.kjob);
+  d.scope_key = t.scope == SYM_CMDPOS ? P.log_base + inst : td_key(P, T, L, t.scope, (uint32_t)w, G.kwf, G.kjob);
+  d.inst_key = td_key(P, T, L, t.inst, (uint32_t)w, G.kwf, G.kjob);
   // (k_tmpl_decide: no merge results in a deferred batch -- the CREATE payload or a static blob)
   const bool cr = t.payload == PAY_CREATE;
   d.payload = cr ? create_ref : t.payload;
   plen = cr ? create_len : arena_len(P.arena, d.payload);
   d.elem = t.elem; d.intent = t.intent; d.kind = t.kind;
-  const ValueConst vc = kload(P.vconst, (uint64_t)d.elem);
+  const ValueConst vc = T.vconst[d.elem];
   vl = (kind_vt(d.kind) == ZB_VT_JOB ? vc.job : vc.wf) + mp_int_len(d.inst_key) + mp_int_len(d.scope_key) +
        mp_bin_len(plen);
   return d;
@@ -73,26 +153,25 @@ __device__ __forceinline__ zb_rec td_record(const TrajParams& P, const TmplLane&
 // lane setup shared by both passes: class, ranks, CREATE payload
 struct TdLane {
   TmplLane L;
-  uint32_t crow, W, create_ref, create_len;
+  uint32_t cls, W, create_ref, create_len;
   int64_t inst;
   bool active;
 };
-__device__ __forceinline__ TdLane td_lane(const TrajParams& P) {
+__device__ __forceinline__ TdLane td_lane(const TrajParams& P, const TdTab& T) {
   TdLane t;
   t.inst = (int64_t)blockIdx.x * TD_WG + threadIdx.x;
   t.active = t.inst < P.n;
   if (!t.active) t.inst = P.n - 1;  // (follows the last instance, writes nothing)
-  uint32_t cls = 0;
+  t.cls = 0;
   if (P.cls) {
     t.L.ncls = __builtin_amdgcn_readfirstlane(P.plan->nc);
-    cls = tmpl_lane_io(P, t.inst, t.L);
+    t.cls = tmpl_lane_io(P, t.inst, t.L);
   } else {
     t.L.ncls = 1;
 #pragma unroll
     for (int c = 0; c < CLS_MAX; c++) t.L.before[c] = c == 0 ? (uint32_t)t.inst : 0;
   }
-  t.crow = cls * CLS_ROW;
-  t.W = t.active ? P.wcount[cls] : 0;
+  t.W = t.active ? P.wcount[t.cls] : 0;  // generations of the instance's class (rows beyond it are not its)
   t.create_ref = P.log[P.log_base + t.inst].payload;
   t.create_len = arena_len(P.arena, t.create_ref);
   return t;
@@ -104,19 +183,22 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 }
 
 __global__ void __launch_bounds__(TD_WG) k_tdrain_size(TDrainParams D) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_tab[];
+  __shared__ unsigned long long s_pay[TD_WG / 64];
   const TrajParams& P = D.t;
-  const TdLane T = td_lane(P);
+  const TdTab T = td_load_tables(D, s_tab, false);
+  const TdLane L = td_lane(P, T);
   const int lane = threadIdx.x & 63;
   const uint64_t wave = (uint64_t)blockIdx.x * (TD_WG / 64) + (threadIdx.x >> 6);
   uint64_t pay = 0;
 #pragma unroll 1
   for (int w = 0; w < (int)D.wmax; w++) {
-    const TdGen G = td_gen(P, T.L, T.crow, w, w < (int)T.W);
+    const TdGen G = td_gen(T, L.L, L.cls, w, w < (int)L.W);
     uint32_t mine = 0;
 #pragma unroll 1
     for (uint32_t k = 0; k < G.nrec; k++) {
       uint32_t vl, plen;
-      (void)td_record(P, T.L, T.crow, w, k, G, T.inst, T.create_ref, T.create_len, vl, plen);
+      (void)td_record(P, T, L.L, L.cls, w, k, G, L.inst, L.create_ref, L.create_len, vl, plen);
       mine += vl;
       pay += plen;
     }
@@ -124,7 +206,6 @@ __global__ void __launch_bounds__(TD_WG) k_tdrain_size(TDrainParams D) {
     if (lane == 0) D.wbytes[(uint64_t)w * D.nwave + wave] = b;
   }
   // payload bytes of the drained records (zb_serialize_stats.payload_bytes): one partial per workgroup
-  __shared__ unsigned long long s_pay[TD_WG / 64];
   unsigned long long y = pay;
   for (int d = 32; d >= 1; d >>= 1) y += __shfl_down(y, d, 64);
   if (lane == 0) s_pay[threadIdx.x >> 6] = y;
@@ -132,20 +213,13 @@ __global__ void __launch_bounds__(TD_WG) k_tdrain_size(TDrainParams D) {
   if (threadIdx.x == 0) D.pay_part[blockIdx.x] = s_pay[0] + s_pay[1] + s_pay[2] + s_pay[3];
 }
 
-// LDS writes of other lanes of the wave are visible to this lane's later reads (and the reverse)
-__device__ __forceinline__ void wave_lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
-
-// image bytes [shift, shift + n) -> out[o, o + n): 16-byte non-temporal stores aligned to the destination,
-// bytes at the two ends (shared with the neighbouring ranges) one at a time
-__device__ __forceinline__ void wave_stream(const uint8_t* img, uint8_t* out, uint64_t o, uint32_t shift, uint32_t n,
-                                            int lane) {
+// image bytes [shift, shift + n) -> out[o, o + n) by the whole workgroup: 16-byte non-temporal stores aligned to
+// the destination, bytes at the two ends (shared with the neighbouring ranges) one at a time
+__device__ __forceinline__ void wg_stream(const uint8_t* img, uint8_t* out, uint64_t o, uint32_t shift, uint32_t n) {
   uint8_t* dst = out + o - shift;
   const uint32_t lim = shift + n;
   const uint32_t full_lo = (shift + 15) & ~15u, full_hi = lim & ~15u;
-  for (uint32_t c = full_lo + 16 * lane; c < full_hi; c += 16 * 64) {
+  for (uint32_t c = full_lo + 16 * threadIdx.x; c < full_hi; c += 16 * TD_WG) {
     const uint4 v = *(const uint4*)(img + c);
     __builtin_nontemporal_store(v.x, (uint32_t*)(dst + c));
     __builtin_nontemporal_store(v.y, (uint32_t*)(dst + c) + 1);
@@ -153,100 +227,90 @@ __device__ __forceinline__ void wave_stream(const uint8_t* img, uint8_t* out, ui
     __builtin_nontemporal_store(v.w, (uint32_t*)(dst + c) + 3);
   }
   const uint32_t head_end = full_lo < lim ? full_lo : lim;
-  for (uint32_t c = shift + lane; c < head_end; c += 64) dst[c] = img[c];
   const uint32_t tail_lo = full_hi > head_end ? full_hi : head_end;
-  for (uint32_t c = tail_lo + lane; c < lim; c += 64) dst[c] = img[c];
+  const uint32_t nh = head_end - shift;  // at most 15 + 15 bytes: one per lane
+  if (threadIdx.x < nh) dst[shift + threadIdx.x] = img[shift + threadIdx.x];
+  else if (threadIdx.x < nh + (lim - tail_lo)) dst[tail_lo + threadIdx.x - nh] = img[tail_lo + threadIdx.x - nh];
 }
 
 __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(4, 4))) k_tdrain_write(TDrainParams D) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_img[TD_WG / 64][TD_IMG + 16];
-  extern __shared__ __attribute__((aligned(16))) uint8_t s_model[];  // the constant runs (sized at launch)
+  __shared__ __attribute__((aligned(16))) uint8_t img[TD_IMG + 16];
+  __shared__ unsigned long long s_lo[TD_WG / 64];
+  __shared__ uint32_t s_n[TD_WG / 64];
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_tab[];  // value segments + the batch's tables
   const TrajParams& P = D.t;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint64_t wave = (uint64_t)blockIdx.x * (TD_WG / 64) + wv;
-  const TdLane T = td_lane(P);
+  const TdTab T = td_load_tables(D, s_tab, true);
+  const TdLane L = td_lane(P, T);
+  const TdLayout lay = td_layout(D, true);
+  const DevValSeg* tab = (const DevValSeg*)(s_tab + lay.tab);
+  const uint8_t* segs = s_tab + lay.pool;
   // the CREATE payload's first words (length + 44 bytes), once per instance
-  const uint64_t* cdw = (const uint64_t*)(P.arena + (uint64_t)T.create_ref * 8);
+  const uint64_t* cdw = (const uint64_t*)(P.arena + (uint64_t)L.create_ref * 8);
   uint64_t cpre[SER_PRE];
 #pragma unroll
   for (int j = 0; j < SER_PRE; j++)
-    cpre[j] = (uint64_t)T.create_ref * 8 + 8 * j + 8 <= P.arena_cap ? cdw[j] : 0;
-  // the elements' constant runs into LDS: table (4-byte words), pool (8-byte words)
-  const uint32_t tb = ((uint32_t)D.n_elems * (uint32_t)sizeof(DevValSeg) + 15) & ~15u;
-  for (uint32_t c = threadIdx.x; c < tb / 4; c += TD_WG) ((uint32_t*)s_model)[c] = ((const uint32_t*)D.vsegs)[c];  // (padded)
-  for (uint32_t c = threadIdx.x; c < D.segpool_len / 8; c += TD_WG)
-    ((uint64_t*)(s_model + tb))[c] = ((const uint64_t*)D.segpool)[c];
-  __syncthreads();
-  const DevValSeg* tab = (const DevValSeg*)s_model;
-  const uint8_t* segs = s_model + tb;
-  uint8_t* img = s_img[wv];
+    cpre[j] = (uint64_t)L.create_ref * 8 + 8 * j + 8 <= P.arena_cap ? cdw[j] : 0;
   uint32_t bad = 0;
-  int64_t hdr_key[TF];
-  uint32_t hdr_meta[TF], hdr_len[TF];
+  // the workgroup's generations: every wave runs the same loop (phases below synchronize the workgroup)
 #pragma unroll 1
   for (int w = 0; w < (int)D.wmax; w++) {
     const uint64_t wbase = D.woffs[(uint64_t)w * D.nwave + wave];
     const uint64_t wend = D.woffs[(uint64_t)w * D.nwave + wave + 1];
-    if (wend == wbase) continue;  // (uniform: no record of this wave in generation w)
-    const TdGen G = td_gen(P, T.L, T.crow, w, w < (int)T.W);
-    uint32_t mine = 0;
-#pragma unroll 1
-    for (uint32_t k = 0; k < G.nrec; k++) {  // value lengths first (the wave's offsets), headers with them
-      uint32_t vl, plen;
-      const zb_rec d = td_record(P, T.L, T.crow, w, k, G, T.inst, T.create_ref, T.create_len, vl, plen);
-      hdr_key[k & 1] = d.key;  // (TF == 2)
-      hdr_meta[k & 1] = (uint32_t)kind_rt(d.kind) | (uint32_t)kind_vt(d.kind) << 8 | (uint32_t)d.intent << 16 |
-                        255u << 24;  // (k_tmpl_decide: no rejections in a deferred batch)
-      hdr_len[k & 1] = vl;
-      mine += vl;
-    }
-    uint32_t incl = mine;
+    const bool any = wend != wbase;  // (uniform per wave)
+    const bool fits = wend <= D.out_cap;
+    if (!fits && lane == 0) atomicOr(D.flags, 1u);  // the host grows the buffer and runs the pass again
+    TdGen G;
+    G.nrec = 0;
+    uint32_t vl0 = 0, vl1 = 0;
+    zb_rec d0, d1;
+    uint64_t off = wbase;
+    if (any && fits) {
+      G = td_gen(T, L.L, L.cls, w, w < (int)L.W);
+      // value lengths first (the lane's offset in the wave's range), then the headers: key, types / intent /
+      // rejection, length, offset (the position is implicit: start + index)
+      uint32_t plen;
+      if (G.nrec > 0) d0 = td_record(P, T, L.L, L.cls, w, 0, G, L.inst, L.create_ref, L.create_len, vl0, plen);
+      if (G.nrec > 1) d1 = td_record(P, T, L.L, L.cls, w, 1, G, L.inst, L.create_ref, L.create_len, vl1, plen);
+      const uint32_t mine = vl0 + vl1;
+      uint32_t incl = mine;
 #pragma unroll
-    for (int k = 1; k < 64; k <<= 1) {
-      const uint32_t y = __shfl_up(incl, k, 64);
-      if (lane >= k) incl += y;
-    }
-    const uint64_t off = wbase + incl - mine;  // this lane's values: [off, off + mine)
-    if (wend > D.out_cap) {  // does not fit: the host grows the buffer and runs the pass again
-      if (lane == 0) atomicOr(D.flags, 1u);
-      continue;
-    }
-    // headers (position implicit: start + index): key, types / intent / rejection, length, offset
-    uint64_t hoff = off;
-#pragma unroll 1
-    for (uint32_t k = 0; k < G.nrec; k++) {
-      uint64_t* dh = (uint64_t*)(D.headers + (G.pos0 + k - D.start));
-      __builtin_nontemporal_store((uint64_t)hdr_key[k & 1], dh);
-      __builtin_nontemporal_store((uint64_t)hdr_meta[k & 1] | (uint64_t)hdr_len[k & 1] << 32, dh + 1);
-      __builtin_nontemporal_store(hoff, dh + 2);
-      hoff += hdr_len[k & 1];
-    }
-    // windows of whole lanes that fit the image, in lane order (the lanes' ranges are consecutive)
-    bool done = mine == 0;
-    if (!done && mine + 16 > TD_IMG) {  // one instance's records exceed the image: the host takes the generic path
-      bad = 1;
-      done = true;
-    }
-#pragma unroll 1
-    while (true) {
-      const uint64_t pend = __ballot(!done);
-      if (!pend) break;
-      const int first = __ffsll((unsigned long long)pend) - 1;
-      const uint64_t wlo = __shfl(off, first, 64);
-      const uint32_t sh = (uint32_t)(((uintptr_t)(D.out + wlo)) & 15);
-      const bool go = !done && (off + mine - wlo) + sh <= TD_IMG;
-      uint64_t hi = go ? off + mine : 0;
-      for (int d = 32; d >= 1; d >>= 1) {
-        const uint64_t y = (uint64_t)__shfl_xor((unsigned long long)hi, d, 64);
-        hi = y > hi ? y : hi;
+      for (int k = 1; k < 64; k <<= 1) {
+        const uint32_t y = __shfl_up(incl, k, 64);
+        if (lane >= k) incl += y;
       }
-      if (go) {
-        uint32_t at = sh + (uint32_t)(off - wlo);
+      off = wbase + incl - mine;  // this lane's values: [off, off + mine)
+#pragma unroll
+      for (int k = 0; k < TF; k++) {
+        if ((uint32_t)k >= G.nrec) break;
+        const zb_rec& d = k ? d1 : d0;
+        uint64_t* dh = (uint64_t*)(D.headers + (G.pos0 + k - D.start));
+        const uint64_t meta = (uint64_t)kind_rt(d.kind) | (uint64_t)kind_vt(d.kind) << 8 | (uint64_t)d.intent << 16 |
+                              255ull << 24 | (uint64_t)(k ? vl1 : vl0) << 32;  // (no rejections: k_tmpl_decide)
+        __builtin_nontemporal_store((uint64_t)d.key, dh);
+        __builtin_nontemporal_store(meta, dh + 1);
+        __builtin_nontemporal_store(off + (k ? vl0 : 0), dh + 2);
+      }
+    }
+    // phase k: wave k encodes its range into the image, then the workgroup streams it out
+    const uint32_t sh = (uint32_t)(((uintptr_t)(D.out + wbase)) & 15);
+    const bool enc = any && fits && (wend - wbase) + sh <= TD_IMG;
+    if (any && fits && !enc) bad = 1;  // a wave's range over the image: the host takes the descriptor path
+    if (lane == 0) {
+      s_lo[wv] = wbase;
+      s_n[wv] = enc ? (uint32_t)(wend - wbase) : 0u;
+    }
 #pragma unroll 1
-        for (uint32_t k = 0; k < G.nrec; k++) {
-          uint32_t vl, plen;
-          const zb_rec d = td_record(P, T.L, T.crow, w, k, G, T.inst, T.create_ref, T.create_len, vl, plen);
-          const bool cr = d.payload == T.create_ref;  // else a static blob (shared by every instance: cached)
+    for (int k = 0; k < TD_WG / 64; k++) {
+      __syncthreads();  // (the image is free; s_lo / s_n are set)
+      if (wv == k && enc) {
+        uint32_t at = sh + (uint32_t)(off - wbase);
+#pragma unroll 1
+        for (uint32_t r = 0; r < G.nrec; r++) {
+          const zb_rec& d = r ? d1 : d0;
+          const uint32_t vl = r ? vl1 : vl0;
+          const bool cr = d.payload == L.create_ref;  // else a static blob (shared by every instance: cached)
           const uint64_t* dw = (const uint64_t*)(P.arena + (uint64_t)d.payload * 8);
           uint64_t pre[SER_PRE];
 #pragma unroll
@@ -259,10 +323,12 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(4, 4
           at += vl;
         }
       }
-      wave_lds_sync();
-      wave_stream(img, D.out, wlo, sh, (uint32_t)(hi - wlo), lane);
-      wave_lds_sync();  // the image is reused by the next window
-      done = done || go;
+      __syncthreads();
+      const uint32_t n = s_n[k];
+      if (n) {
+        const uint64_t lo = s_lo[k];
+        wg_stream(img, D.out, lo, (uint32_t)(((uintptr_t)(D.out + lo)) & 15), n);
+      }
     }
   }
   if (bad) atomicOr(D.flags + 1, 1u);
@@ -309,21 +375,20 @@ __global__ void __launch_bounds__(256) k_tmpl_decide(TrajParams P) {
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) ctl->defer = (s_bad || !P.defer_ok) ? 0u : 1u;
+  // the drain keeps the tables in LDS (TD_MAX_GEN, TD_MAX_CW)
+  const bool fits = ctl->wmax <= TD_MAX_GEN && nc * ctl->wmax <= TD_MAX_CW;
+  if (threadIdx.x == 0) ctl->defer = (s_bad || !fits || !P.defer_ok) ? 0u : 1u;
 }
 
 void launch_tmpl_decide(const TrajParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_tmpl_decide, dim3(1), dim3(256), 0, s, p);
 }
 
-uint32_t tdrain_lds_bytes(const TDrainParams& d) {
-  return (((uint32_t)d.n_elems * (uint32_t)sizeof(DevValSeg) + 15) & ~15u) + d.segpool_len;
-}
 void launch_tdrain_size(const TDrainParams& d, hipStream_t s) {
-  hipLaunchKernelGGL(k_tdrain_size, dim3((unsigned)d.t.nwg), dim3(TD_WG), 0, s, d);
+  hipLaunchKernelGGL(k_tdrain_size, dim3((unsigned)d.t.nwg), dim3(TD_WG), td_layout(d, false).total, s, d);
 }
 void launch_tdrain_write(const TDrainParams& d, hipStream_t s) {
-  hipLaunchKernelGGL(k_tdrain_write, dim3((unsigned)d.t.nwg), dim3(TD_WG), tdrain_lds_bytes(d), s, d);
+  hipLaunchKernelGGL(k_tdrain_write, dim3((unsigned)d.t.nwg), dim3(TD_WG), td_layout(d, true).total, s, d);
   hipLaunchKernelGGL(k_tdrain_sum, dim3((unsigned)std::min<int64_t>(256, (d.t.nwg + 255) / 256)), dim3(256), 0, s, d,
                      (int64_t)d.t.nwg);
 }
