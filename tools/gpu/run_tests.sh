@@ -4,8 +4,9 @@
 set -o pipefail
 O=gpurun_out/tests
 mkdir -p $O
-K=${1:+-k "$1"}
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $K > $O/pytest.log 2>&1
+K=()
+[ -n "$1" ] && K=(-k "$1")
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" > $O/pytest.log 2>&1
 rc=$?
 tail -5 $O/pytest.log
 [ $rc -eq 0 ] || { grep -E "FAILED|Error|error" $O/pytest.log | head -20; exit $rc; }

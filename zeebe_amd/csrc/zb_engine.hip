@@ -209,6 +209,10 @@ struct zb_engine {
   int64_t clock_ms = 0;                   // zb_set_clock (ActorClock of the message stream processor)
   // message batches / delivered exchange batches
   uint8_t* m_prior = nullptr;
+  uint8_t* p_in = nullptr;        // zb_submit_publishes: the caller's keys / payloads / offsets on the device
+  uint64_t p_in_cap = 0;
+  uint64_t* p_gran = nullptr;     // [n + 1] blob granules, [n + 1] their scan, error flags
+  uint64_t p_gran_cap = 0;
   uint64_t m_prior_cap = 0;
   uint64_t* m_cnt = nullptr;
   uint64_t m_cnt_cap = 0;
@@ -1140,7 +1144,7 @@ void zb_engine_destroy(zb_engine* e) {
   void* ms[] = {e->obox[0], e->obox[1], e->okeys[0], e->okeys[1], e->ovar[0], e->ovar[1], e->on, e->subs, e->sub_head,
                 e->sub_next, e->msgs, e->msg_head, e->msg_next, e->d_xcounts, e->xsend, e->xrecv, e->ob_keys, e->ob_idx_in,
                 e->ob_idx_out, e->ob_first, e->ob_sizes, e->ob_goff, e->ob_table, e->ob_base, e->ob_tmp, e->ob_staging,
-                e->m_prior, e->m_cnt, e->m_tmp, e->in_buf};
+                e->m_prior, e->m_cnt, e->m_tmp, e->in_buf, e->p_in, e->p_gran};
   for (void* p : ms)
     if (p) (void)hipFree(p);
   if (e->h_hdr_pinned) (void)hipHostFree(e->h_hdr_pinned);
@@ -2578,19 +2582,32 @@ int scan_u64(zb_engine* e, uint64_t* in, uint64_t* out, uint64_t n, uint64_t* to
 
 // Appends the batch's commands at the log tail and processes them in order, runs of one intent in lockstep
 // (PUBLISH: count, scan, emit; DELETE: emit). Follow-ups come after all the commands, in command order (FIFO).
-int process_messages(zb_engine* e, const MsgBatch& b) {
-  const uint64_t n = b.recs.size();
-  if (n == 0) return ZB_OK;
+// capacity checks of a message batch of n commands (publishes of them) with blob_bytes of blobs
+int check_message_batch(zb_engine* e, uint64_t n, uint64_t publishes, uint64_t blob_bytes) {
   const int64_t base = e->host_hdr.end;
   // upper bounds first: every command writes at most 3 records (itself, PUBLISHED, DELETED)
   if ((uint64_t)(base - e->win_base) + 3 * n > e->cfg.log_capacity)
     return fail(e, ZB_ENOMEM, "log capacity (release drained records with zb_log_release)");
   if ((uint64_t)base + 3 * n >= (1ull << 34)) return fail(e, ZB_EUNSUPPORTED, "log position beyond the outbox order key");
+  if (e->msg_count + publishes > e->store_cap) return fail(e, ZB_ENOMEM, "message store capacity");
+  if ((uint64_t)e->host_hdr.arena_next + blob_bytes > e->cfg.arena_bytes) return fail(e, ZB_ENOMEM, "arena capacity");
+  return ZB_OK;
+}
+
+// the commands of a message batch are in the log at [end, end + n), their blobs at the arena tail (blob_bytes),
+// the intra-batch prior flags in m_prior: process them in runs of one intent (runs: [i0, i1) with its intent)
+int process_uploaded_messages(zb_engine* e, uint64_t n, uint64_t blob_bytes,
+                              const std::vector<std::pair<uint64_t, uint8_t>>& runs);
+
+int process_messages(zb_engine* e, const MsgBatch& b) {
+  const uint64_t n = b.recs.size();
+  if (n == 0) return ZB_OK;
+  const int64_t base = e->host_hdr.end;
   uint64_t publishes = 0;
   for (const zb_rec& r : b.recs) publishes += r.intent == 0 ? 1 : 0;
-  if (e->msg_count + publishes > e->store_cap) return fail(e, ZB_ENOMEM, "message store capacity");
+  int rc0 = check_message_batch(e, n, publishes, b.blobs.size());
+  if (rc0 != ZB_OK) return rc0;
   const uint64_t arena0 = (uint64_t)e->host_hdr.arena_next;
-  if (arena0 + b.blobs.size() > e->cfg.arena_bytes) return fail(e, ZB_ENOMEM, "arena capacity");
   // commands + blobs (refs made absolute on the host), one upload through pinned staging
   uint8_t* stage = host_stage(e, n * sizeof(zb_rec) + b.blobs.size() + n);
   if (!stage) return fail(e, ZB_ENOMEM, "pinned staging memory");
@@ -2602,22 +2619,38 @@ int process_messages(zb_engine* e, const MsgBatch& b) {
   std::memcpy(stage + n * sizeof(zb_rec), b.blobs.data(), b.blobs.size());
   std::memcpy(stage + n * sizeof(zb_rec) + b.blobs.size(), b.prior.data(), n);
   int rc = grow_dev(e, &e->m_prior, &e->m_prior_cap, n);
-  if (rc == ZB_OK) rc = grow_dev(e, (uint8_t**)&e->m_cnt, &e->m_cnt_cap, 2 * (n + 1) * sizeof(uint64_t));
   if (rc != ZB_OK) return rc;
   HIPCHECK(e, hipMemcpyAsync(e->log + base, recs, n * sizeof(zb_rec), hipMemcpyHostToDevice, e->stream));
   HIPCHECK(e, hipMemcpyAsync(e->arena + arena0, stage + n * sizeof(zb_rec), b.blobs.size(), hipMemcpyHostToDevice, e->stream));
   HIPCHECK(e, hipMemcpyAsync(e->m_prior, stage + n * sizeof(zb_rec) + b.blobs.size(), n, hipMemcpyHostToDevice, e->stream));
+  std::vector<std::pair<uint64_t, uint8_t>> runs;
+  for (uint64_t i0 = 0; i0 < n;) {
+    const uint8_t intent = b.recs[i0].intent;
+    uint64_t i1 = i0 + 1;
+    while (i1 < n && b.recs[i1].intent == intent) i1++;
+    runs.emplace_back(i1, intent);
+    i0 = i1;
+  }
+  return process_uploaded_messages(e, n, b.blobs.size(), runs);
+}
+
+int process_uploaded_messages(zb_engine* e, uint64_t n, uint64_t blob_bytes,
+                              const std::vector<std::pair<uint64_t, uint8_t>>& runs) {
+  const int64_t base = e->host_hdr.end;
+  int rc = grow_dev(e, (uint8_t**)&e->m_cnt, &e->m_cnt_cap, 2 * (n + 1) * sizeof(uint64_t));
+  if (rc != ZB_OK) return rc;
   HIPCHECK(e, hipMemsetAsync(e->links + base, 0xff, n * sizeof(uint64_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->srcd + base, 0, n * sizeof(uint32_t), e->stream));  // written by other writers
   // (the verbatim value of a submitted command is its serialized length: the size pass measures the rest)
   HIPCHECK(e, hipMemsetAsync(e->vlen + base, 0xff, n * sizeof(uint32_t), e->stream));
-  e->host_hdr.arena_next += (int64_t)b.blobs.size();
-  e->arena_total += b.blobs.size();
+  e->host_hdr.arena_next += (int64_t)blob_bytes;
+  e->arena_total += blob_bytes;
   int64_t out = base + (int64_t)n;  // the next follow-up position
+  size_t run = 0;
   for (uint64_t i0 = 0; i0 < n;) {
-    const uint8_t intent = b.recs[i0].intent;
-    uint64_t i1 = i0 + 1;
-    while (i1 < n && b.recs[i1].intent == intent && i1 - i0 < (1u << 20)) i1++;
+    while (runs[run].first <= i0) run++;
+    const uint8_t intent = runs[run].second;
+    const uint64_t i1 = std::min<uint64_t>(runs[run].first, i0 + (1u << 20));  // (the count packing: 2^21)
     MsgParams p = msg_params(e);
     p.base = base + (int64_t)i0;
     p.n = (int64_t)(i1 - i0);
@@ -2850,64 +2883,72 @@ int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, c
   if (rc != ZB_OK) return rc;
   if (n == 0) return ZB_OK;
   const uint32_t nn = (uint32_t)std::strlen(name);
-  static const uint8_t EMPTY = 0x80;
-  MsgBatch b;
-  b.recs.resize(n);
-  b.prior.assign(n, 0);
-  // PUBLISH commands (null key, no message id) and their blobs; large batches are built by up to 8 host threads
-  // over contiguous chunks (sized first, then filled)
-  const size_t nth = n >= 65536 ? std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency())) : 1;
-  const size_t chunk = (n + nth - 1) / nth;
-  std::vector<size_t> part_bytes(nth + 1, 0);
-  std::vector<int> part_err(nth, 0);
-  auto run_parts = [&](auto&& body) {
-    std::vector<std::thread> ths;
-    for (size_t t = 1; t < nth; t++) ths.emplace_back(body, t);
-    body((size_t)0);
-    for (auto& th : ths) th.join();
-  };
-  run_parts([&](size_t t) {
-    size_t bytes = 0;
-    for (size_t i = t * chunk; i < std::min(n, (t + 1) * chunk); i++) {
-      const uint64_t nc = ck_offsets[i + 1] - ck_offsets[i];
-      const uint8_t* pl = payloads + payload_offsets[i];
-      uint64_t np = payload_offsets[i + 1] - payload_offsets[i];
-      if (np == 0 || (np == 1 && pl[0] == 0xc0)) np = 1;
-      else if (!((pl[0] & 0xf0) == 0x80 || pl[0] == 0xde || pl[0] == 0xdf)) { part_err[t] = 1; return; }
-      if (nc > 0xffffffffull || np > 0xffffffffull) { part_err[t] = 2; return; }
-      bytes += (MSG_HDR + nn + nc + np + 7) & ~(size_t)7;
-    }
-    part_bytes[t + 1] = bytes;
-  });
-  for (size_t t = 0; t < nth; t++) {
-    if (part_err[t] == 1) return fail(e, ZB_EINVAL, "Document has invalid format. On root level an object is only allowed.");
-    if (part_err[t] == 2) return fail(e, ZB_EINVAL, "correlation key or payload too long");
-  }
-  for (size_t t = 0; t < nth; t++) part_bytes[t + 1] += part_bytes[t];
-  b.blobs.resize(part_bytes[nth]);
-  run_parts([&](size_t t) {
-    std::vector<uint8_t> tmp;
-    size_t off = part_bytes[t];
-    for (size_t i = t * chunk; i < std::min(n, (t + 1) * chunk); i++) {
-      const uint8_t* pl = payloads + payload_offsets[i];
-      uint64_t np = payload_offsets[i + 1] - payload_offsets[i];
-      if (np == 0 || (np == 1 && pl[0] == 0xc0)) { pl = &EMPTY; np = 1; }
-      tmp.clear();
-      add_msg_blob(tmp, (const uint8_t*)name, nn, cks + ck_offsets[i], (uint32_t)(ck_offsets[i + 1] - ck_offsets[i]),
-                   ttl, pl, (uint32_t)np, nullptr, 0);
-      std::memcpy(b.blobs.data() + off, tmp.data(), tmp.size());
-      zb_rec& d = b.recs[i];
-      d.key = -1; d.scope_key = -1; d.inst_key = -1;
-      d.payload = (uint32_t)(off >> 3);
-      d.elem = NO_ELEM; d.intent = 0;  // PUBLISH
-      d.kind = make_kind(ZB_VT_MESSAGE, ZB_RT_COMMAND, false);
-      off += tmp.size();
-    }
-  });
   rc = ensure_stores(e);
   if (rc == ZB_OK) rc = maintain(e, false);
   if (rc != ZB_OK) return rc;
-  return process_messages(e, b);
+  // The caller's correlation keys / payloads go up as they are (one pinned staging copy, by up to 8 host
+  // threads for large batches); the commands and message blobs are built on the device (k_pub_sizes / scan /
+  // k_pub_build, zb_msg.hip) -- all-or-nothing: nothing reaches the log or the arena before the checks pass.
+  const uint64_t ckb = ck_offsets[n] - ck_offsets[0], plb = payload_offsets[n] - payload_offsets[0];
+  const uint64_t offb = (n + 1) * sizeof(uint64_t);
+  const uint64_t a_ck = 0, a_cko = (ckb + 15) & ~15ull, a_pl = a_cko + offb, a_plo = a_pl + ((plb + 15) & ~15ull);
+  const uint64_t a_name = a_plo + offb, total = a_name + ((nn + 16) & ~15ull);
+  uint8_t* stage = host_stage(e, total);
+  if (!stage) return fail(e, ZB_ENOMEM, "pinned staging memory");
+  {
+    struct Piece { uint8_t* dst; const uint8_t* src; uint64_t n; };
+    const Piece pieces[5] = {{stage + a_ck, cks + ck_offsets[0], ckb}, {stage + a_cko, (const uint8_t*)ck_offsets, offb},
+                             {stage + a_pl, payloads + payload_offsets[0], plb},
+                             {stage + a_plo, (const uint8_t*)payload_offsets, offb}, {stage + a_name, (const uint8_t*)name, nn}};
+    const size_t nth = total >= (16u << 20) ? std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency())) : 1;
+    auto body = [&](size_t t) {  // byte range [t, t + 1) / nth of every piece
+      for (const Piece& q : pieces) {
+        const uint64_t lo = q.n * t / nth, hi = q.n * (t + 1) / nth;
+        if (hi > lo) std::memcpy(q.dst + lo, q.src + lo, hi - lo);
+      }
+    };
+    std::vector<std::thread> ths;
+    for (size_t t = 1; t < nth; t++) ths.emplace_back(body, t);
+    body(0);
+    for (auto& th : ths) th.join();
+  }
+  rc = grow_dev(e, &e->p_in, &e->p_in_cap, total);
+  if (rc == ZB_OK) rc = grow_dev(e, (uint8_t**)&e->p_gran, &e->p_gran_cap, 2 * (n + 1) * sizeof(uint64_t) + 16);
+  if (rc == ZB_OK) rc = grow_dev(e, &e->m_prior, &e->m_prior_cap, n);
+  if (rc != ZB_OK) return rc;
+  HIPCHECK(e, hipMemcpyAsync(e->p_in, stage, total, hipMemcpyHostToDevice, e->stream));
+  PubBuild pb{};
+  pb.cks = e->p_in + a_ck;
+  pb.ck_off = (const uint64_t*)(e->p_in + a_cko);
+  pb.pls = e->p_in + a_pl;
+  pb.pl_off = (const uint64_t*)(e->p_in + a_plo);
+  pb.name = e->p_in + a_name;
+  pb.nn = nn;
+  pb.ttl = ttl;
+  pb.n = n;
+  pb.gran = e->p_gran;
+  pb.goff = e->p_gran + (n + 1);
+  uint32_t* err = (uint32_t*)(e->p_gran + 2 * (n + 1));
+  pb.err = err;
+  HIPCHECK(e, hipMemsetAsync(err, 0, 2 * sizeof(uint32_t), e->stream));
+  launch_pub_sizes(pb, e->stream);
+  uint64_t gran = 0;
+  rc = scan_u64(e, e->p_gran, e->p_gran + (n + 1), n, &gran);  // (sets gran[n] = 0 first)
+  if (rc != ZB_OK) return rc;
+  uint32_t herr[2] = {0, 0};
+  HIPCHECK(e, hipMemcpyAsync(herr, err, sizeof(herr), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));  // (the scan's total too)
+  if (herr[0]) return fail(e, ZB_EINVAL, "Document has invalid format. On root level an object is only allowed.");
+  if (herr[1]) return fail(e, ZB_EINVAL, "correlation key or payload too long");
+  rc = check_message_batch(e, n, n, gran * 8);
+  if (rc != ZB_OK) return rc;
+  pb.arena = e->arena;
+  pb.arena0 = (uint64_t)e->host_hdr.arena_next;
+  pb.out = e->log + e->host_hdr.end;
+  launch_pub_build(pb, e->stream);
+  HIPCHECK(e, hipMemsetAsync(e->m_prior, 0, n, e->stream));  // (no message ids: no duplicates)
+  std::vector<std::pair<uint64_t, uint8_t>> runs{{n, (uint8_t)0}};
+  return process_uploaded_messages(e, n, gran * 8, runs);
 }
 
 int zb_expire_messages(zb_engine* e, int64_t now_ms, uint64_t* n_deleted) {

@@ -378,6 +378,55 @@ __global__ void k_outbox_pack(Outbox ob, const uint32_t* idx, const uint64_t* ke
   const uint32_t g = var_granules(r.name_len, r.ck_len, r.payload_len);
   for (uint32_t k = 0; k < g; k++) vd[k] = src[k];
 }
+// ---- zb_submit_publishes on the device. The blob layout is zb_msg.hpp's MsgView (no message id, deadline set
+// when the message is stored); an empty or nil payload document becomes {} (PublishMessageProcessor: payload
+// defaults to the empty document), anything but a map is the reference's "Document has invalid format" rejection
+__global__ void k_pub_sizes(PubBuild p) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > p.n) return;
+  if (i == p.n) { p.gran[i] = 0; return; }
+  const uint64_t nc = p.ck_off[i + 1] - p.ck_off[i];
+  const uint8_t* pl = p.pls + (p.pl_off[i] - p.pl_off[0]);
+  uint64_t np = p.pl_off[i + 1] - p.pl_off[i];
+  if (np == 0 || (np == 1 && pl[0] == 0xc0)) np = 1;
+  else if (!((pl[0] & 0xf0) == 0x80 || pl[0] == 0xde || pl[0] == 0xdf)) atomicOr(p.err, 1u);
+  if (nc > 0xffffffffull || np > 0xffffffffull) atomicOr(p.err + 1, 1u);
+  p.gran[i] = (MSG_HDR + p.nn + nc + np + 7) >> 3;
+}
+__global__ void k_pub_build(PubBuild p) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  const uint64_t at = p.arena0 + p.goff[i] * 8;
+  uint8_t* b = p.arena + at;
+  const uint8_t* ck = p.cks + (p.ck_off[i] - p.ck_off[0]);
+  const uint32_t nc = (uint32_t)(p.ck_off[i + 1] - p.ck_off[i]);
+  const uint8_t* pl = p.pls + (p.pl_off[i] - p.pl_off[0]);
+  uint32_t np = (uint32_t)(p.pl_off[i + 1] - p.pl_off[i]);
+  const bool empty = np == 0 || (np == 1 && pl[0] == 0xc0);
+  if (empty) np = 1;
+  const uint32_t len = MSG_HDR - 4 + p.nn + nc + np;
+  uint32_t* h = (uint32_t*)b;
+  h[0] = len; h[1] = p.nn;
+  *(int64_t*)(b + 8) = p.ttl;
+  *(int64_t*)(b + 16) = 0;  // deadline: set when the message is stored
+  h[6] = nc; h[7] = np; h[8] = 0; h[9] = 0;
+  uint8_t* d = b + MSG_HDR;
+  for (uint32_t k = 0; k < p.nn; k++) d[k] = p.name[k];
+  d += p.nn;
+  for (uint32_t k = 0; k < nc; k++) d[k] = ck[k];
+  d += nc;
+  if (empty) d[0] = 0x80;
+  else for (uint32_t k = 0; k < np; k++) d[k] = pl[k];
+  const uint32_t end = MSG_HDR + p.nn + nc + np, pad_end = (end + 7) & ~7u;
+  for (uint32_t k = end; k < pad_end; k++) b[k] = 0;
+  zb_rec r;
+  r.key = -1; r.scope_key = -1; r.inst_key = -1;
+  r.payload = (uint32_t)(at >> 3);
+  r.elem = NO_ELEM; r.intent = 0;  // PUBLISH
+  r.kind = make_kind(ZB_VT_MESSAGE, ZB_RT_COMMAND, false);
+  p.out[i] = r;
+}
+
 __global__ void k_iota(uint32_t* p, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = (uint32_t)i;
@@ -389,6 +438,12 @@ static unsigned grid_cap(uint64_t n) {
   return (unsigned)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
 }
 
+void launch_pub_sizes(const PubBuild& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_pub_sizes, dim3(blocks((int64_t)p.n + 1)), dim3(256), 0, s, p);
+}
+void launch_pub_build(const PubBuild& p, hipStream_t s) {
+  if (p.n) hipLaunchKernelGGL(k_pub_build, dim3(blocks((int64_t)p.n)), dim3(256), 0, s, p);
+}
 void launch_msg_open(const MsgParams& p, hipStream_t s) {
   if (p.n > 0) hipLaunchKernelGGL(k_msg_open, dim3(blocks(p.n)), dim3(256), 0, s, p);
 }

@@ -25,9 +25,9 @@
 namespace zbg {
 
 constexpr int TD_WG = TRAJ_WG;  // 256 lanes = 256 instances, four waves
-// the workgroup's image holds one wave's values of one generation (64 instances x at most TF records); a range
-// larger than that sends the batch to the descriptor path (ZB_EAGAIN). 28 KB + the tables: four workgroups per CU
-constexpr uint32_t TD_IMG = 28 * 1024 - 16;
+// each wave's image: a round of up to 64 records whose bytes fit it (a single record larger than the image sends
+// the batch to the descriptor path, ZB_EAGAIN). 4 x 7 KB + the tables (~10 KB for C3): four workgroups per CU
+constexpr uint32_t TD_IMG = 7 * 1024 - 16;
 
 // The batch's tables in LDS (every lookup of the generation loop is an LDS read, not a dependent global load):
 //   agg[c][w]  records | wf keys << 16 | job keys << 32 of class c in generation w (one instance)
@@ -213,13 +213,20 @@ __global__ void __launch_bounds__(TD_WG) k_tdrain_size(TDrainParams D) {
   if (threadIdx.x == 0) D.pay_part[blockIdx.x] = s_pay[0] + s_pay[1] + s_pay[2] + s_pay[3];
 }
 
-// image bytes [shift, shift + n) -> out[o, o + n) by the whole workgroup: 16-byte non-temporal stores aligned to
-// the destination, bytes at the two ends (shared with the neighbouring ranges) one at a time
-__device__ __forceinline__ void wg_stream(const uint8_t* img, uint8_t* out, uint64_t o, uint32_t shift, uint32_t n) {
+// LDS writes of other lanes of the wave are visible to this lane's later reads (and the reverse)
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// image bytes [shift, shift + n) -> out[o, o + n) by one wave: 16-byte non-temporal stores aligned to the
+// destination, bytes at the two ends (shared with the neighbouring ranges) one at a time
+__device__ __forceinline__ void wave_stream(const uint8_t* img, uint8_t* out, uint64_t o, uint32_t shift, uint32_t n,
+                                            int lane) {
   uint8_t* dst = out + o - shift;
   const uint32_t lim = shift + n;
   const uint32_t full_lo = (shift + 15) & ~15u, full_hi = lim & ~15u;
-  for (uint32_t c = full_lo + 16 * threadIdx.x; c < full_hi; c += 16 * TD_WG) {
+  for (uint32_t c = full_lo + 16 * lane; c < full_hi; c += 16 * 64) {
     const uint4 v = *(const uint4*)(img + c);
     __builtin_nontemporal_store(v.x, (uint32_t*)(dst + c));
     __builtin_nontemporal_store(v.y, (uint32_t*)(dst + c) + 1);
@@ -229,14 +236,14 @@ __device__ __forceinline__ void wg_stream(const uint8_t* img, uint8_t* out, uint
   const uint32_t head_end = full_lo < lim ? full_lo : lim;
   const uint32_t tail_lo = full_hi > head_end ? full_hi : head_end;
   const uint32_t nh = head_end - shift;  // at most 15 + 15 bytes: one per lane
-  if (threadIdx.x < nh) dst[shift + threadIdx.x] = img[shift + threadIdx.x];
-  else if (threadIdx.x < nh + (lim - tail_lo)) dst[tail_lo + threadIdx.x - nh] = img[tail_lo + threadIdx.x - nh];
+  if ((uint32_t)lane < nh) dst[shift + lane] = img[shift + lane];
+  else if ((uint32_t)lane < nh + (lim - tail_lo)) dst[tail_lo + lane - nh] = img[tail_lo + lane - nh];
 }
 
-__global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(4, 4))) k_tdrain_write(TDrainParams D) {
-  __shared__ __attribute__((aligned(16))) uint8_t img[TD_IMG + 16];
-  __shared__ unsigned long long s_lo[TD_WG / 64];
-  __shared__ uint32_t s_n[TD_WG / 64];
+template <uint32_t IMG>
+__global__ void __launch_bounds__(TD_WG) k_tdrain_write(TDrainParams D) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_img[TD_WG / 64][IMG + 16];
+  __shared__ uint8_t s_own[TD_WG / 64][64 * TF];  // record rank -> owner lane | k << 6
   extern __shared__ __attribute__((aligned(16))) uint8_t s_tab[];  // value segments + the batch's tables
   const TrajParams& P = D.t;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -246,89 +253,97 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(4, 4
   const TdLayout lay = td_layout(D, true);
   const DevValSeg* tab = (const DevValSeg*)(s_tab + lay.tab);
   const uint8_t* segs = s_tab + lay.pool;
-  // the CREATE payload's first words (length + 44 bytes), once per instance
-  const uint64_t* cdw = (const uint64_t*)(P.arena + (uint64_t)L.create_ref * 8);
-  uint64_t cpre[SER_PRE];
-#pragma unroll
-  for (int j = 0; j < SER_PRE; j++)
-    cpre[j] = (uint64_t)L.create_ref * 8 + 8 * j + 8 <= P.arena_cap ? cdw[j] : 0;
+  uint8_t* img = s_img[wv];
+  uint8_t* own = s_own[wv];
   uint32_t bad = 0;
-  // the workgroup's generations: every wave runs the same loop (phases below synchronize the workgroup)
 #pragma unroll 1
   for (int w = 0; w < (int)D.wmax; w++) {
     const uint64_t wbase = D.woffs[(uint64_t)w * D.nwave + wave];
     const uint64_t wend = D.woffs[(uint64_t)w * D.nwave + wave + 1];
-    const bool any = wend != wbase;  // (uniform per wave)
-    const bool fits = wend <= D.out_cap;
-    if (!fits && lane == 0) atomicOr(D.flags, 1u);  // the host grows the buffer and runs the pass again
-    TdGen G;
-    G.nrec = 0;
+    if (wend == wbase) continue;  // (uniform: no record of this wave in generation w)
+    if (wend > D.out_cap) {  // does not fit: the host grows the buffer and runs the pass again
+      if (lane == 0) atomicOr(D.flags, 1u);
+      continue;
+    }
+    const TdGen G = td_gen(T, L.L, L.cls, w, w < (int)L.W);
     uint32_t vl0 = 0, vl1 = 0;
-    zb_rec d0, d1;
-    uint64_t off = wbase;
-    if (any && fits) {
-      G = td_gen(T, L.L, L.cls, w, w < (int)L.W);
-      // value lengths first (the lane's offset in the wave's range), then the headers: key, types / intent /
-      // rejection, length, offset (the position is implicit: start + index)
+    zb_rec d0{}, d1{};
+    {
       uint32_t plen;
       if (G.nrec > 0) d0 = td_record(P, T, L.L, L.cls, w, 0, G, L.inst, L.create_ref, L.create_len, vl0, plen);
       if (G.nrec > 1) d1 = td_record(P, T, L.L, L.cls, w, 1, G, L.inst, L.create_ref, L.create_len, vl1, plen);
-      const uint32_t mine = vl0 + vl1;
-      uint32_t incl = mine;
-#pragma unroll
-      for (int k = 1; k < 64; k <<= 1) {
-        const uint32_t y = __shfl_up(incl, k, 64);
-        if (lane >= k) incl += y;
-      }
-      off = wbase + incl - mine;  // this lane's values: [off, off + mine)
-#pragma unroll
-      for (int k = 0; k < TF; k++) {
-        if ((uint32_t)k >= G.nrec) break;
-        const zb_rec& d = k ? d1 : d0;
-        uint64_t* dh = (uint64_t*)(D.headers + (G.pos0 + k - D.start));
-        const uint64_t meta = (uint64_t)kind_rt(d.kind) | (uint64_t)kind_vt(d.kind) << 8 | (uint64_t)d.intent << 16 |
-                              255ull << 24 | (uint64_t)(k ? vl1 : vl0) << 32;  // (no rejections: k_tmpl_decide)
-        __builtin_nontemporal_store((uint64_t)d.key, dh);
-        __builtin_nontemporal_store(meta, dh + 1);
-        __builtin_nontemporal_store(off + (k ? vl0 : 0), dh + 2);
-      }
     }
-    // phase k: wave k encodes its range into the image, then the workgroup streams it out
-    const uint32_t sh = (uint32_t)(((uintptr_t)(D.out + wbase)) & 15);
-    const bool enc = any && fits && (wend - wbase) + sh <= TD_IMG;
-    if (any && fits && !enc) bad = 1;  // a wave's range over the image: the host takes the descriptor path
-    if (lane == 0) {
-      s_lo[wv] = wbase;
-      s_n[wv] = enc ? (uint32_t)(wend - wbase) : 0u;
-    }
-#pragma unroll 1
-    for (int k = 0; k < TD_WG / 64; k++) {
-      __syncthreads();  // (the image is free; s_lo / s_n are set)
-      if (wv == k && enc) {
-        uint32_t at = sh + (uint32_t)(off - wbase);
-#pragma unroll 1
-        for (uint32_t r = 0; r < G.nrec; r++) {
-          const zb_rec& d = r ? d1 : d0;
-          const uint32_t vl = r ? vl1 : vl0;
-          const bool cr = d.payload == L.create_ref;  // else a static blob (shared by every instance: cached)
-          const uint64_t* dw = (const uint64_t*)(P.arena + (uint64_t)d.payload * 8);
-          uint64_t pre[SER_PRE];
+    const uint32_t mine = vl0 + vl1;
+    uint32_t incl = mine, rincl = G.nrec;
 #pragma unroll
-          for (int j = 0; j < SER_PRE; j++)
-            pre[j] = cr ? cpre[j] : ((uint64_t)d.payload * 8 + 8 * j + 8 <= P.arena_cap ? dw[j] : 0);
-          FastW fw;
-          fw.begin(img, at);
-          fast_encode(fw, d, tab, segs, dw, pre);
-          if (fw.n() != vl) bad = 1;  // the formula and the encoder disagree: never silently
-          at += vl;
-        }
+    for (int k = 1; k < 64; k <<= 1) {
+      const uint32_t y = __shfl_up(incl, k, 64), z = __shfl_up(rincl, k, 64);
+      if (lane >= k) { incl += y; rincl += z; }
+    }
+    const uint32_t rel = incl - mine;  // this lane's values: [wbase + rel, wbase + rel + mine)
+    const uint32_t r0 = rincl - G.nrec, R = __shfl(rincl, 63, 64);
+    // headers: key, types / intent / rejection, length, offset (the position is implicit: start + index)
+#pragma unroll
+    for (int k = 0; k < TF; k++) {
+      if ((uint32_t)k >= G.nrec) break;
+      const zb_rec& d = k ? d1 : d0;
+      uint64_t* dh = (uint64_t*)(D.headers + (G.pos0 + k - D.start));
+      const uint64_t meta = (uint64_t)kind_rt(d.kind) | (uint64_t)kind_vt(d.kind) << 8 | (uint64_t)d.intent << 16 |
+                            255ull << 24 | (uint64_t)(k ? vl1 : vl0) << 32;  // (no rejections: k_tmpl_decide)
+      __builtin_nontemporal_store((uint64_t)d.key, dh);
+      __builtin_nontemporal_store(meta, dh + 1);
+      __builtin_nontemporal_store(wbase + rel + (k ? vl0 : 0), dh + 2);
+      own[r0 + k] = (uint8_t)(lane | k << 6);
+    }
+    wave_lds_sync();
+#pragma unroll 1
+    for (uint32_t a = 0; a < R;) {
+      // record a + lane: its owner, offset in the wave's range and length
+      const uint32_t r = a + (uint32_t)lane;
+      const bool valid = r < R;
+      const uint32_t o = valid ? own[r] : 0u;
+      const int src = (int)(o & 63), k = (int)(o >> 6);
+      const uint32_t o_rel = __shfl(rel, src, 64), o_vl0 = __shfl(vl0, src, 64), o_vl1 = __shfl(vl1, src, 64);
+      const uint32_t roff = o_rel + (k ? o_vl0 : 0u), rlen = k ? o_vl1 : o_vl0;
+      const uint32_t lo = __shfl(roff, 0, 64);  // the round's first byte (record a)
+      const uint32_t sh = (uint32_t)(((uintptr_t)(D.out + wbase + lo)) & 15);
+      const bool fit = valid && roff + rlen - lo + sh <= IMG;  // (a prefix of the lanes: offsets increase with r)
+      const uint32_t nfit = (uint32_t)__builtin_popcountll(__ballot(fit));
+      // the owner's descriptors (every lane takes part in the shuffles)
+      zb_rec d;  // (both of the owner's records are moved; the lane's k selects)
+      const int64_t k0 = __shfl(d0.key, src, 64), k1 = __shfl(d1.key, src, 64);
+      const int64_t s0 = __shfl(d0.scope_key, src, 64), s1 = __shfl(d1.scope_key, src, 64);
+      const int64_t i0 = __shfl(d0.inst_key, src, 64), i1 = __shfl(d1.inst_key, src, 64);
+      const uint32_t p0 = __shfl(d0.payload, src, 64), p1 = __shfl(d1.payload, src, 64);
+      const uint32_t m0 = __shfl((uint32_t)d0.elem | (uint32_t)d0.intent << 16 | (uint32_t)d0.kind << 24, src, 64);
+      const uint32_t m1 = __shfl((uint32_t)d1.elem | (uint32_t)d1.intent << 16 | (uint32_t)d1.kind << 24, src, 64);
+      d.key = k ? k1 : k0;
+      d.scope_key = k ? s1 : s0;
+      d.inst_key = k ? i1 : i0;
+      d.payload = k ? p1 : p0;
+      const uint32_t m = k ? m1 : m0;
+      d.elem = (uint16_t)m;
+      d.intent = (uint8_t)(m >> 16);
+      d.kind = (uint8_t)(m >> 24);
+      if (nfit == 0) {  // one record larger than the image: the host takes the descriptor path
+        bad = 1;
+        break;
       }
-      __syncthreads();
-      const uint32_t n = s_n[k];
-      if (n) {
-        const uint64_t lo = s_lo[k];
-        wg_stream(img, D.out, lo, (uint32_t)(((uintptr_t)(D.out + lo)) & 15), n);
+      if (fit) {
+        const uint64_t* dw = (const uint64_t*)(P.arena + (uint64_t)d.payload * 8);
+        uint64_t pre[SER_PRE];
+#pragma unroll
+        for (int j = 0; j < SER_PRE; j++) pre[j] = (uint64_t)d.payload * 8 + 8 * j + 8 <= P.arena_cap ? dw[j] : 0;
+        FastW fw;
+        fw.begin(img, sh + (roff - lo));
+        fast_encode(fw, d, tab, segs, dw, pre);
+        if (fw.n() != rlen) bad = 1;  // the formula and the encoder disagree: never silently
       }
+      const uint32_t hi = __shfl(roff + rlen, (int)nfit - 1, 64);
+      wave_lds_sync();
+      wave_stream(img, D.out, wbase + lo, sh, hi - lo, lane);
+      wave_lds_sync();  // the image is reused by the next round
+      a += nfit;
     }
   }
   if (bad) atomicOr(D.flags + 1, 1u);
@@ -388,7 +403,7 @@ void launch_tdrain_size(const TDrainParams& d, hipStream_t s) {
   hipLaunchKernelGGL(k_tdrain_size, dim3((unsigned)d.t.nwg), dim3(TD_WG), td_layout(d, false).total, s, d);
 }
 void launch_tdrain_write(const TDrainParams& d, hipStream_t s) {
-  hipLaunchKernelGGL(k_tdrain_write, dim3((unsigned)d.t.nwg), dim3(TD_WG), td_layout(d, true).total, s, d);
+  hipLaunchKernelGGL((k_tdrain_write<TD_IMG>), dim3((unsigned)d.t.nwg), dim3(TD_WG), td_layout(d, true).total, s, d);
   hipLaunchKernelGGL(k_tdrain_sum, dim3((unsigned)std::min<int64_t>(256, (d.t.nwg + 255) / 256)), dim3(256), 0, s, d,
                      (int64_t)d.t.nwg);
 }
