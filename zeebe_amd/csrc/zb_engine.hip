@@ -75,6 +75,7 @@ struct zb_engine {
   DevVec<DevWorkflow> d_wfs;
   DevVec<uint16_t> d_cond;
   DevVec<uint32_t> d_code;
+  DevVec<uint32_t> d_cls_code;  // the program with the split conditions' path operands as extraction slots
   DevVec<DevConst> d_consts;
   DevVec<DevQuery> d_queries;
   DevVec<DevFilter> d_filters;
@@ -572,6 +573,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   p.elems = e->d_elems.p;
   p.cond_flows = e->d_cond.p;
   p.code = e->d_code.p;
+  p.cls_code = e->d_cls_code.p;
   p.consts = e->d_consts.p;
   p.queries = e->d_queries.p;
   p.filters = e->d_filters.p;
@@ -596,7 +598,10 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
     if (grc != ZB_OK) return grc;
     // instance-order emit (k_tmpl_io) over the instance workgroups; ZB_TMPL_IO=0: class-uniform emit, every
     // (block, class) segment padded to whole waves, a multiple of 8 workgroups (XCD mapping)
-    p.io = e->tmpl_io;
+    // (a batch the drain may take from its traces skips the class-uniform slot layout: if it is emitted after all,
+    // now or when materialized, the emit runs in instance order)
+    const bool may_defer = e->tmpl_defer && e->seg_ok && e->d_vsegs.p && e->d_vconst.p;
+    p.io = e->tmpl_io || may_defer;
     if (!p.io) p.nwg_e = (int32_t)(((cls_slot_bound((uint64_t)n, nwg) + TRAJ_WG - 1) / TRAJ_WG + 7) & ~7ull);
     p.nblk = (int32_t)((nwg + CLS_BLK_WG - 1) / CLS_BLK_WG);
     p.segs = e->c_segs;
@@ -1081,7 +1086,8 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   }
   if (hipMalloc(&e->rmeta, e->cfg.row_capacity * sizeof(RowMeta)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->rkeys, e->cfg.row_capacity * sizeof(RowKeys)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipMalloc(&e->arena, e->cfg.arena_bytes) != hipSuccess) return cleanup(ZB_ENOMEM);
+  // (+ ARENA_SLACK: the drain's encoders load a payload document's first words without a bounds check)
+  if (hipMalloc(&e->arena, e->cfg.arena_bytes + ARENA_SLACK) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->hdr, 2 * sizeof(WaveHdr)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->cw, e->wave_cap * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->stage, e->wave_cap * 2 * sizeof(Slot)) != hipSuccess) return cleanup(ZB_ENOMEM);
@@ -1150,7 +1156,7 @@ void zb_engine_destroy(zb_engine* e) {
   if (e->h_hdr_pinned) (void)hipHostFree(e->h_hdr_pinned);
   if (e->h_err_pinned) (void)hipHostFree(e->h_err_pinned);
   if (e->h_ctl_pinned) (void)hipHostFree(e->h_ctl_pinned);
-  e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_consts.free();
+  e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_cls_code.free(); e->d_consts.free();
   e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
   e->d_ranges.free(); e->d_cmd_pool.free(); e->d_lookup_keys.free(); e->d_lookup_pos.free();
   e->d_maps.free();
@@ -1318,6 +1324,33 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
     }
   }
   if (!ext_ok) e->cls_nq = 0;
+  // k_cls_classify runs the split conditions on the extracted operands: their path operand fields name the
+  // extraction slot instead of the query (a wave-uniform index into the extraction)
+  std::vector<uint32_t> cc = e->model.code;
+  if (e->cls_nq) {
+    for (int k = 0; k < e->nsplits; k++) {
+      const DevElem& el = e->model.elems[e->split_elem[k]];
+      for (uint32_t c = 0; c < el.cond_count; c++) {
+        const DevElem& flow = e->model.elems[e->model.cond_flows[el.cond_begin + c]];
+        if (flow.cond_prog == NO_REF) continue;
+        for (uint32_t pc = flow.cond_prog; 2 * pc + 1 < cc.size(); pc++) {
+          const uint32_t w0 = cc[2 * pc];
+          if ((w0 & 0xff) == PC_END) break;
+          if ((w0 & 0xff) != PC_CMP) continue;
+          uint32_t w1 = e->model.code[2 * pc + 1];
+          for (int side = 0; side < 2; side++) {
+            if (!((w0 >> (12 + side)) & 1)) continue;
+            const uint16_t q = (uint16_t)(side ? w1 >> 16 : w1 & 0xffff);
+            uint32_t j = 0;
+            while ((int)j < e->cls_nq && e->cls_q[j] != q) j++;
+            w1 = side ? ((w1 & 0xffffu) | j << 16) : ((w1 & 0xffff0000u) | j);
+          }
+          cc[2 * pc + 1] = w1;
+        }
+      }
+    }
+  }
+  HIPCHECK(e, e->d_cls_code.upload(cc, e->stream));
   return upload_model(e);
 }
 

@@ -93,17 +93,25 @@ struct FastW {
     put(((neg ? 0xd0u : 0xccu) + lg) | be << 8, m < 8 ? m + 1 : 8);
     if (m == 8) put((uint8_t)v, 1);
   }
-  // a constant run: c bytes at s (LDS, 8-aligned, zero-padded to 8); FIRST as in put
+  // a constant run: c bytes at s (LDS, 8-aligned, zero-padded to 8); FIRST as in put. The run's words are read
+  // four at a time, issued together (the pool is padded so that a batch never reads past it): the LDS latency is
+  // paid per batch, not per word
   template <bool FIRST = false>
   __device__ __forceinline__ void seg(const uint8_t* s, uint32_t c) {
     const uint64_t* w = (const uint64_t*)s;
-    uint32_t k = 0;
-    if (FIRST) { put<true>(w[0], 8); k = 8; }
-    for (; k < c; k += 8) put(w[k >> 3], c - k < 8 ? c - k : 8);
+    for (uint32_t k = 0; k < c; k += 32) {
+      const uint64_t v0 = w[(k >> 3)], v1 = w[(k >> 3) + 1], v2 = w[(k >> 3) + 2], v3 = w[(k >> 3) + 3];
+      if (FIRST && k == 0) put<true>(v0, 8);
+      else put(v0, c - k < 8 ? c - k : 8);
+      if (k + 8 < c) put(v1, c - k - 8 < 8 ? c - k - 8 : 8);
+      if (k + 16 < c) put(v2, c - k - 16 < 8 ? c - k - 16 : 8);
+      if (k + 24 < c) put(v3, c - k - 24 < 8 ? c - k - 24 : 8);
+    }
   }
 };
 
 constexpr int SER_PRE = 6;  // payload document words prefetched per record (length + 44 bytes)
+constexpr uint32_t ARENA_SLACK = 64;  // bytes allocated past the arena: SER_PRE words load unchecked
 
 // The constant runs of an element's values, built at deploy time (build_value_segments) and copied into LDS
 // by the write pass: a run is appended 8 bytes at a time from aligned LDS words instead of key by key.
@@ -262,7 +270,7 @@ inline bool build_value_segments(const DevElem* elems, size_t n_elems, const Dev
     seg_key(b, "payload");
     if (!add(b, t.off8[SEG_JOB_C], t.len[SEG_JOB_C])) return false;
   }
-  segs.resize(segs.size() + 8, 0);  // (a run's last word is read whole)
+  segs.resize(segs.size() + 32, 0);  // (a run's last words are read in a batch of four)
   return true;
 }
 

@@ -97,12 +97,14 @@ __device__ __forceinline__ int64_t td_kbase(const TdTab& T, const TmplLane& L, u
   }
   return k;
 }
+// kwf0: the instance's wf key ordinal base of generation 0 (its process instance key: the workflowInstanceKey and
+// the flow scope of most records), computed once per lane
 __device__ __forceinline__ int64_t td_key(const TrajParams& P, const TdTab& T, const TmplLane& L, uint32_t sym,
-                                          uint32_t w, int64_t kwf, int64_t kjob) {
+                                          uint32_t w, int64_t kwf, int64_t kjob, int64_t kwf0) {
   if (sym == NOK) return -1;
   if (sym == JOB_ZERO) return 0;
   const uint32_t g = (sym >> 4) & 0xfff, ord = sym & 15;
-  if (sym & SYMK_WF) return P.wf_start + 5 * ((g == w ? kwf : td_kbase(T, L, g, 1)) + ord);
+  if (sym & SYMK_WF) return P.wf_start + 5 * ((g == w ? kwf : g == 0 ? kwf0 : td_kbase(T, L, g, 1)) + ord);
   return P.job_start + 5 * ((g == w ? kjob : td_kbase(T, L, g, 2)) + ord);
 }
 
@@ -133,12 +135,12 @@ __device__ __forceinline__ TdGen td_gen(const TdTab& T, const TmplLane& L, uint3
 // encoder's, by the formula), plen: its payload document's length
 __device__ __forceinline__ zb_rec td_record(const TrajParams& P, const TdTab& T, const TmplLane& L, uint32_t cls, int w,
                                             uint32_t k, const TdGen& G, int64_t inst, uint32_t create_ref,
-                                            uint32_t create_len, uint32_t& vl, uint32_t& plen) {
+                                            uint32_t create_len, int64_t kwf0, uint32_t& vl, uint32_t& plen) {
   const TmplRec t = T.tmpl[(cls * T.wmax + w) * TF + k];
   zb_rec d;
-  d.key = td_key(P, T, L, t.key, (uint32_t)w, G.kwf, G.kjob);
-  d.scope_key = t.scope == SYM_CMDPOS ? P.log_base + inst : td_key(P, T, L, t.scope, (uint32_t)w, G.kwf, G.kjob);
-  d.inst_key = td_key(P, T, L, t.inst, (uint32_t)w, G.kwf, G.kjob);
+  d.key = td_key(P, T, L, t.key, (uint32_t)w, G.kwf, G.kjob, kwf0);
+  d.scope_key = t.scope == SYM_CMDPOS ? P.log_base + inst : td_key(P, T, L, t.scope, (uint32_t)w, G.kwf, G.kjob, kwf0);
+  d.inst_key = td_key(P, T, L, t.inst, (uint32_t)w, G.kwf, G.kjob, kwf0);
   // (k_tmpl_decide: no merge results in a deferred batch -- the CREATE payload or a static blob)
   const bool cr = t.payload == PAY_CREATE;
   d.payload = cr ? create_ref : t.payload;
@@ -154,7 +156,7 @@ __device__ __forceinline__ zb_rec td_record(const TrajParams& P, const TdTab& T,
 struct TdLane {
   TmplLane L;
   uint32_t cls, W, create_ref, create_len;
-  int64_t inst;
+  int64_t inst, kwf0;
   bool active;
 };
 __device__ __forceinline__ TdLane td_lane(const TrajParams& P, const TdTab& T) {
@@ -174,6 +176,7 @@ __device__ __forceinline__ TdLane td_lane(const TrajParams& P, const TdTab& T) {
   t.W = t.active ? P.wcount[t.cls] : 0;  // generations of the instance's class (rows beyond it are not its)
   t.create_ref = P.log[P.log_base + t.inst].payload;
   t.create_len = arena_len(P.arena, t.create_ref);
+  t.kwf0 = td_kbase(T, t.L, 0, 1);
   return t;
 }
 
@@ -198,7 +201,7 @@ __global__ void __launch_bounds__(TD_WG) k_tdrain_size(TDrainParams D) {
 #pragma unroll 1
     for (uint32_t k = 0; k < G.nrec; k++) {
       uint32_t vl, plen;
-      (void)td_record(P, T, L.L, L.cls, w, k, G, L.inst, L.create_ref, L.create_len, vl, plen);
+      (void)td_record(P, T, L.L, L.cls, w, k, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl, plen);
       mine += vl;
       pay += plen;
     }
@@ -270,8 +273,8 @@ __global__ void __launch_bounds__(TD_WG) k_tdrain_write(TDrainParams D) {
     zb_rec d0{}, d1{};
     {
       uint32_t plen;
-      if (G.nrec > 0) d0 = td_record(P, T, L.L, L.cls, w, 0, G, L.inst, L.create_ref, L.create_len, vl0, plen);
-      if (G.nrec > 1) d1 = td_record(P, T, L.L, L.cls, w, 1, G, L.inst, L.create_ref, L.create_len, vl1, plen);
+      if (G.nrec > 0) d0 = td_record(P, T, L.L, L.cls, w, 0, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl0, plen);
+      if (G.nrec > 1) d1 = td_record(P, T, L.L, L.cls, w, 1, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl1, plen);
     }
     const uint32_t mine = vl0 + vl1;
     uint32_t incl = mine, rincl = G.nrec;
@@ -333,7 +336,7 @@ __global__ void __launch_bounds__(TD_WG) k_tdrain_write(TDrainParams D) {
         const uint64_t* dw = (const uint64_t*)(P.arena + (uint64_t)d.payload * 8);
         uint64_t pre[SER_PRE];
 #pragma unroll
-        for (int j = 0; j < SER_PRE; j++) pre[j] = (uint64_t)d.payload * 8 + 8 * j + 8 <= P.arena_cap ? dw[j] : 0;
+        for (int j = 0; j < SER_PRE; j++) pre[j] = dw[j];  // (ARENA_SLACK: never past the allocation)
         FastW fw;
         fw.begin(img, sh + (roff - lo));
         fast_encode(fw, d, tab, segs, dw, pre);

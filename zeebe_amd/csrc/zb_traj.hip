@@ -1174,7 +1174,8 @@ __device__ __forceinline__ void extract_fast(const TrajParams& P, const uint8_t*
     pos = vend;
   }
 }
-// load_operand_k with the query results taken from the extraction
+// load_operand_k with the query results taken from the extraction: a path operand names its extraction slot
+// (P.cls_code), a wave-uniform index
 __device__ __forceinline__ bool load_operand_x(const TrajParams& P, bool is_path, uint32_t idx, const uint8_t* doc,
                                                const Extract& x, Operand& o, CondOut& out, bool& unsupported) {
   if (!is_path) {
@@ -1183,12 +1184,13 @@ __device__ __forceinline__ bool load_operand_x(const TrajParams& P, bool is_path
     return true;
   }
   if (!x.ok) { unsupported = true; return false; }
+  const uint32_t j = __builtin_amdgcn_readfirstlane(idx);
   uint32_t cnt = 0, rpos = 0, rlen = 0;
 #pragma unroll
-  for (int j = 0; j < CLS_QMAX; j++)
-    if (j < P.cls_nq && P.cls_q[j] == idx) { cnt = x.cnt[j]; rpos = x.pos[j]; rlen = x.len[j]; }
-  if (cnt == 0) { out.err = EC_PATH_NO_RESULT; out.q = (uint16_t)idx; return false; }
-  if (cnt > 1) { out.err = EC_PATH_MULTI; out.q = (uint16_t)idx; return false; }
+  for (int jj = 0; jj < CLS_QMAX; jj++)  // (a scalar compare: no dynamically indexed register array)
+    if ((uint32_t)jj == j) { cnt = x.cnt[jj]; rpos = x.pos[jj]; rlen = x.len[jj]; }
+  if (cnt == 0) { out.err = EC_PATH_NO_RESULT; out.q = (uint16_t)j; return false; }
+  if (cnt > 1) { out.err = EC_PATH_MULTI; out.q = (uint16_t)j; return false; }
   Tok t;
   if (!read_tok(doc + rpos, rlen, t)) { unsupported = true; return false; }
   o.type = t.type; o.bval = t.bval; o.ival = t.ival; o.fval = t.fval;
@@ -1206,8 +1208,9 @@ __device__ __forceinline__ bool eval_condition_sweep(const TrajParams& P, uint32
   bool r = false, done = false;
   uint32_t mine = pc0;
   out.err = 0;
+  const uint32_t* code = EXT ? P.cls_code : P.code;
   for (uint32_t pc = pc0; pc < pc0 + 4096; pc++) {
-    const uint32_t w0 = K(P.code)[2 * pc], w1 = K(P.code)[2 * pc + 1];
+    const uint32_t w0 = K(code)[2 * pc], w1 = K(code)[2 * pc + 1];
     const uint32_t opc = w0 & 0xff;
     if (opc == PC_END) return done ? false : r;
     if (done || mine != pc) continue;
@@ -1292,6 +1295,7 @@ __global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
   s_len[t] = 0;
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * TWG + t;
+  uint32_t mkey = 0, mlen = 0;
   if (i < P.n) {
     const uint32_t ref = P.log[P.log_base + i].payload;
     const uint8_t* pp = P.arena + (uint64_t)ref * 8;
@@ -1307,9 +1311,25 @@ __global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
       for (int k = 0; k < P.nsplits; k++) key += (elem_ctl(P, P.split_elem[k]).cond_count() + 1) * P.split_stride[k];
     }
     P.ikey[i] = (uint8_t)key;
-    atomicAdd(&s_hist[key & 255], 1u);
-    atomicMin(&s_rep[key & 255], (uint32_t)i);
-    atomicAdd(&s_len[key & 255], (unsigned long long)len);
+    mkey = key & 255;
+    mlen = len;
+  }
+  // key histogram: one leader per distinct key of the wave adds the wave's count, first instance and payload
+  // bytes (LDS atomics of 64 lanes on a few addresses serialize)
+  uint64_t act = __ballot(i < P.n);
+  while (act) {
+    const int l = __ffsll((unsigned long long)act) - 1;
+    const uint32_t k0 = __shfl(mkey, l, 64);
+    const bool in = i < P.n && mkey == k0;
+    const uint64_t m = __ballot(in);
+    unsigned long long y = in ? (unsigned long long)mlen : 0ull;
+    for (int d = 32; d >= 1; d >>= 1) y += __shfl_xor(y, d, 64);
+    if ((t & 63) == l) {  // (the first lane of the key: the smallest instance)
+      atomicAdd(&s_hist[k0], (uint32_t)__builtin_popcountll(m));
+      atomicMin(&s_rep[k0], (uint32_t)i);
+      atomicAdd(&s_len[k0], y);
+    }
+    act &= ~m;
   }
   __syncthreads();
   if (s_hist[t]) {
