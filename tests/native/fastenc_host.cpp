@@ -7,6 +7,11 @@
 #define __device__
 #define __host__
 #define __forceinline__ inline
+// v_alignbyte_b32: bytes [s, s + 4) of the little-endian pair (lo, hi), s = c mod 4
+static inline uint32_t host_alignbyte(uint32_t hi, uint32_t lo, uint32_t c) {
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (c & 3)));
+}
+#define __builtin_amdgcn_alignbyte host_alignbyte
 #include "../../zeebe_amd/csrc/zb_fastenc.hpp"
 
 using namespace zbg;

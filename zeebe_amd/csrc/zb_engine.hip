@@ -316,6 +316,8 @@ struct zb_engine {
   bool seg_pending = false;
   int64_t seg_begin = 0, seg_end = 0;
   uint32_t seg_wmax = 0, seg_nc = 1;
+  int64_t seg_key_end = 0;  // every key and position the deferred batch's records carry is below this
+  bool seg_jobs = false;    // the deferred batch created job keys
   TrajParams seg_p{};
   uint64_t* td_wbytes = nullptr;  // [wmax * nwave + 1] (u64: hipcub's scan accumulates in the input type)
   uint64_t* td_woffs = nullptr;
@@ -703,6 +705,8 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
     e->seg_begin = log_base + n;
     e->seg_end = e->host_hdr.end;
     e->seg_wmax = e->h_ctl_pinned->wmax;
+    e->seg_key_end = std::max(std::max(e->host_hdr.wf_next, e->host_hdr.job_next), e->host_hdr.end);
+    e->seg_jobs = e->host_hdr.job_next != p.job_start;
     e->seg_p = p;
     e->seg_nc = 1;
     if (p.cls) HIPCHECK(e, hipMemcpy(&e->seg_nc, e->c_plan, sizeof(uint32_t), hipMemcpyDeviceToHost));  // ClsPlan.nc
@@ -2200,6 +2204,8 @@ static int serialize_deferred(zb_engine* e, int64_t start, int64_t count, zb_ser
   d.segpool_len = e->segpool_len;
   d.n_elems = (int32_t)e->model.elems.size();
   d.nc = e->seg_nc;
+  d.len5_ok = e->seg_key_end <= (int64_t)UINT32_MAX ? 1u : 0u;
+  d.jobs = e->seg_jobs ? 1u : 0u;
   float ms_size = 0, ms_scan = 0, ms_write = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     d.out = e->dr_val;

@@ -93,20 +93,63 @@ struct FastW {
     put(((neg ? 0xd0u : 0xccu) + lg) | be << 8, m < 8 ? m + 1 : 8);
     if (m == 8) put((uint8_t)v, 1);
   }
-  // a constant run: c bytes at s (LDS, 8-aligned, zero-padded to 8); FIRST as in put. The run's words are read
-  // four at a time, issued together (the pool is padded so that a batch never reads past it): the LDS latency is
-  // paid per batch, not per word
+  // a constant run: c bytes at s (LDS, 8-aligned; the pool keeps SEG_PAD_LO readable bytes before its first run
+  // and SEG_PAD_HI after its last); FIRST as in put. The byte shift between the run and the image is fixed for
+  // the whole run, so image slot j is bytes [r, r + 8) of three consecutive run dwords p[2j..2j+2] (p: the run
+  // read from a 4-aligned start chosen by the shift): two v_alignbyte and one aligned ds_write_b64 per slot. The
+  // dwords are read eight at a time, issued together: the LDS latency is paid per four slots.
   template <bool FIRST = false>
   __device__ __forceinline__ void seg(const uint8_t* s, uint32_t c) {
-    const uint64_t* w = (const uint64_t*)s;
-    for (uint32_t k = 0; k < c; k += 32) {
-      const uint64_t v0 = w[(k >> 3)], v1 = w[(k >> 3) + 1], v2 = w[(k >> 3) + 2], v3 = w[(k >> 3) + 3];
-      if (FIRST && k == 0) put<true>(v0, 8);
-      else put(v0, c - k < 8 ? c - k : 8);
-      if (k + 8 < c) put(v1, c - k - 8 < 8 ? c - k - 8 : 8);
-      if (k + 16 < c) put(v2, c - k - 16 < 8 ? c - k - 16 : 8);
-      if (k + 24 < c) put(v3, c - k - 24 < 8 ? c - k - 24 : 8);
+    const uint32_t f = pos & 7, e = 8 - f, r = e & 3;
+    const uint32_t* p = (const uint32_t*)(s + 4 * (e >> 2)) - 2;
+    const uint32_t end = f + c, nf = end >> 3, rem = end & 7;
+    const uint64_t own0 = f ? (~0ull << (8 * f)) : ~0ull;  // slot 0: the run's bytes (below them: acc)
+    const uint32_t slot = pos - f;
+    uint32_t x0 = p[0];
+    for (uint32_t j = 0; j <= nf; j += 4) {
+      uint32_t x[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) x[k] = p[2 * j + 1 + k];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t jj = j + k;
+        if (jj > nf) break;
+        const uint32_t a = k ? x[2 * k - 1] : x0;
+        uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(x[2 * k], a, r) |
+                     (uint64_t)__builtin_amdgcn_alignbyte(x[2 * k + 1], x[2 * k], r) << 32;
+        if (jj == 0) v = acc | (v & own0);
+        if (jj < nf) {
+          if (FIRST && jj == 0 && f) first = v;
+          else *(uint64_t*)(img + slot + 8 * jj) = v;
+        } else {
+          acc = rem ? v & (~0ull >> (64 - 8 * rem)) : 0;
+        }
+      }
+      x0 = x[7];
     }
+    pos += c;
+  }
+  // n bytes (n > 0) of a register-resident run: v[i] = bytes [8i, 8i + 8) (bytes past n are masked off), n <= 8N;
+  // the image shift is fixed for the run: slot i = acc | v[i] << 8f, then acc = v[i] >> (64 - 8f)
+  template <int N>
+  __device__ __forceinline__ void words(const uint64_t (&v)[N], uint32_t n) {
+    const uint32_t f = pos & 7, sl = 8 * f, sr = 63 - sl;
+    const uint32_t end = f + n, nf = end >> 3, rem = end & 7;
+    const uint32_t slot = pos - f;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      if ((uint32_t)i > nf) break;
+      const uint64_t x = (uint32_t)(8 * i) < n ? v[i] : 0ull;
+      const uint64_t o = acc | (x << sl);
+      if ((uint32_t)i < nf) {
+        *(uint64_t*)(img + slot + 8 * i) = o;
+        acc = (x >> 1) >> sr;  // (f == 0: 0)
+      } else {
+        acc = o;
+      }
+    }
+    acc = rem ? acc & (~0ull >> (64 - 8 * rem)) : 0;  // slot nf: the run's last bytes
+    pos += n;
   }
 };
 
@@ -127,6 +170,7 @@ struct DevValSeg {
   uint16_t len[SEG_N];
 };
 static_assert(sizeof(DevValSeg) == 20, "DevValSeg is 20 bytes");
+constexpr uint32_t SEG_PAD_LO = 16, SEG_PAD_HI = 48;  // readable bytes before the first run / after the last
 constexpr uint32_t SEG_LDS_MAX = 16384;  // table (padded to 4 entries) + pool the fast passes copy into LDS
 
 // the payload document [u32 len][bytes] as binary (MsgPackWriter.writeBinary): doc words W_j (8-aligned), the
@@ -137,22 +181,19 @@ __device__ __forceinline__ void fast_bin(FastW& w, const uint64_t* dw, const uin
   if (plen < 256) w.put(0xc4 | (uint64_t)plen << 8, 2);
   else if (plen < 65536) w.put(0xc5 | (uint64_t)__builtin_bswap16((uint16_t)plen) << 8, 3);
   else w.put(0xc6 | (uint64_t)__builtin_bswap32(plen) << 8, 5);
+  if (plen == 0) return;
+  constexpr uint32_t NPRE = 8 * (SER_PRE - 1);  // payload bytes in the prefetched words
+  uint64_t v[SER_PRE - 1];
 #pragma unroll
-  for (int j = 1; j < SER_PRE; j++) {
-    const uint32_t k = 8 * (j - 1);
-    if (k < plen) {
-      const uint64_t v = (pre[j - 1] >> 32) | (pre[j] << 32);
-      const uint32_t r = plen - k;
-      w.put(r < 8 ? v & (~0ull >> (64 - 8 * r)) : v, r < 8 ? r : 8);
-    }
-  }
-  if (plen > 8 * (SER_PRE - 1)) {  // longer payloads: the rest from HBM (no load past the document)
+  for (int j = 1; j < SER_PRE; j++) v[j - 1] = (pre[j - 1] >> 32) | (pre[j] << 32);
+  w.words(v, plen < NPRE ? plen : NPRE);
+  if (plen > NPRE) {  // longer payloads: the rest from HBM (no load past the document)
     uint64_t cur = pre[SER_PRE - 1];
-    for (uint32_t k = 8 * (SER_PRE - 1), j = SER_PRE; k < plen; k += 8, j++) {
+    for (uint32_t k = NPRE, j = SER_PRE; k < plen; k += 8, j++) {
       const uint64_t nx = k + 4 < plen ? dw[j] : 0;
-      const uint64_t v = (cur >> 32) | (nx << 32);
+      const uint64_t x = (cur >> 32) | (nx << 32);
       const uint32_t r = plen - k;
-      w.put(r < 8 ? v & (~0ull >> (64 - 8 * r)) : v, r < 8 ? r : 8);
+      w.put(r < 8 ? x & (~0ull >> (64 - 8 * r)) : x, r < 8 ? r : 8);
       cur = nx;
     }
   }
@@ -220,7 +261,7 @@ inline void seg_key(std::vector<uint8_t>& b, const char* k) {
 inline bool build_value_segments(const DevElem* elems, size_t n_elems, const DevWorkflow* wfs, size_t n_wfs,
                                  const uint8_t* pool, std::vector<DevValSeg>& tab, std::vector<uint8_t>& segs) {
   tab.assign(n_elems, DevValSeg{});
-  segs.clear();
+  segs.assign(SEG_PAD_LO, 0);  // (FastW::seg reads up to 8 bytes before a run)
   auto add = [&](const std::vector<uint8_t>& b, uint16_t& off8, uint16_t& len) {
     if (segs.size() / 8 > 0xffff || b.size() > 0xffff) return false;
     off8 = (uint16_t)(segs.size() / 8);
@@ -270,7 +311,7 @@ inline bool build_value_segments(const DevElem* elems, size_t n_elems, const Dev
     seg_key(b, "payload");
     if (!add(b, t.off8[SEG_JOB_C], t.len[SEG_JOB_C])) return false;
   }
-  segs.resize(segs.size() + 32, 0);  // (a run's last words are read in a batch of four)
+  segs.resize(segs.size() + SEG_PAD_HI, 0);  // (FastW::seg reads up to 40 bytes past a run)
   return true;
 }
 

@@ -25,9 +25,11 @@
 namespace zbg {
 
 constexpr int TD_WG = TRAJ_WG;  // 256 lanes = 256 instances, four waves
-// each wave's image: a round of up to 64 records whose bytes fit it (a single record larger than the image sends
-// the batch to the descriptor path, ZB_EAGAIN). 4 x 7 KB + the tables (~10 KB for C3): four workgroups per CU
-constexpr uint32_t TD_IMG = 7 * 1024 - 16;
+// each wave's image: one round of the wave's records of a generation (64 records of C3, ~10 KB); a lane whose
+// records alone exceed it sends the batch to the descriptor path (ZB_EAGAIN). 4 x 11 KB + the tables (~8 KB for
+// C3): three workgroups per CU, as the 135 VGPRs allow (measured: 7 KB images, four workgroups, 2 rounds per
+// generation: 1.3x the time)
+constexpr uint32_t TD_IMG = 11 * 1024 - 16;
 
 // The batch's tables in LDS (every lookup of the generation loop is an LDS read, not a dependent global load):
 //   agg[c][w]  records | wf keys << 16 | job keys << 32 of class c in generation w (one instance)
@@ -185,6 +187,9 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
   return x;
 }
 
+// msgpack length of a symbolic key / position (td_key) known to be -1, 0 or in [2^16, 2^32)
+__device__ __forceinline__ uint32_t td_len5(uint32_t sym) { return (sym == NOK || sym == JOB_ZERO) ? 1u : 5u; }
+
 __global__ void __launch_bounds__(TD_WG) k_tdrain_size(TDrainParams D) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_tab[];
   __shared__ unsigned long long s_pay[TD_WG / 64];
@@ -193,17 +198,37 @@ __global__ void __launch_bounds__(TD_WG) k_tdrain_size(TDrainParams D) {
   const TdLane L = td_lane(P, T);
   const int lane = threadIdx.x & 63;
   const uint64_t wave = (uint64_t)blockIdx.x * (TD_WG / 64) + (threadIdx.x >> 6);
+  // Short form: when the wave's smallest key and position (its first lane's generation-0 bases, which every later
+  // key of the wave exceeds) are >= 2^16 and the batch's largest is below 2^32, every key / position the wave's
+  // records carry encodes in 5 bytes (MsgPackWriter.writeInteger): the lengths follow from the traces alone,
+  // without resolving a single key. Otherwise (the first 13k keys of a partition) td_record resolves each one.
+  const bool lo_ok = P.wf_start + 5 * L.kwf0 >= 65536 && P.log_base + L.inst >= 65536 &&
+                     (!D.jobs || P.job_start + 5 * td_kbase(T, L.L, 0, 2) >= 65536);
+  const bool len5 = D.len5_ok && __shfl(lo_ok ? 1 : 0, 0, 64);
   uint64_t pay = 0;
 #pragma unroll 1
   for (int w = 0; w < (int)D.wmax; w++) {
-    const TdGen G = td_gen(T, L.L, L.cls, w, w < (int)L.W);
     uint32_t mine = 0;
+    if (len5) {
+      const uint32_t nrec = w < (int)L.W ? (uint32_t)(T.agg[L.cls * T.wmax + w] & 0xffff) : 0u;
+#pragma unroll
+      for (int k = 0; k < TF; k++) {
+        if ((uint32_t)k >= nrec) break;
+        const TmplRec t = T.tmpl[(L.cls * T.wmax + w) * TF + k];
+        const uint32_t plen = t.payload == PAY_CREATE ? L.create_len : arena_len(P.arena, t.payload);
+        const ValueConst vc = T.vconst[t.elem];
+        mine += (kind_vt(t.kind) == ZB_VT_JOB ? vc.job : vc.wf) + td_len5(t.inst) + td_len5(t.scope) + mp_bin_len(plen);
+        pay += plen;
+      }
+    } else {
+      const TdGen G = td_gen(T, L.L, L.cls, w, w < (int)L.W);
 #pragma unroll 1
-    for (uint32_t k = 0; k < G.nrec; k++) {
-      uint32_t vl, plen;
-      (void)td_record(P, T, L.L, L.cls, w, k, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl, plen);
-      mine += vl;
-      pay += plen;
+      for (uint32_t k = 0; k < G.nrec; k++) {
+        uint32_t vl, plen;
+        (void)td_record(P, T, L.L, L.cls, w, k, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl, plen);
+        mine += vl;
+        pay += plen;
+      }
     }
     const uint32_t b = wave_sum(mine);
     if (lane == 0) D.wbytes[(uint64_t)w * D.nwave + wave] = b;
@@ -244,9 +269,8 @@ __device__ __forceinline__ void wave_stream(const uint8_t* img, uint8_t* out, ui
 }
 
 template <uint32_t IMG>
-__global__ void __launch_bounds__(TD_WG) k_tdrain_write(TDrainParams D) {
+__global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4))) k_tdrain_write(TDrainParams D) {
   __shared__ __attribute__((aligned(16))) uint8_t s_img[TD_WG / 64][IMG + 16];
-  __shared__ uint8_t s_own[TD_WG / 64][64 * TF];  // record rank -> owner lane | k << 6
   extern __shared__ __attribute__((aligned(16))) uint8_t s_tab[];  // value segments + the batch's tables
   const TrajParams& P = D.t;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -257,7 +281,11 @@ __global__ void __launch_bounds__(TD_WG) k_tdrain_write(TDrainParams D) {
   const DevValSeg* tab = (const DevValSeg*)(s_tab + lay.tab);
   const uint8_t* segs = s_tab + lay.pool;
   uint8_t* img = s_img[wv];
-  uint8_t* own = s_own[wv];
+  // the instance's CREATE payload document, read once: every record of a deferred batch carries it or a static blob
+  const uint64_t* cdw = (const uint64_t*)(P.arena + (uint64_t)L.create_ref * 8);
+  uint64_t cpre[SER_PRE];
+#pragma unroll
+  for (int j = 0; j < SER_PRE; j++) cpre[j] = cdw[j];  // (ARENA_SLACK: never past the allocation)
   uint32_t bad = 0;
 #pragma unroll 1
   for (int w = 0; w < (int)D.wmax; w++) {
@@ -277,14 +305,13 @@ __global__ void __launch_bounds__(TD_WG) k_tdrain_write(TDrainParams D) {
       if (G.nrec > 1) d1 = td_record(P, T, L.L, L.cls, w, 1, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl1, plen);
     }
     const uint32_t mine = vl0 + vl1;
-    uint32_t incl = mine, rincl = G.nrec;
+    uint32_t incl = mine;
 #pragma unroll
     for (int k = 1; k < 64; k <<= 1) {
-      const uint32_t y = __shfl_up(incl, k, 64), z = __shfl_up(rincl, k, 64);
-      if (lane >= k) { incl += y; rincl += z; }
+      const uint32_t y = __shfl_up(incl, k, 64);
+      if (lane >= k) incl += y;
     }
-    const uint32_t rel = incl - mine;  // this lane's values: [wbase + rel, wbase + rel + mine)
-    const uint32_t r0 = rincl - G.nrec, R = __shfl(rincl, 63, 64);
+    const uint32_t rel = incl - mine;  // this lane's values: [wbase + rel, wbase + incl)
     // headers: key, types / intent / rejection, length, offset (the position is implicit: start + index)
 #pragma unroll
     for (int k = 0; k < TF; k++) {
@@ -296,57 +323,44 @@ __global__ void __launch_bounds__(TD_WG) k_tdrain_write(TDrainParams D) {
       __builtin_nontemporal_store((uint64_t)d.key, dh);
       __builtin_nontemporal_store(meta, dh + 1);
       __builtin_nontemporal_store(wbase + rel + (k ? vl0 : 0), dh + 2);
-      own[r0 + k] = (uint8_t)(lane | k << 6);
     }
-    wave_lds_sync();
+    // rounds: lanes [a, b) whose values fit the image from the round's first byte; each lane encodes its own
+    // records (no redistribution: a generation of C3 is one round of every lane)
 #pragma unroll 1
-    for (uint32_t a = 0; a < R;) {
-      // record a + lane: its owner, offset in the wave's range and length
-      const uint32_t r = a + (uint32_t)lane;
-      const bool valid = r < R;
-      const uint32_t o = valid ? own[r] : 0u;
-      const int src = (int)(o & 63), k = (int)(o >> 6);
-      const uint32_t o_rel = __shfl(rel, src, 64), o_vl0 = __shfl(vl0, src, 64), o_vl1 = __shfl(vl1, src, 64);
-      const uint32_t roff = o_rel + (k ? o_vl0 : 0u), rlen = k ? o_vl1 : o_vl0;
-      const uint32_t lo = __shfl(roff, 0, 64);  // the round's first byte (record a)
+    for (int a = 0; a < 64;) {
+      const uint32_t lo = __shfl(rel, a, 64);  // the round's first byte
       const uint32_t sh = (uint32_t)(((uintptr_t)(D.out + wbase + lo)) & 15);
-      const bool fit = valid && roff + rlen - lo + sh <= IMG;  // (a prefix of the lanes: offsets increase with r)
-      const uint32_t nfit = (uint32_t)__builtin_popcountll(__ballot(fit));
-      // the owner's descriptors (every lane takes part in the shuffles)
-      zb_rec d;  // (both of the owner's records are moved; the lane's k selects)
-      const int64_t k0 = __shfl(d0.key, src, 64), k1 = __shfl(d1.key, src, 64);
-      const int64_t s0 = __shfl(d0.scope_key, src, 64), s1 = __shfl(d1.scope_key, src, 64);
-      const int64_t i0 = __shfl(d0.inst_key, src, 64), i1 = __shfl(d1.inst_key, src, 64);
-      const uint32_t p0 = __shfl(d0.payload, src, 64), p1 = __shfl(d1.payload, src, 64);
-      const uint32_t m0 = __shfl((uint32_t)d0.elem | (uint32_t)d0.intent << 16 | (uint32_t)d0.kind << 24, src, 64);
-      const uint32_t m1 = __shfl((uint32_t)d1.elem | (uint32_t)d1.intent << 16 | (uint32_t)d1.kind << 24, src, 64);
-      d.key = k ? k1 : k0;
-      d.scope_key = k ? s1 : s0;
-      d.inst_key = k ? i1 : i0;
-      d.payload = k ? p1 : p0;
-      const uint32_t m = k ? m1 : m0;
-      d.elem = (uint16_t)m;
-      d.intent = (uint8_t)(m >> 16);
-      d.kind = (uint8_t)(m >> 24);
-      if (nfit == 0) {  // one record larger than the image: the host takes the descriptor path
+      const bool fit = lane >= a && incl - lo + sh <= IMG;  // (a suffix of lanes >= a fails: incl grows)
+      const uint64_t fm = __ballot(fit);
+      const int b = fm ? 64 - __builtin_clzll(fm) : a;
+      if (b == a) {  // one instance's records exceed the image: the host takes the descriptor path
         bad = 1;
         break;
       }
-      if (fit) {
-        const uint64_t* dw = (const uint64_t*)(P.arena + (uint64_t)d.payload * 8);
-        uint64_t pre[SER_PRE];
+      if (fit && mine) {
+#pragma unroll 1
+        for (uint32_t k = 0; k < G.nrec; k++) {
+          const zb_rec d = k ? d1 : d0;
+          const bool cr = d.payload == L.create_ref;
+          const uint64_t* dw = cr ? cdw : (const uint64_t*)(P.arena + (uint64_t)d.payload * 8);
+          uint64_t pre[SER_PRE];
 #pragma unroll
-        for (int j = 0; j < SER_PRE; j++) pre[j] = dw[j];  // (ARENA_SLACK: never past the allocation)
-        FastW fw;
-        fw.begin(img, sh + (roff - lo));
-        fast_encode(fw, d, tab, segs, dw, pre);
-        if (fw.n() != rlen) bad = 1;  // the formula and the encoder disagree: never silently
+          for (int j = 0; j < SER_PRE; j++) pre[j] = cpre[j];
+          if (!cr) {  // a static blob
+#pragma unroll
+            for (int j = 0; j < SER_PRE; j++) pre[j] = dw[j];  // (ARENA_SLACK)
+          }
+          FastW fw;
+          fw.begin(img, sh + (rel - lo) + (k ? vl0 : 0));
+          fast_encode(fw, d, tab, segs, dw, pre);
+          if (fw.n() != (k ? vl1 : vl0)) bad = 1;  // the formula and the encoder disagree: never silently
+        }
       }
-      const uint32_t hi = __shfl(roff + rlen, (int)nfit - 1, 64);
+      const uint32_t hi = __shfl(incl, b - 1, 64);
       wave_lds_sync();
       wave_stream(img, D.out, wbase + lo, sh, hi - lo, lane);
       wave_lds_sync();  // the image is reused by the next round
-      a += nfit;
+      a = b;
     }
   }
   if (bad) atomicOr(D.flags + 1, 1u);

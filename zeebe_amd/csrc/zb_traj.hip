@@ -1139,32 +1139,42 @@ __device__ __forceinline__ bool load_operand_k(const TrajParams& P, bool is_path
 // The operands of every split condition in one scan of the CREATE payload: query_fast ([ROOT, MAP_KEY k]: every
 // top-level value under key k) for all the model's condition keys at once. The scan (token walk, value skips,
 // the container-key check) does not depend on the key, so each key's (count, first result) -- and whether the
-// scan is unsupported -- is what query_fast gives for that key alone.
-struct Extract {
-  uint32_t cnt[CLS_QMAX], pos[CLS_QMAX], len[CLS_QMAX];
+// scan is unsupported -- is what query_fast gives for that key alone. The first result of each key is decoded
+// where the walk reads it (the token load_operand reads), so the VM's path operands are register moves.
+struct Extract {  // per condition key: its first result, decoded
+  uint32_t meta[CLS_QMAX];  // result count (saturating at 255) | token type << 8 | boolean << 16
+  uint32_t sp[CLS_QMAX];    // string / binary bytes: document offset | length << 16 (the LDS copy holds <= 96 bytes)
+  uint64_t num[CLS_QMAX];   // integer, or the double's bits
   bool ok;
 };
 __device__ __forceinline__ void extract_fast(const TrajParams& P, const uint8_t* d, uint32_t n, Extract& x) {
 #pragma unroll
-  for (int j = 0; j < CLS_QMAX; j++) { x.cnt[j] = 0; x.pos[j] = 0; x.len[j] = 0; }
+  for (int j = 0; j < CLS_QMAX; j++) { x.meta[j] = 0; x.sp[j] = 0; x.num[j] = 0; }
   Tok t;
   if (!read_tok(d, n, t)) { x.ok = n == 0; return; }
   x.ok = true;
   if (t.type != TT_MAP) return;  // root filter needs a container; arrays give no key matches
   uint32_t pos = t.total;
   for (uint32_t i = 0; i < t.len; i++) {
-    Tok k;
+    Tok k, v;
     if (pos >= n || !read_tok(d + pos, n - pos, k)) { x.ok = false; return; }
     const uint32_t kpos = pos;
     pos += k.total;
-    const uint32_t vend = skip_value(d, n, pos);
+    // the value: its first token (the operand's token), then the rest of a container
+    if (pos >= n || !read_tok(d + pos, n - pos, v)) { x.ok = false; return; }
+    const uint32_t vend = (v.type == TT_MAP || v.type == TT_ARRAY) ? skip_value(d, n, pos) : pos + v.total;
     if (vend == 0xffffffffu) { x.ok = false; return; }
     if (k.type == TT_STRING) {
 #pragma unroll
       for (int j = 0; j < CLS_QMAX; j++) {
         if (j < P.cls_nq && k.len == P.cls_key_len[j] && bytes_eq(d + kpos + k.hdr, P.pool + P.cls_key_off[j], k.len)) {
-          if (x.cnt[j] == 0) { x.pos[j] = pos; x.len[j] = vend - pos; }
-          x.cnt[j]++;
+          const uint32_t c = x.meta[j] & 255;
+          if (c == 0) {
+            x.meta[j] = (uint32_t)v.type << 8 | (v.bval ? 1u : 0u) << 16;
+            x.sp[j] = (pos + v.hdr) | v.len << 16;
+            x.num[j] = v.type == TT_FLOAT ? (uint64_t)__double_as_longlong(v.fval) : (uint64_t)v.ival;
+          }
+          x.meta[j] = (x.meta[j] & ~255u) | (c < 255 ? c + 1 : 255);
         }
       }
     } else if (k.type == TT_MAP || k.type == TT_ARRAY) {
@@ -1185,16 +1195,20 @@ __device__ __forceinline__ bool load_operand_x(const TrajParams& P, bool is_path
   }
   if (!x.ok) { unsupported = true; return false; }
   const uint32_t j = __builtin_amdgcn_readfirstlane(idx);
-  uint32_t cnt = 0, rpos = 0, rlen = 0;
+  uint32_t meta = 0, sp = 0;
+  uint64_t num = 0;
 #pragma unroll
   for (int jj = 0; jj < CLS_QMAX; jj++)  // (a scalar compare: no dynamically indexed register array)
-    if ((uint32_t)jj == j) { cnt = x.cnt[jj]; rpos = x.pos[jj]; rlen = x.len[jj]; }
+    if ((uint32_t)jj == j) { meta = x.meta[jj]; sp = x.sp[jj]; num = x.num[jj]; }
+  const uint32_t cnt = meta & 255;
   if (cnt == 0) { out.err = EC_PATH_NO_RESULT; out.q = (uint16_t)j; return false; }
   if (cnt > 1) { out.err = EC_PATH_MULTI; out.q = (uint16_t)j; return false; }
-  Tok t;
-  if (!read_tok(doc + rpos, rlen, t)) { unsupported = true; return false; }
-  o.type = t.type; o.bval = t.bval; o.ival = t.ival; o.fval = t.fval;
-  o.s = doc + rpos + t.hdr; o.slen = t.len;
+  o.type = (uint8_t)(meta >> 8);
+  o.bval = (meta >> 16) & 1;
+  o.ival = (int64_t)num;
+  o.fval = __longlong_as_double((long long)num);
+  o.s = doc + (sp & 0xffff);
+  o.slen = sp >> 16;
   return true;
 }
 
