@@ -27,14 +27,60 @@ __device__ __forceinline__ unsigned long long wg_sum256(unsigned long long x, un
   return t;
 }
 
+// the ELEMENT_COMPLETED record carrying a merge result: its value length hint
+__device__ __forceinline__ void merge_hint(const WaveParams& P, const MergeJob& j, uint32_t olen) {
+  if (j.pos >= 0 && P.vconst) {
+    const zb_rec d = P.log[j.pos];
+    const ValueConst vc = P.vconst[d.elem];
+    P.vlen[j.pos] = vc.wf + mp_int_len(d.inst_key) + mp_int_len(d.scope_key) + mp_bin_len(olen);
+  }
+}
+
+// The wave's default output merges (OutputMappingHandler.java:42-85 -> MappingProcessor.merge), in two
+// kernels: k_merge takes every merge of flat documents (merge_flat: scalar values under fixstr keys, the payload
+// shape of nearly every workflow) -- small in registers and without a workspace, so the job list streams at full
+// occupancy -- and queues the rest for k_merge_gen, the general indexer / merger (merge_docs, a per-thread node
+// workspace), which for most waves finds its queue empty.
 __global__ void __launch_bounds__(256) k_merge(WaveParams P) {
   __shared__ unsigned long long s4[4];
   const uint32_t n = P.merge_count[P.wave & 1];
   const MergeJob* jobs = P.merge_jobs + (uint64_t)(P.wave & 1) * P.job_cap;
-  uint32_t err = 0;
+  uint32_t* slow_n = P.merge_slow_count + (P.wave & 1);
   unsigned long long merges = 0, bytes = 0;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const MergeJob j = jobs[i];
+    const uint8_t* sp = P.arena + (uint64_t)j.src * 8;
+    const uint8_t* tp = P.arena + (uint64_t)j.tgt * 8;
+    const uint32_t ns = *(const uint32_t*)sp, nt = *(const uint32_t*)tp;
+    uint8_t* dst = P.arena + (uint64_t)j.dst * 8;
+    uint32_t olen = 0;
+    if (merge_flat(sp + 4, ns, tp + 4, nt, dst + 4, j.cap, olen)) {
+      *(uint32_t*)dst = olen;
+      merge_hint(P, j, olen);
+      merges += 1;
+      bytes += ns + nt + olen;
+    } else {
+      P.merge_slow[atomicAdd(slow_n, 1u)] = i;
+    }
+  }
+  merges = wg_sum256(merges, s4);
+  bytes = wg_sum256(bytes, s4);
+  if (threadIdx.x == 0 && merges) {
+    atomicAdd((unsigned long long*)&P.stats[3], merges);
+    atomicAdd((unsigned long long*)&P.stats[4], bytes);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_merge_gen(WaveParams P) {
+  __shared__ unsigned long long s4[4];
+  const uint32_t n = P.merge_slow_count[P.wave & 1];
+  const MergeJob* jobs = P.merge_jobs + (uint64_t)(P.wave & 1) * P.job_cap;
+  if (blockIdx.x == 0 && threadIdx.x == 0) P.merge_slow_count[(P.wave + 1) & 1] = 0;  // the next wave's queue
+  if (n == 0) return;
+  uint32_t err = 0;
+  unsigned long long merges = 0, bytes = 0;
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+    const MergeJob j = jobs[P.merge_slow[q]];
     const uint8_t* sp = P.arena + (uint64_t)j.src * 8;
     const uint8_t* tp = P.arena + (uint64_t)j.tgt * 8;
     const uint32_t ns = *(const uint32_t*)sp, nt = *(const uint32_t*)tp;
@@ -44,11 +90,7 @@ __global__ void __launch_bounds__(256) k_merge(WaveParams P) {
     if (!merge_docs(sp + 4, ns, tp + 4, nt, o, unsup)) err |= DE_BAD_PAYLOAD;
     else if (unsup || o.n > j.cap) err |= DE_UNSUPPORTED;
     *(uint32_t*)dst = o.n;
-    if (j.pos >= 0 && P.vconst) {  // the ELEMENT_COMPLETED record carrying the result: its value length hint
-      const zb_rec d = P.log[j.pos];
-      const ValueConst vc = P.vconst[d.elem];
-      P.vlen[j.pos] = vc.wf + mp_int_len(d.inst_key) + mp_int_len(d.scope_key) + mp_bin_len(o.n);
-    }
+    merge_hint(P, j, o.n);
     merges += 1;
     bytes += ns + nt + o.n;
   }
@@ -179,6 +221,7 @@ void launch_map(const WaveParams& p, hipStream_t s) {
 
 void launch_merge(const WaveParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_merge, dim3(1024), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(k_merge_gen, dim3(256), dim3(256), 0, s, p);
 }
 void launch_cond(const WaveParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_cond, dim3(1024), dim3(256), 0, s, p);

@@ -123,7 +123,9 @@ struct zb_engine {
   uint64_t* derr_info = nullptr;
   MergeJob* merge_jobs = nullptr;
   uint64_t* cond_jobs = nullptr;
-  uint32_t* job_counts = nullptr;  // [0..1] merge counts, [2..3] cond counts, [4..5] subscribe counts
+  uint32_t* job_counts = nullptr;  // [0..1] merge counts, [2..3] cond counts, [4..5] subscribe counts,
+                                   // [6..7] merges left to the general merger
+  uint32_t* merge_slow = nullptr;  // [job_cap] indices of those merges
   uint64_t* sub_jobs = nullptr;    // [job_cap] subscribe steps of a wave (models with message catch events)
   uint64_t job_cap = 0;
   WaveHdr* h_hdr_pinned = nullptr;  // pinned mirror for D2H polling
@@ -443,6 +445,8 @@ WaveParams wave_params(zb_engine* e) {
   p.err_info = e->derr_info;
   p.merge_jobs = e->merge_jobs;
   p.merge_count = e->job_counts;
+  p.merge_slow = e->merge_slow;
+  p.merge_slow_count = e->job_counts + 6;
   p.cond_jobs = e->cond_jobs;
   p.cond_count = e->job_counts + 2;
   p.sub_jobs = e->sub_jobs;
@@ -1109,7 +1113,8 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   e->job_cap = std::min<uint64_t>(L, 1ull << 26);
   if (hipMalloc(&e->merge_jobs, 2 * e->job_cap * sizeof(MergeJob)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->cond_jobs, 2 * e->job_cap * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipMalloc(&e->job_counts, 6 * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->job_counts, 8 * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->merge_slow, e->job_cap * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_hdr_pinned, 2 * sizeof(WaveHdr)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_err_pinned, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_ctl_pinned, sizeof(TrajCtl)) != hipSuccess) return cleanup(ZB_ENOMEM);
@@ -1144,7 +1149,7 @@ void zb_engine_destroy(zb_engine* e) {
   void* ps[] = {e->vlen_mem, e->vlen_bad, e->jobs.keys, e->jobs.state, e->jobs.tombs, e->c_flag, e->c_new, e->c_tmp,
                 e->c_scratch, e->c_bits, e->c_pop, e->c_off, e->c_count, e->x_keys, e->x_pos, e->x_keys2, e->x_pos2,
                 e->x_tmp, e->mapres, e->map_ws, e->log_mem, e->links_mem, e->srcd_mem, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
-                e->merge_jobs, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
+                e->merge_jobs, e->merge_slow, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
                 e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->need_children};
@@ -1200,7 +1205,7 @@ int zb_reset(zb_engine* e, int keep_staged) {
   HIPCHECK(e, hipMemcpyAsync(e->hdr, &h, sizeof(h), hipMemcpyHostToDevice, e->stream));
   HIPCHECK(e, hipMemsetAsync(e->derr, 0, sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->derr_info, 0xff, sizeof(uint64_t), e->stream));
-  HIPCHECK(e, hipMemsetAsync(e->job_counts, 0, 6 * sizeof(uint32_t), e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->job_counts, 0, 8 * sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->dstats, 0, 8 * sizeof(uint64_t), e->stream));
   if (e->jobs.keys) {
     HIPCHECK(e, hipMemsetAsync(e->jobs.keys, 0, (e->jobs.mask + 1) * sizeof(int64_t), e->stream));  // JOB_EMPTY
@@ -2409,7 +2414,8 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
       wr.tile_offs = e->dr_off;
       e->dr_split = e->ser_fast && !fc && sp.seg_lds && sp.arena_bytes;
       if (e->dr_split) {  // k_ser_fast, then k_ser_write over the tiles it left
-        // pass 1 over every tile (13 KB wave image) -> list A; pass 2 over A (40 KB) -> list B; k_ser_write over B
+        // pass 1 over every tile (k_ser_wave, 11 KB per wave) -> list A; pass 2 over A (40 KB phase form) -> list B;
+        // k_ser_write over B
         uint32_t* cnt = (uint32_t*)(e->dr_total + 3);  // [0] list A, [1] list B (zeroed with dr_total)
         wr.tile_list = e->dr_list;
         wr.tile_list_n = cnt;

@@ -11,6 +11,7 @@
 
 #include "zb_devlib.hpp"
 #include "zb_fastenc.hpp"
+#include "zb_wavelib.hpp"
 #include "zb_kernels.hpp"
 #include "zb_msg.hpp"
 
@@ -704,16 +705,14 @@ __global__ void __launch_bounds__(256) k_ser_sum(SerParams P, int64_t nparts) {
 }
 
 
-// Fast write pass (values + headers, no frames): one workgroup per 256-record tile as k_ser_write, but the
-// LDS image holds ONE wave's records (64 values): the waves encode in turn and all four stream each wave's
-// range out. A workgroup then needs ~17 KB of LDS instead of 52 KB and a third of the registers, so several
-// times more tiles -- and their descriptor / payload loads -- are in flight per CU. Tiles with a record the
-// fast encoder does not take, or a wave range larger than the image, go to k_ser_write (tile_list).
-// A second instantiation with a 40 KB image (3 workgroups per CU) runs over the tiles the first one left when
-// their values are large (jobs and merged payloads, C2 / C4); only what neither takes reaches k_ser_write.
-constexpr int SER_FIMG = 13 * 1024, SER_FIMG_WIDE = 40 * 1024;
+// Fast write pass, phase form (values + headers, no frames): one workgroup per 256-record tile as k_ser_write,
+// but the LDS image holds ONE wave's records (64 values): the waves encode in turn and all four stream each
+// wave's range out. It runs with a 40 KB image (3 workgroups per CU) over the tiles the wave-parallel pass
+// (k_ser_wave, below) leaves because one of their values exceeds its image; tiles with a record the fast encoder
+// does not take, or a wave range larger than 40 KB, go on to k_ser_write (tile_list).
+constexpr int SER_FIMG_WIDE = 40 * 1024;
 template <int IMG, bool LISTED>
-__global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(IMG <= SER_FIMG ? 6 : 3))) k_ser_fast(SerParams P0) {
+__global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3))) k_ser_fast(SerParams P0) {
   __shared__ __attribute__((aligned(16))) uint8_t img[IMG + 16];
   extern __shared__ __attribute__((aligned(16))) uint8_t s_model[];  // the constant runs (sized at launch)
   __shared__ unsigned long long s_wsum[SER_WG / 64], s_pay[SER_WG / 64];
@@ -797,14 +796,101 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(IMG
   if (P0.totals && threadIdx.x == 0) P0.pay_part[tile] = s_pay[0] + s_pay[1] + s_pay[2] + s_pay[3];
 }
 
+// Fast write pass, wave-parallel form (the first pass of the descriptor drain): every wave has an image of its
+// own and encodes its 64 records in rounds -- each lane its own record, the lanes whose values fit the image from
+// the round's first byte -- then streams the round out; the four waves never wait for each other (the phase form
+// above lets one wave encode at a time). A tile with a record the fast encoder does not take, or a single value
+// larger than the image, goes to the next pass (tile_list: the 40 KB phase form, then k_ser_write).
+constexpr uint32_t SER_WIMG = 11 * 1024 - 16;
+__global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 4))) k_ser_wave(SerParams P0) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_img[SER_WG / 64][SER_WIMG + 16];
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_model[];  // the constant runs (sized at launch)
+  __shared__ unsigned long long s_wsum[SER_WG / 64], s_pay[SER_WG / 64];
+  const uint32_t tile = blockIdx.x;
+  const int64_t base = (int64_t)tile * SER_WG;
+  const int64_t i = base + threadIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool live = i < P0.count;
+  const uint64_t o0 = P0.tile_offs[tile], o1 = P0.tile_offs[tile + 1];
+  const uint32_t len = live ? (P0.len_in_vlen ? P0.vlen[P0.start + i] : P0.lengths[i]) : 0;
+  zb_rec d{};
+  if (live) d = P0.log[P0.start + i];
+  const bool fast = live && fast_kind(d);
+  const uint64_t* dw = (const uint64_t*)(P0.arena + (uint64_t)d.payload * 8);
+  uint64_t pre[SER_PRE];
+#pragma unroll
+  for (int j = 0; j < SER_PRE; j++)
+    pre[j] = (fast && (uint64_t)d.payload * 8 + 8 * j + 8 <= P0.arena_bytes) ? dw[j] : 0;
+  uint64_t x = len;  // the wave's inclusive prefix of the value lengths
+#pragma unroll
+  for (int k = 1; k < 64; k <<= 1) {
+    const uint64_t y = (uint64_t)__shfl_up((unsigned long long)x, k, 64);
+    if (lane >= k) x += y;
+  }
+  if (lane == 63) s_wsum[wv] = x;
+  // the elements' constant runs into LDS (their barrier is the vote's): table (4-byte words), pool (8-byte)
+  const uint32_t tb = ((uint32_t)P0.n_elems * (uint32_t)sizeof(DevValSeg) + 15) & ~15u;
+  for (uint32_t c = threadIdx.x; c < tb / 4; c += SER_WG) ((uint32_t*)s_model)[c] = ((const uint32_t*)P0.vsegs)[c];
+  for (uint32_t c = threadIdx.x; c < P0.segpool_len / 8; c += SER_WG)
+    ((uint64_t*)(s_model + tb))[c] = ((const uint64_t*)P0.segpool)[c];
+  const bool all_fast = __syncthreads_and(!live || (fast && len + 16 <= SER_WIMG));
+  if (P0.out_cap && o1 > P0.out_cap) {  // does not fit: the host grows the buffer and runs the pass again
+    if (threadIdx.x == 0) atomicOr(P0.overflow, 1u);
+    return;
+  }
+  if (!all_fast) {  // the next pass takes this tile
+    if (threadIdx.x == 0) P0.tile_list[atomicAdd(P0.tile_list_n, 1u)] = tile;
+    return;
+  }
+  uint64_t pw = 0;
+#pragma unroll
+  for (int k = 0; k < SER_WG / 64; k++)
+    if (k < wv) pw += s_wsum[k];
+  const uint64_t wlo = o0 + pw;  // this wave's range
+  const uint32_t rel = (uint32_t)(x - len), incl = (uint32_t)x;  // this lane's value: [wlo + rel, wlo + incl)
+  if (live) {
+    const zb_record_header h = record_header(d, P0.start + i, len, wlo + rel);
+    const uint64_t* hw = (const uint64_t*)&h;
+    uint64_t* dh = (uint64_t*)(P0.headers + i);
+    for (int k = 0; k < (int)(sizeof(zb_record_header) / 8); k++) __builtin_nontemporal_store(hw[k], dh + k);
+  }
+  if (P0.totals) {
+    unsigned long long y = live ? (uint32_t)pre[0] : 0;
+    for (int dd = 32; dd >= 1; dd >>= 1) y += __shfl_down(y, dd, 64);
+    if (lane == 0) s_pay[wv] = y;
+  }
+  uint8_t* img = s_img[wv];
+  const DevValSeg* tab = (const DevValSeg*)s_model;
+  const uint8_t* segs = s_model + tb;
+#pragma unroll 1
+  for (int a = 0; a < 64;) {  // rounds: lanes [a, b) whose values fit the image from the round's first byte
+    const uint32_t lo = __builtin_amdgcn_readlane(rel, a);
+    const uint32_t sh = (uint32_t)(((uintptr_t)(P0.out + wlo + lo)) & 15);
+    const bool fit = lane >= a && incl - lo + sh <= SER_WIMG;  // (lane a always fits: len + 16 <= the image)
+    const uint64_t fm = __ballot(fit);
+    const int b = 64 - __builtin_clzll(fm);
+    if (fit && len) {
+      FastW w;
+      w.begin(img, sh + (rel - lo));
+      fast_encode(w, d, tab, segs, dw, pre);
+    }
+    const uint32_t hi = __builtin_amdgcn_readlane(incl, b - 1);
+    wave_lds_sync();
+    wave_stream(img, P0.out, wlo + lo, sh, hi - lo, lane);
+    wave_lds_sync();  // the image is reused by the next round
+    a = b;
+  }
+  __syncthreads();
+  if (P0.totals && threadIdx.x == 0) P0.pay_part[tile] = s_pay[0] + s_pay[1] + s_pay[2] + s_pay[3];
+}
+
 // dynamic LDS of the fast passes: the segment table (whole 16-byte rows) + the segment pool
 static uint32_t seg_lds_bytes(const SerParams& p) {
   return (((uint32_t)p.n_elems * (uint32_t)sizeof(DevValSeg) + 15) & ~15u) + p.segpool_len;
 }
 void launch_ser_fast(const SerParams& p, hipStream_t s) {
   if (p.count <= 0) return;
-  hipLaunchKernelGGL((k_ser_fast<SER_FIMG, false>), dim3((unsigned)((p.count + SER_WG - 1) / SER_WG)), dim3(SER_WG),
-                     seg_lds_bytes(p), s, p);
+  hipLaunchKernelGGL(k_ser_wave, dim3((unsigned)((p.count + SER_WG - 1) / SER_WG)), dim3(SER_WG), seg_lds_bytes(p), s, p);
 }
 void launch_ser_fast_wide(const SerParams& p, uint32_t n, hipStream_t s) {
   if (n == 0) return;

@@ -19,8 +19,11 @@
 // first with k_tmpl, so every other API sees the descriptors it always saw.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "zb_fastenc.hpp"
 #include "zb_tmpl.hpp"
+#include "zb_wavelib.hpp"
 
 namespace zbg {
 
@@ -133,6 +136,33 @@ __device__ __forceinline__ TdGen td_gen(const TdTab& T, const TmplLane& L, uint3
   G.nrec = live ? (uint32_t)(T.agg[cls * T.wmax + w] & 0xffff) : 0;
   return G;
 }
+// td_gen for a whole wave of consecutive instances: the first lane's bases by the linear formula, computed from
+// its class ranks in scalar registers (agg and the generation bases through the scalar cache), every other
+// lane's as the first lane's plus an exclusive scan of the lanes' own counts (instance i's records follow those
+// of the instances before it in every generation). b0: the first lane's class ranks, nc classes.
+__device__ __forceinline__ TdGen td_gen_wave(const TrajParams& P, const TdTab& T, const uint32_t (&b0)[CLS_MAX],
+                                             uint32_t nc, uint32_t cls, int w, bool live) {
+  const TrajBase wb = kload(P.wbase, (uint64_t)w);
+  int64_t po = 0, pw = 0, pj = 0;
+#pragma unroll
+  for (int c = 0; c < CLS_MAX; c++) {
+    if (c >= (int)nc) break;
+    const uint64_t n = kload(P.agg, (uint64_t)c * CLS_ROW + (uint64_t)w);
+    po += (int64_t)b0[c] * (int64_t)(n & 0xffff);
+    pw += (int64_t)b0[c] * (int64_t)((n >> 16) & 0xffff);
+    pj += (int64_t)b0[c] * (int64_t)(n >> 32);
+  }
+  const uint64_t own = T.agg[cls * T.wmax + w];  // (what td_gen's dot product counts for this lane's class)
+  const uint32_t x = (uint32_t)(own & 0xff) | (uint32_t)((own >> 16) & 0xfff) << 8 | (uint32_t)((own >> 32) & 0xfff) << 20;
+  const uint32_t ex = wave_incl_scan(x) - x;  // (per instance <= TF records and <= 15 keys of each kind)
+  TdGen G;
+  G.pos0 = wb.pos + po + (ex & 0xff);
+  G.kwf = wb.wf + pw + ((ex >> 8) & 0xfff);
+  G.kjob = wb.job + pj + (ex >> 20);
+  G.nrec = live ? (uint32_t)(own & 0xffff) : 0;
+  return G;
+}
+
 // record k of the instance's generation w, resolved from the class trace; vl: its value length (the
 // encoder's, by the formula), plen: its payload document's length
 __device__ __forceinline__ zb_rec td_record(const TrajParams& P, const TdTab& T, const TmplLane& L, uint32_t cls, int w,
@@ -161,9 +191,9 @@ struct TdLane {
   int64_t inst, kwf0;
   bool active;
 };
-__device__ __forceinline__ TdLane td_lane(const TrajParams& P, const TdTab& T) {
+__device__ __forceinline__ TdLane td_lane(const TrajParams& P, const TdTab& T, int64_t tile) {
   TdLane t;
-  t.inst = (int64_t)blockIdx.x * TD_WG + threadIdx.x;
+  t.inst = tile * TD_WG + threadIdx.x;
   t.active = t.inst < P.n;
   if (!t.active) t.inst = P.n - 1;  // (follows the last instance, writes nothing)
   t.cls = 0;
@@ -182,56 +212,60 @@ __device__ __forceinline__ TdLane td_lane(const TrajParams& P, const TdTab& T) {
   return t;
 }
 
-__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
-  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-  return x;
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {  // (lane 63: the wave's total)
+  return wave_incl_scan(x);
 }
 
 // msgpack length of a symbolic key / position (td_key) known to be -1, 0 or in [2^16, 2^32)
 __device__ __forceinline__ uint32_t td_len5(uint32_t sym) { return (sym == NOK || sym == JOB_ZERO) ? 1u : 5u; }
 
+// Both passes: one workgroup per tile of 256 instances (a persistent grid that copies the tables once per
+// workgroup measured slower: 0.39 -> 0.55 ms for the size pass on C3 10M)
 __global__ void __launch_bounds__(TD_WG) k_tdrain_size(TDrainParams D) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_tab[];
   __shared__ unsigned long long s_pay[TD_WG / 64];
   const TrajParams& P = D.t;
   const TdTab T = td_load_tables(D, s_tab, false);
-  const TdLane L = td_lane(P, T);
   const int lane = threadIdx.x & 63;
-  const uint64_t wave = (uint64_t)blockIdx.x * (TD_WG / 64) + (threadIdx.x >> 6);
-  // Short form: when the wave's smallest key and position (its first lane's generation-0 bases, which every later
-  // key of the wave exceeds) are >= 2^16 and the batch's largest is below 2^32, every key / position the wave's
-  // records carry encodes in 5 bytes (MsgPackWriter.writeInteger): the lengths follow from the traces alone,
-  // without resolving a single key. Otherwise (the first 13k keys of a partition) td_record resolves each one.
-  const bool lo_ok = P.wf_start + 5 * L.kwf0 >= 65536 && P.log_base + L.inst >= 65536 &&
-                     (!D.jobs || P.job_start + 5 * td_kbase(T, L.L, 0, 2) >= 65536);
-  const bool len5 = D.len5_ok && __shfl(lo_ok ? 1 : 0, 0, 64);
   uint64_t pay = 0;
+  {
+    const int64_t tile = blockIdx.x;
+    const TdLane L = td_lane(P, T, tile);
+    const uint64_t wave = (uint64_t)tile * (TD_WG / 64) + (threadIdx.x >> 6);
+    // Short form: when the wave's smallest key and position (its first lane's generation-0 bases, which every
+    // later key of the wave exceeds) are >= 2^16 and the batch's largest is below 2^32, every key / position the
+    // wave's records carry encodes in 5 bytes (MsgPackWriter.writeInteger): the lengths follow from the traces
+    // alone, without resolving a single key. Otherwise (the first 13k keys of a partition) td_record resolves each.
+    const bool lo_ok = P.wf_start + 5 * L.kwf0 >= 65536 && P.log_base + L.inst >= 65536 &&
+                       (!D.jobs || P.job_start + 5 * td_kbase(T, L.L, 0, 2) >= 65536);
+    const bool len5 = D.len5_ok && __builtin_amdgcn_readlane(lo_ok ? 1 : 0, 0);
 #pragma unroll 1
-  for (int w = 0; w < (int)D.wmax; w++) {
-    uint32_t mine = 0;
-    if (len5) {
-      const uint32_t nrec = w < (int)L.W ? (uint32_t)(T.agg[L.cls * T.wmax + w] & 0xffff) : 0u;
+    for (int w = 0; w < (int)D.wmax; w++) {
+      uint32_t mine = 0;
+      if (len5) {
+        const uint32_t nrec = w < (int)L.W ? (uint32_t)(T.agg[L.cls * T.wmax + w] & 0xffff) : 0u;
 #pragma unroll
-      for (int k = 0; k < TF; k++) {
-        if ((uint32_t)k >= nrec) break;
-        const TmplRec t = T.tmpl[(L.cls * T.wmax + w) * TF + k];
-        const uint32_t plen = t.payload == PAY_CREATE ? L.create_len : arena_len(P.arena, t.payload);
-        const ValueConst vc = T.vconst[t.elem];
-        mine += (kind_vt(t.kind) == ZB_VT_JOB ? vc.job : vc.wf) + td_len5(t.inst) + td_len5(t.scope) + mp_bin_len(plen);
-        pay += plen;
-      }
-    } else {
-      const TdGen G = td_gen(T, L.L, L.cls, w, w < (int)L.W);
+        for (int k = 0; k < TF; k++) {
+          if ((uint32_t)k >= nrec) break;
+          const TmplRec t = T.tmpl[(L.cls * T.wmax + w) * TF + k];
+          const uint32_t plen = t.payload == PAY_CREATE ? L.create_len : arena_len(P.arena, t.payload);
+          const ValueConst vc = T.vconst[t.elem];
+          mine += (kind_vt(t.kind) == ZB_VT_JOB ? vc.job : vc.wf) + td_len5(t.inst) + td_len5(t.scope) + mp_bin_len(plen);
+          pay += plen;
+        }
+      } else {
+        const TdGen G = td_gen(T, L.L, L.cls, w, w < (int)L.W);
 #pragma unroll 1
-      for (uint32_t k = 0; k < G.nrec; k++) {
-        uint32_t vl, plen;
-        (void)td_record(P, T, L.L, L.cls, w, k, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl, plen);
-        mine += vl;
-        pay += plen;
+        for (uint32_t k = 0; k < G.nrec; k++) {
+          uint32_t vl, plen;
+          (void)td_record(P, T, L.L, L.cls, w, k, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl, plen);
+          mine += vl;
+          pay += plen;
+        }
       }
+      const uint32_t b = wave_sum(mine);
+      if (lane == 63) D.wbytes[(uint64_t)w * D.nwave + wave] = b;
     }
-    const uint32_t b = wave_sum(mine);
-    if (lane == 0) D.wbytes[(uint64_t)w * D.nwave + wave] = b;
   }
   // payload bytes of the drained records (zb_serialize_stats.payload_bytes): one partial per workgroup
   unsigned long long y = pay;
@@ -241,126 +275,107 @@ __global__ void __launch_bounds__(TD_WG) k_tdrain_size(TDrainParams D) {
   if (threadIdx.x == 0) D.pay_part[blockIdx.x] = s_pay[0] + s_pay[1] + s_pay[2] + s_pay[3];
 }
 
-// LDS writes of other lanes of the wave are visible to this lane's later reads (and the reverse)
-__device__ __forceinline__ void wave_lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
-
-// image bytes [shift, shift + n) -> out[o, o + n) by one wave: 16-byte non-temporal stores aligned to the
-// destination, bytes at the two ends (shared with the neighbouring ranges) one at a time
-__device__ __forceinline__ void wave_stream(const uint8_t* img, uint8_t* out, uint64_t o, uint32_t shift, uint32_t n,
-                                            int lane) {
-  uint8_t* dst = out + o - shift;
-  const uint32_t lim = shift + n;
-  const uint32_t full_lo = (shift + 15) & ~15u, full_hi = lim & ~15u;
-  for (uint32_t c = full_lo + 16 * lane; c < full_hi; c += 16 * 64) {
-    const uint4 v = *(const uint4*)(img + c);
-    __builtin_nontemporal_store(v.x, (uint32_t*)(dst + c));
-    __builtin_nontemporal_store(v.y, (uint32_t*)(dst + c) + 1);
-    __builtin_nontemporal_store(v.z, (uint32_t*)(dst + c) + 2);
-    __builtin_nontemporal_store(v.w, (uint32_t*)(dst + c) + 3);
-  }
-  const uint32_t head_end = full_lo < lim ? full_lo : lim;
-  const uint32_t tail_lo = full_hi > head_end ? full_hi : head_end;
-  const uint32_t nh = head_end - shift;  // at most 15 + 15 bytes: one per lane
-  if ((uint32_t)lane < nh) dst[shift + lane] = img[shift + lane];
-  else if ((uint32_t)lane < nh + (lim - tail_lo)) dst[tail_lo + lane - nh] = img[tail_lo + lane - nh];
-}
-
 template <uint32_t IMG>
 __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4))) k_tdrain_write(TDrainParams D) {
   __shared__ __attribute__((aligned(16))) uint8_t s_img[TD_WG / 64][IMG + 16];
   extern __shared__ __attribute__((aligned(16))) uint8_t s_tab[];  // value segments + the batch's tables
   const TrajParams& P = D.t;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint64_t wave = (uint64_t)blockIdx.x * (TD_WG / 64) + wv;
   const TdTab T = td_load_tables(D, s_tab, true);
-  const TdLane L = td_lane(P, T);
   const TdLayout lay = td_layout(D, true);
   const DevValSeg* tab = (const DevValSeg*)(s_tab + lay.tab);
   const uint8_t* segs = s_tab + lay.pool;
   uint8_t* img = s_img[wv];
-  // the instance's CREATE payload document, read once: every record of a deferred batch carries it or a static blob
-  const uint64_t* cdw = (const uint64_t*)(P.arena + (uint64_t)L.create_ref * 8);
-  uint64_t cpre[SER_PRE];
-#pragma unroll
-  for (int j = 0; j < SER_PRE; j++) cpre[j] = cdw[j];  // (ARENA_SLACK: never past the allocation)
   uint32_t bad = 0;
-#pragma unroll 1
-  for (int w = 0; w < (int)D.wmax; w++) {
-    const uint64_t wbase = D.woffs[(uint64_t)w * D.nwave + wave];
-    const uint64_t wend = D.woffs[(uint64_t)w * D.nwave + wave + 1];
-    if (wend == wbase) continue;  // (uniform: no record of this wave in generation w)
-    if (wend > D.out_cap) {  // does not fit: the host grows the buffer and runs the pass again
-      if (lane == 0) atomicOr(D.flags, 1u);
-      continue;
-    }
-    const TdGen G = td_gen(T, L.L, L.cls, w, w < (int)L.W);
-    uint32_t vl0 = 0, vl1 = 0;
-    zb_rec d0{}, d1{};
-    {
-      uint32_t plen;
-      if (G.nrec > 0) d0 = td_record(P, T, L.L, L.cls, w, 0, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl0, plen);
-      if (G.nrec > 1) d1 = td_record(P, T, L.L, L.cls, w, 1, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl1, plen);
-    }
-    const uint32_t mine = vl0 + vl1;
-    uint32_t incl = mine;
+  {
+    const int64_t tile = blockIdx.x;
+    const TdLane L = td_lane(P, T, tile);
+    // the instance's CREATE payload document, read once: every record of a deferred batch carries it or a static blob
+    const uint64_t* cdw = (const uint64_t*)(P.arena + (uint64_t)L.create_ref * 8);
+    uint64_t cpre[SER_PRE];
 #pragma unroll
-    for (int k = 1; k < 64; k <<= 1) {
-      const uint32_t y = __shfl_up(incl, k, 64);
-      if (lane >= k) incl += y;
-    }
-    const uint32_t rel = incl - mine;  // this lane's values: [wbase + rel, wbase + incl)
-    // headers: key, types / intent / rejection, length, offset (the position is implicit: start + index)
+    for (int j = 0; j < SER_PRE; j++) cpre[j] = cdw[j];  // (ARENA_SLACK: never past the allocation)
+    // the wave's first lane's class ranks (td_gen_wave)
+    uint32_t b0[CLS_MAX];
 #pragma unroll
-    for (int k = 0; k < TF; k++) {
-      if ((uint32_t)k >= G.nrec) break;
-      const zb_rec& d = k ? d1 : d0;
-      uint64_t* dh = (uint64_t*)(D.headers + (G.pos0 + k - D.start));
-      const uint64_t meta = (uint64_t)kind_rt(d.kind) | (uint64_t)kind_vt(d.kind) << 8 | (uint64_t)d.intent << 16 |
-                            255ull << 24 | (uint64_t)(k ? vl1 : vl0) << 32;  // (no rejections: k_tmpl_decide)
-      __builtin_nontemporal_store((uint64_t)d.key, dh);
-      __builtin_nontemporal_store(meta, dh + 1);
-      __builtin_nontemporal_store(wbase + rel + (k ? vl0 : 0), dh + 2);
-    }
-    // rounds: lanes [a, b) whose values fit the image from the round's first byte; each lane encodes its own
-    // records (no redistribution: a generation of C3 is one round of every lane)
+    for (int c = 0; c < CLS_MAX; c++) b0[c] = __builtin_amdgcn_readlane(L.L.before[c], 0);
+    const uint32_t nc = __builtin_amdgcn_readfirstlane(L.L.ncls);
+    const uint64_t swave = (uint64_t)tile * (TD_WG / 64) + __builtin_amdgcn_readfirstlane(wv);
+    // this wave's value range of generation w: woffs[w][wave .. wave + 1], read one generation ahead (scalar loads)
+    uint64_t nbase = K(D.woffs)[swave], nend = K(D.woffs)[swave + 1];
 #pragma unroll 1
-    for (int a = 0; a < 64;) {
-      const uint32_t lo = __shfl(rel, a, 64);  // the round's first byte
-      const uint32_t sh = (uint32_t)(((uintptr_t)(D.out + wbase + lo)) & 15);
-      const bool fit = lane >= a && incl - lo + sh <= IMG;  // (a suffix of lanes >= a fails: incl grows)
-      const uint64_t fm = __ballot(fit);
-      const int b = fm ? 64 - __builtin_clzll(fm) : a;
-      if (b == a) {  // one instance's records exceed the image: the host takes the descriptor path
-        bad = 1;
-        break;
+    for (int w = 0; w < (int)D.wmax; w++) {
+      const uint64_t wbase = nbase, wend = nend;
+      if (w + 1 < (int)D.wmax) {
+        nbase = K(D.woffs)[(uint64_t)(w + 1) * D.nwave + swave];
+        nend = K(D.woffs)[(uint64_t)(w + 1) * D.nwave + swave + 1];
       }
-      if (fit && mine) {
+      if (wend == wbase) continue;  // (uniform: no record of this wave in generation w)
+      if (wend > D.out_cap) {  // does not fit: the host grows the buffer and runs the pass again
+        if (lane == 0) atomicOr(D.flags, 1u);
+        continue;
+      }
+      const TdGen G = td_gen_wave(P, T, b0, nc, L.cls, w, w < (int)L.W);
+      uint32_t vl0 = 0, vl1 = 0;
+      zb_rec d0{}, d1{};
+      {
+        uint32_t plen;
+        if (G.nrec > 0) d0 = td_record(P, T, L.L, L.cls, w, 0, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl0, plen);
+        if (G.nrec > 1) d1 = td_record(P, T, L.L, L.cls, w, 1, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl1, plen);
+      }
+      const uint32_t mine = vl0 + vl1;
+      const uint32_t incl = wave_incl_scan(mine);
+      const uint32_t rel = incl - mine;  // this lane's values: [wbase + rel, wbase + incl)
+      // headers: key, types / intent / rejection, length, offset (the position is implicit: start + index)
+#pragma unroll
+      for (int k = 0; k < TF; k++) {
+        if ((uint32_t)k >= G.nrec) break;
+        const zb_rec& d = k ? d1 : d0;
+        uint64_t* dh = (uint64_t*)(D.headers + (G.pos0 + k - D.start));
+        const uint64_t meta = (uint64_t)kind_rt(d.kind) | (uint64_t)kind_vt(d.kind) << 8 | (uint64_t)d.intent << 16 |
+                              255ull << 24 | (uint64_t)(k ? vl1 : vl0) << 32;  // (no rejections: k_tmpl_decide)
+        __builtin_nontemporal_store((uint64_t)d.key, dh);
+        __builtin_nontemporal_store(meta, dh + 1);
+        __builtin_nontemporal_store(wbase + rel + (k ? vl0 : 0), dh + 2);
+      }
+      // rounds: lanes [a, b) whose values fit the image from the round's first byte; each lane encodes its own
+      // records (no redistribution: a generation of C3 is one round of every lane)
 #pragma unroll 1
-        for (uint32_t k = 0; k < G.nrec; k++) {
-          const zb_rec d = k ? d1 : d0;
-          const bool cr = d.payload == L.create_ref;
-          const uint64_t* dw = cr ? cdw : (const uint64_t*)(P.arena + (uint64_t)d.payload * 8);
-          uint64_t pre[SER_PRE];
-#pragma unroll
-          for (int j = 0; j < SER_PRE; j++) pre[j] = cpre[j];
-          if (!cr) {  // a static blob
-#pragma unroll
-            for (int j = 0; j < SER_PRE; j++) pre[j] = dw[j];  // (ARENA_SLACK)
-          }
-          FastW fw;
-          fw.begin(img, sh + (rel - lo) + (k ? vl0 : 0));
-          fast_encode(fw, d, tab, segs, dw, pre);
-          if (fw.n() != (k ? vl1 : vl0)) bad = 1;  // the formula and the encoder disagree: never silently
+      for (int a = 0; a < 64;) {
+        const uint32_t lo = __builtin_amdgcn_readlane(rel, a);  // the round's first byte
+        const uint32_t sh = (uint32_t)(((uintptr_t)(D.out + wbase + lo)) & 15);
+        const bool fit = lane >= a && incl - lo + sh <= IMG;  // (a suffix of lanes >= a fails: incl grows)
+        const uint64_t fm = __ballot(fit);
+        const int b = fm ? 64 - __builtin_clzll(fm) : a;
+        if (b == a) {  // one instance's records exceed the image: the host takes the descriptor path
+          bad = 1;
+          break;
         }
+        if (fit && mine) {
+#pragma unroll 1
+          for (uint32_t k = 0; k < G.nrec; k++) {
+            const zb_rec d = k ? d1 : d0;
+            const bool cr = d.payload == L.create_ref;
+            const uint64_t* dw = cr ? cdw : (const uint64_t*)(P.arena + (uint64_t)d.payload * 8);
+            uint64_t pre[SER_PRE];
+#pragma unroll
+            for (int j = 0; j < SER_PRE; j++) pre[j] = cpre[j];
+            if (!cr) {  // a static blob
+#pragma unroll
+              for (int j = 0; j < SER_PRE; j++) pre[j] = dw[j];  // (ARENA_SLACK)
+            }
+            FastW fw;
+            fw.begin(img, sh + (rel - lo) + (k ? vl0 : 0));
+            fast_encode(fw, d, tab, segs, dw, pre);
+            if (fw.n() != (k ? vl1 : vl0)) bad = 1;  // the formula and the encoder disagree: never silently
+          }
+        }
+        const uint32_t hi = __builtin_amdgcn_readlane(incl, b - 1);
+        wave_lds_sync();
+        wave_stream(img, D.out, wbase + lo, sh, hi - lo, lane);
+        wave_lds_sync();  // the image is reused by the next round
+        a = b;
       }
-      const uint32_t hi = __shfl(incl, b - 1, 64);
-      wave_lds_sync();
-      wave_stream(img, D.out, wbase + lo, sh, hi - lo, lane);
-      wave_lds_sync();  // the image is reused by the next round
-      a = b;
     }
   }
   if (bad) atomicOr(D.flags + 1, 1u);

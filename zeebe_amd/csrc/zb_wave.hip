@@ -1267,8 +1267,6 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
   __shared__ uint64_t s_ex[LB_FIELDS];   // the tile's exclusive prefix
   __shared__ uint64_t s_tot[LB_FIELDS];  // and its inclusive prefix (the chunk totals on the last tile)
   __shared__ uint32_t s_agg[LB_FIELDS];  // the tile's aggregate
-  __shared__ ItemInfo s_inf[WG];         // per item: merge / incident detail (k_emit's P.info, kept on chip)
-  __shared__ uint64_t s_w[WG];           // per item: count word
   const WaveHdr* hin = P.hdr + (P.wave & 1);
   WaveHdr* hout = P.hdr + ((P.wave + 1) & 1);
   const Chunk c = wave_chunk(P, hin);
@@ -1331,13 +1329,12 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
                        ((uint64_t)t.nrow << CW_NROW) | ((uint64_t)(t.merge ? 1 : 0) << CW_MERGE) |
                        ((uint64_t)(t.detail ? 1 : 0) << CW_DETAIL) | ((uint64_t)nconds << CW_NCOND) |
                        ((uint64_t)t.nexp << CW_NEXP) | ((uint64_t)t.bytes << 32);
-    s_w[threadIdx.x] = w;
-    if (t.merge || t.detail) {
+    if (t.merge || t.detail) {  // (global, not LDS: 8 KB of LDS per workgroup cost a resident workgroup per CU)
       ItemInfo inf;
       inf.m_src = t.m_src; inf.m_tgt = t.m_tgt; inf.m_len = t.m_len; inf.m_bytes = t.merge ? t.m_bytes : 0;
       inf.d_pos = t.d_pos; inf.d_q = t.d_q; inf.d_type = t.d_type; inf.d_code = t.d_code; inf.d_a = t.d_a;
       inf.d_b = t.d_b; inf.has_detail = t.detail; inf.ns = (uint8_t)t.ns;
-      s_inf[threadIdx.x] = inf;
+      P.info[i] = inf;
     }
     if (__ballot(t.sub)) {  // wave-uniform: this tile's subscribe steps, in the wave's job list
       const uint32_t slot = wave_alloc(P.sub_count + (P.wave & 1), t.sub ? 1u : 0u);
@@ -1489,7 +1486,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
     }
     __syncthreads();
     // ---- emit (k_emit) straight from the LDS slots
-    const uint64_t we = s_w[threadIdx.x];
+    const uint64_t we = w;
     const int ns = (int)(we & 7);
     if (r < c.end && (ns || ((we >> CW_NEXP) & 63) || ((we >> CW_DETAIL) & 1))) {
       const uint64_t out_rec = (uint64_t)end + s_ex[0] + (a & 0xffff);
@@ -1499,7 +1496,8 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
       const uint64_t bump = arena_next + s_ex[4] + (b & 0xffffffffffull);
       const uint64_t merge_j = s_ex[6] + ((b >> 40) & 0xfff);
       const uint64_t cond_j = s_ex[7] + (b >> 52);
-      const ItemInfo inf = s_inf[threadIdx.x];
+      ItemInfo inf{};
+      if (we & ((1ull << CW_MERGE) | (1ull << CW_DETAIL))) inf = P.info[i];
       emit_item(P, c, i, we, s_slots + threadIdx.x * MAX_SLOTS, inf, out_rec, wf0, job0, row0, bump, merge_j, cond_j,
                 wf_next, job_next, par);
     }
