@@ -286,6 +286,22 @@ def load_traffic(tag, kernel_prefix):
     return None, None
 
 
+def load_traffic_step(tag, kernel_prefixes):
+    """HBM bytes per tick of every kernel named by the prefixes (PMC averages x dispatches / ticks of the PMC run;
+    the run's ticks = k_inject dispatches, one per tick)."""
+    f = os.path.join(PMC_DIR, "pmc_%s.json" % tag)
+    if not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        d = json.load(fh).get("kernels", {})
+    ticks = sum(v.get("dispatches", 0) for k, v in d.items() if "k_inject" in k)
+    if not ticks:
+        return None
+    tot = sum(v["hbm_bytes"] * v.get("dispatches", 0) for k, v in d.items()
+              if "hbm_bytes" in v and any(k.startswith(p) for p in kernel_prefixes))
+    return tot / ticks
+
+
 def roofline(tot, steps, cfg, n):
     """Dominant kernel of the step: the drain's write pass or the main emit launch, by device time."""
     cands = []
@@ -321,7 +337,12 @@ def roofline(tot, steps, cfg, n):
                       "SURVEY §8d: 96 B per transition + merge + condition bytes over all wave kernels of the step"))
     name, ms, b, model = max(cands, key=lambda c: c[1])
     achieved = b / (ms / 1e3) / 1e9
-    traffic, pmc_kernel = load_traffic("%s_%d" % (cfg, n), name.split(" ")[0].split("<")[0])
+    if name.startswith("zbg::k_wave "):  # every wave kernel of the tick: their PMC bytes per tick
+        traffic = load_traffic_step("%s_%d" % (cfg, n), ("zbg::k_wave", "zbg::k_merge", "zbg::k_cond",
+                                                         "zbg::k_subscribe", "zbg::k_pre", "zbg::k_children"))
+        pmc_kernel = "the wave kernels (per tick)"
+    else:
+        traffic, pmc_kernel = load_traffic("%s_%d" % (cfg, n), name.split(" ")[0].split("<")[0])
     r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
          "traffic": traffic, "kernel": name, "avg_launch_us": ms * 1e3, "alg_bytes_per_launch": b,
          "alg_bytes_model": model,

@@ -185,6 +185,7 @@ struct zb_engine {
   MergeGen* t_mgen = nullptr;     // [TRAJ_MAX_GENERATIONS] uniform batch merge slots
   uint64_t* t_wstats = nullptr;   // [t_nwg_cap + CLS_MAX][6] emit statistics per workgroup
   TrajCtl* h_ctl_pinned = nullptr;
+  uint64_t* h_stats_pinned = nullptr;  // [0..7] counters before a step, [8..15] after, [16] a class batch's ClsPlan.nc
   // class batches (zb_traj.hip k_cls_*): the model's exclusive splits as outcome-key digits
   bool cls_ok = false;            // split outcome keys fit 8 bits and CLS_MAX_SPLITS splits
   int nsplits = 0;
@@ -670,6 +671,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   HIPCHECK(e, hipMemcpyAsync(e->h_hdr_pinned, e->hdr + (e->wave & 1), sizeof(WaveHdr), hipMemcpyDeviceToHost,
                              e->stream));
   HIPCHECK(e, hipMemcpyAsync(e->h_err_pinned, e->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  if (p.cls) HIPCHECK(e, hipMemcpyAsync(e->h_stats_pinned + 16, e->c_plan, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
   float ms0 = 0, ms1 = 0, ms_main = 0;
   HIPCHECK(e, hipEventElapsedTime(&ms0, ev[0], ev[1]));
@@ -713,7 +715,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
     e->seg_jobs = e->host_hdr.job_next != p.job_start;
     e->seg_p = p;
     e->seg_nc = 1;
-    if (p.cls) HIPCHECK(e, hipMemcpy(&e->seg_nc, e->c_plan, sizeof(uint32_t), hipMemcpyDeviceToHost));  // ClsPlan.nc
+    if (p.cls) e->seg_nc = (uint32_t)e->h_stats_pinned[16];  // ClsPlan.nc (copied with the trajectory's results)
   }
   return 1;
 }
@@ -1069,9 +1071,10 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   {
     const char* f = std::getenv("ZB_WAVE_FUSED");
     const int per_cu = (f && atoi(f) == 0) ? 0 : wave_resident_per_cu();
-    // one workgroup per CU below the occupancy limit: every workgroup of the persistent grid is resident with
-    // room to spare, so no tile waits on a workgroup that is not running
-    e->wave_fused_grid = per_cu > 1 ? (per_cu - 1) * e->ncu : (per_cu == 1 ? e->ncu : 0);
+    // the occupancy limit less one workgroup per eight CUs: every workgroup of the persistent grid is resident
+    // with room to spare, so no tile waits on a workgroup that is not running. (A grid of (per_cu - 1) per CU left
+    // a quarter of the wave slots idle: C2 1M wave-only stepping 19.8 ms at 768 workgroups, 17.9 at 1024.)
+    e->wave_fused_grid = per_cu > 1 ? per_cu * e->ncu - std::max(1, e->ncu / 8) : (per_cu == 1 ? e->ncu : 0);
   }
   const uint64_t L = e->cfg.log_capacity;
   e->wave_cap = e->cfg.wave_records ? e->cfg.wave_records : std::min<uint64_t>(L, 1ull << 22);
@@ -1118,6 +1121,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipHostMalloc(&e->h_hdr_pinned, 2 * sizeof(WaveHdr)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_err_pinned, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_ctl_pinned, sizeof(TrajCtl)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipHostMalloc(&e->h_stats_pinned, 17 * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_ctl, sizeof(TrajCtl)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_wtot, TRAJ_WAVE_CAP * sizeof(uint4)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_wbase, TRAJ_WAVE_CAP * sizeof(TrajBase)) != hipSuccess) return cleanup(ZB_ENOMEM);
@@ -1165,6 +1169,7 @@ void zb_engine_destroy(zb_engine* e) {
   if (e->h_hdr_pinned) (void)hipHostFree(e->h_hdr_pinned);
   if (e->h_err_pinned) (void)hipHostFree(e->h_err_pinned);
   if (e->h_ctl_pinned) (void)hipHostFree(e->h_ctl_pinned);
+  if (e->h_stats_pinned) (void)hipHostFree(e->h_stats_pinned);
   e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_cls_code.free(); e->d_consts.free();
   e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
   e->d_ranges.free(); e->d_cmd_pool.free(); e->d_lookup_keys.free(); e->d_lookup_pos.free();
@@ -2012,8 +2017,10 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   }
   const int64_t processed_from = e->host_hdr.begin;
   const int64_t written_from = e->host_hdr.end;
-  uint64_t stats_before[8];
-  HIPCHECK(e, hipMemcpy(stats_before, e->dstats, sizeof(stats_before), hipMemcpyDeviceToHost));
+  // counters before / after the step: stream-ordered copies into pinned memory, read after the step's last sync
+  uint64_t* stats_before = e->h_stats_pinned;
+  uint64_t* stats_after = e->h_stats_pinned + 8;
+  HIPCHECK(e, hipMemcpyAsync(stats_before, e->dstats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
   uint32_t launched = 0;
   bool quiescent = e->host_hdr.begin == e->host_hdr.end;
   if (try_traj && !quiescent) {
@@ -2089,8 +2096,8 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     if (rc != ZB_OK) return rc;
     quiescent = e->host_hdr.begin == e->host_hdr.end;
   }
-  uint64_t stats_after[8];
-  HIPCHECK(e, hipMemcpy(stats_after, e->dstats, sizeof(stats_after), hipMemcpyDeviceToHost));
+  HIPCHECK(e, hipMemcpyAsync(stats_after, e->dstats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
   st.records_processed = (uint64_t)(e->host_hdr.begin - processed_from);
   st.records_written = (uint64_t)(e->host_hdr.end - written_from);
   st.transitions = stats_after[0] - stats_before[0];
