@@ -196,6 +196,7 @@ struct zb_engine {
   ClsPlan* c_plan = nullptr;
   uint64_t cls_cap = 0;           // instances the class buffers hold
   uint8_t* c_ikey = nullptr;
+  uint32_t* c_clen = nullptr;
   uint32_t *c_khist = nullptr, *c_krep = nullptr;  // [CLS_HB][256] each (one allocation with c_klen)
   uint64_t* c_klen = nullptr;                       // [CLS_HB][256]
   TmplRec* t_tmpl = nullptr;     // [CLS_MAX][CLS_ROW][TF] traced records (uniform / class batches)
@@ -515,14 +516,16 @@ uint64_t cls_slot_bound(uint64_t n, uint64_t nwg) {
 
 int grow_class_buffers(zb_engine* e, uint64_t n, uint64_t nwg) {
   if (n <= e->cls_cap) return ZB_OK;
-  void* ps[] = {e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm, e->c_segs, e->c_wcls};
+  void* ps[] = {e->c_ikey, e->c_clen, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm, e->c_segs,
+                e->c_wcls};
   for (void* q : ps)
     if (q) (void)hipFree(q);
-  e->c_ikey = nullptr; e->c_khist = e->c_krep = nullptr; e->c_klen = nullptr; e->c_mask = nullptr;
+  e->c_ikey = nullptr; e->c_clen = nullptr; e->c_khist = e->c_krep = nullptr; e->c_klen = nullptr; e->c_mask = nullptr;
   e->c_woffw = e->c_wgcnt = e->c_wgoff = e->c_perm = e->c_segs = e->c_wcls = nullptr;
   e->cls_cap = 0;
   const uint64_t groups = nwg * (TRAJ_WG / 64);
   HIPCHECK(e, hipMalloc(&e->c_ikey, n));
+  HIPCHECK(e, hipMalloc(&e->c_clen, n * sizeof(uint32_t)));
   HIPCHECK(e, hipMalloc(&e->c_khist, CLS_HB * 256 * (2 * sizeof(uint32_t) + sizeof(uint64_t))));
   e->c_krep = e->c_khist + CLS_HB * 256;
   e->c_klen = (uint64_t*)(e->c_khist + 2 * CLS_HB * 256);
@@ -627,6 +630,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
     }
     p.plan = e->c_plan;
     p.ikey = e->c_ikey;
+    p.clen = e->c_clen;
     p.khist = e->c_khist;
     p.klen = e->c_klen;
     p.krep = e->c_krep;
@@ -1155,7 +1159,7 @@ void zb_engine_destroy(zb_engine* e) {
                 e->x_tmp, e->mapres, e->map_ws, e->log_mem, e->links_mem, e->srcd_mem, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
                 e->merge_jobs, e->merge_slow, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
-                e->c_plan, e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
+                e->c_plan, e->c_ikey, e->c_clen, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
                 e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->need_children};
   for (void* p : ps)
     if (p) (void)hipFree(p);

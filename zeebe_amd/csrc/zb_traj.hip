@@ -1325,6 +1325,7 @@ __global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
       for (int k = 0; k < P.nsplits; k++) key += (elem_ctl(P, P.split_elem[k]).cond_count() + 1) * P.split_stride[k];
     }
     P.ikey[i] = (uint8_t)key;
+    P.clen[i] = len;  // (the template drain's size pass reads 4 bytes per instance instead of two dependent loads)
     mkey = key & 255;
     mlen = len;
   }
