@@ -129,3 +129,27 @@ def test_incident_class_falls_back():
     payloads = [msgpack.packb({"a": i % 3}) for i in range(300)]
     st = _run(m.to_xml(), "inc", payloads)
     assert st["path"] == 1
+
+
+@pytest.mark.parametrize("consts", [("", "a", "abcdefg"), ("abcdefgh", "abcdefghi", "abcdefghijklmno"),
+                                    ("abcdefghijklmnop", "abcdefghijklmnopq", "abcdefghijklmnopqrst")])
+def test_string_conditions_and_long_keys(consts):
+    # k_cls_classify compares condition keys and string constants of at most 16 bytes as words (lds_words16) and
+    # longer ones byte by byte: constants of 0 .. 20 bytes, a key of 18 bytes, values equal to the constant, one byte
+    # shorter / longer, differing in the last byte or in case; three splits (8 classes: the class path runs)
+    long_key = "a_key_of_18_bytes_"
+    keys = ["s0", "s1", long_key]
+    b = bpmn.Bpmn.create_executable_process("strs").start_event("s")
+    for k, c in enumerate(consts):
+        g = b.exclusive_gateway("g%d" % k)
+        g.sequence_flow_id("m%d" % k).condition("$.%s == '%s'" % (keys[k], c)).end_event("e%d" % k)
+        b = g.move_to_node("g%d" % k).default_flow().sequence_flow_id("d%d" % k)
+    m = b.end_event("end").done()
+    r = random.Random(len(consts[0]))
+
+    def val(c):
+        return r.choice([c, c, c[:-1] if c else "x", c + "z", (c[:-1] + "Z") if c else "", c.upper()])
+
+    payloads = [msgpack.packb({keys[k]: val(consts[k]) for k in range(3)}) for _ in range(2000)]
+    st = _run(m.to_xml(), "strs", payloads)
+    assert st["path"] == 2

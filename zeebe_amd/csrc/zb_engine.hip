@@ -77,6 +77,7 @@ struct zb_engine {
   DevVec<uint32_t> d_code;
   DevVec<uint32_t> d_cls_code;  // the program with the split conditions' path operands as extraction slots
   DevVec<DevConst> d_consts;
+  DevVec<uint64_t> d_const_w;  // [consts][2] the bytes of string constants of at most 16 bytes (classify)
   DevVec<DevQuery> d_queries;
   DevVec<DevFilter> d_filters;
   DevVec<uint8_t> d_pool;
@@ -192,6 +193,7 @@ struct zb_engine {
   int cls_nq = 0;                 // distinct fast queries of the split conditions (k_cls_classify extraction)
   uint16_t cls_q[CLS_QMAX] = {};
   uint32_t cls_key_off[CLS_QMAX] = {}, cls_key_len[CLS_QMAX] = {};
+  uint64_t cls_key_w[CLS_QMAX][2] = {};
   uint32_t split_elem[CLS_MAX_SPLITS] = {}, split_stride[CLS_MAX_SPLITS] = {};
   ClsPlan* c_plan = nullptr;
   uint64_t cls_cap = 0;           // instances the class buffers hold
@@ -364,6 +366,16 @@ int upload_model(zb_engine* e) {
   HIPCHECK(e, e->d_cond.upload(e->model.cond_flows, e->stream));
   HIPCHECK(e, e->d_code.upload(e->model.code, e->stream));
   HIPCHECK(e, e->d_consts.upload(e->model.consts, e->stream));
+  {  // string constants as two little-endian words (k_cls_classify compares strings of <= 16 bytes as words)
+    std::vector<uint64_t> w(2 * std::max<size_t>(e->model.consts.size(), 1), 0);
+    for (size_t i = 0; i < e->model.consts.size(); i++) {
+      const DevConst& c = e->model.consts[i];
+      if (c.type != TT_STRING || c.str_len > 16) continue;
+      for (uint32_t b = 0; b < c.str_len; b++)
+        w[2 * i + b / 8] |= (uint64_t)e->model.pool[c.str_off + b] << (8 * (b % 8));
+    }
+    HIPCHECK(e, e->d_const_w.upload(w, e->stream));
+  }
   HIPCHECK(e, e->d_queries.upload(e->model.queries, e->stream));
   HIPCHECK(e, e->d_filters.upload(e->model.filters, e->stream));
   HIPCHECK(e, e->d_pool.upload(e->model.pool, e->stream));
@@ -623,7 +635,10 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
       p.cls_q[j] = e->cls_q[j];
       p.cls_key_off[j] = e->cls_key_off[j];
       p.cls_key_len[j] = e->cls_key_len[j];
+      p.cls_key_w[j][0] = e->cls_key_w[j][0];
+      p.cls_key_w[j][1] = e->cls_key_w[j][1];
     }
+    p.const_w = e->d_const_w.p;
     for (int k = 0; k < CLS_MAX_SPLITS; k++) {
       p.split_elem[k] = e->split_elem[k];
       p.split_stride[k] = e->split_stride[k];
@@ -1174,7 +1189,7 @@ void zb_engine_destroy(zb_engine* e) {
   if (e->h_err_pinned) (void)hipHostFree(e->h_err_pinned);
   if (e->h_ctl_pinned) (void)hipHostFree(e->h_ctl_pinned);
   if (e->h_stats_pinned) (void)hipHostFree(e->h_stats_pinned);
-  e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_cls_code.free(); e->d_consts.free();
+  e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_cls_code.free(); e->d_consts.free(); e->d_const_w.free();
   e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
   e->d_ranges.free(); e->d_cmd_pool.free(); e->d_lookup_keys.free(); e->d_lookup_pos.free();
   e->d_maps.free();
@@ -1336,6 +1351,9 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
           e->cls_q[e->cls_nq] = q;
           e->cls_key_off[e->cls_nq] = f.key_off;
           e->cls_key_len[e->cls_nq] = f.key_len;
+          e->cls_key_w[e->cls_nq][0] = e->cls_key_w[e->cls_nq][1] = 0;
+          for (uint32_t b = 0; b < f.key_len && b < 16; b++)
+            e->cls_key_w[e->cls_nq][b / 8] |= (uint64_t)e->model.pool[f.key_off + b] << (8 * (b % 8));
           e->cls_nq++;
         }
       }
