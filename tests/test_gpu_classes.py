@@ -153,3 +153,34 @@ def test_string_conditions_and_long_keys(consts):
     payloads = [msgpack.packb({keys[k]: val(consts[k]) for k in range(3)}) for _ in range(2000)]
     st = _run(m.to_xml(), "strs", payloads)
     assert st["path"] == 2
+
+
+@pytest.mark.parametrize("io", ["0", "1"])
+def test_growing_class_batches_on_one_engine(io, monkeypatch):
+    """Class batches of 10, 200 and 256 instances on one engine (one trajectory workgroup each): the class
+    buffers allocated for the first batch serve the later, larger ones (the slot arrays of the class-uniform
+    emit, ZB_TMPL_IO=0 without deferral, are sized for the workgroups' capacity, not the first batch)."""
+    from zeebe_amd.engine import Engine
+
+    monkeypatch.setenv("ZB_TMPL_IO", io)
+    monkeypatch.setenv("ZB_TMPL_DEFER", "0")
+    cfg = workloads.CONFIGS["c3"]
+    xml = cfg["workflow"]().to_xml()
+    o = zbref.Oracle()
+    o.deploy(xml, 100, 1)
+    e = Engine()
+    e.deploy(xml, 100, 1)
+    for n in (10, 200, 256):
+        blob, offs = cfg["payloads"](n)
+        pays = workloads.split(blob, offs)
+        for p in pays:
+            o.create(cfg["process"], p)
+        e.create(cfg["process"], pays)
+        o.run()
+        st = e.step()
+        assert st["quiescent"] and st["path"] == 2
+    ref, got = o.records(), e.records()
+    assert len(got) == len(ref)
+    for a, b in zip(ref, got):
+        assert (a.position, a.key, a.intent, a.value) == (b.position, b.key, b.intent, b.value), a.position
+    e.close()

@@ -536,8 +536,10 @@ int grow_class_buffers(zb_engine* e, uint64_t n, uint64_t nwg) {
   e->c_woffw = e->c_wgcnt = e->c_wgoff = e->c_perm = e->c_segs = e->c_wcls = nullptr;
   e->cls_cap = 0;
   const uint64_t groups = nwg * (TRAJ_WG / 64);
-  HIPCHECK(e, hipMalloc(&e->c_ikey, n));
-  HIPCHECK(e, hipMalloc(&e->c_clen, n * sizeof(uint32_t)));
+  // per-instance arrays hold cls_cap = nwg * TRAJ_WG entries: a later batch of up to that many instances reuses them
+  const uint64_t cap = nwg * TRAJ_WG;
+  HIPCHECK(e, hipMalloc(&e->c_ikey, cap));
+  HIPCHECK(e, hipMalloc(&e->c_clen, cap * sizeof(uint32_t)));
   HIPCHECK(e, hipMalloc(&e->c_khist, CLS_HB * 256 * (2 * sizeof(uint32_t) + sizeof(uint64_t))));
   e->c_krep = e->c_khist + CLS_HB * 256;
   e->c_klen = (uint64_t*)(e->c_khist + 2 * CLS_HB * 256);
@@ -546,7 +548,7 @@ int grow_class_buffers(zb_engine* e, uint64_t n, uint64_t nwg) {
   HIPCHECK(e, hipMalloc(&e->c_wgcnt, nwg * CLS_MAX * sizeof(uint32_t)));
   HIPCHECK(e, hipMalloc(&e->c_wgoff, nwg * CLS_MAX * sizeof(uint32_t)));
   const uint64_t nblk = (nwg + CLS_BLK_WG - 1) / CLS_BLK_WG;
-  const uint64_t slots = cls_slot_bound(n, nwg);
+  const uint64_t slots = cls_slot_bound(cap, nwg);  // (for any batch of up to cap instances)
   HIPCHECK(e, hipMalloc(&e->c_perm, slots * sizeof(uint32_t)));
   HIPCHECK(e, hipMalloc(&e->c_segs, nblk * CLS_MAX * sizeof(uint32_t)));
   HIPCHECK(e, hipMalloc(&e->c_wcls, (slots / 64 + 1) * sizeof(uint32_t)));
@@ -3666,7 +3668,8 @@ int zb_restore(zb_engine* e, const uint8_t* buf, size_t len) {
   e->records_total = h.records_total; e->rows_total = h.rows_total; e->arena_total = h.arena_total;
   e->rows_mark = h.rows;  // (a snapshot holds live state only)
   e->arena_mark = STATIC_ARENA_BYTES + h.arena_dyn;
-  e->wave = 0;
+  e->wave = 0;  // (and the per-wave job queues of both parities empty, whatever wave ran last)
+  HIPCHECK(e, hipMemsetAsync(e->job_counts, 0, 8 * sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMemcpy(e->dstats, h.stats, sizeof(h.stats), hipMemcpyHostToDevice));
   return finish_batch(e);
 }
