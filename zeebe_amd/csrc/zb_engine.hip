@@ -77,7 +77,6 @@ struct zb_engine {
   DevVec<uint32_t> d_code;
   DevVec<uint32_t> d_cls_code;  // the program with the split conditions' path operands as extraction slots
   DevVec<DevConst> d_consts;
-  DevVec<uint64_t> d_const_w;  // [consts][2] the bytes of string constants of at most 16 bytes (classify)
   DevVec<DevQuery> d_queries;
   DevVec<DevFilter> d_filters;
   DevVec<uint8_t> d_pool;
@@ -193,12 +192,10 @@ struct zb_engine {
   int cls_nq = 0;                 // distinct fast queries of the split conditions (k_cls_classify extraction)
   uint16_t cls_q[CLS_QMAX] = {};
   uint32_t cls_key_off[CLS_QMAX] = {}, cls_key_len[CLS_QMAX] = {};
-  uint64_t cls_key_w[CLS_QMAX][2] = {};
   uint32_t split_elem[CLS_MAX_SPLITS] = {}, split_stride[CLS_MAX_SPLITS] = {};
   ClsPlan* c_plan = nullptr;
   uint64_t cls_cap = 0;           // instances the class buffers hold
   uint8_t* c_ikey = nullptr;
-  uint32_t* c_clen = nullptr;
   uint32_t *c_khist = nullptr, *c_krep = nullptr;  // [CLS_HB][256] each (one allocation with c_klen)
   uint64_t* c_klen = nullptr;                       // [CLS_HB][256]
   TmplRec* t_tmpl = nullptr;     // [CLS_MAX][CLS_ROW][TF] traced records (uniform / class batches)
@@ -366,16 +363,6 @@ int upload_model(zb_engine* e) {
   HIPCHECK(e, e->d_cond.upload(e->model.cond_flows, e->stream));
   HIPCHECK(e, e->d_code.upload(e->model.code, e->stream));
   HIPCHECK(e, e->d_consts.upload(e->model.consts, e->stream));
-  {  // string constants as two little-endian words (k_cls_classify compares strings of <= 16 bytes as words)
-    std::vector<uint64_t> w(2 * std::max<size_t>(e->model.consts.size(), 1), 0);
-    for (size_t i = 0; i < e->model.consts.size(); i++) {
-      const DevConst& c = e->model.consts[i];
-      if (c.type != TT_STRING || c.str_len > 16) continue;
-      for (uint32_t b = 0; b < c.str_len; b++)
-        w[2 * i + b / 8] |= (uint64_t)e->model.pool[c.str_off + b] << (8 * (b % 8));
-    }
-    HIPCHECK(e, e->d_const_w.upload(w, e->stream));
-  }
   HIPCHECK(e, e->d_queries.upload(e->model.queries, e->stream));
   HIPCHECK(e, e->d_filters.upload(e->model.filters, e->stream));
   HIPCHECK(e, e->d_pool.upload(e->model.pool, e->stream));
@@ -528,18 +515,16 @@ uint64_t cls_slot_bound(uint64_t n, uint64_t nwg) {
 
 int grow_class_buffers(zb_engine* e, uint64_t n, uint64_t nwg) {
   if (n <= e->cls_cap) return ZB_OK;
-  void* ps[] = {e->c_ikey, e->c_clen, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm, e->c_segs,
-                e->c_wcls};
+  void* ps[] = {e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm, e->c_segs, e->c_wcls};
   for (void* q : ps)
     if (q) (void)hipFree(q);
-  e->c_ikey = nullptr; e->c_clen = nullptr; e->c_khist = e->c_krep = nullptr; e->c_klen = nullptr; e->c_mask = nullptr;
+  e->c_ikey = nullptr; e->c_khist = e->c_krep = nullptr; e->c_klen = nullptr; e->c_mask = nullptr;
   e->c_woffw = e->c_wgcnt = e->c_wgoff = e->c_perm = e->c_segs = e->c_wcls = nullptr;
   e->cls_cap = 0;
   const uint64_t groups = nwg * (TRAJ_WG / 64);
   // per-instance arrays hold cls_cap = nwg * TRAJ_WG entries: a later batch of up to that many instances reuses them
   const uint64_t cap = nwg * TRAJ_WG;
   HIPCHECK(e, hipMalloc(&e->c_ikey, cap));
-  HIPCHECK(e, hipMalloc(&e->c_clen, cap * sizeof(uint32_t)));
   HIPCHECK(e, hipMalloc(&e->c_khist, CLS_HB * 256 * (2 * sizeof(uint32_t) + sizeof(uint64_t))));
   e->c_krep = e->c_khist + CLS_HB * 256;
   e->c_klen = (uint64_t*)(e->c_khist + 2 * CLS_HB * 256);
@@ -637,17 +622,13 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
       p.cls_q[j] = e->cls_q[j];
       p.cls_key_off[j] = e->cls_key_off[j];
       p.cls_key_len[j] = e->cls_key_len[j];
-      p.cls_key_w[j][0] = e->cls_key_w[j][0];
-      p.cls_key_w[j][1] = e->cls_key_w[j][1];
     }
-    p.const_w = e->d_const_w.p;
     for (int k = 0; k < CLS_MAX_SPLITS; k++) {
       p.split_elem[k] = e->split_elem[k];
       p.split_stride[k] = e->split_stride[k];
     }
     p.plan = e->c_plan;
     p.ikey = e->c_ikey;
-    p.clen = e->c_clen;
     p.khist = e->c_khist;
     p.klen = e->c_klen;
     p.krep = e->c_krep;
@@ -1176,7 +1157,7 @@ void zb_engine_destroy(zb_engine* e) {
                 e->x_tmp, e->mapres, e->map_ws, e->log_mem, e->links_mem, e->srcd_mem, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
                 e->merge_jobs, e->merge_slow, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
-                e->c_plan, e->c_ikey, e->c_clen, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
+                e->c_plan, e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
                 e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->need_children};
   for (void* p : ps)
     if (p) (void)hipFree(p);
@@ -1191,7 +1172,7 @@ void zb_engine_destroy(zb_engine* e) {
   if (e->h_err_pinned) (void)hipHostFree(e->h_err_pinned);
   if (e->h_ctl_pinned) (void)hipHostFree(e->h_ctl_pinned);
   if (e->h_stats_pinned) (void)hipHostFree(e->h_stats_pinned);
-  e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_cls_code.free(); e->d_consts.free(); e->d_const_w.free();
+  e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_cls_code.free(); e->d_consts.free();
   e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
   e->d_ranges.free(); e->d_cmd_pool.free(); e->d_lookup_keys.free(); e->d_lookup_pos.free();
   e->d_maps.free();
@@ -1353,9 +1334,6 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
           e->cls_q[e->cls_nq] = q;
           e->cls_key_off[e->cls_nq] = f.key_off;
           e->cls_key_len[e->cls_nq] = f.key_len;
-          e->cls_key_w[e->cls_nq][0] = e->cls_key_w[e->cls_nq][1] = 0;
-          for (uint32_t b = 0; b < f.key_len && b < 16; b++)
-            e->cls_key_w[e->cls_nq][b / 8] |= (uint64_t)e->model.pool[f.key_off + b] << (8 * (b % 8));
           e->cls_nq++;
         }
       }
