@@ -16,6 +16,23 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run on the GPU box via gpurun)")
 
 
+@pytest.fixture(autouse=True)
+def _guard_bands(request):
+    """Under the guard-band build (ZB_CHECKED_LIBRARY=1, GPU tests): a test fails when any kernel launched during
+    it wrote outside its buffer (zeebe_amd/csrc/zb_checked.hpp)."""
+    if os.environ.get("ZB_CHECKED_LIBRARY") != "1" or request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    from zeebe_amd import engine
+
+    before = engine.checked_violations()
+    yield
+    after = engine.checked_violations()
+    assert before is not None and after is not None, "ZB_CHECKED_LIBRARY=1 but the guard-band build is not loaded"
+    assert after[0] == before[0], "guard-band violations during the test: %d (see stderr / ZB_CHECKED_TRACE)" % (
+        after[0] - before[0])
+
+
 @pytest.fixture(scope="session")
 def vectors():
     import json

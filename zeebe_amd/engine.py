@@ -12,6 +12,10 @@ from typing import List, NamedTuple, Optional, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libzbgpu.so")
+# ZB_CHECKED_LIBRARY=1 (tests only): the guard-band build of the same sources (zeebe_amd/csrc/zb_checked.hpp), which
+# reports every out-of-bounds device write per kernel launch -- a test instrument, never the product library
+if os.environ.get("ZB_CHECKED_LIBRARY") == "1":
+    LIB_PATH = os.path.join(_HERE, "libzbgpu_checked.so")
 
 CFG_WAVE_ONLY = 1  # zb_config.flags: never take the trajectory path
 CFG_EXTERNAL_JOBS = 2  # zb_config.flags: no canonical job harness (job events come through zb_submit)
@@ -166,6 +170,9 @@ def lib():
         L.zb_compact.argtypes = [vp]
         L.zb_read_memory_stats.argtypes = [vp, ctypes.POINTER(zb_memory_stats)]
         L.zb_restore.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t]
+        if hasattr(L, "zb_checked_violations"):  # (the guard-band build only)
+            L.zb_checked_violations.restype = ctypes.c_ulonglong
+            L.zb_checked_violations.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
         _lib = L
     return _lib
 
@@ -179,6 +186,16 @@ EXPORTED_SYMBOLS = ["zb_engine_create", "zb_engine_destroy", "zb_last_error", "z
                     "zb_serialize_frames", "zb_set_request_metadata", "zb_read_source_positions",
                     "zb_log_release", "zb_compact", "zb_read_memory_stats", "zb_submit_messages", "zb_set_clock",
                     "zb_expire_messages", "zb_rccl_library"]
+
+
+def checked_violations():
+    """(violations, launches checked) of the guard-band build, or None for the product library."""
+    L = lib()
+    if not hasattr(L, "zb_checked_violations"):
+        return None
+    n = ctypes.c_ulonglong(0)
+    v = L.zb_checked_violations(ctypes.byref(n))
+    return int(v), int(n.value)
 
 
 def validate_deployment(xml):
