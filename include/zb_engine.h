@@ -56,6 +56,16 @@ extern "C" {
                                  JOB commands (the workflow's CREATE / CANCEL, a worker's ACTIVATE / COMPLETE /
                                  FAIL / TIME_OUT / UPDATE_RETRIES through zb_submit) are processed at their log
                                  position with per-job states; implies no harness (as ZB_CFG_EXTERNAL_JOBS) */
+/* Diagnostic / measurement flags (never needed for correct output; the defaults are the product configuration): */
+#define ZB_CFG_VLEN_CHECK 8       /* the drain's size pass checks every value length an emitting kernel wrote
+                                     against the encoder's dry run (a mismatch fails zb_serialize with ZB_EDEVICE) */
+#define ZB_CFG_GENERIC_DRAIN 16   /* every drain tile through the generic encoder (k_ser_write): the reference pass
+                                     the fast passes are compared with */
+#define ZB_CFG_NO_DEFER 32        /* trajectory batches always write their descriptors in zb_step (no template drain) */
+#define ZB_CFG_INSTANCE_ORDER 64  /* class batches are emitted in instance order (k_tmpl_io) even when not deferred */
+#define ZB_CFG_WAVE_EVENTS 128    /* timing events around every wave's kernels (zb_step_stats process / emit / aux) */
+#define ZB_CFG_WAVE_SPLIT 256     /* the three-kernel wave pipeline (k_process, k_scan, k_emit) instead of k_wave */
+#define ZB_CFG_SINGLE_PASS_DRAIN 512 /* values drained in one pass with decoupled look-back (measured slower) */
 
 typedef struct zb_engine zb_engine;
 
@@ -109,7 +119,7 @@ typedef struct zb_step_stats {
   double wave_kernel_ms;       /* device time of all wave kernels (HIP events on the engine stream) */
   double wall_ms;              /* host wall time of the zb_step call */
   double process_kernel_ms;    /* k_process share of wave_kernel_ms (trajectory: count pass; wave pipeline without
-                                  ZB_WAVE_EVENTS=1: all of it, timed per batch of waves) */
+                                  ZB_CFG_WAVE_EVENTS: all of it, timed per batch of waves) */
   double emit_kernel_ms;       /* k_scan + k_emit share (trajectory: scans + emit pass) */
   double aux_kernel_ms;        /* k_merge + k_cond share */
   uint64_t path;               /* 0: wave pipeline, 1: trajectory path (zb_traj.hip) ran the step,

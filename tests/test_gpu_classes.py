@@ -155,22 +155,22 @@ def test_string_conditions_and_long_keys(consts):
     assert st["path"] == 2
 
 
-@pytest.mark.parametrize("io", ["0", "1"])
-def test_growing_class_batches_on_one_engine(io, monkeypatch):
-    """Class batches of 10, 200 and 256 instances on one engine (one trajectory workgroup each): the class
-    buffers allocated for the first batch serve the later, larger ones (the slot arrays of the class-uniform
-    emit, ZB_TMPL_IO=0 without deferral, are sized for the workgroups' capacity, not the first batch)."""
-    from zeebe_amd.engine import Engine
+@pytest.mark.parametrize("io", [False, True])
+def test_growing_class_batches_on_one_engine(io):
+    """Class batches of growing and shrinking sizes on one engine: 10, 200, 256 (one trajectory workgroup), 300 and
+    512 (two), 4100 (17 workgroups: two emit blocks of CLS_BLK_WG = 16), then 3000 (12, reusing the larger buffers).
+    The class buffers allocated for an earlier batch serve every later one of at most their capacity (the slot
+    arrays of the class-uniform emit -- ZB_CFG_NO_DEFER without ZB_CFG_INSTANCE_ORDER -- are sized for the
+    workgroups' capacity and the block count, not for the batch that allocated them)."""
+    from zeebe_amd.engine import CFG_INSTANCE_ORDER, CFG_NO_DEFER, Engine
 
-    monkeypatch.setenv("ZB_TMPL_IO", io)
-    monkeypatch.setenv("ZB_TMPL_DEFER", "0")
     cfg = workloads.CONFIGS["c3"]
     xml = cfg["workflow"]().to_xml()
     o = zbref.Oracle()
     o.deploy(xml, 100, 1)
-    e = Engine()
+    e = Engine(flags=CFG_NO_DEFER | (CFG_INSTANCE_ORDER if io else 0))
     e.deploy(xml, 100, 1)
-    for n in (10, 200, 256):
+    for n in (10, 200, 256, 300, 512, 4100, 3000):
         blob, offs = cfg["payloads"](n)
         pays = workloads.split(blob, offs)
         for p in pays:

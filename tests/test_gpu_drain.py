@@ -2,7 +2,7 @@
 
 zb_serialize runs the fast pass (k_ser_fast: per-wave LDS image, the fast WORKFLOW_INSTANCE / JOB encoder)
 over every 256-record tile and hands the tiles it cannot take (other record kinds, a wave's values over its
-image) to the generic pass (k_ser_write). ZB_SER_FAST=0 sends every tile through the generic pass, whose
+image) to the generic pass (k_ser_write). ZB_CFG_GENERIC_DRAIN sends every tile through the generic pass, whose
 bytes every other GPU test compares with the oracle. Here the two drains of the same log must agree byte for
 byte -- values and the 40-byte record headers -- on logs that mix the cases: C3 (all tiles fast), C2 with
 job payloads large enough that tiles overflow the fast image, and the CREATE commands (generic records) at
@@ -20,21 +20,10 @@ pytestmark = pytest.mark.gpu
 
 
 def _drain(make, fast, vlen_check=None, **engine_args):
-    from zeebe_amd.engine import Engine, zb_record_header
+    from zeebe_amd.engine import CFG_GENERIC_DRAIN, CFG_VLEN_CHECK, Engine, zb_record_header
 
-    env = {"ZB_SER_FAST": "1" if fast else "0"}
-    if vlen_check is not None:
-        env["ZB_VLEN_CHECK"] = "1" if vlen_check else "0"
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        e = Engine(**engine_args)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
+    flags = (0 if fast else CFG_GENERIC_DRAIN) | (CFG_VLEN_CHECK if vlen_check else 0)
+    e = Engine(flags=flags, **engine_args)
     make(e)
     st = e.step()
     assert st["quiescent"]
@@ -104,7 +93,7 @@ def test_mixed_kinds_fast_drain_matches_generic():
 
 def test_size_pass_formula_matches_encoder():
     # records without a length from their emitting kernel (the wave pipeline writes none) are sized by the
-    # size pass: WORKFLOW_INSTANCE / JOB records by the emit kernels' formula, unless ZB_VLEN_CHECK=1, which
+    # size pass: WORKFLOW_INSTANCE / JOB records by the emit kernels' formula, unless ZB_CFG_VLEN_CHECK, which
     # runs the encoder's dry run on every record. Both must give the same drain, byte for byte.
     wf = bpmn.chain_workflow(4)
     blob, offs = workloads.order_payloads(2000)
@@ -123,19 +112,11 @@ def test_size_pass_formula_matches_encoder():
 
 
 # ---- the template drain (zb_tdrain.hip): a uniform / class batch left without descriptors by zb_step, encoded
-# straight from its traces by zb_serialize of exactly its records; vs the descriptor path (ZB_TMPL_DEFER=0)
+# straight from its traces by zb_serialize of exactly its records; vs the descriptor path (ZB_CFG_NO_DEFER)
 def _template_drain(make, defer):
-    from zeebe_amd.engine import Engine, zb_record_header
+    from zeebe_amd.engine import CFG_NO_DEFER, Engine, zb_record_header
 
-    old = os.environ.get("ZB_TMPL_DEFER")
-    os.environ["ZB_TMPL_DEFER"] = "1" if defer else "0"
-    try:
-        e = Engine(log_capacity=1 << 22, row_capacity=1 << 16, arena_bytes=64 << 20)
-    finally:
-        if old is None:
-            del os.environ["ZB_TMPL_DEFER"]
-        else:
-            os.environ["ZB_TMPL_DEFER"] = old
+    e = Engine(log_capacity=1 << 22, row_capacity=1 << 16, arena_bytes=64 << 20, flags=0 if defer else CFG_NO_DEFER)
     n = make(e)
     st = e.step()
     assert st["quiescent"] and st["path"] in (1, 2), st

@@ -97,10 +97,9 @@ def test_frames_c2_properties():
 def test_frames_after_values_drain_with_rejections(monkeypatch):
     """records() then frames() over one log holding rejections: the values drain writes the measured
     value lengths back into the engine's length hints, and the frames size pass must still add each rejection's
-    reason. Product configuration (ZB_VLEN_CHECK=0): the size pass trusts the hints."""
+    reason. Product configuration (no ZB_CFG_VLEN_CHECK): the size pass trusts the hints."""
     from zeebe_amd.engine import Engine
 
-    monkeypatch.setenv("ZB_VLEN_CHECK", "0")
     cfg = workloads.CONFIGS["c1"]
     xml = cfg["workflow"]().to_xml()
     o = zbref.Oracle()

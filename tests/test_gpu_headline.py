@@ -1,9 +1,9 @@
 """The bench's headline step (C3, 10M instances, BASELINE.json configs[2]) byte-checked in the configuration that
-produces the number: product build, no ZB_VLEN_CHECK, the batch left without descriptors by zb_step and drained
+produces the number: product configuration (no diagnostic flags), the batch left without descriptors by zb_step and drained
 from its traces (zb_tdrain.hip).
 
   * the template drain's values and record headers equal the generic encoder's over the descriptors
-    (ZB_TMPL_DEFER=0: k_tmpl writes them; ZB_SER_FAST=0: every tile through k_ser_write), byte for byte, for all
+    (ZB_CFG_NO_DEFER: k_tmpl writes them; ZB_CFG_GENERIC_DRAIN: every tile through k_ser_write), byte for byte, for all
     ~101.7M records;
   * a strided sample of instances: every record's value equals the reference's bytes for that instance -- the
     oracle runs the instance alone, its keys are mapped onto the keys the 10M run gave the same records (in
@@ -24,12 +24,10 @@ N = 10_000_000
 
 
 def _run(monkeypatch, fast):
-    from zeebe_amd.engine import Engine
+    from zeebe_amd.engine import CFG_GENERIC_DRAIN, CFG_NO_DEFER, Engine
 
-    monkeypatch.setenv("ZB_VLEN_CHECK", "0")
-    monkeypatch.setenv("ZB_SER_FAST", "1" if fast else "0")
-    monkeypatch.setenv("ZB_TMPL_DEFER", "1" if fast else "0")
-    e = Engine(log_capacity=N * 16, row_capacity=1 << 20, arena_bytes=N * 64 + (64 << 20))
+    e = Engine(log_capacity=N * 16, row_capacity=1 << 20, arena_bytes=N * 64 + (64 << 20),
+               flags=0 if fast else CFG_GENERIC_DRAIN | CFG_NO_DEFER)
     e.deploy(bpmn.xor_workflow().to_xml(), 100, 1)
     blob, offs = workloads.xor_payloads_np(N)
     e.create_packed("xor", blob, offs)

@@ -264,15 +264,59 @@ def test_message_ids_delete_ttl_and_large_fields():
             g.close()
 
 
-def test_rccl_exchange_failure_protocol():
-    """A rank whose local part of zb_comm_exchange fails (ZB_FAIL_EXCHANGE, before its outbox is taken) returns an
-    error from the collective instead of hanging; the next exchange goes through and the run completes."""
+def _xbatch(recs, var=b""):
+    """One exchange batch (include/zb_engine.h): [count][total bytes][count x 64-byte zb_exchange_rec][byte section]."""
+    import struct
+
+    body = b"".join(struct.pack("<iiiIqqqHHIIIQ", *r) for r in recs) + var
+    body += b"\0" * (-len(body) % 8)
+    return struct.pack("<QQ", len(recs), 16 + len(body)) + body
+
+
+def test_inbox_rejects_malformed_batches():
+    """zb_inbox_submit checks every batch before anything reaches the device: a count whose records do
+    not fit the batch (incl. a count * 64 that overflows), a record whose variable bytes run past the batch's byte
+    section, an offset past it, a CORRELATE naming an element the model does not have -- each ZB_EINVAL, with the
+    log unchanged; a well-formed batch is then accepted."""
+    import struct
+
+    from zeebe_amd.engine import Engine, ZbError
+
+    e = Engine(device=0, partition_id=0, partition_count=1, log_capacity=1 << 16, row_capacity=1 << 12)
+    e.deploy(catch_workflow(), 100, 1)
+    e.create("wf", [msgpack.packb({"orderId": "order-1"})])
+    e.run()
+    n0 = e.log_size()
+    name, ck = b"order canceled", b"order-1"
+    ok_open = (1, 0, 0, 0, 1, 6, 3, 1, 0, len(name), len(ck), 0, 0)
+    good = _xbatch([ok_open], name + ck)
+    bad = [
+        struct.pack("<QQ", 1 << 58, 16 + 64) + good[16:16 + 64],                   # count * 64 overflows
+        struct.pack("<QQ", 2, len(good)) + good[16:],                              # two records do not fit
+        _xbatch([(1, 0, 0, 0, 1, 6, 3, 1, 0, len(name), 4096, 0, 0)], name + ck),  # ck runs past the section
+        _xbatch([(1, 0, 0, 0, 1, 6, 3, 1, 0, len(name), len(ck), 0, 1 << 40)], name + ck),  # offset past it
+    ]
+    for b in bad:
+        with pytest.raises(ZbError, match="ZB_EINVAL"):
+            e.inbox(cluster.KIND_OPEN, bytearray(b))
+    with pytest.raises(ZbError, match="ZB_EINVAL"):  # CORRELATE of an element the model does not have
+        e.inbox(cluster.KIND_CORRELATE, bytearray(_xbatch([(2, 0, 0, 0, 1, 6, 3, 60000, 0, len(name), 0, 1, 0)],
+                                                          name + b"\x80")))
+    assert e.log_size() == n0
+    e.inbox(cluster.KIND_OPEN, bytearray(good))  # (OPEN + OPENED)
+    assert e.log_size() == n0 + 2
+    e.close()
+
+
+def _exchange_failure_protocol():
+    """(body of test_rccl_exchange_failure_protocol, run in a process that loaded the guard-band build)"""
     import os
     import socket
 
     import torch.distributed as dist
-    from zeebe_amd.engine import Engine, ZbError
+    from zeebe_amd.engine import Engine, ZbError, checked_violations
 
+    assert checked_violations() is not None, "the failure hook exists only in the guard-band build"
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -297,6 +341,24 @@ def test_rccl_exchange_failure_protocol():
         dc.settle()
         dc.publish(b"order canceled", [b"order-%d" % i for i in range(20)], [b"\x80"] * 20)
         assert e.counters()["completed"] == 20
+        assert checked_violations()[0] == 0
         e.close()
     finally:
         dist.destroy_process_group()
+
+
+def test_rccl_exchange_failure_protocol():
+    """A rank whose local part of zb_comm_exchange fails (injected before its outbox is taken) returns an error from
+    the collective instead of hanging; the next exchange goes through and the run completes. The injection hook
+    (ZB_FAIL_EXCHANGE) exists only in the guard-band test build (zeebe_amd/csrc/zb_checked.hpp), never in the
+    product library, so the case runs in a child process that loads that build."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ZB_CHECKED_LIBRARY="1", PYTHONPATH=os.pathsep.join([root, os.path.join(root, "tests")]))
+    code = "import test_gpu_messages as t; t._exchange_failure_protocol(); print('exchange failure protocol ok')"
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "exchange failure protocol ok" in r.stdout, (r.returncode, r.stdout[-2000:],
+                                                                              r.stderr[-4000:])

@@ -16,21 +16,24 @@ pytestmark = pytest.mark.gpu
 
 # Every case runs through both GPU pipelines: the trajectory path (zb_traj.hip, taken for a batch of
 # CREATEs on an idle partition) and the general wave pipeline (zb_wave.hip, forced by wave_only), each in the
-# product configuration and with ZB_VLEN_CHECK=1 (the drain's size pass checks every value length an emitting
+# product configuration and with ZB_CFG_VLEN_CHECK (the drain's size pass checks every value length an emitting
 # kernel wrote against the encoder's dry run, and fails the drain on a difference).
 PATHS = ["traj", "wave", "traj+vlencheck", "wave+vlencheck"]
+_CASE = {"flags": 0}  # zb_config.flags of every engine the current case creates
 
 
 @pytest.fixture(params=PATHS)
 def path(request, monkeypatch):
-    monkeypatch.setenv("ZB_VLEN_CHECK", "1" if request.param.endswith("+vlencheck") else "0")
+    from zeebe_amd.engine import CFG_VLEN_CHECK
+
+    monkeypatch.setitem(_CASE, "flags", CFG_VLEN_CHECK if request.param.endswith("+vlencheck") else 0)
     return request.param.split("+")[0]
 
 
 def _engine(**kw):
     from zeebe_amd.engine import Engine
 
-    return Engine(**kw)
+    return Engine(flags=_CASE["flags"], **kw)
 
 
 def _run_both(xml, process, payloads, job_payloads=None, wf_key=100, path="traj", expect_traj=False, **cap):

@@ -8,12 +8,10 @@ from zeebe_amd import workloads  # noqa: E402
 
 
 def run(io, n):
-    os.environ["ZB_TMPL_IO"] = str(io)
-    os.environ["ZB_VLEN_CHECK"] = "0"
-    from zeebe_amd.engine import Engine
+    from zeebe_amd.engine import CFG_INSTANCE_ORDER, CFG_NO_DEFER, Engine
     cfg = workloads.CONFIGS["c3"]
     blob, offs = cfg["payloads"](n)
-    e = Engine()
+    e = Engine(flags=CFG_NO_DEFER | (CFG_INSTANCE_ORDER if io else 0))
     e.deploy(cfg["workflow"]().to_xml(), 100, 1)
     e.create(cfg["process"], workloads.split(blob, offs))
     st = e.step()

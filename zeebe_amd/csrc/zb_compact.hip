@@ -62,12 +62,18 @@ __device__ __forceinline__ void mark_granules(const CompactParams& P, uint64_t g
   }
 }
 
-// mark `blobs` consecutive blobs from ref (refs below the static region are never moved)
+// mark `blobs` consecutive blobs from ref (refs below the static region are never moved). A blob is
+// [u32 len][len bytes] padded to 8; one whose length runs past the allocated bytes (arena_next) -- a ref that does
+// not point at a blob header -- marks nothing and flags the partition (the bitmap covers [static, arena_next) only)
 __device__ __forceinline__ void mark_ref(const CompactParams& P, uint32_t ref, int blobs) {
   for (int k = 0; k < blobs; k++) {
     if ((uint64_t)ref < P.static_refs || (uint64_t)ref * 8 >= P.arena_next) return;
     const uint32_t len = *(const uint32_t*)(P.arena + (uint64_t)ref * 8);
     const uint64_t n = (4 + (uint64_t)len + 7) >> 3;
+    if (((uint64_t)ref + n) * 8 > P.arena_next) {
+      atomicOr(P.err, (uint32_t)DE_CORRUPT);
+      return;
+    }
     mark_granules(P, (uint64_t)ref - P.static_refs, n);
     ref += (uint32_t)n;
   }

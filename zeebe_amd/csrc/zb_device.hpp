@@ -185,7 +185,8 @@ enum ErrCode : uint8_t {
 // device error flags (sticky, host checks after each batch of waves)
 enum DevErr : uint32_t {
   DE_LOG_FULL = 1u, DE_ROWS_FULL = 2u, DE_ARENA_FULL = 4u, DE_UNSUPPORTED = 8u, DE_PROCESSING = 16u,
-  DE_BAD_PAYLOAD = 64u, DE_TIMEOUT = 128u
+  DE_BAD_PAYLOAD = 64u, DE_TIMEOUT = 128u,
+  DE_CORRUPT = 256u  // a reference names a blob that runs past the arena's allocated bytes (compaction)
 };
 
 // Per-wave header (double buffered: wave w reads hdr[w&1], k_scan of wave w writes hdr[(w+1)&1]).

@@ -65,8 +65,7 @@ struct zb_engine {
   zb_config cfg{};
   hipStream_t stream = nullptr;
   int32_t ncu = 256;            // compute units of the device
-  int32_t wave_grid_fixed = 0;  // ZB_WAVE_GRID (tuning experiments): fixed wave grid instead of the sized one
-  int32_t wave_fused_grid = 0;  // k_wave: resident workgroups (0 = three-kernel pipeline; ZB_WAVE_FUSED=0 forces it)
+  int32_t wave_fused_grid = 0;  // k_wave: resident workgroups (0 = three-kernel pipeline; ZB_CFG_WAVE_SPLIT forces it)
   uint64_t* lookback = nullptr; // k_wave look-back granules
   std::string err;
 
@@ -77,6 +76,7 @@ struct zb_engine {
   DevVec<uint32_t> d_code;
   DevVec<uint32_t> d_cls_code;  // the program with the split conditions' path operands as extraction slots
   DevVec<DevConst> d_consts;
+  DevVec<uint64_t> d_const_w;  // [consts][2] the bytes of string constants of at most 16 bytes (classify)
   DevVec<DevQuery> d_queries;
   DevVec<DevFilter> d_filters;
   DevVec<uint8_t> d_pool;
@@ -85,8 +85,7 @@ struct zb_engine {
   bool has_io = false;          // some element has a zeebe:ioMapping (k_map runs, no trajectory path)
   uint64_t* mapres = nullptr;   // k_map outcomes [wave_cap + 8]
   MNode* map_ws = nullptr;      // k_map tree workspaces
-  int ser_mode = 0;              // ZB_SER_MODE: 0 = two passes (size, scan, write), 1 = single pass (look-back)
-  int ser_nt = 1;                // ZB_SER_NT=0: plain (not non-temporal) stores in the drain write pass
+  int ser_mode = 0;              // 0 = two passes (size, scan, write), 1 = single pass (look-back, ZB_CFG_SINGLE_PASS_DRAIN)
 
   // device state. The log arrays hold the window [win_base, win_base + log_capacity) of absolute positions;
   // log / links / srcd / vlen are biased pointers (index = absolute position) into the *_mem allocations, so
@@ -106,7 +105,7 @@ struct zb_engine {
   DevVec<uint8_t> d_segpool;
   uint32_t segpool_len = 0;
   bool seg_ok = false;          // the runs fit the fast passes' LDS
-  uint32_t* vlen_bad = nullptr; // ZB_VLEN_CHECK=1: the size pass checks every known length (device flag)
+  uint32_t* vlen_bad = nullptr; // ZB_CFG_VLEN_CHECK: the size pass checks every known length (device flag)
   RowMeta* rmeta = nullptr;
   RowKeys* rkeys = nullptr;
   uint8_t* arena = nullptr;
@@ -192,10 +191,12 @@ struct zb_engine {
   int cls_nq = 0;                 // distinct fast queries of the split conditions (k_cls_classify extraction)
   uint16_t cls_q[CLS_QMAX] = {};
   uint32_t cls_key_off[CLS_QMAX] = {}, cls_key_len[CLS_QMAX] = {};
+  uint64_t cls_key_w[CLS_QMAX][2] = {};
   uint32_t split_elem[CLS_MAX_SPLITS] = {}, split_stride[CLS_MAX_SPLITS] = {};
   ClsPlan* c_plan = nullptr;
   uint64_t cls_cap = 0;           // instances the class buffers hold
   uint8_t* c_ikey = nullptr;
+  uint32_t* c_clen = nullptr;
   uint32_t *c_khist = nullptr, *c_krep = nullptr;  // [CLS_HB][256] each (one allocation with c_klen)
   uint64_t* c_klen = nullptr;                       // [CLS_HB][256]
   TmplRec* t_tmpl = nullptr;     // [CLS_MAX][CLS_ROW][TF] traced records (uniform / class batches)
@@ -298,10 +299,9 @@ struct zb_engine {
   uint32_t dr_wide_tiles = 0;    // tiles the last drain's wide fast pass encoded
   uint32_t dr_slow_tiles = 0;    // how many tiles the last drain ran through k_ser_write
   bool dr_split = false;         // the last drain ran k_ser_fast + k_ser_write (events 2-4, 5-3)
-  int ser_fast = 1;              // ZB_SER_FAST=0: every tile through k_ser_write
-  bool wave_events = false;      // ZB_WAVE_EVENTS=1: timing events around every wave's kernels
-  int tmpl_io = 0;               // ZB_TMPL_IO=1: class batches emitted in instance order (k_tmpl_io)
-  int ser_lenbuf = 0;            // ZB_SER_LENBUF=1: value lengths through their own buffer, not vlen
+  int ser_fast = 1;              // 0 (ZB_CFG_GENERIC_DRAIN): every tile through k_ser_write
+  bool wave_events = false;      // ZB_CFG_WAVE_EVENTS: timing events around every wave's kernels
+  int tmpl_io = 0;               // ZB_CFG_INSTANCE_ORDER: class batches emitted in instance order (k_tmpl_io)
   zb_record_header* dr_hdr = nullptr;
   uint8_t* dr_val = nullptr;
   bool dr_frames = false;       // the drain batch holds log frames (no headers)
@@ -315,7 +315,7 @@ struct zb_engine {
 
   // deferred template batch (zb_tdrain.hip): a uniform / class batch whose descriptors k_tmpl has not written;
   // zb_serialize of exactly [seg_begin, seg_end) encodes it from the traces, anything else materializes it
-  int tmpl_defer = 1;             // ZB_TMPL_DEFER=0: always write the descriptors in zb_step
+  int tmpl_defer = 1;             // 0 (ZB_CFG_NO_DEFER): always write the descriptors in zb_step
   bool seg_pending = false;
   int64_t seg_begin = 0, seg_end = 0;
   uint32_t seg_wmax = 0, seg_nc = 1;
@@ -363,6 +363,16 @@ int upload_model(zb_engine* e) {
   HIPCHECK(e, e->d_cond.upload(e->model.cond_flows, e->stream));
   HIPCHECK(e, e->d_code.upload(e->model.code, e->stream));
   HIPCHECK(e, e->d_consts.upload(e->model.consts, e->stream));
+  {  // string constants as two little-endian words (k_cls_classify compares strings of <= 16 bytes as words)
+    std::vector<uint64_t> w(2 * std::max<size_t>(e->model.consts.size(), 1), 0);
+    for (size_t i = 0; i < e->model.consts.size(); i++) {
+      const DevConst& c = e->model.consts[i];
+      if (c.type != TT_STRING || c.str_len > 16) continue;
+      for (uint32_t b = 0; b < c.str_len; b++)
+        w[2 * i + b / 8] |= (uint64_t)e->model.pool[c.str_off + b] << (8 * (b % 8));
+    }
+    HIPCHECK(e, e->d_const_w.upload(w, e->stream));
+  }
   HIPCHECK(e, e->d_queries.upload(e->model.queries, e->stream));
   HIPCHECK(e, e->d_filters.upload(e->model.filters, e->stream));
   HIPCHECK(e, e->d_pool.upload(e->model.pool, e->stream));
@@ -478,7 +488,6 @@ WaveParams wave_params(zb_engine* e) {
     const int64_t chunk = std::min<int64_t>(gen, (int64_t)e->wave_cap);
     const int64_t g = ((chunk + WAVE_TILE - 1) / WAVE_TILE + 3) / 4;
     p.grid = (int32_t)std::max<int64_t>(256, std::min<int64_t>(g, 1024));
-    if (e->wave_grid_fixed) p.grid = e->wave_grid_fixed;
   }
   return p;
 }
@@ -494,13 +503,14 @@ int check_device_errors(zb_engine* e, uint32_t flags) {
   if (flags & DE_PROCESSING) m += " processing-failure";
   if (flags & DE_BAD_PAYLOAD) m += " malformed-payload";
   if (flags & DE_TIMEOUT) m += " hand-off-timeout";
+  if (flags & DE_CORRUPT) m += " corrupt-arena-reference";
   uint64_t info = ~0ull;
   if (hipMemcpy(&info, e->derr_info, sizeof(info), hipMemcpyDeviceToHost) == hipSuccess && info != ~0ull)
     m += " (first at log position " + std::to_string(info >> 8) + ", site " + std::to_string(info & 0xff) + ")";
   int code = ZB_EPROCESSING;
   if (flags & (DE_LOG_FULL | DE_ROWS_FULL | DE_ARENA_FULL)) code = ZB_ENOMEM;
   else if (flags & DE_UNSUPPORTED) code = ZB_EUNSUPPORTED;
-  if (flags & DE_TIMEOUT) code = ZB_EDEVICE;
+  if (flags & (DE_TIMEOUT | DE_CORRUPT)) code = ZB_EDEVICE;
   return fail(e, code, m);
 }
 
@@ -515,16 +525,18 @@ uint64_t cls_slot_bound(uint64_t n, uint64_t nwg) {
 
 int grow_class_buffers(zb_engine* e, uint64_t n, uint64_t nwg) {
   if (n <= e->cls_cap) return ZB_OK;
-  void* ps[] = {e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm, e->c_segs, e->c_wcls};
+  void* ps[] = {e->c_ikey, e->c_clen, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm, e->c_segs,
+                e->c_wcls};
   for (void* q : ps)
     if (q) (void)hipFree(q);
-  e->c_ikey = nullptr; e->c_khist = e->c_krep = nullptr; e->c_klen = nullptr; e->c_mask = nullptr;
+  e->c_ikey = nullptr; e->c_clen = nullptr; e->c_khist = e->c_krep = nullptr; e->c_klen = nullptr; e->c_mask = nullptr;
   e->c_woffw = e->c_wgcnt = e->c_wgoff = e->c_perm = e->c_segs = e->c_wcls = nullptr;
   e->cls_cap = 0;
   const uint64_t groups = nwg * (TRAJ_WG / 64);
   // per-instance arrays hold cls_cap = nwg * TRAJ_WG entries: a later batch of up to that many instances reuses them
   const uint64_t cap = nwg * TRAJ_WG;
   HIPCHECK(e, hipMalloc(&e->c_ikey, cap));
+  HIPCHECK(e, hipMalloc(&e->c_clen, cap * sizeof(uint32_t)));
   HIPCHECK(e, hipMalloc(&e->c_khist, CLS_HB * 256 * (2 * sizeof(uint32_t) + sizeof(uint64_t))));
   e->c_krep = e->c_khist + CLS_HB * 256;
   e->c_klen = (uint64_t*)(e->c_khist + 2 * CLS_HB * 256);
@@ -605,7 +617,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   if (p.cls) {
     int grc = grow_class_buffers(e, (uint64_t)n, nwg);
     if (grc != ZB_OK) return grc;
-    // instance-order emit (k_tmpl_io) over the instance workgroups; ZB_TMPL_IO=0: class-uniform emit, every
+    // instance-order emit (k_tmpl_io) over the instance workgroups; otherwise class-uniform emit, every
     // (block, class) segment padded to whole waves, a multiple of 8 workgroups (XCD mapping)
     // (a batch the drain may take from its traces skips the class-uniform slot layout: if it is emitted after all,
     // now or when materialized, the emit runs in instance order)
@@ -622,13 +634,17 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
       p.cls_q[j] = e->cls_q[j];
       p.cls_key_off[j] = e->cls_key_off[j];
       p.cls_key_len[j] = e->cls_key_len[j];
+      p.cls_key_w[j][0] = e->cls_key_w[j][0];
+      p.cls_key_w[j][1] = e->cls_key_w[j][1];
     }
+    p.const_w = e->d_const_w.p;
     for (int k = 0; k < CLS_MAX_SPLITS; k++) {
       p.split_elem[k] = e->split_elem[k];
       p.split_stride[k] = e->split_stride[k];
     }
     p.plan = e->c_plan;
     p.ikey = e->c_ikey;
+    p.clen = e->c_clen;
     p.khist = e->c_khist;
     p.klen = e->c_klen;
     p.krep = e->c_krep;
@@ -684,7 +700,8 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   st.emit_kernel_ms += ms1;
   st.wave_kernel_ms += ms0 + ms1;
   st.launches += p.cls ? 11 : p.uni ? 6 : 7;
-  if (p.cls && getenv("ZB_DEBUG_CLS")) {  // class batch internals (debugging aid)
+#ifdef ZB_CHECKED
+  if (p.cls && getenv("ZB_DEBUG_CLS")) {  // class batch internals (debugging aid of the guard-band build)
     ClsPlan pl;
     uint32_t wc[CLS_MAX];
     (void)hipMemcpy(&pl, e->c_plan, sizeof(pl), hipMemcpyDeviceToHost);
@@ -699,6 +716,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
       fprintf(stderr, "\n");
     }
   }
+#endif
   if (e->h_ctl_pinned->flag) {
     // nothing but scratch counts was written: run the batch per instance (or on the wave pipeline)
     if ((p.cls || p.uni) && e->traj_model_ok) return run_trajectory(e, log_base, n, st, false);
@@ -874,6 +892,7 @@ CompactParams compact_params(zb_engine* e) {
   c.win_end = e->host_hdr.end;
   c.msgs = e->msgs; c.msg_count = e->msgs ? e->msg_count : 0;
   c.subs = e->subs; c.sub_count = e->subs ? e->sub_count : 0;
+  c.err = e->derr;
   return c;
 }
 
@@ -1041,14 +1060,12 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   *out = nullptr;
   auto* e = new zb_engine();
   e->cfg = *cfg;
-  if (const char* m = std::getenv("ZB_SER_MODE")) e->ser_mode = std::strcmp(m, "fused") == 0 ? 1 : 0;
-  if (const char* m = std::getenv("ZB_SER_NT")) e->ser_nt = atoi(m);
-  if (const char* m = std::getenv("ZB_SER_FAST")) e->ser_fast = atoi(m);
-  if (const char* m = std::getenv("ZB_TMPL_IO")) e->tmpl_io = atoi(m);
-  if (const char* m = std::getenv("ZB_TMPL_DEFER")) e->tmpl_defer = atoi(m);
-  if (const char* m = std::getenv("ZB_WAVE_EVENTS")) e->wave_events = atoi(m) != 0;
-  if (const char* m = std::getenv("ZB_SER_LENBUF")) e->ser_lenbuf = atoi(m);
-  if (const char* g = std::getenv("ZB_WAVE_GRID")) e->wave_grid_fixed = std::max(0, std::min(atoi(g), (int)WAVE_GRID_MAX));
+  const int32_t fl = e->cfg.flags;
+  e->ser_mode = (fl & ZB_CFG_SINGLE_PASS_DRAIN) ? 1 : 0;
+  e->ser_fast = (fl & ZB_CFG_GENERIC_DRAIN) ? 0 : 1;
+  e->tmpl_io = (fl & ZB_CFG_INSTANCE_ORDER) ? 1 : 0;
+  e->tmpl_defer = (fl & ZB_CFG_NO_DEFER) ? 0 : 1;
+  e->wave_events = (fl & ZB_CFG_WAVE_EVENTS) != 0;
   if (e->cfg.log_capacity == 0) e->cfg.log_capacity = 1ull << 22;
   if (e->cfg.row_capacity == 0) e->cfg.row_capacity = 1ull << 20;
   if (e->cfg.arena_bytes == 0) e->cfg.arena_bytes = 64ull << 20;
@@ -1071,8 +1088,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
       e->ncu = ncu;
   }
   {
-    const char* f = std::getenv("ZB_WAVE_FUSED");
-    const int per_cu = (f && atoi(f) == 0) ? 0 : wave_resident_per_cu();
+    const int per_cu = (e->cfg.flags & ZB_CFG_WAVE_SPLIT) ? 0 : wave_resident_per_cu();
     // the occupancy limit less one workgroup per eight CUs: every workgroup of the persistent grid is resident
     // with room to spare, so no tile waits on a workgroup that is not running. (A grid of (per_cu - 1) per CU left
     // a quarter of the wave slots idle: C2 1M wave-only stepping 19.8 ms at 768 workgroups, 17.9 at 1024.)
@@ -1086,8 +1102,8 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->srcd_mem, L * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->vlen_mem, L * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   rebias(e);
-  if (const char* c = std::getenv("ZB_VLEN_CHECK"))
-    if (atoi(c) && hipMalloc(&e->vlen_bad, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if ((e->cfg.flags & ZB_CFG_VLEN_CHECK) && hipMalloc(&e->vlen_bad, sizeof(uint32_t)) != hipSuccess)
+    return cleanup(ZB_ENOMEM);
   // job states: open addressing at load <= 1/2 for row_capacity live jobs
   if (e->cfg.flags & ZB_CFG_JOB_PROCESSOR) {
     uint64_t slots = 1024;
@@ -1157,7 +1173,7 @@ void zb_engine_destroy(zb_engine* e) {
                 e->x_tmp, e->mapres, e->map_ws, e->log_mem, e->links_mem, e->srcd_mem, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
                 e->merge_jobs, e->merge_slow, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
-                e->c_plan, e->c_ikey, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
+                e->c_plan, e->c_ikey, e->c_clen, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
                 e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->need_children};
   for (void* p : ps)
     if (p) (void)hipFree(p);
@@ -1172,7 +1188,7 @@ void zb_engine_destroy(zb_engine* e) {
   if (e->h_err_pinned) (void)hipHostFree(e->h_err_pinned);
   if (e->h_ctl_pinned) (void)hipHostFree(e->h_ctl_pinned);
   if (e->h_stats_pinned) (void)hipHostFree(e->h_stats_pinned);
-  e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_cls_code.free(); e->d_consts.free();
+  e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_cls_code.free(); e->d_consts.free(); e->d_const_w.free();
   e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
   e->d_ranges.free(); e->d_cmd_pool.free(); e->d_lookup_keys.free(); e->d_lookup_pos.free();
   e->d_maps.free();
@@ -1334,6 +1350,9 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
           e->cls_q[e->cls_nq] = q;
           e->cls_key_off[e->cls_nq] = f.key_off;
           e->cls_key_len[e->cls_nq] = f.key_len;
+          e->cls_key_w[e->cls_nq][0] = e->cls_key_w[e->cls_nq][1] = 0;
+          for (uint32_t b = 0; b < f.key_len && b < 16; b++)
+            e->cls_key_w[e->cls_nq][b / 8] |= (uint64_t)e->model.pool[f.key_off + b] << (8 * (b % 8));
           e->cls_nq++;
         }
       }
@@ -2036,7 +2055,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     next_batch = std::min(2 * next_batch, WAVES_PER_SYNC_MAX);
     if (max_waves) batch = std::min<int>(batch, (int)(max_waves - launched));
     // timing events cost ~5 us of stream time each between kernels (C2: 4 per wave = 2.9 ms of a 41 ms
-    // step): per wave only with ZB_WAVE_EVENTS=1 (process / emit / aux split), else one pair per batch
+    // step): per wave only with ZB_CFG_WAVE_EVENTS (process / emit / aux split), else one pair per batch
     const bool per_wave = e->wave_events;
     if (!per_wave) HIPCHECK(e, hipEventRecord(e->ev[0], e->stream));
     for (int i = 0; i < batch; i++) {
@@ -2338,7 +2357,7 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
   HIPCHECK(e, e->d_cmd_pool.upload(e->cmd_pool, e->stream));
   if (fc && !e->reqs.empty()) HIPCHECK(e, e->d_reqs.upload(e->reqs, e->stream));
   SerParams sp{};
-  sp.nt = e->ser_nt;
+  sp.nt = 1;
   if (fc) {
     sp.frames = 1;
     sp.stream_id = fc->stream_id;
@@ -2405,8 +2424,8 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
       const int64_t tiles = (count + 255) / 256;
       SerParams sz = sp;
       sz.lengths = e->dr_len;
-      // values: lengths in vlen (measured ones filled in); frames (and ZB_SER_LENBUF=1): lengths[]
-      sz.len_in_vlen = (fc || e->ser_lenbuf) ? 0 : 1;
+      // values: lengths in vlen (measured ones filled in); frames: lengths[]
+      sz.len_in_vlen = fc ? 0 : 1;
       sz.vlen_out = e->vlen;
       sz.tile_sums = e->dr_tsum;  // tiles + 1 entries, the last one 0: the scan's last output is the total
       HIPCHECK(e, hipEventRecord(e->dr_ev[0], e->stream));
@@ -2459,10 +2478,10 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
     HIPCHECK(e, hipMemcpyAsync(e->h_dr_total, e->dr_total, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHECK(e, hipStreamSynchronize(e->stream));
     HIPCHECK(e, hipGetLastError());
-    if (e->vlen_bad) {  // ZB_VLEN_CHECK: an emitting kernel's value length disagreed with the encoder
+    if (e->vlen_bad) {  // ZB_CFG_VLEN_CHECK: an emitting kernel's value length disagreed with the encoder
       uint32_t bad = 0;
       HIPCHECK(e, hipMemcpy(&bad, e->vlen_bad, sizeof(bad), hipMemcpyDeviceToHost));
-      if (bad) return fail(e, ZB_EDEVICE, "value length hint differs from the serialized value (ZB_VLEN_CHECK)");
+      if (bad) return fail(e, ZB_EDEVICE, "value length hint differs from the serialized value (ZB_CFG_VLEN_CHECK)");
     }
     const uint32_t overflow = ((const uint32_t*)(e->h_dr_total + 2))[1];
     if (!overflow) break;
@@ -2856,14 +2875,37 @@ int deliver(zb_engine* e, int kind, const uint8_t* buf, const std::vector<uint64
   return finish_batch(e);
 }
 
-// batches laid out back to back: (count, byte offset) of each, from their headers
-bool parse_batches(const uint8_t* p, size_t bytes, std::vector<uint64_t>& counts, std::vector<uint64_t>& offs) {
+// an exchange batch header [count][total bytes] inside the avail bytes left: the records fit the batch (no overflow
+// in count * 64), the total is 8-aligned
+bool batch_header_ok(const uint64_t h[2], size_t avail) {
+  if (h[1] < ZB_XCHG_BATCH_HEADER || h[1] > avail || (h[1] & 7)) return false;
+  return h[0] <= (h[1] - ZB_XCHG_BATCH_HEADER) / sizeof(zb_exchange_rec);
+}
+
+// every record's variable bytes [name][correlation key][payload] lie inside its batch's byte section, and a
+// CORRELATE names a catch element of this partition's model (the inbox kernels read both without a bounds check)
+bool batch_records_ok(const zb_exchange_rec* r, uint64_t cnt, uint64_t total, int kind, size_t n_elems) {
+  const uint64_t var_bytes = total - ZB_XCHG_BATCH_HEADER - cnt * sizeof(zb_exchange_rec);
+  for (uint64_t i = 0; i < cnt; i++) {
+    const uint64_t need = (uint64_t)r[i].name_len + r[i].ck_len + r[i].payload_len;  // (< 2^34: no overflow)
+    if (r[i].var_offset > var_bytes || need > var_bytes - r[i].var_offset) return false;
+    if (kind == ZB_XCHG_CORRELATE && r[i].elem >= n_elems) return false;
+  }
+  return true;
+}
+
+// batches laid out back to back (host memory): (count, byte offset) of each, from their headers, every record checked
+bool parse_batches(const uint8_t* p, size_t bytes, int kind, size_t n_elems, std::vector<uint64_t>& counts,
+                   std::vector<uint64_t>& offs) {
   size_t o = 0;
   while (o < bytes) {
     if (bytes - o < ZB_XCHG_BATCH_HEADER) return false;
     uint64_t h[2];
     std::memcpy(h, p + o, sizeof(h));
-    if (h[1] < ZB_XCHG_BATCH_HEADER + h[0] * sizeof(zb_exchange_rec) || h[1] > bytes - o || (h[1] & 7)) return false;
+    if (!batch_header_ok(h, bytes - o)) return false;
+    std::vector<zb_exchange_rec> r(h[0]);
+    if (h[0]) std::memcpy(r.data(), p + o + ZB_XCHG_BATCH_HEADER, h[0] * sizeof(zb_exchange_rec));
+    if (!batch_records_ok(r.data(), h[0], h[1], kind, n_elems)) return false;
     counts.push_back(h[0]);
     offs.push_back(o);
     o += h[1];
@@ -3050,19 +3092,26 @@ int zb_inbox_submit(zb_engine* e, int kind, const uint8_t* batches, size_t bytes
   if (rc != ZB_OK) return rc;
   if (bytes == 0) return ZB_OK;
   std::vector<uint64_t> counts, offs;
-  if (on_device) {  // batch headers read one after another
+  const size_t n_elems = e->model.elems.size();
+  if (on_device) {  // batch headers and records read one batch after another, checked as for host batches
     size_t o = 0;
+    std::vector<zb_exchange_rec> r;
     while (o < bytes) {
       uint64_t h[2];
       if (bytes - o < sizeof(h)) return fail(e, ZB_EINVAL, "malformed exchange batches");
       HIPCHECK(e, hipMemcpy(h, batches + o, sizeof(h), hipMemcpyDeviceToHost));
-      if (h[1] < ZB_XCHG_BATCH_HEADER + h[0] * sizeof(zb_exchange_rec) || h[1] > bytes - o || (h[1] & 7))
-        return fail(e, ZB_EINVAL, "malformed exchange batches");
+      if (!batch_header_ok(h, bytes - o)) return fail(e, ZB_EINVAL, "malformed exchange batches");
+      r.resize(h[0]);
+      if (h[0])
+        HIPCHECK(e, hipMemcpy(r.data(), batches + o + ZB_XCHG_BATCH_HEADER, h[0] * sizeof(zb_exchange_rec),
+                              hipMemcpyDeviceToHost));
+      if (!batch_records_ok(r.data(), h[0], h[1], kind, n_elems))
+        return fail(e, ZB_EINVAL, "malformed exchange batches: a record's variable bytes or element out of range");
       counts.push_back(h[0]);
       offs.push_back(o);
       o += h[1];
     }
-  } else if (!parse_batches(batches, bytes, counts, offs)) {
+  } else if (!parse_batches(batches, bytes, kind, n_elems, counts, offs)) {
     return fail(e, ZB_EINVAL, "malformed exchange batches");
   }
   rc = ensure_stores(e);
@@ -3257,8 +3306,8 @@ int zb_comm_pending(zb_engine* e, uint64_t global[2]) {
 
 // Collective on every rank, whatever happens locally: a rank whose local work fails still takes part in
 // both agreement steps (sending zero sizes and its status), so every rank returns the same error instead
-// of one rank leaving the collective and its peers blocking in ncclSend / ncclRecv. ZB_FAIL_EXCHANGE=<rank>
-// (tests) makes that rank's local step fail.
+// of one rank leaving the collective and its peers blocking in ncclSend / ncclRecv. In the guard-band test build
+// only (zb_checked.hpp), ZB_FAIL_EXCHANGE=<rank> makes that rank's local step fail.
 int zb_comm_exchange(zb_engine* e, int kind, uint64_t* received) {
   if (!e || !received || (kind != ZB_XCHG_OPEN && kind != ZB_XCHG_CORRELATE)) return ZB_EINVAL;
   if (!e->comm) return e->comm_broken ? fail(e, ZB_EDEVICE, "communicator aborted after an earlier failure") : ZB_EINVAL;
@@ -3268,8 +3317,10 @@ int zb_comm_exchange(zb_engine* e, int kind, uint64_t* received) {
   // 0. local: the outbox as one batch per target into the persistent send buffer
   uint64_t sb[64] = {}, sc[64] = {}, n = 0, total = 0;
   int local = ZB_OK;
+#ifdef ZB_CHECKED
   if (const char* f = std::getenv("ZB_FAIL_EXCHANGE"))  // (before the outbox is taken: a retry still has it)
     if (*f && atoi(f) == e->cfg.partition_id) local = fail(e, ZB_EDEVICE, "injected local failure (ZB_FAIL_EXCHANGE)");
+#endif
   if (local == ZB_OK) local = outbox_pack(e, kind, nullptr, 0, sb, sc, &n, &total);
   if (local == ZB_OK && n) local = grow_dev(e, &e->xsend, &e->xsend_cap, total);
   if (local == ZB_OK && n) local = outbox_pack(e, kind, e->xsend, e->xsend_cap, sb, sc, &n, &total);

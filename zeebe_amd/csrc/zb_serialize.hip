@@ -449,7 +449,7 @@ __global__ void __launch_bounds__(256) k_ser_size(SerParams P0) {
     const bool live = i < P0.count;
     // the value length the emitting kernel knew, else the encoder's dry run (reads the record and its payload)
     n[j] = (live && P0.vlen) ? P0.vlen[P0.start + i] : VLEN_UNKNOWN;
-    measure[j] = live && (n[j] == VLEN_UNKNOWN || P0.vlen_bad);  // (ZB_VLEN_CHECK: measure every record)
+    measure[j] = live && (n[j] == VLEN_UNKNOWN || P0.vlen_bad);  // (ZB_CFG_VLEN_CHECK: measure every record)
     any = any || measure[j];
     if (!live) n[j] = 0;
   }
@@ -462,7 +462,7 @@ __global__ void __launch_bounds__(256) k_ser_size(SerParams P0) {
       const int64_t pos = P.start + i;
       const zb_rec d = P.log[pos];
       // the fast encoder's records: the emit kernels' formula (element constant + key lengths + binary
-      // payload); every other record, and every record under ZB_VLEN_CHECK, by the encoder's dry run
+      // payload); every other record, and every record under ZB_CFG_VLEN_CHECK, by the encoder's dry run
       const uint32_t m = (P.vconst && !P.vlen_bad && fast_kind(d))
           ? (kind_vt(d.kind) == ZB_VT_JOB ? P.vconst[d.elem].job : P.vconst[d.elem].wf) + mp_int_len(d.inst_key) +
                 mp_int_len(d.scope_key) + mp_bin_len(*(const uint32_t*)(P.arena + (uint64_t)d.payload * 8))

@@ -191,7 +191,9 @@ struct TdLane {
   int64_t inst, kwf0;
   bool active;
 };
-__device__ __forceinline__ TdLane td_lane(const TrajParams& P, const TdTab& T, int64_t tile) {
+// need_ref: the CREATE payload's arena ref (the write pass reads the document); a class batch's payload lengths come
+// from k_cls_classify's per-instance array, so the size pass reads 4 bytes per instance and no descriptor
+__device__ __forceinline__ TdLane td_lane(const TrajParams& P, const TdTab& T, int64_t tile, bool need_ref) {
   TdLane t;
   t.inst = tile * TD_WG + threadIdx.x;
   t.active = t.inst < P.n;
@@ -206,8 +208,8 @@ __device__ __forceinline__ TdLane td_lane(const TrajParams& P, const TdTab& T, i
     for (int c = 0; c < CLS_MAX; c++) t.L.before[c] = c == 0 ? (uint32_t)t.inst : 0;
   }
   t.W = t.active ? P.wcount[t.cls] : 0;  // generations of the instance's class (rows beyond it are not its)
-  t.create_ref = P.log[P.log_base + t.inst].payload;
-  t.create_len = arena_len(P.arena, t.create_ref);
+  t.create_ref = (need_ref || !P.clen) ? P.log[P.log_base + t.inst].payload : 0u;
+  t.create_len = P.clen ? P.clen[t.inst] : arena_len(P.arena, t.create_ref);
   t.kwf0 = td_kbase(T, t.L, 0, 1);
   return t;
 }
@@ -230,7 +232,7 @@ __global__ void __launch_bounds__(TD_WG) k_tdrain_size(TDrainParams D) {
   uint64_t pay = 0;
   {
     const int64_t tile = blockIdx.x;
-    const TdLane L = td_lane(P, T, tile);
+    const TdLane L = td_lane(P, T, tile, false);
     const uint64_t wave = (uint64_t)tile * (TD_WG / 64) + (threadIdx.x >> 6);
     // Short form: when the wave's smallest key and position (its first lane's generation-0 bases, which every
     // later key of the wave exceeds) are >= 2^16 and the batch's largest is below 2^32, every key / position the
@@ -289,7 +291,7 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
   uint32_t bad = 0;
   {
     const int64_t tile = blockIdx.x;
-    const TdLane L = td_lane(P, T, tile);
+    const TdLane L = td_lane(P, T, tile, true);
     // the instance's CREATE payload document, read once: every record of a deferred batch carries it or a static blob
     const uint64_t* cdw = (const uint64_t*)(P.arena + (uint64_t)L.create_ref * 8);
     uint64_t cpre[SER_PRE];
@@ -395,7 +397,7 @@ __global__ void __launch_bounds__(256) k_tdrain_sum(TDrainParams D, int64_t npar
 // Decides, after the trace and the generation bases, whether the batch may stay deferred: every traced record
 // is a WORKFLOW_INSTANCE event or a JOB record other than CANCEL(ED) (the fast encoder's kinds and the value-
 // length formula's), no generation merges payloads (the records' payloads are the CREATE payload or static
-// blobs), and the host allows it (TrajParams.defer_ok: value segments deployed, ZB_TMPL_DEFER).
+// blobs), and the host allows it (TrajParams.defer_ok: value segments deployed, ZB_CFG_NO_DEFER).
 __global__ void __launch_bounds__(256) k_tmpl_decide(TrajParams P) {
   __shared__ uint32_t s_bad;
   TrajCtl* ctl = P.ctl;

@@ -1141,6 +1141,19 @@ __device__ __forceinline__ bool load_operand_k(const TrajParams& P, bool is_path
 // the container-key check) does not depend on the key, so each key's (count, first result) -- and whether the
 // scan is unsupported -- is what query_fast gives for that key alone. The first result of each key is decoded
 // where the walk reads it (the token load_operand reads), so the VM's path operands are register moves.
+// n <= 16 bytes at p (the LDS copy of a document, any alignment) as two little-endian words, the bytes past n zero:
+// five dword reads from the 4-aligned address below p and v_alignbyte, instead of a dependent read per byte
+// (reads up to 19 bytes past p: the slot's padding or the next slot, masked off)
+__device__ __forceinline__ void lds_words16(const uint8_t* p, uint32_t n, uint64_t& w0, uint64_t& w1) {
+  const uint32_t a = (uint32_t)(uintptr_t)p & 3;
+  const uint32_t* q = (const uint32_t*)(p - a);
+  const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
+  const uint64_t lo = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, a) | (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, a) << 32;
+  const uint64_t hi = (uint64_t)__builtin_amdgcn_alignbyte(d3, d2, a) | (uint64_t)__builtin_amdgcn_alignbyte(d4, d3, a) << 32;
+  w0 = n >= 8 ? lo : (lo & ((1ull << (8 * n)) - 1));
+  w1 = n >= 16 ? hi : (n <= 8 ? 0ull : (hi & ((1ull << (8 * (n - 8))) - 1)));
+}
+
 struct Extract {  // per condition key: its first result, decoded
   uint32_t meta[CLS_QMAX];  // result count (saturating at 255) | token type << 8 | boolean << 16
   uint32_t sp[CLS_QMAX];    // string / binary bytes: document offset | length << 16 (the LDS copy holds <= 96 bytes)
@@ -1165,9 +1178,14 @@ __device__ __forceinline__ void extract_fast(const TrajParams& P, const uint8_t*
     const uint32_t vend = (v.type == TT_MAP || v.type == TT_ARRAY) ? skip_value(d, n, pos) : pos + v.total;
     if (vend == 0xffffffffu) { x.ok = false; return; }
     if (k.type == TT_STRING) {
+      // the key's bytes as two words (keys of at most 16 bytes; longer ones byte by byte against the pool)
+      uint64_t kw0 = 0, kw1 = 0;
+      if (k.len <= 16) lds_words16(d + kpos + k.hdr, k.len, kw0, kw1);
 #pragma unroll
       for (int j = 0; j < CLS_QMAX; j++) {
-        if (j < P.cls_nq && k.len == P.cls_key_len[j] && bytes_eq(d + kpos + k.hdr, P.pool + P.cls_key_off[j], k.len)) {
+        if (j < P.cls_nq && k.len == P.cls_key_len[j] &&
+            (k.len <= 16 ? (kw0 == P.cls_key_w[j][0] && kw1 == P.cls_key_w[j][1])
+                         : bytes_eq(d + kpos + k.hdr, P.pool + P.cls_key_off[j], k.len))) {
           const uint32_t c = x.meta[j] & 255;
           if (c == 0) {
             x.meta[j] = (uint32_t)v.type << 8 | (v.bval ? 1u : 0u) << 16;
@@ -1212,6 +1230,18 @@ __device__ __forceinline__ bool load_operand_x(const TrajParams& P, bool is_path
   return true;
 }
 
+// a string operand's bytes (<= 16) as two words: a path operand from the document's LDS copy, a constant from the
+// deploy-time table
+__device__ __forceinline__ void str_words(const TrajParams& P, bool is_path, uint32_t idx, const Operand& o,
+                                          uint64_t& w0, uint64_t& w1) {
+  if (is_path) {
+    lds_words16(o.s, o.slen, w0, w1);
+  } else {
+    w0 = K(P.const_w)[2 * (uint64_t)idx];
+    w1 = K(P.const_w)[2 * (uint64_t)idx + 1];
+  }
+}
+
 // The json-el VM (eval_condition, zb_devlib.hpp) as one wave-uniform sweep over the program: every lane
 // runs the same program and its jumps only go forward (zb_model.cpp emit), so instruction pc is
 // fetched once per wave through the scalar cache and executed by the lanes whose own pc is there.
@@ -1250,7 +1280,16 @@ __device__ __forceinline__ bool eval_condition_sweep(const TrajParams& P, uint32
       else {
         if (!same_type(x, y, out)) { done = true; continue; }
         switch (x.type) {
-          case TT_STRING: eq = x.slen == y.slen && bytes_eq(x.s, y.s, x.slen); break;
+          case TT_STRING:
+            if (EXT && x.slen == y.slen && x.slen <= 16) {  // as words: a path operand's bytes from the LDS document,
+              uint64_t a0, a1, b0, b1;                       // a constant's precomputed
+              str_words(P, (w0 >> 12) & 1, w1 & 0xffff, x, a0, a1);
+              str_words(P, (w0 >> 13) & 1, w1 >> 16, y, b0, b1);
+              eq = a0 == b0 && a1 == b1;
+            } else {
+              eq = x.slen == y.slen && bytes_eq(x.s, y.s, x.slen);
+            }
+            break;
           case TT_BOOLEAN: eq = x.bval == y.bval; break;
           case TT_INTEGER: eq = x.ival == y.ival; break;
           case TT_FLOAT: eq = x.fval == y.fval; break;
@@ -1325,6 +1364,7 @@ __global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
       for (int k = 0; k < P.nsplits; k++) key += (elem_ctl(P, P.split_elem[k]).cond_count() + 1) * P.split_stride[k];
     }
     P.ikey[i] = (uint8_t)key;
+    P.clen[i] = len;  // (the template drain's size pass reads 4 bytes per instance instead of two dependent loads)
     mkey = key & 255;
     mlen = len;
   }
@@ -1673,7 +1713,7 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
 // masked). In generation w the wave's 64 instances own ONE contiguous log range (pos0(i + 1) = pos0(i) +
 // records of i), so each lane stages its descriptors / source deltas / value lengths in the wave's slice of
 // the merge workspace and the wave writes the range out with whole-line 16-byte stores. The class-uniform
-// emit (k_tmpl<true>, ZB_TMPL_IO=0) wrote each record from its own lane: a wave's lanes sit among the
+// emit (k_tmpl<true>, class-uniform order) wrote each record from its own lane: a wave's lanes sit among the
 // other classes' instances, every store instruction touched ~64 partly written lines, and the L2 write
 // requests, not HBM, bounded the launch (profiles/r02/tmpl_store_exp.txt).
 template <bool GEN>

@@ -1267,6 +1267,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
   __shared__ uint64_t s_ex[LB_FIELDS];   // the tile's exclusive prefix
   __shared__ uint64_t s_tot[LB_FIELDS];  // and its inclusive prefix (the chunk totals on the last tile)
   __shared__ uint32_t s_agg[LB_FIELDS];  // the tile's aggregate
+  __shared__ int s_void;                 // the look-back timed out: the tile's prefix is unknown, nothing is emitted
   const WaveHdr* hin = P.hdr + (P.wave & 1);
   WaveHdr* hout = P.hdr + ((P.wave + 1) & 1);
   const Chunk c = wave_chunk(P, hin);
@@ -1395,6 +1396,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
         __hip_atomic_store(lb + lane, ((uint64_t)(tile == 0 ? tag_inc : tag_agg) << 32) | my_agg, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       uint64_t acc = 0;  // lanes < 12: exclusive prefix of field `lane`
+      if (lane == 0) s_void = 0;
       if (tile > 0) {
         bool timeout = false;
         const uint64_t t_start = wall_clock64();
@@ -1441,7 +1443,10 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
           if (first < 5) break;
           p -= 5;
         }
-        if (__ballot(timeout) && lane == 0) atomicOr(P.err, (uint32_t)DE_TIMEOUT);  // the others stop waiting too
+        if (__ballot(timeout) && lane == 0) {
+          atomicOr(P.err, (uint32_t)DE_TIMEOUT);  // the others stop waiting too
+          s_void = 1;  // (the host fails the wave: no record, row or blob is written from a partial prefix)
+        }
       }
       // bytes travel as two 32-bit granules (fields 4, 5): recombine the carry
       const uint64_t ex_lo = __shfl(acc, 4, 64), ex_hi = __shfl(acc, 5, 64);
@@ -1488,7 +1493,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
     // ---- emit (k_emit) straight from the LDS slots
     const uint64_t we = w;
     const int ns = (int)(we & 7);
-    if (r < c.end && (ns || ((we >> CW_NEXP) & 63) || ((we >> CW_DETAIL) & 1))) {
+    if (!s_void && r < c.end && (ns || ((we >> CW_NEXP) & 63) || ((we >> CW_DETAIL) & 1))) {
       const uint64_t out_rec = (uint64_t)end + s_ex[0] + (a & 0xffff);
       const uint64_t wf0 = s_ex[1] + ((a >> 16) & 0xffff);
       const uint64_t job0 = s_ex[2] + ((a >> 32) & 0xffff);

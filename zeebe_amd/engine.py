@@ -20,6 +20,14 @@ if os.environ.get("ZB_CHECKED_LIBRARY") == "1":
 CFG_WAVE_ONLY = 1  # zb_config.flags: never take the trajectory path
 CFG_EXTERNAL_JOBS = 2  # zb_config.flags: no canonical job harness (job events come through zb_submit)
 CFG_JOB_PROCESSOR = 4  # zb_config.flags: the job stream processor runs on the GPU (job commands through zb_submit)
+# diagnostic / measurement flags (include/zb_engine.h; the defaults are the product configuration)
+CFG_VLEN_CHECK = 8  # the drain's size pass checks every value-length hint against the encoder
+CFG_GENERIC_DRAIN = 16  # every drain tile through the generic encoder (the reference pass of the fast ones)
+CFG_NO_DEFER = 32  # trajectory batches write their descriptors in zb_step (no template drain)
+CFG_INSTANCE_ORDER = 64  # class batches emitted in instance order even when not deferred
+CFG_WAVE_EVENTS = 128  # timing events around every wave's kernels
+CFG_WAVE_SPLIT = 256  # three-kernel wave pipeline instead of the fused k_wave
+CFG_SINGLE_PASS_DRAIN = 512  # one-pass (look-back) value drain
 
 ZB_OK, ZB_EINVAL, ZB_ENOMEM, ZB_EUNSUPPORTED, ZB_EDEPLOY, ZB_EDEVICE, ZB_EAGAIN, ZB_EPROCESSING = \
     0, -1, -2, -3, -4, -5, -6, -7
@@ -213,9 +221,10 @@ class Engine:
     def __init__(self, device: int = 0, partition_id: int = 0, partition_count: int = 1,
                  log_capacity: int = 1 << 22, row_capacity: int = 1 << 20, arena_bytes: int = 64 << 20,
                  wave_records: int = 0, wave_only: bool = False, external_jobs: bool = False,
-                 job_processor: bool = False):
+                 job_processor: bool = False, flags: int = 0):
+        """flags: further zb_config.flags bits (the CFG_* diagnostic / measurement flags above)."""
         self._L = lib()
-        flags = (CFG_WAVE_ONLY if wave_only else 0) | (CFG_EXTERNAL_JOBS if external_jobs else 0) | \
+        flags = int(flags) | (CFG_WAVE_ONLY if wave_only else 0) | (CFG_EXTERNAL_JOBS if external_jobs else 0) | \
             (CFG_JOB_PROCESSOR if job_processor else 0)
         external_jobs = external_jobs or job_processor
         cfg = zb_config(device, partition_id, partition_count, flags, log_capacity, row_capacity, arena_bytes,
