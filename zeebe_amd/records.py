@@ -156,3 +156,22 @@ def parse_frames(buf) -> list:
                         rejection_type=rj, rejection_reason=reason, value=value))
         off += (framed + FRAME_ALIGNMENT - 1) & ~(FRAME_ALIGNMENT - 1)
     return out
+
+
+def build_frame(f: dict) -> bytes:
+    """The inverse of parse_frames for one record (fields as parse_frames returns them; framed_length and
+    metadata_length are recomputed): what LogStreamBatchWriterImpl.writeEventsToBuffer (:222-268) writes into a
+    claimed fragment, padded to FRAME_ALIGNMENT."""
+    reason = bytes(f.get("rejection_reason", b""))
+    value = bytes(f["value"])
+    mlen = 8 + 34 + 2 + len(reason)
+    framed = _DF.size + _LE.size + mlen + len(value)
+    out = bytearray(_DF.pack(framed, 0, f.get("flags", 0), 0, f.get("stream_id", 0)))
+    out += _LE.pack(0, 0, f["position"], f.get("raft_term", 0), f["producer_id"], f["source_position"], f["key"],
+                    f.get("timestamp", 0), mlen, 0)
+    out += _SBE.pack(34, 200, 0, 1, f["record_type"], f.get("request_stream_id", -(1 << 31)), f.get("request_id", (1 << 64) - 1),
+                     f.get("subscription_id", (1 << 64) - 1), f.get("protocol_version", 1), f["value_type"],
+                     f["intent"], f.get("incident_key", (1 << 64) - 1), f.get("rejection_type", 255))
+    out += struct.pack("<H", len(reason)) + reason + value
+    out += b"\0" * (-len(out) % FRAME_ALIGNMENT)
+    return bytes(out)
