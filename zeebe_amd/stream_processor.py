@@ -215,6 +215,10 @@ class GpuStreamProcessor:
                 self.emap[base + k] = ev["position"]
             frames = R.parse_frames(self.engine.frames(base + n, end - base - n, **self.frame_cfg)) if end > base + n \
                 else []
+            for f in frames:  # a CORRELATE's key is its log position (positionAsKey, SubscriptionApiCommandMessageHandler
+                src = f["source_position"]  # .java:146): the engine gives it, and its follow-ups, its engine position
+                if f["value_type"] == R.VT_WIS and base <= src < base + n and f["key"] == src:
+                    f["key"] = tick[src - base]["key"]
             self.engine.release(end)  # (the frames are on the host; the device window moves on)
             self.ticks.append({"inputs": [ev["position"] for ev in tick], "engine_base": base, "outputs": len(frames)})
             out += frames
