@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="skip the extra C2 wave-only / C4 lines")
     ap.add_argument("--no-drain", action="store_true", help="device stepping only (not the contract's step)")
     ap.add_argument("--wave-only", action="store_true", help="force the general wave pipeline (no trajectory path)")
+    ap.add_argument("--steady", action="store_true",
+                    help="C2 steady state (bench_steady.py): live instances waiting on jobs, ticks of job completions, "
+                         "creates and cancels, external job processor")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on GPU 0 (multi-rank rehearsal on a one-GPU box; not a scaling run)")
     return ap.parse_args()
@@ -404,6 +407,8 @@ def main():
         return float(t.item())
 
     n = a.instances
+    if a.steady:
+        return run_steady_line(a, rank, world, local_rank, dist, barrier, reduce)
     tot = run_workload(a.config, n, a, rank, world, local_rank, barrier, a.steps, a.warmup, drain=not a.no_drain,
                        pcie=(rank == 0 and world == 1 and not a.no_drain))
     elapsed = tot["elapsed"]
@@ -460,6 +465,48 @@ def main():
         dist.destroy_process_group()
 
 
+def steady_line(t, steps, live):
+    return {"value": t["transitions"] / t["elapsed"], "ms_per_step": t["elapsed"] * 1e3 / steps,
+            "stepping_ms": t["step_s"] * 1e3 / steps, "drain_ms": t["drain_s"] * 1e3 / steps,
+            "completed_instances_per_s": t["completed"] / t["elapsed"],
+            "per_tick": {"input_records": t["inputs"] / steps, "job_completions": t["completions"] / steps,
+                         "creates": t["creates"] / steps, "cancels": t["cancels"] / steps,
+                         "records_written": t["written"] / steps, "transitions": t["transitions"] / steps,
+                         "merges": t["merges"] / steps},
+            "live_element_instances": t["live_rows"], "pending_jobs": t["pending_jobs"],
+            "compactions": t["compactions"],
+            "roofline": roofline(t, steps, "c2s", live), "workload": t["desc"]}
+
+
+def run_steady_line(a, rank, world, local_rank, dist, barrier, reduce):
+    import bench_steady
+
+    live = a.instances
+    t = bench_steady.run_steady(a, rank, world, local_rank, barrier, a.steps, a.warmup, live=live)
+    elapsed, all_tr, all_comp = t["elapsed"], t["transitions"], t["completed"]
+    if dist is not None:
+        elapsed = reduce(elapsed, dist.ReduceOp.MAX)
+        all_tr = reduce(all_tr, dist.ReduceOp.SUM)
+        all_comp = reduce(all_comp, dist.ReduceOp.SUM)
+    if rank == 0:
+        line = steady_line(t, a.steps, live)
+        out = {"metric": METRIC, "value": all_tr / elapsed, "unit": "transitions/s", "n_gpus": world,
+               "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed * 1e3 / a.steps,
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+               "data": "synthetic (C2 chain, steady-state job completion schedule, deterministic)",
+               "config": {"workload": t["desc"], "live_instances_per_gpu": live, "partitions": world,
+                          "parallelism": "partition-per-gpu",
+                          "timed_step": "lockstep waves of one tick to quiescence (staged input already in HBM) + "
+                                        "zb_serialize of every record the tick wrote"},
+               "completed_instances_per_s": all_comp / elapsed}
+        out.update({k: v for k, v in line.items() if k not in ("value", "ms_per_step", "workload")})
+        if world == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = bench_steady.cpu_baseline_steady(40_000, 20)
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def extras(a, barrier):
     """Shorter lines on the other single-GPU configurations (same step definition, 3 steps each)."""
     out = {}
@@ -476,6 +523,10 @@ def extras(a, barrier):
                            "stepping_ms": t["step_s"] * 1e3 / 3, "drain_ms": t["drain_s"] * 1e3 / 3,
                            "roofline": roofline(t, 3, "c3w", 10_000_000),
                            "workload": t["desc"] + " (general wave pipeline, no trajectory path)"}
+    import bench_steady
+
+    t = bench_steady.run_steady(a, 0, 1, 0, barrier, 3, 1, live=1_000_000)
+    out["c2_steady"] = steady_line(t, 3, 1_000_000)
     t = run_workload("c4", 1_000_000, a, 0, 1, 0, barrier, 3, 1)
     out["c4"] = {"value": t["transitions"] / t["elapsed"], "ms_per_step": t["elapsed"] * 1e3 / 3,
                  "stepping_ms": t["step_s"] * 1e3 / 3, "drain_ms": t["drain_s"] * 1e3 / 3,

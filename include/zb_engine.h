@@ -214,6 +214,10 @@ typedef struct zb_rec_desc {
 } zb_rec_desc;
 int zb_submit(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* values, size_t values_len);
 
+/* Uploads the staged input batch to the device now (zb_step does it otherwise): a caller overlaps the PCIe
+ * transfer of the next tick's input with the current tick's drain, and keeps it out of the tick. */
+int zb_upload_staged(zb_engine* e);
+
 /* ---- stepping ------------------------------------------------------------------------ */
 /* Injects staged input at the log tail and runs lockstep waves until quiescence (ZB_OK) or
  * max_waves (ZB_EAGAIN). stats may be NULL. */

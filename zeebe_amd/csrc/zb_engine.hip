@@ -287,7 +287,12 @@ struct zb_engine {
   uint64_t x_cap = 0;
   void* x_tmp = nullptr;
   size_t x_tmp_cap = 0;
-  DevVec<int64_t> d_lookup_keys, d_lookup_pos;
+  DevVec<int64_t> d_lookup_keys, d_lookup_pos;    // zb_submit lookups of the staged batch: key, staged index
+  uint64_t staged_nlook = 0;
+  int64_t *look_keys = nullptr, *look_idx = nullptr;  // sorted on the device by zb_step
+  uint64_t look_cap = 0;
+  void* look_tmp = nullptr;
+  size_t look_tmp_cap = 0;
   // drain buffers (zb_serialize), grown on demand and reused
   uint64_t dr_cap = 0, dr_val_cap = 0, dr_tmp_cap = 0;
   uint32_t* dr_len = nullptr;  // value lengths
@@ -1174,7 +1179,8 @@ void zb_engine_destroy(zb_engine* e) {
                 e->merge_jobs, e->merge_slow, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_clen, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
-                e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->need_children};
+                e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->need_children, e->look_keys, e->look_idx,
+                e->look_tmp};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->comm) (void)ncclCommDestroy(e->comm);
@@ -1458,7 +1464,40 @@ void begin_staging(zb_engine* e) {
   e->staged_uploaded = false;
 }
 
+// the staged batch on the device: descriptors, value lengths, arena bytes, and the (key, staged index) pairs of
+// the records that name an element instance (ElementInstanceIndex.getInstance), sorted by zb_step on the device
+int upload_staged(zb_engine* e) {
+  if (e->staged_uploaded) return ZB_OK;
+  HIPCHECK(e, e->d_staged.upload(e->staged, e->stream));
+  HIPCHECK(e, e->d_staged_vlen.upload(e->staged_vlen, e->stream));
+  HIPCHECK(e, e->d_staged_arena.upload(e->staged_arena, e->stream));
+  e->staged_nlook = 0;
+  if (!e->staged_only_creates) {  // (CREATE-only batches name no element instance)
+    std::vector<int64_t> lk, li;
+    for (size_t i = 0; i < e->staged_lookup.size(); i++)
+      if (e->staged_lookup[i] != INT64_MIN) {
+        lk.push_back(e->staged_lookup[i]);
+        li.push_back((int64_t)i);
+      }
+    if (!lk.empty()) {
+      HIPCHECK(e, e->d_lookup_keys.upload(lk, e->stream));
+      HIPCHECK(e, e->d_lookup_pos.upload(li, e->stream));
+      HIPCHECK(e, hipStreamSynchronize(e->stream));  // (the host vectors die here)
+    }
+    e->staged_nlook = lk.size();
+  }
+  e->staged_uploaded = true;
+  return ZB_OK;
+}
+
 extern "C" {
+
+int zb_upload_staged(zb_engine* e) {
+  if (!e) return ZB_EINVAL;
+  if (!e->staged_pending || e->staged.empty()) return ZB_OK;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  return upload_staged(e);
+}
 
 int zb_submit_creates(zb_engine* e, const char* pid, int32_t version, int64_t workflow_key, size_t n,
                       const uint8_t* payloads, const uint64_t* offsets) {
@@ -1979,11 +2018,9 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
       return fail(e, ZB_ENOMEM, "log capacity (release drained records with zb_log_release)");
     if ((uint64_t)e->host_hdr.arena_next + e->staged_arena.size() > e->cfg.arena_bytes)
       return fail(e, ZB_ENOMEM, "arena capacity");
-    if (!e->staged_uploaded) {
-      HIPCHECK(e, e->d_staged.upload(e->staged, e->stream));
-      HIPCHECK(e, e->d_staged_vlen.upload(e->staged_vlen, e->stream));
-      HIPCHECK(e, e->d_staged_arena.upload(e->staged_arena, e->stream));
-      e->staged_uploaded = true;
+    {
+      const int urc = upload_staged(e);  // (already done by zb_upload_staged, or by an earlier step of a kept batch)
+      if (urc != ZB_OK) return urc;
     }
     InjectParams ip;
     ip.log = e->log;
@@ -1999,23 +2036,43 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     ip.arena_base = (uint64_t)e->host_hdr.arena_next;
     ip.staged_bytes = e->staged_arena.size();
     launch_inject(ip, e->stream);
-    // records naming an element instance by key: its row (ElementInstanceIndex.getInstance)
-    std::vector<std::pair<int64_t, int64_t>> look;
-    if (!e->staged_only_creates)  // (CREATE-only batches name no element instance: skip the scan)
-      for (int64_t i = 0; i < n; i++)
-        if (e->staged_lookup[i] != INT64_MIN) look.emplace_back(e->staged_lookup[i], ip.log_base + i);
-    if (!look.empty()) {
-      std::sort(look.begin(), look.end());
-      std::vector<int64_t> lk(look.size()), lp(look.size());
-      for (size_t i = 0; i < look.size(); i++) { lk[i] = look[i].first; lp[i] = look[i].second; }
-      HIPCHECK(e, e->d_lookup_keys.upload(lk, e->stream));
-      HIPCHECK(e, e->d_lookup_pos.upload(lp, e->stream));
+    // records naming an element instance by key: its row (ElementInstanceIndex.getInstance); the (key, index)
+    // pairs were uploaded with the batch and are sorted here, on the device
+    if (e->staged_nlook) {
+      const uint64_t m = e->staged_nlook;
+      if (m > (uint64_t)INT32_MAX) return fail(e, ZB_EUNSUPPORTED, "more than 2^31 staged lookups");
+      if (m > e->look_cap) {
+        HIPCHECK(e, hipStreamSynchronize(e->stream));
+        if (e->look_keys) (void)hipFree(e->look_keys);
+        if (e->look_idx) (void)hipFree(e->look_idx);
+        e->look_keys = e->look_idx = nullptr;
+        e->look_cap = 0;
+        const uint64_t c = std::max<uint64_t>(m + m / 4, 1024);
+        HIPCHECK(e, hipMalloc(&e->look_keys, c * sizeof(int64_t)));
+        HIPCHECK(e, hipMalloc(&e->look_idx, c * sizeof(int64_t)));
+        e->look_cap = c;
+      }
+      size_t tmp = 0;
+      if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, e->d_lookup_keys.p, e->look_keys, e->d_lookup_pos.p,
+                                             e->look_idx, (int)m, 0, 64, e->stream) != hipSuccess)
+        return fail(e, ZB_EDEVICE, "lookup sort sizing");
+      if (tmp > e->look_tmp_cap) {
+        HIPCHECK(e, hipStreamSynchronize(e->stream));
+        if (e->look_tmp) (void)hipFree(e->look_tmp);
+        e->look_tmp = nullptr;
+        e->look_tmp_cap = 0;
+        HIPCHECK(e, hipMalloc(&e->look_tmp, tmp + 16));
+        e->look_tmp_cap = tmp;
+      }
+      tmp = e->look_tmp_cap;
+      if (hipcub::DeviceRadixSort::SortPairs(e->look_tmp, tmp, e->d_lookup_keys.p, e->look_keys, e->d_lookup_pos.p,
+                                             e->look_idx, (int)m, 0, 64, e->stream) != hipSuccess)
+        return fail(e, ZB_EDEVICE, "lookup sort");
       ResolveParams rp{};
       rp.rmeta = e->rmeta; rp.rkeys = e->rkeys; rp.rows = (uint64_t)e->host_hdr.rows_next;
-      rp.keys = e->d_lookup_keys.p; rp.pos = e->d_lookup_pos.p; rp.n = (int64_t)look.size();
+      rp.keys = e->look_keys; rp.pos = e->look_idx; rp.pos_base = ip.log_base; rp.n = (int64_t)m;
       rp.links = e->links;
       launch_resolve(rp, e->stream);
-      HIPCHECK(e, hipStreamSynchronize(e->stream));  // the host vectors die at scope end
     }
     if (e->staged_has_cancel) e->term = true;
     for (const auto& q : e->staged_reqs) e->reqs.push_back(ReqMeta{ip.log_base + q.idx, q.rid, q.sid, 0});
@@ -2862,7 +2919,7 @@ int deliver(zb_engine* e, int kind, const uint8_t* buf, const std::vector<uint64
       return fail(e, ZB_EDEVICE, "inbox sort");
     ResolveParams rp{};
     rp.rmeta = e->rmeta; rp.rkeys = e->rkeys; rp.rows = (uint64_t)e->host_hdr.rows_next;
-    rp.keys = e->x_keys2; rp.pos = e->x_pos2; rp.n = (int64_t)n;
+    rp.keys = e->x_keys2; rp.pos = e->x_pos2; rp.pos_base = 0; rp.n = (int64_t)n;
     rp.links = e->links;
     launch_resolve(rp, e->stream);
     e->host_hdr.end = base + (int64_t)recs;

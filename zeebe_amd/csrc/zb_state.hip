@@ -26,7 +26,7 @@ __global__ void __launch_bounds__(256) k_resolve(ResolveParams P) {
       else hi = mid;
     }
     for (int64_t i = lo; i < P.n && P.keys[i] == key; i++) {
-      uint32_t* link = (uint32_t*)(P.links + P.pos[i]);
+      uint32_t* link = (uint32_t*)(P.links + P.pos_base + P.pos[i]);
       link[0] = (uint32_t)r;  // row-self half
     }
   }

@@ -117,6 +117,11 @@ class Record(NamedTuple):
 
 
 _INST = struct.Struct("<qqqB3xI")  # zb_read_instances record header
+# zb_rec_desc / zb_record_header as numpy records (submit_packed, bulk drains)
+DESC_DTYPE = [("key", "<i8"), ("record_type", "u1"), ("value_type", "u1"), ("intent", "u1"), ("pad", "u1"),
+              ("value_length", "<u4"), ("value_offset", "<u8")]
+HEADER_DTYPE = [("key", "<i8"), ("record_type", "u1"), ("value_type", "u1"), ("intent", "u1"),
+                ("rejection_type", "u1"), ("value_length", "<u4"), ("value_offset", "<u8")]
 
 _lib = None
 
@@ -139,6 +144,7 @@ def lib():
         L.zb_submit_creates.argtypes = [vp, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t,
                                         ctypes.c_void_p, ctypes.c_void_p]
         L.zb_step.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(zb_step_stats)]
+        L.zb_upload_staged.argtypes = [vp]
         L.zb_log_size.restype = ctypes.c_int64
         L.zb_log_size.argtypes = [vp]
         L.zb_read_descriptors.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
@@ -193,7 +199,7 @@ EXPORTED_SYMBOLS = ["zb_engine_create", "zb_engine_destroy", "zb_last_error", "z
                     "zb_validate_deployment", "zb_serialize", "zb_drain_copy", "zb_pinned_alloc", "zb_pinned_free",
                     "zb_serialize_frames", "zb_set_request_metadata", "zb_read_source_positions",
                     "zb_log_release", "zb_compact", "zb_read_memory_stats", "zb_submit_messages", "zb_set_clock",
-                    "zb_expire_messages", "zb_rccl_library"]
+                    "zb_expire_messages", "zb_rccl_library", "zb_upload_staged"]
 
 
 def checked_violations():
@@ -295,6 +301,19 @@ class Engine:
             blob += value
         buf = ctypes.create_string_buffer(bytes(blob), max(len(blob), 1))
         self._check(self._L.zb_submit(self._h, arr, n, buf, len(blob)))
+
+    def submit_packed(self, descs, values: bytes):
+        """zb_submit over prepared arrays: descs a numpy array of zb_rec_desc records (DESC_DTYPE), values the
+        concatenated value bytes they index."""
+        import numpy as np
+
+        descs = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
+        buf = ctypes.create_string_buffer(bytes(values), max(len(values), 1))
+        self._check(self._L.zb_submit(self._h, descs.ctypes.data, len(descs), buf, len(values)))
+
+    def upload_staged(self):
+        """zb_upload_staged: the staged input batch to the device now (not inside the next zb_step)."""
+        self._check(self._L.zb_upload_staged(self._h))
 
     def set_job_processor(self, on: bool):
         """The job stream processor is fixed at creation (job_processor=...): only checks it matches."""
