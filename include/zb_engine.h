@@ -198,10 +198,12 @@ int zb_submit_creates(zb_engine* e, const char* bpmn_process_id, int32_t version
  *   COMMAND WORKFLOW_INSTANCE UPDATE_PAYLOAD  (UpdatePayloadProcessor :557-576)
  *   EVENT   JOB CREATED / COMPLETED           (JobCreatedProcessor :408-426, JobCompletedEventProcessor :428-453)
  *   COMMAND WORKFLOW_INSTANCE_SUBSCRIPTION CORRELATE (:455-509; its key becomes its log position)
- * A tick's records must not race inside one lockstep wave: per workflow instance at most one CANCEL /
- * UPDATE_PAYLOAD and then nothing else, per activity instance at most one record, except a JOB CREATED
- * directly followed by its JOB COMPLETED; anything else returns ZB_EUNSUPPORTED (split the tick:
- * zb_step, then submit the rest). Records other than CREATE are injected only into a quiescent
+ * Any order is accepted, as the reference's processor accepts it: records of one workflow instance that would
+ * race inside one lockstep wave (a CANCEL or UPDATE_PAYLOAD next to other records of its instance, two records
+ * of one activity instance other than a JOB CREATED directly followed by its JOB COMPLETED, a job's commands
+ * that are not two consecutive ones) make the instance a conflicting one for the tick, and zb_step cuts every
+ * generation of the tick before the next record of such an instance, so each is processed after the ones before
+ * it in log order, as the reference does. Records other than CREATE are injected only into a quiescent
  * partition. All-or-nothing: on error nothing is staged. */
 typedef struct zb_rec_desc {
   int64_t key;            /* record key (-1 = null) */

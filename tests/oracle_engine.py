@@ -2,33 +2,16 @@
 controller_sim.py), so that the stream-processor protocol (zeebe_amd/stream_processor.py) runs without a GPU.
 
 It is the oracle (oracle/zbref.cpp, the sequential restatement of the reference) behind the engine's interface:
-a tick's staged records are submitted and run to quiescence; the per-tick race rules of zb_submit
-(zeebe_amd/csrc/zb_engine.hip, "race rules of one tick"; include/zb_engine.h) are restated so that ticks split
-where the GPU engine splits them; snapshot / restore replay the tick history into a fresh oracle. Never product
-code: the GPU variant of the same tests runs the real engine.
+a tick's staged records are submitted and run to quiescence (like zb_submit, it takes records of one instance that
+race in any order: the engine serialises them, the oracle is sequential anyway); snapshot / restore replay the tick
+history into a fresh oracle. Never product code: the GPU variant of the same tests runs the real engine.
 """
 from __future__ import annotations
 
 import base64
 import json
 
-import msgpack
-
 from oracle import zbref
-from zeebe_amd import records as R
-from zeebe_amd.engine import ZB_EUNSUPPORTED, ZbError
-
-
-def _race_keys(rec):
-    """(workflow instance, activity instance, scope command) of a non-CREATE record, as zb_submit decodes them."""
-    rt, vt, it, key, value = rec
-    v = msgpack.unpackb(value, raw=False) if value else {}
-    if vt == R.VT_WORKFLOW_INSTANCE and rt == R.RT_COMMAND:
-        return (key if it == R.WI_CANCEL else v.get("workflowInstanceKey", -1)), None, True
-    if vt == R.VT_JOB:
-        h = v.get("headers", {})
-        return h.get("workflowInstanceKey", -1), h.get("activityInstanceKey", -1), False
-    return v.get("workflowInstanceKey", -1), v.get("activityInstanceKey", -1), False  # CORRELATE
 
 
 class OracleEngine:
@@ -44,25 +27,9 @@ class OracleEngine:
         for xml, k in self.deployments:
             self.o.deploy(xml, k, 1)
         self.staged = []
-        self.inst, self.aiks = {}, set()
 
     def submit_records(self, recs):
         for rec in recs:
-            rt, vt, it, key, value = rec
-            if not (vt == R.VT_WORKFLOW_INSTANCE and rt == R.RT_COMMAND and it == R.WI_CREATE):
-                prev = self.staged[-1][0] if self.staged else None
-                pair = (vt == R.VT_JOB and it == R.JI_COMPLETED and prev is not None and prev[1] == R.VT_JOB and
-                        prev[2] == R.JI_CREATED and prev[3] == key and _race_keys(prev)[1] == _race_keys(rec)[1])
-                if not pair:
-                    inst, aik, scope = _race_keys(rec)
-                    f = self.inst.get(inst, 0)
-                    if (f & 1) or (scope and f):
-                        raise ZbError(ZB_EUNSUPPORTED, "workflow instance %d races in this tick" % inst)
-                    if aik is not None and aik in self.aiks:
-                        raise ZbError(ZB_EUNSUPPORTED, "activity instance %d races in this tick" % aik)
-                    self.inst[inst] = f | (1 if scope else 2)
-                    if aik is not None:
-                        self.aiks.add(aik)
             self.staged.append([rec, None, None])
 
     def set_request_metadata(self, rids, sids):
@@ -80,7 +47,6 @@ class OracleEngine:
 
     def step(self):
         tick, self.staged = self.staged, []
-        self.inst, self.aiks = {}, set()
         self._run_tick(tick)
         self.history.append(tick)
         return {"quiescent": True}

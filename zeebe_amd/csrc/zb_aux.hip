@@ -155,7 +155,7 @@ __global__ void __launch_bounds__(256) k_cond(WaveParams P) {
 __global__ void __launch_bounds__(256) k_map(WaveParams P) {
   WaveHdr* hin = P.hdr + (P.wave & 1);
   const int64_t b = hin->begin, g = hin->gen_end;
-  const int64_t cend = (g - b > (int64_t)P.wave_cap) ? b + (int64_t)P.wave_cap : g;
+  const int64_t cend = chunk_end(P, b, g);
   const int64_t lim = cend + 3 < g ? cend + 3 : g;  // a batch's tail may lie past the chunk end
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   MNode* ws = P.map_ws + tid * MAP_NODES;

@@ -267,6 +267,11 @@ struct zb_engine {
   std::unordered_map<int64_t, uint8_t> tick_inst;  // workflow instance -> 1: scope command, 2: other records
   std::unordered_set<int64_t> tick_aik;
   std::unordered_set<int64_t> tick_jobs;   // job keys with commands in the staged tick (one group each)
+  std::unordered_set<int64_t> tick_conflicts;  // workflow instances whose staged records race (serialised by chunks)
+  DevVec<int64_t> d_conf_keys;             // their open-addressing table (uploaded with the batch)
+  int64_t* conf_first = nullptr;           // [conf_cap] + conf_split
+  uint64_t conf_cap = 0, conf_mask = 0, staged_conf = 0;
+  bool conf_active = false;                // the injected tick has conflicting instances: k_conflict every wave
   JobTable jobs{};                         // ZB_CFG_JOB_PROCESSOR: job states by job key (open addressing)
   // compaction (zb_compact.hip): scratch grown on demand, lifetime totals
   uint32_t *c_flag = nullptr, *c_new = nullptr;  // scan input / output (live rows, live messages)
@@ -484,6 +489,11 @@ WaveParams wave_params(zb_engine* e) {
   p.term = e->term ? 1 : 0;
   p.epoch = e->epoch;
   p.need_children = e->need_children;
+  p.conflicts = e->conf_active ? 1 : 0;
+  p.conf_keys = e->d_conf_keys.p;
+  p.conf_first = e->conf_first;
+  p.conf_split = e->conf_first ? e->conf_first + e->conf_cap : nullptr;
+  p.conf_mask = e->conf_mask;
   // about four 256-record tiles per workgroup for the generation last seen by the host, 256..1024 workgroups
   // (C2 wave-only, 1M records per wave: 1024 workgroups 32.5 ms/step, 2048 33.0, 512 34.3, one tile per
   // workgroup 44.6 -- per-workgroup fixed costs; profiles/r02/grid_sweep.txt); a generation that grows inside
@@ -1180,7 +1190,7 @@ void zb_engine_destroy(zb_engine* e) {
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_clen, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
                 e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->need_children, e->look_keys, e->look_idx,
-                e->look_tmp};
+                e->look_tmp, e->conf_first};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->comm) (void)ncclCommDestroy(e->comm);
@@ -1266,6 +1276,7 @@ int zb_reset(zb_engine* e, int keep_staged) {
     e->staged_uploaded = false;
   }
   e->term = false;
+  e->conf_active = false;
   e->staged_pending = !e->staged.empty();
   e->sub_count = e->msg_count = 0;
   e->msg_key_next = 0;
@@ -1461,6 +1472,7 @@ void begin_staging(zb_engine* e) {
   e->tick_inst.clear();
   e->tick_aik.clear();
   e->tick_jobs.clear();
+  e->tick_conflicts.clear();
   e->staged_uploaded = false;
 }
 
@@ -1485,6 +1497,27 @@ int upload_staged(zb_engine* e) {
       HIPCHECK(e, hipStreamSynchronize(e->stream));  // (the host vectors die here)
     }
     e->staged_nlook = lk.size();
+  }
+  e->staged_conf = e->tick_conflicts.size();
+  if (e->staged_conf) {  // open addressing at load <= 1/2
+    uint64_t cap = 64;
+    while (cap < 2 * e->staged_conf) cap <<= 1;
+    std::vector<int64_t> tab(cap, INT64_MIN);
+    for (int64_t k : e->tick_conflicts) {
+      uint64_t h = ((uint64_t)k * 0x9E3779B97F4A7C15ull >> 32) & (cap - 1);
+      while (tab[h] != INT64_MIN) h = (h + 1) & (cap - 1);
+      tab[h] = k;
+    }
+    HIPCHECK(e, e->d_conf_keys.upload(tab, e->stream));
+    if (cap > e->conf_cap) {
+      HIPCHECK(e, hipStreamSynchronize(e->stream));
+      if (e->conf_first) (void)hipFree(e->conf_first);
+      e->conf_first = nullptr;
+      HIPCHECK(e, hipMalloc(&e->conf_first, (cap + 1) * sizeof(int64_t)));
+      e->conf_cap = cap;
+    }
+    e->conf_mask = cap - 1;
+    HIPCHECK(e, hipStreamSynchronize(e->stream));  // (the host table dies here)
   }
   e->staged_uploaded = true;
   return ZB_OK;
@@ -1866,7 +1899,9 @@ int zb_submit(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* va
       p.cancel = it == WI_CANCEL;
       p.lookup = p.cancel ? r.key : dv.wik;
       p.inst = p.lookup;
-      d.inst_key = dv.wik;
+      // (a CANCEL names its instance by the command key; its descriptor carries it for k_conflict -- the
+      // command's own value is written verbatim, so the descriptor's instance key is not serialized)
+      d.inst_key = p.cancel ? r.key : dv.wik;
       p.canon = reencode(vt, dv, p.doc, p.doc_len);
     } else if (job_cmd) {
       if (it == JI_CREATE && r.key >= 0)
@@ -1895,11 +1930,15 @@ int zb_submit(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* va
       p.canon = reencode(vt, dv, p.doc, p.doc_len);
     }
   }
-  // 2. race rules of one tick (include/zb_engine.h), against what is staged already
-  if (!e->staged_pending) { e->tick_inst.clear(); e->tick_aik.clear(); e->tick_jobs.clear(); }
+  // 2. races of one tick (include/zb_engine.h), against what is staged already: records of one workflow instance
+  // that a lockstep wave could not process as the reference's processor does -- one after the other, each seeing
+  // what the earlier ones did -- make the instance a conflicting one; zb_step then cuts every generation of the
+  // tick before the next record of such an instance (k_conflict), which restores that order for it.
+  if (!e->staged_pending) { e->tick_inst.clear(); e->tick_aik.clear(); e->tick_jobs.clear(); e->tick_conflicts.clear(); }
   std::unordered_map<int64_t, uint8_t> inst = e->staged_pending ? e->tick_inst : std::unordered_map<int64_t, uint8_t>();
   std::unordered_set<int64_t> aiks = e->staged_pending ? e->tick_aik : std::unordered_set<int64_t>();
   std::unordered_set<int64_t> tick_jobs = e->staged_pending ? e->tick_jobs : std::unordered_set<int64_t>();
+  std::unordered_set<int64_t> confl = e->staged_pending ? e->tick_conflicts : std::unordered_set<int64_t>();
   const zb_rec* prev_staged = (e->staged_pending && !e->staged.empty()) ? &e->staged.back() : nullptr;
   for (size_t i = 0; i < n; i++) {
     Prep& p = prep[i];
@@ -1912,37 +1951,20 @@ int zb_submit(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* va
       p.d.kind |= 0x40;
       continue;
     }
-    // a job's commands of one tick: consecutive ones form one group, processed in order by one thread
-    if (p.job_cmd) {
+    // a job's commands of one tick: two consecutive ones form one group, processed in order by one thread (a
+    // group's records share that thread's MAX_SLOTS (2) output slots); any other repeat is a conflict
+    if (p.job_cmd && p.d.key >= 0) {
       if (prev && kind_vt(prev->kind) == ZB_VT_JOB && kind_rt(prev->kind) == ZB_RT_COMMAND && prev->key == p.d.key &&
-          p.d.key >= 0) {
-        // a group's records share one thread's MAX_SLOTS (2) output slots, one per job command: two commands
-        // for a job per tick
-        const bool second = !(prev->kind & 0x40);
-        if (!second)
-          return fail(e, ZB_EUNSUPPORTED, "record " + std::to_string(i) + ": more than 2 commands for job " +
-                                              std::to_string(p.d.key) + " in one tick (split the tick)");
+          !(prev->kind & 0x40) && !confl.count(p.inst)) {
         p.d.kind |= 0x40;
         continue;
       }
-      if (p.d.key >= 0 && !tick_jobs.insert(p.d.key).second)
-        return fail(e, ZB_EUNSUPPORTED, "record " + std::to_string(i) + ": job " + std::to_string(p.d.key) +
-                                            " already has commands in this tick that are not next to this one "
-                                            "(submit a job's commands together, or split the tick)");
+      if (!tick_jobs.insert(p.d.key).second) confl.insert(p.inst);
     }
     uint8_t& f = inst[p.inst];
-    if ((f & 1) || (p.scope_cmd && f)) {
-      return fail(e, ZB_EUNSUPPORTED, "record " + std::to_string(i) + ": workflow instance " + std::to_string(p.inst) +
-                                          " already has a record in this tick next to a CANCEL / UPDATE_PAYLOAD "
-                                          "(split the tick: zb_step, then submit the rest)");
-    }
+    if ((f & 1) || (p.scope_cmd && f)) confl.insert(p.inst);
     f |= p.scope_cmd ? 1 : 2;
-    if (p.aik != INT64_MIN) {
-      if (aiks.count(p.aik))
-        return fail(e, ZB_EUNSUPPORTED, "record " + std::to_string(i) + ": activity instance " + std::to_string(p.aik) +
-                                            " already has a record in this tick (split the tick)");
-      aiks.insert(p.aik);
-    }
+    if (p.aik != INT64_MIN && !aiks.insert(p.aik).second) confl.insert(p.inst);
   }
   // 3. stage
   begin_staging(e);
@@ -1950,6 +1972,7 @@ int zb_submit(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* va
   e->tick_inst.swap(inst);
   e->tick_aik.swap(aiks);
   e->tick_jobs.swap(tick_jobs);
+  e->tick_conflicts.swap(confl);
   for (size_t i = 0; i < n; i++) {
     Prep& p = prep[i];
     // arena: [payload document][verbatim value] (+ [document][re-encoded command value])
@@ -2075,6 +2098,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
       launch_resolve(rp, e->stream);
     }
     if (e->staged_has_cancel) e->term = true;
+    if (e->staged_conf) e->conf_active = true;  // (until the tick is quiescent)
     for (const auto& q : e->staged_reqs) e->reqs.push_back(ReqMeta{ip.log_base + q.idx, q.rid, q.sid, 0});
     for (auto& pr : e->pending_ranges) {
       CmdRange r{};
@@ -2119,6 +2143,11 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
       WaveParams p = wave_params(e);
       hipEvent_t* ev = &e->ev[EV_PER_WAVE * i];
       if (per_wave) HIPCHECK(e, hipEventRecord(ev[0], e->stream));
+      if (p.conflicts) {  // the chunk ends before the next record of a conflicting instance
+        HIPCHECK(e, hipMemsetAsync(e->conf_first, 0x7f, (e->conf_mask + 1) * sizeof(int64_t), e->stream));
+        HIPCHECK(e, hipMemsetAsync(p.conf_split, 0x7f, sizeof(int64_t), e->stream));
+        launch_conflict(p, e->stream);
+      }
       if (p.has_parallel || p.term) {  // scope-wide counters / first-child requests of the chunk
         launch_pre(p, e->stream);
         if (p.term) launch_children(p, e->stream);
@@ -2191,6 +2220,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   if (stats) *stats = st;
   if (!quiescent) return ZB_EAGAIN;
   e->term = false;  // every termination chain has ended
+  e->conf_active = false;
   return ZB_OK;
 }
 

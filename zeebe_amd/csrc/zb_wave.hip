@@ -768,7 +768,7 @@ struct Chunk {
 };
 __device__ __forceinline__ Chunk wave_chunk(const WaveParams& P, const WaveHdr* h) {
   const int64_t b = h->begin, g = h->gen_end;
-  const int64_t e = (g - b > (int64_t)P.wave_cap) ? b + (int64_t)P.wave_cap : g;
+  const int64_t e = chunk_end(P, b, g);
   return Chunk{b, e, e - b};
 }
 // contiguous tile range of workgroup b (identical in k_process and k_emit)
@@ -1508,6 +1508,40 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
     }
     __syncthreads();  // LDS slots and scan scratch are reused by the next tile
   }
+}
+
+// ------------------------------------------------------------------------------ k_conflict
+// The chunk of a generation that holds records of conflicting instances (WaveParams.conf_*) ends at the first
+// record, in log order, of such an instance whose earlier record is in the generation's unprocessed range: two
+// passes over [begin, gen_end) (the first position of each instance, then the smallest later one). A batch's
+// continuation records are processed with their head, in order, by one thread: only heads count.
+__device__ __forceinline__ int64_t conf_slot(const WaveParams& P, int64_t key) {
+  if (key < 0) return -1;
+  uint64_t s = ((uint64_t)key * 0x9E3779B97F4A7C15ull >> 32) & P.conf_mask;
+  for (uint64_t n = 0; n <= P.conf_mask; n++, s = (s + 1) & P.conf_mask) {
+    const int64_t k = P.conf_keys[s];
+    if (k == key) return (int64_t)s;
+    if (k == INT64_MIN) return -1;
+  }
+  return -1;
+}
+template <bool SPLIT>
+__global__ void __launch_bounds__(256) k_conflict(WaveParams P) {
+  const WaveHdr* hin = P.hdr + (P.wave & 1);
+  const int64_t b = hin->begin, g = hin->gen_end;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t r = b + (int64_t)blockIdx.x * 256 + threadIdx.x; r < g; r += stride) {
+    const zb_rec rec = P.log[r];
+    if (grouped(rec)) continue;
+    const int64_t s = conf_slot(P, rec.inst_key);
+    if (s < 0) continue;
+    if (!SPLIT) atomicMin((unsigned long long*)(P.conf_first + s), (unsigned long long)r);
+    else if (r > P.conf_first[s]) atomicMin((unsigned long long*)P.conf_split, (unsigned long long)r);
+  }
+}
+void launch_conflict(const WaveParams& p, hipStream_t stream) {
+  hipLaunchKernelGGL((k_conflict<false>), dim3(512), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL((k_conflict<true>), dim3(512), dim3(256), 0, stream, p);
 }
 
 void launch_wave(const WaveParams& p, int grid, hipStream_t stream) {
