@@ -223,45 +223,48 @@ def _oracle_partition(cfg, n, start, tasks):
     return o
 
 
-def cpu_baseline_line(cfg, tasks, sample):
-    """The oracle (sequential C++ restatement of the reference path, same canonical schedule) on a bounded
-    sample of the same workload: 1 partition on 1 core, and P = min(8, cores) partitions on P cores (one
-    thread per partition, as the reference runs one stream processor per partition)."""
+def _partition_proc(cfg, per, i, tasks, barrier, q):
+    """One oracle partition in its own process (forked before the GPU is touched): built, warmed, run at the
+    barrier; reports (records, transitions, completed, instances, t0, t1)."""
     import ctypes
 
+    w = _oracle_partition(cfg, per, i * per, tasks)  # untimed warm-up: faults in the process's heap
+    w._L.zbref_run_timed(w._h, ctypes.byref(ctypes.c_int64()))
+    w.close()
+    o = _oracle_partition(cfg, per, i * per, tasks)
+    nrec = ctypes.c_int64()
+    barrier.wait()
+    t0 = time.perf_counter()
+    o._L.zbref_run_timed(o._h, ctypes.byref(nrec))
+    t1 = time.perf_counter()
+    c = o.counters()
+    q.put((nrec.value, c["transitions"], c["completed"], c["created"], t0, t1))
+
+
+def cpu_baseline_line(cfg, tasks, sample):
+    """The oracle (sequential C++ restatement of the reference path, same canonical schedule) on a bounded
+    sample of the same workload: 1 partition on 1 core, and P = min(8, cores) partitions on P cores, one process
+    per partition (the reference runs one stream processor per partition; a process each keeps the restatement's
+    allocations per partition, as a JVM's thread-local allocation buffers do -- threads sharing one C heap scaled
+    4.7x on 8 cores, processes scale with the cores). Run from a process forked before the GPU is
+    initialised (main)."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("fork")
     threads = min(8, os.cpu_count() or 1)
     res = {}
     for k in sorted({1, threads}):
         per = sample if k == 1 else max(sample // 2, 1)
-        parts = [None] * k
-        counts = [0] * k
-        ready = threading.Barrier(k + 1)
-
-        def run(i):
-            # each partition is built on its own thread, so its state lives in that thread's malloc arena (built
-            # on the main thread, every free from the workers went through the main arena's lock)
-            w = _oracle_partition(cfg, per, i * per, tasks)  # untimed warm-up: faults in the thread's arena
-            w._L.zbref_run_timed(w._h, ctypes.byref(ctypes.c_int64()))
-            w.close()
-            parts[i] = _oracle_partition(cfg, per, i * per, tasks)
-            ready.wait()
-            nrec = ctypes.c_int64()
-            parts[i]._L.zbref_run_timed(parts[i]._h, ctypes.byref(nrec))
-            counts[i] = nrec.value
-
-        ths = [threading.Thread(target=run, args=(i,)) for i in range(k)]
-        for t in ths:
-            t.start()
-        ready.wait()
-        t0 = time.perf_counter()
-        for t in ths:
-            t.join()
-        wall = time.perf_counter() - t0
-        cs = [p.counters() for p in parts]
-        res[k] = dict(instances=sum(c["created"] for c in cs), transitions=sum(c["transitions"] for c in cs),
-                      completed=sum(c["completed"] for c in cs), records=sum(counts), wall_s=wall)
-        for p in parts:
-            p.close()
+        barrier, q = ctx.Barrier(k), ctx.Queue()
+        ps = [ctx.Process(target=_partition_proc, args=(cfg, per, i, tasks, barrier, q)) for i in range(k)]
+        for p in ps:
+            p.start()
+        out = [q.get() for _ in ps]
+        for p in ps:
+            p.join()
+        wall = max(r[5] for r in out) - min(r[4] for r in out)
+        res[k] = dict(records=sum(r[0] for r in out), transitions=sum(r[1] for r in out),
+                      completed=sum(r[2] for r in out), instances=sum(r[3] for r in out), wall_s=wall)
     one, many = res[1], res[threads]
     return {"value": one["transitions"] / one["wall_s"], "unit": "transitions/s", "cores": 1, "kind": "port",
             "sample": "%s workload, %d instances (%d records processed) run to quiescence by oracle/zbref, 1 thread, "
@@ -272,8 +275,30 @@ def cpu_baseline_line(cfg, tasks, sample):
             "multi_partition": {"value": many["transitions"] / many["wall_s"], "cores": threads,
                                 "partitions": threads, "instances": many["instances"], "wall_s": many["wall_s"],
                                 "completed_instances_per_s": many["completed"] / many["wall_s"],
-                                "note": "one oracle partition per thread, run concurrently (SURVEY §8d: P partitions "
-                                        "on P cores, P = min(8, cores))"}}
+                                "scaling_vs_1": (many["transitions"] / many["wall_s"]) /
+                                                (one["transitions"] / one["wall_s"]),
+                                "note": "one oracle partition per process, run concurrently (SURVEY §8d: P "
+                                        "partitions on P cores, P = min(8, cores))"}}
+
+
+def cpu_baseline_early(a, rank, world):
+    """cpu_baseline_line in a child forked before anything touches the GPU (its partitions fork in turn)."""
+    if rank != 0 or world != 1 or a.no_cpu_baseline or a.config == "c5" or a.steady:
+        return None
+    import multiprocessing as mp
+
+    sample = a.cpu_sample or {"c1": 10_000, "c3": 400_000, "c2": 30_000, "c4": 20_000}[a.config]
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+
+    def run():
+        q.put(cpu_baseline_line(a.config, a.tasks, sample))
+
+    p = ctx.Process(target=run)
+    p.start()
+    r = q.get()
+    p.join()
+    return r
 
 
 # ------------------------------------------------------------------------------ roofline
@@ -374,6 +399,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.instances == 0:
+        a.instances = {"c3": 10_000_000, "c1": 10_000}.get(a.config, 1_000_000)
+    cpu_line = cpu_baseline_early(a, rank, world)  # (forks: before the GPU is initialised)
     # Load libzbgpu.so before torch: its DT_NEEDED HIP runtime and RCCL (/opt/rocm/lib) are then the copies the
     # process binds, so the engine's communicator runs on the system RCCL, not the one torch bundles
     # (zb_rccl_library reports the file; C5 prints it).
@@ -388,8 +416,6 @@ def main():
         # scaling, no data-path collective). gloo keeps torch's own HIP runtime out of the process: the engine
         # (libzbgpu.so) drives its GPU through the system ROCm runtime.
         dist.init_process_group("gloo")
-    if a.instances == 0:
-        a.instances = {"c3": 10_000_000, "c1": 10_000}.get(a.config, 1_000_000)
     if a.config == "c5":
         return run_c5(a, rank, world, local_rank, dist)
 
@@ -457,9 +483,8 @@ def main():
                                    "chunks); PCIe-inclusive rate, never `value` (task contract)"}
         if world == 1 and not a.no_extras and a.config == "c3":
             out["extras"] = extras(a, barrier)
-        if world == 1 and not a.no_cpu_baseline:
-            sample = a.cpu_sample or {"c1": 10_000, "c3": 400_000, "c2": 30_000, "c4": 20_000}[a.config]
-            out["cpu_baseline"] = cpu_baseline_line(a.config, a.tasks, sample)
+        if cpu_line is not None:
+            out["cpu_baseline"] = cpu_line
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
