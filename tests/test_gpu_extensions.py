@@ -285,10 +285,7 @@ def test_submit_validation():
     n0 = e.log_size()
     with pytest.raises(ZbError):  # no workflow processor for JOB ACTIVATED
         e.submit_records([(R.RT_EVENT, R.VT_JOB, R.JI_ACTIVATED, 2, R.job_record())])
-    with pytest.raises(ZbError):  # CANCEL and UPDATE_PAYLOAD of one instance in one tick
-        e.submit_records([(R.RT_COMMAND, R.VT_WORKFLOW_INSTANCE, R.WI_CANCEL, 1, b"\x80"),
-                          (R.RT_COMMAND, R.VT_WORKFLOW_INSTANCE, R.WI_UPDATE_PAYLOAD, 1,
-                           R.wf_record(workflow_instance_key=1))])
+    # (a CANCEL and an UPDATE_PAYLOAD of one instance in one tick are accepted and serialised: test_gpu_races.py)
     with pytest.raises(ZbError):  # malformed value
         e.submit_records([(R.RT_COMMAND, R.VT_WORKFLOW_INSTANCE, R.WI_CANCEL, 1, b"\x81\xa1")])
     # nothing was staged by the failed calls

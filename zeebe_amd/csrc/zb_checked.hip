@@ -130,6 +130,7 @@ void scan(State& S, const char* after) {
     log_line(m, true);
     const uint32_t r = (uint32_t)(bad >> 32);
     (void)hipMemset((void*)(uintptr_t)S.tab[3 * r], PAT, S.tab[3 * r + 1]);  // re-arm, look for more
+    (void)hipDeviceSynchronize();
   }
 }
 
@@ -145,6 +146,10 @@ hipError_t checked_malloc(void** p, size_t n, const char* what, const char* file
     return e;
   }
   e = hipMemset(raw, PAT, FRONT + n + BACK);  // (the buffer too: reads of never-written bytes see the pattern)
+  if (e != hipSuccess) return e;
+  // the fill runs on the null stream, which does not order against the engine's non-blocking stream: it must
+  // have completed before the caller queues anything that writes the buffer
+  e = hipDeviceSynchronize();
   if (e != hipSuccess) return e;
   *p = raw + FRONT;
   const char* base = std::strrchr(file, '/');
