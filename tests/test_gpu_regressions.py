@@ -1,0 +1,56 @@
+"""Regressions of device faults, each driven through the exact buffer sequence that produced it.
+
+Uninitialised CREATE rows (round-3 fault in test_many_ticks_through_small_capacities): a CREATE
+command allocates its instance's row in the wave that processes it, but the instance enters the index only when its
+CREATED event is processed, one wave later. k_children (the first-live-child lookup of a cancellation, zb_wave.hip)
+scans every allocated row, so when a CANCEL's TERMINATING is in the same wave as new CREATED events it read rows whose
+memory still held whatever was there before -- a compacted-away row, another engine's data -- and indexed raux[] with
+that garbage parent. The fault came and went with the allocator's layout. The guard-band build fills every fresh
+allocation with 0xA5, which turns such a read into a certain fault (parent 0xa5a5a5a5), so the case runs there, in a
+child process, as well as on the product build.
+"""
+import os
+import subprocess
+import sys
+
+import msgpack
+import pytest
+
+from test_gpu_long_running import Driver, _job_events
+from zeebe_amd import records as R, workloads
+
+pytestmark = pytest.mark.gpu
+
+
+def _create_and_cancel_in_one_wave():
+    c1, c4t = workloads.CONFIGS["c1"], workloads.CONFIGS["c4twin"]
+    d = Driver({100: c1["workflow"]().to_xml(), 200: c4t["workflow"]().to_xml()},
+               log_capacity=4096, row_capacity=1024, arena_bytes=2 << 20)
+    pay = lambda b, n: [msgpack.packb({"orderId": b + i}) for i in range(n)]  # noqa: E731
+    # tick 0: instances that end up waiting on jobs, some inside a subprocess (a scope with a live child)
+    d.tick([("process", pay(0, 6)), ("subs", pay(10, 6))], [], [])
+    roots = sorted(k for k, parent, *_ in d.e.instances() if parent == -1)
+    for t in range(1, 4):
+        # new CREATEs next to CANCELs: the CANCELs' TERMINATING events share a wave with the CREATED events
+        cancels = [(R.RT_COMMAND, R.VT_WORKFLOW_INSTANCE, R.WI_CANCEL, wik, b"\x80") for wik in roots[:2]]
+        roots = roots[2:]
+        d.pending = [(k, r) for k, r in d.pending
+                     if msgpack.unpackb(r.value, raw=False)["headers"]["workflowInstanceKey"] in roots]
+        done, d.pending = d.pending[:2], d.pending[2:]
+        d.tick([("subs", pay(100 * t, 8)), ("process", pay(100 * t + 50, 8))], _job_events(done, t), cancels)
+        roots = sorted(k for k, parent, *_ in d.e.instances() if parent == -1)
+    assert d.e.counters()["canceled"] == 6
+    d.e.close()
+
+
+def test_create_and_cancel_in_one_wave():
+    _create_and_cancel_in_one_wave()
+
+
+def test_create_and_cancel_in_one_wave_guard_bands():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ZB_CHECKED_LIBRARY="1", PYTHONPATH=os.pathsep.join([root, os.path.join(root, "tests")]))
+    code = ("import test_gpu_regressions as t; from zeebe_amd.engine import checked_violations; "
+            "t._create_and_cancel_in_one_wave(); assert checked_violations()[0] == 0; print('regression ok')")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "regression ok" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])

@@ -11,6 +11,16 @@
 
 #include "../../include/zb_engine.h"
 
+// ZB_DCHECK(cond, fmt, ...): a device-side bounds check of the guard-band build (ZB_CHECKED, zb_checked.hpp): a
+// failed check prints its site and values and evaluates to false, so the caller skips the access instead of
+// faulting; in the product build it is the constant true and costs nothing.
+#ifdef ZB_CHECKED
+#define ZB_DCHECK(cond, ...) \
+  ((cond) ? true : (printf("ZB_DCHECK %s:%d: %s: ", __FILE__, __LINE__, #cond), printf(__VA_ARGS__), false))
+#else
+#define ZB_DCHECK(cond, ...) true
+#endif
+
 namespace zbg {
 
 constexpr uint16_t NO_ELEM = 0xffff;

@@ -13,6 +13,9 @@
 
 namespace zbg {
 
+// the msgpack / json-path readers also build for the host (tests/xmerge_host.cpp runs the exact merge there)
+#define ZB_HD __host__ __device__
+
 // ------------------------------------------------------------------------------ msgpack reading
 struct Tok {
   uint8_t type;      // TokType
@@ -24,14 +27,14 @@ struct Tok {
   bool bval;
 };
 
-__device__ __forceinline__ uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
-__device__ __forceinline__ uint32_t be32(const uint8_t* p) {
+ZB_HD __forceinline__ uint32_t be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
+ZB_HD __forceinline__ uint32_t be32(const uint8_t* p) {
   return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
 }
-__device__ __forceinline__ uint64_t be64(const uint8_t* p) { return ((uint64_t)be32(p) << 32) | be32(p + 4); }
+ZB_HD __forceinline__ uint64_t be64(const uint8_t* p) { return ((uint64_t)be32(p) << 32) | be32(p + 4); }
 
 // Reads the token at p (n bytes available). Returns false on malformed / unsupported input.
-__device__ inline bool read_tok(const uint8_t* p, uint32_t n, Tok& t) {
+ZB_HD inline bool read_tok(const uint8_t* p, uint32_t n, Tok& t) {
   if (n == 0) return false;
   uint8_t b = p[0];
   t.hdr = 1; t.len = 0; t.ival = 0; t.fval = 0; t.bval = false;
@@ -55,11 +58,11 @@ __device__ inline bool read_tok(const uint8_t* p, uint32_t n, Tok& t) {
     case 0xca: {
       if (n < 5) return false;
       uint32_t u = be32(p + 1);
-      t.type = TT_FLOAT; t.fval = (double)__uint_as_float(u); t.total = 5; return true;
+      t.type = TT_FLOAT; t.fval = (double)__builtin_bit_cast(float, u); t.total = 5; return true;
     }
     case 0xcb: {
       if (n < 9) return false;
-      t.type = TT_FLOAT; t.fval = __longlong_as_double((long long)be64(p + 1)); t.total = 9; return true;
+      t.type = TT_FLOAT; t.fval = __builtin_bit_cast(double, be64(p + 1)); t.total = 9; return true;
     }
     case 0xd9: if (n < 2) return false; t.type = TT_STRING; t.len = p[1]; t.hdr = 2; break;
     case 0xda: if (n < 3) return false; t.type = TT_STRING; t.len = be16(p + 1); t.hdr = 3; break;
@@ -80,7 +83,7 @@ __device__ inline bool read_tok(const uint8_t* p, uint32_t n, Tok& t) {
 }
 
 // Returns the offset just past the value starting at pos, or 0xffffffff if malformed.
-__device__ inline uint32_t skip_value(const uint8_t* d, uint32_t n, uint32_t pos) {
+ZB_HD inline uint32_t skip_value(const uint8_t* d, uint32_t n, uint32_t pos) {
   uint64_t pending = 1;
   while (pending > 0) {
     Tok t;
@@ -93,7 +96,7 @@ __device__ inline uint32_t skip_value(const uint8_t* d, uint32_t n, uint32_t pos
   return pos;
 }
 
-__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
+ZB_HD __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
   for (uint32_t i = 0; i < n; i++)
     if (a[i] != b[i]) return false;
   return true;
@@ -107,7 +110,7 @@ struct QueryResult {
 
 // [ROOT, MAP_KEY k] fast path: every top-level value under key k (the executor's results for this
 // two-filter query are exactly those, in document order; container values are whole results).
-__device__ inline bool query_fast(const uint8_t* d, uint32_t n, const uint8_t* key, uint32_t klen,
+ZB_HD inline bool query_fast(const uint8_t* d, uint32_t n, const uint8_t* key, uint32_t klen,
                                   QueryResult& r) {
   r.count = 0; r.pos = 0; r.len = 0;
   Tok t;
@@ -134,7 +137,7 @@ __device__ inline bool query_fast(const uint8_t* d, uint32_t n, const uint8_t* k
 
 // General executor (literal state machine of MsgPackQueryExecutor.visitElement), depth <= 30.
 constexpr int JP_MAX_DEPTH = 30;
-__device__ __noinline__ bool query_general(const uint8_t* d, uint32_t n, const DevFilter* f, uint32_t nf,
+ZB_HD inline __noinline__ bool query_general(const uint8_t* d, uint32_t n, const DevFilter* f, uint32_t nf,
                                      const uint8_t* pool, QueryResult& r) {
   r.count = 0; r.pos = 0; r.len = 0;
   int cur[JP_MAX_DEPTH], num[JP_MAX_DEPTH], app[JP_MAX_DEPTH], dyn[JP_MAX_DEPTH];
@@ -203,7 +206,7 @@ __device__ __noinline__ bool query_general(const uint8_t* d, uint32_t n, const D
   return true;
 }
 
-__device__ inline bool run_query(const uint8_t* d, uint32_t n, const DevQuery& q, const DevFilter* filters,
+ZB_HD inline bool run_query(const uint8_t* d, uint32_t n, const DevQuery& q, const DevFilter* filters,
                                  const uint8_t* pool, QueryResult& r) {
   if (q.fast) {
     const DevFilter& k = filters[q.first + 1];
@@ -329,22 +332,22 @@ constexpr int MERGE_MAX_DEPTH = 16;
 struct Out {
   uint8_t* dst;   // nullptr: size pass
   uint32_t n;
-  __device__ __forceinline__ void put(uint8_t b) { if (dst) dst[n] = b; n++; }
-  __device__ __forceinline__ void put_bytes(const uint8_t* s, uint32_t len) {
+  ZB_HD __forceinline__ void put(uint8_t b) { if (dst) dst[n] = b; n++; }
+  ZB_HD __forceinline__ void put_bytes(const uint8_t* s, uint32_t len) {
     if (dst) for (uint32_t i = 0; i < len; i++) dst[n + i] = s[i];
     n += len;
   }
-  __device__ inline void map_hdr(uint32_t c) {
+  ZB_HD inline void map_hdr(uint32_t c) {
     if (c < 16) put(0x80 | c);
     else if (c < 65536) { put(0xde); put(c >> 8); put(c & 0xff); }
     else { put(0xdf); put(c >> 24); put((c >> 16) & 0xff); put((c >> 8) & 0xff); put(c & 0xff); }
   }
-  __device__ inline void arr_hdr(uint32_t c) {
+  ZB_HD inline void arr_hdr(uint32_t c) {
     if (c < 16) put(0x90 | c);
     else if (c < 65536) { put(0xdc); put(c >> 8); put(c & 0xff); }
     else { put(0xdd); put(c >> 24); put((c >> 16) & 0xff); put((c >> 8) & 0xff); put(c & 0xff); }
   }
-  __device__ inline void str(const uint8_t* s, uint32_t c) {
+  ZB_HD inline void str(const uint8_t* s, uint32_t c) {
     if (c < 32) put(0xa0 | c);
     else if (c < 256) { put(0xd9); put(c); }
     else if (c < 65536) { put(0xda); put(c >> 8); put(c & 0xff); }

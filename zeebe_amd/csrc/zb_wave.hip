@@ -975,10 +975,12 @@ __global__ void __launch_bounds__(WG) k_pre(WaveParams P) {
 // scope k_pre marked: one pass over the allocated rows, only in chunks of a cancellation that need it.
 __global__ void __launch_bounds__(256) k_children(WaveParams P) {
   if (*(volatile uint32_t*)P.need_children == 0) return;
-  const uint64_t rows = (uint64_t)P.hdr[P.wave & 1].rows_next;
+  uint64_t rows = (uint64_t)P.hdr[P.wave & 1].rows_next;
+  if (!ZB_DCHECK(rows <= P.row_cap, "rows_next %llu\n", (unsigned long long)rows)) rows = P.row_cap;
   for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < rows; r += (uint64_t)gridDim.x * 256) {
     const RowMeta m = P.rmeta[r];
     if (m.state == 0 || m.parent == NO_ROW) continue;
+    if (!ZB_DCHECK(m.parent < P.row_cap, "row %llu parent %u\n", (unsigned long long)r, m.parent)) continue;
     if (P.raux[m.parent].mark == P.epoch) atomicMin(&P.raux[m.parent].first, (uint32_t)r);
   }
 }
@@ -1128,12 +1130,18 @@ __device__ __forceinline__ void emit_item(const WaveParams& P, const Chunk& c, i
       if (row >= P.row_cap) { err |= DE_ROWS_FULL; s.rself = NO_ROW; }
       else {
         s.rself = (uint32_t)row;
+        RowMeta m;
         if (s.flags & SF_ROW_INIT) {
-          RowMeta m;
           m.payload = s.d.payload; m.parent = s.rscope; m.elem = s.d.elem; m.state = WI_ELEMENT_READY;
           m.flags = 0; m.nchild = 0;
           P.rmeta[row] = m;
           P.rkeys[row] = RowKeys{s.d.key, s.d.scope_key, s.d.inst_key, 0};
+        } else {
+          // a CREATE's row: the instance enters the index when its CREATED event is processed (next wave), and
+          // until then the row must read as free -- k_children scans every allocated row, and this one still holds
+          // whatever the memory held before (a compacted-away row, or another engine's data)
+          m.payload = 0; m.parent = NO_ROW; m.elem = NO_ELEM; m.state = 0; m.flags = 0; m.nchild = 0;
+          P.rmeta[row] = m;
         }
       }
     }
