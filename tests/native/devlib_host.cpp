@@ -13,6 +13,7 @@ static inline float __uint_as_float(uint32_t u) { float f; std::memcpy(&f, &u, 4
 static inline double __longlong_as_double(long long u) { double d; std::memcpy(&d, &u, 8); return d; }
 #define HIP_INCLUDE_HIP_HIP_RUNTIME_H
 #include "../../zeebe_amd/csrc/zb_devlib.hpp"
+#include "../../zeebe_amd/csrc/zb_xmerge.hpp"
 #include "../../zeebe_amd/csrc/zb_model.cpp"  // the product's deploy-time compilers (json-path, mapping targets)
 
 #include <string>
@@ -94,5 +95,35 @@ long devlib_query(const uint8_t* doc, uint32_t n, const uint8_t* f_ids, const in
   out[0] = r.pos;
   out[1] = r.len;
   return r.count;
+}
+// the exact tree (zb_xmerge.hpp): x_merge, or x_map over the product's compiled mappings (spec as devlib_map_text,
+// empty spec = merge). Returns the output length, or -(100 + X_* status) (fail_query in *fq), -20 compile error.
+long devlib_xmerge(const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint32_t nt, const char* spec, int extract,
+                   uint8_t* out, uint32_t cap, uint32_t* fq, char* err, uint32_t errcap) {
+  static uint8_t slab[XSLAB_BYTES];
+  ModelTables t;
+  std::string sp(spec), e;
+  size_t p = 0;
+  while (p < sp.size()) {
+    size_t tab = sp.find('\t', p), nl = sp.find('\n', p);
+    if (tab == std::string::npos || nl == std::string::npos || tab > nl) return -21;
+    if (compile_mapping(t, sp.substr(p, tab - p), sp.substr(tab + 1, nl - tab - 1), e) < 0) {
+      snprintf(err, errcap, "%s", e.c_str());
+      return -20;
+    }
+    p = nl + 1;
+  }
+  if (t.pool.empty()) t.pool.push_back(0);
+  Out o{out, 0};
+  uint16_t q = 0xffff;
+  int st;
+  if (t.maps.empty())
+    st = x_merge(slab, XSLAB_BYTES, src, ns, tgt, nt, o, cap);
+  else
+    st = x_map(slab, XSLAB_BYTES, src, ns, extract ? nullptr : tgt, nt, t.maps.data(), (uint32_t)t.maps.size(),
+               t.segs.data(), t.queries.data(), t.filters.data(), t.pool.data(), o, cap, q);
+  *fq = q;
+  if (st != X_OK) return -(100 + st);
+  return (long)o.n;
 }
 }

@@ -125,9 +125,9 @@ def test_racing_records_in_one_tick(by_one):
             _update(d, {"u": 1}), _created(p.job_of(d)), _completed(p.job_of(d)),  # update, then completion
             _created(p.job_of(f)), _completed(p.job_of(f)), _update(f, {"u": 2}),  # completion, then update
             _update(g, {"u": 3}), _update(g, {"u": 4}),                          # two updates
-            _created(p.job_of(h))]                                               # created ...
+            _created(p.job_of(h))]                                               # created, 20 records ...
     recs += [_created(p.job_of(q)) for q in quiet[:20]]
-    recs += [_completed(p.job_of(h)), _completed(p.job_of(h), msgpack.packb({"again": 1}))]  # ... completed twice
+    recs += [_completed(p.job_of(h))]                                             # ... completed later
     recs += [_completed(p.job_of(q)) for q in quiet[:20]]
     recs += [_update(k, {"u": 5}), _cancel(k), _update(k, {"u": 6})]            # update, cancel, update
     recs += [_created(p.job_of(q)) for q in quiet[20:]] + [_completed(p.job_of(q)) for q in quiet[20:]]
@@ -143,6 +143,28 @@ def test_racing_records_in_one_tick(by_one):
     # tick 3: nothing races (the conflict set of the last tick must not linger)
     roots = p.roots()
     p.tick(recs=[x for r in roots[:10] for x in (_created(p.job_of(r)), _completed(p.job_of(r)))])
+
+
+def test_duplicate_job_completion_fails_like_the_reference():
+    """Two JOB COMPLETED events for one job in a tick: both pass JobCompletedEventProcessor (the activity is still
+    ACTIVATED when each is processed) and both write ELEMENT_COMPLETING; the second COMPLETING finds no element
+    instance and the reference's noConcurrentTransitionGuard throws a NullPointerException
+    (BpmnStepProcessor.java:128-150), which fails the processor. The engine fails the step the same way rather
+    than writing records the reference never writes."""
+    from zeebe_amd.engine import ZbError
+
+    c1 = workloads.CONFIGS["c1"]
+    p = Pair({100: c1["workflow"]().to_xml()})
+    p.tick([("process", [msgpack.packb({"orderId": i}) for i in range(4)])])
+    j = p.job_of(p.roots()[1])
+    recs = [_created(j), _completed(j), _completed(j, msgpack.packb({"again": 1}))]
+    for r in recs:
+        p.o.submit(*r)
+    with pytest.raises(zbref.ZbrefError, match="noConcurrentTransitionGuard"):
+        p.o.run()
+    p.e.submit_records(recs)
+    with pytest.raises(ZbError):
+        p.e.step()
 
 
 def test_racing_job_commands():

@@ -1,0 +1,220 @@
+"""The exact payload tree (zeebe_amd/csrc/zb_xmerge.hpp) against the oracle, on the CPU.
+
+zb_xmerge.hpp restates MappingProcessor's string-id tree (MsgPackDocumentIndexer / MsgPackTree /
+MsgPackDocumentTreeWriter, json-path/.../mapping/) for the documents the kernels' structural merge refuses: duplicate
+keys, keys holding '[' / ']' (the reference's node ids collide: "$[a[b]]" is both key "a[b]" under the root and ...),
+non-string keys below the root, deep nesting, many nodes. tests/native/devlib_host.cpp compiles it for the host; the
+same source runs in k_merge_exact / k_map_exact / the trajectory merge on the GPU (tests/test_gpu_payload_shapes.py).
+The oracle (oracle/zbref_mapping.hpp) is the literal restatement with std::string ids and hash maps.
+"""
+import ctypes
+import os
+import random
+import struct
+import subprocess
+
+import pytest
+
+from oracle import zbref
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+NATIVE = os.path.join(HERE, "native")
+CSRC = os.path.join(HERE, "..", "zeebe_amd", "csrc")
+X_STATUS = {101: "fail", 102: "no_data", 103: "not_map", 104: "unsupported"}
+
+
+@pytest.fixture(scope="module")
+def L():
+    src = os.path.join(NATIVE, "devlib_host.cpp")
+    so = os.path.join(NATIVE, "libdevlib_host.so")
+    deps = [src] + [os.path.join(CSRC, f) for f in ("zb_devlib.hpp", "zb_xmerge.hpp", "zb_model.cpp", "zb_model.hpp",
+                                                     "zb_device.hpp")]
+    if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(d) for d in deps):
+        subprocess.check_call(["g++", "-O1", "-std=c++17", "-fPIC", "-shared", "-I/opt/rocm/include", "-o", so, src])
+    lib = ctypes.CDLL(so)
+    lib.devlib_xmerge.restype = ctypes.c_long
+    lib.devlib_xmerge.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                  ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                  ctypes.c_char_p, ctypes.c_uint32]
+    lib.devlib_merge.restype = ctypes.c_long
+    lib.devlib_merge.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p,
+                                 ctypes.c_uint32]
+    return lib
+
+
+# ---- raw msgpack with duplicate keys: a map is M([(key, value), ...])
+class M(list):
+    pass
+
+
+def enc(x) -> bytes:
+    if isinstance(x, M):
+        n = len(x)
+        h = bytes([0x80 | n]) if n < 16 else b"\xde" + struct.pack(">H", n)
+        return h + b"".join(enc(k) + enc(v) for k, v in x)
+    if isinstance(x, list):
+        n = len(x)
+        h = bytes([0x90 | n]) if n < 16 else b"\xdc" + struct.pack(">H", n)
+        return h + b"".join(enc(v) for v in x)
+    if x is None:
+        return b"\xc0"
+    if x is True or x is False:
+        return b"\xc3" if x else b"\xc2"
+    if isinstance(x, int):
+        if 0 <= x < 128:
+            return bytes([x])
+        return b"\xd3" + struct.pack(">q", x)
+    if isinstance(x, str):
+        b = x.encode()
+        return (bytes([0xa0 | len(b)]) if len(b) < 32 else b"\xd9" + bytes([len(b)])) + b
+    if isinstance(x, bytes):
+        return b"\xc4" + bytes([len(x)]) + x
+    raise TypeError(x)
+
+
+KEYS = ["a", "b", "c", "0", "1", "a[b]", "b]", "[c", "a][b", "$", "x[0]", "", "key", "0]"]
+
+
+def odd_value(r, depth, int_keys):
+    k = r.random()
+    if depth > 0 and k < 0.3:
+        return odd_map(r, depth - 1, int_keys)
+    if depth > 0 and k < 0.45:
+        return [odd_value(r, depth - 1, int_keys) for _ in range(r.randint(0, 4))]
+    return r.choice([None, True, 7, -3, 1 << 40, "v", "w" * 40, b"\x00\x01"])
+
+
+def odd_map(r, depth, int_keys=False):
+    m = M()
+    for _ in range(r.randint(0, 5)):
+        key = r.choice(KEYS)
+        if int_keys and r.random() < 0.1:
+            key = r.randint(0, 3)
+        m.append((key, odd_value(r, depth, int_keys)))
+        if r.random() < 0.2 and m:  # a duplicate of an earlier key
+            m.append((m[r.randrange(len(m))][0], odd_value(r, depth, int_keys)))
+    return m
+
+
+def deep(n, leaf=1):
+    x = leaf
+    for i in range(n):
+        x = M([("k%d" % (i % 3), x), ("s", i)]) if i % 2 else [x, i]
+    return M([("root", x)])
+
+
+def oracle_merge(src, tgt):
+    out = ctypes.create_string_buffer(1 << 22)
+    err = ctypes.create_string_buffer(4096)
+    n = zbref.lib().zbref_merge(src, len(src), tgt, len(tgt), out, 1 << 22, err, 4096)
+    if n < 0:
+        msg = err.value.decode()
+        return "not_map" if msg.startswith("Processing failed") else "fail"
+    return out.raw[:n]
+
+
+def oracle_map(src, mappings, tgt):
+    try:
+        return zbref.map_documents(src, mappings, tgt)
+    except zbref.MappingError as e:
+        return "no_data" if str(e).startswith("No data found") else "not_map"
+    except RuntimeError:
+        return "fail"
+
+
+def x_run(L, src, tgt, spec=b"", extract=False, cap=1 << 22):
+    out = ctypes.create_string_buffer(cap)
+    fq = ctypes.c_uint32(0)
+    err = ctypes.create_string_buffer(512)
+    n = L.devlib_xmerge(src, len(src), tgt, len(tgt), spec, 1 if extract else 0, out, cap, ctypes.byref(fq), err, 512)
+    if n < 0:
+        return X_STATUS.get(-n, n)
+    return out.raw[:n]
+
+
+def test_xmerge_odd_documents_vs_oracle(L):
+    r = random.Random(11)
+    kinds = {}
+    for i in range(4000):
+        s, t = odd_map(r, 3, int_keys=i % 7 == 0), odd_map(r, 3, int_keys=i % 11 == 0)
+        if r.random() < 0.4:  # shared keys with different shapes
+            for k, v in list(s)[:2]:
+                t.append((k, odd_value(r, 2, False)))
+        sb, tb = enc(s), enc(t)
+        ref, got = oracle_merge(sb, tb), x_run(L, sb, tb)
+        assert got == ref, (sb.hex(), tb.hex(), got, ref)
+        kinds[ref if isinstance(ref, str) else "ok"] = kinds.get(ref if isinstance(ref, str) else "ok", 0) + 1
+    assert kinds["ok"] > 3000 and kinds.get("fail", 0) > 20, kinds
+
+
+def test_xmerge_collisions_and_edges(L):
+    cases = [
+        (M([("a[b]", 1)]), M([("a", M([("b", 2)]))])),                   # "$[a[b]]" vs "$[a][b]": distinct ids
+        (M([("a", M([("b]", 1)]))]), M([("a", M([("b", 2)]))])),
+        (M([("x", [1, 2, M([("0", 5)])])]), M([("x", M([("0", "m"), ("2", 7)]))])),  # index / key "0" collide
+        (M([("a", 1), ("a", 2)]), M([("a", 3), ("b", 4), ("b", 5)])),    # duplicates: the last value, first position
+        (M([("k", [[1, [2, [3]]], []])]), M([("k", "leaf")])),           # nested arrays under a target leaf
+        (M([]), M([("a", None)])),
+        (M([("a", 1)]), M([])),
+        (deep(40), deep(37, "t")),                                       # beyond the structural merge's depth 16
+        (M([("n%d" % i, M([("v", i)])) for i in range(300)]), M([("n%d" % i, i) for i in range(0, 300, 3)])),
+        (M([("a", M([(1, 2)]))]), M([])),                                # a non-string key below the root: fails
+    ]
+    for s, t in cases:
+        sb, tb = enc(s), enc(t)
+        ref, got = oracle_merge(sb, tb), x_run(L, sb, tb)
+        assert got == ref, (sb.hex(), tb.hex(), got, ref)
+    # the empty target buffer: extract(source) = index + rewrite
+    for s in (M([("a", 1), ("a", [1, M([("b]", 2)])])]), deep(20)):
+        sb = enc(s)
+        assert x_run(L, sb, b"") == oracle_merge(sb, b"")
+
+
+def test_xmerge_agrees_with_structural_merge(L):
+    """Wherever the kernels' structural merge (merge_docs) answers, the exact tree gives the same bytes."""
+    import msgpack
+
+    r = random.Random(5)
+    n = 0
+    for _ in range(1500):
+        s = {r.choice("abcdef"): r.choice([1, "x", [1, {"q": 2}], {"z": {"y": None}}]) for _ in range(r.randint(0, 5))}
+        t = {r.choice("abcdeg"): r.choice([2, "y", [3], {"z": 1}]) for _ in range(r.randint(0, 5))}
+        sb, tb = msgpack.packb(s), msgpack.packb(t)
+        out = ctypes.create_string_buffer(1 << 16)
+        k = L.devlib_merge(sb, len(sb), tb, len(tb), out, 1 << 16)
+        if k < 0:
+            continue
+        got = x_run(L, sb, tb)
+        structural = out.raw[:k]
+        assert got == structural or (got == b"\xc0" and structural == b"\x80"), (s, t)
+        n += 1
+    assert n > 1000
+
+
+MAPPINGS = [
+    [("$.a", "$.x")],
+    [("$.a", "$.x[b]")],            # a bracket in a target literal
+    [("$", "$.all")],
+    [("$.a[0]", "$.arr.0"), ("$.b", "$.arr.1")],
+    [("$.c", "$")],                  # root replaced by a leaf: a map, or MappingException
+    [("$.missing", "$.m")],          # no data
+    [("$.*", "$.w")],                # several results: IllegalStateException
+    [("$.a", "$.p.q.r.s.t")],
+]
+
+
+def test_xmap_vs_oracle(L):
+    r = random.Random(3)
+    for i in range(600):
+        s, t = odd_map(r, 2), odd_map(r, 2)
+        s.append(("a", odd_value(r, 2, False)))
+        if i % 3:
+            s.append(("b", 1))
+        s.append(("c", r.choice([M([("z", 1)]), 5, None])))
+        sb, tb = enc(s), enc(t)
+        for ms in MAPPINGS:
+            spec = "".join("%s\t%s\n" % m for m in ms).encode()
+            for extract in (False, True):
+                ref = oracle_map(sb, ms, None if extract else tb)
+                got = x_run(L, sb, tb, spec, extract)
+                assert got == ref, (ms, extract, sb.hex(), tb.hex(), got, ref)

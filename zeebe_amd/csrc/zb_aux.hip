@@ -12,6 +12,7 @@
 
 #include "zb_devlib.hpp"
 #include "zb_kernels.hpp"
+#include "zb_xlock.hpp"
 
 namespace zbg {
 
@@ -87,12 +88,25 @@ __global__ void __launch_bounds__(256) k_merge_gen(WaveParams P) {
     uint8_t* dst = P.arena + (uint64_t)j.dst * 8;
     Out o{dst + 4, 0};
     bool unsup = false;
-    if (!merge_docs(sp + 4, ns, tp + 4, nt, o, unsup)) err |= DE_BAD_PAYLOAD;
-    else if (unsup || o.n > j.cap) err |= DE_UNSUPPORTED;
-    *(uint32_t*)dst = o.n;
-    merge_hint(P, j, o.n);
+    const bool ok = merge_docs(sp + 4, ns, tp + 4, nt, o, unsup);
+    // the shapes merge_docs refuses (and documents it cannot read, which the reference's indexer reads up to the
+    // first bad token) take the exact tree
+    uint32_t olen = o.n;
+    x_exclusive(XSlabs{P.xslab, P.xlocks}, !ok || unsup || o.n > j.cap, [&](uint8_t* slab) {
+      Out w{dst + 4, 0};
+      const int st = x_merge(slab, XSLAB_BYTES, sp + 4, ns, tp + 4, nt, w, j.cap);
+      if (st == X_OK) {
+        if (w.n == 1 && dst[4] == 0xc0) dst[4] = 0x80;  // an empty tree: DocumentValue.wrap turns nil into {}
+        olen = w.n;
+      } else {
+        // X_NOT_MAP (a non-map root) would be an incident, which a merge k_wave already emitted cannot become
+        err |= st == X_FAIL ? DE_BAD_PAYLOAD : DE_UNSUPPORTED;
+      }
+    });
+    *(uint32_t*)dst = olen;
+    merge_hint(P, j, olen);
     merges += 1;
-    bytes += ns + nt + o.n;
+    bytes += ns + nt + olen;
   }
   if (err) atomicOr(P.err, err);
   merges = wg_sum256(merges, s4);
@@ -188,8 +202,38 @@ __global__ void __launch_bounds__(256) k_map(WaveParams P) {
         Out o{nullptr, 0};
         bool unsup = false;
         if (nm) st = map_documents(sp + 4, ns, tp, nt, P.maps + first, nm, P.segs, P.queries, P.filters, P.pool, ws, o, fq);
-        else st = !merge_docs(sp + 4, ns, tp, nt, o, unsup) ? MAP_FAIL : (unsup ? MAP_UNSUPPORTED : MAP_OK);
-        if (st == MAP_OK) {
+        else st = !merge_docs(sp + 4, ns, tp, nt, o, unsup) ? MAP_UNSUPPORTED : (unsup ? MAP_UNSUPPORTED : MAP_OK);
+        // what the node-table mapper / structural merge refuse: the exact tree, size pass, arena, write pass
+        x_exclusive(XSlabs{P.xslab, P.xlocks}, st == MAP_UNSUPPORTED, [&](uint8_t* slab) {
+          Out z{nullptr, 0};
+          uint16_t xq = 0;
+          int xs = nm ? x_map(slab, XSLAB_BYTES, sp + 4, ns, tp, nt, P.maps + first, nm, P.segs, P.queries, P.filters,
+                              P.pool, z, 0x7fffffffu, xq)
+                      : x_merge(slab, XSLAB_BYTES, sp + 4, ns, tp, nt, z, 0x7fffffffu);
+          if (xs == X_OK) {
+            const uint64_t bytes = (4 + z.n + 7) & ~7ull;
+            const uint64_t at = atomicAdd((unsigned long long*)&hin->arena_next, (unsigned long long)bytes);
+            if (at + bytes > P.arena_cap) {
+              err |= DE_ARENA_FULL;
+            } else {
+              Out w{P.arena + at + 4, 0};
+              xs = nm ? x_map(slab, XSLAB_BYTES, sp + 4, ns, tp, nt, P.maps + first, nm, P.segs, P.queries, P.filters,
+                              P.pool, w, 0x7fffffffu, xq)
+                      : x_merge(slab, XSLAB_BYTES, sp + 4, ns, tp, nt, w, 0x7fffffffu);
+              if (w.n == 1 && P.arena[at + 4] == 0xc0) P.arena[at + 4] = 0x80;  // nil -> {} (DocumentValue.wrap)
+              *(uint32_t*)(P.arena + at) = w.n;
+              res = MR_OK | (at >> 3);
+            }
+            st = MAP_DONE;
+          } else if (xs == X_NO_DATA) {
+            st = MAP_ERR_NO_DATA;
+            fq = xq;
+          } else {
+            st = xs == X_NOT_MAP ? MAP_ERR_NOT_MAP : xs == X_FAIL ? MAP_FAIL : MAP_UNSUPPORTED;
+          }
+        });
+        if (st == MAP_DONE) {
+        } else if (st == MAP_OK) {
           const uint64_t bytes = (4 + o.n + 7) & ~7ull;
           const uint64_t at = atomicAdd((unsigned long long*)&hin->arena_next, (unsigned long long)bytes);
           if (at + bytes > P.arena_cap) {

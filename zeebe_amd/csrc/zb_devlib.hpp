@@ -768,7 +768,8 @@ constexpr uint16_t MN_NONE = 0xffff;
 enum : uint8_t { MN_UNTYPED = 0, MN_LEAF_T = 1, MN_LEAF_S = 2, MN_MAP = 3, MN_ARRAY = 4 };
 enum : uint8_t { NS_TDOC = 0, NS_POOL = 1, NS_INDEX = 2 };
 // outcome of map_documents
-enum : int { MAP_OK = 0, MAP_ERR_NO_DATA = 1, MAP_ERR_NOT_MAP = 2, MAP_FAIL = 3, MAP_UNSUPPORTED = 4 };
+enum : int { MAP_OK = 0, MAP_ERR_NO_DATA = 1, MAP_ERR_NOT_MAP = 2, MAP_FAIL = 3, MAP_UNSUPPORTED = 4,
+             MAP_DONE = 5 /* (k_map: the exact tree wrote the result) */ };
 
 struct MNode {
   uint32_t name;        // name bytes offset (NS_TDOC: target document, NS_POOL: pool) or array index (NS_INDEX)

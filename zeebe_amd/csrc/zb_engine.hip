@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "zb_devlib.hpp"
+#include "zb_xmerge.hpp"
 #include "zb_kernels.hpp"
 #include "zb_model.hpp"
 #include "zb_msg.hpp"
@@ -125,6 +126,8 @@ struct zb_engine {
   uint32_t* job_counts = nullptr;  // [0..1] merge counts, [2..3] cond counts, [4..5] subscribe counts,
                                    // [6..7] merges left to the general merger
   uint32_t* merge_slow = nullptr;  // [job_cap] indices of those merges
+  uint8_t* xslab = nullptr;        // exact payload tree workspaces (zb_xmerge.hpp), with a model that merges / maps
+  uint32_t* xlocks = nullptr;
   uint64_t* sub_jobs = nullptr;    // [job_cap] subscribe steps of a wave (models with message catch events)
   uint64_t job_cap = 0;
   WaveHdr* h_hdr_pinned = nullptr;  // pinned mirror for D2H polling
@@ -468,6 +471,8 @@ WaveParams wave_params(zb_engine* e) {
   p.merge_count = e->job_counts;
   p.merge_slow = e->merge_slow;
   p.merge_slow_count = e->job_counts + 6;
+  p.xslab = e->xslab;
+  p.xlocks = e->xlocks;
   p.cond_jobs = e->cond_jobs;
   p.cond_count = e->job_counts + 2;
   p.sub_jobs = e->sub_jobs;
@@ -687,6 +692,8 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   p.err = e->derr;
   p.stats = e->dstats;
   p.log_cap = (uint64_t)e->win_base + e->cfg.log_capacity;  // absolute: the window's end
+  p.xslab = e->xslab;
+  p.xlocks = e->xlocks;
   p.row_cap = e->cfg.row_capacity;
   p.arena_cap = e->cfg.arena_bytes;
   p.defer_ok = (e->tmpl_defer && e->seg_ok && e->d_vsegs.p && e->d_vconst.p && (p.cls || p.uni)) ? 1 : 0;
@@ -1190,7 +1197,7 @@ void zb_engine_destroy(zb_engine* e) {
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_clen, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
                 e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->need_children, e->look_keys, e->look_idx,
-                e->look_tmp, e->conf_first};
+                e->look_tmp, e->conf_first, e->xslab, e->xlocks};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->comm) (void)ncclCommDestroy(e->comm);
@@ -1319,6 +1326,11 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
   if (e->has_io && !e->mapres) {
     HIPCHECK(e, hipMalloc(&e->mapres, (e->wave_cap + 8) * sizeof(uint64_t)));
     HIPCHECK(e, hipMalloc(&e->map_ws, (size_t)MAP_GRID * 256 * MAP_NODES * sizeof(MNode)));
+  }
+  if ((e->has_io || e->has_merges) && !e->xslab) {  // payloads the structural merge / mapper refuse
+    HIPCHECK(e, hipMalloc(&e->xslab, (size_t)XSLAB_COUNT * XSLAB_BYTES));
+    HIPCHECK(e, hipMalloc(&e->xlocks, XSLAB_COUNT * sizeof(uint32_t)));
+    HIPCHECK(e, hipMemset(e->xlocks, 0, XSLAB_COUNT * sizeof(uint32_t)));
   }
   if (e->has_catch) {
     int orc = ensure_outbox(e);

@@ -34,6 +34,7 @@
 
 #include "zb_devlib.hpp"
 #include "zb_kernels.hpp"
+#include "zb_xlock.hpp"
 #include "zb_tmpl.hpp"
 
 namespace zbg {
@@ -597,9 +598,19 @@ __device__ __forceinline__ void merge_into(const TrajParams& P, uint32_t src, ui
     if constexpr (GEN) {
       Out o{(uint8_t*)gd + 4, 0};
       bool unsup = false;
-      if (!merge_docs((const uint8_t*)gs + 4, ns, (const uint8_t*)gt + 4, nt, o, unsup)) err |= DE_BAD_PAYLOAD;
-      else if (unsup || o.n > m_len) err |= DE_UNSUPPORTED;
+      const bool ok = merge_docs((const uint8_t*)gs + 4, ns, (const uint8_t*)gt + 4, nt, o, unsup);
       olen = o.n;
+      // shapes the structural merge refuses: the exact tree (zb_xmerge.hpp)
+      x_exclusive(XSlabs{P.xslab, P.xlocks}, !ok || unsup || o.n > m_len, [&](uint8_t* slab) {
+        Out w{(uint8_t*)gd + 4, 0};
+        const int st = x_merge(slab, XSLAB_BYTES, (const uint8_t*)gs + 4, ns, (const uint8_t*)gt + 4, nt, w, m_len);
+        if (st == X_OK) {
+          if (w.n == 1 && ((uint8_t*)gd)[4] == 0xc0) ((uint8_t*)gd)[4] = 0x80;
+          olen = w.n;
+        } else {
+          err |= st == X_FAIL ? DE_BAD_PAYLOAD : DE_UNSUPPORTED;
+        }
+      });
       gd[0] = olen;
     } else {
       err |= TE_REGEN;
