@@ -10,7 +10,7 @@ f=$(find $O/prof -name '*kernel_stats.csv' | head -1); cp $f $O/kernel_stats.csv
 python3 - $O <<'PY'
 import csv, json, sys
 d = json.load(open(sys.argv[1] + '/bench.json'))
-print(round(d['value'] / 1e9, 3), 'G/s', round(d['ms_per_step'], 3), 'ms/step', {k: round(x, 3) for k, x in d['step_breakdown_ms'].items()})
+print(round(d['value'] / 1e9, 3), 'G/s', round(d['ms_per_step'], 3), 'ms/step', {k: round(x, 3) for k, x in d.get('step_breakdown_ms', {}).items()})
 rows = list(csv.DictReader(open(sys.argv[1] + '/kernel_stats.csv')))
 tot = sum(float(r['TotalDurationNs']) for r in rows)
 for r in sorted(rows, key=lambda r: -float(r['TotalDurationNs']))[:14]:

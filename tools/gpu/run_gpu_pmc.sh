@@ -11,7 +11,7 @@ IFS=';' read -ra SETS <<< "${PMC_SETS:-FETCH_SIZE;WRITE_SIZE}"
 i=0
 for s in "${SETS[@]}"; do
   i=$((i+1))
-  timeout -s KILL 150 rocprofv3 --pmc $s --kernel-trace -d $OUT/p$i -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ${BENCH_ARGS} > $OUT/p$i.json 2> $OUT/p$i.err || { echo "pmc pass $i ($s) failed rc=$?"; tail -5 $OUT/p$i.err; exit 1; }
+  timeout -s KILL 150 rocprofv3 --pmc $s --kernel-trace -d $OUT/p$i -o run --output-format csv -- python3 bench.py --steps ${PMC_STEPS:-1} --warmup 0 --no-cpu-baseline ${BENCH_ARGS} > $OUT/p$i.json 2> $OUT/p$i.err || { echo "pmc pass $i ($s) failed rc=$?"; tail -5 $OUT/p$i.err; exit 1; }
   echo "$s" > $OUT/p$i.set
   echo "pass $i done: $s"
 done

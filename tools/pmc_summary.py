@@ -27,11 +27,23 @@ XCDS = 8
 
 
 def per_kernel(pass_dir):
+    """PMC_SKIP_TICKS=k (environment): drop every dispatch before the (k+1)-th k_inject, i.e. the run's first k ticks
+    (the steady-state bench's population tick)."""
     acc = defaultdict(lambda: defaultdict(float))
     calls = defaultdict(lambda: defaultdict(set))
+    rows = []
     for f in glob.glob(os.path.join(pass_dir, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
-            for row in csv.DictReader(fh):
+            rows += list(csv.DictReader(fh))
+    skip = int(os.environ.get("PMC_SKIP_TICKS", "0"))
+    if skip:
+        did = lambda r: int(r.get("Dispatch_Id") or r.get("Correlation_Id") or 0)  # noqa: E731
+        inj = sorted({did(r) for r in rows if "k_inject" in r["Kernel_Name"]})
+        first = inj[skip] if len(inj) > skip else float("inf")
+        rows = [r for r in rows if did(r) >= first]
+    if True:
+        if True:
+            for row in rows:
                 k = row["Kernel_Name"]
                 c = row.get("Counter_Name")
                 acc[k][c] += float(row["Counter_Value"])

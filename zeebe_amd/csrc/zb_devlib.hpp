@@ -558,7 +558,38 @@ __device__ inline bool check_root(const uint8_t* d, uint32_t n, uint32_t first, 
   return true;
 }
 
-// Performs the merge into o (size pass when o.dst == nullptr). Returns false when malformed.
+// Every map key in the document is a string, as MsgPackDocumentIndexer requires of both documents it indexes (it
+// throws on any other key, anywhere -- also under a container the merge later shadows). False also for documents
+// nested deeper than the check's stack and for unreadable tokens: the exact tree (zb_xmerge.hpp) takes those.
+ZB_HD inline bool keys_are_strings(const uint8_t* d, uint32_t n) {
+  constexpr int D = 32;
+  uint32_t rem[D];
+  bool is_map[D];
+  int depth = 0;
+  uint32_t pos = 0;
+  bool root = true;
+  while (root || depth > 0) {
+    if (depth > 0 && rem[depth - 1] == 0) { depth--; continue; }
+    Tok t;
+    if (pos >= n || !read_tok(d + pos, n - pos, t)) return false;
+    if (depth > 0) {
+      const uint32_t k = --rem[depth - 1];
+      if (is_map[depth - 1] && (k & 1) && t.type != TT_STRING) return false;  // an odd count left: a key
+    }
+    root = false;
+    pos += t.total;
+    if (t.type == TT_MAP || t.type == TT_ARRAY) {
+      if (depth == D) return false;
+      rem[depth] = t.type == TT_MAP ? 2 * t.len : t.len;
+      is_map[depth] = t.type == TT_MAP;
+      depth++;
+    }
+  }
+  return true;
+}
+
+// Performs the merge into o (size pass when o.dst == nullptr). Returns false when malformed -- and for any
+// document keys_are_strings refuses: the exact tree gives the reference's outcome for those.
 __device__ __noinline__ bool merge_docs(const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint32_t nt, Out& o,
                                   bool& unsupported) {
   Tok ts, tt;
@@ -570,6 +601,7 @@ __device__ __noinline__ bool merge_docs(const uint8_t* src, uint32_t ns, const u
   if (src_nil && tgt_nil) { o.put(0x80); return true; }
   uint32_t sc = src_nil ? 0 : ts.len, tc = tgt_nil ? 0 : tt.len;
   uint32_t sf = src_nil ? 0 : ts.total, tf = tgt_nil ? 0 : tt.total;
+  if ((!src_nil && !keys_are_strings(src, ns)) || (!tgt_nil && !keys_are_strings(tgt, nt))) return false;
   if (!src_nil && !check_root(src, ns, sf, sc, unsupported)) return false;
   if (!tgt_nil && !check_root(tgt, nt, tf, tc, unsupported)) return false;
   if (unsupported) return true;
