@@ -19,7 +19,7 @@ import pytest
 
 from test_gpu_parity import _compare, _run_both
 from test_gpu_races import Pair, _completed, _created
-from test_xmerge_host import M, deep, enc, odd_map
+from test_xmerge_host import M, deep, enc, odd_map, oracle_merge
 from oracle import zbref
 from zeebe_amd import bpmn, workloads
 
@@ -87,7 +87,12 @@ def test_many_exact_merges_in_one_wave():
     for i, wik in enumerate(roots):
         j = p.job_of(wik)
         recs.append(_created(j))
-        pl = enc(odd_map(r, 3)) if i % 2 else enc(M([("k", "late"), ("x", M([(str(i % 3), "collide")])), ("k", 1)]))
+        pl = enc(M([("k", "late"), ("x", M([(str(i % 3), "collide")])), ("k", 1)]))
+        if i % 2:  # a random odd document, as long as the reference merges it (some make its writer throw)
+            while True:
+                pl = enc(odd_map(r, 3))
+                if not isinstance(oracle_merge(pl, creates[i]), str):
+                    break
         recs.append(_completed(j, pl))
     n = p.tick(recs=recs)
     assert n > 600
@@ -117,19 +122,30 @@ def test_mappings_over_odd_documents():
         M([("res", deep(33)), ("res2", M([("q[1]", 1)]))]),
         M([("res", 1), ("res2", big)]),
     ]
+    from zeebe_amd.engine import ZbError
+
+    outcomes = {"ok": 0, "fail": 0}
     for model in models:
         xml = model.to_xml()
         for job in jobs:
-            o, e = zbref.Oracle(), Engine(log_capacity=1 << 14, row_capacity=1 << 10, arena_bytes=16 << 20)
-            for x in (o, e):
-                x.deploy(xml, 100, 1)
-                x.set_job_payload(100, "t", enc(job))
             for c in creates:
+                o, e = zbref.Oracle(), Engine(log_capacity=1 << 14, row_capacity=1 << 10, arena_bytes=16 << 20)
+                for x in (o, e):
+                    x.deploy(xml, 100, 1)
+                    x.set_job_payload(100, "t", enc(job))
                 o.create("m", enc(c))
-            e.create("m", [enc(c) for c in creates])
-            o.run()
-            st = e.step()
-            assert st["quiescent"]
-            _compare(o, e)
-            assert o.instances() == e.instances()
-            e.close()
+                e.create("m", [enc(c)])
+                try:
+                    o.run()
+                except zbref.ZbrefError:  # e.g. a duplicate key matched twice by a source query: the processor fails
+                    with pytest.raises(ZbError):
+                        e.step()
+                    outcomes["fail"] += 1
+                else:
+                    st = e.step()
+                    assert st["quiescent"]
+                    _compare(o, e)
+                    assert o.instances() == e.instances()
+                    outcomes["ok"] += 1
+                e.close()
+    assert outcomes["ok"] >= 12 and outcomes["fail"] >= 1, outcomes
