@@ -4,7 +4,7 @@ zb_xmerge.hpp restates MappingProcessor's string-id tree (MsgPackDocumentIndexer
 MsgPackDocumentTreeWriter, json-path/.../mapping/) for the documents the kernels' structural merge refuses: duplicate
 keys, keys holding '[' / ']' (the reference's node ids collide: "$[a[b]]" is both key "a[b]" under the root and ...),
 non-string keys below the root, deep nesting, many nodes. tests/native/devlib_host.cpp compiles it for the host; the
-same source runs in k_merge_exact / k_map_exact / the trajectory merge on the GPU (tests/test_gpu_payload_shapes.py).
+same source runs in k_merge_gen / k_map / the trajectory merge on the GPU (tests/test_gpu_payload_shapes.py).
 The oracle (oracle/zbref_mapping.hpp) is the literal restatement with std::string ids and hash maps.
 """
 import ctypes
@@ -218,3 +218,16 @@ def test_xmap_vs_oracle(L):
                 ref = oracle_map(sb, ms, None if extract else tb)
                 got = x_run(L, sb, tb, spec, extract)
                 assert got == ref, (ms, extract, sb.hex(), tb.hex(), got, ref)
+
+
+def test_xmap_deep_documents(L):
+    """Source queries over documents nested beyond the kernels' executor depth (30): the exact mapper keeps the
+    traversal state in its workspace."""
+    src = enc(M([("res", deep(45)), ("k", M([("a", deep(35, "x"))])), ("n", 3)]))
+    tgt = enc(M([("t", deep(40))]))
+    for ms in ([("$.res", "$.out")], [("$.k.a", "$.t.u")], [("$.n", "$.t")], [("$.res", "$.t.root")]):
+        spec = "".join("%s\t%s\n" % m for m in ms).encode()
+        for extract in (False, True):
+            ref = oracle_map(src, ms, None if extract else tgt)
+            got = x_run(L, src, tgt, spec, extract)
+            assert got == ref and not isinstance(ref, str), (ms, extract, got if isinstance(got, str) else len(got))

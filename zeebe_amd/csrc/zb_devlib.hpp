@@ -137,11 +137,11 @@ ZB_HD inline bool query_fast(const uint8_t* d, uint32_t n, const uint8_t* key, u
 
 // General executor (literal state machine of MsgPackQueryExecutor.visitElement), depth <= 30.
 constexpr int JP_MAX_DEPTH = 30;
-ZB_HD inline __noinline__ bool query_general(const uint8_t* d, uint32_t n, const DevFilter* f, uint32_t nf,
-                                     const uint8_t* pool, QueryResult& r) {
+// (the traversal state per open container lives in caller-provided arrays of maxd entries)
+ZB_HD __forceinline__ bool query_walk(const uint8_t* d, uint32_t n, const DevFilter* f, uint32_t nf,
+                                     const uint8_t* pool, QueryResult& r, int* cur, int* num, int* app, int* dyn,
+                                     bool* ismap, int maxd) {
   r.count = 0; r.pos = 0; r.len = 0;
-  int cur[JP_MAX_DEPTH], num[JP_MAX_DEPTH], app[JP_MAX_DEPTH], dyn[JP_MAX_DEPTH];
-  bool ismap[JP_MAX_DEPTH];
   int depth = 0;
   int matching = -1;
   uint32_t mstart = 0;
@@ -172,7 +172,7 @@ ZB_HD inline __noinline__ bool query_general(const uint8_t* d, uint32_t n, const
       }
     }
     if (t.type == TT_MAP || t.type == TT_ARRAY) {
-      if (depth >= JP_MAX_DEPTH) return false;
+      if (depth >= maxd) return false;
       cur[depth] = -1;
       num[depth] = t.type == TT_MAP ? 2 * (int)t.len : (int)t.len;
       app[depth] = -1;
@@ -204,6 +204,13 @@ ZB_HD inline __noinline__ bool query_general(const uint8_t* d, uint32_t n, const
     }
   }
   return true;
+}
+
+ZB_HD inline __noinline__ bool query_general(const uint8_t* d, uint32_t n, const DevFilter* f, uint32_t nf,
+                                            const uint8_t* pool, QueryResult& r) {
+  int cur[JP_MAX_DEPTH], num[JP_MAX_DEPTH], app[JP_MAX_DEPTH], dyn[JP_MAX_DEPTH];
+  bool ismap[JP_MAX_DEPTH];
+  return query_walk(d, n, f, nf, pool, r, cur, num, app, dyn, ismap, JP_MAX_DEPTH);
 }
 
 ZB_HD inline bool run_query(const uint8_t* d, uint32_t n, const DevQuery& q, const DevFilter* filters,

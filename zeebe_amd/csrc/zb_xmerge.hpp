@@ -515,8 +515,22 @@ ZB_HD inline __noinline__ int x_map(uint8_t* slab, uint32_t slab_bytes, const ui
       if (T.status != X_OK) return T.status;
       parent = id;
     }
-    QueryResult r;  // executeLeafMapping
-    if (!run_query(src, ns, queries[m.query], filters, pool, r)) return X_UNSUP;
+    QueryResult r;  // executeLeafMapping (the executor's per-depth state in the pool: any nesting depth)
+    {
+      const DevQuery& q = queries[m.query];
+      if (q.fast) {
+        if (!run_query(src, ns, q, filters, pool, r)) return X_UNSUP;
+      } else {
+        const uint32_t maxd = x_tokens(src, ns) + 1;
+        const XStr w = T.str_new(maxd * 17 + 16);
+        if (T.status != X_OK) return T.status;
+        int* qi = (int*)(T.pool + ((w.off + 3) & ~3u));
+        if (!query_walk(src, ns, filters + q.first, q.count, pool, r, qi, qi + maxd, qi + 2 * maxd, qi + 3 * maxd,
+                        (bool*)(qi + 4 * maxd), (int)maxd))
+          return X_UNSUP;
+        T.pool_n = w.off;  // (scratch)
+      }
+    }
     if (r.count == 0) { fail_query = m.query; return X_NO_DATA; }
     if (r.count > 1) return X_FAIL;  // IllegalStateException: more than one matching source
     T.add_leaf(0, parent, r.pos, r.len, true);
