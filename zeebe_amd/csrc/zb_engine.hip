@@ -126,6 +126,7 @@ struct zb_engine {
   uint32_t* job_counts = nullptr;  // [0..1] merge counts, [2..3] cond counts, [4..5] subscribe counts,
                                    // [6..7] merges left to the general merger
   uint32_t* merge_slow = nullptr;  // [job_cap] indices of those merges
+  unsigned long long* phase = nullptr;  // (ZB_PHASES measurement build) k_wave phase sums
   uint8_t* xslab = nullptr;        // exact payload tree workspaces (zb_xmerge.hpp), with a model that merges / maps
   uint32_t* xlocks = nullptr;
   uint64_t* sub_jobs = nullptr;    // [job_cap] subscribe steps of a wave (models with message catch events)
@@ -473,6 +474,7 @@ WaveParams wave_params(zb_engine* e) {
   p.merge_slow_count = e->job_counts + 6;
   p.xslab = e->xslab;
   p.xlocks = e->xlocks;
+  p.phase = e->phase;
   p.cond_jobs = e->cond_jobs;
   p.cond_count = e->job_counts + 2;
   p.sub_jobs = e->sub_jobs;
@@ -1170,6 +1172,10 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->t_cstat, CLS_MAX * TSTAT * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->raux, e->cfg.row_capacity * sizeof(RowAux)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMemset(e->raux, 0, e->cfg.row_capacity * sizeof(RowAux)) != hipSuccess) return cleanup(ZB_EDEVICE);
+#ifdef ZB_PHASES
+  if (hipMalloc(&e->phase, 8 * sizeof(unsigned long long)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMemset(e->phase, 0, 8 * sizeof(unsigned long long)) != hipSuccess) return cleanup(ZB_EDEVICE);
+#endif
   if (hipMalloc(&e->need_children, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMemset(e->need_children, 0, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_EDEVICE);
   e->ev.resize(EV_PER_WAVE * WAVES_PER_SYNC_MAX);
@@ -1197,7 +1203,7 @@ void zb_engine_destroy(zb_engine* e) {
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_clen, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
                 e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->need_children, e->look_keys, e->look_idx,
-                e->look_tmp, e->conf_first, e->xslab, e->xlocks};
+                e->look_tmp, e->conf_first, e->xslab, e->xlocks, e->phase};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->comm) (void)ncclCommDestroy(e->comm);
@@ -1233,6 +1239,17 @@ void zb_engine_destroy(zb_engine* e) {
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
+
+#ifdef ZB_PHASES
+// the measurement build's k_wave phase sums since the engine was created (wall-clock ticks of 10 ns, summed over
+// workgroups): [0] process + tile scan, [1] look-back, [2] emit, [3] tiles
+int zb_phase_times(zb_engine* e, unsigned long long* out4) {
+  if (!e || !out4) return ZB_EINVAL;
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  HIPCHECK(e, hipMemcpy(out4, e->phase, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return ZB_OK;
+}
+#endif
 
 const char* zb_last_error(const zb_engine* e) { return e ? e->err.c_str() : "null engine"; }
 

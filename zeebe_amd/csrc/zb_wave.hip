@@ -1297,6 +1297,12 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
   const uint64_t par = (uint64_t)(P.wave & 1) * P.job_cap;
   const uint32_t tag_agg = lb_tag(P.epoch, 0), tag_inc = lb_tag(P.epoch, 1);
 
+#ifdef ZB_PHASES
+  uint64_t ph_t = wall_clock64(), ph[4] = {0, 0, 0, 0};
+#define ZB_PHASE(k) do { const uint64_t ph_n = wall_clock64(); ph[k] += ph_n - ph_t; ph_t = ph_n; } while (0)
+#else
+#define ZB_PHASE(k) do { } while (0)
+#endif
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t i = tile * WG + threadIdx.x;  // wave-relative index
     const int64_t r = c.begin + i;
@@ -1375,6 +1381,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
     if (lane == 63) { s_a[wv] = a; s_b[wv] = b; }
     if (lane == 0) { s_st[wv][0] = st0; s_st[wv][1] = st1; }
     __syncthreads();
+    ZB_PHASE(0);  // process + tile scan
     uint64_t ta = 0, tb = 0;
 #pragma unroll
     for (int k = 0; k < WG / 64; k++) {
@@ -1498,6 +1505,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
       }
     }
     __syncthreads();
+    ZB_PHASE(1);  // look-back (+ the chunk's header on the last tile)
     // ---- emit (k_emit) straight from the LDS slots
     const uint64_t we = w;
     const int ns = (int)(we & 7);
@@ -1515,7 +1523,15 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
                 wf_next, job_next, par);
     }
     __syncthreads();  // LDS slots and scan scratch are reused by the next tile
+    ZB_PHASE(2);  // emit
   }
+#ifdef ZB_PHASES
+  if (threadIdx.x == 0 && P.phase) {
+    for (int k = 0; k < 3; k++) atomicAdd(P.phase + k, (unsigned long long)ph[k]);
+    atomicAdd(P.phase + 3, (unsigned long long)((ntiles - blockIdx.x + gridDim.x - 1) / gridDim.x));
+  }
+#endif
+#undef ZB_PHASE
 }
 
 // ------------------------------------------------------------------------------ k_conflict

@@ -16,6 +16,9 @@ LIB_PATH = os.path.join(_HERE, "libzbgpu.so")
 # reports every out-of-bounds device write per kernel launch -- a test instrument, never the product library
 if os.environ.get("ZB_CHECKED_LIBRARY") == "1":
     LIB_PATH = os.path.join(_HERE, "libzbgpu_checked.so")
+# ZB_PHASES_LIBRARY=1 (measurement only): the phase-timing build (-DZB_PHASES): k_wave's time per phase of its tiles
+if os.environ.get("ZB_PHASES_LIBRARY") == "1":
+    LIB_PATH = os.path.join(_HERE, "libzbgpu_phases.so")
 
 CFG_WAVE_ONLY = 1  # zb_config.flags: never take the trajectory path
 CFG_EXTERNAL_JOBS = 2  # zb_config.flags: no canonical job harness (job events come through zb_submit)
@@ -417,6 +420,14 @@ class Engine:
     def compact(self):
         """zb_compact: drop dead element-instance rows, unreachable payload blobs, removed messages / job states."""
         self._check(self._L.zb_compact(self._h))
+
+    def phase_times(self):
+        """(measurement build ZB_PHASES_LIBRARY=1 only) k_wave's wall-clock ticks (10 ns) per phase, summed over its
+        workgroups: process + tile scan, look-back, emit, and the tiles processed."""
+        out = (ctypes.c_ulonglong * 4)()
+        self._L.zb_phase_times.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        self._check(self._L.zb_phase_times(self._h, out))
+        return dict(process=out[0], lookback=out[1], emit=out[2], tiles=out[3])
 
     def memory_stats(self) -> dict:
         m = zb_memory_stats()
