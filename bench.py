@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--instances", type=int, default=0, help="per GPU (default: C3 10,000,000, C2/C4/C5 1,000,000)")
     ap.add_argument("--tasks", type=int, default=20)
     ap.add_argument("--cpu-sample", type=int, default=0, help="instances in the 1-thread oracle sample (0: default)")
-    ap.add_argument("--cpu-partitions", type=int, default=0, help="C5: oracle partitions of the CPU sample (0: 4)")
+    ap.add_argument("--cpu-partitions", type=int, default=0, help="C5: oracle partitions (threads) of the CPU sample (0: 8)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the extra C2 wave-only / C4 lines")
     ap.add_argument("--no-drain", action="store_true", help="device stepping only (not the contract's step)")

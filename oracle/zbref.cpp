@@ -34,6 +34,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -1979,6 +1980,99 @@ int64_t zbref_encode_float(double v, uint8_t* out) {
 }
 
 // Wall-clock timing helper for the CPU baseline: run to quiescence, return seconds.
+// C5 CPU baseline (bench.py --config c5, cpu_baseline): P oracle partitions, each stepped on its own thread, with
+// the exchange of zeebe_amd.cluster.LocalCluster.settle restated here (no Python in the timed region): run every
+// partition to quiescence; if any emitted OPEN side effects, deliver them (per target partition: sources in
+// partition order, emission order within a source) and repeat; else the same for CORRELATE; else done.
+// Workload: n instances per partition of the deployed message workflow, instance i on partition
+// i % P with payload {orderId: "order-<i>"}; then PUBLISH name "order", correlation key "order-<i>", payload
+// {paid: true} on partition abs(hash % P). out: [0] wall seconds, [1] transitions, [2] completed, [3] rounds.
+int zbref_c5_bench(int P, int64_t n, const char* xml, size_t xml_len, double* out) {
+  std::vector<Engine*> parts;
+  for (int p = 0; p < P; p++) parts.push_back((Engine*)zbref_new(p, P));
+  for (Engine* e : parts)
+    if (zbref_deploy(e, xml, xml_len, 100, 1) != 0) return -1;
+  struct Fx { std::vector<SideEffect> v; };
+  std::vector<Fx> fx(P);
+  int64_t rounds = 0;
+  bool failed = false;
+  auto run_all = [&]() {
+    std::vector<std::thread> ts;
+    for (int p = 0; p < P; p++)
+      ts.emplace_back([&, p]() {
+        if (zbref_run(parts[p], -1) < 0) failed = true;
+        for (auto& f : parts[p]->side_effects) fx[p].v.push_back(f);
+        parts[p]->side_effects.clear();
+      });
+    for (auto& t : ts) t.join();
+  };
+  auto settle = [&]() {
+    for (;;) {
+      run_all();
+      rounds++;
+      if (failed) return;
+      for (int kind = 1; kind <= 2; kind++) {
+        bool any = false;
+        for (int p = 0; p < P && !any; p++)
+          for (auto& f : fx[p].v) any |= f.kind == kind;
+        if (!any) continue;
+        for (int q = 0; q < P; q++)
+          for (int p = 0; p < P; p++)
+            for (auto& f : fx[p].v)
+              if (f.kind == kind && f.partition == q) {
+                if (kind == 1) parts[q]->submit_open(f.wf_partition, f.workflow_instance_key, f.activity_instance_key,
+                                                    f.message_name, f.correlation_key);
+                else parts[q]->submit_correlate(f.workflow_instance_key, f.activity_instance_key, f.message_name,
+                                                f.payload);
+              }
+        for (int p = 0; p < P; p++) {
+          std::vector<SideEffect> rest;
+          for (auto& f : fx[p].v)
+            if (f.kind != kind) rest.push_back(f);
+          fx[p].v.swap(rest);
+        }
+        goto next;
+      }
+      return;
+    next:;
+    }
+  };
+  auto mp_str = [](const std::string& s) {
+    bytes b;
+    if (s.size() < 32) b.push_back((char)(0xa0 | s.size()));
+    else { b.push_back((char)0xd9); b.push_back((char)s.size()); }
+    b += s;
+    return b;
+  };
+  const bytes paid = std::string("\x81\xa4paid\xc3", 7);
+  const int64_t N = n * P;
+  const auto t0 = std::chrono::steady_clock::now();
+  try {
+    for (int64_t i = 0; i < N; i++)
+      parts[i % P]->submit_create("msg", -1, -1, std::string("\x81\xa7orderId", 9) + mp_str("order-" + std::to_string(i)));
+  } catch (const std::exception&) {
+    failed = true;
+  }
+  if (!failed) settle();
+  for (int64_t i = 0; i < N && !failed; i++) {
+    const std::string ck = "order-" + std::to_string(i);
+    const int32_t h = zbref_subscription_hash((const uint8_t*)ck.data(), ck.size());
+    const int q = std::abs((int)(h % P));  // abs(hash % P), Java's remainder (SubscriptionCommandSender.java:105-109)
+    parts[q]->submit_publish("order", ck, 3600000, paid, bytes());
+  }
+  if (!failed) settle();
+  const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  int64_t tr = 0, comp = 0, c[16];
+  for (Engine* e : parts) {
+    zbref_counters(e, c);
+    tr += c[6];
+    comp += c[1];
+  }
+  out[0] = wall; out[1] = (double)tr; out[2] = (double)comp; out[3] = (double)rounds;
+  for (Engine* e : parts) zbref_free(e);
+  return failed ? -1 : 0;
+}
+
 double zbref_run_timed(void* h, int64_t* processed) {
   auto t0 = std::chrono::steady_clock::now();
   int64_t n = zbref_run(h, -1);

@@ -364,6 +364,18 @@ def encode_float(v: float) -> bytes:
     return buf.raw[:n]
 
 
+def c5_bench(partitions: int, per_partition: int, xml: str):
+    """zbref_c5_bench: the C5 schedule over `partitions` oracle partitions, one thread each, exchange in C++.
+    Returns (wall seconds, transitions, completed instances, exchange rounds)."""
+    out = (ctypes.c_double * 4)()
+    x = xml.encode()
+    lib().zbref_c5_bench.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_char_p, ctypes.c_size_t,
+                                     ctypes.POINTER(ctypes.c_double)]
+    if lib().zbref_c5_bench(partitions, per_partition, x, len(x), out) != 0:
+        raise ZbrefError("c5 bench failed")
+    return out[0], int(out[1]), int(out[2]), int(out[3])
+
+
 class OraclePartition(Oracle):
     """An oracle partition with the partition interface of zeebe_amd.cluster (LocalCluster / DistCluster):
     side effects become exchange records (zb_exchange_rec layout) sorted by target partition, stable in

@@ -1260,7 +1260,8 @@ __global__ void __launch_bounds__(WG) k_emit(WaveParams P) {
 // a resident predecessor that the scheduler time-slices out keeps its waiters spinning without progress for
 // as long as it is descheduled): a hand-off that has not arrived after LB_TIMEOUT_TICKS sets DE_TIMEOUT, the
 // wave's results are void and the host stops the partition -- it never hangs the device.
-constexpr int LB_FIELDS = 12;  // rec wf job row bytes_lo bytes_hi merges conds | transitions completed created canceled
+constexpr int LB_FIELDS = 8;  // rec wf job row bytes_lo bytes_hi merges conds (8 predecessors per look-back round)
+constexpr int LB_ROUND = 64 / LB_FIELDS;  // predecessors read per look-back round
 constexpr int LB_STRIDE = 16;  // granules per tile (128 B)
 constexpr uint64_t LB_TIMEOUT_TICKS = 400000000ull;  // 4 s of the 100 MHz wall clock per look-back, then DE_TIMEOUT
 
@@ -1296,6 +1297,9 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
   const uint64_t rows_next = (uint64_t)hin->rows_next, arena_next = (uint64_t)hin->arena_next;
   const uint64_t par = (uint64_t)(P.wave & 1) * P.job_cap;
   const uint32_t tag_agg = lb_tag(P.epoch, 0), tag_inc = lb_tag(P.epoch, 1);
+  // the workgroup's statistics (transitions, completed, created, canceled): summed over its tiles, added to the
+  // partition counters once at the end (they are not part of the scan, so the look-back carries 8 fields, not 12)
+  uint64_t wg_sa = 0, wg_sb = 0;
 
 #ifdef ZB_PHASES
   uint64_t ph_t = wall_clock64(), ph[4] = {0, 0, 0, 0};
@@ -1400,11 +1404,12 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
       s_agg[2] = (uint32_t)((ta >> 32) & 0xffff); s_agg[3] = (uint32_t)(ta >> 48);
       s_agg[4] = (uint32_t)tbytes; s_agg[5] = (uint32_t)(tbytes >> 32);
       s_agg[6] = (uint32_t)((tb >> 40) & 0xfff); s_agg[7] = (uint32_t)(tb >> 52);
-      s_agg[8] = (uint32_t)sa; s_agg[9] = (uint32_t)(sa >> 32); s_agg[10] = (uint32_t)sb; s_agg[11] = (uint32_t)(sb >> 32);
+      wg_sa += sa;
+      wg_sb += sb;
     }
     if (wv == 0) {
-      const int f = lane % LB_FIELDS, j = lane / LB_FIELDS;  // field, predecessor distance - 1 (j < 5 for lane < 60)
-      const bool lb_lane = lane < 5 * LB_FIELDS;
+      const int f = lane % LB_FIELDS, j = lane / LB_FIELDS;  // field, predecessor distance - 1 (j < 8)
+      const bool lb_lane = lane < LB_ROUND * LB_FIELDS;
       const uint32_t my_agg = lane < LB_FIELDS ? s_agg[lane] : 0;
       uint64_t* lb = P.lookback + (uint64_t)tile * LB_STRIDE;
       if (lane < LB_FIELDS)
@@ -1434,14 +1439,14 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
               __builtin_amdgcn_s_sleep(1);
             }
           }
-          // a predecessor is usable when its 12 granules carry one tag (a reader can catch it between its
+          // a predecessor is usable when its LB_FIELDS granules carry one tag (a reader can catch it between its
           // aggregate and inclusive publication): re-read the round otherwise
           const uint64_t m_agg = __ballot(lb_lane && tg == tag_agg), m_inc = __ballot(!lb_lane || tg == tag_inc);
           bool consistent = true, found = false;
-          int first = 5;
+          int first = LB_ROUND;
 #pragma unroll
-          for (int k = 0; k < 5; k++) {
-            const uint64_t gm = 0xfffull << (LB_FIELDS * k);
+          for (int k = 0; k < LB_ROUND; k++) {
+            const uint64_t gm = ((1ull << LB_FIELDS) - 1) << (LB_FIELDS * k);
             const bool inc_k = (m_inc & gm) == gm, agg_k = (m_agg & gm) == gm;
             if (!found) {
               if (!inc_k && !agg_k) consistent = false;
@@ -1450,13 +1455,14 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
           }
           if (__ballot(timeout)) { timeout = true; break; }
           if (!consistent) continue;  // same p again (bounded by the per-granule spins above)
-          // sum field f over predecessors j <= first: lanes f, f + 12, ..., f + 48
+          // sum field f over predecessors j <= first: lanes f, f + 8, ..., f + 56 (butterfly over the lane bits
+          // above the field)
           uint64_t x = (lb_lane && j <= first) ? (uint64_t)v : 0;
-          const uint64_t x12 = __shfl(x, (lane + 12) & 63, 64), x24 = __shfl(x, (lane + 24) & 63, 64);
-          const uint64_t x36 = __shfl(x, (lane + 36) & 63, 64), x48 = __shfl(x, (lane + 48) & 63, 64);
-          if (lane < LB_FIELDS) acc += x + x12 + x24 + x36 + x48;
-          if (first < 5) break;
-          p -= 5;
+#pragma unroll
+          for (int d = LB_FIELDS; d < 64; d <<= 1) x += __shfl_xor(x, d, 64);
+          if (lane < LB_FIELDS) acc += x;
+          if (first < LB_ROUND) break;
+          p -= LB_ROUND;
         }
         if (__ballot(timeout) && lane == 0) {
           atomicOr(P.err, (uint32_t)DE_TIMEOUT);  // the others stop waiting too
@@ -1486,11 +1492,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
         h.job_next = hin->job_next + 5 * (int64_t)s_tot[2];
         h.rows_next = hin->rows_next + (int64_t)s_tot[3];
         h.arena_next = hin->arena_next + (int64_t)s_tot[4];
-        P.stats[0] += s_tot[8];
-        P.stats[1] += s_tot[9];
-        P.stats[2] += s_tot[10];
         P.stats[6] += 1;
-        P.stats[7] += s_tot[11];
         uint32_t err = 0;
         if ((uint64_t)h.end > P.log_cap) err |= DE_LOG_FULL;
         if ((uint64_t)h.rows_next > P.row_cap) err |= DE_ROWS_FULL;
@@ -1524,6 +1526,12 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
     }
     __syncthreads();  // LDS slots and scan scratch are reused by the next tile
     ZB_PHASE(2);  // emit
+  }
+  if (threadIdx.x == 0 && (wg_sa | wg_sb)) {
+    atomicAdd((unsigned long long*)&P.stats[0], (unsigned long long)(uint32_t)wg_sa);  // transitions
+    atomicAdd((unsigned long long*)&P.stats[1], (unsigned long long)(wg_sa >> 32));    // completed instances
+    atomicAdd((unsigned long long*)&P.stats[2], (unsigned long long)(uint32_t)wg_sb);  // created
+    atomicAdd((unsigned long long*)&P.stats[7], (unsigned long long)(wg_sb >> 32));    // canceled
   }
 #ifdef ZB_PHASES
   if (threadIdx.x == 0 && P.phase) {
