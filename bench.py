@@ -38,7 +38,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BYTES_PER_TRANSITION = 96  # 32 B row read + 32 B row write + 32 B record descriptor
 DESC_BYTES = 32  # one zb_rec descriptor per log record
 HDR_BYTES = 24  # one zb_record_header per drained record
-PMC_DIR = os.path.join(ROOT, "profiles", "r03")
+PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r04", "r03")]  # newest first
 METRIC = "BPMN element transitions/sec (+ completed instances/sec) per node; % HBM roofline"
 
 
@@ -302,9 +302,17 @@ def cpu_baseline_early(a, rank, world):
 
 
 # ------------------------------------------------------------------------------ roofline
+def _pmc_file(tag):
+    for d in PMC_DIRS:
+        f = os.path.join(d, "pmc_%s.json" % tag)
+        if os.path.exists(f):
+            return f
+    return None
+
+
 def load_traffic(tag, kernel_prefix):
-    f = os.path.join(PMC_DIR, "pmc_%s.json" % tag)
-    if not os.path.exists(f):
+    f = _pmc_file(tag)
+    if f is None:
         return None, None
     with open(f) as fh:
         d = json.load(fh)
@@ -317,8 +325,8 @@ def load_traffic(tag, kernel_prefix):
 def load_traffic_step(tag, kernel_prefixes):
     """HBM bytes per tick of every kernel named by the prefixes (PMC averages x dispatches / ticks of the PMC run;
     the run's ticks = k_inject dispatches, one per tick)."""
-    f = os.path.join(PMC_DIR, "pmc_%s.json" % tag)
-    if not os.path.exists(f):
+    f = _pmc_file(tag)
+    if f is None:
         return None
     with open(f) as fh:
         d = json.load(fh).get("kernels", {})
@@ -375,7 +383,8 @@ def roofline(tot, steps, cfg, n):
          "traffic": traffic, "kernel": name, "avg_launch_us": ms * 1e3, "alg_bytes_per_launch": b,
          "alg_bytes_model": model,
          "traffic_note": ("HBM bytes per launch of %s from rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (separate --pmc "
-                          "passes, profiles/r03/pmc_%s_%d.json)" % (pmc_kernel, cfg, n)) if traffic else
+                          "passes, %s)" % (pmc_kernel, os.path.relpath(_pmc_file("%s_%d" % (cfg, n)), ROOT)))
+                         if traffic else
                          "no committed PMC passes for this workload"}
     r["other_kernels"] = [{"kernel": c[0], "avg_launch_us": c[1] * 1e3, "alg_bytes_per_launch": c[2],
                            "achieved": c[2] / (c[1] / 1e3) / 1e9, "frac": c[2] / (c[1] / 1e3) / 1e9 / HBM_PEAK_GBS}
