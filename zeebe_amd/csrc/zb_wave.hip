@@ -1413,11 +1413,12 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
       const int f = lane & (LB_FIELDS - 1), sub = lane / LB_FIELDS;  // field; predecessor sub-slot (hop B)
       const uint32_t my_agg = lane < LB_FIELDS ? s_agg[lane] : 0;
       uint64_t* lb = P.lookback + (uint64_t)tile * LB_STRIDE;
-      // the aggregate goes to granules [0, 8), the inclusive prefix to [8, 16) (tile 0's aggregate is its prefix)
-      if (lane < LB_FIELDS)
-        __hip_atomic_store(lb + (tile == 0 ? LB_FIELDS : 0) + lane,
-                           ((uint64_t)(tile == 0 ? tag_inc : tag_agg) << 32) | my_agg, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+      // the aggregate goes to granules [0, 8), the inclusive prefix to [8, 16); tile 0's aggregate is also its
+      // prefix (a reader that has not seen that prefix yet takes the empty start and tile 0's aggregate)
+      const uint32_t agg_f = __shfl(my_agg, f, 64);
+      if (lane < 2 * LB_FIELDS && (lane < LB_FIELDS || tile == 0))
+        __hip_atomic_store(lb + lane, ((uint64_t)(lane < LB_FIELDS ? tag_agg : tag_inc) << 32) | agg_f,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       uint64_t acc = 0;  // lanes < 8: exclusive prefix of field `lane`
       if (lane == 0) s_void = 0;
       if (tile > 0) {
