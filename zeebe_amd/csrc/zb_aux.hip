@@ -42,21 +42,43 @@ __device__ __forceinline__ void merge_hint(const WaveParams& P, const MergeJob& 
 // shape of nearly every workflow) -- small in registers and without a workspace, so the job list streams at full
 // occupancy -- and queues the rest for k_merge_gen, the general indexer / merger (merge_docs, a per-thread node
 // workspace), which for most waves finds its queue empty.
+// small documents are merged in an LDS copy: the flat merge re-reads its documents byte by byte, and a byte read
+// from LDS costs a fraction of one from global memory (the workflows' payloads are a few keys: C2's merges are
+// {orderId, step} documents of ~20 bytes)
+constexpr int KM_WORDS = 12;                 // 48-byte document slots: documents of <= 44 bytes
+constexpr int KM_STRIDE = 3 * KM_WORDS + 1;  // source, target, result; odd stride: distinct banks per lane
+
 __global__ void __launch_bounds__(256) k_merge(WaveParams P) {
   __shared__ unsigned long long s4[4];
+  __shared__ uint32_t s_m[256 * KM_STRIDE];
   const uint32_t n = P.merge_count[P.wave & 1];
   const MergeJob* jobs = P.merge_jobs + (uint64_t)(P.wave & 1) * P.job_cap;
   uint32_t* slow_n = P.merge_slow_count + (P.wave & 1);
+  uint32_t* reg = s_m + threadIdx.x * KM_STRIDE;
   unsigned long long merges = 0, bytes = 0;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const MergeJob j = jobs[i];
-    const uint8_t* sp = P.arena + (uint64_t)j.src * 8;
-    const uint8_t* tp = P.arena + (uint64_t)j.tgt * 8;
-    const uint32_t ns = *(const uint32_t*)sp, nt = *(const uint32_t*)tp;
+    const uint32_t* gs = (const uint32_t*)(P.arena + (uint64_t)j.src * 8);
+    const uint32_t* gt = (const uint32_t*)(P.arena + (uint64_t)j.tgt * 8);
+    const uint32_t ns = gs[0], nt = gt[0];
     uint8_t* dst = P.arena + (uint64_t)j.dst * 8;
     uint32_t olen = 0;
-    if (merge_flat(sp + 4, ns, tp + 4, nt, dst + 4, j.cap, olen)) {
-      *(uint32_t*)dst = olen;
+    bool done;
+    if (ns + nt + 3 <= 4 * KM_WORDS - 4) {  // (the result is at most ns + nt + 3 bytes)
+      for (uint32_t k = 0; k < (ns + 7) / 4; k++) reg[k] = gs[k];
+      for (uint32_t k = 0; k < (nt + 7) / 4; k++) reg[KM_WORDS + k] = gt[k];
+      uint8_t* lo = (uint8_t*)(reg + 2 * KM_WORDS);
+      done = merge_flat((const uint8_t*)reg + 4, ns, (const uint8_t*)(reg + KM_WORDS) + 4, nt, lo + 4,
+                        4 * KM_WORDS - 4, olen);
+      if (done) {
+        reg[2 * KM_WORDS] = olen;
+        for (uint32_t k = 0; k < (olen + 7) / 4; k++) ((uint32_t*)dst)[k] = reg[2 * KM_WORDS + k];
+      }
+    } else {
+      done = merge_flat((const uint8_t*)gs + 4, ns, (const uint8_t*)gt + 4, nt, dst + 4, j.cap, olen);
+      if (done) *(uint32_t*)dst = olen;
+    }
+    if (done) {
       merge_hint(P, j, olen);
       merges += 1;
       bytes += ns + nt + olen;
