@@ -10,6 +10,7 @@ python3 -c "import json; d=json.load(open('$O/bench_default.json')); print('C3',
 TAG=c3 BENCH_ARGS="--config c3" bash tools/gpu/prof_cfg.sh || exit 1
 TAG=c2s STEPS=5 BENCH_ARGS="--config c2 --steady" bash tools/gpu/prof_cfg.sh || exit 1
 TAG=c2w BENCH_ARGS="--config c2 --wave-only" bash tools/gpu/prof_cfg.sh || exit 1
+TAG=c5 BENCH_ARGS="--config c5" bash tools/gpu/prof_cfg.sh || exit 1
 SQ="GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_BUSY_CYCLES;SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD"
 TAG=c2s_1000000 PMC_STEPS=3 BENCH_ARGS="--config c2 --steady --no-extras" PMC_SETS="FETCH_SIZE;WRITE_SIZE;$SQ" bash tools/gpu/run_gpu_pmc.sh || exit 1
 PMC_SKIP_TICKS=1 python3 tools/pmc_summary.py gpurun_out/pmc_c2s_1000000 $O/pmc_c2s_1000000.json > $O/pmc_c2s_1000000.txt || exit 1

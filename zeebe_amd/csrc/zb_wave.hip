@@ -1594,7 +1594,8 @@ void launch_pre(const WaveParams& p, hipStream_t stream) {
   hipLaunchKernelGGL(k_pre, dim3(p.grid), dim3(WG), 0, stream, p);
 }
 void launch_children(const WaveParams& p, hipStream_t stream) {
-  hipLaunchKernelGGL(k_children, dim3(1024), dim3(256), 0, stream, p);
+  // (one workgroup per CU: in most waves of a tick with a cancellation no scope asks, and the launch exits at once)
+  hipLaunchKernelGGL(k_children, dim3(256), dim3(256), 0, stream, p);
 }
 void launch_process(const WaveParams& p, hipStream_t stream) {
   hipLaunchKernelGGL(k_process, dim3(p.grid), dim3(WG), 0, stream, p);
