@@ -7,6 +7,8 @@ O=gpurun_out/r04
 mkdir -p $O
 timeout -k 10 600 python3 -u bench.py > $O/bench_default.json 2> $O/bench_default.err || { echo "bench failed"; tail -5 $O/bench_default.err; exit 1; }
 python3 -c "import json; d=json.load(open('$O/bench_default.json')); print('C3', d['value']/1e9, 'G/s', d['ms_per_step'], 'ms', d['roofline']['kernel'], d['roofline']['frac']); [print(k, v['ms_per_step'], v['roofline']['frac']) for k, v in d.get('extras', {}).items()]"
+timeout -k 10 300 python3 -u bench.py --config c1 --steps 20 --warmup 2 > $O/bench_c1.json 2> $O/bench_c1.err || { echo "c1 failed"; tail -5 $O/bench_c1.err; exit 1; }
+timeout -k 10 400 python3 -u bench.py --config c5 --steps 3 --warmup 1 > $O/bench_c5.json 2> $O/bench_c5.err || { echo "c5 failed"; tail -5 $O/bench_c5.err; exit 1; }
 TAG=c3 BENCH_ARGS="--config c3" bash tools/gpu/prof_cfg.sh || exit 1
 TAG=c2s STEPS=5 BENCH_ARGS="--config c2 --steady" bash tools/gpu/prof_cfg.sh || exit 1
 TAG=c2w BENCH_ARGS="--config c2 --wave-only" bash tools/gpu/prof_cfg.sh || exit 1

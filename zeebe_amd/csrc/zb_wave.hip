@@ -1253,17 +1253,15 @@ __global__ void __launch_bounds__(WG) k_emit(WaveParams P) {
 // single-workgroup scan between the passes. The grid is persistent (every workgroup resident, tiles dealt
 // round-robin in increasing order), so a tile only ever waits for tiles that are already running.
 //
-// Look-back state: per tile 2 x LB_FIELDS 8-byte granules {tag, value} (agent-scope atomic stores and loads; the
-// data is its own flag, cdna_hip_programming.md Guideline 16 R2): the tile's aggregate (tag = epoch:AGG) and, once
-// known, its inclusive prefix (tag = epoch:INC) in a second set, so an aggregate is never overwritten. A reader
-// takes 64 predecessors per round in two hops: one granule each to find the nearest inclusive prefix, then the
-// aggregates up to it and that prefix (measured with the phase build: the one-set form, 8 predecessors per hop,
-// spent 54 % of k_wave's tile time in the look-back on C2). Waiting is bounded in time (the constant-rate wall clock, not a spin count:
+// Look-back state: per tile LB_FIELDS 8-byte granules {tag, value} (agent-scope atomic stores and loads; the
+// data is its own flag, cdna_hip_programming.md Guideline 16 R2). A tile first publishes its aggregate
+// (tag = epoch:AGG), then its inclusive prefix (tag = epoch:INC); a reader accepts a tile's granules only when
+// all of them carry the same tag. Waiting is bounded in time (the constant-rate wall clock, not a spin count:
 // a resident predecessor that the scheduler time-slices out keeps its waiters spinning without progress for
 // as long as it is descheduled): a hand-off that has not arrived after LB_TIMEOUT_TICKS sets DE_TIMEOUT, the
 // wave's results are void and the host stops the partition -- it never hangs the device.
-constexpr int LB_FIELDS = 8;  // rec wf job row bytes_lo bytes_hi merges conds
-constexpr int LB_ROUND = 64 / LB_FIELDS;  // predecessors per load round of a lane (hop B)
+constexpr int LB_FIELDS = 8;  // rec wf job row bytes_lo bytes_hi merges conds (8 predecessors per look-back round)
+constexpr int LB_ROUND = 64 / LB_FIELDS;  // predecessors read per look-back round
 constexpr int LB_STRIDE = 16;  // granules per tile (128 B)
 constexpr uint64_t LB_TIMEOUT_TICKS = 400000000ull;  // 4 s of the 100 MHz wall clock per look-back, then DE_TIMEOUT
 
@@ -1410,47 +1408,28 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
       wg_sb += sb;
     }
     if (wv == 0) {
-      const int f = lane & (LB_FIELDS - 1), sub = lane / LB_FIELDS;  // field; predecessor sub-slot (hop B)
+      const int f = lane % LB_FIELDS, j = lane / LB_FIELDS;  // field, predecessor distance - 1 (j < 8)
+      const bool lb_lane = lane < LB_ROUND * LB_FIELDS;
       const uint32_t my_agg = lane < LB_FIELDS ? s_agg[lane] : 0;
       uint64_t* lb = P.lookback + (uint64_t)tile * LB_STRIDE;
-      // the aggregate goes to granules [0, 8), the inclusive prefix to [8, 16); tile 0's aggregate is also its
-      // prefix (a reader that has not seen that prefix yet takes the empty start and tile 0's aggregate)
-      const uint32_t agg_f = __shfl(my_agg, f, 64);
-      if (lane < 2 * LB_FIELDS && (lane < LB_FIELDS || tile == 0))
-        __hip_atomic_store(lb + lane, ((uint64_t)(lane < LB_FIELDS ? tag_agg : tag_inc) << 32) | agg_f,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uint64_t acc = 0;  // lanes < 8: exclusive prefix of field `lane`
+      if (lane < LB_FIELDS)
+        __hip_atomic_store(lb + lane, ((uint64_t)(tile == 0 ? tag_inc : tag_agg) << 32) | my_agg, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      uint64_t acc = 0;  // lanes < 12: exclusive prefix of field `lane`
       if (lane == 0) s_void = 0;
       if (tile > 0) {
         bool timeout = false;
         const uint64_t t_start = wall_clock64();
-        for (int64_t base = tile - 1;;) {
-          // hop A: the nearest of the 64 predecessors base, base - 1, ... whose inclusive prefix is out (one
-          // granule each; before tile 0 lies the empty inclusive start)
-          const int64_t qa = base - lane;
-          bool inc = qa < 0;
-          if (qa >= 0)
-            inc = (uint32_t)(__hip_atomic_load(P.lookback + (uint64_t)qa * LB_STRIDE + LB_FIELDS, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT) >> 32) == tag_inc;
-          const uint64_t m_inc = __ballot(inc);
-          const int f0 = m_inc ? __builtin_ctzll(m_inc) : 64;
-          const int nd = f0 < 64 ? f0 + 1 : 64;
-          // hop B: field f of the aggregates of the predecessors before it and of its inclusive prefix (a granule
-          // of an earlier epoch, or one not published yet, carries another tag: wait for it). Lane = field f of
-          // predecessors sub, sub + 8, ...: all loads of a lane are independent
-          uint64_t x = 0;
-          for (int d = sub; d < nd && !timeout; d += LB_ROUND) {
-            const int64_t q = base - d;
-            if (q < 0) continue;
-            const bool want_inc = d == f0;
-            const uint64_t* g = P.lookback + (uint64_t)q * LB_STRIDE + (want_inc ? LB_FIELDS : 0) + f;
-            const uint32_t want = want_inc ? tag_inc : tag_agg;
+        for (int64_t p = tile - 1;;) {
+          const int64_t q = p - j;
+          uint32_t v = 0, tg = tag_inc;  // predecessors before tile 0 count as the (empty) inclusive start
+          if (lb_lane && q >= 0) {
+            const uint64_t* g = P.lookback + (uint64_t)q * LB_STRIDE + f;
             for (uint32_t spins = 0;; spins++) {
-              const uint64_t v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              if ((uint32_t)(v >> 32) == want) {
-                x += (uint32_t)v;
-                break;
-              }
+              const uint64_t x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              tg = (uint32_t)(x >> 32);
+              v = (uint32_t)x;
+              if (tg == tag_agg || tg == tag_inc) break;
               if ((spins & 255) == 255 &&
                   (wall_clock64() - t_start > LB_TIMEOUT_TICKS ||
                    (__hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & DE_TIMEOUT))) {
@@ -1460,13 +1439,33 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
               __builtin_amdgcn_s_sleep(1);
             }
           }
+          // a predecessor is usable when its LB_FIELDS granules carry one tag (a reader can catch it between its
+          // aggregate and inclusive publication): re-read the round otherwise. (Measured against a two-hop form with the
+// aggregates and prefixes in separate granule sets, 64 predecessors per round: 4 % slower on C2, same box. The
+// phase build shows why: the look-back's time is waiting for the predecessors' aggregates -- every tile of a round
+// needs all earlier tiles of the round processed -- not the hops.)
+          const uint64_t m_agg = __ballot(lb_lane && tg == tag_agg), m_inc = __ballot(!lb_lane || tg == tag_inc);
+          bool consistent = true, found = false;
+          int first = LB_ROUND;
+#pragma unroll
+          for (int k = 0; k < LB_ROUND; k++) {
+            const uint64_t gm = ((1ull << LB_FIELDS) - 1) << (LB_FIELDS * k);
+            const bool inc_k = (m_inc & gm) == gm, agg_k = (m_agg & gm) == gm;
+            if (!found) {
+              if (!inc_k && !agg_k) consistent = false;
+              if (inc_k) { first = k; found = true; }
+            }
+          }
           if (__ballot(timeout)) { timeout = true; break; }
-          // sum of field f over the lanes f, f + 8, ..., f + 56 (butterfly over the lane bits above the field)
+          if (!consistent) continue;  // same p again (bounded by the per-granule spins above)
+          // sum field f over predecessors j <= first: lanes f, f + 8, ..., f + 56 (butterfly over the lane bits
+          // above the field)
+          uint64_t x = (lb_lane && j <= first) ? (uint64_t)v : 0;
 #pragma unroll
           for (int d = LB_FIELDS; d < 64; d <<= 1) x += __shfl_xor(x, d, 64);
           if (lane < LB_FIELDS) acc += x;
-          if (f0 < 64) break;
-          base -= 64;
+          if (first < LB_ROUND) break;
+          p -= LB_ROUND;
         }
         if (__ballot(timeout) && lane == 0) {
           atomicOr(P.err, (uint32_t)DE_TIMEOUT);  // the others stop waiting too
@@ -1480,8 +1479,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
       if (tile > 0 && lane < LB_FIELDS) {
         const uint64_t incb = exb + tbytes;
         const uint32_t val = lane == 4 ? (uint32_t)incb : lane == 5 ? (uint32_t)(incb >> 32) : (uint32_t)(acc + my_agg);
-        __hip_atomic_store(lb + LB_FIELDS + lane, ((uint64_t)tag_inc << 32) | val, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(lb + lane, ((uint64_t)tag_inc << 32) | val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       if (lane < LB_FIELDS) {
         s_ex[lane] = lane == 4 ? exb : lane == 5 ? 0 : acc;
