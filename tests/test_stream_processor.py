@@ -109,12 +109,12 @@ def run_schedule(make_engine, rounds=9, snapshot_every=0, crash_rounds=(), crash
     log = Log()
     world = World(log, mid_creates, crash_batches)
     storage = SnapshotStorage()
-    stats = dict(incarnations=1, reprocessed=0, ticks=[], reconciled=0, resumed=0, written=0, splits=0)
+    stats = dict(incarnations=1, reprocessed=0, ticks=[], reconciled=0, resumed=0, written=0)
 
     def collect(c):
         stats["ticks"] += c.sp.ticks
         stats["reprocessed"] += c.reprocessed
-        for k in ("reconciled", "resumed", "written", "splits"):
+        for k in ("reconciled", "resumed", "written"):
             stats[k] += c.sp.stats[k]
 
     def make_processor(writer, has_next):

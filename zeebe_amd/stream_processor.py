@@ -24,7 +24,7 @@ in reference FIFO order, each with the engine position of the record that produc
 The processor therefore does not process its own follow-ups when it reads them back:
 
 * live: an input's ``processEvent`` stages it; the tick closes when the reader has caught up (or ``max_tick``
-  inputs are staged, or ``zb_submit`` reports a same-instance race: the staged part is stepped first). The tick's
+  inputs are staged; records of one instance may race inside a tick, the engine serialises them). The tick's
   follow-ups are written as one batch per processed record -- source position mapped from engine to log positions,
   producer id of the processor the reference would have written it with (70 workflow, 10 job, 90 message) -- so the
   log holds the bytes the reference writes, batch flags included.
@@ -34,8 +34,7 @@ The processor therefore does not process its own follow-ups when it reads them b
   reconciliation. A follow-up an earlier incarnation wrote after the snapshot is *reconciled*, not processed. Its
   tick's inputs are recovered from the log by the rule a live tick closes with: every input precedes its tick's
   first follow-up, and a live tick closes on its last input once the reader has caught up (so it holds every staged
-  input before its first follow-up), or on its ``max_tick``-th. The engine steps them without writing (splitting
-  at the same zb_submit race as the live tick did), and each follow-up it regenerates is matched, field by field,
+  input before its first follow-up), or on its ``max_tick``-th. The engine steps them without writing, and each follow-up it regenerates is matched, field by field,
   against the record already in the log; the generation-1 follow-ups (source = an input) are read before the tick
   is formed. An earlier incarnation that died while writing leaves a prefix: the rest is written once the reader
   has caught up. In the broker, another writer's command claimed between the reader catching up and the tick's
@@ -140,7 +139,7 @@ class GpuStreamProcessor:
         self.recovering = True                 # until the reader first catches up: no live tick is closed while
                                                # an earlier incarnation's follow-ups may still be unread
         self.ticks: List[dict] = []            # observers (tests): inputs of every engine tick, replayed or not
-        self.stats = {"reconciled": 0, "resumed": 0, "written": 0, "splits": 0}
+        self.stats = {"reconciled": 0, "resumed": 0, "written": 0}
 
     # ---- StreamProcessor
     def on_event(self, ev: dict):
@@ -184,46 +183,30 @@ class GpuStreamProcessor:
 
     # ---- ticks
     def _step(self, inputs: List[dict]) -> List[dict]:
-        """Runs inputs through the engine in as few ticks as zb_submit's race rules allow; returns the follow-ups
-        (frames with engine positions) and maps the inputs' engine positions to their log positions."""
-        from .engine import ZB_EUNSUPPORTED, ZbError
-
-        out: List[dict] = []
-        i = 0
-        while i < len(inputs):
-            base = self.engine.log_size()
-            n = 0
-            while i + n < len(inputs):
-                ev = inputs[i + n]
-                try:
-                    self.engine.submit_records([(ev["record_type"], ev["value_type"], ev["intent"], ev["key"],
-                                                 ev["value"])])
-                except ZbError as err:
-                    if err.code != ZB_EUNSUPPORTED or n == 0:
-                        raise
-                    self.stats["splits"] += 1
-                    break  # a same-instance race inside the tick: step what is staged, the rest follows
-                if ev["request_id"] != NULL_REQUEST_ID:
-                    self.engine.set_request_metadata([ev["request_id"]], [ev["request_stream_id"]])
-                n += 1
-            tick = inputs[i:i + n]
-            st = self.engine.step()
-            if not st["quiescent"]:
-                raise RuntimeError("engine did not reach quiescence")
-            end = self.engine.log_size()
-            for k, ev in enumerate(tick):
-                self.emap[base + k] = ev["position"]
-            frames = R.parse_frames(self.engine.frames(base + n, end - base - n, **self.frame_cfg)) if end > base + n \
-                else []
-            for f in frames:  # a CORRELATE's key is its log position (positionAsKey, SubscriptionApiCommandMessageHandler
-                src = f["source_position"]  # .java:146): the engine gives it, and its follow-ups, its engine position
-                if f["value_type"] == R.VT_WIS and base <= src < base + n and f["key"] == src:
-                    f["key"] = tick[src - base]["key"]
-            self.engine.release(end)  # (the frames are on the host; the device window moves on)
-            self.ticks.append({"inputs": [ev["position"] for ev in tick], "engine_base": base, "outputs": len(frames)})
-            out += frames
-            i += n
-        return out
+        """Runs the inputs through the engine as one tick (records of one instance may race in any order: zb_submit
+        marks the instance and zb_step serialises its records); returns the follow-ups (frames with engine
+        positions) and maps the inputs' engine positions to their log positions."""
+        base = self.engine.log_size()
+        n = len(inputs)
+        for ev in inputs:
+            self.engine.submit_records([(ev["record_type"], ev["value_type"], ev["intent"], ev["key"], ev["value"])])
+            if ev["request_id"] != NULL_REQUEST_ID:
+                self.engine.set_request_metadata([ev["request_id"]], [ev["request_stream_id"]])
+        st = self.engine.step()
+        if not st["quiescent"]:
+            raise RuntimeError("engine did not reach quiescence")
+        end = self.engine.log_size()
+        for k, ev in enumerate(inputs):
+            self.emap[base + k] = ev["position"]
+        frames = R.parse_frames(self.engine.frames(base + n, end - base - n, **self.frame_cfg)) if end > base + n \
+            else []
+        for f in frames:  # a CORRELATE's key is its log position (positionAsKey, SubscriptionApiCommandMessageHandler
+            src = f["source_position"]  # .java:146): the engine gives it, and its follow-ups, its engine position
+            if f["value_type"] == R.VT_WIS and base <= src < base + n and f["key"] == src:
+                f["key"] = inputs[src - base]["key"]
+        self.engine.release(end)  # (the frames are on the host; the device window moves on)
+        self.ticks.append({"inputs": [ev["position"] for ev in inputs], "engine_base": base, "outputs": len(frames)})
+        return frames
 
     def _write(self, frames: List[dict]) -> int:
         """One batch per processed record (consecutive follow-ups of one source), source / producer of the batch."""
@@ -293,7 +276,7 @@ class GpuStreamProcessor:
         """The tick whose generation-1 follow-ups are in run: every staged input before its first follow-up, at most
         max_tick -- exactly the inputs a live tick closes with (on its last input once the reader has caught up, or
         on its max_tick-th). (Inputs with no follow-up of their own, such as a JOB CREATED, are among them: moving
-        one into another tick could change where zb_submit's race rules split it.)"""
+        one into another tick could change the order in which the tick's racing records are serialised.)"""
         first = self.run[0]["position"]
         k = min(sum(1 for x in self.pending if x["position"] < first), self.max_tick)
         if k == 0:
