@@ -9,7 +9,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-fo
 f=$(find $O/prof -name '*kernel_stats.csv' | head -1); cp $f $O/kernel_stats.csv
 python3 - $O <<'PY'
 import csv, json, sys
-d = json.load(open(sys.argv[1] + '/bench.json'))
+d = json.loads([l for l in open(sys.argv[1] + '/bench.json').read().splitlines() if l.startswith('{')][-1])
 print(round(d['value'] / 1e9, 3), 'G/s', round(d['ms_per_step'], 3), 'ms/step', {k: round(x, 3) for k, x in d.get('step_breakdown_ms', {}).items()})
 rows = list(csv.DictReader(open(sys.argv[1] + '/kernel_stats.csv')))
 tot = sum(float(r['TotalDurationNs']) for r in rows)
