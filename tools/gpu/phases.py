@@ -34,10 +34,11 @@ def main():
         d = {k: p1[k] - p0[k] for k in p1}
         tot = d["process"] + d["lookback"] + d["emit"]
         print("step %d: %.2f ms, waves %d, wave kernels %.2f ms; tiles %d; per tile us: process %.2f lookback %.2f "
-              "emit %.2f; shares %.2f / %.2f / %.2f" % (
+              "emit %.2f; shares %.2f / %.2f / %.2f; look-back rounds per tile %.1f" % (
                   it, (t1 - t0) * 1e3, st["waves"], st["wave_kernel_ms"], d["tiles"],
                   d["process"] / 100 / max(d["tiles"], 1), d["lookback"] / 100 / max(d["tiles"], 1),
-                  d["emit"] / 100 / max(d["tiles"], 1), d["process"] / tot, d["lookback"] / tot, d["emit"] / tot),
+                  d["emit"] / 100 / max(d["tiles"], 1), d["process"] / tot, d["lookback"] / tot, d["emit"] / tot,
+                  d["rounds"] / max(d["tiles"], 1)),
               flush=True)
     eng.close()
 

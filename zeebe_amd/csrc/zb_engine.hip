@@ -1242,11 +1242,11 @@ void zb_engine_destroy(zb_engine* e) {
 
 #ifdef ZB_PHASES
 // the measurement build's k_wave phase sums since the engine was created (wall-clock ticks of 10 ns, summed over
-// workgroups): [0] process + tile scan, [1] look-back, [2] emit, [3] tiles
-int zb_phase_times(zb_engine* e, unsigned long long* out4) {
-  if (!e || !out4) return ZB_EINVAL;
+// workgroups): [0] process + tile scan, [1] look-back, [2] emit, [3] tiles, [4] look-back rounds
+int zb_phase_times(zb_engine* e, unsigned long long* out5) {
+  if (!e || !out5) return ZB_EINVAL;
   HIPCHECK(e, hipStreamSynchronize(e->stream));
-  HIPCHECK(e, hipMemcpy(out4, e->phase, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  HIPCHECK(e, hipMemcpy(out5, e->phase, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return ZB_OK;
 }
 #endif

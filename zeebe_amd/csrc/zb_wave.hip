@@ -1302,7 +1302,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
   uint64_t wg_sa = 0, wg_sb = 0;
 
 #ifdef ZB_PHASES
-  uint64_t ph_t = wall_clock64(), ph[4] = {0, 0, 0, 0};
+  uint64_t ph_t = wall_clock64(), ph[4] = {0, 0, 0, 0};  // process, look-back, emit, look-back rounds
 #define ZB_PHASE(k) do { const uint64_t ph_n = wall_clock64(); ph[k] += ph_n - ph_t; ph_t = ph_n; } while (0)
 #else
 #define ZB_PHASE(k) do { } while (0)
@@ -1421,6 +1421,9 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
         bool timeout = false;
         const uint64_t t_start = wall_clock64();
         for (int64_t p = tile - 1;;) {
+#ifdef ZB_PHASES
+          if (lane == 0) ph[3] += 1;  // look-back rounds (8 predecessors each)
+#endif
           const int64_t q = p - j;
           uint32_t v = 0, tg = tag_inc;  // predecessors before tile 0 count as the (empty) inclusive start
           if (lb_lane && q >= 0) {
@@ -1539,6 +1542,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
 #ifdef ZB_PHASES
   if (threadIdx.x == 0 && P.phase) {
     for (int k = 0; k < 3; k++) atomicAdd(P.phase + k, (unsigned long long)ph[k]);
+    atomicAdd(P.phase + 4, (unsigned long long)ph[3]);
     atomicAdd(P.phase + 3, (unsigned long long)((ntiles - blockIdx.x + gridDim.x - 1) / gridDim.x));
   }
 #endif

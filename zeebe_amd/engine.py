@@ -424,10 +424,10 @@ class Engine:
     def phase_times(self):
         """(measurement build ZB_PHASES_LIBRARY=1 only) k_wave's wall-clock ticks (10 ns) per phase, summed over its
         workgroups: process + tile scan, look-back, emit, and the tiles processed."""
-        out = (ctypes.c_ulonglong * 4)()
+        out = (ctypes.c_ulonglong * 5)()
         self._L.zb_phase_times.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         self._check(self._L.zb_phase_times(self._h, out))
-        return dict(process=out[0], lookback=out[1], emit=out[2], tiles=out[3])
+        return dict(process=out[0], lookback=out[1], emit=out[2], tiles=out[3], rounds=out[4])
 
     def memory_stats(self) -> dict:
         m = zb_memory_stats()
