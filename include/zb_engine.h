@@ -244,6 +244,12 @@ int zb_submit_messages(zb_engine* e, const zb_rec_desc* recs, size_t n, const ui
  * (correlation keys / payloads concatenated, n+1 offsets each): same processing as zb_submit_messages. */
 int zb_submit_publishes(zb_engine* e, const char* message_name, int64_t ttl, size_t n, const uint8_t* cks,
                         const uint64_t* ck_offsets, const uint8_t* payloads, const uint64_t* payload_offsets);
+/* zb_submit_publishes in two parts: the batch goes to HBM (zb_upload_publishes; any partition state, returns when
+ * the data is resident) and is processed later (zb_publish_uploaded; quiescent, nothing staged) -- so a broker
+ * overlaps the next batch's PCIe copy with the current tick. Another upload replaces a batch not processed yet. */
+int zb_upload_publishes(zb_engine* e, const char* message_name, int64_t ttl, size_t n, const uint8_t* cks,
+                        const uint64_t* ck_offsets, const uint8_t* payloads, const uint64_t* payload_offsets);
+int zb_publish_uploaded(zb_engine* e);
 /* MessageTimeToLiveChecker.run (MessageTimeToLiveChecker.java:44-68) at now_ms: a DELETE command for every
  * stored message with deadline <= now_ms, in store order, then their processing. *n_deleted = commands written. */
 int zb_expire_messages(zb_engine* e, int64_t now_ms, uint64_t* n_deleted);

@@ -62,6 +62,15 @@ struct DevVec {
 
 }  // namespace
 
+// a PUBLISH batch resident in p_in (zb_upload_publishes): byte offsets of its pieces
+struct PubUpload {
+  bool valid;
+  uint64_t n;
+  uint32_t nn;
+  int64_t ttl;
+  uint64_t a_ck, a_cko, a_pl, a_plo, a_name;
+};
+
 struct zb_engine {
   zb_config cfg{};
   hipStream_t stream = nullptr;
@@ -127,6 +136,7 @@ struct zb_engine {
                                    // [6..7] merges left to the general merger
   uint32_t* merge_slow = nullptr;  // [job_cap] indices of those merges
   unsigned long long* phase = nullptr;  // (ZB_PHASES measurement build) k_wave phase sums
+  PubUpload pub_up{};                   // a PUBLISH batch uploaded by zb_upload_publishes, not processed yet
   uint8_t* xslab = nullptr;        // exact payload tree workspaces (zb_xmerge.hpp), with a model that merges / maps
   uint32_t* xlocks = nullptr;
   uint64_t* sub_jobs = nullptr;    // [job_cap] subscribe steps of a wave (models with message catch events)
@@ -3087,20 +3097,19 @@ int zb_submit_messages(zb_engine* e, const zb_rec_desc* recs, size_t n, const ui
   return process_messages(e, b);
 }
 
-int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, const uint8_t* cks,
+int zb_upload_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, const uint8_t* cks,
                         const uint64_t* ck_offsets, const uint8_t* payloads, const uint64_t* payload_offsets) {
   if (!e || !name || (n > 0 && (!cks || !ck_offsets || !payloads || !payload_offsets))) return ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
-  int rc = require_idle(e);
-  if (rc != ZB_OK) return rc;
+  e->pub_up.valid = false;
   if (n == 0) return ZB_OK;
   const uint32_t nn = (uint32_t)std::strlen(name);
-  rc = ensure_stores(e);
-  if (rc == ZB_OK) rc = maintain(e, false);
+  int rc = ensure_stores(e);
   if (rc != ZB_OK) return rc;
   // The caller's correlation keys / payloads go up as they are (one pinned staging copy, by up to 8 host
   // threads for large batches); the commands and message blobs are built on the device (k_pub_sizes / scan /
-  // k_pub_build, zb_msg.hip) -- all-or-nothing: nothing reaches the log or the arena before the checks pass.
+  // k_pub_build, zb_msg.hip) when the batch is processed -- all-or-nothing: nothing reaches the log or the arena
+  // before the checks pass.
   const uint64_t ckb = ck_offsets[n] - ck_offsets[0], plb = payload_offsets[n] - payload_offsets[0];
   const uint64_t offb = (n + 1) * sizeof(uint64_t);
   const uint64_t a_ck = 0, a_cko = (ckb + 15) & ~15ull, a_pl = a_cko + offb, a_plo = a_pl + ((plb + 15) & ~15ull);
@@ -3129,14 +3138,30 @@ int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, c
   if (rc == ZB_OK) rc = grow_dev(e, &e->m_prior, &e->m_prior_cap, n);
   if (rc != ZB_OK) return rc;
   HIPCHECK(e, hipMemcpyAsync(e->p_in, stage, total, hipMemcpyHostToDevice, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));  // (resident; the staging memory is free again)
+  e->pub_up = PubUpload{true, n, nn, ttl, a_ck, a_cko, a_pl, a_plo, a_name};
+  return ZB_OK;
+}
+
+int zb_publish_uploaded(zb_engine* e) {
+  if (!e) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  if (!e->pub_up.valid) return fail(e, ZB_EINVAL, "no uploaded publish batch (zb_upload_publishes)");
+  int rc = require_idle(e);
+  if (rc != ZB_OK) return rc;
+  rc = maintain(e, false);
+  if (rc != ZB_OK) return rc;
+  const PubUpload u = e->pub_up;
+  e->pub_up.valid = false;
+  const uint64_t n = u.n;
   PubBuild pb{};
-  pb.cks = e->p_in + a_ck;
-  pb.ck_off = (const uint64_t*)(e->p_in + a_cko);
-  pb.pls = e->p_in + a_pl;
-  pb.pl_off = (const uint64_t*)(e->p_in + a_plo);
-  pb.name = e->p_in + a_name;
-  pb.nn = nn;
-  pb.ttl = ttl;
+  pb.cks = e->p_in + u.a_ck;
+  pb.ck_off = (const uint64_t*)(e->p_in + u.a_cko);
+  pb.pls = e->p_in + u.a_pl;
+  pb.pl_off = (const uint64_t*)(e->p_in + u.a_plo);
+  pb.name = e->p_in + u.a_name;
+  pb.nn = u.nn;
+  pb.ttl = u.ttl;
   pb.n = n;
   pb.gran = e->p_gran;
   pb.goff = e->p_gran + (n + 1);
@@ -3161,6 +3186,17 @@ int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, c
   HIPCHECK(e, hipMemsetAsync(e->m_prior, 0, n, e->stream));  // (no message ids: no duplicates)
   std::vector<std::pair<uint64_t, uint8_t>> runs{{n, (uint8_t)0}};
   return process_uploaded_messages(e, n, gran * 8, runs);
+}
+
+int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, const uint8_t* cks,
+                        const uint64_t* ck_offsets, const uint8_t* payloads, const uint64_t* payload_offsets) {
+  if (!e || !name || (n > 0 && (!cks || !ck_offsets || !payloads || !payload_offsets))) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  int rc = require_idle(e);
+  if (rc != ZB_OK) return rc;
+  if (n == 0) return ZB_OK;
+  rc = zb_upload_publishes(e, name, ttl, n, cks, ck_offsets, payloads, payload_offsets);
+  return rc == ZB_OK ? zb_publish_uploaded(e) : rc;
 }
 
 int zb_expire_messages(zb_engine* e, int64_t now_ms, uint64_t* n_deleted) {

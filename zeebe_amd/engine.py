@@ -158,6 +158,9 @@ def lib():
         u64p = ctypes.POINTER(ctypes.c_uint64)
         L.zb_submit_publishes.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.zb_upload_publishes.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.zb_publish_uploaded.argtypes = [vp]
         L.zb_inbox_submit.argtypes = [vp, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         L.zb_outbox_count.argtypes = [vp, ctypes.c_int, u64p]
         L.zb_outbox_take.argtypes = [vp, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, u64p, u64p, u64p]
@@ -196,7 +199,8 @@ def lib():
 
 EXPORTED_SYMBOLS = ["zb_engine_create", "zb_engine_destroy", "zb_last_error", "zb_reset", "zb_deploy",
                     "zb_set_job_completion_payload", "zb_submit_creates", "zb_step", "zb_log_size",
-                    "zb_read_descriptors", "zb_drain", "zb_counters", "zb_submit_publishes", "zb_inbox_submit",
+                    "zb_read_descriptors", "zb_drain", "zb_counters", "zb_submit_publishes", "zb_upload_publishes",
+                    "zb_publish_uploaded", "zb_inbox_submit",
                     "zb_outbox_count", "zb_outbox_take", "zb_comm_unique_id", "zb_comm_init", "zb_comm_pending",
                     "zb_comm_exchange", "zb_submit", "zb_read_instances", "zb_snapshot", "zb_restore",
                     "zb_validate_deployment", "zb_serialize", "zb_drain_copy", "zb_pinned_alloc", "zb_pinned_free",
@@ -553,6 +557,23 @@ class Engine:
         n = len(ck_off) - 1
         self._check(self._L.zb_submit_publishes(self._h, name, ttl, n, ck_blob, ck_off.ctypes.data, pl_blob,
                                                 pl_off.ctypes.data))
+
+    def upload_publishes_packed(self, name: bytes, ck_blob: bytes, ck_off, pl_blob: bytes, pl_off,
+                                ttl: int = 3600000):
+        """zb_upload_publishes: publish_packed's batch to HBM now, processed by publish_uploaded()."""
+        import numpy as np
+
+        if isinstance(name, str):
+            name = name.encode()
+        ck_off = np.ascontiguousarray(ck_off, dtype=np.uint64)
+        pl_off = np.ascontiguousarray(pl_off, dtype=np.uint64)
+        n = len(ck_off) - 1
+        self._check(self._L.zb_upload_publishes(self._h, name, ttl, n, ck_blob, ck_off.ctypes.data, pl_blob,
+                                                pl_off.ctypes.data))
+
+    def publish_uploaded(self):
+        """zb_publish_uploaded: the uploaded PUBLISH batch's commands, processed."""
+        self._check(self._L.zb_publish_uploaded(self._h))
 
     def submit_messages(self, recs):
         """zb_submit_messages: recs = [(intent, key, MessageRecord value bytes), ...] (MESSAGE commands: PUBLISH 0,
