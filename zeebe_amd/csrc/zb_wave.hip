@@ -24,8 +24,6 @@ namespace zbg {
 
 constexpr int WG = WAVE_TILE;
 constexpr int MAX_SLOTS = 2;  // output records per item (one parent's batch emits <= 2 in every handler)
-constexpr int SLOT_STRIDE_W = 26;  // k_wave: dwords per thread's slot pair (2 x 48 B + 8 B of padding)
-static_assert(SLOT_STRIDE_W * 4 >= MAX_SLOTS * 48 && (SLOT_STRIDE_W * 4) % 8 == 0, "slot stride");
 
 enum SlotFlags : uint8_t {
   SF_KEY_WF = 1,       // key = new wf key #ord
@@ -1272,9 +1270,7 @@ __device__ __forceinline__ uint32_t lb_tag(int64_t epoch, uint32_t inc) {
 }
 
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8))) k_wave(WaveParams P) {
-  // each thread's MAX_SLOTS slots at a stride of 26 dwords (104 B, 8-aligned): at the packed 24-dword stride the
-  // lanes of a wave hit 8 banks (PMC: 0.46 of LDS cycles in bank conflicts on C2), at 26 they spread over 32
-  __shared__ __attribute__((aligned(16))) uint32_t s_slot_words[WG * SLOT_STRIDE_W];
+  __shared__ Slot s_slots[WG * MAX_SLOTS];
   __shared__ uint64_t s_a[WG / 64], s_b[WG / 64];
   __shared__ uint64_t s_st[WG / 64][2];  // transitions | completed << 32, created | canceled << 32
   __shared__ uint64_t s_ex[LB_FIELDS];   // the tile's exclusive prefix
@@ -1316,7 +1312,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
     const int64_t r = c.begin + i;
     // ---- process (k_process)
     TState t;
-    t.s = (Slot*)(s_slot_words + threadIdx.x * SLOT_STRIDE_W);
+    t.s = s_slots + threadIdx.x * MAX_SLOTS;
     t.ns = t.nwf = t.njob = t.nrow = 0;
     t.bytes = 0; t.merge = false; t.detail = false; t.err = 0; t.err_site = 0;
     t.transitions = t.completed = t.created = t.merges = t.canceled = 0;
@@ -1531,7 +1527,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
       const uint64_t cond_j = s_ex[7] + (b >> 52);
       ItemInfo inf{};
       if (we & ((1ull << CW_MERGE) | (1ull << CW_DETAIL))) inf = P.info[i];
-      emit_item(P, c, i, we, (const Slot*)(s_slot_words + threadIdx.x * SLOT_STRIDE_W), inf, out_rec, wf0, job0, row0, bump, merge_j, cond_j,
+      emit_item(P, c, i, we, s_slots + threadIdx.x * MAX_SLOTS, inf, out_rec, wf0, job0, row0, bump, merge_j, cond_j,
                 wf_next, job_next, par);
     }
     __syncthreads();  // LDS slots and scan scratch are reused by the next tile
