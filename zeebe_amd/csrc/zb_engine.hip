@@ -7,6 +7,7 @@
 // reported as ZB_EUNSUPPORTED.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 #include <rccl/rccl.h>
 
 #include <dlfcn.h>
@@ -198,7 +199,8 @@ struct zb_engine {
   MergeGen* t_mgen = nullptr;     // [TRAJ_MAX_GENERATIONS] uniform batch merge slots
   uint64_t* t_wstats = nullptr;   // [t_nwg_cap + CLS_MAX][6] emit statistics per workgroup
   TrajCtl* h_ctl_pinned = nullptr;
-  uint64_t* h_stats_pinned = nullptr;  // [0..7] counters before a step, [8..15] after, [16] a class batch's ClsPlan.nc
+  uint64_t* h_stats_pinned = nullptr;  // [0..7] counters before a step, [8..15] after, [16] a class batch's ClsPlan.nc,
+                                       // [17] sort_pairs' key spread, [18] the waves counter before a wave loop
   // class batches (zb_traj.hip k_cls_*): the model's exclusive splits as outcome-key digits
   bool cls_ok = false;            // split outcome keys fit 8 bits and CLS_MAX_SPLITS splits
   int nsplits = 0;
@@ -262,8 +264,11 @@ struct zb_engine {
   uint64_t* ob_first = nullptr;  // [65]
   uint32_t *ob_sizes = nullptr, *ob_goff = nullptr;
   uint64_t *ob_table = nullptr, *ob_base = nullptr;
-  void* ob_tmp = nullptr;
+  void* ob_tmp = nullptr;  // (scan scratch)
   size_t ob_tmp_bytes = 0;
+  int wave_hint = 0;     // non-empty waves of the last step's wave loop (its first batch, zb_step)
+  int ob_plan_kind = 0;  // the outbox kind outbox_plan sorted and sized last (0: none)
+  uint64_t ob_plan_n = 0, ob_plan_total = 0, ob_plan_base[64] = {};
   uint8_t* ob_staging = nullptr;
   uint64_t ob_staging_cap = 0;
 
@@ -304,14 +309,14 @@ struct zb_engine {
   // inbox CORRELATE resolution by activity instance key (zb_inbox_submit)
   int64_t *x_keys = nullptr, *x_pos = nullptr, *x_keys2 = nullptr, *x_pos2 = nullptr;
   uint64_t x_cap = 0;
-  void* x_tmp = nullptr;
-  size_t x_tmp_cap = 0;
   DevVec<int64_t> d_lookup_keys, d_lookup_pos;    // zb_submit lookups of the staged batch: key, staged index
   uint64_t staged_nlook = 0;
   int64_t *look_keys = nullptr, *look_idx = nullptr;  // sorted on the device by zb_step
   uint64_t look_cap = 0;
-  void* look_tmp = nullptr;
-  size_t look_tmp_cap = 0;
+  // radix sorts of (key, value) pairs (sort_pairs): scratch and the spread of the keys
+  uint8_t* sort_tmp = nullptr;
+  uint64_t sort_tmp_cap = 0;
+  uint64_t* d_spread = nullptr;
   // drain buffers (zb_serialize), grown on demand and reused
   uint64_t dr_cap = 0, dr_val_cap = 0, dr_tmp_cap = 0;
   uint32_t* dr_len = nullptr;  // value lengths
@@ -319,7 +324,7 @@ struct zb_engine {
   uint8_t* h_stage = nullptr;    // pinned staging of host-built uploads (zb_submit_publishes)
   size_t h_stage_cap = 0;
   uint32_t* dr_list = nullptr;   // tiles the first fast pass leaves to the wide one
-  uint32_t* dr_list2 = nullptr;  // tiles the wide fast pass leaves to k_ser_write
+  uint32_t* dr_list2 = nullptr;  // tiles for k_ser_write (left by either fast pass)
   uint32_t dr_wide_tiles = 0;    // tiles the last drain's wide fast pass encoded
   uint32_t dr_slow_tiles = 0;    // how many tiles the last drain ran through k_ser_write
   bool dr_split = false;         // the last drain ran k_ser_fast + k_ser_write (events 2-4, 5-3)
@@ -813,6 +818,50 @@ int ensure_stores(zb_engine* e) {
 
 
 // the partition must be idle for a message-side batch (canonical schedule, zeebe_amd/cluster.py)
+// Radix sort of (key, value) pairs by 64-bit keys, stable, into kout / vout. Only the key bits that differ
+// between the keys are sorted (k_key_spread; the others are equal in every key): the outbox keys (target, source
+// position, emission) and the instance keys of a tick span ~25 of their 64 bits, so Onesweep makes 4 passes
+// instead of 8. Always Onesweep: rocprim's default takes its merge sort below 2^20 pairs, which made 21 launches
+// and ~190 us of a 1M-pair outbox on MI355X (C5 kernel trace, round 4). Signed keys: the sign flip of the radix
+// order is the same in every key, so the differing bits are those of the raw keys.
+using OnesweepSort = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                rocprim::default_config, 0>;
+template <class K, class V>
+int sort_pairs(zb_engine* e, const K* kin, K* kout, const V* vin, V* vout, uint64_t n, const char* what) {
+  static_assert(sizeof(K) == 8, "64-bit keys");
+  if (n == 0) return ZB_OK;
+  if (n > (uint64_t)INT32_MAX) return fail(e, ZB_EUNSUPPORTED, std::string(what) + ": more than 2^31 keys");
+  HIPCHECK(e, hipMemsetAsync(e->d_spread, 0, sizeof(uint64_t), e->stream));
+  launch_key_spread((const uint64_t*)kin, n, e->d_spread, e->stream);
+  HIPCHECK(e, hipMemcpyAsync(e->h_stats_pinned + 17, e->d_spread, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  const uint64_t spread = e->h_stats_pinned[17];
+  if (spread == 0) {  // one key (or all equal): the input order
+    HIPCHECK(e, hipMemcpyAsync(kout, kin, n * sizeof(K), hipMemcpyDeviceToDevice, e->stream));
+    HIPCHECK(e, hipMemcpyAsync(vout, vin, n * sizeof(V), hipMemcpyDeviceToDevice, e->stream));
+    return ZB_OK;
+  }
+  const unsigned begin = (unsigned)__builtin_ctzll(spread), end = 64u - (unsigned)__builtin_clzll(spread);
+  size_t need = 0;
+  if (rocprim::radix_sort_pairs<OnesweepSort>(nullptr, need, kin, kout, vin, vout, (size_t)n, begin, end,
+                                              e->stream) != hipSuccess)
+    return fail(e, ZB_EDEVICE, std::string(what) + ": sort sizing");
+  if (need + 16 > e->sort_tmp_cap) {
+    HIPCHECK(e, hipStreamSynchronize(e->stream));
+    if (e->sort_tmp) (void)hipFree(e->sort_tmp);
+    e->sort_tmp = nullptr;
+    e->sort_tmp_cap = 0;
+    const uint64_t c = std::max<uint64_t>(need + need / 2 + 16, 1 << 20);
+    HIPCHECK(e, hipMalloc(&e->sort_tmp, c));
+    e->sort_tmp_cap = c;
+  }
+  size_t have = e->sort_tmp_cap;
+  if (rocprim::radix_sort_pairs<OnesweepSort>(e->sort_tmp, have, kin, kout, vin, vout, (size_t)n, begin, end,
+                                              e->stream) != hipSuccess)
+    return fail(e, ZB_EDEVICE, std::string(what) + ": sort");
+  return ZB_OK;
+}
+
 int require_idle(zb_engine* e) {
   if (e->failed) return fail(e, ZB_EPROCESSING, "partition stopped after a processing failure: " + e->err);
   if (e->host_hdr.begin != e->host_hdr.end || (e->staged_pending && !e->staged.empty()))
@@ -1173,7 +1222,8 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipHostMalloc(&e->h_hdr_pinned, 2 * sizeof(WaveHdr)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_err_pinned, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_ctl_pinned, sizeof(TrajCtl)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipHostMalloc(&e->h_stats_pinned, 17 * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipHostMalloc(&e->h_stats_pinned, 19 * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->d_spread, sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_ctl, sizeof(TrajCtl)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_wtot, TRAJ_WAVE_CAP * sizeof(uint4)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_wbase, TRAJ_WAVE_CAP * sizeof(TrajBase)) != hipSuccess) return cleanup(ZB_ENOMEM);
@@ -1208,12 +1258,12 @@ void zb_engine_destroy(zb_engine* e) {
     if (x) (void)hipEventDestroy(x);
   void* ps[] = {e->vlen_mem, e->vlen_bad, e->jobs.keys, e->jobs.state, e->jobs.tombs, e->c_flag, e->c_new, e->c_tmp,
                 e->c_scratch, e->c_bits, e->c_pop, e->c_off, e->c_count, e->x_keys, e->x_pos, e->x_keys2, e->x_pos2,
-                e->x_tmp, e->mapres, e->map_ws, e->log_mem, e->links_mem, e->srcd_mem, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
+                e->sort_tmp, e->d_spread, e->mapres, e->map_ws, e->log_mem, e->links_mem, e->srcd_mem, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
                 e->merge_jobs, e->merge_slow, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_clen, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
                 e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->need_children, e->look_keys, e->look_idx,
-                e->look_tmp, e->conf_first, e->xslab, e->xlocks, e->phase};
+                e->conf_first, e->xslab, e->xlocks, e->phase};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->comm) (void)ncclCommDestroy(e->comm);
@@ -2114,22 +2164,9 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
         HIPCHECK(e, hipMalloc(&e->look_idx, c * sizeof(int64_t)));
         e->look_cap = c;
       }
-      size_t tmp = 0;
-      if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, e->d_lookup_keys.p, e->look_keys, e->d_lookup_pos.p,
-                                             e->look_idx, (int)m, 0, 64, e->stream) != hipSuccess)
-        return fail(e, ZB_EDEVICE, "lookup sort sizing");
-      if (tmp > e->look_tmp_cap) {
-        HIPCHECK(e, hipStreamSynchronize(e->stream));
-        if (e->look_tmp) (void)hipFree(e->look_tmp);
-        e->look_tmp = nullptr;
-        e->look_tmp_cap = 0;
-        HIPCHECK(e, hipMalloc(&e->look_tmp, tmp + 16));
-        e->look_tmp_cap = tmp;
-      }
-      tmp = e->look_tmp_cap;
-      if (hipcub::DeviceRadixSort::SortPairs(e->look_tmp, tmp, e->d_lookup_keys.p, e->look_keys, e->d_lookup_pos.p,
-                                             e->look_idx, (int)m, 0, 64, e->stream) != hipSuccess)
-        return fail(e, ZB_EDEVICE, "lookup sort");
+      int rc = sort_pairs(e, (const int64_t*)e->d_lookup_keys.p, e->look_keys, (const int64_t*)e->d_lookup_pos.p,
+                          e->look_idx, m, "lookup");
+      if (rc != ZB_OK) return rc;
       ResolveParams rp{};
       rp.rmeta = e->rmeta; rp.rkeys = e->rkeys; rp.rows = (uint64_t)e->host_hdr.rows_next;
       rp.keys = e->look_keys; rp.pos = e->look_idx; rp.pos_base = ip.log_base; rp.n = (int64_t)m;
@@ -2169,10 +2206,18 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     if (rc < 0) return rc;
     quiescent = e->host_hdr.begin == e->host_hdr.end;
   }
-  int next_batch = WAVES_PER_SYNC;
+  // the first batch: as many waves as the last step's wave loop had (a tick of the same workload settles in as
+  // many waves, and each launch past quiescence costs ~20 us of empty kernels), else WAVES_PER_SYNC; later
+  // batches WAVES_PER_SYNC, doubling
+  int next_batch = e->wave_hint > 0 ? std::min<int>(e->wave_hint, WAVES_PER_SYNC_MAX) : WAVES_PER_SYNC;
+  const bool loop = !quiescent && (max_waves == 0 || launched < max_waves);
+  if (loop) HIPCHECK(e, hipMemcpyAsync(e->h_stats_pinned + 18, e->dstats + 6, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                       e->stream));  // (the waves counter before the loop)
+  bool first_batch = true;
   while (!quiescent && (max_waves == 0 || launched < max_waves)) {
     int batch = next_batch;
-    next_batch = std::min(2 * next_batch, WAVES_PER_SYNC_MAX);
+    next_batch = first_batch ? WAVES_PER_SYNC : std::min(2 * next_batch, WAVES_PER_SYNC_MAX);
+    first_batch = false;
     if (max_waves) batch = std::min<int>(batch, (int)(max_waves - launched));
     // timing events cost ~5 us of stream time each between kernels (C2: 4 per wave = 2.9 ms of a 41 ms
     // step): per wave only with ZB_CFG_WAVE_EVENTS (process / emit / aux split), else one pair per batch
@@ -2244,6 +2289,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   }
   HIPCHECK(e, hipMemcpyAsync(stats_after, e->dstats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
+  if (loop && quiescent) e->wave_hint = (int)(stats_after[6] - e->h_stats_pinned[18]);  // the loop's non-empty waves
   st.records_processed = (uint64_t)(e->host_hdr.begin - processed_from);
   st.records_written = (uint64_t)(e->host_hdr.end - written_from);
   st.transitions = stats_after[0] - stats_before[0];
@@ -2568,32 +2614,38 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
       wr.tile_offs = e->dr_off;
       e->dr_split = e->ser_fast && !fc && sp.seg_lds && sp.arena_bytes;
       if (e->dr_split) {  // k_ser_fast, then k_ser_write over the tiles it left
-        // pass 1 over every tile (k_ser_wave, 11 KB per wave) -> list A; pass 2 over A (40 KB phase form) -> list B;
+        // pass 1 over every tile (k_ser_wave, 11 KB per wave) -> list A (a value over its image) and list B (a
+        // record kind the fast encoder does not take); pass 2 over A (40 KB phase form) -> more of list B;
         // k_ser_write over B
         uint32_t* cnt = (uint32_t*)(e->dr_total + 3);  // [0] list A, [1] list B (zeroed with dr_total)
         wr.tile_list = e->dr_list;
+        wr.tile_list_slow = e->dr_list2;
         wr.tile_list_n = cnt;
         launch_ser_fast(wr, e->stream);
         HIPCHECK(e, hipEventRecord(e->dr_ev[4], e->stream));
         HIPCHECK(e, hipMemcpyAsync(e->h_dr_total + 3, e->dr_total + 3, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
         HIPCHECK(e, hipStreamSynchronize(e->stream));
-        uint32_t nA = ((const uint32_t*)(e->h_dr_total + 3))[0], nB = 0;
+        const uint32_t nA = ((const uint32_t*)(e->h_dr_total + 3))[0];
+        uint32_t nB = ((const uint32_t*)(e->h_dr_total + 3))[1];
         HIPCHECK(e, hipEventRecord(e->dr_ev[5], e->stream));  // (the host round trips are not write-pass time)
+        const uint32_t nB1 = nB;
         if (nA) {
           SerParams w2 = wr;
           w2.tile_list_in = e->dr_list;
-          w2.tile_list = e->dr_list2;
+          w2.tile_list = e->dr_list2;  // (appended after pass 1's entries)
           w2.tile_list_n = cnt + 1;
           launch_ser_fast_wide(w2, nA, e->stream);
           HIPCHECK(e, hipMemcpyAsync(e->h_dr_total + 3, e->dr_total + 3, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
           HIPCHECK(e, hipStreamSynchronize(e->stream));
           nB = ((const uint32_t*)(e->h_dr_total + 3))[1];
+        }
+        if (nB) {
           SerParams w3 = wr;
           w3.tile_list_in = e->dr_list2;
           launch_ser_write_list(w3, nB, e->stream);
         }
         e->dr_slow_tiles = nB;
-        e->dr_wide_tiles = nA - nB;
+        e->dr_wide_tiles = nA - (nB - nB1);
         launch_ser_sum(wr, e->stream);
       } else {
         e->dr_slow_tiles = (uint32_t)tiles;
@@ -2976,16 +3028,8 @@ int deliver(zb_engine* e, int kind, const uint8_t* buf, const std::vector<uint64
     p.lookup_keys = e->x_keys;
     p.lookup_pos = e->x_pos;
     launch_wis_inject(p, e->stream);
-    size_t tmp = 0;
-    if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, e->x_keys, e->x_keys2, e->x_pos, e->x_pos2, (int)n, 0, 64,
-                                           e->stream) != hipSuccess)
-      return fail(e, ZB_EDEVICE, "inbox sort sizing");
-    int rc = grow_dev(e, (uint8_t**)&e->x_tmp, &e->x_tmp_cap, tmp + 16);
+    int rc = sort_pairs(e, e->x_keys, e->x_keys2, e->x_pos, e->x_pos2, n, "inbox");
     if (rc != ZB_OK) return rc;
-    tmp = e->x_tmp_cap;
-    if (hipcub::DeviceRadixSort::SortPairs(e->x_tmp, tmp, e->x_keys, e->x_keys2, e->x_pos, e->x_pos2, (int)n, 0, 64,
-                                           e->stream) != hipSuccess)
-      return fail(e, ZB_EDEVICE, "inbox sort");
     ResolveParams rp{};
     rp.rmeta = e->rmeta; rp.rkeys = e->rkeys; rp.rows = (uint64_t)e->host_hdr.rows_next;
     rp.keys = e->x_keys2; rp.pos = e->x_pos2; rp.pos_base = 0; rp.n = (int64_t)n;
@@ -3296,15 +3340,16 @@ int zb_outbox_count(zb_engine* e, int kind, uint64_t* n) {
 }  // extern "C"
 
 namespace {
-// Sorts the outbox of `kind` and lays it out as one exchange batch per target (target order) at dst (device):
-// per-target byte sizes into bytes_per_target, *total = their sum. With dst == nullptr only the sizes are
-// computed (the outbox is left as it is).
-int outbox_pack(zb_engine* e, int kind, uint8_t* dst, uint64_t cap, uint64_t* bytes_per_target, uint64_t* counts,
-                uint64_t* n_out, uint64_t* total) {
+// outbox_plan sorts the outbox of `kind` by (target, source position, emission) and sizes one exchange batch per
+// target: per-target byte sizes into bytes_per_target, *total = their sum (the outbox is left as it is).
+// outbox_emit then lays the planned batches out at dst (device, target order) and takes the outbox: one sort per
+// exchange.
+int outbox_plan(zb_engine* e, int kind, uint64_t* bytes_per_target, uint64_t* counts, uint64_t* n_out, uint64_t* total) {
   const int P = e->cfg.partition_count;
   if (P > 64) return fail(e, ZB_EUNSUPPORTED, "more than 64 partitions");
   for (int q = 0; q < P; q++) bytes_per_target[q] = counts[q] = 0;
   *total = 0;
+  e->ob_plan_kind = 0;
   uint64_t n = 0;
   int rc = zb_outbox_count(e, kind, &n);
   if (rc != ZB_OK) return rc;
@@ -3318,23 +3363,17 @@ int outbox_pack(zb_engine* e, int kind, uint8_t* dst, uint64_t cap, uint64_t* by
         hipMalloc(&e->ob_sizes, (c + 1) * 4) != hipSuccess || hipMalloc(&e->ob_goff, (c + 1) * 4) != hipSuccess ||
         hipMalloc(&e->ob_table, 2 * 64 * 8) != hipSuccess || hipMalloc(&e->ob_base, 64 * 8) != hipSuccess)
       return fail(e, ZB_ENOMEM, "outbox sort buffers");
-    if (hipcub::DeviceRadixSort::SortPairs(nullptr, e->ob_tmp_bytes, e->okeys[0], e->ob_keys, e->ob_idx_in,
-                                           e->ob_idx_out, (int)c, 0, 64, e->stream) != hipSuccess)
-      return fail(e, ZB_ENOMEM, "outbox sort scratch");
-    size_t scan_bytes = 0;
-    if (hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, e->ob_sizes, e->ob_goff, (int)(c + 1), e->stream) != hipSuccess)
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, e->ob_tmp_bytes, e->ob_sizes, e->ob_goff, (int)(c + 1), e->stream) !=
+        hipSuccess)
       return fail(e, ZB_ENOMEM, "outbox scan scratch");
-    e->ob_tmp_bytes = std::max(e->ob_tmp_bytes, scan_bytes);
-    if (hipMalloc(&e->ob_tmp, e->ob_tmp_bytes + 16) != hipSuccess) return fail(e, ZB_ENOMEM, "outbox sort scratch");
+    if (hipMalloc(&e->ob_tmp, e->ob_tmp_bytes + 16) != hipSuccess) return fail(e, ZB_ENOMEM, "outbox scan scratch");
   }
   launch_iota(e->ob_idx_in, n, e->stream);
-  size_t tmp_bytes = e->ob_tmp_bytes;
-  if (hipcub::DeviceRadixSort::SortPairs(e->ob_tmp, tmp_bytes, e->okeys[k], e->ob_keys, e->ob_idx_in, e->ob_idx_out,
-                                         (int)n, 0, 64, e->stream) != hipSuccess)
-    return fail(e, ZB_EDEVICE, "outbox sort");
+  rc = sort_pairs(e, (const uint64_t*)e->okeys[k], e->ob_keys, (const uint32_t*)e->ob_idx_in, e->ob_idx_out, n, "outbox");
+  if (rc != ZB_OK) return rc;
   const Outbox ob = outbox(e, kind);
   launch_outbox_sizes(ob, e->ob_idx_out, n, e->ob_sizes, e->stream);
-  tmp_bytes = e->ob_tmp_bytes;
+  size_t tmp_bytes = e->ob_tmp_bytes;
   if (hipcub::DeviceScan::ExclusiveSum(e->ob_tmp, tmp_bytes, e->ob_sizes, e->ob_goff, (int)(n + 1), e->stream) != hipSuccess)
     return fail(e, ZB_EDEVICE, "outbox scan");
   launch_outbox_bounds(e->ob_keys, n, e->ob_first, P, e->stream);
@@ -3342,18 +3381,29 @@ int outbox_pack(zb_engine* e, int kind, uint8_t* dst, uint64_t cap, uint64_t* by
   uint64_t table[128];
   HIPCHECK(e, hipMemcpyAsync(table, e->ob_table, 2 * P * 8, hipMemcpyDeviceToHost, e->stream));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
-  uint64_t base[64], o = 0;
+  uint64_t o = 0;
   for (int q = 0; q < P; q++) {
     counts[q] = table[2 * q];
     bytes_per_target[q] = counts[q] ? ZB_XCHG_BATCH_HEADER + counts[q] * sizeof(zb_exchange_rec) + 8 * table[2 * q + 1] : 0;
-    base[q] = o;
+    e->ob_plan_base[q] = o;
     o += bytes_per_target[q];
   }
   *total = o;
-  if (!dst) return ZB_OK;
-  if (o > cap) return fail(e, ZB_ENOMEM, "outbox destination too small");
-  HIPCHECK(e, hipMemcpyAsync(e->ob_base, base, P * 8, hipMemcpyHostToDevice, e->stream));
-  launch_outbox_pack(ob, e->ob_idx_out, e->ob_keys, n, e->ob_first, e->ob_goff, e->ob_base, dst, e->stream);
+  e->ob_plan_kind = kind;
+  e->ob_plan_n = n;
+  e->ob_plan_total = o;
+  return ZB_OK;
+}
+
+int outbox_emit(zb_engine* e, int kind, uint8_t* dst, uint64_t cap) {
+  if (e->ob_plan_kind != kind) return fail(e, ZB_EDEVICE, "outbox emit without a plan");
+  e->ob_plan_kind = 0;
+  if (e->ob_plan_total > cap) return fail(e, ZB_ENOMEM, "outbox destination too small");
+  const int P = e->cfg.partition_count;
+  const int k = kind - 1;
+  HIPCHECK(e, hipMemcpyAsync(e->ob_base, e->ob_plan_base, P * 8, hipMemcpyHostToDevice, e->stream));
+  launch_outbox_pack(outbox(e, kind), e->ob_idx_out, e->ob_keys, e->ob_plan_n, e->ob_first, e->ob_goff, e->ob_base, dst,
+                     e->stream);
   HIPCHECK(e, hipMemsetAsync(e->on + k, 0, sizeof(uint32_t), e->stream));      // the outbox is taken
   HIPCHECK(e, hipMemsetAsync(e->on + 2 + k, 0, sizeof(uint32_t), e->stream));  // (and its byte section)
   HIPCHECK(e, hipStreamSynchronize(e->stream));
@@ -3369,7 +3419,7 @@ int zb_outbox_take(zb_engine* e, int kind, uint8_t* dst, size_t cap, int dst_on_
     return ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
   uint64_t counts[64];
-  int rc = outbox_pack(e, kind, nullptr, 0, bytes_per_target, counts, n_out, total);  // sizes only
+  int rc = outbox_plan(e, kind, bytes_per_target, counts, n_out, total);
   if (rc != ZB_OK || *n_out == 0) return rc;
   if (!dst || cap < *total) return ZB_ENOMEM;
   uint8_t* out = dst;
@@ -3378,7 +3428,7 @@ int zb_outbox_take(zb_engine* e, int kind, uint8_t* dst, size_t cap, int dst_on_
     if (rc != ZB_OK) return rc;
     out = e->ob_staging;
   }
-  rc = outbox_pack(e, kind, out, dst_on_device ? cap : e->ob_staging_cap, bytes_per_target, counts, n_out, total);
+  rc = outbox_emit(e, kind, out, dst_on_device ? cap : e->ob_staging_cap);
   if (rc != ZB_OK) return rc;
   if (!dst_on_device) {
     HIPCHECK(e, hipMemcpyAsync(dst, e->ob_staging, *total, hipMemcpyDeviceToHost, e->stream));
@@ -3473,9 +3523,9 @@ int zb_comm_exchange(zb_engine* e, int kind, uint64_t* received) {
   if (const char* f = std::getenv("ZB_FAIL_EXCHANGE"))  // (before the outbox is taken: a retry still has it)
     if (*f && atoi(f) == e->cfg.partition_id) local = fail(e, ZB_EDEVICE, "injected local failure (ZB_FAIL_EXCHANGE)");
 #endif
-  if (local == ZB_OK) local = outbox_pack(e, kind, nullptr, 0, sb, sc, &n, &total);
+  if (local == ZB_OK) local = outbox_plan(e, kind, sb, sc, &n, &total);
   if (local == ZB_OK && n) local = grow_dev(e, &e->xsend, &e->xsend_cap, total);
-  if (local == ZB_OK && n) local = outbox_pack(e, kind, e->xsend, e->xsend_cap, sb, sc, &n, &total);
+  if (local == ZB_OK && n) local = outbox_emit(e, kind, e->xsend, e->xsend_cap);
   if (local != ZB_OK) for (int q = 0; q < P; q++) sb[q] = sc[q] = 0;
   const std::string local_err = local != ZB_OK ? e->err : std::string();
   // 1. agreement + sizes: every rank sends every peer (bytes, commands, status) for it; always posted

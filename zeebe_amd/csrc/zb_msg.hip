@@ -23,6 +23,8 @@
 // (keys are handed out in command order), so DELETE finds its message by binary search.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "zb_devlib.hpp"
 #include "zb_kernels.hpp"
 #include "zb_msg.hpp"
@@ -432,6 +434,17 @@ __global__ void k_iota(uint32_t* p, uint64_t n) {
   if (i < n) p[i] = (uint32_t)i;
 }
 
+// the key bits that differ between the keys of a sort: OR over i of keys[i] ^ keys[0] (the radix sort then runs over
+// [lowest, highest] of them only)
+__global__ void k_key_spread(const uint64_t* keys, uint64_t n, unsigned long long* out) {
+  const uint64_t k0 = keys[0];
+  uint64_t acc = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    acc |= keys[i] ^ k0;
+  for (int o = 32; o > 0; o >>= 1) acc |= (uint64_t)__shfl_xor((unsigned long long)acc, o, 64);
+  if ((threadIdx.x & 63) == 0 && acc) atomicOr(out, (unsigned long long)acc);
+}
+
 static unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
 static unsigned grid_cap(uint64_t n) {
   const uint64_t g = (n + 255) / 256;
@@ -480,6 +493,10 @@ void launch_outbox_pack(const Outbox& ob, const uint32_t* idx, const uint64_t* k
 }
 void launch_iota(uint32_t* p, uint64_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_iota, dim3(blocks((int64_t)n)), dim3(256), 0, s, p, n);
+}
+void launch_key_spread(const uint64_t* keys, uint64_t n, uint64_t* out, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_key_spread, dim3(std::min<uint64_t>((n + 1023) / 1024, 1024)), dim3(256), 0, s, keys, n,
+                           (unsigned long long*)out);
 }
 
 }  // namespace zbg

@@ -800,7 +800,8 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3))
 // own and encodes its 64 records in rounds -- each lane its own record, the lanes whose values fit the image from
 // the round's first byte -- then streams the round out; the four waves never wait for each other (the phase form
 // above lets one wave encode at a time). A tile with a record the fast encoder does not take, or a single value
-// larger than the image, goes to the next pass (tile_list: the 40 KB phase form, then k_ser_write).
+// larger than the image, goes to the next pass (tile_list: the 40 KB phase form, then k_ser_write; tile_list_slow:
+// k_ser_write directly, for the tiles holding a record of a kind the fast encoder does not take).
 constexpr uint32_t SER_WIMG = 11 * 1024 - 16;
 __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 4))) k_ser_wave(SerParams P0) {
   __shared__ __attribute__((aligned(16))) uint8_t s_img[SER_WG / 64][SER_WIMG + 16];
@@ -838,8 +839,12 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
     if (threadIdx.x == 0) atomicOr(P0.overflow, 1u);
     return;
   }
-  if (!all_fast) {  // the next pass takes this tile
-    if (threadIdx.x == 0) P0.tile_list[atomicAdd(P0.tile_list_n, 1u)] = tile;
+  if (!all_fast) {  // the next pass takes this tile: the 40 KB phase form if only a value's size is the reason
+    const bool kinds = __syncthreads_and(!live || fast);
+    if (threadIdx.x == 0) {
+      if (kinds) P0.tile_list[atomicAdd(P0.tile_list_n, 1u)] = tile;
+      else P0.tile_list_slow[atomicAdd(P0.tile_list_n + 1, 1u)] = tile;
+    }
     return;
   }
   uint64_t pw = 0;
