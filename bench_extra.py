@@ -122,7 +122,8 @@ def run_c5(a, rank, world, local_rank, dist, barrier, reduce_max, reduce_sum):
            "dtype": "int64", "data": "synthetic (SURVEY §8d C5: orderId 'order-<i>', payload {paid: true})",
            "config": {"workload": "C5: message catch correlated across partitions (RCCL exchange), "
                                   "%d instances per GPU" % n, "instances_per_gpu": n, "partitions": world,
-                      "parallelism": "partition-per-gpu", "exchange": "RCCL ncclSend/ncclRecv (engine)",
+                      "parallelism": "partition-per-gpu", "exchange": "RCCL ncclSend/ncclRecv (engine)" if world > 1 else
+                      "one partition: its outbox is its own inbox, on the device (no peer to exchange with)",
                       "timed_step": "CREATE injection to quiescence, exchange rounds, publish to quiescence, "
                                     "zb_serialize of every record of the partition's log (values + headers, in HBM); "
                                     "the CREATE and PUBLISH inputs are uploaded before the timed region"},

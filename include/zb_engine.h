@@ -66,6 +66,9 @@ extern "C" {
 #define ZB_CFG_WAVE_EVENTS 128    /* timing events around every wave's kernels (zb_step_stats process / emit / aux) */
 #define ZB_CFG_WAVE_SPLIT 256     /* the three-kernel wave pipeline (k_process, k_scan, k_emit) instead of k_wave */
 #define ZB_CFG_SINGLE_PASS_DRAIN 512 /* values drained in one pass with decoupled look-back (measured slower) */
+#define ZB_CFG_RCCL_SELF 1024     /* a one-partition engine still exchanges through its RCCL communicator (both agreement
+                                     collectives and ncclSend / ncclRecv to itself: the P > 1 code path); without it a
+                                     single partition hands its outbox to its own inbox on the device */
 
 typedef struct zb_engine zb_engine;
 

@@ -138,14 +138,16 @@ def test_c5_scale_properties():
     assert total == n * (1 + 13 + 2) + n * 2 + n * 2, total
 
 
-def test_rccl_exchange_single_rank():
-    """DistCluster with the engine's own RCCL communicator (world size 1 here: the one-GPU box; the
-    exchange still goes through ncclSend / ncclRecv to self) against the oracle."""
+@pytest.mark.parametrize("rccl_self", [True, False])
+def test_rccl_exchange_single_rank(rccl_self):
+    """DistCluster with the engine's own RCCL communicator (world size 1 here: the one-GPU box) against the oracle:
+    with ZB_CFG_RCCL_SELF the exchange goes through the agreement collectives and ncclSend / ncclRecv to self (the
+    P > 1 code path), without it the one partition delivers its outbox to its own inbox on the device."""
     import os
     import socket
 
     import torch.distributed as dist
-    from zeebe_amd.engine import Engine
+    from zeebe_amd.engine import CFG_RCCL_SELF, Engine
 
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -155,7 +157,8 @@ def test_rccl_exchange_single_rank():
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=0, world_size=1)
     try:
-        e = Engine(device=0, partition_id=0, partition_count=1, log_capacity=1 << 20, row_capacity=1 << 18)
+        e = Engine(device=0, partition_id=0, partition_count=1, log_capacity=1 << 20, row_capacity=1 << 18,
+                   flags=CFG_RCCL_SELF if rccl_self else 0)
         o = zbref.OraclePartition(0, 1)
         for x in (e, o):
             x.deploy(catch_workflow(), 100, 1)
@@ -314,7 +317,7 @@ def _exchange_failure_protocol():
     import socket
 
     import torch.distributed as dist
-    from zeebe_amd.engine import Engine, ZbError, checked_violations
+    from zeebe_amd.engine import CFG_RCCL_SELF, Engine, ZbError, checked_violations
 
     assert checked_violations() is not None, "the failure hook exists only in the guard-band build"
     s = socket.socket()
@@ -325,7 +328,8 @@ def _exchange_failure_protocol():
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=0, world_size=1)
     try:
-        e = Engine(device=0, partition_id=0, partition_count=1, log_capacity=1 << 20, row_capacity=1 << 18)
+        e = Engine(device=0, partition_id=0, partition_count=1, log_capacity=1 << 20, row_capacity=1 << 18,
+                   flags=CFG_RCCL_SELF)  # (the P > 1 code path: collectives and send / recv to self)
         e.deploy(catch_workflow(), 100, 1)
         e.create("wf", [msgpack.packb({"orderId": "order-%d" % i}) for i in range(20)])
         dc = cluster.DistCluster(e)

@@ -3498,6 +3498,11 @@ int zb_comm_pending(zb_engine* e, uint64_t global[2]) {
     int rc = zb_outbox_count(e, k + 1, &local[k]);
     if (rc != ZB_OK) return rc;
   }
+  if (e->cfg.partition_count == 1 && !(e->cfg.flags & ZB_CFG_RCCL_SELF)) {  // no peer: the sum is the local count
+    global[0] = local[0];
+    global[1] = local[1];
+    return ZB_OK;
+  }
   HIPCHECK(e, hipMemcpyAsync(e->d_xcounts, local, sizeof(local), hipMemcpyHostToDevice, e->stream));
   ncclResult_t nr = ncclAllReduce(e->d_xcounts, e->d_xcounts, 2, ncclUint64, ncclSum, e->comm, e->stream);
   if (nr != ncclSuccess) return comm_fail(e, "pending counts", nr);
@@ -3526,6 +3531,15 @@ int zb_comm_exchange(zb_engine* e, int kind, uint64_t* received) {
   if (local == ZB_OK) local = outbox_plan(e, kind, sb, sc, &n, &total);
   if (local == ZB_OK && n) local = grow_dev(e, &e->xsend, &e->xsend_cap, total);
   if (local == ZB_OK && n) local = outbox_emit(e, kind, e->xsend, e->xsend_cap);
+  if (P == 1 && !(e->cfg.flags & ZB_CFG_RCCL_SELF)) {  // no peer: the batch is this partition's own inbox
+    if (local != ZB_OK || n == 0) return local;
+    std::vector<uint64_t> rcounts{sc[0]}, roffs{0};
+    int rc = require_idle(e);
+    if (rc == ZB_OK) rc = ensure_stores(e);
+    if (rc == ZB_OK) rc = maintain(e, false);
+    if (rc == ZB_OK) rc = deliver(e, kind, e->xsend, rcounts, roffs, received);
+    return rc;
+  }
   if (local != ZB_OK) for (int q = 0; q < P; q++) sb[q] = sc[q] = 0;
   const std::string local_err = local != ZB_OK ? e->err : std::string();
   // 1. agreement + sizes: every rank sends every peer (bytes, commands, status) for it; always posted
