@@ -200,7 +200,8 @@ struct zb_engine {
   uint64_t* t_wstats = nullptr;   // [t_nwg_cap + CLS_MAX][6] emit statistics per workgroup
   TrajCtl* h_ctl_pinned = nullptr;
   uint64_t* h_stats_pinned = nullptr;  // [0..7] counters before a step, [8..15] after, [16] a class batch's ClsPlan.nc,
-                                       // [17] sort_pairs' key spread, [18] the waves counter before a wave loop
+                                       // [17] sort_pairs' key spread, [18] the waves counter before a wave loop,
+                                       // [19..20] the outbox counts (zb_outbox_count)
   // class batches (zb_traj.hip k_cls_*): the model's exclusive splits as outcome-key digits
   bool cls_ok = false;            // split outcome keys fit 8 bits and CLS_MAX_SPLITS splits
   int nsplits = 0;
@@ -266,6 +267,7 @@ struct zb_engine {
   uint64_t *ob_table = nullptr, *ob_base = nullptr;
   void* ob_tmp = nullptr;  // (scan scratch)
   size_t ob_tmp_bytes = 0;
+  uint32_t ob_counts_read[2] = {0, 0};  // both outbox command counts at the last zb_outbox_count
   int wave_hint = 0;     // non-empty waves of the last step's wave loop (its first batch, zb_step)
   int ob_plan_kind = 0;  // the outbox kind outbox_plan sorted and sized last (0: none)
   uint64_t ob_plan_n = 0, ob_plan_total = 0, ob_plan_base[64] = {};
@@ -1222,7 +1224,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipHostMalloc(&e->h_hdr_pinned, 2 * sizeof(WaveHdr)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_err_pinned, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_ctl_pinned, sizeof(TrajCtl)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipHostMalloc(&e->h_stats_pinned, 19 * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipHostMalloc(&e->h_stats_pinned, 21 * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->d_spread, sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_ctl, sizeof(TrajCtl)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_wtot, TRAJ_WAVE_CAP * sizeof(uint4)) != hipSuccess) return cleanup(ZB_ENOMEM);
@@ -3328,12 +3330,15 @@ int zb_outbox_count(zb_engine* e, int kind, uint64_t* n) {
   *n = 0;
   if (!e->on) return ZB_OK;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
-  uint32_t c[4] = {0, 0, 0, 0};
-  HIPCHECK(e, hipMemcpyAsync(c, e->on, sizeof(c), hipMemcpyDeviceToHost, e->stream));
+  uint32_t* c = (uint32_t*)(e->h_stats_pinned + 19);  // (pinned: commands OPEN, CORRELATE, granules OPEN, CORRELATE)
+  HIPCHECK(e, hipMemcpyAsync(c, e->on, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
-  if ((uint64_t)c[kind - 1] > e->ocap || (uint64_t)c[kind + 1] > e->ovar_cap)
-    return fail(e, ZB_ENOMEM, "outbox overflow (commands or their variable bytes)");
+  for (int k = 1; k <= 2; k++)
+    if ((uint64_t)c[k - 1] > e->ocap || (uint64_t)c[k + 1] > e->ovar_cap)
+      return fail(e, ZB_ENOMEM, "outbox overflow (commands or their variable bytes)");
   *n = c[kind - 1];
+  e->ob_counts_read[0] = c[0];
+  e->ob_counts_read[1] = c[1];
   return ZB_OK;
 }
 
@@ -3494,10 +3499,9 @@ int zb_comm_pending(zb_engine* e, uint64_t global[2]) {
   if (!e->comm) return e->comm_broken ? fail(e, ZB_EDEVICE, "communicator aborted after an earlier failure") : ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
   uint64_t local[2] = {0, 0};
-  for (int k = 0; k < 2; k++) {
-    int rc = zb_outbox_count(e, k + 1, &local[k]);
-    if (rc != ZB_OK) return rc;
-  }
+  int rc0 = zb_outbox_count(e, ZB_XCHG_OPEN, &local[0]);  // (one read of both counts)
+  if (rc0 != ZB_OK) return rc0;
+  local[1] = e->ob_counts_read[1];
   if (e->cfg.partition_count == 1 && !(e->cfg.flags & ZB_CFG_RCCL_SELF)) {  // no peer: the sum is the local count
     global[0] = local[0];
     global[1] = local[1];

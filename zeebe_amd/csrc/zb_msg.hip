@@ -36,6 +36,17 @@ __device__ __forceinline__ bool bytes_equal(const uint8_t* a, const uint8_t* b, 
     if (a[i] != b[i]) return false;
   return true;
 }
+// n bytes at two 8-aligned addresses inside 8-aligned arena blobs, compared a word at a time (the last word's bytes
+// past n -- still inside both blobs -- are masked off)
+__device__ __forceinline__ bool words_equal(const uint8_t* a, const uint8_t* b, uint32_t n) {
+  const uint64_t* wa = (const uint64_t*)a;
+  const uint64_t* wb = (const uint64_t*)b;
+  uint64_t diff = 0;
+  uint32_t k = 0;
+  for (; k + 8 <= n; k += 8) diff |= wa[k / 8] ^ wb[k / 8];
+  if (k < n) diff |= (wa[k / 8] ^ wb[k / 8]) & ((1ull << (8 * (n - k))) - 1);
+  return diff == 0;
+}
 
 __device__ __forceinline__ void put_record(const MsgParams& P, int64_t pos, const zb_rec& d, uint32_t srcd) {
   P.log[pos] = d;
@@ -80,6 +91,8 @@ __device__ __forceinline__ void flag_error(const MsgParams& P, uint32_t err) {
 
 // ------------------------------------------------------------------------------ OPEN
 __global__ void __launch_bounds__(256) k_msg_open(MsgParams P) {
+  __shared__ uint32_t s_alloc[2 * (256 / 64) + 2];
+  __shared__ uint64_t s_alloc64[256 / 64 + 1];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool act = i < P.n;
   uint32_t err = 0, ncorr = 0, best_blob = 0, gran = 0;
@@ -88,12 +101,22 @@ __global__ void __launch_bounds__(256) k_msg_open(MsgParams P) {
   zb_exchange_rec r{};
   const uint8_t* var = nullptr;
   uint32_t sref = 0;
+  if (act) r = delivered(P, i, var);
+  // the subscription blob (the serializer and the store read wf partition / name / correlation key from it)
+  const uint32_t blen = SUB_HDR - 4 + r.name_len + r.ck_len;
+  const uint64_t bbytes = act ? ((4 + (uint64_t)blen + 7) & ~7ull) : 0;
+  const uint64_t bat = block_alloc64<256>((unsigned long long*)&P.hdr->arena_next, bbytes, s_alloc64);
   if (act) {
-    r = delivered(P, i, var);
     const uint8_t* name = var;
     const uint8_t* ck = var + r.name_len;
-    // the subscription blob (the serializer and the store read wf partition / name / correlation key from it)
-    uint8_t* b = alloc_blob(P, SUB_HDR - 4 + r.name_len + r.ck_len, sref, err);
+    uint8_t* b = nullptr;
+    if (bat + bbytes > P.arena_cap) err |= DE_ARENA_FULL;
+    else {
+      b = P.arena + bat;
+      *(uint32_t*)b = blen;
+      for (uint64_t k = 4 + blen; k < bbytes; k++) b[k] = 0;
+      sref = (uint32_t)(bat >> 3);
+    }
     if (b) {
       *(int32_t*)(b + 4) = r.wf_partition;
       *(uint32_t*)(b + 8) = r.token;
@@ -124,7 +147,9 @@ __global__ void __launch_bounds__(256) k_msg_open(MsgParams P) {
         const MsgEntry m = P.msgs[e];
         if (m.h != h || m.dead) continue;
         const MsgView v = msg_view(P.arena, m.blob);
-        if (v.nn != r.name_len || v.nc != r.ck_len || !bytes_equal(v.name, name, v.nn) || !bytes_equal(v.ck, ck, v.nc))
+        if (v.nn != r.name_len || v.nc != r.ck_len) continue;
+        if (b ? !words_equal(v.name, b + SUB_HDR, v.nn + v.nc)  // (name + key contiguous in both blobs, 8-aligned)
+              : (!bytes_equal(v.name, name, v.nn) || !bytes_equal(v.ck, ck, v.nc)))
           continue;
         if (best < 0 || m.pos < best) { best = m.pos; best_blob = m.blob; }
       }
@@ -134,8 +159,8 @@ __global__ void __launch_bounds__(256) k_msg_open(MsgParams P) {
       gran = var_granules(r.name_len, 0, msg_view(P.arena, best_blob).np);
     }
   }
-  const uint32_t slot = wave_alloc(P.ob.n, ncorr);
-  const uint32_t vat = wave_alloc(P.ob.var_n, gran);
+  uint32_t slot, vat;
+  block_alloc2<256>(P.ob.n, ncorr, P.ob.var_n, gran, s_alloc, slot, vat);
   if (act && ncorr) {
     const MsgView v = msg_view(P.arena, best_blob);
     if (slot >= P.ob.cap || (uint64_t)vat + gran > P.ob.var_cap) err |= DE_LOG_FULL;
@@ -183,10 +208,12 @@ __global__ void __launch_bounds__(256) k_pub_count(MsgParams P) {
 }
 
 __device__ __forceinline__ bool sub_matches(const SubView& sb, const MsgView& v) {
-  return sb.nn == v.nn && sb.nc == v.nc && bytes_equal(sb.name, v.name, v.nn) && bytes_equal(sb.ck, v.ck, v.nc);
+  // (name + correlation key are contiguous and 8-aligned in both blobs: SUB_HDR, MSG_HDR)
+  return sb.nn == v.nn && sb.nc == v.nc && words_equal(sb.name, v.name, v.nn + v.nc);
 }
 
 __global__ void __launch_bounds__(256) k_pub_emit(MsgParams P) {
+  __shared__ uint32_t s_alloc[2 * (256 / 64) + 2];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool act = i < P.n;
   const int64_t pos = P.base + i;
@@ -196,6 +223,7 @@ __global__ void __launch_bounds__(256) k_pub_emit(MsgParams P) {
   MsgView v{};
   bool acc = false;
   uint64_t off = 0;
+  uint32_t e1 = NO_ENTRY;  // the first matching subscription of the chain
   if (act) {
     d = P.log[pos];
     v = msg_view(P.arena, d.payload);
@@ -219,20 +247,24 @@ __global__ void __launch_bounds__(256) k_pub_emit(MsgParams P) {
       h = name_ck_hash(v.name, v.nn, v.ck, v.nc);
       for (uint32_t e = P.sub_head[h & P.sub_mask]; e != NO_ENTRY; e = P.sub_next[e]) {
         const SubEntry s = P.subs[e];
-        if (s.h == h && sub_matches(sub_view(P.arena, s.blob), v)) nmatch++;
+        if (s.h == h && sub_matches(sub_view(P.arena, s.blob), v)) {
+          if (nmatch++ == 0) e1 = e;
+        }
       }
       gran = nmatch * var_granules(v.nn, 0, v.np);
     }
   }
-  uint32_t slot = wave_alloc(P.ob.n, nmatch);
-  uint32_t vat = wave_alloc(P.ob.var_n, gran);
+  uint32_t slot, vat;
+  block_alloc2<256>(P.ob.n, nmatch, P.ob.var_n, gran, s_alloc, slot, vat);
   if (act && nmatch) {  // correlateMessage :107-124: one command per matching subscription
     const uint32_t g = var_granules(v.nn, 0, v.np);
-    for (uint32_t e = P.sub_head[h & P.sub_mask]; e != NO_ENTRY; e = P.sub_next[e]) {
+    uint32_t left = nmatch;
+    for (uint32_t e = e1; e != NO_ENTRY && left; e = P.sub_next[e]) {
       const SubEntry s = P.subs[e];
       if (s.h != h) continue;
       const SubView sb = sub_view(P.arena, s.blob);
-      if (!sub_matches(sb, v)) continue;
+      if (e != e1 && !sub_matches(sb, v)) continue;
+      left--;
       if (slot >= P.ob.cap || (uint64_t)vat + g > P.ob.var_cap) { err |= DE_LOG_FULL; break; }
       outbox_write(P.ob, slot, vat, ZB_XCHG_CORRELATE, sb.wfp, sb.wfp, sb.token, s.wik, s.aik, pos, sb.elem, v.name, v.nn,
                    nullptr, 0, v.payload, v.np, s.idx);  // findSubscriptions: insertion order
@@ -304,15 +336,28 @@ __global__ void __launch_bounds__(256) k_ttl_write(MsgParams P) {
 
 // ------------------------------------------------------------------------------ CORRELATE inbox
 __global__ void __launch_bounds__(256) k_wis_inject(MsgParams P) {
+  __shared__ uint64_t s_alloc64[256 / 64 + 1];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P.n) return;
-  const uint8_t* var;
-  const zb_exchange_rec r = delivered(P, i, var);
+  const bool act = i < P.n;
+  const uint8_t* var = nullptr;
+  zb_exchange_rec r{};
+  if (act) r = delivered(P, i, var);
   const uint8_t* pl = var + r.name_len + r.ck_len;
   const uint32_t np = r.payload_len;
-  const bool empty = np == 0 || (np == 1 && pl[0] == 0xc0);  // DocumentValue: nil / empty -> {}
+  const bool empty = act && (np == 0 || (np == 1 && pl[0] == 0xc0));  // DocumentValue: nil / empty -> {}
+  const uint32_t blen = empty ? 1 : np;
+  const uint64_t bbytes = act ? ((4 + (uint64_t)blen + 7) & ~7ull) : 0;
+  const uint64_t bat = block_alloc64<256>((unsigned long long*)&P.hdr->arena_next, bbytes, s_alloc64);
+  if (!act) return;
   uint32_t err = 0, ref = 0;
-  uint8_t* b = alloc_blob(P, empty ? 1 : np, ref, err);
+  uint8_t* b = nullptr;
+  if (bat + bbytes > P.arena_cap) err |= DE_ARENA_FULL;
+  else {
+    b = P.arena + bat;
+    *(uint32_t*)b = blen;
+    for (uint64_t k = 4 + blen; k < bbytes; k++) b[k] = 0;
+    ref = (uint32_t)(bat >> 3);
+  }
   if (b) {
     if (empty) b[4] = 0x80;
     else copy_bytes(b + 4, pl, np);
@@ -436,13 +481,17 @@ __global__ void k_iota(uint32_t* p, uint64_t n) {
 
 // the key bits that differ between the keys of a sort: OR over i of keys[i] ^ keys[0] (the radix sort then runs over
 // [lowest, highest] of them only)
-__global__ void k_key_spread(const uint64_t* keys, uint64_t n, unsigned long long* out) {
+__global__ void __launch_bounds__(256) k_key_spread(const uint64_t* keys, uint64_t n, unsigned long long* out) {
+  __shared__ uint64_t s[4];
   const uint64_t k0 = keys[0];
   uint64_t acc = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     acc |= keys[i] ^ k0;
   for (int o = 32; o > 0; o >>= 1) acc |= (uint64_t)__shfl_xor((unsigned long long)acc, o, 64);
-  if ((threadIdx.x & 63) == 0 && acc) atomicOr(out, (unsigned long long)acc);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  // one atomic per workgroup (same-address atomics serialize)
+  if (threadIdx.x == 0 && (s[0] | s[1] | s[2] | s[3])) atomicOr(out, (unsigned long long)(s[0] | s[1] | s[2] | s[3]));
 }
 
 static unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
@@ -495,7 +544,7 @@ void launch_iota(uint32_t* p, uint64_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_iota, dim3(blocks((int64_t)n)), dim3(256), 0, s, p, n);
 }
 void launch_key_spread(const uint64_t* keys, uint64_t n, uint64_t* out, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_key_spread, dim3(std::min<uint64_t>((n + 1023) / 1024, 1024)), dim3(256), 0, s, keys, n,
+  if (n) hipLaunchKernelGGL(k_key_spread, dim3(std::min<uint64_t>((n + 1023) / 1024, 512)), dim3(256), 0, s, keys, n,
                            (unsigned long long*)out);
 }
 

@@ -701,8 +701,9 @@ __device__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t p
 // element instance's payload, routed to abs(hash(correlationKey) % P), ordered by the catch event's log
 // position. One thread per subscribe step of the wave (k_process listed them).
 __global__ void __launch_bounds__(256) k_subscribe(WaveParams P) {
+  __shared__ uint32_t s_alloc[2 * (256 / 64) + 2];
   const uint32_t n = P.sub_count[P.wave & 1];
-  // (uniform trip count per wave: wave_alloc below is a wave-wide operation)
+  // (uniform trip count per workgroup: block_alloc2 below is a workgroup-wide operation)
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t j0 = (uint64_t)blockIdx.x * 256; j0 < n && j0 < P.job_cap; j0 += stride) {
     const uint64_t j = j0 + threadIdx.x;
@@ -738,8 +739,8 @@ __global__ void __launch_bounds__(256) k_subscribe(WaveParams P) {
       }
       if (!err) gran = var_granules(el->msg_len, ck_len, 0);
     }
-    const uint32_t slot = wave_alloc(P.obx.n, act && !err ? 1u : 0u);
-    const uint32_t vat = wave_alloc(P.obx.var_n, gran);
+    uint32_t slot, vat;
+    block_alloc2<256>(P.obx.n, act && !err ? 1u : 0u, P.obx.var_n, gran, s_alloc, slot, vat);
     if (act && !err) {
       if (slot >= P.obx.cap || (uint64_t)vat + gran > P.obx.var_cap) { err = DE_LOG_FULL; site = 36; }
       else {
@@ -1609,7 +1610,9 @@ void launch_emit(const WaveParams& p, hipStream_t stream) {
   hipLaunchKernelGGL(k_emit, dim3(p.grid), dim3(WG), 0, stream, p);
 }
 void launch_subscribe(const WaveParams& p, hipStream_t stream) {
-  hipLaunchKernelGGL(k_subscribe, dim3(256), dim3(256), 0, stream, p);
+  // five workgroups per CU (82 VGPRs): the correlation-key queries of a wave that opens 1M subscriptions are
+  // latency-bound (C5: 426 us on one workgroup per CU); a wave without subscribe steps exits at the count
+  hipLaunchKernelGGL(k_subscribe, dim3(1280), dim3(256), 0, stream, p);
 }
 
 }  // namespace zbg
