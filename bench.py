@@ -354,8 +354,8 @@ def roofline(tot, steps, cfg, n):
         # per launch: every drained record's descriptor read + header write, its value bytes written and the
         # payload documents copied into them read (SURVEY §8d payload term)
         b = (tot["drained"] * (DESC_BYTES + HDR_BYTES) + tot["value_bytes"] + tot["payload_bytes"]) / steps
-        # two passes: the fast write pass (k_ser_write over the tiles it leaves, if any) / single pass
-        kname = ("zbg::k_ser_fast" if tot["generic_tiles"] == 0 else "zbg::k_ser_fast (+ k_ser_write on %d tiles)"
+        # the wave-parallel fast write pass (k_ser_write over the tiles it leaves, if any) / single pass
+        kname = ("zbg::k_ser_wave" if tot["generic_tiles"] == 0 else "zbg::k_ser_wave (+ k_ser_write on %d tiles)"
                  % (tot["generic_tiles"] // steps)) if tot["ser_size_ms"] > 0 else "zbg::k_ser_fused"
         cands.append((kname, tot["ser_write_ms"] / steps, b,
                       "32 B descriptor read + 24 B header write per drained record + value bytes written + payload "

@@ -266,8 +266,18 @@ __global__ void __launch_bounds__(256) k_pub_emit(MsgParams P) {
       if (e != e1 && !sub_matches(sb, v)) continue;
       left--;
       if (slot >= P.ob.cap || (uint64_t)vat + g > P.ob.var_cap) { err |= DE_LOG_FULL; break; }
+      // emission order = findSubscriptions' insertion order: the subscription's rank by store index among this
+      // message's matches (a few bits: the outbox sort then covers the positions and little more), or the index
+      // itself for a message with many matches
+      uint32_t em = 0;
+      if (nmatch > 32) em = s.idx;
+      else if (nmatch > 1)
+        for (uint32_t e2 = e1; e2 != NO_ENTRY; e2 = P.sub_next[e2]) {
+          const SubEntry s2 = P.subs[e2];
+          if (s2.h == h && s2.idx < s.idx && sub_matches(sub_view(P.arena, s2.blob), v)) em++;
+        }
       outbox_write(P.ob, slot, vat, ZB_XCHG_CORRELATE, sb.wfp, sb.wfp, sb.token, s.wik, s.aik, pos, sb.elem, v.name, v.nn,
-                   nullptr, 0, v.payload, v.np, s.idx);  // findSubscriptions: insertion order
+                   nullptr, 0, v.payload, v.np, em);
       slot++;
       vat += g;
     }
@@ -457,15 +467,19 @@ __global__ void k_pub_build(PubBuild p) {
   *(int64_t*)(b + 8) = p.ttl;
   *(int64_t*)(b + 16) = 0;  // deadline: set when the message is stored
   h[6] = nc; h[7] = np; h[8] = 0; h[9] = 0;
-  uint8_t* d = b + MSG_HDR;
-  for (uint32_t k = 0; k < p.nn; k++) d[k] = p.name[k];
-  d += p.nn;
-  for (uint32_t k = 0; k < nc; k++) d[k] = ck[k];
-  d += nc;
-  if (empty) d[0] = 0x80;
-  else for (uint32_t k = 0; k < np; k++) d[k] = pl[k];
-  const uint32_t end = MSG_HDR + p.nn + nc + np, pad_end = (end + 7) & ~7u;
-  for (uint32_t k = end; k < pad_end; k++) b[k] = 0;
+  // name, correlation key, payload (and the zero padding) as whole 8-byte words (b + MSG_HDR is 8-aligned)
+  uint64_t* d = (uint64_t*)(b + MSG_HDR);
+  const uint32_t n_all = p.nn + nc + np;
+  uint64_t acc = 0;
+  for (uint32_t k = 0; k < n_all; k++) {
+    const uint8_t x = k < p.nn ? p.name[k] : k < p.nn + nc ? ck[k - p.nn] : empty ? (uint8_t)0x80 : pl[k - p.nn - nc];
+    acc |= (uint64_t)x << (8 * (k & 7));
+    if ((k & 7) == 7) {
+      d[k >> 3] = acc;
+      acc = 0;
+    }
+  }
+  if (n_all & 7) d[n_all >> 3] = acc;
   zb_rec r;
   r.key = -1; r.scope_key = -1; r.inst_key = -1;
   r.payload = (uint32_t)(at >> 3);
