@@ -136,6 +136,16 @@ def run_c5(a, rank, world, local_rank, dist, barrier, reduce_max, reduce_sum):
                         "alg_bytes_model": "SURVEY §8d: 96 B per transition + payload terms, all partitions",
                         "path_frac": path_bytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS},
            "note": "excludes payload generation and hash routing of the published keys (input preparation)"}
+    # HBM bytes of the step's kernels (every zbg / rocprim kernel of a PMC run of one step: FETCH_SIZE x2 + WRITE_SIZE,
+    # separate rocprofv3 --pmc passes; the runtime's fill / copy kernels of the untimed reset and uploads excluded)
+    from bench import ROOT, _pmc_file, load_traffic_step
+
+    traffic = load_traffic_step("c5_%d" % n, ("zbg::", "void zbg::", "void rocprim::"))
+    if traffic:
+        out["roofline"]["traffic"] = traffic
+        out["roofline"]["traffic_note"] = ("HBM bytes per step of every engine kernel (zbg / rocprim) from rocprofv3 "
+                                           "FETCH_SIZE x2 + WRITE_SIZE (%s)" % os.path.relpath(_pmc_file("c5_%d" % n),
+                                                                                                 ROOT))
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_c5(8 if a.cpu_partitions == 0 else a.cpu_partitions, a.cpu_sample or 8000)
     _emit(out, rank)
