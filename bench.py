@@ -360,7 +360,7 @@ def roofline(tot, steps, cfg, n):
         cands.append((kname, tot["ser_write_ms"] / steps, b,
                       "32 B descriptor read + 24 B header write per drained record + value bytes written + payload "
                       "bytes read"))
-    if tot["main_ms"] > 0:
+    if tot["main_ms"] > 0 and tot["template_drain"] != steps:  # (a deferred batch writes no descriptors)
         b = (DESC_BYTES * tot["written"] + tot["merge_bytes"] + tot["cond_bytes"]) / steps
         kname = {1: "zbg::k_tmpl<false, false>", 2: "zbg::k_tmpl<true, false>"}.get(tot["path"], "zbg::k_tmpl")
         cands.append((kname, tot["main_ms"] / steps, b,

@@ -142,7 +142,7 @@ struct zb_engine {
   uint32_t* xlocks = nullptr;
   uint64_t* sub_jobs = nullptr;    // [job_cap] subscribe steps of a wave (models with message catch events)
   uint64_t job_cap = 0;
-  WaveHdr* h_hdr_pinned = nullptr;  // pinned mirror for D2H polling
+  WaveHdr* h_hdr_pinned = nullptr;  // pinned mirror for D2H polling [0], the source of deliver's header upload [1]
   uint32_t* h_err_pinned = nullptr;
 
   int64_t wave = 0;
@@ -3040,11 +3040,20 @@ int deliver(zb_engine* e, int kind, const uint8_t* buf, const std::vector<uint64
     e->host_hdr.end = base + (int64_t)recs;
     e->host_hdr.gen_end = e->host_hdr.end;
   }
-  int rc = pull_header(e);  // blobs were allocated on the device header
+  // blobs were allocated on the device header: its arena pointer and the error word in one round trip, then the
+  // host's header (log range) back to the device, stream-ordered before the next step's kernels
+  HIPCHECK(e, hipMemcpyAsync(e->h_hdr_pinned, e->hdr + (e->wave & 1), sizeof(WaveHdr), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipMemcpyAsync(e->h_err_pinned, e->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  e->host_hdr.arena_next = e->h_hdr_pinned[0].arena_next;
+  int rc = check_device_errors(e, *e->h_err_pinned);
   if (rc != ZB_OK) return rc;
   e->records_total += recs;
   e->arena_total += (uint64_t)(e->host_hdr.arena_next - arena_before);
-  return finish_batch(e);
+  e->h_hdr_pinned[1] = e->host_hdr;  // (pinned source: the copy may run after this call returns)
+  HIPCHECK(e, hipMemcpyAsync(e->hdr + (e->wave & 1), e->h_hdr_pinned + 1, sizeof(WaveHdr), hipMemcpyHostToDevice,
+                             e->stream));
+  return ZB_OK;
 }
 
 // an exchange batch header [count][total bytes] inside the avail bytes left: the records fit the batch (no overflow
@@ -3411,8 +3420,7 @@ int outbox_emit(zb_engine* e, int kind, uint8_t* dst, uint64_t cap) {
                      e->stream);
   HIPCHECK(e, hipMemsetAsync(e->on + k, 0, sizeof(uint32_t), e->stream));      // the outbox is taken
   HIPCHECK(e, hipMemsetAsync(e->on + 2 + k, 0, sizeof(uint32_t), e->stream));  // (and its byte section)
-  HIPCHECK(e, hipStreamSynchronize(e->stream));
-  return ZB_OK;
+  return ZB_OK;  // (stream-ordered: the exchange's sends / the local delivery follow on the same stream)
 }
 }  // namespace
 
@@ -3435,10 +3443,8 @@ int zb_outbox_take(zb_engine* e, int kind, uint8_t* dst, size_t cap, int dst_on_
   }
   rc = outbox_emit(e, kind, out, dst_on_device ? cap : e->ob_staging_cap);
   if (rc != ZB_OK) return rc;
-  if (!dst_on_device) {
-    HIPCHECK(e, hipMemcpyAsync(dst, e->ob_staging, *total, hipMemcpyDeviceToHost, e->stream));
-    HIPCHECK(e, hipStreamSynchronize(e->stream));
-  }
+  if (!dst_on_device) HIPCHECK(e, hipMemcpyAsync(dst, e->ob_staging, *total, hipMemcpyDeviceToHost, e->stream));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));  // (the batches are complete on return)
   return ZB_OK;
 }
 
