@@ -142,7 +142,7 @@ struct zb_engine {
   uint32_t* xlocks = nullptr;
   uint64_t* sub_jobs = nullptr;    // [job_cap] subscribe steps of a wave (models with message catch events)
   uint64_t job_cap = 0;
-  WaveHdr* h_hdr_pinned = nullptr;  // pinned mirror for D2H polling [0], the source of deliver's header upload [1]
+  WaveHdr* h_hdr_pinned = nullptr;  // pinned mirror for D2H polling
   uint32_t* h_err_pinned = nullptr;
 
   int64_t wave = 0;
@@ -364,9 +364,41 @@ struct zb_engine {
 
   // timing
   std::vector<hipEvent_t> ev;
+  // pinned upload ring (upload_async)
+  uint8_t* h_up = nullptr;
+  uint64_t h_up_cap = 0, h_up_off = 0;
 };
 
 namespace {
+
+// Host -> device copy of n bytes through the engine's pinned upload ring. A copy from pageable memory makes the
+// host wait until the GPU has run it (a staged, synchronous round trip: ~20-40 us each, a dozen per C5 step); from
+// the ring it is only stream-ordered. The ring wraps after a stream synchronisation (every earlier copy out of it
+// has run by then); a copy larger than the ring goes the pageable way.
+hipError_t upload_async(zb_engine* e, void* dst, const void* src, size_t n) {
+  if (n == 0) return hipSuccess;
+  if (!e->h_up || n > e->h_up_cap) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, e->stream);
+  if (e->h_up_off + n > e->h_up_cap) {
+    const hipError_t r = hipStreamSynchronize(e->stream);
+    if (r != hipSuccess) return r;
+    e->h_up_off = 0;
+  }
+  uint8_t* at = e->h_up + e->h_up_off;
+  std::memcpy(at, src, n);
+  e->h_up_off = (e->h_up_off + n + 63) & ~63ull;
+  return hipMemcpyAsync(dst, at, n, hipMemcpyHostToDevice, e->stream);
+}
+template <class T>
+hipError_t upload_vec(zb_engine* e, DevVec<T>& d, const std::vector<T>& v) {
+  if (v.size() > d.n || !d.p) {
+    d.free();
+    const size_t cap = v.empty() ? 1 : v.size();
+    const hipError_t r = hipMalloc(&d.p, cap * sizeof(T));
+    if (r != hipSuccess) return r;
+    d.n = cap;
+  }
+  return upload_async(e, d.p, v.data(), v.size() * sizeof(T));
+}
 
 int fail(zb_engine* e, int code, const std::string& msg) {
   e->err = msg;
@@ -872,7 +904,7 @@ int require_idle(zb_engine* e) {
 }
 
 int finish_batch(zb_engine* e) {
-  HIPCHECK(e, hipMemcpyAsync(e->hdr + (e->wave & 1), &e->host_hdr, sizeof(WaveHdr), hipMemcpyHostToDevice, e->stream));
+  HIPCHECK(e, upload_async(e, e->hdr + (e->wave & 1), &e->host_hdr, sizeof(WaveHdr)));
   HIPCHECK(e, hipGetLastError());
   HIPCHECK(e, hipMemcpyAsync(e->h_err_pinned, e->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
@@ -1289,6 +1321,8 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipHostMalloc(&e->h_err_pinned, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_ctl_pinned, sizeof(TrajCtl)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_stats_pinned, 21 * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipHostMalloc(&e->h_up, 1 << 20) != hipSuccess) return cleanup(ZB_ENOMEM);
+  e->h_up_cap = 1 << 20;
   if (hipMalloc(&e->d_spread, sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_ctl, sizeof(TrajCtl)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->t_wtot, TRAJ_WAVE_CAP * sizeof(uint4)) != hipSuccess) return cleanup(ZB_ENOMEM);
@@ -1344,6 +1378,7 @@ void zb_engine_destroy(zb_engine* e) {
   if (e->h_err_pinned) (void)hipHostFree(e->h_err_pinned);
   if (e->h_ctl_pinned) (void)hipHostFree(e->h_ctl_pinned);
   if (e->h_stats_pinned) (void)hipHostFree(e->h_stats_pinned);
+  if (e->h_up) (void)hipHostFree(e->h_up);
   e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_cls_code.free(); e->d_consts.free(); e->d_const_w.free();
   e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
   e->d_ranges.free(); e->d_cmd_pool.free(); e->d_lookup_keys.free(); e->d_lookup_pos.free();
@@ -2256,8 +2291,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     if (e->host_hdr.begin == e->host_hdr.gen_end) e->host_hdr.gen_end = e->host_hdr.end + n;
     e->host_hdr.end += n;
     e->host_hdr.arena_next += (int64_t)e->staged_arena.size();
-    HIPCHECK(e, hipMemcpyAsync(e->hdr + (e->wave & 1), &e->host_hdr, sizeof(WaveHdr), hipMemcpyHostToDevice,
-                               e->stream));
+    HIPCHECK(e, upload_async(e, e->hdr + (e->wave & 1), &e->host_hdr, sizeof(WaveHdr)));
     e->staged_pending = false;
   }
   const int64_t processed_from = e->host_hdr.begin;
@@ -2280,7 +2314,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   const bool loop = !quiescent && (max_waves == 0 || launched < max_waves);
   if (loop) HIPCHECK(e, hipMemcpyAsync(e->h_stats_pinned + 18, e->dstats + 6, sizeof(uint64_t), hipMemcpyDeviceToHost,
                                        e->stream));  // (the waves counter before the loop)
-  bool first_batch = true;
+  bool first_batch = true, stats_fresh = false;
   while (!quiescent && (max_waves == 0 || launched < max_waves)) {
     int batch = next_batch;
     next_batch = first_batch ? WAVES_PER_SYNC : std::min(2 * next_batch, WAVES_PER_SYNC_MAX);
@@ -2328,7 +2362,10 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     HIPCHECK(e, hipMemcpyAsync(e->h_hdr_pinned, e->hdr + (e->wave & 1), sizeof(WaveHdr), hipMemcpyDeviceToHost,
                                e->stream));
     HIPCHECK(e, hipMemcpyAsync(e->h_err_pinned, e->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    // (the counters too: after the batch that ends the loop they need no round trip of their own)
+    HIPCHECK(e, hipMemcpyAsync(stats_after, e->dstats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHECK(e, hipStreamSynchronize(e->stream));
+    stats_fresh = true;
     if (per_wave) {
       for (int i = 0; i < batch; i++) {
         const hipEvent_t* ev = &e->ev[EV_PER_WAVE * i];
@@ -2354,8 +2391,10 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     if (rc != ZB_OK) return rc;
     quiescent = e->host_hdr.begin == e->host_hdr.end;
   }
-  HIPCHECK(e, hipMemcpyAsync(stats_after, e->dstats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
-  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  if (!stats_fresh) {
+    HIPCHECK(e, hipMemcpyAsync(stats_after, e->dstats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHECK(e, hipStreamSynchronize(e->stream));
+  }
   if (loop && quiescent) e->wave_hint = (int)(stats_after[6] - e->h_stats_pinned[18]);  // the loop's non-empty waves
   st.records_processed = (uint64_t)(e->host_hdr.begin - processed_from);
   st.records_written = (uint64_t)(e->host_hdr.end - written_from);
@@ -2592,9 +2631,9 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
     const int rc = materialize(e);
     if (rc != ZB_OK) return rc;
   }
-  HIPCHECK(e, e->d_ranges.upload(e->ranges, e->stream));
-  HIPCHECK(e, e->d_cmd_pool.upload(e->cmd_pool, e->stream));
-  if (fc && !e->reqs.empty()) HIPCHECK(e, e->d_reqs.upload(e->reqs, e->stream));
+  HIPCHECK(e, upload_vec(e, e->d_ranges, e->ranges));
+  HIPCHECK(e, upload_vec(e, e->d_cmd_pool, e->cmd_pool));
+  if (fc && !e->reqs.empty()) HIPCHECK(e, upload_vec(e, e->d_reqs, e->reqs));
   SerParams sp{};
   sp.nt = 1;
   if (fc) {
@@ -3060,7 +3099,7 @@ int deliver(zb_engine* e, int kind, const uint8_t* buf, const std::vector<uint64
     return fail(e, ZB_ENOMEM, "subscription store capacity");
   std::vector<uint64_t> table(first);
   table.insert(table.end(), off.begin(), off.end());
-  HIPCHECK(e, e->d_slices.upload(table, e->stream));
+  HIPCHECK(e, upload_vec(e, e->d_slices, table));
   MsgParams p = msg_params(e);
   p.in = buf;
   p.nslices = (int32_t)first.size();
@@ -3115,9 +3154,7 @@ int deliver(zb_engine* e, int kind, const uint8_t* buf, const std::vector<uint64
   if (rc != ZB_OK) return rc;
   e->records_total += recs;
   e->arena_total += (uint64_t)(e->host_hdr.arena_next - arena_before);
-  e->h_hdr_pinned[1] = e->host_hdr;  // (pinned source: the copy may run after this call returns)
-  HIPCHECK(e, hipMemcpyAsync(e->hdr + (e->wave & 1), e->h_hdr_pinned + 1, sizeof(WaveHdr), hipMemcpyHostToDevice,
-                             e->stream));
+  HIPCHECK(e, upload_async(e, e->hdr + (e->wave & 1), &e->host_hdr, sizeof(WaveHdr)));
   return ZB_OK;
 }
 
@@ -3480,7 +3517,7 @@ int outbox_emit(zb_engine* e, int kind, uint8_t* dst, uint64_t cap) {
   if (e->ob_plan_total > cap) return fail(e, ZB_ENOMEM, "outbox destination too small");
   const int P = e->cfg.partition_count;
   const int k = kind - 1;
-  HIPCHECK(e, hipMemcpyAsync(e->ob_base, e->ob_plan_base, P * 8, hipMemcpyHostToDevice, e->stream));
+  HIPCHECK(e, upload_async(e, e->ob_base, e->ob_plan_base, P * 8));
   launch_outbox_pack(outbox(e, kind), e->ob_idx_out, e->ob_keys, e->ob_plan_n, e->ob_first, e->ob_goff, e->ob_base, dst,
                      e->stream);
   HIPCHECK(e, hipMemsetAsync(e->on + k, 0, sizeof(uint32_t), e->stream));      // the outbox is taken
