@@ -93,6 +93,27 @@ def test_published_first_ttl_duplicates_and_rejections():
     assert recs, "expected CORRELATE rejections"
 
 
+@pytest.mark.parametrize("P", [1, 3])
+def test_one_message_many_subscriptions(P):
+    """One PUBLISH matching many open subscriptions: its CORRELATE commands leave in findSubscriptions' insertion
+    order (the outbox orders them by their rank among the message's matches, up to 32, and by the store index
+    beyond), interleaved with other messages' correlations."""
+    gpu, ref, cg, co = clusters(P, catch_workflow())
+    keys = ["shared"] * 45 + ["five"] * 5 + ["order-%d" % i for i in range(10)]
+    for i, key in enumerate(keys):
+        gpu[i % P].create("wf", [msgpack.packb({"orderId": key})])
+        ref[i % P].create("wf", msgpack.packb({"orderId": key}))
+    cg.settle()
+    co.settle()
+    compare(gpu, ref)
+    cks = [b"order-3", b"shared", b"five", b"order-7"]
+    pls = [msgpack.packb({"m": i}) for i in range(len(cks))]
+    cg.publish(b"order canceled", cks, pls)
+    co.publish(b"order canceled", cks, pls)
+    compare(gpu, ref)
+    assert sum(g.counters()["completed"] for g in gpu) == 45 + 5 + 2
+
+
 def test_integer_correlation_key():
     # extractCorrelationKey: a long becomes its 8 little-endian bytes (hash routing and store key)
     P = 3
