@@ -860,15 +860,21 @@ int ensure_stores(zb_engine* e) {
 // order is the same in every key, so the differing bits are those of the raw keys.
 using OnesweepSort = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                                 rocprim::default_config, 0>;
+// spread_known: the spread is already in h_stats_pinned[17] (the caller launched k_key_spread and read it back with
+// a round trip of its own)
 template <class K, class V>
-int sort_pairs(zb_engine* e, const K* kin, K* kout, const V* vin, V* vout, uint64_t n, const char* what) {
+int sort_pairs(zb_engine* e, const K* kin, K* kout, const V* vin, V* vout, uint64_t n, const char* what,
+               bool spread_known = false) {
   static_assert(sizeof(K) == 8, "64-bit keys");
   if (n == 0) return ZB_OK;
   if (n > (uint64_t)INT32_MAX) return fail(e, ZB_EUNSUPPORTED, std::string(what) + ": more than 2^31 keys");
-  HIPCHECK(e, hipMemsetAsync(e->d_spread, 0, sizeof(uint64_t), e->stream));
-  launch_key_spread((const uint64_t*)kin, n, e->d_spread, e->stream);
-  HIPCHECK(e, hipMemcpyAsync(e->h_stats_pinned + 17, e->d_spread, sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
-  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  if (!spread_known) {
+    HIPCHECK(e, hipMemsetAsync(e->d_spread, 0, sizeof(uint64_t), e->stream));
+    launch_key_spread((const uint64_t*)kin, n, e->d_spread, e->stream);
+    HIPCHECK(e, hipMemcpyAsync(e->h_stats_pinned + 17, e->d_spread, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                               e->stream));
+    HIPCHECK(e, hipStreamSynchronize(e->stream));
+  }
   const uint64_t spread = e->h_stats_pinned[17];
   if (spread == 0) {  // one key (or all equal): the input order
     HIPCHECK(e, hipMemcpyAsync(kout, kin, n * sizeof(K), hipMemcpyDeviceToDevice, e->stream));
@@ -3466,12 +3472,19 @@ int outbox_plan(zb_engine* e, int kind, uint64_t* bytes_per_target, uint64_t* co
   for (int q = 0; q < P; q++) bytes_per_target[q] = counts[q] = 0;
   *total = 0;
   e->ob_plan_kind = 0;
+  const int k = kind - 1;
+  // the key spread of the sort below, over the device-side count: read back in the count's round trip
+  if (e->on) {
+    HIPCHECK(e, hipMemsetAsync(e->d_spread, 0, sizeof(uint64_t), e->stream));
+    launch_key_spread(e->okeys[k], e->ocap, e->d_spread, e->stream, e->on + k);
+    HIPCHECK(e, hipMemcpyAsync(e->h_stats_pinned + 17, e->d_spread, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                               e->stream));
+  }
   uint64_t n = 0;
-  int rc = zb_outbox_count(e, kind, &n);
+  int rc = zb_outbox_count(e, kind, &n);  // (its synchronisation covers the spread)
   if (rc != ZB_OK) return rc;
   *n_out = n;
   if (n == 0) return ZB_OK;
-  const int k = kind - 1;
   if (!e->ob_keys) {  // sort buffers, allocated once at the outbox capacity
     const uint64_t c = e->ocap;
     if (hipMalloc(&e->ob_keys, c * 8) != hipSuccess || hipMalloc(&e->ob_idx_in, c * 4) != hipSuccess ||
@@ -3485,7 +3498,8 @@ int outbox_plan(zb_engine* e, int kind, uint64_t* bytes_per_target, uint64_t* co
     if (hipMalloc(&e->ob_tmp, e->ob_tmp_bytes + 16) != hipSuccess) return fail(e, ZB_ENOMEM, "outbox scan scratch");
   }
   launch_iota(e->ob_idx_in, n, e->stream);
-  rc = sort_pairs(e, (const uint64_t*)e->okeys[k], e->ob_keys, (const uint32_t*)e->ob_idx_in, e->ob_idx_out, n, "outbox");
+  rc = sort_pairs(e, (const uint64_t*)e->okeys[k], e->ob_keys, (const uint32_t*)e->ob_idx_in, e->ob_idx_out, n, "outbox",
+                  true);
   if (rc != ZB_OK) return rc;
   const Outbox ob = outbox(e, kind);
   launch_outbox_sizes(ob, e->ob_idx_out, n, e->ob_sizes, e->stream);

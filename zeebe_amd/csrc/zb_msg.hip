@@ -494,8 +494,12 @@ __global__ void k_iota(uint32_t* p, uint64_t n) {
 }
 
 // the key bits that differ between the keys of a sort: OR over i of keys[i] ^ keys[0] (the radix sort then runs over
-// [lowest, highest] of them only)
-__global__ void __launch_bounds__(256) k_key_spread(const uint64_t* keys, uint64_t n, unsigned long long* out) {
+// [lowest, highest] of them only). n_dev: the count is read on the device (min(*n_dev, n)), so that the host reads the
+// spread in the same round trip as the count
+__global__ void __launch_bounds__(256) k_key_spread(const uint64_t* keys, uint64_t n, unsigned long long* out,
+                                                    const uint32_t* n_dev) {
+  if (n_dev) n = std::min<uint64_t>(n, *n_dev);
+  if (n == 0) return;
   __shared__ uint64_t s[4];
   const uint64_t k0 = keys[0];
   uint64_t acc = 0;
@@ -557,9 +561,9 @@ void launch_outbox_pack(const Outbox& ob, const uint32_t* idx, const uint64_t* k
 void launch_iota(uint32_t* p, uint64_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_iota, dim3(blocks((int64_t)n)), dim3(256), 0, s, p, n);
 }
-void launch_key_spread(const uint64_t* keys, uint64_t n, uint64_t* out, hipStream_t s) {
+void launch_key_spread(const uint64_t* keys, uint64_t n, uint64_t* out, hipStream_t s, const uint32_t* n_dev) {
   if (n) hipLaunchKernelGGL(k_key_spread, dim3(std::min<uint64_t>((n + 1023) / 1024, 512)), dim3(256), 0, s, keys, n,
-                           (unsigned long long*)out);
+                           (unsigned long long*)out, n_dev);
 }
 
 }  // namespace zbg
