@@ -32,7 +32,8 @@ using namespace zbg;
 namespace {
 
 constexpr int WAVES_PER_SYNC = 16;      // the first batch; each later batch of the step doubles, up to
-constexpr int WAVES_PER_SYNC_MAX = 64;  // (long chains: fewer host round trips, at most one batch of empty waves)
+constexpr int WAVES_PER_SYNC_MAX = 64;
+constexpr int TRAJ_RETRY = 15;  // batches that go straight to the wave pipeline after a trajectory fallback  // (long chains: fewer host round trips, at most one batch of empty waves)
 constexpr int EV_PER_WAVE = 4;  // before k_process, after k_process, after k_emit, after the aux kernels
 constexpr uint64_t STATIC_ARENA_BYTES = 1ull << 20;  // {} at ref 0 + harness job completion payloads
 constexpr uint64_t TRAJ_BUDGET_BYTES = 256ull << 20;  // per-(generation, workgroup) counts of the trajectory path
@@ -268,7 +269,8 @@ struct zb_engine {
   void* ob_tmp = nullptr;  // (scan scratch)
   size_t ob_tmp_bytes = 0;
   uint32_t ob_counts_read[2] = {0, 0};  // both outbox command counts at the last zb_outbox_count
-  int wave_hint = 0;     // non-empty waves of the last step's wave loop (its first batch, zb_step)
+  int wave_hint = 0;
+  int traj_skip = 0;     // batches left that skip the trajectory attempt after a fallback (zb_step)     // non-empty waves of the last step's wave loop (its first batch, zb_step)
   int ob_plan_kind = 0;  // the outbox kind outbox_plan sorted and sized last (0: none)
   uint64_t ob_plan_n = 0, ob_plan_total = 0, ob_plan_base[64] = {};
   uint8_t* ob_staging = nullptr;
@@ -1523,6 +1525,7 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
   }
   // the trajectory count pass skips payload merges, so conditions must never read a merge result
   e->traj_model_ok = !(e->has_merges && e->has_splits) && !e->has_io;
+  e->traj_skip = 0;  // (a new model: try the trajectory path again)
   // class batches: every split of the model is one digit (radix conditions + 2) of an 8-bit outcome key
   e->nsplits = 0;
   e->cls_ok = true;
@@ -2308,9 +2311,17 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   HIPCHECK(e, hipMemcpyAsync(stats_before, e->dstats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
   uint32_t launched = 0;
   bool quiescent = e->host_hdr.begin == e->host_hdr.end;
+  // A batch the trajectory path falls back from (a message subscription, a termination, ... on some instance's
+  // path) costs a class attempt and a per-instance attempt before the wave pipeline runs it (C5: ~0.35 ms of a
+  // 6.6 ms step); after a fallback the next TRAJ_RETRY batches of the model go straight to the wave pipeline.
+  if (try_traj && e->traj_skip > 0) {
+    e->traj_skip--;
+    try_traj = false;
+  }
   if (try_traj && !quiescent) {
     int rc = run_trajectory(e, traj_base, traj_n, st, true);
     if (rc < 0) return rc;
+    if (rc == 0) e->traj_skip = TRAJ_RETRY;
     quiescent = e->host_hdr.begin == e->host_hdr.end;
   }
   // the first batch: as many waves as the last step's wave loop had (a tick of the same workload settles in as
