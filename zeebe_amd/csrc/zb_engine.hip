@@ -32,8 +32,9 @@ using namespace zbg;
 namespace {
 
 constexpr int WAVES_PER_SYNC = 16;      // the first batch; each later batch of the step doubles, up to
-constexpr int WAVES_PER_SYNC_MAX = 64;
-constexpr int TRAJ_RETRY = 15;  // batches that go straight to the wave pipeline after a trajectory fallback  // (long chains: fewer host round trips, at most one batch of empty waves)
+constexpr int WAVES_PER_SYNC_MAX = 64;  // (long chains: fewer host round trips, at most one batch of empty waves)
+constexpr int TRAJ_RETRY = 15;  // batches that go straight to the wave pipeline after a trajectory fallback
+constexpr int JOB_COUNTS = 8 + 2 * SUB_STRIPES;  // merge / cond / (unused) / slow-merge counts, the subscribe stripes
 constexpr int EV_PER_WAVE = 4;  // before k_process, after k_process, after k_emit, after the aux kernels
 constexpr uint64_t STATIC_ARENA_BYTES = 1ull << 20;  // {} at ref 0 + harness job completion payloads
 constexpr uint64_t TRAJ_BUDGET_BYTES = 256ull << 20;  // per-(generation, workgroup) counts of the trajectory path
@@ -134,8 +135,8 @@ struct zb_engine {
   uint64_t* derr_info = nullptr;
   MergeJob* merge_jobs = nullptr;
   uint64_t* cond_jobs = nullptr;
-  uint32_t* job_counts = nullptr;  // [0..1] merge counts, [2..3] cond counts, [4..5] subscribe counts,
-                                   // [6..7] merges left to the general merger
+  uint32_t* job_counts = nullptr;  // [0..1] merge counts, [2..3] cond counts, [4..5] unused,
+                                   // [6..7] merges left to the general merger, [8..] subscribe counts [2][SUB_STRIPES]
   uint32_t* merge_slow = nullptr;  // [job_cap] indices of those merges
   unsigned long long* phase = nullptr;  // (ZB_PHASES measurement build) k_wave phase sums
   PubUpload pub_up{};                   // a PUBLISH batch uploaded by zb_upload_publishes, not processed yet
@@ -529,7 +530,7 @@ WaveParams wave_params(zb_engine* e) {
   p.cond_jobs = e->cond_jobs;
   p.cond_count = e->job_counts + 2;
   p.sub_jobs = e->sub_jobs;
-  p.sub_count = e->job_counts + 4;
+  p.sub_count = e->job_counts + 8;  // [2][SUB_STRIPES]
   p.job_cap = e->job_cap;
   p.stats = e->dstats;
   p.log_cap = (uint64_t)e->win_base + e->cfg.log_capacity;  // absolute: the window's end
@@ -1323,7 +1324,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   e->job_cap = std::min<uint64_t>(L, 1ull << 26);
   if (hipMalloc(&e->merge_jobs, 2 * e->job_cap * sizeof(MergeJob)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->cond_jobs, 2 * e->job_cap * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipMalloc(&e->job_counts, 8 * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->job_counts, JOB_COUNTS * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->merge_slow, e->job_cap * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_hdr_pinned, 2 * sizeof(WaveHdr)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_err_pinned, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
@@ -1438,7 +1439,7 @@ int zb_reset(zb_engine* e, int keep_staged) {
   HIPCHECK(e, hipMemcpyAsync(e->hdr, &h, sizeof(h), hipMemcpyHostToDevice, e->stream));
   HIPCHECK(e, hipMemsetAsync(e->derr, 0, sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->derr_info, 0xff, sizeof(uint64_t), e->stream));
-  HIPCHECK(e, hipMemsetAsync(e->job_counts, 0, 8 * sizeof(uint32_t), e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->job_counts, 0, JOB_COUNTS * sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->dstats, 0, 8 * sizeof(uint64_t), e->stream));
   if (e->jobs.keys) {
     HIPCHECK(e, hipMemsetAsync(e->jobs.keys, 0, (e->jobs.mask + 1) * sizeof(int64_t), e->stream));  // JOB_EMPTY
@@ -4051,7 +4052,7 @@ int zb_restore(zb_engine* e, const uint8_t* buf, size_t len) {
   e->rows_mark = h.rows;  // (a snapshot holds live state only)
   e->arena_mark = STATIC_ARENA_BYTES + h.arena_dyn;
   e->wave = 0;  // (and the per-wave job queues of both parities empty, whatever wave ran last)
-  HIPCHECK(e, hipMemsetAsync(e->job_counts, 0, 8 * sizeof(uint32_t), e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->job_counts, 0, JOB_COUNTS * sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMemcpy(e->dstats, h.stats, sizeof(h.stats), hipMemcpyHostToDevice));
   return finish_batch(e);
 }

@@ -696,18 +696,27 @@ __device__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t p
   }
 }
 
+// the next wave's subscribe-step counters (one thread)
+__device__ __forceinline__ void clear_sub_counts(const WaveParams& P) {
+  for (int s = 0; s < SUB_STRIPES; s++) P.sub_count[((P.wave + 1) & 1) * SUB_STRIPES + s] = 0;
+}
+
 // The open-subscription command of a SUBSCRIBE step (SubscribeMessageHandler :77-141,
 // SubscriptionCommandSender.openMessageSubscription :83-103): the correlation key extracted from the
 // element instance's payload, routed to abs(hash(correlationKey) % P), ordered by the catch event's log
 // position. One thread per subscribe step of the wave (k_process listed them).
 __global__ void __launch_bounds__(256) k_subscribe(WaveParams P) {
   __shared__ uint32_t s_alloc[2 * (256 / 64) + 2];
-  const uint32_t n = P.sub_count[P.wave & 1];
-  // (uniform trip count per workgroup: block_alloc2 below is a workgroup-wide operation)
+  const uint64_t scap = P.job_cap / SUB_STRIPES;
   const uint64_t stride = (uint64_t)gridDim.x * 256;
-  for (uint64_t j0 = (uint64_t)blockIdx.x * 256; j0 < n && j0 < P.job_cap; j0 += stride) {
+#pragma unroll 1
+  for (int s = 0; s < SUB_STRIPES; s++) {
+  const uint64_t n = std::min<uint64_t>(P.sub_count[(P.wave & 1) * SUB_STRIPES + s], scap);
+  const uint64_t* jobs = P.sub_jobs + s * scap;
+  // (uniform trip count per workgroup: block_alloc2 below is a workgroup-wide operation)
+  for (uint64_t j0 = (uint64_t)blockIdx.x * 256; j0 < n; j0 += stride) {
     const uint64_t j = j0 + threadIdx.x;
-    const bool act = j < n && j < P.job_cap;
+    const bool act = j < n;
     uint32_t err = 0, site = 0, ck_len = 0, gran = 0, rself = NO_ROW;
     int64_t pos = 0;
     zb_rec rec{};
@@ -715,7 +724,7 @@ __global__ void __launch_bounds__(256) k_subscribe(WaveParams P) {
     uint8_t ckbuf[8];
     const DevElem* el = nullptr;
     if (act) {
-      pos = (int64_t)P.sub_jobs[j];
+      pos = (int64_t)jobs[j];
       rec = P.log[pos];
       rself = (uint32_t)P.links[pos];
       el = &P.elems[rec.elem];
@@ -753,6 +762,7 @@ __global__ void __launch_bounds__(256) k_subscribe(WaveParams P) {
       atomicOr(P.err, err);
       atomicMin((unsigned long long*)P.err_info, ((unsigned long long)pos << 8) | site);
     }
+  }
   }
 }
 
@@ -862,10 +872,12 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
              ((uint64_t)t.completed << 48);
     acc_bytes += t.bytes;
     acc_created += t.created | (t.canceled << 16);
-    if (__ballot(t.sub)) {  // wave-uniform: this tile's subscribe steps, in the wave's job list
-      const uint32_t slot = wave_alloc(P.sub_count + (P.wave & 1), t.sub ? 1u : 0u);
+    if (__ballot(t.sub)) {  // wave-uniform: this tile's subscribe steps, in the wave's job list (its stripe)
+      const uint32_t s = blockIdx.x % SUB_STRIPES;
+      const uint64_t scap = P.job_cap / SUB_STRIPES;
+      const uint32_t slot = wave_alloc(P.sub_count + (P.wave & 1) * SUB_STRIPES + s, t.sub ? 1u : 0u);
       if (t.sub) {
-        if (slot < P.job_cap) P.sub_jobs[slot] = (uint64_t)t.sub_pos;
+        if (slot < scap) P.sub_jobs[s * scap + slot] = (uint64_t)t.sub_pos;
         else fail_at(t, DE_LOG_FULL, 36);
       }
     }
@@ -1065,7 +1077,7 @@ __global__ void __launch_bounds__(SCAN_WG) k_scan(WaveParams P) {
     *hout = h;
     if (P.need_children) *P.need_children = 0;  // k_pre of the next chunk sets it again
     P.merge_count[P.wave & 1] = c.n > 0 ? (uint32_t)tot[5] : 0;
-    if (P.sub_count) P.sub_count[(P.wave + 1) & 1] = 0;  // the next wave's subscribe list
+    if (P.sub_count) clear_sub_counts(P);  // the next wave's subscribe list
     P.cond_count[P.wave & 1] = c.n > 0 ? (uint32_t)tot[6] : 0;
   }
 }
@@ -1287,7 +1299,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
       if (P.need_children) *P.need_children = 0;
       P.merge_count[P.wave & 1] = 0;
       P.cond_count[P.wave & 1] = 0;
-      if (P.sub_count) P.sub_count[(P.wave + 1) & 1] = 0;
+      if (P.sub_count) clear_sub_counts(P);
     }
     return;
   }
@@ -1356,10 +1368,12 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
       inf.d_b = t.d_b; inf.has_detail = t.detail; inf.ns = (uint8_t)t.ns;
       P.info[i] = inf;
     }
-    if (__ballot(t.sub)) {  // wave-uniform: this tile's subscribe steps, in the wave's job list
-      const uint32_t slot = wave_alloc(P.sub_count + (P.wave & 1), t.sub ? 1u : 0u);
+    if (__ballot(t.sub)) {  // wave-uniform: this tile's subscribe steps, in the wave's job list (its stripe)
+      const uint32_t s = blockIdx.x % SUB_STRIPES;
+      const uint64_t scap = P.job_cap / SUB_STRIPES;
+      const uint32_t slot = wave_alloc(P.sub_count + (P.wave & 1) * SUB_STRIPES + s, t.sub ? 1u : 0u);
       if (t.sub) {
-        if (slot < P.job_cap) P.sub_jobs[slot] = (uint64_t)t.sub_pos;
+        if (slot < scap) P.sub_jobs[s * scap + slot] = (uint64_t)t.sub_pos;
         else fail_at(t, DE_LOG_FULL, 36);
       }
     }
@@ -1510,7 +1524,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
         if (P.need_children) *P.need_children = 0;  // k_pre of the next chunk sets it again
         P.merge_count[P.wave & 1] = (uint32_t)s_tot[6];
         P.cond_count[P.wave & 1] = (uint32_t)s_tot[7];
-        if (P.sub_count) P.sub_count[(P.wave + 1) & 1] = 0;  // the next wave's subscribe list
+        if (P.sub_count) clear_sub_counts(P);  // the next wave's subscribe list
       }
     }
     __syncthreads();
