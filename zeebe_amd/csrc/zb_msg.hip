@@ -55,21 +55,6 @@ __device__ __forceinline__ void put_record(const MsgParams& P, int64_t pos, cons
   P.vlen[pos] = VLEN_UNKNOWN;
 }
 
-// an arena blob of `len` bytes after its length word, allocated on the wave header's bump pointer
-__device__ __forceinline__ uint8_t* alloc_blob(const MsgParams& P, uint32_t len, uint32_t& ref, uint32_t& err) {
-  const uint64_t bytes = (4 + (uint64_t)len + 7) & ~7ull;
-  const uint64_t at = atomicAdd((unsigned long long*)&P.hdr->arena_next, (unsigned long long)bytes);
-  if (at + bytes > P.arena_cap) {
-    err |= DE_ARENA_FULL;
-    return nullptr;
-  }
-  uint8_t* b = P.arena + at;
-  *(uint32_t*)b = len;
-  for (uint64_t k = 4 + len; k < bytes; k++) b[k] = 0;
-  ref = (uint32_t)(at >> 3);
-  return b;
-}
-
 // command i of the delivered batches: its header and its variable bytes
 __device__ __forceinline__ zb_exchange_rec delivered(const MsgParams& P, int64_t i, const uint8_t*& var) {
   int lo = 0, hi = P.nslices - 1;
