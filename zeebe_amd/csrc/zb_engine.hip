@@ -316,6 +316,7 @@ struct zb_engine {
   uint64_t x_cap = 0;
   DevVec<int64_t> d_lookup_keys, d_lookup_pos;    // zb_submit lookups of the staged batch: key, staged index
   uint64_t staged_nlook = 0;
+  uint64_t staged_lookup_spread = 0;  // OR of key ^ first key over the staged lookups (upload_staged)
   int64_t *look_keys = nullptr, *look_idx = nullptr;  // sorted on the device by zb_step
   uint64_t look_cap = 0;
   // radix sorts of (key, value) pairs (sort_pairs): scratch and the spread of the keys
@@ -1687,11 +1688,14 @@ int upload_staged(zb_engine* e) {
   e->staged_nlook = 0;
   if (!e->staged_only_creates) {  // (CREATE-only batches name no element instance)
     std::vector<int64_t> lk, li;
+    uint64_t spread = 0;  // (the device sort's key bits, known here: zb_step needs no round trip for them)
     for (size_t i = 0; i < e->staged_lookup.size(); i++)
       if (e->staged_lookup[i] != INT64_MIN) {
         lk.push_back(e->staged_lookup[i]);
         li.push_back((int64_t)i);
+        spread |= (uint64_t)lk.back() ^ (uint64_t)lk[0];
       }
+    e->staged_lookup_spread = spread;
     if (!lk.empty()) {
       HIPCHECK(e, e->d_lookup_keys.upload(lk, e->stream));
       HIPCHECK(e, e->d_lookup_pos.upload(li, e->stream));
@@ -2276,8 +2280,9 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
         HIPCHECK(e, hipMalloc(&e->look_idx, c * sizeof(int64_t)));
         e->look_cap = c;
       }
+      e->h_stats_pinned[17] = e->staged_lookup_spread;  // (computed on the host by upload_staged)
       int rc = sort_pairs(e, (const int64_t*)e->d_lookup_keys.p, e->look_keys, (const int64_t*)e->d_lookup_pos.p,
-                          e->look_idx, m, "lookup");
+                          e->look_idx, m, "lookup", true);
       if (rc != ZB_OK) return rc;
       ResolveParams rp{};
       rp.rmeta = e->rmeta; rp.rkeys = e->rkeys; rp.rows = (uint64_t)e->host_hdr.rows_next;
