@@ -2217,6 +2217,14 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   if (e->failed) return fail(e, ZB_EPROCESSING, "partition stopped after a processing failure: " + e->err);
   HIPCHECK(e, hipSetDevice(e->cfg.device));
   auto t0 = std::chrono::steady_clock::now();
+#ifdef ZB_PHASES  // (measurement build: host time per part of the step, waits at its round trips included)
+  auto sp0 = t0;
+  double sp[6] = {0};
+#define ZB_SP(k) do { auto n_ = std::chrono::steady_clock::now(); \
+    sp[k] += std::chrono::duration<double, std::milli>(n_ - sp0).count(); sp0 = n_; } while (0)
+#else
+#define ZB_SP(k) do { } while (0)
+#endif
   zb_step_stats st{};
   bool try_traj = false;
   {
@@ -2225,6 +2233,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     mrc = maintain(e, false);  // released records leave the window; compaction when a region is half full
     if (mrc != ZB_OK) return mrc;
   }
+  ZB_SP(0);  // settle / maintain (compaction)
   const int64_t rows_before = e->host_hdr.rows_next, arena_before = e->host_hdr.arena_next;
   const int64_t end_before = e->host_hdr.end;  // records appended by this call: injected input + follow-ups
   int64_t traj_base = 0, traj_n = 0;
@@ -2309,6 +2318,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     HIPCHECK(e, upload_async(e, e->hdr + (e->wave & 1), &e->host_hdr, sizeof(WaveHdr)));
     e->staged_pending = false;
   }
+  ZB_SP(1);  // inject, lookups
   const int64_t processed_from = e->host_hdr.begin;
   const int64_t written_from = e->host_hdr.end;
   // counters before / after the step: stream-ordered copies into pinned memory, read after the step's last sync
@@ -2330,6 +2340,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     if (rc == 0) e->traj_skip = TRAJ_RETRY;
     quiescent = e->host_hdr.begin == e->host_hdr.end;
   }
+  ZB_SP(2);  // trajectory
   // the first batch: as many waves as the last step's wave loop had (a tick of the same workload settles in as
   // many waves, and each launch past quiescence costs ~20 us of empty kernels), else WAVES_PER_SYNC; later
   // batches WAVES_PER_SYNC, doubling
@@ -2414,6 +2425,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     if (rc != ZB_OK) return rc;
     quiescent = e->host_hdr.begin == e->host_hdr.end;
   }
+  ZB_SP(3);  // wave loop
   if (!stats_fresh) {
     HIPCHECK(e, hipMemcpyAsync(stats_after, e->dstats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHECK(e, hipStreamSynchronize(e->stream));
@@ -2431,6 +2443,12 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   e->arena_total += (uint64_t)std::max<int64_t>(0, e->host_hdr.arena_next - arena_before);
   e->records_total += (uint64_t)(e->host_hdr.end - end_before);
   st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  ZB_SP(4);  // tail
+#ifdef ZB_PHASES
+  if (launched) fprintf(stderr, "step ms: maintain %.3f inject %.3f traj %.3f waves %.3f tail %.3f (%u launches)\n",
+                        sp[0], sp[1], sp[2], sp[3], sp[4], launched);
+#endif
+#undef ZB_SP
   if (stats) *stats = st;
   if (!quiescent) return ZB_EAGAIN;
   e->term = false;  // every termination chain has ended
