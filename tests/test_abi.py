@@ -25,6 +25,16 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, s), s
 
 
+def test_config_flags_match_header():
+    """Every ZB_CFG_* flag of include/zb_engine.h has the same value as engine.CFG_* (the Python binding's copy)."""
+    src = open(os.path.join(ROOT, "include", "zb_engine.h")).read()
+    flags = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define ZB_CFG_(\w+)\s+(\d+)", src)}
+    assert flags and "RCCL_SELF" in flags, flags
+    for name, value in flags.items():
+        assert getattr(engine, "CFG_" + name) == value, name
+    assert len(set(flags.values())) == len(flags)  # (distinct bits)
+
+
 def test_config_struct_layout_matches_header():
     assert ctypes.sizeof(engine.zb_config) == 48
     assert ctypes.sizeof(engine.zb_rec) == 32
