@@ -2348,11 +2348,13 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   const bool loop = !quiescent && (max_waves == 0 || launched < max_waves);
   if (loop) HIPCHECK(e, hipMemcpyAsync(e->h_stats_pinned + 18, e->dstats + 6, sizeof(uint64_t), hipMemcpyDeviceToHost,
                                        e->stream));  // (the waves counter before the loop)
-  bool first_batch = true, stats_fresh = false;
+  // batches follow the hint until it is used up (C2: 148 waves as 64 + 64 + 20, not 64 + 16 + 32 + 64 with 28 empty
+  // waves), then WAVES_PER_SYNC, doubling
+  const int hint = e->wave_hint;
+  int grow = WAVES_PER_SYNC;
+  bool stats_fresh = false;
   while (!quiescent && (max_waves == 0 || launched < max_waves)) {
     int batch = next_batch;
-    next_batch = first_batch ? WAVES_PER_SYNC : std::min(2 * next_batch, WAVES_PER_SYNC_MAX);
-    first_batch = false;
     if (max_waves) batch = std::min<int>(batch, (int)(max_waves - launched));
     // timing events cost ~5 us of stream time each between kernels (C2: 4 per wave = 2.9 ms of a 41 ms
     // step): per wave only with ZB_CFG_WAVE_EVENTS (process / emit / aux split), else one pair per batch
@@ -2420,6 +2422,12 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     }
     launched += batch;
     st.launches += batch;
+    if (hint > (int)launched) {
+      next_batch = std::min<int>(hint - (int)launched, WAVES_PER_SYNC_MAX);
+    } else {
+      next_batch = grow;
+      grow = std::min(2 * grow, WAVES_PER_SYNC_MAX);
+    }
     e->host_hdr = e->h_hdr_pinned[0];
     int rc = check_device_errors(e, *e->h_err_pinned);
     if (rc != ZB_OK) return rc;
