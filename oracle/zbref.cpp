@@ -1941,6 +1941,68 @@ int64_t zbref_map(const uint8_t* src, size_t ns, const uint8_t* tgt, size_t nt, 
   }
 }
 
+// MsgPackTree as MsgPackDocumentIndexer.index (mode 0) or MsgPackDocumentExtractor.extract (mode 1, mappings
+// "source\ttarget\n"...) builds it for doc, in the dump format of tests/native/devlib_host.cpp devlib_xtree_dump (nodes
+// sorted by id here). Returns the dump length, -1 MappingException / -2 other failure (err has the message).
+int64_t zbref_tree_dump(const uint8_t* doc, size_t n, const char* mappings, int mode, char* out, size_t cap, char* err,
+                        size_t errcap) {
+  try {
+    bytes d((const char*)doc, n);
+    MsgPackTree t;
+    if (mode == 0) {
+      DocumentIndexer ix;
+      ix.index(t, d);
+    } else {
+      std::vector<Mapping> ms;
+      JsonPathCompiler jc;
+      std::string all(mappings);
+      size_t p = 0;
+      while (p < all.size()) {
+        size_t nl = all.find('\n', p);
+        if (nl == std::string::npos) nl = all.size();
+        std::string line = all.substr(p, nl - p);
+        size_t tab = line.find('\t');
+        if (tab != std::string::npos) ms.push_back({jc.compile(line.substr(0, tab)), line.substr(tab + 1)});
+        p = nl + 1;
+      }
+      extract_mappings(t, d, ms);
+    }
+    std::vector<std::string> ids;
+    for (auto& kv : t.node_type) ids.push_back(kv.first);
+    std::sort(ids.begin(), ids.end());
+    std::string o;
+    static const char HEX[] = "0123456789abcdef";
+    for (auto& id : ids) {
+      const NodeType nt = t.node_type.at(id);
+      o += nt == NodeType::MAP ? 'M' : nt == NodeType::ARRAY ? 'A' : nt == NodeType::EXTRACTED_LEAF ? 'X' : 'L';
+      o += '\0';
+      o += id;
+      o += '\0';
+      auto c = t.childs.find(id);
+      if (c != t.childs.end())
+        for (size_t k = 0; k < c->second.order.size(); k++) {
+          if (k) o += '\x1e';
+          o += c->second.order[k];
+        }
+      o += '\0';
+      auto l = t.leaf.find(id);
+      if (l != t.leaf.end()) {
+        const uint32_t pos = (uint32_t)(l->second >> 32), len = (uint32_t)l->second;
+        for (uint32_t k = 0; k < len; k++) { o += HEX[(uint8_t)d[pos + k] >> 4]; o += HEX[(uint8_t)d[pos + k] & 15]; }
+      }
+      o += '\n';
+    }
+    if (o.size() <= cap) std::memcpy(out, o.data(), o.size());
+    return (int64_t)o.size();
+  } catch (const MappingError& ex) {
+    std::snprintf(err, errcap, "%s", ex.what());
+    return -1;
+  } catch (const std::exception& ex) {
+    std::snprintf(err, errcap, "%s", ex.what());
+    return -2;
+  }
+}
+
 // returns #results (positions/lengths written pairwise), -1 invalid query (err has message)
 int zbref_query(const char* path, const uint8_t* doc, size_t n, int32_t* out, int cap, char* err, size_t errcap) {
   JsonPathCompiler jc;
@@ -1957,6 +2019,69 @@ int zbref_query(const char* path, const uint8_t* doc, size_t n, int32_t* out, in
     k++;
   }
   return k;
+}
+
+// JsonPathTokenizer.tokenize: (token, position, length) triples in visit order, token = JpToken's enum index
+int zbref_jp_tokens(const char* expr, int32_t* out, int cap) {
+  int k = 0;
+  jp_tokenize(bytes(expr), [&](JpToken t, int off, int len) {
+    if (k < cap) { out[3 * k] = (int32_t)t; out[3 * k + 1] = off; out[3 * k + 2] = len; }
+    k++;
+  });
+  return k;
+}
+
+// JsonPathQueryCompiler.compile: the filter instances (filter id, index) -- #instances, or -1 for an invalid query
+// with its invalid position and error reason (JsonPathQuery.getInvalidPosition / getErrorReason)
+int zbref_jp_compile(const char* expr, int32_t* ids, int32_t* idx, int cap, int32_t* invalid_pos, char* err,
+                     size_t errcap) {
+  JsonPathCompiler jc;
+  JsonPathQuery q = jc.compile(bytes(expr));
+  *invalid_pos = q.invalid_position;
+  if (!q.valid()) {
+    std::snprintf(err, errcap, "%s", q.error.c_str());
+    return -1;
+  }
+  int k = 0;
+  for (auto& f : q.filters) {
+    if (k < cap) { ids[k] = f.id; idx[k] = f.index; }
+    k++;
+  }
+  return k;
+}
+
+// MsgPackReader.readToken on p[0, n): out = type (MpType index), boolean, size, value offset, value length, bytes
+// consumed; 0, or -1 with the reader's exception message
+int zbref_read_token(const uint8_t* p, size_t n, int64_t* ival, double* fval, int32_t* out, char* err, size_t errcap) {
+  MpReader r(p, n);
+  try {
+    MpToken t = r.read_token();
+    *ival = t.ival;
+    *fval = t.fval;
+    out[0] = (int32_t)t.type; out[1] = t.bval ? 1 : 0; out[2] = (int32_t)t.size;
+    out[3] = t.data ? (int32_t)(t.data - p) : -1; out[4] = (int32_t)t.len; out[5] = (int32_t)r.off;
+    return 0;
+  } catch (const std::exception& e) {
+    std::snprintf(err, errcap, "%s", e.what());
+    return -1;
+  }
+}
+
+// MsgPackTraverser.traverse: 1 when every token reads; 0 with getInvalidPosition / getErrorMessage otherwise
+int zbref_traverse(const uint8_t* doc, size_t n, int32_t* invalid_pos, char* err, size_t errcap) {
+  MpReader r(doc, n);
+  *invalid_pos = -1;
+  while (r.has_next()) {
+    const size_t pos = r.off;
+    try {
+      (void)r.read_token();
+    } catch (const std::exception& e) {
+      *invalid_pos = (int32_t)pos;
+      std::snprintf(err, errcap, "%s", e.what());
+      return 0;
+    }
+  }
+  return 1;
 }
 
 int32_t zbref_subscription_hash(const uint8_t* p, size_t n) {

@@ -74,6 +74,18 @@ def lib():
         L.zbref_map.restype = i64
         L.zbref_map.argtypes = [u8p, sz, u8p, sz, ctypes.c_char_p, ctypes.c_void_p, sz, ctypes.c_char_p, sz]
         L.zbref_query.argtypes = [cp, u8p, sz, ctypes.POINTER(i32), ctypes.c_int, ctypes.c_char_p, sz]
+        L.zbref_jp_tokens.restype = ctypes.c_int
+        L.zbref_jp_tokens.argtypes = [cp, ctypes.POINTER(i32), ctypes.c_int]
+        L.zbref_jp_compile.restype = ctypes.c_int
+        L.zbref_jp_compile.argtypes = [cp, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.c_int, ctypes.POINTER(i32),
+                                       ctypes.c_char_p, sz]
+        L.zbref_read_token.restype = ctypes.c_int
+        L.zbref_read_token.argtypes = [u8p, sz, ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32),
+                                       ctypes.c_char_p, sz]
+        L.zbref_traverse.restype = ctypes.c_int
+        L.zbref_traverse.argtypes = [u8p, sz, ctypes.POINTER(i32), ctypes.c_char_p, sz]
+        L.zbref_tree_dump.restype = i64
+        L.zbref_tree_dump.argtypes = [u8p, sz, cp, ctypes.c_int, ctypes.c_void_p, sz, ctypes.c_char_p, sz]
         L.zbref_subscription_hash.restype = i32
         L.zbref_subscription_hash.argtypes = [u8p, sz]
         L.zbref_encode_int.restype = i64
@@ -346,6 +358,83 @@ def query(path: str, doc: bytes):
     if n < 0:
         raise ValueError(err.value.decode())
     return [doc[out[2 * i]:out[2 * i] + out[2 * i + 1]] for i in range(min(n, 128))]
+
+
+JP_TOKENS = ["START_INPUT", "END_INPUT", "ROOT_OBJECT", "CHILD_OPERATOR", "RECURSION_OPERATOR", "WILDCARD",
+             "SUBSCRIPT_OPERATOR_BEGIN", "SUBSCRIPT_OPERATOR_END", "CHILD_BRACKET_OPERATOR_BEGIN",
+             "CHILD_BRACKET_OPERATOR_END", "LITERAL"]  # zbref_jsonpath.hpp JpToken order
+MP_TYPES = ["INTEGER", "FLOAT", "BOOLEAN", "NIL", "MAP", "ARRAY", "BINARY", "STRING", "EXTENSION", "NEVER_USED"]
+
+
+def jp_tokens(expr: str):
+    """JsonPathTokenizer.tokenize: [(token name, position, length)]."""
+    out = (ctypes.c_int32 * 768)()
+    n = lib().zbref_jp_tokens(expr.encode(), out, 256)
+    return [(JP_TOKENS[out[3 * i]], out[3 * i + 1], out[3 * i + 2]) for i in range(min(n, 256))]
+
+
+def jp_compile(expr: str):
+    """JsonPathQueryCompiler.compile: ([(filter id, index)], None) or (None, (invalid position, error reason))."""
+    ids, idx, pos = (ctypes.c_int32 * 256)(), (ctypes.c_int32 * 256)(), ctypes.c_int32()
+    err = ctypes.create_string_buffer(512)
+    n = lib().zbref_jp_compile(expr.encode(), ids, idx, 256, ctypes.byref(pos), err, 512)
+    if n < 0:
+        return None, (pos.value, err.value.decode())
+    return [(ids[i], idx[i]) for i in range(n)], None
+
+
+def read_token(b: bytes):
+    """MsgPackReader.readToken: dict(type, int, float, bool, size, value, consumed), or the exception message."""
+    iv, fv, out = ctypes.c_int64(), ctypes.c_double(), (ctypes.c_int32 * 6)()
+    err = ctypes.create_string_buffer(512)
+    if lib().zbref_read_token(b, len(b), ctypes.byref(iv), ctypes.byref(fv), out, err, 512) < 0:
+        return err.value.decode()
+    return {"type": MP_TYPES[out[0]], "int": iv.value, "float": fv.value, "bool": bool(out[1]), "size": out[2],
+            "value": b[out[3]:out[3] + out[4]] if out[3] >= 0 else None, "consumed": out[5]}
+
+
+def traverse(doc: bytes):
+    """MsgPackTraverser.traverse: (True, None) or (False, (invalid position, error message))."""
+    pos = ctypes.c_int32()
+    err = ctypes.create_string_buffer(512)
+    if lib().zbref_traverse(doc, len(doc), ctypes.byref(pos), err, 512):
+        return True, None
+    return False, (pos.value, err.value.decode())
+
+
+def query_positions(path: str, doc: bytes):
+    """MsgPackQueryExecutor results as (position, length) pairs."""
+    out = (ctypes.c_int32 * 256)()
+    err = ctypes.create_string_buffer(4096)
+    n = lib().zbref_query(path.encode(), doc, len(doc), out, 128, err, 4096)
+    if n < 0:
+        raise ValueError(err.value.decode())
+    return [(out[2 * i], out[2 * i + 1]) for i in range(min(n, 128))]
+
+
+def parse_tree_dump(buf: bytes) -> dict:
+    """A tree dump (zbref_tree_dump / devlib_xtree_dump) -> {id: (type, [children], leaf bytes or None)}."""
+    out = {}
+    for line in buf.split(b"\n"):
+        if not line:
+            continue
+        ty, nid, ch, leaf = line.split(b"\0")
+        out[nid.decode()] = (ty.decode(), [c.decode() for c in ch.split(b"\x1e")] if ch else [],
+                             bytes.fromhex(leaf.decode()) if leaf else None)
+    return out
+
+
+def tree(doc: bytes, mappings=None) -> dict:
+    """MsgPackDocumentIndexer.index(doc) (mappings None) or MsgPackDocumentExtractor.extract(mappings) of doc, as
+    parse_tree_dump gives it; a failure raises MappingError / RuntimeError with the processor's message."""
+    spec = "".join("%s\t%s\n" % m for m in (mappings or [])).encode()
+    err = ctypes.create_string_buffer(4096)
+    need = lib().zbref_tree_dump(doc, len(doc), spec, 1 if mappings else 0, None, 0, err, 4096)
+    if need < 0:
+        raise (MappingError if need == -1 else RuntimeError)(err.value.decode())
+    buf = ctypes.create_string_buffer(need)
+    lib().zbref_tree_dump(doc, len(doc), spec, 1 if mappings else 0, buf, need, err, 4096)
+    return parse_tree_dump(buf.raw[:need])
 
 
 def subscription_hash(b: bytes) -> int:

@@ -579,6 +579,235 @@ def job_sequences():
     ]
 
 
+# ---- json-path and msgpack reader (SURVEY §8c pins for the query walker every condition and correlation key uses)
+def jsonpath_tokens():
+    # json-path/src/test/java/io/zeebe/msgpack/jsonpath/JsonPathTokenizerTest.java:28-124 (token, position, length)
+    return [
+        {"expr": "$.key1.key2[index]", "tokens": [
+            ["START_INPUT", 0, 18], ["ROOT_OBJECT", 0, 1], ["CHILD_OPERATOR", 1, 1], ["LITERAL", 2, 4],
+            ["CHILD_OPERATOR", 6, 1], ["LITERAL", 7, 4], ["SUBSCRIPT_OPERATOR_BEGIN", 11, 1], ["LITERAL", 12, 5],
+            ["SUBSCRIPT_OPERATOR_END", 17, 1], ["END_INPUT", 0, 18]]},
+        {"expr": "$['key1.key2'].test[index]", "tokens": [
+            ["START_INPUT", 0, 26], ["ROOT_OBJECT", 0, 1], ["CHILD_BRACKET_OPERATOR_BEGIN", 1, 2], ["LITERAL", 3, 9],
+            ["CHILD_BRACKET_OPERATOR_END", 12, 2], ["CHILD_OPERATOR", 14, 1], ["LITERAL", 15, 4],
+            ["SUBSCRIPT_OPERATOR_BEGIN", 19, 1], ["LITERAL", 20, 5], ["SUBSCRIPT_OPERATOR_END", 25, 1],
+            ["END_INPUT", 0, 26]]},
+        {"expr": "$.a[b].c", "tokens": [
+            ["START_INPUT", 0, 8], ["ROOT_OBJECT", 0, 1], ["CHILD_OPERATOR", 1, 1], ["LITERAL", 2, 1],
+            ["SUBSCRIPT_OPERATOR_BEGIN", 3, 1], ["LITERAL", 4, 1], ["SUBSCRIPT_OPERATOR_END", 5, 1],
+            ["CHILD_OPERATOR", 6, 1], ["LITERAL", 7, 1], ["END_INPUT", 0, 8]]},
+    ]
+
+
+def jsonpath_compile():
+    # JsonPathQueryCompilerTest.java:31-79: the filter id of every filter instance (0 root, 1 map value with key,
+    # 2 array index, 3 wildcard); :81-96 the query keeps its expression (checked by the compiler tests as is)
+    return [{"expr": "$.key1.key2[1].key3", "filter_ids": [0, 1, 1, 2, 1]},
+            {"expr": "$.*", "filter_ids": [0, 3]}]
+
+
+def jsonpath_invalid():
+    # JsonPathQueryValidationTest.java:29-38: (path, invalid position, error reason)
+    return [{"expr": "$..", "position": 1, "error": "Unexpected json-path token RECURSION_OPERATOR"},
+            {"expr": "foo", "position": 0, "error": "Unexpected json-path token LITERAL"},
+            {"expr": "$.foo.$", "position": 6, "error": "Unexpected json-path token ROOT_OBJECT"},
+            {"expr": "$.[foo", "position": 2, "error": "Unexpected json-path token SUBSCRIPT_OPERATOR_BEGIN"}]
+
+
+def _mpj_long(v):
+    """msgpack-java MessagePacker.packLong: the smallest format of the value."""
+    import struct
+    if -32 <= v < 128:
+        return struct.pack("b", v)
+    if v >= 0:
+        for fmt, code, lim in ((">B", 0xcc, 1 << 8), (">H", 0xcd, 1 << 16), (">I", 0xce, 1 << 32)):
+            if v < lim:
+                return bytes([code]) + struct.pack(fmt, v)
+        return b"\xcf" + struct.pack(">Q", v)
+    for fmt, code, lim in ((">b", 0xd0, 1 << 7), (">h", 0xd1, 1 << 15), (">i", 0xd2, 1 << 31)):
+        if v >= -lim:
+            return bytes([code]) + struct.pack(fmt, v)
+    return b"\xd3" + struct.pack(">q", v)
+
+
+def queries():
+    """Query results as (position, length) pairs, with the type of a single result where the test asserts one."""
+    import struct
+    foo = bytes.fromhex("a3666f6f")
+    nt = bytes.fromhex("ae") + b"NOT_THE_TARGET"
+    out = [
+        # JsonPathTest.java:39-104 (Jackson msgpack of {"foo": "bar"})
+        {"src": "JsonPathTest :39-104", "path": "$.foo", "doc": mp({"foo": "bar"}), "results": [[5, 4]],
+         "type": "STRING", "value": "a3626172"},
+        # MsgPackQueryProcessorTest.java:38-146
+        {"src": "MsgPackQueryProcessorTest :38-43, :86-93", "path": "$.foo", "doc": "80", "results": [],
+         "single_error": "no result found"},
+        {"src": "MsgPackQueryProcessorTest :45-62", "path": "$.foo", "doc": "81a3666f6fa3626172", "results": [[5, 4]],
+         "type": "STRING", "value": "a3626172"},
+        {"src": "MsgPackQueryProcessorTest :64-84", "path": "$.foo", "doc": "81a3666f6f01", "results": [[5, 1]],
+         "type": "INTEGER", "long_buffer": struct.pack("<q", 1).hex()},
+        {"src": "MsgPackQueryProcessorTest :95-110", "path": "$.*", "doc": "82a17800a17901", "results": [[3, 1], [6, 1]],
+         "single_error": "found more than one result"},
+        {"src": "MsgPackQueryProcessorTest :112-146", "path": "$.foo", "doc": "81a3666f6fc2", "results": [[5, 1]],
+         "type": "BOOLEAN", "string_error": "expected String but found 'BOOLEAN'",
+         "long_error": "expected Long but found 'BOOLEAN'"},
+        # MsgPackTraverserTest.java:111-155 ($.foo[1].bar), :157-191 ($.target), :193-228 ($.*)
+        {"src": "MsgPackTraverserTest :111-155", "path": "$.foo[1].bar",
+         "doc": (b"\x82" + nt + nt + foo + b"\x92" + nt + b"\x82" + nt + nt + bytes.fromhex("a3626172") +
+                 b"\xaaTHE_TARGET").hex(), "results": [[86, 11]]},
+        {"src": "MsgPackTraverserTest :157-191", "path": "$.target",
+         "doc": (b"\x82" + foo + foo + b"\xa6target\x81" + foo + foo).hex(), "results": [[16, 9]]},
+        {"src": "MsgPackTraverserTest :193-228", "path": "$.*",
+         "doc": (b"\x82\xa4key1\xa4val1\xa4key2\xa4val2").hex(), "results": [[6, 5], [16, 5]]},
+    ]
+    # MsgPackQueryValueFormatsTest.java:39-116: {"foo": value} -> the value's bytes (msgpack-java encodings)
+    vals = [foo, b"\xc3", b"\xc2", b"\xcb" + struct.pack(">d", 1.444), b"\xca" + struct.pack(">f", 1.555),
+            _mpj_long(1 << 4), _mpj_long(-(1 << 2)), _mpj_long(1 << 7), _mpj_long(1 << 14), _mpj_long(1 << 29),
+            _mpj_long((1 << 31) - 1 + 10), b"\xc0", _mpj_long(123)]
+    for v in vals:
+        out.append({"src": "MsgPackQueryValueFormatsTest :39-116", "path": "$.foo", "doc": (b"\x81" + foo + v).hex(),
+                    "results": [[5, len(v)]], "value": v.hex()})
+    return out
+
+
+def traversal_errors():
+    # MsgPackTraverserTest.java:230-256: a valid string followed by 0xc7 (ext 8, unsupported)
+    return [{"doc": "a3666f6fc7", "position": 4, "error": "Unsupported token format"}]
+
+
+def read_tokens():
+    # msgpack-core/src/test/java/io/zeebe/msgpack/spec/MsgPackReadTokenTest.java:55-241 (the reader consumes the
+    # whole input in every row)
+    import struct
+    r = [("positive fixint", "7f", "INTEGER", {"int": 0x7f}), ("fixmap", "8f", "MAP", {"size": 15}),
+         ("fixarray", "9f", "ARRAY", {"size": 15}), ("fixstr", "a122", "STRING", {"value": "22"}),
+         ("nil", "c0", "NIL", {}), ("false", "c2", "BOOLEAN", {"bool": False}), ("true", "c3", "BOOLEAN", {"bool": True}),
+         ("bin 8", "c40122", "BINARY", {"value": "22"}), ("bin 16", "c5000122", "BINARY", {"value": "22"}),
+         ("bin 32", "c60000000122", "BINARY", {"value": "22"}),
+         ("float 32", "ca" + struct.pack(">f", 123123.12).hex(), "FLOAT",
+          {"float": struct.unpack(">f", struct.pack(">f", 123123.12))[0]}),
+         ("float 64", "cb" + struct.pack(">d", 123123.123).hex(), "FLOAT", {"float": 123123.123}),
+         ("uint 8", "ccff", "INTEGER", {"int": (1 << 8) - 1}), ("uint 16", "cdffff", "INTEGER", {"int": (1 << 16) - 1}),
+         ("uint 32", "ceffffffff", "INTEGER", {"int": (1 << 32) - 1}),
+         ("uint 64", "cf7fffffffffffffff", "INTEGER", {"int": (1 << 63) - 1}),
+         ("int 8", "d080", "INTEGER", {"int": -128}), ("int 16", "d18000", "INTEGER", {"int": -32768}),
+         ("int 32", "d280000000", "INTEGER", {"int": -(1 << 31)}),
+         ("int 64", "d38000000000000000", "INTEGER", {"int": -(1 << 63)}),
+         ("str 8", "d90122", "STRING", {"value": "22"}), ("str 16", "da000122", "STRING", {"value": "22"}),
+         ("str 32", "db0000000122", "STRING", {"value": "22"}),
+         ("array 16", "dcffff", "ARRAY", {"size": 0xffff}), ("array 32", "dd7fffffff", "ARRAY", {"size": (1 << 31) - 1}),
+         ("map 16", "deffff", "MAP", {"size": 0xffff}), ("map 32", "df00ffffff", "MAP", {"size": 0x00ffffff}),
+         ("negative fixint", "e0", "INTEGER", {"int": -32})]
+    return [dict(name=n, bytes=b, type=t, **a) for n, b, t, a in r]
+
+
+# ---- the payload tree (MsgPackDocumentIndexer / MsgPackTree / MsgPackDocumentExtractor / MsgPackDocumentTreeWriter):
+# the pins of the exact tree (zeebe_amd/csrc/zb_xmerge.hpp) and of the oracle's zbref_mapping.hpp
+def _nid(*names):
+    """MappingTestUtil.constructNodeId: "$" + "[name]"..."""
+    return names[0] + "".join("[%s]" % n for n in names[1:])
+
+
+def _mapping_payload():
+    """MappingTestUtil.java:36-80 JSON_PAYLOAD (MSG_PACK_BYTES; a HashMap, so its key order is not part of any test)."""
+    return {"string": "value", "boolean": False, "integer": 1024, "long": (1 << 63) - 1, "double": 0.3,
+            "array": [0, 1, 2, 3], "jsonObject": {"testAttr": "test"}}
+
+
+def trees():
+    """Each row: a document, the mappings of an extraction (none: the document is indexed), and the assertions of the
+    test on the resulting tree: ["map" | "array", node id, its children (as a set)] or ["leaf", node id, the leaf's
+    msgpack bytes] (assertThatIsMapNode / assertThatIsArrayNode / assertThatIsLeafNode, MappingTestUtil.java:85-117),
+    or the failure message."""
+    P = _mapping_payload()
+    doc = mp(P)
+    keys = list(P)
+    rows = []
+    # json-path/src/test/java/io/zeebe/msgpack/mapping/MsgPackDocumentIndexerTest.java:47-102
+    rows.append({"src": "MsgPackDocumentIndexerTest.shouldIndexDocument :47-102", "doc": doc, "mappings": None,
+                 "expect": [["map", "$", keys], ["map", _nid("$", "jsonObject"), ["testAttr"]],
+                            ["array", _nid("$", "array"), ["0", "1", "2", "3"]],
+                            ["leaf", _nid("$", "string"), mp("value")], ["leaf", _nid("$", "boolean"), mp(False)],
+                            ["leaf", _nid("$", "integer"), mp(1024)], ["leaf", _nid("$", "long"), mp((1 << 63) - 1)],
+                            ["leaf", _nid("$", "double"), mp(0.3)]] +
+                           [["leaf", _nid("$", "array", str(i)), mp(i)] for i in range(4)] +
+                           [["leaf", _nid("$", "jsonObject", "testAttr"), mp("test")]]})
+    d2 = _tree("{'first': { 'range': [0, 2], 'friends': [-1, {'id': 0, 'name': 'Rodriguez Richards'}],"
+               "'greeting': 'Hello, Bauer! You have 7 unread messages.', 'favoriteFruit': 'apple'}}")
+    f = ("$", "first")
+    rows.append({"src": "MsgPackDocumentIndexerTest.shouldIndexDocumentWithMoreArrays :104-161", "doc": mp(d2),
+                 "mappings": None,
+                 "expect": [["map", "$", ["first"]], ["map", _nid(*f), ["range", "friends", "greeting", "favoriteFruit"]],
+                            ["array", _nid(*f, "range"), ["0", "1"]], ["leaf", _nid(*f, "range", "0"), mp(0)],
+                            ["leaf", _nid(*f, "range", "1"), mp(2)], ["array", _nid(*f, "friends"), ["0", "1"]],
+                            ["leaf", _nid(*f, "friends", "0"), mp(-1)],
+                            ["map", _nid(*f, "friends", "1"), ["id", "name"]],
+                            ["leaf", _nid(*f, "friends", "1", "id"), mp(0)],
+                            ["leaf", _nid(*f, "friends", "1", "name"), mp("Rodriguez Richards")],
+                            ["leaf", _nid(*f, "greeting"), mp("Hello, Bauer! You have 7 unread messages.")],
+                            ["leaf", _nid(*f, "favoriteFruit"), mp("apple")]]})
+    d3 = _tree("{'friends': [{'id': 0, 'name': 'Rodriguez Richards'}, {'id': 0, 'name': 'Rodriguez Richards'}]}")
+    rows.append({"src": "MsgPackDocumentIndexerTest.shouldIndexDocumentWitObjectArray :163-199", "doc": mp(d3),
+                 "mappings": None,
+                 "expect": [["map", "$", ["friends"]], ["array", _nid("$", "friends"), ["0", "1"]]] +
+                           [e for i in ("0", "1") for e in (
+                               ["map", _nid("$", "friends", i), ["id", "name"]],
+                               ["leaf", _nid("$", "friends", i, "id"), mp(0)],
+                               ["leaf", _nid("$", "friends", i, "name"), mp("Rodriguez Richards")])]})
+    rows.append({"src": "MsgPackDocumentIndexerTest.shouldIndexDocumentWitArrayAndObjectWithIndex :201-223",
+                 "doc": mp(_tree("{'a':['foo'], 'a0':{'b':'c'}}")), "mappings": None,
+                 "expect": [["map", "$", ["a", "a0"]], ["array", _nid("$", "a"), ["0"]],
+                            ["leaf", _nid("$", "a", "0"), mp("foo")], ["map", _nid("$", "a0"), ["b"]],
+                            ["leaf", _nid("$", "a0", "b"), mp("c")]]})
+    # MsgPackDocumentExtractorTest.java:41-219
+    ja = mp({"testAttr": "test"})
+    ex = [
+        (":41-53 shouldExtractHoleDocument", [["$", "$"]], [["leaf", "$", doc]]),
+        (":55-68 shouldExtractHoleDocumentAndCreateNewObject", [["$", "$.old"]],
+         [["map", "$", ["old"]], ["leaf", _nid("$", "old"), doc]]),
+        (":70-84 shouldExtractHoleDocumentAndCreateNewDeepObject", [["$", "$.old.test"]],
+         [["map", "$", ["old"]], ["map", _nid("$", "old"), ["test"]], ["leaf", _nid("$", "old", "test"), doc]]),
+        (":86-104 shouldCreateOrRenameObject", [["$.jsonObject", "$.testObj"]],
+         [["map", "$", ["testObj"]], ["leaf", _nid("$", "testObj"), ja]]),
+        (":106-124 shouldCreateObjectOnRoot", [["$.jsonObject", "$"]], [["leaf", "$", ja]]),
+        (":126-145 shouldCreateValueOnArrayIndex", [["$.array[1]", "$.array[0]"]],
+         [["map", "$", ["array"]], ["array", _nid("$", "array"), ["0"]], ["leaf", _nid("$", "array", "0"), mp(1)]]),
+        (":147-169 shouldCreateValueOnArrayIndexObject", [["$.array[1]", "$.array[0].test"]],
+         [["map", "$", ["array"]], ["array", _nid("$", "array"), ["0"]], ["map", _nid("$", "array", "0"), ["test"]],
+          ["leaf", _nid("$", "array", "0", "test"), mp(1)]]),
+        (":171-202 shouldExtractWithMoreMappings",
+         [["$.boolean", "$.newBoolean"], ["$.array", "$.newArray"], ["$.jsonObject", "$.newObject"]],
+         [["map", "$", ["newBoolean", "newArray", "newObject"]], ["leaf", _nid("$", "newBoolean"), mp(False)],
+          ["leaf", _nid("$", "newArray"), mp([0, 1, 2, 3])], ["leaf", _nid("$", "newObject"), ja]]),
+    ]
+    for name, ms, exp in ex:
+        rows.append({"src": "MsgPackDocumentExtractorTest" + name, "doc": doc, "mappings": ms, "expect": exp})
+    rows.append({"src": "MsgPackDocumentExtractorTest :204-219 shouldThrowExceptionIfMappingMatchesTwice",
+                 "doc": mp(_tree("{'foo':'bar', 'foa':'baz'}")), "mappings": [["$.*", "$"]],
+                 "error": "JSON path mapping has more than one matching source."})
+    # MsgPackTreeTest.java:36-84, through the extractor: a leaf of the whole document, and a leaf that reads the
+    # extract document (setExtractDocument) rather than the underlying one
+    inner = {"aObject": {"test": "test"}, "string": "stringValue"}
+    rows.append({"src": "MsgPackTreeTest :36-47 shouldUseUnderlyingDocument (as extract $ -> $)", "doc": doc,
+                 "mappings": [["$", "$"]], "expect": [["leaf", "$", doc]]})
+    rows.append({"src": "MsgPackTreeTest :49-84 shouldDifferBetweenUnderlyingAndExtractDocument (as extract "
+                        "$.aObject -> $)", "doc": mp(inner), "mappings": [["$.aObject", "$"]],
+                 "expect": [["leaf", "$", mp({"test": "test"})]]})
+    return rows
+
+
+def tree_writes():
+    """MsgPackDocumentTreeWriterTest.java:33-70: index the test resource largeJsonDocument.json (Jackson msgpack of its
+    JSON tree) and write the tree: the result has the document's length and JSON value. The resource is copied as data
+    to tests/golden/mapping_largeJsonDocument.json."""
+    src = os.path.join(REF, "json-path/src/test/resources/io/zeebe/msgpack/mapping/largeJsonDocument.json")
+    with open(src, "rb") as f:
+        text = f.read()
+    with open(os.path.join(HERE, "mapping_largeJsonDocument.json"), "wb") as f:
+        f.write(text)
+    return [{"src": "MsgPackDocumentTreeWriterTest :33-70", "json_file": "mapping_largeJsonDocument.json"}]
+
+
 def main():
     data = {
         "conditions": conditions(),
@@ -595,6 +824,14 @@ def main():
         "io_workflows": io_workflows(),
         "job_sequences": job_sequences(),
         "wf_intents": WF,
+        "jsonpath_tokens": jsonpath_tokens(),
+        "jsonpath_compile": jsonpath_compile(),
+        "jsonpath_invalid": jsonpath_invalid(),
+        "queries": queries(),
+        "traversal_errors": traversal_errors(),
+        "read_tokens": read_tokens(),
+        "trees": trees(),
+        "tree_writes": tree_writes(),
     }
     with open(os.path.join(HERE, "reference_vectors.json"), "w") as f:
         json.dump(data, f, indent=1, allow_nan=False, default=str)

@@ -17,6 +17,7 @@ static inline double __longlong_as_double(long long u) { double d; std::memcpy(&
 #include "../../zeebe_amd/csrc/zb_model.cpp"  // the product's deploy-time compilers (json-path, mapping targets)
 
 #include <string>
+#include <vector>
 
 using namespace zbg;
 
@@ -95,6 +96,93 @@ long devlib_query(const uint8_t* doc, uint32_t n, const uint8_t* f_ids, const in
   out[0] = r.pos;
   out[1] = r.len;
   return r.count;
+}
+// the product's json-path compiler (zb_model.cpp compile_filters, JsonPathQueryCompiler): the filter instances
+// (filter id, index) -- #instances, or -1 with the error reason
+long devlib_compile_path(const char* expr, int32_t* ids, int32_t* idx, uint32_t cap, char* err, uint32_t errcap) {
+  ModelTables t;
+  std::vector<DevFilter> fs;
+  std::string e;
+  if (!compile_filters(expr, fs, t, e)) {
+    snprintf(err, errcap, "%s", e.c_str());
+    return -1;
+  }
+  for (uint32_t i = 0; i < fs.size() && i < cap; i++) { ids[i] = fs[i].id; idx[i] = fs[i].index; }
+  return (long)fs.size();
+}
+// a json-path compiled by the product's compiler (compile_query) and run by the kernels' query entry (run_query, the
+// one k_subscribe and the condition VM use): #results, first result in out[0..1]; -1 unsupported, -20 invalid path
+long devlib_query_text(const char* expr, const uint8_t* doc, uint32_t n, uint32_t* out) {
+  ModelTables t;
+  std::string e;
+  const int q = compile_query(t, expr, e);
+  if (q < 0) return -20;
+  if (t.pool.empty()) t.pool.push_back(0);
+  QueryResult r;
+  if (!run_query(doc, n, t.queries[q], t.filters.data(), t.pool.data(), r)) return -1;
+  out[0] = r.pos;
+  out[1] = r.len;
+  return r.count;
+}
+// read_tok (the kernels' MsgPackReader.readToken): out = type (TokType), boolean, size / length, header length,
+// bytes consumed; 0, or -1 when the token does not read
+long devlib_read_token(const uint8_t* p, uint32_t n, int64_t* ival, double* fval, int32_t* out) {
+  Tok t;
+  if (!read_tok(p, n, t)) return -1;
+  *ival = t.ival;
+  *fval = t.fval;
+  out[0] = t.type; out[1] = t.bval ? 1 : 0; out[2] = (int32_t)t.len; out[3] = t.hdr; out[4] = (int32_t)t.total;
+  return 0;
+}
+// The exact tree (zb_xmerge.hpp) as built for a document -- indexed (mode 0: MsgPackDocumentIndexer.index) or
+// extracted by mappings (mode 1: MsgPackDocumentExtractor.extract, spec as devlib_map_text) -- dumped as one line per
+// typed node: type (M map, A array, L existing leaf, X extracted leaf), NUL, id, NUL, children joined by 0x1e in
+// insertion order, NUL, leaf bytes (hex; empty: no leaf), '\n'. Returns the dump length, or -(100 + X_* status).
+long devlib_xtree_dump(const uint8_t* doc, uint32_t n, const char* spec, int mode, char* out, uint32_t cap) {
+  static uint8_t slab[XSLAB_BYTES];
+  XTree T;
+  int st;
+  if (mode == 0) {
+    if (!T.init(slab, XSLAB_BYTES, x_tokens(doc, n))) return -(100 + T.status);
+    T.index(0, doc, n, false);
+    st = T.status;
+  } else {
+    ModelTables t;
+    std::string sp(spec), e;
+    size_t p = 0;
+    while (p < sp.size()) {
+      size_t tab = sp.find('\t', p), nl = sp.find('\n', p);
+      if (tab == std::string::npos || nl == std::string::npos || tab > nl) return -21;
+      if (compile_mapping(t, sp.substr(p, tab - p), sp.substr(tab + 1, nl - tab - 1), e) < 0) return -20;
+      p = nl + 1;
+    }
+    if (t.pool.empty()) t.pool.push_back(0);
+    uint16_t q = 0xffff;
+    st = x_map_tree(T, slab, XSLAB_BYTES, doc, n, nullptr, 0, t.maps.data(), (uint32_t)t.maps.size(), t.segs.data(),
+                    t.queries.data(), t.filters.data(), t.pool.data(), q);
+  }
+  if (st != X_OK) return -(100 + st);
+  std::string d;
+  static const char HEX[] = "0123456789abcdef";
+  for (uint32_t i = 0; i < T.nn; i++) {
+    const XNode& x = T.nodes[i];
+    if (x.tree != 0 || x.type == XT_NONE) continue;
+    d += x.type == XT_MAP ? 'M' : x.type == XT_ARRAY ? 'A' : x.type == XT_EXTRACTED_LEAF ? 'X' : 'L';
+    d += '\0';
+    d.append((const char*)T.s(x.id), x.id.len);
+    d += '\0';
+    if (x.has_childs)
+      for (uint32_t c = x.cfirst; c != XNONE; c = T.ch[c].next) {
+        if (c != x.cfirst) d += '\x1e';
+        d.append((const char*)T.s(T.ch[c].name), T.ch[c].name.len);
+      }
+    d += '\0';
+    if (x.has_leaf)  // (extracted and indexed leaves both come from the one document here)
+      for (uint32_t k = 0; k < x.llen; k++) { d += HEX[doc[x.lpos + k] >> 4]; d += HEX[doc[x.lpos + k] & 15]; }
+    d += '\n';
+  }
+  if (d.size() <= cap) memcpy(out, d.data(), d.size());
+  return (long)d.size();
 }
 // the exact tree (zb_xmerge.hpp): x_merge, or x_map over the product's compiled mappings (spec as devlib_map_text,
 // empty spec = merge). Returns the output length, or -(100 + X_* status) (fail_query in *fq), -20 compile error.

@@ -202,3 +202,32 @@ def test_racing_job_commands():
     recs += [comp(j, {"late": i}) for i, j in enumerate(jobs) if i % 4 == 2]
     p.tick(recs=recs)
     p.tick(recs=[act(j) for i, j in enumerate(jobs) if i % 4 == 1])
+
+
+def test_racing_commands_of_jobs_without_headers():
+    """Jobs created by JOB CREATE commands with no workflow headers (JobHeaders.workflowInstanceKey -1,
+    JobHeaders.java:33-51) under the job stream processor: their commands race only with the same job's commands, so
+    zb_submit keys them by job key (conflict_key, zb_device.hpp) and k_conflict cuts the generation before the next
+    command of such a job. Before that key, two commands of one such job that were not next to each other ran in one
+    lockstep wave against the same job state (JobInstanceStreamProcessor.java:70-242 takes them in log order)."""
+    c1 = workloads.CONFIGS["c1"]
+    p = Pair({100: c1["workflow"]().to_xml()}, job_processor=True)
+    creates = [(R.RT_COMMAND, R.VT_JOB, R.JI_CREATE, -1, R.job_record(type="ext%d" % i, retries=3)) for i in range(8)]
+    p.tick([("process", [msgpack.packb({"orderId": i}) for i in range(8)])], recs=creates)
+    free = [j for j in p.jobs if j[2] == -1]
+    bound = [j for j in p.jobs if j[2] != -1]
+    assert len(free) == 8 and len(bound) == 8
+
+    def cmd(intent, j, **kw):
+        v = msgpack.unpackb(j[1], raw=False)
+        v.update(kw)
+        return (R.RT_COMMAND, R.VT_JOB, intent, j[0], msgpack.packb(v))
+
+    recs = [cmd(R.JI_ACTIVATE, j, worker="w", deadline=10 ** 12) for j in free + bound]  # every job activated ...
+    recs += [cmd(R.JI_COMPLETE, j) for j in free[:4]]                                   # ... then completed
+    recs += [cmd(R.JI_FAIL, j, retries=0) for j in free[4:]]                            # ... or failed
+    recs += [cmd(R.JI_COMPLETE, j) for j in bound]
+    recs += [cmd(R.JI_UPDATE_RETRIES, j, retries=2) for j in free[4:]]                   # failed -> retries updated
+    recs += [cmd(R.JI_ACTIVATE, j, worker="x", deadline=10 ** 12) for j in free]        # rejected for the completed
+    p.tick(recs=recs)
+    p.tick(recs=[cmd(R.JI_CANCEL, j) for j in free] + [cmd(R.JI_CANCEL, j) for j in free[:2]])

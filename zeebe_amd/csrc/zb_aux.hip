@@ -114,7 +114,10 @@ __global__ void __launch_bounds__(256) k_merge_gen(WaveParams P) {
     // the shapes merge_docs refuses (and documents it cannot read, which the reference's indexer reads up to the
     // first bad token) take the exact tree
     uint32_t olen = o.n;
-    x_exclusive(XSlabs{P.xslab, P.xlocks}, !ok || unsup || o.n > j.cap, [&](uint8_t* slab) {
+    // (|result| <= ns + nt + 3 <= cap for every document merge_docs takes; a first pass past the blob would already
+    // have overwritten its neighbour, so it fails the partition instead of going on through the exact tree)
+    if (o.n > j.cap) err |= DE_UNSUPPORTED;
+    x_exclusive(XSlabs{P.xslab, P.xlocks}, (!ok || unsup) && o.n <= j.cap, [&](uint8_t* slab) {
       Out w{dst + 4, 0};
       const int st = x_merge(slab, XSLAB_BYTES, sp + 4, ns, tp + 4, nt, w, j.cap);
       if (st == X_OK) {

@@ -69,6 +69,16 @@ __host__ __device__ inline uint8_t kind_vt(uint8_t k) { return k & 0x0f; }
 __host__ __device__ inline uint8_t kind_rt(uint8_t k) { return (k >> 4) & 0x03; }
 __host__ __device__ inline bool kind_cont(uint8_t k) { return (k & 0x40) != 0; }
 
+// What k_conflict serialises a tick's racing records by (zb_submit marks the racing ones): the workflow instance;
+// a job command of a job with no workflow headers (JobHeaders.workflowInstanceKey -1, JobHeaders.java:33-51) races
+// only with that job's own commands, so it is keyed by its job key, tagged apart from instance keys. -1: none.
+constexpr int64_t CONF_JOB_TAG = 1ll << 62;
+__host__ __device__ inline int64_t conflict_key(int64_t inst_key, int64_t key, uint8_t kind) {
+  if (inst_key >= 0) return inst_key;
+  if (kind_vt(kind) == ZB_VT_JOB && kind_rt(kind) == ZB_RT_COMMAND && key >= 0) return key | CONF_JOB_TAG;
+  return -1;
+}
+
 struct DevElem {              // 72 bytes
   uint8_t kind;
   uint8_t flags;              // bit0: has io mapping (rejected at deploy for now)

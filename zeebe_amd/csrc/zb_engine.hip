@@ -79,7 +79,9 @@ struct zb_engine {
   hipStream_t stream = nullptr;
   int32_t ncu = 256;            // compute units of the device
   int32_t wave_fused_grid = 0;  // k_wave: resident workgroups (0 = three-kernel pipeline; ZB_CFG_WAVE_SPLIT forces it)
-  uint64_t* lookback = nullptr; // k_wave look-back granules
+  uint64_t* lookback = nullptr; // k_wave hand-off granules (WaveParams.lookback)
+  uint64_t lb_tiles = 0;
+  uint64_t lb_seq = 0;          // k_wave launches (aggregate tags: 1 + lb_seq % 255)
   std::string err;
 
   ModelTables model;
@@ -518,6 +520,7 @@ WaveParams wave_params(zb_engine* e) {
   p.block_agg = e->block_agg;
   p.block_off = e->block_off;
   p.lookback = e->lookback;
+  p.lb_tiles = e->lb_tiles;
   p.wave_cap = e->wave_cap;
   p.err = e->derr;
   p.err_info = e->derr_info;
@@ -1023,31 +1026,42 @@ int scan_reserve(zb_engine* e, uint64_t n) {
   return ZB_OK;
 }
 
-// Every compaction buffer sized for the partition's capacities, once, when the engine is created: rows and
-// messages (flags and their scan), the dynamic arena's granule words (bitmap, popcounts, their scan), the scan
-// scratch for the largest scan, and the gather scratch for the largest phase (the live rows or the whole dynamic
-// arena). Grown per compaction instead, a partition that keeps growing freed and reallocated them -- each a
-// device-wide synchronisation -- at nearly every compaction (C2 steady state: 3.2 ms ticks against 1.1 ms).
+// The compaction buffers that scale with the capacities' index space, sized once when the engine is created: rows
+// and messages (flags and their scan), the dynamic arena's granule words (bitmap, popcounts, their scan) and the
+// scan scratch for the largest scan -- a few bytes per row and per 64 arena granules. Grown per compaction instead, a
+// partition that keeps growing freed and reallocated them -- each a device-wide synchronisation -- at nearly every
+// compaction (C2 steady state: 3.2 ms ticks against 1.1 ms). The gather scratch (the live rows or the live dynamic
+// arena, up to the whole arena) is reserve_gather's, at the first compaction.
 int reserve_compaction(zb_engine* e) {
   const uint64_t nflag = std::max<uint64_t>(e->cfg.row_capacity, 1024) + 1;  // (rows; the stores hold as many)
   const uint64_t words_cap = ((e->cfg.arena_bytes - STATIC_ARENA_BYTES) / 8 + 63) / 64 + 1;
-  const uint64_t row_bytes = sizeof(RowMeta) + sizeof(RowKeys) + sizeof(RowAux);
-  const uint64_t scratch = std::max<uint64_t>(e->cfg.row_capacity * row_bytes, e->cfg.arena_bytes - STATIC_ARENA_BYTES);
   int rc = grow(e, &e->c_flag, &e->c_flag_cap, nflag);
   if (rc == ZB_OK) rc = grow(e, &e->c_new, &e->c_new_cap, nflag);
   if (rc == ZB_OK) rc = grow(e, &e->c_bits, &e->c_bits_cap, words_cap);
   if (rc == ZB_OK) rc = grow(e, &e->c_pop, &e->c_pop_cap, words_cap + 1);
   if (rc == ZB_OK) rc = grow(e, &e->c_off, &e->c_off_cap, words_cap + 1);
   if (rc == ZB_OK) rc = scan_reserve(e, std::max(nflag, words_cap + 1));
-  if (rc == ZB_OK && (!e->c_scratch || e->c_scratch_cap < scratch)) {  // (exactly: it is the largest of them)
-    HIPCHECK(e, hipStreamSynchronize(e->stream));
-    if (e->c_scratch) (void)hipFree(e->c_scratch);
-    e->c_scratch = nullptr;
-    e->c_scratch_cap = 0;
-    HIPCHECK(e, hipMalloc(&e->c_scratch, scratch));
-    e->c_scratch_cap = scratch;
-  }
   return rc;
+}
+
+// The gather scratch, at a compaction: room for what this one can gather (the allocated rows, the used dynamic arena)
+// doubled, capped at the capacities -- an engine that never compacts holds none, and one that keeps growing
+// reallocates it a few times, not at every compaction. (Reserved for the whole arena at creation, it doubled a large
+// partition's device memory.)
+int reserve_gather(zb_engine* e) {
+  const uint64_t row_bytes = sizeof(RowMeta) + sizeof(RowKeys) + sizeof(RowAux);
+  const uint64_t full = std::max<uint64_t>(e->cfg.row_capacity * row_bytes, e->cfg.arena_bytes - STATIC_ARENA_BYTES);
+  const uint64_t need = std::max<uint64_t>((uint64_t)e->host_hdr.rows_next * row_bytes,
+                                           (uint64_t)e->host_hdr.arena_next - STATIC_ARENA_BYTES);
+  if (e->c_scratch && e->c_scratch_cap >= need) return ZB_OK;
+  const uint64_t c = std::max<uint64_t>(std::min<uint64_t>(2 * need, full), std::max<uint64_t>(need, 1 << 20));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  if (e->c_scratch) (void)hipFree(e->c_scratch);
+  e->c_scratch = nullptr;
+  e->c_scratch_cap = 0;
+  HIPCHECK(e, hipMalloc(&e->c_scratch, c));
+  e->c_scratch_cap = c;
+  return ZB_OK;
 }
 
 CompactParams compact_params(zb_engine* e) {
@@ -1082,6 +1096,7 @@ int compact_state(zb_engine* e) {
 #endif
   const uint64_t rows = (uint64_t)e->host_hdr.rows_next;
   int rc = reserve_compaction(e);  // (no-op: zb_engine_create reserved them)
+  if (rc == ZB_OK) rc = reserve_gather(e);
   if (rc != ZB_OK) return rc;
   // 1. rows: live ones to the front (index order kept), parents renamed
   CompactParams c = compact_params(e);
@@ -1315,7 +1330,8 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->block_agg, WAVE_GRID_MAX * sizeof(BlockAgg)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->block_off, WAVE_GRID_MAX * sizeof(BlockOff)) != hipSuccess) return cleanup(ZB_ENOMEM);
   {
-    const size_t lb = (e->wave_cap / WAVE_TILE + 1) * 16 * sizeof(uint64_t);
+    e->lb_tiles = e->wave_cap / WAVE_TILE + 1;
+    const size_t lb = (2 * e->lb_tiles + 8 * (e->lb_tiles + 512) + 8 * (e->lb_tiles + 2)) * sizeof(uint64_t);
     if (hipMalloc(&e->lookback, lb) != hipSuccess) return cleanup(ZB_ENOMEM);
     if (hipMemset(e->lookback, 0, lb) != hipSuccess) return cleanup(ZB_EDEVICE);
   }
@@ -1470,6 +1486,7 @@ int zb_reset(zb_engine* e, int keep_staged) {
     e->tick_aik.clear();
     e->tick_jobs.clear();
     e->staged_uploaded = false;
+    e->wave_hint = 0;  // (a reset that keeps the staged batch runs the same tick again: the hint stays)
   }
   e->term = false;
   e->conf_active = false;
@@ -1505,6 +1522,7 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
   std::string msg;
   int rc = compile_deployment(e->model, std::string((const char*)xml, len), workflow_key, version, msg);
   if (rc != ZB_OK) return fail(e, rc, msg);
+  e->wave_hint = 0;  // (the last tick's wave count says nothing about the new model's ticks)
   for (const DevElem& el : e->model.elems) {
     if (el.step[WI_ELEMENT_COMPLETING] == ST_APPLY_OUTPUT_MAPPING) e->has_merges = true;
     if (el.step[WI_GATEWAY_ACTIVATED] == ST_EXCLUSIVE_SPLIT) e->has_splits = true;
@@ -2114,7 +2132,7 @@ int zb_submit(zb_engine* e, const zb_rec_desc* recs, size_t n, const uint8_t* va
                                         "the partition's job key generator)");
       p.job_cmd = true;
       p.lookup = dv.aik;
-      p.inst = dv.wik;
+      p.inst = conflict_key(dv.wik, r.key, d.kind);  // (a job without workflow headers: by its job key)
       d.scope_key = dv.aik;
       d.inst_key = dv.wik;
       if (it == JI_UPDATE_RETRIES) d.elem = dv.retries > 0 ? 1 : 0;  // (job_command reads it)
@@ -2375,6 +2393,11 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
       }
       if (e->has_io) launch_map(p, e->stream);  // io-mapping results of the chunk's records
       if (e->wave_fused_grid) {  // process + scan + emit in one launch (k_wave)
+        // tile aggregates carry an 8-bit tag: when it wraps, no granule may hold a tag of an earlier launch
+        if (e->lb_seq % 255 == 0 && e->lb_seq)
+          HIPCHECK(e, hipMemsetAsync(e->lookback, 0, 2 * e->lb_tiles * sizeof(uint64_t), e->stream));
+        p.lb_tag8 = (uint32_t)(1 + e->lb_seq % 255);
+        e->lb_seq++;
         launch_wave(p, e->wave_fused_grid, e->stream);
         if (per_wave) HIPCHECK(e, hipEventRecord(ev[1], e->stream));
         if (per_wave) HIPCHECK(e, hipEventRecord(ev[2], e->stream));

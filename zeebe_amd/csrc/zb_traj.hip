@@ -600,8 +600,9 @@ __device__ __forceinline__ void merge_into(const TrajParams& P, uint32_t src, ui
       bool unsup = false;
       const bool ok = merge_docs((const uint8_t*)gs + 4, ns, (const uint8_t*)gt + 4, nt, o, unsup);
       olen = o.n;
+      if (o.n > m_len) err |= DE_UNSUPPORTED;  // (never for a document merge_docs takes: as k_merge_gen)
       // shapes the structural merge refuses: the exact tree (zb_xmerge.hpp)
-      x_exclusive(XSlabs{P.xslab, P.xlocks}, !ok || unsup || o.n > m_len, [&](uint8_t* slab) {
+      x_exclusive(XSlabs{P.xslab, P.xlocks}, (!ok || unsup) && o.n <= m_len, [&](uint8_t* slab) {
         Out w{(uint8_t*)gd + 4, 0};
         const int st = x_merge(slab, XSLAB_BYTES, (const uint8_t*)gs + 4, ns, (const uint8_t*)gt + 4, nt, w, m_len);
         if (st == X_OK) {

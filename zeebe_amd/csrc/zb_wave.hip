@@ -547,7 +547,8 @@ __device__ void job_command(const WaveParams& P, const zb_rec& rec, uint32_t rse
   }
 }
 
-__device__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t pos, uint32_t rself,
+// (always inlined: as a call it takes the parameter block through scratch -- k_wave 128 -> 1104 B of scratch per lane)
+__device__ __forceinline__ void process_record(const WaveParams& P, const zb_rec& rec, int64_t pos, uint32_t rself,
                                uint32_t rscope, TState& t) {
   const uint8_t vt = kind_vt(rec.kind), rt = kind_rt(rec.kind);
   if (vt == ZB_VT_WORKFLOW_INSTANCE) {
@@ -1261,25 +1262,75 @@ __global__ void __launch_bounds__(WG) k_emit(WaveParams P) {
 
 // ------------------------------------------------------------------------------ k_wave (fused)
 // k_process + k_scan + k_emit in one launch: each 256-record tile is processed (follow-ups staged in LDS),
-// scanned in LDS, gets its offsets from its predecessors by decoupled look-back, and writes its follow-ups
-// straight from LDS -- no count words, staging slots or side information round-trip through HBM, and no
-// single-workgroup scan between the passes. The grid is persistent (every workgroup resident, tiles dealt
-// round-robin in increasing order), so a tile only ever waits for tiles that are already running.
+// scanned in LDS, gets its offsets from its predecessors, and writes its follow-ups straight from LDS -- no count
+// words, staging slots or side information round-trip through HBM (the three-kernel form that does: C2 1M stepping
+// 28.1 against 20.5 ms, profiles/r05/wave_exp_split_r05a.txt), and no single-workgroup scan between the passes.
+// The grid is persistent (every workgroup resident, tiles dealt round-robin in increasing order): round k is tiles
+// [kG, (k+1)G), and a tile only ever waits for tiles of its own or an earlier round, which are already running.
 //
-// Look-back state: per tile LB_FIELDS 8-byte granules {tag, value} (agent-scope atomic stores and loads; the
-// data is its own flag, cdna_hip_programming.md Guideline 16 R2). A tile first publishes its aggregate
-// (tag = epoch:AGG), then its inclusive prefix (tag = epoch:INC); a reader accepts a tile's granules only when
-// all of them carry the same tag. Waiting is bounded in time (the constant-rate wall clock, not a spin count:
-// a resident predecessor that the scheduler time-slices out keeps its waiters spinning without progress for
-// as long as it is descheduled): a hand-off that has not arrived after LB_TIMEOUT_TICKS sets DE_TIMEOUT, the
-// wave's results are void and the host stops the partition -- it never hangs the device.
-constexpr int LB_FIELDS = 8;  // rec wf job row bytes_lo bytes_hi merges conds (8 predecessors per look-back round)
-constexpr int LB_ROUND = 64 / LB_FIELDS;  // predecessors read per look-back round
-constexpr int LB_STRIDE = 16;  // granules per tile (128 B)
-constexpr uint64_t LB_TIMEOUT_TICKS = 400000000ull;  // 4 s of the 100 MHz wall clock per look-back, then DE_TIMEOUT
+// Offsets (a hierarchical hand-off instead of a decoupled look-back: the look-back walked 8.8 rounds of 8
+// predecessors per tile, 55 % of tile time, because the tiles of a round all finish processing together and
+// inclusive prefixes then trickle forward one round of loads at a time, profiles/r04/phases_c2w_r04f.txt). Within
+// a round the tiles form groups of LB_GROUP:
+//   * every tile publishes its aggregate, packed into two granules (lbA);
+//   * a tile's exclusive prefix inside its group is the sum of its group predecessors' aggregates -- one load per
+//     lane of the first wave, all at once; the group's last tile publishes the group total (lbG) right away;
+//   * the sum of the earlier groups of the round: their totals, read by the second wave at the same time;
+//   * the round's base (lbR): published by the last tile of the previous round.
+// So a tile waits for the slowest tile of its group, then ~2 dependent round trips -- no chain along the round.
+//
+// Hand-off state: 8-byte granules {tag, value} written and read by agent-scope atomics (the data is its own
+// flag, cdna_hip_programming.md Guideline 16 R2). Aggregates carry an 8-bit tag (lb_seq, the host zeroes lbA when it
+// wraps); group totals and round bases one granule per field with a 32-bit epoch tag. Waiting is bounded in time
+// (the constant-rate wall clock, not a spin count: a resident predecessor that the scheduler time-slices out keeps
+// its waiters spinning without progress for as long as it is descheduled): a hand-off that has not arrived after
+// LB_TIMEOUT_TICKS sets DE_TIMEOUT, the wave's results are void and the host stops the partition -- it never hangs
+// the device.
+constexpr int LB_FIELDS = 8;   // group totals / round bases: rec wf job row bytes_lo bytes_hi merges conds
+constexpr int LB_GROUP = 64;   // tiles per group (one lane each)
+constexpr uint64_t LB_TIMEOUT_TICKS = 400000000ull;  // 4 s of the 100 MHz wall clock per hand-off, then DE_TIMEOUT
 
-__device__ __forceinline__ uint32_t lb_tag(int64_t epoch, uint32_t inc) {
-  return (uint32_t)((((uint64_t)epoch + 1) << 1) | inc);
+__device__ __forceinline__ uint32_t lb_tag(int64_t epoch, uint32_t kind) {
+  return (uint32_t)((((uint64_t)epoch + 1) << 1) | kind);
+}
+// a tile aggregate: a = rec:17 wf:17 job:11 row:11, b = merges:9 conds:11 bytes:36, each under the 8-bit tag
+__device__ __forceinline__ uint64_t lb_pack_a(uint32_t tag8, uint64_t ta) {
+  return ((uint64_t)tag8 << 56) | ((ta & 0xffff) << 39) | (((ta >> 16) & 0xffff) << 22) |
+         (((ta >> 32) & 0x7ff) << 11) | ((ta >> 48) & 0x7ff);
+}
+// field f of a tile aggregate (the tile scan's packed totals; bytes, field 4, are handled by the callers)
+__device__ __forceinline__ uint64_t lb_field(uint64_t ta, uint64_t merges, uint64_t conds, int f) {
+  return f == 0 ? (ta & 0xffff) : f == 1 ? ((ta >> 16) & 0xffff) : f == 2 ? ((ta >> 32) & 0xffff) :
+         f == 3 ? (ta >> 48) : f == 6 ? merges : f == 7 ? conds : 0;
+}
+__device__ __forceinline__ uint64_t lb_pack_b(uint32_t tag8, uint64_t tbytes, uint64_t merges, uint64_t conds) {
+  return ((uint64_t)tag8 << 56) | (merges << 47) | (conds << 36) | tbytes;
+}
+
+// wait until every granule this lane reads carries its tag (n: granules, 0..2); false: timed out / another tile did
+template <int N>
+__device__ __forceinline__ bool lb_wait(uint32_t* err, const uint64_t* const (&g)[N], const uint32_t (&tag)[N],
+                                        int shift, bool active, uint64_t (&v)[N], uint64_t t_start) {
+  bool timeout = false;
+  if (active) {
+    for (uint32_t spins = 0;; spins++) {
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < N; k++) {
+        v[k] = __hip_atomic_load(g[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok &= (uint32_t)(v[k] >> shift) == tag[k];
+      }
+      if (ok) break;
+      if ((spins & 255) == 255 &&
+          (wall_clock64() - t_start > LB_TIMEOUT_TICKS ||
+           (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & DE_TIMEOUT))) {
+        timeout = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  return !__ballot(timeout);
 }
 
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8))) k_wave(WaveParams P) {
@@ -1287,9 +1338,8 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
   __shared__ uint64_t s_a[WG / 64], s_b[WG / 64];
   __shared__ uint64_t s_st[WG / 64][2];  // transitions | completed << 32, created | canceled << 32
   __shared__ uint64_t s_ex[LB_FIELDS];   // the tile's exclusive prefix
-  __shared__ uint64_t s_tot[LB_FIELDS];  // and its inclusive prefix (the chunk totals on the last tile)
-  __shared__ uint32_t s_agg[LB_FIELDS];  // the tile's aggregate
-  __shared__ int s_void;                 // the look-back timed out: the tile's prefix is unknown, nothing is emitted
+  __shared__ uint64_t s_part[3][LB_FIELDS];  // its parts: in the group, earlier groups of the round, the round base
+  __shared__ int s_void;                 // a hand-off timed out: the tile's prefix is unknown, nothing is emitted
   const WaveHdr* hin = P.hdr + (P.wave & 1);
   WaveHdr* hout = P.hdr + ((P.wave + 1) & 1);
   const Chunk c = wave_chunk(P, hin);
@@ -1309,18 +1359,23 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
   const int64_t end = hin->end, wf_next = hin->wf_next, job_next = hin->job_next;
   const uint64_t rows_next = (uint64_t)hin->rows_next, arena_next = (uint64_t)hin->arena_next;
   const uint64_t par = (uint64_t)(P.wave & 1) * P.job_cap;
-  const uint32_t tag_agg = lb_tag(P.epoch, 0), tag_inc = lb_tag(P.epoch, 1);
+  const int64_t G = gridDim.x;
+  const int64_t GPR = (G + LB_GROUP - 1) / LB_GROUP;  // groups per round
+  const uint32_t tag8 = P.lb_tag8, tag_grp = lb_tag(P.epoch, 0), tag_rnd = lb_tag(P.epoch, 1);
+  uint64_t* const lbA = P.lookback;
+  uint64_t* const lbG = P.lookback + 2 * P.lb_tiles;
+  uint64_t* const lbR = lbG + (uint64_t)LB_FIELDS * (P.lb_tiles + 512);
   // the workgroup's statistics (transitions, completed, created, canceled): summed over its tiles, added to the
-  // partition counters once at the end (they are not part of the scan, so the look-back carries 8 fields, not 12)
+  // partition counters once at the end (they are not part of the scan)
   uint64_t wg_sa = 0, wg_sb = 0;
 
 #ifdef ZB_PHASES
-  uint64_t ph_t = wall_clock64(), ph[4] = {0, 0, 0, 0};  // process, look-back, emit, look-back rounds
+  uint64_t ph_t = wall_clock64(), ph[4] = {0, 0, 0, 0};  // process, hand-off, emit, hand-off spins (first wave)
 #define ZB_PHASE(k) do { const uint64_t ph_n = wall_clock64(); ph[k] += ph_n - ph_t; ph_t = ph_n; } while (0)
 #else
 #define ZB_PHASE(k) do { } while (0)
 #endif
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += G) {
     const int64_t i = tile * WG + threadIdx.x;  // wave-relative index
     const int64_t r = c.begin + i;
     // ---- process (k_process)
@@ -1333,6 +1388,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
     t.sub = false;
     t.nexp = 0; t.exp_ord = 0; t.src_off = 0;
     uint32_t nconds = 0;
+    if (threadIdx.x == 0) s_void = 0;  // (ordered before every wave's hand-off by the tile scan's barrier)
     if (r < c.end) {
       const zb_rec rec = P.log[r];
       if (!grouped(rec)) {
@@ -1409,126 +1465,131 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
     }
     a -= a0;
     b -= b0;
-    // ---- decoupled look-back (first wave): lane L < 60 reads granule L % 12 of predecessor tile p - L / 12,
-    // so a round covers 5 predecessors and every lane keeps one running sum (field L % 12)
-    if (threadIdx.x == 0) {
-      const uint64_t sa = s_st[0][0] + s_st[1][0] + s_st[2][0] + s_st[3][0];
-      const uint64_t sb = s_st[0][1] + s_st[1][1] + s_st[2][1] + s_st[3][1];
-      const uint64_t tbytes = tb & 0xffffffffffull;
-      s_agg[0] = (uint32_t)(ta & 0xffff); s_agg[1] = (uint32_t)((ta >> 16) & 0xffff);
-      s_agg[2] = (uint32_t)((ta >> 32) & 0xffff); s_agg[3] = (uint32_t)(ta >> 48);
-      s_agg[4] = (uint32_t)tbytes; s_agg[5] = (uint32_t)(tbytes >> 32);
-      s_agg[6] = (uint32_t)((tb >> 40) & 0xfff); s_agg[7] = (uint32_t)(tb >> 52);
-      wg_sa += sa;
-      wg_sb += sb;
-    }
+    // ---- offsets: this tile's place in its round (k) and group (gi, position u)
+    const int64_t k = tile / G, j = tile - k * G;
+    const int64_t gi = j / LB_GROUP, u = j % LB_GROUP;
+    const int64_t t_grp0 = tile - u;  // the group's first tile
+    const bool last_of_chunk = tile == ntiles - 1;
+    const bool last_of_group = u == LB_GROUP - 1 || j == G - 1 || last_of_chunk;
+    const uint64_t gg = (uint64_t)(k * GPR + gi);  // the group's index among the wave's groups
+    const uint64_t t_start = wall_clock64();
     if (wv == 0) {
-      const int f = lane % LB_FIELDS, j = lane / LB_FIELDS;  // field, predecessor distance - 1 (j < 8)
-      const bool lb_lane = lane < LB_ROUND * LB_FIELDS;
-      const uint32_t my_agg = lane < LB_FIELDS ? s_agg[lane] : 0;
-      uint64_t* lb = P.lookback + (uint64_t)tile * LB_STRIDE;
-      if (lane < LB_FIELDS)
-        __hip_atomic_store(lb + lane, ((uint64_t)(tile == 0 ? tag_inc : tag_agg) << 32) | my_agg, __ATOMIC_RELAXED,
+      // the aggregate, published first (lane 0), then this tile's exclusive prefix within its group
+      const uint64_t tbytes = tb & 0xffffffffffull;
+      const uint64_t tmerge = (tb >> 40) & 0xfff, tcond = tb >> 52;
+      if (lane == 0) {
+        const uint64_t tb36 = tbytes < (1ull << 36) ? tbytes : (1ull << 36) - 1;
+        if (tbytes != tb36) atomicOr(P.err, (uint32_t)DE_ARENA_FULL);  // (a tile's blobs past 64 GB: no arena holds them)
+        __hip_atomic_store(lbA + 2 * tile, lb_pack_a(tag8, ta), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(lbA + 2 * tile + 1, lb_pack_b(tag8, tb36, tmerge, tcond), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-      uint64_t acc = 0;  // lanes < 12: exclusive prefix of field `lane`
-      if (lane == 0) s_void = 0;
-      if (tile > 0) {
-        bool timeout = false;
-        const uint64_t t_start = wall_clock64();
-        for (int64_t p = tile - 1;;) {
-#ifdef ZB_PHASES
-          if (lane == 0) ph[3] += 1;  // look-back rounds (8 predecessors each)
-#endif
-          const int64_t q = p - j;
-          uint32_t v = 0, tg = tag_inc;  // predecessors before tile 0 count as the (empty) inclusive start
-          if (lb_lane && q >= 0) {
-            const uint64_t* g = P.lookback + (uint64_t)q * LB_STRIDE + f;
-            for (uint32_t spins = 0;; spins++) {
-              const uint64_t x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              tg = (uint32_t)(x >> 32);
-              v = (uint32_t)x;
-              if (tg == tag_agg || tg == tag_inc) break;
-              if ((spins & 255) == 255 &&
-                  (wall_clock64() - t_start > LB_TIMEOUT_TICKS ||
-                   (__hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & DE_TIMEOUT))) {
-                timeout = true;
-                break;
-              }
-              __builtin_amdgcn_s_sleep(1);
-            }
-          }
-          // a predecessor is usable when its LB_FIELDS granules carry one tag (a reader can catch it between its
-          // aggregate and inclusive publication): re-read the round otherwise. (Measured against a two-hop form with the
-// aggregates and prefixes in separate granule sets, 64 predecessors per round: 4 % slower on C2, same box. The
-// phase build shows why: the look-back's time is waiting for the predecessors' aggregates -- every tile of a round
-// needs all earlier tiles of the round processed -- not the hops.)
-          const uint64_t m_agg = __ballot(lb_lane && tg == tag_agg), m_inc = __ballot(!lb_lane || tg == tag_inc);
-          bool consistent = true, found = false;
-          int first = LB_ROUND;
+        wg_sa += s_st[0][0] + s_st[1][0] + s_st[2][0] + s_st[3][0];
+        wg_sb += s_st[0][1] + s_st[1][1] + s_st[2][1] + s_st[3][1];
+      }
+      const uint64_t* gp[2] = {lbA + 2 * (t_grp0 + lane), lbA + 2 * (t_grp0 + lane) + 1};
+      const uint32_t tg[2] = {tag8, tag8};
+      uint64_t v[2] = {0, 0};
+      const bool ok = lb_wait<2>(P.err, gp, tg, 56, lane < u, v, t_start);
+      uint64_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;  // rec | wf << 32, job | row << 32, merges | conds << 32, bytes
+      if (lane < u) {
+        x0 = ((v[0] >> 39) & 0x1ffff) | (((v[0] >> 22) & 0x1ffff) << 32);
+        x1 = ((v[0] >> 11) & 0x7ff) | ((v[0] & 0x7ff) << 32);
+        x2 = ((v[1] >> 47) & 0x1ff) | (((v[1] >> 36) & 0x7ff) << 32);
+        x3 = v[1] & ((1ull << 36) - 1);
+      }
 #pragma unroll
-          for (int k = 0; k < LB_ROUND; k++) {
-            const uint64_t gm = ((1ull << LB_FIELDS) - 1) << (LB_FIELDS * k);
-            const bool inc_k = (m_inc & gm) == gm, agg_k = (m_agg & gm) == gm;
-            if (!found) {
-              if (!inc_k && !agg_k) consistent = false;
-              if (inc_k) { first = k; found = true; }
-            }
-          }
-          if (__ballot(timeout)) { timeout = true; break; }
-          if (!consistent) continue;  // same p again (bounded by the per-granule spins above)
-          // sum field f over predecessors j <= first: lanes f, f + 8, ..., f + 56 (butterfly over the lane bits
-          // above the field)
-          uint64_t x = (lb_lane && j <= first) ? (uint64_t)v : 0;
+      for (int d = 32; d >= 1; d >>= 1) {
+        x0 += __shfl_xor(x0, d, 64); x1 += __shfl_xor(x1, d, 64);
+        x2 += __shfl_xor(x2, d, 64); x3 += __shfl_xor(x3, d, 64);
+      }
+      // lane f < 8: field f of the exclusive prefix within the group (bytes whole in field 4, field 5 zero)
+      const uint64_t e = lane == 0 ? (uint32_t)x0 : lane == 1 ? x0 >> 32 : lane == 2 ? (uint32_t)x1 :
+                         lane == 3 ? x1 >> 32 : lane == 4 ? x3 : lane == 6 ? (uint32_t)x2 : lane == 7 ? x2 >> 32 : 0;
+      if (!ok && lane == 0) s_void = 1;
+      if (lane < LB_FIELDS) s_part[0][lane] = ok ? e : 0;
+      if (ok && last_of_group && lane < LB_FIELDS) {  // the group's total, for the later groups of the round
+        const uint64_t own = lane == 4 ? tbytes : lane == 5 ? 0 : lb_field(ta, tmerge, tcond, lane);
+        const uint64_t tot = e + own;
+        const uint32_t val = lane == 4 ? (uint32_t)tot : lane == 5 ? (uint32_t)((x3 + tbytes) >> 32) : (uint32_t)tot;
+        __hip_atomic_store(lbG + gg * LB_FIELDS + lane, ((uint64_t)tag_grp << 32) | val, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else if (wv == 1) {
+      // the totals of the round's earlier groups: lane = 8 * group + field, 8 groups per pass
+      uint64_t acc = 0;
+      bool ok = true;
+      for (int64_t base = 0; base < gi && ok; base += 64 / LB_FIELDS) {
+        const int64_t q = base + lane / LB_FIELDS;
+        const uint64_t* gp[1] = {lbG + (uint64_t)(k * GPR + q) * LB_FIELDS + lane % LB_FIELDS};
+        const uint32_t tg[1] = {tag_grp};
+        uint64_t v[1] = {0};
+        ok = lb_wait<1>(P.err, gp, tg, 32, q < gi, v, t_start);
+        uint64_t x = q < gi ? (uint32_t)v[0] : 0;
 #pragma unroll
-          for (int d = LB_FIELDS; d < 64; d <<= 1) x += __shfl_xor(x, d, 64);
-          if (lane < LB_FIELDS) acc += x;
-          if (first < LB_ROUND) break;
-          p -= LB_ROUND;
-        }
-        if (__ballot(timeout) && lane == 0) {
-          atomicOr(P.err, (uint32_t)DE_TIMEOUT);  // the others stop waiting too
-          s_void = 1;  // (the host fails the wave: no record, row or blob is written from a partial prefix)
-        }
+        for (int d = LB_FIELDS; d < 64; d <<= 1) x += __shfl_xor(x, d, 64);
+        acc += x;
       }
       // bytes travel as two 32-bit granules (fields 4, 5): recombine the carry
-      const uint64_t ex_lo = __shfl(acc, 4, 64), ex_hi = __shfl(acc, 5, 64);
-      const uint64_t exb = ex_lo + (ex_hi << 32);
-      const uint64_t tbytes = (uint64_t)s_agg[4] | ((uint64_t)s_agg[5] << 32);
-      if (tile > 0 && lane < LB_FIELDS) {
-        const uint64_t incb = exb + tbytes;
-        const uint32_t val = lane == 4 ? (uint32_t)incb : lane == 5 ? (uint32_t)(incb >> 32) : (uint32_t)(acc + my_agg);
-        __hip_atomic_store(lb + lane, ((uint64_t)tag_inc << 32) | val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (lane < LB_FIELDS) {
-        s_ex[lane] = lane == 4 ? exb : lane == 5 ? 0 : acc;
-        s_tot[lane] = lane == 4 ? exb + tbytes : lane == 5 ? 0 : acc + my_agg;
-      }
-      // the chunk's last tile: totals -> next wave header, counters, job counts (k_scan's job)
-      if (tile == ntiles - 1 && lane == 0) {
-        WaveHdr h = *hin;
-        h.begin = c.end;
-        h.end = hin->end + (int64_t)s_tot[0];
-        h.gen_end = (c.end == hin->gen_end) ? h.end : hin->gen_end;
-        h.wf_next = hin->wf_next + 5 * (int64_t)s_tot[1];
-        h.job_next = hin->job_next + 5 * (int64_t)s_tot[2];
-        h.rows_next = hin->rows_next + (int64_t)s_tot[3];
-        h.arena_next = hin->arena_next + (int64_t)s_tot[4];
-        P.stats[6] += 1;
-        uint32_t err = 0;
-        if ((uint64_t)h.end > P.log_cap) err |= DE_LOG_FULL;
-        if ((uint64_t)h.rows_next > P.row_cap) err |= DE_ROWS_FULL;
-        if ((uint64_t)h.arena_next > P.arena_cap) err |= DE_ARENA_FULL;
-        if (s_tot[6] > P.job_cap || s_tot[7] > P.job_cap) err |= DE_LOG_FULL;
-        if (err) atomicOr(P.err, err);
-        *hout = h;
-        if (P.need_children) *P.need_children = 0;  // k_pre of the next chunk sets it again
-        P.merge_count[P.wave & 1] = (uint32_t)s_tot[6];
-        P.cond_count[P.wave & 1] = (uint32_t)s_tot[7];
-        if (P.sub_count) clear_sub_counts(P);  // the next wave's subscribe list
+      const uint64_t lo = __shfl(acc, 4, 64), hi = __shfl(acc, 5, 64);
+      if (!ok && lane == 0) s_void = 1;
+      if (lane < LB_FIELDS) s_part[1][lane] = !ok ? 0 : lane == 4 ? lo + (hi << 32) : lane == 5 ? 0 : acc;
+    } else if (wv == 2) {
+      // the round's base, published by the previous round's last tile
+      const uint64_t* gp[1] = {lbR + (uint64_t)k * LB_FIELDS + lane % LB_FIELDS};
+      const uint32_t tg[1] = {tag_rnd};
+      uint64_t v[1] = {0};
+      const bool ok = lb_wait<1>(P.err, gp, tg, 32, k > 0 && lane < LB_FIELDS, v, t_start);
+      const uint64_t x = k > 0 ? (uint32_t)v[0] : 0;
+      const uint64_t hi = __shfl(x, 5, 64);
+      if (!ok && lane == 0) s_void = 1;
+      if (lane < LB_FIELDS) s_part[2][lane] = !ok ? 0 : lane == 4 ? x + (hi << 32) : lane == 5 ? 0 : x;
+    }
+    __syncthreads();
+    if (wv == 0) {
+      const uint64_t tbytes = tb & 0xffffffffffull;
+      const uint64_t own = lane == 4 ? tbytes : lane == 5 ? 0 : lb_field(ta, (tb >> 40) & 0xfff, tb >> 52, lane);
+      const uint64_t ex = lane < LB_FIELDS ? s_part[0][lane] + s_part[1][lane] + s_part[2][lane] : 0;
+      const uint64_t inc = ex + own;
+      const uint64_t t0 = __shfl(inc, 0, 64), t1 = __shfl(inc, 1, 64), t2 = __shfl(inc, 2, 64);
+      const uint64_t t3 = __shfl(inc, 3, 64), t4 = __shfl(inc, 4, 64), t6 = __shfl(inc, 6, 64);
+      const uint64_t t7 = __shfl(inc, 7, 64);
+      if (s_void) {
+        if (lane == 0) atomicOr(P.err, (uint32_t)DE_TIMEOUT);  // (the host fails the wave: nothing is written from a
+      } else {                                                 //  partial prefix; the other tiles stop waiting too)
+        if (lane < LB_FIELDS) s_ex[lane] = ex;
+        // the last tile of a round hands the next round its base
+        if (j == G - 1 && !last_of_chunk && lane < LB_FIELDS) {
+          const uint32_t val = lane == 4 ? (uint32_t)t4 : lane == 5 ? (uint32_t)(t4 >> 32) : (uint32_t)inc;
+          __hip_atomic_store(lbR + (uint64_t)(k + 1) * LB_FIELDS + lane, ((uint64_t)tag_rnd << 32) | val,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // the chunk's last tile: totals -> next wave header, counters, job counts (k_scan's job)
+        if (last_of_chunk && lane == 0) {
+          WaveHdr h = *hin;
+          h.begin = c.end;
+          h.end = hin->end + (int64_t)t0;
+          h.gen_end = (c.end == hin->gen_end) ? h.end : hin->gen_end;
+          h.wf_next = hin->wf_next + 5 * (int64_t)t1;
+          h.job_next = hin->job_next + 5 * (int64_t)t2;
+          h.rows_next = hin->rows_next + (int64_t)t3;
+          h.arena_next = hin->arena_next + (int64_t)t4;
+          P.stats[6] += 1;
+          uint32_t err = 0;
+          if ((uint64_t)h.end > P.log_cap) err |= DE_LOG_FULL;
+          if ((uint64_t)h.rows_next > P.row_cap) err |= DE_ROWS_FULL;
+          if ((uint64_t)h.arena_next > P.arena_cap) err |= DE_ARENA_FULL;
+          if (t6 > P.job_cap || t7 > P.job_cap) err |= DE_LOG_FULL;
+          if (err) atomicOr(P.err, err);
+          *hout = h;
+          if (P.need_children) *P.need_children = 0;  // k_pre of the next chunk sets it again
+          P.merge_count[P.wave & 1] = (uint32_t)t6;
+          P.cond_count[P.wave & 1] = (uint32_t)t7;
+          if (P.sub_count) clear_sub_counts(P);  // the next wave's subscribe list
+        }
       }
     }
     __syncthreads();
-    ZB_PHASE(1);  // look-back (+ the chunk's header on the last tile)
+    ZB_PHASE(1);  // hand-off (+ the chunk's header on the last tile)
     // ---- emit (k_emit) straight from the LDS slots
     const uint64_t we = w;
     const int ns = (int)(we & 7);
@@ -1557,7 +1618,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
 #ifdef ZB_PHASES
   if (threadIdx.x == 0 && P.phase) {
     for (int k = 0; k < 3; k++) atomicAdd(P.phase + k, (unsigned long long)ph[k]);
-    atomicAdd(P.phase + 4, (unsigned long long)ph[3]);
+    atomicAdd(P.phase + 4, (unsigned long long)((ntiles - blockIdx.x + gridDim.x - 1) / gridDim.x));
     atomicAdd(P.phase + 3, (unsigned long long)((ntiles - blockIdx.x + gridDim.x - 1) / gridDim.x));
   }
 #endif
@@ -1587,7 +1648,7 @@ __global__ void __launch_bounds__(256) k_conflict(WaveParams P) {
   for (int64_t r = b + (int64_t)blockIdx.x * 256 + threadIdx.x; r < g; r += stride) {
     const zb_rec rec = P.log[r];
     if (grouped(rec)) continue;
-    const int64_t s = conf_slot(P, rec.inst_key);
+    const int64_t s = conf_slot(P, conflict_key(rec.inst_key, rec.key, rec.kind));
     if (s < 0) continue;
     if (!SPLIT) atomicMin((unsigned long long*)(P.conf_first + s), (unsigned long long)r);
     else if (r > P.conf_first[s]) atomicMin((unsigned long long*)P.conf_split, (unsigned long long)r);

@@ -477,13 +477,14 @@ ZB_HD inline __noinline__ int x_merge(uint8_t* slab, uint32_t slab_bytes, const 
   return x_emit(T, tgt, nt, src, ns, o, limit);
 }
 
-// MappingProcessor.extract(source, mappings) (tgt == nullptr) or .merge(source, target, mappings), nmaps >= 1
-ZB_HD inline __noinline__ int x_map(uint8_t* slab, uint32_t slab_bytes, const uint8_t* src, uint32_t ns, const uint8_t* tgt,
-                       uint32_t nt, const DevMapping* maps, uint32_t nmaps, const DevSeg* segs, const DevQuery* queries,
-                       const DevFilter* filters, const uint8_t* pool, Out& o, uint32_t limit, uint16_t& fail_query) {
+// The tree of MappingProcessor.extract(source, mappings) (tgt == nullptr) or .merge(source, target, mappings) with
+// nmaps >= 1, before it is written: the target indexed, then every mapping's target path and extracted leaf
+ZB_HD inline int x_map_tree(XTree& T, uint8_t* slab, uint32_t slab_bytes, const uint8_t* src, uint32_t ns,
+                            const uint8_t* tgt, uint32_t nt, const DevMapping* maps, uint32_t nmaps, const DevSeg* segs,
+                            const DevQuery* queries, const DevFilter* filters, const uint8_t* pool,
+                            uint16_t& fail_query) {
   uint32_t segn = 0;
   for (uint32_t i = 0; i < nmaps; i++) segn += maps[i].nseg + 1;
-  XTree T;
   if (!T.init(slab, slab_bytes, (tgt ? x_tokens(tgt, nt) : 0) + 2 * segn)) return T.status;
   if (tgt && nt) {
     T.index(0, tgt, nt, false);
@@ -536,6 +537,16 @@ ZB_HD inline __noinline__ int x_map(uint8_t* slab, uint32_t slab_bytes, const ui
     T.add_leaf(0, parent, r.pos, r.len, true);
     if (T.status != X_OK) return T.status;
   }
+  return X_OK;
+}
+
+// MappingProcessor.extract(source, mappings) (tgt == nullptr) or .merge(source, target, mappings), nmaps >= 1
+ZB_HD inline __noinline__ int x_map(uint8_t* slab, uint32_t slab_bytes, const uint8_t* src, uint32_t ns, const uint8_t* tgt,
+                       uint32_t nt, const DevMapping* maps, uint32_t nmaps, const DevSeg* segs, const DevQuery* queries,
+                       const DevFilter* filters, const uint8_t* pool, Out& o, uint32_t limit, uint16_t& fail_query) {
+  XTree T;
+  const int st = x_map_tree(T, slab, slab_bytes, src, ns, tgt, nt, maps, nmaps, segs, queries, filters, pool, fail_query);
+  if (st != X_OK) return st;
   return x_emit(T, tgt, tgt ? nt : 0, src, ns, o, limit);
 }
 
