@@ -38,12 +38,23 @@ class JobWorld:
     """The other writers: the job processor (job keys 2 + 5j, KeyGenerator.createJobKeyGenerator) with its
     workers, and clients creating / cancelling instances."""
 
-    def __init__(self, live):
+    def __init__(self, live, cancels=CANCELS):
         self.live = live
+        self.cancels = cancels
         self.pending = []    # [wik, aik, task index, JOB CREATE value bytes] of every waiting instance
         self.next_job = 0
         self.tick = 0
         self.created = 0
+
+    def harvest_oracle(self, o, start):
+        """The same from the oracle's records (the sequential restatement writes the identical log)."""
+        import msgpack
+
+        for r in o.records(start):
+            if r.value_type == R.VT_JOB and r.record_type == R.RT_COMMAND and r.intent == R.JI_CREATE:
+                h = msgpack.unpackb(r.value, raw=False)["headers"]
+                self.pending.append([h["workflowInstanceKey"], h["activityInstanceKey"], int(h["activityId"][1:]),
+                                     r.value])
 
     def harvest(self, eng, start, count, ser=None):
         """The tick's JOB CREATE commands, from its drained records (ser: the zb_serialize of exactly that range,
@@ -77,7 +88,7 @@ class JobWorld:
         self.tick += 1
         done = [p for i, p in enumerate(self.pending) if (i + t) % FRACTION == 0]
         rest = [p for i, p in enumerate(self.pending) if (i + t) % FRACTION != 0]
-        cancel, self.pending = rest[:CANCELS], rest[CANCELS:]
+        cancel, self.pending = rest[:self.cancels], rest[self.cancels:]
         n_create = max(1, self.live // (FRACTION * TASKS))
         pay = [b"\x81\xa7orderId" + _mp_int(self.created + i) for i in range(n_create)]
         self.created += n_create
@@ -188,8 +199,6 @@ def run_steady(a, rank, world, local_rank, barrier, steps, warmup, live=1_000_00
 def cpu_baseline_steady(live, ticks):
     """The oracle (sequential C++ restatement) driven by the same schedule on a bounded sample: `live` instances,
     then `ticks` ticks of the same mix; timed from the first input of the first tick to quiescence of the last."""
-    import msgpack
-
     from oracle import zbref
     from zeebe_amd import bpmn
 
@@ -202,11 +211,7 @@ def cpu_baseline_steady(live, ticks):
     w = JobWorld(live)
 
     def harvest(start):
-        for r in o.records(start):
-            if r.value_type == R.VT_JOB and r.record_type == R.RT_COMMAND and r.intent == R.JI_CREATE:
-                h = msgpack.unpackb(r.value, raw=False)["headers"]
-                w.pending.append([h["workflowInstanceKey"], h["activityInstanceKey"],
-                                  int(h["activityId"][1:]), r.value])
+        w.harvest_oracle(o, start)
 
     harvest(0)
     c0 = o.counters()

@@ -355,6 +355,12 @@ void zb_pinned_free(void* p);
  * zb_submit_publishes, zb_inbox_submit) the window starts there, and released records can no longer be
  * drained. Positions stay absolute (LogStream positions are the caller's). */
 int zb_log_release(zb_engine* e, int64_t position);
+/* The partition's log continues at `position` (>= its current end): a processor that resumes on a logstream whose
+ * earlier records it does not process (StreamProcessorController.java:296-414 reprocesses from a snapshot position;
+ * LogEntryDescriptor.java:28-121 positions are 64-bit). Positions, source positions and position keys of everything
+ * written afterwards follow from it. Only on an idle partition whose window is empty (everything written released)
+ * and with nothing staged. */
+int zb_log_start(zb_engine* e, int64_t position);
 /* Compaction of a quiescent partition (also run automatically between ticks when the element-instance rows,
  * the payload arena or the job table are more than half full): element instances removed on COMPLETED /
  * TERMINATED free their rows (ElementInstanceIndex.removeInstance, ElementInstanceIndex.java:54-64), payload

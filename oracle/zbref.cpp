@@ -730,8 +730,10 @@ class Engine {
     return best;
   }
 
+  int64_t pos_base = 0;  // the position of log[0] (zbref_set_position_base; the engine's zb_log_start)
+
   void append(Record r) {
-    r.position = (int64_t)log.size();
+    r.position = pos_base + (int64_t)log.size();
     log.push_back(std::move(r));
   }
 
@@ -760,7 +762,7 @@ class Engine {
     r.record_type = RT_COMMAND;
     r.value_type = VT_WORKFLOW_INSTANCE_SUBSCRIPTION;
     r.intent = WIS_CORRELATE;
-    r.key = (int64_t)log.size();  // positionAsKey (SubscriptionApiCommandMessageHandler.java:131-151)
+    r.key = pos_base + (int64_t)log.size();  // positionAsKey (SubscriptionApiCommandMessageHandler.java:131-151)
     r.wis.workflow_instance_key = wf_instance_key;
     r.wis.activity_instance_key = activity_instance_key;
     r.wis.message_name = name;
@@ -787,7 +789,7 @@ class Engine {
     // a MESSAGE DELETE command is written by the time-to-live checker's own command writer (producer id 0)
     if (record_type == RT_COMMAND && value_type == VT_MESSAGE && intent == MSG_DELETE) r.producer_id = 0;
     if (record_type == RT_COMMAND && value_type == VT_WORKFLOW_INSTANCE_SUBSCRIPTION && intent == WIS_CORRELATE)
-      r.key = (int64_t)log.size();  // positionAsKey (SubscriptionApiCommandMessageHandler.java:131-151)
+      r.key = pos_base + (int64_t)log.size();  // positionAsKey (SubscriptionApiCommandMessageHandler.java:131-151)
     append(std::move(r));
   }
 
@@ -912,7 +914,7 @@ class Engine {
     r.record_type = RT_COMMAND;
     r.value_type = VT_MESSAGE_SUBSCRIPTION;
     r.intent = MSUB_OPEN;
-    r.key = (int64_t)log.size();
+    r.key = pos_base + (int64_t)log.size();
     r.msub.wf_partition = wfp;
     r.msub.workflow_instance_key = wik;
     r.msub.activity_instance_key = aik;
@@ -1028,7 +1030,7 @@ class Engine {
       dispatch(rec);
     } catch (const ZbError& e) {
       // StreamProcessorController.onFailure: the partition stops processing
-      last_error = std::string("processing failed at position ") + std::to_string(pos) + ": " + e.what();
+      last_error = std::string("processing failed at position ") + std::to_string(pos_base + (int64_t)pos) + ": " + e.what();
       throw;
     }
     w_ = nullptr;
@@ -1782,8 +1784,17 @@ int64_t zbref_run(void* h, int64_t max_records) {
 }
 
 // request metadata of a submitted command (the client API's requestId / requestStreamId)
+// positions of the API below are log positions: log[position - pos_base]
+int zbref_set_position_base(void* h, int64_t base) {
+  Engine* e = (Engine*)h;
+  if (!e->log.empty() || base < 0) return -1;
+  e->pos_base = base;
+  return 0;
+}
+
 int zbref_set_request(void* h, int64_t position, uint64_t request_id, int32_t request_stream_id) {
   Engine* e = (Engine*)h;
+  position -= e->pos_base;
   if (position < 0 || position >= (int64_t)e->log.size()) return -1;
   e->log[(size_t)position].request_id = request_id;
   e->log[(size_t)position].request_stream_id = request_stream_id;
@@ -1794,7 +1805,9 @@ int zbref_set_request(void* h, int64_t position, uint64_t request_id, int32_t re
 int64_t zbref_frames(void* h, int64_t from, int64_t to, int32_t stream_id, int32_t raft_term, int64_t timestamp,
                      uint8_t* buf, size_t cap) {
   Engine* e = (Engine*)h;
-  if (to < 0 || to > (int64_t)e->log.size()) to = (int64_t)e->log.size();
+  from = std::max<int64_t>(from - e->pos_base, 0);
+  to = to < 0 ? (int64_t)e->log.size() : to - e->pos_base;
+  if (to > (int64_t)e->log.size()) to = (int64_t)e->log.size();
   size_t off = 0;
   for (int64_t i = from; i < to; i++) {
     const bytes f = encode_frame(e->log[(size_t)i], stream_id, raft_term, timestamp);
@@ -1804,12 +1817,12 @@ int64_t zbref_frames(void* h, int64_t from, int64_t to, int32_t stream_id, int32
   return (int64_t)off;
 }
 
-int64_t zbref_log_size(void* h) { return (int64_t)((Engine*)h)->log.size(); }
+int64_t zbref_log_size(void* h) { return ((Engine*)h)->pos_base + (int64_t)((Engine*)h)->log.size(); }
 
 // Fills header and returns the encoded value into buf (if cap suffices); returns value length.
 int64_t zbref_get_record(void* h, int64_t i, zbref_record* out, uint8_t* buf, size_t cap) {
   Engine* e = (Engine*)h;
-  const Record& r = e->log.at((size_t)i);
+  const Record& r = e->log.at((size_t)(i - e->pos_base));
   bytes v = r.encode_value();
   out->position = r.position;
   out->source_position = r.source_position;
@@ -1827,7 +1840,9 @@ int64_t zbref_get_record(void* h, int64_t i, zbref_record* out, uint8_t* buf, si
 int64_t zbref_dump_log(void* h, int64_t from, int64_t to, uint8_t* buf, size_t cap) {
   Engine* e = (Engine*)h;
   size_t off = 0;
-  if (to < 0 || to > (int64_t)e->log.size()) to = (int64_t)e->log.size();
+  from = std::max<int64_t>(from - e->pos_base, 0);
+  to = to < 0 ? (int64_t)e->log.size() : to - e->pos_base;
+  if (to > (int64_t)e->log.size()) to = (int64_t)e->log.size();
   for (int64_t i = from; i < to; i++) {
     const Record& r = e->log[(size_t)i];
     bytes v = r.encode_value();

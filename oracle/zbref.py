@@ -84,6 +84,7 @@ def lib():
                                        ctypes.c_char_p, sz]
         L.zbref_traverse.restype = ctypes.c_int
         L.zbref_traverse.argtypes = [u8p, sz, ctypes.POINTER(i32), ctypes.c_char_p, sz]
+        L.zbref_set_position_base.argtypes = [vp, i64]
         L.zbref_tree_dump.restype = i64
         L.zbref_tree_dump.argtypes = [u8p, sz, cp, ctypes.c_int, ctypes.c_void_p, sz, ctypes.c_char_p, sz]
         L.zbref_subscription_hash.restype = i32
@@ -187,6 +188,11 @@ class Oracle:
 
     def cancel(self, key: int):
         self._L.zbref_submit_cancel(self._h, key)
+
+    def set_position_base(self, base: int):
+        """The log's first position (the engine's zb_log_start): positions, source positions, position keys follow."""
+        if self._L.zbref_set_position_base(self._h, base):
+            raise ZbrefError("position base on a non-empty log")
 
     def set_harness(self, on: bool):
         """Canonical job harness on (default) / off (JOB CREATE commands wait for submitted job events)."""

@@ -387,3 +387,39 @@ def test_rccl_exchange_failure_protocol():
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "exchange failure protocol ok" in r.stdout, (r.returncode, r.stdout[-2000:],
                                                                               r.stderr[-4000:])
+
+
+@pytest.mark.parametrize("P", [1, 3])
+def test_positions_past_2_34(P):
+    """Log positions are 64-bit and never rebased (LogEntryDescriptor.java:28-121; positionAsKey,
+    SubscriptionApiCommandMessageHandler.java:146): partitions whose logs continue at and across 2^34 (zb_log_start; the
+    oracle with the same position base) correlate exactly as at position 0 -- the outbox order keys hold positions
+    relative to the outbox's last take (zb_msg.hpp outbox_key), so a tick straddling 2^34 orders its exchange as any
+    other. Covers CORRELATE keys (= positions), source positions, log frames and a message matching more than 32
+    subscriptions (the emission index by store-index span)."""
+    gpu, ref, cg, co = clusters(P, catch_workflow())
+    bases = [(1 << 34) - 40 + p * ((1 << 35) + 7) for p in range(P)]  # partition 0 crosses 2^34 in its first tick
+    for g, o, b in zip(gpu, ref, bases):
+        g.log_start(b)
+        o.set_position_base(b)
+        assert g.log_size() == o.log_size() == b
+    keys = ["shared"] * 40 + ["order-%d" % i for i in range(30)]
+    for i, key in enumerate(keys):
+        gpu[i % P].create("wf", [msgpack.packb({"orderId": key})])
+        ref[i % P].create("wf", msgpack.packb({"orderId": key}))
+    cg.settle()
+    co.settle()
+    cks = [b"order-%d" % i for i in range(0, 30, 2)] + [b"shared"] + [b"order-%d" % i for i in range(1, 30, 2)]
+    pls = [msgpack.packb({"m": i}) for i in range(len(cks))]
+    cg.publish(b"order canceled", cks, pls)
+    co.publish(b"order canceled", cks, pls)
+    for p, (g, o, b) in enumerate(zip(gpu, ref, bases)):
+        a, c = o.records(b), g.records(b)
+        assert len(a) == len(c) and len(a) > 0, (p, len(a), len(c))
+        assert a[-1].position >= (1 << 34), (p, a[-1].position)
+        for x, y in zip(a, c):
+            assert (x.position, x.source_position, x.key, x.record_type, x.value_type, x.intent) == \
+                   (y.position, y.source_position, y.key, y.record_type, y.value_type, y.intent), (p, x, y)
+            assert x.value == y.value, (p, x.position)
+        assert_frames_equal(o, g, b)
+    assert sum(g.counters()["completed"] for g in gpu) == len(keys)

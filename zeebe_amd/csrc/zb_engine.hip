@@ -231,6 +231,7 @@ struct zb_engine {
   uint64_t* okeys[2] = {nullptr, nullptr};
   uint8_t* ovar[2] = {nullptr, nullptr};  // their commands' variable bytes
   uint32_t* on = nullptr;  // [4] device counters: commands of [0] / [1], byte-section granules of [0] / [1]
+  int64_t ob_pos_base[2] = {0, 0};  // Outbox.pos_base of [0] / [1]: the processing frontier at its last take
   uint64_t ocap = 0, ovar_cap = 0;        // commands, granules
   int64_t clock_ms = 0;                   // zb_set_clock (ActorClock of the message stream processor)
   // message batches / delivered exchange batches
@@ -488,6 +489,7 @@ Outbox outbox(zb_engine* e, int kind) {
   o.var = e->ovar[k];
   o.var_n = e->on ? e->on + 2 + k : nullptr;
   o.var_cap = e->ovar_cap;
+  o.pos_base = e->ob_pos_base[k];
   return o;
 }
 
@@ -1494,6 +1496,7 @@ int zb_reset(zb_engine* e, int keep_staged) {
   e->sub_count = e->msg_count = 0;
   e->msg_key_next = 0;
   if (e->on) HIPCHECK(e, hipMemsetAsync(e->on, 0, 4 * sizeof(uint32_t), e->stream));
+  e->ob_pos_base[0] = e->ob_pos_base[1] = 0;
   e->clock_ms = 0;
   if (e->subs) {
     HIPCHECK(e, hipMemsetAsync(e->sub_head, 0xff, (e->head_mask + 1) * sizeof(uint32_t), e->stream));
@@ -3011,13 +3014,19 @@ int scan_u64(zb_engine* e, uint64_t* in, uint64_t* out, uint64_t n, uint64_t* to
 
 // Appends the batch's commands at the log tail and processes them in order, runs of one intent in lockstep
 // (PUBLISH: count, scan, emit; DELETE: emit). Follow-ups come after all the commands, in command order (FIFO).
+// the outbox order keys of commands from records up to `end` fit their position field (zb_msg.hpp outbox_key)
+bool outbox_span_ok(const zb_engine* e, int64_t end) {
+  return (uint64_t)(end - std::min(e->ob_pos_base[0], e->ob_pos_base[1])) < (1ull << OB_REL_BITS);
+}
+
 // capacity checks of a message batch of n commands (publishes of them) with blob_bytes of blobs
 int check_message_batch(zb_engine* e, uint64_t n, uint64_t publishes, uint64_t blob_bytes) {
   const int64_t base = e->host_hdr.end;
   // upper bounds first: every command writes at most 3 records (itself, PUBLISHED, DELETED)
   if ((uint64_t)(base - e->win_base) + 3 * n > e->cfg.log_capacity)
     return fail(e, ZB_ENOMEM, "log capacity (release drained records with zb_log_release)");
-  if ((uint64_t)base + 3 * n >= (1ull << 34)) return fail(e, ZB_EUNSUPPORTED, "log position beyond the outbox order key");
+  if (!outbox_span_ok(e, base + 3 * (int64_t)n))
+    return fail(e, ZB_EUNSUPPORTED, "more than 2^34 log positions since the outbox was last taken");
   if (e->msg_count + publishes > e->store_cap) return fail(e, ZB_ENOMEM, "message store capacity");
   if ((uint64_t)e->host_hdr.arena_next + blob_bytes > e->cfg.arena_bytes) return fail(e, ZB_ENOMEM, "arena capacity");
   return ZB_OK;
@@ -3166,7 +3175,8 @@ int deliver(zb_engine* e, int kind, const uint8_t* buf, const std::vector<uint64
   const int64_t base = e->host_hdr.end;
   const uint64_t recs = kind == ZB_XCHG_OPEN ? 2 * n : n;
   if ((uint64_t)(base - e->win_base) + recs > e->cfg.log_capacity) return fail(e, ZB_ENOMEM, "log capacity");
-  if ((uint64_t)base + recs >= (1ull << 34)) return fail(e, ZB_EUNSUPPORTED, "log position beyond the outbox order key");
+  if (!outbox_span_ok(e, base + (int64_t)recs))
+    return fail(e, ZB_EUNSUPPORTED, "more than 2^34 log positions since the outbox was last taken");
   if (kind == ZB_XCHG_OPEN && (e->sub_count + n > e->store_cap || e->sub_count + n >= (1ull << 32)))
     return fail(e, ZB_ENOMEM, "subscription store capacity");
   std::vector<uint64_t> table(first);
@@ -3602,6 +3612,8 @@ int outbox_emit(zb_engine* e, int kind, uint8_t* dst, uint64_t cap) {
                      e->stream);
   HIPCHECK(e, hipMemsetAsync(e->on + k, 0, sizeof(uint32_t), e->stream));      // the outbox is taken
   HIPCHECK(e, hipMemsetAsync(e->on + 2 + k, 0, sizeof(uint32_t), e->stream));  // (and its byte section)
+  // the commands written from here on come from records at or after the processing frontier
+  e->ob_pos_base[k] = e->host_hdr.begin;
   return ZB_OK;  // (stream-ordered: the exchange's sends / the local delivery follow on the same stream)
 }
 }  // namespace
@@ -3802,6 +3814,27 @@ int zb_log_release(zb_engine* e, int64_t position) {
   // only processed records can leave the window (the engine still reads the unprocessed ones)
   if (position > e->host_hdr.begin) return fail(e, ZB_EINVAL, "cannot release unprocessed records");
   e->released = std::max(e->released, position);
+  return ZB_OK;
+}
+
+int zb_log_start(zb_engine* e, int64_t position) {
+  if (!e) return ZB_EINVAL;
+  HIPCHECK(e, hipSetDevice(e->cfg.device));
+  if (e->failed) return fail(e, ZB_EPROCESSING, "partition stopped after a processing failure: " + e->err);
+  if (e->host_hdr.begin != e->host_hdr.end) return fail(e, ZB_EINVAL, "partition not quiescent");
+  if (e->staged_pending && !e->staged.empty()) return fail(e, ZB_EINVAL, "staged input not injected yet");
+  if (position < e->host_hdr.end) return fail(e, ZB_EINVAL, "log positions only grow");
+  if (std::max(e->released, e->win_base) < e->host_hdr.end) return fail(e, ZB_EINVAL, "unreleased records in the window");
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  e->host_hdr.begin = e->host_hdr.end = e->host_hdr.gen_end = position;
+  e->win_base = e->released = position;
+  e->ob_pos_base[0] = e->ob_pos_base[1] = position;
+  e->ranges.clear();
+  e->reqs.clear();
+  e->cmd_pool.clear();
+  rebias(e);
+  HIPCHECK(e, upload_async(e, e->hdr + (e->wave & 1), &e->host_hdr, sizeof(WaveHdr)));
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
   return ZB_OK;
 }
 
@@ -4098,6 +4131,7 @@ int zb_restore(zb_engine* e, const uint8_t* buf, size_t len) {
   e->host_hdr.begin = e->host_hdr.gen_end = e->host_hdr.end;
   // the log itself lives in the logstream, not in the snapshot: the window starts empty at its end
   e->win_base = e->released = e->host_hdr.end;
+  e->ob_pos_base[0] = e->ob_pos_base[1] = e->host_hdr.end;
   rebias(e);
   e->epoch = std::max(e->epoch, h.epoch);
   e->msg_key_next = h.msg_key_next;

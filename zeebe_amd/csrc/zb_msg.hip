@@ -149,9 +149,10 @@ __global__ void __launch_bounds__(256) k_msg_open(MsgParams P) {
   if (act && ncorr) {
     const MsgView v = msg_view(P.arena, best_blob);
     if (slot >= P.ob.cap || (uint64_t)vat + gran > P.ob.var_cap) err |= DE_LOG_FULL;
-    else
-      outbox_write(P.ob, slot, vat, ZB_XCHG_CORRELATE, r.wf_partition, r.wf_partition, r.token, r.workflow_instance_key,
-                   r.activity_instance_key, pos, r.elem, var, r.name_len, nullptr, 0, v.payload, v.np, 0);
+    else if (!outbox_write(P.ob, slot, vat, ZB_XCHG_CORRELATE, r.wf_partition, r.wf_partition, r.token,
+                           r.workflow_instance_key, r.activity_instance_key, pos, r.elem, var, r.name_len, nullptr, 0,
+                           v.payload, v.np, 0))
+      err |= DE_UNSUPPORTED;
   }
   if (act) {  // MessageSubscriptionDataStore.addSubscription
     const uint32_t idx = (uint32_t)(P.sub_count + i);
@@ -209,6 +210,7 @@ __global__ void __launch_bounds__(256) k_pub_emit(MsgParams P) {
   bool acc = false;
   uint64_t off = 0;
   uint32_t e1 = NO_ENTRY;  // the first matching subscription of the chain
+  uint32_t idx0 = 0xffffffffu;  // the smallest store index among the matches
   if (act) {
     d = P.log[pos];
     v = msg_view(P.arena, d.payload);
@@ -234,6 +236,7 @@ __global__ void __launch_bounds__(256) k_pub_emit(MsgParams P) {
         const SubEntry s = P.subs[e];
         if (s.h == h && sub_matches(sub_view(P.arena, s.blob), v)) {
           if (nmatch++ == 0) e1 = e;
+          idx0 = s.idx < idx0 ? s.idx : idx0;
         }
       }
       gran = nmatch * var_granules(v.nn, 0, v.np);
@@ -252,17 +255,21 @@ __global__ void __launch_bounds__(256) k_pub_emit(MsgParams P) {
       left--;
       if (slot >= P.ob.cap || (uint64_t)vat + g > P.ob.var_cap) { err |= DE_LOG_FULL; break; }
       // emission order = findSubscriptions' insertion order: the subscription's rank by store index among this
-      // message's matches (a few bits: the outbox sort then covers the positions and little more), or the index
-      // itself for a message with many matches
+      // message's matches (a few bits: the outbox sort then covers the positions and little more), or, for a message
+      // with many matches, its store index past the smallest of them (the same order; outbox_write refuses a span
+      // past 2^24 entries instead of wrapping it)
       uint32_t em = 0;
-      if (nmatch > 32) em = s.idx;
+      if (nmatch > 32) em = s.idx - idx0;
       else if (nmatch > 1)
         for (uint32_t e2 = e1; e2 != NO_ENTRY; e2 = P.sub_next[e2]) {
           const SubEntry s2 = P.subs[e2];
           if (s2.h == h && s2.idx < s.idx && sub_matches(sub_view(P.arena, s2.blob), v)) em++;
         }
-      outbox_write(P.ob, slot, vat, ZB_XCHG_CORRELATE, sb.wfp, sb.wfp, sb.token, s.wik, s.aik, pos, sb.elem, v.name, v.nn,
-                   nullptr, 0, v.payload, v.np, em);
+      if (!outbox_write(P.ob, slot, vat, ZB_XCHG_CORRELATE, sb.wfp, sb.wfp, sb.token, s.wik, s.aik, pos, sb.elem, v.name,
+                        v.nn, nullptr, 0, v.payload, v.np, em)) {
+        err |= DE_UNSUPPORTED;
+        break;
+      }
       slot++;
       vat += g;
     }

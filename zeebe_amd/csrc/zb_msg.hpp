@@ -84,9 +84,13 @@ __device__ __forceinline__ uint64_t name_ck_hash(const uint8_t* name, uint32_t n
 
 // outbox order: (target partition, source log position, emission index) — the order in which the
 // reference's processors produce the commands (side effects run in processing order;
-// findSubscriptions returns subscriptions in insertion order)
-__device__ __forceinline__ uint64_t outbox_key(int32_t target, int64_t pos, uint32_t emission) {
-  return ((uint64_t)target << 58) | (((uint64_t)pos & ((1ull << 34) - 1)) << 24) | (emission & 0xffffffu);
+// findSubscriptions returns subscriptions in insertion order). Log positions are 64-bit and never rebased
+// (LogEntryDescriptor.java:28-121): the key holds the position relative to the outbox's base (Outbox.pos_base), so
+// the fields stay exact for any absolute position; OB_REL_BITS / OB_EMIT_BITS bound what one outbox can hold
+// between two takes (outbox_write refuses the rest instead of wrapping).
+constexpr int OB_REL_BITS = 34, OB_EMIT_BITS = 24;
+__device__ __forceinline__ uint64_t outbox_key(int32_t target, uint64_t rel, uint32_t emission) {
+  return ((uint64_t)target << (OB_REL_BITS + OB_EMIT_BITS)) | (rel << OB_EMIT_BITS) | emission;
 }
 
 // slots for `cnt` records per lane from one atomic per wave (lanes that reach this point together;
@@ -171,10 +175,14 @@ __device__ __forceinline__ uint32_t var_granules(uint32_t nn, uint32_t nc, uint3
 __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint32_t n) {
   for (uint32_t i = 0; i < n; i++) dst[i] = src[i];
 }
-__device__ __forceinline__ void outbox_write(const Outbox& ob, uint32_t slot, uint32_t var_at, int32_t kind, int32_t target,
+// false (nothing written): the source position or the emission index does not fit the order key -- the caller fails
+// the partition (DE_UNSUPPORTED) rather than ordering the exchange wrongly
+__device__ __forceinline__ bool outbox_write(const Outbox& ob, uint32_t slot, uint32_t var_at, int32_t kind, int32_t target,
                                              int32_t wfp, uint32_t token, int64_t wik, int64_t aik, int64_t spos,
                                              uint16_t elem, const uint8_t* name, uint32_t nn, const uint8_t* ck,
                                              uint32_t nc, const uint8_t* payload, uint32_t np, uint32_t emission) {
+  const uint64_t rel = (uint64_t)(spos - ob.pos_base);
+  if (spos < ob.pos_base || rel >= (1ull << OB_REL_BITS) || emission >= (1u << OB_EMIT_BITS)) return false;
   zb_exchange_rec r;
   r.kind = kind; r.target_partition = target; r.wf_partition = wfp; r.token = token;
   r.workflow_instance_key = wik; r.activity_instance_key = aik; r.source_position = spos;
@@ -187,7 +195,8 @@ __device__ __forceinline__ void outbox_write(const Outbox& ob, uint32_t slot, ui
   copy_bytes(v + nn + nc, payload, np);
   for (uint32_t i = nn + nc + np; i < var_granules(nn, nc, np) * 8; i++) v[i] = 0;
   ob.rec[slot] = r;
-  ob.keys[slot] = outbox_key(target, spos, emission);
+  ob.keys[slot] = outbox_key(target, rel, emission);
+  return true;
 }
 
 }  // namespace zbg

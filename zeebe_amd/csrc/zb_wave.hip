@@ -755,8 +755,10 @@ __global__ void __launch_bounds__(256) k_subscribe(WaveParams P) {
       if (slot >= P.obx.cap || (uint64_t)vat + gran > P.obx.var_cap) { err = DE_LOG_FULL; site = 36; }
       else {
         const int32_t target = subscription_partition(ck, ck_len, P.partition_count);
-        outbox_write(P.obx, slot, vat, ZB_XCHG_OPEN, target, P.partition_id, rself, rec.inst_key, rec.key, pos, rec.elem,
-                     P.pool + el->msg_off, el->msg_len, ck, ck_len, nullptr, 0, 0);
+        if (!outbox_write(P.obx, slot, vat, ZB_XCHG_OPEN, target, P.partition_id, rself, rec.inst_key, rec.key, pos,
+                          rec.elem, P.pool + el->msg_off, el->msg_len, ck, ck_len, nullptr, 0, 0)) {
+          err = DE_UNSUPPORTED; site = 37;
+        }
       }
     }
     if (err) {

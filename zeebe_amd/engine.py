@@ -188,6 +188,7 @@ def lib():
         L.zb_read_instances.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t, szp, u64p]
         L.zb_snapshot.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t, szp]
         L.zb_log_release.argtypes = [vp, ctypes.c_int64]
+        L.zb_log_start.argtypes = [vp, ctypes.c_int64]
         L.zb_compact.argtypes = [vp]
         L.zb_read_memory_stats.argtypes = [vp, ctypes.POINTER(zb_memory_stats)]
         L.zb_restore.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t]
@@ -206,7 +207,7 @@ EXPORTED_SYMBOLS = ["zb_engine_create", "zb_engine_destroy", "zb_last_error", "z
                     "zb_comm_exchange", "zb_submit", "zb_read_instances", "zb_snapshot", "zb_restore",
                     "zb_validate_deployment", "zb_serialize", "zb_drain_copy", "zb_pinned_alloc", "zb_pinned_free",
                     "zb_serialize_frames", "zb_set_request_metadata", "zb_read_source_positions",
-                    "zb_log_release", "zb_compact", "zb_read_memory_stats", "zb_submit_messages", "zb_set_clock",
+                    "zb_log_release", "zb_log_start", "zb_compact", "zb_read_memory_stats", "zb_submit_messages", "zb_set_clock",
                     "zb_expire_messages", "zb_rccl_library", "zb_upload_staged"]
 
 
@@ -421,6 +422,10 @@ class Engine:
     def release(self, position: int):
         """zb_log_release: records below position were appended by the caller; they leave the device window."""
         self._check(self._L.zb_log_release(self._h, position))
+
+    def log_start(self, position: int):
+        """zb_log_start: the (idle, fully released) partition's log continues at position."""
+        self._check(self._L.zb_log_start(self._h, position))
 
     def compact(self):
         """zb_compact: drop dead element-instance rows, unreachable payload blobs, removed messages / job states."""
