@@ -19,6 +19,7 @@ from zeebe_amd import records as R, workloads
 pytestmark = pytest.mark.gpu
 
 STATIC = 1 << 20  # the engine's static arena region (harness payloads, {}); never compacted
+ROW_BYTES = 64 + 48  # an element instance in a snapshot: its row (zb_device.hpp Row) + its scope state (RowAux)
 
 
 def _compare_tick(o, e, start):
@@ -140,13 +141,13 @@ def test_many_ticks_through_small_capacities():
     assert m["arena_total"] >= 10 * (arena - STATIC), m
     assert m["compactions"] > 0
     assert d.e.counters()["completed"] > 0 and d.e.counters()["canceled"] > 0
-    # the snapshot holds live state only: live rows (96 B) + reachable blobs, not what was ever allocated
+    # the snapshot holds live state only: live rows (ROW_BYTES) + reachable blobs, not what was ever allocated
     snap = d.e.snapshot()
     live_rows = len(d.e.instances())
     m2 = d.e.memory_stats()
     assert m2["rows_allocated"] == live_rows
-    assert len(snap) <= 4096 + 96 * live_rows + (m2["arena_used"] - STATIC), (len(snap), live_rows, m2)
-    assert len(snap) * 10 < m["arena_total"] + 96 * m["rows_total"]
+    assert len(snap) <= 4096 + ROW_BYTES * live_rows + (m2["arena_used"] - STATIC), (len(snap), live_rows, m2)
+    assert len(snap) * 10 < m["arena_total"] + ROW_BYTES * m["rows_total"]
     # restore into a fresh engine and continue: the same records as the original run
     e2 = _engine(external_jobs=True, log_capacity=log_cap, row_capacity=row_cap, arena_bytes=arena)
     e2.deploy(c1["workflow"]().to_xml(), 100, 1)

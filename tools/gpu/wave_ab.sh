@@ -12,7 +12,7 @@ for rep in $(seq ${REPS:-2}); do
     cp $l zeebe_amd/libzbgpu.so
     t=$(basename $l .so)
     for cfg in ${CFGS:-c2 c4}; do
-      timeout -k 10 200 python3 -u tools/gpu/wave_exp.py $cfg 1000000 0 > $O/$t.$cfg.$rep.txt 2>&1 || { echo "$t $cfg failed"; tail -5 $O/$t.$cfg.$rep.txt; cp $O/.head.so zeebe_amd/libzbgpu.so; exit 1; }
+      ZB_AB_LIBRARY=1 timeout -k 10 200 python3 -u tools/gpu/wave_exp.py $cfg 1000000 0 > $O/$t.$cfg.$rep.txt 2>&1 || { echo "$t $cfg failed"; tail -5 $O/$t.$cfg.$rep.txt; cp $O/.head.so zeebe_amd/libzbgpu.so; exit 1; }
       echo "$t: $(cat $O/$t.$cfg.$rep.txt | tail -1)"
     done
   done

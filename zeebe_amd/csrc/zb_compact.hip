@@ -41,12 +41,26 @@ __global__ void __launch_bounds__(256) k_row_gather(CompactParams P) {
     if (m.state == 0) continue;
     const uint32_t n = P.row_new[r];
     if (m.parent != NO_ROW) m.parent = (m.parent < P.rows && P.rmeta[m.parent].state != 0) ? P.row_new[m.parent] : NO_ROW;
-    P.m2[n] = m;
-    P.k2[n] = P.rkeys[r];
+    Row x;
+    x.m = m;
+    x.k = P.rkeys[r];
+    x.c_head = x.c_next = NO_ROW;  // (k_row_relink)
+    x.pad[0] = x.pad[1] = 0;
+    P.r2[n] = x;
     RowAux a = P.raux[r];
     a.first = NO_ROW;
     a.mark = 0;
     P.a2[n] = a;
+  }
+}
+
+// the children lists of the compacted rows [0, live_rows): every row with a parent links itself into it
+__global__ void __launch_bounds__(256) k_row_relink(CompactParams P) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < P.live_rows; r += stride) {
+    const uint32_t p = P.row_arr[r].m.parent;
+    if (p != NO_ROW && ZB_DCHECK(p < P.live_rows, "row %llu parent %u\n", (unsigned long long)r, p))
+      P.row_arr[r].c_next = atomicExch(&P.row_arr[p].c_head, (uint32_t)r);
   }
 }
 
@@ -206,6 +220,9 @@ void launch_row_flags(const CompactParams& p, hipStream_t s) {
 }
 void launch_row_gather(const CompactParams& p, hipStream_t s) {
   if (p.rows) hipLaunchKernelGGL(k_row_gather, dim3(grid_for(p.rows)), dim3(256), 0, s, p);
+}
+void launch_row_relink(const CompactParams& p, hipStream_t s) {
+  if (p.live_rows) hipLaunchKernelGGL(k_row_relink, dim3(grid_for(p.live_rows)), dim3(256), 0, s, p);
 }
 void launch_mark(const CompactParams& p, hipStream_t s) {
   uint64_t n = p.live_rows;

@@ -121,8 +121,7 @@ struct zb_engine {
   uint32_t segpool_len = 0;
   bool seg_ok = false;          // the runs fit the fast passes' LDS
   uint32_t* vlen_bad = nullptr; // ZB_CFG_VLEN_CHECK: the size pass checks every known length (device flag)
-  RowMeta* rmeta = nullptr;
-  RowKeys* rkeys = nullptr;
+  Row* rows = nullptr;           // element-instance rows (one 64-byte line each)
   uint8_t* arena = nullptr;
   WaveHdr* hdr = nullptr;
   uint32_t* derr = nullptr;
@@ -282,7 +281,6 @@ struct zb_engine {
 
   // scope-wide row state (RowAux), first-live-child requests, wave epoch
   RowAux* raux = nullptr;
-  uint32_t* need_children = nullptr;
   int64_t epoch = 1;
   bool has_parallel = false;
   bool term = false;               // a CANCEL was injected: terminations may run until quiescence
@@ -499,8 +497,9 @@ WaveParams wave_params(zb_engine* e) {
   p.links = e->links;
   p.srcd = e->srcd;
   p.vlen = e->vlen;
-  p.rmeta = e->rmeta;
-  p.rkeys = e->rkeys;
+  p.rmeta = RowMetaArr{e->rows};
+  p.rkeys = RowKeysArr{e->rows};
+  p.rows = e->rows;
   p.arena = e->arena;
   p.elems = e->d_elems.p;
   p.wfs = e->d_wfs.p;
@@ -553,7 +552,6 @@ WaveParams wave_params(zb_engine* e) {
   p.jobs = e->jobs;
   p.term = e->term ? 1 : 0;
   p.epoch = e->epoch;
-  p.need_children = e->need_children;
   p.conflicts = e->conf_active ? 1 : 0;
   p.conf_keys = e->d_conf_keys.p;
   p.conf_first = e->conf_first;
@@ -669,8 +667,9 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   p.srcd = e->srcd;
   p.vlen = e->vlen;
   p.arena = e->arena;
-  p.rmeta = e->rmeta;
-  p.rkeys = e->rkeys;
+  p.rmeta = RowMetaArr{e->rows};
+  p.rkeys = RowKeysArr{e->rows};
+  p.rows = e->rows;
   p.elems = e->d_elems.p;
   p.cond_flows = e->d_cond.p;
   p.code = e->d_code.p;
@@ -1051,7 +1050,7 @@ int reserve_compaction(zb_engine* e) {
 // reallocates it a few times, not at every compaction. (Reserved for the whole arena at creation, it doubled a large
 // partition's device memory.)
 int reserve_gather(zb_engine* e) {
-  const uint64_t row_bytes = sizeof(RowMeta) + sizeof(RowKeys) + sizeof(RowAux);
+  const uint64_t row_bytes = sizeof(Row) + sizeof(RowAux);
   const uint64_t full = std::max<uint64_t>(e->cfg.row_capacity * row_bytes, e->cfg.arena_bytes - STATIC_ARENA_BYTES);
   const uint64_t need = std::max<uint64_t>((uint64_t)e->host_hdr.rows_next * row_bytes,
                                            (uint64_t)e->host_hdr.arena_next - STATIC_ARENA_BYTES);
@@ -1068,7 +1067,7 @@ int reserve_gather(zb_engine* e) {
 
 CompactParams compact_params(zb_engine* e) {
   CompactParams c{};
-  c.rmeta = e->rmeta; c.rkeys = e->rkeys; c.raux = e->raux;
+  c.rmeta = RowMetaArr{e->rows}; c.rkeys = RowKeysArr{e->rows}; c.row_arr = e->rows; c.raux = e->raux;
   c.rows = (uint64_t)e->host_hdr.rows_next;
   c.live_rows = c.rows;
   c.row_flag = e->c_flag; c.row_new = e->c_new;
@@ -1107,18 +1106,18 @@ int compact_state(zb_engine* e) {
     launch_row_flags(c, e->stream);
     rc = scan_u32(e, e->c_flag, e->c_new, rows, &live);
     if (rc != ZB_OK) return rc;
-    const uint64_t row_bytes = sizeof(RowMeta) + sizeof(RowKeys) + sizeof(RowAux);
+    const uint64_t row_bytes = sizeof(Row) + sizeof(RowAux);
     rc = grow(e, &e->c_scratch, &e->c_scratch_cap, std::max<uint64_t>(live, 1) * row_bytes);
     if (rc != ZB_OK) return rc;
     c.row_new = e->c_new;
-    c.m2 = (RowMeta*)e->c_scratch;
-    c.k2 = (RowKeys*)(e->c_scratch + live * sizeof(RowMeta));
-    c.a2 = (RowAux*)(e->c_scratch + live * (sizeof(RowMeta) + sizeof(RowKeys)));
+    c.r2 = (Row*)e->c_scratch;
+    c.a2 = (RowAux*)(e->c_scratch + live * sizeof(Row));
     launch_row_gather(c, e->stream);
     if (live) {
-      HIPCHECK(e, hipMemcpyAsync(e->rmeta, c.m2, live * sizeof(RowMeta), hipMemcpyDeviceToDevice, e->stream));
-      HIPCHECK(e, hipMemcpyAsync(e->rkeys, c.k2, live * sizeof(RowKeys), hipMemcpyDeviceToDevice, e->stream));
+      HIPCHECK(e, hipMemcpyAsync(e->rows, c.r2, live * sizeof(Row), hipMemcpyDeviceToDevice, e->stream));
       HIPCHECK(e, hipMemcpyAsync(e->raux, c.a2, live * sizeof(RowAux), hipMemcpyDeviceToDevice, e->stream));
+      c.live_rows = live;  // the children lists of the renamed rows, relinked
+      launch_row_relink(c, e->stream);
     }
   }
   e->host_hdr.rows_next = (int64_t)live;
@@ -1321,8 +1320,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
         hipMalloc(&e->jobs.state, slots) != hipSuccess || hipMalloc(&e->jobs.tombs, sizeof(uint32_t)) != hipSuccess)
       return cleanup(ZB_ENOMEM);
   }
-  if (hipMalloc(&e->rmeta, e->cfg.row_capacity * sizeof(RowMeta)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipMalloc(&e->rkeys, e->cfg.row_capacity * sizeof(RowKeys)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->rows, e->cfg.row_capacity * sizeof(Row)) != hipSuccess) return cleanup(ZB_ENOMEM);
   // (+ ARENA_SLACK: the drain's encoders load a payload document's first words without a bounds check)
   if (hipMalloc(&e->arena, e->cfg.arena_bytes + ARENA_SLACK) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->hdr, 2 * sizeof(WaveHdr)) != hipSuccess) return cleanup(ZB_ENOMEM);
@@ -1364,8 +1362,6 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->phase, 8 * sizeof(unsigned long long)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMemset(e->phase, 0, 8 * sizeof(unsigned long long)) != hipSuccess) return cleanup(ZB_EDEVICE);
 #endif
-  if (hipMalloc(&e->need_children, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipMemset(e->need_children, 0, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_EDEVICE);
   e->ev.resize(EV_PER_WAVE * WAVES_PER_SYNC_MAX);
   for (auto& x : e->ev)
     if (hipEventCreate(&x) != hipSuccess) return cleanup(ZB_EDEVICE);
@@ -1387,11 +1383,11 @@ void zb_engine_destroy(zb_engine* e) {
     if (x) (void)hipEventDestroy(x);
   void* ps[] = {e->vlen_mem, e->vlen_bad, e->jobs.keys, e->jobs.state, e->jobs.tombs, e->c_flag, e->c_new, e->c_tmp,
                 e->c_scratch, e->c_bits, e->c_pop, e->c_off, e->c_count, e->x_keys, e->x_pos, e->x_keys2, e->x_pos2,
-                e->sort_tmp, e->d_spread, e->mapres, e->map_ws, e->log_mem, e->links_mem, e->srcd_mem, e->rmeta, e->rkeys, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
+                e->sort_tmp, e->d_spread, e->mapres, e->map_ws, e->log_mem, e->links_mem, e->srcd_mem, e->rows, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
                 e->merge_jobs, e->merge_slow, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_clen, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
-                e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->need_children, e->look_keys, e->look_idx,
+                e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->look_keys, e->look_idx,
                 e->conf_first, e->xslab, e->xlocks, e->phase};
   for (void* p : ps)
     if (p) (void)hipFree(p);
@@ -2315,7 +2311,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
                           e->look_idx, m, "lookup", true);
       if (rc != ZB_OK) return rc;
       ResolveParams rp{};
-      rp.rmeta = e->rmeta; rp.rkeys = e->rkeys; rp.rows = (uint64_t)e->host_hdr.rows_next;
+      rp.rmeta = RowMetaArr{e->rows}; rp.rkeys = RowKeysArr{e->rows}; rp.rows = (uint64_t)e->host_hdr.rows_next;
       rp.keys = e->look_keys; rp.pos = e->look_idx; rp.pos_base = ip.log_base; rp.n = (int64_t)m;
       rp.links = e->links;
       launch_resolve(rp, e->stream);
@@ -2390,10 +2386,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
         HIPCHECK(e, hipMemsetAsync(p.conf_split, 0x7f, sizeof(int64_t), e->stream));
         launch_conflict(p, e->stream);
       }
-      if (p.has_parallel || p.term) {  // scope-wide counters / first-child requests of the chunk
-        launch_pre(p, e->stream);
-        if (p.term) launch_children(p, e->stream);
-      }
+      if (p.has_parallel || p.term) launch_pre(p, e->stream);  // scope-wide counters / first live children
       if (e->has_io) launch_map(p, e->stream);  // io-mapping results of the chunk's records
       if (e->wave_fused_grid) {  // process + scan + emit in one launch (k_wave)
         // tile aggregates carry an 8-bit tag: when it wraps, no granule may hold a tag of an earlier launch
@@ -3219,7 +3212,7 @@ int deliver(zb_engine* e, int kind, const uint8_t* buf, const std::vector<uint64
     int rc = sort_pairs(e, e->x_keys, e->x_keys2, e->x_pos, e->x_pos2, n, "inbox");
     if (rc != ZB_OK) return rc;
     ResolveParams rp{};
-    rp.rmeta = e->rmeta; rp.rkeys = e->rkeys; rp.rows = (uint64_t)e->host_hdr.rows_next;
+    rp.rmeta = RowMetaArr{e->rows}; rp.rkeys = RowKeysArr{e->rows}; rp.rows = (uint64_t)e->host_hdr.rows_next;
     rp.keys = e->x_keys2; rp.pos = e->x_pos2; rp.pos_base = 0; rp.n = (int64_t)n;
     rp.links = e->links;
     launch_resolve(rp, e->stream);
@@ -3922,7 +3915,7 @@ int zb_read_instances(zb_engine* e, uint8_t* buf, size_t cap, size_t* len, uint6
         hipMalloc(&d_rows, rows * 4) != hipSuccess) { rc = fail(e, ZB_ENOMEM, "read_instances buffers"); break; }
     if (hipMemsetAsync(d_count, 0, 4, e->stream) != hipSuccess) { rc = ZB_EDEVICE; break; }
     LiveParams lp{};
-    lp.rmeta = e->rmeta; lp.rkeys = e->rkeys; lp.rows = rows; lp.count = d_count; lp.cap = rows;
+    lp.rmeta = RowMetaArr{e->rows}; lp.rkeys = RowKeysArr{e->rows}; lp.rows = rows; lp.count = d_count; lp.cap = rows;
     lp.keys = d_keys; lp.row_of = d_rows;
     launch_live_rows(lp, e->stream);
     uint32_t live = 0;
@@ -4019,7 +4012,7 @@ uint64_t model_hash(const zb_engine* e) {  // FNV-1a over the deployed tables
 }
 
 size_t snap_bytes(const SnapHead& h) {
-  return sizeof(h) + h.rows * (sizeof(RowMeta) + sizeof(RowKeys) + sizeof(RowAux)) + h.arena_dyn +
+  return sizeof(h) + h.rows * (sizeof(Row) + sizeof(RowAux)) + h.arena_dyn +
          h.jobs * (sizeof(int64_t) + 1) + h.sub_count * sizeof(SubEntry) + h.msg_count * sizeof(MsgEntry);
 }
 }  // namespace
@@ -4069,7 +4062,7 @@ int zb_snapshot(zb_engine* e, uint8_t* buf, size_t cap, size_t* len) {
     o += n;
     return true;
   };
-  bool ok = get(e->rmeta, h.rows * sizeof(RowMeta)) && get(e->rkeys, h.rows * sizeof(RowKeys)) &&
+  bool ok = get(e->rows, h.rows * sizeof(Row)) &&
             get(e->raux, h.rows * sizeof(RowAux)) && get(e->arena + STATIC_ARENA_BYTES, h.arena_dyn);
   if (!ok) return fail(e, ZB_EDEVICE, "snapshot copy");
   if (h.jobs) {
@@ -4110,7 +4103,7 @@ int zb_restore(zb_engine* e, const uint8_t* buf, size_t len) {
     o += n;
     return true;
   };
-  bool ok = put(e->rmeta, h.rows * sizeof(RowMeta)) && put(e->rkeys, h.rows * sizeof(RowKeys)) &&
+  bool ok = put(e->rows, h.rows * sizeof(Row)) &&
             put(e->raux, h.rows * sizeof(RowAux)) && put(e->arena + STATIC_ARENA_BYTES, h.arena_dyn);
   if (!ok) return fail(e, ZB_EDEVICE, "restore copy");
   if (h.jobs) {

@@ -904,6 +904,17 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
 #pragma unroll
     for (int k = 0; k < TR; k++)
       if ((live >> k) & 1) gid[k] = (uint32_t)(r0 + n++);
+    // the children lists (Row.c_head / c_next): every row of the instance is this thread's, parents included
+    u32x4 head = NO_ROW, next = NO_ROW;
+#pragma unroll
+    for (int k = 0; k < TR; k++) {
+      const int par = (int)(I.rmeta[k] >> 24);
+      if (((live >> k) & 1) && par != LN) {
+#pragma unroll
+        for (int q = 0; q < TR; q++)
+          if (q == par) { next[k] = head[q]; head[q] = gid[k]; }
+      }
+    }
 #pragma unroll
     for (int k = 0; k < TR; k++) {
       if (!((live >> k) & 1)) continue;
@@ -917,10 +928,15 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
       m.state = (uint8_t)(meta >> 16);
       m.flags = 0;
       m.nchild = I.rnch[k];
-      P.rmeta[gid[k]] = m;
       const uint32_t jk = I.rjob[k];
-      P.rkeys[gid[k]] = RowKeys{wf_key(P, I.rkey[k]), wf_key(P, I.scope_of(k)), wf_key(P, I.inst_key),
-                                jk == JOB_ZERO ? 0 : job_key(P, jk)};
+      Row x;
+      x.m = m;
+      x.k = RowKeys{wf_key(P, I.rkey[k]), wf_key(P, I.scope_of(k)), wf_key(P, I.inst_key),
+                    jk == JOB_ZERO ? 0 : job_key(P, jk)};
+      x.c_head = head[k];
+      x.c_next = next[k];
+      x.pad[0] = x.pad[1] = 0;
+      P.rows[gid[k]] = x;
     }
   }
   // ---- statistics

@@ -940,7 +940,6 @@ __global__ void __launch_bounds__(WG) k_pre(WaveParams P) {
   const WaveHdr* hin = P.hdr + (P.wave & 1);
   const Chunk c = wave_chunk(P, hin);
   const int64_t stride = (int64_t)gridDim.x * WG;
-  bool need = false;
   for (int64_t r = c.begin + (int64_t)blockIdx.x * WG + threadIdx.x; r < c.end; r += stride) {
     const zb_rec rec = P.log[r];
     if (kind_vt(rec.kind) != ZB_VT_WORKFLOW_INSTANCE || kind_rt(rec.kind) != ZB_RT_EVENT) continue;
@@ -969,7 +968,10 @@ __global__ void __launch_bounds__(WG) k_pre(WaveParams P) {
       }
     }
     if (P.term) {
-      // scopes that look up their first live child this chunk (k_children answers)
+      // the first live child of a scope being terminated (TerminateContainedElementsHandler :31-53 children.get(0)):
+      // the smallest live row of its children list (rows are allocated in insertion order). Every record of the chunk
+      // that asks for a scope's first child computes the same row from the state before the chunk (k_process has not
+      // run), so the stores agree.
       uint32_t row = NO_ROW;
       if (it == WI_ELEMENT_TERMINATING && step == ST_TERMINATE_CONTAINED_INSTANCES && rself != NO_ROW &&
           P.rmeta[rself].state != 0 && P.rmeta[rself].nchild > 0)
@@ -978,26 +980,17 @@ __global__ void __launch_bounds__(WG) k_pre(WaveParams P) {
                P.rmeta[rscope].nchild > 0)
         row = rscope;
       if (row != NO_ROW) {
-        P.raux[row].first = NO_ROW;
+        uint32_t first = NO_ROW;
+        uint64_t n = 0;
+        for (uint32_t ch = P.rows[row].c_head; ch != NO_ROW && n < P.row_cap; ch = P.rows[ch].c_next, n++) {
+          if (!ZB_DCHECK(ch < P.row_cap, "row %u child %u\n", row, ch)) break;
+          const RowMeta cm = P.rmeta[ch];
+          if (cm.state != 0 && cm.parent == row && ch < first) first = ch;
+        }
+        P.raux[row].first = first;
         P.raux[row].mark = P.epoch;
-        need = true;
       }
     }
-  }
-  if (need) atomicOr(P.need_children, 1u);
-}
-
-// First live child (min row index = first in insertion order, ElementInstance.children.get(0)) of every
-// scope k_pre marked: one pass over the allocated rows, only in chunks of a cancellation that need it.
-__global__ void __launch_bounds__(256) k_children(WaveParams P) {
-  if (*(volatile uint32_t*)P.need_children == 0) return;
-  uint64_t rows = (uint64_t)P.hdr[P.wave & 1].rows_next;
-  if (!ZB_DCHECK(rows <= P.row_cap, "rows_next %llu\n", (unsigned long long)rows)) rows = P.row_cap;
-  for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < rows; r += (uint64_t)gridDim.x * 256) {
-    const RowMeta m = P.rmeta[r];
-    if (m.state == 0 || m.parent == NO_ROW) continue;
-    if (!ZB_DCHECK(m.parent < P.row_cap, "row %llu parent %u\n", (unsigned long long)r, m.parent)) continue;
-    if (P.raux[m.parent].mark == P.epoch) atomicMin(&P.raux[m.parent].first, (uint32_t)r);
   }
 }
 
@@ -1078,7 +1071,6 @@ __global__ void __launch_bounds__(SCAN_WG) k_scan(WaveParams P) {
       if (err) atomicOr(P.err, err);
     }
     *hout = h;
-    if (P.need_children) *P.need_children = 0;  // k_pre of the next chunk sets it again
     P.merge_count[P.wave & 1] = c.n > 0 ? (uint32_t)tot[5] : 0;
     if (P.sub_count) clear_sub_counts(P);  // the next wave's subscribe list
     P.cond_count[P.wave & 1] = c.n > 0 ? (uint32_t)tot[6] : 0;
@@ -1146,19 +1138,21 @@ __device__ __forceinline__ void emit_item(const WaveParams& P, const Chunk& c, i
       if (row >= P.row_cap) { err |= DE_ROWS_FULL; s.rself = NO_ROW; }
       else {
         s.rself = (uint32_t)row;
-        RowMeta m;
+        Row x;  // (the whole line in one go)
+        x.c_head = NO_ROW; x.c_next = NO_ROW; x.pad[0] = x.pad[1] = 0;
         if (s.flags & SF_ROW_INIT) {
-          m.payload = s.d.payload; m.parent = s.rscope; m.elem = s.d.elem; m.state = WI_ELEMENT_READY;
-          m.flags = 0; m.nchild = 0;
-          P.rmeta[row] = m;
-          P.rkeys[row] = RowKeys{s.d.key, s.d.scope_key, s.d.inst_key, 0};
+          x.m.payload = s.d.payload; x.m.parent = s.rscope; x.m.elem = s.d.elem; x.m.state = WI_ELEMENT_READY;
+          x.m.flags = 0; x.m.nchild = 0;
+          x.k = RowKeys{s.d.key, s.d.scope_key, s.d.inst_key, 0};
+          // ElementInstance.children.add: into the flow scope's list (read from the next wave on)
+          if (s.rscope != NO_ROW) x.c_next = atomicExch(&P.rows[s.rscope].c_head, (uint32_t)row);
         } else {
           // a CREATE's row: the instance enters the index when its CREATED event is processed (next wave), and
-          // until then the row must read as free -- k_children scans every allocated row, and this one still holds
-          // whatever the memory held before (a compacted-away row, or another engine's data)
-          m.payload = 0; m.parent = NO_ROW; m.elem = NO_ELEM; m.state = 0; m.flags = 0; m.nchild = 0;
-          P.rmeta[row] = m;
+          // until then the row reads as free (state 0, no parent, no children), whatever the memory held before
+          x.m.payload = 0; x.m.parent = NO_ROW; x.m.elem = NO_ELEM; x.m.state = 0; x.m.flags = 0; x.m.nchild = 0;
+          x.k = RowKeys{0, 0, 0, 0};
         }
+        P.rows[row] = x;
       }
     }
     if (out_rec >= P.log_cap) { err |= DE_LOG_FULL; }
@@ -1348,7 +1342,6 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
   if (c.n <= 0) {  // nothing in this wave (the batch outran quiescence): carry the header forward
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       *hout = *hin;
-      if (P.need_children) *P.need_children = 0;
       P.merge_count[P.wave & 1] = 0;
       P.cond_count[P.wave & 1] = 0;
       if (P.sub_count) clear_sub_counts(P);
@@ -1583,8 +1576,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
           if (t6 > P.job_cap || t7 > P.job_cap) err |= DE_LOG_FULL;
           if (err) atomicOr(P.err, err);
           *hout = h;
-          if (P.need_children) *P.need_children = 0;  // k_pre of the next chunk sets it again
-          P.merge_count[P.wave & 1] = (uint32_t)t6;
+                P.merge_count[P.wave & 1] = (uint32_t)t6;
           P.cond_count[P.wave & 1] = (uint32_t)t7;
           if (P.sub_count) clear_sub_counts(P);  // the next wave's subscribe list
         }
@@ -1672,10 +1664,6 @@ int wave_resident_per_cu() {
 
 void launch_pre(const WaveParams& p, hipStream_t stream) {
   hipLaunchKernelGGL(k_pre, dim3(p.grid), dim3(WG), 0, stream, p);
-}
-void launch_children(const WaveParams& p, hipStream_t stream) {
-  // (one workgroup per CU: in most waves of a tick with a cancellation no scope asks, and the launch exits at once)
-  hipLaunchKernelGGL(k_children, dim3(256), dim3(256), 0, stream, p);
 }
 void launch_process(const WaveParams& p, hipStream_t stream) {
   hipLaunchKernelGGL(k_process, dim3(p.grid), dim3(WG), 0, stream, p);
