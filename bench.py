@@ -562,10 +562,51 @@ def extras(a, barrier):
     # (8 ticks: the partition compacts about every sixth tick, and the line's average carries its share)
     t = bench_steady.run_steady(a, 0, 1, 0, barrier, 8, 1, live=1_000_000)
     out["c2_steady"] = steady_line(t, 8, 1_000_000)
+    out["c1_exact_tree"] = run_exact_tree(a)
     t = run_workload("c4", 1_000_000, a, 0, 1, 0, barrier, 3, 1)
     out["c4"] = {"value": t["transitions"] / t["elapsed"], "ms_per_step": t["elapsed"] * 1e3 / 3,
                  "stepping_ms": t["step_s"] * 1e3 / 3, "drain_ms": t["drain_s"] * 1e3 / 3,
                  "roofline": roofline(t, 3, "c4", 1_000_000), "workload": t["desc"]}
+    return out
+
+
+def run_exact_tree(a, n=1_000_000, steps=3):
+    """The exact payload tree under load (zb_xmerge.hpp): C1 (start -> service task -> end), n instances whose job
+    completion payload has a duplicate key, so every default output merge is one the structural merge refuses and the
+    reference's own tree takes (MsgPackDocumentIndexer keeps the first position and the last value). Against the same
+    tick with a flat completion payload; both on the trajectory path (the default) and on the general wave pipeline."""
+    from zeebe_amd import workloads
+
+    out = {}
+    dup = b"\x82" + workloads.mp_str("step") + workloads.mp_int(1) + workloads.mp_str("step") + workloads.mp_int(2)
+    flat = b"\x81" + workloads.mp_str("step") + workloads.mp_int(1)
+    for wave_only in (False, True):
+        for name, jp in (("flat", flat), ("exact", dup)):
+            import copy
+
+            b = copy.copy(a)
+            b.wave_only = wave_only
+            xml, pid, blob, offs, _, desc = workload("c1", n, 0)
+            eng = make_engine("c1", n, b, 0, 1, 0)
+            eng.deploy(xml, 100, 1)
+            eng.set_job_payload(100, "t1", jp)
+            eng.create_packed(pid, blob, offs)
+            ms = []
+            for it in range(steps + 1):
+                eng.reset(keep_staged=True)
+                t0 = time.perf_counter()
+                st = eng.step()
+                t1 = time.perf_counter()
+                assert st["quiescent"] and st["merges"] == n, st
+                if it:
+                    ms.append((t1 - t0) * 1e3)
+            eng.close()
+            out["%s_%s" % ("wave" if wave_only else "traj", name)] = sum(ms) / len(ms)
+    for p in ("traj", "wave"):
+        out["%s_ratio" % p] = out["%s_exact" % p] / out["%s_flat" % p]
+    out["workload"] = ("C1, %d instances per tick, every job completion payload with a duplicate key (the exact tree "
+                       "for each of the %d default output merges) vs a flat completion payload; stepping ms per tick, "
+                       "trajectory path and general wave pipeline" % (n, n))
     return out
 
 

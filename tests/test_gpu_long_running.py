@@ -19,7 +19,7 @@ from zeebe_amd import records as R, workloads
 pytestmark = pytest.mark.gpu
 
 STATIC = 1 << 20  # the engine's static arena region (harness payloads, {}); never compacted
-ROW_BYTES = 64 + 48  # an element instance in a snapshot: its row (zb_device.hpp Row) + its scope state (RowAux)
+ROW_BYTES = 16 + 32 + 48  # an element instance in a snapshot: RowMeta + RowKeys + RowAux (zb_device.hpp)
 
 
 def _compare_tick(o, e, start):

@@ -41,12 +41,8 @@ __global__ void __launch_bounds__(256) k_row_gather(CompactParams P) {
     if (m.state == 0) continue;
     const uint32_t n = P.row_new[r];
     if (m.parent != NO_ROW) m.parent = (m.parent < P.rows && P.rmeta[m.parent].state != 0) ? P.row_new[m.parent] : NO_ROW;
-    Row x;
-    x.m = m;
-    x.k = P.rkeys[r];
-    x.c_head = x.c_next = NO_ROW;  // (k_row_relink)
-    x.pad[0] = x.pad[1] = 0;
-    P.r2[n] = x;
+    P.m2[n] = m;
+    P.k2[n] = P.rkeys[r];  // (links: k_row_relink)
     RowAux a = P.raux[r];
     a.first = NO_ROW;
     a.mark = 0;
@@ -58,9 +54,9 @@ __global__ void __launch_bounds__(256) k_row_gather(CompactParams P) {
 __global__ void __launch_bounds__(256) k_row_relink(CompactParams P) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x; r < P.live_rows; r += stride) {
-    const uint32_t p = P.row_arr[r].m.parent;
+    const uint32_t p = P.rmeta[r].parent;
     if (p != NO_ROW && ZB_DCHECK(p < P.live_rows, "row %llu parent %u\n", (unsigned long long)r, p))
-      P.row_arr[r].c_next = atomicExch(&P.row_arr[p].c_head, (uint32_t)r);
+      P.rlink[r].c_next = atomicExch(&P.rlink[p].c_head, (uint32_t)r);
   }
 }
 
@@ -76,15 +72,19 @@ __device__ __forceinline__ void mark_granules(const CompactParams& P, uint64_t g
   }
 }
 
+// a byte range of an allocated blob: in [static, arena_next) or in the staged documents' [arena_top, arena_end)
+__device__ __forceinline__ bool arena_span(const CompactParams& P, uint64_t b0, uint64_t b1) {
+  return (b0 >= P.static_refs * 8 && b1 <= P.arena_next) || (b0 >= P.arena_top && b1 <= P.arena_end);
+}
 // mark `blobs` consecutive blobs from ref (refs below the static region are never moved). A blob is
-// [u32 len][len bytes] padded to 8; one whose length runs past the allocated bytes (arena_next) -- a ref that does
-// not point at a blob header -- marks nothing and flags the partition (the bitmap covers [static, arena_next) only)
+// [u32 len][len bytes] padded to 8; one whose length runs past its region -- a ref that does not point at a blob
+// header -- marks nothing and flags the partition (the bitmap covers the allocated regions only)
 __device__ __forceinline__ void mark_ref(const CompactParams& P, uint32_t ref, int blobs) {
   for (int k = 0; k < blobs; k++) {
-    if ((uint64_t)ref < P.static_refs || (uint64_t)ref * 8 >= P.arena_next) return;
+    if (!arena_span(P, (uint64_t)ref * 8, (uint64_t)ref * 8 + 8)) return;
     const uint32_t len = *(const uint32_t*)(P.arena + (uint64_t)ref * 8);
     const uint64_t n = (4 + (uint64_t)len + 7) >> 3;
-    if (((uint64_t)ref + n) * 8 > P.arena_next) {
+    if (!arena_span(P, (uint64_t)ref * 8, ((uint64_t)ref + n) * 8)) {
       atomicOr(P.err, (uint32_t)DE_CORRUPT);
       return;
     }
@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(256) k_word_pop(CompactParams P) {
 // a ref's position after compaction: the static region stays, a dynamic granule goes to its rank among the
 // marked ones
 __device__ __forceinline__ uint32_t renamed(const CompactParams& P, uint32_t ref) {
-  if ((uint64_t)ref < P.static_refs || (uint64_t)ref * 8 >= P.arena_next) return ref;
+  if (!arena_span(P, (uint64_t)ref * 8, (uint64_t)ref * 8 + 8)) return ref;
   const uint64_t g = (uint64_t)ref - P.static_refs;
   const uint64_t w = g >> 6, b = g & 63;
   const uint64_t below = b ? (P.bits[w] & ((1ull << b) - 1)) : 0;

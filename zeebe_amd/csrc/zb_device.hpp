@@ -225,9 +225,11 @@ struct WaveHdr {
 static_assert(sizeof(WaveHdr) == 128, "WaveHdr is 128 bytes");
 static_assert(sizeof(zb_record_header) == 24, "zb_record_header is 24 bytes (the drain writes one per record)");
 
-// An element instance (ElementInstance.java:30-111) is one 64-byte row, one cache line: its state (RowMeta), its keys
-// (RowKeys) and its place among its flow scope's children. A wave that touches an instance reads one line for all of
-// it (the separate 16 B / 32 B arrays of earlier rounds cost two lines per touch, three with RowAux).
+// An element instance (ElementInstance.java:30-111) is a row of three planes, each its own array indexed by row: its
+// state (RowMeta, 16 B), its keys (RowKeys, 32 B) and its place among its flow scope's children (RowLink, 8 B). The
+// wave pipeline's record processing reads the state of the instances it steps, which are mostly consecutive rows:
+// 16-byte entries put eight of them in a 128-byte line. (One 64-byte line per row, all planes together, measured
+// slower on C2: every touched instance cost a whole line)
 struct RowMeta {
   uint32_t payload;
   uint32_t parent;
@@ -243,28 +245,17 @@ struct RowKeys {
 // before it (any order: concurrent inserts of one wave link in arrival order). TerminateContainedElementsHandler's
 // children.get(0) is the first live child in insertion order, which is the smallest live row index of the list (rows
 // are allocated in insertion order); removed children stay linked (k_pre skips them) until compaction relinks.
-struct Row {
-  RowMeta m;
-  RowKeys k;
+struct RowLink {
   uint32_t c_head, c_next;
-  uint32_t pad[2];
 };
-static_assert(sizeof(Row) == 64, "Row is one 64-byte line");
-// views of the row array as the arrays of its parts (rmeta[i] == rows[i].m)
-struct RowMetaArr {
-  Row* r;
-  __host__ __device__ inline RowMeta& operator[](uint64_t i) const { return r[i].m; }
-};
-struct RowKeysArr {
-  Row* r;
-  __host__ __device__ inline RowKeys& operator[](uint64_t i) const { return r[i].k; }
-};
+static_assert(sizeof(RowMeta) == 16 && sizeof(RowKeys) == 32 && sizeof(RowLink) == 8, "row planes");
+constexpr uint64_t ROW_BYTES = sizeof(RowMeta) + sizeof(RowKeys) + sizeof(RowLink);  // one row, all planes
 // Scope-wide state touched only by scope operations (never on the chain-stepping hot path):
 // EXTENSION token / join counters of a scope with parallel gateways, and the first
 // live child of a scope being terminated (TerminateContainedElementsHandler :31-53 children.get(0)).
 struct RowAux {
   int32_t tokens;              // live tokens of the scope (+ merged arrivals pending their GATEWAY_ACTIVATED)
-  uint32_t first;              // min live child row (k_pre, from Row.c_head), valid when mark == the wave's epoch
+  uint32_t first;              // min live child row (k_pre, from RowLink.c_head), valid when mark == the wave's epoch
   uint32_t join_cnt[JOIN_SLOTS];
   int64_t consume_pos;         // max log position of a CONSUME_TOKEN on this scope (k_pre)
   int64_t join_pos[JOIN_SLOTS];// max log position of an arrival per join slot (k_pre)

@@ -121,7 +121,10 @@ struct zb_engine {
   uint32_t segpool_len = 0;
   bool seg_ok = false;          // the runs fit the fast passes' LDS
   uint32_t* vlen_bad = nullptr; // ZB_CFG_VLEN_CHECK: the size pass checks every known length (device flag)
-  Row* rows = nullptr;           // element-instance rows (one 64-byte line each)
+  uint8_t* row_mem = nullptr;   // element-instance rows: the three planes below, one allocation
+  RowMeta* rmeta = nullptr;     // [row_capacity]
+  RowKeys* rkeys = nullptr;     // [row_capacity]
+  RowLink* rlink = nullptr;     // [row_capacity]
   uint8_t* arena = nullptr;
   WaveHdr* hdr = nullptr;
   uint32_t* derr = nullptr;
@@ -143,6 +146,7 @@ struct zb_engine {
   PubUpload pub_up{};                   // a PUBLISH batch uploaded by zb_upload_publishes, not processed yet
   uint8_t* xslab = nullptr;        // exact payload tree workspaces (zb_xmerge.hpp), with a model that merges / maps
   uint32_t* xlocks = nullptr;
+  uint8_t* xlane = nullptr;        // per-thread exact-tree workspaces (XLANE_COUNT x XLANE_BYTES), with xslab
   uint64_t* sub_jobs = nullptr;    // [job_cap] subscribe steps of a wave (models with message catch events)
   uint64_t job_cap = 0;
   WaveHdr* h_hdr_pinned = nullptr;  // pinned mirror for D2H polling
@@ -172,6 +176,12 @@ struct zb_engine {
   DevVec<zb_rec> d_staged;
   DevVec<uint8_t> d_staged_arena;
   bool staged_uploaded = false;
+  // Staged CREATE documents are uploaded in place, into the top of the arena (k_inject references them, no copy):
+  // the device allocators grow [STATIC, arena_next) up to arena_top, and [arena_top, arena_bytes) holds the
+  // documents of staged batches, newest lowest. Compaction moves the live ones down with everything else.
+  uint64_t arena_top = 0;        // the device allocators' ceiling (arena_bytes when no documents are in place)
+  bool staged_in_place = false;  // the uploaded batch's documents are at [staged_base, staged_top)
+  uint64_t staged_base = 0, staged_top = 0;
   bool staged_pending = false;  // the staged batch has not been injected yet (zb_reset(keep) re-arms it)
   uint16_t staged_elem = NO_ELEM;  // process element of the staged CREATEs ...
   bool staged_uniform = true;      // ... when they all address the same one
@@ -497,9 +507,9 @@ WaveParams wave_params(zb_engine* e) {
   p.links = e->links;
   p.srcd = e->srcd;
   p.vlen = e->vlen;
-  p.rmeta = RowMetaArr{e->rows};
-  p.rkeys = RowKeysArr{e->rows};
-  p.rows = e->rows;
+  p.rmeta = e->rmeta;
+  p.rkeys = e->rkeys;
+  p.rlink = e->rlink;
   p.arena = e->arena;
   p.elems = e->d_elems.p;
   p.wfs = e->d_wfs.p;
@@ -531,6 +541,7 @@ WaveParams wave_params(zb_engine* e) {
   p.merge_slow_count = e->job_counts + 6;
   p.xslab = e->xslab;
   p.xlocks = e->xlocks;
+  p.xlane = e->xlane;
   p.phase = e->phase;
   p.cond_jobs = e->cond_jobs;
   p.cond_count = e->job_counts + 2;
@@ -540,7 +551,7 @@ WaveParams wave_params(zb_engine* e) {
   p.stats = e->dstats;
   p.log_cap = (uint64_t)e->win_base + e->cfg.log_capacity;  // absolute: the window's end
   p.row_cap = e->cfg.row_capacity;
-  p.arena_cap = e->cfg.arena_bytes;
+  p.arena_cap = e->arena_top;  // (the allocators' ceiling: staged documents above it)
   p.wave = e->wave;
   p.obx = outbox(e, ZB_XCHG_OPEN);
   p.partition_id = e->cfg.partition_id;
@@ -667,9 +678,9 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   p.srcd = e->srcd;
   p.vlen = e->vlen;
   p.arena = e->arena;
-  p.rmeta = RowMetaArr{e->rows};
-  p.rkeys = RowKeysArr{e->rows};
-  p.rows = e->rows;
+  p.rmeta = e->rmeta;
+  p.rkeys = e->rkeys;
+  p.rlink = e->rlink;
   p.elems = e->d_elems.p;
   p.cond_flows = e->d_cond.p;
   p.code = e->d_code.p;
@@ -753,8 +764,9 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   p.log_cap = (uint64_t)e->win_base + e->cfg.log_capacity;  // absolute: the window's end
   p.xslab = e->xslab;
   p.xlocks = e->xlocks;
+  p.xlane = e->xlane;
   p.row_cap = e->cfg.row_capacity;
-  p.arena_cap = e->cfg.arena_bytes;
+  p.arena_cap = e->arena_top;  // (the allocators' ceiling: staged documents above it)
   p.defer_ok = (e->tmpl_defer && e->seg_ok && e->d_vsegs.p && e->d_vconst.p && (p.cls || p.uni)) ? 1 : 0;
   hipEvent_t* ev = e->ev.data();
   HIPCHECK(e, hipEventRecord(ev[0], e->stream));
@@ -1050,10 +1062,11 @@ int reserve_compaction(zb_engine* e) {
 // reallocates it a few times, not at every compaction. (Reserved for the whole arena at creation, it doubled a large
 // partition's device memory.)
 int reserve_gather(zb_engine* e) {
-  const uint64_t row_bytes = sizeof(Row) + sizeof(RowAux);
+  const uint64_t row_bytes = ROW_BYTES + sizeof(RowAux);
   const uint64_t full = std::max<uint64_t>(e->cfg.row_capacity * row_bytes, e->cfg.arena_bytes - STATIC_ARENA_BYTES);
   const uint64_t need = std::max<uint64_t>((uint64_t)e->host_hdr.rows_next * row_bytes,
-                                           (uint64_t)e->host_hdr.arena_next - STATIC_ARENA_BYTES);
+                                           (uint64_t)e->host_hdr.arena_next - STATIC_ARENA_BYTES +
+                                               (e->cfg.arena_bytes - e->arena_top));
   if (e->c_scratch && e->c_scratch_cap >= need) return ZB_OK;
   const uint64_t c = std::max<uint64_t>(std::min<uint64_t>(2 * need, full), std::max<uint64_t>(need, 1 << 20));
   HIPCHECK(e, hipStreamSynchronize(e->stream));
@@ -1067,13 +1080,15 @@ int reserve_gather(zb_engine* e) {
 
 CompactParams compact_params(zb_engine* e) {
   CompactParams c{};
-  c.rmeta = RowMetaArr{e->rows}; c.rkeys = RowKeysArr{e->rows}; c.row_arr = e->rows; c.raux = e->raux;
+  c.rmeta = e->rmeta; c.rkeys = e->rkeys; c.rlink = e->rlink; c.raux = e->raux;
   c.rows = (uint64_t)e->host_hdr.rows_next;
   c.live_rows = c.rows;
   c.row_flag = e->c_flag; c.row_new = e->c_new;
   c.arena = e->arena;
   c.static_refs = STATIC_ARENA_BYTES / 8;
   c.arena_next = (uint64_t)e->host_hdr.arena_next;
+  c.arena_top = e->arena_top;
+  c.arena_end = e->cfg.arena_bytes;
   c.log = e->log;
   c.win_begin = e->win_base;
   c.win_end = e->host_hdr.end;
@@ -1106,17 +1121,20 @@ int compact_state(zb_engine* e) {
     launch_row_flags(c, e->stream);
     rc = scan_u32(e, e->c_flag, e->c_new, rows, &live);
     if (rc != ZB_OK) return rc;
-    const uint64_t row_bytes = sizeof(Row) + sizeof(RowAux);
+    const uint64_t row_bytes = ROW_BYTES + sizeof(RowAux);
     rc = grow(e, &e->c_scratch, &e->c_scratch_cap, std::max<uint64_t>(live, 1) * row_bytes);
     if (rc != ZB_OK) return rc;
     c.row_new = e->c_new;
-    c.r2 = (Row*)e->c_scratch;
-    c.a2 = (RowAux*)(e->c_scratch + live * sizeof(Row));
+    c.m2 = (RowMeta*)e->c_scratch;
+    c.k2 = (RowKeys*)(e->c_scratch + live * sizeof(RowMeta));
+    c.a2 = (RowAux*)(e->c_scratch + live * (sizeof(RowMeta) + sizeof(RowKeys)));
     launch_row_gather(c, e->stream);
     if (live) {
-      HIPCHECK(e, hipMemcpyAsync(e->rows, c.r2, live * sizeof(Row), hipMemcpyDeviceToDevice, e->stream));
+      HIPCHECK(e, hipMemcpyAsync(e->rmeta, c.m2, live * sizeof(RowMeta), hipMemcpyDeviceToDevice, e->stream));
+      HIPCHECK(e, hipMemcpyAsync(e->rkeys, c.k2, live * sizeof(RowKeys), hipMemcpyDeviceToDevice, e->stream));
       HIPCHECK(e, hipMemcpyAsync(e->raux, c.a2, live * sizeof(RowAux), hipMemcpyDeviceToDevice, e->stream));
       c.live_rows = live;  // the children lists of the renamed rows, relinked
+      HIPCHECK(e, hipMemsetAsync(e->rlink, 0xff, live * sizeof(RowLink), e->stream));  // (NO_ROW)
       launch_row_relink(c, e->stream);
     }
   }
@@ -1144,7 +1162,9 @@ int compact_state(zb_engine* e) {
   // 3. arena: blobs reachable from live rows, the unreleased log window and the stores
   c = compact_params(e);
   c.live_rows = live;
-  const uint64_t dyn = (uint64_t)e->host_hdr.arena_next - STATIC_ARENA_BYTES;
+  // (the bitmap spans the staged documents at the top too, when there are any: they move down with the rest)
+  const uint64_t dyn = (e->arena_top < e->cfg.arena_bytes ? e->cfg.arena_bytes : (uint64_t)e->host_hdr.arena_next) -
+                       STATIC_ARENA_BYTES;
   const uint64_t words = (dyn / 8 + 63) / 64;
   if (words) {
     rc = grow(e, &e->c_bits, &e->c_bits_cap, words);
@@ -1167,6 +1187,21 @@ int compact_state(zb_engine* e) {
     if (granules)
       HIPCHECK(e, hipMemcpyAsync(e->arena + STATIC_ARENA_BYTES, e->c_scratch, granules * 8, hipMemcpyDeviceToDevice, e->stream));
     e->host_hdr.arena_next = (int64_t)(STATIC_ARENA_BYTES + granules * 8);
+  }
+  // every live document of the top region moved down. A batch uploaded in place but not injected yet (no record
+  // references it, nothing marked or moved it) stays where it is when the compacted bytes end below it; else it is
+  // uploaded again by the step that injects it.
+  const bool keep_pending = e->staged_in_place && e->staged_pending &&
+                            (uint64_t)e->host_hdr.arena_next <= e->staged_base;
+  if (keep_pending) {
+    e->arena_top = e->staged_base;
+    e->staged_top = e->cfg.arena_bytes;  // (a re-upload of the batch gives everything above it back)
+  } else {
+    e->arena_top = e->cfg.arena_bytes;
+    if (e->staged_in_place) {
+      e->staged_in_place = false;
+      e->staged_uploaded = false;
+    }
   }
   ZB_CT();  // arena gather
   // 4. job table: tombstones dropped (live entries collected, table cleared, refilled)
@@ -1242,11 +1277,17 @@ int maintain(zb_engine* e, bool force) {
   if (rc != ZB_OK) return rc;
   const uint64_t rm = std::min<uint64_t>(e->rows_mark, e->cfg.row_capacity);
   const uint64_t am = std::max<uint64_t>(std::min<uint64_t>(e->arena_mark, e->cfg.arena_bytes), STATIC_ARENA_BYTES);
-  const uint64_t ru = (uint64_t)e->host_hdr.rows_next, au = (uint64_t)e->host_hdr.arena_next;
-  const uint64_t rc_ = e->cfg.row_capacity, ac = e->cfg.arena_bytes;
+  const uint64_t ru = (uint64_t)e->host_hdr.rows_next;
+  // the arena: allocated bytes + the documents of injected batches at the top; a batch uploaded in place but not
+  // injected yet is neither (compaction cannot reclaim it: it is the capacity the rest has to live beside)
+  const bool pend = e->staged_in_place && e->staged_pending;
+  const uint64_t pend_bytes = pend ? e->staged_top - e->staged_base : 0;
+  const uint64_t au = (uint64_t)e->host_hdr.arena_next + (e->cfg.arena_bytes - (pend ? e->staged_top : e->arena_top));
+  const uint64_t rc_ = e->cfg.row_capacity, ac = e->cfg.arena_bytes - pend_bytes;
+  const uint64_t am_ = std::min(am, ac);
   // (and whenever less than an eighth is left: then compacting is the only way on)
   const bool rows_half = ru > rm + (rc_ - rm) / 2 || rc_ - std::min(ru, rc_) < rc_ / 8;
-  const bool arena_half = au > am + (ac - am) / 2 || ac - std::min(au, ac) < (ac - STATIC_ARENA_BYTES) / 8;
+  const bool arena_half = au > am_ + (ac - am_) / 2 || ac - std::min(au, ac) < (ac - STATIC_ARENA_BYTES) / 8;
   bool jobs_half = false;
   if (e->jobs.keys && !force && !rows_half && !arena_half) {
     uint32_t tombs = 0;
@@ -1320,7 +1361,10 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
         hipMalloc(&e->jobs.state, slots) != hipSuccess || hipMalloc(&e->jobs.tombs, sizeof(uint32_t)) != hipSuccess)
       return cleanup(ZB_ENOMEM);
   }
-  if (hipMalloc(&e->rows, e->cfg.row_capacity * sizeof(Row)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->row_mem, e->cfg.row_capacity * ROW_BYTES) != hipSuccess) return cleanup(ZB_ENOMEM);
+  e->rmeta = (RowMeta*)e->row_mem;
+  e->rkeys = (RowKeys*)(e->row_mem + e->cfg.row_capacity * sizeof(RowMeta));
+  e->rlink = (RowLink*)(e->row_mem + e->cfg.row_capacity * (sizeof(RowMeta) + sizeof(RowKeys)));
   // (+ ARENA_SLACK: the drain's encoders load a payload document's first words without a bounds check)
   if (hipMalloc(&e->arena, e->cfg.arena_bytes + ARENA_SLACK) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->hdr, 2 * sizeof(WaveHdr)) != hipSuccess) return cleanup(ZB_ENOMEM);
@@ -1336,7 +1380,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
     if (hipMemset(e->lookback, 0, lb) != hipSuccess) return cleanup(ZB_EDEVICE);
   }
   if (hipMalloc(&e->derr, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipMalloc(&e->dstats, 8 * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMalloc(&e->dstats, STAT_WORDS * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->derr_info, sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   e->job_cap = std::min<uint64_t>(L, 1ull << 26);
   if (hipMalloc(&e->merge_jobs, 2 * e->job_cap * sizeof(MergeJob)) != hipSuccess) return cleanup(ZB_ENOMEM);
@@ -1383,12 +1427,12 @@ void zb_engine_destroy(zb_engine* e) {
     if (x) (void)hipEventDestroy(x);
   void* ps[] = {e->vlen_mem, e->vlen_bad, e->jobs.keys, e->jobs.state, e->jobs.tombs, e->c_flag, e->c_new, e->c_tmp,
                 e->c_scratch, e->c_bits, e->c_pop, e->c_off, e->c_count, e->x_keys, e->x_pos, e->x_keys2, e->x_pos2,
-                e->sort_tmp, e->d_spread, e->mapres, e->map_ws, e->log_mem, e->links_mem, e->srcd_mem, e->rows, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
+                e->sort_tmp, e->d_spread, e->mapres, e->map_ws, e->log_mem, e->links_mem, e->srcd_mem, e->row_mem, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
                 e->merge_jobs, e->merge_slow, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_clen, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
                 e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->look_keys, e->look_idx,
-                e->conf_first, e->xslab, e->xlocks, e->phase};
+                e->conf_first, e->xslab, e->xlocks, e->xlane, e->phase};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->comm) (void)ncclCommDestroy(e->comm);
@@ -1455,7 +1499,7 @@ int zb_reset(zb_engine* e, int keep_staged) {
   HIPCHECK(e, hipMemsetAsync(e->derr, 0, sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->derr_info, 0xff, sizeof(uint64_t), e->stream));
   HIPCHECK(e, hipMemsetAsync(e->job_counts, 0, JOB_COUNTS * sizeof(uint32_t), e->stream));
-  HIPCHECK(e, hipMemsetAsync(e->dstats, 0, 8 * sizeof(uint64_t), e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->dstats, 0, STAT_WORDS * sizeof(uint64_t), e->stream));  // (banks too)
   if (e->jobs.keys) {
     HIPCHECK(e, hipMemsetAsync(e->jobs.keys, 0, (e->jobs.mask + 1) * sizeof(int64_t), e->stream));  // JOB_EMPTY
     HIPCHECK(e, hipMemsetAsync(e->jobs.state, 0, e->jobs.mask + 1, e->stream));
@@ -1467,6 +1511,11 @@ int zb_reset(zb_engine* e, int keep_staged) {
   e->rows_total = e->arena_total = e->records_total = e->compactions = 0;
   e->rows_mark = 0;
   e->arena_mark = STATIC_ARENA_BYTES;
+  // (a kept batch's documents stay where they were uploaded; everything above them is free again)
+  const bool keep_docs = keep_staged && e->staged_uploaded && e->staged_in_place;
+  e->arena_top = keep_docs ? e->staged_base : e->cfg.arena_bytes;
+  if (keep_docs) e->staged_top = e->cfg.arena_bytes;
+  else e->staged_in_place = false;
   HIPCHECK(e, hipStreamSynchronize(e->stream));
   e->ranges.clear();
   e->cmd_pool.clear();
@@ -1537,6 +1586,7 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
     HIPCHECK(e, hipMalloc(&e->xslab, (size_t)XSLAB_COUNT * XSLAB_BYTES));
     HIPCHECK(e, hipMalloc(&e->xlocks, XSLAB_COUNT * sizeof(uint32_t)));
     HIPCHECK(e, hipMemset(e->xlocks, 0, XSLAB_COUNT * sizeof(uint32_t)));
+    HIPCHECK(e, hipMalloc(&e->xlane, (size_t)XLANE_COUNT * XLANE_BYTES));
   }
   if (e->has_catch) {
     int orc = ensure_outbox(e);
@@ -1680,6 +1730,7 @@ bool is_doc(const uint8_t* p, uint64_t len) {  // DocumentValue: nil / empty -> 
 // the staged batch of the last zb_step was injected: start a new one
 void begin_staging(zb_engine* e) {
   if (e->staged_pending) return;
+  e->staged_in_place = false;  // (the injected batch's documents belong to the arena's top region now)
   e->staged_reqs.clear();
   e->staged.clear();
   e->staged_vlen.clear();
@@ -1701,7 +1752,20 @@ int upload_staged(zb_engine* e) {
   if (e->staged_uploaded) return ZB_OK;
   HIPCHECK(e, e->d_staged.upload(e->staged, e->stream));
   HIPCHECK(e, e->d_staged_vlen.upload(e->staged_vlen, e->stream));
-  HIPCHECK(e, e->d_staged_arena.upload(e->staged_arena, e->stream));
+  // the documents: in place at the top of the arena when they fit above the allocators' bytes (an earlier upload
+  // of this same batch gives its room back first), else into a staging buffer that k_inject copies from
+  if (e->staged_in_place) e->arena_top = e->staged_top;
+  e->staged_in_place = false;
+  const uint64_t sb = e->staged_arena.size();  // (whole granules: add_blob)
+  if (sb && e->arena_top >= (uint64_t)e->host_hdr.arena_next + sb) {
+    e->staged_top = e->arena_top;
+    e->staged_base = e->arena_top - sb;
+    HIPCHECK(e, hipMemcpyAsync(e->arena + e->staged_base, e->staged_arena.data(), sb, hipMemcpyHostToDevice, e->stream));
+    e->arena_top = e->staged_base;
+    e->staged_in_place = true;
+  } else {
+    HIPCHECK(e, e->d_staged_arena.upload(e->staged_arena, e->stream));
+  }
   e->staged_nlook = 0;
   if (!e->staged_only_creates) {  // (CREATE-only batches name no element instance)
     std::vector<int64_t> lk, li;
@@ -2270,12 +2334,12 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     const int64_t n = (int64_t)e->staged.size();
     if ((uint64_t)(e->host_hdr.end + n - e->win_base) > e->cfg.log_capacity)
       return fail(e, ZB_ENOMEM, "log capacity (release drained records with zb_log_release)");
-    if ((uint64_t)e->host_hdr.arena_next + e->staged_arena.size() > e->cfg.arena_bytes)
-      return fail(e, ZB_ENOMEM, "arena capacity");
     {
       const int urc = upload_staged(e);  // (already done by zb_upload_staged, or by an earlier step of a kept batch)
       if (urc != ZB_OK) return urc;
     }
+    if (!e->staged_in_place && (uint64_t)e->host_hdr.arena_next + e->staged_arena.size() > e->arena_top)
+      return fail(e, ZB_ENOMEM, "arena capacity");
     InjectParams ip;
     ip.log = e->log;
     ip.links = e->links;
@@ -2287,8 +2351,9 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     ip.staged_arena = e->d_staged_arena.p;
     ip.n = n;
     ip.log_base = e->host_hdr.end;
-    ip.arena_base = (uint64_t)e->host_hdr.arena_next;
-    ip.staged_bytes = e->staged_arena.size();
+    // documents in place: only the refs are rebased (the batch's documents are referenced where they lie)
+    ip.arena_base = e->staged_in_place ? e->staged_base : (uint64_t)e->host_hdr.arena_next;
+    ip.staged_bytes = e->staged_in_place ? 0 : e->staged_arena.size();
     launch_inject(ip, e->stream);
     // records naming an element instance by key: its row (ElementInstanceIndex.getInstance); the (key, index)
     // pairs were uploaded with the batch and are sorted here, on the device
@@ -2311,7 +2376,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
                           e->look_idx, m, "lookup", true);
       if (rc != ZB_OK) return rc;
       ResolveParams rp{};
-      rp.rmeta = RowMetaArr{e->rows}; rp.rkeys = RowKeysArr{e->rows}; rp.rows = (uint64_t)e->host_hdr.rows_next;
+      rp.rmeta = e->rmeta; rp.rkeys = e->rkeys; rp.rows = (uint64_t)e->host_hdr.rows_next;
       rp.keys = e->look_keys; rp.pos = e->look_idx; rp.pos_base = ip.log_base; rp.n = (int64_t)m;
       rp.links = e->links;
       launch_resolve(rp, e->stream);
@@ -2331,7 +2396,8 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     }
     if (e->host_hdr.begin == e->host_hdr.gen_end) e->host_hdr.gen_end = e->host_hdr.end + n;
     e->host_hdr.end += n;
-    e->host_hdr.arena_next += (int64_t)e->staged_arena.size();
+    if (e->staged_in_place) e->arena_total += e->staged_arena.size();  // (allocated at the top, not by arena_next)
+    else e->host_hdr.arena_next += (int64_t)e->staged_arena.size();
     HIPCHECK(e, upload_async(e, e->hdr + (e->wave & 1), &e->host_hdr, sizeof(WaveHdr)));
     e->staged_pending = false;
   }
@@ -2412,6 +2478,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
       e->wave++;
       e->epoch++;
     }
+    if (e->wave_fused_grid) launch_stat_fold(e->dstats, e->stream);  // k_wave's statistics banks -> the counters
     if (!per_wave) HIPCHECK(e, hipEventRecord(e->ev[1], e->stream));
     HIPCHECK(e, hipGetLastError());
     HIPCHECK(e, hipMemcpyAsync(e->h_hdr_pinned, e->hdr + (e->wave & 1), sizeof(WaveHdr), hipMemcpyDeviceToHost,
@@ -2957,7 +3024,7 @@ MsgParams msg_params(zb_engine* e) {
   p.log = e->log; p.links = e->links; p.srcd = e->srcd; p.vlen = e->vlen;
   p.arena = e->arena;
   p.hdr = e->hdr + (e->wave & 1);
-  p.arena_cap = e->cfg.arena_bytes;
+  p.arena_cap = e->arena_top;  // (the allocators' ceiling: staged documents above it)
   p.subs = e->subs; p.sub_head = e->sub_head; p.sub_next = e->sub_next;
   p.sub_mask = e->head_mask; p.sub_count = e->sub_count; p.sub_cap = e->store_cap;
   p.msgs = e->msgs; p.msg_head = e->msg_head; p.msg_next = e->msg_next;
@@ -3021,7 +3088,7 @@ int check_message_batch(zb_engine* e, uint64_t n, uint64_t publishes, uint64_t b
   if (!outbox_span_ok(e, base + 3 * (int64_t)n))
     return fail(e, ZB_EUNSUPPORTED, "more than 2^34 log positions since the outbox was last taken");
   if (e->msg_count + publishes > e->store_cap) return fail(e, ZB_ENOMEM, "message store capacity");
-  if ((uint64_t)e->host_hdr.arena_next + blob_bytes > e->cfg.arena_bytes) return fail(e, ZB_ENOMEM, "arena capacity");
+  if ((uint64_t)e->host_hdr.arena_next + blob_bytes > e->arena_top) return fail(e, ZB_ENOMEM, "arena capacity");
   return ZB_OK;
 }
 
@@ -3212,7 +3279,7 @@ int deliver(zb_engine* e, int kind, const uint8_t* buf, const std::vector<uint64
     int rc = sort_pairs(e, e->x_keys, e->x_keys2, e->x_pos, e->x_pos2, n, "inbox");
     if (rc != ZB_OK) return rc;
     ResolveParams rp{};
-    rp.rmeta = RowMetaArr{e->rows}; rp.rkeys = RowKeysArr{e->rows}; rp.rows = (uint64_t)e->host_hdr.rows_next;
+    rp.rmeta = e->rmeta; rp.rkeys = e->rkeys; rp.rows = (uint64_t)e->host_hdr.rows_next;
     rp.keys = e->x_keys2; rp.pos = e->x_pos2; rp.pos_base = 0; rp.n = (int64_t)n;
     rp.links = e->links;
     launch_resolve(rp, e->stream);
@@ -3847,7 +3914,7 @@ int zb_read_memory_stats(zb_engine* e, zb_memory_stats* out) {
   m.log_capacity = e->cfg.log_capacity;
   m.rows_allocated = (uint64_t)e->host_hdr.rows_next;
   m.row_capacity = e->cfg.row_capacity;
-  m.arena_used = (uint64_t)e->host_hdr.arena_next;
+  m.arena_used = (uint64_t)e->host_hdr.arena_next + (e->cfg.arena_bytes - e->arena_top);
   m.arena_bytes = e->cfg.arena_bytes;
   m.records_total = e->records_total;
   m.rows_total = e->rows_total;
@@ -3915,7 +3982,7 @@ int zb_read_instances(zb_engine* e, uint8_t* buf, size_t cap, size_t* len, uint6
         hipMalloc(&d_rows, rows * 4) != hipSuccess) { rc = fail(e, ZB_ENOMEM, "read_instances buffers"); break; }
     if (hipMemsetAsync(d_count, 0, 4, e->stream) != hipSuccess) { rc = ZB_EDEVICE; break; }
     LiveParams lp{};
-    lp.rmeta = RowMetaArr{e->rows}; lp.rkeys = RowKeysArr{e->rows}; lp.rows = rows; lp.count = d_count; lp.cap = rows;
+    lp.rmeta = e->rmeta; lp.rkeys = e->rkeys; lp.rows = rows; lp.count = d_count; lp.cap = rows;
     lp.keys = d_keys; lp.row_of = d_rows;
     launch_live_rows(lp, e->stream);
     uint32_t live = 0;
@@ -3984,7 +4051,7 @@ int zb_read_instances(zb_engine* e, uint8_t* buf, size_t cap, size_t* len, uint6
 namespace {
 constexpr uint64_t SNAP_MAGIC = 0x32504e53425a4755ull;  // "UGZBSNP2"
 // A snapshot holds the live state only (taken right after a forced compaction): the element-instance rows
-// [0, live), the arena's dynamic region [STATIC, arena_next) (the static region comes with the deployments),
+// [0, live) (state, keys and scope state; the children links are rebuilt on restore), the arena's dynamic region [STATIC, arena_next) (the static region comes with the deployments),
 // the live job states as (key, state) pairs, and the store entries (chains are rebuilt on restore).
 struct SnapHead {
   uint64_t magic;
@@ -4012,7 +4079,7 @@ uint64_t model_hash(const zb_engine* e) {  // FNV-1a over the deployed tables
 }
 
 size_t snap_bytes(const SnapHead& h) {
-  return sizeof(h) + h.rows * (sizeof(Row) + sizeof(RowAux)) + h.arena_dyn +
+  return sizeof(h) + h.rows * (sizeof(RowMeta) + sizeof(RowKeys) + sizeof(RowAux)) + h.arena_dyn +
          h.jobs * (sizeof(int64_t) + 1) + h.sub_count * sizeof(SubEntry) + h.msg_count * sizeof(MsgEntry);
 }
 }  // namespace
@@ -4062,7 +4129,7 @@ int zb_snapshot(zb_engine* e, uint8_t* buf, size_t cap, size_t* len) {
     o += n;
     return true;
   };
-  bool ok = get(e->rows, h.rows * sizeof(Row)) &&
+  bool ok = get(e->rmeta, h.rows * sizeof(RowMeta)) && get(e->rkeys, h.rows * sizeof(RowKeys)) &&
             get(e->raux, h.rows * sizeof(RowAux)) && get(e->arena + STATIC_ARENA_BYTES, h.arena_dyn);
   if (!ok) return fail(e, ZB_EDEVICE, "snapshot copy");
   if (h.jobs) {
@@ -4103,9 +4170,15 @@ int zb_restore(zb_engine* e, const uint8_t* buf, size_t len) {
     o += n;
     return true;
   };
-  bool ok = put(e->rows, h.rows * sizeof(Row)) &&
+  bool ok = put(e->rmeta, h.rows * sizeof(RowMeta)) && put(e->rkeys, h.rows * sizeof(RowKeys)) &&
             put(e->raux, h.rows * sizeof(RowAux)) && put(e->arena + STATIC_ARENA_BYTES, h.arena_dyn);
   if (!ok) return fail(e, ZB_EDEVICE, "restore copy");
+  if (h.rows) {  // the children lists are not in the snapshot: rebuilt from the parents (as after a compaction)
+    CompactParams c = compact_params(e);
+    c.live_rows = h.rows;
+    HIPCHECK(e, hipMemsetAsync(e->rlink, 0xff, h.rows * sizeof(RowLink), e->stream));
+    launch_row_relink(c, e->stream);
+  }
   if (h.jobs) {
     rc = grow(e, &e->c_scratch, &e->c_scratch_cap, h.jobs * (sizeof(int64_t) + 1));
     if (rc != ZB_OK) return rc;

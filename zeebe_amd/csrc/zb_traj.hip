@@ -602,15 +602,17 @@ __device__ __forceinline__ void merge_into(const TrajParams& P, uint32_t src, ui
       olen = o.n;
       if (o.n > m_len) err |= DE_UNSUPPORTED;  // (never for a document merge_docs takes: as k_merge_gen)
       // shapes the structural merge refuses: the exact tree (zb_xmerge.hpp)
-      x_exclusive(XSlabs{P.xslab, P.xlocks}, (!ok || unsup) && o.n <= m_len, [&](uint8_t* slab) {
+      x_run(XSlabs{P.xslab, P.xlocks, P.xlane}, (!ok || unsup) && o.n <= m_len, [&](uint8_t* slab, uint32_t sb, bool fin) {
         Out w{(uint8_t*)gd + 4, 0};
-        const int st = x_merge(slab, XSLAB_BYTES, (const uint8_t*)gs + 4, ns, (const uint8_t*)gt + 4, nt, w, m_len);
+        const int st = x_merge(slab, sb, (const uint8_t*)gs + 4, ns, (const uint8_t*)gt + 4, nt, w, m_len);
+        if (st == X_UNSUP && !fin) return st;
         if (st == X_OK) {
           if (w.n == 1 && ((uint8_t*)gd)[4] == 0xc0) ((uint8_t*)gd)[4] = 0x80;
           olen = w.n;
         } else {
           err |= st == X_FAIL ? DE_BAD_PAYLOAD : DE_UNSUPPORTED;
         }
+        return st;
       });
       gd[0] = olen;
     } else {
@@ -904,7 +906,7 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
 #pragma unroll
     for (int k = 0; k < TR; k++)
       if ((live >> k) & 1) gid[k] = (uint32_t)(r0 + n++);
-    // the children lists (Row.c_head / c_next): every row of the instance is this thread's, parents included
+    // the children lists (RowLink.c_head / c_next): every row of the instance is this thread's, parents included
     u32x4 head = NO_ROW, next = NO_ROW;
 #pragma unroll
     for (int k = 0; k < TR; k++) {
@@ -929,14 +931,10 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
       m.flags = 0;
       m.nchild = I.rnch[k];
       const uint32_t jk = I.rjob[k];
-      Row x;
-      x.m = m;
-      x.k = RowKeys{wf_key(P, I.rkey[k]), wf_key(P, I.scope_of(k)), wf_key(P, I.inst_key),
-                    jk == JOB_ZERO ? 0 : job_key(P, jk)};
-      x.c_head = head[k];
-      x.c_next = next[k];
-      x.pad[0] = x.pad[1] = 0;
-      P.rows[gid[k]] = x;
+      P.rmeta[gid[k]] = m;
+      P.rkeys[gid[k]] = RowKeys{wf_key(P, I.rkey[k]), wf_key(P, I.scope_of(k)), wf_key(P, I.inst_key),
+                                jk == JOB_ZERO ? 0 : job_key(P, jk)};
+      P.rlink[gid[k]] = RowLink{head[k], next[k]};
     }
   }
   // ---- statistics

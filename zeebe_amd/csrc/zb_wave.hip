@@ -89,10 +89,12 @@ __device__ __forceinline__ uint32_t formula_base(const WaveParams& P, const zb_r
   const ValueConst vc = P.vconst[d.elem];
   return (kind_vt(d.kind) == ZB_VT_JOB ? vc.job : vc.wf) + mp_int_len(d.inst_key) + mp_int_len(d.scope_key);
 }
-__device__ __forceinline__ uint32_t payload_len_of(const WaveParams& P, const zb_rec& rec, int64_t pos) {
+// (vl: the record's own hint, vlen[pos], loaded with the record: process_record's stores to the rows would otherwise
+// keep the compiler from issuing the load before them, one more dependent round trip at the end of every record)
+__device__ __forceinline__ uint32_t payload_len_of(const WaveParams& P, const zb_rec& rec, uint32_t vl) {
   if (kind_vt(rec.kind) == ZB_VT_INCIDENT) return VLEN_UNKNOWN;  // (payload: an incident detail blob)
   if (fast_kind(rec) && P.vconst) {
-    const uint32_t v = P.vlen[pos];
+    const uint32_t v = vl;
     if (v != VLEN_UNKNOWN) {
       const uint32_t x = v - formula_base(P, rec);  // mp_bin_len(plen)
       return x <= 257 ? x - 2 : (x <= 65538 ? x - 3 : x - 5);
@@ -101,14 +103,14 @@ __device__ __forceinline__ uint32_t payload_len_of(const WaveParams& P, const zb
   return *(const uint32_t*)(P.arena + (uint64_t)rec.payload * 8);
 }
 // after process_record(rec at pos) staged slots [ns0, t.ns): their payload lengths
-__device__ __forceinline__ void annotate_slots(const WaveParams& P, TState& t, int ns0, const zb_rec& rec, int64_t pos) {
+__device__ __forceinline__ void annotate_slots(const WaveParams& P, TState& t, int ns0, const zb_rec& rec, uint32_t vl) {
   uint32_t rl = VLEN_UNKNOWN;
   bool have = false;
   for (int k = ns0; k < t.ns; k++) {
     Slot& s = t.s[k];
     if (s.flags & (SF_PAY_MERGED | SF_PAY_DETAIL) || !fast_kind(s.d)) continue;
     if (s.d.payload == rec.payload && !(rec.kind & KIND_RAW)) {
-      if (!have) { rl = payload_len_of(P, rec, pos); have = true; }
+      if (!have) { rl = payload_len_of(P, rec, vl); have = true; }
       s.plen = rl;
     } else {
       s.plen = *(const uint32_t*)(P.arena + (uint64_t)s.d.payload * 8);
@@ -836,16 +838,18 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
       // a thread owns its record plus the continuation records that follow it (one parent's batch);
       // a batch never spans generations, so its tail may lie past a chunk end (skipped there as cont)
       const uint64_t lk = P.links[r];
+      const uint32_t vl = P.vlen[r];
       process_record(P, rec, r, (uint32_t)lk, (uint32_t)(lk >> 32), t);
-      annotate_slots(P, t, 0, rec, r);
+      annotate_slots(P, t, 0, rec, vl);
       for (int64_t q = r + 1; q < gen_end && q < r + 4; q++) {
         const zb_rec rec2 = P.log[q];
         if (!grouped(rec2)) break;
         const uint64_t lk2 = P.links[q];
+        const uint32_t vl2 = P.vlen[q];
         t.src_off = (uint32_t)(q - r);
         const int ns0 = t.ns;
         process_record(P, rec2, q, (uint32_t)lk2, (uint32_t)(lk2 >> 32), t);
-        annotate_slots(P, t, ns0, rec2, q);
+        annotate_slots(P, t, ns0, rec2, vl2);
       }
     }
     // stage the follow-ups and the count word
@@ -982,7 +986,7 @@ __global__ void __launch_bounds__(WG) k_pre(WaveParams P) {
       if (row != NO_ROW) {
         uint32_t first = NO_ROW;
         uint64_t n = 0;
-        for (uint32_t ch = P.rows[row].c_head; ch != NO_ROW && n < P.row_cap; ch = P.rows[ch].c_next, n++) {
+        for (uint32_t ch = P.rlink[row].c_head; ch != NO_ROW && n < P.row_cap; ch = P.rlink[ch].c_next, n++) {
           if (!ZB_DCHECK(ch < P.row_cap, "row %u child %u\n", row, ch)) break;
           const RowMeta cm = P.rmeta[ch];
           if (cm.state != 0 && cm.parent == row && ch < first) first = ch;
@@ -1138,21 +1142,24 @@ __device__ __forceinline__ void emit_item(const WaveParams& P, const Chunk& c, i
       if (row >= P.row_cap) { err |= DE_ROWS_FULL; s.rself = NO_ROW; }
       else {
         s.rself = (uint32_t)row;
-        Row x;  // (the whole line in one go)
-        x.c_head = NO_ROW; x.c_next = NO_ROW; x.pad[0] = x.pad[1] = 0;
+        RowMeta m;
+        RowKeys k;
+        uint32_t c_next = NO_ROW;
         if (s.flags & SF_ROW_INIT) {
-          x.m.payload = s.d.payload; x.m.parent = s.rscope; x.m.elem = s.d.elem; x.m.state = WI_ELEMENT_READY;
-          x.m.flags = 0; x.m.nchild = 0;
-          x.k = RowKeys{s.d.key, s.d.scope_key, s.d.inst_key, 0};
+          m.payload = s.d.payload; m.parent = s.rscope; m.elem = s.d.elem; m.state = WI_ELEMENT_READY;
+          m.flags = 0; m.nchild = 0;
+          k = RowKeys{s.d.key, s.d.scope_key, s.d.inst_key, 0};
           // ElementInstance.children.add: into the flow scope's list (read from the next wave on)
-          if (s.rscope != NO_ROW) x.c_next = atomicExch(&P.rows[s.rscope].c_head, (uint32_t)row);
+          if (s.rscope != NO_ROW) c_next = atomicExch(&P.rlink[s.rscope].c_head, (uint32_t)row);
         } else {
           // a CREATE's row: the instance enters the index when its CREATED event is processed (next wave), and
           // until then the row reads as free (state 0, no parent, no children), whatever the memory held before
-          x.m.payload = 0; x.m.parent = NO_ROW; x.m.elem = NO_ELEM; x.m.state = 0; x.m.flags = 0; x.m.nchild = 0;
-          x.k = RowKeys{0, 0, 0, 0};
+          m.payload = 0; m.parent = NO_ROW; m.elem = NO_ELEM; m.state = 0; m.flags = 0; m.nchild = 0;
+          k = RowKeys{0, 0, 0, 0};
         }
-        P.rows[row] = x;
+        P.rmeta[row] = m;
+        P.rkeys[row] = k;
+        P.rlink[row] = RowLink{NO_ROW, c_next};
       }
     }
     if (out_rec >= P.log_cap) { err |= DE_LOG_FULL; }
@@ -1386,18 +1393,20 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
     if (threadIdx.x == 0) s_void = 0;  // (ordered before every wave's hand-off by the tile scan's barrier)
     if (r < c.end) {
       const zb_rec rec = P.log[r];
+      const uint64_t lk = P.links[r];
+      const uint32_t vl = P.vlen[r];
       if (!grouped(rec)) {
-        const uint64_t lk = P.links[r];
         process_record(P, rec, r, (uint32_t)lk, (uint32_t)(lk >> 32), t);
-        annotate_slots(P, t, 0, rec, r);
+        annotate_slots(P, t, 0, rec, vl);
         for (int64_t q = r + 1; q < gen_end && q < r + 4; q++) {
           const zb_rec rec2 = P.log[q];
           if (!grouped(rec2)) break;
           const uint64_t lk2 = P.links[q];
+          const uint32_t vl2 = P.vlen[q];
           t.src_off = (uint32_t)(q - r);
           const int ns0 = t.ns;
           process_record(P, rec2, q, (uint32_t)lk2, (uint32_t)(lk2 >> 32), t);
-          annotate_slots(P, t, ns0, rec2, q);
+          annotate_slots(P, t, ns0, rec2, vl2);
         }
       }
     }
@@ -1603,11 +1612,12 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
     __syncthreads();  // LDS slots and scan scratch are reused by the next tile
     ZB_PHASE(2);  // emit
   }
-  if (threadIdx.x == 0 && (wg_sa | wg_sb)) {
-    atomicAdd((unsigned long long*)&P.stats[0], (unsigned long long)(uint32_t)wg_sa);  // transitions
-    atomicAdd((unsigned long long*)&P.stats[1], (unsigned long long)(wg_sa >> 32));    // completed instances
-    atomicAdd((unsigned long long*)&P.stats[2], (unsigned long long)(uint32_t)wg_sb);  // created
-    atomicAdd((unsigned long long*)&P.stats[7], (unsigned long long)(wg_sb >> 32));    // canceled
+  if (threadIdx.x == 0 && (wg_sa | wg_sb)) {  // (into the workgroup's bank: launch_stat_fold)
+    unsigned long long* bank = (unsigned long long*)(P.stats + 8 + 8 * (blockIdx.x % STAT_BANKS));
+    atomicAdd(bank + 0, (unsigned long long)(uint32_t)wg_sa);  // transitions
+    atomicAdd(bank + 1, (unsigned long long)(wg_sa >> 32));    // completed instances
+    atomicAdd(bank + 2, (unsigned long long)(uint32_t)wg_sb);  // created
+    atomicAdd(bank + 3, (unsigned long long)(wg_sb >> 32));    // canceled
   }
 #ifdef ZB_PHASES
   if (threadIdx.x == 0 && P.phase) {
@@ -1651,6 +1661,29 @@ __global__ void __launch_bounds__(256) k_conflict(WaveParams P) {
 void launch_conflict(const WaveParams& p, hipStream_t stream) {
   hipLaunchKernelGGL((k_conflict<false>), dim3(512), dim3(256), 0, stream, p);
   hipLaunchKernelGGL((k_conflict<true>), dim3(512), dim3(256), 0, stream, p);
+}
+
+__global__ void __launch_bounds__(64) k_stat_fold(uint64_t* stats) {
+  uint64_t* bank = stats + 8 + 8 * threadIdx.x;
+  uint64_t x[4];
+#pragma unroll
+  for (int f = 0; f < 4; f++) {
+    x[f] = bank[f];
+    bank[f] = 0;
+  }
+#pragma unroll
+  for (int f = 0; f < 4; f++)
+    for (int d = 32; d >= 1; d >>= 1) x[f] += __shfl_xor(x[f], d, 64);
+  if (threadIdx.x == 0) {
+    stats[0] += x[0];
+    stats[1] += x[1];
+    stats[2] += x[2];
+    stats[7] += x[3];
+  }
+}
+void launch_stat_fold(uint64_t* stats, hipStream_t stream) {
+  static_assert(STAT_BANKS == 64, "one lane per bank");
+  hipLaunchKernelGGL(k_stat_fold, dim3(1), dim3(64), 0, stream, stats);
 }
 
 void launch_wave(const WaveParams& p, int grid, hipStream_t stream) {

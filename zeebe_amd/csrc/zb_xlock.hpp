@@ -1,5 +1,6 @@
 // zb_xlock.hpp — the exact payload tree (zb_xmerge.hpp) inside the kernels: a lane whose document pair the fast
-// paths refused takes one of XSLAB_COUNT workspace slabs for the duration of one x_merge / x_map.
+// paths refused runs it in a small workspace of its own (x_run) or, when the pair's tree does not fit it, takes one of
+// XSLAB_COUNT big workspace slabs for the duration of one x_merge / x_map.
 //
 // The lanes of a wave that need it take their turns one at a time (the mask comes from a ballot, so the loop is
 // wave-uniform), and the single active lane spins on the slab's lock. No holder ever waits for anything while
@@ -14,6 +15,7 @@ namespace zbg {
 struct XSlabs {
   uint8_t* base;    // XSLAB_COUNT x XSLAB_BYTES
   uint32_t* locks;  // XSLAB_COUNT, 0 = free
+  uint8_t* lanes;   // XLANE_COUNT x XLANE_BYTES: one per thread of a launch (global thread id), no lock
 };
 
 template <class F>
@@ -33,6 +35,19 @@ __device__ __forceinline__ void x_exclusive(const XSlabs& X, bool need, F&& f) {
     }
     m &= m - 1;
   }
+}
+
+// The exact tree for every lane with `need`: first each in its own XLANE_BYTES workspace, all lanes at once; a pair
+// whose tree does not fit it (X_UNSUP, nothing written yet) then takes a big slab in turns (x_exclusive).
+// f(slab, bytes, final) -> X_* status; it commits its outcome unless it returns X_UNSUP with final false.
+template <class F>
+__device__ __forceinline__ void x_run(const XSlabs& X, bool need, F&& f) {
+  bool again = need;
+  if (need && X.lanes) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < XLANE_COUNT) again = f(X.lanes + t * XLANE_BYTES, XLANE_BYTES, false) == X_UNSUP;
+  }
+  x_exclusive(X, again, [&](uint8_t* slab) { (void)f(slab, XSLAB_BYTES, true); });
 }
 
 }  // namespace zbg

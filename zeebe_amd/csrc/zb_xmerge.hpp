@@ -23,6 +23,10 @@ namespace zbg {
 
 constexpr uint32_t XSLAB_BYTES = 4u << 20;  // workspace of one document pair
 constexpr uint32_t XSLAB_COUNT = 32;        // pairs in flight (zb_xlock.hpp: one lock per slab)
+// every lane of a launch (up to XLANE_COUNT) first tries its pair in a small workspace of its own, concurrently: 32 KB
+// holds the tree of ~140 tokens (2 x source + target), the documents of a typical job / message payload merge
+constexpr uint32_t XLANE_BYTES = 32u << 10;
+constexpr uint32_t XLANE_COUNT = 16384;
 
 // node types (MsgPackTree.nodeTypeMap values; XT_NONE = no entry)
 enum : uint8_t { XT_NONE = 0, XT_EXISTING_LEAF = 1, XT_EXTRACTED_LEAF = 2, XT_MAP = 3, XT_ARRAY = 4 };
