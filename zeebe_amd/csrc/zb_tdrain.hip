@@ -163,8 +163,30 @@ __device__ __forceinline__ TdGen td_gen_wave(const TrajParams& P, const TdTab& T
   return G;
 }
 
+// The first SER_PRE words of a static payload blob (a trace's literal ref, the same for every lane of its class)
+// through the scalar cache, one scalar load sequence per distinct ref of the wave: inside the write pass's
+// generation loop a vector load would wait for every store the wave issued before it (vmcnt counts loads and
+// stores together, in order), i.e. for the previous generation's whole image stream. `mine`: this lane's record
+// has a static payload, ref; the other lanes' pre is left as it is.
+template <int N>
+__device__ __forceinline__ void td_static_pre(const uint8_t* arena, bool mine, uint32_t ref, uint64_t (&pre)[N]) {
+  uint64_t need = __ballot(mine);
+  while (need) {
+    const uint32_t r = __builtin_amdgcn_readlane(ref, __builtin_ctzll(need));
+    const cptr<uint64_t> src = K((const uint64_t*)(arena + (uint64_t)r * 8));
+    uint64_t w[N];
+#pragma unroll
+    for (int j = 0; j < N; j++) w[j] = src[j];  // (ARENA_SLACK: never past the allocation)
+    const bool take = mine && ref == r;
+#pragma unroll
+    for (int j = 0; j < N; j++) pre[j] = take ? w[j] : pre[j];  // (a select: in a branch on ref == r the compiler
+    need &= ~__ballot(take);                                     //  turns the loads into vector ones)
+  }
+}
+
 // record k of the instance's generation w, resolved from the class trace; vl: its value length (the
 // encoder's, by the formula), plen: its payload document's length
+template <bool SCALAR_STATIC = false>
 __device__ __forceinline__ zb_rec td_record(const TrajParams& P, const TdTab& T, const TmplLane& L, uint32_t cls, int w,
                                             uint32_t k, const TdGen& G, int64_t inst, uint32_t create_ref,
                                             uint32_t create_len, int64_t kwf0, uint32_t& vl, uint32_t& plen) {
@@ -176,7 +198,13 @@ __device__ __forceinline__ zb_rec td_record(const TrajParams& P, const TdTab& T,
   // (k_tmpl_decide: no merge results in a deferred batch -- the CREATE payload or a static blob)
   const bool cr = t.payload == PAY_CREATE;
   d.payload = cr ? create_ref : t.payload;
-  plen = cr ? create_len : arena_len(P.arena, d.payload);
+  if (SCALAR_STATIC) {  // (the write pass: a static blob's length word through the scalar cache)
+    uint64_t w0[1] = {0};
+    td_static_pre(P.arena, !cr, d.payload, w0);  // (the active lanes: a waterfall over their refs)
+    plen = cr ? create_len : (uint32_t)w0[0];
+  } else {
+    plen = cr ? create_len : arena_len(P.arena, d.payload);
+  }
   d.elem = t.elem; d.intent = t.intent; d.kind = t.kind;
   const ValueConst vc = T.vconst[d.elem];
   vl = (kind_vt(d.kind) == ZB_VT_JOB ? vc.job : vc.wf) + mp_int_len(d.inst_key) + mp_int_len(d.scope_key) +
@@ -297,6 +325,11 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
     uint64_t cpre[SER_PRE];
 #pragma unroll
     for (int j = 0; j < SER_PRE; j++) cpre[j] = cdw[j];  // (ARENA_SLACK: never past the allocation)
+    // the loads retired here, before the first store: an empty asm that redefines the words makes the compiler wait
+    // for them once, instead of at the generation loop's first use of them, where the wait (vmcnt) would also take
+    // every store issued so far
+#pragma unroll
+    for (int j = 0; j < SER_PRE; j++) asm volatile("" : "+v"(cpre[j]));
     // the wave's first lane's class ranks (td_gen_wave)
     uint32_t b0[CLS_MAX];
 #pragma unroll
@@ -322,8 +355,8 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
       zb_rec d0{}, d1{};
       {
         uint32_t plen;
-        if (G.nrec > 0) d0 = td_record(P, T, L.L, L.cls, w, 0, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl0, plen);
-        if (G.nrec > 1) d1 = td_record(P, T, L.L, L.cls, w, 1, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl1, plen);
+        if (G.nrec > 0) d0 = td_record<true>(P, T, L.L, L.cls, w, 0, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl0, plen);
+        if (G.nrec > 1) d1 = td_record<true>(P, T, L.L, L.cls, w, 1, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl1, plen);
       }
       const uint32_t mine = vl0 + vl1;
       const uint32_t incl = wave_incl_scan(mine);
@@ -362,10 +395,7 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
             uint64_t pre[SER_PRE];
 #pragma unroll
             for (int j = 0; j < SER_PRE; j++) pre[j] = cpre[j];
-            if (!cr) {  // a static blob
-#pragma unroll
-              for (int j = 0; j < SER_PRE; j++) pre[j] = dw[j];  // (ARENA_SLACK)
-            }
+            td_static_pre(P.arena, !cr, d.payload, pre);  // a static blob: through the scalar cache
             FastW fw;
             fw.begin(img, sh + (rel - lo) + (k ? vl0 : 0));
             fast_encode(fw, d, tab, segs, dw, pre);
