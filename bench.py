@@ -600,6 +600,8 @@ def run_exact_tree(a, n=1_000_000, steps=3):
                 assert st["quiescent"] and st["merges"] == n, st
                 if it:
                     ms.append((t1 - t0) * 1e3)
+                print("exact-tree %s %s step %d: %.2f ms" % ("wave" if wave_only else "traj", name, it, (t1 - t0) * 1e3),
+                      file=sys.stderr, flush=True)
             eng.close()
             out["%s_%s" % ("wave" if wave_only else "traj", name)] = sum(ms) / len(ms)
     for p in ("traj", "wave"):

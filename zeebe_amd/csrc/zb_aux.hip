@@ -294,8 +294,9 @@ void launch_map(const WaveParams& p, hipStream_t s) {
 
 void launch_merge(const WaveParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_merge, dim3(1024), dim3(256), 0, s, p);
-  // (the general merge's queue is empty for flat payloads -- nearly every wave -- and the launch exits at once)
-  hipLaunchKernelGGL(k_merge_gen, dim3(64), dim3(256), 0, s, p);
+  // (the general merge's queue is empty for flat payloads -- nearly every wave -- and the launch exits at once; a full
+  // queue of exact-tree merges keeps every lane workspace busy: XLANE_COUNT lanes, latency-bound per lane)
+  hipLaunchKernelGGL(k_merge_gen, dim3(XLANE_COUNT / 256), dim3(256), 0, s, p);
 }
 void launch_cond(const WaveParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_cond, dim3(1024), dim3(256), 0, s, p);

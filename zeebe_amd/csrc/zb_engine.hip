@@ -1584,8 +1584,8 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
   }
   if ((e->has_io || e->has_merges) && !e->xslab) {  // payloads the structural merge / mapper refuse
     HIPCHECK(e, hipMalloc(&e->xslab, (size_t)XSLAB_COUNT * XSLAB_BYTES));
-    HIPCHECK(e, hipMalloc(&e->xlocks, XSLAB_COUNT * sizeof(uint32_t)));
-    HIPCHECK(e, hipMemset(e->xlocks, 0, XSLAB_COUNT * sizeof(uint32_t)));
+    HIPCHECK(e, hipMalloc(&e->xlocks, XLOCK_COUNT * sizeof(uint32_t)));
+    HIPCHECK(e, hipMemset(e->xlocks, 0, XLOCK_COUNT * sizeof(uint32_t)));
     HIPCHECK(e, hipMalloc(&e->xlane, (size_t)XLANE_COUNT * XLANE_BYTES));
   }
   if (e->has_catch) {

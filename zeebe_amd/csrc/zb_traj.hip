@@ -87,7 +87,8 @@ enum TrajFlags : uint8_t {
 };
 
 // trajectory-path error bits (count pass -> host falls back to the wave path)
-enum TrajErr : uint32_t { TE_FALLBACK = 1u, TE_REGEN = 1u << 30 };
+// TE_XTREE: a merge needs the exact payload tree (zb_xmerge.hpp), which the wave pipeline runs: the batch falls back
+enum TrajErr : uint32_t { TE_FALLBACK = 1u, TE_XTREE = 1u << 29, TE_REGEN = 1u << 30 };
 
 // flat-merge staging in LDS (emit pass): per thread the two input blobs and the output blob
 constexpr int FM_WORDS = 12;                  // 48-byte blob slots: documents of <= 44 bytes
@@ -601,19 +602,10 @@ __device__ __forceinline__ void merge_into(const TrajParams& P, uint32_t src, ui
       const bool ok = merge_docs((const uint8_t*)gs + 4, ns, (const uint8_t*)gt + 4, nt, o, unsup);
       olen = o.n;
       if (o.n > m_len) err |= DE_UNSUPPORTED;  // (never for a document merge_docs takes: as k_merge_gen)
-      // shapes the structural merge refuses: the exact tree (zb_xmerge.hpp)
-      x_run(XSlabs{P.xslab, P.xlocks, P.xlane}, (!ok || unsup) && o.n <= m_len, [&](uint8_t* slab, uint32_t sb, bool fin) {
-        Out w{(uint8_t*)gd + 4, 0};
-        const int st = x_merge(slab, sb, (const uint8_t*)gs + 4, ns, (const uint8_t*)gt + 4, nt, w, m_len);
-        if (st == X_UNSUP && !fin) return st;
-        if (st == X_OK) {
-          if (w.n == 1 && ((uint8_t*)gd)[4] == 0xc0) ((uint8_t*)gd)[4] = 0x80;
-          olen = w.n;
-        } else {
-          err |= st == X_FAIL ? DE_BAD_PAYLOAD : DE_UNSUPPORTED;
-        }
-        return st;
-      });
+      // shapes the structural merge refuses: the exact tree (zb_xmerge.hpp) on the wave pipeline, where k_merge_gen
+      // runs a wave's refused merges with a lane workspace each (here a batch of 1M lanes would queue for the
+      // XLANE_GROUPS lane groups: 38 ms per 1M-instance tick against 14 ms there, profiles/r05/exact_tree_r05k.txt)
+      if (!ok || unsup) err |= TE_XTREE;
       gd[0] = olen;
     } else {
       err |= TE_REGEN;
@@ -950,7 +942,8 @@ __global__ void __launch_bounds__(TWG) k_traj(TrajParams P) {
   }
   if (!active) I.err = 0;
   if (I.err & TE_REGEN) atomicOr(&ctl->regen, 1u);
-  const uint32_t derr = I.err & ~(uint32_t)(TE_FALLBACK | TE_REGEN);
+  if (I.err & TE_XTREE) atomicOr(&ctl->flag, TE_FALLBACK);  // (nothing commits: the wave pipeline runs the batch)
+  const uint32_t derr = I.err & ~(uint32_t)(TE_FALLBACK | TE_REGEN | TE_XTREE);
   if (I.err & TE_FALLBACK) atomicOr(&ctl->derr, (uint32_t)DE_PROCESSING);  // count and emit passes disagree
   if (derr) atomicOr(&ctl->derr, derr);
 }
@@ -1730,7 +1723,8 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
   }
   if (!active) err = 0;
   if (err & TE_REGEN) atomicOr(&ctl->regen, 1u);
-  const uint32_t derr = err & ~(uint32_t)(TE_FALLBACK | TE_REGEN);
+  if (err & TE_XTREE) atomicOr(&ctl->flag, TE_FALLBACK);  // (nothing commits: the wave pipeline runs the batch)
+  const uint32_t derr = err & ~(uint32_t)(TE_FALLBACK | TE_REGEN | TE_XTREE);
   if (derr) atomicOr(&ctl->derr, derr);
 }
 
@@ -1883,7 +1877,8 @@ __global__ void __launch_bounds__(TWG) k_tmpl_io(TrajParams P) {
   }
   if (!active) err &= DE_LOG_FULL;  // (the range copy is the wave's: an inactive lane may see its overflow)
   if (err & TE_REGEN) atomicOr(&ctl->regen, 1u);
-  const uint32_t derr = err & ~(uint32_t)(TE_FALLBACK | TE_REGEN);
+  if (err & TE_XTREE) atomicOr(&ctl->flag, TE_FALLBACK);  // (nothing commits: the wave pipeline runs the batch)
+  const uint32_t derr = err & ~(uint32_t)(TE_FALLBACK | TE_REGEN | TE_XTREE);
   if (derr) atomicOr(&ctl->derr, derr);
 }
 

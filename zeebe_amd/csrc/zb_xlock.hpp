@@ -14,8 +14,8 @@ namespace zbg {
 
 struct XSlabs {
   uint8_t* base;    // XSLAB_COUNT x XSLAB_BYTES
-  uint32_t* locks;  // XSLAB_COUNT, 0 = free
-  uint8_t* lanes;   // XLANE_COUNT x XLANE_BYTES: one per thread of a launch (global thread id), no lock
+  uint32_t* locks;  // XSLAB_COUNT slab locks, then XLANE_GROUPS lane-group locks; 0 = free
+  uint8_t* lanes;   // XLANE_COUNT x XLANE_BYTES: XLANE_GROUPS groups of 64 lane workspaces
 };
 
 template <class F>
@@ -37,15 +37,28 @@ __device__ __forceinline__ void x_exclusive(const XSlabs& X, bool need, F&& f) {
   }
 }
 
-// The exact tree for every lane with `need`: first each in its own XLANE_BYTES workspace, all lanes at once; a pair
-// whose tree does not fit it (X_UNSUP, nothing written yet) then takes a big slab in turns (x_exclusive).
+// The exact tree for every lane with `need`: first each in a XLANE_BYTES workspace of its own, all lanes of the wave at
+// once; a pair whose tree does not fit it (X_UNSUP, nothing written yet) then takes a big slab in turns (x_exclusive).
+// The wave's lanes use the 64 workspaces of one lane group (by the wave's index in the launch, modulo XLANE_GROUPS),
+// which the wave holds for the duration: a launch of more waves than groups (a trajectory batch of 100K instances is
+// 1,563 waves) shares them, a wave waiting for its group while another wave runs its trees in it. (Indexed by the
+// global thread id instead, every thread past XLANE_COUNT took the locked big slab: 4.9 s per 100K-instance tick.)
 // f(slab, bytes, final) -> X_* status; it commits its outcome unless it returns X_UNSUP with final false.
 template <class F>
 __device__ __forceinline__ void x_run(const XSlabs& X, bool need, F&& f) {
   bool again = need;
-  if (need && X.lanes) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < XLANE_COUNT) again = f(X.lanes + t * XLANE_BYTES, XLANE_BYTES, false) == X_UNSUP;
+  const uint64_t m = (uint64_t)__ballot(need);
+  if (m && X.lanes) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t g = (uint32_t)(((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % XLANE_GROUPS);
+    uint32_t* lock = X.locks + XSLAB_COUNT + g;
+    const int l0 = __ffsll((unsigned long long)m) - 1;
+    if (lane == l0)
+      while (atomicCAS(lock, 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(4);
+    __threadfence();
+    if (need) again = f(X.lanes + ((uint64_t)g * 64 + lane) * XLANE_BYTES, XLANE_BYTES, false) == X_UNSUP;
+    __threadfence();
+    if (lane == l0) atomicExch(lock, 0u);
   }
   x_exclusive(X, again, [&](uint8_t* slab) { (void)f(slab, XSLAB_BYTES, true); });
 }

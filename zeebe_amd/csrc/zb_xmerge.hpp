@@ -23,10 +23,13 @@ namespace zbg {
 
 constexpr uint32_t XSLAB_BYTES = 4u << 20;  // workspace of one document pair
 constexpr uint32_t XSLAB_COUNT = 32;        // pairs in flight (zb_xlock.hpp: one lock per slab)
-// every lane of a launch (up to XLANE_COUNT) first tries its pair in a small workspace of its own, concurrently: 32 KB
-// holds the tree of ~140 tokens (2 x source + target), the documents of a typical job / message payload merge
+// every lane first tries its pair in a small workspace of its own (XLANE_COUNT of them, held 64 at a time by a wave:
+// zb_xlock.hpp x_run): 32 KB holds the tree of ~140 tokens (2 x source + target), the documents of a typical job /
+// message payload merge
 constexpr uint32_t XLANE_BYTES = 32u << 10;
-constexpr uint32_t XLANE_COUNT = 16384;
+constexpr uint32_t XLANE_COUNT = 32768;  // (1 GiB; k_merge_gen's grid: 128 workgroups of 256 lanes)
+constexpr uint32_t XLANE_GROUPS = XLANE_COUNT / 64;          // lane groups (one wave's 64 workspaces)
+constexpr uint32_t XLOCK_COUNT = XSLAB_COUNT + XLANE_GROUPS;  // slab locks, then lane-group locks
 
 // node types (MsgPackTree.nodeTypeMap values; XT_NONE = no entry)
 enum : uint8_t { XT_NONE = 0, XT_EXISTING_LEAF = 1, XT_EXTRACTED_LEAF = 2, XT_MAP = 3, XT_ARRAY = 4 };
