@@ -138,16 +138,19 @@ def _simple_workflow():
     return bpmn.Bpmn.create_executable_process("simple").start_event().end_event().done().to_xml()
 
 
-@pytest.mark.parametrize("shape", ["c3", "uniform"])
+@pytest.mark.parametrize("shape", ["c3", "c3_100k", "uniform"])
 def test_template_drain_matches_descriptor_drain(shape):
-    if shape == "c3":
+    """c3_200k: past the first 65536 instances (keys / positions >= 2^16) the size pass takes the class formula
+    (k_tdrain_sizes) instead of resolving every record (k_tdrain_size): both parts in one batch."""
+    if shape.startswith("c3"):
         cfg = workloads.CONFIGS["c3"]
-        blob, offs = cfg["payloads"](30000)
+        n_inst = 100000 if shape == "c3_100k" else 30000
+        blob, offs = workloads.xor_payloads_np(n_inst)
 
         def make(e):
             e.deploy(cfg["workflow"]().to_xml(), 100, 1)
             e.create_packed(cfg["process"], blob, offs)
-            return 30000
+            return n_inst
     else:
         blob, offs = workloads.order_payloads(7000)
 

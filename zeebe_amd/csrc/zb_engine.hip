@@ -232,6 +232,7 @@ struct zb_engine {
   TmplRec* t_tmpl = nullptr;     // [CLS_MAX][CLS_ROW][TF] traced records (uniform / class batches)
   uint32_t* t_cstat = nullptr;   // [CLS_MAX][TSTAT]
   uint64_t* c_mask = nullptr;
+  uint64_t* c_cg = nullptr;     // [groups][CLS_MAX][2] CREATE payload bytes per wave and class (k_cls_masks)
   uint32_t *c_woffw = nullptr, *c_wgcnt = nullptr, *c_wgoff = nullptr, *c_perm = nullptr;
   uint32_t *c_segs = nullptr, *c_wcls = nullptr;
 
@@ -615,11 +616,12 @@ uint64_t cls_slot_bound(uint64_t n, uint64_t nwg) {
 int grow_class_buffers(zb_engine* e, uint64_t n, uint64_t nwg) {
   if (n <= e->cls_cap) return ZB_OK;
   void* ps[] = {e->c_ikey, e->c_clen, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm, e->c_segs,
-                e->c_wcls};
+                e->c_wcls, e->c_cg};
   for (void* q : ps)
     if (q) (void)hipFree(q);
   e->c_ikey = nullptr; e->c_clen = nullptr; e->c_khist = e->c_krep = nullptr; e->c_klen = nullptr; e->c_mask = nullptr;
   e->c_woffw = e->c_wgcnt = e->c_wgoff = e->c_perm = e->c_segs = e->c_wcls = nullptr;
+  e->c_cg = nullptr;
   e->cls_cap = 0;
   const uint64_t groups = nwg * (TRAJ_WG / 64);
   // per-instance arrays hold cls_cap = nwg * TRAJ_WG entries: a later batch of up to that many instances reuses them
@@ -630,6 +632,7 @@ int grow_class_buffers(zb_engine* e, uint64_t n, uint64_t nwg) {
   e->c_krep = e->c_khist + CLS_HB * 256;
   e->c_klen = (uint64_t*)(e->c_khist + 2 * CLS_HB * 256);
   HIPCHECK(e, hipMalloc(&e->c_mask, groups * CLS_MAX * sizeof(uint64_t)));
+  HIPCHECK(e, hipMalloc(&e->c_cg, groups * CLS_MAX * 2 * sizeof(uint64_t)));
   HIPCHECK(e, hipMalloc(&e->c_woffw, groups * CLS_MAX * sizeof(uint32_t)));
   HIPCHECK(e, hipMalloc(&e->c_wgcnt, nwg * CLS_MAX * sizeof(uint32_t)));
   HIPCHECK(e, hipMalloc(&e->c_wgoff, nwg * CLS_MAX * sizeof(uint32_t)));
@@ -739,6 +742,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
     p.klen = e->c_klen;
     p.krep = e->c_krep;
     p.cmask = e->c_mask;
+    p.cg = e->c_cg;
     p.woffw = e->c_woffw;
     p.wgcnt = e->c_wgcnt;
     p.wgoff = e->c_wgoff;
@@ -1430,7 +1434,7 @@ void zb_engine_destroy(zb_engine* e) {
                 e->sort_tmp, e->d_spread, e->mapres, e->map_ws, e->log_mem, e->links_mem, e->srcd_mem, e->row_mem, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
                 e->merge_jobs, e->merge_slow, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
-                e->c_plan, e->c_ikey, e->c_clen, e->c_khist, e->c_mask, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
+                e->c_plan, e->c_ikey, e->c_clen, e->c_khist, e->c_mask, e->c_cg, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
                 e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->look_keys, e->look_idx,
                 e->conf_first, e->xslab, e->xlocks, e->xlane, e->phase};
   for (void* p : ps)
@@ -2660,7 +2664,15 @@ static int serialize_deferred(zb_engine* e, int64_t start, int64_t count, zb_ser
     HIPCHECK(e, hipMemsetAsync(e->td_flags, 0, 4 * sizeof(uint32_t), e->stream));
     HIPCHECK(e, hipMemsetAsync(e->td_wbytes + (ent - 1), 0, sizeof(uint64_t), e->stream));
     HIPCHECK(e, hipEventRecord(e->dr_ev[0], e->stream));
-    launch_tdrain_size(d, e->stream);
+    // a class batch without job keys: the workgroups whose every key encodes in 5 bytes get their sizes from the
+    // per-wave class counts and CREATE payload sums (k_tdrain_sizes); the first ones (keys / positions below 2^16)
+    // resolve every record (k_tdrain_size)
+    uint32_t wg0 = (uint32_t)p.nwg;
+    if (p.cls && !d.jobs && d.len5_ok) {
+      const int64_t thr = std::max<int64_t>(65536 - p.log_base, (65536 - p.wf_start + 4) / 5);
+      wg0 = (uint32_t)std::min<int64_t>(p.nwg, (std::max<int64_t>(thr, 0) + TRAJ_WG - 1) / TRAJ_WG);
+    }
+    launch_tdrain_size(d, wg0, e->stream);
     HIPCHECK(e, hipEventRecord(e->dr_ev[1], e->stream));
     size_t tmp = e->td_tmp_cap;
     if (hipcub::DeviceScan::ExclusiveSum(e->td_tmp, tmp, e->td_wbytes, e->td_woffs, (int)ent, e->stream) != hipSuccess)

@@ -305,6 +305,67 @@ __global__ void __launch_bounds__(TD_WG) k_tdrain_size(TDrainParams D) {
   if (threadIdx.x == 0) D.pay_part[blockIdx.x] = s_pay[0] + s_pay[1] + s_pay[2] + s_pay[3];
 }
 
+// The sizes of a class batch whose every key / position encodes in 5 bytes, with no record resolved: a class-c
+// instance's value bytes in generation w are the class's constant part (per record: element constant + 5-byte keys,
+// a static payload's binary) plus, per record that carries the CREATE payload, that payload as binary -- so a wave's
+// bytes are sum_c (instances of c) x const[c][w] + creates[c][w] x (the wave's class-c CREATE binary lengths), from
+// k_cls_masks' per-wave class masks and sums. One thread per instance workgroup (its four waves), workgroups
+// [wg0, nwg); what k_tdrain_size writes: wbytes[w][wave] and the workgroup's payload bytes.
+__global__ void __launch_bounds__(256) k_tdrain_sizes(TDrainParams D, uint32_t wg0) {
+  __shared__ uint32_t s_cs[TD_MAX_CW], s_m[TD_MAX_CW], s_sp[TD_MAX_CW];
+  const TrajParams& P = D.t;
+  const uint32_t nc = D.nc, W = D.wmax;
+  for (uint32_t e = threadIdx.x; e < nc * W; e += 256) {
+    const uint32_t c = e / W, w = e % W;
+    const uint64_t row = (uint64_t)c * CLS_ROW + w;
+    const uint32_t nrec = w < P.wcount[c] ? (uint32_t)(P.agg[row] & 0xffff) : 0u;
+    uint32_t cs = 0, m = 0, sp = 0;
+    for (uint32_t k = 0; k < nrec && k < (uint32_t)TF; k++) {
+      const TmplRec t = P.tmpl[row * TF + k];
+      const ValueConst vc = P.vconst[t.elem];
+      cs += (kind_vt(t.kind) == ZB_VT_JOB ? vc.job : vc.wf) + td_len5(t.inst) + td_len5(t.scope);
+      if (t.payload == PAY_CREATE) {
+        m += 1;
+      } else {
+        const uint32_t pl = arena_len(P.arena, t.payload);
+        cs += mp_bin_len(pl);
+        sp += pl;
+      }
+    }
+    s_cs[e] = cs;
+    s_m[e] = m;
+    s_sp[e] = sp;
+  }
+  __syncthreads();
+  const uint64_t g = (uint64_t)wg0 + (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (uint64_t)P.nwg) return;
+  uint64_t pay = 0;
+  for (int v = 0; v < TD_WG / 64; v++) {
+    const uint64_t wave = g * (TD_WG / 64) + v, grp = wave * CLS_MAX;
+    uint32_t n[CLS_MAX];
+    uint64_t gb[CLS_MAX], pb[CLS_MAX];
+#pragma unroll
+    for (int c = 0; c < CLS_MAX; c++) {
+      const bool in = c < (int)nc;
+      n[c] = in ? (uint32_t)__builtin_popcountll(P.cmask[grp + c]) : 0u;
+      gb[c] = in ? P.cg[2 * (grp + c)] : 0ull;
+      pb[c] = in ? P.cg[2 * (grp + c) + 1] : 0ull;
+    }
+    for (uint32_t w = 0; w < W; w++) {
+      uint64_t b = 0;
+#pragma unroll
+      for (int c = 0; c < CLS_MAX; c++) {
+        if (c >= (int)nc) break;
+        const uint32_t e = c * W + w;
+        b += (uint64_t)n[c] * s_cs[e] + (uint64_t)s_m[e] * gb[c];
+        pay += (uint64_t)s_m[e] * pb[c] + (uint64_t)n[c] * s_sp[e];
+      }
+      D.wbytes[(uint64_t)w * D.nwave + wave] = b;
+    }
+  }
+  D.pay_part[g] = pay;
+}
+
 template <uint32_t IMG>
 __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4))) k_tdrain_write(TDrainParams D) {
   __shared__ __attribute__((aligned(16))) uint8_t s_img[TD_WG / 64][IMG + 16];
@@ -369,9 +430,11 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
         uint64_t* dh = (uint64_t*)(D.headers + (G.pos0 + k - D.start));
         const uint64_t meta = (uint64_t)kind_rt(d.kind) | (uint64_t)kind_vt(d.kind) << 8 | (uint64_t)d.intent << 16 |
                               255ull << 24 | (uint64_t)(k ? vl1 : vl0) << 32;  // (no rejections: k_tmpl_decide)
+#ifndef ZB_EXP_NO_HEADERS  // (measurement variants only: tools/ab_variant.sh)
         __builtin_nontemporal_store((uint64_t)d.key, dh);
         __builtin_nontemporal_store(meta, dh + 1);
         __builtin_nontemporal_store(wbase + rel + (k ? vl0 : 0), dh + 2);
+#endif
       }
       // rounds: lanes [a, b) whose values fit the image from the round's first byte; each lane encodes its own
       // records (no redistribution: a generation of C3 is one round of every lane)
@@ -386,7 +449,11 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
           bad = 1;
           break;
         }
+#ifdef ZB_EXP_NO_ENCODE
+        if (false) {
+#else
         if (fit && mine) {
+#endif
 #pragma unroll 1
           for (uint32_t k = 0; k < G.nrec; k++) {
             const zb_rec d = k ? d1 : d0;
@@ -404,7 +471,9 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
         }
         const uint32_t hi = __builtin_amdgcn_readlane(incl, b - 1);
         wave_lds_sync();
+#ifndef ZB_EXP_NO_STREAM
         wave_stream(img, D.out, wbase + lo, sh, hi - lo, lane);
+#endif
         wave_lds_sync();  // the image is reused by the next round
         a = b;
       }
@@ -463,8 +532,10 @@ void launch_tmpl_decide(const TrajParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_tmpl_decide, dim3(1), dim3(256), 0, s, p);
 }
 
-void launch_tdrain_size(const TDrainParams& d, hipStream_t s) {
-  hipLaunchKernelGGL(k_tdrain_size, dim3((unsigned)d.t.nwg), dim3(TD_WG), td_layout(d, false).total, s, d);
+void launch_tdrain_size(const TDrainParams& d, uint32_t wg0, hipStream_t s) {
+  if (wg0) hipLaunchKernelGGL(k_tdrain_size, dim3(wg0), dim3(TD_WG), td_layout(d, false).total, s, d);
+  const uint64_t rest = (uint64_t)d.t.nwg - wg0;
+  if (rest) hipLaunchKernelGGL(k_tdrain_sizes, dim3((unsigned)((rest + 255) / 256)), dim3(256), 0, s, d, wg0);
 }
 void launch_tdrain_write(const TDrainParams& d, hipStream_t s) {
   hipLaunchKernelGGL((k_tdrain_write<TD_IMG>), dim3((unsigned)d.t.nwg), dim3(TD_WG), td_layout(d, true).total, s, d);

@@ -1378,7 +1378,15 @@ __global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
     if (((len + 11) & ~7u) <= CL_STRIDE * 4) {  // (stage_copy writes whole 8-byte words)
       stage_copy(pp, len, s_doc + t * CL_STRIDE);
       const uint8_t* doc = (const uint8_t*)(s_doc + t * CL_STRIDE) + 4;
+#if defined(ZB_EXP_CLS_NOEVAL)  // (measurement variants only: tools/ab_variant.sh)
+      Extract ext;
+      extract_fast(P, doc, len, ext);
+      key = ext.ok ? (ext.meta[0] & 1) : 0;
+#elif defined(ZB_EXP_CLS_COPYONLY)
+      key = doc[len - 1] & 1;
+#else
       key = P.cls_nq ? outcome_key<true>(P, doc, len) : outcome_key<false>(P, doc, len);
+#endif
     } else {
       for (int k = 0; k < P.nsplits; k++) key += (elem_ctl(P, P.split_elem[k]).cond_count() + 1) * P.split_stride[k];
     }
@@ -1458,10 +1466,18 @@ __global__ void __launch_bounds__(TWG) k_cls_masks(TrajParams P) {
   const int64_t i = (int64_t)blockIdx.x * TWG + t;
   const uint32_t c = i < P.n ? pl->cid[P.ikey[i]] : 0xffu;
   const uint64_t grp = ((uint64_t)blockIdx.x * (TWG / 64) + wv) * CLS_MAX;
+  // (the template drain's size formula: per class the CREATE payloads' binary lengths and byte counts)
+  const uint32_t cl = i < P.n ? P.clen[i] : 0u;
+  const uint64_t bl = (uint64_t)cl + (cl < 256 ? 2 : cl < 65536 ? 3 : 5);  // mp_bin_len
   for (uint32_t k = 0; k < nc; k++) {
     const uint64_t m = __ballot(c == k);
+    uint64_t g = c == k ? bl : 0, q = c == k ? (uint64_t)cl : 0;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) { g += __shfl_xor(g, d, 64); q += __shfl_xor(q, d, 64); }
     if (lane == 0) {
       P.cmask[grp + k] = m;
+      P.cg[2 * (grp + k)] = g;
+      P.cg[2 * (grp + k) + 1] = q;
       s_cnt[wv][k] = (uint32_t)__builtin_popcountll(m);
     }
   }
