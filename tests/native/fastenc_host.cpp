@@ -63,4 +63,37 @@ long fastenc(int vt, int intent, int64_t inst_key, int64_t scope_key, int64_t wf
   fast_encode(w, d, tab.data(), (const uint8_t*)seg_words.data(), doc, pre);
   return w.n();
 }
+
+// Encodes one message-side record (WORKFLOW_INSTANCE_SUBSCRIPTION / MESSAGE_SUBSCRIPTION / MESSAGE) with
+// fast_encode_msg. blob: the record's arena blob (8-aligned, padded; a WIS record's payload document), msg: the
+// element's message name (WIS). Returns the encoded length, -1 when the kind is not a fast message kind.
+long fastenc_msg(int vt, int64_t inst_key, int64_t scope_key, const uint8_t* msg, uint32_t msg_len,
+                 const uint64_t* blob, uint32_t blob_words, uint8_t* out, uint32_t head) {
+  static uint8_t pool[1 << 16];
+  std::memset(pool, 0xcd, sizeof(pool));
+  std::memcpy(pool, msg, msg_len);
+  DevElem e{};
+  e.kind = EK_CATCH;
+  e.wf = 0;
+  e.msg_off = 0;
+  e.msg_len = (uint16_t)msg_len;
+  DevWorkflow wf{};
+  zb_rec d{};
+  d.inst_key = inst_key;
+  d.scope_key = scope_key;
+  d.elem = 0;
+  d.kind = make_kind((uint8_t)vt, ZB_RT_EVENT, false);
+  if (!fast_msg_kind(d)) return -1;
+  std::vector<DevValSeg> tab;
+  std::vector<uint8_t> segs;
+  if (!build_value_segments(&e, 1, &wf, 1, pool, tab, segs)) return -2;
+  std::vector<uint64_t> seg_words((segs.size() + 7) / 8);
+  std::memcpy(seg_words.data(), segs.data(), segs.size());
+  uint64_t pre[SER_PRE];
+  for (int j = 0; j < SER_PRE; j++) pre[j] = (uint32_t)j < blob_words ? blob[j] : 0xa5a5a5a5a5a5a5a5ull;
+  FastWT<true> w;
+  w.begin(out, head);
+  fast_encode_msg(w, d, tab.data(), (const uint8_t*)seg_words.data(), blob, pre);
+  return w.n();
+}
 }

@@ -20,6 +20,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 NATIVE = os.path.join(HERE, "native")
 CSRC = os.path.join(HERE, "..", "zeebe_amd", "csrc")
 VT_JOB, VT_WI = 0, 5
+VT_MSG, VT_MSG_SUB, VT_WIS = 10, 11, 12
 GUARD = 0xEE
 
 
@@ -34,6 +35,9 @@ def lib():
     L.fastenc.restype = ctypes.c_long
     L.fastenc.argtypes = ([ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
                            ctypes.c_int32, ctypes.c_char_p] + [ctypes.c_uint32] * 9 + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32])
+    L.fastenc_msg.restype = ctypes.c_long
+    L.fastenc_msg.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p, ctypes.c_uint32,
+                              ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
     return L
 
 
@@ -112,3 +116,54 @@ def test_fast_kind_excludes_cancel(lib):
         n = lib.fastenc(VT_JOB, intent, 1, 1, 1, 1, 3, b"x", 1, 0, 1, 0, 1, 0, 1, 0xFFFFFFFF, 0,
                         ctypes.create_string_buffer(16), ctypes.create_string_buffer(256), 0)
         assert n == -1
+
+
+def encode_msg(lib, vt, inst, scope, msg, blob, head):
+    """One message-side value through fast_encode_msg (checked stores): bytes, and nothing stored outside them."""
+    blob = blob + b"\0" * (-len(blob) % 8) + b"\xa5" * 64  # padded to 8, then whatever follows in the arena
+    bbuf = ctypes.create_string_buffer(blob, len(blob))
+    cap = (4096 + len(blob) + 7) // 8 * 8
+    out = (ctypes.c_uint64 * (cap // 8))()
+    ctypes.memset(out, GUARD, cap)
+    n = lib.fastenc_msg(vt, inst, scope, msg, len(msg), bbuf, len(blob) // 8, out, head)
+    raw = bytes(out)
+    assert n > 0
+    assert all(b == GUARD for b in raw[:head]), "store before the value start (the previous lane's bytes)"
+    assert all(b == GUARD for b in raw[head + n:]), "store past the value end"
+    return raw[head:head + n]
+
+
+def test_fast_encoder_message_kinds_fuzz(lib):
+    """WorkflowInstanceSubscriptionRecord.java:26-38, MessageSubscriptionRecord.java:26-41, MessageRecord.java:26-42
+    (the layouts encode_value writes), from the arena blobs zb_msg.hpp reads (SubView / MsgView)."""
+    r = random.Random(17)
+    for it in range(3000):
+        inst, scope = rand_int(r), rand_int(r)
+        head = r.randrange(24)
+        kind = it % 3
+        if kind == 0:
+            msg = rand_str(r).encode()
+            payload = bytes(r.randrange(256) for _ in range(r.choice([0, 1, 7, 8, 9, 43, 44, 45, 100, 300, 70000])))
+            blob = struct.pack("<I", len(payload)) + payload
+            got = encode_msg(lib, VT_WIS, inst, scope, msg, blob, head)
+            want = msgpack.packb({"workflowInstanceKey": inst, "activityInstanceKey": scope, "messageName": msg.decode(),
+                                  "payload": payload}, use_bin_type=True)
+        elif kind == 1:
+            name, ck = rand_str(r).encode(), rand_str(r).encode()
+            wfp = r.choice([0, 1, 7, 127, 128, 255, 256, 65535, 65536, 2 ** 31 - 1])
+            blob = struct.pack("<IiIH2xII", 24 + len(name) + len(ck), wfp, r.randrange(2 ** 32), r.randrange(2 ** 16),
+                               len(name), len(ck)) + name + ck
+            got = encode_msg(lib, VT_MSG_SUB, inst, scope, b"", blob, head)
+            want = msgpack.packb({"workflowInstancePartitionId": wfp, "workflowInstanceKey": inst,
+                                  "activityInstanceKey": scope, "messageName": name.decode(),
+                                  "correlationKey": ck.decode()}, use_bin_type=True)
+        else:
+            name, ck, mid = rand_str(r).encode(), rand_str(r).encode(), rand_str(r).encode()
+            payload = bytes(r.randrange(256) for _ in range(r.choice([0, 1, 5, 8, 13, 64, 255, 256, 1000])))
+            ttl = rand_int(r)
+            blob = (struct.pack("<IIqqIII4x", 40 + len(name) + len(ck) + len(payload) + len(mid), len(name), ttl,
+                                r.randrange(2 ** 40), len(ck), len(payload), len(mid)) + name + ck + payload + mid)
+            got = encode_msg(lib, VT_MSG, inst, scope, b"", blob, head)
+            want = msgpack.packb({"name": name.decode(), "correlationKey": ck.decode(), "timeToLive": ttl,
+                                  "payload": payload, "messageId": mid.decode()}, use_bin_type=True)
+        assert got == want, (it, kind, head)

@@ -91,6 +91,30 @@ def test_mixed_kinds_fast_drain_matches_generic():
     _compare(make)
 
 
+def test_message_kinds_fast_drain_matches_generic():
+    """Message correlation on one partition (its outbox delivered to its own inbox): WORKFLOW_INSTANCE_SUBSCRIPTION,
+    MESSAGE_SUBSCRIPTION and MESSAGE records (fast_encode_msg) interleaved with WORKFLOW_INSTANCE ones in every tile,
+    published messages that correlate, that are stored and that expire."""
+    from zeebe_amd import cluster
+
+    xml = (bpmn.Bpmn.create_executable_process("wf").start_event()
+           .intermediate_catch_event("catch-event", message="order canceled", correlation_key="$.orderId")
+           .sequence_flow_id("to-end").end_event().done().to_xml())
+
+    def make(e):
+        e.deploy(xml, 100, 1)
+        c = cluster.LocalCluster([e])
+        e.create("wf", [msgpack.packb({"orderId": "order-%d" % i, "pad": "p" * (i % 40)}) for i in range(3000)])
+        c.settle()
+        c.publish(b"order canceled", [b"order-%d" % i for i in range(0, 3000, 2)],
+                  [msgpack.packb({"n": i, "s": "x" * (i % 70)}) for i in range(0, 3000, 2)])
+        c.publish(b"order canceled", [b"nobody-%d" % i for i in range(200)], [b"\x80"] * 200)
+        c.publish(b"order canceled", [b"late-%d" % i for i in range(100)], [b"\x80"] * 100, ttl=0)
+
+    sf = _compare(make)
+    assert sf["generic_tiles"] * 4 < (sf["records"] + 255) // 256  # (tiles with submitted commands stay generic)
+
+
 def test_size_pass_formula_matches_encoder():
     # records without a length from their emitting kernel (the wave pipeline writes none) are sized by the
     # size pass: WORKFLOW_INSTANCE / JOB records by the emit kernels' formula, unless ZB_CFG_VLEN_CHECK, which

@@ -13,6 +13,7 @@ import bench_steady  # noqa: E402
 from zeebe_amd import engine as zbe  # noqa: E402
 
 ROWS = []
+MEM = []
 
 
 def main():
@@ -25,6 +26,10 @@ def main():
         st = step0(self, *a, **k)
         ROWS.append(("step", (time.perf_counter() - t) * 1e3, st["wall_ms"], st["wave_kernel_ms"], st["launches"],
                      st["waves"]))
+        m = self.memory_stats()
+        MEM.append("arena_used %.0f MB of %.0f, rows %d, compactions %d" % (m["arena_used"] / 2**20,
+                                                                          m["arena_bytes"] / 2**20,
+                                                                          m["rows_allocated"], m["compactions"]))
         return st
 
     @functools.wraps(ser0)
@@ -42,6 +47,8 @@ def main():
     print("%-10s %9s %9s %9s %8s %6s" % ("call", "py ms", "wall ms", "kernel ms", "launches", "waves"))
     for r in ROWS[-2 * ticks:]:
         print("%-10s %9.3f %9.3f %9.3f %8d %6d" % r)
+    for m in MEM[-ticks - 2:]:
+        print(m)
 
 
 if __name__ == "__main__":

@@ -72,6 +72,12 @@ __device__ __forceinline__ void mark_granules(const CompactParams& P, uint64_t g
   }
 }
 
+// bitmap index of a granule: [static, arena_next) and [arena_top, arena_end) back to back (the free gap between them
+// has no bits)
+__device__ __forceinline__ uint64_t bit_of(const CompactParams& P, uint64_t ref) {
+  const uint64_t g = ref - P.static_refs, lo = P.arena_next / 8 - P.static_refs;
+  return g < lo ? g : g - (P.arena_top - P.arena_next) / 8;
+}
 // a byte range of an allocated blob: in [static, arena_next) or in the staged documents' [arena_top, arena_end)
 __device__ __forceinline__ bool arena_span(const CompactParams& P, uint64_t b0, uint64_t b1) {
   return (b0 >= P.static_refs * 8 && b1 <= P.arena_next) || (b0 >= P.arena_top && b1 <= P.arena_end);
@@ -88,7 +94,7 @@ __device__ __forceinline__ void mark_ref(const CompactParams& P, uint32_t ref, i
       atomicOr(P.err, (uint32_t)DE_CORRUPT);
       return;
     }
-    mark_granules(P, (uint64_t)ref - P.static_refs, n);
+    mark_granules(P, bit_of(P, ref), n);
     ref += (uint32_t)n;
   }
 }
@@ -120,7 +126,7 @@ __global__ void __launch_bounds__(256) k_word_pop(CompactParams P) {
 // marked ones
 __device__ __forceinline__ uint32_t renamed(const CompactParams& P, uint32_t ref) {
   if (!arena_span(P, (uint64_t)ref * 8, (uint64_t)ref * 8 + 8)) return ref;
-  const uint64_t g = (uint64_t)ref - P.static_refs;
+  const uint64_t g = bit_of(P, ref);
   const uint64_t w = g >> 6, b = g & 63;
   const uint64_t below = b ? (P.bits[w] & ((1ull << b) - 1)) : 0;
   return (uint32_t)(P.static_refs + P.word_off[w] + (uint64_t)__popcll((unsigned long long)below));
@@ -133,12 +139,13 @@ __global__ void __launch_bounds__(256) k_arena_gather(CompactParams P) {
   const uint64_t* src = (const uint64_t*)(P.arena + P.static_refs * 8);
   uint64_t* dst = (uint64_t*)P.scratch;
   const uint64_t ng = P.words * 64;
+  const uint64_t lo = P.arena_next / 8 - P.static_refs, gap = (P.arena_top - P.arena_next) / 8;
   for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < ng; g += stride) {
     const uint64_t w = g >> 6, b = g & 63;
     const uint64_t word = P.bits[w];
     if (!((word >> b) & 1)) continue;
     const uint64_t below = b ? (word & ((1ull << b) - 1)) : 0;
-    dst[P.word_off[w] + (uint64_t)__popcll((unsigned long long)below)] = src[g];
+    dst[P.word_off[w] + (uint64_t)__popcll((unsigned long long)below)] = src[g < lo ? g : g + gap];
   }
 }
 

@@ -232,7 +232,7 @@ struct zb_engine {
   TmplRec* t_tmpl = nullptr;     // [CLS_MAX][CLS_ROW][TF] traced records (uniform / class batches)
   uint32_t* t_cstat = nullptr;   // [CLS_MAX][TSTAT]
   uint64_t* c_mask = nullptr;
-  uint64_t* c_cg = nullptr;     // [groups][CLS_MAX][2] CREATE payload bytes per wave and class (k_cls_masks)
+  uint32_t* c_cg = nullptr;     // [groups][CLS_MAX][2] CREATE payload bytes per wave and class (k_cls_masks)
   uint32_t *c_woffw = nullptr, *c_wgcnt = nullptr, *c_wgoff = nullptr, *c_perm = nullptr;
   uint32_t *c_segs = nullptr, *c_wcls = nullptr;
 
@@ -632,7 +632,7 @@ int grow_class_buffers(zb_engine* e, uint64_t n, uint64_t nwg) {
   e->c_krep = e->c_khist + CLS_HB * 256;
   e->c_klen = (uint64_t*)(e->c_khist + 2 * CLS_HB * 256);
   HIPCHECK(e, hipMalloc(&e->c_mask, groups * CLS_MAX * sizeof(uint64_t)));
-  HIPCHECK(e, hipMalloc(&e->c_cg, groups * CLS_MAX * 2 * sizeof(uint64_t)));
+  HIPCHECK(e, hipMalloc(&e->c_cg, groups * CLS_MAX * 2 * sizeof(uint32_t)));
   HIPCHECK(e, hipMalloc(&e->c_woffw, groups * CLS_MAX * sizeof(uint32_t)));
   HIPCHECK(e, hipMalloc(&e->c_wgcnt, nwg * CLS_MAX * sizeof(uint32_t)));
   HIPCHECK(e, hipMalloc(&e->c_wgoff, nwg * CLS_MAX * sizeof(uint32_t)));
@@ -1061,24 +1061,20 @@ int reserve_compaction(zb_engine* e) {
   return rc;
 }
 
-// The gather scratch, at a compaction: room for what this one can gather (the allocated rows, the used dynamic arena)
-// doubled, capped at the capacities -- an engine that never compacts holds none, and one that keeps growing
-// reallocates it a few times, not at every compaction. (Reserved for the whole arena at creation, it doubled a large
-// partition's device memory.)
+// The gather scratch: reserved at the partition's first compaction for its capacities (the row table, the dynamic
+// arena) -- grown on demand it was reallocated, each time a device-wide synchronisation, at the first compactions of a
+// growing partition (C2 steady state: 0.6-1.2 ms of a 1.6-2.0 ms compaction). An engine that never compacts holds
+// none. (At creation, for every engine, it doubled a large partition's device memory.)
 int reserve_gather(zb_engine* e) {
-  const uint64_t row_bytes = ROW_BYTES + sizeof(RowAux);
+  const uint64_t row_bytes = sizeof(RowMeta) + sizeof(RowKeys) + sizeof(RowAux);
   const uint64_t full = std::max<uint64_t>(e->cfg.row_capacity * row_bytes, e->cfg.arena_bytes - STATIC_ARENA_BYTES);
-  const uint64_t need = std::max<uint64_t>((uint64_t)e->host_hdr.rows_next * row_bytes,
-                                           (uint64_t)e->host_hdr.arena_next - STATIC_ARENA_BYTES +
-                                               (e->cfg.arena_bytes - e->arena_top));
-  if (e->c_scratch && e->c_scratch_cap >= need) return ZB_OK;
-  const uint64_t c = std::max<uint64_t>(std::min<uint64_t>(2 * need, full), std::max<uint64_t>(need, 1 << 20));
+  if (e->c_scratch && e->c_scratch_cap >= full) return ZB_OK;
   HIPCHECK(e, hipStreamSynchronize(e->stream));
   if (e->c_scratch) (void)hipFree(e->c_scratch);
   e->c_scratch = nullptr;
   e->c_scratch_cap = 0;
-  HIPCHECK(e, hipMalloc(&e->c_scratch, c));
-  e->c_scratch_cap = c;
+  HIPCHECK(e, hipMalloc(&e->c_scratch, full));
+  e->c_scratch_cap = full;
   return ZB_OK;
 }
 
@@ -1163,13 +1159,18 @@ int compact_state(zb_engine* e) {
     }
   }
   ZB_CT();  // messages
-  // 3. arena: blobs reachable from live rows, the unreleased log window and the stores
+  // 3. arena: blobs reachable from live rows, the unreleased log window and the stores. A batch uploaded in place
+  // but not injected yet (no record references it) is not part of it: it goes to the very top of the arena
+  // afterwards (through the scratch when it has to move), so that the allocators get everything below it back.
   c = compact_params(e);
   c.live_rows = live;
-  // (the bitmap spans the staged documents at the top too, when there are any: they move down with the rest)
-  const uint64_t dyn = (e->arena_top < e->cfg.arena_bytes ? e->cfg.arena_bytes : (uint64_t)e->host_hdr.arena_next) -
-                       STATIC_ARENA_BYTES;
+  const bool pend = e->staged_in_place && e->staged_pending;
+  const uint64_t pb = pend ? e->staged_top - e->staged_base : 0;  // its bytes
+  const bool pend_moves = pend && e->staged_base != e->cfg.arena_bytes - pb;
+  // (the bitmap spans the staged documents at the top too, after the allocated bytes: they move down with the rest)
+  const uint64_t dyn = (uint64_t)e->host_hdr.arena_next - STATIC_ARENA_BYTES + (e->cfg.arena_bytes - e->arena_top);
   const uint64_t words = (dyn / 8 + 63) / 64;
+  uint64_t granules = 0;
   if (words) {
     rc = grow(e, &e->c_bits, &e->c_bits_cap, words);
     if (rc == ZB_OK) rc = grow(e, &e->c_pop, &e->c_pop_cap, words + 1);
@@ -1179,12 +1180,17 @@ int compact_state(zb_engine* e) {
     c.bits = e->c_bits; c.word_pop = e->c_pop; c.word_off = e->c_off; c.words = words;
     launch_mark(c, e->stream);
     launch_word_pop(c, e->stream);
-    uint64_t granules = 0;
     rc = scan_u32(e, e->c_pop, e->c_off, words, &granules);
     if (rc != ZB_OK) return rc;
     ZB_CT();  // arena marking
-    rc = grow(e, &e->c_scratch, &e->c_scratch_cap, std::max<uint64_t>(granules, 1) * 8);
-    if (rc != ZB_OK) return rc;
+  }
+  const bool room = STATIC_ARENA_BYTES + granules * 8 + pb <= e->cfg.arena_bytes;
+  rc = grow(e, &e->c_scratch, &e->c_scratch_cap, std::max<uint64_t>(granules * 8 + (pend_moves && room ? pb : 0), 8));
+  if (rc != ZB_OK) return rc;
+  if (pend_moves && room)  // (stashed before the live bytes are copied back over the region it may lie in)
+    HIPCHECK(e, hipMemcpyAsync(e->c_scratch + granules * 8, e->arena + e->staged_base, pb, hipMemcpyDeviceToDevice,
+                               e->stream));
+  if (words) {
     c.scratch = e->c_scratch;
     launch_arena_gather(c, e->stream);
     launch_rename(c, e->stream);
@@ -1192,17 +1198,16 @@ int compact_state(zb_engine* e) {
       HIPCHECK(e, hipMemcpyAsync(e->arena + STATIC_ARENA_BYTES, e->c_scratch, granules * 8, hipMemcpyDeviceToDevice, e->stream));
     e->host_hdr.arena_next = (int64_t)(STATIC_ARENA_BYTES + granules * 8);
   }
-  // every live document of the top region moved down. A batch uploaded in place but not injected yet (no record
-  // references it, nothing marked or moved it) stays where it is when the compacted bytes end below it; else it is
-  // uploaded again by the step that injects it.
-  const bool keep_pending = e->staged_in_place && e->staged_pending &&
-                            (uint64_t)e->host_hdr.arena_next <= e->staged_base;
-  if (keep_pending) {
+  if (pend && room) {
+    if (pend_moves)
+      HIPCHECK(e, hipMemcpyAsync(e->arena + e->cfg.arena_bytes - pb, e->c_scratch + granules * 8, pb,
+                                 hipMemcpyDeviceToDevice, e->stream));
+    e->staged_base = e->cfg.arena_bytes - pb;
+    e->staged_top = e->cfg.arena_bytes;
     e->arena_top = e->staged_base;
-    e->staged_top = e->cfg.arena_bytes;  // (a re-upload of the batch gives everything above it back)
   } else {
     e->arena_top = e->cfg.arena_bytes;
-    if (e->staged_in_place) {
+    if (e->staged_in_place) {  // (no room beside the live bytes: the step that injects it uploads it again)
       e->staged_in_place = false;
       e->staged_uploaded = false;
     }
@@ -1322,6 +1327,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (e->cfg.row_capacity == 0) e->cfg.row_capacity = 1ull << 20;
   if (e->cfg.arena_bytes == 0) e->cfg.arena_bytes = 64ull << 20;
   if (e->cfg.arena_bytes < 2 * STATIC_ARENA_BYTES) e->cfg.arena_bytes = 2 * STATIC_ARENA_BYTES;
+  e->cfg.arena_bytes &= ~7ull;  // (whole 8-byte granules: refs are granule indexes, documents sit at its top)
   if (e->cfg.partition_count <= 0) e->cfg.partition_count = 1;
   if (e->cfg.log_capacity >= (1ull << 40) || e->cfg.row_capacity >= 0xffffffffull ||
       e->cfg.arena_bytes >= (8ull << 32)) {

@@ -18,7 +18,11 @@ namespace zbg {
 // from the LDS copy of the pool with aligned b64 reads, payload documents are copied as 8-byte words.
 // Same bytes as encode_value: the GPU tests compare every value with the oracle's, and
 // tests/test_fastenc_host.py fuzzes this on the host with guard bytes around each value.
-struct FastW {
+// CHK: every slot store checks whether it is the value's first slot (values whose first bytes come from a
+// variable-length run -- MESSAGE records -- cannot say which put completes it); without it a value's first put is
+// marked FIRST and whole 8-byte.
+template <bool CHK = false>
+struct FastWT {
   uint8_t* img;   // LDS image base (8-aligned)
   uint32_t pos;   // image offset of the next byte
   uint32_t head;  // image offset of the value's first byte
@@ -32,6 +36,11 @@ struct FastW {
     first = 0;
   }
   __device__ __forceinline__ uint32_t n() const { return pos - head; }
+  // a whole image slot (CHK: the value's first slot is kept for end())
+  __device__ __forceinline__ void st(uint32_t slot, uint64_t v) {
+    if (CHK && (head & 7) && slot == (head & ~7u)) first = v;
+    else *(uint64_t*)(img + slot) = v;
+  }
   // bytes [b, e) of slot word v at image offset slot, with naturally aligned stores (0 <= b < e <= 8)
   __device__ __forceinline__ void part(uint32_t slot, uint64_t v, uint32_t b, uint32_t e) {
     if ((b & 1) && b < e) { img[slot + b] = (uint8_t)(v >> (8 * b)); b += 1; }
@@ -51,7 +60,7 @@ struct FastW {
     const uint64_t hi = (v >> 1) >> (63 - 8 * f);  // the bytes past the slot (0 when f == 0)
     if (f + k >= 8) {
       if (FIRST && f) first = lo;
-      else *(uint64_t*)(img + (pos - f)) = lo;
+      else st(pos - f, lo);
       acc = hi;
     } else {
       acc = lo;
@@ -120,7 +129,7 @@ struct FastW {
         if (jj == 0) v = acc | (v & own0);
         if (jj < nf) {
           if (FIRST && jj == 0 && f) first = v;
-          else *(uint64_t*)(img + slot + 8 * jj) = v;
+          else st(slot + 8 * jj, v);
         } else {
           acc = rem ? v & (~0ull >> (64 - 8 * rem)) : 0;
         }
@@ -142,7 +151,7 @@ struct FastW {
       const uint64_t x = (uint32_t)(8 * i) < n ? v[i] : 0ull;
       const uint64_t o = acc | (x << sl);
       if ((uint32_t)i < nf) {
-        *(uint64_t*)(img + slot + 8 * i) = o;
+        st(slot + 8 * i, o);
         acc = (x >> 1) >> sr;  // (f == 0: 0)
       } else {
         acc = o;
@@ -151,7 +160,34 @@ struct FastW {
     acc = rem ? acc & (~0ull >> (64 - 8 * rem)) : 0;  // slot nf: the run's last bytes
     pos += n;
   }
+  // MsgPackWriter.writeStringHeader / writeBinaryHeader
+  __device__ __forceinline__ void str_hdr(uint32_t c) {
+    if (c < 32) put(0xa0 | c, 1);
+    else if (c < 256) put(0xd9 | (uint64_t)c << 8, 2);
+    else if (c < 65536) put(0xda | (uint64_t)__builtin_bswap16((uint16_t)c) << 8, 3);
+    else put(0xdb | (uint64_t)__builtin_bswap32(c) << 8, 5);
+  }
+  __device__ __forceinline__ void bin_hdr(uint32_t c) {
+    if (c < 256) put(0xc4 | (uint64_t)c << 8, 2);
+    else if (c < 65536) put(0xc5 | (uint64_t)__builtin_bswap16((uint16_t)c) << 8, 3);
+    else put(0xc6 | (uint64_t)__builtin_bswap32(c) << 8, 5);
+  }
+  // n bytes at p in global memory, any alignment: whole 8-byte words around them are read (arena blobs are 8-aligned
+  // and padded, and the arena has ARENA_SLACK readable bytes past its end)
+  __device__ __forceinline__ void gbytes(const uint8_t* p, uint32_t n) {
+    const uint32_t a = (uint32_t)((uintptr_t)p & 7);
+    const uint64_t* q = (const uint64_t*)(p - a);
+    uint64_t cur = q[0];
+    for (uint32_t k = 0, j = 1; k < n; k += 8, j++) {
+      const uint64_t nx = a + n > k + 8 ? q[j] : 0ull;  // (the word holding bytes past k + 8 - a, when there are any)
+      const uint64_t x = a ? (cur >> (8 * a)) | (nx << (64 - 8 * a)) : cur;
+      const uint32_t r = n - k;
+      put(r < 8 ? x & (~0ull >> (64 - 8 * r)) : x, r < 8 ? r : 8);
+      cur = nx;
+    }
+  }
 };
+using FastW = FastWT<false>;
 
 constexpr int SER_PRE = 6;  // payload document words prefetched per record (length + 44 bytes)
 constexpr uint32_t ARENA_SLACK = 64;  // bytes allocated past the arena: SER_PRE words load unchecked
@@ -163,20 +199,22 @@ constexpr uint32_t ARENA_SLACK = 64;  // bytes allocated past the arena: SER_PRE
 //   JOB_A {0x87 "deadline" MIN "worker" "" "retries" r "type" t "headers" 0x86 "bpmnProcessId" pid
 //          "workflowDefinitionVersion" v "workflowKey" k "workflowInstanceKey"}
 //   JOB_B {"activityId" id "activityInstanceKey"}      JOB_C {"customHeaders" h "payload"}
+//   WIS   {"messageName" name "payload"}               (elements that subscribe to a message)
 // Each run starts 8-aligned in the segment pool and is zero-padded to 8 bytes.
-enum { SEG_WI_A = 0, SEG_WI_B, SEG_JOB_A, SEG_JOB_B, SEG_JOB_C, SEG_N };
+enum { SEG_WI_A = 0, SEG_WI_B, SEG_JOB_A, SEG_JOB_B, SEG_JOB_C, SEG_WIS, SEG_N };
 struct DevValSeg {
   uint16_t off8[SEG_N];  // offset / 8 in the segment pool
   uint16_t len[SEG_N];
 };
-static_assert(sizeof(DevValSeg) == 20, "DevValSeg is 20 bytes");
+static_assert(sizeof(DevValSeg) == 24, "DevValSeg is 24 bytes");
 constexpr uint32_t SEG_PAD_LO = 16, SEG_PAD_HI = 48;  // readable bytes before the first run / after the last
 constexpr uint32_t SEG_LDS_MAX = 16384;  // table (padded to 4 entries) + pool the fast passes copy into LDS
 
 // the payload document [u32 len][bytes] as binary (MsgPackWriter.writeBinary): doc words W_j (8-aligned), the
 // first SER_PRE already loaded (words past the document hold whatever follows it: only bytes past the payload
 // come from them, and those are masked off); payload bytes [8k, 8k + 8) = W_k >> 32 | W_(k+1) << 32
-__device__ __forceinline__ void fast_bin(FastW& w, const uint64_t* dw, const uint64_t (&pre)[SER_PRE]) {
+template <bool CHK>
+__device__ __forceinline__ void fast_bin(FastWT<CHK>& w, const uint64_t* dw, const uint64_t (&pre)[SER_PRE]) {
   const uint32_t plen = (uint32_t)pre[0];
   if (plen < 256) w.put(0xc4 | (uint64_t)plen << 8, 2);
   else if (plen < 65536) w.put(0xc5 | (uint64_t)__builtin_bswap16((uint16_t)plen) << 8, 3);
@@ -199,6 +237,13 @@ __device__ __forceinline__ void fast_bin(FastW& w, const uint64_t* dw, const uin
   }
 }
 
+// the message-side records it takes too (encode_value's WORKFLOW_INSTANCE_SUBSCRIPTION / MESSAGE_SUBSCRIPTION / MESSAGE
+// branches: fast_encode_msg); their lengths come from the size pass's dry run, not from a formula
+__device__ __forceinline__ bool fast_msg_kind(const zb_rec& d) {
+  if (d.kind & KIND_RAW) return false;
+  const uint8_t vt = kind_vt(d.kind);
+  return vt == ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION || vt == ZB_VT_MESSAGE_SUBSCRIPTION || vt == ZB_VT_MESSAGE;
+}
 __device__ __forceinline__ bool fast_kind(const zb_rec& d) {
   if (d.kind & KIND_RAW) return false;
   const uint8_t vt = kind_vt(d.kind), rt = kind_rt(d.kind);
@@ -226,6 +271,58 @@ __device__ __forceinline__ void fast_encode(FastW& w, const zb_rec& d, const Dev
     w.ival(d.scope_key);
     w.seg(segs + 8 * t.off8[SEG_JOB_C], t.len[SEG_JOB_C]);
     fast_bin(w, dw, pre);
+  }
+  w.end();
+}
+
+// The message-side values, from the record's blob (dw: its first word; zb_msg.hpp MsgView / SubView layouts) and,
+// for a WORKFLOW_INSTANCE_SUBSCRIPTION, its element's message name run and the payload document. Checked stores: a
+// MESSAGE value's first slot is completed inside its name.
+__device__ __forceinline__ void fast_encode_msg(FastWT<true>& w, const zb_rec& d, const DevValSeg* tab,
+                                                const uint8_t* segs, const uint64_t* dw,
+                                                const uint64_t (&pre)[SER_PRE]) {
+  const uint8_t vt = kind_vt(d.kind);
+  const uint8_t* b = (const uint8_t*)dw;
+  if (vt == ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION) {  // WorkflowInstanceSubscriptionRecord.java:26-38
+    const DevValSeg& t = tab[d.elem];
+    w.lit("\x84" "\xb3" "workflowInstanceKey");
+    w.ival(d.inst_key);
+    w.lit("\xb3" "activityInstanceKey");
+    w.ival(d.scope_key);
+    w.seg(segs + 8 * t.off8[SEG_WIS], t.len[SEG_WIS]);
+    fast_bin(w, dw, pre);
+  } else if (vt == ZB_VT_MESSAGE_SUBSCRIPTION) {  // MessageSubscriptionRecord.java:26-41 (SubView: wfp, names at 24)
+    const uint32_t nn = *(const uint32_t*)(b + 16), nc = *(const uint32_t*)(b + 20);
+    w.lit("\x85" "\xbb" "workflowInstancePartitionId");
+    w.ival(*(const int32_t*)(b + 4));
+    w.lit("\xb3" "workflowInstanceKey");
+    w.ival(d.inst_key);
+    w.lit("\xb3" "activityInstanceKey");
+    w.ival(d.scope_key);
+    w.lit("\xab" "messageName");
+    w.str_hdr(nn);
+    w.gbytes(b + 24, nn);
+    w.lit("\xae" "correlationKey");
+    w.str_hdr(nc);
+    w.gbytes(b + 24 + nn, nc);
+  } else {  // MessageRecord.java:26-42 (MsgView: name, correlation key, payload, id from byte 40)
+    const uint32_t nn = *(const uint32_t*)(b + 4), nc = *(const uint32_t*)(b + 24), np = *(const uint32_t*)(b + 28);
+    const uint32_t nid = *(const uint32_t*)(b + 32);
+    const uint8_t* name = b + 40;
+    w.lit("\x85" "\xa4" "name");
+    w.str_hdr(nn);
+    w.gbytes(name, nn);
+    w.lit("\xae" "correlationKey");
+    w.str_hdr(nc);
+    w.gbytes(name + nn, nc);
+    w.lit("\xaa" "timeToLive");
+    w.ival(*(const int64_t*)(b + 8));
+    w.lit("\xa7" "payload");
+    w.bin_hdr(np);
+    w.gbytes(name + nn + nc, np);
+    w.lit("\xa9" "messageId");
+    w.str_hdr(nid);
+    w.gbytes(name + nn + nc + np, nid);
   }
   w.end();
 }
@@ -289,6 +386,11 @@ inline bool build_value_segments(const DevElem* elems, size_t n_elems, const Dev
     std::vector<uint8_t> b;
     seg_key(b, "activityId"); seg_str(b, pool + e.id_off, e.id_len); seg_key(b, "payload");
     if (!add(b, t.off8[SEG_WI_B], t.len[SEG_WI_B])) return false;
+    if (e.kind == EK_CATCH) {  // (a message subscription: its WORKFLOW_INSTANCE_SUBSCRIPTION records)
+      b.clear();
+      seg_key(b, "messageName"); seg_str(b, pool + e.msg_off, e.msg_len); seg_key(b, "payload");
+      if (!add(b, t.off8[SEG_WIS], t.len[SEG_WIS])) return false;
+    }
     if (e.kind != EK_TASK) continue;  // only service tasks write JOB records
     b = {0x87};
     seg_key(b, "deadline"); seg_int(b, INT64_MIN);

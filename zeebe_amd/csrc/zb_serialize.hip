@@ -725,7 +725,8 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3))
   const uint32_t len = live ? (P0.len_in_vlen ? P0.vlen[P0.start + i] : P0.lengths[i]) : 0;
   zb_rec d{};
   if (live) d = P0.log[P0.start + i];
-  const bool fast = live && fast_kind(d);
+  const bool msg = live && fast_msg_kind(d);
+  const bool fast = (live && fast_kind(d)) || msg;
   const uint64_t* dw = (const uint64_t*)(P0.arena + (uint64_t)d.payload * 8);
   uint64_t pre[SER_PRE];
 #pragma unroll
@@ -786,9 +787,16 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3))
   for (int k = 0; k < wv; k++) stream_wave(k);
   if (live) {
     const uint64_t lo = o0 + pw;  // this wave's range starts at the tile start + the waves before it
-    FastW w;
-    w.begin(img, (uint32_t)(((uintptr_t)(P0.out + lo)) & 15) + (uint32_t)(off - lo));
-    fast_encode(w, d, (const DevValSeg*)s_model, s_model + tb, dw, pre);
+    const uint32_t at = (uint32_t)(((uintptr_t)(P0.out + lo)) & 15) + (uint32_t)(off - lo);
+    if (msg) {
+      FastWT<true> w;
+      w.begin(img, at);
+      fast_encode_msg(w, d, (const DevValSeg*)s_model, s_model + tb, dw, pre);
+    } else {
+      FastW w;
+      w.begin(img, at);
+      fast_encode(w, d, (const DevValSeg*)s_model, s_model + tb, dw, pre);
+    }
   }
   stream_wave(wv);
 #pragma unroll 1
@@ -816,7 +824,8 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
   const uint32_t len = live ? (P0.len_in_vlen ? P0.vlen[P0.start + i] : P0.lengths[i]) : 0;
   zb_rec d{};
   if (live) d = P0.log[P0.start + i];
-  const bool fast = live && fast_kind(d);
+  const bool msg = live && fast_msg_kind(d);
+  const bool fast = (live && fast_kind(d)) || msg;
   const uint64_t* dw = (const uint64_t*)(P0.arena + (uint64_t)d.payload * 8);
   uint64_t pre[SER_PRE];
 #pragma unroll
@@ -875,9 +884,15 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
     const uint64_t fm = __ballot(fit);
     const int b = 64 - __builtin_clzll(fm);
     if (fit && len) {
-      FastW w;
-      w.begin(img, sh + (rel - lo));
-      fast_encode(w, d, tab, segs, dw, pre);
+      if (msg) {
+        FastWT<true> w;
+        w.begin(img, sh + (rel - lo));
+        fast_encode_msg(w, d, tab, segs, dw, pre);
+      } else {
+        FastW w;
+        w.begin(img, sh + (rel - lo));
+        fast_encode(w, d, tab, segs, dw, pre);
+      }
     }
     const uint32_t hi = __builtin_amdgcn_readlane(incl, b - 1);
     wave_lds_sync();

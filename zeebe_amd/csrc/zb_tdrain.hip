@@ -52,7 +52,7 @@ __host__ __device__ __forceinline__ uint32_t td_r16(uint32_t x) { return (x + 15
 __host__ __device__ __forceinline__ TdLayout td_layout(const TDrainParams& d, bool model) {
   TdLayout l;
   l.tab = 0;
-  const uint32_t tb = model ? td_r16((uint32_t)d.n_elems * 20u) : 0u;  // DevValSeg table (20 B each)
+  const uint32_t tb = model ? td_r16((uint32_t)d.n_elems * (uint32_t)sizeof(DevValSeg)) : 0u;  // DevValSeg table
   l.pool = l.tab + tb;
   l.agg = l.pool + (model ? td_r16(d.segpool_len) : 0u);
   l.wbase = l.agg + td_r16(d.nc * d.wmax * 8u);
@@ -67,7 +67,7 @@ __device__ __forceinline__ TdTab td_load_tables(const TDrainParams& D, uint8_t* 
   const TrajParams& P = D.t;
   const int t = threadIdx.x;
   if (model) {
-    const uint32_t tb = td_r16((uint32_t)D.n_elems * 20u);  // (the table is padded to 4 entries at deploy)
+    const uint32_t tb = td_r16((uint32_t)D.n_elems * (uint32_t)sizeof(DevValSeg));  // (padded to 4 entries at deploy)
     for (uint32_t c = t; c < tb / 4; c += TD_WG) ((uint32_t*)(sm + l.tab))[c] = ((const uint32_t*)D.vsegs)[c];
     for (uint32_t c = t; c < D.segpool_len / 8; c += TD_WG) ((uint64_t*)(sm + l.pool))[c] = ((const uint64_t*)D.segpool)[c];
   }
@@ -343,13 +343,13 @@ __global__ void __launch_bounds__(256) k_tdrain_sizes(TDrainParams D, uint32_t w
   for (int v = 0; v < TD_WG / 64; v++) {
     const uint64_t wave = g * (TD_WG / 64) + v, grp = wave * CLS_MAX;
     uint32_t n[CLS_MAX];
-    uint64_t gb[CLS_MAX], pb[CLS_MAX];
+    uint32_t gb[CLS_MAX], pb[CLS_MAX];
 #pragma unroll
     for (int c = 0; c < CLS_MAX; c++) {
       const bool in = c < (int)nc;
       n[c] = in ? (uint32_t)__builtin_popcountll(P.cmask[grp + c]) : 0u;
-      gb[c] = in ? P.cg[2 * (grp + c)] : 0ull;
-      pb[c] = in ? P.cg[2 * (grp + c) + 1] : 0ull;
+      gb[c] = in ? P.cg[2 * (grp + c)] : 0u;
+      pb[c] = in ? P.cg[2 * (grp + c) + 1] : 0u;
     }
     for (uint32_t w = 0; w < W; w++) {
       uint64_t b = 0;

@@ -34,6 +34,7 @@
 
 #include "zb_devlib.hpp"
 #include "zb_kernels.hpp"
+#include "zb_wavelib.hpp"
 #include "zb_xlock.hpp"
 #include "zb_tmpl.hpp"
 
@@ -1467,17 +1468,19 @@ __global__ void __launch_bounds__(TWG) k_cls_masks(TrajParams P) {
   const uint32_t c = i < P.n ? pl->cid[P.ikey[i]] : 0xffu;
   const uint64_t grp = ((uint64_t)blockIdx.x * (TWG / 64) + wv) * CLS_MAX;
   // (the template drain's size formula: per class the CREATE payloads' binary lengths and byte counts)
+  // (32-bit DPP sums: a deferred batch's values fit the drain's 11 KB wave image, so a wave's sum is below 2^20; a
+  // batch that does not fit leaves the template drain, whatever these say)
   const uint32_t cl = i < P.n ? P.clen[i] : 0u;
-  const uint64_t bl = (uint64_t)cl + (cl < 256 ? 2 : cl < 65536 ? 3 : 5);  // mp_bin_len
+  const uint32_t bl = mp_bin_len(cl);
   for (uint32_t k = 0; k < nc; k++) {
     const uint64_t m = __ballot(c == k);
-    uint64_t g = c == k ? bl : 0, q = c == k ? (uint64_t)cl : 0;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) { g += __shfl_xor(g, d, 64); q += __shfl_xor(q, d, 64); }
-    if (lane == 0) {
-      P.cmask[grp + k] = m;
+    const uint32_t g = wave_incl_scan(c == k ? bl : 0u), q = wave_incl_scan(c == k ? cl : 0u);
+    if (lane == 63) {
       P.cg[2 * (grp + k)] = g;
       P.cg[2 * (grp + k) + 1] = q;
+    }
+    if (lane == 0) {
+      P.cmask[grp + k] = m;
       s_cnt[wv][k] = (uint32_t)__builtin_popcountll(m);
     }
   }
