@@ -10,7 +10,7 @@ for rep in $(seq ${REPS:-2}); do
     cp $l zeebe_amd/libzbgpu.so
     t=$(basename $l .so)
     ZB_AB_LIBRARY=1 timeout -k 10 300 python3 bench.py --no-extras --no-cpu-baseline --steps 5 ${BENCH_ARGS} > $O/$t.json 2> $O/$t.err || { echo "$t failed"; tail -5 $O/$t.err; cp $O/.libzbgpu_head.so zeebe_amd/libzbgpu.so; exit 1; }
-    python3 -c "import json; d=json.load(open('$O/$t.json')); b=d.get('step_breakdown_ms', {}); print('$t', round(d['value']/1e9,3), 'G/s', round(d['ms_per_step'],3), 'ms', {k: round(x,3) for k,x in b.items()})"
+    python3 -c "import json; d=json.loads([l for l in open('$O/$t.json').read().splitlines() if l.startswith('{')][-1]); b=d.get('step_breakdown_ms', {}); print('$t', round(d['value']/1e9,3), 'G/s', round(d['ms_per_step'],3), 'ms', {k: round(x,3) for k,x in b.items()})"
   done
 done
 cp $O/.libzbgpu_head.so zeebe_amd/libzbgpu.so

@@ -283,7 +283,10 @@ struct zb_engine {
   void* ob_tmp = nullptr;  // (scan scratch)
   size_t ob_tmp_bytes = 0;
   uint32_t ob_counts_read[2] = {0, 0};  // both outbox command counts at the last zb_outbox_count
-  int wave_hint = 0;
+  // non-empty waves of the last wave loop, per kind of input (a partition that alternates kinds -- C5: CREATE batches,
+  // then the correlations delivered to its inbox -- settles each kind in its own count): 1 staged CREATEs only,
+  // 2 other staged records, 3 records already in the log (inbox deliveries)
+  int wave_hint[4] = {0, 0, 0, 0};
   int traj_skip = 0;     // batches left that skip the trajectory attempt after a fallback (zb_step)     // non-empty waves of the last step's wave loop (its first batch, zb_step)
   int ob_plan_kind = 0;  // the outbox kind outbox_plan sorted and sized last (0: none)
   uint64_t ob_plan_n = 0, ob_plan_total = 0, ob_plan_base[64] = {};
@@ -1543,7 +1546,7 @@ int zb_reset(zb_engine* e, int keep_staged) {
     e->tick_aik.clear();
     e->tick_jobs.clear();
     e->staged_uploaded = false;
-    e->wave_hint = 0;  // (a reset that keeps the staged batch runs the same tick again: the hint stays)
+    for (int& h : e->wave_hint) h = 0;  // (a reset that keeps the staged batch runs the same tick again: hints stay)
   }
   e->term = false;
   e->conf_active = false;
@@ -1580,7 +1583,7 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
   std::string msg;
   int rc = compile_deployment(e->model, std::string((const char*)xml, len), workflow_key, version, msg);
   if (rc != ZB_OK) return fail(e, rc, msg);
-  e->wave_hint = 0;  // (the last tick's wave count says nothing about the new model's ticks)
+  for (int& h : e->wave_hint) h = 0;  // (the last tick's wave count says nothing about the new model's ticks)
   for (const DevElem& el : e->model.elems) {
     if (el.step[WI_ELEMENT_COMPLETING] == ST_APPLY_OUTPUT_MAPPING) e->has_merges = true;
     if (el.step[WI_GATEWAY_ACTIVATED] == ST_EXCLUSIVE_SPLIT) e->has_splits = true;
@@ -2328,6 +2331,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   const int64_t rows_before = e->host_hdr.rows_next, arena_before = e->host_hdr.arena_next;
   const int64_t end_before = e->host_hdr.end;  // records appended by this call: injected input + follow-ups
   int64_t traj_base = 0, traj_n = 0;
+  const int hint_key = (e->staged_pending && !e->staged.empty()) ? (e->staged_only_creates ? 1 : 2) : 3;
   // ---- inject staged input at the log tail (engine is quiescent between steps)
   if (e->staged_pending && !e->staged.empty()) {
     if (!e->staged_only_creates && e->host_hdr.begin != e->host_hdr.end)
@@ -2434,17 +2438,16 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     quiescent = e->host_hdr.begin == e->host_hdr.end;
   }
   ZB_SP(2);  // trajectory
-  // the first batch: as many waves as the last step's wave loop had (a tick of the same workload settles in as
-  // many waves, and each launch past quiescence costs ~20 us of empty kernels), else WAVES_PER_SYNC; later
-  // batches WAVES_PER_SYNC, doubling
-  int next_batch = e->wave_hint > 0 ? std::min<int>(e->wave_hint, WAVES_PER_SYNC_MAX) : WAVES_PER_SYNC;
+  // the first batch: as many waves as the last wave loop over the same kind of input had (a tick of the same workload
+  // settles in as many waves, and each launch past quiescence costs ~20 us of empty kernels), else WAVES_PER_SYNC
   const bool loop = !quiescent && (max_waves == 0 || launched < max_waves);
   if (loop) HIPCHECK(e, hipMemcpyAsync(e->h_stats_pinned + 18, e->dstats + 6, sizeof(uint64_t), hipMemcpyDeviceToHost,
                                        e->stream));  // (the waves counter before the loop)
   // batches follow the hint until it is used up (C2: 148 waves as 64 + 64 + 20, not 64 + 16 + 32 + 64 with 28 empty
-  // waves), then WAVES_PER_SYNC, doubling
-  const int hint = e->wave_hint;
-  int grow = WAVES_PER_SYNC;
+  // waves), then -- the tick needs a few more -- 4, doubling; without a hint WAVES_PER_SYNC, doubling
+  const int hint = e->wave_hint[hint_key];
+  int next_batch = hint > 0 ? std::min<int>(hint, WAVES_PER_SYNC_MAX) : WAVES_PER_SYNC;
+  int grow = hint > 0 ? 4 : WAVES_PER_SYNC;
   bool stats_fresh = false;
   while (!quiescent && (max_waves == 0 || launched < max_waves)) {
     int batch = next_batch;
@@ -2534,7 +2537,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     HIPCHECK(e, hipMemcpyAsync(stats_after, e->dstats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHECK(e, hipStreamSynchronize(e->stream));
   }
-  if (loop && quiescent) e->wave_hint = (int)(stats_after[6] - e->h_stats_pinned[18]);  // the loop's non-empty waves
+  if (loop && quiescent) e->wave_hint[hint_key] = (int)(stats_after[6] - e->h_stats_pinned[18]);  // its non-empty waves
   st.records_processed = (uint64_t)(e->host_hdr.begin - processed_from);
   st.records_written = (uint64_t)(e->host_hdr.end - written_from);
   st.transitions = stats_after[0] - stats_before[0];
