@@ -3623,7 +3623,10 @@ namespace {
 // target: per-target byte sizes into bytes_per_target, *total = their sum (the outbox is left as it is).
 // outbox_emit then lays the planned batches out at dst (device, target order) and takes the outbox: one sort per
 // exchange.
-int outbox_plan(zb_engine* e, int kind, uint64_t* bytes_per_target, uint64_t* counts, uint64_t* n_out, uint64_t* total) {
+// local: one partition delivering to its own inbox -- the batch sizes are needed only as a capacity bound, so the
+// per-target table is not read back (one host round trip less per exchange)
+int outbox_plan(zb_engine* e, int kind, uint64_t* bytes_per_target, uint64_t* counts, uint64_t* n_out, uint64_t* total,
+                bool local = false) {
   const int P = e->cfg.partition_count;
   if (P > 64) return fail(e, ZB_EUNSUPPORTED, "more than 64 partitions");
   for (int q = 0; q < P; q++) bytes_per_target[q] = counts[q] = 0;
@@ -3664,6 +3667,17 @@ int outbox_plan(zb_engine* e, int kind, uint64_t* bytes_per_target, uint64_t* co
   if (hipcub::DeviceScan::ExclusiveSum(e->ob_tmp, tmp_bytes, e->ob_sizes, e->ob_goff, (int)(n + 1), e->stream) != hipSuccess)
     return fail(e, ZB_EDEVICE, "outbox scan");
   launch_outbox_bounds(e->ob_keys, n, e->ob_first, P, e->stream);
+  if (local && P == 1) {  // (the command count and variable granules came with the count's round trip)
+    const uint32_t* c = (const uint32_t*)(e->h_stats_pinned + 19);
+    counts[0] = n;
+    bytes_per_target[0] = ZB_XCHG_BATCH_HEADER + n * sizeof(zb_exchange_rec) + 8 * (uint64_t)c[kind + 1];
+    e->ob_plan_base[0] = 0;
+    *total = bytes_per_target[0];
+    e->ob_plan_kind = kind;
+    e->ob_plan_n = n;
+    e->ob_plan_total = *total;
+    return ZB_OK;
+  }
   launch_outbox_table(e->ob_first, e->ob_goff, P, e->ob_table, e->stream);
   uint64_t table[128];
   HIPCHECK(e, hipMemcpyAsync(table, e->ob_table, 2 * P * 8, hipMemcpyDeviceToHost, e->stream));
@@ -3813,7 +3827,8 @@ int zb_comm_exchange(zb_engine* e, int kind, uint64_t* received) {
   if (const char* f = std::getenv("ZB_FAIL_EXCHANGE"))  // (before the outbox is taken: a retry still has it)
     if (*f && atoi(f) == e->cfg.partition_id) local = fail(e, ZB_EDEVICE, "injected local failure (ZB_FAIL_EXCHANGE)");
 #endif
-  if (local == ZB_OK) local = outbox_plan(e, kind, sb, sc, &n, &total);
+  const bool self = P == 1 && !(e->cfg.flags & ZB_CFG_RCCL_SELF);
+  if (local == ZB_OK) local = outbox_plan(e, kind, sb, sc, &n, &total, self);
   if (local == ZB_OK && n) local = grow_dev(e, &e->xsend, &e->xsend_cap, total);
   if (local == ZB_OK && n) local = outbox_emit(e, kind, e->xsend, e->xsend_cap);
   if (P == 1 && !(e->cfg.flags & ZB_CFG_RCCL_SELF)) {  // no peer: the batch is this partition's own inbox
