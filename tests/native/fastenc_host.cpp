@@ -16,14 +16,15 @@ static inline uint32_t host_alignbyte(uint32_t hi, uint32_t lo, uint32_t c) {
 
 using namespace zbg;
 
-extern "C" {
 // Encodes one record with fast_encode into out + head (out 8-aligned, pre-filled by the caller with guard bytes).
 // pool: element id / type / process id / headers bytes (offsets below); doc: [u32 len][payload], 8-aligned,
-// padded to 8. Returns the encoded length (the caller checks out[n..cap) is still guard).
-long fastenc(int vt, int intent, int64_t inst_key, int64_t scope_key, int64_t wf_key, int32_t version,
+// padded to 8. Returns the encoded length (the caller checks out[n..cap) is still guard). BF: the branch-free
+// writer (the template drain's), its dummy slot at image offset dummy.
+template <bool BF>
+static long fastenc_t(int vt, int intent, int64_t inst_key, int64_t scope_key, int64_t wf_key, int32_t version,
              int32_t retries, const uint8_t* pool_in, uint32_t pool_len, uint32_t pid_off, uint32_t pid_len,
              uint32_t id_off, uint32_t id_len, uint32_t type_off, uint32_t type_len, uint32_t hdr_off, uint32_t hdr_len,
-             const uint64_t* doc, uint8_t* out, uint32_t head) {
+             const uint64_t* doc, uint8_t* out, uint32_t head, uint32_t dummy) {
   static uint8_t pool[1 << 16];
   std::memset(pool, 0xcd, sizeof(pool));
   std::memcpy(pool, pool_in, pool_len);
@@ -58,10 +59,26 @@ long fastenc(int vt, int intent, int64_t inst_key, int64_t scope_key, int64_t wf
   uint64_t pre[SER_PRE];
   const uint32_t words = (4 + (uint32_t)doc[0] + 7) / 8;  // (doc[0] low half: the payload length)
   for (int j = 0; j < SER_PRE; j++) pre[j] = (uint32_t)j < words ? doc[j] : 0xa5a5a5a5a5a5a5a5ull;  // (next doc)
-  FastW w;
-  w.begin(out, head);  // (out: 8-aligned image; the value starts at byte head of it)
+  FastWT<false, BF> w;
+  w.begin(out, head, dummy);  // (out: 8-aligned image; the value starts at byte head of it)
   fast_encode(w, d, tab.data(), (const uint8_t*)seg_words.data(), doc, pre);
   return w.n();
+}
+
+extern "C" {
+long fastenc(int vt, int intent, int64_t inst_key, int64_t scope_key, int64_t wf_key, int32_t version,
+             int32_t retries, const uint8_t* pool_in, uint32_t pool_len, uint32_t pid_off, uint32_t pid_len,
+             uint32_t id_off, uint32_t id_len, uint32_t type_off, uint32_t type_len, uint32_t hdr_off, uint32_t hdr_len,
+             const uint64_t* doc, uint8_t* out, uint32_t head) {
+  return fastenc_t<false>(vt, intent, inst_key, scope_key, wf_key, version, retries, pool_in, pool_len, pid_off, pid_len,
+                          id_off, id_len, type_off, type_len, hdr_off, hdr_len, doc, out, head, 0);
+}
+long fastenc_bf(int vt, int intent, int64_t inst_key, int64_t scope_key, int64_t wf_key, int32_t version,
+                int32_t retries, const uint8_t* pool_in, uint32_t pool_len, uint32_t pid_off, uint32_t pid_len,
+                uint32_t id_off, uint32_t id_len, uint32_t type_off, uint32_t type_len, uint32_t hdr_off,
+                uint32_t hdr_len, const uint64_t* doc, uint8_t* out, uint32_t head, uint32_t dummy) {
+  return fastenc_t<true>(vt, intent, inst_key, scope_key, wf_key, version, retries, pool_in, pool_len, pid_off, pid_len,
+                         id_off, id_len, type_off, type_len, hdr_off, hdr_len, doc, out, head, dummy);
 }
 
 // Encodes one message-side record (WORKFLOW_INSTANCE_SUBSCRIPTION / MESSAGE_SUBSCRIPTION / MESSAGE) with

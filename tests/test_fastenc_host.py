@@ -35,6 +35,8 @@ def lib():
     L.fastenc.restype = ctypes.c_long
     L.fastenc.argtypes = ([ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
                            ctypes.c_int32, ctypes.c_char_p] + [ctypes.c_uint32] * 9 + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32])
+    L.fastenc_bf.restype = ctypes.c_long
+    L.fastenc_bf.argtypes = L.fastenc.argtypes + [ctypes.c_uint32]
     L.fastenc_msg.restype = ctypes.c_long
     L.fastenc_msg.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_char_p, ctypes.c_uint32,
                               ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
@@ -51,7 +53,8 @@ def rand_str(r):
     return "".join(r.choice("abcxyz_-0") for _ in range(r.choice([0, 1, 5, 7, 8, 9, 15, 31, 32, 33, 40, 255, 256, 300])))
 
 
-def encode(lib, vt, intent, inst, scope, wfkey, version, retries, pid, act, jtype, headers, payload, head=0):
+def encode(lib, vt, intent, inst, scope, wfkey, version, retries, pid, act, jtype, headers, payload, head=0, bf=False):
+    """bf: the branch-free writer (the template drain's); its dummy slot is the 8 bytes past the checked image."""
     pool = b""
     offs = {}
     for name, v in (("pid", pid), ("act", act), ("type", jtype), ("hdr", headers or b"")):
@@ -61,12 +64,13 @@ def encode(lib, vt, intent, inst, scope, wfkey, version, retries, pid, act, jtyp
     doc += b"\0" * (-len(doc) % 8) + b"\xa5" * 64  # padded to 8, then whatever follows in the arena
     dbuf = ctypes.create_string_buffer(doc, len(doc))
     cap = (2048 + len(payload) + len(pool) + 7) // 8 * 8
-    out = (ctypes.c_uint64 * (cap // 8))()  # 8-aligned image
+    out = (ctypes.c_uint64 * (cap // 8 + 1))()  # 8-aligned image (+ the dummy slot)
     ctypes.memset(out, GUARD, cap)
-    n = lib.fastenc(vt, intent, inst, scope, wfkey, version, retries, pool, len(pool), offs["pid"], len(pid),
-                    offs["act"], len(act), offs["type"], len(jtype), offs["hdr"] if headers else 0xFFFFFFFF,
-                    len(headers or b""), dbuf, out, head)
-    raw = bytes(out)
+    args = (vt, intent, inst, scope, wfkey, version, retries, pool, len(pool), offs["pid"], len(pid),
+            offs["act"], len(act), offs["type"], len(jtype), offs["hdr"] if headers else 0xFFFFFFFF,
+            len(headers or b""), dbuf, out, head)
+    n = lib.fastenc_bf(*args, cap) if bf else lib.fastenc(*args)
+    raw = bytes(out)[:cap]
     assert n > 0
     assert all(b == GUARD for b in raw[:head]), "store before the value start (the previous lane's bytes)"
     assert all(b == GUARD for b in raw[head + n:]), "store past the value end"
@@ -91,7 +95,8 @@ def expect_job(pid, version, wfkey, inst, act, payload, scope, retries, jtype, h
     return b"\x87" + head[1:] + msgpack.packb("payload") + msgpack.packb(payload, use_bin_type=True)
 
 
-def test_fast_encoder_fuzz(lib):
+@pytest.mark.parametrize("bf", [False, True])
+def test_fast_encoder_fuzz(lib, bf):
     r = random.Random(11)
     for it in range(3000):
         pid, act, jtype = (rand_str(r).encode() for _ in range(3))
@@ -102,11 +107,11 @@ def test_fast_encoder_fuzz(lib):
         headers = r.choice([None, msgpack.packb({"k": "v" * r.randrange(20)})])
         if it % 2 == 0:
             got = encode(lib, VT_WI, 4, inst, scope, wfkey, version, retries, pid, act, jtype, headers, payload,
-                         head=r.randrange(24))
+                         head=r.randrange(24), bf=bf)
             assert got == expect_wi(pid, version, wfkey, inst, act, payload, scope), it
         else:
             got = encode(lib, VT_JOB, 5, inst, scope, wfkey, version, retries, pid, act, jtype, headers, payload,
-                         head=r.randrange(24))
+                         head=r.randrange(24), bf=bf)
             assert got == expect_job(pid, version, wfkey, inst, act, payload, scope, retries, jtype, headers), it
 
 

@@ -1416,8 +1416,8 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->raux, e->cfg.row_capacity * sizeof(RowAux)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMemset(e->raux, 0, e->cfg.row_capacity * sizeof(RowAux)) != hipSuccess) return cleanup(ZB_EDEVICE);
 #ifdef ZB_PHASES
-  if (hipMalloc(&e->phase, 8 * sizeof(unsigned long long)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipMemset(e->phase, 0, 8 * sizeof(unsigned long long)) != hipSuccess) return cleanup(ZB_EDEVICE);
+  if (hipMalloc(&e->phase, 16 * sizeof(unsigned long long)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipMemset(e->phase, 0, 16 * sizeof(unsigned long long)) != hipSuccess) return cleanup(ZB_EDEVICE);
 #endif
   e->ev.resize(EV_PER_WAVE * WAVES_PER_SYNC_MAX);
   for (auto& x : e->ev)
@@ -1490,6 +1490,14 @@ int zb_phase_times(zb_engine* e, unsigned long long* out5) {
   if (!e || !out5) return ZB_EINVAL;
   HIPCHECK(e, hipStreamSynchronize(e->stream));
   HIPCHECK(e, hipMemcpy(out5, e->phase, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return ZB_OK;
+}
+// k_tdrain_write's phase sums (ticks of 10 ns summed over waves): [0] generation setup (bases, records, scan),
+// [1] headers, [2] encode, [3] image stream (with its two wave syncs), [4] waves, [5] generations
+int zb_tdrain_phase_times(zb_engine* e, unsigned long long* out6) {
+  if (!e || !out6) return ZB_EINVAL;
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  HIPCHECK(e, hipMemcpy(out6, e->phase + 8, 6 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return ZB_OK;
 }
 #endif
@@ -2665,6 +2673,9 @@ static int serialize_deferred(zb_engine* e, int64_t start, int64_t count, zb_ser
   d.nc = e->seg_nc;
   d.len5_ok = e->seg_key_end <= (int64_t)UINT32_MAX ? 1u : 0u;
   d.jobs = e->seg_jobs ? 1u : 0u;
+#ifdef ZB_PHASES
+  d.phase = e->phase ? e->phase + 8 : nullptr;
+#endif
   float ms_size = 0, ms_scan = 0, ms_write = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     d.out = e->dr_val;

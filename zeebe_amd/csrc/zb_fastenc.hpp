@@ -21,19 +21,24 @@ namespace zbg {
 // CHK: every slot store checks whether it is the value's first slot (values whose first bytes come from a
 // variable-length run -- MESSAGE records -- cannot say which put completes it); without it a value's first put is
 // marked FIRST and whole 8-byte.
-template <bool CHK = false>
+// BF (branch-free; CHK false only): a slot store that must not happen goes to the lane's own 8-byte dummy slot instead
+// (an image offset the caller reserves past the image, begin()): no divergent branch around the stores of put / seg
+template <bool CHK = false, bool BF = false>
 struct FastWT {
+  static_assert(!(CHK && BF), "the checked writer branches");
   uint8_t* img;   // LDS image base (8-aligned)
   uint32_t pos;   // image offset of the next byte
   uint32_t head;  // image offset of the value's first byte
   uint64_t acc;   // the current slot's bytes below pos (low bytes first)
   uint64_t first; // the first slot's word (stored by end(): its bytes below head are the previous value's)
+  uint32_t dummy; // (BF) this lane's dummy slot
 
-  __device__ __forceinline__ void begin(uint8_t* base, uint32_t at) {
+  __device__ __forceinline__ void begin(uint8_t* base, uint32_t at, uint32_t dummy_slot = 0) {
     img = base;
     pos = head = at;
     acc = 0;
     first = 0;
+    dummy = dummy_slot;
   }
   __device__ __forceinline__ uint32_t n() const { return pos - head; }
   // a whole image slot (CHK: the value's first slot is kept for end())
@@ -58,6 +63,14 @@ struct FastWT {
     const uint32_t f = pos & 7;
     const uint64_t lo = acc | (v << (8 * f));
     const uint64_t hi = (v >> 1) >> (63 - 8 * f);  // the bytes past the slot (0 when f == 0)
+    if (BF) {
+      const bool full = f + k >= 8;
+      if (FIRST) first = lo;  // (used by end() only when f != 0)
+      *(uint64_t*)(img + ((full && !(FIRST && f)) ? pos - f : dummy)) = lo;
+      acc = full ? hi : lo;
+      pos += k;
+      return;
+    }
     if (f + k >= 8) {
       if (FIRST && f) first = lo;
       else st(pos - f, lo);
@@ -102,6 +115,11 @@ struct FastWT {
     put(((neg ? 0xd0u : 0xccu) + lg) | be << 8, m < 8 ? m + 1 : 8);
     if (m == 8) put((uint8_t)v, 1);
   }
+  // a key known to be -1, 0 or in [2^16, 2^32) (the template drain's short form): a fixint or 0xce + 4 bytes
+  __device__ __forceinline__ void ival5(int64_t v) {
+    const bool sp = (uint64_t)(v + 1) <= 1;
+    put(sp ? (uint64_t)(uint8_t)v : (0xceull | (uint64_t)__builtin_bswap32((uint32_t)v) << 8), sp ? 1u : 5u);
+  }
   // a constant run: c bytes at s (LDS, 8-aligned; the pool keeps SEG_PAD_LO readable bytes before its first run
   // and SEG_PAD_HI after its last); FIRST as in put. The byte shift between the run and the image is fixed for
   // the whole run, so image slot j is bytes [r, r + 8) of three consecutive run dwords p[2j..2j+2] (p: the run
@@ -115,6 +133,30 @@ struct FastWT {
     const uint64_t own0 = f ? (~0ull << (8 * f)) : ~0ull;  // slot 0: the run's bytes (below them: acc)
     const uint32_t slot = pos - f;
     uint32_t x0 = p[0];
+    if (BF) {  // every slot of the group stored (a slot past the run's whole slots: to the dummy); slot nf kept in acc
+      uint64_t last = 0;
+      for (uint32_t j = 0; j <= nf; j += 4) {
+        uint32_t x[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) x[k] = p[2 * j + 1 + k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t jj = j + k;
+          const uint32_t a = k ? x[2 * k - 1] : x0;
+          uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(x[2 * k], a, r) |
+                       (uint64_t)__builtin_amdgcn_alignbyte(x[2 * k + 1], x[2 * k], r) << 32;
+          if (k == 0) v = jj == 0 ? (acc | (v & own0)) : v;
+          if (FIRST && k == 0) first = jj == 0 ? v : first;
+          const bool sto = jj < nf && !(FIRST && jj == 0 && f);
+          *(uint64_t*)(img + (sto ? slot + 8 * jj : dummy)) = v;
+          last = jj == nf ? v : last;
+        }
+        x0 = x[7];
+      }
+      acc = rem ? last & (~0ull >> (64 - 8 * rem)) : 0;
+      pos += c;
+      return;
+    }
     for (uint32_t j = 0; j <= nf; j += 4) {
       uint32_t x[8];
 #pragma unroll
@@ -145,6 +187,19 @@ struct FastWT {
     const uint32_t f = pos & 7, sl = 8 * f, sr = 63 - sl;
     const uint32_t end = f + n, nf = end >> 3, rem = end & 7;
     const uint32_t slot = pos - f;
+    if (BF) {  // all N slots: the ones past the run's whole slots to the dummy, slot nf's bytes kept in acc
+#pragma unroll
+      for (int i = 0; i < N; i++) {
+        const uint64_t x = (uint32_t)(8 * i) < n ? v[i] : 0ull;
+        const uint64_t o = acc | (x << sl);
+        const bool full = (uint32_t)i < nf;
+        *(uint64_t*)(img + (full ? slot + 8 * i : dummy)) = o;
+        acc = full ? (x >> 1) >> sr : ((uint32_t)i == nf ? o : acc);
+      }
+      acc = rem ? acc & (~0ull >> (64 - 8 * rem)) : 0;
+      pos += n;
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < N; i++) {
       if ((uint32_t)i > nf) break;
@@ -188,6 +243,7 @@ struct FastWT {
   }
 };
 using FastW = FastWT<false>;
+using FastWB = FastWT<false, true>;
 
 constexpr int SER_PRE = 6;  // payload document words prefetched per record (length + 44 bytes)
 constexpr uint32_t ARENA_SLACK = 64;  // bytes allocated past the arena: SER_PRE words load unchecked
@@ -213,8 +269,8 @@ constexpr uint32_t SEG_LDS_MAX = 16384;  // table (padded to 4 entries) + pool t
 // the payload document [u32 len][bytes] as binary (MsgPackWriter.writeBinary): doc words W_j (8-aligned), the
 // first SER_PRE already loaded (words past the document hold whatever follows it: only bytes past the payload
 // come from them, and those are masked off); payload bytes [8k, 8k + 8) = W_k >> 32 | W_(k+1) << 32
-template <bool CHK>
-__device__ __forceinline__ void fast_bin(FastWT<CHK>& w, const uint64_t* dw, const uint64_t (&pre)[SER_PRE]) {
+template <bool CHK, bool BF>
+__device__ __forceinline__ void fast_bin(FastWT<CHK, BF>& w, const uint64_t* dw, const uint64_t (&pre)[SER_PRE]) {
   const uint32_t plen = (uint32_t)pre[0];
   if (plen < 256) w.put(0xc4 | (uint64_t)plen << 8, 2);
   else if (plen < 65536) w.put(0xc5 | (uint64_t)__builtin_bswap16((uint16_t)plen) << 8, 3);
@@ -254,21 +310,23 @@ __device__ __forceinline__ bool fast_kind(const zb_rec& d) {
 
 // encode_value's WORKFLOW_INSTANCE (non-submitted) and JOB branches from the constant runs of the record's
 // element (tab / pool in LDS) and its variable fields: keys, payload
-__device__ __forceinline__ void fast_encode(FastW& w, const zb_rec& d, const DevValSeg* tab, const uint8_t* segs,
+// L5: every key in ival5's range
+template <bool L5 = false, bool BF = false>
+__device__ __forceinline__ void fast_encode(FastWT<false, BF>& w, const zb_rec& d, const DevValSeg* tab, const uint8_t* segs,
                                             const uint64_t* dw, const uint64_t (&pre)[SER_PRE]) {
   const DevValSeg& t = tab[d.elem];
   if (kind_vt(d.kind) == ZB_VT_WORKFLOW_INSTANCE) {  // WorkflowInstanceRecord.java:39-60
-    w.seg<true>(segs + 8 * t.off8[SEG_WI_A], t.len[SEG_WI_A]);
-    w.ival(d.inst_key);
+    w.template seg<true>(segs + 8 * t.off8[SEG_WI_A], t.len[SEG_WI_A]);
+    if (L5) w.ival5(d.inst_key); else w.ival(d.inst_key);
     w.seg(segs + 8 * t.off8[SEG_WI_B], t.len[SEG_WI_B]);
     fast_bin(w, dw, pre);
     w.lit("\xb0" "scopeInstanceKey");
-    w.ival(d.scope_key);
+    if (L5) w.ival5(d.scope_key); else w.ival(d.scope_key);
   } else {  // JobRecord.java:35-53 + JobHeaders.java:33-51
-    w.seg<true>(segs + 8 * t.off8[SEG_JOB_A], t.len[SEG_JOB_A]);
-    w.ival(d.inst_key);
+    w.template seg<true>(segs + 8 * t.off8[SEG_JOB_A], t.len[SEG_JOB_A]);
+    if (L5) w.ival5(d.inst_key); else w.ival(d.inst_key);
     w.seg(segs + 8 * t.off8[SEG_JOB_B], t.len[SEG_JOB_B]);
-    w.ival(d.scope_key);
+    if (L5) w.ival5(d.scope_key); else w.ival(d.scope_key);
     w.seg(segs + 8 * t.off8[SEG_JOB_C], t.len[SEG_JOB_C]);
     fast_bin(w, dw, pre);
   }

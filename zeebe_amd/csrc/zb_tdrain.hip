@@ -113,6 +113,32 @@ __device__ __forceinline__ int64_t td_key(const TrajParams& P, const TdTab& T, c
   return P.job_start + 5 * ((g == w ? kjob : td_kbase(T, L, g, 2)) + ord);
 }
 
+// td_kbase / td_key for a wave whose every key / position lies in [2^16, 2^32) or is -1 / 0 (the size pass's short
+// form): the same values in 32-bit arithmetic (exact: every result is below 2^32)
+__device__ __forceinline__ uint32_t td_kbase32(const TdTab& T, const TmplLane& L, uint32_t g, int f) {
+  const TrajBase wb = T.wbase[g];
+  uint32_t k = (uint32_t)(f == 1 ? wb.wf : wb.job);
+#pragma unroll
+  for (int c = 0; c < CLS_MAX; c++) {
+    if (c >= (int)L.ncls) break;
+    const uint64_t n = T.agg[c * T.wmax + g];
+    k += L.before[c] * (f == 1 ? (uint32_t)((n >> 16) & 0xffff) : (uint32_t)(n >> 32));
+  }
+  return k;
+}
+__device__ __forceinline__ int64_t td_key5(const TrajParams& P, const TdTab& T, const TmplLane& L, uint32_t sym,
+                                           uint32_t w, int64_t kwf, int64_t kjob, int64_t kwf0) {
+  if (sym == NOK) return -1;
+  if (sym == JOB_ZERO) return 0;
+  const uint32_t g = (sym >> 4) & 0xfff, ord = sym & 15;
+  if (sym & SYMK_WF)
+    return (int64_t)((uint32_t)P.wf_start +
+                     5u * ((g == w ? (uint32_t)kwf : g == 0 ? (uint32_t)kwf0 : td_kbase32(T, L, g, 1)) + ord));
+  return (int64_t)((uint32_t)P.job_start + 5u * ((g == w ? (uint32_t)kjob : td_kbase32(T, L, g, 2)) + ord));
+}
+// msgpack length of such a key: -1 / 0 are fixints, the rest 0xce + 4 bytes
+__device__ __forceinline__ uint32_t td_klen5(int64_t v) { return (uint64_t)(v + 1) <= 1 ? 1u : 5u; }
+
 // one instance's generation w: log position and key bases (linear in the class ranks), record count
 struct TdGen {
   int64_t pos0, kwf, kjob;
@@ -186,15 +212,21 @@ __device__ __forceinline__ void td_static_pre(const uint8_t* arena, bool mine, u
 
 // record k of the instance's generation w, resolved from the class trace; vl: its value length (the
 // encoder's, by the formula), plen: its payload document's length
-template <bool SCALAR_STATIC = false>
+template <bool SCALAR_STATIC = false, bool L5 = false>
 __device__ __forceinline__ zb_rec td_record(const TrajParams& P, const TdTab& T, const TmplLane& L, uint32_t cls, int w,
                                             uint32_t k, const TdGen& G, int64_t inst, uint32_t create_ref,
                                             uint32_t create_len, int64_t kwf0, uint32_t& vl, uint32_t& plen) {
   const TmplRec t = T.tmpl[(cls * T.wmax + w) * TF + k];
   zb_rec d;
-  d.key = td_key(P, T, L, t.key, (uint32_t)w, G.kwf, G.kjob, kwf0);
-  d.scope_key = t.scope == SYM_CMDPOS ? P.log_base + inst : td_key(P, T, L, t.scope, (uint32_t)w, G.kwf, G.kjob, kwf0);
-  d.inst_key = td_key(P, T, L, t.inst, (uint32_t)w, G.kwf, G.kjob, kwf0);
+  if (L5) {
+    d.key = td_key5(P, T, L, t.key, (uint32_t)w, G.kwf, G.kjob, kwf0);
+    d.scope_key = t.scope == SYM_CMDPOS ? P.log_base + inst : td_key5(P, T, L, t.scope, (uint32_t)w, G.kwf, G.kjob, kwf0);
+    d.inst_key = td_key5(P, T, L, t.inst, (uint32_t)w, G.kwf, G.kjob, kwf0);
+  } else {
+    d.key = td_key(P, T, L, t.key, (uint32_t)w, G.kwf, G.kjob, kwf0);
+    d.scope_key = t.scope == SYM_CMDPOS ? P.log_base + inst : td_key(P, T, L, t.scope, (uint32_t)w, G.kwf, G.kjob, kwf0);
+    d.inst_key = td_key(P, T, L, t.inst, (uint32_t)w, G.kwf, G.kjob, kwf0);
+  }
   // (k_tmpl_decide: no merge results in a deferred batch -- the CREATE payload or a static blob)
   const bool cr = t.payload == PAY_CREATE;
   d.payload = cr ? create_ref : t.payload;
@@ -207,7 +239,8 @@ __device__ __forceinline__ zb_rec td_record(const TrajParams& P, const TdTab& T,
   }
   d.elem = t.elem; d.intent = t.intent; d.kind = t.kind;
   const ValueConst vc = T.vconst[d.elem];
-  vl = (kind_vt(d.kind) == ZB_VT_JOB ? vc.job : vc.wf) + mp_int_len(d.inst_key) + mp_int_len(d.scope_key) +
+  vl = (kind_vt(d.kind) == ZB_VT_JOB ? vc.job : vc.wf) +
+       (L5 ? td_klen5(d.inst_key) + td_klen5(d.scope_key) : mp_int_len(d.inst_key) + mp_int_len(d.scope_key)) +
        mp_bin_len(plen);
   return d;
 }
@@ -368,7 +401,8 @@ __global__ void __launch_bounds__(256) k_tdrain_sizes(TDrainParams D, uint32_t w
 
 template <uint32_t IMG>
 __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4))) k_tdrain_write(TDrainParams D) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_img[TD_WG / 64][IMG + 16];
+  // each wave's image, then its lanes' dummy slots (the branch-free writer's stores that must not land: FastWB)
+  __shared__ __attribute__((aligned(16))) uint8_t s_img[TD_WG / 64][IMG + 16 + 8 * 64];
   extern __shared__ __attribute__((aligned(16))) uint8_t s_tab[];  // value segments + the batch's tables
   const TrajParams& P = D.t;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -378,6 +412,12 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
   const uint8_t* segs = s_tab + lay.pool;
   uint8_t* img = s_img[wv];
   uint32_t bad = 0;
+#ifdef ZB_PHASES  // (measurement build: wall-clock ticks per phase, summed by lane 0 of every wave)
+  uint64_t ph_t = wall_clock64(), ph[4] = {0, 0, 0, 0}, ph_g = 0;
+#define TD_PHASE(k) do { const uint64_t ph_n = wall_clock64(); ph[k] += ph_n - ph_t; ph_t = ph_n; } while (0)
+#else
+#define TD_PHASE(k) do { } while (0)
+#endif
   {
     const int64_t tile = blockIdx.x;
     const TdLane L = td_lane(P, T, tile, true);
@@ -399,6 +439,9 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
     const uint64_t swave = (uint64_t)tile * (TD_WG / 64) + __builtin_amdgcn_readfirstlane(wv);
     // this wave's value range of generation w: woffs[w][wave .. wave + 1], read one generation ahead (scalar loads)
     uint64_t nbase = K(D.woffs)[swave], nend = K(D.woffs)[swave + 1];
+    // L5: every key / position of the wave in [2^16, 2^32) (k_tdrain_size's short form): 32-bit keys, 5-byte integers
+    auto gen_loop = [&](auto l5) {
+    constexpr bool L5 = decltype(l5)::value;
 #pragma unroll 1
     for (int w = 0; w < (int)D.wmax; w++) {
       const uint64_t wbase = nbase, wend = nend;
@@ -416,12 +459,16 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
       zb_rec d0{}, d1{};
       {
         uint32_t plen;
-        if (G.nrec > 0) d0 = td_record<true>(P, T, L.L, L.cls, w, 0, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl0, plen);
-        if (G.nrec > 1) d1 = td_record<true>(P, T, L.L, L.cls, w, 1, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl1, plen);
+        if (G.nrec > 0) d0 = td_record<true, L5>(P, T, L.L, L.cls, w, 0, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl0, plen);
+        if (G.nrec > 1) d1 = td_record<true, L5>(P, T, L.L, L.cls, w, 1, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl1, plen);
       }
       const uint32_t mine = vl0 + vl1;
       const uint32_t incl = wave_incl_scan(mine);
       const uint32_t rel = incl - mine;  // this lane's values: [wbase + rel, wbase + incl)
+#ifdef ZB_PHASES
+      ph_g++;
+#endif
+      TD_PHASE(0);
       // headers: key, types / intent / rejection, length, offset (the position is implicit: start + index)
 #pragma unroll
       for (int k = 0; k < TF; k++) {
@@ -430,12 +477,17 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
         uint64_t* dh = (uint64_t*)(D.headers + (G.pos0 + k - D.start));
         const uint64_t meta = (uint64_t)kind_rt(d.kind) | (uint64_t)kind_vt(d.kind) << 8 | (uint64_t)d.intent << 16 |
                               255ull << 24 | (uint64_t)(k ? vl1 : vl0) << 32;  // (no rejections: k_tmpl_decide)
-#ifndef ZB_EXP_NO_HEADERS  // (measurement variants only: tools/ab_variant.sh)
+#if defined(ZB_EXP_HDR_PLAIN)  // (measurement variants only: tools/ab_variant.sh)
+        dh[0] = (uint64_t)d.key;
+        dh[1] = meta;
+        dh[2] = wbase + rel + (k ? vl0 : 0);
+#elif !defined(ZB_EXP_NO_HEADERS)
         __builtin_nontemporal_store((uint64_t)d.key, dh);
         __builtin_nontemporal_store(meta, dh + 1);
         __builtin_nontemporal_store(wbase + rel + (k ? vl0 : 0), dh + 2);
 #endif
       }
+      TD_PHASE(1);
       // rounds: lanes [a, b) whose values fit the image from the round's first byte; each lane encodes its own
       // records (no redistribution: a generation of C3 is one round of every lane)
 #pragma unroll 1
@@ -463,23 +515,40 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
 #pragma unroll
             for (int j = 0; j < SER_PRE; j++) pre[j] = cpre[j];
             td_static_pre(P.arena, !cr, d.payload, pre);  // a static blob: through the scalar cache
-            FastW fw;
-            fw.begin(img, sh + (rel - lo) + (k ? vl0 : 0));
-            fast_encode(fw, d, tab, segs, dw, pre);
+            FastWB fw;
+            fw.begin(img, sh + (rel - lo) + (k ? vl0 : 0), IMG + 16 + 8 * lane);
+            fast_encode<L5>(fw, d, tab, segs, dw, pre);
             if (fw.n() != (k ? vl1 : vl0)) bad = 1;  // the formula and the encoder disagree: never silently
           }
         }
         const uint32_t hi = __builtin_amdgcn_readlane(incl, b - 1);
+        TD_PHASE(2);
         wave_lds_sync();
-#ifndef ZB_EXP_NO_STREAM
+#if defined(ZB_EXP_STREAM4)
+        wave_stream4(img, D.out, wbase + lo, sh, hi - lo, lane);
+#elif !defined(ZB_EXP_NO_STREAM)
         wave_stream(img, D.out, wbase + lo, sh, hi - lo, lane);
 #endif
         wave_lds_sync();  // the image is reused by the next round
+        TD_PHASE(3);
         a = b;
       }
     }
+    };
+    const bool lo_ok = P.wf_start + 5 * L.kwf0 >= 65536 && P.log_base + L.inst >= 65536 &&
+                       (!D.jobs || P.job_start + 5 * td_kbase(T, L.L, 0, 2) >= 65536);
+    if (D.len5_ok && __builtin_amdgcn_readlane(lo_ok ? 1 : 0, 0)) gen_loop(std::true_type{});
+    else gen_loop(std::false_type{});
   }
   if (bad) atomicOr(D.flags + 1, 1u);
+#ifdef ZB_PHASES
+  if (lane == 0 && D.phase) {
+    for (int k = 0; k < 4; k++) atomicAdd(D.phase + k, (unsigned long long)ph[k]);
+    atomicAdd(D.phase + 4, 1ull);
+    atomicAdd(D.phase + 5, (unsigned long long)ph_g);
+  }
+#endif
+#undef TD_PHASE
 }
 
 // payload-byte total over the per-workgroup partials

@@ -453,6 +453,14 @@ class Engine:
         self._check(self._L.zb_phase_times(self._h, out))
         return dict(process=out[0], lookback=out[1], emit=out[2], tiles=out[3], rounds=out[4])
 
+    def tdrain_phase_times(self):
+        """(measurement build ZB_PHASES_LIBRARY=1 only) k_tdrain_write's wall-clock ticks (10 ns) per phase, summed over
+        its waves: generation setup, headers, encode, image stream; and the waves and generations counted."""
+        out = (ctypes.c_ulonglong * 6)()
+        self._L.zb_tdrain_phase_times.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        self._check(self._L.zb_tdrain_phase_times(self._h, out))
+        return dict(setup=out[0], headers=out[1], encode=out[2], stream=out[3], waves=out[4], gens=out[5])
+
     def memory_stats(self) -> dict:
         m = zb_memory_stats()
         self._check(self._L.zb_read_memory_stats(self._h, ctypes.byref(m)))
