@@ -637,7 +637,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
       if (NT) {
         const uint64_t* hw = (const uint64_t*)&h;
         uint64_t* dh = (uint64_t*)(P.headers + i);
-        for (int k = 0; k < (int)(sizeof(zb_record_header) / 8); k++) __builtin_nontemporal_store(hw[k], dh + k);
+        for (int k = 0; k < (int)(sizeof(zb_record_header) / 8); k++) dh[k] = hw[k];  // (plain: L2 merges lines)
       } else {
         P.headers[i] = h;
       }
@@ -765,7 +765,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3))
     const zb_record_header h = record_header(d, P0.start + i, len, off);
     const uint64_t* hw = (const uint64_t*)&h;
     uint64_t* dh = (uint64_t*)(P0.headers + i);
-    for (int k = 0; k < (int)(sizeof(zb_record_header) / 8); k++) __builtin_nontemporal_store(hw[k], dh + k);
+    for (int k = 0; k < (int)(sizeof(zb_record_header) / 8); k++) dh[k] = hw[k];  // (plain: L2 merges lines)
   }
   if (P0.totals) {
     unsigned long long y = live ? (uint32_t)pre[0] : 0;
@@ -866,7 +866,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
     const zb_record_header h = record_header(d, P0.start + i, len, wlo + rel);
     const uint64_t* hw = (const uint64_t*)&h;
     uint64_t* dh = (uint64_t*)(P0.headers + i);
-    for (int k = 0; k < (int)(sizeof(zb_record_header) / 8); k++) __builtin_nontemporal_store(hw[k], dh + k);
+    for (int k = 0; k < (int)(sizeof(zb_record_header) / 8); k++) dh[k] = hw[k];  // (plain: L2 merges lines)
   }
   if (P0.totals) {
     unsigned long long y = live ? (uint32_t)pre[0] : 0;

@@ -477,14 +477,12 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
         uint64_t* dh = (uint64_t*)(D.headers + (G.pos0 + k - D.start));
         const uint64_t meta = (uint64_t)kind_rt(d.kind) | (uint64_t)kind_vt(d.kind) << 8 | (uint64_t)d.intent << 16 |
                               255ull << 24 | (uint64_t)(k ? vl1 : vl0) << 32;  // (no rejections: k_tmpl_decide)
-#if defined(ZB_EXP_HDR_PLAIN)  // (measurement variants only: tools/ab_variant.sh)
+        // plain stores: a header line is written by three stores of every lane (24-byte stride), which L2 merges into
+        // whole lines; as non-temporal stores they reached HBM as partial lines (write pass 4.55 -> 4.25 ms same box)
+#ifndef ZB_EXP_NO_HEADERS  // (measurement variants only: tools/ab_variant.sh)
         dh[0] = (uint64_t)d.key;
         dh[1] = meta;
         dh[2] = wbase + rel + (k ? vl0 : 0);
-#elif !defined(ZB_EXP_NO_HEADERS)
-        __builtin_nontemporal_store((uint64_t)d.key, dh);
-        __builtin_nontemporal_store(meta, dh + 1);
-        __builtin_nontemporal_store(wbase + rel + (k ? vl0 : 0), dh + 2);
 #endif
       }
       TD_PHASE(1);
