@@ -363,6 +363,37 @@ struct Out {
   }
 };
 
+// Out with a capacity: bytes at or past cap are counted but not written (the exact tree's single write pass into a
+// preallocated blob: an oversized result is detected by n > cap with nothing written past the blob)
+struct OutCap {
+  uint8_t* dst;
+  uint32_t n;
+  uint32_t cap;
+  ZB_HD __forceinline__ void put(uint8_t b) { if (n < cap) dst[n] = b; n++; }
+  ZB_HD __forceinline__ void put_bytes(const uint8_t* s, uint32_t len) {
+    const uint32_t k = n < cap ? (cap - n < len ? cap - n : len) : 0u;
+    for (uint32_t i = 0; i < k; i++) dst[n + i] = s[i];
+    n += len;
+  }
+  ZB_HD inline void map_hdr(uint32_t c) {
+    if (c < 16) put(0x80 | c);
+    else if (c < 65536) { put(0xde); put(c >> 8); put(c & 0xff); }
+    else { put(0xdf); put(c >> 24); put((c >> 16) & 0xff); put((c >> 8) & 0xff); put(c & 0xff); }
+  }
+  ZB_HD inline void arr_hdr(uint32_t c) {
+    if (c < 16) put(0x90 | c);
+    else if (c < 65536) { put(0xdc); put(c >> 8); put(c & 0xff); }
+    else { put(0xdd); put(c >> 24); put((c >> 16) & 0xff); put((c >> 8) & 0xff); put(c & 0xff); }
+  }
+  ZB_HD inline void str(const uint8_t* s, uint32_t c) {
+    if (c < 32) put(0xa0 | c);
+    else if (c < 256) { put(0xd9); put(c); }
+    else if (c < 65536) { put(0xda); put(c >> 8); put(c & 0xff); }
+    else { put(0xdb); put(c >> 24); put((c >> 16) & 0xff); put((c >> 8) & 0xff); put(c & 0xff); }
+    put_bytes(s, c);
+  }
+};
+
 __device__ inline bool key_ok(const uint8_t* s, uint32_t n) {
   for (uint32_t i = 0; i < n; i++)
     if (s[i] == '[' || s[i] == ']') return false;

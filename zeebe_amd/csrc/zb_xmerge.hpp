@@ -27,7 +27,8 @@ constexpr uint32_t XSLAB_COUNT = 32;        // pairs in flight (zb_xlock.hpp: on
 // zb_xlock.hpp x_run): 32 KB holds the tree of ~140 tokens (2 x source + target), the documents of a typical job /
 // message payload merge
 constexpr uint32_t XLANE_BYTES = 32u << 10;
-constexpr uint32_t XLANE_COUNT = 32768;  // (1 GiB; k_merge_gen's grid: 128 workgroups of 256 lanes)
+constexpr uint32_t XLANE_COUNT = 65536;  // (2 GiB; k_merge_gen's grid: 256 workgroups of 256 lanes. C1 1M exact-tree
+                                         //  tick: 16K lanes 14.3 ms, 32K 10.4, 64K 9.5, 128K 12.1, 256K 12.4)
 constexpr uint32_t XLANE_GROUPS = XLANE_COUNT / 64;          // lane groups (one wave's 64 workspaces)
 constexpr uint32_t XLOCK_COUNT = XSLAB_COUNT + XLANE_GROUPS;  // slab locks, then lane-group locks
 
@@ -373,7 +374,8 @@ struct XTree {
 
   // ---- MsgPackDocumentTreeWriter over tree 0: leaves are read from the node type's buffer (extracted: x,
   // existing: u); o.n past limit stops it (X_UNSUP)
-  ZB_HD void node_out(XStr id, const uint8_t* u, uint32_t un, const uint8_t* x, uint32_t xn, Out& o, uint32_t& depth) {
+  template <class O>
+  ZB_HD void node_out(XStr id, const uint8_t* u, uint32_t un, const uint8_t* x, uint32_t xn, O& o, uint32_t& depth) {
     const uint32_t k = find(0, id);
     if (k != XNONE && nodes[k].has_leaf) {
       const XNode& m = nodes[k];
@@ -394,7 +396,8 @@ struct XTree {
     fr[depth++] = XFrame{id, nodes[k].cfirst, arr ? 1u : 0u};
   }
 
-  ZB_HD void write(const uint8_t* u, uint32_t un, const uint8_t* x, uint32_t xn, Out& o, uint32_t limit) {
+  template <class O>
+  ZB_HD void write(const uint8_t* u, uint32_t un, const uint8_t* x, uint32_t xn, O& o, uint32_t limit) {
     if (typed[0] == 0) { o.put(0xc0); return; }  // empty tree: writeNil
     const uint32_t mark = pool_n;
     uint32_t depth = 0;
@@ -448,18 +451,23 @@ ZB_HD inline uint32_t x_tokens(const uint8_t* d, uint32_t n) {
   return k;
 }
 
-// Size pass then (o.dst set) write pass of a built tree; the result must be a map or nil.
+// A built tree written (o.dst set: one pass into o.dst that writes nothing at or past limit; an oversized result is
+// X_UNSUP, as a size pass would have found it) or sized (o.dst null); the result must be a map or nil.
 ZB_HD inline int x_emit(XTree& T, const uint8_t* u, uint32_t un, const uint8_t* x, uint32_t xn, Out& o, uint32_t limit) {
+  if (o.dst) {
+    OutCap oc{o.dst, 0, limit};
+    T.write(u, un, x, xn, oc, limit);
+    if (T.status != X_OK) return T.status;
+    const int rc = T.root_check(u, x);
+    if (rc != X_OK) return rc;
+    o.n = oc.n;
+    return X_OK;
+  }
   Out sz{nullptr, 0};
   T.write(u, un, x, xn, sz, limit);
   if (T.status != X_OK) return T.status;
   const int rc = T.root_check(u, x);
   if (rc != X_OK) return rc;
-  if (o.dst) {
-    o.n = 0;
-    T.write(u, un, x, xn, o, limit);
-    if (T.status != X_OK) return T.status;
-  }
   o.n = sz.n;
   return X_OK;
 }
