@@ -812,7 +812,12 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3))
 // k_ser_write directly, for the tiles holding a record of a kind the fast encoder does not take).
 constexpr uint32_t SER_WIMG = 11 * 1024 - 16;
 __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 4))) k_ser_wave(SerParams P0) {
+#ifndef ZB_EXP_SER_NOBF  // (measurement variants only: tools/ab_variant.sh)
+  // each wave's image, then its lanes' dummy slots (the branch-free writer's stores that must not land: FastWB)
+  __shared__ __attribute__((aligned(16))) uint8_t s_img[SER_WG / 64][SER_WIMG + 16 + 8 * 64];
+#else
   __shared__ __attribute__((aligned(16))) uint8_t s_img[SER_WG / 64][SER_WIMG + 16];
+#endif
   extern __shared__ __attribute__((aligned(16))) uint8_t s_model[];  // the constant runs (sized at launch)
   __shared__ unsigned long long s_wsum[SER_WG / 64], s_pay[SER_WG / 64];
   const uint32_t tile = blockIdx.x;
@@ -876,6 +881,9 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
   uint8_t* img = s_img[wv];
   const DevValSeg* tab = (const DevValSeg*)s_model;
   const uint8_t* segs = s_model + tb;
+  // every key the wave's WORKFLOW_INSTANCE / JOB values carry is -1, 0 or in [2^16, 2^32): 5-byte integers (ival5)
+  auto in5 = [](int64_t v) { return (uint64_t)(v + 1) <= 1 || (v >= 65536 && v < (1ll << 32)); };
+  const bool l5 = __all(!live || msg || (in5(d.inst_key) && in5(d.scope_key)));
 #pragma unroll 1
   for (int a = 0; a < 64;) {  // rounds: lanes [a, b) whose values fit the image from the round's first byte
     const uint32_t lo = __builtin_amdgcn_readlane(rel, a);
@@ -889,9 +897,15 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
         w.begin(img, sh + (rel - lo));
         fast_encode_msg(w, d, tab, segs, dw, pre);
       } else {
+#ifndef ZB_EXP_SER_NOBF
+        FastWB w;
+        w.begin(img, sh + (rel - lo), SER_WIMG + 16 + 8 * lane);
+#else
         FastW w;
         w.begin(img, sh + (rel - lo));
-        fast_encode(w, d, tab, segs, dw, pre);
+#endif
+        if (l5) fast_encode<true>(w, d, tab, segs, dw, pre);
+        else fast_encode<false>(w, d, tab, segs, dw, pre);
       }
     }
     const uint32_t hi = __builtin_amdgcn_readlane(incl, b - 1);

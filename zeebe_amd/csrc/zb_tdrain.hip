@@ -403,6 +403,10 @@ template <uint32_t IMG>
 __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4))) k_tdrain_write(TDrainParams D) {
   // each wave's image, then its lanes' dummy slots (the branch-free writer's stores that must not land: FastWB)
   __shared__ __attribute__((aligned(16))) uint8_t s_img[TD_WG / 64][IMG + 16 + 8 * 64];
+#ifdef ZB_EXP_OCC2  // (measurement variant: two workgroups per CU)
+  __shared__ uint8_t s_occ[24 * 1024];
+  if (D.wmax == 0xffffffffu) s_occ[threadIdx.x] = 1;
+#endif
   extern __shared__ __attribute__((aligned(16))) uint8_t s_tab[];  // value segments + the batch's tables
   const TrajParams& P = D.t;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
