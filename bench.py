@@ -509,6 +509,8 @@ def steady_line(t, steps, live):
                          "merges": t["merges"] / steps},
             "live_element_instances": t["live_rows"], "pending_jobs": t["pending_jobs"],
             "compactions": t["compactions"],
+            "tick_ms_median": sorted(t["tick_ms"])[len(t["tick_ms"]) // 2] if t.get("tick_ms") else None,
+            "tick_ms_max": max(t["tick_ms"]) if t.get("tick_ms") else None,
             "roofline": roofline(t, steps, "c2s", live), "workload": t["desc"]}
 
 
@@ -559,9 +561,9 @@ def extras(a, barrier):
                            "workload": t["desc"] + " (general wave pipeline, no trajectory path)"}
     import bench_steady
 
-    # (8 ticks: the partition compacts about every sixth tick, and the line's average carries its share)
-    t = bench_steady.run_steady(a, 0, 1, 0, barrier, 8, 1, live=1_000_000)
-    out["c2_steady"] = steady_line(t, 8, 1_000_000)
+    # (24 ticks: the partition compacts about every fifth tick, and the line's average carries its share)
+    t = bench_steady.run_steady(a, 0, 1, 0, barrier, 24, 1, live=1_000_000)
+    out["c2_steady"] = steady_line(t, 24, 1_000_000)
     out["c1_exact_tree"] = run_exact_tree(a)
     t = run_workload("c4", 1_000_000, a, 0, 1, 0, barrier, 3, 1)
     out["c4"] = {"value": t["transitions"] / t["elapsed"], "ms_per_step": t["elapsed"] * 1e3 / 3,

@@ -118,6 +118,9 @@ def run_steady(a, rank, world, local_rank, barrier, steps, warmup, live=1_000_00
     from zeebe_amd.engine import Engine
 
     recs_tick = live // FRACTION * 8 + (live // (FRACTION * TASKS)) * 12 + CANCELS * 10
+    # (per tick ~290K rows and ~130 MB of documents become garbage: the partition compacts about every fifth tick.
+    # Measured with 9M rows / a 5 GB arena instead: 2 compactions in 24 ticks but 2.2 ms each against 0.85 -- the
+    # mark / gather passes span every allocated byte -- and 1.32 ms per tick either way)
     eng = Engine(device=0 if a.same_device else local_rank, partition_id=rank, partition_count=world,
                  log_capacity=max(live * 12, 4 * recs_tick), row_capacity=4 * live + (1 << 20),
                  arena_bytes=(live * 1200) + (256 << 20), external_jobs=True)
@@ -139,7 +142,7 @@ def run_steady(a, rank, world, local_rank, barrier, steps, warmup, live=1_000_00
                process_ms=0.0, emit_ms=0.0, aux_ms=0.0, main_ms=0.0, launches=0, waves=0, step_s=0.0, drain_s=0.0,
                ser_write_ms=0.0, ser_size_ms=0.0, value_bytes=0, payload_bytes=0, drained=0, path=0, generic_tiles=0,
                template_drain=0, create_bytes=0, instances=live, inputs=0, completions=0, cancels=0, creates=0,
-               elapsed=0.0, live_rows=0)
+               elapsed=0.0, live_rows=0, tick_ms=[])
 
     def one_tick(timed):
         pay, descs, vals, n_done, n_cancel, n_create = w.inputs()
@@ -158,6 +161,7 @@ def run_steady(a, rank, world, local_rank, barrier, steps, warmup, live=1_000_00
         t2 = time.perf_counter()
         assert st["quiescent"], st
         if timed:
+            tot["tick_ms"].append((t2 - t0) * 1e3)
             tot["elapsed"] += t2 - t0
             tot["step_s"] += t1 - t0
             tot["drain_s"] += t2 - t1
