@@ -90,6 +90,9 @@ struct zb_engine {
   DevVec<uint16_t> d_cond;
   DevVec<uint32_t> d_code;
   DevVec<uint32_t> d_cls_code;  // the program with the split conditions' path operands as extraction slots
+  DevVec<uint32_t> d_cls_atom;  // outcome table (k_cls_classify): the conditions' comparisons (pcs)
+  DevVec<uint8_t> d_cls_table;  //   and the class key of every combination of their outcomes
+  int cls_natoms = 0;
   DevVec<DevConst> d_consts;
   DevVec<uint64_t> d_const_w;  // [consts][2] the bytes of string constants of at most 16 bytes (classify)
   DevVec<DevQuery> d_queries;
@@ -726,6 +729,9 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
     if (!p.io) HIPCHECK(e, hipMemsetAsync(e->c_perm, 0xff, cls_slot_bound((uint64_t)n, nwg) * sizeof(uint32_t), e->stream));
     p.nsplits = e->nsplits;
     p.cls_nq = e->cls_nq;
+    p.cls_natoms = e->cls_natoms;
+    p.cls_atom_pc = e->d_cls_atom.p;
+    p.cls_table = e->d_cls_table.p;
     for (int j = 0; j < CLS_QMAX; j++) {
       p.cls_q[j] = e->cls_q[j];
       p.cls_key_off[j] = e->cls_key_off[j];
@@ -1460,7 +1466,7 @@ void zb_engine_destroy(zb_engine* e) {
   if (e->h_ctl_pinned) (void)hipHostFree(e->h_ctl_pinned);
   if (e->h_stats_pinned) (void)hipHostFree(e->h_stats_pinned);
   if (e->h_up) (void)hipHostFree(e->h_up);
-  e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_cls_code.free(); e->d_consts.free(); e->d_const_w.free();
+  e->d_elems.free(); e->d_wfs.free(); e->d_cond.free(); e->d_code.free(); e->d_cls_code.free(); e->d_cls_atom.free(); e->d_cls_table.free(); e->d_consts.free(); e->d_const_w.free();
   e->d_queries.free(); e->d_filters.free(); e->d_pool.free(); e->d_staged.free(); e->d_staged_arena.free();
   e->d_ranges.free(); e->d_cmd_pool.free(); e->d_lookup_keys.free(); e->d_lookup_pos.free();
   e->d_maps.free();
@@ -1693,6 +1699,68 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
     }
   }
   HIPCHECK(e, e->d_cls_code.upload(cc, e->stream));
+  // The outcome table: with at most CLS_TABLE_ATOMS comparisons in the split conditions, the class key is a function
+  // of their outcomes (false / true / error), which the conditions' programs give by this walk -- the control flow of
+  // eval_condition_sweep: forward jumps on the last result, an error ends the condition (its split's digit: cc + 1)
+  e->cls_natoms = 0;
+  if (e->cls_nq) {
+    std::vector<uint32_t> atoms;
+    bool ok = true;
+    for (int k = 0; k < e->nsplits && ok; k++) {
+      const DevElem& el = e->model.elems[e->split_elem[k]];
+      for (uint32_t c = 0; c < el.cond_count && ok; c++) {
+        const DevElem& flow = e->model.elems[e->model.cond_flows[el.cond_begin + c]];
+        if (flow.cond_prog == NO_REF) { ok = false; break; }
+        for (uint32_t pc = flow.cond_prog; ; pc++) {
+          if (2 * pc + 1 >= cc.size()) { ok = false; break; }
+          const uint32_t op = cc[2 * pc] & 0xff;
+          if (op == PC_END) break;
+          if (op == PC_CMP && std::find(atoms.begin(), atoms.end(), pc) == atoms.end()) atoms.push_back(pc);
+        }
+      }
+    }
+    if (ok && !atoms.empty() && atoms.size() <= CLS_TABLE_ATOMS) {
+      uint32_t entries = 1;
+      for (size_t a = 0; a < atoms.size(); a++) entries *= 3;
+      std::vector<uint8_t> table(entries);
+      std::vector<uint8_t> out(atoms.size());
+      for (uint32_t idx = 0; idx < entries && ok; idx++) {
+        for (size_t a = 0, v = idx; a < atoms.size(); a++, v /= 3) out[a] = (uint8_t)(v % 3);
+        uint32_t key = 0;
+        for (int k = 0; k < e->nsplits; k++) {
+          const DevElem& el = e->model.elems[e->split_elem[k]];
+          uint32_t o = el.cond_count;
+          for (uint32_t c = 0; c < el.cond_count; c++) {
+            const DevElem& flow = e->model.elems[e->model.cond_flows[el.cond_begin + c]];
+            int res = 0;  // 0 false, 1 true, 2 error
+            bool r = false;
+            for (uint32_t pc = flow.cond_prog; 2 * pc + 1 < cc.size();) {
+              const uint32_t w0 = cc[2 * pc], opc = w0 & 0xff;
+              if (opc == PC_END) { res = r ? 1 : 0; break; }
+              if (opc == PC_JF || opc == PC_JT) {
+                pc = ((opc == PC_JF) ? !r : r) ? (w0 >> 16) : pc + 1;
+                continue;
+              }
+              const uint8_t v = out[std::find(atoms.begin(), atoms.end(), pc) - atoms.begin()];
+              if (v == 2) { res = 2; break; }
+              r = v == 1;
+              pc++;
+            }
+            if (res == 2) { o = el.cond_count + 1; break; }
+            if (res == 1) { o = c; break; }
+          }
+          key += o * e->split_stride[k];
+        }
+        if (key > 255) ok = false;
+        table[idx] = (uint8_t)key;
+      }
+      if (ok) {
+        HIPCHECK(e, e->d_cls_atom.upload(atoms, e->stream));
+        HIPCHECK(e, e->d_cls_table.upload(table, e->stream));
+        e->cls_natoms = (int)atoms.size();
+      }
+    }
+  }
   return upload_model(e);
 }
 

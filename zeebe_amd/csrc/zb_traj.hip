@@ -1262,6 +1262,57 @@ __device__ __forceinline__ void str_words(const TrajParams& P, bool is_path, uin
   }
 }
 
+// One comparison of the json-el VM (eval_condition, zb_devlib.hpp) on the extraction (EXT) or the document: 0 false,
+// 1 true, 2 an error (out / unsupported say which), with eval_condition's operand loading and type rules.
+template <bool EXT>
+__device__ __forceinline__ int eval_atom(const TrajParams& P, uint32_t w0, uint32_t w1, const uint8_t* doc, uint32_t n,
+                                         const Extract& ext, CondOut& out, bool& unsupported) {
+  const uint32_t op = (w0 >> 8) & 0xf;
+  Operand x, y;
+  const bool lx = EXT ? load_operand_x(P, (w0 >> 12) & 1, w1 & 0xffff, doc, ext, x, out, unsupported)
+                      : load_operand_k(P, (w0 >> 12) & 1, w1 & 0xffff, doc, n, x, out, unsupported);
+  const bool ly = lx && (EXT ? load_operand_x(P, (w0 >> 13) & 1, w1 >> 16, doc, ext, y, out, unsupported)
+                             : load_operand_k(P, (w0 >> 13) & 1, w1 >> 16, doc, n, y, out, unsupported));
+  if (!lx || !ly) return 2;
+  bool r;
+  if (op == OP_EQ || op == OP_NE) {
+    bool eq = false;
+    if (x.type == TT_NIL) eq = y.type == TT_NIL;
+    else if (y.type == TT_NIL) eq = false;
+    else {
+      if (!same_type(x, y, out)) return 2;
+      switch (x.type) {
+        case TT_STRING:
+          if (EXT && x.slen == y.slen && x.slen <= 16) {  // as words: a path operand's bytes from the LDS document,
+            uint64_t a0, a1, b0, b1;                       // a constant's precomputed
+            str_words(P, (w0 >> 12) & 1, w1 & 0xffff, x, a0, a1);
+            str_words(P, (w0 >> 13) & 1, w1 >> 16, y, b0, b1);
+            eq = a0 == b0 && a1 == b1;
+          } else {
+            eq = x.slen == y.slen && bytes_eq(x.s, y.s, x.slen);
+          }
+          break;
+        case TT_BOOLEAN: eq = x.bval == y.bval; break;
+        case TT_INTEGER: eq = x.ival == y.ival; break;
+        case TT_FLOAT: eq = x.fval == y.fval; break;
+        default: out.err = EC_CMP_TYPE; out.a = x.type; return 2;
+      }
+    }
+    r = (op == OP_EQ) ? eq : !eq;
+  } else {
+    if (!same_type(x, y, out)) return 2;
+    if (x.type != TT_INTEGER && x.type != TT_FLOAT) { out.err = EC_NOT_NUMBER; out.a = x.type; return 2; }
+    if (x.type == TT_INTEGER) {
+      r = op == OP_LT ? x.ival < y.ival : op == OP_LE ? x.ival <= y.ival : op == OP_GT ? x.ival > y.ival
+                                                                                     : x.ival >= y.ival;
+    } else {
+      r = op == OP_LT ? x.fval < y.fval : op == OP_LE ? x.fval <= y.fval : op == OP_GT ? x.fval > y.fval
+                                                                                     : x.fval >= y.fval;
+    }
+  }
+  return r ? 1 : 0;
+}
+
 // The json-el VM (eval_condition, zb_devlib.hpp) as one wave-uniform sweep over the program: every lane
 // runs the same program and its jumps only go forward (zb_model.cpp emit), so instruction pc is
 // fetched once per wave through the scalar cache and executed by the lanes whose own pc is there.
@@ -1283,51 +1334,12 @@ __device__ __forceinline__ bool eval_condition_sweep(const TrajParams& P, uint32
       continue;
     }
     mine = pc + 1;
-    const uint32_t op = (w0 >> 8) & 0xf;
-    Operand x, y;
-    const bool lx = EXT ? load_operand_x(P, (w0 >> 12) & 1, w1 & 0xffff, doc, ext, x, out, unsupported)
-                        : load_operand_k(P, (w0 >> 12) & 1, w1 & 0xffff, doc, n, x, out, unsupported);
-    const bool ly = lx && (EXT ? load_operand_x(P, (w0 >> 13) & 1, w1 >> 16, doc, ext, y, out, unsupported)
-                               : load_operand_k(P, (w0 >> 13) & 1, w1 >> 16, doc, n, y, out, unsupported));
-    if (!lx || !ly) {
+    const int o = eval_atom<EXT>(P, w0, w1, doc, n, ext, out, unsupported);
+    if (o == 2) {
       done = true;
       continue;
     }
-    if (op == OP_EQ || op == OP_NE) {
-      bool eq = false;
-      if (x.type == TT_NIL) eq = y.type == TT_NIL;
-      else if (y.type == TT_NIL) eq = false;
-      else {
-        if (!same_type(x, y, out)) { done = true; continue; }
-        switch (x.type) {
-          case TT_STRING:
-            if (EXT && x.slen == y.slen && x.slen <= 16) {  // as words: a path operand's bytes from the LDS document,
-              uint64_t a0, a1, b0, b1;                       // a constant's precomputed
-              str_words(P, (w0 >> 12) & 1, w1 & 0xffff, x, a0, a1);
-              str_words(P, (w0 >> 13) & 1, w1 >> 16, y, b0, b1);
-              eq = a0 == b0 && a1 == b1;
-            } else {
-              eq = x.slen == y.slen && bytes_eq(x.s, y.s, x.slen);
-            }
-            break;
-          case TT_BOOLEAN: eq = x.bval == y.bval; break;
-          case TT_INTEGER: eq = x.ival == y.ival; break;
-          case TT_FLOAT: eq = x.fval == y.fval; break;
-          default: out.err = EC_CMP_TYPE; out.a = x.type; done = true; continue;
-        }
-      }
-      r = (op == OP_EQ) ? eq : !eq;
-    } else {
-      if (!same_type(x, y, out)) { done = true; continue; }
-      if (x.type != TT_INTEGER && x.type != TT_FLOAT) { out.err = EC_NOT_NUMBER; out.a = x.type; done = true; continue; }
-      if (x.type == TT_INTEGER) {
-        r = op == OP_LT ? x.ival < y.ival : op == OP_LE ? x.ival <= y.ival : op == OP_GT ? x.ival > y.ival
-                                                                                       : x.ival >= y.ival;
-      } else {
-        r = op == OP_LT ? x.fval < y.fval : op == OP_LE ? x.fval <= y.fval : op == OP_GT ? x.fval > y.fval
-                                                                                       : x.fval >= y.fval;
-      }
-    }
+    r = o == 1;
   }
   unsupported = true;
   return false;
@@ -1338,6 +1350,17 @@ template <bool EXT>
 __device__ __forceinline__ uint32_t outcome_key(const TrajParams& P, const uint8_t* doc, uint32_t len) {
   Extract ext;
   if (EXT) extract_fast(P, doc, len, ext);
+  if (EXT && P.cls_natoms) {  // the outcome table: every comparison once, then one lookup
+    uint32_t idx = 0, mul = 1;
+    for (int a = 0; a < P.cls_natoms; a++) {
+      const uint32_t pc = K(P.cls_atom_pc)[a];
+      CondOut co{0, 0, 0, 0};
+      bool unsup = false;
+      idx += (uint32_t)eval_atom<true>(P, K(P.cls_code)[2 * pc], K(P.cls_code)[2 * pc + 1], doc, len, ext, co, unsup) * mul;
+      mul *= 3;
+    }
+    return P.cls_table[idx];
+  }
   uint32_t key = 0;
   for (int k = 0; k < P.nsplits; k++) {
     const ElemCtl el = elem_ctl(P, P.split_elem[k]);
