@@ -184,3 +184,35 @@ def test_growing_class_batches_on_one_engine(io):
     for a, b in zip(ref, got):
         assert (a.position, a.key, a.intent, a.value) == (b.position, b.key, b.intent, b.value), a.position
     e.close()
+
+
+def _short_circuit_model():
+    b = bpmn.Bpmn.create_executable_process("sc").start_event("s").exclusive_gateway("g")
+    b.sequence_flow_id("f1").condition("$.a < 5 && $.b == 'x'").end_event("e1")
+    b.move_to_node("g").sequence_flow_id("f2").condition("$.a >= 5 || $.c > 1.5").end_event("e2")
+    return b.move_to_node("g").default_flow().sequence_flow_id("f3").end_event("e3").done()
+
+
+@pytest.mark.parametrize("errors", [False, True])
+def test_outcome_table_short_circuit(errors):
+    # k_cls_classify's outcome table (every comparison once, the class key looked up): short-circuit && / ||, and
+    # comparisons whose operand is missing or of another type (an error only where the program reaches it: `$.b`
+    # is never read when `$.a < 5` is false)
+    rng = random.Random(3)
+    payloads = []
+    for i in range(900):
+        d = {"a": rng.randrange(10), "b": rng.choice(["x", "y"]), "c": rng.choice([1.0, 2.0])}
+        if errors:
+            r = rng.random()
+            if r < 0.1:
+                del d["b"]
+            elif r < 0.2:
+                d["b"] = 7
+            elif r < 0.3:
+                del d["c"]
+            elif r < 0.35:
+                d["a"] = "s"
+        payloads.append(msgpack.packb(d))
+    st = _run(_short_circuit_model().to_xml(), "sc", payloads)
+    if not errors:
+        assert st["path"] == 2  # (with errors: incident classes send the batch to the per-instance path)
