@@ -38,7 +38,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BYTES_PER_TRANSITION = 96  # 32 B row read + 32 B row write + 32 B record descriptor
 DESC_BYTES = 32  # one zb_rec descriptor per log record
 HDR_BYTES = 24  # one zb_record_header per drained record
-PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r04", "r03")]  # newest first
+PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r05", "r04", "r03")]  # newest first
 METRIC = "BPMN element transitions/sec (+ completed instances/sec) per node; % HBM roofline"
 
 
