@@ -90,7 +90,7 @@ struct zb_engine {
   DevVec<uint16_t> d_cond;
   DevVec<uint32_t> d_code;
   DevVec<uint32_t> d_cls_code;  // the program with the split conditions' path operands as extraction slots
-  DevVec<uint32_t> d_cls_atom;  // outcome table (k_cls_classify): the conditions' comparisons (pcs)
+  DevVec<uint32_t> d_cls_atom;  // outcome table (k_cls_classify): the conditions' comparisons (their code words)
   DevVec<uint8_t> d_cls_table;  //   and the class key of every combination of their outcomes
   int cls_natoms = 0;
   DevVec<DevConst> d_consts;
@@ -730,7 +730,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
     p.nsplits = e->nsplits;
     p.cls_nq = e->cls_nq;
     p.cls_natoms = e->cls_natoms;
-    p.cls_atom_pc = e->d_cls_atom.p;
+    p.cls_atom_w = e->d_cls_atom.p;
     p.cls_table = e->d_cls_table.p;
     for (int j = 0; j < CLS_QMAX; j++) {
       p.cls_q[j] = e->cls_q[j];
@@ -1755,7 +1755,9 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
         table[idx] = (uint8_t)key;
       }
       if (ok) {
-        HIPCHECK(e, e->d_cls_atom.upload(atoms, e->stream));
+        std::vector<uint32_t> aw;  // (the code words themselves: no dependent load of the pc on the device)
+        for (uint32_t pc : atoms) { aw.push_back(cc[2 * pc]); aw.push_back(cc[2 * pc + 1]); }
+        HIPCHECK(e, e->d_cls_atom.upload(aw, e->stream));
         HIPCHECK(e, e->d_cls_table.upload(table, e->stream));
         e->cls_natoms = (int)atoms.size();
       }

@@ -525,6 +525,9 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
         }
         const uint32_t hi = __builtin_amdgcn_readlane(incl, b - 1);
         TD_PHASE(2);
+#ifdef ZB_EXP_PRIO  // (measurement variant: the stream at raised wave priority)
+        __builtin_amdgcn_s_setprio(2);
+#endif
         wave_lds_sync();
 #if defined(ZB_EXP_STREAM4)
         wave_stream4(img, D.out, wbase + lo, sh, hi - lo, lane);
@@ -532,6 +535,9 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
         wave_stream(img, D.out, wbase + lo, sh, hi - lo, lane);
 #endif
         wave_lds_sync();  // the image is reused by the next round
+#ifdef ZB_EXP_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
         TD_PHASE(3);
         a = b;
       }

@@ -1351,12 +1351,18 @@ __device__ __forceinline__ uint32_t outcome_key(const TrajParams& P, const uint8
   Extract ext;
   if (EXT) extract_fast(P, doc, len, ext);
   if (EXT && P.cls_natoms) {  // the outcome table: every comparison once, then one lookup
+    // (the comparisons' code words all loaded up front: one scalar load round trip, not one per comparison)
+    const int na = P.cls_natoms;
+    uint32_t aw[2 * CLS_TABLE_ATOMS];
+#pragma unroll
+    for (int a = 0; a < 2 * CLS_TABLE_ATOMS; a++) aw[a] = a < 2 * na ? K(P.cls_atom_w)[a] : 0u;
     uint32_t idx = 0, mul = 1;
-    for (int a = 0; a < P.cls_natoms; a++) {
-      const uint32_t pc = K(P.cls_atom_pc)[a];
+#pragma unroll
+    for (int a = 0; a < CLS_TABLE_ATOMS; a++) {
+      if (a >= na) break;
       CondOut co{0, 0, 0, 0};
       bool unsup = false;
-      idx += (uint32_t)eval_atom<true>(P, K(P.cls_code)[2 * pc], K(P.cls_code)[2 * pc + 1], doc, len, ext, co, unsup) * mul;
+      idx += (uint32_t)eval_atom<true>(P, aw[2 * a], aw[2 * a + 1], doc, len, ext, co, unsup) * mul;
       mul *= 3;
     }
     return P.cls_table[idx];
