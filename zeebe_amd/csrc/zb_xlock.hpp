@@ -37,12 +37,18 @@ __device__ __forceinline__ void x_exclusive(const XSlabs& X, bool need, F&& f) {
   }
 }
 
+// The XCD this wave runs on (HW_REG_XCC_ID, 0..7)
+__device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u; }
+
 // The exact tree for every lane with `need`: first each in a XLANE_BYTES workspace of its own, all lanes of the wave at
 // once; a pair whose tree does not fit it (X_UNSUP, nothing written yet) then takes a big slab in turns (x_exclusive).
-// The wave's lanes use the 64 workspaces of one lane group (by the wave's index in the launch, modulo XLANE_GROUPS),
-// which the wave holds for the duration: a launch of more waves than groups (a trajectory batch of 100K instances is
-// 1,563 waves) shares them, a wave waiting for its group while another wave runs its trees in it. (Indexed by the
-// global thread id instead, every thread past XLANE_COUNT took the locked big slab: 4.9 s per 100K-instance tick.)
+// The wave's lanes use the 64 workspaces of one lane group, which the wave holds for the duration (a lock no holder
+// waits on anything while holding). The groups are split among the 8 XCDs and a wave takes one of its own XCD's
+// (HW_REG_XCC_ID; within it by the block's rank among the blocks dealt to that XCD): a workspace is only ever
+// written through one XCD's L2, so a holder needs no agent-scope fence -- its stores reaching that L2 before the lock
+// is released (vmcnt) is enough, and x_merge / x_map read only workspace bytes they wrote in the same call. (Across
+// XCDs the per-XCD L2s are not coherent: a workspace shared by two XCDs needed __threadfence -- an L2 write-back and
+// an L1 invalidate -- around every hold, 3 ms of an 8.9 ms tick that merges 1M documents through the tree.)
 // f(slab, bytes, final) -> X_* status; it commits its outcome unless it returns X_UNSUP with final false.
 template <class F>
 __device__ __forceinline__ void x_run(const XSlabs& X, bool need, F&& f) {
@@ -50,14 +56,18 @@ __device__ __forceinline__ void x_run(const XSlabs& X, bool need, F&& f) {
   const uint64_t m = (uint64_t)__ballot(need);
   if (m && X.lanes) {
     const int lane = threadIdx.x & 63;
-    const uint32_t g = (uint32_t)(((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % XLANE_GROUPS);
+    constexpr uint32_t GPX = XLANE_GROUPS / 8;  // groups per XCD
+    static_assert(XLANE_GROUPS % 8 == 0, "lane groups split evenly over the XCDs");
+    const uint32_t local = (uint32_t)(((uint64_t)(blockIdx.x / 8) * (blockDim.x >> 6) + (threadIdx.x >> 6)) % GPX);
+    const uint32_t g = __builtin_amdgcn_readfirstlane(xcc_id()) * GPX + local;
     uint32_t* lock = X.locks + XSLAB_COUNT + g;
     const int l0 = __ffsll((unsigned long long)m) - 1;
     if (lane == l0)
       while (atomicCAS(lock, 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(4);
-    __threadfence();
+    __builtin_amdgcn_wave_barrier();
     if (need) again = f(X.lanes + ((uint64_t)g * 64 + lane) * XLANE_BYTES, XLANE_BYTES, false) == X_UNSUP;
-    __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (every lane's workspace stores are in the XCD's L2)
+    __builtin_amdgcn_wave_barrier();
     if (lane == l0) atomicExch(lock, 0u);
   }
   x_exclusive(X, again, [&](uint8_t* slab) { (void)f(slab, XSLAB_BYTES, true); });
