@@ -230,6 +230,9 @@ struct zb_engine {
   uint64_t cls_cap = 0;           // instances the class buffers hold
   uint8_t* c_ikey = nullptr;
   uint32_t* c_clen = nullptr;
+  uint32_t* d_cref = nullptr;  // [cref_cap] the last injected batch's payload refs (k_inject), at log position cref_base
+  uint64_t cref_cap = 0;
+  int64_t cref_base = -1;
   uint32_t *c_khist = nullptr, *c_krep = nullptr;  // [CLS_HB][256] each (one allocation with c_klen)
   uint64_t* c_klen = nullptr;                       // [CLS_HB][256]
   TmplRec* t_tmpl = nullptr;     // [CLS_MAX][CLS_ROW][TF] traced records (uniform / class batches)
@@ -700,6 +703,8 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   p.pool = e->d_pool.p;
   p.log_base = log_base;
   p.n = n;
+  // (the batch k_inject just wrote: its CREATE payload refs as a compact array)
+  p.cref = (e->d_cref && e->cref_base == log_base && (uint64_t)n <= e->cref_cap) ? e->d_cref : nullptr;
   p.wf_start = e->host_hdr.wf_next;
   p.job_start = e->host_hdr.job_next;
   p.nwg = (int32_t)nwg;
@@ -1449,7 +1454,7 @@ void zb_engine_destroy(zb_engine* e) {
                 e->sort_tmp, e->d_spread, e->mapres, e->map_ws, e->log_mem, e->links_mem, e->srcd_mem, e->row_mem, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
                 e->merge_jobs, e->merge_slow, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
-                e->c_plan, e->c_ikey, e->c_clen, e->c_khist, e->c_mask, e->c_cg, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
+                e->c_plan, e->c_ikey, e->c_clen, e->d_cref, e->c_khist, e->c_mask, e->c_cg, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
                 e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->look_keys, e->look_idx,
                 e->conf_first, e->xslab, e->xlocks, e->xlane, e->phase};
   for (void* p : ps)
@@ -2446,6 +2451,15 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     // documents in place: only the refs are rebased (the batch's documents are referenced where they lie)
     ip.arena_base = e->staged_in_place ? e->staged_base : (uint64_t)e->host_hdr.arena_next;
     ip.staged_bytes = e->staged_in_place ? 0 : e->staged_arena.size();
+    if ((uint64_t)n > e->cref_cap) {
+      if (e->d_cref) (void)hipFree(e->d_cref);
+      e->d_cref = nullptr;
+      e->cref_cap = 0;
+      HIPCHECK(e, hipMalloc(&e->d_cref, (uint64_t)n * sizeof(uint32_t)));
+      e->cref_cap = (uint64_t)n;
+    }
+    ip.cref = e->d_cref;
+    e->cref_base = ip.log_base;
     launch_inject(ip, e->stream);
     // records naming an element instance by key: its row (ElementInstanceIndex.getInstance); the (key, index)
     // pairs were uploaded with the batch and are sorted here, on the device

@@ -1103,6 +1103,7 @@ __global__ void k_inject(InjectParams P) {
     P.links[P.log_base + i] = ~0ull;  // no rows yet
     P.srcd[P.log_base + i] = 0;       // written by another writer (client API, job processor, ...)
     P.vlen[P.log_base + i] = P.staged_vlen[i];
+    P.cref[i] = d.payload;
   }
   const uint64_t nw = P.staged_bytes / 8;
   const uint64_t* src = (const uint64_t*)P.staged_arena;

@@ -269,7 +269,7 @@ __device__ __forceinline__ TdLane td_lane(const TrajParams& P, const TdTab& T, i
     for (int c = 0; c < CLS_MAX; c++) t.L.before[c] = c == 0 ? (uint32_t)t.inst : 0;
   }
   t.W = t.active ? P.wcount[t.cls] : 0;  // generations of the instance's class (rows beyond it are not its)
-  t.create_ref = (need_ref || !P.clen) ? P.log[P.log_base + t.inst].payload : 0u;
+  t.create_ref = (need_ref || !P.clen) ? (P.cref ? P.cref[t.inst] : P.log[P.log_base + t.inst].payload) : 0u;
   t.create_len = P.clen ? P.clen[t.inst] : arena_len(P.arena, t.create_ref);
   t.kwf0 = td_kbase(T, t.L, 0, 1);
   return t;

@@ -1399,7 +1399,7 @@ __global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
   const int64_t i = (int64_t)blockIdx.x * TWG + t;
   uint32_t mkey = 0, mlen = 0;
   if (i < P.n) {
-    const uint32_t ref = P.log[P.log_base + i].payload;
+    const uint32_t ref = P.cref ? P.cref[i] : P.log[P.log_base + i].payload;
     const uint8_t* pp = P.arena + (uint64_t)ref * 8;
     const uint32_t len = *(const uint32_t*)pp;
     // the VM inlined on the LDS copy (LDS loads per token); a document too large for the copy gets the
