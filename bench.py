@@ -56,6 +56,12 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="skip the extra C2 wave-only / C4 lines")
     ap.add_argument("--no-drain", action="store_true", help="device stepping only (not the contract's step)")
     ap.add_argument("--wave-only", action="store_true", help="force the general wave pipeline (no trajectory path)")
+    ap.add_argument("--jobs", choices=("harness", "external", "processor"), default="harness",
+                    help="job mode: the canonical in-kernel harness, ZB_CFG_EXTERNAL_JOBS or ZB_CFG_JOB_PROCESSOR (the "
+                         "modes INTEGRATION.md binds)")
+    ap.add_argument("--frames", action="store_true",
+                    help="drain log frames (zb_serialize_frames, with request metadata on every CREATE) instead of "
+                         "values + headers")
     ap.add_argument("--steady", action="store_true",
                     help="C2 steady state (bench_steady.py): live instances waiting on jobs, ticks of job completions, "
                          "creates and cancels, external job processor")
@@ -106,8 +112,13 @@ def make_engine(cfg, n, a, rank, world, local_rank):
     # row per live element instance: C3 wave-only needs the process + gateway / task rows of every instance)
     rows = {"c1": n * 3, "c2": n * (a.tasks + 2), "c3": n * 3 if a.wave_only else 1 << 20, "c4": n * 20}[cfg]
     arena = {"c1": n * 96, "c2": n * (48 + 48 * a.tasks), "c3": n * 64, "c4": n * 1200}[cfg] + (64 << 20)
+    jobs = getattr(a, "jobs", "harness")
     return Engine(device=0 if a.same_device else local_rank, partition_id=rank, partition_count=world,
-                  log_capacity=int(n * recs), row_capacity=int(rows), arena_bytes=int(arena), wave_only=a.wave_only)
+                  log_capacity=int(n * recs), row_capacity=int(rows), arena_bytes=int(arena), wave_only=a.wave_only,
+                  external_jobs=jobs == "external", job_processor=jobs == "processor")
+
+
+FRAME_CFG = dict(stream_id=1, raft_term=3, timestamp=1_700_000_000_000)  # (the broker's log stream / raft term)
 
 
 def run_workload(cfg, n, a, rank, world, local_rank, barrier, steps, warmup, drain=True, pcie=False):
@@ -119,6 +130,12 @@ def run_workload(cfg, n, a, rank, world, local_rank, barrier, steps, warmup, dra
     eng.create_packed(pid, blob, offs)
     create_bytes = len(blob) + 4 * n  # the CREATE payload documents ([u32 len][bytes]) in the arena
     del blob
+    frames = getattr(a, "frames", False)
+    if frames:  # every CREATE carries its client request (CreateWorkflowInstanceRequest: request id, stream id)
+        import numpy as np
+
+        eng.set_request_metadata_np(np.arange(n, dtype=np.uint64) + (rank << 40), np.arange(n, dtype=np.int32) % 64)
+    eng.upload_staged()  # (the staged batch in HBM before the timed region)
 
     def one_step():
         eng.reset(keep_staged=True)
@@ -127,7 +144,9 @@ def run_workload(cfg, n, a, rank, world, local_rank, barrier, steps, warmup, dra
         t1 = time.perf_counter()
         assert st["quiescent"], st
         ser = None
-        if drain:  # the tick's emitted records (everything after the n injected commands)
+        if drain and frames:  # the tick's records as log frames (the broker appends them: INTEGRATION.md)
+            ser = eng.serialize_frames(n, eng.log_size() - n, **FRAME_CFG)
+        elif drain:  # the tick's emitted records (everything after the n injected commands)
             ser = eng.serialize(n, eng.log_size() - n)
         t2 = time.perf_counter()
         return st, ser, t1 - t0, t2 - t1
@@ -170,6 +189,8 @@ def run_workload(cfg, n, a, rank, world, local_rank, barrier, steps, warmup, dra
     tot["elapsed"] = time.perf_counter() - t0
     tot["desc"] = desc
     tot["create_bytes"] = create_bytes
+    tot["frames"] = frames
+    tot["jobs"] = getattr(a, "jobs", "harness")
     if pcie and drain:
         tot["pcie"] = pcie_step(eng, n, one_step)
     eng.close()
@@ -341,7 +362,14 @@ def load_traffic_step(tag, kernel_prefixes):
 def roofline(tot, steps, cfg, n):
     """Dominant kernel of the step: the drain's write pass or the main emit launch, by device time."""
     cands = []
-    if tot["ser_write_ms"] > 0 and tot["template_drain"] == steps:
+    if tot["ser_write_ms"] > 0 and tot["template_drain"] == steps and tot.get("frames"):
+        # the template drain writing log frames: every drained record's frame (104-byte prefix + value + padding)
+        # written, per instance its CREATE descriptor, CREATE payload document and request metadata (24 B) read once
+        b = (tot["value_bytes"] + steps * (tot["instances"] * (DESC_BYTES + 24) + tot["create_bytes"])) / steps
+        cands.append(("zbg::k_tdrain_write<frames>", tot["ser_write_ms"] / steps, b,
+                      "log frame bytes written per drained record (104 B prefix + value + padding) + 32 B CREATE "
+                      "descriptor, the CREATE payload document and 24 B of request metadata read per instance"))
+    elif tot["ser_write_ms"] > 0 and tot["template_drain"] == steps:
         # the template drain (zb_tdrain.hip): per launch every drained record's header and value written, and per
         # instance its CREATE descriptor and CREATE payload document read once (the traces and generation bases
         # are a few KB, read from the scalar cache)
@@ -468,10 +496,11 @@ def main():
             "dtype": "int64",
             "data": "synthetic (SURVEY §8d %s inputs, deterministic)" % a.config.upper(),
             "config": {"workload": tot["desc"], "instances_per_gpu": n, "partitions": world,
-                       "parallelism": "partition-per-gpu",
+                       "parallelism": "partition-per-gpu", "jobs": a.jobs,
                        "timed_step": "inject staged CREATEs (in HBM) + lockstep waves to quiescence" +
-                                     ("" if a.no_drain else " + zb_serialize of every emitted record (values + "
-                                                              "headers, in HBM)")},
+                                     ("" if a.no_drain else
+                                      " + zb_serialize_frames of every emitted record (log frames, in HBM)" if a.frames
+                                      else " + zb_serialize of every emitted record (values + headers, in HBM)")},
             "completed_instances_per_s": all_comp / elapsed,
             "records_written_per_step": tot["written"] / steps,
             "wave_launches_per_step": tot["launches"] / steps,
@@ -480,7 +509,7 @@ def main():
                                   "drain_size_kernel": tot["ser_size_ms"] / steps,
                                   "drain_write_kernel": tot["ser_write_ms"] / steps},
             "value_stepping_only": tot["transitions"] / tot["step_s"] if tot["step_s"] else None,
-            "drained_bytes_per_step": tot["value_bytes"] / steps + HDR_BYTES * tot["drained"] / steps,
+            "drained_bytes_per_step": tot["value_bytes"] / steps + (0 if a.frames else HDR_BYTES * tot["drained"] / steps),
             "roofline": roofline(tot, steps, a.config, n),
         }
         if "pcie" in tot:
@@ -547,6 +576,21 @@ def extras(a, barrier):
     """Shorter lines on the other single-GPU configurations (same step definition, 3 steps each)."""
     out = {}
     import copy
+
+    # the integration's own configuration (INTEGRATION.md: ZB_CFG_EXTERNAL_JOBS; the broker appends log frames through
+    # LogStreamBatchWriter): C3 10M with values + headers, and with log frames carrying every CREATE's request metadata
+    for name, frames in (("c3_integration_values", False), ("c3_integration_frames", True)):
+        b = copy.copy(a)
+        b.jobs, b.frames, b.wave_only = "external", frames, False
+        t = run_workload("c3", 10_000_000, b, 0, 1, 0, barrier, 3, 1)
+        out[name] = {"value": t["transitions"] / t["elapsed"], "ms_per_step": t["elapsed"] * 1e3 / 3,
+                     "stepping_ms": t["step_s"] * 1e3 / 3, "drain_ms": t["drain_s"] * 1e3 / 3,
+                     "path": t["path"], "template_drain": t["template_drain"] == 3,
+                     "drained_bytes_per_step": t["value_bytes"] / 3 + (0 if frames else HDR_BYTES * t["drained"] / 3),
+                     "roofline": roofline(t, 3, "c3f" if frames else "c3x", 10_000_000),
+                     "workload": t["desc"] + ", ZB_CFG_EXTERNAL_JOBS, drain: " +
+                                 ("log frames (zb_serialize_frames, request metadata on every CREATE)" if frames else
+                                  "values + 24-byte headers (zb_serialize)")}
 
     b = copy.copy(a)
     b.wave_only = True

@@ -78,7 +78,7 @@ typedef struct zb_config {
   int32_t partition_count;
   int32_t flags;            /* ZB_CFG_* bits */
   uint64_t log_capacity;    /* max records in the device log (32 B descriptor + 8 B row links each) */
-  uint64_t row_capacity;    /* max element-instance rows (SoA state, 64 B each) */
+  uint64_t row_capacity;    /* max element-instance rows (SoA planes: RowMeta 16 + RowKeys 32 + RowLink 8 + RowAux 48 B) */
   uint64_t arena_bytes;     /* payload arena (msgpack documents, 8-byte aligned blobs) */
   uint64_t wave_records;    /* max records processed per wave (chunk of a generation); 0 = min(log_capacity, 2^22) */
 } zb_config;

@@ -15,6 +15,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -150,6 +152,7 @@ struct zb_engine {
   uint8_t* xslab = nullptr;        // exact payload tree workspaces (zb_xmerge.hpp), with a model that merges / maps
   uint32_t* xlocks = nullptr;
   uint8_t* xlane = nullptr;        // per-thread exact-tree workspaces (XLANE_COUNT x XLANE_BYTES), with xslab
+  bool xpool_held = false;         // xslab / xlocks / xlane are the device's shared set (xpool_acquire)
   uint64_t* sub_jobs = nullptr;    // [job_cap] subscribe steps of a wave (models with message catch events)
   uint64_t job_cap = 0;
   WaveHdr* h_hdr_pinned = nullptr;  // pinned mirror for D2H polling
@@ -158,6 +161,7 @@ struct zb_engine {
   int64_t wave = 0;
   WaveHdr host_hdr{};
   bool has_merges = false, has_splits = false;
+  bool has_tasks = false;  // some deployed element is a service task (writes JOB CREATE commands)
   bool failed = false;
 
   // static arena region (ref 0 = {}, harness payloads)
@@ -191,10 +195,16 @@ struct zb_engine {
   uint32_t staged_max_len = 1;     // longest staged CREATE payload (uniform batch merge bounds)
 
   // request metadata: of staged records (staged index), then of injected ones (log position, sorted)
-  struct StagedReq { int64_t idx; uint64_t rid; int32_t sid; };
+  using StagedReq = zbg::StagedReq;
   std::vector<StagedReq> staged_reqs;
-  std::vector<ReqMeta> reqs;
-  DevVec<ReqMeta> d_reqs;
+  DevVec<StagedReq> d_staged_reqs;  // (uploaded with the staged batch)
+  bool staged_reqs_uploaded = false;
+  // request metadata of the injected commands, device-resident and sorted by position (k_req_append at each injection,
+  // no host copy): entries [req_lo, req_n) are live; one run per injection (its positions and entries)
+  ReqMeta* d_req = nullptr;
+  uint64_t req_cap = 0, req_lo = 0, req_n = 0;
+  struct ReqRun { int64_t first, last; uint64_t lo, n; };
+  std::vector<ReqRun> req_runs;
 
   // submitted command ranges (serialization of CREATE commands / rejections)
   std::vector<CmdRange> ranges;
@@ -423,6 +433,64 @@ hipError_t upload_vec(zb_engine* e, DevVec<T>& d, const std::vector<T>& v) {
     d.n = cap;
   }
   return upload_async(e, d.p, v.data(), v.size() * sizeof(T));
+}
+
+// The exact-tree workspaces (zb_xmerge.hpp) of one device, shared by every engine on it: slabs and lane groups are held
+// under device-wide locks (zb_xlock.hpp), so the partitions of one GPU need one set, not 2 GiB each. Taken by the first
+// engine whose model merges or maps, freed with the last. Lanes that cannot be allocated leave the engines on the big-slab
+// path (XTree with lanes == nullptr) instead of failing the deploy.
+struct XPool {
+  uint8_t* slab = nullptr;
+  uint32_t* locks = nullptr;
+  uint8_t* lane = nullptr;
+  int refs = 0;
+};
+std::mutex g_xpool_mu;
+std::map<int, XPool> g_xpool;
+
+int fail(zb_engine* e, int code, const std::string& msg);
+
+int xpool_acquire(zb_engine* e) {
+  if (e->xpool_held) return ZB_OK;
+  std::lock_guard<std::mutex> g(g_xpool_mu);
+  XPool& x = g_xpool[e->cfg.device];
+  if (!x.refs) {
+    if (hipMalloc(&x.slab, (size_t)XSLAB_COUNT * XSLAB_BYTES) != hipSuccess ||
+        hipMalloc(&x.locks, XLOCK_COUNT * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(x.locks, 0, XLOCK_COUNT * sizeof(uint32_t)) != hipSuccess) {
+      if (x.slab) (void)hipFree(x.slab);
+      if (x.locks) (void)hipFree(x.locks);
+      x = XPool{};
+      return fail(e, ZB_ENOMEM, "exact payload tree slabs");
+    }
+    if (hipMalloc(&x.lane, (size_t)XLANE_COUNT * XLANE_BYTES) != hipSuccess) {
+      (void)hipGetLastError();
+      x.lane = nullptr;  // (the slab path)
+    }
+  }
+  x.refs++;
+  e->xslab = x.slab;
+  e->xlocks = x.locks;
+  e->xlane = x.lane;
+  e->xpool_held = true;
+  return ZB_OK;
+}
+
+void xpool_release(zb_engine* e) {
+  if (!e->xpool_held) return;
+  std::lock_guard<std::mutex> g(g_xpool_mu);
+  XPool& x = g_xpool[e->cfg.device];
+  if (--x.refs == 0) {
+    (void)hipDeviceSynchronize();  // (another engine's stream may still run a merge on it: none left now)
+    if (x.slab) (void)hipFree(x.slab);
+    if (x.locks) (void)hipFree(x.locks);
+    if (x.lane) (void)hipFree(x.lane);
+    x = XPool{};
+  }
+  e->xslab = nullptr;
+  e->xlocks = nullptr;
+  e->xlane = nullptr;
+  e->xpool_held = false;
 }
 
 int fail(zb_engine* e, int code, const std::string& msg) {
@@ -972,6 +1040,45 @@ void rebias(zb_engine* e) {
 // Records the caller released move out of the window: [released, end) go to the front of the arrays (the
 // partition is quiescent: nothing below end is unprocessed). Chunks of at most (released - win_base) records,
 // front to back, never overlap a source not yet copied.
+// request metadata of released records: the runs wholly below the window go (a run the window cuts stays whole: its
+// entries below the window are never looked up); an empty table starts again at entry 0
+void drop_requests(zb_engine* e) {
+  size_t k = 0;
+  while (k < e->req_runs.size() && e->req_runs[k].last < e->win_base) k++;
+  e->req_runs.erase(e->req_runs.begin(), e->req_runs.begin() + k);
+  if (e->req_runs.empty()) e->req_lo = e->req_n = 0;
+  else e->req_lo = e->req_runs.front().lo;
+}
+
+// the staged batch's request metadata appended to the device table (positions log_base + staged index)
+int append_requests(zb_engine* e, int64_t log_base) {
+  const uint64_t m = e->staged_reqs.size();
+  if (!m) return ZB_OK;
+  if (!e->staged_reqs_uploaded) {
+    HIPCHECK(e, e->d_staged_reqs.upload(e->staged_reqs, e->stream));
+    e->staged_reqs_uploaded = true;
+  }
+  if (e->req_n + m > e->req_cap) {  // grow, keeping only the live entries
+    const uint64_t live = e->req_n - e->req_lo;
+    const uint64_t cap = std::max<uint64_t>(2 * (live + m), 1024);
+    ReqMeta* p = nullptr;
+    HIPCHECK(e, hipMalloc(&p, cap * sizeof(ReqMeta)));
+    if (live) HIPCHECK(e, hipMemcpyAsync(p, e->d_req + e->req_lo, live * sizeof(ReqMeta), hipMemcpyDeviceToDevice, e->stream));
+    HIPCHECK(e, hipStreamSynchronize(e->stream));
+    if (e->d_req) (void)hipFree(e->d_req);
+    e->d_req = p;
+    e->req_cap = cap;
+    for (auto& r : e->req_runs) r.lo -= e->req_lo;
+    e->req_n = live;
+    e->req_lo = 0;
+  }
+  launch_req_append(e->d_staged_reqs.p, m, log_base, e->d_req + e->req_n, e->stream);
+  e->req_runs.push_back(zb_engine::ReqRun{log_base + e->staged_reqs.front().idx, log_base + e->staged_reqs.back().idx,
+                                          e->req_n, m});
+  e->req_n += m;
+  return ZB_OK;
+}
+
 int rebase_log(zb_engine* e) {
   const int64_t from = std::min(e->released, e->host_hdr.end);
   if (from <= e->win_base) return ZB_OK;
@@ -988,8 +1095,7 @@ int rebase_log(zb_engine* e) {
   // submitted-command ranges and request metadata of released records are no longer needed by the drain
   e->ranges.erase(std::remove_if(e->ranges.begin(), e->ranges.end(),
                                  [&](const CmdRange& r) { return r.pos_end <= e->win_base; }), e->ranges.end());
-  e->reqs.erase(std::remove_if(e->reqs.begin(), e->reqs.end(), [&](const ReqMeta& r) { return r.pos < e->win_base; }),
-                e->reqs.end());
+  drop_requests(e);
   // the process-id strings they name: only those of the remaining (and the staged) ranges are kept
   std::vector<uint8_t> pool;
   auto keep_str = [&](uint32_t& off, uint16_t len) {
@@ -1456,9 +1562,10 @@ void zb_engine_destroy(zb_engine* e) {
                 e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
                 e->c_plan, e->c_ikey, e->c_clen, e->d_cref, e->c_khist, e->c_mask, e->c_cg, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
                 e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->look_keys, e->look_idx,
-                e->conf_first, e->xslab, e->xlocks, e->xlane, e->phase};
+                e->conf_first, e->phase};
   for (void* p : ps)
     if (p) (void)hipFree(p);
+  xpool_release(e);
   if (e->comm) (void)ncclCommDestroy(e->comm);
   void* ms[] = {e->obox[0], e->obox[1], e->okeys[0], e->okeys[1], e->ovar[0], e->ovar[1], e->on, e->subs, e->sub_head,
                 e->sub_next, e->msgs, e->msg_head, e->msg_next, e->d_xcounts, e->xsend, e->xrecv, e->ob_keys, e->ob_idx_in,
@@ -1480,7 +1587,8 @@ void zb_engine_destroy(zb_engine* e) {
   e->d_vsegs.free();
   e->d_segpool.free();
   e->d_staged_vlen.free();
-  e->d_reqs.free();
+  e->d_staged_reqs.free();
+  if (e->d_req) (void)hipFree(e->d_req);
   e->d_slices.free();
   void* dr[] = {e->dr_len, e->dr_off, e->dr_hdr, e->dr_val, e->dr_tmp, e->dr_total, e->dr_tiles, e->dr_pay, e->dr_tsum,
                 e->dr_list, e->dr_list2};
@@ -1551,9 +1659,11 @@ int zb_reset(zb_engine* e, int keep_staged) {
   HIPCHECK(e, hipStreamSynchronize(e->stream));
   e->ranges.clear();
   e->cmd_pool.clear();
-  e->reqs.clear();
+  e->req_runs.clear();
+  e->req_lo = e->req_n = 0;
   if (!keep_staged) {
     e->staged_reqs.clear();
+    e->staged_reqs_uploaded = false;
     e->staged.clear();
     e->staged_vlen.clear();
     e->staged_arena.clear();
@@ -1609,16 +1719,15 @@ int zb_deploy(zb_engine* e, int64_t workflow_key, int32_t version, const uint8_t
     if (el.kind == EK_CATCH) e->has_catch = true;
     if (el.kind == EK_PAR) e->has_parallel = true;
     if (el.flags & EF_IO) e->has_io = true;
+    if (el.kind == EK_TASK || el.step[WI_ELEMENT_ACTIVATED] == ST_CREATE_JOB) e->has_tasks = true;
   }
   if (e->has_io && !e->mapres) {
     HIPCHECK(e, hipMalloc(&e->mapres, (e->wave_cap + 8) * sizeof(uint64_t)));
     HIPCHECK(e, hipMalloc(&e->map_ws, (size_t)MAP_GRID * 256 * MAP_NODES * sizeof(MNode)));
   }
-  if ((e->has_io || e->has_merges) && !e->xslab) {  // payloads the structural merge / mapper refuse
-    HIPCHECK(e, hipMalloc(&e->xslab, (size_t)XSLAB_COUNT * XSLAB_BYTES));
-    HIPCHECK(e, hipMalloc(&e->xlocks, XLOCK_COUNT * sizeof(uint32_t)));
-    HIPCHECK(e, hipMemset(e->xlocks, 0, XLOCK_COUNT * sizeof(uint32_t)));
-    HIPCHECK(e, hipMalloc(&e->xlane, (size_t)XLANE_COUNT * XLANE_BYTES));
+  if (e->has_io || e->has_merges) {  // payloads the structural merge / mapper refuse: the device's shared workspaces
+    const int xrc = xpool_acquire(e);
+    if (xrc != ZB_OK) return xrc;
   }
   if (e->has_catch) {
     int orc = ensure_outbox(e);
@@ -1828,6 +1937,7 @@ void begin_staging(zb_engine* e) {
   if (e->staged_pending) return;
   e->staged_in_place = false;  // (the injected batch's documents belong to the arena's top region now)
   e->staged_reqs.clear();
+  e->staged_reqs_uploaded = false;
   e->staged.clear();
   e->staged_vlen.clear();
   e->staged_arena.clear();
@@ -1847,6 +1957,10 @@ void begin_staging(zb_engine* e) {
 int upload_staged(zb_engine* e) {
   if (e->staged_uploaded) return ZB_OK;
   HIPCHECK(e, e->d_staged.upload(e->staged, e->stream));
+  if (!e->staged_reqs.empty() && !e->staged_reqs_uploaded) {
+    HIPCHECK(e, e->d_staged_reqs.upload(e->staged_reqs, e->stream));
+    e->staged_reqs_uploaded = true;
+  }
   HIPCHECK(e, e->d_staged_vlen.upload(e->staged_vlen, e->stream));
   // the documents: in place at the top of the arena when they fit above the allocators' bytes (an earlier upload
   // of this same batch gives its room back first), else into a staging buffer that k_inject copies from
@@ -2420,9 +2534,14 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     if (!e->staged_only_creates && e->host_hdr.begin != e->host_hdr.end)
       return fail(e, ZB_EINVAL, "records other than CREATE are injected into a quiescent partition only: "
                                 "step it to quiescence first");
-    // an idle partition fed only CREATE commands runs as independent trajectories (zb_traj.hip) -- with the
-    // canonical job harness and no parallel gateways (the general wave pipeline covers everything else)
-    try_traj = !(e->cfg.flags & (ZB_CFG_WAVE_ONLY | ZB_CFG_EXTERNAL_JOBS | ZB_CFG_JOB_PROCESSOR)) && max_waves == 0 &&
+    // an idle partition fed only CREATE commands runs as independent trajectories (zb_traj.hip) -- no parallel
+    // gateways, and either the canonical job harness or no service task in any deployed model: the workflow
+    // processor writes the same records for a CREATE whichever job processor shares the log
+    // (WorkflowInstanceStreamProcessor.java:233-368; JobInstanceStreamProcessor is a separate registration,
+    // JobInstanceStreamProcessor.java:77-83), so a model without service tasks never meets the job mode
+    // (the general wave pipeline covers everything else)
+    const bool job_mode_ok = !(e->cfg.flags & (ZB_CFG_EXTERNAL_JOBS | ZB_CFG_JOB_PROCESSOR)) || !e->has_tasks;
+    try_traj = !(e->cfg.flags & ZB_CFG_WAVE_ONLY) && job_mode_ok && max_waves == 0 &&
                e->staged_only_creates && !e->has_parallel && !e->has_io &&
                (e->traj_model_ok || (e->cls_ok && e->staged_uniform)) &&
                e->host_hdr.begin == e->host_hdr.end;
@@ -2489,7 +2608,10 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     }
     if (e->staged_has_cancel) e->term = true;
     if (e->staged_conf) e->conf_active = true;  // (until the tick is quiescent)
-    for (const auto& q : e->staged_reqs) e->reqs.push_back(ReqMeta{ip.log_base + q.idx, q.rid, q.sid, 0});
+    {
+      const int qrc = append_requests(e, ip.log_base);
+      if (qrc != ZB_OK) return qrc;
+    }
     for (auto& pr : e->pending_ranges) {
       CmdRange r{};
       r.pos_begin = ip.log_base + pr.first;
@@ -2704,7 +2826,8 @@ int zb_set_request_metadata(zb_engine* e, size_t n, const uint64_t* request_ids,
     const int64_t idx = first + (int64_t)i;
     if (!e->staged_reqs.empty() && e->staged_reqs.back().idx >= idx)
       return fail(e, ZB_EINVAL, "request metadata already set for these records");
-    e->staged_reqs.push_back(zb_engine::StagedReq{idx, request_ids[i], request_stream_ids[i]});
+    e->staged_reqs.push_back(zb_engine::StagedReq{idx, request_ids[i], request_stream_ids[i], 0});
+    e->staged_reqs_uploaded = false;
   }
   return ZB_OK;
 }
@@ -2712,7 +2835,8 @@ int zb_set_request_metadata(zb_engine* e, size_t n, const uint64_t* request_ids,
 // zb_serialize of exactly a deferred template batch: k_tdrain_size -> scan -> k_tdrain_write (zb_tdrain.hip).
 // ZB_EAGAIN: the batch needs the descriptor path (an instance's records exceed the wave image, or a value length
 // disagreed with the encoder -- never silently).
-static int serialize_deferred(zb_engine* e, int64_t start, int64_t count, zb_serialize_stats& st) {
+static int serialize_deferred(zb_engine* e, int64_t start, int64_t count, const zb_frame_config* fc,
+                              zb_serialize_stats& st) {
   const TrajParams& p = e->seg_p;
   const uint64_t nwave = (uint64_t)p.nwg * (TRAJ_WG / 64);
   const uint64_t ent = (uint64_t)e->seg_wmax * nwave + 1;
@@ -2760,6 +2884,22 @@ static int serialize_deferred(zb_engine* e, int64_t start, int64_t count, zb_ser
 #ifdef ZB_PHASES
   d.phase = e->phase ? e->phase + 8 : nullptr;
 #endif
+  if (fc) {  // log frames: no headers; the request metadata of the batch's CREATE commands [log_base, log_base + n)
+    d.frames = 1;
+    d.stream_id = fc->stream_id;
+    d.raft_term = fc->raft_term;
+    d.timestamp = fc->timestamp;
+    for (const auto& r : e->req_runs)  // the batch's own run covers every CREATE: entry i is instance i's
+      if (r.first == p.log_base && r.last == p.log_base + p.n - 1 && (int64_t)r.n == p.n) {
+        d.reqs = e->d_req + r.lo;
+        d.nreqs = p.n;
+        d.req_dense = 1;
+      }
+    if (!d.req_dense && e->req_n > e->req_lo) {  // otherwise a search of the whole table
+      d.reqs = e->d_req + e->req_lo;
+      d.nreqs = (int64_t)(e->req_n - e->req_lo);
+    }
+  }
   float ms_size = 0, ms_scan = 0, ms_write = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     d.out = e->dr_val;
@@ -2772,7 +2912,7 @@ static int serialize_deferred(zb_engine* e, int64_t start, int64_t count, zb_ser
     // per-wave class counts and CREATE payload sums (k_tdrain_sizes); the first ones (keys / positions below 2^16)
     // resolve every record (k_tdrain_size)
     uint32_t wg0 = (uint32_t)p.nwg;
-    if (p.cls && !d.jobs && d.len5_ok) {
+    if (p.cls && !d.jobs && d.len5_ok && !d.frames) {  // (frame padding is not linear in the payload lengths)
       const int64_t thr = std::max<int64_t>(65536 - p.log_base, (65536 - p.wf_start + 4) / 5);
       wg0 = (uint32_t)std::min<int64_t>(p.nwg, (std::max<int64_t>(thr, 0) + TRAJ_WG - 1) / TRAJ_WG);
     }
@@ -2866,12 +3006,12 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
     e->dr_val_cap = cap;
   }
   if (e->seg_pending) {  // a deferred template batch: encoded from its traces, or materialized first
-    if (!fc && start == e->seg_begin && count == e->seg_end - e->seg_begin) {
-      const int rc = serialize_deferred(e, start, count, st);
+    if (start == e->seg_begin && count == e->seg_end - e->seg_begin) {
+      const int rc = serialize_deferred(e, start, count, fc, st);
       if (rc == ZB_OK) {
         e->dr_count = count;
         e->dr_bytes = st.value_bytes;
-        e->dr_frames = false;
+        e->dr_frames = fc != nullptr;
         st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         if (stats) *stats = st;
         return ZB_OK;
@@ -2884,7 +3024,6 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
   }
   HIPCHECK(e, upload_vec(e, e->d_ranges, e->ranges));
   HIPCHECK(e, upload_vec(e, e->d_cmd_pool, e->cmd_pool));
-  if (fc && !e->reqs.empty()) HIPCHECK(e, upload_vec(e, e->d_reqs, e->reqs));
   SerParams sp{};
   sp.nt = 1;
   if (fc) {
@@ -2894,8 +3033,8 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
     sp.timestamp = fc->timestamp;
     sp.log_begin = e->win_base;
     sp.log_end = e->host_hdr.end;
-    sp.reqs = e->reqs.empty() ? nullptr : e->d_reqs.p;
-    sp.nreqs = (int64_t)e->reqs.size();
+    sp.reqs = e->req_n > e->req_lo ? e->d_req + e->req_lo : nullptr;
+    sp.nreqs = (int64_t)(e->req_n - e->req_lo);
   }
   sp.log = e->log;
   sp.srcd = e->srcd;
@@ -2969,11 +3108,12 @@ static int serialize(zb_engine* e, int64_t start, int64_t count, const zb_frame_
       wr.lengths = e->dr_len;
       wr.len_in_vlen = sz.len_in_vlen;
       wr.tile_offs = e->dr_off;
-      e->dr_split = e->ser_fast && !fc && sp.seg_lds && sp.arena_bytes;
+      e->dr_split = e->ser_fast && sp.seg_lds && sp.arena_bytes;
       if (e->dr_split) {  // k_ser_fast, then k_ser_write over the tiles it left
         // pass 1 over every tile (k_ser_wave, 11 KB per wave) -> list A (a value over its image) and list B (a
         // record kind the fast encoder does not take); pass 2 over A (40 KB phase form) -> more of list B;
-        // k_ser_write over B
+        // k_ser_write over B. Frames: k_ser_wave<true> (prefix + value + padding per lane), every tile it leaves
+        // (a rejection reason, a kind it does not take, a frame over its image) in list B for k_ser_write<true>
         uint32_t* cnt = (uint32_t*)(e->dr_total + 3);  // [0] list A, [1] list B (zeroed with dr_total)
         wr.tile_list = e->dr_list;
         wr.tile_list_slow = e->dr_list2;
@@ -3708,6 +3848,11 @@ int zb_outbox_count(zb_engine* e, int kind, uint64_t* n) {
   *n = c[kind - 1];
   e->ob_counts_read[0] = c[0];
   e->ob_counts_read[1] = c[1];
+  // an empty outbox takes the processing frontier as its order-key base now, not only at its next take: every command
+  // it receives from here on comes from a record at or after it (a kind that stays empty for long would otherwise keep
+  // an old base, and a later command -- or the span check of a message batch -- would meet the 2^34 relative-key limit)
+  for (int k = 0; k < 2; k++)
+    if (c[k] == 0) e->ob_pos_base[k] = std::max(e->ob_pos_base[k], e->host_hdr.begin);
   return ZB_OK;
 }
 
@@ -4016,12 +4161,20 @@ int zb_log_start(zb_engine* e, int64_t position) {
   if (e->staged_pending && !e->staged.empty()) return fail(e, ZB_EINVAL, "staged input not injected yet");
   if (position < e->host_hdr.end) return fail(e, ZB_EINVAL, "log positions only grow");
   if (std::max(e->released, e->win_base) < e->host_hdr.end) return fail(e, ZB_EINVAL, "unreleased records in the window");
+  if (e->on) {  // queued exchange commands carry order keys relative to the old base: take them first
+    uint64_t n_open = 0, n_corr = 0;
+    int rc = zb_outbox_count(e, ZB_XCHG_OPEN, &n_open);
+    if (rc == ZB_OK) rc = zb_outbox_count(e, ZB_XCHG_CORRELATE, &n_corr);
+    if (rc != ZB_OK) return rc;
+    if (n_open || n_corr) return fail(e, ZB_EINVAL, "untaken exchange commands in the outbox: exchange them first");
+  }
   HIPCHECK(e, hipStreamSynchronize(e->stream));
   e->host_hdr.begin = e->host_hdr.end = e->host_hdr.gen_end = position;
   e->win_base = e->released = position;
   e->ob_pos_base[0] = e->ob_pos_base[1] = position;
   e->ranges.clear();
-  e->reqs.clear();
+  e->req_runs.clear();
+  e->req_lo = e->req_n = 0;
   e->cmd_pool.clear();
   rebias(e);
   HIPCHECK(e, upload_async(e, e->hdr + (e->wave & 1), &e->host_hdr, sizeof(WaveHdr)));

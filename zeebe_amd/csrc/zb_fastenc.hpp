@@ -86,6 +86,15 @@ struct FastWT {
     if (head & 7) part(head & ~7u, first, head & 7, 8);
     if (pos & 7) part(pos & ~7u, acc, 0, pos & 7);
   }
+  // instead of end() for a log frame's value (zb_frame.hpp): the value starts 8-aligned after the frame prefix, so its
+  // first slot is its own; the last slot is stored whole, its bytes past the value zero (the frame's padding to 8)
+  __device__ __forceinline__ void end_frame() {
+    if (BF) {
+      *(uint64_t*)(img + ((pos & 7) ? (pos & ~7u) : dummy)) = acc;
+      return;
+    }
+    if (pos & 7) *(uint64_t*)(img + (pos & ~7u)) = acc;
+  }
   // N - 1 literal bytes (may hold NULs), as immediates; FIRST: the value starts with them (N - 1 >= 8)
   template <bool FIRST = false, int N>
   __device__ __forceinline__ void lit(const char (&s)[N]) {
@@ -310,8 +319,8 @@ __device__ __forceinline__ bool fast_kind(const zb_rec& d) {
 
 // encode_value's WORKFLOW_INSTANCE (non-submitted) and JOB branches from the constant runs of the record's
 // element (tab / pool in LDS) and its variable fields: keys, payload
-// L5: every key in ival5's range
-template <bool L5 = false, bool BF = false>
+// L5: every key in ival5's range; FR: the value of a log frame (end_frame)
+template <bool L5 = false, bool BF = false, bool FR = false>
 __device__ __forceinline__ void fast_encode(FastWT<false, BF>& w, const zb_rec& d, const DevValSeg* tab, const uint8_t* segs,
                                             const uint64_t* dw, const uint64_t (&pre)[SER_PRE]) {
   const DevValSeg& t = tab[d.elem];
@@ -330,12 +339,14 @@ __device__ __forceinline__ void fast_encode(FastWT<false, BF>& w, const zb_rec& 
     w.seg(segs + 8 * t.off8[SEG_JOB_C], t.len[SEG_JOB_C]);
     fast_bin(w, dw, pre);
   }
-  w.end();
+  if (FR) w.end_frame();
+  else w.end();
 }
 
 // The message-side values, from the record's blob (dw: its first word; zb_msg.hpp MsgView / SubView layouts) and,
 // for a WORKFLOW_INSTANCE_SUBSCRIPTION, its element's message name run and the payload document. Checked stores: a
 // MESSAGE value's first slot is completed inside its name.
+template <bool FR = false>
 __device__ __forceinline__ void fast_encode_msg(FastWT<true>& w, const zb_rec& d, const DevValSeg* tab,
                                                 const uint8_t* segs, const uint64_t* dw,
                                                 const uint64_t (&pre)[SER_PRE]) {
@@ -382,7 +393,8 @@ __device__ __forceinline__ void fast_encode_msg(FastWT<true>& w, const zb_rec& d
     w.str_hdr(nid);
     w.gbytes(name + nn + nc + np, nid);
   }
-  w.end();
+  if (FR) w.end_frame();
+  else w.end();
 }
 
 // ---- host: the constant runs of every element's values (deploy time)

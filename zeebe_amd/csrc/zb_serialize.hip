@@ -11,6 +11,7 @@
 
 #include "zb_devlib.hpp"
 #include "zb_fastenc.hpp"
+#include "zb_frame.hpp"
 #include "zb_wavelib.hpp"
 #include "zb_kernels.hpp"
 #include "zb_msg.hpp"
@@ -302,14 +303,7 @@ __device__ __forceinline__ uint8_t rejection_type(const zb_rec& d) {
 }
 
 // ------------------------------------------------------------------------------ log frames (§8f rank 1)
-// A record as LogStreamBatchWriterImpl.writeEventsToBuffer (:222-268) / LogStreamWriterImpl lay it into the
-// dispatcher buffer: DataFrameDescriptor header (DataFrameDescriptor.java:53-96: framed length, version 0,
-// batch flags, TYPE_MESSAGE, stream id), LogEntryDescriptor header (LogEntryDescriptor.java:28-121: version,
-// position, raft term, producer id, source event position, key, timestamp, metadata length), RecordMetadata
-// (RecordMetadata.java:96-128: SBE header {34, 200, 0, 1} + block + varData rejectionReason), the value, and
-// zero padding to FRAME_ALIGNMENT 8. The 104-byte prefix goes out as 13 aligned 8-byte words (frames start
-// 8-aligned in the image and in HBM).
-constexpr uint32_t FRAME_PREFIX = 12 + 48 + 8 + 34 + 2;
+// The frame layout and its 104-byte prefix: zb_frame.hpp (shared with the fast frame drains).
 
 // rejection reasons of the commands this path rejects (WorkflowInstanceStreamProcessor.java:346-347, :527-529,
 // :573, :478-479), of the job commands (JobInstanceStreamProcessor.java:155-158, :172-173, :186-187, :193,
@@ -343,17 +337,6 @@ __device__ __forceinline__ uint32_t reason_len(const SerParams& P, const zb_rec&
   return dstrlen(REASONS[r < 11 ? r : 0]);
 }
 
-__device__ __forceinline__ const ReqMeta* find_req(const SerParams& P, int64_t pos) {
-  int64_t lo = 0, hi = P.nreqs - 1;
-  while (lo <= hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    const int64_t p = P.reqs[mid].pos;
-    if (p == pos) return &P.reqs[mid];
-    if (p < pos) lo = mid + 1; else hi = mid - 1;
-  }
-  return nullptr;
-}
-
 __device__ __forceinline__ int64_t source_of(const SerParams& P, int64_t pos) {
   const uint32_t s = P.srcd[pos];
   return s ? pos - (int64_t)s : -1;
@@ -371,51 +354,21 @@ __device__ inline uint32_t encode_frame(const SerParams& P, int64_t pos, const z
   if (!dst) return fsize;
   const uint8_t vt = kind_vt(d.kind), rt = kind_rt(d.kind);
   const int64_t src = source_of(P, pos);
-  // ClaimedFragmentBatch.commit :130-147: BEGIN on the first and END on the last fragment of a batch with more
-  // than one; a batch is the records one processed record wrote (contiguous, same source)
   uint32_t flags = 0;
   if (src >= 0) {
     const bool first = pos - 1 < P.log_begin || source_of(P, pos - 1) != src;
     const bool last = pos + 1 >= P.log_end || source_of(P, pos + 1) != src;
-    if (!(first && last)) flags = first ? 0x80 : (last ? 0x40 : 0);
+    flags = frame_flags(first, last);
   }
-  // TypedStreamProcessor producer ids (StreamProcessorIds.java:23-39): harness job events 10 (the job
-  // processor), message partition records 90, everything else the workflow instance processor 70; records
-  // other writers appended keep the writer's default -1
-  // (a MESSAGE DELETE command comes from the time-to-live checker's own command writer: producer id 0,
-  // TypedCommandWriterImpl never configured, MessageService.java:118-120)
-  const int32_t producer = src < 0 ? ((vt == ZB_VT_MESSAGE && rt == ZB_RT_COMMAND && d.intent == 2) ? 0 : -1)
-                         : (vt == ZB_VT_JOB && rt != ZB_RT_COMMAND) ? 10
-                         : (vt == ZB_VT_MESSAGE || vt == ZB_VT_MESSAGE_SUBSCRIPTION) ? 90 : 70;
-  uint64_t rid = ~0ull;
-  uint32_t sid = 0x80000000u;
-  if (P.nreqs) {
-    int64_t q = -1;
-    if (src < 0) q = pos;
-    else if (vt == ZB_VT_WORKFLOW_INSTANCE && ((rt == ZB_RT_EVENT && d.intent == WI_CREATED) ||
-                                               (rt == ZB_RT_COMMAND_REJECTION && d.intent == WI_CREATE)))
-      q = src;
-    if (q >= 0) {
-      const ReqMeta* m = find_req(P, q);
-      if (m) { rid = m->request_id; sid = (uint32_t)m->request_stream_id; }
-    }
-  }
-  const uint64_t rej = rejection_type(d);
-  const uint64_t mlen = 8 + 34 + 2 + rlen;
-  uint64_t* h = (uint64_t*)dst;
-  h[0] = (uint64_t)framed | (uint64_t)flags << 40;                          // length, version 0, flags, type 0
-  h[1] = (uint64_t)(uint32_t)P.stream_id;                                    // stream id, entry version, reserved
-  h[2] = (uint64_t)pos;
-  h[3] = (uint64_t)(uint32_t)P.raft_term | (uint64_t)(uint32_t)producer << 32;
-  h[4] = (uint64_t)src;
-  h[5] = (uint64_t)d.key;
-  h[6] = (uint64_t)P.timestamp;
-  h[7] = mlen | 34ull << 32 | 200ull << 48;                                   // metadata length | blockLength, templateId
-  h[8] = 1ull << 16 | (uint64_t)rt << 32 | (uint64_t)(sid & 0xffffffu) << 40; // schemaId 0, version 1 | recordType
-  h[9] = (uint64_t)(sid >> 24) | rid << 8;                                    // requestStreamId | requestId
-  h[10] = (rid >> 56) | 0xffffffffffffff00ull;                                // | subscriptionId (null)
-  h[11] = 0xffull | 1ull << 8 | (uint64_t)vt << 24 | (uint64_t)d.intent << 32 | 0xffffffull << 40;  // protocolVersion 1
-  h[12] = 0xffffffffffull | rej << 40 | (uint64_t)rlen << 48;                  // incidentKey (null) | rejectionType
+  uint64_t rid;
+  uint32_t sid;
+  frame_request(P.reqs, P.nreqs, frame_request_pos(pos, src, vt, rt, d.intent), rid, sid);
+  uint64_t h[13];
+  frame_words(h, FrameConst{P.stream_id, P.raft_term, P.timestamp}, framed, flags, pos, frame_producer(src, vt, rt, d.intent),
+              src, d.key, rt, vt, d.intent, rejection_type(d), rlen, rid, sid);
+  uint64_t* hd = (uint64_t*)dst;
+#pragma unroll
+  for (int j = 0; j < 13; j++) hd[j] = h[j];
   W r;
   r.dst = dst + FRAME_PREFIX;
   r.n = 0;
@@ -811,13 +764,12 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3))
 // larger than the image, goes to the next pass (tile_list: the 40 KB phase form, then k_ser_write; tile_list_slow:
 // k_ser_write directly, for the tiles holding a record of a kind the fast encoder does not take).
 constexpr uint32_t SER_WIMG = 11 * 1024 - 16;
+// FRAMES (zb_serialize_frames): each lane's frame -- the 13 prefix words (zb_frame.hpp) and the value, padded to 8 --
+// goes into the image at its 8-aligned offset; records with a rejection reason go to k_ser_write<true>
+template <bool FRAMES>
 __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 4))) k_ser_wave(SerParams P0) {
-#ifndef ZB_EXP_SER_NOBF  // (measurement variants only: tools/ab_variant.sh)
   // each wave's image, then its lanes' dummy slots (the branch-free writer's stores that must not land: FastWB)
   __shared__ __attribute__((aligned(16))) uint8_t s_img[SER_WG / 64][SER_WIMG + 16 + 8 * 64];
-#else
-  __shared__ __attribute__((aligned(16))) uint8_t s_img[SER_WG / 64][SER_WIMG + 16];
-#endif
   extern __shared__ __attribute__((aligned(16))) uint8_t s_model[];  // the constant runs (sized at launch)
   __shared__ unsigned long long s_wsum[SER_WG / 64], s_pay[SER_WG / 64];
   const uint32_t tile = blockIdx.x;
@@ -829,13 +781,26 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
   const uint32_t len = live ? (P0.len_in_vlen ? P0.vlen[P0.start + i] : P0.lengths[i]) : 0;
   zb_rec d{};
   if (live) d = P0.log[P0.start + i];
-  const bool msg = live && fast_msg_kind(d);
-  const bool fast = (live && fast_kind(d)) || msg;
+  const bool rej = FRAMES && kind_rt(d.kind) == ZB_RT_COMMAND_REJECTION;  // (frames: a rejection reason)
+  const bool msg = live && !rej && fast_msg_kind(d);
+  const bool fast = (live && !rej && fast_kind(d)) || msg;
   const uint64_t* dw = (const uint64_t*)(P0.arena + (uint64_t)d.payload * 8);
   uint64_t pre[SER_PRE];
 #pragma unroll
   for (int j = 0; j < SER_PRE; j++)
     pre[j] = (fast && (uint64_t)d.payload * 8 + 8 * j + 8 <= P0.arena_bytes) ? dw[j] : 0;
+  // frames: the record's source and its neighbours' (batch flags)
+  int64_t src = -1;
+  uint32_t fflags = 0;
+  if (FRAMES && live) {
+    const int64_t pos = P0.start + i;
+    src = source_of(P0, pos);
+    if (src >= 0) {
+      const bool first = pos - 1 < P0.log_begin || source_of(P0, pos - 1) != src;
+      const bool last = pos + 1 >= P0.log_end || source_of(P0, pos + 1) != src;
+      fflags = frame_flags(first, last);
+    }
+  }
   uint64_t x = len;  // the wave's inclusive prefix of the value lengths
 #pragma unroll
   for (int k = 1; k < 64; k <<= 1) {
@@ -856,8 +821,8 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
   if (!all_fast) {  // the next pass takes this tile: the 40 KB phase form if only a value's size is the reason
     const bool kinds = __syncthreads_and(!live || fast);
     if (threadIdx.x == 0) {
-      if (kinds) P0.tile_list[atomicAdd(P0.tile_list_n, 1u)] = tile;
-      else P0.tile_list_slow[atomicAdd(P0.tile_list_n + 1, 1u)] = tile;
+      if (kinds && !FRAMES) P0.tile_list[atomicAdd(P0.tile_list_n, 1u)] = tile;
+      else P0.tile_list_slow[atomicAdd(P0.tile_list_n + 1, 1u)] = tile;  // (frames: k_ser_write<true>)
     }
     return;
   }
@@ -867,11 +832,17 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
     if (k < wv) pw += s_wsum[k];
   const uint64_t wlo = o0 + pw;  // this wave's range
   const uint32_t rel = (uint32_t)(x - len), incl = (uint32_t)x;  // this lane's value: [wlo + rel, wlo + incl)
-  if (live) {
+  if (live && !FRAMES) {
     const zb_record_header h = record_header(d, P0.start + i, len, wlo + rel);
     const uint64_t* hw = (const uint64_t*)&h;
     uint64_t* dh = (uint64_t*)(P0.headers + i);
     for (int k = 0; k < (int)(sizeof(zb_record_header) / 8); k++) dh[k] = hw[k];  // (plain: L2 merges lines)
+  }
+  uint64_t rid = ~0ull;
+  uint32_t sid = 0x80000000u;
+  if (FRAMES && live && P0.nreqs) {
+    const int64_t pos = P0.start + i;
+    frame_request(P0.reqs, P0.nreqs, frame_request_pos(pos, src, kind_vt(d.kind), kind_rt(d.kind), d.intent), rid, sid);
   }
   if (P0.totals) {
     unsigned long long y = live ? (uint32_t)pre[0] : 0;
@@ -884,6 +855,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
   // every key the wave's WORKFLOW_INSTANCE / JOB values carry is -1, 0 or in [2^16, 2^32): 5-byte integers (ival5)
   auto in5 = [](int64_t v) { return (uint64_t)(v + 1) <= 1 || (v >= 65536 && v < (1ll << 32)); };
   const bool l5 = __all(!live || msg || (in5(d.inst_key) && in5(d.scope_key)));
+  constexpr uint32_t VO = FRAMES ? FRAME_PREFIX : 0u;  // the value's offset in the record's bytes
 #pragma unroll 1
   for (int a = 0; a < 64;) {  // rounds: lanes [a, b) whose values fit the image from the round's first byte
     const uint32_t lo = __builtin_amdgcn_readlane(rel, a);
@@ -892,20 +864,28 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
     const uint64_t fm = __ballot(fit);
     const int b = 64 - __builtin_clzll(fm);
     if (fit && len) {
+      const uint32_t at = sh + (rel - lo);
+      uint32_t vn;
       if (msg) {
         FastWT<true> w;
-        w.begin(img, sh + (rel - lo));
-        fast_encode_msg(w, d, tab, segs, dw, pre);
+        w.begin(img, at + VO);
+        fast_encode_msg<FRAMES>(w, d, tab, segs, dw, pre);
+        vn = w.n();
       } else {
-#ifndef ZB_EXP_SER_NOBF
         FastWB w;
-        w.begin(img, sh + (rel - lo), SER_WIMG + 16 + 8 * lane);
-#else
-        FastW w;
-        w.begin(img, sh + (rel - lo));
-#endif
-        if (l5) fast_encode<true>(w, d, tab, segs, dw, pre);
-        else fast_encode<false>(w, d, tab, segs, dw, pre);
+        w.begin(img, at + VO, SER_WIMG + 16 + 8 * lane);
+        if (l5) fast_encode<true, true, FRAMES>(w, d, tab, segs, dw, pre);
+        else fast_encode<false, true, FRAMES>(w, d, tab, segs, dw, pre);
+        vn = w.n();
+      }
+      if (FRAMES) {  // the prefix, once the value's length is known
+        const uint8_t vt = kind_vt(d.kind), rt = kind_rt(d.kind);
+        uint64_t h[13];
+        frame_words(h, FrameConst{P0.stream_id, P0.raft_term, P0.timestamp}, FRAME_PREFIX + vn, fflags,
+                    P0.start + i, frame_producer(src, vt, rt, d.intent), src, d.key, rt, vt, d.intent, 255, 0, rid, sid);
+        uint64_t* hd = (uint64_t*)(img + at);
+#pragma unroll
+        for (int j = 0; j < 13; j++) hd[j] = h[j];
       }
     }
     const uint32_t hi = __builtin_amdgcn_readlane(incl, b - 1);
@@ -924,7 +904,9 @@ static uint32_t seg_lds_bytes(const SerParams& p) {
 }
 void launch_ser_fast(const SerParams& p, hipStream_t s) {
   if (p.count <= 0) return;
-  hipLaunchKernelGGL(k_ser_wave, dim3((unsigned)((p.count + SER_WG - 1) / SER_WG)), dim3(SER_WG), seg_lds_bytes(p), s, p);
+  const dim3 g((unsigned)((p.count + SER_WG - 1) / SER_WG));
+  if (p.frames) hipLaunchKernelGGL(k_ser_wave<true>, g, dim3(SER_WG), seg_lds_bytes(p), s, p);
+  else hipLaunchKernelGGL(k_ser_wave<false>, g, dim3(SER_WG), seg_lds_bytes(p), s, p);
 }
 void launch_ser_fast_wide(const SerParams& p, uint32_t n, hipStream_t s) {
   if (n == 0) return;
@@ -932,7 +914,8 @@ void launch_ser_fast_wide(const SerParams& p, uint32_t n, hipStream_t s) {
 }
 void launch_ser_write_list(const SerParams& p, uint32_t n, hipStream_t s) {
   if (n == 0) return;
-  if (p.nt) hipLaunchKernelGGL((k_ser_write<false, true>), dim3(n), dim3(SER_WG), 0, s, p);
+  if (p.frames) hipLaunchKernelGGL((k_ser_write<true, true>), dim3(n), dim3(SER_WG), 0, s, p);
+  else if (p.nt) hipLaunchKernelGGL((k_ser_write<false, true>), dim3(n), dim3(SER_WG), 0, s, p);
   else hipLaunchKernelGGL((k_ser_write<false, false>), dim3(n), dim3(SER_WG), 0, s, p);
 }
 void launch_ser_sum(const SerParams& p, hipStream_t s) {
@@ -1109,6 +1092,19 @@ __global__ void k_inject(InjectParams P) {
   const uint64_t* src = (const uint64_t*)P.staged_arena;
   uint64_t* dst = (uint64_t*)(P.arena + P.arena_base);
   for (uint64_t i = tid; i < nw; i += stride) dst[i] = src[i];
+}
+
+__global__ void k_req_append(const StagedReq* in, uint64_t n, int64_t log_base, ReqMeta* out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const StagedReq r = in[i];
+    out[i] = ReqMeta{log_base + r.idx, r.rid, r.sid, 0};
+  }
+}
+
+void launch_req_append(const StagedReq* in, uint64_t n, int64_t log_base, ReqMeta* out, hipStream_t s) {
+  if (n == 0) return;
+  const uint64_t g = std::min<uint64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_req_append, dim3((unsigned)g), dim3(256), 0, s, in, n, log_base, out);
 }
 
 void launch_inject(const InjectParams& p, hipStream_t s) {

@@ -22,6 +22,7 @@
 #include <algorithm>
 
 #include "zb_fastenc.hpp"
+#include "zb_frame.hpp"
 #include "zb_tmpl.hpp"
 #include "zb_wavelib.hpp"
 
@@ -284,6 +285,12 @@ __device__ __forceinline__ uint32_t td_len5(uint32_t sym) { return (sym == NOK |
 
 // Both passes: one workgroup per tile of 256 instances (a persistent grid that copies the tables once per
 // workgroup measured slower: 0.39 -> 0.55 ms for the size pass on C3 10M)
+// a record's bytes in the drain: its value, or (FR) its frame -- prefix + value, padded to 8 (no rejection reasons in a
+// deferred batch)
+template <bool FR>
+__device__ __forceinline__ uint32_t td_bytes(uint32_t vl) { return FR ? (FRAME_PREFIX + vl + 7) & ~7u : vl; }
+
+template <bool FR>
 __global__ void __launch_bounds__(TD_WG) k_tdrain_size(TDrainParams D) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_tab[];
   __shared__ unsigned long long s_pay[TD_WG / 64];
@@ -313,7 +320,8 @@ __global__ void __launch_bounds__(TD_WG) k_tdrain_size(TDrainParams D) {
           const TmplRec t = T.tmpl[(L.cls * T.wmax + w) * TF + k];
           const uint32_t plen = t.payload == PAY_CREATE ? L.create_len : arena_len(P.arena, t.payload);
           const ValueConst vc = T.vconst[t.elem];
-          mine += (kind_vt(t.kind) == ZB_VT_JOB ? vc.job : vc.wf) + td_len5(t.inst) + td_len5(t.scope) + mp_bin_len(plen);
+          mine += td_bytes<FR>((kind_vt(t.kind) == ZB_VT_JOB ? vc.job : vc.wf) + td_len5(t.inst) + td_len5(t.scope) +
+                               mp_bin_len(plen));
           pay += plen;
         }
       } else {
@@ -322,7 +330,7 @@ __global__ void __launch_bounds__(TD_WG) k_tdrain_size(TDrainParams D) {
         for (uint32_t k = 0; k < G.nrec; k++) {
           uint32_t vl, plen;
           (void)td_record(P, T, L.L, L.cls, w, k, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl, plen);
-          mine += vl;
+          mine += td_bytes<FR>(vl);
           pay += plen;
         }
       }
@@ -399,14 +407,14 @@ __global__ void __launch_bounds__(256) k_tdrain_sizes(TDrainParams D, uint32_t w
   D.pay_part[g] = pay;
 }
 
-template <uint32_t IMG>
+// FR: log frames (zb_serialize_frames): each record's 13 prefix words (zb_frame.hpp) go into the image before its value,
+// which the writer ends with the frame's zero padding; no headers. A record's source is its parent in the instance's
+// previous generation (TmplRec.pad[0], as k_tmpl writes srcd), the first generation's the instance's CREATE; a batch
+// (same source, contiguous) is at most the instance's TF records of one generation.
+template <uint32_t IMG, bool FR>
 __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4))) k_tdrain_write(TDrainParams D) {
   // each wave's image, then its lanes' dummy slots (the branch-free writer's stores that must not land: FastWB)
   __shared__ __attribute__((aligned(16))) uint8_t s_img[TD_WG / 64][IMG + 16 + 8 * 64];
-#ifdef ZB_EXP_OCC2  // (measurement variant: two workgroups per CU)
-  __shared__ uint8_t s_occ[24 * 1024];
-  if (D.wmax == 0xffffffffu) s_occ[threadIdx.x] = 1;
-#endif
   extern __shared__ __attribute__((aligned(16))) uint8_t s_tab[];  // value segments + the batch's tables
   const TrajParams& P = D.t;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -435,6 +443,21 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
     // every store issued so far
 #pragma unroll
     for (int j = 0; j < SER_PRE; j++) asm volatile("" : "+v"(cpre[j]));
+    // frames: request metadata of the instance's CREATE (its CREATED event carries it), the instance's records of the
+    // previous generation (sources)
+    uint64_t rid = ~0ull;
+    uint32_t sid = 0x80000000u;
+    if (FR && D.nreqs) {
+      if (D.req_dense) {
+        rid = D.reqs[L.inst].request_id;
+        sid = (uint32_t)D.reqs[L.inst].request_stream_id;
+      } else {
+        frame_request(D.reqs, D.nreqs, P.log_base + L.inst, rid, sid);
+      }
+      asm volatile("" : "+v"(rid), "+v"(sid));  // (retired before the first store, as the payload words)
+    }
+    int64_t prev0 = P.log_base + L.inst;
+    const FrameConst fcst{D.stream_id, D.raft_term, D.timestamp};
     // the wave's first lane's class ranks (td_gen_wave)
     uint32_t b0[CLS_MAX];
 #pragma unroll
@@ -466,9 +489,16 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
         if (G.nrec > 0) d0 = td_record<true, L5>(P, T, L.L, L.cls, w, 0, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl0, plen);
         if (G.nrec > 1) d1 = td_record<true, L5>(P, T, L.L, L.cls, w, 1, G, L.inst, L.create_ref, L.create_len, L.kwf0, vl1, plen);
       }
-      const uint32_t mine = vl0 + vl1;
+      const uint32_t f0 = G.nrec > 0 ? td_bytes<FR>(vl0) : 0u, f1 = G.nrec > 1 ? td_bytes<FR>(vl1) : 0u;
+      const uint32_t mine = f0 + f1;
       const uint32_t incl = wave_incl_scan(mine);
       const uint32_t rel = incl - mine;  // this lane's values: [wbase + rel, wbase + incl)
+      // the size pass's byte total of the wave (a formula for most waves: k_tdrain_sizes) must be what the records
+      // encode to; a mismatch writes nothing and sends the batch to the descriptor drain instead of past its range
+      if (wbase + (uint64_t)__builtin_amdgcn_readlane(incl, 63) != wend) {
+        bad = 1;
+        continue;
+      }
 #ifdef ZB_PHASES
       ph_g++;
 #endif
@@ -476,18 +506,18 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
       // headers: key, types / intent / rejection, length, offset (the position is implicit: start + index)
 #pragma unroll
       for (int k = 0; k < TF; k++) {
-        if ((uint32_t)k >= G.nrec) break;
+        if (FR || (uint32_t)k >= G.nrec) break;
         const zb_rec& d = k ? d1 : d0;
         uint64_t* dh = (uint64_t*)(D.headers + (G.pos0 + k - D.start));
         const uint64_t meta = (uint64_t)kind_rt(d.kind) | (uint64_t)kind_vt(d.kind) << 8 | (uint64_t)d.intent << 16 |
                               255ull << 24 | (uint64_t)(k ? vl1 : vl0) << 32;  // (no rejections: k_tmpl_decide)
         // plain stores: a header line is written by three stores of every lane (24-byte stride), which L2 merges into
         // whole lines; as non-temporal stores they reached HBM as partial lines (write pass 4.55 -> 4.25 ms same box)
-#ifndef ZB_EXP_NO_HEADERS  // (measurement variants only: tools/ab_variant.sh)
-        dh[0] = (uint64_t)d.key;
-        dh[1] = meta;
-        dh[2] = wbase + rel + (k ? vl0 : 0);
-#endif
+        if (!FR) {
+          dh[0] = (uint64_t)d.key;
+          dh[1] = meta;
+          dh[2] = wbase + rel + (k ? vl0 : 0);
+        }
       }
       TD_PHASE(1);
       // rounds: lanes [a, b) whose values fit the image from the round's first byte; each lane encodes its own
@@ -503,11 +533,14 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
           bad = 1;
           break;
         }
-#ifdef ZB_EXP_NO_ENCODE
-        if (false) {
-#else
         if (fit && mine) {
-#endif
+          // frames: the sources of the instance's records (TmplRec.pad[0]: its parent's index in the previous generation)
+          uint32_t sp0 = 0, sp1 = 0;
+          if (FR) {
+            const TmplRec* tr = T.tmpl + (L.cls * T.wmax + w) * TF;
+            sp0 = tr[0].pad[0];
+            sp1 = G.nrec > 1 ? tr[1].pad[0] : sp0 + 1;
+          }
 #pragma unroll 1
           for (uint32_t k = 0; k < G.nrec; k++) {
             const zb_rec d = k ? d1 : d0;
@@ -517,30 +550,36 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
 #pragma unroll
             for (int j = 0; j < SER_PRE; j++) pre[j] = cpre[j];
             td_static_pre(P.arena, !cr, d.payload, pre);  // a static blob: through the scalar cache
+            const uint32_t at = sh + (rel - lo) + (k ? f0 : 0);
+            const uint32_t vl = k ? vl1 : vl0;
             FastWB fw;
-            fw.begin(img, sh + (rel - lo) + (k ? vl0 : 0), IMG + 16 + 8 * lane);
-            fast_encode<L5>(fw, d, tab, segs, dw, pre);
-            if (fw.n() != (k ? vl1 : vl0)) bad = 1;  // the formula and the encoder disagree: never silently
+            fw.begin(img, at + (FR ? FRAME_PREFIX : 0u), IMG + 16 + 8 * lane);
+            fast_encode<L5, true, FR>(fw, d, tab, segs, dw, pre);
+            if (fw.n() != vl) bad = 1;  // the formula and the encoder disagree: never silently
+            if (FR) {
+              const int64_t src = prev0 + (k ? sp1 : sp0);
+              const bool pair = G.nrec > 1 && sp0 == sp1;  // (the instance's two records share their source)
+              const uint8_t vt = kind_vt(d.kind), rt = kind_rt(d.kind);
+              const bool req = vt == ZB_VT_WORKFLOW_INSTANCE && rt == ZB_RT_EVENT && d.intent == WI_CREATED;
+              uint64_t h[13];
+              frame_words(h, fcst, FRAME_PREFIX + vl, frame_flags(k == 0 || !pair, k == 1 || !pair), G.pos0 + k,
+                          frame_producer(src, vt, rt, d.intent), src, d.key, rt, vt, d.intent, 255, 0,
+                          req ? rid : ~0ull, req ? sid : 0x80000000u);
+              uint64_t* hd = (uint64_t*)(img + at);
+#pragma unroll
+              for (int j = 0; j < 13; j++) hd[j] = h[j];
+            }
           }
         }
         const uint32_t hi = __builtin_amdgcn_readlane(incl, b - 1);
         TD_PHASE(2);
-#ifdef ZB_EXP_PRIO  // (measurement variant: the stream at raised wave priority)
-        __builtin_amdgcn_s_setprio(2);
-#endif
         wave_lds_sync();
-#if defined(ZB_EXP_STREAM4)
-        wave_stream4(img, D.out, wbase + lo, sh, hi - lo, lane);
-#elif !defined(ZB_EXP_NO_STREAM)
         wave_stream(img, D.out, wbase + lo, sh, hi - lo, lane);
-#endif
         wave_lds_sync();  // the image is reused by the next round
-#ifdef ZB_EXP_PRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
         TD_PHASE(3);
         a = b;
       }
+      if (G.nrec) prev0 = G.pos0;
     }
     };
     const bool lo_ok = P.wf_start + 5 * L.kwf0 >= 65536 && P.log_base + L.inst >= 65536 &&
@@ -610,12 +649,16 @@ void launch_tmpl_decide(const TrajParams& p, hipStream_t s) {
 }
 
 void launch_tdrain_size(const TDrainParams& d, uint32_t wg0, hipStream_t s) {
-  if (wg0) hipLaunchKernelGGL(k_tdrain_size, dim3(wg0), dim3(TD_WG), td_layout(d, false).total, s, d);
+  if (wg0 && d.frames) hipLaunchKernelGGL(k_tdrain_size<true>, dim3(wg0), dim3(TD_WG), td_layout(d, false).total, s, d);
+  else if (wg0) hipLaunchKernelGGL(k_tdrain_size<false>, dim3(wg0), dim3(TD_WG), td_layout(d, false).total, s, d);
   const uint64_t rest = (uint64_t)d.t.nwg - wg0;
   if (rest) hipLaunchKernelGGL(k_tdrain_sizes, dim3((unsigned)((rest + 255) / 256)), dim3(256), 0, s, d, wg0);
 }
 void launch_tdrain_write(const TDrainParams& d, hipStream_t s) {
-  hipLaunchKernelGGL((k_tdrain_write<TD_IMG>), dim3((unsigned)d.t.nwg), dim3(TD_WG), td_layout(d, true).total, s, d);
+  if (d.frames)
+    hipLaunchKernelGGL((k_tdrain_write<TD_IMG, true>), dim3((unsigned)d.t.nwg), dim3(TD_WG), td_layout(d, true).total, s, d);
+  else
+    hipLaunchKernelGGL((k_tdrain_write<TD_IMG, false>), dim3((unsigned)d.t.nwg), dim3(TD_WG), td_layout(d, true).total, s, d);
   hipLaunchKernelGGL(k_tdrain_sum, dim3((unsigned)std::min<int64_t>(256, (d.t.nwg + 255) / 256)), dim3(256), 0, s, d,
                      (int64_t)d.t.nwg);
 }

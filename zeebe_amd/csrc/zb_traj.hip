@@ -1408,15 +1408,7 @@ __global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
     if (((len + 11) & ~7u) <= CL_STRIDE * 4) {  // (stage_copy writes whole 8-byte words)
       stage_copy(pp, len, s_doc + t * CL_STRIDE);
       const uint8_t* doc = (const uint8_t*)(s_doc + t * CL_STRIDE) + 4;
-#if defined(ZB_EXP_CLS_NOEVAL)  // (measurement variants only: tools/ab_variant.sh)
-      Extract ext;
-      extract_fast(P, doc, len, ext);
-      key = ext.ok ? (ext.meta[0] & 1) : 0;
-#elif defined(ZB_EXP_CLS_COPYONLY)
-      key = doc[len - 1] & 1;
-#else
       key = P.cls_nq ? outcome_key<true>(P, doc, len) : outcome_key<false>(P, doc, len);
-#endif
     } else {
       for (int k = 0; k < P.nsplits; k++) key += (elem_ctl(P, P.split_elem[k]).cond_count() + 1) * P.split_stride[k];
     }

@@ -1629,325 +1629,6 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
 #undef ZB_PHASE
 }
 
-// k_wave with the hand-off of tile t overlapped by the process phase of the workgroup's next tile (t + G): the tile's
-// aggregate is published right after its process phase, then the next tile is processed into the other LDS slot
-// buffer, and only then does the workgroup wait for tile t's prefix and emit it. A process phase never depends on an
-// emit of the same wave (the three-kernel form runs every process before any emit), so the order is free; no wait
-// depends on a later step of its own workgroup (aggregates are published before any wait), so nothing deadlocks.
-__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(3, 8))) k_wave2(WaveParams P) {
-  __shared__ Slot s_slots[2][WG * MAX_SLOTS];
-  __shared__ uint64_t s_a[WG / 64], s_b[WG / 64];
-  __shared__ uint64_t s_st[WG / 64][2];  // transitions | completed << 32, created | canceled << 32
-  __shared__ uint64_t s_ex[LB_FIELDS];   // the tile's exclusive prefix
-  __shared__ uint64_t s_part[3][LB_FIELDS];  // its parts: in the group, earlier groups of the round, the round base
-  __shared__ int s_void;                 // a hand-off timed out: the tile's prefix is unknown, nothing is emitted
-  const WaveHdr* hin = P.hdr + (P.wave & 1);
-  WaveHdr* hout = P.hdr + ((P.wave + 1) & 1);
-  const Chunk c = wave_chunk(P, hin);
-  if (c.n <= 0) {  // nothing in this wave (the batch outran quiescence): carry the header forward
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      *hout = *hin;
-      P.merge_count[P.wave & 1] = 0;
-      P.cond_count[P.wave & 1] = 0;
-      if (P.sub_count) clear_sub_counts(P);
-    }
-    return;
-  }
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t ntiles = (c.n + WG - 1) / WG;
-  const int64_t gen_end = hin->gen_end;
-  const int64_t end = hin->end, wf_next = hin->wf_next, job_next = hin->job_next;
-  const uint64_t rows_next = (uint64_t)hin->rows_next, arena_next = (uint64_t)hin->arena_next;
-  const uint64_t par = (uint64_t)(P.wave & 1) * P.job_cap;
-  const int64_t G = gridDim.x;
-  const int64_t GPR = (G + LB_GROUP - 1) / LB_GROUP;  // groups per round
-  const uint32_t tag8 = P.lb_tag8, tag_grp = lb_tag(P.epoch, 0), tag_rnd = lb_tag(P.epoch, 1);
-  uint64_t* const lbA = P.lookback;
-  uint64_t* const lbG = P.lookback + 2 * P.lb_tiles;
-  uint64_t* const lbR = lbG + (uint64_t)LB_FIELDS * (P.lb_tiles + 512);
-  // the workgroup's statistics (transitions, completed, created, canceled): summed over its tiles, added to the
-  // partition counters once at the end (they are not part of the scan)
-  uint64_t wg_sa = 0, wg_sb = 0;
-
-#ifdef ZB_PHASES
-  uint64_t ph_t = wall_clock64(), ph[4] = {0, 0, 0, 0};  // process, hand-off, emit, hand-off spins (first wave)
-#define ZB_PHASE(k) do { const uint64_t ph_n = wall_clock64(); ph[k] += ph_n - ph_t; ph_t = ph_n; } while (0)
-#else
-#define ZB_PHASE(k) do { } while (0)
-#endif
-  if (threadIdx.x == 0) s_void = 0;
-  // per tile carried from its process phase to its hand-off / emit
-  int64_t tile = blockIdx.x;
-  int64_t i = 0, r = 0;
-  uint64_t w = 0, a = 0, b = 0, ta = 0, tb = 0;
-  int64_t n_i = 0, n_r = 0;
-  uint64_t n_w = 0, n_a = 0, n_b = 0, n_ta = 0, n_tb = 0;
-  auto process_tile = [&](const int64_t tile, Slot* const sl, int64_t& i, int64_t& r, uint64_t& w, uint64_t& a,
-                          uint64_t& b, uint64_t& ta, uint64_t& tb) {
-    i = tile * WG + threadIdx.x;  // wave-relative index
-    r = c.begin + i;
-    // ---- process (k_process)
-    TState t;
-    t.s = sl + threadIdx.x * MAX_SLOTS;
-    t.ns = t.nwf = t.njob = t.nrow = 0;
-    t.bytes = 0; t.merge = false; t.detail = false; t.err = 0; t.err_site = 0;
-    t.transitions = t.completed = t.created = t.merges = t.canceled = 0;
-    t.merge_bytes = t.cond_bytes = 0;
-    t.sub = false;
-    t.nexp = 0; t.exp_ord = 0; t.src_off = 0;
-    uint32_t nconds = 0;
-    if (r < c.end) {
-      const zb_rec rec = P.log[r];
-      const uint64_t lk = P.links[r];
-      const uint32_t vl = P.vlen[r];
-      if (!grouped(rec)) {
-        process_record(P, rec, r, (uint32_t)lk, (uint32_t)(lk >> 32), t);
-        annotate_slots(P, t, 0, rec, vl);
-        for (int64_t q = r + 1; q < gen_end && q < r + 4; q++) {
-          const zb_rec rec2 = P.log[q];
-          if (!grouped(rec2)) break;
-          const uint64_t lk2 = P.links[q];
-          const uint32_t vl2 = P.vlen[q];
-          t.src_off = (uint32_t)(q - r);
-          const int ns0 = t.ns;
-          process_record(P, rec2, q, (uint32_t)lk2, (uint32_t)(lk2 >> 32), t);
-          annotate_slots(P, t, ns0, rec2, vl2);
-        }
-      }
-    }
-    for (int k = 0; k < t.ns; k++) {
-      const Slot& sl = t.s[k];
-      nconds += (sl.flags & SF_COND_JOB) ? 1 : 0;
-      if (kind_vt(sl.d.kind) == ZB_VT_WORKFLOW_INSTANCE && kind_rt(sl.d.kind) == ZB_RT_EVENT) t.transitions++;
-    }
-    t.transitions += t.nexp;  // a fork's SEQUENCE_FLOW_TAKEN events
-    const uint64_t nwf_staged = (uint64_t)t.nwf - t.nexp;
-    w = (uint64_t)t.ns | (nwf_staged << CW_NWF) | ((uint64_t)t.njob << CW_NJOB) |
-                       ((uint64_t)t.nrow << CW_NROW) | ((uint64_t)(t.merge ? 1 : 0) << CW_MERGE) |
-                       ((uint64_t)(t.detail ? 1 : 0) << CW_DETAIL) | ((uint64_t)nconds << CW_NCOND) |
-                       ((uint64_t)t.nexp << CW_NEXP) | ((uint64_t)t.bytes << 32);
-    if (t.merge || t.detail) {  // (global, not LDS: 8 KB of LDS per workgroup cost a resident workgroup per CU)
-      ItemInfo inf;
-      inf.m_src = t.m_src; inf.m_tgt = t.m_tgt; inf.m_len = t.m_len; inf.m_bytes = t.merge ? t.m_bytes : 0;
-      inf.d_pos = t.d_pos; inf.d_q = t.d_q; inf.d_type = t.d_type; inf.d_code = t.d_code; inf.d_a = t.d_a;
-      inf.d_b = t.d_b; inf.has_detail = t.detail; inf.ns = (uint8_t)t.ns;
-      P.info[i] = inf;
-    }
-    if (__ballot(t.sub)) {  // wave-uniform: this tile's subscribe steps, in the wave's job list (its stripe)
-      const uint32_t s = blockIdx.x % SUB_STRIPES;
-      const uint64_t scap = P.job_cap / SUB_STRIPES;
-      const uint32_t slot = wave_alloc(P.sub_count + (P.wave & 1) * SUB_STRIPES + s, t.sub ? 1u : 0u);
-      if (t.sub) {
-        if (slot < scap) P.sub_jobs[s * scap + slot] = (uint64_t)t.sub_pos;
-        else fail_at(t, DE_LOG_FULL, 36);
-      }
-    }
-    if (t.err) {
-      atomicOr(P.err, t.err);
-      atomicMin((unsigned long long*)P.err_info, ((unsigned long long)r << 8) | (t.err_site & 0xff));
-    }
-    // ---- tile scan (packed as in k_emit): a = outputs | wf << 16 | job << 32 | row << 48,
-    //      b = bytes | merges << 40 | conds << 52
-    const uint64_t nexp = (w >> CW_NEXP) & 63;
-    const uint64_t a0 = ((w & 7) + nexp) | ((((w >> CW_NWF) & 7) + nexp) << 16) | (((w >> CW_NJOB) & 7) << 32) |
-                        (((w >> CW_NROW) & 7) << 48);
-    const uint64_t b0 = (w >> 32) | (((w >> CW_MERGE) & 1) << 40) | (((w >> CW_NCOND) & 7) << 52);
-    a = a0; b = b0;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint64_t ua = shfl_up64(a, d), ub = shfl_up64(b, d);
-      if (lane >= d) { a += ua; b += ub; }
-    }
-    uint64_t st0 = (uint64_t)t.transitions | ((uint64_t)t.completed << 32);
-    uint64_t st1 = (uint64_t)t.created | ((uint64_t)t.canceled << 32);
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) { st0 += shfl_down64(st0, d); st1 += shfl_down64(st1, d); }
-    if (lane == 63) { s_a[wv] = a; s_b[wv] = b; }
-    if (lane == 0) { s_st[wv][0] = st0; s_st[wv][1] = st1; }
-    __syncthreads();
-    ZB_PHASE(0);  // process + tile scan
-    ta = 0; tb = 0;
-#pragma unroll
-    for (int k = 0; k < WG / 64; k++) {
-      if (k < wv) { a += s_a[k]; b += s_b[k]; }
-      ta += s_a[k]; tb += s_b[k];
-    }
-    a -= a0;
-    b -= b0;
-    // the tile's aggregate, published as soon as it is known (before this workgroup waits for anything)
-    if (threadIdx.x == 0) {
-      const uint64_t tbytes = tb & 0xffffffffffull;
-      const uint64_t tmerge = (tb >> 40) & 0xfff, tcond = tb >> 52;
-      const uint64_t tb36 = tbytes < (1ull << 36) ? tbytes : (1ull << 36) - 1;
-      if (tbytes != tb36) atomicOr(P.err, (uint32_t)DE_ARENA_FULL);  // (a tile's blobs past 64 GB: no arena holds them)
-      __hip_atomic_store(lbA + 2 * tile, lb_pack_a(tag8, ta), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(lbA + 2 * tile + 1, lb_pack_b(tag8, tb36, tmerge, tcond), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      wg_sa += s_st[0][0] + s_st[1][0] + s_st[2][0] + s_st[3][0];
-      wg_sb += s_st[0][1] + s_st[1][1] + s_st[2][1] + s_st[3][1];
-    }
-  };
-  auto handoff_emit = [&](const int64_t tile, Slot* const sl, const int64_t i, const int64_t r, const uint64_t w,
-                          const uint64_t a, const uint64_t b, const uint64_t ta, const uint64_t tb) {
-    // ---- offsets: this tile's place in its round (k) and group (gi, position u)
-    const int64_t k = tile / G, j = tile - k * G;
-    const int64_t gi = j / LB_GROUP, u = j % LB_GROUP;
-    const int64_t t_grp0 = tile - u;  // the group's first tile
-    const bool last_of_chunk = tile == ntiles - 1;
-    const bool last_of_group = u == LB_GROUP - 1 || j == G - 1 || last_of_chunk;
-    const uint64_t gg = (uint64_t)(k * GPR + gi);  // the group's index among the wave's groups
-    const uint64_t t_start = wall_clock64();
-    if (wv == 0) {
-      // the aggregate, published first (lane 0), then this tile's exclusive prefix within its group
-      const uint64_t tbytes = tb & 0xffffffffffull;
-      const uint64_t tmerge = (tb >> 40) & 0xfff, tcond = tb >> 52;
-      const uint64_t* gp[2] = {lbA + 2 * (t_grp0 + lane), lbA + 2 * (t_grp0 + lane) + 1};
-      const uint32_t tg[2] = {tag8, tag8};
-      uint64_t v[2] = {0, 0};
-      const bool ok = lb_wait<2>(P.err, gp, tg, 56, lane < u, v, t_start);
-      uint64_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;  // rec | wf << 32, job | row << 32, merges | conds << 32, bytes
-      if (lane < u) {
-        x0 = ((v[0] >> 39) & 0x1ffff) | (((v[0] >> 22) & 0x1ffff) << 32);
-        x1 = ((v[0] >> 11) & 0x7ff) | ((v[0] & 0x7ff) << 32);
-        x2 = ((v[1] >> 47) & 0x1ff) | (((v[1] >> 36) & 0x7ff) << 32);
-        x3 = v[1] & ((1ull << 36) - 1);
-      }
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) {
-        x0 += __shfl_xor(x0, d, 64); x1 += __shfl_xor(x1, d, 64);
-        x2 += __shfl_xor(x2, d, 64); x3 += __shfl_xor(x3, d, 64);
-      }
-      // lane f < 8: field f of the exclusive prefix within the group (bytes whole in field 4, field 5 zero)
-      const uint64_t e = lane == 0 ? (uint32_t)x0 : lane == 1 ? x0 >> 32 : lane == 2 ? (uint32_t)x1 :
-                         lane == 3 ? x1 >> 32 : lane == 4 ? x3 : lane == 6 ? (uint32_t)x2 : lane == 7 ? x2 >> 32 : 0;
-      if (!ok && lane == 0) s_void = 1;
-      if (lane < LB_FIELDS) s_part[0][lane] = ok ? e : 0;
-      if (ok && last_of_group && lane < LB_FIELDS) {  // the group's total, for the later groups of the round
-        const uint64_t own = lane == 4 ? tbytes : lane == 5 ? 0 : lb_field(ta, tmerge, tcond, lane);
-        const uint64_t tot = e + own;
-        const uint32_t val = lane == 4 ? (uint32_t)tot : lane == 5 ? (uint32_t)((x3 + tbytes) >> 32) : (uint32_t)tot;
-        __hip_atomic_store(lbG + gg * LB_FIELDS + lane, ((uint64_t)tag_grp << 32) | val, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      }
-    } else if (wv == 1) {
-      // the totals of the round's earlier groups: lane = 8 * group + field, 8 groups per pass
-      uint64_t acc = 0;
-      bool ok = true;
-      for (int64_t base = 0; base < gi && ok; base += 64 / LB_FIELDS) {
-        const int64_t q = base + lane / LB_FIELDS;
-        const uint64_t* gp[1] = {lbG + (uint64_t)(k * GPR + q) * LB_FIELDS + lane % LB_FIELDS};
-        const uint32_t tg[1] = {tag_grp};
-        uint64_t v[1] = {0};
-        ok = lb_wait<1>(P.err, gp, tg, 32, q < gi, v, t_start);
-        uint64_t x = q < gi ? (uint32_t)v[0] : 0;
-#pragma unroll
-        for (int d = LB_FIELDS; d < 64; d <<= 1) x += __shfl_xor(x, d, 64);
-        acc += x;
-      }
-      // bytes travel as two 32-bit granules (fields 4, 5): recombine the carry
-      const uint64_t lo = __shfl(acc, 4, 64), hi = __shfl(acc, 5, 64);
-      if (!ok && lane == 0) s_void = 1;
-      if (lane < LB_FIELDS) s_part[1][lane] = !ok ? 0 : lane == 4 ? lo + (hi << 32) : lane == 5 ? 0 : acc;
-    } else if (wv == 2) {
-      // the round's base, published by the previous round's last tile
-      const uint64_t* gp[1] = {lbR + (uint64_t)k * LB_FIELDS + lane % LB_FIELDS};
-      const uint32_t tg[1] = {tag_rnd};
-      uint64_t v[1] = {0};
-      const bool ok = lb_wait<1>(P.err, gp, tg, 32, k > 0 && lane < LB_FIELDS, v, t_start);
-      const uint64_t x = k > 0 ? (uint32_t)v[0] : 0;
-      const uint64_t hi = __shfl(x, 5, 64);
-      if (!ok && lane == 0) s_void = 1;
-      if (lane < LB_FIELDS) s_part[2][lane] = !ok ? 0 : lane == 4 ? x + (hi << 32) : lane == 5 ? 0 : x;
-    }
-    __syncthreads();
-    if (wv == 0) {
-      const uint64_t tbytes = tb & 0xffffffffffull;
-      const uint64_t own = lane == 4 ? tbytes : lane == 5 ? 0 : lb_field(ta, (tb >> 40) & 0xfff, tb >> 52, lane);
-      const uint64_t ex = lane < LB_FIELDS ? s_part[0][lane] + s_part[1][lane] + s_part[2][lane] : 0;
-      const uint64_t inc = ex + own;
-      const uint64_t t0 = __shfl(inc, 0, 64), t1 = __shfl(inc, 1, 64), t2 = __shfl(inc, 2, 64);
-      const uint64_t t3 = __shfl(inc, 3, 64), t4 = __shfl(inc, 4, 64), t6 = __shfl(inc, 6, 64);
-      const uint64_t t7 = __shfl(inc, 7, 64);
-      if (s_void) {
-        if (lane == 0) atomicOr(P.err, (uint32_t)DE_TIMEOUT);  // (the host fails the wave: nothing is written from a
-      } else {                                                 //  partial prefix; the other tiles stop waiting too)
-        if (lane < LB_FIELDS) s_ex[lane] = ex;
-        // the last tile of a round hands the next round its base
-        if (j == G - 1 && !last_of_chunk && lane < LB_FIELDS) {
-          const uint32_t val = lane == 4 ? (uint32_t)t4 : lane == 5 ? (uint32_t)(t4 >> 32) : (uint32_t)inc;
-          __hip_atomic_store(lbR + (uint64_t)(k + 1) * LB_FIELDS + lane, ((uint64_t)tag_rnd << 32) | val,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        // the chunk's last tile: totals -> next wave header, counters, job counts (k_scan's job)
-        if (last_of_chunk && lane == 0) {
-          WaveHdr h = *hin;
-          h.begin = c.end;
-          h.end = hin->end + (int64_t)t0;
-          h.gen_end = (c.end == hin->gen_end) ? h.end : hin->gen_end;
-          h.wf_next = hin->wf_next + 5 * (int64_t)t1;
-          h.job_next = hin->job_next + 5 * (int64_t)t2;
-          h.rows_next = hin->rows_next + (int64_t)t3;
-          h.arena_next = hin->arena_next + (int64_t)t4;
-          P.stats[6] += 1;
-          uint32_t err = 0;
-          if ((uint64_t)h.end > P.log_cap) err |= DE_LOG_FULL;
-          if ((uint64_t)h.rows_next > P.row_cap) err |= DE_ROWS_FULL;
-          if ((uint64_t)h.arena_next > P.arena_cap) err |= DE_ARENA_FULL;
-          if (t6 > P.job_cap || t7 > P.job_cap) err |= DE_LOG_FULL;
-          if (err) atomicOr(P.err, err);
-          *hout = h;
-                P.merge_count[P.wave & 1] = (uint32_t)t6;
-          P.cond_count[P.wave & 1] = (uint32_t)t7;
-          if (P.sub_count) clear_sub_counts(P);  // the next wave's subscribe list
-        }
-      }
-    }
-    __syncthreads();
-    ZB_PHASE(1);  // hand-off (+ the chunk's header on the last tile)
-    // ---- emit (k_emit) straight from the LDS slots
-    const uint64_t we = w;
-    const int ns = (int)(we & 7);
-    if (!s_void && r < c.end && (ns || ((we >> CW_NEXP) & 63) || ((we >> CW_DETAIL) & 1))) {
-      const uint64_t out_rec = (uint64_t)end + s_ex[0] + (a & 0xffff);
-      const uint64_t wf0 = s_ex[1] + ((a >> 16) & 0xffff);
-      const uint64_t job0 = s_ex[2] + ((a >> 32) & 0xffff);
-      const uint64_t row0 = rows_next + s_ex[3] + (a >> 48);
-      const uint64_t bump = arena_next + s_ex[4] + (b & 0xffffffffffull);
-      const uint64_t merge_j = s_ex[6] + ((b >> 40) & 0xfff);
-      const uint64_t cond_j = s_ex[7] + (b >> 52);
-      ItemInfo inf{};
-      if (we & ((1ull << CW_MERGE) | (1ull << CW_DETAIL))) inf = P.info[i];
-      emit_item(P, c, i, we, sl + threadIdx.x * MAX_SLOTS, inf, out_rec, wf0, job0, row0, bump, merge_j, cond_j,
-                wf_next, job_next, par);
-    }
-    __syncthreads();  // the scan scratch is reused by the next hand-off
-    if (threadIdx.x == 0) s_void = 0;  // (ordered before the next hand-off by the next tile scan's barrier)
-    ZB_PHASE(2);  // emit
-    };
-  if (tile < ntiles) process_tile(tile, s_slots[0], i, r, w, a, b, ta, tb);
-#pragma unroll 1
-  for (int it = 0; tile < ntiles; it++, tile += G) {
-    if (tile + G < ntiles) process_tile(tile + G, s_slots[(it + 1) & 1], n_i, n_r, n_w, n_a, n_b, n_ta, n_tb);
-    handoff_emit(tile, s_slots[it & 1], i, r, w, a, b, ta, tb);
-    i = n_i; r = n_r; w = n_w; a = n_a; b = n_b; ta = n_ta; tb = n_tb;
-  }
-  if (threadIdx.x == 0 && (wg_sa | wg_sb)) {  // (into the workgroup's bank: launch_stat_fold)
-    unsigned long long* bank = (unsigned long long*)(P.stats + 8 + 8 * (blockIdx.x % STAT_BANKS));
-    atomicAdd(bank + 0, (unsigned long long)(uint32_t)wg_sa);  // transitions
-    atomicAdd(bank + 1, (unsigned long long)(wg_sa >> 32));    // completed instances
-    atomicAdd(bank + 2, (unsigned long long)(uint32_t)wg_sb);  // created
-    atomicAdd(bank + 3, (unsigned long long)(wg_sb >> 32));    // canceled
-  }
-#ifdef ZB_PHASES
-  if (threadIdx.x == 0 && P.phase) {
-    for (int k = 0; k < 3; k++) atomicAdd(P.phase + k, (unsigned long long)ph[k]);
-    atomicAdd(P.phase + 4, (unsigned long long)((ntiles - blockIdx.x + gridDim.x - 1) / gridDim.x));
-    atomicAdd(P.phase + 3, (unsigned long long)((ntiles - blockIdx.x + gridDim.x - 1) / gridDim.x));
-  }
-#endif
-#undef ZB_PHASE
-}
-
 
 // ------------------------------------------------------------------------------ k_conflict
 // The chunk of a generation that holds records of conflicting instances (WaveParams.conf_*) ends at the first
@@ -2006,17 +1687,12 @@ void launch_stat_fold(uint64_t* stats, hipStream_t stream) {
   hipLaunchKernelGGL(k_stat_fold, dim3(1), dim3(64), 0, stream, stats);
 }
 
-#ifdef ZB_EXP_PIPE  // (measurement variant: k_wave2, the hand-off overlapped with the next tile's process phase)
-#define ZB_K_WAVE k_wave2
-#else
-#define ZB_K_WAVE k_wave
-#endif
 void launch_wave(const WaveParams& p, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(ZB_K_WAVE, dim3(grid), dim3(WG), 0, stream, p);
+  hipLaunchKernelGGL(k_wave, dim3(grid), dim3(WG), 0, stream, p);
 }
 int wave_resident_per_cu() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ZB_K_WAVE, WG, 0) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_wave, WG, 0) != hipSuccess) return 0;
   return n;
 }
 

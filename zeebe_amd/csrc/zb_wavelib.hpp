@@ -34,50 +34,14 @@ __device__ __forceinline__ void wave_stream(const uint8_t* img, uint8_t* out, ui
   const uint32_t full_lo = (shift + 15) & ~15u, full_hi = lim & ~15u;
   for (uint32_t c = full_lo + 16 * lane; c < full_hi; c += 16 * 64) {
     const uint4 v = *(const uint4*)(img + c);
-#ifdef ZB_EXP_STREAM_PLAIN  // (measurement variants only)
-    *(uint4*)(dst + c) = v;
-#else
     __builtin_nontemporal_store(v.x, (uint32_t*)(dst + c));
     __builtin_nontemporal_store(v.y, (uint32_t*)(dst + c) + 1);
     __builtin_nontemporal_store(v.z, (uint32_t*)(dst + c) + 2);
     __builtin_nontemporal_store(v.w, (uint32_t*)(dst + c) + 3);
-#endif
   }
   const uint32_t head_end = full_lo < lim ? full_lo : lim;
   const uint32_t tail_lo = full_hi > head_end ? full_hi : head_end;
   const uint32_t nh = head_end - shift;  // at most 15 + 15 bytes: one per lane
-  if ((uint32_t)lane < nh) dst[shift + lane] = img[shift + lane];
-  else if ((uint32_t)lane < nh + (lim - tail_lo)) dst[tail_lo + lane - nh] = img[tail_lo + lane - nh];
-}
-
-// wave_stream with the image reads of four 1 KB chunks issued before their stores (one LDS latency per four chunks
-// instead of one per chunk)
-__device__ __forceinline__ void wave_stream4(const uint8_t* img, uint8_t* out, uint64_t o, uint32_t shift, uint32_t n,
-                                             int lane) {
-  uint8_t* dst = out + o - shift;
-  const uint32_t lim = shift + n;
-  const uint32_t full_lo = (shift + 15) & ~15u, full_hi = lim & ~15u;
-  for (uint32_t c = full_lo + 16 * lane; c < full_hi; c += 4 * 16 * 64) {
-    uint4 v[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t ck = c + 1024 * k;
-      v[k] = *(const uint4*)(img + (ck < full_hi ? ck : c));  // (past the range: a harmless re-read)
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t ck = c + 1024 * k;
-      if (ck < full_hi) {
-        __builtin_nontemporal_store(v[k].x, (uint32_t*)(dst + ck));
-        __builtin_nontemporal_store(v[k].y, (uint32_t*)(dst + ck) + 1);
-        __builtin_nontemporal_store(v[k].z, (uint32_t*)(dst + ck) + 2);
-        __builtin_nontemporal_store(v[k].w, (uint32_t*)(dst + ck) + 3);
-      }
-    }
-  }
-  const uint32_t head_end = full_lo < lim ? full_lo : lim;
-  const uint32_t tail_lo = full_hi > head_end ? full_hi : head_end;
-  const uint32_t nh = head_end - shift;
   if ((uint32_t)lane < nh) dst[shift + lane] = img[shift + lane];
   else if ((uint32_t)lane < nh + (lim - tail_lo)) dst[tail_lo + lane - nh] = img[tail_lo + lane - nh];
 }

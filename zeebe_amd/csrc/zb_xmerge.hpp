@@ -27,12 +27,9 @@ constexpr uint32_t XSLAB_COUNT = 32;        // pairs in flight (zb_xlock.hpp: on
 // zb_xlock.hpp x_run): 32 KB holds the tree of ~140 tokens (2 x source + target), the documents of a typical job /
 // message payload merge
 constexpr uint32_t XLANE_BYTES = 32u << 10;
-#ifndef ZB_EXP_XLANES  // (measurement variants only: tools/ab_variant.sh)
-constexpr uint32_t XLANE_COUNT = 65536;  // (2 GiB; k_merge_gen's grid: 256 workgroups of 256 lanes. C1 1M exact-tree
-                                         //  tick: 16K lanes 14.3 ms, 32K 10.4, 64K 9.5, 128K 12.1, 256K 12.4)
-#else
-constexpr uint32_t XLANE_COUNT = ZB_EXP_XLANES;
-#endif
+constexpr uint32_t XLANE_COUNT = 65536;  // (2 GiB per device, shared by its engines; k_merge_gen's grid: 256 workgroups of
+                                         //  256 lanes. C1 1M exact-tree tick: 16K lanes 14.3 ms, 32K 10.4, 64K 9.5, 128K
+                                         //  12.1, 256K 12.4)
 constexpr uint32_t XLANE_GROUPS = XLANE_COUNT / 64;          // lane groups (one wave's 64 workspaces)
 constexpr uint32_t XLOCK_COUNT = XSLAB_COUNT + XLANE_GROUPS;  // slab locks, then lane-group locks
 

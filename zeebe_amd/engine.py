@@ -426,6 +426,15 @@ class Engine:
         sids = (ctypes.c_int32 * max(n, 1))(*request_stream_ids)
         self._check(self._L.zb_set_request_metadata(self._h, n, ids, sids))
 
+    def set_request_metadata_np(self, request_ids, request_stream_ids):
+        """set_request_metadata from numpy arrays (uint64 / int32), without per-element conversion."""
+        import numpy as np
+
+        ids = np.ascontiguousarray(request_ids, dtype=np.uint64)
+        sids = np.ascontiguousarray(request_stream_ids, dtype=np.int32)
+        assert len(ids) == len(sids)
+        self._check(self._L.zb_set_request_metadata(self._h, len(ids), ids.ctypes.data, sids.ctypes.data))
+
     def drain_copy(self, dst_ptr: int, value_off: int, nbytes: int, headers_ptr=None):
         """zb_drain_copy into caller memory (an address, e.g. from pinned_alloc)."""
         self._check(self._L.zb_drain_copy(self._h, headers_ptr, dst_ptr, value_off, nbytes))
