@@ -623,7 +623,7 @@ def run_exact_tree(a, n=1_000_000, steps=3):
     tick with a flat completion payload; both on the trajectory path (the default) and on the general wave pipeline."""
     from zeebe_amd import workloads
 
-    out = {}
+    out, samples = {}, {}
     dup = b"\x82" + workloads.mp_str("step") + workloads.mp_int(1) + workloads.mp_str("step") + workloads.mp_int(2)
     flat = b"\x81" + workloads.mp_str("step") + workloads.mp_int(1)
     for wave_only in (False, True):
@@ -648,13 +648,35 @@ def run_exact_tree(a, n=1_000_000, steps=3):
                     ms.append((t1 - t0) * 1e3)
                 print("exact-tree %s %s step %d: %.2f ms" % ("wave" if wave_only else "traj", name, it, (t1 - t0) * 1e3),
                       file=sys.stderr, flush=True)
+            samples["%s_%s" % ("wave" if wave_only else "traj", name)] = _completion_sample(eng)
             eng.close()
             out["%s_%s" % ("wave" if wave_only else "traj", name)] = sum(ms) / len(ms)
     for p in ("traj", "wave"):
         out["%s_ratio" % p] = out["%s_exact" % p] / out["%s_flat" % p]
+        # the results checked: the duplicate key keeps the first position and the last value (MsgPackDocumentIndexer),
+        # so every exact-tree result is the structural merge's flat result with "step" 2 instead of 1
+        flat, exact = samples["%s_flat" % p], samples["%s_exact" % p]
+        assert len(exact) > 1000 and exact.keys() == flat.keys(), (p, len(exact), len(flat))
+        for k, pairs in flat.items():
+            assert exact[k] == [(a, 2 if a == "step" else b) for a, b in pairs], (p, k, exact[k], pairs)
+        out["%s_checked" % p] = len(exact)
     out["workload"] = ("C1, %d instances per tick, every job completion payload with a duplicate key (the exact tree "
                        "for each of the %d default output merges) vs a flat completion payload; stepping ms per tick, "
                        "trajectory path and general wave pipeline" % (n, n))
+    return out
+
+
+def _completion_sample(eng, m=30000):
+    """{workflow instance key: the process's final payload as (key, value) pairs} from the last m records of the tick
+    (the last generations: every instance's END_EVENT / process ELEMENT_COMPLETED carries its merge result)."""
+    import msgpack
+
+    L = eng.log_size()
+    out = {}
+    for r in eng.records(L - m, m):
+        v = msgpack.unpackb(r.value, raw=False)
+        if r.record_type == 0 and v.get("activityId") == "chain" and r.intent == 9:  # the process's ELEMENT_COMPLETED
+            out[v["workflowInstanceKey"]] = msgpack.unpackb(v["payload"], raw=False, object_pairs_hook=list)
     return out
 
 

@@ -58,7 +58,9 @@ def _documents(n, seed, ref, partner=None):
             d = enc(m)
             src, tgt = (d, partner[i]) if partner is not None else (DUP_JOB, d)
             out = ref(src, tgt)
-            if out is not None:
+            # (the engine reserves |source| + |target| + 8 bytes per result -- DESIGN.md §4 Exact payload tree: only id
+            # collisions that duplicate a subtree exceed it, and those fail the step with ZB_EUNSUPPORTED)
+            if out is not None and len(out) + 4 <= len(src) + len(tgt) + 8:
                 break
         docs.append(d)
         want.append(out)

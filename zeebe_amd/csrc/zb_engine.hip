@@ -222,6 +222,8 @@ struct zb_engine {
   uint4* t_wtot = nullptr;
   TrajBase* t_wbase = nullptr;
   TrajCtl* t_ctl = nullptr;
+  uint64_t* t_xq = nullptr;        // the template emit's exact-tree queue (TrajParams.xq), one entry per instance
+  uint64_t t_xq_cap = 0;
   MergeGen* t_mgen = nullptr;     // [TRAJ_MAX_GENERATIONS] uniform batch merge slots
   uint64_t* t_wstats = nullptr;   // [t_nwg_cap + CLS_MAX][6] emit statistics per workgroup
   TrajCtl* h_ctl_pinned = nullptr;
@@ -851,6 +853,16 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   p.xslab = e->xslab;
   p.xlocks = e->xlocks;
   p.xlane = e->xlane;
+  if (e->has_merges && e->xslab) {  // (a model that merges: refused pairs go to k_tmpl_xtree)
+    if ((uint64_t)n > e->t_xq_cap) {
+      if (e->t_xq) (void)hipFree(e->t_xq);
+      e->t_xq = nullptr;
+      e->t_xq_cap = 0;
+      HIPCHECK(e, hipMalloc(&e->t_xq, (uint64_t)n * sizeof(uint64_t)));
+      e->t_xq_cap = (uint64_t)n;
+    }
+    p.xq = e->t_xq;
+  }
   p.row_cap = e->cfg.row_capacity;
   p.arena_cap = e->arena_top;  // (the allocators' ceiling: staged documents above it)
   p.defer_ok = (e->tmpl_defer && e->seg_ok && e->d_vsegs.p && e->d_vconst.p && (p.cls || p.uni)) ? 1 : 0;
@@ -1559,7 +1571,7 @@ void zb_engine_destroy(zb_engine* e) {
                 e->c_scratch, e->c_bits, e->c_pop, e->c_off, e->c_count, e->x_keys, e->x_pos, e->x_keys2, e->x_pos2,
                 e->sort_tmp, e->d_spread, e->mapres, e->map_ws, e->log_mem, e->links_mem, e->srcd_mem, e->row_mem, e->arena, e->hdr, e->derr, e->dstats, e->derr_info,
                 e->merge_jobs, e->merge_slow, e->cond_jobs, e->job_counts, e->sub_jobs, e->cw, e->stage, e->info, e->block_agg, e->block_off, e->lookback,
-                e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats,
+                e->t_agg, e->t_woff, e->t_wcount, e->t_wtot, e->t_wbase, e->t_ctl, e->t_mgen, e->t_wstats, e->t_xq,
                 e->c_plan, e->c_ikey, e->c_clen, e->d_cref, e->c_khist, e->c_mask, e->c_cg, e->c_woffw, e->c_wgcnt, e->c_wgoff, e->c_perm,
                 e->t_tmpl, e->t_cstat, e->c_segs, e->c_wcls, e->raux, e->look_keys, e->look_idx,
                 e->conf_first, e->phase};

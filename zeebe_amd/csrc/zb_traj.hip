@@ -567,9 +567,12 @@ __device__ __forceinline__ void block_scan2(uint64_t& a, uint64_t& b, uint64_t& 
 // into the blob at arena byte offset at (capacity m_len): LDS-staged flat-map fast path; a non-flat
 // document sets TE_REGEN (first pass) or runs the general indexer / merger (GEN rerun).
 // PK_OUT / PK_IN != 0: packed layout (inputs back to back in PK_IN words, output blob of PK_OUT words)
+// tree (template emit): a pair the structural merge refuses is left to k_tmpl_xtree (*tree set, the blob unwritten)
+// instead of sending the batch to the wave pipeline (TE_XTREE)
 template <bool GEN, int PK_OUT = 0, int PK_IN = 0>
 __device__ __forceinline__ void merge_into(const TrajParams& P, uint32_t src, uint32_t tgt, uint32_t m_len, uint64_t at,
-                                           uint32_t* reg, uint32_t& err, uint32_t& ns, uint32_t& nt, uint32_t& olen) {
+                                           uint32_t* reg, uint32_t& err, uint32_t& ns, uint32_t& nt, uint32_t& olen,
+                                           bool* tree = nullptr) {
   constexpr bool PACKED = PK_OUT != 0;
   constexpr uint32_t OUT_BYTES = PACKED ? 4 * PK_OUT : FM_BYTES;
   constexpr uint32_t OUT_OFF = PACKED ? PK_IN : 2 * FM_WORDS;
@@ -603,11 +606,16 @@ __device__ __forceinline__ void merge_into(const TrajParams& P, uint32_t src, ui
       const bool ok = merge_docs((const uint8_t*)gs + 4, ns, (const uint8_t*)gt + 4, nt, o, unsup);
       olen = o.n;
       if (o.n > m_len) err |= DE_UNSUPPORTED;  // (never for a document merge_docs takes: as k_merge_gen)
-      // shapes the structural merge refuses: the exact tree (zb_xmerge.hpp) on the wave pipeline, where k_merge_gen
-      // runs a wave's refused merges with a lane workspace each (here a batch of 1M lanes would queue for the
-      // XLANE_GROUPS lane groups: 38 ms per 1M-instance tick against 14 ms there, profiles/r05/exact_tree_r05k.txt)
-      if (!ok || unsup) err |= TE_XTREE;
-      gd[0] = olen;
+      // shapes the structural merge refuses: the exact tree (zb_xmerge.hpp) -- in k_tmpl_xtree after the template
+      // emit (a grid of XLANE_COUNT lanes, one lane workspace each; in the emit itself a batch of 1M lanes would queue
+      // for the XLANE_GROUPS lane groups: 38 ms per 1M-instance tick, profiles/r05/exact_tree_r05k.txt), or, for the
+      // per-instance path, on the wave pipeline
+      if (!ok || unsup) {
+        if (tree) *tree = true;
+        else err |= TE_XTREE;
+      } else {
+        gd[0] = olen;
+      }
     } else {
       err |= TE_REGEN;
     }
@@ -1671,6 +1679,7 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
   uint32_t pc_len = create_len;
   uint32_t* reg = s_merge + threadIdx.x * TL::STRIDE;
   int64_t prev0 = P.log_base + inst;  // the instance's first record of the previous generation (the CREATE)
+  int xg = 0x7fffffff;  // the first generation whose merge k_tmpl_xtree finishes (every later merge of it too)
 
 #pragma unroll 1
   for (int w = 0; w < W; w++) {
@@ -1699,15 +1708,25 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
       const uint64_t at = tmpl_mslot(P, L, (uint32_t)w);
       merged_ref = (uint32_t)(at >> 3);
       merged_len = 0;
-      if (active) {
+      if (active && w > xg) {  // (a pending chain: k_tmpl_xtree merges it, in order)
+        merged_len = VLEN_UNKNOWN;
+      } else if (active) {
         const uint32_t m_len = arena_len(P.arena, src) + arena_len(P.arena, tgt) + 8;
         if (tblob_bytes(m_len) > g.stride) err |= DE_UNSUPPORTED;
         else if (at + g.stride > P.arena_cap) err |= DE_ARENA_FULL;
         else {
           uint32_t ns = 0, nt = 0, olen = 0;
-          merge_into<GEN, TL::OUT_WORDS, TL::IN_WORDS>(P, src, tgt, m_len, at, reg, err, ns, nt, olen);
-          merge_bytes += ns + nt + olen;
-          merged_len = olen;
+          bool tree = false;
+          merge_into<GEN, TL::OUT_WORDS, TL::IN_WORDS>(P, src, tgt, m_len, at, reg, err, ns, nt, olen,
+                                                        P.xq ? &tree : nullptr);
+          if (tree) {
+            xg = w;
+            merged_len = VLEN_UNKNOWN;
+            P.xq[atomicAdd(&ctl->xq_n, 1u)] = (uint64_t)inst | (uint64_t)w << 40;
+          } else {
+            merge_bytes += ns + nt + olen;
+            merged_len = olen;
+          }
         }
       }
     }
@@ -1724,7 +1743,8 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
       else if (pay == PAY_CREATE) { pay = create_ref; plen = create_len; }
       else if (pay & PAY_MERGE) {
         const uint32_t r = (uint32_t)(tmpl_mslot(P, L, pay & 0xffff) >> 3);
-        plen = active ? arena_len(P.arena, r) : 0;
+        const bool pend = (int)(pay & 0xffff) >= xg;  // (k_tmpl_xtree writes it: no length yet)
+        plen = (active && !pend) ? arena_len(P.arena, r) : (pend ? VLEN_UNKNOWN : 0);
         pc_sym = pay;
         pc_ref = r;
         pc_len = plen;
@@ -1740,10 +1760,11 @@ __global__ void __launch_bounds__(TWG) k_tmpl(TrajParams P) {
           P.log[pos0 + k] = d;
           P.srcd[pos0 + k] = (uint32_t)(pos0 + k - (prev0 + t.pad[0]));
           // the value's length (zb_serialize.hip encode_value) from the element's constants and the variable fields
+          // (a pending merge result's length is not known yet: the drain's size pass measures it)
           const uint8_t vt = kind_vt(d.kind), rt = kind_rt(d.kind);
           uint32_t vl = VLEN_UNKNOWN;
-          if (!(d.kind & KIND_RAW) && ((vt == ZB_VT_WORKFLOW_INSTANCE && rt == ZB_RT_EVENT) ||
-                                       (vt == ZB_VT_JOB && (d.intent | 1) != JI_CANCELED))) {
+          if (plen != VLEN_UNKNOWN && !(d.kind & KIND_RAW) && ((vt == ZB_VT_WORKFLOW_INSTANCE && rt == ZB_RT_EVENT) ||
+                                                              (vt == ZB_VT_JOB && (d.intent | 1) != JI_CANCELED))) {
             const ValueConst vc = kload(P.vconst, (uint64_t)d.elem);
             vl = (vt == ZB_VT_JOB ? vc.job : vc.wf) + mp_int_len(d.inst_key) + mp_int_len(d.scope_key) + mp_bin_len(plen);
           }
@@ -1813,6 +1834,7 @@ __global__ void __launch_bounds__(TWG) k_tmpl_io(TrajParams P) {
   uint32_t* s_srcd = (uint32_t*)(stage + 64 * TF * 32);
   uint32_t* s_vlen = s_srcd + 64 * TF;
   int64_t prev0 = P.log_base + inst;  // the instance's first record of the previous generation (the CREATE)
+  int xg = 0x7fffffff;  // the first generation whose merge k_tmpl_xtree finishes (every later merge of it too)
 
 #pragma unroll 1
   for (int w = 0; w < Wmax; w++) {
@@ -1840,14 +1862,26 @@ __global__ void __launch_bounds__(TWG) k_tmpl_io(TrajParams P) {
       else if (tgt & PAY_MERGE) tgt = (uint32_t)(tmpl_mslot(P, L, tgt & 0xffff) >> 3);
       const uint64_t at = tmpl_mslot(P, L, (uint32_t)w);
       merged_ref = (uint32_t)(at >> 3);
-      const uint32_t m_len = arena_len(P.arena, src) + arena_len(P.arena, tgt) + 8;
-      if (tblob_bytes(m_len) > g.stride) err |= DE_UNSUPPORTED;
-      else if (at + g.stride > P.arena_cap) err |= DE_ARENA_FULL;
-      else {
-        uint32_t ns = 0, nt = 0, olen = 0;
-        merge_into<GEN, TL::OUT_WORDS, TL::IN_WORDS>(P, src, tgt, m_len, at, reg, err, ns, nt, olen);
-        merge_bytes += ns + nt + olen;
-        merged_len = olen;
+      if (w > xg) {  // (a pending chain: k_tmpl_xtree merges it, in order)
+        merged_len = VLEN_UNKNOWN;
+      } else {
+        const uint32_t m_len = arena_len(P.arena, src) + arena_len(P.arena, tgt) + 8;
+        if (tblob_bytes(m_len) > g.stride) err |= DE_UNSUPPORTED;
+        else if (at + g.stride > P.arena_cap) err |= DE_ARENA_FULL;
+        else {
+          uint32_t ns = 0, nt = 0, olen = 0;
+          bool tree = false;
+          merge_into<GEN, TL::OUT_WORDS, TL::IN_WORDS>(P, src, tgt, m_len, at, reg, err, ns, nt, olen,
+                                                        P.xq ? &tree : nullptr);
+          if (tree) {
+            xg = w;
+            merged_len = VLEN_UNKNOWN;
+            P.xq[atomicAdd(&ctl->xq_n, 1u)] = (uint64_t)inst | (uint64_t)w << 40;
+          } else {
+            merge_bytes += ns + nt + olen;
+            merged_len = olen;
+          }
+        }
       }
     }
     // the wave's range of this generation: [base, base + span)
@@ -1868,7 +1902,7 @@ __global__ void __launch_bounds__(TWG) k_tmpl_io(TrajParams P) {
       else if (pay == PAY_CREATE) { pay = create_ref; plen = create_len; }
       else if (pay & PAY_MERGE) {
         const uint32_t r = (uint32_t)(tmpl_mslot(P, L, pay & 0xffff) >> 3);
-        plen = arena_len(P.arena, r);
+        plen = (int)(pay & 0xffff) >= xg ? VLEN_UNKNOWN : arena_len(P.arena, r);  // (pending: k_tmpl_xtree writes it)
         pc_sym = pay;
         pc_ref = r;
         pc_len = plen;
@@ -1880,10 +1914,11 @@ __global__ void __launch_bounds__(TWG) k_tmpl_io(TrajParams P) {
       d.payload = pay;
       d.elem = t.elem; d.intent = t.intent; d.kind = t.kind;
       // the value's length (zb_serialize.hip encode_value) from the element's constants and the variable fields
+      // (a pending merge result's length is not known yet: the drain's size pass measures it)
       const uint8_t vt = kind_vt(d.kind), rt = kind_rt(d.kind);
       uint32_t vl = VLEN_UNKNOWN;
-      if (!(d.kind & KIND_RAW) && ((vt == ZB_VT_WORKFLOW_INSTANCE && rt == ZB_RT_EVENT) ||
-                                   (vt == ZB_VT_JOB && (d.intent | 1) != JI_CANCELED))) {
+      if (plen != VLEN_UNKNOWN && !(d.kind & KIND_RAW) && ((vt == ZB_VT_WORKFLOW_INSTANCE && rt == ZB_RT_EVENT) ||
+                                                          (vt == ZB_VT_JOB && (d.intent | 1) != JI_CANCELED))) {
         const ValueConst vc = kload(P.vconst, (uint64_t)d.elem);
         vl = (vt == ZB_VT_JOB ? vc.job : vc.wf) + mp_int_len(d.inst_key) + mp_int_len(d.scope_key) + mp_bin_len(plen);
       }
@@ -1920,6 +1955,106 @@ __global__ void __launch_bounds__(TWG) k_tmpl_io(TrajParams P) {
   if (err & TE_XTREE) atomicOr(&ctl->flag, TE_FALLBACK);  // (nothing commits: the wave pipeline runs the batch)
   const uint32_t derr = err & ~(uint32_t)(TE_FALLBACK | TE_REGEN | TE_XTREE);
   if (derr) atomicOr(&ctl->derr, derr);
+}
+
+// The exact tree for the merge chains the template emit left (zb_xmerge.hpp; as k_merge_gen on the wave pipeline): the
+// GEN pass queued every instance whose merge the structural merge refused (P.xq: instance | first generation << 40)
+// and wrote its descriptors with the merge slots' refs. Here each queued instance runs its merges from that generation
+// on, in generation order (a later merge may read an earlier one's result): the structural merge first, the exact tree
+// where it refuses (MsgPackDocumentIndexer.java:136-283, MsgPackTree.java:141-166). One lane per queued instance over a
+// grid of XLANE_COUNT lanes, so each wave holds one lane group of workspaces at a time (x_run, wave-uniform calls).
+template <bool CLS>
+__global__ void __launch_bounds__(256) k_tmpl_xtree(TrajParams P) {
+  __shared__ unsigned long long s_b[4];
+  const TrajCtl* ctl = P.ctl;
+  if (ctl->flag) return;
+  const uint32_t n = ctl->xq_n;
+  if (n == 0) return;
+  uint32_t err = 0;
+  unsigned long long bytes = 0;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t rounds = (n + stride - 1) / stride;  // (every lane of a wave walks the same rounds)
+  for (uint32_t rd = 0; rd < rounds; rd++) {
+    const uint32_t q = rd * stride + blockIdx.x * blockDim.x + threadIdx.x;
+    const bool act = q < n;
+    const uint64_t ent = act ? P.xq[q] : 0;
+    const int64_t inst = (int64_t)(ent & ((1ull << 40) - 1));
+    const int xg = (int)(ent >> 40);
+    TmplLane L;
+    uint32_t cls = 0;
+    if (CLS) {
+      L.ncls = __builtin_amdgcn_readfirstlane(P.plan->nc);
+      cls = tmpl_lane_io(P, inst, L);
+    } else {
+      L.ncls = 1;
+#pragma unroll
+      for (int c = 0; c < CLS_MAX; c++) L.before[c] = c == 0 ? (uint32_t)inst : 0;
+    }
+    const int W = act ? (int)P.wcount[cls] : 0;
+    int Wmax = W;
+    for (int d = 32; d >= 1; d >>= 1) Wmax = max(Wmax, __shfl_xor(Wmax, d, 64));
+    const uint32_t create_ref = act ? P.log[P.log_base + inst].payload : 0u;
+    for (int w = 0; w < Wmax; w++) {
+      const MergeGen g = (act && w >= xg && w < W) ? P.mgen[(uint64_t)cls * CLS_ROW + w] : MergeGen{};
+      bool need = false;
+      const uint8_t *sp = nullptr, *tp = nullptr;
+      uint8_t* dst = nullptr;
+      uint32_t ns = 0, nt = 0, cap = 0, olen = 0;
+      if (g.has) {
+        uint32_t src = g.src, tgt = g.tgt;  // (resolved as the emit does: its pc_sym cache names the same refs)
+        if (src == PAY_CREATE) src = create_ref;
+        else if (src & PAY_MERGE) src = (uint32_t)(tmpl_mslot(P, L, src & 0xffff) >> 3);
+        if (tgt == PAY_CREATE) tgt = create_ref;
+        else if (tgt & PAY_MERGE) tgt = (uint32_t)(tmpl_mslot(P, L, tgt & 0xffff) >> 3);
+        sp = P.arena + (uint64_t)src * 8;
+        tp = P.arena + (uint64_t)tgt * 8;
+        ns = *(const uint32_t*)sp;
+        nt = *(const uint32_t*)tp;
+        cap = ns + nt + 8;
+        const uint64_t at = tmpl_mslot(P, L, (uint32_t)w);
+        dst = P.arena + at;
+        if (tblob_bytes(cap) > g.stride) {
+          err |= DE_UNSUPPORTED;
+        } else if (at + g.stride > P.arena_cap) {
+          err |= DE_ARENA_FULL;
+        } else {
+          Out o{dst + 4, 0};
+          bool unsup = false;
+          const bool ok = merge_docs(sp + 4, ns, tp + 4, nt, o, unsup);
+          olen = o.n;
+          if (o.n > cap) err |= DE_UNSUPPORTED;
+          need = (!ok || unsup) && o.n <= cap;
+          if (!need && o.n <= cap) {
+            *(uint32_t*)dst = olen;
+            bytes += ns + nt + olen;
+          }
+        }
+      }
+      x_run(XSlabs{P.xslab, P.xlocks, P.xlane}, need, [&](uint8_t* slab, uint32_t sb, bool fin) {
+        Out o{dst + 4, 0};
+        const int st = x_merge(slab, sb, sp + 4, ns, tp + 4, nt, o, cap);
+        if (st == X_UNSUP && !fin) return st;
+        if (st == X_OK) {
+          if (o.n == 1 && dst[4] == 0xc0) dst[4] = 0x80;  // an empty tree: DocumentValue.wrap turns nil into {}
+          olen = o.n;
+        } else {
+          // X_NOT_MAP (a non-map root) would be an incident, which a merge already emitted cannot become
+          err |= st == X_FAIL ? DE_BAD_PAYLOAD : DE_UNSUPPORTED;
+        }
+        return st;
+      });
+      if (need) {
+        *(uint32_t*)dst = olen;
+        bytes += ns + nt + olen;
+      }
+    }
+  }
+  if (err) atomicOr(P.err, err);
+  for (int d = 32; d >= 1; d >>= 1) bytes += __shfl_down(bytes, d, 64);
+  if ((threadIdx.x & 63) == 0) s_b[threadIdx.x >> 6] = bytes;
+  __syncthreads();
+  if (threadIdx.x == 0 && (s_b[0] | s_b[1] | s_b[2] | s_b[3]))
+    atomicAdd((unsigned long long*)P.stats + 4, s_b[0] + s_b[1] + s_b[2] + s_b[3]);  // merge bytes
 }
 
 // conditions are compiled into the count / emit kernels only when the model has exclusive splits
@@ -1990,6 +2125,10 @@ void launch_traj_emit(const TrajParams& p, hipStream_t s, hipEvent_t* ev_main) {
     hipLaunchKernelGGL((k_traj<true, false, false, true, false, false>), g, b, 0, s, p);
   }
   if (!p.materialize) hipLaunchKernelGGL(k_traj_commit, dim3(1), dim3(256), 0, s, p);
+  if (p.xq && (p.uni || p.cls) && !p.materialize) {  // the merge chains the template emit queued for the exact tree (none: exits at once)
+    if (p.cls) hipLaunchKernelGGL(k_tmpl_xtree<true>, dim3(XLANE_COUNT / 256), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(k_tmpl_xtree<false>, dim3(XLANE_COUNT / 256), dim3(256), 0, s, p);
+  }
 }
 
 }  // namespace zbg
