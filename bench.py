@@ -38,7 +38,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 BYTES_PER_TRANSITION = 96  # 32 B row read + 32 B row write + 32 B record descriptor
 DESC_BYTES = 32  # one zb_rec descriptor per log record
 HDR_BYTES = 24  # one zb_record_header per drained record
-PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r05", "r04", "r03")]  # newest first
+PMC_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r06", "r05", "r04", "r03")]  # newest first
 METRIC = "BPMN element transitions/sec (+ completed instances/sec) per node; % HBM roofline"
 
 
@@ -56,9 +56,11 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="skip the extra C2 wave-only / C4 lines")
     ap.add_argument("--no-drain", action="store_true", help="device stepping only (not the contract's step)")
     ap.add_argument("--wave-only", action="store_true", help="force the general wave pipeline (no trajectory path)")
-    ap.add_argument("--jobs", choices=("harness", "external", "processor"), default="harness",
+    ap.add_argument("--jobs", choices=("harness", "external", "processor"), default=None,
                     help="job mode: the canonical in-kernel harness, ZB_CFG_EXTERNAL_JOBS or ZB_CFG_JOB_PROCESSOR (the "
-                         "modes INTEGRATION.md binds)")
+                         "modes INTEGRATION.md binds). Default: external for C3 (no service task: the integration's "
+                         "configuration), the harness for the configurations with service tasks (their bench ticks "
+                         "complete jobs in-kernel)")
     ap.add_argument("--frames", action="store_true",
                     help="drain log frames (zb_serialize_frames, with request metadata on every CREATE) instead of "
                          "values + headers")
@@ -67,7 +69,12 @@ def parse():
                          "creates and cancels, external job processor")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on GPU 0 (multi-rank rehearsal on a one-GPU box; not a scaling run)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.jobs is None:
+        a.jobs = "external" if a.config == "c3" else "harness"
+    if a.jobs != "harness" and a.config != "c3":
+        ap.error("--jobs %s: only C3 (no service task) runs a tick to quiescence without a job processor" % a.jobs)
+    return a
 
 
 # ------------------------------------------------------------------------------ workloads
@@ -112,7 +119,7 @@ def make_engine(cfg, n, a, rank, world, local_rank):
     # row per live element instance: C3 wave-only needs the process + gateway / task rows of every instance)
     rows = {"c1": n * 3, "c2": n * (a.tasks + 2), "c3": n * 3 if a.wave_only else 1 << 20, "c4": n * 20}[cfg]
     arena = {"c1": n * 96, "c2": n * (48 + 48 * a.tasks), "c3": n * 64, "c4": n * 1200}[cfg] + (64 << 20)
-    jobs = getattr(a, "jobs", "harness")
+    jobs = getattr(a, "jobs", "harness") if cfg == "c3" else "harness"  # (service tasks: the in-kernel harness)
     return Engine(device=0 if a.same_device else local_rank, partition_id=rank, partition_count=world,
                   log_capacity=int(n * recs), row_capacity=int(rows), arena_bytes=int(arena), wave_only=a.wave_only,
                   external_jobs=jobs == "external", job_processor=jobs == "processor")
@@ -190,7 +197,9 @@ def run_workload(cfg, n, a, rank, world, local_rank, barrier, steps, warmup, dra
     tot["desc"] = desc
     tot["create_bytes"] = create_bytes
     tot["frames"] = frames
-    tot["jobs"] = getattr(a, "jobs", "harness")
+    tot["jobs"] = getattr(a, "jobs", "harness") if cfg == "c3" else "harness"
+    tot["desc"] += {"harness": ", canonical job harness", "external": ", ZB_CFG_EXTERNAL_JOBS (the integration's job mode)",
+                    "processor": ", ZB_CFG_JOB_PROCESSOR"}[tot["jobs"]] if cfg == "c3" else ""
     if pcie and drain:
         tot["pcie"] = pcie_step(eng, n, one_step)
     eng.close()
