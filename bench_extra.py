@@ -147,5 +147,9 @@ def run_c5(a, rank, world, local_rank, dist, barrier, reduce_max, reduce_sum):
                                            "FETCH_SIZE x2 + WRITE_SIZE (%s)" % os.path.relpath(_pmc_file("c5_%d" % n),
                                                                                                  ROOT))
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline_c5(8 if a.cpu_partitions == 0 else a.cpu_partitions, a.cpu_sample or 8000)
+        # the shape of this line (one partition, its outbox delivered to its own inbox) on one core, and the node's
+        # shape (P partitions exchanging, one core each) beside it
+        one = cpu_baseline_c5(1, a.cpu_sample or 8000)
+        one["multi_partition"] = cpu_baseline_c5(8 if a.cpu_partitions == 0 else a.cpu_partitions, a.cpu_sample or 8000)
+        out["cpu_baseline"] = one
     _emit(out, rank)
