@@ -21,6 +21,14 @@ static inline double __longlong_as_double(long long u) { double d; std::memcpy(&
 
 using namespace zbg;
 
+// the exact tree's string chunks read up to 7 bytes past a document (the device arena keeps ARENA_SLACK readable bytes
+// past its end): documents from Python are copied into padded buffers
+static std::vector<uint8_t> padded(const uint8_t* p, uint32_t n) {
+  std::vector<uint8_t> v(n + 64, 0);
+  if (n) std::memcpy(v.data(), p, n);
+  return v;
+}
+
 extern "C" {
 // returns length, -1 malformed, -2 unsupported
 long devlib_merge(const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint32_t nt, uint8_t* out, uint32_t cap) {
@@ -138,8 +146,10 @@ long devlib_read_token(const uint8_t* p, uint32_t n, int64_t* ival, double* fval
 // extracted by mappings (mode 1: MsgPackDocumentExtractor.extract, spec as devlib_map_text) -- dumped as one line per
 // typed node: type (M map, A array, L existing leaf, X extracted leaf), NUL, id, NUL, children joined by 0x1e in
 // insertion order, NUL, leaf bytes (hex; empty: no leaf), '\n'. Returns the dump length, or -(100 + X_* status).
-long devlib_xtree_dump(const uint8_t* doc, uint32_t n, const char* spec, int mode, char* out, uint32_t cap) {
+long devlib_xtree_dump(const uint8_t* doc0, uint32_t n, const char* spec, int mode, char* out, uint32_t cap) {
   static uint8_t slab[XSLAB_BYTES];
+  const std::vector<uint8_t> dv = padded(doc0, n);
+  const uint8_t* doc = dv.data();
   XTree T;
   int st;
   if (mode == 0) {
@@ -186,9 +196,12 @@ long devlib_xtree_dump(const uint8_t* doc, uint32_t n, const char* spec, int mod
 }
 // the exact tree (zb_xmerge.hpp): x_merge, or x_map over the product's compiled mappings (spec as devlib_map_text,
 // empty spec = merge). Returns the output length, or -(100 + X_* status) (fail_query in *fq), -20 compile error.
-long devlib_xmerge(const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint32_t nt, const char* spec, int extract,
+long devlib_xmerge(const uint8_t* src0, uint32_t ns, const uint8_t* tgt0, uint32_t nt, const char* spec, int extract,
                    uint8_t* out, uint32_t cap, uint32_t* fq, char* err, uint32_t errcap) {
   static uint8_t slab[XSLAB_BYTES];
+  const std::vector<uint8_t> sv = padded(src0, ns), tv = padded(tgt0, nt);
+  const uint8_t* src = sv.data();
+  const uint8_t* tgt = tv.data();
   ModelTables t;
   std::string sp(spec), e;
   size_t p = 0;

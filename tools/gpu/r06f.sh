@@ -1,0 +1,9 @@
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+O=gpurun_out/r06f
+mkdir -p $O
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 -u tools/gpu/exact_line.py > $O/exact.json 2> $O/exact.err || { echo "prof failed"; tail -5 $O/exact.err; exit 1; }
+f=$(find $O/prof -name '*kernel_stats.csv' | head -1); cp $f $O/kernel_stats_exact.csv
+timeout -s KILL 200 rocprofv3 --pmc TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum --kernel-trace -d $O/pmc -o run --output-format csv -- python3 -u tools/gpu/exact_line.py > $O/exact_pmc.json 2> $O/exact_pmc.err || { echo "pmc failed"; tail -5 $O/exact_pmc.err; exit 1; }
+echo done

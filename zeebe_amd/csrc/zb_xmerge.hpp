@@ -23,6 +23,7 @@ namespace zbg {
 
 constexpr uint32_t XSLAB_BYTES = 4u << 20;  // workspace of one document pair
 constexpr uint32_t XSLAB_COUNT = 32;        // pairs in flight (zb_xlock.hpp: one lock per slab)
+constexpr uint32_t XPOOL_SLACK = 16;        // bytes past a workspace's string pool its 8-byte string chunks may touch
 // every lane first tries its pair in a small workspace of its own (XLANE_COUNT of them, held 64 at a time by a wave:
 // zb_xlock.hpp x_run): 32 KB holds the tree of ~140 tokens (2 x source + target), the documents of a typical job /
 // message payload merge
@@ -109,9 +110,14 @@ struct XTree {
     hc = (uint32_t*)take((uint64_t)h * sizeof(uint32_t));
     nn_cap = nc_cap = st_cap = n;
     ht_mask = hc_mask = h - 1;
-    for (uint32_t i = 0; i < h; i++) { ht[i] = 0; hc[i] = 0; }
+    // both tables cleared with 16-byte stores (adjacent, 16-aligned, h a multiple of 4): in the kernels every store
+    // of a lane is a request of its own (the lanes' workspaces are 32 KB apart), and a byte-wise clear was a quarter
+    // of a small merge's requests
+    struct alignas(16) Q { uint64_t a, b; };
+    for (uint32_t i = 0; i < 2 * h; i += 4) *(Q*)(ht + i) = Q{0, 0};
     pool = p;
-    pool_cap = (uint32_t)(slab + bytes - p);
+    // (XPOOL_SLACK bytes kept free past the pool: the string helpers read and write whole 8-byte chunks)
+    pool_cap = (uint32_t)(slab + bytes - p) - XPOOL_SLACK;
     pool_n = 0;
     nn = nc = 0;
     n_par = n_arr = n_typ = 0;
@@ -120,7 +126,18 @@ struct XTree {
     return status == X_OK;
   }
 
-  // ---- strings
+  // ---- strings, 8 bytes at a time (unaligned 8-byte accesses: a byte loop was one memory request per byte). A chunk
+  // may read up to 7 bytes past a string (inside the pool's slack, or past a document: the arena keeps ARENA_SLACK
+  // readable bytes) and a copy may write up to 7 bytes past it (free pool space above the top, overwritten later)
+  ZB_HD static uint64_t ld8(const uint8_t* p) {
+    uint64_t v;
+    __builtin_memcpy(&v, p, 8);
+    return v;
+  }
+  ZB_HD static void st8(uint8_t* p, uint64_t v) { __builtin_memcpy(p, &v, 8); }
+  ZB_HD static void copy8(uint8_t* d, const uint8_t* s, uint32_t n) {
+    for (uint32_t i = 0; i < n; i += 8) st8(d + i, ld8(s + i));
+  }
   ZB_HD XStr str_new(uint32_t len) {
     XStr r{pool_n, len};
     if ((uint64_t)pool_n + len > pool_cap) { status = X_UNSUP; r.len = 0; return r; }
@@ -129,18 +146,17 @@ struct XTree {
   }
   ZB_HD XStr str_from(const uint8_t* p, uint32_t len) {
     XStr r = str_new(len);
-    if (status == X_OK)
-      for (uint32_t i = 0; i < len; i++) pool[r.off + i] = p[i];
+    if (status == X_OK) copy8(pool + r.off, p, len);
     return r;
   }
-  // MsgPackTreeNodeIdConstructor.construct: parent + "[" + name + "]"
+  // MsgPackTreeNodeIdConstructor.construct: parent + "[" + name + "]" (at the pool's top: above both sources)
   ZB_HD XStr cat(XStr parent, XStr name) {
     XStr r = str_new(parent.len + name.len + 2);
     if (status != X_OK) return r;
     uint8_t* d = pool + r.off;
-    for (uint32_t i = 0; i < parent.len; i++) d[i] = pool[parent.off + i];
+    copy8(d, pool + parent.off, parent.len);
     d[parent.len] = '[';
-    for (uint32_t i = 0; i < name.len; i++) d[parent.len + 1 + i] = pool[name.off + i];
+    copy8(d + parent.len + 1, pool + name.off, name.len);
     d[parent.len + 1 + name.len] = ']';
     return r;
   }
@@ -155,13 +171,20 @@ struct XTree {
   }
   ZB_HD bool eq(XStr a, XStr b) const {
     if (a.len != b.len) return false;
-    for (uint32_t i = 0; i < a.len; i++)
-      if (pool[a.off + i] != pool[b.off + i]) return false;
+    for (uint32_t i = 0; i < a.len; i += 8) {
+      uint64_t x = ld8(pool + a.off + i) ^ ld8(pool + b.off + i);
+      if (a.len - i < 8) x &= ~0ull >> (64 - 8 * (a.len - i));
+      if (x) return false;
+    }
     return true;
   }
   ZB_HD uint32_t hash(XStr a, uint32_t seed) const {  // FNV-1a
     uint32_t h = 2166136261u ^ (seed * 0x9e3779b9u);
-    for (uint32_t i = 0; i < a.len; i++) h = (h ^ pool[a.off + i]) * 16777619u;
+    for (uint32_t i = 0; i < a.len; i += 8) {
+      uint64_t w = ld8(pool + a.off + i);
+      const uint32_t m = a.len - i < 8 ? a.len - i : 8;
+      for (uint32_t k = 0; k < m; k++, w >>= 8) h = (h ^ (uint32_t)(w & 0xff)) * 16777619u;
+    }
     return h;
   }
 
