@@ -77,6 +77,19 @@ __host__ __device__ __forceinline__ int64_t frame_request_pos(int64_t pos, int64
   return -1;
 }
 
+// the 13 prefix words into an LDS image at an 8-aligned offset: six 16-byte stores and one 8-byte store, without a
+// divergent branch on the offset's alignment (the odd word is the first when the offset is 8 mod 16, else the last)
+__device__ __forceinline__ void frame_store_lds(uint8_t* img, uint32_t at, const uint64_t (&h)[13]) {
+  const bool o = (at & 8) != 0;
+  *(uint64_t*)(img + at + (o ? 0u : 96u)) = o ? h[0] : h[12];
+  uint4* q = (uint4*)(img + at + (o ? 8u : 0u));
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    const uint64_t a = o ? h[1 + 2 * j] : h[2 * j], b = o ? h[2 + 2 * j] : h[2 * j + 1];
+    q[j] = uint4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+  }
+}
+
 // request metadata of the record at pos whose request is the command at q (q < 0: none) in a sorted table
 __device__ __forceinline__ void frame_request(const ReqMeta* reqs, int64_t nreqs, int64_t q, uint64_t& rid, uint32_t& sid) {
   rid = ~0ull;

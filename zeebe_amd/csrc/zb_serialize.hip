@@ -883,9 +883,7 @@ __global__ void __launch_bounds__(SER_WG) __attribute__((amdgpu_waves_per_eu(3, 
         uint64_t h[13];
         frame_words(h, FrameConst{P0.stream_id, P0.raft_term, P0.timestamp}, FRAME_PREFIX + vn, fflags,
                     P0.start + i, frame_producer(src, vt, rt, d.intent), src, d.key, rt, vt, d.intent, 255, 0, rid, sid);
-        uint64_t* hd = (uint64_t*)(img + at);
-#pragma unroll
-        for (int j = 0; j < 13; j++) hd[j] = h[j];
+        frame_store_lds(img, at, h);
       }
     }
     const uint32_t hi = __builtin_amdgcn_readlane(incl, b - 1);

@@ -565,9 +565,7 @@ __global__ void __launch_bounds__(TD_WG) __attribute__((amdgpu_waves_per_eu(3, 4
               frame_words(h, fcst, FRAME_PREFIX + vl, frame_flags(k == 0 || !pair, k == 1 || !pair), G.pos0 + k,
                           frame_producer(src, vt, rt, d.intent), src, d.key, rt, vt, d.intent, 255, 0,
                           req ? rid : ~0ull, req ? sid : 0x80000000u);
-              uint64_t* hd = (uint64_t*)(img + at);
-#pragma unroll
-              for (int j = 0; j < 13; j++) hd[j] = h[j];
+              frame_store_lds(img, at, h);
             }
           }
         }
