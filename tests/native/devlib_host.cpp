@@ -153,7 +153,7 @@ long devlib_xtree_dump(const uint8_t* doc0, uint32_t n, const char* spec, int mo
   XTree T;
   int st;
   if (mode == 0) {
-    if (!T.init(slab, XSLAB_BYTES, x_tokens(doc, n))) return -(100 + T.status);
+    if (!T.init(XWs{slab, XSLAB_BYTES, 0, 1}, x_tokens(doc, n))) return -(100 + T.status);
     T.index(0, doc, n, false);
     st = T.status;
   } else {
@@ -168,7 +168,7 @@ long devlib_xtree_dump(const uint8_t* doc0, uint32_t n, const char* spec, int mo
     }
     if (t.pool.empty()) t.pool.push_back(0);
     uint16_t q = 0xffff;
-    st = x_map_tree(T, slab, XSLAB_BYTES, doc, n, nullptr, 0, t.maps.data(), (uint32_t)t.maps.size(), t.segs.data(),
+    st = x_map_tree(T, XWs{slab, XSLAB_BYTES, 0, 1}, doc, n, nullptr, 0, t.maps.data(), (uint32_t)t.maps.size(), t.segs.data(),
                     t.queries.data(), t.filters.data(), t.pool.data(), q);
   }
   if (st != X_OK) return -(100 + st);
@@ -196,9 +196,14 @@ long devlib_xtree_dump(const uint8_t* doc0, uint32_t n, const char* spec, int mo
 }
 // the exact tree (zb_xmerge.hpp): x_merge, or x_map over the product's compiled mappings (spec as devlib_map_text,
 // empty spec = merge). Returns the output length, or -(100 + X_* status) (fail_query in *fq), -20 compile error.
+// lane < 0: one slab of its own (the kernels' big slabs); lane 0..63: lane `lane` of an interleaved group of 64
+// XLANE_BYTES workspaces (the kernels' lane workspaces, zb_xlock.hpp x_run) -- X_UNSUP when the pair does not fit it
 long devlib_xmerge(const uint8_t* src0, uint32_t ns, const uint8_t* tgt0, uint32_t nt, const char* spec, int extract,
-                   uint8_t* out, uint32_t cap, uint32_t* fq, char* err, uint32_t errcap) {
+                   uint8_t* out, uint32_t cap, uint32_t* fq, char* err, uint32_t errcap, int lane) {
   static uint8_t slab[XSLAB_BYTES];
+  static std::vector<uint8_t> group;
+  if (lane >= 0 && group.empty()) group.assign((size_t)64 * XLANE_BYTES, 0xA5);
+  const XWs ws = lane < 0 ? XWs{slab, XSLAB_BYTES, 0, 1} : XWs{group.data(), XLANE_BYTES, (uint32_t)lane, 64};
   const std::vector<uint8_t> sv = padded(src0, ns), tv = padded(tgt0, nt);
   const uint8_t* src = sv.data();
   const uint8_t* tgt = tv.data();
@@ -219,9 +224,9 @@ long devlib_xmerge(const uint8_t* src0, uint32_t ns, const uint8_t* tgt0, uint32
   uint16_t q = 0xffff;
   int st;
   if (t.maps.empty())
-    st = x_merge(slab, XSLAB_BYTES, src, ns, tgt, nt, o, cap);
+    st = x_merge(ws, src, ns, tgt, nt, o, cap);
   else
-    st = x_map(slab, XSLAB_BYTES, src, ns, extract ? nullptr : tgt, nt, t.maps.data(), (uint32_t)t.maps.size(),
+    st = x_map(ws, src, ns, extract ? nullptr : tgt, nt, t.maps.data(), (uint32_t)t.maps.size(),
                t.segs.data(), t.queries.data(), t.filters.data(), t.pool.data(), o, cap, q);
   *fq = q;
   if (st != X_OK) return -(100 + st);

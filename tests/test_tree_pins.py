@@ -86,5 +86,5 @@ def test_tree_writer_round_trip(vectors, devlib):  # noqa: F811
         out = ctypes.create_string_buffer(1 << 16)
         fq, err = ctypes.c_uint32(), ctypes.create_string_buffer(256)
         devlib.devlib_xmerge.restype = ctypes.c_long
-        n = devlib.devlib_xmerge(doc, len(doc), b"", 0, b"", 0, out, 1 << 16, ctypes.byref(fq), err, 256)
+        n = devlib.devlib_xmerge(doc, len(doc), b"", 0, b"", 0, out, 1 << 16, ctypes.byref(fq), err, 256, -1)
         assert n == len(doc) and out.raw[:n] == ref

@@ -35,7 +35,7 @@ def L():
     lib.devlib_xmerge.restype = ctypes.c_long
     lib.devlib_xmerge.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                   ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
-                                  ctypes.c_char_p, ctypes.c_uint32]
+                                  ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int]
     lib.devlib_merge.restype = ctypes.c_long
     lib.devlib_merge.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p,
                                  ctypes.c_uint32]
@@ -122,11 +122,13 @@ def oracle_map(src, mappings, tgt):
         return "fail"
 
 
-def x_run(L, src, tgt, spec=b"", extract=False, cap=1 << 22):
+def x_run(L, src, tgt, spec=b"", extract=False, cap=1 << 22, lane=-1):
+    """lane -1: a slab of its own; 0..63: that lane of an interleaved group of 64 lane workspaces (zb_xlock.hpp)."""
     out = ctypes.create_string_buffer(cap)
     fq = ctypes.c_uint32(0)
     err = ctypes.create_string_buffer(512)
-    n = L.devlib_xmerge(src, len(src), tgt, len(tgt), spec, 1 if extract else 0, out, cap, ctypes.byref(fq), err, 512)
+    n = L.devlib_xmerge(src, len(src), tgt, len(tgt), spec, 1 if extract else 0, out, cap, ctypes.byref(fq), err, 512,
+                        lane)
     if n < 0:
         return X_STATUS.get(-n, n)
     return out.raw[:n]
@@ -145,6 +147,28 @@ def test_xmerge_odd_documents_vs_oracle(L):
         assert got == ref, (sb.hex(), tb.hex(), got, ref)
         kinds[ref if isinstance(ref, str) else "ok"] = kinds.get(ref if isinstance(ref, str) else "ok", 0) + 1
     assert kinds["ok"] > 3000 and kinds.get("fail", 0) > 20, kinds
+
+
+def test_xmerge_lane_workspaces_vs_oracle(L):
+    """The kernels' lane workspaces: the tree's arrays interleaved over a group of 64 lanes (XWs), each lane's pool its
+    own. Lanes run one after another into one group buffer (filled with 0xA5 once, then holding whatever the earlier
+    lanes left), so a pair's lane must neither read stale bytes nor write another lane's elements. A pair that does not
+    fit a 32 KB workspace is X_UNSUP there (the kernels then take a slab)."""
+    r = random.Random(29)
+    n_ok = n_unsup = 0
+    for i in range(1500):
+        s, t = odd_map(r, 3, int_keys=i % 9 == 0), odd_map(r, 3)
+        if i % 50 == 0:  # some pairs too large for a lane workspace
+            s = M([("n%d" % k, M([("v", k), ("w", [k, k + 1])])) for k in range(200)])
+        sb, tb = enc(s), enc(t)
+        ref = oracle_merge(sb, tb)
+        got = x_run(L, sb, tb, lane=(7 * i) % 64)
+        if got == "unsupported":
+            n_unsup += 1
+            continue
+        assert got == ref, (i, sb.hex(), tb.hex(), got, ref)
+        n_ok += 1
+    assert n_ok > 1000 and n_unsup >= 20, (n_ok, n_unsup)
 
 
 def test_xmerge_collisions_and_edges(L):

@@ -117,9 +117,9 @@ __global__ void __launch_bounds__(256) k_merge_gen(WaveParams P) {
     // (|result| <= ns + nt + 3 <= cap for every document merge_docs takes; a first pass past the blob would already
     // have overwritten its neighbour, so it fails the partition instead of going on through the exact tree)
     if (o.n > j.cap) err |= DE_UNSUPPORTED;
-    x_run(XSlabs{P.xslab, P.xlocks, P.xlane}, (!ok || unsup) && o.n <= j.cap, [&](uint8_t* slab, uint32_t sb, bool fin) {
+    x_run(XSlabs{P.xslab, P.xlocks, P.xlane}, (!ok || unsup) && o.n <= j.cap, [&](const XWs& ws, bool fin) {
       Out w{dst + 4, 0};
-      const int st = x_merge(slab, sb, sp + 4, ns, tp + 4, nt, w, j.cap);
+      const int st = x_merge(ws, sp + 4, ns, tp + 4, nt, w, j.cap);
       if (st == X_UNSUP && !fin) return st;
       if (st == X_OK) {
         if (w.n == 1 && dst[4] == 0xc0) dst[4] = 0x80;  // an empty tree: DocumentValue.wrap turns nil into {}
@@ -231,12 +231,12 @@ __global__ void __launch_bounds__(256) k_map(WaveParams P) {
         if (nm) st = map_documents(sp + 4, ns, tp, nt, P.maps + first, nm, P.segs, P.queries, P.filters, P.pool, ws, o, fq);
         else st = !merge_docs(sp + 4, ns, tp, nt, o, unsup) ? MAP_UNSUPPORTED : (unsup ? MAP_UNSUPPORTED : MAP_OK);
         // what the node-table mapper / structural merge refuse: the exact tree, size pass, arena, write pass
-        x_run(XSlabs{P.xslab, P.xlocks, P.xlane}, st == MAP_UNSUPPORTED, [&](uint8_t* slab, uint32_t sb, bool fin) {
+        x_run(XSlabs{P.xslab, P.xlocks, P.xlane}, st == MAP_UNSUPPORTED, [&](const XWs& ws, bool fin) {
           Out z{nullptr, 0};
           uint16_t xq = 0;
-          int xs = nm ? x_map(slab, sb, sp + 4, ns, tp, nt, P.maps + first, nm, P.segs, P.queries, P.filters,
+          int xs = nm ? x_map(ws, sp + 4, ns, tp, nt, P.maps + first, nm, P.segs, P.queries, P.filters,
                               P.pool, z, 0x7fffffffu, xq)
-                      : x_merge(slab, sb, sp + 4, ns, tp, nt, z, 0x7fffffffu);
+                      : x_merge(ws, sp + 4, ns, tp, nt, z, 0x7fffffffu);
           if (xs == X_UNSUP && !fin) return xs;
           if (xs == X_OK) {
             const uint64_t bytes = (4 + z.n + 7) & ~7ull;
@@ -245,9 +245,9 @@ __global__ void __launch_bounds__(256) k_map(WaveParams P) {
               err |= DE_ARENA_FULL;
             } else {
               Out w{P.arena + at + 4, 0};
-              xs = nm ? x_map(slab, sb, sp + 4, ns, tp, nt, P.maps + first, nm, P.segs, P.queries, P.filters,
+              xs = nm ? x_map(ws, sp + 4, ns, tp, nt, P.maps + first, nm, P.segs, P.queries, P.filters,
                               P.pool, w, 0x7fffffffu, xq)
-                      : x_merge(slab, sb, sp + 4, ns, tp, nt, w, 0x7fffffffu);
+                      : x_merge(ws, sp + 4, ns, tp, nt, w, 0x7fffffffu);
               if (w.n == 1 && P.arena[at + 4] == 0xc0) P.arena[at + 4] = 0x80;  // nil -> {} (DocumentValue.wrap)
               *(uint32_t*)(P.arena + at) = w.n;
               res = MR_OK | (at >> 3);

@@ -2030,9 +2030,9 @@ __global__ void __launch_bounds__(256) k_tmpl_xtree(TrajParams P) {
           }
         }
       }
-      x_run(XSlabs{P.xslab, P.xlocks, P.xlane}, need, [&](uint8_t* slab, uint32_t sb, bool fin) {
+      x_run(XSlabs{P.xslab, P.xlocks, P.xlane}, need, [&](const XWs& ws, bool fin) {
         Out o{dst + 4, 0};
-        const int st = x_merge(slab, sb, sp + 4, ns, tp + 4, nt, o, cap);
+        const int st = x_merge(ws, sp + 4, ns, tp + 4, nt, o, cap);
         if (st == X_UNSUP && !fin) return st;
         if (st == X_OK) {
           if (o.n == 1 && dst[4] == 0xc0) dst[4] = 0x80;  // an empty tree: DocumentValue.wrap turns nil into {}

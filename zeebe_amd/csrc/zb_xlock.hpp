@@ -29,7 +29,7 @@ __device__ __forceinline__ void x_exclusive(const XSlabs& X, bool need, F&& f) {
     if (lane == l) {
       while (atomicCAS(&X.locks[slot], 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(4);
       __threadfence();
-      f(X.base + (uint64_t)slot * XSLAB_BYTES);
+      f(XWs{X.base + (uint64_t)slot * XSLAB_BYTES, XSLAB_BYTES, 0u, 1u});
       __threadfence();
       atomicExch(&X.locks[slot], 0u);
     }
@@ -49,7 +49,7 @@ __device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg(
 // is released (vmcnt) is enough, and x_merge / x_map read only workspace bytes they wrote in the same call. (Across
 // XCDs the per-XCD L2s are not coherent: a workspace shared by two XCDs needed __threadfence -- an L2 write-back and
 // an L1 invalidate -- around every hold, 3 ms of an 8.9 ms tick that merges 1M documents through the tree.)
-// f(slab, bytes, final) -> X_* status; it commits its outcome unless it returns X_UNSUP with final false.
+// f(workspace, final) -> X_* status; it commits its outcome unless it returns X_UNSUP with final false.
 template <class F>
 __device__ __forceinline__ void x_run(const XSlabs& X, bool need, F&& f) {
   bool again = need;
@@ -65,12 +65,13 @@ __device__ __forceinline__ void x_run(const XSlabs& X, bool need, F&& f) {
     if (lane == l0)
       while (atomicCAS(lock, 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(4);
     __builtin_amdgcn_wave_barrier();
-    if (need) again = f(X.lanes + ((uint64_t)g * 64 + lane) * XLANE_BYTES, XLANE_BYTES, false) == X_UNSUP;
+    // (the group's 64 workspaces interleaved: XWs)
+    if (need) again = f(XWs{X.lanes + (uint64_t)g * 64 * XLANE_BYTES, XLANE_BYTES, (uint32_t)lane, 64u}, false) == X_UNSUP;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (every lane's workspace stores are in the XCD's L2)
     __builtin_amdgcn_wave_barrier();
     if (lane == l0) atomicExch(lock, 0u);
   }
-  x_exclusive(X, again, [&](uint8_t* slab) { (void)f(slab, XSLAB_BYTES, true); });
+  x_exclusive(X, again, [&](const XWs& w) { (void)f(w, true); });
 }
 
 }  // namespace zbg

@@ -45,6 +45,22 @@ struct XStr {  // bytes in the slab's string pool
   uint32_t off, len;
 };
 
+// A workspace: bytes per lane at base, shared by S lanes (S = 1: one lane's own slab -- the big slabs, the host). The
+// tree's arrays are interleaved element by element over the S lanes (lane l's element j at j * S + l), so the lanes of a
+// wave that walk alike -- documents of one shape -- touch adjacent elements, one memory request for many lanes instead
+// of one per lane; each lane's string pool is its own contiguous region after the arrays.
+struct XWs {
+  uint8_t* base;
+  uint32_t bytes;  // per lane
+  uint32_t lane, S;
+};
+template <class T>
+struct XArr {  // a lane's view of an interleaved array
+  T* p;         // its element 0
+  uint32_t s;   // stride in elements (S)
+  ZB_HD T& operator[](uint32_t j) const { return p[(uint64_t)j * s]; }
+};
+
 struct XNode {
   XStr id;
   uint32_t hash;
@@ -67,57 +83,81 @@ struct XFrame {  // writer stack: a container being written
 struct XTree {
   uint8_t* pool;
   uint32_t pool_n, pool_cap;
-  XNode* nodes;
+  XArr<XNode> nodes;
   uint32_t nn, nn_cap;
-  XChild* ch;
+  XArr<XChild> ch;
   uint32_t nc, nc_cap;
-  uint32_t* ht;  // (tree, id) -> node + 1
+  XArr<uint32_t> ht;  // (tree, id) -> node + 1
   uint32_t ht_mask;
-  uint32_t* hc;  // (parent node, child name) -> child + 1
+  XArr<uint32_t> hc;  // (parent node, child name) -> child + 1
   uint32_t hc_mask;
-  XStr* st_par;  // the indexer's parentsStack / isArrayValueStack / lastTypeStack (ArrayDeque push/pop at the front)
-  uint8_t* st_arr;
-  uint8_t* st_typ;
+  XArr<XStr> st_par;  // the indexer's parentsStack / isArrayValueStack / lastTypeStack (ArrayDeque push/pop at the front)
+  XArr<uint8_t> st_arr;
+  XArr<uint8_t> st_typ;
   uint32_t n_par, n_arr, n_typ, st_cap;
-  XFrame* fr;
+  XArr<XFrame> fr;
   uint32_t typed[2];  // nodes with a node type, per tree
   XStr dollar;
   int status;
 
   ZB_HD uint8_t* s(XStr x) const { return pool + x.off; }
 
-  ZB_HD bool init(uint8_t* slab, uint32_t bytes, uint32_t items) {
-    status = X_OK;
-    const uint32_t n = items + 16;
-    uint32_t h = 64;
+  ZB_HD static uint64_t need_of(uint32_t items, uint32_t& n, uint32_t& h) {
+    n = items + 16;
+    h = 64;
     while (h < 2 * n) h <<= 1;
-    uint64_t need = (uint64_t)n * (sizeof(XNode) + sizeof(XChild) + sizeof(XStr) + 2 + sizeof(XFrame)) +
-                    2ull * h * sizeof(uint32_t) + 64;
-    if (need > bytes / 2) { status = X_UNSUP; return false; }
-    uint8_t* p = slab;
-    auto take = [&](uint64_t b) {
-      uint8_t* r = p;
-      p += (b + 15) & ~15ull;
+    return (uint64_t)n * (sizeof(XNode) + sizeof(XChild) + sizeof(XStr) + 2 + sizeof(XFrame)) +
+           2ull * h * sizeof(uint32_t) + 64;
+  }
+  ZB_HD bool init(const XWs& w, uint32_t items) {
+    status = X_OK;
+    uint32_t n, h;
+    if (need_of(items, n, h) > w.bytes / 2) { status = X_UNSUP; return false; }
+#ifdef __HIP_DEVICE_COMPILE__
+    if (w.S > 1) {
+      // the interleaved arrays must have one layout for every lane of the group that uses them at once: the lanes of
+      // the wave that got here (each fits) size it for the largest of them
+      uint64_t act = __ballot(1);
+      uint32_t m = 0;
+      while (act) {
+        const int l = __ffsll((unsigned long long)act) - 1;
+        m = max(m, (uint32_t)__builtin_amdgcn_readlane(items, l));
+        act &= act - 1;
+      }
+      (void)need_of(m, n, h);
+    }
+#endif
+    const uint32_t S = w.S;
+    uint64_t off = 0;  // the arrays of all S lanes, then the S pools
+    auto take = [&](uint32_t elem, uint64_t count) {
+      uint8_t* r = w.base + off + (uint64_t)w.lane * elem;
+      off += ((uint64_t)elem * count * S + 15) & ~15ull;
       return r;
     };
-    nodes = (XNode*)take((uint64_t)n * sizeof(XNode));
-    ch = (XChild*)take((uint64_t)n * sizeof(XChild));
-    st_par = (XStr*)take((uint64_t)n * sizeof(XStr));
-    fr = (XFrame*)take((uint64_t)n * sizeof(XFrame));
-    st_arr = take(n);
-    st_typ = take(n);
-    ht = (uint32_t*)take((uint64_t)h * sizeof(uint32_t));
-    hc = (uint32_t*)take((uint64_t)h * sizeof(uint32_t));
+    nodes = XArr<XNode>{(XNode*)take(sizeof(XNode), n), S};
+    ch = XArr<XChild>{(XChild*)take(sizeof(XChild), n), S};
+    st_par = XArr<XStr>{(XStr*)take(sizeof(XStr), n), S};
+    fr = XArr<XFrame>{(XFrame*)take(sizeof(XFrame), n), S};
+    st_arr = XArr<uint8_t>{take(1, n), S};
+    st_typ = XArr<uint8_t>{take(1, n), S};
+    uint8_t* tabs = take(sizeof(uint32_t), 2ull * h);  // ht, then hc: 2h entries of one lane
+    ht = XArr<uint32_t>{(uint32_t*)tabs, S};
+    hc = XArr<uint32_t>{(uint32_t*)tabs + (uint64_t)h * S, S};
     nn_cap = nc_cap = st_cap = n;
     ht_mask = hc_mask = h - 1;
-    // both tables cleared with 16-byte stores (adjacent, 16-aligned, h a multiple of 4): in the kernels every store
-    // of a lane is a request of its own (the lanes' workspaces are 32 KB apart), and a byte-wise clear was a quarter
-    // of a small merge's requests
-    struct alignas(16) Q { uint64_t a, b; };
-    for (uint32_t i = 0; i < 2 * h; i += 4) *(Q*)(ht + i) = Q{0, 0};
-    pool = p;
-    // (XPOOL_SLACK bytes kept free past the pool: the string helpers read and write whole 8-byte chunks)
-    pool_cap = (uint32_t)(slab + bytes - p) - XPOOL_SLACK;
+    if (S == 1) {
+      // both tables cleared with 16-byte stores (adjacent, 16-aligned, h a multiple of 4): in the kernels every store
+      // of a lane is a request of its own, and a dword-wise clear was a quarter of a small merge's requests
+      struct alignas(16) Q { uint64_t a, b; };
+      for (uint32_t i = 0; i < 2 * h; i += 4) *(Q*)((uint32_t*)tabs + i) = Q{0, 0};
+    } else {
+      for (uint32_t i = 0; i < 2 * h; i++) ht[i] = 0;  // (interleaved: the wave's lanes clear adjacent dwords)
+    }
+    // the lane's pool: its share of what the arrays leave (XPOOL_SLACK bytes kept free past it: the string helpers read
+    // and write whole 8-byte chunks)
+    const uint64_t pool_bytes = (((uint64_t)w.bytes * S - off) / S) & ~15ull;
+    pool = w.base + off + (uint64_t)w.lane * pool_bytes;
+    pool_cap = (uint32_t)pool_bytes - XPOOL_SLACK;
     pool_n = 0;
     nn = nc = 0;
     n_par = n_arr = n_typ = 0;
@@ -497,11 +537,11 @@ ZB_HD inline int x_emit(XTree& T, const uint8_t* u, uint32_t un, const uint8_t* 
 }
 
 // MappingProcessor.merge(source, target) without mappings (has_tgt: the target buffer is not empty)
-ZB_HD inline __noinline__ int x_merge(uint8_t* slab, uint32_t slab_bytes, const uint8_t* src, uint32_t ns, const uint8_t* tgt,
-                         uint32_t nt, Out& o, uint32_t limit) {
+ZB_HD inline __noinline__ int x_merge(const XWs& ws, const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint32_t nt,
+                                      Out& o, uint32_t limit) {
   XTree T;
   // nodes / child entries / stack: each token makes at most one of each, the source's twice (merge_in)
-  if (!T.init(slab, slab_bytes, 2 * x_tokens(src, ns) + x_tokens(tgt, nt))) return T.status;
+  if (!T.init(ws, 2 * x_tokens(src, ns) + x_tokens(tgt, nt))) return T.status;
   if (nt == 0) {  // extract(source): index + write
     T.index(0, src, ns, false);
     if (T.status != X_OK) return T.status;
@@ -518,13 +558,13 @@ ZB_HD inline __noinline__ int x_merge(uint8_t* slab, uint32_t slab_bytes, const 
 
 // The tree of MappingProcessor.extract(source, mappings) (tgt == nullptr) or .merge(source, target, mappings) with
 // nmaps >= 1, before it is written: the target indexed, then every mapping's target path and extracted leaf
-ZB_HD inline int x_map_tree(XTree& T, uint8_t* slab, uint32_t slab_bytes, const uint8_t* src, uint32_t ns,
+ZB_HD inline int x_map_tree(XTree& T, const XWs& ws, const uint8_t* src, uint32_t ns,
                             const uint8_t* tgt, uint32_t nt, const DevMapping* maps, uint32_t nmaps, const DevSeg* segs,
                             const DevQuery* queries, const DevFilter* filters, const uint8_t* pool,
                             uint16_t& fail_query) {
   uint32_t segn = 0;
   for (uint32_t i = 0; i < nmaps; i++) segn += maps[i].nseg + 1;
-  if (!T.init(slab, slab_bytes, (tgt ? x_tokens(tgt, nt) : 0) + 2 * segn)) return T.status;
+  if (!T.init(ws, (tgt ? x_tokens(tgt, nt) : 0) + 2 * segn)) return T.status;
   if (tgt && nt) {
     T.index(0, tgt, nt, false);
     if (T.status != X_OK) return T.status;
@@ -580,11 +620,12 @@ ZB_HD inline int x_map_tree(XTree& T, uint8_t* slab, uint32_t slab_bytes, const 
 }
 
 // MappingProcessor.extract(source, mappings) (tgt == nullptr) or .merge(source, target, mappings), nmaps >= 1
-ZB_HD inline __noinline__ int x_map(uint8_t* slab, uint32_t slab_bytes, const uint8_t* src, uint32_t ns, const uint8_t* tgt,
-                       uint32_t nt, const DevMapping* maps, uint32_t nmaps, const DevSeg* segs, const DevQuery* queries,
-                       const DevFilter* filters, const uint8_t* pool, Out& o, uint32_t limit, uint16_t& fail_query) {
+ZB_HD inline __noinline__ int x_map(const XWs& ws, const uint8_t* src, uint32_t ns, const uint8_t* tgt, uint32_t nt,
+                                    const DevMapping* maps, uint32_t nmaps, const DevSeg* segs, const DevQuery* queries,
+                                    const DevFilter* filters, const uint8_t* pool, Out& o, uint32_t limit,
+                                    uint16_t& fail_query) {
   XTree T;
-  const int st = x_map_tree(T, slab, slab_bytes, src, ns, tgt, nt, maps, nmaps, segs, queries, filters, pool, fail_query);
+  const int st = x_map_tree(T, ws, src, ns, tgt, nt, maps, nmaps, segs, queries, filters, pool, fail_query);
   if (st != X_OK) return st;
   return x_emit(T, tgt, tgt ? nt : 0, src, ns, o, limit);
 }
