@@ -1083,14 +1083,17 @@ __global__ void k_traj_regen(TrajParams P) {
   ctl->derr = 0;
 }
 
-__global__ void __launch_bounds__(256) k_traj_commit(TrajParams P) {
-  __shared__ uint64_t s_st[256 / 64][6];
+constexpr int COMMIT_WG = 1024;
+__global__ void __launch_bounds__(COMMIT_WG) k_traj_commit(TrajParams P) {
+  __shared__ uint64_t s_st[COMMIT_WG / 64][6];
   const TrajCtl* ctl = P.ctl;
   if (ctl->flag) return;
   uint64_t st[6] = {0, 0, 0, 0, 0, 0};
-  for (int b = threadIdx.x; b < P.nwg_e; b += blockDim.x)
+  // the emit workgroups' statistics (a deferred batch's emit wrote none: every workgroup's are zero)
+  if (!ctl->defer)
+    for (int b = threadIdx.x; b < P.nwg_e; b += blockDim.x)
 #pragma unroll
-    for (int f = 0; f < 6; f++) st[f] += P.wstats[(uint64_t)b * 6 + f];
+      for (int f = 0; f < 6; f++) st[f] += P.wstats[(uint64_t)b * 6 + f];
 #pragma unroll
   for (int f = 0; f < 6; f++) {
     uint64_t x = st[f];
@@ -1099,7 +1102,8 @@ __global__ void __launch_bounds__(256) k_traj_commit(TrajParams P) {
   }
   __syncthreads();
   if (threadIdx.x != 0) return;
-  for (int f = 0; f < 6; f++) P.stats[f] += s_st[0][f] + s_st[1][f] + s_st[2][f] + s_st[3][f];
+  for (int f = 0; f < 6; f++)
+    for (int k = 0; k < COMMIT_WG / 64; k++) P.stats[f] += s_st[k][f];
   if (P.uni || P.cls) {  // template emit: per-class traced statistics x class sizes
     const uint32_t nc = P.cls ? P.plan->nc : 1;
     for (uint32_t c = 0; c < nc; c++) {
@@ -2124,7 +2128,7 @@ void launch_traj_emit(const TrajParams& p, hipStream_t s, hipEvent_t* ev_main) {
     hipLaunchKernelGGL(k_traj_regen, dim3(1), dim3(1), 0, s, p);
     hipLaunchKernelGGL((k_traj<true, false, false, true, false, false>), g, b, 0, s, p);
   }
-  if (!p.materialize) hipLaunchKernelGGL(k_traj_commit, dim3(1), dim3(256), 0, s, p);
+  if (!p.materialize) hipLaunchKernelGGL(k_traj_commit, dim3(1), dim3(COMMIT_WG), 0, s, p);
   if (p.xq && (p.uni || p.cls) && !p.materialize) {  // the merge chains the template emit queued for the exact tree (none: exits at once)
     if (p.cls) hipLaunchKernelGGL(k_tmpl_xtree<true>, dim3(XLANE_COUNT / 256), dim3(256), 0, s, p);
     else hipLaunchKernelGGL(k_tmpl_xtree<false>, dim3(XLANE_COUNT / 256), dim3(256), 0, s, p);
