@@ -104,10 +104,12 @@ def run_c5(a, rank, world, local_rank, dist, barrier, reduce_max, reduce_sum):
         step()
     barrier()
     el = 0.0
+    step_ms = []
     for _ in range(a.steps):
         barrier()
         dt, ser = step()
-        el += reduce_max(dt)
+        step_ms.append(reduce_max(dt) * 1e3)
+        el += step_ms[-1] / 1e3
         tot["records"] += ser["records"]
         tot["value_bytes"] += ser["value_bytes"]
         tot["ser_ms"] += ser["write_kernel_ms"] + ser["size_kernel_ms"]
@@ -128,6 +130,7 @@ def run_c5(a, rank, world, local_rank, dist, barrier, reduce_max, reduce_sum):
                                     "zb_serialize of every record of the partition's log (values + headers, in HBM); "
                                     "the CREATE and PUBLISH inputs are uploaded before the timed region"},
            "completed_instances_per_s": N * a.steps / el,
+           "step_ms": [round(x, 3) for x in step_ms],
            "drained_records_per_step_rank0": tot["records"] / a.steps,
            "rccl_library": rccl_library(),
            "roofline": {"bound": "hbm", "achieved": path_bytes / (ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -39,7 +39,15 @@ def main():
                                "--no-cpu-baseline"]
     a = bench.parse()
     bench.run_c5(a, 0, 1, 0, None)
-    last = max(i for i, x in enumerate(SEQ) if x[0] == "reset")
+    resets = [i for i, x in enumerate(SEQ) if x[0] == "reset"] + [len(SEQ)]
+    spans = []
+    for a_, b_ in zip(resets, resets[1:]):  # the timed part: first step call .. the serialize's end
+        seg = SEQ[a_:b_]
+        s0 = next(t for name, t, d in seg if name == "step")
+        s1 = max(t + d for name, t, d in seg if name == "serialize")
+        spans.append((s1 - s0) * 1e3)
+    print("timed span per step (ms):", " ".join("%.3f" % x for x in spans))
+    last = resets[-2]
     t0 = SEQ[last][1]
     print("last step, call by call (start ms, duration ms):")
     for name, t, d in SEQ[last:]:

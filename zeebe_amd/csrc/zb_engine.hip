@@ -74,6 +74,7 @@ struct PubUpload {
   uint32_t nn;
   int64_t ttl;
   uint64_t a_ck, a_cko, a_pl, a_plo, a_name;
+  uint64_t gran;  // the batch's blob granules (8 bytes), scanned at upload
 };
 
 struct zb_engine {
@@ -301,6 +302,10 @@ struct zb_engine {
   void* ob_tmp = nullptr;  // (scan scratch)
   size_t ob_tmp_bytes = 0;
   uint32_t ob_counts_read[2] = {0, 0};  // both outbox command counts at the last zb_outbox_count
+  // the outbox counters (commands, granules) in h_stats_pinned[19..20] are current: copied in the round trip that
+  // ended the last work able to change them (a wave batch, a delivery, a message batch), so zb_outbox_count
+  // needs no round trip of its own; cleared by everything that enqueues such work
+  bool ob_counts_valid = false;
   // non-empty waves of the last wave loop, per kind of input (a partition that alternates kinds -- C5: CREATE batches,
   // then the correlations delivered to its inbox -- settles each kind in its own count): 1 staged CREATEs only,
   // 2 other staged records, 3 records already in the log (inbox deliveries)
@@ -346,6 +351,8 @@ struct zb_engine {
   uint64_t rows_mark = 0, arena_mark = 0;  // rows / arena bytes live after the last compaction (maintain)
   // inbox CORRELATE resolution by activity instance key (zb_inbox_submit)
   int64_t *x_keys = nullptr, *x_pos = nullptr, *x_keys2 = nullptr, *x_pos2 = nullptr;
+  uint32_t* d_unresolved = nullptr;  // delivered CORRELATEs whose token named no live row of their key (running count)
+  uint32_t unresolved_seen = 0;
   uint64_t x_cap = 0;
   DevVec<int64_t> d_lookup_keys, d_lookup_pos;    // zb_submit lookups of the staged batch: key, staged index
   uint64_t staged_nlook = 0;
@@ -436,6 +443,23 @@ hipError_t upload_vec(zb_engine* e, DevVec<T>& d, const std::vector<T>& v) {
   }
   return upload_async(e, d.p, v.data(), v.size() * sizeof(T));
 }
+
+// stream-ordered read-back of a few device words into pinned host memory with one launch (k_status) instead of one
+// copy per item; valid on the host after the stream's next synchronisation
+struct StatusReads {
+  StatusCopy c{};
+  void add(void* host, const void* dev, size_t bytes) {
+    if (c.count >= StatusCopy::MAX) std::abort();  // (a programming error: the call sites are fixed)
+    c.src[c.count] = (const uint32_t*)dev;
+    c.dst[c.count] = (uint32_t*)host;
+    c.words[c.count] = (uint32_t)(bytes / 4);
+    c.count++;
+  }
+  hipError_t launch(hipStream_t s) const {
+    launch_status(c, s);
+    return hipGetLastError();
+  }
+};
 
 // The exact-tree workspaces (zb_xmerge.hpp) of one device, shared by every engine on it: slabs and lane groups are held
 // under device-wide locks (zb_xlock.hpp), so the partitions of one GPU need one set, not 2 GiB each. Taken by the first
@@ -876,11 +900,14 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   launch_traj_emit(p, e->stream, &ev[3]);
   HIPCHECK(e, hipEventRecord(ev[2], e->stream));
   HIPCHECK(e, hipGetLastError());
-  HIPCHECK(e, hipMemcpyAsync(e->h_ctl_pinned, e->t_ctl, sizeof(TrajCtl), hipMemcpyDeviceToHost, e->stream));
-  HIPCHECK(e, hipMemcpyAsync(e->h_hdr_pinned, e->hdr + (e->wave & 1), sizeof(WaveHdr), hipMemcpyDeviceToHost,
-                             e->stream));
-  HIPCHECK(e, hipMemcpyAsync(e->h_err_pinned, e->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
-  if (p.cls) HIPCHECK(e, hipMemcpyAsync(e->h_stats_pinned + 16, e->c_plan, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  {
+    StatusReads r;
+    r.add(e->h_ctl_pinned, e->t_ctl, sizeof(TrajCtl));
+    r.add(e->h_hdr_pinned, e->hdr + (e->wave & 1), sizeof(WaveHdr));
+    r.add(e->h_err_pinned, e->derr, sizeof(uint32_t));
+    if (p.cls) r.add(e->h_stats_pinned + 16, e->c_plan, sizeof(uint32_t));
+    HIPCHECK(e, r.launch(e->stream));
+  }
   HIPCHECK(e, hipStreamSynchronize(e->stream));
   float ms0 = 0, ms1 = 0, ms_main = 0;
   HIPCHECK(e, hipEventElapsedTime(&ms0, ev[0], ev[1]));
@@ -945,6 +972,7 @@ int ensure_outbox(zb_engine* e) {
   }
   HIPCHECK(e, hipMalloc(&e->on, 4 * sizeof(uint32_t)));
   HIPCHECK(e, hipMemsetAsync(e->on, 0, 4 * sizeof(uint32_t), e->stream));
+  e->ob_counts_valid = false;
   if (!e->sub_jobs) HIPCHECK(e, hipMalloc(&e->sub_jobs, e->job_cap * sizeof(uint64_t)));
   return ZB_OK;
 }
@@ -1030,8 +1058,15 @@ int require_idle(zb_engine* e) {
 int finish_batch(zb_engine* e) {
   HIPCHECK(e, upload_async(e, e->hdr + (e->wave & 1), &e->host_hdr, sizeof(WaveHdr)));
   HIPCHECK(e, hipGetLastError());
-  HIPCHECK(e, hipMemcpyAsync(e->h_err_pinned, e->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  {
+    StatusReads r;
+    r.add(e->h_err_pinned, e->derr, sizeof(uint32_t));
+    // (a message batch's correlations are in the outbox: the exchange decision reads the counters from here)
+    if (e->on) r.add(e->h_stats_pinned + 19, e->on, 4 * sizeof(uint32_t));
+    HIPCHECK(e, r.launch(e->stream));
+  }
   HIPCHECK(e, hipStreamSynchronize(e->stream));
+  e->ob_counts_valid = e->on != nullptr;
   return check_device_errors(e, *e->h_err_pinned);
 }
 
@@ -1530,7 +1565,7 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->job_counts, JOB_COUNTS * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipMalloc(&e->merge_slow, e->job_cap * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_hdr_pinned, 2 * sizeof(WaveHdr)) != hipSuccess) return cleanup(ZB_ENOMEM);
-  if (hipHostMalloc(&e->h_err_pinned, sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
+  if (hipHostMalloc(&e->h_err_pinned, 2 * sizeof(uint32_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_ctl_pinned, sizeof(TrajCtl)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_stats_pinned, 21 * sizeof(uint64_t)) != hipSuccess) return cleanup(ZB_ENOMEM);
   if (hipHostMalloc(&e->h_up, 1 << 20) != hipSuccess) return cleanup(ZB_ENOMEM);
@@ -1582,7 +1617,7 @@ void zb_engine_destroy(zb_engine* e) {
   void* ms[] = {e->obox[0], e->obox[1], e->okeys[0], e->okeys[1], e->ovar[0], e->ovar[1], e->on, e->subs, e->sub_head,
                 e->sub_next, e->msgs, e->msg_head, e->msg_next, e->d_xcounts, e->xsend, e->xrecv, e->ob_keys, e->ob_idx_in,
                 e->ob_idx_out, e->ob_first, e->ob_sizes, e->ob_goff, e->ob_table, e->ob_base, e->ob_tmp, e->ob_staging,
-                e->m_prior, e->m_cnt, e->m_tmp, e->in_buf, e->p_in, e->p_gran};
+                e->m_prior, e->m_cnt, e->m_tmp, e->in_buf, e->p_in, e->p_gran, e->d_unresolved};
   for (void* p : ms)
     if (p) (void)hipFree(p);
   if (e->h_hdr_pinned) (void)hipHostFree(e->h_hdr_pinned);
@@ -1687,7 +1722,8 @@ int zb_reset(zb_engine* e, int keep_staged) {
     e->tick_aik.clear();
     e->tick_jobs.clear();
     e->staged_uploaded = false;
-    for (int& h : e->wave_hint) h = 0;  // (a reset that keeps the staged batch runs the same tick again: hints stay)
+    // (the wave hints stay: a reset starts the log again, not a new workload -- the next tick of the same model
+    // settles in as many waves, as it would on a partition that never resets; zb_deploy clears them)
   }
   e->term = false;
   e->conf_active = false;
@@ -1695,6 +1731,7 @@ int zb_reset(zb_engine* e, int keep_staged) {
   e->sub_count = e->msg_count = 0;
   e->msg_key_next = 0;
   if (e->on) HIPCHECK(e, hipMemsetAsync(e->on, 0, 4 * sizeof(uint32_t), e->stream));
+  e->ob_counts_valid = false;
   e->ob_pos_base[0] = e->ob_pos_base[1] = 0;
   e->clock_ms = 0;
   if (e->subs) {
@@ -2541,8 +2578,17 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   const int64_t end_before = e->host_hdr.end;  // records appended by this call: injected input + follow-ups
   int64_t traj_base = 0, traj_n = 0;
   const int hint_key = (e->staged_pending && !e->staged.empty()) ? (e->staged_only_creates ? 1 : 2) : 3;
+  const bool injecting = e->staged_pending && !e->staged.empty();
+  if (!injecting && e->host_hdr.begin == e->host_hdr.end) {  // nothing to process: no kernel, no round trip
+    st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (stats) *stats = st;
+    e->term = false;
+    e->conf_active = false;
+    return ZB_OK;
+  }
+  e->ob_counts_valid = false;  // (the waves below may write the outbox)
   // ---- inject staged input at the log tail (engine is quiescent between steps)
-  if (e->staged_pending && !e->staged.empty()) {
+  if (injecting) {
     if (!e->staged_only_creates && e->host_hdr.begin != e->host_hdr.end)
       return fail(e, ZB_EINVAL, "records other than CREATE are injected into a quiescent partition only: "
                                 "step it to quiescence first");
@@ -2720,12 +2766,18 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     if (e->wave_fused_grid) launch_stat_fold(e->dstats, e->stream);  // k_wave's statistics banks -> the counters
     if (!per_wave) HIPCHECK(e, hipEventRecord(e->ev[1], e->stream));
     HIPCHECK(e, hipGetLastError());
-    HIPCHECK(e, hipMemcpyAsync(e->h_hdr_pinned, e->hdr + (e->wave & 1), sizeof(WaveHdr), hipMemcpyDeviceToHost,
-                               e->stream));
-    HIPCHECK(e, hipMemcpyAsync(e->h_err_pinned, e->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
-    // (the counters too: after the batch that ends the loop they need no round trip of their own)
-    HIPCHECK(e, hipMemcpyAsync(stats_after, e->dstats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+    {
+      StatusReads r;
+      r.add(e->h_hdr_pinned, e->hdr + (e->wave & 1), sizeof(WaveHdr));
+      r.add(e->h_err_pinned, e->derr, sizeof(uint32_t));
+      // (the counters too: after the batch that ends the loop they need no round trip of their own)
+      r.add(stats_after, e->dstats, 8 * sizeof(uint64_t));
+      // (and the outbox counters: the exchange decision after a quiescent step needs no round trip of its own)
+      if (e->on) r.add(e->h_stats_pinned + 19, e->on, 4 * sizeof(uint32_t));
+      HIPCHECK(e, r.launch(e->stream));
+    }
     HIPCHECK(e, hipStreamSynchronize(e->stream));
+    e->ob_counts_valid = e->on != nullptr;
     stats_fresh = true;
     if (per_wave) {
       for (int i = 0; i < batch; i++) {
@@ -2760,8 +2812,12 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   }
   ZB_SP(3);  // wave loop
   if (!stats_fresh) {
-    HIPCHECK(e, hipMemcpyAsync(stats_after, e->dstats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+    StatusReads r;
+    r.add(stats_after, e->dstats, 8 * sizeof(uint64_t));
+    if (e->on) r.add(e->h_stats_pinned + 19, e->on, 4 * sizeof(uint32_t));
+    HIPCHECK(e, r.launch(e->stream));
     HIPCHECK(e, hipStreamSynchronize(e->stream));
+    e->ob_counts_valid = e->on != nullptr;
   }
   if (loop && quiescent) e->wave_hint[hint_key] = (int)(stats_after[6] - e->h_stats_pinned[18]);  // its non-empty waves
   st.records_processed = (uint64_t)(e->host_hdr.begin - processed_from);
@@ -3363,7 +3419,7 @@ int check_message_batch(zb_engine* e, uint64_t n, uint64_t publishes, uint64_t b
 // the commands of a message batch are in the log at [end, end + n), their blobs at the arena tail (blob_bytes),
 // the intra-batch prior flags in m_prior: process them in runs of one intent (runs: [i0, i1) with its intent)
 int process_uploaded_messages(zb_engine* e, uint64_t n, uint64_t blob_bytes,
-                              const std::vector<std::pair<uint64_t, uint8_t>>& runs);
+                              const std::vector<std::pair<uint64_t, uint8_t>>& runs, int uniform_out = 0);
 
 int process_messages(zb_engine* e, const MsgBatch& b) {
   const uint64_t n = b.recs.size();
@@ -3400,15 +3456,22 @@ int process_messages(zb_engine* e, const MsgBatch& b) {
   return process_uploaded_messages(e, n, b.blobs.size(), runs);
 }
 
+// uniform_out (zb_publish_uploaded): every command is a PUBLISH without a message id -- none can be rejected
+// (MessageDataStore.hasMessage needs an id), each writes uniform_out records (PUBLISHED, + DELETED when ttl <= 0: 2)
+// and is stored iff uniform_out == 1 -- so the per-command counts and their scan are the closed form i * uniform_out
+// (no count pass, no round trip); k_pub_build already initialized the commands' links / sources / lengths
 int process_uploaded_messages(zb_engine* e, uint64_t n, uint64_t blob_bytes,
-                              const std::vector<std::pair<uint64_t, uint8_t>>& runs) {
+                              const std::vector<std::pair<uint64_t, uint8_t>>& runs, int uniform_out) {
   const int64_t base = e->host_hdr.end;
-  int rc = grow_dev(e, (uint8_t**)&e->m_cnt, &e->m_cnt_cap, 2 * (n + 1) * sizeof(uint64_t));
+  e->ob_counts_valid = false;  // (k_pub_emit writes correlations; finish_batch reads the counters back)
+  int rc = uniform_out ? ZB_OK : grow_dev(e, (uint8_t**)&e->m_cnt, &e->m_cnt_cap, 2 * (n + 1) * sizeof(uint64_t));
   if (rc != ZB_OK) return rc;
-  HIPCHECK(e, hipMemsetAsync(e->links + base, 0xff, n * sizeof(uint64_t), e->stream));
-  HIPCHECK(e, hipMemsetAsync(e->srcd + base, 0, n * sizeof(uint32_t), e->stream));  // written by other writers
-  // (the verbatim value of a submitted command is its serialized length: the size pass measures the rest)
-  HIPCHECK(e, hipMemsetAsync(e->vlen + base, 0xff, n * sizeof(uint32_t), e->stream));
+  if (!uniform_out) {
+    HIPCHECK(e, hipMemsetAsync(e->links + base, 0xff, n * sizeof(uint64_t), e->stream));
+    HIPCHECK(e, hipMemsetAsync(e->srcd + base, 0, n * sizeof(uint32_t), e->stream));  // written by other writers
+    // (the verbatim value of a submitted command is its serialized length: the size pass measures the rest)
+    HIPCHECK(e, hipMemsetAsync(e->vlen + base, 0xff, n * sizeof(uint32_t), e->stream));
+  }
   e->host_hdr.arena_next += (int64_t)blob_bytes;
   e->arena_total += blob_bytes;
   int64_t out = base + (int64_t)n;  // the next follow-up position
@@ -3421,7 +3484,15 @@ int process_uploaded_messages(zb_engine* e, uint64_t n, uint64_t blob_bytes,
     p.base = base + (int64_t)i0;
     p.n = (int64_t)(i1 - i0);
     p.out_base = out;
-    if (intent == 0) {  // PUBLISH
+    if (intent == 0 && uniform_out) {
+      const uint64_t m = i1 - i0;
+      p.key_base = e->msg_key_next;
+      p.uni_out = uniform_out;
+      launch_pub_emit(p, e->stream);
+      out += (int64_t)(m * (uint64_t)uniform_out);
+      e->msg_key_next += (int64_t)m;
+      if (uniform_out == 1) e->msg_count += m;
+    } else if (intent == 0) {  // PUBLISH
       p.prior = e->m_prior + i0;
       p.cnt = e->m_cnt;
       p.cnt_off = e->m_cnt + (n + 1);
@@ -3518,6 +3589,7 @@ int deliver(zb_engine* e, int kind, const uint8_t* buf, const std::vector<uint64
   p.n = (int64_t)n;
   p.base = base;
   const int64_t arena_before = e->host_hdr.arena_next;
+  e->ob_counts_valid = false;  // (k_msg_open writes correlations; read back below)
   if (kind == ZB_XCHG_OPEN) {
     launch_msg_open(p, e->stream);  // processed at once: OPEN commands + OPENED events
     e->sub_count += n;
@@ -3525,7 +3597,14 @@ int deliver(zb_engine* e, int kind, const uint8_t* buf, const std::vector<uint64
     e->host_hdr.begin = e->host_hdr.gen_end = e->host_hdr.end;
   } else {
     // CORRELATE commands: the next zb_step processes them; the element instance each names is looked up by its
-    // activity instance key (ElementInstanceIndex.getInstance): keys sorted, then one pass over the rows
+    // activity instance key (ElementInstanceIndex.getInstance). k_wis_inject takes the row the subscription's token
+    // names when that row still holds the key (live); the others -- a foreign or stale token -- are counted, and only
+    // then are the keys sorted and the rows searched (k_resolve, below)
+    if (!e->d_unresolved) {
+      HIPCHECK(e, hipMalloc(&e->d_unresolved, sizeof(uint32_t)));
+      HIPCHECK(e, hipMemsetAsync(e->d_unresolved, 0, sizeof(uint32_t), e->stream));
+      e->unresolved_seen = 0;
+    }
     if (n > e->x_cap) {
       HIPCHECK(e, hipStreamSynchronize(e->stream));
       void* xs[] = {e->x_keys, e->x_pos, e->x_keys2, e->x_pos2};
@@ -3543,25 +3622,41 @@ int deliver(zb_engine* e, int kind, const uint8_t* buf, const std::vector<uint64
     if (n > (uint64_t)INT32_MAX) return fail(e, ZB_EUNSUPPORTED, "more than 2^31 delivered commands");
     p.lookup_keys = e->x_keys;
     p.lookup_pos = e->x_pos;
+    p.rmeta = e->rmeta;
+    p.rkeys = e->rkeys;
+    p.rows = (uint64_t)e->host_hdr.rows_next;
+    p.unresolved = e->d_unresolved;
     launch_wis_inject(p, e->stream);
-    int rc = sort_pairs(e, e->x_keys, e->x_keys2, e->x_pos, e->x_pos2, n, "inbox");
+    e->host_hdr.end = base + (int64_t)recs;
+    e->host_hdr.gen_end = e->host_hdr.end;
+  }
+  // blobs were allocated on the device header: its arena pointer and the error word in one round trip (with the
+  // outbox counters and the unresolved count), then the host's header (log range) back to the device, stream-ordered
+  // before the next step's kernels
+  uint32_t* unres = e->h_err_pinned + 1;
+  {
+    StatusReads r;
+    r.add(e->h_hdr_pinned, e->hdr + (e->wave & 1), sizeof(WaveHdr));
+    r.add(e->h_err_pinned, e->derr, sizeof(uint32_t));
+    if (e->on) r.add(e->h_stats_pinned + 19, e->on, 4 * sizeof(uint32_t));
+    if (kind != ZB_XCHG_OPEN) r.add(unres, e->d_unresolved, sizeof(uint32_t));
+    HIPCHECK(e, r.launch(e->stream));
+  }
+  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  e->ob_counts_valid = e->on != nullptr;
+  e->host_hdr.arena_next = e->h_hdr_pinned[0].arena_next;
+  int rc = check_device_errors(e, *e->h_err_pinned);
+  if (rc != ZB_OK) return rc;
+  if (kind != ZB_XCHG_OPEN && *unres != e->unresolved_seen) {  // (a running count: no reset between deliveries)
+    e->unresolved_seen = *unres;
+    rc = sort_pairs(e, e->x_keys, e->x_keys2, e->x_pos, e->x_pos2, n, "inbox");
     if (rc != ZB_OK) return rc;
     ResolveParams rp{};
     rp.rmeta = e->rmeta; rp.rkeys = e->rkeys; rp.rows = (uint64_t)e->host_hdr.rows_next;
     rp.keys = e->x_keys2; rp.pos = e->x_pos2; rp.pos_base = 0; rp.n = (int64_t)n;
     rp.links = e->links;
-    launch_resolve(rp, e->stream);
-    e->host_hdr.end = base + (int64_t)recs;
-    e->host_hdr.gen_end = e->host_hdr.end;
+    launch_resolve(rp, e->stream);  // (every key of the delivery: the token rows it finds again are the same rows)
   }
-  // blobs were allocated on the device header: its arena pointer and the error word in one round trip, then the
-  // host's header (log range) back to the device, stream-ordered before the next step's kernels
-  HIPCHECK(e, hipMemcpyAsync(e->h_hdr_pinned, e->hdr + (e->wave & 1), sizeof(WaveHdr), hipMemcpyDeviceToHost, e->stream));
-  HIPCHECK(e, hipMemcpyAsync(e->h_err_pinned, e->derr, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
-  HIPCHECK(e, hipStreamSynchronize(e->stream));
-  e->host_hdr.arena_next = e->h_hdr_pinned[0].arena_next;
-  int rc = check_device_errors(e, *e->h_err_pinned);
-  if (rc != ZB_OK) return rc;
   e->records_total += recs;
   e->arena_total += (uint64_t)(e->host_hdr.arena_next - arena_before);
   HIPCHECK(e, upload_async(e, e->hdr + (e->wave & 1), &e->host_hdr, sizeof(WaveHdr)));
@@ -3664,6 +3759,27 @@ int zb_submit_messages(zb_engine* e, const zb_rec_desc* recs, size_t n, const ui
   return process_messages(e, b);
 }
 
+}  // extern "C"
+namespace {
+// the device-side view of an uploaded PUBLISH batch (zb_upload_publishes: p_in holds the caller's bytes as they are)
+PubBuild pub_build_params(zb_engine* e, const PubUpload& u) {
+  PubBuild pb{};
+  pb.cks = e->p_in + u.a_ck;
+  pb.ck_off = (const uint64_t*)(e->p_in + u.a_cko);
+  pb.pls = e->p_in + u.a_pl;
+  pb.pl_off = (const uint64_t*)(e->p_in + u.a_plo);
+  pb.name = e->p_in + u.a_name;
+  pb.nn = u.nn;
+  pb.ttl = u.ttl;
+  pb.n = u.n;
+  pb.gran = e->p_gran;
+  pb.goff = e->p_gran + (u.n + 1);
+  pb.err = (uint32_t*)(e->p_gran + 2 * (u.n + 1));
+  return pb;
+}
+}  // namespace
+extern "C" {
+
 int zb_upload_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, const uint8_t* cks,
                         const uint64_t* ck_offsets, const uint8_t* payloads, const uint64_t* payload_offsets) {
   if (!e || !name || (n > 0 && (!cks || !ck_offsets || !payloads || !payload_offsets))) return ZB_EINVAL;
@@ -3705,8 +3821,18 @@ int zb_upload_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, c
   if (rc == ZB_OK) rc = grow_dev(e, &e->m_prior, &e->m_prior_cap, n);
   if (rc != ZB_OK) return rc;
   HIPCHECK(e, hipMemcpyAsync(e->p_in, stage, total, hipMemcpyHostToDevice, e->stream));
-  HIPCHECK(e, hipStreamSynchronize(e->stream));  // (resident; the staging memory is free again)
-  e->pub_up = PubUpload{true, n, nn, ttl, a_ck, a_cko, a_pl, a_plo, a_name};
+  // the batch checked and its blobs sized now (k_pub_sizes, scan): processing it needs no round trip for them
+  PubUpload u{true, n, nn, ttl, a_ck, a_cko, a_pl, a_plo, a_name, 0};
+  PubBuild pb = pub_build_params(e, u);
+  HIPCHECK(e, hipMemsetAsync(pb.err, 0, 2 * sizeof(uint32_t), e->stream));
+  launch_pub_sizes(pb, e->stream);
+  uint32_t herr[2] = {0, 0};
+  HIPCHECK(e, hipMemcpyAsync(herr, pb.err, sizeof(herr), hipMemcpyDeviceToHost, e->stream));
+  rc = scan_u64(e, e->p_gran, e->p_gran + (n + 1), n, &u.gran);  // (sets gran[n] = 0 first; its round trip covers
+  if (rc != ZB_OK) return rc;                                      // the upload and the error words too)
+  if (herr[0]) return fail(e, ZB_EINVAL, "Document has invalid format. On root level an object is only allowed.");
+  if (herr[1]) return fail(e, ZB_EINVAL, "correlation key or payload too long");
+  e->pub_up = u;
   return ZB_OK;
 }
 
@@ -3721,38 +3847,18 @@ int zb_publish_uploaded(zb_engine* e) {
   const PubUpload u = e->pub_up;
   e->pub_up.valid = false;
   const uint64_t n = u.n;
-  PubBuild pb{};
-  pb.cks = e->p_in + u.a_ck;
-  pb.ck_off = (const uint64_t*)(e->p_in + u.a_cko);
-  pb.pls = e->p_in + u.a_pl;
-  pb.pl_off = (const uint64_t*)(e->p_in + u.a_plo);
-  pb.name = e->p_in + u.a_name;
-  pb.nn = u.nn;
-  pb.ttl = u.ttl;
-  pb.n = n;
-  pb.gran = e->p_gran;
-  pb.goff = e->p_gran + (n + 1);
-  uint32_t* err = (uint32_t*)(e->p_gran + 2 * (n + 1));
-  pb.err = err;
-  HIPCHECK(e, hipMemsetAsync(err, 0, 2 * sizeof(uint32_t), e->stream));
-  launch_pub_sizes(pb, e->stream);
-  uint64_t gran = 0;
-  rc = scan_u64(e, e->p_gran, e->p_gran + (n + 1), n, &gran);  // (sets gran[n] = 0 first)
+  rc = check_message_batch(e, n, n, u.gran * 8);
   if (rc != ZB_OK) return rc;
-  uint32_t herr[2] = {0, 0};
-  HIPCHECK(e, hipMemcpyAsync(herr, err, sizeof(herr), hipMemcpyDeviceToHost, e->stream));
-  HIPCHECK(e, hipStreamSynchronize(e->stream));  // (the scan's total too)
-  if (herr[0]) return fail(e, ZB_EINVAL, "Document has invalid format. On root level an object is only allowed.");
-  if (herr[1]) return fail(e, ZB_EINVAL, "correlation key or payload too long");
-  rc = check_message_batch(e, n, n, gran * 8);
-  if (rc != ZB_OK) return rc;
+  PubBuild pb = pub_build_params(e, u);
   pb.arena = e->arena;
   pb.arena0 = (uint64_t)e->host_hdr.arena_next;
   pb.out = e->log + e->host_hdr.end;
+  pb.links = e->links + e->host_hdr.end;
+  pb.srcd = e->srcd + e->host_hdr.end;
+  pb.vlen = e->vlen + e->host_hdr.end;
   launch_pub_build(pb, e->stream);
-  HIPCHECK(e, hipMemsetAsync(e->m_prior, 0, n, e->stream));  // (no message ids: no duplicates)
   std::vector<std::pair<uint64_t, uint8_t>> runs{{n, (uint8_t)0}};
-  return process_uploaded_messages(e, n, gran * 8, runs);
+  return process_uploaded_messages(e, n, u.gran * 8, runs, u.ttl > 0 ? 1 : 2);
 }
 
 int zb_submit_publishes(zb_engine* e, const char* name, int64_t ttl, size_t n, const uint8_t* cks,
@@ -3852,8 +3958,13 @@ int zb_outbox_count(zb_engine* e, int kind, uint64_t* n) {
   if (!e->on) return ZB_OK;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
   uint32_t* c = (uint32_t*)(e->h_stats_pinned + 19);  // (pinned: commands OPEN, CORRELATE, granules OPEN, CORRELATE)
-  HIPCHECK(e, hipMemcpyAsync(c, e->on, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
-  HIPCHECK(e, hipStreamSynchronize(e->stream));
+  if (!e->ob_counts_valid) {
+    StatusReads r;
+    r.add(c, e->on, 4 * sizeof(uint32_t));
+    HIPCHECK(e, r.launch(e->stream));
+    HIPCHECK(e, hipStreamSynchronize(e->stream));
+    e->ob_counts_valid = true;
+  }
   for (int k = 1; k <= 2; k++)
     if ((uint64_t)c[k - 1] > e->ocap || (uint64_t)c[k + 1] > e->ovar_cap)
       return fail(e, ZB_ENOMEM, "outbox overflow (commands or their variable bytes)");
@@ -3885,15 +3996,21 @@ int outbox_plan(zb_engine* e, int kind, uint64_t* bytes_per_target, uint64_t* co
   *total = 0;
   e->ob_plan_kind = 0;
   const int k = kind - 1;
+  if (e->on && e->ob_counts_valid && ((const uint32_t*)(e->h_stats_pinned + 19))[k] == 0)  // (nothing to take)
+    return zb_outbox_count(e, kind, n_out);
   // the key spread of the sort below, over the device-side count: read back in the count's round trip
-  if (e->on) {
+  if (e->on) {  // (the counters read again, in the spread's round trip)
     HIPCHECK(e, hipMemsetAsync(e->d_spread, 0, sizeof(uint64_t), e->stream));
     launch_key_spread(e->okeys[k], e->ocap, e->d_spread, e->stream, e->on + k);
-    HIPCHECK(e, hipMemcpyAsync(e->h_stats_pinned + 17, e->d_spread, sizeof(uint64_t), hipMemcpyDeviceToHost,
-                               e->stream));
+    StatusReads r;
+    r.add(e->h_stats_pinned + 17, e->d_spread, sizeof(uint64_t));
+    r.add(e->h_stats_pinned + 19, e->on, 4 * sizeof(uint32_t));
+    HIPCHECK(e, r.launch(e->stream));
+    HIPCHECK(e, hipStreamSynchronize(e->stream));
+    e->ob_counts_valid = true;
   }
   uint64_t n = 0;
-  int rc = zb_outbox_count(e, kind, &n);  // (its synchronisation covers the spread)
+  int rc = zb_outbox_count(e, kind, &n);
   if (rc != ZB_OK) return rc;
   *n_out = n;
   if (n == 0) return ZB_OK;
@@ -3959,6 +4076,10 @@ int outbox_emit(zb_engine* e, int kind, uint8_t* dst, uint64_t cap) {
                      e->stream);
   HIPCHECK(e, hipMemsetAsync(e->on + k, 0, sizeof(uint32_t), e->stream));      // the outbox is taken
   HIPCHECK(e, hipMemsetAsync(e->on + 2 + k, 0, sizeof(uint32_t), e->stream));  // (and its byte section)
+  if (e->ob_counts_valid) {  // (the other kind's counters are untouched: the read-back copy stays current)
+    uint32_t* c = (uint32_t*)(e->h_stats_pinned + 19);
+    c[k] = c[2 + k] = 0;
+  }
   // the commands written from here on come from records at or after the processing frontier
   e->ob_pos_base[k] = e->host_hdr.begin;
   return ZB_OK;  // (stream-ordered: the exchange's sends / the local delivery follow on the same stream)

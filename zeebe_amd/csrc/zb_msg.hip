@@ -98,19 +98,13 @@ __global__ void __launch_bounds__(256) k_msg_open(MsgParams P) {
     if (bat + bbytes > P.arena_cap) err |= DE_ARENA_FULL;
     else {
       b = P.arena + bat;
-      *(uint32_t*)b = blen;
-      for (uint64_t k = 4 + blen; k < bbytes; k++) b[k] = 0;
       sref = (uint32_t)(bat >> 3);
-    }
-    if (b) {
-      *(int32_t*)(b + 4) = r.wf_partition;
-      *(uint32_t*)(b + 8) = r.token;
-      *(uint16_t*)(b + 12) = r.elem;
-      *(uint16_t*)(b + 14) = 0;
-      *(uint32_t*)(b + 16) = r.name_len;
-      *(uint32_t*)(b + 20) = r.ck_len;
-      copy_bytes(b + SUB_HDR, name, r.name_len);
-      copy_bytes(b + SUB_HDR + r.name_len, ck, r.ck_len);
+      WordWriter w(b);  // (the SUB_HDR words, then name + key: contiguous in the batch's variable bytes)
+      w.push((uint64_t)blen | (uint64_t)(uint32_t)r.wf_partition << 32, 8);
+      w.push((uint64_t)r.token | (uint64_t)r.elem << 32, 8);
+      w.push((uint64_t)r.name_len | (uint64_t)r.ck_len << 32, 8);
+      w.bytes(name, r.name_len + r.ck_len);
+      w.finish();
     }
     zb_rec d;
     d.key = pos;  // positionAsKey (SubscriptionApiCommandMessageHandler.java:144-149)
@@ -214,8 +208,13 @@ __global__ void __launch_bounds__(256) k_pub_emit(MsgParams P) {
   if (act) {
     d = P.log[pos];
     v = msg_view(P.arena, d.payload);
-    acc = (P.cnt[i] >> PC_ACC) & 1;
-    off = P.cnt_off[i];
+    if (P.uni_out) {  // (the closed form of k_pub_count + scan for a batch without message ids)
+      acc = true;
+      off = (uint64_t)i * (uint64_t)P.uni_out | (uint64_t)i << PC_ACC | (P.uni_out == 1 ? (uint64_t)i << PC_STORED : 0);
+    } else {
+      acc = (P.cnt[i] >> PC_ACC) & 1;
+      off = P.cnt_off[i];
+    }
     const int64_t fpos = P.out_base + (int64_t)(off & PC_MASK);
     zb_rec f = d;  // follow-ups re-encode record.getValue(): the message blob, not the verbatim command value
     if (!acc) {  // writeRejection(record, BAD_VALUE, "message with id '%s' is already published")
@@ -356,13 +355,12 @@ __global__ void __launch_bounds__(256) k_wis_inject(MsgParams P) {
   if (bat + bbytes > P.arena_cap) err |= DE_ARENA_FULL;
   else {
     b = P.arena + bat;
-    *(uint32_t*)b = blen;
-    for (uint64_t k = 4 + blen; k < bbytes; k++) b[k] = 0;
     ref = (uint32_t)(bat >> 3);
-  }
-  if (b) {
-    if (empty) b[4] = 0x80;
-    else copy_bytes(b + 4, pl, np);
+    WordWriter w(b);
+    w.push(blen, 4);
+    if (empty) w.push(0x80, 1);
+    else w.bytes(pl, np);
+    w.finish();
   }
   const int64_t pos = P.base + i;
   zb_rec d;
@@ -373,9 +371,17 @@ __global__ void __launch_bounds__(256) k_wis_inject(MsgParams P) {
   d.elem = r.elem;
   d.intent = 0;  // CORRELATE
   d.kind = make_kind(ZB_VT_WORKFLOW_INSTANCE_SUBSCRIPTION, ZB_RT_COMMAND, false);
-  // row_self: found by activity instance key (k_resolve after this kernel; the sender's row token can be stale
-  // once the workflow partition compacted its rows)
   put_record(P, pos, d, 0);
+  // row_self (ElementInstanceIndex.getInstance(activityInstanceKey)): the row the subscription's token names when it
+  // is live and holds the key -- rows are never reused and a key names at most one live row, so that row is the
+  // instance. A token from another partition's numbering, or stale after this partition compacted its rows, is
+  // counted instead: the host then sorts the keys and k_resolve searches the rows for them.
+  const uint32_t t = r.token;
+  const bool hit = t < P.rows && P.rmeta[t].state != 0 && P.rkeys[t].key == r.activity_instance_key;
+  if (hit) P.links[pos] = 0xffffffff00000000ull | t;  // (the row-self half; no parent link)
+  const uint64_t miss = __ballot(!hit);
+  if (miss && (threadIdx.x & 63) == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1))
+    atomicAdd(P.unresolved, (uint32_t)__popcll(miss));
   P.lookup_keys[i] = r.activity_instance_key;
   P.lookup_pos[i] = pos;
   flag_error(P, err);
@@ -454,30 +460,26 @@ __global__ void k_pub_build(PubBuild p) {
   const bool empty = np == 0 || (np == 1 && pl[0] == 0xc0);
   if (empty) np = 1;
   const uint32_t len = MSG_HDR - 4 + p.nn + nc + np;
-  uint32_t* h = (uint32_t*)b;
-  h[0] = len; h[1] = p.nn;
-  *(int64_t*)(b + 8) = p.ttl;
-  *(int64_t*)(b + 16) = 0;  // deadline: set when the message is stored
-  h[6] = nc; h[7] = np; h[8] = 0; h[9] = 0;
-  // name, correlation key, payload (and the zero padding) as whole 8-byte words (b + MSG_HDR is 8-aligned)
-  uint64_t* d = (uint64_t*)(b + MSG_HDR);
-  const uint32_t n_all = p.nn + nc + np;
-  uint64_t acc = 0;
-  for (uint32_t k = 0; k < n_all; k++) {
-    const uint8_t x = k < p.nn ? p.name[k] : k < p.nn + nc ? ck[k - p.nn] : empty ? (uint8_t)0x80 : pl[k - p.nn - nc];
-    acc |= (uint64_t)x << (8 * (k & 7));
-    if ((k & 7) == 7) {
-      d[k >> 3] = acc;
-      acc = 0;
-    }
-  }
-  if (n_all & 7) d[n_all >> 3] = acc;
+  WordWriter w(b);  // MSG_HDR, then name, correlation key, payload (and the zero padding) as whole 8-byte words
+  w.push((uint64_t)len | (uint64_t)p.nn << 32, 8);
+  w.push((uint64_t)p.ttl, 8);
+  w.push(0, 8);  // deadline: set when the message is stored
+  w.push((uint64_t)nc | (uint64_t)np << 32, 8);
+  w.push(0, 8);  // (no message id; pad)
+  w.bytes(p.name, p.nn);
+  w.bytes(ck, nc);
+  if (empty) w.push(0x80, 1);
+  else w.bytes(pl, np);
+  w.finish();
   zb_rec r;
   r.key = -1; r.scope_key = -1; r.inst_key = -1;
   r.payload = (uint32_t)(at >> 3);
   r.elem = NO_ELEM; r.intent = 0;  // PUBLISH
   r.kind = make_kind(ZB_VT_MESSAGE, ZB_RT_COMMAND, false);
   p.out[i] = r;
+  p.links[i] = ~0ull;
+  p.srcd[i] = 0;             // (submitted: no source record)
+  p.vlen[i] = VLEN_UNKNOWN;  // (the size pass measures it)
 }
 
 __global__ void k_iota(uint32_t* p, uint64_t n) {

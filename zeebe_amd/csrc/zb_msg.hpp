@@ -67,19 +67,29 @@ __device__ __forceinline__ int32_t subscription_partition(const uint8_t* ck, uin
   return r < 0 ? -r : r;
 }
 
-// store hash of (message name, correlation key); equality is always re-checked on the bytes
-__device__ __forceinline__ uint64_t fnv_bytes(uint64_t h, const uint8_t* p, uint32_t n) {
-  for (uint32_t i = 0; i < n; i++) {
-    h ^= p[i];
-    h *= 0x100000001b3ull;
+// store hash of (message name, correlation key): FNV-1a over the bytes, read as the aligned words that hold them (a
+// byte loop was a memory request per byte); equality is always re-checked on the bytes
+__device__ __forceinline__ uint64_t fnv_words(uint64_t h, const uint8_t* s, uint32_t n) {
+  if (!n) return h;
+  const uint64_t* a = (const uint64_t*)((uintptr_t)s & ~(uintptr_t)7);
+  uint32_t off = (uint32_t)((uintptr_t)s & 7);
+  while (n) {
+    uint64_t w = *a++ >> (8 * off);
+    const uint32_t take = 8 - off < n ? 8 - off : n;
+    for (uint32_t k = 0; k < take; k++) {
+      h ^= (uint8_t)(w >> (8 * k));
+      h *= 0x100000001b3ull;
+    }
+    n -= take;
+    off = 0;
   }
   return h;
 }
 __device__ __forceinline__ uint64_t name_ck_hash(const uint8_t* name, uint32_t nn, const uint8_t* ck, uint32_t nc) {
-  uint64_t h = fnv_bytes(0xcbf29ce484222325ull, name, nn);
+  uint64_t h = fnv_words(0xcbf29ce484222325ull, name, nn);
   h ^= 0x1ff;
   h *= 0x100000001b3ull;
-  return fnv_bytes(h, ck, nc);
+  return fnv_words(h, ck, nc);
 }
 
 // outbox order: (target partition, source log position, emission index) — the order in which the
@@ -172,9 +182,45 @@ __device__ __forceinline__ uint32_t var_granules(uint32_t nn, uint32_t nc, uint3
   return (nn + nc + np + 7) >> 3;
 }
 
-__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint32_t n) {
-  for (uint32_t i = 0; i < n; i++) dst[i] = src[i];
-}
+// Bytes appended to an 8-aligned destination as whole 8-byte words: a byte loop was one memory request per byte
+// (the message kernels were bound by them). Sources are read as the aligned words that hold them (a load never
+// reaches past the aligned word of a source's last byte, so never past its allocation's page); the last word is
+// zero-padded, and nothing is written past it.
+struct WordWriter {
+  uint64_t* d;
+  uint64_t acc;
+  uint32_t fill;  // bytes in acc (< 8)
+  __device__ __forceinline__ explicit WordWriter(uint8_t* dst) : d((uint64_t*)dst), acc(0), fill(0) {}
+  // the low nb bytes of w (1 <= nb <= 8; the bytes above them zero)
+  __device__ __forceinline__ void push(uint64_t w, uint32_t nb) {
+    acc |= w << (8 * fill);
+    const uint32_t f = fill + nb;
+    if (f >= 8) {
+      *d++ = acc;
+      acc = fill ? (w >> (8 * (8 - fill))) : 0;
+      fill = f - 8;
+    } else {
+      fill = f;
+    }
+  }
+  __device__ __forceinline__ void bytes(const uint8_t* s, uint32_t n) {
+    if (!n) return;
+    const uint64_t* a = (const uint64_t*)((uintptr_t)s & ~(uintptr_t)7);
+    uint32_t off = (uint32_t)((uintptr_t)s & 7);
+    while (n) {
+      const uint32_t take = 8 - off < n ? 8 - off : n;
+      uint64_t w = *a++ >> (8 * off);
+      if (take < 8) w &= (1ull << (8 * take)) - 1;
+      push(w, take);
+      n -= take;
+      off = 0;
+    }
+  }
+  __device__ __forceinline__ void finish() {
+    if (fill) *d = acc;
+  }
+};
+
 // false (nothing written): the source position or the emission index does not fit the order key -- the caller fails
 // the partition (DE_UNSUPPORTED) rather than ordering the exchange wrongly
 __device__ __forceinline__ bool outbox_write(const Outbox& ob, uint32_t slot, uint32_t var_at, int32_t kind, int32_t target,
@@ -189,11 +235,11 @@ __device__ __forceinline__ bool outbox_write(const Outbox& ob, uint32_t slot, ui
   r.elem = elem; r.pad = 0;
   r.name_len = nn; r.ck_len = nc; r.payload_len = np;
   r.var_offset = (uint64_t)var_at * 8;
-  uint8_t* v = ob.var + (uint64_t)var_at * 8;
-  copy_bytes(v, name, nn);
-  copy_bytes(v + nn, ck, nc);
-  copy_bytes(v + nn + nc, payload, np);
-  for (uint32_t i = nn + nc + np; i < var_granules(nn, nc, np) * 8; i++) v[i] = 0;
+  WordWriter v(ob.var + (uint64_t)var_at * 8);  // (exactly var_granules(nn, nc, np) words, zero-padded)
+  v.bytes(name, nn);
+  v.bytes(ck, nc);
+  v.bytes(payload, np);
+  v.finish();
   ob.rec[slot] = r;
   ob.keys[slot] = outbox_key(target, rel, emission);
   return true;

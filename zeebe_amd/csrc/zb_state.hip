@@ -67,6 +67,11 @@ __global__ void __launch_bounds__(256) k_row_descs(LiveParams P) {
   P.heads[i] = h;
 }
 
+__global__ void __launch_bounds__(64) k_status(StatusCopy c) {
+  for (int k = 0; k < c.count; k++)
+    for (uint32_t i = threadIdx.x; i < c.words[k]; i += 64) c.dst[k][i] = c.src[k][i];
+}
+
 void launch_resolve(const ResolveParams& p, hipStream_t s) {
   if (p.rows == 0 || p.n == 0) return;
   const uint64_t g = (p.rows + 255) / 256;
@@ -80,6 +85,10 @@ void launch_live_rows(const LiveParams& p, hipStream_t s) {
 void launch_row_descs(const LiveParams& p, hipStream_t s) {
   if (p.n == 0) return;
   hipLaunchKernelGGL(k_row_descs, dim3((unsigned)((p.n + 255) / 256)), dim3(256), 0, s, p);
+}
+
+void launch_status(const StatusCopy& c, hipStream_t s) {
+  if (c.count) hipLaunchKernelGGL(k_status, dim3(1), dim3(64), 0, s, c);
 }
 
 }  // namespace zbg
