@@ -280,7 +280,9 @@ int zb_comm_unique_id(uint8_t id[128]);
  * loaded another copy of the library first -- e.g. torch's -- resolves to that one: load libzbgpu.so first). */
 const char* zb_rccl_library(void);
 int zb_comm_init(zb_engine* e, const uint8_t id[128], int nranks, int rank);
-/* Collective: global[k] = sum over ranks of the pending commands of kind k+1 (ZB_XCHG_OPEN, _CORRELATE). */
+/* A single partition (partition_count 1, no ZB_CFG_RCCL_SELF) needs no zb_comm_init: its exchange delivers its outbox
+ * to its own inbox on the device, without a collective.
+ * Collective: global[k] = sum over ranks of the pending commands of kind k+1 (ZB_XCHG_OPEN, _CORRELATE). */
 int zb_comm_pending(zb_engine* e, uint64_t global[2]);
 /* Collective: every rank takes its pending commands of `kind` (zb_outbox_take order), sends each target
  * its batch (ncclSend / ncclRecv in one group), and delivers what it receives in source-rank order

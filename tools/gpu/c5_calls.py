@@ -7,6 +7,10 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+if os.environ.get("ZB_SYSRT"):  # bind the system HIP runtime first, as bench.py's main does
+    from zeebe_amd.engine import lib  # noqa: E402
+
+    lib()
 
 import bench  # noqa: E402
 from zeebe_amd import engine as zbe  # noqa: E402

@@ -191,7 +191,9 @@ class DistCluster:
         self.device = device if device is not None else torch.device("cpu")
         self.rounds = 0
         self.rccl = hasattr(partition, "comm_exchange") if rccl is None else rccl
-        if self.rccl:
+        # (one partition with no collective to run: its exchange is a device-side delivery to itself, no communicator)
+        needs = getattr(partition, "needs_communicator", lambda: True)()
+        if self.rccl and needs:
             # the 128-byte RCCL id travels over the control plane; the data path is RCCL (xGMI)
             obj = [partition.comm_unique_id() if self.rank == 0 else None]
             dist.broadcast_object_list(obj, src=0, group=group)

@@ -4162,9 +4162,15 @@ int comm_fail(zb_engine* e, const std::string& what, ncclResult_t r) {
 
 extern "C" {
 
+// a single partition without ZB_CFG_RCCL_SELF exchanges with itself on the device: it needs no communicator
+static bool comm_local(const zb_engine* e) {
+  return e->cfg.partition_count == 1 && !(e->cfg.flags & ZB_CFG_RCCL_SELF);
+}
+
 int zb_comm_pending(zb_engine* e, uint64_t global[2]) {
   if (!e || !global) return ZB_EINVAL;
-  if (!e->comm) return e->comm_broken ? fail(e, ZB_EDEVICE, "communicator aborted after an earlier failure") : ZB_EINVAL;
+  if (!e->comm && !comm_local(e))
+    return e->comm_broken ? fail(e, ZB_EDEVICE, "communicator aborted after an earlier failure") : ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
   uint64_t local[2] = {0, 0};
   int rc0 = zb_outbox_count(e, ZB_XCHG_OPEN, &local[0]);  // (one read of both counts)
@@ -4189,7 +4195,8 @@ int zb_comm_pending(zb_engine* e, uint64_t global[2]) {
 // only (zb_checked.hpp), ZB_FAIL_EXCHANGE=<rank> makes that rank's local step fail.
 int zb_comm_exchange(zb_engine* e, int kind, uint64_t* received) {
   if (!e || !received || (kind != ZB_XCHG_OPEN && kind != ZB_XCHG_CORRELATE)) return ZB_EINVAL;
-  if (!e->comm) return e->comm_broken ? fail(e, ZB_EDEVICE, "communicator aborted after an earlier failure") : ZB_EINVAL;
+  if (!e->comm && !comm_local(e))
+    return e->comm_broken ? fail(e, ZB_EDEVICE, "communicator aborted after an earlier failure") : ZB_EINVAL;
   HIPCHECK(e, hipSetDevice(e->cfg.device));
   const int P = e->cfg.partition_count;
   *received = 0;

@@ -558,6 +558,11 @@ class Engine:
     def comm_init(self, unique_id: bytes, nranks: int, rank: int):
         self._check(self._L.zb_comm_init(self._h, unique_id, nranks, rank))
 
+    def needs_communicator(self) -> bool:
+        """A single partition delivers its outbox to its own inbox on the device: no RCCL communicator (unless
+        CFG_RCCL_SELF asks for the collective path anyway)."""
+        return self._parts > 1 or bool(self._flags & CFG_RCCL_SELF)
+
     def comm_pending(self):
         g = (ctypes.c_uint64 * 2)()
         self._check(self._L.zb_comm_pending(self._h, g))
