@@ -352,6 +352,9 @@ struct zb_engine {
   // inbox CORRELATE resolution by activity instance key (zb_inbox_submit)
   int64_t *x_keys = nullptr, *x_pos = nullptr, *x_keys2 = nullptr, *x_pos2 = nullptr;
   uint32_t* d_unresolved = nullptr;  // delivered CORRELATEs whose token named no live row of their key (running count)
+  uint32_t *cs_cnt = nullptr, *cs_off = nullptr;  // the outbox's counting sort: buckets, their exclusive scan
+  void* cs_tmp = nullptr;
+  uint64_t cs_cap = 0, cs_tmp_cap = 0;
   uint32_t unresolved_seen = 0;
   uint64_t x_cap = 0;
   DevVec<int64_t> d_lookup_keys, d_lookup_pos;    // zb_submit lookups of the staged batch: key, staged index
@@ -1617,7 +1620,8 @@ void zb_engine_destroy(zb_engine* e) {
   void* ms[] = {e->obox[0], e->obox[1], e->okeys[0], e->okeys[1], e->ovar[0], e->ovar[1], e->on, e->subs, e->sub_head,
                 e->sub_next, e->msgs, e->msg_head, e->msg_next, e->d_xcounts, e->xsend, e->xrecv, e->ob_keys, e->ob_idx_in,
                 e->ob_idx_out, e->ob_first, e->ob_sizes, e->ob_goff, e->ob_table, e->ob_base, e->ob_tmp, e->ob_staging,
-                e->m_prior, e->m_cnt, e->m_tmp, e->in_buf, e->p_in, e->p_gran, e->d_unresolved};
+                e->m_prior, e->m_cnt, e->m_tmp, e->in_buf, e->p_in, e->p_gran, e->d_unresolved, e->cs_cnt, e->cs_off,
+                e->cs_tmp};
   for (void* p : ms)
     if (p) (void)hipFree(p);
   if (e->h_hdr_pinned) (void)hipHostFree(e->h_hdr_pinned);
@@ -4026,10 +4030,43 @@ int outbox_plan(zb_engine* e, int kind, uint64_t* bytes_per_target, uint64_t* co
       return fail(e, ZB_ENOMEM, "outbox scan scratch");
     if (hipMalloc(&e->ob_tmp, e->ob_tmp_bytes + 16) != hipSuccess) return fail(e, ZB_ENOMEM, "outbox scan scratch");
   }
-  launch_iota(e->ob_idx_in, n, e->stream);
-  rc = sort_pairs(e, (const uint64_t*)e->okeys[k], e->ob_keys, (const uint32_t*)e->ob_idx_in, e->ob_idx_out, n, "outbox",
-                  true);
-  if (rc != ZB_OK) return rc;
+  // the sort: by counting when the keys' spread is narrow and dense enough (a tick's commands: a position range a
+  // few times the command count), else the radix sort over the spread's bits
+  const uint64_t spread = e->h_stats_pinned[17];
+  const int cs_begin = spread ? __builtin_ctzll(spread) : 0;
+  const int cs_bits = spread ? 64 - __builtin_clzll(spread) - cs_begin : 0;
+  if (spread && cs_bits <= 24 && (1ull << cs_bits) <= 32 * n) {
+    const uint64_t nb = 1ull << cs_bits;
+    size_t tmp = 0;
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->cs_cnt, e->cs_off, (int)nb, e->stream) != hipSuccess)
+      return fail(e, ZB_EDEVICE, "outbox count scan sizing");
+    if (nb > e->cs_cap || tmp + 16 > e->cs_tmp_cap) {
+      HIPCHECK(e, hipStreamSynchronize(e->stream));
+      void* ps[] = {e->cs_cnt, e->cs_off, e->cs_tmp};
+      for (void* q : ps)
+        if (q) (void)hipFree(q);
+      e->cs_cnt = e->cs_off = nullptr;
+      e->cs_tmp = nullptr;
+      e->cs_cap = e->cs_tmp_cap = 0;
+      HIPCHECK(e, hipMalloc(&e->cs_cnt, nb * 4));
+      HIPCHECK(e, hipMalloc(&e->cs_off, nb * 4));
+      HIPCHECK(e, hipMalloc(&e->cs_tmp, tmp + 16));
+      e->cs_cap = nb;
+      e->cs_tmp_cap = tmp + 16;
+    }
+    HIPCHECK(e, hipMemsetAsync(e->cs_cnt, 0, nb * 4, e->stream));
+    launch_cs_hist((const uint64_t*)e->okeys[k], n, cs_begin, cs_bits, e->cs_cnt, e->stream);
+    size_t have = e->cs_tmp_cap;
+    if (hipcub::DeviceScan::ExclusiveSum(e->cs_tmp, have, e->cs_cnt, e->cs_off, (int)nb, e->stream) != hipSuccess)
+      return fail(e, ZB_EDEVICE, "outbox count scan");
+    launch_cs_scatter((const uint64_t*)e->okeys[k], n, cs_begin, cs_bits, e->cs_off, e->ob_keys, e->ob_idx_out,
+                      e->stream);
+  } else {
+    launch_iota(e->ob_idx_in, n, e->stream);
+    rc = sort_pairs(e, (const uint64_t*)e->okeys[k], e->ob_keys, (const uint32_t*)e->ob_idx_in, e->ob_idx_out, n,
+                    "outbox", true);
+    if (rc != ZB_OK) return rc;
+  }
   const Outbox ob = outbox(e, kind);
   launch_outbox_sizes(ob, e->ob_idx_out, n, e->ob_sizes, e->stream);
   size_t tmp_bytes = e->ob_tmp_bytes;

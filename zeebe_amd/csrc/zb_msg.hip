@@ -482,6 +482,25 @@ __global__ void k_pub_build(PubBuild p) {
   p.vlen[i] = VLEN_UNKNOWN;  // (the size pass measures it)
 }
 
+// the outbox order by counting: the keys of one take differ only in the bits of their spread (k_key_spread), and a
+// take's keys are distinct (a source position emits one command per emission index), so their ranks are the
+// exclusive scan of the per-bucket counts over those bits -- one histogram, one scan, one scatter instead of the
+// radix sort's passes (equal keys, were there any, keep no particular order: neither did the outbox slots)
+__global__ void __launch_bounds__(256) k_cs_hist(const uint64_t* keys, uint64_t n, int begin, uint64_t mask,
+                                                 uint32_t* cnt) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) atomicAdd(&cnt[(keys[i] >> begin) & mask], 1u);
+}
+__global__ void __launch_bounds__(256) k_cs_scatter(const uint64_t* keys, uint64_t n, int begin, uint64_t mask,
+                                                    uint32_t* off, uint64_t* kout, uint32_t* vout) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t k = keys[i];
+  const uint32_t p = atomicAdd(&off[(k >> begin) & mask], 1u);
+  kout[p] = k;
+  vout[p] = (uint32_t)i;
+}
+
 __global__ void k_iota(uint32_t* p, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = (uint32_t)i;
@@ -551,6 +570,15 @@ void launch_outbox_table(const uint64_t* first, const uint32_t* goff, int parts,
 void launch_outbox_pack(const Outbox& ob, const uint32_t* idx, const uint64_t* keys, uint64_t n, const uint64_t* first,
                         const uint32_t* goff, const uint64_t* base, uint8_t* dst, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_outbox_pack, dim3(blocks((int64_t)n)), dim3(256), 0, s, ob, idx, keys, n, first, goff, base, dst);
+}
+void launch_cs_hist(const uint64_t* keys, uint64_t n, int begin, int bits, uint32_t* cnt, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_cs_hist, dim3(blocks((int64_t)n)), dim3(256), 0, s, keys, n, begin, (1ull << bits) - 1, cnt);
+}
+void launch_cs_scatter(const uint64_t* keys, uint64_t n, int begin, int bits, uint32_t* off, uint64_t* kout,
+                       uint32_t* vout, hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(k_cs_scatter, dim3(blocks((int64_t)n)), dim3(256), 0, s, keys, n, begin, (1ull << bits) - 1, off,
+                       kout, vout);
 }
 void launch_iota(uint32_t* p, uint64_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_iota, dim3(blocks((int64_t)n)), dim3(256), 0, s, p, n);
