@@ -352,9 +352,11 @@ struct zb_engine {
   // inbox CORRELATE resolution by activity instance key (zb_inbox_submit)
   int64_t *x_keys = nullptr, *x_pos = nullptr, *x_keys2 = nullptr, *x_pos2 = nullptr;
   uint32_t* d_unresolved = nullptr;  // delivered CORRELATEs whose token named no live row of their key (running count)
-  uint32_t *cs_cnt = nullptr, *cs_off = nullptr;  // the outbox's counting sort: buckets, their exclusive scan
+  // the outbox's counting sort: per bucket (commands << 40 | variable granules), their exclusive scan
+  unsigned long long *cs_cnt = nullptr, *cs_off = nullptr;
   void* cs_tmp = nullptr;
   uint64_t cs_cap = 0, cs_tmp_cap = 0;
+  bool ob_plan_cs = false;  // the plan is a local batch from the counting sort (outbox_emit: k_local_pack)
   uint32_t unresolved_seen = 0;
   uint64_t x_cap = 0;
   DevVec<int64_t> d_lookup_keys, d_lookup_pos;    // zb_submit lookups of the staged batch: key, staged index
@@ -465,7 +467,7 @@ struct StatusReads {
 };
 
 // The exact-tree workspaces (zb_xmerge.hpp) of one device, shared by every engine on it: slabs and lane groups are held
-// under device-wide locks (zb_xlock.hpp), so the partitions of one GPU need one set, not 2 GiB each. Taken by the first
+// under device-wide locks (zb_xlock.hpp), so the partitions of one GPU need one set, not 4 GiB each. Taken by the first
 // engine whose model merges or maps, freed with the last. Lanes that cannot be allocated leave the engines on the big-slab
 // path (XTree with lanes == nullptr) instead of failing the deploy.
 struct XPool {
@@ -4035,6 +4037,8 @@ int outbox_plan(zb_engine* e, int kind, uint64_t* bytes_per_target, uint64_t* co
   const uint64_t spread = e->h_stats_pinned[17];
   const int cs_begin = spread ? __builtin_ctzll(spread) : 0;
   const int cs_bits = spread ? 64 - __builtin_clzll(spread) - cs_begin : 0;
+  const Outbox ob = outbox(e, kind);
+  e->ob_plan_cs = false;
   if (spread && cs_bits <= 24 && (1ull << cs_bits) <= 32 * n) {
     const uint64_t nb = 1ull << cs_bits;
     size_t tmp = 0;
@@ -4048,26 +4052,36 @@ int outbox_plan(zb_engine* e, int kind, uint64_t* bytes_per_target, uint64_t* co
       e->cs_cnt = e->cs_off = nullptr;
       e->cs_tmp = nullptr;
       e->cs_cap = e->cs_tmp_cap = 0;
-      HIPCHECK(e, hipMalloc(&e->cs_cnt, nb * 4));
-      HIPCHECK(e, hipMalloc(&e->cs_off, nb * 4));
+      HIPCHECK(e, hipMalloc(&e->cs_cnt, nb * 8));
+      HIPCHECK(e, hipMalloc(&e->cs_off, nb * 8));
       HIPCHECK(e, hipMalloc(&e->cs_tmp, tmp + 16));
       e->cs_cap = nb;
       e->cs_tmp_cap = tmp + 16;
     }
-    HIPCHECK(e, hipMemsetAsync(e->cs_cnt, 0, nb * 4, e->stream));
-    launch_cs_hist((const uint64_t*)e->okeys[k], n, cs_begin, cs_bits, e->cs_cnt, e->stream);
+    HIPCHECK(e, hipMemsetAsync(e->cs_cnt, 0, nb * 8, e->stream));
+    launch_cs_hist(ob, n, cs_begin, cs_bits, e->cs_cnt, e->stream);
     size_t have = e->cs_tmp_cap;
     if (hipcub::DeviceScan::ExclusiveSum(e->cs_tmp, have, e->cs_cnt, e->cs_off, (int)nb, e->stream) != hipSuccess)
       return fail(e, ZB_EDEVICE, "outbox count scan");
-    launch_cs_scatter((const uint64_t*)e->okeys[k], n, cs_begin, cs_bits, e->cs_off, e->ob_keys, e->ob_idx_out,
-                      e->stream);
+    if (local && P == 1) {  // the slots and variable places come out of the scatter (outbox_emit: k_local_pack)
+      launch_cs_scatter(ob, n, cs_begin, cs_bits, e->cs_off, nullptr, e->ob_idx_out, e->ob_goff, e->stream);
+      const uint32_t* c = (const uint32_t*)(e->h_stats_pinned + 19);
+      counts[0] = n;
+      bytes_per_target[0] = ZB_XCHG_BATCH_HEADER + n * sizeof(zb_exchange_rec) + 8 * (uint64_t)c[kind + 1];
+      *total = bytes_per_target[0];
+      e->ob_plan_cs = true;
+      e->ob_plan_kind = kind;
+      e->ob_plan_n = n;
+      e->ob_plan_total = *total;
+      return ZB_OK;
+    }
+    launch_cs_scatter(ob, n, cs_begin, cs_bits, e->cs_off, e->ob_keys, e->ob_idx_out, nullptr, e->stream);
   } else {
     launch_iota(e->ob_idx_in, n, e->stream);
     rc = sort_pairs(e, (const uint64_t*)e->okeys[k], e->ob_keys, (const uint32_t*)e->ob_idx_in, e->ob_idx_out, n,
                     "outbox", true);
     if (rc != ZB_OK) return rc;
   }
-  const Outbox ob = outbox(e, kind);
   launch_outbox_sizes(ob, e->ob_idx_out, n, e->ob_sizes, e->stream);
   size_t tmp_bytes = e->ob_tmp_bytes;
   if (hipcub::DeviceScan::ExclusiveSum(e->ob_tmp, tmp_bytes, e->ob_sizes, e->ob_goff, (int)(n + 1), e->stream) != hipSuccess)
@@ -4108,11 +4122,16 @@ int outbox_emit(zb_engine* e, int kind, uint8_t* dst, uint64_t cap) {
   if (e->ob_plan_total > cap) return fail(e, ZB_ENOMEM, "outbox destination too small");
   const int P = e->cfg.partition_count;
   const int k = kind - 1;
-  HIPCHECK(e, upload_async(e, e->ob_base, e->ob_plan_base, P * 8));
-  launch_outbox_pack(outbox(e, kind), e->ob_idx_out, e->ob_keys, e->ob_plan_n, e->ob_first, e->ob_goff, e->ob_base, dst,
-                     e->stream);
-  HIPCHECK(e, hipMemsetAsync(e->on + k, 0, sizeof(uint32_t), e->stream));      // the outbox is taken
-  HIPCHECK(e, hipMemsetAsync(e->on + 2 + k, 0, sizeof(uint32_t), e->stream));  // (and its byte section)
+  if (e->ob_plan_cs) {  // one batch in the counting sort's order; the pack also takes the outbox
+    launch_local_pack(outbox(e, kind), e->ob_idx_out, e->ob_goff, e->ob_plan_n, e->ob_plan_total, dst, e->on + k,
+                      e->on + 2 + k, e->stream);
+  } else {
+    HIPCHECK(e, upload_async(e, e->ob_base, e->ob_plan_base, P * 8));
+    launch_outbox_pack(outbox(e, kind), e->ob_idx_out, e->ob_keys, e->ob_plan_n, e->ob_first, e->ob_goff, e->ob_base,
+                       dst, e->stream);
+    HIPCHECK(e, hipMemsetAsync(e->on + k, 0, sizeof(uint32_t), e->stream));      // the outbox is taken
+    HIPCHECK(e, hipMemsetAsync(e->on + 2 + k, 0, sizeof(uint32_t), e->stream));  // (and its byte section)
+  }
   if (e->ob_counts_valid) {  // (the other kind's counters are untouched: the read-back copy stays current)
     uint32_t* c = (uint32_t*)(e->h_stats_pinned + 19);
     c[k] = c[2 + k] = 0;

@@ -483,22 +483,57 @@ __global__ void k_pub_build(PubBuild p) {
 }
 
 // the outbox order by counting: the keys of one take differ only in the bits of their spread (k_key_spread), and a
-// take's keys are distinct (a source position emits one command per emission index), so their ranks are the
+// take's keys are distinct (a source position emits one command per emission index), so a command's slot is the
 // exclusive scan of the per-bucket counts over those bits -- one histogram, one scan, one scatter instead of the
-// radix sort's passes (equal keys, were there any, keep no particular order: neither did the outbox slots)
-__global__ void __launch_bounds__(256) k_cs_hist(const uint64_t* keys, uint64_t n, int begin, uint64_t mask,
-                                                 uint32_t* cnt) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) atomicAdd(&cnt[(keys[i] >> begin) & mask], 1u);
-}
-__global__ void __launch_bounds__(256) k_cs_scatter(const uint64_t* keys, uint64_t n, int begin, uint64_t mask,
-                                                    uint32_t* off, uint64_t* kout, uint32_t* vout) {
+// radix sort's passes. A bucket holds (commands << 40 | variable granules): one atomic gives a command both its slot
+// and its variable bytes' place (equal keys, were there any, keep no particular order: neither did the outbox slots)
+constexpr int CS_SHIFT = 40;
+__global__ void __launch_bounds__(256) k_cs_hist(Outbox ob, uint64_t n, int begin, uint64_t mask,
+                                                 unsigned long long* cnt) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint64_t k = keys[i];
-  const uint32_t p = atomicAdd(&off[(k >> begin) & mask], 1u);
-  kout[p] = k;
+  const zb_exchange_rec& r = ob.rec[i];
+  const uint32_t g = var_granules(r.name_len, r.ck_len, r.payload_len);
+  atomicAdd(&cnt[(ob.keys[i] >> begin) & mask], (1ull << CS_SHIFT) | g);
+}
+// every command's slot in key order: its key and index (kout may be null), and with goff its variable granules' place
+__global__ void __launch_bounds__(256) k_cs_scatter(Outbox ob, uint64_t n, int begin, uint64_t mask,
+                                                    unsigned long long* off, uint64_t* kout, uint32_t* vout,
+                                                    uint32_t* goff) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t k = ob.keys[i];
+  uint64_t add = 1ull << CS_SHIFT;
+  if (goff) {
+    const zb_exchange_rec& r = ob.rec[i];
+    add |= var_granules(r.name_len, r.ck_len, r.payload_len);
+  }
+  const uint64_t o = atomicAdd(&off[(k >> begin) & mask], add);
+  const uint64_t p = o >> CS_SHIFT;
+  if (kout) kout[p] = k;
   vout[p] = (uint32_t)i;
+  if (goff) goff[p] = (uint32_t)(o & ((1ull << CS_SHIFT) - 1));
+}
+// a partition delivering to itself: its one exchange batch, written in key order (coalesced stores: the records and
+// their variable bytes are read where the outbox holds them); the outbox is taken
+__global__ void __launch_bounds__(256) k_local_pack(Outbox ob, const uint32_t* idx, const uint32_t* goff, uint64_t n,
+                                                    uint64_t total, uint8_t* dst, uint32_t* taken_n,
+                                                    uint32_t* taken_var) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) {  // the batch header; the outbox is taken (stream order: nothing in flight reads the counters)
+    ((uint64_t*)dst)[0] = n;
+    ((uint64_t*)dst)[1] = total;
+    *taken_n = 0;
+    *taken_var = 0;
+  }
+  if (i >= n) return;
+  zb_exchange_rec r = ob.rec[idx[i]];
+  const uint32_t g = var_granules(r.name_len, r.ck_len, r.payload_len);
+  const uint64_t* src = (const uint64_t*)(ob.var + r.var_offset);
+  r.var_offset = 8 * (uint64_t)goff[i];
+  ((zb_exchange_rec*)(dst + ZB_XCHG_BATCH_HEADER))[i] = r;
+  uint64_t* vd = (uint64_t*)(dst + ZB_XCHG_BATCH_HEADER + n * sizeof(zb_exchange_rec) + r.var_offset);
+  for (uint32_t k = 0; k < g; k++) vd[k] = src[k];
 }
 
 __global__ void k_iota(uint32_t* p, uint64_t n) {
@@ -571,14 +606,19 @@ void launch_outbox_pack(const Outbox& ob, const uint32_t* idx, const uint64_t* k
                         const uint32_t* goff, const uint64_t* base, uint8_t* dst, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_outbox_pack, dim3(blocks((int64_t)n)), dim3(256), 0, s, ob, idx, keys, n, first, goff, base, dst);
 }
-void launch_cs_hist(const uint64_t* keys, uint64_t n, int begin, int bits, uint32_t* cnt, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_cs_hist, dim3(blocks((int64_t)n)), dim3(256), 0, s, keys, n, begin, (1ull << bits) - 1, cnt);
+void launch_cs_hist(const Outbox& ob, uint64_t n, int begin, int bits, unsigned long long* cnt, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_cs_hist, dim3(blocks((int64_t)n)), dim3(256), 0, s, ob, n, begin, (1ull << bits) - 1, cnt);
 }
-void launch_cs_scatter(const uint64_t* keys, uint64_t n, int begin, int bits, uint32_t* off, uint64_t* kout,
-                       uint32_t* vout, hipStream_t s) {
+void launch_cs_scatter(const Outbox& ob, uint64_t n, int begin, int bits, unsigned long long* off, uint64_t* kout,
+                       uint32_t* vout, uint32_t* goff, hipStream_t s) {
   if (n)
-    hipLaunchKernelGGL(k_cs_scatter, dim3(blocks((int64_t)n)), dim3(256), 0, s, keys, n, begin, (1ull << bits) - 1, off,
-                       kout, vout);
+    hipLaunchKernelGGL(k_cs_scatter, dim3(blocks((int64_t)n)), dim3(256), 0, s, ob, n, begin, (1ull << bits) - 1, off,
+                       kout, vout, goff);
+}
+void launch_local_pack(const Outbox& ob, const uint32_t* idx, const uint32_t* goff, uint64_t n, uint64_t total,
+                       uint8_t* dst, uint32_t* taken_n, uint32_t* taken_var, hipStream_t s) {
+  hipLaunchKernelGGL(k_local_pack, dim3(blocks((int64_t)n + 1)), dim3(256), 0, s, ob, idx, goff, n, total, dst, taken_n,
+                     taken_var);
 }
 void launch_iota(uint32_t* p, uint64_t n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_iota, dim3(blocks((int64_t)n)), dim3(256), 0, s, p, n);

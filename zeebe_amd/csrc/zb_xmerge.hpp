@@ -26,11 +26,15 @@ constexpr uint32_t XSLAB_COUNT = 32;        // pairs in flight (zb_xlock.hpp: on
 constexpr uint32_t XPOOL_SLACK = 16;        // bytes past a workspace's string pool its 8-byte string chunks may touch
 // every lane first tries its pair in a small workspace of its own (XLANE_COUNT of them, held 64 at a time by a wave:
 // zb_xlock.hpp x_run): 32 KB holds the tree of ~140 tokens (2 x source + target), the documents of a typical job /
-// message payload merge
+// message payload merge (a larger pair takes the slab path)
 constexpr uint32_t XLANE_BYTES = 32u << 10;
-constexpr uint32_t XLANE_COUNT = 65536;  // (2 GiB per device, shared by its engines; k_merge_gen's grid: 256 workgroups of
-                                         //  256 lanes. C1 1M exact-tree tick: 16K lanes 14.3 ms, 32K 10.4, 64K 9.5, 128K
-                                         //  12.1, 256K 12.4)
+constexpr uint32_t XLANE_COUNT = 131072;  // (4 GiB per device, shared by its engines; k_merge_gen's grid: 512 workgroups
+                                          //  of 256 lanes. C1 1M exact-tree tick on the trajectory path, one box
+                                          //  (profiles/r06/ab_xlanes_r06ac.txt): 64K x 32 KB 3.06 ms, 128K x 32 KB 2.53,
+                                          //  128K x 16 KB 2.48 and 256K x 16 KB 2.48 -- but at 16 KB half the pairs of
+                                          //  test_xmerge_lane_workspaces_vs_oracle leave for a slab. Before the arrays
+                                          //  were interleaved, 64K lanes were best: their scattered lines fell out of
+                                          //  the Infinity Cache above that)
 constexpr uint32_t XLANE_GROUPS = XLANE_COUNT / 64;          // lane groups (one wave's 64 workspaces)
 constexpr uint32_t XLOCK_COUNT = XSLAB_COUNT + XLANE_GROUPS;  // slab locks, then lane-group locks
 
