@@ -2021,6 +2021,8 @@ __global__ void __launch_bounds__(256) k_tmpl_xtree(TrajParams P) {
           err |= DE_UNSUPPORTED;
         } else if (at + g.stride > P.arena_cap) {
           err |= DE_ARENA_FULL;
+        } else if (w == xg) {  // (the GEN pass's structural merge refused this very pair: straight to the tree)
+          need = true;
         } else {
           Out o{dst + 4, 0};
           bool unsup = false;
