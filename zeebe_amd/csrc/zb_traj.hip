@@ -1398,7 +1398,11 @@ __device__ __forceinline__ uint32_t outcome_key(const TrajParams& P, const uint8
   return key;
 }
 
-constexpr int CL_STRIDE = 25;  // classify: per-thread document slot, [u32 len][document <= 96 bytes], odd stride
+// classify: per-thread document slot [u32 len][document], an odd stride in words: 25 (documents <= 92 bytes) or, when
+// every staged CREATE payload fits 44 bytes (P.max_create; C3's are <= 38), 13 -- the slots are what bounds the
+// occupancy (25: 5 workgroups per CU by LDS, 13: 8, at 64 VGPRs), and the kernel is latency-bound on its two dependent
+// loads per instance
+template <int CL_STRIDE>
 __global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
   __shared__ uint32_t s_doc[TWG * CL_STRIDE];
   __shared__ uint32_t s_hist[256], s_rep[256];
@@ -2078,7 +2082,8 @@ void launch_traj_count_uniform(const TrajParams& p, hipStream_t s) {
 }
 // class batch: classify, plan, group masks, offsets, emit permutation, one traced representative per class
 void launch_traj_count_classes(const TrajParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_cls_classify, dim3(p.nwg), dim3(TWG), 0, s, p);
+  if (((p.max_create + 11) & ~7u) <= 13 * 4) hipLaunchKernelGGL(k_cls_classify<13>, dim3(p.nwg), dim3(TWG), 0, s, p);
+  else hipLaunchKernelGGL(k_cls_classify<25>, dim3(p.nwg), dim3(TWG), 0, s, p);
   hipLaunchKernelGGL(k_cls_plan, dim3(1), dim3(256), 0, s, p);
   hipLaunchKernelGGL(k_cls_masks, dim3(p.nwg), dim3(TWG), 0, s, p);
   hipLaunchKernelGGL(k_cls_scan, dim3(CLS_MAX), dim3(1024), 0, s, p);
