@@ -352,6 +352,9 @@ struct zb_engine {
   // inbox CORRELATE resolution by activity instance key (zb_inbox_submit)
   int64_t *x_keys = nullptr, *x_pos = nullptr, *x_keys2 = nullptr, *x_pos2 = nullptr;
   uint32_t* d_unresolved = nullptr;  // delivered CORRELATEs whose token named no live row of their key (running count)
+  // a class batch's injection, left to the classification kernel (run_trajectory), or to zb_step if that never ran
+  bool inject_deferred = false;
+  InjectParams inject_ip{};
   // the outbox's counting sort: per bucket (commands << 40 | variable granules), their exclusive scan
   unsigned long long *cs_cnt = nullptr, *cs_off = nullptr;
   void* cs_tmp = nullptr;
@@ -897,7 +900,11 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
   p.defer_ok = (e->tmpl_defer && e->seg_ok && e->d_vsegs.p && e->d_vconst.p && (p.cls || p.uni)) ? 1 : 0;
   hipEvent_t* ev = e->ev.data();
   HIPCHECK(e, hipEventRecord(ev[0], e->stream));
-  if (p.cls) launch_traj_count_classes(p, e->stream);
+  if (p.cls) {
+    const bool inj = e->inject_deferred && e->inject_ip.log_base == log_base && e->inject_ip.n == n;
+    launch_traj_count_classes(p, inj ? &e->inject_ip : nullptr, e->stream);
+    if (inj) e->inject_deferred = false;
+  }
   else if (p.uni) launch_traj_count_uniform(p, e->stream);
   else launch_traj_count(p, e->stream);
   HIPCHECK(e, hipEventRecord(ev[1], e->stream));
@@ -2643,7 +2650,16 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     }
     ip.cref = e->d_cref;
     e->cref_base = ip.log_base;
-    launch_inject(ip, e->stream);
+    // a batch headed for the class path (run_trajectory: classify, then trace the classes) is injected by the
+    // classification kernel itself, one thread per CREATE (k_cls_classify<.., true>); anything else by k_inject
+    const bool fuse = try_traj && e->traj_skip == 0 && e->has_splits && e->staged_uniform && e->cls_ok &&
+                      ip.staged_bytes == 0 && e->staged_nlook == 0;
+    if (fuse) {
+      e->inject_ip = ip;
+      e->inject_deferred = true;
+    } else {
+      launch_inject(ip, e->stream);
+    }
     // records naming an element instance by key: its row (ElementInstanceIndex.getInstance); the (key, index)
     // pairs were uploaded with the batch and are sorted here, on the device
     if (e->staged_nlook) {
@@ -2711,9 +2727,17 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   }
   if (try_traj && !quiescent) {
     int rc = run_trajectory(e, traj_base, traj_n, st, true);
+    if (e->inject_deferred) {  // (run_trajectory returned before its classification: inject here, stream-ordered)
+      e->inject_deferred = false;
+      launch_inject(e->inject_ip, e->stream);
+    }
     if (rc < 0) return rc;
     if (rc == 0) e->traj_skip = TRAJ_RETRY;
     quiescent = e->host_hdr.begin == e->host_hdr.end;
+  }
+  if (e->inject_deferred) {  // (not reached in practice: the fuse condition implies the trajectory run above)
+    e->inject_deferred = false;
+    launch_inject(e->inject_ip, e->stream);
   }
   ZB_SP(2);  // trajectory
   // the first batch: as many waves as the last wave loop over the same kind of input had (a tick of the same workload

@@ -1401,9 +1401,12 @@ __device__ __forceinline__ uint32_t outcome_key(const TrajParams& P, const uint8
 // classify: per-thread document slot [u32 len][document], an odd stride in words: 25 (documents <= 92 bytes) or, when
 // every staged CREATE payload fits 44 bytes (P.max_create; C3's are <= 38), 13 -- the slots are what bounds the
 // occupancy (25: 5 workgroups per CU by LDS, 13: 8, at 64 VGPRs), and the kernel is latency-bound on its two dependent
-// loads per instance
-template <int CL_STRIDE>
-__global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
+// loads per instance.
+// INJ: the batch's injection (k_inject's per-record work: descriptor, links, source, value length, CREATE ref) in the
+// same thread, which then classifies from the ref it just computed -- the stores of the injection overlap the loads of
+// the classification, and the ref is not written and read back (the documents are in place: no staged bytes to copy)
+template <int CL_STRIDE, bool INJ>
+__global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P, InjectParams I) {
   __shared__ uint32_t s_doc[TWG * CL_STRIDE];
   __shared__ uint32_t s_hist[256], s_rep[256];
   __shared__ unsigned long long s_len[256];
@@ -1415,7 +1418,20 @@ __global__ void __launch_bounds__(TWG) k_cls_classify(TrajParams P) {
   const int64_t i = (int64_t)blockIdx.x * TWG + t;
   uint32_t mkey = 0, mlen = 0;
   if (i < P.n) {
-    const uint32_t ref = P.cref ? P.cref[i] : P.log[P.log_base + i].payload;
+    uint32_t ref;
+    if (INJ) {
+      zb_rec d = I.staged[i];
+      d.payload += (uint32_t)(I.arena_base >> 3);
+      if (d.key == KEY_IS_POSITION) d.key = I.log_base + i;
+      I.log[I.log_base + i] = d;
+      I.links[I.log_base + i] = ~0ull;  // no rows yet
+      I.srcd[I.log_base + i] = 0;       // written by another writer (client API, job processor, ...)
+      I.vlen[I.log_base + i] = I.staged_vlen[i];
+      I.cref[i] = d.payload;
+      ref = d.payload;
+    } else {
+      ref = P.cref ? P.cref[i] : P.log[P.log_base + i].payload;
+    }
     const uint8_t* pp = P.arena + (uint64_t)ref * 8;
     const uint32_t len = *(const uint32_t*)pp;
     // the VM inlined on the LDS copy (LDS loads per token); a document too large for the copy gets the
@@ -2081,9 +2097,13 @@ void launch_traj_count_uniform(const TrajParams& p, hipStream_t s) {
   hipLaunchKernelGGL((k_traj<false, false, false, false, true, false>), dim3(1), dim3(TWG), 0, s, q);
 }
 // class batch: classify, plan, group masks, offsets, emit permutation, one traced representative per class
-void launch_traj_count_classes(const TrajParams& p, hipStream_t s) {
-  if (((p.max_create + 11) & ~7u) <= 13 * 4) hipLaunchKernelGGL(k_cls_classify<13>, dim3(p.nwg), dim3(TWG), 0, s, p);
-  else hipLaunchKernelGGL(k_cls_classify<25>, dim3(p.nwg), dim3(TWG), 0, s, p);
+void launch_traj_count_classes(const TrajParams& p, const InjectParams* inj, hipStream_t s) {
+  const InjectParams ip = inj ? *inj : InjectParams{};
+  const bool small = ((p.max_create + 11) & ~7u) <= 13 * 4;
+  if (inj && small) hipLaunchKernelGGL((k_cls_classify<13, true>), dim3(p.nwg), dim3(TWG), 0, s, p, ip);
+  else if (inj) hipLaunchKernelGGL((k_cls_classify<25, true>), dim3(p.nwg), dim3(TWG), 0, s, p, ip);
+  else if (small) hipLaunchKernelGGL((k_cls_classify<13, false>), dim3(p.nwg), dim3(TWG), 0, s, p, ip);
+  else hipLaunchKernelGGL((k_cls_classify<25, false>), dim3(p.nwg), dim3(TWG), 0, s, p, ip);
   hipLaunchKernelGGL(k_cls_plan, dim3(1), dim3(256), 0, s, p);
   hipLaunchKernelGGL(k_cls_masks, dim3(p.nwg), dim3(TWG), 0, s, p);
   hipLaunchKernelGGL(k_cls_scan, dim3(CLS_MAX), dim3(1024), 0, s, p);
