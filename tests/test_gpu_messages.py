@@ -114,6 +114,35 @@ def test_one_message_many_subscriptions(P):
     assert sum(g.counters()["completed"] for g in gpu) == 45 + 5 + 2
 
 
+def test_outbox_single_target_counting_sort():
+    """Every command of an outbox for one target partition: the keys' spread then leaves out the target bits and the
+    take sorts by counting (k_cs_hist / k_cs_scatter) on the outbox path (zb_outbox_take, P > 1) -- the OPEN commands of
+    each workflow partition, and the CORRELATE commands of one message partition to one workflow partition, many of them
+    one message's matches (emission indexes 0..44 at one source position)."""
+    P = 3
+    cks = [k for k in ("key-%d" % i for i in range(400)) if cluster.subscription_partition(k.encode(), P) == 0]
+    shared, single = cks[0], cks[1:21]
+    keys = [shared] * 45 + single
+    gpu, ref, cg, co = clusters(P, catch_workflow())
+    for i, key in enumerate(keys):  # every instance on partition 1, every subscription on partition 0
+        gpu[1].create("wf", [msgpack.packb({"orderId": key})])
+        ref[1].create("wf", msgpack.packb({"orderId": key}))
+    cg.settle()
+    co.settle()
+    compare(gpu, ref)
+    # one message first (its 45 correlations share a source position: the keys differ in the emission bits only),
+    # then several (positions and emission 0)
+    for c in (cg, co):
+        c.publish(b"order canceled", [shared.encode()], [msgpack.packb({"m": 0})])
+    compare(gpu, ref)
+    pub = [k.encode() for k in single[::2]]
+    pls = [msgpack.packb({"m": i + 1}) for i in range(len(pub))]
+    cg.publish(b"order canceled", pub, pls)
+    co.publish(b"order canceled", pub, pls)
+    compare(gpu, ref)
+    assert sum(g.counters()["completed"] for g in gpu) == 45 + len(pub)
+
+
 def test_integer_correlation_key():
     # extractCorrelationKey: a long becomes its 8 little-endian bytes (hash routing and store key)
     P = 3
