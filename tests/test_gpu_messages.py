@@ -143,6 +143,47 @@ def test_outbox_single_target_counting_sort():
     assert sum(g.counters()["completed"] for g in gpu) == 45 + len(pub)
 
 
+def test_correlate_with_stale_and_foreign_tokens():
+    """A delivered CORRELATE takes the row its token names only when that row is live and holds its activity instance
+    key; a foreign token (NO_TOKEN) or another instance's row is counted and resolved by the sorted key search
+    (k_resolve) -- the records must be those of the oracle, which resolves every command by key."""
+    import numpy as np
+
+    from zeebe_amd.engine import Engine
+
+    n = 90
+    e = Engine(device=0, partition_id=0, partition_count=1, log_capacity=1 << 16, row_capacity=1 << 12)
+    o = zbref.OraclePartition(0, 1)
+    co = cluster.LocalCluster([o])
+    for x in (e, o):
+        x.deploy(catch_workflow(), 100, 1)
+    for i in range(n):
+        e.create("wf", [msgpack.packb({"orderId": "order-%d" % i})])
+        o.create("wf", msgpack.packb({"orderId": "order-%d" % i}))
+    e.run()
+    buf, _ = e.outbox(cluster.KIND_OPEN)
+    e.inbox(cluster.KIND_OPEN, buf)
+    e.run()
+    co.settle()
+    cks = [b"order-%d" % i for i in range(n)]
+    pls = [msgpack.packb({"paid": i}) for i in range(n)]
+    e.publish(b"order canceled", cks, pls)
+    co.publish(b"order canceled", cks, pls)
+    buf, _ = e.outbox(cluster.KIND_CORRELATE)
+    b = bytearray(np.asarray(buf, dtype=np.uint8).tobytes())
+    cnt = int.from_bytes(b[0:8], "little")
+    assert cnt == n
+    toks = [int.from_bytes(b[16 + 64 * j + 12:16 + 64 * j + 16], "little") for j in range(cnt)]
+    for j in range(cnt):
+        t = 0xFFFFFFFF if j % 3 == 0 else toks[(j + 1) % cnt] if j % 3 == 1 else toks[j]
+        b[16 + 64 * j + 12:16 + 64 * j + 16] = t.to_bytes(4, "little")
+    e.inbox(cluster.KIND_CORRELATE, b)
+    e.run()
+    compare([e], [o])
+    assert e.counters()["completed"] == n
+    e.close()
+
+
 def test_integer_correlation_key():
     # extractCorrelationKey: a long becomes its 8 little-endian bytes (hash routing and store key)
     P = 3
