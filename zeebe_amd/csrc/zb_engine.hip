@@ -355,6 +355,7 @@ struct zb_engine {
   // a class batch's injection, left to the classification kernel (run_trajectory), or to zb_step if that never ran
   bool inject_deferred = false;
   InjectParams inject_ip{};
+  bool traj_stats_fresh = false;  // the last trajectory run's read-back holds the counters (h_stats_pinned + 8)
   // the outbox's counting sort: per bucket (commands << 40 | variable granules), their exclusive scan
   unsigned long long *cs_cnt = nullptr, *cs_off = nullptr;
   void* cs_tmp = nullptr;
@@ -742,6 +743,9 @@ int grow_class_buffers(zb_engine* e, uint64_t n, uint64_t nwg) {
   HIPCHECK(e, hipMalloc(&e->c_khist, CLS_HB * 256 * (2 * sizeof(uint32_t) + sizeof(uint64_t))));
   e->c_krep = e->c_khist + CLS_HB * 256;
   e->c_klen = (uint64_t*)(e->c_khist + 2 * CLS_HB * 256);
+  HIPCHECK(e, hipMemsetAsync(e->c_khist, 0, CLS_HB * 256 * sizeof(uint32_t), e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->c_klen, 0, CLS_HB * 256 * sizeof(uint64_t), e->stream));
+  HIPCHECK(e, hipMemsetAsync(e->c_krep, 0xff, CLS_HB * 256 * sizeof(uint32_t), e->stream));
   HIPCHECK(e, hipMalloc(&e->c_mask, groups * CLS_MAX * sizeof(uint64_t)));
   HIPCHECK(e, hipMalloc(&e->c_cg, groups * CLS_MAX * 2 * sizeof(uint32_t)));
   HIPCHECK(e, hipMalloc(&e->c_woffw, groups * CLS_MAX * sizeof(uint32_t)));
@@ -863,9 +867,7 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
     p.wgcnt = e->c_wgcnt;
     p.wgoff = e->c_wgoff;
     p.perm = e->c_perm;
-    HIPCHECK(e, hipMemsetAsync(e->c_khist, 0, CLS_HB * 256 * sizeof(uint32_t), e->stream));
-    HIPCHECK(e, hipMemsetAsync(e->c_klen, 0, CLS_HB * 256 * sizeof(uint64_t), e->stream));
-    HIPCHECK(e, hipMemsetAsync(e->c_krep, 0xff, CLS_HB * 256 * sizeof(uint32_t), e->stream));
+    // (the key banks are empty here: allocated so, and k_cls_plan empties them after every classification)
   }
   p.agg = e->t_agg;
   p.wcount = e->t_wcount;
@@ -918,9 +920,14 @@ int run_trajectory(zb_engine* e, int64_t log_base, int64_t n, zb_step_stats& st,
     r.add(e->h_hdr_pinned, e->hdr + (e->wave & 1), sizeof(WaveHdr));
     r.add(e->h_err_pinned, e->derr, sizeof(uint32_t));
     if (p.cls) r.add(e->h_stats_pinned + 16, e->c_plan, sizeof(uint32_t));
+    // (and the counters: a step the trajectory run makes quiescent needs no round trip of its own for them, zb_step)
+    r.add(e->h_stats_pinned + 8, e->dstats, 8 * sizeof(uint64_t));
+    if (e->on) r.add(e->h_stats_pinned + 19, e->on, 4 * sizeof(uint32_t));
     HIPCHECK(e, r.launch(e->stream));
   }
   HIPCHECK(e, hipStreamSynchronize(e->stream));
+  e->traj_stats_fresh = true;
+  if (e->on) e->ob_counts_valid = true;
   float ms0 = 0, ms1 = 0, ms_main = 0;
   HIPCHECK(e, hipEventElapsedTime(&ms0, ev[0], ev[1]));
   HIPCHECK(e, hipEventElapsedTime(&ms1, ev[1], ev[2]));
@@ -2725,6 +2732,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
     e->traj_skip--;
     try_traj = false;
   }
+  e->traj_stats_fresh = false;
   if (try_traj && !quiescent) {
     int rc = run_trajectory(e, traj_base, traj_n, st, true);
     if (e->inject_deferred) {  // (run_trajectory returned before its classification: inject here, stream-ordered)
@@ -2743,6 +2751,7 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   // the first batch: as many waves as the last wave loop over the same kind of input had (a tick of the same workload
   // settles in as many waves, and each launch past quiescence costs ~20 us of empty kernels), else WAVES_PER_SYNC
   const bool loop = !quiescent && (max_waves == 0 || launched < max_waves);
+  bool stats_fresh = quiescent && e->traj_stats_fresh;  // (the trajectory run read the counters back at its end)
   if (loop) HIPCHECK(e, hipMemcpyAsync(e->h_stats_pinned + 18, e->dstats + 6, sizeof(uint64_t), hipMemcpyDeviceToHost,
                                        e->stream));  // (the waves counter before the loop)
   // batches follow the hint until it is used up (C2: 148 waves as 64 + 64 + 20, not 64 + 16 + 32 + 64 with 28 empty
@@ -2750,7 +2759,6 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
   const int hint = e->wave_hint[hint_key];
   int next_batch = hint > 0 ? std::min<int>(hint, WAVES_PER_SYNC_MAX) : WAVES_PER_SYNC;
   int grow = hint > 0 ? 4 : WAVES_PER_SYNC;
-  bool stats_fresh = false;
   while (!quiescent && (max_waves == 0 || launched < max_waves)) {
     int batch = next_batch;
     if (max_waves) batch = std::min<int>(batch, (int)(max_waves - launched));

@@ -1486,6 +1486,11 @@ __global__ void __launch_bounds__(256) k_cls_plan(TrajParams P) {
     cnt += P.khist[b * 256 + t];
     rep = min(rep, P.krep[b * 256 + t]);
     lsum += P.klen[b * 256 + t];
+    // the banks back to their empty state for the next batch (allocated empty: grow_class_buffers; only k_cls_classify
+    // adds to them, and this launch follows it in every class run)
+    P.khist[b * 256 + t] = 0;
+    P.krep[b * 256 + t] = 0xffffffffu;
+    P.klen[b * 256 + t] = 0;
   }
   const uint64_t m = __ballot(cnt > 0);
   if (lane == 0) s_w[wv] = (uint32_t)__builtin_popcountll(m);
