@@ -1,6 +1,6 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
-O=gpurun_out/r06final
+O=gpurun_out/r06final2
 mkdir -p $O
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "gpu suite failed"; tail -30 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
