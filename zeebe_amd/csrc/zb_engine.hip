@@ -4071,7 +4071,9 @@ int outbox_plan(zb_engine* e, int kind, uint64_t* bytes_per_target, uint64_t* co
   const int cs_bits = spread ? 64 - __builtin_clzll(spread) - cs_begin : 0;
   const Outbox ob = outbox(e, kind);
   e->ob_plan_cs = false;
-  if (spread && cs_bits <= 24 && (1ull << cs_bits) <= 32 * n) {
+  // (a bucket packs commands << 40 | granules: fewer than 2^24 commands and 2^40 granules per take)
+  const uint64_t var_gran = ((const uint32_t*)(e->h_stats_pinned + 19))[kind + 1];
+  if (spread && cs_bits <= 24 && (1ull << cs_bits) <= 32 * n && n < (1ull << 24) && var_gran < (1ull << 40)) {
     const uint64_t nb = 1ull << cs_bits;
     size_t tmp = 0;
     if (hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->cs_cnt, e->cs_off, (int)nb, e->stream) != hipSuccess)
