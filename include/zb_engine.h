@@ -248,8 +248,10 @@ int zb_submit_messages(zb_engine* e, const zb_rec_desc* recs, size_t n, const ui
 int zb_submit_publishes(zb_engine* e, const char* message_name, int64_t ttl, size_t n, const uint8_t* cks,
                         const uint64_t* ck_offsets, const uint8_t* payloads, const uint64_t* payload_offsets);
 /* zb_submit_publishes in two parts: the batch goes to HBM (zb_upload_publishes; any partition state, returns when
- * the data is resident) and is processed later (zb_publish_uploaded; quiescent, nothing staged) -- so a broker
- * overlaps the next batch's PCIe copy with the current tick. Another upload replaces a batch not processed yet. */
+ * the data is resident, checked -- a payload that is not a map or nil, a key or payload over 4 GB: ZB_EINVAL here -- and
+ * its message blobs sized) and is processed later (zb_publish_uploaded; quiescent, nothing staged; without message ids
+ * every command is accepted, so its record counts need no count pass) -- so a broker overlaps the next batch's PCIe copy
+ * with the current tick. Another upload replaces a batch not processed yet. */
 int zb_upload_publishes(zb_engine* e, const char* message_name, int64_t ttl, size_t n, const uint8_t* cks,
                         const uint64_t* ck_offsets, const uint8_t* payloads, const uint64_t* payload_offsets);
 int zb_publish_uploaded(zb_engine* e);
