@@ -112,7 +112,7 @@ RECS_PER_INST = {"c1": lambda t: 18, "c2": lambda t: 2 + 8 + 5 * t + 3 * t, "c3"
 
 
 def make_engine(cfg, n, a, rank, world, local_rank):
-    from zeebe_amd.engine import Engine
+    from zeebe_amd.engine import CFG_SHARED_GPU, Engine
 
     recs = RECS_PER_INST[cfg](a.tasks)
     # (the trajectory path allocates no rows for instances that complete in the tick; the wave pipeline holds a
@@ -122,7 +122,8 @@ def make_engine(cfg, n, a, rank, world, local_rank):
     jobs = getattr(a, "jobs", "harness") if cfg == "c3" else "harness"  # (service tasks: the in-kernel harness)
     return Engine(device=0 if a.same_device else local_rank, partition_id=rank, partition_count=world,
                   log_capacity=int(n * recs), row_capacity=int(rows), arena_bytes=int(arena), wave_only=a.wave_only,
-                  external_jobs=jobs == "external", job_processor=jobs == "processor")
+                  external_jobs=jobs == "external", job_processor=jobs == "processor",
+                  flags=CFG_SHARED_GPU if a.same_device and world > 1 else 0)
 
 
 FRAME_CFG = dict(stream_id=1, raft_term=3, timestamp=1_700_000_000_000)  # (the broker's log stream / raft term)

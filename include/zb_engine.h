@@ -69,6 +69,11 @@ extern "C" {
 #define ZB_CFG_RCCL_SELF 1024     /* a one-partition engine still exchanges through its RCCL communicator (both agreement
                                      collectives and ncclSend / ncclRecv to itself: the P > 1 code path); without it a
                                      single partition hands its outbox to its own inbox on the device */
+#define ZB_CFG_SHARED_GPU 2048    /* the GPU is shared with other processes' engines: the wave pipeline's persistent
+                                     kernel claims its tiles from a counter, so its hand-off progresses when only part
+                                     of its grid is resident (without it, engines of several processes stepping on one
+                                     GPU at once can time out their hand-off, DE_TIMEOUT; the claims cost one contended
+                                     atomic per tile) */
 
 typedef struct zb_engine zb_engine;
 

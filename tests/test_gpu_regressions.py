@@ -8,6 +8,12 @@ memory still held whatever was there before -- a compacted-away row, another eng
 that garbage parent. The fault came and went with the allocator's layout. The guard-band build fills every fresh
 allocation with 0xA5, which turns such a read into a certain fault (parent 0xa5a5a5a5), so the case runs there, in a
 child process, as well as on the product build.
+
+A log overflow in the middle of a tick (round-6 fault, found by test_gpu_shared_gpu.py with too small a log): the
+wave that runs past the log window stops emitting at its end and flags DE_LOG_FULL, but its header still carries the
+unbounded end / generation end, and the waves the host had already queued behind it (a batch of waves runs between
+two status reads) processed "records" past the log array -- garbage element indices, an illegal memory access. Every
+wave kernel now bounds its range by the window (gen_limit, zb_kernels.hpp); the step fails with ZB_ENOMEM.
 """
 import os
 import subprocess
@@ -54,3 +60,26 @@ def test_create_and_cancel_in_one_wave_guard_bands():
             "t._create_and_cancel_in_one_wave(); assert checked_violations()[0] == 0; print('regression ok')")
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "regression ok" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+
+
+def test_log_overflow_mid_tick_fails_cleanly():
+    from zeebe_amd import bpmn
+    from zeebe_amd.engine import Engine, ZbError
+
+    n = 600_000  # 9 records per instance: 5.4M records into a 4.8M-record log, several waves after the overflow
+    wf = bpmn.Bpmn.create_executable_process("p").start_event("s").end_event("e").done()
+    e = Engine(wave_only=True, log_capacity=n * 8, row_capacity=n * 3, arena_bytes=n * 256 + (64 << 20))
+    e.deploy(wf.to_xml(), 100, 1)
+    blob, offs = workloads.order_payloads(n)
+    e.create_packed("p", blob, offs)
+    with pytest.raises(ZbError) as ex:
+        e.step()
+    assert ex.value.code == -2 and "log-capacity" in str(ex.value), ex.value
+    e.close()
+    # the device is usable afterwards: the same tick in a log that holds it
+    e = Engine(wave_only=True, log_capacity=n * 10, row_capacity=n * 3, arena_bytes=n * 256 + (64 << 20))
+    e.deploy(wf.to_xml(), 100, 1)
+    e.create_packed("p", blob, offs)
+    st = e.step()
+    assert st["quiescent"] and st["completed_instances"] == n and e.log_size() == 9 * n, st
+    e.close()

@@ -1,0 +1,17 @@
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+O=gpurun_out/r06au
+mkdir -p $O
+# the log-overflow regression first (it faulted the device before the window bound), alone, then the rest
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_regressions.py -m gpu -x -v --timeout 120 --timeout-method thread -k overflow > $O/pytest_overflow.log 2>&1 || { tail -30 $O/pytest_overflow.log; exit 1; }
+tail -n 2 $O/pytest_overflow.log
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_shared_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_shared.log 2>&1 || { tail -30 $O/pytest_shared.log; exit 1; }
+tail -n 3 $O/pytest_shared.log
+LIBS="ab/head.so ab/optin.so" REPS=2 OUT=$O/ab bash tools/gpu/wave_ab.sh || exit 1
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "gpu suite failed"; tail -30 $O/pytest_gpu.log; exit 1; }
+tail -n 1 $O/pytest_gpu.log
+ZB_CHECKED_LIBRARY=1 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu_checked.log 2>&1 || { echo "checked suite failed"; tail -30 $O/pytest_gpu_checked.log; exit 1; }
+tail -n 1 $O/pytest_gpu_checked.log
+timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
+tail -n 3 $O/smoke.log
+echo ok

@@ -30,7 +30,7 @@ __device__ __forceinline__ unsigned long long wg_sum256(unsigned long long x, un
 
 // the ELEMENT_COMPLETED record carrying a merge result: its value length hint
 __device__ __forceinline__ void merge_hint(const WaveParams& P, const MergeJob& j, uint32_t olen) {
-  if (j.pos >= 0 && P.vconst) {
+  if (j.pos >= 0 && (uint64_t)j.pos < P.log_cap && P.vconst) {  // (a slot past the window was not written)
     const zb_rec d = P.log[j.pos];
     const ValueConst vc = P.vconst[d.elem];
     P.vlen[j.pos] = vc.wf + mp_int_len(d.inst_key) + mp_int_len(d.scope_key) + mp_bin_len(olen);
@@ -195,7 +195,7 @@ __global__ void __launch_bounds__(256) k_cond(WaveParams P) {
 // row, and a flow scope's value changes only with records of the scope itself.
 __global__ void __launch_bounds__(256) k_map(WaveParams P) {
   WaveHdr* hin = P.hdr + (P.wave & 1);
-  const int64_t b = hin->begin, g = hin->gen_end;
+  const int64_t b = hin->begin, g = gen_limit(P, hin);
   const int64_t cend = chunk_end(P, b, g);
   const int64_t lim = cend + 3 < g ? cend + 3 : g;  // a batch's tail may lie past the chunk end
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -1571,7 +1571,8 @@ int zb_engine_create(const zb_config* cfg, zb_engine** out) {
   if (hipMalloc(&e->block_off, WAVE_GRID_MAX * sizeof(BlockOff)) != hipSuccess) return cleanup(ZB_ENOMEM);
   {
     e->lb_tiles = e->wave_cap / WAVE_TILE + 1;
-    const size_t lb = (2 * e->lb_tiles + 8 * (e->lb_tiles + 512) + 8 * (e->lb_tiles + 2)) * sizeof(uint64_t);
+    // (+ 1: the two k_wave tile counters)
+    const size_t lb = (2 * e->lb_tiles + 8 * (e->lb_tiles + 512) + 8 * (e->lb_tiles + 2) + 1) * sizeof(uint64_t);
     if (hipMalloc(&e->lookback, lb) != hipSuccess) return cleanup(ZB_ENOMEM);
     if (hipMemset(e->lookback, 0, lb) != hipSuccess) return cleanup(ZB_EDEVICE);
   }
@@ -2782,6 +2783,10 @@ int zb_step(zb_engine* e, uint32_t max_waves, zb_step_stats* stats) {
         if (e->lb_seq % 255 == 0 && e->lb_seq)
           HIPCHECK(e, hipMemsetAsync(e->lookback, 0, 2 * e->lb_tiles * sizeof(uint64_t), e->stream));
         p.lb_tag8 = (uint32_t)(1 + e->lb_seq % 255);
+        uint32_t* const claims = (uint32_t*)(e->lookback + 2 * e->lb_tiles + 8 * (e->lb_tiles + 512) + 8 * (e->lb_tiles + 2));
+        const bool shared = (e->cfg.flags & ZB_CFG_SHARED_GPU) != 0;
+        p.tile_claim = shared ? claims + (e->lb_seq & 1) : nullptr;
+        p.tile_claim_next = shared ? claims + ((e->lb_seq + 1) & 1) : nullptr;
         e->lb_seq++;
         launch_wave(p, e->wave_fused_grid, e->stream);
         if (per_wave) HIPCHECK(e, hipEventRecord(ev[1], e->stream));

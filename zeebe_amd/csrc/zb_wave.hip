@@ -783,7 +783,7 @@ struct Chunk {
   int64_t begin, end, n;  // [begin, end) records processed by this wave
 };
 __device__ __forceinline__ Chunk wave_chunk(const WaveParams& P, const WaveHdr* h) {
-  const int64_t b = h->begin, g = h->gen_end;
+  const int64_t b = h->begin, g = gen_limit(P, h);
   const int64_t e = chunk_end(P, b, g);
   return Chunk{b, e, e - b};
 }
@@ -809,7 +809,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
   const WaveHdr* hin = P.hdr + (P.wave & 1);
   const Chunk c = wave_chunk(P, hin);
   if (c.n <= 0) return;
-  const int64_t gen_end = hin->gen_end;
+  const int64_t gen_end = gen_limit(P, hin);  // (the batch tails read below)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int64_t t0, t1;
   block_tiles(c, t0, t1);
@@ -1270,6 +1270,12 @@ __global__ void __launch_bounds__(WG) k_emit(WaveParams P) {
 // 28.1 against 20.5 ms, profiles/r05/wave_exp_split_r05a.txt), and no single-workgroup scan between the passes.
 // The grid is persistent (every workgroup resident, tiles dealt round-robin in increasing order): round k is tiles
 // [kG, (k+1)G), and a tile only ever waits for tiles of its own or an earlier round, which are already running.
+// On a GPU shared with other processes not every workgroup of the grid is resident, and round-robin tiles then wait
+// for workgroups that are never dispatched (profiles/r06/c4_8rank_samedevice_r06aq.err.txt): with ZB_CFG_SHARED_GPU
+// (tile_claim set) tiles are claimed from a counter instead, in increasing order, so every smaller tile is held by a
+// running workgroup and the hand-off progresses whatever the device keeps resident. The claims are one contended
+// device-scope atomic per tile -- C2 wave-only 16.5 -> 25.2 ms per step (profiles/r06/ab_tile_claim_r06ar.txt) --
+// so the product default is the round-robin deal. The next tile is claimed when the current one starts.
 //
 // Offsets (a hierarchical hand-off instead of a decoupled look-back: the look-back walked 8.8 rounds of 8
 // predecessors per tile, 55 % of tile time, because the tiles of a round all finish processing together and
@@ -1343,6 +1349,9 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
   __shared__ uint64_t s_ex[LB_FIELDS];   // the tile's exclusive prefix
   __shared__ uint64_t s_part[3][LB_FIELDS];  // its parts: in the group, earlier groups of the round, the round base
   __shared__ int s_void;                 // a hand-off timed out: the tile's prefix is unknown, nothing is emitted
+  __shared__ uint32_t s_tile;            // ZB_CFG_SHARED_GPU: the workgroup's next claimed tile
+  const bool claim = P.tile_claim != nullptr;
+  if (claim && blockIdx.x == 0 && threadIdx.x == 0) *P.tile_claim_next = 0;  // (the next launch starts after this one ends)
   const WaveHdr* hin = P.hdr + (P.wave & 1);
   WaveHdr* hout = P.hdr + ((P.wave + 1) & 1);
   const Chunk c = wave_chunk(P, hin);
@@ -1357,7 +1366,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t ntiles = (c.n + WG - 1) / WG;
-  const int64_t gen_end = hin->gen_end;
+  const int64_t gen_end = gen_limit(P, hin);  // (the batch tails read below)
   const int64_t end = hin->end, wf_next = hin->wf_next, job_next = hin->job_next;
   const uint64_t rows_next = (uint64_t)hin->rows_next, arena_next = (uint64_t)hin->arena_next;
   const uint64_t par = (uint64_t)(P.wave & 1) * P.job_cap;
@@ -1377,7 +1386,20 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
 #else
 #define ZB_PHASE(k) do { } while (0)
 #endif
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += G) {
+  // (the tile index stays wave-uniform, in scalar registers: read from LDS it would take vector registers and make
+  //  every offset computed from it per-lane work -- C2 wave-only 16.6 -> 17.8 ms)
+  int64_t tile = blockIdx.x;
+  if (claim) {
+    if (threadIdx.x == 0) s_tile = atomicAdd(P.tile_claim, 1u);
+    __syncthreads();
+    tile = (int64_t)__builtin_amdgcn_readfirstlane(s_tile);
+  }
+  [[maybe_unused]] int64_t ntl = 0;  // tiles this workgroup processed (ZB_PHASES)
+  while (tile < ntiles) {
+    ntl++;
+    // the next claim: in flight while this tile loads its records (s_tile is rewritten after the tile scan's barrier)
+    uint32_t next_claim = 0;
+    if (claim && threadIdx.x == 0) next_claim = atomicAdd(P.tile_claim, 1u);
     const int64_t i = tile * WG + threadIdx.x;  // wave-relative index
     const int64_t r = c.begin + i;
     // ---- process (k_process)
@@ -1476,6 +1498,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
     const bool last_of_chunk = tile == ntiles - 1;
     const bool last_of_group = u == LB_GROUP - 1 || j == G - 1 || last_of_chunk;
     const uint64_t gg = (uint64_t)(k * GPR + gi);  // the group's index among the wave's groups
+    if (claim && threadIdx.x == 0) s_tile = next_claim;  // (every thread has read this tile's index)
     const uint64_t t_start = wall_clock64();
     if (wv == 0) {
       // the aggregate, published first (lane 0), then this tile's exclusive prefix within its group
@@ -1611,6 +1634,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
     }
     __syncthreads();  // LDS slots and scan scratch are reused by the next tile
     ZB_PHASE(2);  // emit
+    tile = claim ? (int64_t)__builtin_amdgcn_readfirstlane(s_tile) : tile + G;
   }
   if (threadIdx.x == 0 && (wg_sa | wg_sb)) {  // (into the workgroup's bank: launch_stat_fold)
     unsigned long long* bank = (unsigned long long*)(P.stats + 8 + 8 * (blockIdx.x % STAT_BANKS));
@@ -1622,8 +1646,8 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
 #ifdef ZB_PHASES
   if (threadIdx.x == 0 && P.phase) {
     for (int k = 0; k < 3; k++) atomicAdd(P.phase + k, (unsigned long long)ph[k]);
-    atomicAdd(P.phase + 4, (unsigned long long)((ntiles - blockIdx.x + gridDim.x - 1) / gridDim.x));
-    atomicAdd(P.phase + 3, (unsigned long long)((ntiles - blockIdx.x + gridDim.x - 1) / gridDim.x));
+    atomicAdd(P.phase + 4, (unsigned long long)ntl);
+    atomicAdd(P.phase + 3, (unsigned long long)ntl);
   }
 #endif
 #undef ZB_PHASE
@@ -1648,7 +1672,7 @@ __device__ __forceinline__ int64_t conf_slot(const WaveParams& P, int64_t key) {
 template <bool SPLIT>
 __global__ void __launch_bounds__(256) k_conflict(WaveParams P) {
   const WaveHdr* hin = P.hdr + (P.wave & 1);
-  const int64_t b = hin->begin, g = hin->gen_end;
+  const int64_t b = hin->begin, g = gen_limit(P, hin);
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t r = b + (int64_t)blockIdx.x * 256 + threadIdx.x; r < g; r += stride) {
     const zb_rec rec = P.log[r];

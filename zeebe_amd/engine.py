@@ -32,6 +32,7 @@ CFG_WAVE_EVENTS = 128  # timing events around every wave's kernels
 CFG_WAVE_SPLIT = 256  # three-kernel wave pipeline instead of the fused k_wave
 CFG_SINGLE_PASS_DRAIN = 512  # one-pass (look-back) value drain
 CFG_RCCL_SELF = 1024  # a one-partition engine exchanges through RCCL anyway (tests of the P > 1 path on one GPU)
+CFG_SHARED_GPU = 2048  # the GPU is shared with other processes' engines: the wave kernel claims its tiles
 
 ZB_OK, ZB_EINVAL, ZB_ENOMEM, ZB_EUNSUPPORTED, ZB_EDEPLOY, ZB_EDEVICE, ZB_EAGAIN, ZB_EPROCESSING = \
     0, -1, -2, -3, -4, -5, -6, -7
