@@ -83,3 +83,34 @@ def test_log_overflow_mid_tick_fails_cleanly():
     st = e.step()
     assert st["quiescent"] and st["completed_instances"] == n and e.log_size() == 9 * n, st
     e.close()
+
+
+def test_arena_overflow_mid_tick_fails_cleanly():
+    # the merge results of the canonical job harness outgrow the arena in the middle of the tick: the wave that
+    # overflows counts merge jobs it could not reserve (their list entries unwritten); k_merge / k_cond of that wave
+    # and every later one skip their lists once a device error is flagged (wave_void, zb_kernels.hpp)
+    from zeebe_amd import bpmn
+    from zeebe_amd.engine import Engine, ZbError
+
+    n = 200_000
+    wf = bpmn.chain_workflow(4)
+    jp = {"t%d" % k: msgpack.packb({"k%d" % k: "v" * (8 * k)}) for k in range(1, 5)}
+    blob, offs = workloads.order_payloads(n)
+
+    def run(arena):
+        e = Engine(wave_only=True, log_capacity=n * 48, row_capacity=n * 8, arena_bytes=arena)  # (42 records per instance)
+        e.deploy(wf.to_xml(), 100, 1)
+        for act, p in jp.items():
+            e.set_job_payload(100, act, p)
+        e.create_packed("chain", blob, offs)
+        return e
+
+    e = run(24 << 20)  # (the CREATE payloads take ~3 MB; the four merges per instance ~40 MB)
+    with pytest.raises(ZbError) as ex:
+        e.step()
+    assert ex.value.code == -2 and "arena-capacity" in str(ex.value), ex.value
+    e.close()
+    e = run(n * 512 + (64 << 20))
+    st = e.step()
+    assert st["quiescent"] and st["completed_instances"] == n, st
+    e.close()

@@ -51,7 +51,8 @@ constexpr int KM_STRIDE = 3 * KM_WORDS + 1;  // source, target, result; odd stri
 __global__ void __launch_bounds__(256) k_merge(WaveParams P) {
   __shared__ unsigned long long s4[4];
   __shared__ uint32_t s_m[256 * KM_STRIDE];
-  const uint32_t n = P.merge_count[P.wave & 1];
+  if (wave_void(P)) return;
+  const uint32_t n = (uint32_t)std::min<uint64_t>(P.merge_count[P.wave & 1], P.job_cap);
   const MergeJob* jobs = P.merge_jobs + (uint64_t)(P.wave & 1) * P.job_cap;
   uint32_t* slow_n = P.merge_slow_count + (P.wave & 1);
   uint32_t* reg = s_m + threadIdx.x * KM_STRIDE;
@@ -99,7 +100,7 @@ __global__ void __launch_bounds__(256) k_merge_gen(WaveParams P) {
   const uint32_t n = P.merge_slow_count[P.wave & 1];
   const MergeJob* jobs = P.merge_jobs + (uint64_t)(P.wave & 1) * P.job_cap;
   if (blockIdx.x == 0 && threadIdx.x == 0) P.merge_slow_count[(P.wave + 1) & 1] = 0;  // the next wave's queue
-  if (n == 0) return;
+  if (n == 0 || wave_void(P)) return;
   uint32_t err = 0;
   unsigned long long merges = 0, bytes = 0;
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
@@ -146,7 +147,8 @@ __global__ void __launch_bounds__(256) k_merge_gen(WaveParams P) {
 
 __global__ void __launch_bounds__(256) k_cond(WaveParams P) {
   __shared__ unsigned long long s4[4];
-  const uint32_t n = P.cond_count[P.wave & 1];
+  if (wave_void(P)) return;
+  const uint32_t n = (uint32_t)std::min<uint64_t>(P.cond_count[P.wave & 1], P.job_cap);
   const uint64_t* jobs = P.cond_jobs + (uint64_t)(P.wave & 1) * P.job_cap;
   unsigned long long bytes = 0;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {

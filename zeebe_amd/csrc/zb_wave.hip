@@ -1342,6 +1342,9 @@ __device__ __forceinline__ bool lb_wait(uint32_t* err, const uint64_t* const (&g
   return !__ballot(timeout);
 }
 
+template <bool CLAIM>  // ZB_CFG_SHARED_GPU: tiles claimed from P.tile_claim (a kernel of its own, so the default path
+                       // carries none of the claim code; C2 wave-only within 1-2 % of the round-6 head either way,
+                       // profiles/r06/ab_shared_gpu_optin_r06au.txt)
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8))) k_wave(WaveParams P) {
   __shared__ Slot s_slots[WG * MAX_SLOTS];
   __shared__ uint64_t s_a[WG / 64], s_b[WG / 64];
@@ -1350,7 +1353,7 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4, 8)))
   __shared__ uint64_t s_part[3][LB_FIELDS];  // its parts: in the group, earlier groups of the round, the round base
   __shared__ int s_void;                 // a hand-off timed out: the tile's prefix is unknown, nothing is emitted
   __shared__ uint32_t s_tile;            // ZB_CFG_SHARED_GPU: the workgroup's next claimed tile
-  const bool claim = P.tile_claim != nullptr;
+  constexpr bool claim = CLAIM;
   if (claim && blockIdx.x == 0 && threadIdx.x == 0) *P.tile_claim_next = 0;  // (the next launch starts after this one ends)
   const WaveHdr* hin = P.hdr + (P.wave & 1);
   WaveHdr* hout = P.hdr + ((P.wave + 1) & 1);
@@ -1712,11 +1715,12 @@ void launch_stat_fold(uint64_t* stats, hipStream_t stream) {
 }
 
 void launch_wave(const WaveParams& p, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(k_wave, dim3(grid), dim3(WG), 0, stream, p);
+  if (p.tile_claim) hipLaunchKernelGGL(k_wave<true>, dim3(grid), dim3(WG), 0, stream, p);
+  else hipLaunchKernelGGL(k_wave<false>, dim3(grid), dim3(WG), 0, stream, p);
 }
 int wave_resident_per_cu() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_wave, WG, 0) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_wave<false>, WG, 0) != hipSuccess) return 0;
   return n;
 }
 
