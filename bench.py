@@ -365,7 +365,7 @@ def load_traffic_step(tag, kernel_prefixes):
     if not ticks:
         return None
     tot = sum(v["hbm_bytes"] * v.get("dispatches", 0) for k, v in d.items()
-              if "hbm_bytes" in v and any(k.startswith(p) for p in kernel_prefixes))
+              if "hbm_bytes" in v and any(k.startswith(p) or k.startswith("void " + p) for p in kernel_prefixes))
     return tot / ticks
 
 
