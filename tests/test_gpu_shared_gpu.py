@@ -112,8 +112,14 @@ def test_processes_sharing_one_gpu(tmp_path):
     procs = [subprocess.Popen([sys.executable, "-c", _CHILD, "125000", "4", "p%d" % k, "4", str(gate)], env=env,
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for k in range(4)]
     outs = []
-    for p in procs:
-        out, err = p.communicate(timeout=240)
-        assert p.returncode == 0, (p.returncode, out[-2000:], err[-4000:])
-        outs.append(out.split()[-1])
+    try:
+        for p in procs:
+            out, err = p.communicate(timeout=240)
+            assert p.returncode == 0, (p.returncode, out[-2000:], err[-4000:])
+            outs.append(out.split()[-1])
+    finally:
+        for p in procs:  # (a failed or timed-out case leaves no process on the GPU)
+            if p.poll() is None:
+                p.kill()
+                p.wait()
     assert len(set(outs)) == 1, outs
